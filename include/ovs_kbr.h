@@ -1,0 +1,187 @@
+/*
+ * ovs_kbr.h -- C ABI of the MI355X batched KBR lookup-routing engine.
+ *
+ * This is the drop-in boundary for OverSim's iterative key lookup.  In the
+ * reference the boundary is C++ virtual dispatch inside one process; each
+ * entry point below names the reference interface it replaces:
+ *
+ *   BaseOverlay::findNode          src/common/BaseOverlay.h:693-696
+ *     Chord::findNode              src/overlay/chord/Chord.cc:548-599
+ *     Kademlia::findNode           src/overlay/kademlia/Kademlia.cc:1101-1246
+ *   BaseOverlay::isSiblingFor      src/common/BaseOverlay.h:417-418
+ *     Chord::isSiblingFor          src/overlay/chord/Chord.cc:422-500
+ *     Kademlia::isSiblingFor       src/overlay/kademlia/Kademlia.cc:888-962
+ *   BaseOverlay::findNodeRpc       src/common/BaseOverlay.cc:1841-1915 (siblings flag)
+ *   AbstractLookup::lookup +       src/common/AbstractLookup.h, IterativeLookup.cc:695-723
+ *   LookupListener::lookupFinished src/common/LookupListener.h, BaseOverlay.cc:1241-1307
+ *   SimpleNodeEntry::calcDelay     src/underlay/simpleunderlay/SimpleNodeEntry.cc:155-195
+ *   .ini parameter binding         simulations/default.ini (same key names)
+ *
+ * Plain C: no C++ exceptions cross this boundary, no torch types.  Every call
+ * returns an ovs_status; ovs_last_error() gives the message (the C++ adapter
+ * in INTEGRATION.md turns it into a cRuntimeError, like the reference's
+ * throws at Chord.cc:560,619,672).
+ *
+ * Threading: one context per HIP device; calls on one context are
+ * stream-ordered and must not race; different contexts are independent.
+ * Ownership: the caller owns every input/output buffer; the context owns the
+ * device routing tables.  Buffers are host memory unless the call's `flags`
+ * include OVS_DEVICE_PTRS, in which case they are device pointers on the
+ * context's device and the call is asynchronous on `stream` (NULL = the
+ * context's own stream).  Host-pointer calls are synchronous.
+ */
+#ifndef OVS_KBR_H
+#define OVS_KBR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OVS_ABI_VERSION 1
+
+/* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
+ * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
+ * (OverlayKey.cc:41-47, 835-838; keyLength = 160, default.ini:393). */
+typedef struct ovs_key160 { uint32_t w[5]; } ovs_key160;
+
+typedef enum ovs_status {
+    OVS_OK = 0,
+    OVS_EINVAL = 1,    /* bad argument (reference: cRuntimeError / opp_error) */
+    OVS_ENOMEM = 2,
+    OVS_EDEVICE = 3,   /* HIP error or no device */
+    OVS_ESTATE = 4,    /* no network loaded / wrong overlay for this call */
+    OVS_ENOTSUP = 5    /* parameter combination the engine does not implement */
+} ovs_status;
+
+/* per-lookup status (why IterativeLookup::isValid() is false) */
+enum {
+    OVS_LOOKUP_OK = 0,
+    OVS_LOOKUP_TIMEOUT = 1,      /* response after startTime + LOOKUP_TIMEOUT (IterativeLookup.cc:808-815) */
+    OVS_LOOKUP_RPC_TIMEOUT = 2,  /* RTT >= rpcUdpTimeout (BaseRpc.cc:191-211) */
+    OVS_LOOKUP_HOPMAX = 3,       /* hops >= hopCountMax (IterativeLookup.cc:1074-1086) */
+    OVS_LOOKUP_NO_NEXT = 4,      /* no unvisited next hop (IterativeLookup.cc:1147-1168) */
+    OVS_LOOKUP_BROKEN = 5        /* Chord successor list broken (Chord.cc:615-620, 671-672) */
+};
+
+enum { OVS_OVERLAY_CHORD = 1, OVS_OVERLAY_KADEMLIA = 2 };
+
+/* flags */
+#define OVS_DEVICE_PTRS  0x1u   /* buffers are device pointers; call is async on `stream` */
+
+/* Parameters.  Field names are the NED/.ini parameter names. */
+typedef struct ovs_params {
+    int32_t overlay;                    /* OVS_OVERLAY_* */
+    int32_t keyLength;                  /* **.keyLength = 160 (only 160 supported) */
+    int32_t hopCountMax;                /* **.hopCountMax = 50 */
+    int32_t successorListSize;          /* **.chord.successorListSize = 8 */
+    int32_t extendedFingerTable;        /* **.chord.extendedFingerTable = false (only false) */
+    int32_t numFingerCandidates;        /* **.chord.numFingerCandidates = 3 */
+    int32_t k, s, b;                    /* **.kademlia.k/s/b = 8/8/1 (b = 1 only) */
+    int32_t lookupRedundantNodes;
+    int32_t lookupParallelPaths;        /* 1 only */
+    int32_t lookupParallelRpcs;
+    int32_t lookupMerge;
+    int32_t lookupStrictParallelRpcs;
+    int32_t lookupVisitOnlyOnce;
+    int32_t lookupAcceptLateSiblings;
+    int32_t lookupUseAllParallelResponses;
+    int32_t lookupNewRpcOnEveryTimeout;
+    int32_t lookupNewRpcOnEveryResponse;
+    int32_t lookupFinishOnFirstUnchanged;
+    int32_t lookupVerifySiblings;       /* false only */
+    int32_t lookupMajoritySiblings;     /* false only */
+    int32_t routingType;                /* 0 = "iterative" (only) */
+    int32_t numSiblings;                /* sendToKey numSiblings (1 for KBRTestApp one-way) */
+    int32_t useCoordinateBasedDelay;    /* **.udp.useCoordinateBasedDelay = true */
+    int32_t simtimeRound;               /* SimTime(double): 1 = round half up, 0 = truncate */
+    int32_t testMsgSize;                /* **.kbrTestApp.testMsgSize = 100 B */
+    int32_t _pad0;
+    double  rpcUdpTimeout;              /* **.rpcUdpTimeout = 1.5 s */
+    double  lookupTimeout;              /* LOOKUP_TIMEOUT = 10 s (IterativeLookup.h:44) */
+    double  jitter;                     /* **.udp.jitter (must be 0 for bit-exact latency) */
+    double  constantDelay;              /* **.udp.constantDelay = 50 ms */
+    double  datarate;                   /* channel datarate, simple_ethernetline = 10 Mbps */
+    double  accessDelay;                /* channel delay = 0 ms */
+    uint64_t kadSeed;                   /* Kademlia snapshot bucket-sampling seed */
+} ovs_params;
+
+/* Result of one one-way KBR test lookup (KBRTestApp with kbrOneWayTest). */
+typedef struct ovs_route_out {
+    uint32_t responsible;   /* node index (sorted-ID order) of getResult()[0]; 0xFFFFFFFF on failure */
+    uint16_t hops;          /* IterativeLookup::getMinHops() */
+    uint8_t  status;        /* OVS_LOOKUP_* */
+    uint8_t  one_way_hops;  /* "KBRTestApp: One-way Hop Count" = hops + (responsible != source) */
+    int64_t  latency_ns;    /* "KBRTestApp: One-way Latency" in ns (simtime-scale -9); -1 on failure */
+} ovs_route_out;
+
+typedef struct ovs_ctx ovs_ctx;
+
+int         ovs_abi_version(void);
+void        ovs_params_default(int32_t overlay, ovs_params* out);
+/* Parse OMNeT++ .ini text (sections [General] / [Config X] with `extends`,
+ * wildcard keys such as `**.overlay*.chord.successorListSize = 8`, units s/ms/B/Mbps)
+ * and overwrite the matching fields of *p.  config_name may be NULL ([General]). */
+ovs_status  ovs_params_from_ini(ovs_params* p, const char* ini_text, const char* config_name,
+                                char* err, int err_len);
+
+ovs_status  ovs_ctx_create(int hip_device, ovs_ctx** out);
+void        ovs_ctx_destroy(ovs_ctx* ctx);
+const char* ovs_last_error(const ovs_ctx* ctx);
+ovs_status  ovs_set_params(ovs_ctx* ctx, const ovs_params* p);
+ovs_status  ovs_get_params(const ovs_ctx* ctx, ovs_params* p);
+
+/* Chord stable (NoChurn, converged) network: ids sorted ascending and unique,
+ * xy = 2n doubles (SimpleUnderlay coordinates).  The context builds the
+ * stabilised successor lists and finger tables on the device
+ * (Chord.cc:845-875 fixfingers fixed point). */
+ovs_status  ovs_chord_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n,
+                           const double* xy, uint32_t flags);
+/* Explicit (possibly non-converged) Chord snapshot.  pred[n] (0xFFFFFFFF =
+ * unspecified), succ[n*successorListSize] with nsucc[n] valid entries,
+ * fingers[n*160] by finger position (0xFFFFFFFF = unspecified entry),
+ * deque_size[n] = ChordFingerTable deque size (ChordFingerTable.cc:61-87). */
+ovs_status  ovs_chord_load_tables(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n,
+                                  const double* xy, const uint32_t* pred, const uint32_t* succ,
+                                  const uint8_t* nsucc, const uint32_t* fingers,
+                                  const uint8_t* deque_size, uint32_t flags);
+/* Kademlia snapshot (DESIGN.md "Kademlia snapshot rule"), built on the device. */
+ovs_status  ovs_kad_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n,
+                         const double* xy, uint32_t flags);
+/* copy the device Kademlia tables out (host buffers): siblings[n*5s],
+ * bucket_count[n*160], bucket_nodes[n*160*k] (0xFFFFFFFF padded) */
+ovs_status  ovs_kad_export(ovs_ctx* ctx, uint32_t* siblings, uint8_t* bucket_count,
+                           uint32_t* bucket_nodes);
+/* copy the resolved Chord finger table out: out[n*160] = getFinger(pos) */
+ovs_status  ovs_chord_export_fingers(ovs_ctx* ctx, uint32_t* out);
+
+/* Batched iterative lookups: lookup i routes keys[i] from node src[i]
+ * (KBRTestApp one-way test: createDestKey -> callRoute -> sendToKey ->
+ * IterativeLookup -> sendRouteMessage).  hop_seq may be NULL, else
+ * n*hopCountMax node indices (accepted responders in order, 0xFFFFFFFF padded).
+ * rpcs may be NULL, else n FindNodeCall counts. */
+ovs_status  ovs_route_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
+                            uint64_t n, ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs,
+                            uint32_t flags, void* stream);
+
+/* Batched responder step: for each i, findNode(keys[i], numRedundantNodes,
+ * numSiblings) evaluated at node[i] and the findNodeRpc siblings flag
+ * isSiblingFor(node[i], keys[i], numSiblings).  out_nodes has max_out slots per
+ * query (0xFFFFFFFF padded), out_count the result size. */
+ovs_status  ovs_find_node_batch(ovs_ctx* ctx, const uint32_t* node, const ovs_key160* keys,
+                                uint64_t n, int32_t numRedundantNodes, int32_t numSiblings,
+                                uint32_t* out_nodes, uint32_t max_out, uint8_t* out_count,
+                                uint8_t* out_sibling, uint32_t flags, void* stream);
+
+/* SimpleNodeEntry::calcDelay (idle queues) for n (a,b,bytes) triples, in ns */
+ovs_status  ovs_delay_batch(ovs_ctx* ctx, const uint32_t* a, const uint32_t* b,
+                            const int32_t* bytes, uint64_t n, int64_t* out_ns,
+                            uint32_t flags, void* stream);
+
+ovs_status  ovs_sync(ovs_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OVS_KBR_H */

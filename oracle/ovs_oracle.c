@@ -1,0 +1,1160 @@
+/*
+ * ovs_oracle.c -- CPU restatement of OverSim's iterative KBR lookup path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ovs_oracle.h).  This is the checker for the
+ * MI355X engine; it is never linked into, called by, or used as a fallback of
+ * the product library.
+ *
+ * Layout of this file follows the reference:
+ *   1. OverlayKey on GMP-style 64-bit limbs   (src/common/OverlayKey.cc)
+ *   2. BaseKeySortedVector::add                (src/common/NodeVector.h:381-512)
+ *   3. SimpleUnderlay delay                    (src/underlay/simpleunderlay/SimpleNodeEntry.cc:145-195,
+ *                                               SimpleUDP.cc:320-373)
+ *   4. Chord stable state + routing            (src/overlay/chord/Chord.cc, ChordFingerTable.cc,
+ *                                               ChordSuccessorList.cc)
+ *   5. Kademlia snapshot + routing             (src/overlay/kademlia/Kademlia.cc)
+ *   6. IterativeLookup / IterativePathLookup   (src/common/IterativeLookup.cc) driven by a
+ *      per-lookup future-event list in simulated int64 ns.
+ *
+ * Compile with -ffp-contract=off: the delay arithmetic must round exactly like
+ * the reference's x86-64 build (no FMA contraction).
+ */
+#include "ovs_oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static __thread char g_err[256];
+const char* orc_last_error(void) { return g_err; }
+static void set_err(const char* m) { snprintf(g_err, sizeof g_err, "%s", m); }
+
+/* ===================================================================== */
+/* 1. OverlayKey (OverlayKey.cc) with keyLength=160 => aSize=3 limbs of   */
+/*    64 bits, GMP_MSB_MASK = 2^32-1 (OverlayKey.cc:41-47,143-148).        */
+/* ===================================================================== */
+#define A_SIZE 3
+#define MSB_MASK 0xFFFFFFFFull
+typedef struct { uint64_t key[A_SIZE]; int isUnspec; } OKey;
+
+static OKey ok_from(const orc_key* k)
+{
+    OKey r;
+    r.key[0] = (uint64_t)k->w[0] | ((uint64_t)k->w[1] << 32);
+    r.key[1] = (uint64_t)k->w[2] | ((uint64_t)k->w[3] << 32);
+    r.key[2] = (uint64_t)k->w[4];
+    r.isUnspec = 0;
+    return r;
+}
+static void ok_to(const OKey* k, orc_key* o)
+{
+    o->w[0] = (uint32_t)k->key[0]; o->w[1] = (uint32_t)(k->key[0] >> 32);
+    o->w[2] = (uint32_t)k->key[1]; o->w[3] = (uint32_t)(k->key[1] >> 32);
+    o->w[4] = (uint32_t)k->key[2];
+}
+static void ok_trim(OKey* k) { k->key[A_SIZE - 1] &= MSB_MASK; }           /* 835-838 */
+
+static int g_unspec_cmp = 0;  /* compareTo on unspecified keys -> opp_error (844-845) */
+static int ok_cmp(const OKey* a, const OKey* b)                           /* 842-847: mpn_cmp */
+{
+    if (a->isUnspec || b->isUnspec) { g_unspec_cmp = 1; return 0; }
+    for (int i = A_SIZE - 1; i >= 0; --i) {
+        if (a->key[i] != b->key[i]) return a->key[i] > b->key[i] ? 1 : -1;
+    }
+    return 0;
+}
+static OKey ok_add(OKey a, const OKey* b)                                 /* 247-253 */
+{
+    uint64_t c = 0;
+    for (int i = 0; i < A_SIZE; ++i) {                                     /* mpn_add_n */
+        uint64_t s = a.key[i] + b->key[i];
+        uint64_t c1 = s < a.key[i];
+        uint64_t s2 = s + c;
+        uint64_t c2 = s2 < s;
+        a.key[i] = s2; c = c1 | c2;
+    }
+    ok_trim(&a); a.isUnspec = 0; return a;
+}
+static OKey ok_sub(OKey a, const OKey* b)                                 /* 256-262 */
+{
+    uint64_t br = 0;
+    for (int i = 0; i < A_SIZE; ++i) {                                     /* mpn_sub_n */
+        uint64_t d = a.key[i] - b->key[i];
+        uint64_t b1 = a.key[i] < b->key[i];
+        uint64_t d2 = d - br;
+        uint64_t b2 = d < br;
+        a.key[i] = d2; br = b1 | b2;
+    }
+    ok_trim(&a); a.isUnspec = 0; return a;
+}
+static OKey ok_xor(OKey a, const OKey* b)                                 /* 341-349 */
+{
+    for (int i = 0; i < A_SIZE; ++i) a.key[i] ^= b->key[i];
+    return a;
+}
+#define LT(x, y) (ok_cmp((x), (y)) < 0)
+#define GT(x, y) (ok_cmp((x), (y)) > 0)
+#define LE(x, y) (ok_cmp((x), (y)) <= 0)
+#define GE(x, y) (ok_cmp((x), (y)) >= 0)
+#define EQ(x, y) (ok_cmp((x), (y)) == 0)
+
+static int ok_isBetween(const OKey* x, const OKey* a, const OKey* b)      /* 587-599 */
+{
+    if (x->isUnspec || a->isUnspec || b->isUnspec) return 0;
+    if (EQ(x, a)) return 0;
+    else if (LT(a, b)) return GT(x, a) && LT(x, b);
+    else return GT(x, a) || LT(x, b);
+}
+static int ok_isBetweenR(const OKey* x, const OKey* a, const OKey* b)     /* 602-614 */
+{
+    if (x->isUnspec || a->isUnspec || b->isUnspec) return 0;
+    if (EQ(a, b) && EQ(x, a)) return 1;
+    else if (LE(a, b)) return GT(x, a) && LE(x, b);
+    else return GT(x, a) || LE(x, b);
+}
+static int ok_isBetweenL(const OKey* x, const OKey* a, const OKey* b)     /* 617-629 */
+{
+    if (x->isUnspec || a->isUnspec || b->isUnspec) return 0;
+    if (EQ(a, b) && EQ(x, a)) return 1;
+    else if (LE(a, b)) return GE(x, a) && LT(x, b);
+    else return GE(x, a) || LT(x, b);
+}
+static int ok_isBetweenLR(const OKey* x, const OKey* a, const OKey* b)    /* 632-644 */
+{
+    if (x->isUnspec || a->isUnspec || b->isUnspec) return 0;
+    if (EQ(a, b) && EQ(x, a)) return 1;
+    else if (LE(a, b)) return GE(x, a) && LE(x, b);
+    else return GE(x, a) || LE(x, b);
+}
+static uint32_t ok_getBitRange(const OKey* k, uint32_t p, uint32_t n)     /* 458-474 */
+{
+    int i = p / 64, f = p % 64, f2 = f + (int)n - 64;
+    if ((p + n > 160) || (n > 32)) { set_err("getBitRange: invalid range"); return 0; }
+    uint64_t lo = k->key[i] >> f;
+    uint64_t hi = (f2 > 0) ? (k->key[i + 1] << (64 - f)) : 0;
+    return (uint32_t)((lo | hi) & (((uint32_t)(~0u)) >> (32 - n)));
+}
+static OKey ok_pow2(uint32_t e)                                           /* 704-717 */
+{
+    OKey r; memset(&r, 0, sizeof r);
+    if (e >= 160) { set_err("pow2: exponent >= keyLength"); return r; }
+    r.key[e / 64] = (uint64_t)1 << (e % 64);
+    return r;
+}
+static int ok_log2(const OKey* k)                                         /* 558-578 */
+{
+    int i = A_SIZE - 1;
+    while (i >= 0 && k->key[i] == 0) i--;
+    if (i < 0) return -1;
+    uint64_t j = k->key[i];
+    i *= 64;
+    while (j != 0) { j >>= 1; i++; }
+    return i - 1;
+}
+
+/* public wrappers */
+int orc_key_cmp(const orc_key* a, const orc_key* b) { OKey x = ok_from(a), y = ok_from(b); return ok_cmp(&x, &y); }
+void orc_key_add(const orc_key* a, const orc_key* b, orc_key* out) { OKey x = ok_from(a), y = ok_from(b); x = ok_add(x, &y); ok_to(&x, out); }
+void orc_key_sub(const orc_key* a, const orc_key* b, orc_key* out) { OKey x = ok_from(a), y = ok_from(b); x = ok_sub(x, &y); ok_to(&x, out); }
+void orc_key_xor(const orc_key* a, const orc_key* b, orc_key* out) { OKey x = ok_from(a), y = ok_from(b); x = ok_xor(x, &y); ok_to(&x, out); }
+int orc_key_between(int which, const orc_key* x, const orc_key* a, const orc_key* b, int m)
+{
+    OKey X = ok_from(x), A = ok_from(a), B = ok_from(b);
+    X.isUnspec = (m & 1) != 0; A.isUnspec = (m & 2) != 0; B.isUnspec = (m & 4) != 0;
+    switch (which) {
+    case 0: return ok_isBetween(&X, &A, &B);
+    case 1: return ok_isBetweenR(&X, &A, &B);
+    case 2: return ok_isBetweenL(&X, &A, &B);
+    default: return ok_isBetweenLR(&X, &A, &B);
+    }
+}
+uint32_t orc_key_bit_range(const orc_key* k, uint32_t p, uint32_t n) { OKey x = ok_from(k); return ok_getBitRange(&x, p, n); }
+uint32_t orc_key_shared_prefix(const orc_key* a, const orc_key* b, uint32_t bitsPerDigit) /* 530-555 */
+{
+    OKey x = ok_from(a), y = ok_from(b);
+    if (ok_cmp(&x, &y) == 0) return 160;
+    uint32_t length = 0; int msb = 1;
+    for (int i = A_SIZE - 1; i >= 0; --i) {
+        if (x.key[i] != y.key[i]) {
+            uint64_t d = x.key[i] ^ y.key[i];
+            uint32_t j;
+            if (msb) d <<= (64 - (160 % 64));
+            for (j = 63; d >>= 1; --j);
+            length += j;
+            break;
+        }
+        length += 64;
+        msb = 0;
+    }
+    return length / bitsPerDigit;
+}
+int orc_key_log2(const orc_key* k) { OKey x = ok_from(k); return ok_log2(&x); }
+void orc_key_pow2(uint32_t e, orc_key* out) { OKey x = ok_pow2(e); ok_to(&x, out); }
+
+/* ===================================================================== */
+/* parameters                                                            */
+/* ===================================================================== */
+static void params_common(orc_params* p)
+{
+    memset(p, 0, sizeof *p);
+    p->hopCountMax = 50;
+    p->successorListSize = 8;
+    p->numFingerCandidates = 3;
+    p->k = 8; p->s = 8; p->b = 1;
+    p->lookupRedundantNodes = 1;
+    p->lookupParallelRpcs = 1;
+    p->lookupMerge = 0;
+    p->lookupStrictParallelRpcs = 1;
+    p->lookupVisitOnlyOnce = 1;
+    p->lookupAcceptLateSiblings = 1;
+    p->numSiblings = 1;
+    p->simtimeRound = 1;
+    p->rpcUdpTimeout = 1.5;
+    p->lookupTimeout = 10.0;
+    p->datarate = 10e6;
+    p->accessDelay = 0.0;
+    p->callBytes = 55 + 28;      /* FINDNODECALL_L = 440 bits, CommonMessages.msg:68-69; UDP+IP 28 B SimpleUDP.cc:291 */
+    p->respBaseBytes = 33 + 28;  /* FINDNODERESPONSE_L = 264 + 208c bits, CommonMessages.msg:71-72 */
+    p->respPerNodeBytes = 26;    /* NODEHANDLE_L = 208 bits */
+    p->routeBytes = 158 + 28;    /* BASEROUTE_L 424 + BASEAPPDATA_L 40 + testMsgSize 100 B */
+    p->kadSeed = 0x4b41444dull;
+}
+void orc_params_chord_default(orc_params* p) { params_common(p); }
+void orc_params_kad_default(orc_params* p)
+{
+    params_common(p);
+    p->lookupRedundantNodes = 8;   /* default.ini:186 */
+    p->lookupParallelRpcs = 3;     /* default.ini:188 */
+    p->lookupMerge = 1;            /* default.ini:189 */
+}
+
+/* ===================================================================== */
+/* networks                                                              */
+/* ===================================================================== */
+enum { NET_CHORD = 1, NET_KAD = 2 };
+#define NONE 0xFFFFFFFFu
+
+struct orc_net {
+    int type;
+    uint32_t n;
+    OKey* ids;
+    double* xy;
+    orc_params p;
+    /* Chord */
+    uint32_t* pred;         /* n */
+    uint32_t* succ;         /* n * sls */
+    uint8_t* nsucc;         /* n */
+    uint32_t sls;
+    uint32_t* fdeque;       /* n * 160: deque entry p (p = 159 - pos), NONE = unspecified */
+    uint8_t* fsize;         /* deque size */
+    /* Kademlia */
+    uint32_t* sib;          /* n * 5s, sorted by XOR to self */
+    uint8_t* nsib;
+    uint32_t* bucket;       /* n * 160 * k */
+    uint8_t* bcount;        /* n * 160 */
+};
+
+void orc_net_free(orc_net* net)
+{
+    if (!net) return;
+    free(net->ids); free(net->xy); free(net->pred); free(net->succ); free(net->nsucc);
+    free(net->fdeque); free(net->fsize); free(net->sib); free(net->nsib); free(net->bucket);
+    free(net->bcount); free(net);
+}
+
+static orc_net* net_alloc(int type, const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    orc_net* net = (orc_net*)calloc(1, sizeof *net);
+    net->type = type; net->n = n; net->p = *p;
+    net->ids = (OKey*)malloc(sizeof(OKey) * (size_t)n);
+    for (uint32_t i = 0; i < n; ++i) net->ids[i] = ok_from(&ids[i]);
+    net->xy = (double*)malloc(sizeof(double) * 2 * (size_t)n);
+    memcpy(net->xy, xy, sizeof(double) * 2 * (size_t)n);
+    for (uint32_t i = 1; i < n; ++i) {
+        if (ok_cmp(&net->ids[i - 1], &net->ids[i]) >= 0) {
+            set_err("ids must be sorted ascending and unique");
+            orc_net_free(net);
+            return NULL;
+        }
+    }
+    return net;
+}
+
+/* responsible(key): the node m with key in (pred(m), m] (Chord.cc:422-457) ==
+ * first id >= key, wrapping to ids[0]. */
+static uint32_t ring_responsible(const orc_net* net, const OKey* key)
+{
+    uint32_t lo = 0, hi = net->n;
+    while (lo < hi) {
+        uint32_t mid = lo + (hi - lo) / 2;
+        if (ok_cmp(&net->ids[mid], key) < 0) lo = mid + 1; else hi = mid;
+    }
+    return lo == net->n ? 0 : lo;
+}
+
+/* ---- ChordFingerTable (ChordFingerTable.cc) -------------------------------- */
+static void ft_setFinger(orc_net* net, uint32_t node, uint32_t pos, uint32_t v)   /* 66-87 */
+{
+    uint32_t p = 160 - pos - 1;
+    uint32_t* dq = net->fdeque + (size_t)node * 160;
+    while (net->fsize[node] <= p) dq[net->fsize[node]++] = NONE;
+    dq[p] = v;
+}
+static void ft_removeFinger(orc_net* net, uint32_t node, uint32_t pos)            /* 154-172 */
+{
+    uint32_t p = 160 - pos - 1;
+    if (p >= net->fsize[node]) return;
+    else if (p == (uint32_t)net->fsize[node] - 1) net->fsize[node]--;
+    else net->fdeque[(size_t)node * 160 + p] = NONE;
+}
+static uint32_t succ_get(const orc_net* net, uint32_t node, uint32_t pos)
+{
+    return net->succ[(size_t)node * net->sls + pos];
+}
+static uint32_t ft_getFinger(const orc_net* net, uint32_t node, uint32_t pos)     /* 174-193 */
+{
+    uint32_t p = 160 - pos - 1;
+    const uint32_t* dq = net->fdeque + (size_t)node * 160;
+    uint32_t size = net->fsize[node];
+    if (p >= size) return succ_get(net, node, 0);
+    while (dq[p] == NONE && (p < size - 1)) ++p;
+    if (dq[p] == NONE) return succ_get(net, node, 0);
+    return dq[p];
+}
+
+/* Stable (NoChurn, converged) Chord state:
+ *  - predecessor = previous id on the ring,
+ *  - successor list = next min(successorListSize, n-1) ids (ChordSuccessorList.cc:122-151,
+ *    keyed by succ-(self+1); self evicted once others are known, 170-194),
+ *  - fingers as left by handleFixFingersTimerExpired (Chord.cc:845-875): for
+ *    nextFinger = 0..159, trivial fingers (2^i <= succ - self) are removed, the
+ *    others set to the node answering rpcFixfingers for self+2^i, i.e. the
+ *    responsible node (Chord.cc:1228-1270, non-extended finger table). */
+orc_net* orc_chord_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    if (n < 2) { set_err("chord: need at least 2 nodes"); return NULL; }
+    orc_net* net = net_alloc(NET_CHORD, ids, n, xy, p);
+    if (!net) return NULL;
+    uint32_t sls = (uint32_t)p->successorListSize;
+    net->sls = sls;
+    net->pred = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    net->succ = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sls);
+    net->nsucc = (uint8_t*)malloc(n);
+    net->fdeque = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160);
+    net->fsize = (uint8_t*)calloc(n, 1);
+    uint32_t ns = (n - 1 < sls) ? n - 1 : sls;
+    for (uint32_t i = 0; i < n; ++i) {
+        net->pred[i] = (i + n - 1) % n;
+        net->nsucc[i] = (uint8_t)ns;
+        for (uint32_t j = 0; j < ns; ++j) net->succ[(size_t)i * sls + j] = (i + 1 + j) % n;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const OKey* self = &net->ids[i];
+        OKey d = ok_sub(net->ids[succ_get(net, i, 0)], self);
+        for (uint32_t nf = 0; nf < 160; ++nf) {
+            OKey off = ok_pow2(nf);
+            OKey lk = ok_add(*self, &off);
+            if (ok_cmp(&off, &d) > 0) ft_setFinger(net, i, nf, ring_responsible(net, &lk));
+            else ft_removeFinger(net, i, nf);
+        }
+    }
+    return net;
+}
+
+orc_net* orc_chord_build_tables(const orc_key* ids, uint32_t n, const double* xy,
+                                const uint32_t* pred, const uint32_t* succ, const uint8_t* nsucc,
+                                uint32_t succ_stride, const uint32_t* fingers,
+                                const uint8_t* deque_size, const orc_params* p)
+{
+    orc_net* net = net_alloc(NET_CHORD, ids, n, xy, p);
+    if (!net) return NULL;
+    net->sls = succ_stride;
+    net->pred = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    net->succ = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * succ_stride);
+    net->nsucc = (uint8_t*)malloc(n);
+    net->fdeque = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160);
+    net->fsize = (uint8_t*)malloc(n);
+    memcpy(net->pred, pred, sizeof(uint32_t) * n);
+    memcpy(net->succ, succ, sizeof(uint32_t) * (size_t)n * succ_stride);
+    memcpy(net->nsucc, nsucc, n);
+    memcpy(net->fsize, deque_size, n);
+    for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t pos = 0; pos < 160; ++pos)
+            net->fdeque[(size_t)i * 160 + (160 - pos - 1)] = fingers[(size_t)i * 160 + pos];
+    return net;
+}
+
+void orc_chord_export_fingers(const orc_net* net, uint32_t* out)
+{
+    for (uint32_t i = 0; i < net->n; ++i)
+        for (uint32_t pos = 0; pos < 160; ++pos) out[(size_t)i * 160 + pos] = ft_getFinger(net, i, pos);
+}
+
+/* ---- NodeVector / BaseKeySortedVector::add (NodeVector.h:381-512) ----------- */
+typedef struct {
+    uint32_t v[128];
+    int size;
+    int maxSize;            /* 0 = unbounded */
+    int metric;             /* 0 none (push only), 1 XOR, 2 uni-ring (Chord::distance) */
+    OKey rel;               /* relative key of the comparator */
+} NVec;
+
+static OKey metric_dist(int metric, const OKey* x, const OKey* key)
+{
+    if (metric == 1) return ok_xor(*x, key);              /* KeyXorMetric, Comparator.h:90-106 */
+    return ok_sub(*key, x);                               /* KeyUniRingMetric: y - x, Comparator.h:137-153 */
+}
+static int nv_compare(const orc_net* net, const NVec* nv, uint32_t a, uint32_t b) /* Comparator.h:193-222 */
+{
+    OKey da = metric_dist(nv->metric, &net->ids[a], &nv->rel);
+    OKey db = metric_dist(nv->metric, &net->ids[b], &nv->rel);
+    return ok_cmp(&da, &db);
+}
+static void nv_init(NVec* nv, int maxSize, int metric, const OKey* rel)
+{
+    nv->size = 0; nv->maxSize = maxSize; nv->metric = metric;
+    if (rel) nv->rel = *rel; else memset(&nv->rel, 0, sizeof nv->rel);
+}
+static int nv_isFull(const NVec* nv) { return nv->maxSize != 0 && nv->size == nv->maxSize; }
+static int nv_isAddable(const orc_net* net, const NVec* nv, uint32_t e)          /* 381-399 */
+{
+    if (nv->maxSize == 0) return 1;
+    return nv->size != nv->maxSize || (nv->metric && nv_compare(net, nv, e, nv->v[nv->size - 1]) <= 0);
+}
+static void nv_push_back(NVec* nv, uint32_t e) { if (nv->size < 128) nv->v[nv->size++] = e; }
+static int nv_add(const orc_net* net, NVec* nv, uint32_t e)                      /* 432-512 */
+{
+    int pos = -1;
+    if (!nv_isAddable(net, nv, e)) return -1;
+    if (nv->size != 0 && nv->metric) {
+        int i;
+        for (i = 0, pos = 0; i < nv->size; i++, pos++) {
+            if (EQ(&net->ids[e], &net->ids[nv->v[i]])) return -1;
+            if (nv_compare(net, nv, e, nv->v[i]) < 0) {
+                memmove(&nv->v[i + 1], &nv->v[i], sizeof(uint32_t) * (size_t)(nv->size - i));
+                nv->v[i] = e; nv->size++;
+                break;
+            }
+        }
+        if (i == nv->size && pos == nv->size) { /* reached end without insert */
+            pos = nv->size;
+            nv_push_back(nv, e);
+        }
+    } else {
+        for (int i = 0; i < nv->size; i++)
+            if (EQ(&net->ids[e], &net->ids[nv->v[i]])) return -1;
+        pos = nv->size;
+        nv_push_back(nv, e);
+    }
+    if (nv->maxSize != 0 && nv->size > nv->maxSize) nv->size = nv->maxSize;
+    return pos;
+}
+static void nv_downsizeTo(NVec* nv, int m) { if (nv->size > m) nv->size = m; }  /* 566-571 */
+static int nv_contains(const orc_net* net, const NVec* nv, const OKey* key)
+{
+    for (int i = 0; i < nv->size; ++i) if (EQ(&net->ids[nv->v[i]], key)) return 1;
+    return 0;
+}
+
+/* ---- Chord routing (Chord.cc) ------------------------------------------------ */
+static int chord_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self,
+                              const OKey* key, int numSiblings, int* err)          /* 422-500 */
+{
+    /* state == READY; numSiblings <= successorListSize asserted by caller */
+    if (numSiblings == -1) numSiblings = net->p.successorListSize;
+    uint32_t pred = net->pred[self];
+    int predUnspec = (pred == NONE);
+    int ssize = net->nsucc[self];
+    if (predUnspec && node == self) {
+        int isEmpty = (ssize == 1 && succ_get(net, self, 0) == self) || ssize == 0;
+        if (isEmpty || EQ(&net->ids[node], key)) { *err = 0; return 1; }
+        *err = 1; return 0;
+    }
+    if (node == self && ok_isBetweenR(key, &net->ids[pred], &net->ids[self])) { *err = 0; return 1; }
+    uint32_t prevNode = pred, curNode;
+    for (int i = -1; i < ssize; i++, prevNode = curNode) {
+        curNode = (i < 0) ? self : succ_get(net, self, (uint32_t)i);
+        if (node == curNode) {
+            OKey prevKey = (prevNode == NONE) ? (OKey){{0, 0, 0}, 1} : net->ids[prevNode];
+            if (ok_isBetweenR(key, &prevKey, &net->ids[curNode])) {
+                if (numSiblings <= (ssize - i)) { *err = 0; return 1; }
+                *err = 1; return 0;
+            } else {
+                if (numSiblings <= 1) { *err = 0; return 0; }
+                *err = 1; return 0;
+            }
+        }
+    }
+    *err = 1;
+    return 0;
+}
+
+static int chord_closestPreceedingNode(const orc_net* net, uint32_t self, const OKey* key, NVec* out) /* 602-674 */
+{
+    uint32_t temp = NONE;
+    int ssize = net->nsucc[self];
+    for (int j = ssize - 1; j >= 0; j--) {
+        uint32_t s = succ_get(net, self, (uint32_t)j);
+        if (ok_isBetweenR(&net->ids[s], &net->ids[self], key)) { temp = s; break; }
+    }
+    if (temp == NONE) { set_err("Chord::closestPreceedingNode(): Successor list broken"); return -1; }
+    for (int i = 160 - 1; i >= 0; i--) {
+        uint32_t f = ft_getFinger(net, self, (uint32_t)i);
+        if (ok_isBetweenLR(&net->ids[f], &net->ids[temp], key)) {   /* !extendedFingerTable */
+            nv_push_back(out, f);
+            return 0;
+        }
+    }
+    for (int i = ssize - 1; i >= 0 && out->size <= net->p.numFingerCandidates; i--) {
+        uint32_t s = succ_get(net, self, (uint32_t)i);
+        if (ok_isBetween(&net->ids[s], &net->ids[self], key)) nv_push_back(out, s);
+    }
+    if (out->size != 0) return 0;
+    if (net->pred[self] == NONE && succ_get(net, self, 0) == self) { nv_push_back(out, self); return 0; }
+    set_err("Error in Chord::closestPreceedingNode()!");
+    return -1;
+}
+
+static int chord_findNode(const orc_net* net, uint32_t self, const OKey* key,
+                          int numRedundantNodes, int numSiblings, NVec* out)       /* 548-599 */
+{
+    int err;
+    nv_init(out, 0, 0, NULL);
+    if (key->isUnspec) { nv_push_back(out, self); return 0; }
+    if (chord_isSiblingFor(net, self, self, key, 1, &err)) {
+        nv_push_back(out, self);
+        for (int i = 0; i < net->nsucc[self]; i++) nv_push_back(out, succ_get(net, self, (uint32_t)i));
+        nv_downsizeTo(out, numSiblings);
+    } else if (ok_isBetweenR(key, &net->ids[self], &net->ids[succ_get(net, self, 0)])) {
+        for (int i = 0; i < net->nsucc[self]; i++) nv_push_back(out, succ_get(net, self, (uint32_t)i));
+        nv_downsizeTo(out, numRedundantNodes);
+    } else {
+        if (chord_closestPreceedingNode(net, self, key, out) < 0) return -1;
+        nv_downsizeTo(out, numRedundantNodes);
+    }
+    return 0;
+}
+
+/* ---- Kademlia (Kademlia.cc) -------------------------------------------------- */
+static int kad_routingBucketIndex(const orc_net* net, uint32_t self, const OKey* key, int firstOnLayer) /* 357-382 */
+{
+    int b = net->p.b;
+    OKey delta = ok_xor(*key, &net->ids[self]);
+    int i;
+    for (i = 160 - b; i >= 0 && ok_getBitRange(&delta, (uint32_t)i, (uint32_t)b) == 0; i -= b);
+    if (i < 0) return -1;
+    if (!firstOnLayer) return (i / b) * ((1 << b) - 1) + (int)(ok_getBitRange(&delta, (uint32_t)i, (uint32_t)b) - 1);
+    return (i / b) * ((1 << b) - 1) + (int)(pow(2, b) - 2);
+}
+
+static int kad_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self, const OKey* key,
+                            int numSiblings, int* err)                              /* 888-962 */
+{
+    int sibCap = 5 * net->p.s;
+    if (numSiblings == -1) numSiblings = net->p.s;
+    if (numSiblings == 0) { *err = 0; return EQ(&net->ids[node], key); }
+    int nsib = net->nsib[self];
+    const uint32_t* sib = net->sib + (size_t)self * sibCap;
+    if (nsib < numSiblings) { *err = 0; return 1; }
+    if (nsib == sibCap) {
+        OKey a = ok_xor(net->ids[self], key);
+        OKey b = ok_xor(net->ids[self], &net->ids[sib[nsib - 1]]);
+        if (ok_cmp(&a, &b) > 0) { *err = 1; return 0; }
+    }
+    NVec result; nv_init(&result, numSiblings, 1, key);
+    for (int i = 0; i < nsib; i++) nv_add(net, &result, sib[i]);
+    nv_add(net, &result, self);
+    *err = 0;
+    return nv_contains(net, &result, &net->ids[node]);
+}
+
+static int kad_findNode(const orc_net* net, uint32_t self, const OKey* key,
+                        int numRedundantNodes, int numSiblings, NVec* result)       /* 1101-1246 */
+{
+    int err, resultSize;
+    int k = net->p.k, sibCap = 5 * net->p.s;
+    if (numSiblings < 0) resultSize = numRedundantNodes;
+    else resultSize = kad_isSiblingFor(net, self, self, key, numSiblings, &err) ?
+                      (numSiblings ? numSiblings : 1) : numRedundantNodes;
+    nv_init(result, resultSize, 1, key);
+    int nsib = net->nsib[self];
+    const uint32_t* sib = net->sib + (size_t)self * sibCap;
+    if (nsib == 0) { nv_add(net, result, self); return 0; }
+    int mainIndex = kad_routingBucketIndex(net, self, key, 0);
+    int startIndex = kad_routingBucketIndex(net, self, key, 1);
+    int endIndex = kad_routingBucketIndex(net, self, &net->ids[sib[nsib - 1]], 0);
+    const uint8_t* bc = net->bcount + (size_t)self * 160;
+    const uint32_t* bk = net->bucket + (size_t)self * 160 * k;
+    if (mainIndex != -1) {
+        for (int i = 0; i < bc[mainIndex]; ++i) nv_add(net, result, bk[(size_t)mainIndex * k + i]);
+    }
+    if (startIndex >= endIndex || !nv_isFull(result)) {
+        for (int index = startIndex; index >= endIndex; --index) {
+            if (index == mainIndex) continue;
+            for (int i = 0; i < bc[index]; ++i) nv_add(net, result, bk[(size_t)index * k + i]);
+        }
+        for (int i = 0; i < nsib; ++i) nv_add(net, result, sib[i]);
+        nv_add(net, result, self);
+    }
+    for (int index = mainIndex + 1; !nv_isFull(result) && index < 160; ++index)
+        for (int i = 0; i < bc[index]; ++i) nv_add(net, result, bk[(size_t)index * k + i]);
+    return 0;
+}
+
+/* Kademlia snapshot rule: sibling table = the min(5s, n-1) XOR-closest
+ * nodes (what routingAdd, Kademlia.cc:537-616, converges to), buckets hold up to k
+ * of the remaining nodes of each subtree, chosen by Floyd sampling driven by
+ * splitmix64(seed, node, bucket, j); bucket order is irrelevant to findNode since
+ * the result NodeVector is XOR-sorted and XOR distances are unique. */
+static uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+static uint64_t kad_hash(uint64_t seed, uint32_t node, uint32_t m, uint32_t j)
+{
+    return splitmix64(seed ^ splitmix64(((uint64_t)node << 32) ^ ((uint64_t)m << 16) ^ (uint64_t)j));
+}
+/* index range of ids sharing the top (159-m) bits of `key` with bit m flipped */
+static void subtree_range(const orc_net* net, const OKey* key, int m, uint32_t* lo, uint32_t* hi)
+{
+    /* prefix block: bits > m equal key's, bit m = !key bit m, bits < m free */
+    OKey base = *key;
+    int li = m / 64, bi = m % 64;
+    base.key[li] ^= (uint64_t)1 << bi;
+    /* clear bits below m */
+    for (int i = 0; i < li; ++i) base.key[i] = 0;
+    base.key[li] &= ~(((uint64_t)1 << bi) - 1);
+    OKey top = base;
+    for (int i = 0; i < li; ++i) top.key[i] = ~0ull;
+    top.key[li] |= (((uint64_t)1 << bi) - 1);
+    ok_trim(&top);
+    /* lower_bound(base), upper_bound(top) */
+    uint32_t a = 0, b = net->n;
+    while (a < b) { uint32_t mid = a + (b - a) / 2; if (ok_cmp(&net->ids[mid], &base) < 0) a = mid + 1; else b = mid; }
+    *lo = a;
+    b = net->n;
+    while (a < b) { uint32_t mid = a + (b - a) / 2; if (ok_cmp(&net->ids[mid], &top) <= 0) a = mid + 1; else b = mid; }
+    *hi = a;
+}
+
+orc_net* orc_kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    if (p->b != 1) { set_err("kademlia: only b=1 supported"); return NULL; }
+    orc_net* net = net_alloc(NET_KAD, ids, n, xy, p);
+    if (!net) return NULL;
+    int k = p->k, sibCap = 5 * p->s;
+    net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
+    net->nsib = (uint8_t*)calloc(n, 1);
+    net->bucket = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160 * k);
+    net->bcount = (uint8_t*)calloc((size_t)n * 160, 1);
+    for (uint32_t i = 0; i < (size_t)n * sibCap; ++i) net->sib[i] = NONE;
+    for (uint32_t self = 0; self < n; ++self) {
+        /* sibling table: walk subtrees m = 0.. upward, gather members, keep 5s closest */
+        NVec sib; nv_init(&sib, sibCap, 1, &net->ids[self]);
+        int m;
+        for (m = 0; m < 160; ++m) {
+            uint32_t lo, hi;
+            subtree_range(net, &net->ids[self], m, &lo, &hi);
+            for (uint32_t x = lo; x < hi; ++x) nv_add(net, &sib, x);
+            if (nv_isFull(&sib)) break;   /* all later subtrees are farther (XOR >= 2^(m+1)) */
+        }
+        net->nsib[self] = (uint8_t)sib.size;
+        memcpy(net->sib + (size_t)self * sibCap, sib.v, sizeof(uint32_t) * (size_t)sib.size);
+        /* buckets */
+        for (m = 0; m < 160; ++m) {
+            uint32_t lo, hi;
+            subtree_range(net, &net->ids[self], m, &lo, &hi);
+            if (hi <= lo) continue;
+            /* members not in the sibling table, in ascending id order */
+            uint32_t cnt = hi - lo;
+            uint32_t nsib_in = 0;
+            for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] >= lo && sib.v[s2] < hi) nsib_in++;
+            uint32_t c = cnt - nsib_in;
+            uint32_t* dst = net->bucket + ((size_t)self * 160 + m) * k;
+            uint32_t chosen[64]; int nch = 0;
+            if (c <= (uint32_t)k) {
+                for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
+            } else {
+                for (uint32_t j = c - (uint32_t)k; j < c; ++j) {       /* Floyd sampling */
+                    uint32_t t = (uint32_t)(kad_hash(p->kadSeed, self, (uint32_t)m, j) % (uint64_t)(j + 1));
+                    int dup = 0;
+                    for (int q = 0; q < nch; ++q) if (chosen[q] == t) { dup = 1; break; }
+                    chosen[nch++] = dup ? j : t;
+                }
+                /* ascending member order */
+                for (int a = 1; a < nch; ++a) { uint32_t v = chosen[a]; int q = a - 1; while (q >= 0 && chosen[q] > v) { chosen[q + 1] = chosen[q]; q--; } chosen[q + 1] = v; }
+            }
+            /* map member rank -> node index (skipping siblings) */
+            int out = 0;
+            if (nsib_in == 0) {
+                for (int q = 0; q < nch; ++q) dst[out++] = lo + chosen[q];
+            } else {
+                uint32_t rank = 0; int q = 0;
+                for (uint32_t x = lo; x < hi && q < nch; ++x) {
+                    int is_sib = 0;
+                    for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] == x) { is_sib = 1; break; }
+                    if (is_sib) continue;
+                    if (rank == chosen[q]) { dst[out++] = x; q++; }
+                    rank++;
+                }
+            }
+            net->bcount[(size_t)self * 160 + m] = (uint8_t)out;
+        }
+    }
+    return net;
+}
+
+void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes)
+{
+    size_t sc = (size_t)5 * net->p.s, k = (size_t)net->p.k;
+    memcpy(siblings, net->sib, sizeof(uint32_t) * net->n * sc);
+    memcpy(bucket_count, net->bcount, (size_t)net->n * 160);
+    for (size_t i = 0; i < (size_t)net->n * 160; ++i)
+        for (size_t j = 0; j < k; ++j)
+            bucket_nodes[i * k + j] = j < net->bcount[i] ? net->bucket[i * k + j] : NONE;
+}
+
+/* ---- overlay dispatch ---------------------------------------------------------- */
+static int ov_findNode(const orc_net* net, uint32_t self, const OKey* key, int nr, int ns, NVec* out)
+{
+    if (net->type == NET_CHORD) return chord_findNode(net, self, key, nr, ns, out);
+    return kad_findNode(net, self, key, nr, ns, out);
+}
+static int ov_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self, const OKey* key, int ns, int* err)
+{
+    if (net->type == NET_CHORD) return chord_isSiblingFor(net, node, self, key, ns, err);
+    return kad_isSiblingFor(net, node, self, key, ns, err);
+}
+static int ov_maxRedundant(const orc_net* net)
+{
+    return net->type == NET_CHORD ? 1 : net->p.k;   /* Chord.cc:416-419 (!extendedFingerTable), Kademlia.cc:352-355 */
+}
+
+int orc_find_node(const orc_net* net, uint32_t node, const orc_key* key, int numRedundantNodes,
+                  int numSiblings, uint32_t* out, int* sibling_flag)
+{
+    OKey k = ok_from(key);
+    NVec v;
+    int err = 0;
+    if (ov_findNode(net, node, &k, numRedundantNodes, numSiblings, &v) < 0) return -1;
+    for (int i = 0; i < v.size && i < 64; ++i) out[i] = v.v[i];
+    *sibling_flag = ov_isSiblingFor(net, node, node, &k, numSiblings, &err);
+    return v.size;
+}
+
+/* ===================================================================== */
+/* 3. SimpleUnderlay delay                                               */
+/* ===================================================================== */
+static int64_t simtime(double d, int rnd)       /* SimTime(double) at simtime-scale -9 (default.ini:27) */
+{
+    double x = d * 1e9;
+    return rnd ? (int64_t)floor(x + 0.5) : (int64_t)x;
+}
+float orc_coord_dist(const orc_net* net, uint32_t a, uint32_t b)                 /* SimpleNodeEntry.cc:145-153 */
+{
+    double sum_of_squares = 0;
+    for (int i = 0; i < 2; i++) {
+        double d = net->xy[2 * (size_t)a + i] - net->xy[2 * (size_t)b + i];
+        sum_of_squares += d * d;                  /* pow(d, 2) == d*d */
+    }
+    return (float)sqrt(sum_of_squares);
+}
+/* calcDelay with the sender's tx.finished state (SimpleNodeEntry.cc:155-195) */
+static int64_t calc_delay(const orc_net* net, uint32_t a, uint32_t b, int32_t bytes,
+                          int64_t now, int64_t* txFinished)
+{
+    if (a == b) return 0;                                                          /* SimpleUDP.cc:322 */
+    const orc_params* p = &net->p;
+    int64_t bw = simtime((double)((int64_t)bytes * 8) / p->datarate, p->simtimeRound);
+    int64_t newTx = (*txFinished > now ? *txFinished : now) + bw;
+    *txFinished = newTx;
+    int64_t access = simtime(p->accessDelay, p->simtimeRound);
+    int64_t destBw = simtime((double)((int64_t)bytes * 8) / p->datarate, p->simtimeRound);
+    int64_t coord = simtime(0.001 * (double)orc_coord_dist(net, a, b), p->simtimeRound);
+    return (newTx - now) + access + coord + destBw + access;
+}
+int64_t orc_delay_ns(const orc_net* net, uint32_t a, uint32_t b, int32_t bytes)
+{
+    int64_t tx = 0;
+    return calc_delay(net, a, b, bytes, 0, &tx);
+}
+
+/* ===================================================================== */
+/* 6. IterativeLookup restatement (parallelPaths = 1, ITERATIVE_ROUTING, */
+/*    no verify/majority siblings, failedNodeRpcs = false).              */
+/* ===================================================================== */
+#define MAXRPC 256
+#define MAXNH 64
+
+typedef struct { uint32_t handle; int alreadyUsed; } LEntry;
+
+typedef struct {
+    uint32_t node;          /* destination */
+    int active;             /* in rpcs map / pending events */
+    int64_t tResp, tTimeout, tIns;
+    uint64_t seqResp, seqTimeout;
+    int nInfo;
+    int vrpcId[8];          /* RpcInfoVector (one path) */
+} Rpc;
+
+typedef struct {
+    const orc_net* net;
+    OKey key;
+    uint32_t S;
+    int numSiblings, hopCountMax;
+    /* lookup */
+    int finished, success, running;
+    int64_t startTime, now, txFinished;
+    uint32_t siblings[16]; int nsiblings;
+    uint32_t* visited; int nvisited, capVisited;
+    uint32_t dead[MAXRPC]; int ndead;
+    int finishedPaths, successfulPaths, minHops;
+    Rpc rpcs[MAXRPC]; int nrpcs;
+    uint64_t seq;
+    /* path */
+    LEntry nh[MAXNH]; int nnh;
+    int hops, step, pendingRpcs, pfinished, psuccess;
+    /* outputs */
+    uint32_t* hopseq; int nhop;
+    uint32_t rpcsSent;
+} Lookup;
+
+static int lk_getVisited(Lookup* L, uint32_t n)
+{
+    for (int i = 0; i < L->nvisited; ++i) if (L->visited[i] == n) return 1;
+    return 0;
+}
+static void lk_setVisited(Lookup* L, uint32_t n)
+{
+    if (lk_getVisited(L, n)) return;
+    if (L->nvisited == L->capVisited) {
+        L->capVisited = L->capVisited ? 2 * L->capVisited : 64;
+        L->visited = (uint32_t*)realloc(L->visited, sizeof(uint32_t) * (size_t)L->capVisited);
+    }
+    L->visited[L->nvisited++] = n;
+}
+static int lk_getDead(Lookup* L, uint32_t n)
+{
+    for (int i = 0; i < L->ndead; ++i) if (L->dead[i] == n) return 1;
+    return 0;
+}
+static Rpc* lk_findRpc(Lookup* L, uint32_t n)
+{
+    for (int i = 0; i < L->nrpcs; ++i) if (L->rpcs[i].active && L->rpcs[i].node == n) return &L->rpcs[i];
+    return NULL;
+}
+static int lk_activeRpcs(Lookup* L)
+{
+    int c = 0;
+    for (int i = 0; i < L->nrpcs; ++i) c += L->rpcs[i].active;
+    return c;
+}
+
+/* LookupVector comparator: IterativeLookup::compare -> overlay->distance(., key) (IterativeLookup.cc:397-400) */
+static int lv_compare(Lookup* L, uint32_t a, uint32_t b)
+{
+    int metric = L->net->type == NET_CHORD ? 2 : 1;
+    OKey da = metric_dist(metric, &L->net->ids[a], &L->key);
+    OKey db = metric_dist(metric, &L->net->ids[b], &L->key);
+    return ok_cmp(&da, &db);
+}
+/* LookupVector::add (BaseKeySortedVector::add with LookupEntry, cap = redundantNodes) */
+static int lv_add(Lookup* L, uint32_t h)
+{
+    int maxSize = L->net->p.lookupRedundantNodes;
+    if (!(L->nnh != maxSize || lv_compare(L, h, L->nh[L->nnh - 1].handle) <= 0)) return -1;
+    int pos = -1, i;
+    if (L->nnh != 0) {
+        for (i = 0, pos = 0; i < L->nnh; i++, pos++) {
+            if (EQ(&L->net->ids[h], &L->net->ids[L->nh[i].handle])) return -1;
+            if (lv_compare(L, h, L->nh[i].handle) < 0) {
+                memmove(&L->nh[i + 1], &L->nh[i], sizeof(LEntry) * (size_t)(L->nnh - i));
+                L->nh[i].handle = h; L->nh[i].alreadyUsed = 0; L->nnh++;
+                break;
+            }
+        }
+        if (i == L->nnh && pos == L->nnh) { pos = L->nnh; L->nh[L->nnh].handle = h; L->nh[L->nnh].alreadyUsed = 0; L->nnh++; }
+    } else {
+        pos = 0; L->nh[0].handle = h; L->nh[0].alreadyUsed = 0; L->nnh = 1;
+    }
+    if (L->nnh > maxSize) L->nnh = maxSize;
+    return pos;
+}
+static int path_add(Lookup* L, uint32_t h)                                       /* 1184-1195 */
+{
+    if (L->net->p.lookupMerge) return lv_add(L, h);
+    if (L->nnh < MAXNH) { L->nh[L->nnh].handle = h; L->nh[L->nnh].alreadyUsed = 0; L->nnh++; }
+    return L->nnh - 1;
+}
+
+static void lk_addSibling(Lookup* L, uint32_t h)                                /* 406-449 */
+{
+    /* numSiblings != 0, parallelPaths == 1, !verifySiblings -> push_back if not full */
+    int cap = L->numSiblings == 0 ? 1 : L->numSiblings;
+    if (L->numSiblings == 0) {
+        if (EQ(&L->net->ids[h], &L->key)) { L->siblings[0] = h; L->nsiblings = 1; }
+        return;
+    }
+    if (L->nsiblings < cap) L->siblings[L->nsiblings++] = h;
+}
+
+/* IterativeLookup::sendRpc (656-689) + BaseRpc::sendRpcCall timeout (BaseRpc.cc:173-253) */
+static void lk_sendRpc(Lookup* L, uint32_t handle, int rpcId)
+{
+    if (L->finished || !L->running) return;
+    Rpc* r = lk_findRpc(L, handle);
+    if (!r) {
+        if (L->nrpcs == MAXRPC) { set_err("too many rpcs"); return; }
+        r = &L->rpcs[L->nrpcs++];
+        memset(r, 0, sizeof *r);
+        r->node = handle; r->active = 1;
+        const orc_params* p = &L->net->p;
+        r->tTimeout = L->now + simtime(p->rpcUdpTimeout, p->simtimeRound);
+        r->seqTimeout = L->seq++;
+        /* the call travels S -> handle, the responder answers at once */
+        int64_t d1 = calc_delay(L->net, L->S, handle, p->callBytes, L->now, &L->txFinished);
+        int64_t tArr = L->now + d1;
+        NVec res; int sflag, err;
+        ov_findNode(L->net, handle, &L->key, p->lookupRedundantNodes, L->numSiblings, &res);
+        sflag = ov_isSiblingFor(L->net, handle, handle, &L->key, L->numSiblings, &err);
+        (void)sflag;
+        int64_t respTx = 0;   /* responder's tx queue idle */
+        int64_t d2 = calc_delay(L->net, handle, L->S, p->respBaseBytes + p->respPerNodeBytes * res.size, tArr, &respTx);
+        r->tResp = tArr + d2;
+        r->tIns = tArr;
+        r->seqResp = L->seq++;
+        L->rpcsSent++;
+    }
+    if (r->nInfo < 8) r->vrpcId[r->nInfo++] = rpcId;
+}
+
+static void path_sendRpc(Lookup* L, int num)                                     /* 1067-1170 */
+{
+    const orc_params* p = &L->net->p;
+    if (L->pfinished) return;
+    if (L->hopCountMax && (L->hops >= L->hopCountMax)) { L->pfinished = 1; L->psuccess = 0; return; }
+    if (p->lookupStrictParallelRpcs) num = num < (p->lookupParallelRpcs - L->pendingRpcs) ? num : (p->lookupParallelRpcs - L->pendingRpcs);
+    if ((num == 0) && (L->pendingRpcs == 0) && !p->lookupFinishOnFirstUnchanged) num = p->lookupParallelRpcs;
+    for (int i = 0; num > 0 && i < p->lookupRedundantNodes; i++) {
+        LEntry* it = NULL;
+        for (int q = 0; q < L->nnh; ++q) {                                       /* getNextEntry 1172-1182 */
+            if (L->nh[q].alreadyUsed || lk_getDead(L, L->nh[q].handle)) continue;
+            it = &L->nh[q]; break;
+        }
+        if (it == NULL) break;
+        if (!p->lookupVisitOnlyOnce || !lk_getVisited(L, it->handle)) {
+            L->pendingRpcs++;
+            num--;
+            lk_sendRpc(L, it->handle, L->step);
+        }
+        it->alreadyUsed = 1;
+    }
+    if (L->pendingRpcs == 0) { L->psuccess = 0; L->pfinished = 1; }
+}
+
+static void path_sendNewRpcAfterTimeout(Lookup* L)                               /* 923-933 */
+{
+    if (L->net->p.lookupNewRpcOnEveryTimeout) path_sendRpc(L, 1);
+    else if (L->pendingRpcs == 0) path_sendRpc(L, L->net->p.lookupParallelRpcs);
+}
+
+static void path_handleTimeout(Lookup* L)                                        /* 935-1023 */
+{
+    if (L->pfinished) return;
+    L->pendingRpcs--;
+    if (L->now > L->startTime + simtime(L->net->p.lookupTimeout, L->net->p.simtimeRound)) {
+        L->pfinished = 1; L->psuccess = 0; return;
+    }
+    path_sendNewRpcAfterTimeout(L);   /* failedNodeRpcs = false */
+}
+
+static int path_accepts(Lookup* L, int rpcId)                                    /* 786-801 */
+{
+    if (L->pfinished) return 0;
+    if (L->net->p.lookupUseAllParallelResponses && L->net->p.lookupMerge) return 1;
+    return rpcId == L->step;
+}
+
+static void path_handleResponse(Lookup* L, uint32_t source, const NVec* closest, int siblingsFlag) /* 803-921 */
+{
+    const orc_params* p = &L->net->p;
+    if (L->pfinished) return;
+    if (L->now > L->startTime + simtime(p->lookupTimeout, p->simtimeRound)) { L->pfinished = 1; L->psuccess = 0; return; }
+    if (source != L->S) {
+        L->hops++;
+        if (L->hopseq && L->nhop < L->hopCountMax) L->hopseq[L->nhop] = source;
+        L->nhop++;
+    }
+    lk_setVisited(L, source);
+    L->step++;
+    L->pendingRpcs--;
+    if (closest->size != 0 && !p->lookupMerge) L->nnh = 0;
+    int numNewRpcs = 0;
+    for (int i = 0; i < closest->size; i++) {
+        uint32_t h = closest->v[i];
+        int pos = path_add(L, h);
+        if ((pos >= 0) && (pos < p->lookupRedundantNodes)) numNewRpcs++;
+        if ((L->numSiblings == 0) && EQ(&L->net->ids[h], &L->key)) {
+            lk_addSibling(L, h);
+            L->pfinished = 1; L->psuccess = 1; return;
+        } else if (L->numSiblings != 0 && siblingsFlag) {
+            lk_addSibling(L, h);
+        }
+    }
+    if (siblingsFlag && closest->size != 0 && L->numSiblings != 0) { L->pfinished = 1; L->psuccess = 1; return; }
+    if ((numNewRpcs == 0) && p->lookupNewRpcOnEveryResponse) numNewRpcs = 1;
+    path_sendRpc(L, numNewRpcs < p->lookupParallelRpcs ? numNewRpcs : p->lookupParallelRpcs);
+}
+
+static void lk_countFinished(Lookup* L)
+{
+    if (L->pfinished) {
+        L->finishedPaths++;
+        if (L->hops < L->minHops) L->minHops = L->hops;
+        if (L->psuccess) L->successfulPaths++;
+    }
+}
+
+/* checkStop (295-349) with parallelPaths = 1, numSiblings > 0 */
+static int lk_checkStop(Lookup* L)
+{
+    int finishLookup = 0;
+    if ((L->successfulPaths >= 1 && L->numSiblings == 0 && L->nsiblings >= 1) ||
+        (L->finishedPaths == 1 && L->numSiblings > 0)) {
+        L->success |= L->psuccess;
+        finishLookup = 1;
+    } else if (lk_activeRpcs(L) == 0) {
+        finishLookup = 1;
+    }
+    if (finishLookup) {
+        if (L->successfulPaths >= 1) L->success = 1;
+        L->success |= L->psuccess;   /* stop(): success |= paths[i]->success */
+        L->running = 0; L->finished = 1;
+        return 1;
+    }
+    return 0;
+}
+
+static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out,
+                       uint32_t* hopseq, uint32_t* rpcsOut)
+{
+    const orc_params* p = &net->p;
+    Lookup* L = (Lookup*)calloc(1, sizeof(Lookup));
+    L->net = net; L->key = *key; L->S = S;
+    L->numSiblings = p->numSiblings; L->hopCountMax = p->hopCountMax;
+    L->hopseq = hopseq;
+    L->minHops = 0x7fffffff;
+    L->running = 1; L->startTime = 0; L->now = 0; L->txFinished = 0;
+    /* start() 133-244 */
+    NVec nextHops; int err;
+    ov_findNode(net, S, key, ov_maxRedundant(net), L->numSiblings, &nextHops);
+    lk_setVisited(L, S);
+    if (nextHops.size == 0) {
+        L->finished = 1; L->success = 0;
+    } else if (L->numSiblings != 0 && ov_isSiblingFor(net, S, S, key, L->numSiblings, &err)) {
+        for (int i = 0; i < nextHops.size; i++) lk_addSibling(L, nextHops.v[i]);
+        L->success = L->finished = 1;
+    }
+    int done = L->finished;
+    if (!done) {
+        for (int i = 0; i < nextHops.size; ++i) path_add(L, nextHops.v[i]);
+        path_sendRpc(L, p->lookupParallelRpcs);
+        done = lk_checkStop(L);
+    }
+    /* event loop */
+    while (!done) {
+        /* earliest pending event: (time, insertion time, seq); timeouts inserted at send */
+        int best = -1, bestIsTimeout = 0;
+        int64_t bt = 0, bi = 0; uint64_t bs = 0;
+        for (int i = 0; i < L->nrpcs; ++i) {
+            Rpc* r = &L->rpcs[i];
+            if (!r->active) continue;
+            int64_t t, ti; uint64_t s; int isTo;
+            if (r->tTimeout <= r->tResp) { t = r->tTimeout; ti = r->tTimeout - simtime(p->rpcUdpTimeout, p->simtimeRound); s = r->seqTimeout; isTo = 1; }
+            else { t = r->tResp; ti = r->tIns; s = r->seqResp; isTo = 0; }
+            if (best < 0 || t < bt || (t == bt && (ti < bi || (ti == bi && s < bs)))) {
+                best = i; bt = t; bi = ti; bs = s; bestIsTimeout = isTo;
+            }
+        }
+        if (best < 0) { done = 1; break; }
+        Rpc r = L->rpcs[best];
+        L->rpcs[best].active = 0;            /* rpcs.erase(src) */
+        L->now = bt;
+        if (bestIsTimeout) {                 /* handleRpcTimeout 588-654 */
+            if (L->ndead < MAXRPC) L->dead[L->ndead++] = r.node;
+            for (int q = 0; q < r.nInfo; ++q) {
+                if (L->pfinished) continue;
+                path_handleTimeout(L);
+                lk_countFinished(L);
+            }
+        } else {                             /* handleRpcResponse 488-585 */
+            NVec res; int sflag, err2;
+            ov_findNode(net, r.node, key, p->lookupRedundantNodes, L->numSiblings, &res);  /* BaseOverlay.cc:1857-1871 */
+            sflag = ov_isSiblingFor(net, r.node, r.node, key, L->numSiblings, &err2);
+            int rpcHandled = 0;
+            for (int q = 0; q < r.nInfo; ++q) {
+                if (L->pfinished) continue;
+                if (!rpcHandled && (path_accepts(L, r.vrpcId[q]) || (sflag && p->lookupAcceptLateSiblings))) {
+                    path_handleResponse(L, r.node, &res, sflag);
+                    rpcHandled = 1;
+                } else {
+                    path_handleTimeout(L);
+                }
+                lk_countFinished(L);
+            }
+        }
+        done = lk_checkStop(L);
+    }
+    /* stop() -> SendToKeyListener::lookupFinished (BaseOverlay.cc:1241-1307) */
+    int valid = L->success && L->finished;
+    int minHops = (L->minHops == 0x7fffffff) ? 0 : L->minHops;
+    out->hops = (uint16_t)minHops;
+    if (valid && L->nsiblings > 0) {
+        uint32_t R = L->siblings[0];
+        out->responsible = R;
+        out->status = 0;
+        out->one_way_hops = (uint8_t)(minHops + (R != S ? 1 : 0));    /* sendRouteMessage 1130-1132 */
+        int64_t tx = L->txFinished;
+        int64_t dfin = calc_delay(net, S, R, p->routeBytes, L->now, &tx);
+        out->latency_ns = L->now - L->startTime + dfin;
+    } else {
+        out->responsible = NONE;
+        /* classify the failure */
+        if (L->now > L->startTime + simtime(p->lookupTimeout, p->simtimeRound)) out->status = 1;
+        else if (L->ndead > 0) out->status = 2;
+        else if (L->hopCountMax && L->hops >= L->hopCountMax) out->status = 3;
+        else out->status = 4;
+        out->one_way_hops = 0;
+        out->latency_ns = -1;
+    }
+    if (rpcsOut) *rpcsOut = L->rpcsSent;
+    free(L->visited);
+    free(L);
+}
+
+uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
+                         orc_route_out* out, uint32_t* hop_seq, uint32_t* rpcs_out, int nthreads)
+{
+    uint64_t total = 0;
+    int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
+    if (hop_seq) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) hop_seq[i] = NONE;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : total) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        OKey k = ok_from(&keys[i]);
+        run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
+                   rpcs_out ? &rpcs_out[i] : NULL);
+        total += out[i].hops;
+    }
+    (void)nthreads;
+    return total;
+}

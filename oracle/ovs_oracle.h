@@ -1,0 +1,127 @@
+/*
+ * ovs_oracle.h -- CPU restatement of OverSim's iterative KBR lookup path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the *checker* for the MI355X
+ * engine in oversim_amd/: only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product path never links,
+ * calls or falls back to it.
+ *
+ * Parity status: the reference (trucndt/oversim) cannot be built here -- it
+ * needs OMNeT++ 4.x, INET and opp_msgc output.  The
+ * reference ships no golden vectors for routing results, so the routing parts
+ * of this restatement are "parity unpinned" against reference outputs; they
+ * are pinned only by hand-derived known answers taken from the input cases of
+ * OverlayKey::test() (OverlayKey.cc:720-828) and by a second, independent
+ * pure-Python restatement in tests/refmodel.py for small rings.
+ *
+ * Every function cites the reference file:line it restates.
+ */
+#ifndef OVS_ORACLE_H
+#define OVS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- keys: 5 x u32, w[0] least significant (same wire layout as ovs_key160) */
+typedef struct { uint32_t w[5]; } orc_key;
+
+/* OverlayKey operations (OverlayKey.cc).  Results are written to *out. */
+int      orc_key_cmp(const orc_key* a, const orc_key* b);                  /* compareTo 842-847 */
+void     orc_key_add(const orc_key* a, const orc_key* b, orc_key* out);    /* operator+ 247-253,283-288 */
+void     orc_key_sub(const orc_key* a, const orc_key* b, orc_key* out);    /* operator- 256-262,291-296 */
+void     orc_key_xor(const orc_key* a, const orc_key* b, orc_key* out);    /* operator^ 341-349 */
+/* which: 0=isBetween (a,b), 1=isBetweenR (a,b], 2=isBetweenL [a,b), 3=isBetweenLR [a,b]
+ * unspec_mask bit0: x unspecified, bit1: a unspecified, bit2: b unspecified */
+int      orc_key_between(int which, const orc_key* x, const orc_key* a, const orc_key* b,
+                         int unspec_mask);                                 /* 587-644 */
+uint32_t orc_key_bit_range(const orc_key* k, uint32_t p, uint32_t n);      /* getBitRange 458-474 */
+uint32_t orc_key_shared_prefix(const orc_key* a, const orc_key* b, uint32_t bitsPerDigit); /* 530-555 */
+int      orc_key_log2(const orc_key* k);                                   /* log_2 558-578 */
+void     orc_key_pow2(uint32_t e, orc_key* out);                           /* pow2 704-717 */
+
+/* ---- parameters (names follow the .ini / NED parameter names) */
+typedef struct {
+    int32_t hopCountMax;              /* BaseOverlay.ned, default.ini:385 = 50 */
+    int32_t successorListSize;        /* Chord.ned, default.ini:174 = 8 */
+    int32_t numFingerCandidates;      /* default.ini:176 = 3 */
+    int32_t k, s, b;                  /* Kademlia.ned, default.ini:197-199 */
+    int32_t lookupRedundantNodes;
+    int32_t lookupParallelRpcs;
+    int32_t lookupMerge;
+    int32_t lookupStrictParallelRpcs;
+    int32_t lookupVisitOnlyOnce;
+    int32_t lookupAcceptLateSiblings;
+    int32_t lookupUseAllParallelResponses;
+    int32_t lookupNewRpcOnEveryTimeout;
+    int32_t lookupNewRpcOnEveryResponse;
+    int32_t lookupFinishOnFirstUnchanged;
+    int32_t numSiblings;              /* sendToKey(..., numSiblings=1) for KBRTestApp one-way */
+    int32_t simtimeRound;             /* 1: SimTime(double) rounds half-up, 0: truncates */
+    double  rpcUdpTimeout;            /* default.ini:483 = 1.5 s */
+    double  lookupTimeout;            /* IterativeLookup.h:44 LOOKUP_TIMEOUT = 10 s */
+    double  datarate;                 /* channels.ned simple_ethernetline = 10 Mbps */
+    double  accessDelay;              /* channels.ned = 0 ms */
+    int32_t callBytes;                /* FindNodeCall incl. 28 B UDP/IP = 83 */
+    int32_t respBaseBytes;            /* FindNodeResponse with 0 nodes incl. UDP/IP = 61 */
+    int32_t respPerNodeBytes;         /* + 26 B per NodeHandle */
+    int32_t routeBytes;               /* one-way KBRTestMessage route msg = 186 */
+    uint64_t kadSeed;                 /* Kademlia snapshot bucket-sampling seed */
+} orc_params;
+
+void orc_params_chord_default(orc_params* p);
+void orc_params_kad_default(orc_params* p);
+
+/* ---- networks */
+typedef struct orc_net orc_net;
+/* Chord stable state: ids sorted ascending, unique.  xy = 2n doubles.      */
+orc_net* orc_chord_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
+/* Explicit Chord snapshot: pred[n], succ[n*succ_stride] (count in nsucc[n]),
+ * fingers[n*160] indexed by finger position i (0..159), 0xFFFFFFFF = unspecified.
+ * deque_size[n] = fingerTable.size() (ChordFingerTable.cc:61-87). */
+orc_net* orc_chord_build_tables(const orc_key* ids, uint32_t n, const double* xy,
+                                const uint32_t* pred, const uint32_t* succ, const uint8_t* nsucc,
+                                uint32_t succ_stride, const uint32_t* fingers,
+                                const uint8_t* deque_size, const orc_params* p);
+/* Kademlia snapshot (DESIGN.md "Kademlia snapshot rule"). */
+orc_net* orc_kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
+void     orc_net_free(orc_net* net);
+
+/* export the Kademlia snapshot so the GPU builder can be checked:
+ * siblings[n*5s] (UINT32_MAX padded), bucket_count[n*160], bucket_nodes[n*160*k] */
+void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes);
+/* export the Chord finger table resolved through getFinger(): out[n*160] */
+void orc_chord_export_fingers(const orc_net* net, uint32_t* out);
+
+/* findNode at `node` (Chord.cc:548-599 / Kademlia.cc:1101-1246).
+ * returns count, nodes in out[] (cap 64); *sibling_flag = isSiblingFor(node,key,numSiblings) */
+int orc_find_node(const orc_net* net, uint32_t node, const orc_key* key, int numRedundantNodes,
+                  int numSiblings, uint32_t* out, int* sibling_flag);
+
+/* ---- batched one-way lookups (KBRTestApp one-way test, iterative routing) */
+typedef struct {
+    uint32_t responsible;   /* node index or 0xFFFFFFFF */
+    uint16_t hops;          /* IterativeLookup::getMinHops() */
+    uint8_t  status;        /* 0 ok, see ovs_kbr.h */
+    uint8_t  one_way_hops;  /* KBRTestApp "One-way Hop Count" = hops + (R != S) */
+    int64_t  latency_ns;    /* "One-way Latency" in ns */
+} orc_route_out;
+
+/* hop_seq may be NULL; else n*hopCountMax entries (accepted responders, UINT32_MAX padded).
+ * rpcs_out may be NULL; else per-lookup count of FindNodeCalls sent.
+ * nthreads<=0 -> all OpenMP threads. Returns total accepted hops. */
+uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
+                         orc_route_out* out, uint32_t* hop_seq, uint32_t* rpcs_out, int nthreads);
+
+/* SimpleNodeEntry::calcDelay for an idle tx queue, in ns (SimpleNodeEntry.cc:155-195) */
+int64_t orc_delay_ns(const orc_net* net, uint32_t a, uint32_t b, int32_t bytes);
+/* float distance (SimpleNodeEntry.cc:145-153) */
+float orc_coord_dist(const orc_net* net, uint32_t a, uint32_t b);
+
+const char* orc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,520 @@
+// chord.hip -- Chord iterative-lookup kernels for gfx950 (MI355X).
+//
+// K1 chord_route: one lane per in-flight lookup, the whole lookup runs in
+// registers (no per-round state round trip through HBM); a wave refills its
+// finished lanes from its own contiguous slice of the batch (ballot + popcount
+// prefix, no atomics), so all 64 lanes stay busy until the slice drains.
+// Per hop the lane evaluates the responder's Chord::findNode + isSiblingFor
+// (Chord.cc:422-500, 548-674) and charges the SimpleUnderlay delay
+// (SimpleNodeEntry.cc:145-195) in exact int64 ns.
+//
+// Memory per hop (ideal tables): the responder's ring window (pred, succ0,
+// succ[ns-1], 24 B records), its coordinates, one finger-row word and the
+// finger's record -- two dependent gather rounds.  Nothing here is a dense
+// contraction, so there is no MFMA; the kernel is HBM/Infinity-Cache gather
+// bound.
+#include <hipcub/hipcub.hpp>
+
+#include "engine.hpp"
+#include "launch.hpp"
+
+namespace ovs {
+
+// ---------------------------------------------------------------------------
+// table builder (ideal NoChurn state, Chord.cc:845-875 fixed point)
+
+__global__ void k_check_sorted(const KeyRec* __restrict__ recs, uint32_t n, uint32_t* bad)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i + 1 < n) {
+        const K160 a = key_of(load_rec(recs, i)), b = key_of(load_rec(recs, i + 1));
+        if (!k_lt(a, b)) atomicOr(bad, 1u);
+    }
+}
+
+// row length = number of non-trivial fingers: i with 2^i > succ0 - self
+__global__ void k_chord_rowlen(const KeyRec* __restrict__ recs, uint32_t n, uint64_t* rowlen)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const K160 self = key_of(load_rec(recs, v));
+    const K160 s0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
+    const int ilo = k_msb(k_sub(s0, self)) + 1;
+    rowlen[v] = (uint64_t)(KEYBITS - ilo);
+}
+
+__global__ void k_set_aux(KeyRec* recs, const uint64_t* off, uint32_t n)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < n) recs[v].aux = (uint32_t)off[v];
+}
+
+// first index with key >= target, wrapping to 0 (the responsible node)
+__device__ __forceinline__ uint32_t ring_lower_bound(const KeyRec* __restrict__ recs, uint32_t n,
+                                                     const K160& t)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (k_lt(key_of(load_rec(recs, mid)), t)) lo = mid + 1; else hi = mid;
+    }
+    return lo == n ? 0 : lo;
+}
+
+// finger i of node v = responsible(v + 2^i) (rpcFixfingers answers thisNode, Chord.cc:1228-1270)
+__global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32_t* __restrict__ fingers)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const KeyRec r = load_rec(recs, v);
+    const K160 self = key_of(r);
+    const K160 s0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
+    const int ilo = k_msb(k_sub(s0, self)) + 1;
+    uint32_t* row = fingers + r.aux;
+    for (int i = KEYBITS - 1; i >= ilo; --i)
+        row[KEYBITS - 1 - i] = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
+}
+
+// resolved getFinger(pos) for every position (test export)
+__global__ void k_chord_export(const KeyRec* __restrict__ recs, const uint32_t* __restrict__ fingers,
+                               uint32_t n, uint32_t* __restrict__ out)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n * KEYBITS) return;
+    const uint32_t v = (uint32_t)(t / KEYBITS);
+    const int pos = (int)(t % KEYBITS);
+    const KeyRec r = load_rec(recs, v);
+    const uint32_t s0i = v + 1 == n ? 0 : v + 1;
+    const int ilo = k_msb(k_sub(key_of(load_rec(recs, s0i)), key_of(r))) + 1;
+    out[t] = pos >= ilo ? fingers[r.aux + (KEYBITS - 1 - pos)] : s0i;
+}
+
+// ---------------------------------------------------------------------------
+// findNode + isSiblingFor at responder c for key K (numRedundantNodes = 1,
+// numSiblings = 1): the per-hop routing decision.
+
+struct Decision {
+    uint32_t next;   // next hop (== c when c is responsible)
+    KeyRec rec;      // its record
+    uint8_t sib;     // siblings flag of the FindNodeResponse
+    uint8_t broken;  // Chord::closestPreceedingNode threw
+};
+
+__device__ __forceinline__ uint32_t ring_next(uint32_t i, uint32_t d, uint32_t n)
+{
+    uint32_t j = i + d;
+    return j >= n ? j - n : j;
+}
+
+// ideal tables: successor j of c is c+1+j, predecessor c-1
+__device__ __forceinline__ Decision decide_ideal(const ChordView& V, uint32_t c, const KeyRec& crec,
+                                                 const K160& K)
+{
+    Decision d;
+    d.broken = 0; d.sib = 0;
+    const K160 C = key_of(crec);
+    const uint32_t pidx = c == 0 ? V.n - 1 : c - 1;
+    const uint32_t s0 = ring_next(c, 1, V.n);
+    // issue every independent gather of this hop up front
+    const K160 D = k_sub(K, C);
+    const int i0 = k_msb(D);                       // -1 only when K == C (then c is responsible)
+    const uint32_t slot0 = (uint32_t)(KEYBITS - 1 - (i0 < 0 ? KEYBITS - 1 : i0));
+    const uint32_t f0 = V.fingers[crec.aux + slot0];   // in bounds: rows are padded by 160 words
+    const KeyRec P = load_rec(V.recs, pidx);
+    const KeyRec S0 = load_rec(V.recs, s0);
+    const uint32_t slast = ring_next(c, (uint32_t)V.ns, V.n);
+    const KeyRec SL = load_rec(V.recs, slast);
+    const K160 PK = key_of(P), S0K = key_of(S0);
+
+    // isSiblingFor(thisNode, key, 1): key in (pred, self]  (Chord.cc:452-457)
+    if (between_R(K, PK, C)) {
+        d.sib = 1; d.next = c; d.rec = crec;
+        return d;
+    }
+    // key in (self, succ0]  (Chord.cc:583-590)
+    if (between_R(K, C, S0K)) {
+        d.next = s0; d.rec = S0;
+        return d;
+    }
+    // closestPreceedingNode (Chord.cc:602-674)
+    // temp = farthest successor in (self, key]
+    int tj = -1;
+    K160 T;
+    if (between_R(key_of(SL), C, K)) {
+        tj = V.ns - 1; T = key_of(SL);
+    } else {
+        for (int j = V.ns - 2; j >= 0; --j) {
+            const K160 SJ = key_of(load_rec(V.recs, ring_next(c, (uint32_t)j + 1, V.n)));
+            if (between_R(SJ, C, K)) { tj = j; T = SJ; break; }
+        }
+    }
+    if (tj < 0) { d.broken = 1; d.next = NONE; return d; }
+    // finger scan from i0 down (fingers above i0 lie beyond the key)
+    const int ilo = k_msb(k_sub(S0K, C)) + 1;
+    for (int i = i0; i >= ilo; --i) {
+        const uint32_t f = (i == i0) ? f0 : V.fingers[crec.aux + (uint32_t)(KEYBITS - 1 - i)];
+        const KeyRec F = load_rec(V.recs, f);
+        if (between_LR(key_of(F), T, K)) { d.next = f; d.rec = F; return d; }
+    }
+    // trivial positions resolve to succ0 (ChordFingerTable.cc:183-184)
+    if (between_LR(S0K, T, K)) { d.next = s0; d.rec = S0; return d; }
+    // no finger: farthest successor in the OPEN interval (self, key) (Chord.cc:653-658)
+    for (int j = V.ns - 1; j >= 0; --j) {
+        const uint32_t sj = ring_next(c, (uint32_t)j + 1, V.n);
+        const KeyRec SJ = (j == V.ns - 1) ? SL : load_rec(V.recs, sj);
+        if (between_open(key_of(SJ), C, K)) { d.next = sj; d.rec = SJ; return d; }
+    }
+    d.broken = 1; d.next = NONE;
+    return d;
+}
+
+// general (explicit snapshot) tables: literal restatement incl. unspecified predecessor
+__device__ __forceinline__ bool sibling_general(const ChordView& V, uint32_t self, const K160& K,
+                                                int numSiblings)
+{
+    const uint32_t pred = V.pred[self];
+    const int ssize = V.nsucc[self];
+    const K160 C = key_of(load_rec(V.recs, self));
+    if (pred == NONE) {
+        const bool isEmpty = ssize == 0 || (ssize == 1 && V.succ[(uint64_t)self * V.sls] == self);
+        return isEmpty || k_eq(C, K);
+    }
+    const K160 PK = key_of(load_rec(V.recs, pred));
+    if (between_R(K, PK, C)) return true;
+    // loop of Chord.cc:462-495 with node == thisNode matches at i = -1 only
+    (void)numSiblings;
+    return false;
+}
+
+__device__ __forceinline__ Decision decide_general(const ChordView& V, uint32_t c, const KeyRec& crec,
+                                                   const K160& K)
+{
+    Decision d;
+    d.broken = 0; d.sib = 0;
+    const K160 C = key_of(crec);
+    const uint64_t sb = (uint64_t)c * V.sls;
+    const int ssize = V.nsucc[c];
+    if (sibling_general(V, c, K, 1)) { d.sib = 1; d.next = c; d.rec = crec; return d; }
+    const uint32_t s0 = V.succ[sb];
+    const KeyRec S0 = load_rec(V.recs, s0);
+    if (between_R(K, C, key_of(S0))) { d.next = s0; d.rec = S0; return d; }
+    int tj = -1;
+    K160 T;
+    for (int j = ssize - 1; j >= 0; --j) {
+        const K160 SJ = key_of(load_rec(V.recs, V.succ[sb + j]));
+        if (between_R(SJ, C, K)) { tj = j; T = SJ; break; }
+    }
+    if (tj < 0) { d.broken = 1; d.next = NONE; return d; }
+    for (int i = KEYBITS - 1; i >= 0; --i) {
+        const uint32_t f = V.fres[(uint64_t)c * KEYBITS + i];
+        const KeyRec F = load_rec(V.recs, f);
+        if (between_LR(key_of(F), T, K)) { d.next = f; d.rec = F; return d; }
+    }
+    for (int j = ssize - 1; j >= 0; --j) {
+        const uint32_t sj = V.succ[sb + j];
+        const KeyRec SJ = load_rec(V.recs, sj);
+        if (between_open(key_of(SJ), C, K)) { d.next = sj; d.rec = SJ; return d; }
+    }
+    if (V.pred[c] == NONE && s0 == c) { d.next = c; d.rec = crec; return d; }
+    d.broken = 1; d.next = NONE;
+    return d;
+}
+
+// ---------------------------------------------------------------------------
+// K1: batched one-way lookups
+
+template <bool IDEAL, bool RECORD>
+__global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC, LookupConsts LC,
+                                                     const K160* __restrict__ qkeys,
+                                                     const uint32_t* __restrict__ qsrc, uint64_t nq,
+                                                     uint64_t chunk, ovs_route_out* __restrict__ out,
+                                                     uint32_t* __restrict__ hopseq)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    uint64_t cursor = wave * chunk;                       // wave-uniform
+    const uint64_t end = min(cursor + chunk, nq);
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    bool active = false;
+    uint64_t q = 0;
+    uint32_t S = 0, cur = 0;
+    K160 K;
+    KeyRec crec;
+    double sx = 0, sy = 0;
+    int64_t t = 0;
+    int hops = 0;
+    bool local = true;
+
+    while (true) {
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && cursor < end) {
+            const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
+            if (!active && mine < end) {
+                q = mine;
+                active = true;
+                K = qkeys[q];
+                S = qsrc[q];
+                crec = load_rec(V.recs, S);
+                const double2 sxy = V.xy[S];
+                sx = sxy.x; sy = sxy.y;
+                cur = S; t = 0; hops = 0; local = true;
+            }
+            cursor += (uint64_t)__popcll(need);
+        }
+        if (!__any(active)) break;
+        if (!active) continue;
+
+        // responder coordinates are independent of the routing decision: issue first
+        const double2 cxy = V.xy[cur];
+        const Decision d = IDEAL ? decide_ideal(V, cur, crec, K) : decide_general(V, cur, crec, K);
+
+        uint8_t status = 0xFF;   // 0xFF = still running
+        uint32_t R = NONE;
+        if (local) {
+            // IterativeLookup::start (IterativeLookup.cc:157-204): local step, no hop, no delay
+            local = false;
+            if (d.broken) status = OVS_LOOKUP_BROKEN;
+            else if (d.sib) { status = OVS_LOOKUP_OK; R = S; }
+        } else {
+            // FindNodeCall S->cur, FindNodeResponse cur->S (one NodeHandle)
+            const int64_t cd = coord_ns(sx, sy, cxy.x, cxy.y, DC.round);
+            const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
+            if (rtt >= DC.rpcTimeout) {
+                status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
+            } else {
+                t += rtt;
+                if (t > DC.lookupTimeout) status = OVS_LOOKUP_TIMEOUT;   // IterativeLookup.cc:808-815
+                else {
+                    if (RECORD && hops < LC.hopCountMax) hopseq[q * (uint64_t)LC.hopCountMax + hops] = cur;
+                    ++hops;
+                    if (d.broken) status = OVS_LOOKUP_BROKEN;
+                    else if (d.sib) { status = OVS_LOOKUP_OK; R = cur; }  // IterativeLookup.cc:896-905
+                }
+            }
+        }
+        if (status == 0xFF) {
+            // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
+            if (LC.hopCountMax && hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;
+            else {
+                bool visited = (d.next == S);
+                if (!IDEAL && !visited) {
+                    // explicit tables can loop: check every responder so far
+                    for (int h = 0; h < hops && h < LC.hopCountMax; ++h)
+                        visited |= hopseq[q * (uint64_t)LC.hopCountMax + h] == d.next;
+                }
+                if (visited) status = OVS_LOOKUP_NO_NEXT;
+                else { cur = d.next; crec = d.rec; }
+            }
+        }
+        if (status != 0xFF) {
+            ovs_route_out o;
+            o.hops = (uint16_t)hops;
+            o.status = status;
+            if (status == OVS_LOOKUP_OK) {
+                o.responsible = R;
+                o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
+                // sendRouteMessage to result[0] (BaseOverlay.cc:1107-1146); 0 delay to self
+                o.latency_ns = t + (R != S ? DC.msgRoute + coord_ns(sx, sy, cxy.x, cxy.y, DC.round) : 0);
+            } else {
+                o.responsible = NONE;
+                o.one_way_hops = 0;
+                o.latency_ns = -1;
+            }
+            out[q] = o;
+            active = false;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// findNode batch (general numRedundantNodes / numSiblings), Chord.cc:548-599
+
+__global__ void k_chord_find_node(ChordView V, int ideal, const uint32_t* __restrict__ node,
+                                  const K160* __restrict__ keys, uint64_t n, int numRedundant,
+                                  int numSiblings, uint32_t* __restrict__ out_nodes, uint32_t max_out,
+                                  uint8_t* __restrict__ out_count, uint8_t* __restrict__ out_sib)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = node[i];
+    const K160 K = keys[i];
+    const KeyRec crec = load_rec(V.recs, c);
+    const K160 C = key_of(crec);
+    uint32_t* o = out_nodes + i * max_out;
+    for (uint32_t j = 0; j < max_out; ++j) o[j] = NONE;
+    const int ssize = ideal ? V.ns : V.nsucc[c];
+    auto succ_at = [&](int j) -> uint32_t {
+        return ideal ? ring_next(c, (uint32_t)j + 1, V.n) : V.succ[(uint64_t)c * V.sls + j];
+    };
+    // getFinger(pos) (ChordFingerTable.cc:174-193), resolved
+    const uint32_t s0 = ssize > 0 ? succ_at(0) : c;
+    const int ilo = ideal ? k_msb(k_sub(key_of(load_rec(V.recs, s0)), C)) + 1 : 0;
+    auto finger_at = [&](int pos) -> uint32_t {
+        if (ideal) return pos >= ilo ? V.fingers[crec.aux + (uint32_t)(KEYBITS - 1 - pos)] : s0;
+        return V.fres[(uint64_t)c * KEYBITS + pos];
+    };
+    const bool sib = ideal ? between_R(K, key_of(load_rec(V.recs, c == 0 ? V.n - 1 : c - 1)), C)
+                           : sibling_general(V, c, K, 1);
+    int cnt = 0;
+    auto push = [&](uint32_t v) { if ((uint32_t)cnt < max_out) o[cnt] = v; ++cnt; };
+    if (sib) {
+        // [self, succ...] downsized to numSiblings (Chord.cc:573-580)
+        push(c);
+        for (int j = 0; j < ssize; ++j) push(succ_at(j));
+        if (cnt > numSiblings) cnt = numSiblings;
+    } else if (ssize > 0 && between_R(K, C, key_of(load_rec(V.recs, s0)))) {
+        // [succ...] downsized to numRedundantNodes (Chord.cc:583-590)
+        for (int j = 0; j < ssize; ++j) push(succ_at(j));
+        if (cnt > numRedundant) cnt = numRedundant;
+    } else {
+        // closestPreceedingNode (Chord.cc:602-674)
+        K160 T;
+        int tj = -1;
+        for (int j = ssize - 1; j >= 0; --j) {
+            const K160 SJ = key_of(load_rec(V.recs, succ_at(j)));
+            if (between_R(SJ, C, K)) { tj = j; T = SJ; break; }
+        }
+        bool hit = false;
+        for (int pos = KEYBITS - 1; pos >= 0 && tj >= 0; --pos) {
+            const uint32_t f = finger_at(pos);
+            if (between_LR(key_of(load_rec(V.recs, f)), T, K)) { push(f); hit = true; break; }
+        }
+        if (!hit && tj >= 0) {
+            for (int j = ssize - 1; j >= 0 && cnt <= V.numFingerCandidates; --j) {
+                const uint32_t sj = succ_at(j);
+                if (between_open(key_of(load_rec(V.recs, sj)), C, K)) push(sj);
+            }
+        }
+        if (cnt > numRedundant) cnt = numRedundant;
+    }
+    out_count[i] = (uint8_t)(cnt < (int)max_out ? cnt : (int)max_out);
+    // findNodeRpc siblings flag: isSiblingFor(thisNode, key, numSiblings) (BaseOverlay.cc:1866-1871)
+    out_sib[i] = (uint8_t)sib;
+}
+
+__global__ void k_delay(const double2* __restrict__ xy, DelayConsts DC, const uint32_t* __restrict__ a,
+                        const uint32_t* __restrict__ b, const int32_t* __restrict__ bytes, uint64_t n,
+                        int64_t* __restrict__ out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (a[i] == b[i]) { out[i] = 0; return; }   // SimpleUDP.cc:322
+    const double2 p = xy[a[i]], r = xy[b[i]];
+    const int64_t bw = bw_ns(bytes[i], DC.datarate, DC.round);
+    out[i] = 2 * bw + DC.access2 + coord_ns(p.x, p.y, r.x, r.y, DC.round);
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+
+static inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hipStream_t s)
+{
+    if (n < 2) return hipSuccess;
+    hipLaunchKernelGGL(k_check_sorted, dim3(nblk(n, 256)), dim3(256), 0, s, recs, n, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t** fingers_out, uint64_t* nfing_out,
+                              hipStream_t s)
+{
+    hipError_t e;
+    uint64_t* rowlen = nullptr;
+    uint64_t* off = nullptr;
+    void* tmp = nullptr;
+    size_t tmpb = 0;
+    *fingers_out = nullptr;
+    if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (n + 1))) != hipSuccess) return e;
+    if ((e = hipMalloc(&off, sizeof(uint64_t) * (n + 1))) != hipSuccess) { hipFree(rowlen); return e; }
+    hipLaunchKernelGGL(k_chord_rowlen, dim3(nblk(n, 256)), dim3(256), 0, s, recs, n, rowlen);
+    hipMemsetAsync(rowlen + n, 0, sizeof(uint64_t), s);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, rowlen, off, n + 1, s);
+    if ((e = hipMalloc(&tmp, tmpb)) != hipSuccess) { hipFree(rowlen); hipFree(off); return e; }
+    hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, rowlen, off, n + 1, s);
+    uint64_t total = 0;
+    hipMemcpyAsync(&total, off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    if (total + KEYBITS >= 0xFFFFFFFFull) { hipFree(rowlen); hipFree(off); hipFree(tmp); return hipErrorInvalidValue; }
+    uint32_t* fing = nullptr;
+    // +160 words of padding: the kernel's speculative first-finger read may run past a row
+    if ((e = hipMalloc(&fing, sizeof(uint32_t) * (total + KEYBITS))) != hipSuccess) {
+        hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
+    }
+    hipMemsetAsync(fing, 0, sizeof(uint32_t) * (total + KEYBITS), s);
+    hipLaunchKernelGGL(k_set_aux, dim3(nblk(n, 256)), dim3(256), 0, s, recs, off, n);
+    hipLaunchKernelGGL(k_chord_fill, dim3(nblk(n, 128)), dim3(128), 0, s, recs, n, fing);
+    e = hipStreamSynchronize(s);
+    hipFree(rowlen); hipFree(off); hipFree(tmp);
+    if (e != hipSuccess) { hipFree(fing); return e; }
+    *fingers_out = fing;
+    *nfing_out = total;
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint32_t n, uint32_t* out,
+                               hipStream_t s)
+{
+    const uint64_t tot = (uint64_t)n * KEYBITS;
+    hipLaunchKernelGGL(k_chord_export, dim3(nblk(tot, 256)), dim3(256), 0, s, recs, fingers, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
+                              const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
+                              uint32_t* hopseq, int grid_blocks, hipStream_t s)
+{
+    if (nq == 0) return hipSuccess;
+    const uint64_t waves = (uint64_t)grid_blocks * 4;   // 256 threads = 4 waves
+    uint64_t blocks = (uint64_t)grid_blocks;
+    uint64_t chunk = (nq + waves - 1) / waves;
+    if (chunk < 1) chunk = 1;
+    // small batches: do not launch waves that have nothing to do
+    const uint64_t need_waves = (nq + chunk - 1) / chunk;
+    blocks = (need_waves + 3) / 4;
+    const dim3 g((unsigned)blocks), b(256);
+    if (ideal) {
+        if (hopseq) hipLaunchKernelGGL((k_chord_route<true, true>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);
+        else hipLaunchKernelGGL((k_chord_route<true, false>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);
+    } else {
+        hipLaunchKernelGGL((k_chord_route<false, true>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,
+                                  uint64_t n, int numRedundant, int numSiblings, uint32_t* out_nodes,
+                                  uint32_t max_out, uint8_t* out_count, uint8_t* out_sib, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chord_find_node, dim3(nblk(n, 128)), dim3(128), 0, s, V, ideal ? 1 : 0, node, keys, n,
+                       numRedundant, numSiblings, out_nodes, max_out, out_count, out_sib);
+    return hipGetLastError();
+}
+
+__global__ void k_fill_rpcs(const ovs_route_out* __restrict__ out, uint64_t n, uint32_t* __restrict__ rpcs)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    // alpha = 1: one FindNodeCall per counted hop, plus the call whose response came too late
+    const ovs_route_out o = out[i];
+    rpcs[i] = o.hops + ((o.status == OVS_LOOKUP_TIMEOUT || o.status == OVS_LOOKUP_RPC_TIMEOUT) ? 1u : 0u);
+}
+
+hipError_t launch_fill_rpcs_from_hops(const ovs_route_out* out, uint64_t n, uint32_t* rpcs, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_rpcs, dim3(nblk(n, 256)), dim3(256), 0, s, out, n, rpcs);
+    return hipGetLastError();
+}
+
+hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t* a, const uint32_t* b,
+                        const int32_t* bytes, uint64_t n, int64_t* out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delay, dim3(nblk(n, 256)), dim3(256), 0, s, xy, DC, a, b, bytes, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace ovs

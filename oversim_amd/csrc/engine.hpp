@@ -1,0 +1,94 @@
+// engine.hpp -- device-side data layout and shared device functions of the
+// MI355X lookup-routing engine (internal; the public boundary is include/ovs_kbr.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "key160.hpp"
+#include "../../include/ovs_kbr.h"
+
+namespace ovs {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr int KEYBITS = 160;
+
+// ---------------------------------------------------------------------------
+// Per-launch constants derived from ovs_params on the host.  All times are
+// int64 ns (simtime-scale = -9, default.ini:27).
+struct DelayConsts {
+    int64_t msgCall;     // 2*T(L*8/datarate) + 2*T(accessDelay) for FindNodeCall (83 B)
+    int64_t msgResp1;    // same for a FindNodeResponse with one NodeHandle (87 B)
+    int64_t msgRoute;    // same for the one-way route message (186 B)
+    int64_t rpcTimeout;  // T(rpcUdpTimeout)
+    int64_t lookupTimeout;  // T(LOOKUP_TIMEOUT)
+    int32_t round;       // SimTime(double) rounding rule
+    int32_t respBase;    // FindNodeResponse bytes with zero nodes (61 B)
+    int32_t respPerNode; // 26 B per NodeHandle
+    int32_t callBytes;   // 83 B
+    double datarate;
+    int64_t access2;     // 2*T(accessDelay)
+};
+
+// SimTime(double) at scale 1e-9: truncation or round-half-up (recorded in every fixture)
+__device__ __forceinline__ int64_t simtime_ns(double seconds, int round)
+{
+    const double x = __dmul_rn(seconds, 1e9);
+    return round ? (int64_t)floor(__dadd_rn(x, 0.5)) : (int64_t)x;
+}
+
+// coordDelay = SimTime(0.001 * (float)||a-b||), SimpleNodeEntry.cc:145-153,186.
+// Explicit _rn operations: no FMA contraction, identical rounding to the
+// reference's x86-64 double arithmetic; sqrt correctly rounded, then to float.
+__device__ __forceinline__ int64_t coord_ns(double ax, double ay, double bx, double by, int round)
+{
+    const double dx = __dsub_rn(ax, bx);
+    const double dy = __dsub_rn(ay, by);
+    const double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+    const float f = __double2float_rn(__dsqrt_rn(s));
+    return simtime_ns(__dmul_rn(0.001, (double)f), round);
+}
+
+// T(L*8 / datarate): the serialisation delay of an L-byte packet
+__device__ __forceinline__ int64_t bw_ns(int32_t bytes, double datarate, int round)
+{
+    return simtime_ns(__ddiv_rn((double)((int64_t)bytes * 8), datarate), round);
+}
+
+__device__ __forceinline__ KeyRec load_rec(const KeyRec* __restrict__ recs, uint32_t i)
+{
+    const uint2* p = reinterpret_cast<const uint2*>(recs + i);
+    const uint2 a = p[0], b = p[1], c = p[2];
+    KeyRec r;
+    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = b.x; r.w[3] = b.y; r.w[4] = c.x; r.aux = c.y;
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// Chord device view.
+//  recs[n]      : sorted node keys, aux = offset of the node's finger row
+//  xy[n]        : SimpleUnderlay coordinates (fp64)
+//  fingers[...] : ideal mode -- CSR rows, row(v)[159 - i] = finger i for the
+//                 non-trivial positions i >= i_lo(v) = msb(succ0 - v) + 1
+//                 (trivial positions resolve to succ0, ChordFingerTable.cc:183-184)
+//  general mode : pred[n], succ[n*sls], nsucc[n], fres[n*160] = getFinger(i) resolved
+struct ChordView {
+    const KeyRec* __restrict__ recs;
+    const double2* __restrict__ xy;
+    const uint32_t* __restrict__ fingers;
+    const uint32_t* __restrict__ pred;
+    const uint32_t* __restrict__ succ;
+    const uint8_t* __restrict__ nsucc;
+    const uint32_t* __restrict__ fres;
+    uint32_t n;
+    int32_t ns;        // ideal: min(successorListSize, n-1)
+    int32_t sls;       // successor list stride (general)
+    int32_t numFingerCandidates;
+};
+
+struct LookupConsts {
+    int32_t hopCountMax;
+    int32_t numSiblings;
+    int32_t numRedundantNodes;
+};
+
+}  // namespace ovs

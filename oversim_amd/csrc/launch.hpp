@@ -1,0 +1,22 @@
+// launch.hpp -- host launchers of the device kernels (internal).
+#pragma once
+#include "engine.hpp"
+
+namespace ovs {
+
+hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hipStream_t s);
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t** fingers_out, uint64_t* nfing_out,
+                              hipStream_t s);
+hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint32_t n, uint32_t* out,
+                               hipStream_t s);
+hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
+                              const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
+                              uint32_t* hopseq, int grid_blocks, hipStream_t s);
+hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,
+                                  uint64_t n, int numRedundant, int numSiblings, uint32_t* out_nodes,
+                                  uint32_t max_out, uint8_t* out_count, uint8_t* out_sib, hipStream_t s);
+hipError_t launch_fill_rpcs_from_hops(const ovs_route_out* out, uint64_t n, uint32_t* rpcs, hipStream_t s);
+hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t* a, const uint32_t* b,
+                        const int32_t* bytes, uint64_t n, int64_t* out, hipStream_t s);
+
+}  // namespace ovs

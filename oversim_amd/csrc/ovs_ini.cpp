@@ -1,0 +1,310 @@
+// ovs_ini.cpp -- OMNeT++ .ini subset parser binding the reference's parameter
+// names to ovs_params (include/ovs_kbr.h).
+//
+// Semantics kept from OMNeT++ 4.x Cmdenv configuration:
+//  * sections [General] and [Config <name>], `extends = A, B` chains,
+//    lookup order: the named config, its extends chain (depth first), then
+//    [General]; within a section the FIRST matching line wins;
+//  * keys are module-path patterns: `*` matches within one path component,
+//    `**` across components (e.g. `**.overlay*.chord.successorListSize`);
+//  * values: numbers with units (s, ms, us, ns, B, KiB, MiB, MB, bps, Kbps,
+//    Mbps, Gbps), true/false, quoted strings.  ${...} iterations are rejected.
+// Parameters are resolved against the module paths of an OverSim
+// SimpleUnderlayNetwork host (default.ini:1-30, 166-222, 383-433, 483, 540-560).
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ovs_kbr.h"
+
+namespace {
+
+struct Entry {
+    std::string key, value;
+};
+struct Section {
+    std::vector<Entry> entries;
+    std::vector<std::string> extends;
+};
+
+std::string trim(const std::string& s)
+{
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) ++a;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) --b;
+    return s.substr(a, b - a);
+}
+
+// OMNeT++ wildcard match: '*' = [^.]*, '**' = .*, '?' = one non-dot char
+bool glob(const char* p, const char* s)
+{
+    while (*p) {
+        if (p[0] == '*' && p[1] == '*') {
+            p += 2;
+            for (const char* t = s;; ++t) {
+                if (glob(p, t)) return true;
+                if (!*t) return false;
+            }
+        }
+        if (*p == '*') {
+            ++p;
+            for (const char* t = s;; ++t) {
+                if (glob(p, t)) return true;
+                if (!*t || *t == '.') return false;
+            }
+        }
+        if (*p == '?') {
+            if (!*s || *s == '.') return false;
+            ++p; ++s;
+            continue;
+        }
+        if (*p != *s) return false;
+        ++p; ++s;
+    }
+    return *s == 0;
+}
+
+bool parse_number(const std::string& v0, double* out, std::string* unit)
+{
+    std::string v = trim(v0);
+    if (v.empty()) return false;
+    char* end = nullptr;
+    const double x = std::strtod(v.c_str(), &end);
+    if (end == v.c_str()) return false;
+    *unit = trim(std::string(end));
+    *out = x;
+    return true;
+}
+
+bool to_seconds(const std::string& v, double* out)
+{
+    double x; std::string u;
+    if (!parse_number(v, &x, &u)) return false;
+    if (u.empty() || u == "s") *out = x;
+    else if (u == "ms") *out = x * 1e-3;
+    else if (u == "us") *out = x * 1e-6;
+    else if (u == "ns") *out = x * 1e-9;
+    else if (u == "min") *out = x * 60;
+    else return false;
+    return true;
+}
+
+bool to_bytes(const std::string& v, double* out)
+{
+    double x; std::string u;
+    if (!parse_number(v, &x, &u)) return false;
+    if (u.empty() || u == "B") *out = x;
+    else if (u == "KiB") *out = x * 1024;
+    else if (u == "MiB") *out = x * 1024 * 1024;
+    else if (u == "KB" || u == "kB") *out = x * 1000;
+    else if (u == "MB") *out = x * 1e6;
+    else if (u == "b") *out = x / 8;
+    else return false;
+    return true;
+}
+
+bool to_bps(const std::string& v, double* out)
+{
+    double x; std::string u;
+    if (!parse_number(v, &x, &u)) return false;
+    if (u.empty() || u == "bps") *out = x;
+    else if (u == "Kbps" || u == "kbps") *out = x * 1e3;
+    else if (u == "Mbps") *out = x * 1e6;
+    else if (u == "Gbps") *out = x * 1e9;
+    else return false;
+    return true;
+}
+
+bool to_bool(const std::string& v, int32_t* out)
+{
+    const std::string t = trim(v);
+    if (t == "true") { *out = 1; return true; }
+    if (t == "false") { *out = 0; return true; }
+    return false;
+}
+
+bool to_int(const std::string& v, int32_t* out)
+{
+    double x; std::string u;
+    if (!parse_number(v, &x, &u) || !u.empty()) return false;
+    *out = (int32_t)x;
+    return true;
+}
+
+std::string unquote(const std::string& v)
+{
+    std::string t = trim(v);
+    if (t.size() >= 2 && t.front() == '"' && t.back() == '"') return t.substr(1, t.size() - 2);
+    return t;
+}
+
+}  // namespace
+
+extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, const char* config_name, char* err,
+                                          int err_len)
+{
+    auto set_err = [&](const std::string& m) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", m.c_str());
+    };
+    if (!p || !ini_text) { set_err("null argument"); return OVS_EINVAL; }
+    std::map<std::string, Section> secs;
+    std::string cur = "General";
+    secs[cur];
+    // parse (with backslash line continuation)
+    std::string text(ini_text);
+    size_t pos = 0;
+    int lineno = 0;
+    while (pos <= text.size()) {
+        size_t nl = text.find('\n', pos);
+        if (nl == std::string::npos) nl = text.size();
+        std::string line = text.substr(pos, nl - pos);
+        pos = nl + 1;
+        ++lineno;
+        while (!line.empty() && line.back() == '\\' && pos <= text.size()) {
+            size_t nl2 = text.find('\n', pos);
+            if (nl2 == std::string::npos) nl2 = text.size();
+            line = line.substr(0, line.size() - 1) + text.substr(pos, nl2 - pos);
+            pos = nl2 + 1;
+            ++lineno;
+        }
+        // strip comment (not inside quotes)
+        bool inq = false;
+        for (size_t i = 0; i < line.size(); ++i) {
+            if (line[i] == '"') inq = !inq;
+            if (line[i] == '#' && !inq) { line = line.substr(0, i); break; }
+        }
+        line = trim(line);
+        if (line.empty()) continue;
+        if (line.front() == '[') {
+            const size_t e = line.find(']');
+            if (e == std::string::npos) { set_err("bad section header at line " + std::to_string(lineno)); return OVS_EINVAL; }
+            std::string name = trim(line.substr(1, e - 1));
+            if (name.rfind("Config ", 0) == 0) name = trim(name.substr(7));
+            cur = name;
+            secs[cur];
+            continue;
+        }
+        const size_t eq = line.find('=');
+        if (eq == std::string::npos) { set_err("expected key = value at line " + std::to_string(lineno)); return OVS_EINVAL; }
+        const std::string k = trim(line.substr(0, eq)), v = trim(line.substr(eq + 1));
+        if (k == "extends") {
+            size_t a = 0;
+            while (a <= v.size()) {
+                size_t c = v.find(',', a);
+                if (c == std::string::npos) c = v.size();
+                const std::string nm = trim(v.substr(a, c - a));
+                if (!nm.empty()) secs[cur].extends.push_back(nm);
+                a = c + 1;
+            }
+            continue;
+        }
+        secs[cur].entries.push_back({k, v});
+    }
+    // section lookup order
+    std::vector<std::string> order;
+    std::vector<std::string> stack;
+    if (config_name && *config_name && std::strcmp(config_name, "General") != 0) {
+        if (!secs.count(config_name)) { set_err(std::string("no such config: ") + config_name); return OVS_EINVAL; }
+        stack.push_back(config_name);
+    }
+    while (!stack.empty()) {
+        const std::string s = stack.front();
+        stack.erase(stack.begin());
+        bool seen = false;
+        for (auto& o : order) seen |= (o == s);
+        if (seen) continue;
+        if (!secs.count(s)) { set_err("extends unknown config: " + s); return OVS_EINVAL; }
+        order.push_back(s);
+        const auto& ex = secs[s].extends;
+        stack.insert(stack.begin(), ex.begin(), ex.end());
+    }
+    order.push_back("General");
+
+    std::string iter_key;
+    auto lookup = [&](const std::string& path, std::string* val) -> bool {
+        for (const auto& sname : order) {
+            for (const auto& e : secs[sname].entries) {
+                if (glob(e.key.c_str(), path.c_str())) {
+                    *val = e.value;
+                    if (e.value.find("${") != std::string::npos) iter_key = e.key;
+                    return true;
+                }
+            }
+        }
+        return false;
+    };
+
+    const std::string ov = p->overlay == OVS_OVERLAY_KADEMLIA ? "kademlia" : "chord";
+    const std::string host = "SimpleUnderlayNetwork.overlayTerminal[0]";
+    const std::string ovp = host + ".overlay." + ov + ".";
+    std::string v, bad;
+
+    auto want_int = [&](const std::string& name, int32_t* f) {
+        if (lookup(ovp + name, &v) && !to_int(unquote(v), f)) bad = name;
+    };
+    auto want_bool = [&](const std::string& name, int32_t* f) {
+        if (lookup(ovp + name, &v) && !to_bool(unquote(v), f)) bad = name;
+    };
+    want_int("keyLength", &p->keyLength);
+    want_int("hopCountMax", &p->hopCountMax);
+    if (p->overlay == OVS_OVERLAY_CHORD) {
+        want_int("successorListSize", &p->successorListSize);
+        want_bool("extendedFingerTable", &p->extendedFingerTable);
+        want_int("numFingerCandidates", &p->numFingerCandidates);
+    } else {
+        want_int("k", &p->k);
+        want_int("s", &p->s);
+        want_int("b", &p->b);
+    }
+    want_int("lookupRedundantNodes", &p->lookupRedundantNodes);
+    want_int("lookupParallelPaths", &p->lookupParallelPaths);
+    want_int("lookupParallelRpcs", &p->lookupParallelRpcs);
+    want_bool("lookupMerge", &p->lookupMerge);
+    want_bool("lookupStrictParallelRpcs", &p->lookupStrictParallelRpcs);
+    want_bool("lookupVisitOnlyOnce", &p->lookupVisitOnlyOnce);
+    want_bool("lookupAcceptLateSiblings", &p->lookupAcceptLateSiblings);
+    want_bool("lookupUseAllParallelResponses", &p->lookupUseAllParallelResponses);
+    want_bool("lookupNewRpcOnEveryTimeout", &p->lookupNewRpcOnEveryTimeout);
+    want_bool("lookupNewRpcOnEveryResponse", &p->lookupNewRpcOnEveryResponse);
+    want_bool("lookupFinishOnFirstUnchanged", &p->lookupFinishOnFirstUnchanged);
+    want_bool("lookupVerifySiblings", &p->lookupVerifySiblings);
+    want_bool("lookupMajoritySiblings", &p->lookupMajoritySiblings);
+    if (lookup(ovp + "routingType", &v)) {
+        const std::string rt = unquote(v);
+        if (rt == "iterative") p->routingType = 0;
+        else { set_err("routingType \"" + rt + "\" not supported (iterative only)"); return OVS_ENOTSUP; }
+    }
+    if (lookup(ovp + "rpcUdpTimeout", &v) && !to_seconds(unquote(v), &p->rpcUdpTimeout)) bad = "rpcUdpTimeout";
+    const std::string udp = host + ".udp.";
+    if (lookup(udp + "jitter", &v)) {
+        double x; std::string u;
+        if (!parse_number(unquote(v), &x, &u) || !u.empty()) bad = "jitter"; else p->jitter = x;
+    }
+    if (lookup(udp + "useCoordinateBasedDelay", &v) && !to_bool(unquote(v), &p->useCoordinateBasedDelay))
+        bad = "useCoordinateBasedDelay";
+    if (lookup(udp + "constantDelay", &v) && !to_seconds(unquote(v), &p->constantDelay)) bad = "constantDelay";
+    const std::string app = host + ".tier1.kbrTestApp.";
+    if (lookup(app + "testMsgSize", &v)) {
+        double b;
+        if (!to_bytes(unquote(v), &b)) bad = "testMsgSize"; else p->testMsgSize = (int32_t)b;
+    }
+    // channel parameters (channels.ned defaults unless overridden as ovs.datarate/ovs.accessDelay)
+    if (lookup("ovs.datarate", &v) && !to_bps(unquote(v), &p->datarate)) bad = "datarate";
+    if (lookup("ovs.accessDelay", &v) && !to_seconds(unquote(v), &p->accessDelay)) bad = "accessDelay";
+    if (lookup("ovs.simtimeRounding", &v)) {
+        const std::string r = unquote(v);
+        if (r == "round") p->simtimeRound = 1;
+        else if (r == "truncate") p->simtimeRound = 0;
+        else bad = "simtimeRounding";
+    }
+    if (!bad.empty()) { set_err("cannot parse value of " + bad + ": " + v); return OVS_EINVAL; }
+    if (!iter_key.empty()) {
+        set_err("parameter studies (${...}) are not supported: " + iter_key);
+        return OVS_ENOTSUP;
+    }
+    return OVS_OK;
+}

@@ -1,0 +1,557 @@
+// ovs_kbr.cpp -- host implementation of the C ABI declared in include/ovs_kbr.h.
+//
+// The context owns the device routing tables (sorted 24 B node records,
+// fp64 coordinates, CSR finger rows / Kademlia buckets) and one HIP stream.
+// Host-pointer calls stage through context-owned scratch buffers and are
+// synchronous; OVS_DEVICE_PTRS calls launch asynchronously on the caller's
+// stream.  No C++ exception crosses the boundary.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kad.hpp"
+#include "launch.hpp"
+
+using namespace ovs;
+
+struct ovs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    ovs_params P{};
+    int overlay = 0;          // loaded overlay
+    uint64_t n = 0;
+    bool ideal = true;
+    int num_cu = 0;
+    // chord
+    KeyRec* recs = nullptr;
+    double2* xy = nullptr;
+    uint32_t* fingers = nullptr;
+    uint64_t nfing = 0;
+    uint32_t* pred = nullptr;
+    uint32_t* succ = nullptr;
+    uint8_t* nsucc = nullptr;
+    uint32_t* fres = nullptr;
+    int sls = 0;
+    // kademlia
+    KadTables kad{};
+    // scratch for host-pointer calls
+    std::vector<void*> scratch;
+};
+
+namespace {
+
+ovs_status fail(ovs_ctx* c, ovs_status s, const std::string& m)
+{
+    if (c) c->err = m;
+    return s;
+}
+
+ovs_status hip_fail(ovs_ctx* c, hipError_t e, const char* where)
+{
+    return fail(c, OVS_EDEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(c, expr)                                        \
+    do {                                                       \
+        hipError_t e_ = (expr);                                \
+        if (e_ != hipSuccess) return hip_fail((c), e_, #expr); \
+    } while (0)
+
+void free_tables(ovs_ctx* c)
+{
+    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    c->recs = nullptr; c->xy = nullptr; c->fingers = nullptr; c->pred = nullptr;
+    c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
+    kad_free(c->kad);
+    c->overlay = 0; c->n = 0; c->nfing = 0;
+}
+
+void free_scratch(ovs_ctx* c)
+{
+    for (void* p : c->scratch)
+        if (p) hipFree(p);
+    c->scratch.clear();
+}
+
+// SimTime(double) on the host (identical IEEE double arithmetic to the device path)
+int64_t simtime_host(double seconds, int round)
+{
+    const double x = seconds * 1e9;
+    return round ? (int64_t)std::floor(x + 0.5) : (int64_t)x;
+}
+
+int32_t route_bytes(const ovs_params& P)
+{
+    // BASEROUTE_L 424 bits + BASEAPPDATA_L 40 bits + KBRTestMessage payload + UDP/IP 28 B
+    // (CommonMessages.msg:50-59, SimpleUDP.cc:291)
+    return 58 + P.testMsgSize + 28;
+}
+
+DelayConsts delay_consts(const ovs_params& P)
+{
+    DelayConsts d{};
+    d.round = P.simtimeRound;
+    auto bw = [&](int32_t bytes) { return simtime_host((double)((int64_t)bytes * 8) / P.datarate, P.simtimeRound); };
+    const int64_t acc = simtime_host(P.accessDelay, P.simtimeRound);
+    d.access2 = 2 * acc;
+    d.callBytes = 83;        // FINDNODECALL_L 440 bits + 28 B
+    d.respBase = 61;         // FINDNODERESPONSE_L 264 bits + 28 B
+    d.respPerNode = 26;      // NODEHANDLE_L 208 bits
+    d.msgCall = 2 * bw(d.callBytes) + 2 * acc;
+    d.msgResp1 = 2 * bw(d.respBase + d.respPerNode) + 2 * acc;
+    d.msgRoute = 2 * bw(route_bytes(P)) + 2 * acc;
+    d.rpcTimeout = simtime_host(P.rpcUdpTimeout, P.simtimeRound);
+    d.lookupTimeout = simtime_host(P.lookupTimeout, P.simtimeRound);
+    d.datarate = P.datarate;
+    return d;
+}
+
+ovs_status check_common(ovs_ctx* c, const ovs_params& P)
+{
+    if (P.keyLength != 160) return fail(c, OVS_ENOTSUP, "keyLength != 160 not supported");
+    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "only routingType = \"iterative\" is implemented");
+    if (P.lookupParallelPaths != 1) return fail(c, OVS_ENOTSUP, "lookupParallelPaths != 1 not supported");
+    if (P.lookupVerifySiblings || P.lookupMajoritySiblings)
+        return fail(c, OVS_ENOTSUP, "lookupVerifySiblings/lookupMajoritySiblings not supported");
+    if (P.jitter != 0.0)
+        return fail(c, OVS_ENOTSUP, "udp.jitter must be 0 (truncnormal jitter is not reproducible)");
+    if (!P.useCoordinateBasedDelay) return fail(c, OVS_ENOTSUP, "useCoordinateBasedDelay = false not supported");
+    if (P.numSiblings < 0 || P.numSiblings > 8) return fail(c, OVS_EINVAL, "numSiblings out of range");
+    if (P.hopCountMax < 0 || P.hopCountMax > 255) return fail(c, OVS_EINVAL, "hopCountMax out of range");
+    if (!(P.datarate > 0)) return fail(c, OVS_EINVAL, "datarate must be > 0");
+    return OVS_OK;
+}
+
+ovs_status check_chord_route(ovs_ctx* c, const ovs_params& P)
+{
+    if (P.lookupMerge) return fail(c, OVS_EINVAL, "Chord doesn't work with iterativeLookupConfig.merge = true!");
+    if (P.extendedFingerTable) return fail(c, OVS_ENOTSUP, "extendedFingerTable = true not supported");
+    if (P.lookupRedundantNodes != 1 || P.lookupParallelRpcs != 1 || P.numSiblings != 1)
+        return fail(c, OVS_ENOTSUP,
+                    "Chord route kernel implements lookupRedundantNodes=1, lookupParallelRpcs=1, numSiblings=1");
+    return OVS_OK;
+}
+
+template <class T>
+ovs_status to_device(ovs_ctx* c, const T* src, uint64_t count, bool dev, T** out, bool* owned)
+{
+    if (dev) { *out = const_cast<T*>(src); *owned = false; return OVS_OK; }
+    T* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, sizeof(T) * (count ? count : 1)));
+    if (count) HIPCHK(c, hipMemcpyAsync(d, src, sizeof(T) * count, hipMemcpyHostToDevice, c->stream));
+    *out = d; *owned = true;
+    return OVS_OK;
+}
+
+ChordView chord_view(const ovs_ctx* c)
+{
+    ChordView V{};
+    V.recs = c->recs; V.xy = c->xy; V.fingers = c->fingers; V.pred = c->pred; V.succ = c->succ;
+    V.nsucc = c->nsucc; V.fres = c->fres; V.n = (uint32_t)c->n;
+    V.ns = (int)std::min<uint64_t>((uint64_t)c->P.successorListSize, c->n - 1);
+    V.sls = c->sls;
+    V.numFingerCandidates = c->P.numFingerCandidates;
+    return V;
+}
+
+// upload sorted ids (+ coordinates) into KeyRec / double2 arrays
+ovs_status upload_nodes(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, bool dev)
+{
+    if (n < 2) return fail(c, OVS_EINVAL, "need at least 2 nodes");
+    if (n >= 0xFFFFFFFFull) return fail(c, OVS_EINVAL, "too many nodes for 32-bit node indices");
+    HIPCHK(c, hipMalloc(&c->recs, sizeof(KeyRec) * n));
+    HIPCHK(c, hipMalloc(&c->xy, sizeof(double2) * n));
+    // interleave 20 B keys into 24 B records with a strided 2-D copy
+    HIPCHK(c, hipMemset2DAsync(c->recs, sizeof(KeyRec), 0, sizeof(KeyRec), n, c->stream));
+    HIPCHK(c, hipMemcpy2DAsync(c->recs, sizeof(KeyRec), ids, sizeof(ovs_key160), sizeof(ovs_key160), n,
+                               dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->xy, xy, sizeof(double2) * n, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                             c->stream));
+    uint32_t* bad = nullptr;
+    HIPCHK(c, hipMalloc(&bad, sizeof(uint32_t)));
+    HIPCHK(c, hipMemsetAsync(bad, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, launch_check_sorted(c->recs, (uint32_t)n, bad, c->stream));
+    uint32_t hbad = 0;
+    HIPCHK(c, hipMemcpyAsync(&hbad, bad, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(bad);
+    if (hbad) return fail(c, OVS_EINVAL, "node ids must be sorted ascending and unique");
+    c->n = n;
+    return OVS_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+int ovs_abi_version(void) { return OVS_ABI_VERSION; }
+
+void ovs_params_default(int32_t overlay, ovs_params* p)
+{
+    std::memset(p, 0, sizeof *p);
+    p->overlay = overlay;
+    p->keyLength = 160;                 // default.ini:393
+    p->hopCountMax = 50;                // default.ini:385
+    p->successorListSize = 8;           // default.ini:174
+    p->extendedFingerTable = 0;         // default.ini:176
+    p->numFingerCandidates = 3;         // default.ini:177
+    p->k = 8; p->s = 8; p->b = 1;       // default.ini:197-199
+    p->lookupParallelPaths = 1;
+    p->lookupStrictParallelRpcs = 1;    // default.ini:425-433
+    p->lookupVisitOnlyOnce = 1;
+    p->lookupAcceptLateSiblings = 1;
+    p->numSiblings = 1;                 // BaseOverlay::route -> sendToKey(..., 1, ...) (BaseOverlay.cc:1357)
+    p->useCoordinateBasedDelay = 1;     // default.ini:546
+    p->simtimeRound = 1;
+    p->testMsgSize = 100;               // default.ini:37
+    p->rpcUdpTimeout = 1.5;             // default.ini:483
+    p->lookupTimeout = 10.0;            // IterativeLookup.h:44
+    p->jitter = 0.0;                    // default.ini:549 has 0.1; bit-exact latency needs 0
+    p->constantDelay = 0.05;            // default.ini:544
+    p->datarate = 10e6;                 // channels.ned simple_ethernetline
+    p->accessDelay = 0.0;
+    p->kadSeed = 0x4b41444dull;
+    if (overlay == OVS_OVERLAY_KADEMLIA) {
+        p->lookupRedundantNodes = 8;    // default.ini:186
+        p->lookupParallelRpcs = 3;      // default.ini:188
+        p->lookupMerge = 1;             // default.ini:189
+    } else {
+        p->lookupRedundantNodes = 1;    // default.ini:423
+        p->lookupParallelRpcs = 1;      // default.ini:425
+        p->lookupMerge = 0;             // default.ini:428
+    }
+}
+
+ovs_status ovs_ctx_create(int hip_device, ovs_ctx** out)
+{
+    if (!out) return OVS_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return OVS_EDEVICE;
+    if (hip_device < 0 || hip_device >= ndev) return OVS_EINVAL;
+    ovs_ctx* c = new (std::nothrow) ovs_ctx();
+    if (!c) return OVS_ENOMEM;
+    c->device = hip_device;
+    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return OVS_EDEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess) c->num_cu = prop.multiProcessorCount;
+    if (c->num_cu <= 0) c->num_cu = 256;
+    ovs_params_default(OVS_OVERLAY_CHORD, &c->P);
+    *out = c;
+    return OVS_OK;
+}
+
+void ovs_ctx_destroy(ovs_ctx* c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_tables(c);
+    free_scratch(c);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* ovs_last_error(const ovs_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+ovs_status ovs_set_params(ovs_ctx* c, const ovs_params* p)
+{
+    if (!c || !p) return OVS_EINVAL;
+    ovs_status s = check_common(c, *p);
+    if (s != OVS_OK) return s;
+    if (c->overlay && p->overlay != c->overlay) return fail(c, OVS_ESTATE, "overlay type differs from loaded network");
+    if (c->overlay == OVS_OVERLAY_KADEMLIA &&
+        (p->k != c->P.k || p->s != c->P.s || p->b != c->P.b || p->kadSeed != c->P.kadSeed))
+        return fail(c, OVS_ESTATE, "k/s/b/kadSeed are fixed once a Kademlia network is loaded");
+    c->P = *p;
+    return OVS_OK;
+}
+
+ovs_status ovs_get_params(const ovs_ctx* c, ovs_params* p)
+{
+    if (!c || !p) return OVS_EINVAL;
+    *p = c->P;
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint32_t flags)
+{
+    if (!c || !ids || !xy) return OVS_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    if (c->P.overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "params.overlay is not Chord");
+    ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    hipError_t e = launch_chord_build(c->recs, (uint32_t)n, &c->fingers, &c->nfing, c->stream);
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "chord finger build"); }
+    c->overlay = OVS_OVERLAY_CHORD;
+    c->ideal = true;
+    c->sls = c->P.successorListSize;
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy,
+                                 const uint32_t* pred, const uint32_t* succ, const uint8_t* nsucc,
+                                 const uint32_t* fingers, const uint8_t* deque_size, uint32_t flags)
+{
+    if (!c || !ids || !xy || !pred || !succ || !nsucc || !fingers || !deque_size) return OVS_EINVAL;
+    if (flags & OVS_DEVICE_PTRS) return fail(c, OVS_ENOTSUP, "explicit tables are taken from host memory");
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    if (c->P.overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "params.overlay is not Chord");
+    ovs_status s = upload_nodes(c, ids, n, xy, false);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    const int sls = c->P.successorListSize;
+    // resolve ChordFingerTable::getFinger(pos) on the host (ChordFingerTable.cc:174-193)
+    std::vector<uint32_t> fres((size_t)n * 160);
+    for (uint64_t v = 0; v < n; ++v) {
+        for (int pos = 0; pos < 160; ++pos) {
+            const uint32_t size = deque_size[v];
+            uint32_t p = 160 - pos - 1;
+            uint32_t r;
+            // deque entry p holds position 159 - p
+            auto entry = [&](uint32_t pp) { return fingers[v * 160 + (159 - pp)]; };
+            if (nsucc[v] == 0) return fail(c, OVS_EINVAL, "empty successor list");
+            if (p >= size) r = succ[v * sls];
+            else {
+                while (entry(p) == 0xFFFFFFFFu && (p < size - 1)) ++p;
+                r = entry(p) == 0xFFFFFFFFu ? succ[v * sls] : entry(p);
+            }
+            if (r >= n) return fail(c, OVS_EINVAL, "finger index out of range");
+            fres[v * 160 + pos] = r;
+        }
+        if (pred[v] != 0xFFFFFFFFu && pred[v] >= n) return fail(c, OVS_EINVAL, "pred index out of range");
+        if (nsucc[v] > sls) return fail(c, OVS_EINVAL, "nsucc > successorListSize");
+        for (int j = 0; j < nsucc[v]; ++j)
+            if (succ[v * sls + j] >= n) return fail(c, OVS_EINVAL, "successor index out of range");
+    }
+    HIPCHK(c, hipMalloc(&c->pred, sizeof(uint32_t) * n));
+    HIPCHK(c, hipMalloc(&c->succ, sizeof(uint32_t) * n * sls));
+    HIPCHK(c, hipMalloc(&c->nsucc, n));
+    HIPCHK(c, hipMalloc(&c->fres, sizeof(uint32_t) * n * 160));
+    HIPCHK(c, hipMemcpy(c->pred, pred, sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->succ, succ, sizeof(uint32_t) * n * sls, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->nsucc, nsucc, n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->fres, fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
+    c->overlay = OVS_OVERLAY_CHORD;
+    c->ideal = false;
+    c->sls = sls;
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_export_fingers(ovs_ctx* c, uint32_t* out)
+{
+    if (!c || !out) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "no Chord network loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t tot = c->n * 160;
+    if (!c->ideal) {
+        HIPCHK(c, hipMemcpy(out, c->fres, sizeof(uint32_t) * tot, hipMemcpyDeviceToHost));
+        return OVS_OK;
+    }
+    uint32_t* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, sizeof(uint32_t) * tot));
+    HIPCHK(c, launch_chord_export(c->recs, c->fingers, (uint32_t)c->n, d, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, d, sizeof(uint32_t) * tot, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(d);
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint32_t flags)
+{
+    if (!c || !ids || !xy) return OVS_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
+    if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
+    if (c->P.k < 1 || c->P.k > 32 || c->P.s < 1 || 5 * c->P.s > 64)
+        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..32 and 5*s <= 64");
+    ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    hipError_t e = kad_build(c->recs, (uint32_t)n, c->P.k, c->P.s, c->P.kadSeed, c->kad, c->stream);
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "kademlia table build"); }
+    c->overlay = OVS_OVERLAY_KADEMLIA;
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_export(ovs_ctx* c, uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes)
+{
+    if (!c || !siblings || !bucket_count || !bucket_nodes) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipError_t e = kad_export(c->kad, (uint32_t)c->n, siblings, bucket_count, bucket_nodes, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "kademlia export");
+    return OVS_OK;
+}
+
+ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                           ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs, uint32_t flags, void* stream)
+{
+    if (!c || (!keys && n) || (!src && n) || (!out && n)) return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    ovs_status st = check_common(c, c->P);
+    if (st != OVS_OK) return st;
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = (dev && stream) ? (hipStream_t)stream : c->stream;
+    const int H = c->P.hopCountMax > 0 ? c->P.hopCountMax : 1;
+    if (c->overlay == OVS_OVERLAY_CHORD) {
+        st = check_chord_route(c, c->P);
+        if (st != OVS_OK) return st;
+    }
+    if (n == 0) return OVS_OK;
+    // stage inputs
+    K160* dk = nullptr; uint32_t* ds = nullptr; ovs_route_out* dout = nullptr;
+    uint32_t* dhop = nullptr; uint32_t* drpc = nullptr;
+    bool ok_k = false, ok_s = false;
+    if (!dev) {
+        st = to_device(c, reinterpret_cast<const K160*>(keys), n, false, &dk, &ok_k);
+        if (st != OVS_OK) return st;
+        st = to_device(c, src, n, false, &ds, &ok_s);
+        if (st != OVS_OK) { hipFree(dk); return st; }
+        HIPCHK(c, hipMalloc(&dout, sizeof(ovs_route_out) * n));
+    } else {
+        dk = const_cast<K160*>(reinterpret_cast<const K160*>(keys));
+        ds = const_cast<uint32_t*>(src);
+        dout = out;
+    }
+    // hop sequence buffer: always needed for explicit Chord tables (visited check) and Kademlia
+    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal);
+    bool own_hop = false;
+    if (need_hop) {
+        if (dev && hop_seq) dhop = hop_seq;
+        else { HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H)); own_hop = true; }
+        HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
+    }
+    bool own_rpc = false;
+    if (rpcs) {
+        if (dev) drpc = rpcs;
+        else { HIPCHK(c, hipMalloc(&drpc, sizeof(uint32_t) * n)); own_rpc = true; }
+    }
+    hipError_t e;
+    if (c->overlay == OVS_OVERLAY_CHORD) {
+        LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes};
+        if (drpc) {
+            // Chord with alpha = 1: one FindNodeCall per hop; filled after the route below
+        }
+        e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, dk, ds, n, dout, dhop, c->num_cu, s);
+        if (e == hipSuccess && drpc) e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
+    } else {
+        e = kad_route(c->kad, c->recs, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
+                      c->num_cu, s);
+    }
+    if (e != hipSuccess) return hip_fail(c, e, "route kernel");
+    if (!dev) {
+        HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(ovs_route_out) * n, hipMemcpyDeviceToHost, s));
+        if (hop_seq) HIPCHK(c, hipMemcpyAsync(hop_seq, dhop, sizeof(uint32_t) * n * H, hipMemcpyDeviceToHost, s));
+        if (rpcs) HIPCHK(c, hipMemcpyAsync(rpcs, drpc, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        hipFree(dk); hipFree(ds); hipFree(dout);
+    } else if (own_hop || own_rpc) {
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    if (own_hop) hipFree(dhop);
+    if (own_rpc) hipFree(drpc);
+    return OVS_OK;
+}
+
+ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key160* keys, uint64_t n,
+                               int32_t numRedundantNodes, int32_t numSiblings, uint32_t* out_nodes,
+                               uint32_t max_out, uint8_t* out_count, uint8_t* out_sibling, uint32_t flags,
+                               void* stream)
+{
+    if (!c || (n && (!node || !keys || !out_nodes || !out_count || !out_sibling)) || max_out == 0) return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (numSiblings > (c->overlay == OVS_OVERLAY_CHORD ? c->P.successorListSize : c->P.s))
+        return fail(c, OVS_EINVAL, "numSiblings too big!");
+    if (numRedundantNodes < 1 || numRedundantNodes > 64) return fail(c, OVS_EINVAL, "numRedundantNodes out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = (dev && stream) ? (hipStream_t)stream : c->stream;
+    if (n == 0) return OVS_OK;
+    uint32_t* dn = nullptr; K160* dk = nullptr; uint32_t* dout = nullptr; uint8_t* dc = nullptr; uint8_t* dsb = nullptr;
+    bool o1, o2;
+    ovs_status st = to_device(c, node, n, dev, &dn, &o1);
+    if (st != OVS_OK) return st;
+    st = to_device(c, reinterpret_cast<const K160*>(keys), n, dev, &dk, &o2);
+    if (st != OVS_OK) return st;
+    if (!dev) {
+        HIPCHK(c, hipMalloc(&dout, sizeof(uint32_t) * n * max_out));
+        HIPCHK(c, hipMalloc(&dc, n));
+        HIPCHK(c, hipMalloc(&dsb, n));
+    } else { dout = out_nodes; dc = out_count; dsb = out_sibling; }
+    // validate node indices on the host for host calls
+    if (!dev) {
+        for (uint64_t i = 0; i < n; ++i)
+            if (node[i] >= c->n) return fail(c, OVS_EINVAL, "node index out of range");
+    }
+    hipError_t e;
+    if (c->overlay == OVS_OVERLAY_CHORD)
+        e = launch_chord_find_node(chord_view(c), c->ideal, dn, dk, n, numRedundantNodes, numSiblings, dout, max_out,
+                                   dc, dsb, s);
+    else
+        e = kad_find_node(c->kad, c->recs, (uint32_t)c->n, c->P, dn, dk, n, numRedundantNodes, numSiblings, dout,
+                          max_out, dc, dsb, s);
+    if (e != hipSuccess) return hip_fail(c, e, "findNode kernel");
+    if (!dev) {
+        HIPCHK(c, hipMemcpyAsync(out_nodes, dout, sizeof(uint32_t) * n * max_out, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(out_count, dc, n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(out_sibling, dsb, n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        hipFree(dn); hipFree(dk); hipFree(dout); hipFree(dc); hipFree(dsb);
+    }
+    return OVS_OK;
+}
+
+ovs_status ovs_delay_batch(ovs_ctx* c, const uint32_t* a, const uint32_t* b, const int32_t* bytes, uint64_t n,
+                           int64_t* out_ns, uint32_t flags, void* stream)
+{
+    if (!c || (n && (!a || !b || !bytes || !out_ns))) return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = (dev && stream) ? (hipStream_t)stream : c->stream;
+    if (n == 0) return OVS_OK;
+    if (!dev) {
+        for (uint64_t i = 0; i < n; ++i)
+            if (a[i] >= c->n || b[i] >= c->n) return fail(c, OVS_EINVAL, "node index out of range");
+    }
+    uint32_t *da, *db; int32_t* dbytes; int64_t* dout;
+    bool o1, o2, o3;
+    ovs_status st = to_device(c, a, n, dev, &da, &o1);
+    if (st == OVS_OK) st = to_device(c, b, n, dev, &db, &o2);
+    if (st == OVS_OK) st = to_device(c, bytes, n, dev, &dbytes, &o3);
+    if (st != OVS_OK) return st;
+    if (!dev) HIPCHK(c, hipMalloc(&dout, sizeof(int64_t) * n)); else dout = out_ns;
+    hipError_t e = launch_delay(c->xy, delay_consts(c->P), da, db, dbytes, n, dout, s);
+    if (e != hipSuccess) return hip_fail(c, e, "delay kernel");
+    if (!dev) {
+        HIPCHK(c, hipMemcpyAsync(out_ns, dout, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        hipFree(da); hipFree(db); hipFree(dbytes); hipFree(dout);
+    }
+    return OVS_OK;
+}
+
+ovs_status ovs_sync(ovs_ctx* c)
+{
+    if (!c) return OVS_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipDeviceSynchronize());
+    return OVS_OK;
+}
+
+}  // extern "C"

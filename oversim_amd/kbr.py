@@ -1,0 +1,316 @@
+"""Host-side mirror of OverSim's KBR lookup interface over the C ABI (include/ovs_kbr.h).
+
+Names follow the reference so a test reads like OverSim code:
+
+  KbrEngine.findNode(node, key, numRedundantNodes, numSiblings)
+        -> BaseOverlay::findNode (BaseOverlay.h:693-696; Chord.cc:548-599,
+           Kademlia.cc:1101-1246), evaluated at `node`
+  KbrEngine.isSiblingFor(node, key, numSiblings)
+        -> BaseOverlay::isSiblingFor (BaseOverlay.h:417-418), node == thisNode
+  KbrEngine.lookup(keys, src)
+        -> AbstractLookup::lookup + LookupListener::lookupFinished for a batch
+           of KBRTestApp one-way tests (IterativeLookup.cc:695-723,
+           BaseOverlay.cc:1241-1307)
+
+Errors raised by the engine become KbrError (the reference throws
+cRuntimeError).  There is no CPU fallback: importing this module without the
+built HIP library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+_LIB_PATH = Path(__file__).resolve().parent / "libovs_kbr.so"
+
+OVERLAY_CHORD = 1
+OVERLAY_KADEMLIA = 2
+DEVICE_PTRS = 0x1
+NONE = 0xFFFFFFFF
+
+STATUS = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "ESTATE", 5: "ENOTSUP"}
+LOOKUP_STATUS = {0: "OK", 1: "TIMEOUT", 2: "RPC_TIMEOUT", 3: "HOPMAX", 4: "NO_NEXT", 5: "BROKEN"}
+
+
+class KbrError(RuntimeError):
+    """cRuntimeError equivalent raised from an ovs_status != OVS_OK."""
+
+
+class Params(C.Structure):
+    """ovs_params; field names are the NED/.ini parameter names."""
+
+    _fields_ = [
+        ("overlay", C.c_int32), ("keyLength", C.c_int32), ("hopCountMax", C.c_int32),
+        ("successorListSize", C.c_int32), ("extendedFingerTable", C.c_int32),
+        ("numFingerCandidates", C.c_int32), ("k", C.c_int32), ("s", C.c_int32), ("b", C.c_int32),
+        ("lookupRedundantNodes", C.c_int32), ("lookupParallelPaths", C.c_int32),
+        ("lookupParallelRpcs", C.c_int32), ("lookupMerge", C.c_int32),
+        ("lookupStrictParallelRpcs", C.c_int32), ("lookupVisitOnlyOnce", C.c_int32),
+        ("lookupAcceptLateSiblings", C.c_int32), ("lookupUseAllParallelResponses", C.c_int32),
+        ("lookupNewRpcOnEveryTimeout", C.c_int32), ("lookupNewRpcOnEveryResponse", C.c_int32),
+        ("lookupFinishOnFirstUnchanged", C.c_int32), ("lookupVerifySiblings", C.c_int32),
+        ("lookupMajoritySiblings", C.c_int32), ("routingType", C.c_int32), ("numSiblings", C.c_int32),
+        ("useCoordinateBasedDelay", C.c_int32), ("simtimeRound", C.c_int32), ("testMsgSize", C.c_int32),
+        ("_pad0", C.c_int32), ("rpcUdpTimeout", C.c_double), ("lookupTimeout", C.c_double),
+        ("jitter", C.c_double), ("constantDelay", C.c_double), ("datarate", C.c_double),
+        ("accessDelay", C.c_double), ("kadSeed", C.c_uint64),
+    ]
+
+    @classmethod
+    def default(cls, overlay: int = OVERLAY_CHORD) -> "Params":
+        p = cls()
+        lib().ovs_params_default(overlay, C.byref(p))
+        return p
+
+    @classmethod
+    def chord(cls) -> "Params":
+        return cls.default(OVERLAY_CHORD)
+
+    @classmethod
+    def kademlia(cls) -> "Params":
+        return cls.default(OVERLAY_KADEMLIA)
+
+    @classmethod
+    def from_ini(cls, text: str, config: str | None = None, overlay: int = OVERLAY_CHORD,
+                 base: "Params | None" = None) -> "Params":
+        p = cls()
+        C.memmove(C.byref(p), C.byref(base), C.sizeof(cls)) if base is not None else lib().ovs_params_default(overlay, C.byref(p))
+        err = C.create_string_buffer(512)
+        st = lib().ovs_params_from_ini(C.byref(p), text.encode(), config.encode() if config else None, err, 512)
+        if st != 0:
+            raise KbrError(f"ovs_params_from_ini: {STATUS.get(st, st)}: {err.value.decode()}")
+        return p
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_ if not f.startswith("_")}
+
+    def replace(self, **kw) -> "Params":
+        p = Params()
+        C.memmove(C.byref(p), C.byref(self), C.sizeof(Params))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+
+ROUTE_OUT_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                            ("one_way_hops", "u1"), ("latency_ns", "<i8")])
+assert ROUTE_OUT_DTYPE.itemsize == 16
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libovs_kbr.so; raises if the HIP engine was not built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _LIB_PATH.exists():
+        raise ImportError(f"{_LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(the MI355X engine has no CPU fallback)")
+    L = C.CDLL(str(_LIB_PATH))
+    vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32
+    sigs = {
+        "ovs_abi_version": ([], C.c_int),
+        "ovs_params_default": ([i32, vp], None),
+        "ovs_params_from_ini": ([vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int], C.c_int),
+        "ovs_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
+        "ovs_ctx_destroy": ([vp], None),
+        "ovs_last_error": ([vp], C.c_char_p),
+        "ovs_set_params": ([vp, vp], C.c_int),
+        "ovs_get_params": ([vp, vp], C.c_int),
+        "ovs_chord_load": ([vp, vp, u64, vp, u32], C.c_int),
+        "ovs_chord_load_tables": ([vp, vp, u64, vp, vp, vp, vp, vp, vp, u32], C.c_int),
+        "ovs_kad_load": ([vp, vp, u64, vp, u32], C.c_int),
+        "ovs_kad_export": ([vp, vp, vp, vp], C.c_int),
+        "ovs_chord_export_fingers": ([vp, vp], C.c_int),
+        "ovs_route_batch": ([vp, vp, vp, u64, vp, vp, vp, u32, vp], C.c_int),
+        "ovs_find_node_batch": ([vp, vp, vp, u64, i32, i32, vp, u32, vp, vp, u32, vp], C.c_int),
+        "ovs_delay_batch": ([vp, vp, vp, vp, u64, vp, u32, vp], C.c_int),
+        "ovs_sync": ([vp], C.c_int),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def keys_array(keys) -> np.ndarray:
+    """(n,5) uint32 little-endian 32-bit words, w[0] least significant."""
+    a = np.ascontiguousarray(keys, dtype=np.uint32)
+    if a.ndim != 2 or a.shape[1] != 5:
+        raise ValueError("keys must have shape (n, 5) uint32")
+    return a
+
+
+def key_from_int(x: int) -> np.ndarray:
+    x &= (1 << 160) - 1
+    return np.array([(x >> (32 * i)) & 0xFFFFFFFF for i in range(5)], dtype=np.uint32)
+
+
+def key_to_int(w) -> int:
+    return sum(int(w[i]) << (32 * i) for i in range(5))
+
+
+class KbrEngine:
+    """One engine context per HIP device (ovs_ctx)."""
+
+    def __init__(self, device: int = 0, params: Params | None = None):
+        self._L = lib()
+        h = C.c_void_p()
+        st = self._L.ovs_ctx_create(device, C.byref(h))
+        if st != 0:
+            raise KbrError(f"ovs_ctx_create(device={device}) failed: {STATUS.get(st, st)}")
+        self._h = h
+        self.n = 0
+        self.overlay = 0
+        if params is not None:
+            self.set_params(params)
+
+    # -- plumbing
+    def _chk(self, st: int, what: str):
+        if st != 0:
+            msg = self._L.ovs_last_error(self._h)
+            raise KbrError(f"{what}: {STATUS.get(st, st)}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ovs_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self) -> int:
+        return self._h.value
+
+    # -- parameters
+    def set_params(self, p: Params):
+        self._chk(self._L.ovs_set_params(self._h, C.byref(p)), "ovs_set_params")
+
+    def get_params(self) -> Params:
+        p = Params()
+        self._chk(self._L.ovs_get_params(self._h, C.byref(p)), "ovs_get_params")
+        return p
+
+    # -- networks
+    def chord_load(self, ids, xy):
+        ids = keys_array(ids)
+        xy = np.ascontiguousarray(xy, dtype=np.float64)
+        self._chk(self._L.ovs_chord_load(self._h, _ptr(ids), len(ids), _ptr(xy), 0), "ovs_chord_load")
+        self.n, self.overlay = len(ids), OVERLAY_CHORD
+
+    def chord_load_tables(self, ids, xy, pred, succ, nsucc, fingers, deque_size):
+        ids = keys_array(ids)
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+                ((xy, np.float64), (pred, np.uint32), (succ, np.uint32), (nsucc, np.uint8),
+                 (fingers, np.uint32), (deque_size, np.uint8))]
+        self._chk(self._L.ovs_chord_load_tables(self._h, _ptr(ids), len(ids), *[_ptr(a) for a in arrs], 0),
+                  "ovs_chord_load_tables")
+        self.n, self.overlay = len(ids), OVERLAY_CHORD
+
+    def kad_load(self, ids, xy):
+        ids = keys_array(ids)
+        xy = np.ascontiguousarray(xy, dtype=np.float64)
+        self._chk(self._L.ovs_kad_load(self._h, _ptr(ids), len(ids), _ptr(xy), 0), "ovs_kad_load")
+        self.n, self.overlay = len(ids), OVERLAY_KADEMLIA
+
+    def chord_fingers(self) -> np.ndarray:
+        out = np.empty((self.n, 160), dtype=np.uint32)
+        self._chk(self._L.ovs_chord_export_fingers(self._h, _ptr(out)), "ovs_chord_export_fingers")
+        return out
+
+    def kad_tables(self):
+        p = self.get_params()
+        sib = np.empty((self.n, 5 * p.s), dtype=np.uint32)
+        cnt = np.empty((self.n, 160), dtype=np.uint8)
+        nodes = np.empty((self.n, 160, p.k), dtype=np.uint32)
+        self._chk(self._L.ovs_kad_export(self._h, _ptr(sib), _ptr(cnt), _ptr(nodes)), "ovs_kad_export")
+        return sib, cnt, nodes
+
+    # -- the hot path
+    def lookup(self, keys, src, record_hops: bool = False, count_rpcs: bool = False) -> dict:
+        """Batched KBRTestApp one-way lookups; returns numpy arrays by field."""
+        keys = keys_array(keys)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        if len(src) != n:
+            raise ValueError("keys and src differ in length")
+        out = np.empty(n, dtype=ROUTE_OUT_DTYPE)
+        H = max(self.get_params().hopCountMax, 1)
+        hop = np.empty((n, H), dtype=np.uint32) if record_hops else None
+        rpcs = np.empty(n, dtype=np.uint32) if count_rpcs else None
+        self._chk(self._L.ovs_route_batch(self._h, _ptr(keys), _ptr(src), n, _ptr(out), _ptr(hop), _ptr(rpcs), 0,
+                                          None), "ovs_route_batch")
+        res = {f: out[f].copy() for f in ROUTE_OUT_DTYPE.names}
+        if hop is not None:
+            res["hop_seq"] = hop
+        if rpcs is not None:
+            res["rpcs"] = rpcs
+        return res
+
+    def lookup_device(self, keys_ptr: int, src_ptr: int, n: int, out_ptr: int, stream: int | None = None,
+                      hop_ptr: int | None = None):
+        """Device-resident batch (pointers on this context's device, async on `stream`)."""
+        self._chk(self._L.ovs_route_batch(self._h, C.c_void_p(keys_ptr), C.c_void_p(src_ptr), n,
+                                          C.c_void_p(out_ptr), C.c_void_p(hop_ptr) if hop_ptr else None, None,
+                                          DEVICE_PTRS, C.c_void_p(stream) if stream else None), "ovs_route_batch")
+
+    def findNode(self, node, keys, numRedundantNodes: int, numSiblings: int, max_out: int = 16):
+        keys = keys_array(keys)
+        node = np.ascontiguousarray(node, dtype=np.uint32)
+        n = len(keys)
+        nodes = np.empty((n, max_out), dtype=np.uint32)
+        cnt = np.empty(n, dtype=np.uint8)
+        sib = np.empty(n, dtype=np.uint8)
+        self._chk(self._L.ovs_find_node_batch(self._h, _ptr(node), _ptr(keys), n, numRedundantNodes, numSiblings,
+                                              _ptr(nodes), max_out, _ptr(cnt), _ptr(sib), 0, None),
+                  "ovs_find_node_batch")
+        return nodes, cnt, sib
+
+    def isSiblingFor(self, node, keys, numSiblings: int = 1) -> np.ndarray:
+        _, _, sib = self.findNode(node, keys, 1, numSiblings, max_out=1)
+        return sib.astype(bool)
+
+    def delay_ns(self, a, b, nbytes) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        b = np.ascontiguousarray(b, dtype=np.uint32)
+        nbytes = np.ascontiguousarray(nbytes, dtype=np.int32)
+        out = np.empty(len(a), dtype=np.int64)
+        self._chk(self._L.ovs_delay_batch(self._h, _ptr(a), _ptr(b), _ptr(nbytes), len(a), _ptr(out), 0, None),
+                  "ovs_delay_batch")
+        return out
+
+    def sync(self):
+        self._chk(self._L.ovs_sync(self._h), "ovs_sync")
+
+
+@dataclass
+class Network:
+    """A generated overlay population: sorted unique ids + SimpleUnderlay coordinates."""
+
+    ids: np.ndarray   # (n,5) uint32
+    xy: np.ndarray    # (n,2) float64
+
+    @property
+    def n(self) -> int:
+        return len(self.ids)

@@ -1,0 +1,83 @@
+"""Seeded synthetic populations and lookup batches.
+
+The reference draws node IDs with OverlayKey::random() (OverlayKey.cc:673-682),
+lookup keys with KBRTestApp::createDestKey (KBRTestApp.cc:447-456: the ID of a
+random live node when lookupNodeIds = true, else a random key) and coordinates
+from nodes_2d_15000.xml (SimpleUnderlayConfigurator.cc:161-184) or
+uniform(0, fieldSize) - fieldSize/2 (SimpleNodeEntry.cc:86-87).  OMNeT++'s
+Mersenne-Twister streams are not reproduced; IDs, keys, sources and
+coordinates are *inputs* generated here from numpy PCG64 seeds and recorded
+in every fixture.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+
+_COORDS = Path(__file__).resolve().parent / "data" / "nodes_2d_15000.f64"
+
+
+def file_coords() -> np.ndarray:
+    """The 15 000 records of the reference's nodes_2d_15000.xml, (15000, 2) float64."""
+    return np.fromfile(_COORDS, dtype="<f8").reshape(-1, 2)
+
+
+def random_keys(n: int, rng: np.random.Generator) -> np.ndarray:
+    """Uniform 160-bit keys as (n,5) uint32 words (w[0] least significant)."""
+    return rng.integers(0, 1 << 32, size=(n, 5), dtype=np.uint64).astype(np.uint32)
+
+
+def sorted_unique_ids(n: int, seed: int) -> np.ndarray:
+    """n distinct uniform 160-bit IDs in ascending order."""
+    rng = np.random.default_rng(seed)
+    out = np.empty((0, 5), dtype=np.uint32)
+    need = n
+    while need > 0:
+        k = random_keys(need + need // 1000 + 8, rng)
+        out = np.concatenate([out, k])
+        # sort by the top 64 bits, ties by the rest (lexsort: last key is primary)
+        top = (out[:, 4].astype(np.uint64) << np.uint64(32)) | out[:, 3].astype(np.uint64)
+        low = (out[:, 2].astype(np.uint64) << np.uint64(32)) | out[:, 1].astype(np.uint64)
+        order = np.lexsort((out[:, 0], low, top))
+        out = out[order]
+        dup = np.zeros(len(out), dtype=bool)
+        dup[1:] = np.all(out[1:] == out[:-1], axis=1)
+        out = out[~dup]
+        if len(out) > n:
+            # drop surplus uniformly at random (keeps the distribution uniform)
+            keep = np.sort(rng.choice(len(out), size=n, replace=False))
+            out = out[keep]
+        need = n - len(out)
+    return np.ascontiguousarray(out)
+
+
+def coordinates(n: int, seed: int, field_size: int = 150, use_file: bool | None = None) -> np.ndarray:
+    """SimpleUnderlay coordinates: file records (n <= 15000) or uniform(-fs/2, fs/2)."""
+    rng = np.random.default_rng(seed ^ 0xC0FFEE)
+    recs = file_coords()
+    if use_file is None:
+        use_file = n <= len(recs)
+    if use_file:
+        if n > len(recs):
+            raise ValueError("No unused coordinates left (SimpleUnderlayConfigurator.cc:165-176)")
+        return np.ascontiguousarray(recs[rng.permutation(len(recs))[:n]])
+    # uniform(0, fieldSize) - fieldSize / 2  (integer division of the uint32 fieldSize)
+    return rng.random((n, 2)) * float(field_size) - float(field_size // 2)
+
+
+def lookups(ids: np.ndarray, m: int, seed: int, node_ids: bool = True) -> tuple[np.ndarray, np.ndarray]:
+    """m (key, source) pairs: key = ID of a uniform random node (lookupNodeIds) or a uniform key."""
+    rng = np.random.default_rng(seed)
+    n = len(ids)
+    src = rng.integers(0, n, size=m, dtype=np.int64).astype(np.uint32)
+    if node_ids:
+        keys = ids[rng.integers(0, n, size=m, dtype=np.int64)]
+    else:
+        keys = random_keys(m, rng)
+    return np.ascontiguousarray(keys), src
+
+
+def population(n: int, seed: int, use_file: bool | None = None):
+    from .kbr import Network
+    return Network(ids=sorted_unique_ids(n, seed), xy=coordinates(n, seed, use_file=use_file))

@@ -1,0 +1,93 @@
+"""Generate the committed golden vectors under tests/golden/.
+
+Provenance: the reference (trucndt/oversim) needs OMNeT++ 4.x + INET and cannot
+be built in this image, and ships no routing fixtures.  These vectors are
+therefore produced by the CPU restatement in oracle/ (ovs_oracle.c) and, for
+every Chord case, re-derived independently by tests/refmodel.py before being
+written; a disagreement aborts generation.  They freeze the restated
+reference semantics so that regressions of either the oracle or the engine
+are caught.  Inputs (IDs, coordinates, keys, sources) come from the seeded
+generator in oversim_amd/workload.py; coordinates for N <= 15000 are records of
+the reference's simulations/nodes_2d_15000.xml.
+
+Each .npz records the SimTime rounding rule it was generated with.
+Run: python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent.parent))
+sys.path.insert(0, str(HERE.parent))
+
+from oversim_amd import workload as W  # noqa: E402
+from oracle_lib import OracleNet, chord_params, kad_params  # noqa: E402
+import refmodel  # noqa: E402
+
+
+def chord_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: int):
+    net = W.population(n, seed)
+    k1, s1 = W.lookups(net.ids, m_ids, seed + 1, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m_rand, seed + 2, node_ids=False)
+    keys = np.concatenate([k1, k2])
+    src = np.concatenate([s1, s2])
+    o = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd))
+    r = o.route(keys, src, record_hops=True)
+    ring = refmodel.ChordRing(net.ids, net.xy, rnd=bool(rnd))
+    for i in range(len(keys)):
+        m = ring.lookup(keys[i], int(src[i]))
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+            assert int(r[f][i]) == int(m[f]), (name, i, f, r[f][i], m[f])
+        assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == m["hop_seq"], (name, i)
+    H = int(r["hops"].max()) + 1
+    np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=keys, src=src,
+                        responsible=r["responsible"], hops=r["hops"], status=r["status"],
+                        one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"],
+                        hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed))
+    print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
+
+
+def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
+    net = W.population(n, seed)
+    k1, s1 = W.lookups(net.ids, m, seed + 1, node_ids=True)
+    p = kad_params(lookupParallelRpcs=alpha, simtimeRound=rnd)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sib, cnt, nodes = o.kad_tables()
+    # findNode restated twice: oracle vs refmodel on the oracle's own snapshot
+    tab = refmodel.KadTables(net.ids, sib, cnt, nodes, k=p.k, s=p.s)
+    rng = np.random.default_rng(seed + 3)
+    fn_node = rng.integers(0, n, 512).astype(np.uint32)
+    fn_key = np.concatenate([W.random_keys(256, rng), net.ids[rng.integers(0, n, 256)]])
+    fn_out = np.full((512, 8), 0xFFFFFFFF, dtype=np.uint32)
+    fn_sib = np.zeros(512, dtype=np.uint8)
+    for i in range(512):
+        res, flag = o.find_node(int(fn_node[i]), fn_key[i], 8, 1)
+        ref = tab.find_node(int(fn_node[i]), refmodel.to_int(fn_key[i]), 8, 1)
+        assert [int(x) for x in res] == ref, (name, i, res, ref)
+        assert flag == tab.is_sibling_for(int(fn_node[i]), refmodel.to_int(fn_key[i]), 1)
+        fn_out[i, :len(res)] = res
+        fn_sib[i] = flag
+    r = o.route(k1, s1, record_hops=True, count_rpcs=True)
+    H = int(r["hops"].max()) + 1
+    np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=k1, src=s1, alpha=np.int32(alpha),
+                        responsible=r["responsible"], hops=r["hops"], status=r["status"],
+                        one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"], rpcs=r["rpcs"],
+                        hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed),
+                        kad_seed=np.uint64(p.kadSeed), fn_node=fn_node, fn_key=fn_key, fn_out=fn_out,
+                        fn_sib=fn_sib)
+    print(name, "lookups", len(k1), "mean hops", r["hops"].mean(), "rpcs", r["rpcs"].mean(),
+          "status", np.bincount(r["status"]))
+
+
+if __name__ == "__main__":
+    chord_case("chord_n1000_round", 1000, 0x4213, 4096, 4096, 1)
+    chord_case("chord_n1000_trunc", 1000, 0x4213, 2048, 2048, 0)
+    chord_case("chord_n9", 9, 5, 256, 256, 1)
+    chord_case("chord_n2", 2, 6, 64, 64, 1)
+    if "--kad" in sys.argv:
+        kad_case("kad_n2000_a1", 2000, 0x4b41, 2048, 1)
+        kad_case("kad_n2000_a3", 2000, 0x4b41, 2048, 3)

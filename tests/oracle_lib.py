@@ -1,0 +1,167 @@
+"""ctypes binding of the CPU oracle (oracle/ovs_oracle.h) -- test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+_SO = ROOT / "oracle" / "_build" / "libovs_oracle.so"
+
+ROUTE_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                        ("one_way_hops", "u1"), ("latency_ns", "<i8")])
+
+
+class OrcParams(C.Structure):
+    _fields_ = [
+        ("hopCountMax", C.c_int32), ("successorListSize", C.c_int32), ("numFingerCandidates", C.c_int32),
+        ("k", C.c_int32), ("s", C.c_int32), ("b", C.c_int32),
+        ("lookupRedundantNodes", C.c_int32), ("lookupParallelRpcs", C.c_int32), ("lookupMerge", C.c_int32),
+        ("lookupStrictParallelRpcs", C.c_int32), ("lookupVisitOnlyOnce", C.c_int32),
+        ("lookupAcceptLateSiblings", C.c_int32), ("lookupUseAllParallelResponses", C.c_int32),
+        ("lookupNewRpcOnEveryTimeout", C.c_int32), ("lookupNewRpcOnEveryResponse", C.c_int32),
+        ("lookupFinishOnFirstUnchanged", C.c_int32), ("numSiblings", C.c_int32), ("simtimeRound", C.c_int32),
+        ("rpcUdpTimeout", C.c_double), ("lookupTimeout", C.c_double), ("datarate", C.c_double),
+        ("accessDelay", C.c_double), ("callBytes", C.c_int32), ("respBaseBytes", C.c_int32),
+        ("respPerNodeBytes", C.c_int32), ("routeBytes", C.c_int32), ("kadSeed", C.c_uint64),
+    ]
+
+    def replace(self, **kw) -> "OrcParams":
+        p = OrcParams()
+        C.memmove(C.byref(p), C.byref(self), C.sizeof(OrcParams))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+
+_L = None
+
+
+def lib() -> C.CDLL:
+    global _L
+    if _L is None:
+        if not _SO.exists():
+            import subprocess
+            subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+        L = C.CDLL(str(_SO))
+        vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+        for name, args, res in [
+            ("orc_key_cmp", [vp, vp], C.c_int),
+            ("orc_key_add", [vp, vp, vp], None),
+            ("orc_key_sub", [vp, vp, vp], None),
+            ("orc_key_xor", [vp, vp, vp], None),
+            ("orc_key_between", [C.c_int, vp, vp, vp, C.c_int], C.c_int),
+            ("orc_key_bit_range", [vp, u32, u32], u32),
+            ("orc_key_shared_prefix", [vp, vp, u32], u32),
+            ("orc_key_log2", [vp], C.c_int),
+            ("orc_key_pow2", [u32, vp], None),
+            ("orc_params_chord_default", [vp], None),
+            ("orc_params_kad_default", [vp], None),
+            ("orc_chord_build", [vp, u32, vp, vp], vp),
+            ("orc_chord_build_tables", [vp, u32, vp, vp, vp, vp, u32, vp, vp, vp], vp),
+            ("orc_kad_build", [vp, u32, vp, vp], vp),
+            ("orc_net_free", [vp], None),
+            ("orc_kad_export", [vp, vp, vp, vp], None),
+            ("orc_chord_export_fingers", [vp, vp], None),
+            ("orc_find_node", [vp, u32, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int)], C.c_int),
+            ("orc_route_batch", [vp, vp, vp, u64, vp, vp, vp, C.c_int], u64),
+            ("orc_delay_ns", [vp, u32, u32, i32], C.c_int64),
+            ("orc_coord_dist", [vp, u32, u32], C.c_float),
+            ("orc_last_error", [], C.c_char_p),
+        ]:
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _L = L
+    return _L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def chord_params(**kw) -> OrcParams:
+    p = OrcParams()
+    lib().orc_params_chord_default(C.byref(p))
+    return p.replace(**kw) if kw else p
+
+
+def kad_params(**kw) -> OrcParams:
+    p = OrcParams()
+    lib().orc_params_kad_default(C.byref(p))
+    return p.replace(**kw) if kw else p
+
+
+class OracleNet:
+    """A network built by the oracle (Chord stable state or Kademlia snapshot)."""
+
+    def __init__(self, kind: str, ids, xy, params: OrcParams | None = None, tables: dict | None = None):
+        self.ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        self.xy = np.ascontiguousarray(xy, dtype=np.float64)
+        self.kind = kind
+        L = lib()
+        n = len(self.ids)
+        if kind == "chord":
+            self.params = params or chord_params()
+            if tables is None:
+                h = L.orc_chord_build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+            else:
+                t = {k: np.ascontiguousarray(v) for k, v in tables.items()}
+                self._keep = t
+                h = L.orc_chord_build_tables(_p(self.ids), n, _p(self.xy), _p(t["pred"].astype(np.uint32)),
+                                             _p(t["succ"]), _p(t["nsucc"]), t["succ"].shape[1], _p(t["fingers"]),
+                                             _p(t["deque_size"]), C.byref(self.params))
+        else:
+            self.params = params or kad_params()
+            h = L.orc_kad_build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+        if not h:
+            raise RuntimeError(f"oracle build failed: {L.orc_last_error().decode()}")
+        self._h = C.c_void_p(h)
+        self.n = n
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_net_free(self._h)
+            self._h = None
+
+    def route(self, keys, src, record_hops=True, count_rpcs=False, nthreads=0) -> dict:
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        out = np.empty(n, dtype=ROUTE_DTYPE)
+        H = max(self.params.hopCountMax, 1)
+        hop = np.empty((n, H), dtype=np.uint32) if record_hops else None
+        rpcs = np.empty(n, dtype=np.uint32) if count_rpcs else None
+        lib().orc_route_batch(self._h, _p(keys), _p(src), n, _p(out), _p(hop), _p(rpcs), nthreads)
+        res = {f: out[f].copy() for f in ROUTE_DTYPE.names}
+        if hop is not None:
+            res["hop_seq"] = hop
+        if rpcs is not None:
+            res["rpcs"] = rpcs
+        return res
+
+    def find_node(self, node: int, key, numRedundantNodes: int, numSiblings: int):
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        out = np.empty(64, dtype=np.uint32)
+        flag = C.c_int(0)
+        cnt = lib().orc_find_node(self._h, int(node), _p(key), numRedundantNodes, numSiblings, _p(out), C.byref(flag))
+        return list(out[:cnt]), bool(flag.value)
+
+    def chord_fingers(self) -> np.ndarray:
+        out = np.empty((self.n, 160), dtype=np.uint32)
+        lib().orc_chord_export_fingers(self._h, _p(out))
+        return out
+
+    def kad_tables(self):
+        sib = np.empty((self.n, 5 * self.params.s), dtype=np.uint32)
+        cnt = np.empty((self.n, 160), dtype=np.uint8)
+        nodes = np.empty((self.n, 160, self.params.k), dtype=np.uint32)
+        lib().orc_kad_export(self._h, _p(sib), _p(cnt), _p(nodes))
+        return sib, cnt, nodes
+
+    def delay_ns(self, a: int, b: int, nbytes: int) -> int:
+        return int(lib().orc_delay_ns(self._h, a, b, nbytes))
