@@ -461,18 +461,32 @@ hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint
     return hipGetLastError();
 }
 
+template <bool IDEAL, bool RECORD>
+static int route_blocks_per_cu()
+{
+    static int bpc = 0;
+    if (bpc == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_route<IDEAL, RECORD>, 256, 0) != hipSuccess || b < 1)
+            b = 1;
+        bpc = b;
+    }
+    return bpc;
+}
+
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                              uint32_t* hopseq, int grid_blocks, hipStream_t s)
+                              uint32_t* hopseq, int num_cu, hipStream_t s)
 {
     if (nq == 0) return hipSuccess;
-    const uint64_t waves = (uint64_t)grid_blocks * 4;   // 256 threads = 4 waves
-    uint64_t blocks = (uint64_t)grid_blocks;
+    // persistent grid: every resident wave owns one contiguous slice of the batch
+    const int bpc = ideal ? (hopseq ? route_blocks_per_cu<true, true>() : route_blocks_per_cu<true, false>())
+                          : route_blocks_per_cu<false, true>();
+    const uint64_t waves = (uint64_t)num_cu * bpc * 4;   // 256 threads = 4 waves per block
     uint64_t chunk = (nq + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
-    // small batches: do not launch waves that have nothing to do
     const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    blocks = (need_waves + 3) / 4;
+    const uint64_t blocks = (need_waves + 3) / 4;
     const dim3 g((unsigned)blocks), b(256);
     if (ideal) {
         if (hopseq) hipLaunchKernelGGL((k_chord_route<true, true>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);

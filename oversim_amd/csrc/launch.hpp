@@ -11,7 +11,7 @@ hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint
                                hipStream_t s);
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                              uint32_t* hopseq, int grid_blocks, hipStream_t s);
+                              uint32_t* hopseq, int num_cu, hipStream_t s);
 hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,
                                   uint64_t n, int numRedundant, int numSiblings, uint32_t* out_nodes,
                                   uint32_t max_out, uint8_t* out_count, uint8_t* out_sib, hipStream_t s);
