@@ -25,6 +25,7 @@ struct DelayConsts {
     int32_t respBase;    // FindNodeResponse bytes with zero nodes (61 B)
     int32_t respPerNode; // 26 B per NodeHandle
     int32_t callBytes;   // 83 B
+    int32_t routeBytes;  // one-way route message, 186 B for testMsgSize = 100 B
     double datarate;
     int64_t access2;     // 2*T(accessDelay)
 };

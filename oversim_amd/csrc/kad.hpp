@@ -4,18 +4,47 @@
 
 namespace ovs {
 
-// Kademlia snapshot on the device (DESIGN.md "Kademlia snapshot rule").
-//  sib[n*S5]      : sibling table, XOR-sorted to the owner, NONE padded (S5 = 5s)
-//  nsib[n]
-//  boff[n*161]    : CSR offsets of the owner's non-empty buckets by index m
-//  bnodes[...]    : bucket members (up to k per bucket)
+// 64 B node record of the Kademlia snapshot (one HBM line per responder visit):
+//  key   : node id
+//  R     : key ^ back(siblingTable)  -- the sibling radius; isSiblingFor's
+//          "(self ^ key) > (self ^ back)" test (Kademlia.cc:923-935)
+//  mask  : OR over siblings s of 2^msb(s ^ key) -- with it, "self is the
+//          XOR-closest of siblings + self" is (D & mask) == 0 for D = self ^ lookup key
+//  boff  : first bucket slot of the node's row; slot s <-> bucket m = 159 - s,
+//          for m = 159 .. endIndex = msb(R) (buckets below endIndex are all siblings)
+struct alignas(16) KadRec {
+    uint32_t key[5];
+    uint32_t R[5];
+    uint32_t mask[5];
+    uint32_t boff;
+};
+static_assert(sizeof(KadRec) == 64, "KadRec must be one 64 B line");
+
+// bucket entry with the member's key inline (24 B); a slot holds k entries,
+// NONE idx marks an empty entry (entries are packed at the front)
+struct KadEntry {
+    uint32_t key[5];
+    uint32_t idx;
+};
+
 struct KadTables {
-    uint32_t* sib = nullptr;
-    uint8_t* nsib = nullptr;
-    uint32_t* bcount = nullptr;   // n*160 packed counts (u8 in u32 words: 4 per word) -- see kad.hip
-    uint32_t* bnodes = nullptr;   // n*160*k, NONE padded
+    KadRec* recs = nullptr;
+    uint32_t* sib = nullptr;      // n * S5 member indices (unordered set), NONE padded
+    KadEntry* slots = nullptr;    // total_slots * k
+    uint64_t total_slots = 0;
     int k = 8, s = 8;
     uint64_t seed = 0;
+};
+
+struct KadView {
+    const KadRec* __restrict__ recs;
+    const double2* __restrict__ xy;
+    const uint32_t* __restrict__ sib;
+    const KadEntry* __restrict__ slots;
+    uint32_t n;
+    int k;
+    int S5;       // sibling table capacity 5s
+    int nsib;     // entries in every sibling table = min(5s, n-1)
 };
 
 void kad_free(KadTables& t);

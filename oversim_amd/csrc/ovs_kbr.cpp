@@ -104,6 +104,7 @@ DelayConsts delay_consts(const ovs_params& P)
     d.callBytes = 83;        // FINDNODECALL_L 440 bits + 28 B
     d.respBase = 61;         // FINDNODERESPONSE_L 264 bits + 28 B
     d.respPerNode = 26;      // NODEHANDLE_L 208 bits
+    d.routeBytes = route_bytes(P);
     d.msgCall = 2 * bw(d.callBytes) + 2 * acc;
     d.msgResp1 = 2 * bw(d.respBase + d.respPerNode) + 2 * acc;
     d.msgRoute = 2 * bw(route_bytes(P)) + 2 * acc;

@@ -1,0 +1,115 @@
+"""GPU parity tests for the Kademlia path (snapshot builder, findNode, K2 kad_route).
+
+Same bar as Chord: bit-exact responsible node, hop count, hop sequence, status,
+RPC count and int64-ns latency against the CPU oracle and the golden vectors.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oversim_amd import KbrEngine, Params, workload as W
+from oracle_lib import OracleNet, kad_params
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+FIELDS = ("responsible", "hops", "status", "one_way_hops", "latency_ns")
+
+
+def _eq(a, b, label, hop_cols=None, rpcs=False):
+    for f in FIELDS + (("rpcs",) if rpcs else ()):
+        x, y = np.asarray(a[f]).astype(np.int64), np.asarray(b[f]).astype(np.int64)
+        bad = np.nonzero(x != y)[0]
+        assert len(bad) == 0, f"{label}: {f} differs at {bad[:8]}: gpu={x[bad[:8]]} ref={y[bad[:8]]}"
+    if hop_cols:
+        assert np.array_equal(a["hop_seq"][:, :hop_cols], b["hop_seq"][:, :hop_cols]), f"{label}: hop sequences"
+
+
+def _load(engine, ids, xy, **kw):
+    engine.set_params(Params.kademlia().replace(**kw))
+    engine.kad_load(ids, xy)
+
+
+@pytest.mark.parametrize("n,seed", [(2, 1), (9, 2), (40, 3), (41, 4), (42, 5), (2000, 6), (15000, 0x4b41)])
+def test_snapshot_tables_match_oracle(engine: KbrEngine, n, seed):
+    net = W.population(n, seed)
+    _load(engine, net.ids, net.xy)
+    sib, cnt, nodes = engine.kad_tables()
+    o = OracleNet("kademlia", net.ids, net.xy)
+    osib, ocnt, onodes = o.kad_tables()
+    for v in range(n):
+        assert set(sib[v][sib[v] != 0xFFFFFFFF]) == set(osib[v][osib[v] != 0xFFFFFFFF]), f"siblings of {v}"
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(nodes, onodes)
+
+
+@pytest.mark.parametrize("name", ["kad_n2000_a1", "kad_n2000_a3"])
+def test_golden_vectors(engine: KbrEngine, name):
+    g = np.load(GOLD / f"{name}.npz")
+    _load(engine, g["ids"], g["xy"], lookupParallelRpcs=int(g["alpha"]), simtimeRound=int(g["simtime_round"]),
+          kadSeed=int(g["kad_seed"]))
+    nodes, cnt, sib = engine.findNode(g["fn_node"], g["fn_key"], 8, 1, max_out=8)
+    assert np.array_equal(nodes, g["fn_out"])
+    assert np.array_equal(sib, g["fn_sib"])
+    r = engine.lookup(g["keys"], g["src"], record_hops=True, count_rpcs=True)
+    H = g["hop_seq"].shape[1]
+    _eq(r, {f: g[f] for f in FIELDS + ("rpcs", "hop_seq")}, name, hop_cols=H, rpcs=True)
+
+
+def test_find_node_matches_oracle(engine: KbrEngine):
+    net = W.population(15000, 0x4b41)
+    _load(engine, net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy)
+    rng = np.random.default_rng(9)
+    node = rng.integers(0, 15000, 4000).astype(np.uint32)
+    keys = np.concatenate([W.random_keys(2000, rng), net.ids[rng.integers(0, 15000, 2000)]])
+    keys[:200] = net.ids[node[:200]]                      # own id
+    keys[200:400] = net.ids[(node[200:400].astype(np.int64) + 1) % 15000]
+    for nr in (8, 3, 16):
+        got, cnt, sib = engine.findNode(node, keys, nr, 1, max_out=16)
+        for i in range(len(node)):
+            ref, flag = o.find_node(int(node[i]), keys[i], nr, 1)
+            assert list(got[i, :cnt[i]]) == ref, (nr, i)
+            assert bool(sib[i]) == flag, (nr, i)
+
+
+@pytest.mark.parametrize("alpha", [1, 2, 3])
+def test_route_config_b(engine: KbrEngine, alpha):
+    """Config B: 15000 nodes (nodes_2d_15000 coordinates), node-ID keys."""
+    net = W.population(15000, 0x4b41)
+    p = kad_params(lookupParallelRpcs=alpha)
+    _load(engine, net.ids, net.xy, lookupParallelRpcs=alpha)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    k1, s1 = W.lookups(net.ids, 30000, 40 + alpha, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 10000, 50 + alpha, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    g = engine.lookup(keys, src, record_hops=True, count_rpcs=True)
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    _eq(g, r, f"kad 15000 alpha={alpha}", hop_cols=50, rpcs=True)
+
+
+def test_route_large_ring_vs_oracle(engine: KbrEngine):
+    net = W.population(1 << 18, 77)
+    p = kad_params(lookupParallelRpcs=3)
+    _load(engine, net.ids, net.xy, lookupParallelRpcs=3)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    keys, src = W.lookups(net.ids, 50000, 78, node_ids=False)
+    g = engine.lookup(keys, src, record_hops=True, count_rpcs=True)
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    _eq(g, r, "kad 2^18 alpha=3", hop_cols=50, rpcs=True)
+
+
+def test_route_config_b_full_batch(engine: KbrEngine):
+    """Config B at full size (1M lookups): size-independent properties."""
+    net = W.population(15000, 0x4b41)
+    _load(engine, net.ids, net.xy, lookupParallelRpcs=1)
+    keys, src = W.lookups(net.ids, 1_000_000, 60, node_ids=True)
+    g = engine.lookup(keys, src, count_rpcs=True)
+    assert np.all(g["status"] == 0)
+    ok = g["responsible"]
+    # node-ID keys: the lookup must end at the node that owns the key
+    kid = keys.view(np.uint32).reshape(-1, 5)
+    assert np.array_equal(net.ids[ok], kid)
+    assert np.all(g["rpcs"] == g["hops"])          # alpha = 1: every RPC answered and accepted
