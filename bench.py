@@ -129,6 +129,7 @@ def main():
             sh.run()
 
     torch.cuda.synchronize()
+    torch.cuda.set_stream(stream)        # every launch of the step is ordered on `stream`
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()

@@ -27,8 +27,9 @@
  * Ownership: the caller owns every input/output buffer; the context owns the
  * device routing tables.  Buffers are host memory unless the call's `flags`
  * include OVS_DEVICE_PTRS, in which case they are device pointers on the
- * context's device and the call is asynchronous on `stream` (NULL = the
- * context's own stream).  Host-pointer calls are synchronous.
+ * context's device and the call is asynchronous on `stream` (NULL = the HIP
+ * default stream, as everywhere in HIP).  Host-pointer calls are synchronous
+ * and run on the context's own stream.
  */
 #ifndef OVS_KBR_H
 #define OVS_KBR_H
@@ -180,6 +181,47 @@ ovs_status  ovs_delay_batch(ovs_ctx* ctx, const uint32_t* a, const uint32_t* b,
                             uint32_t flags, void* stream);
 
 ovs_status  ovs_sync(ovs_ctx* ctx);
+
+/* ---- multi-GPU sharding (one process per GPU; the host exchanges records) ----
+ * The sorted ring is cut into contiguous arcs, one per rank.  Node keys and
+ * coordinates are replicated (24 + 16 B per node); the finger rows -- the bulk
+ * of the routing state -- exist only for the rank's own arc, so a lookup is
+ * handed to the rank that owns its next responder.  The exchange of in-flight
+ * records between hop rounds is done by the caller (RCCL all-to-allv over xGMI,
+ * see oversim_amd/shard.py).  All shard calls take device pointers. */
+typedef struct ovs_lookup_rec {     /* 48 B in-flight lookup */
+    uint32_t key[5];                /* lookup key */
+    uint32_t src;                   /* global index of the source node */
+    uint32_t cur;                   /* global index of the node whose findNode runs next */
+    uint32_t qid;                   /* caller's lookup id */
+    int64_t  t_ns;                  /* simulated time since lookup start */
+    uint16_t hops;
+    uint8_t  local;                 /* 1: the source's local step (no hop, no delay) is pending */
+    uint8_t  pad[5];
+} ovs_lookup_rec;
+
+typedef struct ovs_done_rec {       /* 24 B finished lookup */
+    uint32_t qid;
+    uint32_t pad;
+    ovs_route_out out;
+} ovs_done_rec;
+
+/* Load arc [lo, hi) of a Chord ring of n_total nodes (ids/xy of the whole ring). */
+ovs_status  ovs_chord_load_shard(ovs_ctx* ctx, const ovs_key160* ids_all_sorted, uint64_t n_total,
+                                 const double* xy_all, uint64_t lo, uint64_t hi, uint32_t flags);
+/* Initial records for lookups whose sources lie on this arc: qid = qid_base + i. */
+ovs_status  ovs_shard_make_records(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
+                                   uint64_t n, uint32_t qid_base, ovs_lookup_rec* recs, void* stream);
+/* One hop round: advance every record of `in` while its responder is on this
+ * arc.  Records whose next responder is remote are appended to `out` with the
+ * owner rank in out_dest; finished lookups are appended to `done`.
+ * *out_count and *done_count are device counters incremented by the kernel.
+ * shard_lo is a HOST array of nshards+1 arc boundaries (sorted-index space). */
+ovs_status  ovs_shard_step(ovs_ctx* ctx, const ovs_lookup_rec* in, uint64_t n_in,
+                           ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
+                           unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                           unsigned long long* done_count, const uint64_t* shard_lo,
+                           uint32_t nshards, void* stream);
 
 #ifdef __cplusplus
 }

@@ -33,20 +33,21 @@ __global__ void k_check_sorted(const KeyRec* __restrict__ recs, uint32_t n, uint
 }
 
 // row length = number of non-trivial fingers: i with 2^i > succ0 - self
-__global__ void k_chord_rowlen(const KeyRec* __restrict__ recs, uint32_t n, uint64_t* rowlen)
+__global__ void k_chord_rowlen(const KeyRec* __restrict__ recs, uint32_t n, uint32_t lo, uint32_t cnt, uint64_t* rowlen)
 {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint32_t v = lo + t;
     const K160 self = key_of(load_rec(recs, v));
     const K160 s0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
     const int ilo = k_msb(k_sub(s0, self)) + 1;
-    rowlen[v] = (uint64_t)(KEYBITS - ilo);
+    rowlen[t] = (uint64_t)(KEYBITS - ilo);
 }
 
-__global__ void k_set_aux(KeyRec* recs, const uint64_t* off, uint32_t n)
+__global__ void k_set_aux(KeyRec* recs, const uint64_t* off, uint32_t lo, uint32_t cnt)
 {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < n) recs[v].aux = (uint32_t)off[v];
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < cnt) recs[lo + t].aux = (uint32_t)off[t];
 }
 
 // first index with key >= target, wrapping to 0 (the responsible node)
@@ -62,10 +63,12 @@ __device__ __forceinline__ uint32_t ring_lower_bound(const KeyRec* __restrict__ 
 }
 
 // finger i of node v = responsible(v + 2^i) (rpcFixfingers answers thisNode, Chord.cc:1228-1270)
-__global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32_t* __restrict__ fingers)
+__global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32_t lo, uint32_t cnt,
+                             uint32_t* __restrict__ fingers)
 {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint32_t v = lo + t;
     const KeyRec r = load_rec(recs, v);
     const K160 self = key_of(r);
     const K160 s0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
@@ -328,6 +331,160 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
 }
 
 // ---------------------------------------------------------------------------
+// multi-GPU: one hop round over in-flight records (ovs_shard_step)
+
+// owner rank of node c: r with lo[r] <= c < lo[r+1] (uniform trip count, no divergent loop)
+__device__ __forceinline__ int shard_owner(const uint64_t* __restrict__ lo, int nsh, uint32_t c)
+{
+    int r = 0;
+    for (int i = 1; i < nsh; ++i) r += ((uint64_t)c >= lo[i]) ? 1 : 0;
+    return r;
+}
+
+__device__ __forceinline__ ovs_lookup_rec load_lrec(const ovs_lookup_rec* __restrict__ p, uint64_t i)
+{
+    const uint4* q = reinterpret_cast<const uint4*>(p + i);
+    const uint4 a = q[0], b = q[1], c = q[2];
+    ovs_lookup_rec r;
+    r.key[0] = a.x; r.key[1] = a.y; r.key[2] = a.z; r.key[3] = a.w; r.key[4] = b.x;
+    r.src = b.y; r.cur = b.z; r.qid = b.w;
+    r.t_ns = (int64_t)((uint64_t)c.x | ((uint64_t)c.y << 32));
+    r.hops = (uint16_t)(c.z & 0xFFFF);
+    r.local = (uint8_t)((c.z >> 16) & 0xFF);
+    return r;
+}
+
+__device__ __forceinline__ void store_lrec(ovs_lookup_rec* __restrict__ p, uint64_t i, const K160& K, uint32_t S,
+                                           uint32_t cur, uint32_t qid, int64_t t, int hops, int local)
+{
+    uint4* q = reinterpret_cast<uint4*>(p + i);
+    q[0] = make_uint4(K.w[0], K.w[1], K.w[2], K.w[3]);
+    q[1] = make_uint4(K.w[4], S, cur, qid);
+    q[2] = make_uint4((uint32_t)(uint64_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)hops | ((uint32_t)local << 16), 0u);
+}
+
+__global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayConsts DC, LookupConsts LC,
+                                                          const uint64_t* __restrict__ shard_lo, int nsh, int me, const ovs_lookup_rec* __restrict__ in, uint64_t nin,
+                                                          uint64_t chunk, ovs_lookup_rec* __restrict__ out,
+                                                          uint32_t* __restrict__ out_dest, uint64_t out_cap,
+                                                          unsigned long long* out_count, ovs_done_rec* __restrict__ done,
+                                                          uint64_t done_cap, unsigned long long* done_count)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    uint64_t cursor = wave * chunk;
+    const uint64_t end = min(cursor + chunk, nin);
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    bool active = false;
+    uint32_t S = 0, cur = 0, qid = 0;
+    K160 K;
+    KeyRec crec;
+    double sx = 0, sy = 0;
+    int64_t t = 0;
+    int hops = 0;
+    bool local = false;
+
+    while (true) {
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && cursor < end) {
+            const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
+            if (!active && mine < end) {
+                const ovs_lookup_rec r = load_lrec(in, mine);
+                active = true;
+                for (int w = 0; w < 5; ++w) K.w[w] = r.key[w];
+                S = r.src; cur = r.cur; qid = r.qid; t = r.t_ns; hops = r.hops; local = r.local != 0;
+                crec = load_rec(V.recs, cur);
+                const double2 sxy = V.xy[S];
+                sx = sxy.x; sy = sxy.y;
+            }
+            cursor += (uint64_t)__popcll(need);
+        }
+        if (!__any(active)) break;
+
+        bool emit_done = false, emit_out = false;
+        int dest = 0;
+        ovs_route_out o;
+        if (active) {
+            const double2 cxy = V.xy[cur];
+            const Decision d = decide_ideal(V, cur, crec, K);
+            uint8_t status = 0xFF;
+            uint32_t R = NONE;
+            if (local) {
+                local = false;
+                if (d.broken) status = OVS_LOOKUP_BROKEN;
+                else if (d.sib) { status = OVS_LOOKUP_OK; R = S; }
+            } else {
+                const int64_t cd = coord_ns(sx, sy, cxy.x, cxy.y, DC.round);
+                const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
+                if (rtt >= DC.rpcTimeout) {
+                    status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
+                } else {
+                    t += rtt;
+                    if (t > DC.lookupTimeout) status = OVS_LOOKUP_TIMEOUT;
+                    else {
+                        ++hops;
+                        if (d.broken) status = OVS_LOOKUP_BROKEN;
+                        else if (d.sib) { status = OVS_LOOKUP_OK; R = cur; }
+                    }
+                }
+            }
+            if (status == 0xFF) {
+                if (LC.hopCountMax && hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;
+                else if (d.next == S) status = OVS_LOOKUP_NO_NEXT;
+                else {
+                    cur = d.next;
+                    crec = d.rec;
+                    dest = shard_owner(shard_lo, nsh, cur);
+                    if (dest != me) { emit_out = true; active = false; }
+                }
+            }
+            if (status != 0xFF) {
+                o.hops = (uint16_t)hops;
+                o.status = status;
+                if (status == OVS_LOOKUP_OK) {
+                    o.responsible = R;
+                    o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
+                    o.latency_ns = t + (R != S ? DC.msgRoute + coord_ns(sx, sy, cxy.x, cxy.y, DC.round) : 0);
+                } else {
+                    o.responsible = NONE;
+                    o.one_way_hops = 0;
+                    o.latency_ns = -1;
+                }
+                emit_done = true;
+                active = false;
+            }
+        }
+        // append (hipcc turns these per-lane adds into one wave-level atomic per counter)
+        if (emit_done) {
+            const unsigned long long di = atomicAdd(done_count, 1ull);
+            if (di < done_cap) {
+                ovs_done_rec dr;
+                dr.qid = qid; dr.pad = 0; dr.out = o;
+                done[di] = dr;
+            }
+        }
+        if (emit_out) {
+            const unsigned long long oi = atomicAdd(out_count, 1ull);
+            if (oi < out_cap) {
+                store_lrec(out, oi, K, S, cur, qid, t, hops, 0);
+                out_dest[oi] = (uint32_t)dest;
+            }
+        }
+    }
+}
+
+__global__ void k_make_records(const KeyRec* __restrict__ recs, const K160* __restrict__ keys,
+                               const uint32_t* __restrict__ src, uint64_t n, uint32_t qid_base,
+                               ovs_lookup_rec* __restrict__ out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    (void)recs;
+    store_lrec(out, i, keys[i], src[i], src[i], qid_base + (uint32_t)i, 0, 0, 1);
+}
+
+// ---------------------------------------------------------------------------
 // findNode batch (general numRedundantNodes / numSiblings), Chord.cc:548-599
 
 __global__ void k_chord_find_node(ChordView V, int ideal, const uint32_t* __restrict__ node,
@@ -417,24 +574,25 @@ hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hi
     return hipGetLastError();
 }
 
-hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t** fingers_out, uint64_t* nfing_out,
-                              hipStream_t s)
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, uint32_t** fingers_out,
+                              uint64_t* nfing_out, hipStream_t s)
 {
     hipError_t e;
     uint64_t* rowlen = nullptr;
     uint64_t* off = nullptr;
     void* tmp = nullptr;
     size_t tmpb = 0;
+    const uint32_t cnt = hi - lo;
     *fingers_out = nullptr;
-    if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (n + 1))) != hipSuccess) return e;
-    if ((e = hipMalloc(&off, sizeof(uint64_t) * (n + 1))) != hipSuccess) { hipFree(rowlen); return e; }
-    hipLaunchKernelGGL(k_chord_rowlen, dim3(nblk(n, 256)), dim3(256), 0, s, recs, n, rowlen);
-    hipMemsetAsync(rowlen + n, 0, sizeof(uint64_t), s);
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, rowlen, off, n + 1, s);
+    if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (cnt + 1))) != hipSuccess) return e;
+    if ((e = hipMalloc(&off, sizeof(uint64_t) * (cnt + 1))) != hipSuccess) { hipFree(rowlen); return e; }
+    hipLaunchKernelGGL(k_chord_rowlen, dim3(nblk(cnt, 256)), dim3(256), 0, s, recs, n, lo, cnt, rowlen);
+    hipMemsetAsync(rowlen + cnt, 0, sizeof(uint64_t), s);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, rowlen, off, cnt + 1, s);
     if ((e = hipMalloc(&tmp, tmpb)) != hipSuccess) { hipFree(rowlen); hipFree(off); return e; }
-    hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, rowlen, off, n + 1, s);
+    hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, rowlen, off, cnt + 1, s);
     uint64_t total = 0;
-    hipMemcpyAsync(&total, off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&total, off + cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     if (total + KEYBITS >= 0xFFFFFFFFull) { hipFree(rowlen); hipFree(off); hipFree(tmp); return hipErrorInvalidValue; }
     uint32_t* fing = nullptr;
@@ -443,8 +601,8 @@ hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t** fingers_out, 
         hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
     }
     hipMemsetAsync(fing, 0, sizeof(uint32_t) * (total + KEYBITS), s);
-    hipLaunchKernelGGL(k_set_aux, dim3(nblk(n, 256)), dim3(256), 0, s, recs, off, n);
-    hipLaunchKernelGGL(k_chord_fill, dim3(nblk(n, 128)), dim3(128), 0, s, recs, n, fing);
+    hipLaunchKernelGGL(k_set_aux, dim3(nblk(cnt, 256)), dim3(256), 0, s, recs, off, lo, cnt);
+    hipLaunchKernelGGL(k_chord_fill, dim3(nblk(cnt, 128)), dim3(128), 0, s, recs, n, lo, cnt, fing);
     e = hipStreamSynchronize(s);
     hipFree(rowlen); hipFree(off); hipFree(tmp);
     if (e != hipSuccess) { hipFree(fing); return e; }
@@ -528,6 +686,41 @@ hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_delay, dim3(nblk(n, 256)), dim3(256), 0, s, xy, DC, a, b, bytes, n, out);
+    return hipGetLastError();
+}
+
+static int shard_blocks_per_cu()
+{
+    static int bpc = 0;
+    if (bpc == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_shard_step, 256, 0) != hipSuccess || b < 1) b = 1;
+        bpc = b;
+    }
+    return bpc;
+}
+
+hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
+                                   const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
+                                   ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
+                                   unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                                   unsigned long long* done_count, int num_cu, hipStream_t s)
+{
+    if (nin == 0) return hipSuccess;
+    const uint64_t waves = (uint64_t)num_cu * shard_blocks_per_cu() * 4;
+    uint64_t chunk = (nin + waves - 1) / waves;
+    if (chunk < 1) chunk = 1;
+    const uint64_t need_waves = (nin + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_chord_shard_step, dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, s, V, DC, LC, shard_lo, nsh, me, in,
+                       nin, chunk, out, out_dest, out_cap, out_count, done, done_cap, done_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
+                               ovs_lookup_rec* out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_make_records, dim3(nblk(n, 256)), dim3(256), 0, s, recs, keys, src, n, qid_base, out);
     return hipGetLastError();
 }
 

@@ -86,6 +86,12 @@ struct ChordView {
     int32_t numFingerCandidates;
 };
 
+constexpr int MAXSHARDS = 64;
+struct ShardMap {
+    uint64_t lo[MAXSHARDS + 1];   // arc r = [lo[r], lo[r+1]) of the sorted ring
+    int n;
+};
+
 struct LookupConsts {
     int32_t hopCountMax;
     int32_t numSiblings;

@@ -5,8 +5,15 @@
 namespace ovs {
 
 hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hipStream_t s);
-hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t** fingers_out, uint64_t* nfing_out,
-                              hipStream_t s);
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, uint32_t** fingers_out,
+                              uint64_t* nfing_out, hipStream_t s);
+hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
+                                   const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
+                                   ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
+                                   unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                                   unsigned long long* done_count, int num_cu, hipStream_t s);
+hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
+                               ovs_lookup_rec* out, hipStream_t s);
 hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s);
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,

@@ -37,6 +37,8 @@ struct ovs_ctx {
     uint8_t* nsucc = nullptr;
     uint32_t* fres = nullptr;
     int sls = 0;
+    uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
+    uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     // kademlia
     KadTables kad{};
     // scratch for host-pointer calls
@@ -260,6 +262,7 @@ void ovs_ctx_destroy(ovs_ctx* c)
     if (c->stream) hipStreamSynchronize(c->stream);
     free_tables(c);
     free_scratch(c);
+    if (c->d_bounds) hipFree(c->d_bounds);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -294,11 +297,73 @@ ovs_status ovs_chord_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const d
     if (c->P.overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "params.overlay is not Chord");
     ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
     if (s != OVS_OK) { free_tables(c); return s; }
-    hipError_t e = launch_chord_build(c->recs, (uint32_t)n, &c->fingers, &c->nfing, c->stream);
+    hipError_t e = launch_chord_build(c->recs, (uint32_t)n, 0, (uint32_t)n, &c->fingers, &c->nfing, c->stream);
     if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "chord finger build"); }
     c->overlay = OVS_OVERLAY_CHORD;
     c->ideal = true;
     c->sls = c->P.successorListSize;
+    c->shard_lo = 0; c->shard_hi = n;
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_load_shard(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint64_t lo,
+                                uint64_t hi, uint32_t flags)
+{
+    if (!c || !ids || !xy || lo >= hi || hi > n) return OVS_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    if (c->P.overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "params.overlay is not Chord");
+    ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    hipError_t e = launch_chord_build(c->recs, (uint32_t)n, (uint32_t)lo, (uint32_t)hi, &c->fingers, &c->nfing, c->stream);
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "chord finger build"); }
+    c->overlay = OVS_OVERLAY_CHORD;
+    c->ideal = true;
+    c->sls = c->P.successorListSize;
+    c->shard_lo = lo; c->shard_hi = hi;
+    return OVS_OK;
+}
+
+ovs_status ovs_shard_make_records(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                                  uint32_t qid_base, ovs_lookup_rec* recs, void* stream)
+{
+    if (!c || (n && (!keys || !src || !recs))) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD || !c->ideal) return fail(c, OVS_ESTATE, "no Chord ring (shard) loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;   // device-pointer call: NULL = the default stream
+    HIPCHK(c, launch_make_records(c->recs, reinterpret_cast<const K160*>(keys), src, n, qid_base, recs, s));
+    return OVS_OK;
+}
+
+ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out,
+                          uint32_t* out_dest, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,
+                          uint64_t done_cap, unsigned long long* done_count, const uint64_t* shard_lo,
+                          uint32_t nshards, void* stream)
+{
+    if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
+    if (n_in && (!in || !out || !out_dest || !out_count || !done || !done_count)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD || !c->ideal) return fail(c, OVS_ESTATE, "no Chord ring (shard) loaded");
+    ovs_status st = check_common(c, c->P);
+    if (st == OVS_OK) st = check_chord_route(c, c->P);
+    if (st != OVS_OK) return st;
+    ShardMap M{};
+    M.n = (int)nshards;
+    int me = -1;
+    for (uint32_t r = 0; r <= nshards; ++r) {
+        M.lo[r] = shard_lo[r];
+        if (r > 0 && shard_lo[r] < shard_lo[r - 1]) return fail(c, OVS_EINVAL, "shard_lo must be non-decreasing");
+    }
+    if (shard_lo[0] != 0 || shard_lo[nshards] != c->n) return fail(c, OVS_EINVAL, "shard_lo must cover [0, n)");
+    for (uint32_t r = 0; r < nshards; ++r)
+        if (shard_lo[r] == c->shard_lo && shard_lo[r + 1] == c->shard_hi) me = (int)r;
+    if (me < 0) return fail(c, OVS_EINVAL, "this context's arc is not one of shard_lo's arcs");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;   // device-pointer call: NULL = the default stream
+    if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
+    HIPCHK(c, hipMemcpyAsync(c->d_bounds, M.lo, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice, s));
+    LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes};
+    HIPCHK(c, launch_chord_shard_step(chord_view(c), delay_consts(c->P), LC, c->d_bounds, (int)nshards, me, in, n_in, out,
+                                      out_dest, out_cap, out_count, done, done_cap, done_count, c->num_cu, s));
     return OVS_OK;
 }
 
@@ -355,6 +420,7 @@ ovs_status ovs_chord_export_fingers(ovs_ctx* c, uint32_t* out)
 {
     if (!c || !out) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "no Chord network loaded");
+    if (c->ideal && (c->shard_lo != 0 || c->shard_hi != c->n)) return fail(c, OVS_ESTATE, "sharded ring");
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t tot = c->n * 160;
     if (!c->ideal) {
@@ -406,11 +472,13 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     if (st != OVS_OK) return st;
     HIPCHK(c, hipSetDevice(c->device));
     const bool dev = flags & OVS_DEVICE_PTRS;
-    hipStream_t s = (dev && stream) ? (hipStream_t)stream : c->stream;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;   // NULL = the default stream
     const int H = c->P.hopCountMax > 0 ? c->P.hopCountMax : 1;
     if (c->overlay == OVS_OVERLAY_CHORD) {
         st = check_chord_route(c, c->P);
         if (st != OVS_OK) return st;
+        if (c->ideal && (c->shard_lo != 0 || c->shard_hi != c->n))
+            return fail(c, OVS_ESTATE, "context holds one arc of a sharded ring: use ovs_shard_step");
     }
     if (n == 0) return OVS_OK;
     // stage inputs
@@ -480,7 +548,7 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
     if (numRedundantNodes < 1 || numRedundantNodes > 64) return fail(c, OVS_EINVAL, "numRedundantNodes out of range");
     HIPCHK(c, hipSetDevice(c->device));
     const bool dev = flags & OVS_DEVICE_PTRS;
-    hipStream_t s = (dev && stream) ? (hipStream_t)stream : c->stream;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;   // NULL = the default stream
     if (n == 0) return OVS_OK;
     uint32_t* dn = nullptr; K160* dk = nullptr; uint32_t* dout = nullptr; uint8_t* dc = nullptr; uint8_t* dsb = nullptr;
     bool o1, o2;
@@ -523,7 +591,7 @@ ovs_status ovs_delay_batch(ovs_ctx* c, const uint32_t* a, const uint32_t* b, con
     if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
     HIPCHK(c, hipSetDevice(c->device));
     const bool dev = flags & OVS_DEVICE_PTRS;
-    hipStream_t s = (dev && stream) ? (hipStream_t)stream : c->stream;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;   // NULL = the default stream
     if (n == 0) return OVS_OK;
     if (!dev) {
         for (uint64_t i = 0; i < n; ++i)

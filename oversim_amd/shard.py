@@ -1,0 +1,244 @@
+"""Multi-GPU Chord: the sorted ring cut into contiguous arcs, one per rank, with
+lookups handed between ranks every hop round by an all-to-allv.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm, the
+exchange runs over xGMI).  Node keys and coordinates are replicated on every
+rank (24 + 16 B per node), finger rows exist only for the rank's own arc, so a
+lookup is forwarded to the rank that owns its next responder -- the message a
+FindNodeCall would be in OverSim (BaseOverlay.cc:1841-1915).  Per round:
+
+  1. ovs_shard_step advances every inbound record while its responder is
+     local; remote hand-offs go to an outbox tagged with the owner rank,
+     finished lookups to the rank's done buffer;
+  2. the outbox is grouped by destination (stable sort on the tag);
+  3. counts all-to-all, then records all-to-allv (48 B per lookup);
+  4. a 1-element all-reduce decides termination.
+
+The orchestration is independent of the stepper (the HIP kernel here, a CPU
+test double in tests/) and of the exchange (torch.distributed, or an in-process
+emulation of W shards on one device).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .kbr import DEVICE_PTRS, KbrEngine, Params, lib
+
+REC_DTYPE = np.dtype([("key", "<u4", 5), ("src", "<u4"), ("cur", "<u4"), ("qid", "<u4"), ("t_ns", "<i8"),
+                      ("hops", "<u2"), ("local", "u1"), ("pad", "u1", 5)])
+DONE_DTYPE = np.dtype([("qid", "<u4"), ("pad", "<u4"), ("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                       ("one_way_hops", "u1"), ("latency_ns", "<i8")])
+assert REC_DTYPE.itemsize == 48 and DONE_DTYPE.itemsize == 24
+REC_BYTES, DONE_BYTES = 48, 24
+
+
+def arc_bounds(n_total: int, world: int) -> list[int]:
+    """Contiguous arcs of the sorted ID array, as equal as possible."""
+    return [r * n_total // world for r in range(world + 1)]
+
+
+# ---------------------------------------------------------------------------
+# steppers
+
+class GpuShardStepper:
+    """One rank's arc on one device: owns the engine context and the device buffers."""
+
+    def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device, stream=None,
+                 capacity: int = 1 << 20, params: Params | None = None):
+        import torch
+        self.torch = torch
+        self.dev = device
+        self.stream = stream
+        self.rank, self.bounds, self.world = rank, [int(b) for b in bounds], len(bounds) - 1
+        self.eng = KbrEngine(device.index if device.index is not None else 0)
+        self.eng.set_params(params or Params.chord())
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        xy = np.ascontiguousarray(xy, dtype=np.float64)
+        st = lib().ovs_chord_load_shard(self.eng._h, ids.ctypes.data_as(C.c_void_p), len(ids),
+                                        xy.ctypes.data_as(C.c_void_p), self.bounds[rank], self.bounds[rank + 1], 0)
+        self.eng._chk(st, "ovs_chord_load_shard")
+        self.n_total = len(ids)
+        self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
+        self.cap = 0
+        self._ensure(capacity)
+        self.done_count = torch.zeros(1, dtype=torch.int64, device=device)
+        self.done = torch.empty((max(capacity, 1), DONE_BYTES), dtype=torch.uint8, device=device)
+        self.done_cap = max(capacity, 1)
+
+    def _ensure(self, cap: int):
+        torch = self.torch
+        if cap <= self.cap:
+            return
+        self.cap = cap
+        self.out = torch.empty((cap, REC_BYTES), dtype=torch.uint8, device=self.dev)
+        self.out_dest = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.out_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+
+    def _s(self):
+        # every kernel of the round runs on torch's current stream, so the torch ops around it
+        # (counter resets, grouping, the collectives) are ordered with it
+        return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def reset(self, capacity: int):
+        self.done_count.zero_()
+        if capacity > self.done_cap:
+            self.done = self.torch.empty((capacity, DONE_BYTES), dtype=self.torch.uint8, device=self.dev)
+            self.done_cap = capacity
+
+    def make_records(self, keys_t, src_t, qid_base: int):
+        n = keys_t.shape[0]
+        recs = self.torch.empty((n, REC_BYTES), dtype=self.torch.uint8, device=self.dev)
+        st = lib().ovs_shard_make_records(self.eng._h, C.c_void_p(keys_t.data_ptr()), C.c_void_p(src_t.data_ptr()),
+                                          n, qid_base, C.c_void_p(recs.data_ptr()), self._s())
+        self.eng._chk(st, "ovs_shard_make_records")
+        return recs
+
+    def step(self, inbox):
+        n_in = inbox.shape[0]
+        self._ensure(n_in)
+        self.out_count.zero_()
+        st = lib().ovs_shard_step(self.eng._h, C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(self.out.data_ptr()),
+                                  C.c_void_p(self.out_dest.data_ptr()), self.cap, C.c_void_p(self.out_count.data_ptr()),
+                                  C.c_void_p(self.done.data_ptr()), self.done_cap,
+                                  C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
+        self.eng._chk(st, "ovs_shard_step")
+        m = int(self.out_count.item())
+        return self.out[:m], self.out_dest[:m]
+
+    def finished(self):
+        k = int(self.done_count.item())
+        if k > self.done_cap:
+            raise RuntimeError("done buffer overflow")
+        return self.done[:k]
+
+
+for _name, _args in {
+    "ovs_chord_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
+    "ovs_shard_make_records": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p],
+    "ovs_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                       C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
+}.items():
+    _f = getattr(lib(), _name)
+    _f.argtypes = _args
+    _f.restype = C.c_int
+
+
+# ---------------------------------------------------------------------------
+# exchanges
+
+class TorchExchange:
+    """all-to-allv of lookup records over torch.distributed (RCCL on GPUs, gloo on CPU)."""
+
+    def __init__(self, world: int, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.world, self.group = torch, dist, world, group
+        self.comm_dev = device   # tensors handed to the collective live here
+
+    def exchange(self, send, send_counts):
+        torch, dist = self.torch, self.dist
+        sc = send_counts.to(self.comm_dev, dtype=torch.int64)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        total = sc.sum().reshape(1)
+        dist.all_reduce(total, group=self.group)
+        if int(total.item()) == 0:
+            return None
+        rcl, scl = rc.tolist(), sc.tolist()
+        recv = torch.empty((sum(rcl), REC_BYTES), dtype=torch.uint8, device=self.comm_dev)
+        dist.all_to_all_single(recv, send.to(self.comm_dev), rcl, scl, group=self.group)
+        return recv
+
+
+def group_by_dest(out, dest, world: int):
+    """Stable grouping of the outbox by destination rank (counting sort)."""
+    import torch
+    if out.shape[0] == 0:
+        return out, torch.zeros(world, dtype=torch.int64, device=out.device)
+    d = dest.to(torch.int64)
+    order = torch.argsort(d, stable=True)
+    counts = torch.bincount(d, minlength=world)
+    return out.index_select(0, order), counts
+
+
+def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 10_000):
+    """Route one batch of lookups originating on this rank; returns (done records, rounds)."""
+    inbox = stepper.make_records(keys_t, src_t, qid_base)
+    rounds = 0
+    while True:
+        rounds += 1
+        out, dest = stepper.step(inbox)
+        send, counts = group_by_dest(out, dest, exchange.world)
+        recv = exchange.exchange(send, counts)
+        if recv is None:
+            break
+        inbox = recv if recv.device == out.device else recv.to(out.device)
+        if rounds > max_rounds:
+            raise RuntimeError("sharded routing did not terminate")
+    return stepper.finished(), rounds
+
+
+def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_rounds: int = 10_000):
+    """Single-process emulation of W ranks (e.g. W contexts on one GPU): the exchange is a concatenation."""
+    import torch
+    W = len(steppers)
+    inbox = [steppers[r].make_records(keys_per_shard[r], src_per_shard[r], qid_bases[r]) for r in range(W)]
+    rounds = 0
+    while True:
+        rounds += 1
+        buckets = [[] for _ in range(W)]
+        moved = 0
+        for r in range(W):
+            out, dest = steppers[r].step(inbox[r])
+            send, counts = group_by_dest(out, dest, W)
+            off = 0
+            for d, c in enumerate(counts.tolist()):
+                if c:
+                    buckets[d].append(send[off:off + c].clone())
+                    moved += c
+                off += c
+        if moved == 0:
+            break
+        dev = steppers[0].dev
+        inbox = [torch.cat(b) if b else torch.empty((0, REC_BYTES), dtype=torch.uint8, device=dev) for b in buckets]
+        if rounds > max_rounds:
+            raise RuntimeError("sharded routing did not terminate")
+    return [s.finished() for s in steppers], rounds
+
+
+def done_to_numpy(done_t) -> np.ndarray:
+    return done_t.cpu().numpy().view(DONE_DTYPE).ravel()
+
+
+class ShardedChord:
+    """bench.py driver for one rank: ring arc + lookups resident in HBM + RCCL exchange."""
+
+    def __init__(self, rank, world, ids, xy, keys, src, device, stream):
+        import torch
+        self.bounds = arc_bounds(len(ids), world)
+        lo, hi = self.bounds[rank], self.bounds[rank + 1]
+        assert np.all((src >= lo) & (src < hi)), "lookups must originate on this rank's arc"
+        n = len(keys)
+        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, stream=stream,
+                                       capacity=max(2 * n, 1024))
+        self.stepper.reset(world * n + 1024)
+        self.exchange = TorchExchange(world, device)
+        self.keys_t = torch.from_numpy(np.ascontiguousarray(keys)).to(device)
+        self.src_t = torch.from_numpy(np.ascontiguousarray(src)).to(device)
+        self.qid_base = rank * n
+        self._done = None
+        self.rounds = 0
+
+    def run(self):
+        self.stepper.reset(self.stepper.done_cap)
+        self._done, self.rounds = route_sharded(self.stepper, self.exchange, self.keys_t, self.src_t, self.qid_base)
+
+    def hop_total(self) -> int:
+        d = done_to_numpy(self._done)
+        return int(d["hops"].astype(np.int64).sum())
+
+    def ok_total(self) -> int:
+        d = done_to_numpy(self._done)
+        return int((d["status"] == 0).sum())

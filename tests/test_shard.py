@@ -1,0 +1,226 @@
+"""Multi-GPU (sharded ring) path.
+
+CPU (world_size 2, gloo): route_sharded + TorchExchange + grouping/termination,
+driven by a pure-Python stepper that restates the per-hop semantics (refmodel).
+GPU: the ovs_shard_step kernel with W arcs emulated in one process, and two
+processes sharing cuda:0 with a gloo exchange; both compared with the
+single-GPU engine and the oracle.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import refmodel
+from oversim_amd import workload as W
+
+ROUTE_FIELDS = ("responsible", "hops", "status", "one_way_hops", "latency_ns")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class CpuShardStepper:
+    """Test double of GpuShardStepper: same record format, per-hop logic from refmodel."""
+
+    def __init__(self, ids, xy, bounds, rank):
+        from oversim_amd.shard import DONE_DTYPE, REC_DTYPE
+        self.REC, self.DONE = REC_DTYPE, DONE_DTYPE
+        self.ring = refmodel.ChordRing(ids, xy)
+        self.lo, self.hi = bounds[rank], bounds[rank + 1]
+        self.bounds = bounds
+        self.done = []
+        self.dev = torch.device("cpu")
+
+    def make_records(self, keys_t, src_t, qid_base):
+        keys, src = keys_t.numpy(), src_t.numpy()
+        r = np.zeros(len(keys), dtype=self.REC)
+        r["key"], r["src"], r["cur"] = keys, src, src
+        r["qid"] = qid_base + np.arange(len(keys))
+        r["local"] = 1
+        return torch.from_numpy(r.view(np.uint8).reshape(-1, 48).copy())
+
+    def owner(self, c):
+        return int(np.searchsorted(self.bounds, c, side="right") - 1)
+
+    def step(self, inbox):
+        recs = inbox.numpy().view(self.REC).ravel()
+        out, dest = [], []
+        ring = self.ring
+        call, resp, route = refmodel.msg_ns(83), refmodel.msg_ns(87), refmodel.msg_ns(186)
+        for rec in recs:
+            K = refmodel.to_int(rec["key"])
+            S, cur, t, hops, local = int(rec["src"]), int(rec["cur"]), int(rec["t_ns"]), int(rec["hops"]), bool(rec["local"])
+            while True:
+                assert self.lo <= cur < self.hi
+                sib, nxt = ring.decide(cur, K)
+                status, R = None, None
+                if local:
+                    local = False
+                    if sib:
+                        status, R = 0, S
+                else:
+                    cd = refmodel.coord_ns(ring.xy, S, cur)
+                    t += call + resp + 2 * cd
+                    hops += 1
+                    if sib:
+                        status, R = 0, cur
+                if status is None:
+                    if hops >= 50:
+                        status = 3
+                    elif nxt == S:
+                        status = 4
+                if status is not None:
+                    lat = t + (route + refmodel.coord_ns(ring.xy, S, R) if (status == 0 and R != S) else 0)
+                    self.done.append((int(rec["qid"]), R if status == 0 else 0xFFFFFFFF, hops, status,
+                                      hops + (R != S) if status == 0 else 0, lat if status == 0 else -1))
+                    break
+                cur = nxt
+                if not (self.lo <= cur < self.hi):
+                    o = rec.copy()
+                    o["cur"], o["t_ns"], o["hops"], o["local"] = cur, t, hops, 0
+                    out.append(o)
+                    dest.append(self.owner(cur))
+                    break
+        o = np.array(out, dtype=self.REC) if out else np.zeros(0, dtype=self.REC)
+        return (torch.from_numpy(o.view(np.uint8).reshape(-1, 48).copy()),
+                torch.tensor(dest, dtype=torch.int32))
+
+    def finished(self):
+        d = np.zeros(len(self.done), dtype=self.DONE)
+        for i, (q, R, h, st, ow, lat) in enumerate(self.done):
+            d[i]["qid"], d[i]["responsible"], d[i]["hops"], d[i]["status"] = q, R, h, st
+            d[i]["one_way_hops"], d[i]["latency_ns"] = ow, lat
+        return torch.from_numpy(d.view(np.uint8).reshape(-1, 24).copy())
+
+
+def _cpu_worker(rank, world, port, n, m, q):
+    import torch.distributed as dist
+    from oversim_amd.shard import TorchExchange, arc_bounds, done_to_numpy, route_sharded
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    net = W.population(n, 91)
+    bounds = arc_bounds(n, world)
+    keys, src = W.lookups(net.ids, m, 92 + rank, node_ids=rank == 0)
+    src = (bounds[rank] + src.astype(np.int64) % (bounds[rank + 1] - bounds[rank])).astype(np.uint32)
+    st = CpuShardStepper(net.ids, net.xy, bounds, rank)
+    done, rounds = route_sharded(st, TorchExchange(world, torch.device("cpu")), torch.from_numpy(keys),
+                                 torch.from_numpy(src), rank * m)
+    q.put((rank, done_to_numpy(done), keys, src, rounds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_orchestration_gloo_cpu():
+    import torch.multiprocessing as mp
+    world, n, m = 2, 600, 300
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, n, m, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    net = W.population(n, 91)
+    ring = refmodel.ChordRing(net.ids, net.xy)
+    all_done = np.concatenate([r[1] for r in res])
+    assert len(all_done) == world * m and len(np.unique(all_done["qid"])) == world * m
+    by_q = {int(d["qid"]): d for d in all_done}
+    for rank, _, keys, src, rounds in res:
+        assert rounds >= 2
+        for i in range(m):
+            ref = ring.lookup(keys[i], int(src[i]))
+            d = by_q[rank * m + i]
+            for f in ROUTE_FIELDS:
+                assert int(d[f]) == int(ref[f]), (rank, i, f)
+
+
+# ---------------------------------------------------------------------------- GPU
+
+def _single_gpu_reference(net, keys, src):
+    from oversim_amd import KbrEngine, Params
+    with KbrEngine(0) as e:
+        e.set_params(Params.chord())
+        e.chord_load(net.ids, net.xy)
+        return e.lookup(keys, src)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shard_step_emulated_on_one_gpu(world):
+    from oversim_amd.shard import GpuShardStepper, arc_bounds, done_to_numpy, route_local_shards
+    n, m = 1 << 16, 6000
+    net = W.population(n, 93)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m) for r in range(world)]
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s = W.lookups(net.ids, m, 94 + r, node_ids=(r % 2 == 0))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k).to(dev)); ss.append(torch.from_numpy(s).to(dev)); qb.append(r * m)
+        allk.append(k); alls.append(s)
+    for st in steppers:
+        st.reset(world * m)
+    dones, rounds = route_local_shards(steppers, ks, ss, qb)
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    ref = _single_gpu_reference(net, np.concatenate(allk), np.concatenate(alls))
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    assert rounds >= 2
+
+
+def _gpu_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oversim_amd.shard import GpuShardStepper, TorchExchange, arc_bounds, done_to_numpy, route_sharded
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, m = 1 << 15, 4000
+    net = W.population(n, 95)
+    bounds = arc_bounds(n, world)
+    k, s = W.lookups(net.ids, m, 96 + rank, node_ids=False)
+    s = (bounds[rank] + s.astype(np.int64) % (bounds[rank + 1] - bounds[rank])).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    st = GpuShardStepper(net.ids, net.xy, bounds, rank, dev, capacity=world * m)
+    st.reset(world * m)
+    done, rounds = route_sharded(st, TorchExchange(world, torch.device("cpu")), torch.from_numpy(k).to(dev),
+                                 torch.from_numpy(s).to(dev), rank * m)
+    q.put((rank, done_to_numpy(done), k, s))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_processes_share_one_gpu_gloo():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    d = np.concatenate([r[1] for r in res])
+    d = d[np.argsort(d["qid"])]
+    net = W.population(1 << 15, 95)
+    ref = _single_gpu_reference(net, np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res]))
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
