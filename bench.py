@@ -1,16 +1,22 @@
 #!/usr/bin/env python3
-"""Benchmark: routed lookup hops/s of the MI355X Chord iterative-lookup engine.
+"""Benchmark: routed lookup hops/s of the MI355X KBR lookup engine (BASELINE.json).
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`, one process
 per GPU (torch.distributed.run for N > 1).  A *step* is one pass of the hot
-path over one batch of synthetic lookups resident in HBM: config C of
-BASELINE.json -- Chord ring of 2^20 nodes (random coordinates, fieldSize 150),
-10M uniform random-key one-way KBR lookups, iterative routing, successor list
-8, hopCountMax 50.  Prints ONE JSON line on rank 0.
+path over one batch of synthetic lookups already resident in HBM.  rank 0
+prints ONE JSON line.
 
-Multi-GPU: each rank owns one 2^20-node arc of an N x 2^20 ring and originates
-10M lookups (weak scaling); lookups whose next responder lies on another arc
-are exchanged every hop round with an RCCL all-to-allv.
+Workloads (--workload, default C):
+  C  Chord, 2^20 ring nodes per GPU (random coordinates, fieldSize 150), 10M
+     uniform random-key one-way lookups per GPU.  N > 1: the N x 2^20 ring is
+     sharded over the GPUs and in-flight lookups are exchanged every hop round
+     with an RCCL all-to-allv (oversim_amd/shard.py).  Weak scaling.
+  D  Chord, 2^26-node ring (config D), 8M random-key lookups per GPU, ring
+     sharded over the N GPUs (RCCL all-to-allv).  Weak scaling in lookups.
+  B  Kademlia, 15 000 nodes (nodes_2d_15000.xml coordinates), k=8, alpha=1,
+     1M node-ID lookups per GPU.  N > 1: independent replicas.
+  E  Kademlia, 2^24 nodes, alpha=3, 4M random-key lookups per GPU.  N > 1:
+     replicas (the XOR-prefix sharded exchange is future work).
 """
 from __future__ import annotations
 
@@ -28,6 +34,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 B_HOP = 512                    # algorithmic bytes per Chord hop
+B_RPC = 448                    # algorithmic bytes per evaluated Kademlia RPC
 
 
 def parse():
@@ -35,24 +42,37 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--nodes", type=int, default=1 << 20, help="ring nodes per GPU")
-    ap.add_argument("--lookups", type=int, default=10_000_000, help="lookups per GPU per step")
+    ap.add_argument("--workload", choices=["B", "C", "D", "E"], default="C")
+    ap.add_argument("--nodes", type=int, default=None, help="override ring size (per GPU for C, total for D/E)")
+    ap.add_argument("--lookups", type=int, default=None, help="override lookups per GPU per step")
     ap.add_argument("--seed", type=int, default=0xC)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv for `traffic`")
+    ap.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv file(s), comma separated")
     return ap.parse_args()
 
 
-def cpu_baseline(ids, xy, keys, src, target_s: float) -> dict:
+WL = {
+    "C": dict(overlay="chord", nodes=1 << 20, per_gpu_nodes=True, lookups=10_000_000, node_ids=False,
+              desc="C: Chord 2^20 nodes per GPU (ring sharded over GPUs), 10M random-key iterative one-way lookups per GPU"),
+    "D": dict(overlay="chord", nodes=1 << 26, per_gpu_nodes=False, lookups=8_000_000, node_ids=False,
+              desc="D: Chord 2^26-node ring sharded over the GPUs, 8M random-key iterative one-way lookups per GPU"),
+    "B": dict(overlay="kademlia", nodes=15000, per_gpu_nodes=False, lookups=1_000_000, node_ids=True, alpha=1,
+              desc="B: Kademlia 15000 nodes (nodes_2d_15000.xml), k=8, alpha=1, 1M node-ID lookups per GPU"),
+    "E": dict(overlay="kademlia", nodes=1 << 24, per_gpu_nodes=False, lookups=4_000_000, node_ids=False, alpha=3,
+              desc="E: Kademlia 2^24 nodes, k=8, alpha=3, 4M random-key lookups per GPU (replicas for N>1)"),
+}
+
+
+def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1) -> dict:
     """The oracle (CPU restatement, kind 'port') on a bounded sample of the same workload."""
     sys.path.insert(0, str(ROOT / "tests"))
-    from oracle_lib import OracleNet
+    from oracle_lib import OracleNet, kad_params
     nthreads = min(os.cpu_count() or 1, 16)
-    o = OracleNet("chord", ids, xy)
+    o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia" else None)
     m = 20000
     t = time.perf_counter()
-    r = o.route(keys[:m], src[:m], record_hops=False, nthreads=nthreads)
+    o.route(keys[:m], src[:m], record_hops=False, nthreads=nthreads)
     dt = time.perf_counter() - t
     m2 = int(min(len(keys), max(m, m * target_s / max(dt, 1e-6))))
     t = time.perf_counter()
@@ -61,27 +81,30 @@ def cpu_baseline(ids, xy, keys, src, target_s: float) -> dict:
     hops = int(r["hops"].astype(np.int64).sum())
     return {"value": hops / dt, "unit": "hops/s", "cores": nthreads, "kind": "port",
             "sample": f"oracle/ovs_oracle.c restatement, {m2} of the step's lookups on the same "
-                      f"{len(ids)}-node ring, OpenMP {nthreads} threads, {dt:.1f} s",
+                      f"{len(ids)}-node {kind} network, OpenMP {nthreads} threads, {dt:.1f} s",
             "lookups_per_s": m2 / dt}
 
 
-def traffic_from_csv(path: str | None, kernel_substr: str = "k_chord_route"):
-    if not path or not Path(path).exists():
+def traffic_from_csv(path: str | None, kernel_substr: str):
+    """HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs (KB units;
+    gfx950 FETCH_SIZE tallies 128-B requests as 64 B -> x2 on the read side, MI355X_MICROARCH.md §HBM)."""
+    if not path:
         return None
     import csv
     tot, n = {}, {}
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            c = row.get("Counter_Name")
-            tot[c] = tot.get(c, 0.0) + float(row.get("Counter_Value", 0))
-            n[c] = n.get(c, 0) + 1
-    if not tot:
+    for p in path.split(","):
+        if not Path(p).exists():
+            continue
+        with open(p) as f:
+            for row in csv.DictReader(f):
+                if kernel_substr not in row.get("Kernel_Name", ""):
+                    continue
+                c = row.get("Counter_Name")
+                tot[c] = tot.get(c, 0.0) + float(row.get("Counter_Value", 0))
+                n[c] = n.get(c, 0) + 1
+    if "FETCH_SIZE" not in tot:
         return None
-    # FETCH_SIZE / WRITE_SIZE are in KB (x1024); gfx950 FETCH_SIZE counts 128-B requests
-    # as 64 B (MI355X_MICROARCH.md §HBM) -> x2 on the read side
-    fetch = 2 * 1024 * tot.get("FETCH_SIZE", 0.0) / max(n.get("FETCH_SIZE", 1), 1)
+    fetch = 2 * 1024 * tot["FETCH_SIZE"] / n["FETCH_SIZE"]
     write = 1024 * tot.get("WRITE_SIZE", 0.0) / max(n.get("WRITE_SIZE", 1), 1)
     return fetch + write
 
@@ -94,42 +117,82 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    backend = os.environ.get("OVS_BENCH_BACKEND", "nccl")      # gloo: rehearse N ranks on one GPU
+    ndev = torch.cuda.device_count()
+    dev_index = local % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from oversim_amd import KbrEngine, Params, workload as W
 
-    nodes_total = a.nodes * world
-    ids = W.sorted_unique_ids(nodes_total, a.seed)
-    xy = W.coordinates(nodes_total, a.seed, use_file=False)
-    keys, src = W.lookups(ids, a.lookups, a.seed + 1000 + rank, node_ids=False)
-    if world > 1:
-        # lookups originate on this rank's arc
-        lo, hi = rank * nodes_total // world, (rank + 1) * nodes_total // world
-        src = (lo + (src.astype(np.int64) % (hi - lo))).astype(np.uint32)
-
-    dev = torch.device("cuda", local)
+    wl = dict(WL[a.workload])
+    nodes = a.nodes or wl["nodes"]
+    n_total = nodes * world if wl["per_gpu_nodes"] else nodes
+    m = a.lookups or wl["lookups"]
+    kind = wl["overlay"]
     stream = torch.cuda.Stream(device=dev)
-    if world == 1:
-        eng = KbrEngine(local)
-        eng.set_params(Params.chord())
-        eng.chord_load(ids, xy)
-        dkeys = torch.from_numpy(keys).to(dev)
-        dsrc = torch.from_numpy(src).to(dev)
-        dout = torch.empty((a.lookups, 16), dtype=torch.uint8, device=dev)
+    sharded = kind == "chord" and world > 1
+    small = n_total <= (1 << 22)
 
-        def step():
-            eng.lookup_device(dkeys.data_ptr(), dsrc.data_ptr(), a.lookups, dout.data_ptr(), stream.cuda_stream)
+    # ---- population (identical on every rank) and this rank's lookups, resident in HBM
+    if small:
+        ids = W.sorted_unique_ids(n_total, a.seed)
+        xy = W.coordinates(n_total, a.seed, use_file=(kind == "kademlia" and n_total <= 15000))
+        ids_t = torch.from_numpy(ids.view(np.int32)).to(dev)
+        xy_t = torch.from_numpy(xy).to(dev)
     else:
+        ids_t, xy_t = W.device_population(n_total, a.seed, dev)
+        ids = xy = None
+    if sharded:
+        from oversim_amd.shard import arc_bounds
+        b = arc_bounds(n_total, world)
+        lo, hi = b[rank], b[rank + 1]
+    else:
+        lo, hi = 0, n_total
+    if small:
+        keys, src = W.lookups(ids, m, a.seed + 1000 + rank, node_ids=wl["node_ids"])
+        src = (lo + (src.astype(np.int64) % (hi - lo))).astype(np.uint32)
+        dkeys = torch.from_numpy(keys.view(np.int32)).to(dev)
+        dsrc = torch.from_numpy(src.view(np.int32)).to(dev)
+    else:
+        dkeys, dsrc = W.device_lookups(n_total, m, a.seed + 1000 + rank, dev, lo, hi)
+        keys = src = None
+
+    # ---- engine
+    if sharded:
         from oversim_amd.shard import ShardedChord
-        sh = ShardedChord(rank, world, ids, xy, keys, src, dev, stream)
+        ids_np = ids if ids is not None else ids_t.cpu().numpy().view(np.uint32)
+        xy_np = xy if xy is not None else xy_t.cpu().numpy()
+        comm = dev if backend == "nccl" else torch.device("cpu")
+        sh = ShardedChord(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm)
+        kname = "k_chord_shard_step"
 
         def step():
             sh.run()
+    else:
+        eng = KbrEngine(dev_index)
+        if kind == "chord":
+            eng.set_params(Params.chord())
+            eng.chord_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
+            kname = "k_chord_route"
+        else:
+            eng.set_params(Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
+            eng.kad_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
+            kname = "k_kad_route"
+        dout = torch.empty((m, 16), dtype=torch.uint8, device=dev)
+        drpc = torch.empty(m, dtype=torch.int32, device=dev) if kind == "kademlia" else None
+
+        def step():
+            eng.lookup_device(dkeys.data_ptr(), dsrc.data_ptr(), m, dout.data_ptr(), stream.cuda_stream,
+                              rpcs_ptr=drpc.data_ptr() if drpc is not None else None)
 
     torch.cuda.synchronize()
-    torch.cuda.set_stream(stream)        # every launch of the step is ordered on `stream`
+    torch.cuda.set_stream(stream)        # every launch of a step is ordered on `stream`
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -148,35 +211,54 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / max(a.steps, 1)
+    step_ms = ev0.elapsed_time(ev1) / max(a.steps, 1)
 
-    # hops of one step (identical every step: same inputs)
-    if world == 1:
-        outs = dout.cpu().numpy().view(np.uint8).reshape(-1, 16)
-        hops = outs[:, 4:6].copy().view(np.uint16).ravel().astype(np.int64)
-        status = outs[:, 6]
-        n_ok = int((status == 0).sum())
-        hop_total = int(hops.sum())
-    else:
+    # ---- work of one step (identical every step: same inputs)
+    rpc_total = None
+    if sharded:
         hop_total, n_ok = sh.hop_total(), sh.ok_total()
-
-    t = torch.tensor([wall, float(hop_total), float(n_ok)], dtype=torch.float64, device=dev)
-    if world > 1:
-        w = t[:1].clone()
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        s = t[1:].clone()
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        wall_max, hop_all, ok_all = float(w[0]), float(s[0]), float(s[1])
+        kern_ms = sh.kernel_ms / max(sh.runs, 1)
     else:
-        wall_max, hop_all, ok_all = wall, float(hop_total), float(n_ok)
+        outs = dout.cpu().numpy().reshape(-1, 16)
+        hop_total = int(outs[:, 4:6].copy().view(np.uint16).astype(np.int64).sum())
+        n_ok = int((outs[:, 6] == 0).sum())
+        if drpc is not None:
+            rpc_total = int(drpc.cpu().numpy().astype(np.int64).sum())
+        kern_ms = step_ms
+
+    t = torch.tensor([wall, float(hop_total), float(n_ok), float(rpc_total or 0)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tt = t.to("cpu") if backend != "nccl" else t
+        w = tt[:1].clone()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        s = tt[1:].clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        wall_max, hop_all, ok_all, rpc_all = float(w[0]), float(s[0]), float(s[1]), float(s[2])
+    else:
+        wall_max, hop_all, ok_all, rpc_all = wall, float(hop_total), float(n_ok), float(rpc_total or 0)
 
     if rank == 0:
         value = hop_all * a.steps / wall_max
-        achieved = (hop_total * B_HOP) / (kern_ms * 1e-3) / 1e9
-        traffic = traffic_from_csv(a.traffic_csv)
+        if kind == "chord":
+            per_launch_bytes, bper = hop_total * B_HOP, B_HOP
+        else:
+            per_launch_bytes, bper = rpc_total * B_RPC, B_RPC
+        achieved = per_launch_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = traffic_from_csv(a.traffic_csv, kname)
         cpu = None
-        if world == 1 and not a.no_cpu_baseline:
-            cpu = cpu_baseline(ids, xy, keys, src, a.cpu_seconds)
+        if world == 1 and not a.no_cpu_baseline and small:
+            cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1))
+        cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
+               "hopCountMax": 50, "parallelism": (f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)"
+                                                  if sharded else ("replicas" if world > 1 else "1 GPU")),
+               "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1)}
+        if kind == "kademlia":
+            cfg.update({"k": 8, "alpha": wl["alpha"], "rpcs_per_s": rpc_all * a.steps / wall_max,
+                        "mean_rpcs": rpc_all / max(ok_all, 1)})
+        else:
+            cfg.update({"successorListSize": 8})
+        if sharded:
+            cfg.update({"hop_rounds": sh.rounds})
         line = {
             "metric": "routed lookup hops/sec (whole node)",
             "value": value,
@@ -188,22 +270,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32 keys (160-bit int), int64 ns, fp64 coords",
-            "data": "synthetic: seeded uniform 160-bit node IDs and keys, uniform(-75,75) coordinates",
-            "config": {
-                "workload": "C: Chord 2^20 nodes per GPU, 10M random-key iterative one-way lookups per GPU",
-                "overlay": "chord", "nodes_per_gpu": a.nodes, "nodes_total": nodes_total,
-                "lookups_per_gpu": a.lookups, "successorListSize": 8, "hopCountMax": 50,
-                "parallelism": f"ring sharded over {world} GPU(s)",
-                "lookups_per_s": ok_all * a.steps / wall_max,
-                "mean_hops": hop_all / max(ok_all, 1),
-            },
+            "dtype": "u32 (160-bit keys), int64 ns, fp64 coordinates",
+            "data": "synthetic: seeded uniform 160-bit node IDs and keys; coordinates uniform(-75,75) "
+                    "or nodes_2d_15000.xml records (B)",
+            "config": cfg,
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": (traffic / 1.0) if traffic else None,
-                "kernel": "k_chord_route", "kernel_ms": kern_ms,
-                "bytes_per_hop_algorithmic": B_HOP,
+                "traffic": traffic,
+                "kernel": kname, "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_unit": bper, "unit_of_work": "hop" if kind == "chord" else "RPC",
             },
             "cpu_baseline": cpu,
         }

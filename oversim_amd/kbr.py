@@ -219,6 +219,17 @@ class KbrEngine:
         self._chk(self._L.ovs_chord_load(self._h, _ptr(ids), len(ids), _ptr(xy), 0), "ovs_chord_load")
         self.n, self.overlay = len(ids), OVERLAY_CHORD
 
+    def chord_load_device(self, ids_ptr: int, xy_ptr: int, n: int):
+        """Load a Chord ring whose sorted ids / coordinates already live on this device."""
+        self._chk(self._L.ovs_chord_load(self._h, C.c_void_p(ids_ptr), n, C.c_void_p(xy_ptr), DEVICE_PTRS),
+                  "ovs_chord_load")
+        self.n, self.overlay = n, OVERLAY_CHORD
+
+    def kad_load_device(self, ids_ptr: int, xy_ptr: int, n: int):
+        self._chk(self._L.ovs_kad_load(self._h, C.c_void_p(ids_ptr), n, C.c_void_p(xy_ptr), DEVICE_PTRS),
+                  "ovs_kad_load")
+        self.n, self.overlay = n, OVERLAY_KADEMLIA
+
     def chord_load_tables(self, ids, xy, pred, succ, nsucc, fingers, deque_size):
         ids = keys_array(ids)
         arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
@@ -269,10 +280,11 @@ class KbrEngine:
         return res
 
     def lookup_device(self, keys_ptr: int, src_ptr: int, n: int, out_ptr: int, stream: int | None = None,
-                      hop_ptr: int | None = None):
-        """Device-resident batch (pointers on this context's device, async on `stream`)."""
+                      hop_ptr: int | None = None, rpcs_ptr: int | None = None):
+        """Device-resident batch (pointers on this context's device, async on `stream`, 0 = default stream)."""
         self._chk(self._L.ovs_route_batch(self._h, C.c_void_p(keys_ptr), C.c_void_p(src_ptr), n,
-                                          C.c_void_p(out_ptr), C.c_void_p(hop_ptr) if hop_ptr else None, None,
+                                          C.c_void_p(out_ptr), C.c_void_p(hop_ptr) if hop_ptr else None,
+                                          C.c_void_p(rpcs_ptr) if rpcs_ptr else None,
                                           DEVICE_PTRS, C.c_void_p(stream) if stream else None), "ovs_route_batch")
 
     def findNode(self, node, keys, numRedundantNodes: int, numSiblings: int, max_out: int = 16):

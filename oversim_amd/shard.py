@@ -66,6 +66,10 @@ class GpuShardStepper:
         self.done_count = torch.zeros(1, dtype=torch.int64, device=device)
         self.done = torch.empty((max(capacity, 1), DONE_BYTES), dtype=torch.uint8, device=device)
         self.done_cap = max(capacity, 1)
+        self.timing = False
+        self.kernel_ms = 0.0
+        self._ev0 = torch.cuda.Event(enable_timing=True)
+        self._ev1 = torch.cuda.Event(enable_timing=True)
 
     def _ensure(self, cap: int):
         torch = self.torch
@@ -99,12 +103,18 @@ class GpuShardStepper:
         n_in = inbox.shape[0]
         self._ensure(n_in)
         self.out_count.zero_()
+        if self.timing:
+            self._ev0.record()
         st = lib().ovs_shard_step(self.eng._h, C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(self.out.data_ptr()),
                                   C.c_void_p(self.out_dest.data_ptr()), self.cap, C.c_void_p(self.out_count.data_ptr()),
                                   C.c_void_p(self.done.data_ptr()), self.done_cap,
                                   C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
         self.eng._chk(st, "ovs_shard_step")
+        if self.timing:
+            self._ev1.record()
         m = int(self.out_count.item())
+        if self.timing:
+            self.kernel_ms += self._ev0.elapsed_time(self._ev1)
         return self.out[:m], self.out_dest[:m]
 
     def finished(self):
@@ -215,25 +225,26 @@ def done_to_numpy(done_t) -> np.ndarray:
 class ShardedChord:
     """bench.py driver for one rank: ring arc + lookups resident in HBM + RCCL exchange."""
 
-    def __init__(self, rank, world, ids, xy, keys, src, device, stream):
-        import torch
+    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None):
         self.bounds = arc_bounds(len(ids), world)
-        lo, hi = self.bounds[rank], self.bounds[rank + 1]
-        assert np.all((src >= lo) & (src < hi)), "lookups must originate on this rank's arc"
-        n = len(keys)
-        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, stream=stream,
-                                       capacity=max(2 * n, 1024))
+        n = keys_t.shape[0]
+        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(2 * n, 1024))
         self.stepper.reset(world * n + 1024)
-        self.exchange = TorchExchange(world, device)
-        self.keys_t = torch.from_numpy(np.ascontiguousarray(keys)).to(device)
-        self.src_t = torch.from_numpy(np.ascontiguousarray(src)).to(device)
+        self.stepper.timing = True
+        self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)
+        self.keys_t, self.src_t = keys_t, src_t
         self.qid_base = rank * n
         self._done = None
         self.rounds = 0
+        self.runs = 0
+        self.kernel_ms = 0.0
 
     def run(self):
         self.stepper.reset(self.stepper.done_cap)
+        self.stepper.kernel_ms = 0.0
         self._done, self.rounds = route_sharded(self.stepper, self.exchange, self.keys_t, self.src_t, self.qid_base)
+        self.runs += 1
+        self.kernel_ms += self.stepper.kernel_ms
 
     def hop_total(self) -> int:
         d = done_to_numpy(self._done)

@@ -81,3 +81,52 @@ def lookups(ids: np.ndarray, m: int, seed: int, node_ids: bool = True) -> tuple[
 def population(n: int, seed: int, use_file: bool | None = None):
     from .kbr import Network
     return Network(ids=sorted_unique_ids(n, seed), xy=coordinates(n, seed, use_file=use_file))
+
+
+def device_population(n: int, seed: int, device, field_size: int = 150):
+    """Large rings generated on the GPU (configs D/E): sorted unique uniform 160-bit IDs
+    and uniform(-fs/2, fs/2) coordinates as device tensors ((n,5) int32 view of u32, (n,2) f64).
+    Sorting is on the top 64 bits (torch int64 sort, sign bit flipped); the rare groups of
+    equal top 64 bits are ordered by the low 96 bits on the host."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    w = torch.randint(-(1 << 31), 1 << 31, (n, 5), dtype=torch.int64, device=device, generator=g)
+    w = w.to(torch.int32)
+    top = (w[:, 4].to(torch.int64) << 32) | (w[:, 3].to(torch.int64) & 0xFFFFFFFF)
+    top = top ^ (-(1 << 63))                    # unsigned order as signed
+    order = torch.argsort(top)
+    w = w[order].contiguous()
+    top = top[order]
+    eq = (top[1:] == top[:-1]).nonzero().flatten()
+    if eq.numel():
+        wc = w.cpu().numpy().view(np.uint32)
+        idx = sorted(set(eq.tolist()) | set((eq + 1).tolist()))
+        # sort each run of equal top words by the remaining words (exact 160-bit order)
+        runs, cur = [], [idx[0]]
+        for i in idx[1:]:
+            if i == cur[-1] + 1 and top[i] == top[cur[0]]:
+                cur.append(i)
+            else:
+                runs.append(cur); cur = [i]
+        runs.append(cur)
+        for r in runs:
+            sub = wc[r]
+            o = np.lexsort((sub[:, 0], sub[:, 1], sub[:, 2]))
+            wc[r] = sub[o]
+        w = torch.from_numpy(wc.view(np.int32)).to(device)
+        full = [tuple(x) for x in wc[idx]]
+        assert len(set(full)) == len(full), "duplicate 160-bit id (re-seed)"
+    xy = torch.rand((n, 2), dtype=torch.float64, device=device, generator=g) * float(field_size) - float(field_size // 2)
+    return w, xy
+
+
+def device_lookups(n_nodes: int, m: int, seed: int, device, src_lo: int = 0, src_hi: int | None = None):
+    """m uniform random 160-bit keys and uniform sources in [src_lo, src_hi) as device tensors."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    keys = torch.randint(-(1 << 31), 1 << 31, (m, 5), dtype=torch.int64, device=device, generator=g).to(torch.int32)
+    hi = n_nodes if src_hi is None else src_hi
+    src = torch.randint(src_lo, hi, (m,), dtype=torch.int64, device=device, generator=g).to(torch.int32)
+    return keys.contiguous(), src.contiguous()
