@@ -182,6 +182,53 @@ ovs_status  ovs_delay_batch(ovs_ctx* ctx, const uint32_t* a, const uint32_t* b,
 
 ovs_status  ovs_sync(ovs_ctx* ctx);
 
+/* ---- KBRTestApp statistics (one-way test) ----
+ * Replaces the statistics a KBRTestApp run hands to GlobalStatistics:
+ *   KBRTestApp::evaluateData -> recordOutVector("KBRTestApp: One-way Hop Count" /
+ *     "One-way Latency")                    KBRTestApp.cc:479-496
+ *   KBRTestApp::deliver lookupNodeIds check  KBRTestApp.cc:380-440 (numDropped)
+ *   KBRTestApp::finishApp -> addStdDev(...)  KBRTestApp.cc:498-520
+ *   SendToKeyListener failed lookup          BaseOverlay.cc:1258-1270 (overlay numDropped)
+ *   GlobalStatistics::finalizeStatistics     GlobalStatistics.cc:103-140 (".mean" scalars)
+ * One cStdDev summary over the nodes of the network (every node runs
+ * finishApp; the delivery ratio only for nodes with numSent > 0). */
+typedef struct ovs_stddev {
+    uint64_t count;
+    double   mean, stddev, min, max;    /* cStdDev: stddev = sample (n-1) deviation, 0 if n < 2 */
+} ovs_stddev;
+
+typedef struct ovs_kbrtest_stats {
+    uint64_t num_sent;               /* one-way test messages (= lookups in the batch) */
+    uint64_t num_delivered;          /* evaluateData calls */
+    uint64_t num_dropped;            /* lookupNodeIds: delivered to a node whose key != destKey */
+    uint64_t num_lookup_failed;      /* !isValid(): dropped by SendToKeyListener (overlay numDropped) */
+    uint64_t bytes_sent, bytes_delivered, bytes_dropped;
+    uint64_t hop_count_sum;          /* sum of One-way Hop Count over delivered messages */
+    int64_t  latency_sum_ns;         /* sum of One-way Latency over delivered messages */
+    uint32_t hop_count_min, hop_count_max;
+    int64_t  latency_min_ns, latency_max_ns;
+    double   hop_count_mean;         /* "Vector: KBRTestApp: One-way Hop Count.mean" */
+    double   latency_mean_s;         /* "Vector: KBRTestApp: One-way Latency.mean" */
+    uint64_t status_count[8];        /* lookups by OVS_LOOKUP_* status */
+    uint64_t hop_hist[64];           /* delivered messages by one-way hop count (63 = 63 or more) */
+    ovs_stddev delivered_msgs_per_s; /* "KBRTestApp: One-way Delivered Messages/s" */
+    ovs_stddev delivered_bytes_per_s;
+    ovs_stddev dropped_msgs_per_s;
+    ovs_stddev dropped_bytes_per_s;
+    ovs_stddev delivery_ratio;       /* "KBRTestApp: One-way Delivery Ratio" ((float)d / (float)s) */
+} ovs_kbrtest_stats;
+
+/* Reduce a batch of route results (out/keys/src as passed to ovs_route_batch)
+ * to KBRTestApp statistics.  measured_time_s = each node's measured lifetime
+ * (GlobalStatistics::calcMeasuredLifetime); per-node rates are only produced
+ * when it is >= GlobalStatistics::MIN_MEASURED = 0.1 s.  lookup_node_ids =
+ * the kbrTestApp.lookupNodeIds parameter; message sizes come from
+ * testMsgSize.  *stats is host memory; out/keys/src follow `flags`. */
+ovs_status  ovs_kbrtest_stats_batch(ovs_ctx* ctx, const ovs_route_out* out, const ovs_key160* keys,
+                                    const uint32_t* src, uint64_t n, double measured_time_s,
+                                    int32_t lookup_node_ids, ovs_kbrtest_stats* stats,
+                                    uint32_t flags, void* stream);
+
 /* ---- multi-GPU sharding (one process per GPU; the host exchanges records) ----
  * The sorted ring is cut into contiguous arcs, one per rank.  Node keys and
  * coordinates are replicated (24 + 16 B per node); the finger rows -- the bulk

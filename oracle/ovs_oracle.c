@@ -1158,3 +1158,87 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
     (void)nthreads;
     return total;
 }
+
+/* ======================================================================== */
+/* KBRTestApp one-way statistics                                             */
+/* ======================================================================== */
+
+typedef struct { uint64_t n; double sum, sqrsum, min, max; } StdDev;   /* OMNeT++ cStdDev */
+
+static void sd_collect(StdDev* s, double v)                 /* cStdDev::collect */
+{
+    if (s->n == 0 || v < s->min) s->min = v;
+    if (s->n == 0 || v > s->max) s->max = v;
+    s->n++;
+    s->sum += v;
+    s->sqrsum += v * v;
+}
+
+static void sd_finish(const StdDev* s, orc_stddev* o)       /* getMean / getStddev */
+{
+    o->count = s->n;
+    o->mean = o->stddev = o->min = o->max = 0;
+    if (!s->n) return;
+    o->mean = s->sum / (double)s->n;
+    double var = 0;
+    if (s->n > 1) {
+        var = (s->sqrsum - s->sum * s->sum / (double)s->n) / (double)(s->n - 1);
+        if (var < 0) var = 0;
+    }
+    o->stddev = sqrt(var);
+    o->min = s->min;
+    o->max = s->max;
+}
+
+void orc_kbrtest_stats(const orc_net* net, const orc_route_out* out, const orc_key* keys, const uint32_t* src,
+                       uint64_t n, double T, int lookupNodeIds, int32_t testMsgSize, orc_kbrtest_result* st)
+{
+    /* per-node KBRTestApp members numSent / numDelivered / numDropped (KBRTestApp.cc:70-80) */
+    uint64_t* sent = calloc(net->n, sizeof(uint64_t));
+    uint64_t* deliv = calloc(net->n, sizeof(uint64_t));
+    uint64_t* drop = calloc(net->n, sizeof(uint64_t));
+    memset(st, 0, sizeof *st);
+    double hopVec = 0, latVec = 0;     /* GlobalStatistics OutVector value sums */
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t s = src[i];
+        if (s < net->n) sent[s]++;                        /* handleTimerEvent: numSent++ (180-181) */
+        st->num_sent++;
+        if (out[i].status != 0) {                         /* SendToKeyListener: lookup failed (1258-1270) */
+            st->num_lookup_failed++;
+            continue;
+        }
+        int match = 1;
+        if (lookupNodeIds) {                              /* deliver: thisNode.key == destKey (407) */
+            OKey k = ok_from(&keys[i]);
+            match = out[i].responsible < net->n && ok_cmp(&net->ids[out[i].responsible], &k) == 0;
+        }
+        if (!match) {                                     /* deliver: numDropped++ (411-413) */
+            st->num_dropped++;
+            if (s < net->n) drop[s]++;
+            continue;
+        }
+        st->num_delivered++;                              /* evaluateData (481-482) */
+        if (s < net->n) deliv[s]++;
+        st->hop_count_sum += out[i].one_way_hops;
+        st->latency_sum_ns += out[i].latency_ns;
+        hopVec += (double)out[i].one_way_hops;            /* recordOutVector (492-495) */
+        latVec += (double)out[i].latency_ns * 1e-9;       /* SIMTIME_DBL(latency) */
+    }
+    if (st->num_delivered) {                              /* finalizeStatistics (134-139) */
+        st->hop_count_mean = hopVec / (double)st->num_delivered;
+        st->latency_mean_s = latVec / (double)st->num_delivered;
+    }
+    StdDev sd[5];
+    memset(sd, 0, sizeof sd);
+    if (T >= 0.1) {                                       /* finishApp: time >= MIN_MEASURED (502) */
+        for (uint32_t c = 0; c < net->n; ++c) {
+            sd_collect(&sd[0], (double)deliv[c] / T);
+            sd_collect(&sd[1], (double)(deliv[c] * (uint64_t)testMsgSize) / T);
+            sd_collect(&sd[2], (double)drop[c] / T);
+            sd_collect(&sd[3], (double)(drop[c] * (uint64_t)testMsgSize) / T);
+            if (sent[c] > 0) sd_collect(&sd[4], (double)((float)deliv[c] / (float)sent[c]));
+        }
+    }
+    for (int k = 0; k < 5; ++k) sd_finish(&sd[k], &st->sd[k]);
+    free(sent); free(deliv); free(drop);
+}

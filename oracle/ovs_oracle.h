@@ -119,6 +119,21 @@ int64_t orc_delay_ns(const orc_net* net, uint32_t a, uint32_t b, int32_t bytes);
 /* float distance (SimpleNodeEntry.cc:145-153) */
 float orc_coord_dist(const orc_net* net, uint32_t a, uint32_t b);
 
+/* ---- KBRTestApp one-way statistics (KBRTestApp.cc:380-520, BaseOverlay.cc:1258-1270,
+ * GlobalStatistics.cc:103-200).  Per-node KBRTestApp counters, then finishApp in node
+ * order feeding cStdDev accumulators (OMNeT++ cStdDev: n, sum, sqrsum, min, max;
+ * sample variance, 0 below two values).  Rates only when T >= MIN_MEASURED = 0.1 s. */
+typedef struct { uint64_t count; double mean, stddev, min, max; } orc_stddev;
+typedef struct {
+    uint64_t num_sent, num_delivered, num_dropped, num_lookup_failed;
+    uint64_t hop_count_sum;
+    int64_t  latency_sum_ns;
+    double   hop_count_mean, latency_mean_s;   /* "Vector: ... .mean" scalars */
+    orc_stddev sd[5];   /* delivered msg/s, delivered B/s, dropped msg/s, dropped B/s, delivery ratio */
+} orc_kbrtest_result;
+void orc_kbrtest_stats(const orc_net* net, const orc_route_out* out, const orc_key* keys, const uint32_t* src,
+                       uint64_t n, double measured_time_s, int lookupNodeIds, int32_t testMsgSize,
+                       orc_kbrtest_result* st);
 const char* orc_last_error(void);
 
 #ifdef __cplusplus

@@ -20,8 +20,9 @@ void kad_free(KadTables& t)
 {
     if (t.recs) hipFree(t.recs);
     if (t.sib) hipFree(t.sib);
+    if (t.sibe) hipFree(t.sibe);
     if (t.slots) hipFree(t.slots);
-    t.recs = nullptr; t.sib = nullptr; t.slots = nullptr; t.total_slots = 0;
+    t.recs = nullptr; t.sib = nullptr; t.sibe = nullptr; t.slots = nullptr; t.total_slots = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -144,6 +145,19 @@ __global__ void k_kad_siblings(const KeyRec* __restrict__ recs, uint32_t n, int 
     o.boff = 0;
     out[v] = o;
     rowlen[v] = cnt > 0 ? (uint64_t)(KEYBITS - k_msb(R)) : 0;
+}
+
+__global__ void k_kad_sibentries(const KeyRec* __restrict__ recs, const uint32_t* __restrict__ sib, uint64_t total,
+                                 KadEntry* __restrict__ sibe)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const uint32_t x = sib[i];
+    KadEntry e;
+    e.idx = x;
+    const K160 k = x == NONE ? K160{{0, 0, 0, 0, 0}} : kload(recs, x);
+    for (int w = 0; w < 5; ++w) e.key[w] = k.w[w];
+    sibe[i] = e;
 }
 
 __global__ void k_kad_set_boff(KadRec* recs, const uint64_t* off, uint32_t n)
@@ -321,15 +335,37 @@ __device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadRec& 
     return ((D.w[0] & M.w[0]) | (D.w[1] & M.w[1]) | (D.w[2] & M.w[2]) | (D.w[3] & M.w[3]) | (D.w[4] & M.w[4])) == 0;
 }
 
+// insert up to 8 entries of a contiguous entry array (bucket slot or sibling block); the
+// loads are issued together before the dependent sorted inserts
+template <int CAP>
+__device__ __forceinline__ void add_entries8(SVec<CAP>& res, int cap, const KadEntry* __restrict__ s, int cnt,
+                                             const K160& K, const KadRec* __restrict__ recs)
+{
+    uint32_t ix[8];
+    uint64_t dd[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (q < cnt) {
+            const uint2* p = reinterpret_cast<const uint2*>(s + q);
+            const uint2 a = p[0], b = p[1], c = p[2];
+            ix[q] = c.y;
+            dd[q] = ((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(b.y ^ K.w[3]);
+            (void)a;
+        } else {
+            ix[q] = NONE;
+            dd[q] = 0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (ix[q] != NONE) svec_add(res, cap, ix[q], dd[q], K, recs);
+}
+
 template <int CAP>
 __device__ __forceinline__ void add_slot(SVec<CAP>& res, int cap, const KadView& V, uint32_t slot, const K160& K)
 {
-    const KadEntry* s = V.slots + (uint64_t)slot * V.k;
-    for (int q = 0; q < V.k; ++q) {
-        const KadEntry e = s[q];
-        if (e.idx == NONE) break;
-        svec_add(res, cap, e.idx, dist_hi(as_key(e.key), K), K, V.recs);
-    }
+    const KadEntry* e = V.slots + (uint64_t)slot * V.k;
+    for (int q0 = 0; q0 < V.k; q0 += 8) add_entries8(res, cap, e + q0, min(8, V.k - q0), K, V.recs);
 }
 
 // Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246)
@@ -355,11 +391,8 @@ __device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, con
         // nothing below bucket m can beat a full result unless siblings share bucket m
         if (!(m > endIndex && res.n >= cap)) {
             for (int b = m - 1; b >= endIndex; --b) add_slot(res, cap, V, slot_of(b), K);
-            const uint32_t* L = V.sib + (uint64_t)c * V.S5;
-            for (int i = 0; i < V.nsib; ++i) {
-                const uint32_t x = L[i];
-                svec_add(res, cap, x, dist_hi(kad_key(V.recs, x), K), K, V.recs);
-            }
+            const KadEntry* L = V.sibe + (uint64_t)c * V.S5;
+            for (int i = 0; i < V.nsib; i += 8) add_entries8(res, cap, L + i, min(8, V.nsib - i), K, V.recs);
             svec_add(res, cap, c, dist_hi(me, K), K, V.recs);
         }
     }
@@ -378,7 +411,115 @@ struct KadLC {
     int maxRedundantLocal;   // getMaxNumRedundantNodes() = k
 };
 
-template <bool RECORD>
+// One in-flight FindNodeCall = one future event: its response arrival or its RPC timeout.
+// Event order: (time, insertion time, insertion sequence); insertion time is kept as the
+// (always < 2^32 ns) gap back from the event time.
+struct Pend {
+    uint32_t node;
+    uint32_t tag;      // step at send (bits 0..15) | insertion sequence (bits 16..30) | timeout (bit 31)
+    int64_t t;         // event time
+    uint32_t dins;     // t - insertion time
+};
+
+// per-lane lookup state (IterativeLookup + its single IterativePathLookup)
+template <int A>
+struct KadLookup {
+    K160 K;
+    uint32_t S;
+    double sx, sy;
+    int64_t now, txf;
+    uint32_t seq;
+    SVec<8> nh;            // LookupVector nextHops (cap redundantNodes), used bits = alreadyUsed
+    Pend p[A];
+    uint32_t pvalid;
+    int step, hops, pending;
+    bool pfinished, psuccess, any_to;
+    uint32_t result, nsent;
+};
+
+// FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
+// SimpleNodeEntry::calcDelay with the source's tx queue)
+template <int A>
+__device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
+                                         uint32_t x)
+{
+    const double2 cxy = V.xy[x];
+    const KadRec rr = kad_rec(V.recs, x);
+    const bool sb = kad_is_sibling1(V, rr, L.K);
+    // the response carries findNode's result: 1 node when x is sibling, else min(redundant, n)
+    const int csz = sb ? 1 : (LC.redundant < (int)V.n ? LC.redundant : (int)V.n);
+    const int64_t cd = coord_ns(L.sx, L.sy, cxy.x, cxy.y, DC.round);
+    const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
+    const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
+    L.txf = newTx;
+    const int64_t d1 = (newTx - L.now) + DC.access2 + cd + bwc;
+    const int64_t bwr = bw_ns(DC.respBase + DC.respPerNode * csz, DC.datarate, DC.round);
+    const int64_t d2 = 2 * bwr + DC.access2 + cd;
+    const int64_t tTo = L.now + DC.rpcTimeout;
+    const int64_t tResp = L.now + d1 + d2;
+    const bool isTo = tTo <= tResp;   // the timeout was scheduled first: it wins ties
+    const uint32_t sTo = L.seq++;
+    const uint32_t sR = L.seq++;
+    const uint32_t tag = (uint32_t)L.step | ((isTo ? sTo : sR) << 16) | (isTo ? 0x80000000u : 0u);
+    int slot = 0;
+#pragma unroll
+    for (int i = A - 1; i >= 0; --i)
+        if (!((L.pvalid >> i) & 1u)) slot = i;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+        if (i == slot) {
+            L.p[i].node = x;
+            L.p[i].t = isTo ? tTo : tResp;
+            L.p[i].dins = (uint32_t)(isTo ? DC.rpcTimeout : d2);
+            L.p[i].tag = tag;
+        }
+    }
+    L.pvalid |= 1u << slot;
+    ++L.nsent;
+}
+
+// IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
+template <int A>
+__device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
+                                              int num)
+{
+    if (L.pfinished) return;
+    if (LC.hopCountMax && L.hops >= LC.hopCountMax) { L.pfinished = true; L.psuccess = false; return; }
+    if (LC.strict) num = min(num, LC.alpha - L.pending);
+    if (num == 0 && L.pending == 0 && !LC.finishOnFirst) num = LC.alpha;
+    for (int i = 0; num > 0 && i < LC.redundant; ++i) {
+        // getNextEntry: first entry not alreadyUsed (no node is ever dead in a stable network)
+        const uint32_t unused = ~L.nh.used & ((1u << L.nh.n) - 1u);
+        if (!unused) break;
+        const int e = __ffs((int)unused) - 1;
+        uint32_t h = NONE;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j == e) h = L.nh.idx[j];
+        // visitOnlyOnce: an unused entry can only be a visited node if it is the source
+        // (responders stay in nextHops as used entries or are evicted for good)
+        if (!LC.visitOnlyOnce || h != L.S) {
+            ++L.pending;
+            --num;
+            kad_send(L, V, DC, LC, h);
+        }
+        L.nh.used |= 1u << e;
+    }
+    if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
+}
+
+template <int A>
+__device__ __forceinline__ void kad_timeoutlike(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
+                                                const KadLC& LC)
+{
+    // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
+    --L.pending;
+    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
+    else if (LC.newOnTimeout) kad_send_rpcs(L, V, DC, LC, 1);
+    else if (L.pending == 0) kad_send_rpcs(L, V, DC, LC, LC.alpha);
+}
+
+template <int A, bool RECORD>
 __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, KadLC LC, const K160* __restrict__ qkeys,
                                                    const uint32_t* __restrict__ qsrc, uint64_t nq, uint64_t chunk,
                                                    ovs_route_out* __restrict__ out, uint32_t* __restrict__ hopseq,
@@ -392,94 +533,8 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
 
     bool active = false;
     uint64_t q = 0;
-    K160 K;
-    uint32_t S = 0;
-    double sx = 0, sy = 0;
-    int64_t now = 0, txf = 0;
-    uint32_t seq = 0;
-    SVec<8> nh;
-    svec_clear(nh);
-    // pending FindNodeCalls: one future event each (response arrival or RPC timeout)
-    uint32_t pnode[MAXA];
-    int64_t pt[MAXA], pins[MAXA];
-    uint32_t pseq[MAXA];
-    int pvr[MAXA];
-    uint32_t pvalid = 0, pto = 0;
-    int step = 0, hops = 0, pending = 0;
-    bool pfinished = false, psuccess = false;
-    uint32_t result = NONE;
-    uint32_t nsent = 0;
-    bool any_to = false;
-
-    const int64_t T_rpc = DC.rpcTimeout;
-
-    // send one FindNodeCall to node x at `now` (IterativeLookup::sendRpc, BaseRpc timeout)
-    auto send = [&](uint32_t x) {
-        const double2 cxy = V.xy[x];
-        const KadRec rr = kad_rec(V.recs, x);
-        const bool sb = kad_is_sibling1(V, rr, K);
-        // response size: findNode result count (1 if sibling, else min(8, candidates) )
-        const int csz = sb ? 1 : (LC.redundant < (int)V.n ? LC.redundant : (int)V.n);
-        const int64_t cd = coord_ns(sx, sy, cxy.x, cxy.y, DC.round);
-        const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
-        const int64_t newTx = (txf > now ? txf : now) + bwc;
-        txf = newTx;
-        const int64_t d1 = (newTx - now) + DC.access2 + cd + bwc;
-        const int64_t bwr = bw_ns(DC.respBase + DC.respPerNode * csz, DC.datarate, DC.round);
-        const int64_t d2 = 2 * bwr + DC.access2 + cd;
-        const int64_t tTo = now + T_rpc;
-        const int64_t tResp = now + d1 + d2;
-        // free slot (static index)
-        int slot = 0;
-#pragma unroll
-        for (int i = MAXA - 1; i >= 0; --i)
-            if (!((pvalid >> i) & 1u)) slot = i;
-        const bool isTo = tTo <= tResp;
-        const uint32_t sTo = seq++;
-        const uint32_t sR = seq++;
-#pragma unroll
-        for (int i = 0; i < MAXA; ++i) {
-            if (i == slot) {
-                pnode[i] = x;
-                pt[i] = isTo ? tTo : tResp;
-                pins[i] = isTo ? now : now + d1;
-                pseq[i] = isTo ? sTo : sR;
-                pvr[i] = step;
-            }
-        }
-        pvalid |= 1u << slot;
-        pto = isTo ? (pto | (1u << slot)) : (pto & ~(1u << slot));
-        ++nsent;
-    };
-
-    // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
-    auto send_rpcs = [&](int num) {
-        if (pfinished) return;
-        if (LC.hopCountMax && hops >= LC.hopCountMax) { pfinished = true; psuccess = false; return; }
-        if (LC.strict) num = min(num, LC.alpha - pending);
-        if (num == 0 && pending == 0 && !LC.finishOnFirst) num = LC.alpha;
-        for (int i = 0; num > 0 && i < LC.redundant; ++i) {
-            // getNextEntry: first entry not alreadyUsed (no node is ever dead in a stable network)
-            int e = -1;
-#pragma unroll
-            for (int j = 7; j >= 0; --j)
-                if (j < nh.n && !((nh.used >> j) & 1u)) e = j;
-            if (e < 0) break;
-            uint32_t h = NONE;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j == e) h = nh.idx[j];
-            // visitOnlyOnce: an unused entry can only be a visited node if it is the source
-            // (responders stay in nextHops as used entries or are permanently evicted)
-            if (!LC.visitOnlyOnce || h != S) {
-                ++pending;
-                --num;
-                send(h);
-            }
-            nh.used |= 1u << e;
-        }
-        if (pending == 0) { psuccess = false; pfinished = true; }
-    };
+    KadLookup<A> L;
+    SVec<8> res;
 
     while (true) {
         const uint64_t need = __ballot(!active);
@@ -488,32 +543,30 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
             if (!active && mine < end) {
                 q = mine;
                 active = true;
-                K = qkeys[q];
-                S = qsrc[q];
-                const double2 sxy = V.xy[S];
-                sx = sxy.x; sy = sxy.y;
-                now = 0; txf = 0; seq = 0;
-                svec_clear(nh);
-                pvalid = 0; pto = 0;
-                step = 0; hops = 0; pending = 0;
-                pfinished = false; psuccess = false;
-                result = NONE;
-                nsent = 0;
-                any_to = false;
+                L.K = qkeys[q];
+                L.S = qsrc[q];
+                const double2 sxy = V.xy[L.S];
+                L.sx = sxy.x; L.sy = sxy.y;
+                L.now = 0; L.txf = 0; L.seq = 0;
+                svec_clear(L.nh);
+                L.pvalid = 0;
+                L.step = 0; L.hops = 0; L.pending = 0;
+                L.pfinished = false; L.psuccess = false; L.any_to = false;
+                L.result = NONE;
+                L.nsent = 0;
                 // IterativeLookup::start (IterativeLookup.cc:133-244): local findNode at S
-                const KadRec rs = kad_rec(V.recs, S);
-                const bool sb = kad_is_sibling1(V, rs, K);
-                SVec<8> loc;
-                kad_find_node1(V, S, rs, K, LC.maxRedundantLocal, sb, loc);
-                if (loc.n == 0) { pfinished = true; psuccess = false; }
+                const KadRec rs = kad_rec(V.recs, L.S);
+                const bool sb = kad_is_sibling1(V, rs, L.K);
+                kad_find_node1(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res);
+                if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
                 else if (LC.numSiblings != 0 && sb) {
-                    result = loc.idx[0];
-                    pfinished = true; psuccess = true;
+                    L.result = res.idx[0];
+                    L.pfinished = true; L.psuccess = true;
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
-                        if (j < loc.n) svec_add(nh, LC.redundant, loc.idx[j], loc.d[j], K, V.recs);
-                    send_rpcs(LC.alpha);
+                        if (j < res.n) svec_add(L.nh, LC.redundant, res.idx[j], res.d[j], L.K, V.recs);
+                    kad_send_rpcs(L, V, DC, LC, LC.alpha);
                 }
             }
             cursor += (uint64_t)__popcll(need);
@@ -521,102 +574,96 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
         if (!__any(active)) break;
         if (!active) continue;
 
-        if (!pfinished && pvalid) {
-            // earliest event: (time, insertion time, insertion sequence)
+        if (!L.pfinished && L.pvalid) {
+            // earliest event
             int e = -1;
             int64_t bt = 0, bi = 0;
             uint32_t bs = 0;
 #pragma unroll
-            for (int i = 0; i < MAXA; ++i) {
-                if ((pvalid >> i) & 1u) {
-                    const bool better = e < 0 || pt[i] < bt || (pt[i] == bt && (pins[i] < bi || (pins[i] == bi && pseq[i] < bs)));
-                    if (better) { e = i; bt = pt[i]; bi = pins[i]; bs = pseq[i]; }
+            for (int i = 0; i < A; ++i) {
+                if ((L.pvalid >> i) & 1u) {
+                    const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
+                    const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
+                    const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
+                    if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
                 }
             }
-            uint32_t r = 0;
-            int vr = 0;
+            uint32_t r = 0, tag = 0;
 #pragma unroll
-            for (int i = 0; i < MAXA; ++i)
-                if (i == e) { r = pnode[i]; vr = pvr[i]; }
-            const bool isTo = (pto >> e) & 1u;
-            pvalid &= ~(1u << e);
-            now = bt;
-            const int64_t lkTo = DC.lookupTimeout;
-            if (isTo) {
-                // handleRpcTimeout -> IterativePathLookup::handleTimeout (IterativeLookup.cc:588-654, 935-1023)
-                any_to = true;
-                --pending;
-                if (now > lkTo) { pfinished = true; psuccess = false; }
-                else if (LC.newOnTimeout) send_rpcs(1);
-                else if (pending == 0) send_rpcs(LC.alpha);
+            for (int i = 0; i < A; ++i)
+                if (i == e) { r = L.p[i].node; tag = L.p[i].tag; }
+            L.pvalid &= ~(1u << e);
+            L.now = bt;
+            const int vr = (int)(tag & 0xFFFFu);
+            if (tag & 0x80000000u) {
+                // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
+                L.any_to = true;
+                kad_timeoutlike(L, V, DC, LC);
             } else {
                 const KadRec rr = kad_rec(V.recs, r);
-                const bool sb = kad_is_sibling1(V, rr, K);
-                const bool acc = (LC.useAll && LC.merge) ? true : (vr == step);
+                const bool sb = kad_is_sibling1(V, rr, L.K);
+                const bool acc = (LC.useAll && LC.merge) ? true : (vr == L.step);
                 if (acc || (sb && LC.acceptLateSiblings)) {
                     // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
-                    if (now > lkTo) { pfinished = true; psuccess = false; }
+                    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
                     else {
-                        if (r != S) {
-                            if (RECORD && hops < LC.hopCountMax) hopseq[q * (uint64_t)LC.hopCountMax + hops] = r;
-                            ++hops;
+                        if (r != L.S) {
+                            if (RECORD && L.hops < LC.hopCountMax)
+                                hopseq[q * (uint64_t)LC.hopCountMax + L.hops] = r;
+                            ++L.hops;
                         }
-                        ++step;
-                        --pending;
-                        SVec<8> res;
-                        kad_find_node1(V, r, rr, K, LC.redundant, sb, res);
+                        ++L.step;
+                        --L.pending;
+                        kad_find_node1(V, r, rr, L.K, LC.redundant, sb, res);
                         int numNew = 0;
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
                             if (j < res.n) {
-                                const int pos = svec_add(nh, LC.redundant, res.idx[j], res.d[j], K, V.recs);
+                                const int pos = svec_add(L.nh, LC.redundant, res.idx[j], res.d[j], L.K, V.recs);
                                 if (pos >= 0 && pos < LC.redundant) ++numNew;
-                                if (LC.numSiblings != 0 && sb && result == NONE) result = res.idx[j];
                             }
                         }
-                        if (sb && res.n != 0 && LC.numSiblings != 0) { pfinished = true; psuccess = true; }
+                        if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
+                        if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
                         else {
                             if (numNew == 0 && LC.newOnResp) numNew = 1;
-                            send_rpcs(min(numNew, LC.alpha));
+                            kad_send_rpcs(L, V, DC, LC, min(numNew, LC.alpha));
                         }
                     }
                 } else {
                     // not accepted: handled as a timeout, its nodes are dropped
-                    --pending;
-                    if (now > lkTo) { pfinished = true; psuccess = false; }
-                    else if (LC.newOnTimeout) send_rpcs(1);
-                    else if (pending == 0) send_rpcs(LC.alpha);
+                    kad_timeoutlike(L, V, DC, LC);
                 }
             }
         }
         // checkStop (IterativeLookup.cc:295-349): the single path finished, or nothing pending
-        if (pfinished || pvalid == 0) {
+        if (L.pfinished || L.pvalid == 0) {
             ovs_route_out o;
-            o.hops = (uint16_t)hops;
-            if (pfinished && psuccess && result != NONE) {
+            o.hops = (uint16_t)L.hops;
+            if (L.pfinished && L.psuccess && L.result != NONE) {
                 o.status = OVS_LOOKUP_OK;
-                o.responsible = result;
-                o.one_way_hops = (uint8_t)(hops + (result != S ? 1 : 0));
-                int64_t lat = now;
-                if (result != S) {
+                o.responsible = L.result;
+                o.one_way_hops = (uint8_t)(L.hops + (L.result != L.S ? 1 : 0));
+                int64_t lat = L.now;
+                if (L.result != L.S) {
                     // sendRouteMessage through the source's tx queue (SimpleNodeEntry.cc:164-194)
-                    const double2 rxy = V.xy[result];
+                    const double2 rxy = V.xy[L.result];
                     const int64_t bwr = bw_ns(DC.routeBytes, DC.datarate, DC.round);
-                    const int64_t newTx = (txf > now ? txf : now) + bwr;
-                    lat = newTx + DC.access2 + coord_ns(sx, sy, rxy.x, rxy.y, DC.round) + bwr;
+                    const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwr;
+                    lat = newTx + DC.access2 + coord_ns(L.sx, L.sy, rxy.x, rxy.y, DC.round) + bwr;
                 }
                 o.latency_ns = lat;
             } else {
                 o.responsible = NONE;
                 o.one_way_hops = 0;
                 o.latency_ns = -1;
-                if (now > DC.lookupTimeout) o.status = OVS_LOOKUP_TIMEOUT;
-                else if (any_to) o.status = OVS_LOOKUP_RPC_TIMEOUT;
-                else if (LC.hopCountMax && hops >= LC.hopCountMax) o.status = OVS_LOOKUP_HOPMAX;
+                if (L.now > DC.lookupTimeout) o.status = OVS_LOOKUP_TIMEOUT;
+                else if (L.any_to) o.status = OVS_LOOKUP_RPC_TIMEOUT;
+                else if (LC.hopCountMax && L.hops >= LC.hopCountMax) o.status = OVS_LOOKUP_HOPMAX;
                 else o.status = OVS_LOOKUP_NO_NEXT;
             }
             out[q] = o;
-            if (rpcs_out) rpcs_out[q] = nsent;
+            if (rpcs_out) rpcs_out[q] = L.nsent;
             active = false;
         }
     }
@@ -676,6 +723,11 @@ hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed
         hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
     }
     hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.recs, off, n);
+    if ((e = hipMalloc(&t.sibe, sizeof(KadEntry) * (uint64_t)n * S5)) != hipSuccess) {
+        hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
+    }
+    hipLaunchKernelGGL(k_kad_sibentries, dim3(nblk((uint64_t)n * S5, 256)), dim3(256), 0, st, recs, t.sib,
+                       (uint64_t)n * S5, t.sibe);
     hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.recs, n, k, S5, seed, t.sib, t.slots);
     e = hipStreamSynchronize(st);
     hipFree(rowlen); hipFree(off); hipFree(tmp);
@@ -705,21 +757,35 @@ hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_
 static KadView make_view(const KadTables& t, const double2* xy, uint32_t n)
 {
     KadView V{};
-    V.recs = t.recs; V.xy = xy; V.sib = t.sib; V.slots = t.slots; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
+    V.recs = t.recs; V.xy = xy; V.sib = t.sib; V.sibe = t.sibe; V.slots = t.slots; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
     V.nsib = (int)((uint64_t)(n - 1) < (uint64_t)V.S5 ? n - 1 : (uint32_t)V.S5);
     return V;
 }
 
-template <bool RECORD>
+template <int A, bool RECORD>
 static int kad_blocks_per_cu()
 {
     static int bpc = 0;
     if (bpc == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<RECORD>, 256, 0) != hipSuccess || b < 1) b = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD>, 256, 0) != hipSuccess || b < 1) b = 1;
         bpc = b;
     }
     return bpc;
+}
+
+template <int A, bool RECORD>
+static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
+                             const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
+                             int num_cu, hipStream_t st)
+{
+    const uint64_t waves = (uint64_t)num_cu * kad_blocks_per_cu<A, RECORD>() * 4;
+    uint64_t chunk = (nq + waves - 1) / waves;
+    if (chunk < 1) chunk = 1;
+    const uint64_t need_waves = (nq + chunk - 1) / chunk;
+    hipLaunchKernelGGL((k_kad_route<A, RECORD>), dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, st, V, DC, LC,
+                       qkeys, qsrc, nq, chunk, out, hopseq, rpcs);
+    return hipGetLastError();
 }
 
 hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, uint32_t n, const ovs_params& P,
@@ -729,7 +795,8 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
     (void)recs;
     if (nq == 0) return hipSuccess;
     if (P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > MAXA || P.lookupRedundantNodes < 1 ||
-        P.lookupRedundantNodes > 8 || !P.lookupMerge || P.numSiblings != 1 || t.k > 8)
+        P.lookupRedundantNodes > 8 || !P.lookupMerge || !P.lookupStrictParallelRpcs || P.numSiblings != 1 || t.k > 8 ||
+        P.hopCountMax > 0x7FFF)
         return hipErrorNotSupported;
     KadLC LC{};
     LC.hopCountMax = P.hopCountMax;
@@ -746,15 +813,17 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
     LC.finishOnFirst = P.lookupFinishOnFirstUnchanged;
     LC.maxRedundantLocal = t.k;
     const KadView V = make_view(t, xy, n);
-    const int bpc = hopseq ? kad_blocks_per_cu<true>() : kad_blocks_per_cu<false>();
-    const uint64_t waves = (uint64_t)num_cu * bpc * 4;
-    uint64_t chunk = (nq + waves - 1) / waves;
-    if (chunk < 1) chunk = 1;
-    const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    const dim3 g((unsigned)((need_waves + 3) / 4)), b(256);
-    if (hopseq) hipLaunchKernelGGL(k_kad_route<true>, g, b, 0, st, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq, rpcs);
-    else hipLaunchKernelGGL(k_kad_route<false>, g, b, 0, st, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq, rpcs);
-    return hipGetLastError();
+    // strictParallelRpcs: never more than alpha FindNodeCalls in flight (IterativeLookup.cc:1078-1079)
+    const int A = P.lookupParallelRpcs;
+#define KL(a) (hopseq ? kad_launch<a, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st) \
+                      : kad_launch<a, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st))
+    switch (A) {
+    case 1: return KL(1);
+    case 2: return KL(2);
+    case 3: return KL(3);
+    default: return KL(4);
+    }
+#undef KL
 }
 
 hipError_t kad_find_node(const KadTables& t, const KeyRec* recs, uint32_t n, const ovs_params& P, const uint32_t* node,

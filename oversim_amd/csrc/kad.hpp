@@ -30,6 +30,7 @@ struct KadEntry {
 struct KadTables {
     KadRec* recs = nullptr;
     uint32_t* sib = nullptr;      // n * S5 member indices (unordered set), NONE padded
+    KadEntry* sibe = nullptr;     // n * S5 sibling entries with the member key inline
     KadEntry* slots = nullptr;    // total_slots * k
     uint64_t total_slots = 0;
     int k = 8, s = 8;
@@ -40,6 +41,7 @@ struct KadView {
     const KadRec* __restrict__ recs;
     const double2* __restrict__ xy;
     const uint32_t* __restrict__ sib;
+    const KadEntry* __restrict__ sibe;
     const KadEntry* __restrict__ slots;
     uint32_t n;
     int k;

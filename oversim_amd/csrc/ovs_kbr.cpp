@@ -15,6 +15,7 @@
 
 #include "kad.hpp"
 #include "launch.hpp"
+#include "stats.hpp"
 
 using namespace ovs;
 
@@ -610,6 +611,106 @@ ovs_status ovs_delay_batch(ovs_ctx* c, const uint32_t* a, const uint32_t* b, con
         HIPCHK(c, hipMemcpyAsync(out_ns, dout, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         hipFree(da); hipFree(db); hipFree(dbytes); hipFree(dout);
+    }
+    return OVS_OK;
+}
+
+ovs_status ovs_kbrtest_stats_batch(ovs_ctx* c, const ovs_route_out* out, const ovs_key160* keys, const uint32_t* src,
+                                   uint64_t n, double measured_time_s, int32_t lookup_node_ids,
+                                   ovs_kbrtest_stats* stats, uint32_t flags, void* stream)
+{
+    if (!c || !stats || (n && (!out || !src || (lookup_node_ids && !keys)))) return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (!(measured_time_s >= 0)) return fail(c, OVS_EINVAL, "measured_time_s must be >= 0");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;   // NULL = the default stream
+    const ovs_route_out* dout = out;
+    const K160* dk = reinterpret_cast<const K160*>(keys);
+    const uint32_t* ds = src;
+    std::vector<void*> owned;
+    auto cleanup = [&]() { for (void* p : owned) hipFree(p); };
+    if (!dev && n) {
+        ovs_route_out* o; K160* k = nullptr; uint32_t* r; bool ow;
+        ovs_status st = to_device(c, out, n, false, &o, &ow);
+        if (st != OVS_OK) return st;
+        owned.push_back(o);
+        st = to_device(c, src, n, false, &r, &ow);
+        if (st != OVS_OK) { cleanup(); return st; }
+        owned.push_back(r);
+        if (lookup_node_ids) {
+            st = to_device(c, reinterpret_cast<const K160*>(keys), n, false, &k, &ow);
+            if (st != OVS_OK) { cleanup(); return st; }
+            owned.push_back(k);
+        }
+        dout = o; dk = k; ds = r;
+    }
+    StatsDev* S = nullptr; uint32_t* counts = nullptr; double* partial = nullptr; double* result = nullptr;
+    if (hipMalloc(&S, sizeof(StatsDev)) != hipSuccess ||
+        hipMalloc(&counts, sizeof(uint32_t) * 3 * c->n) != hipSuccess ||
+        hipMalloc(&partial, sizeof(double) * STATS_NODE_BLOCKS * NSTAT * 5) != hipSuccess ||
+        hipMalloc(&result, sizeof(double) * NSTAT * 5) != hipSuccess) {
+        owned.push_back(S); owned.push_back(counts); owned.push_back(partial); owned.push_back(result);
+        cleanup();
+        return fail(c, OVS_ENOMEM, "statistics scratch allocation failed");
+    }
+    owned.push_back(S); owned.push_back(counts); owned.push_back(partial); owned.push_back(result);
+    // GlobalStatistics::MIN_MEASURED = 0.1 s (GlobalStatistics.cc:32, KBRTestApp.cc:502)
+    const int rates = measured_time_s >= 0.1;
+    hipError_t e = launch_stats(dout, dk, ds, c->recs, n, (uint32_t)c->n, lookup_node_ids,
+                                measured_time_s, (uint64_t)c->P.testMsgSize, rates, S, counts,
+                                partial, result, c->num_cu, s);
+    StatsDev h{};
+    double r[NSTAT * 5];
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, S, sizeof h, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(r, result, sizeof r, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    cleanup();
+    if (e != hipSuccess) return hip_fail(c, e, "statistics kernels");
+
+    ovs_kbrtest_stats& o = *stats;
+    std::memset(&o, 0, sizeof o);
+    const uint64_t B = (uint64_t)c->P.testMsgSize;
+    o.num_sent = n;
+    o.num_delivered = h.delivered;
+    o.num_dropped = h.dropped;
+    o.num_lookup_failed = h.failed;
+    o.bytes_sent = n * B;
+    o.bytes_delivered = h.delivered * B;
+    o.bytes_dropped = h.dropped * B;
+    o.hop_count_sum = h.hop_sum;
+    o.latency_sum_ns = (int64_t)h.lat_sum;
+    if (h.delivered) {
+        o.hop_count_min = (uint32_t)h.hop_min;
+        o.hop_count_max = (uint32_t)h.hop_max;
+        o.latency_min_ns = (int64_t)h.lat_min;
+        o.latency_max_ns = (int64_t)h.lat_max;
+        // GlobalStatistics::finalizeStatistics: OutVector value / count (GlobalStatistics.cc:134-139);
+        // latency values are SIMTIME_DBL(latency), summed here exactly in ns
+        o.hop_count_mean = (double)h.hop_sum / (double)h.delivered;
+        o.latency_mean_s = ((double)h.lat_sum / (double)h.delivered) * 1e-9;
+    }
+    for (int i = 0; i < 8; ++i) o.status_count[i] = h.status[i];
+    for (int i = 0; i < 64; ++i) o.hop_hist[i] = h.hist[i];
+    ovs_stddev* sd[NSTAT] = {&o.delivered_msgs_per_s, &o.delivered_bytes_per_s, &o.dropped_msgs_per_s,
+                             &o.dropped_bytes_per_s, &o.delivery_ratio};
+    for (int k = 0; k < NSTAT; ++k) {
+        const double sum = r[k * 5 + 0], sq = r[k * 5 + 1];
+        uint64_t cnt;
+        std::memcpy(&cnt, &r[k * 5 + 4], sizeof cnt);
+        ovs_stddev& d = *sd[k];
+        d.count = cnt;
+        if (!cnt) continue;
+        // cStdDev::getMean / getVariance (OMNeT++ 4.x): sample variance, 0 below two values or if negative
+        d.mean = sum / (double)cnt;
+        double var = 0.0;
+        if (cnt > 1) {
+            var = (sq - sum * sum / (double)cnt) / (double)(cnt - 1);
+            if (var < 0) var = 0;
+        }
+        d.stddev = std::sqrt(var);
+        d.min = r[k * 5 + 2];
+        d.max = r[k * 5 + 3];
     }
     return OVS_OK;
 }

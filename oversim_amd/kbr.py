@@ -100,6 +100,37 @@ ROUTE_OUT_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", 
                             ("one_way_hops", "u1"), ("latency_ns", "<i8")])
 assert ROUTE_OUT_DTYPE.itemsize == 16
 
+class StdDev(C.Structure):
+    """ovs_stddev: one cStdDev summary (GlobalStatistics::addStdDev)."""
+
+    _fields_ = [("count", C.c_uint64), ("mean", C.c_double), ("stddev", C.c_double),
+                ("min", C.c_double), ("max", C.c_double)]
+
+
+class KbrTestStats(C.Structure):
+    """ovs_kbrtest_stats: KBRTestApp one-way statistics of a batch (KBRTestApp.cc:380-520)."""
+
+    _fields_ = [
+        ("num_sent", C.c_uint64), ("num_delivered", C.c_uint64), ("num_dropped", C.c_uint64),
+        ("num_lookup_failed", C.c_uint64), ("bytes_sent", C.c_uint64), ("bytes_delivered", C.c_uint64),
+        ("bytes_dropped", C.c_uint64), ("hop_count_sum", C.c_uint64), ("latency_sum_ns", C.c_int64),
+        ("hop_count_min", C.c_uint32), ("hop_count_max", C.c_uint32),
+        ("latency_min_ns", C.c_int64), ("latency_max_ns", C.c_int64),
+        ("hop_count_mean", C.c_double), ("latency_mean_s", C.c_double),
+        ("status_count", C.c_uint64 * 8), ("hop_hist", C.c_uint64 * 64),
+        ("delivered_msgs_per_s", StdDev), ("delivered_bytes_per_s", StdDev),
+        ("dropped_msgs_per_s", StdDev), ("dropped_bytes_per_s", StdDev), ("delivery_ratio", StdDev),
+    ]
+
+    STDDEV_NAMES = {
+        "delivered_msgs_per_s": "KBRTestApp: One-way Delivered Messages/s",
+        "delivered_bytes_per_s": "KBRTestApp: One-way Delivered Bytes/s",
+        "dropped_msgs_per_s": "KBRTestApp: One-way Dropped Messages/s",
+        "dropped_bytes_per_s": "KBRTestApp: One-way Dropped Bytes/s",
+        "delivery_ratio": "KBRTestApp: One-way Delivery Ratio",
+    }
+
+
 _lib = None
 
 
@@ -131,6 +162,7 @@ def lib() -> C.CDLL:
         "ovs_find_node_batch": ([vp, vp, vp, u64, i32, i32, vp, u32, vp, vp, u32, vp], C.c_int),
         "ovs_delay_batch": ([vp, vp, vp, vp, u64, vp, u32, vp], C.c_int),
         "ovs_sync": ([vp], C.c_int),
+        "ovs_kbrtest_stats_batch": ([vp, vp, vp, vp, u64, C.c_double, i32, vp, u32, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -314,6 +346,37 @@ class KbrEngine:
 
     def sync(self):
         self._chk(self._L.ovs_sync(self._h), "ovs_sync")
+
+    # -- KBRTestApp statistics
+    def kbrtest_stats(self, result: dict | np.ndarray, keys, src, measured_time_s: float,
+                      lookupNodeIds: bool = True) -> KbrTestStats:
+        """Reduce lookup() results to the KBRTestApp one-way statistics on the device."""
+        if isinstance(result, dict):
+            out = np.empty(len(result["responsible"]), dtype=ROUTE_OUT_DTYPE)
+            for f in ROUTE_OUT_DTYPE.names:
+                out[f] = result[f]
+        else:
+            out = np.ascontiguousarray(result, dtype=ROUTE_OUT_DTYPE)
+        keys = keys_array(keys)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        if not (len(out) == len(keys) == len(src)):
+            raise ValueError("result, keys and src differ in length")
+        st = KbrTestStats()
+        self._chk(self._L.ovs_kbrtest_stats_batch(self._h, _ptr(out), _ptr(keys), _ptr(src), len(out),
+                                                  float(measured_time_s), int(bool(lookupNodeIds)), C.byref(st),
+                                                  0, None), "ovs_kbrtest_stats_batch")
+        return st
+
+    def kbrtest_stats_device(self, out_ptr: int, keys_ptr: int, src_ptr: int, n: int, measured_time_s: float,
+                             lookupNodeIds: bool = True, stream: int | None = None) -> KbrTestStats:
+        """Same as kbrtest_stats for a device-resident batch (synchronises `stream`)."""
+        st = KbrTestStats()
+        self._chk(self._L.ovs_kbrtest_stats_batch(self._h, C.c_void_p(out_ptr), C.c_void_p(keys_ptr),
+                                                  C.c_void_p(src_ptr), n, float(measured_time_s),
+                                                  int(bool(lookupNodeIds)), C.byref(st), DEVICE_PTRS,
+                                                  C.c_void_p(stream) if stream else None),
+                  "ovs_kbrtest_stats_batch")
+        return st
 
 
 @dataclass

@@ -72,12 +72,28 @@ def lib() -> C.CDLL:
             ("orc_delay_ns", [vp, u32, u32, i32], C.c_int64),
             ("orc_coord_dist", [vp, u32, u32], C.c_float),
             ("orc_last_error", [], C.c_char_p),
+            ("orc_kbrtest_stats", [vp, vp, vp, vp, u64, C.c_double, C.c_int, i32, vp], None),
         ]:
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
         _L = L
     return _L
+
+
+class OrcStdDev(C.Structure):
+    _fields_ = [("count", C.c_uint64), ("mean", C.c_double), ("stddev", C.c_double),
+                ("min", C.c_double), ("max", C.c_double)]
+
+
+class OrcKbrTestResult(C.Structure):
+    _fields_ = [("num_sent", C.c_uint64), ("num_delivered", C.c_uint64), ("num_dropped", C.c_uint64),
+                ("num_lookup_failed", C.c_uint64), ("hop_count_sum", C.c_uint64), ("latency_sum_ns", C.c_int64),
+                ("hop_count_mean", C.c_double), ("latency_mean_s", C.c_double), ("sd", OrcStdDev * 5)]
+
+
+SD_FIELDS = ("delivered_msgs_per_s", "delivered_bytes_per_s", "dropped_msgs_per_s", "dropped_bytes_per_s",
+             "delivery_ratio")
 
 
 def _p(a):
@@ -143,6 +159,22 @@ class OracleNet:
         if rpcs is not None:
             res["rpcs"] = rpcs
         return res
+
+    def kbrtest_stats(self, result: dict, keys, src, measured_time_s: float, lookupNodeIds: bool = True,
+                      testMsgSize: int = 100) -> dict:
+        out = np.empty(len(result["responsible"]), dtype=ROUTE_DTYPE)
+        for f in ROUTE_DTYPE.names:
+            out[f] = result[f]
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        st = OrcKbrTestResult()
+        lib().orc_kbrtest_stats(self._h, _p(out), _p(keys), _p(src), len(out), float(measured_time_s),
+                                int(bool(lookupNodeIds)), int(testMsgSize), C.byref(st))
+        d = {f: getattr(st, f) for f, _ in OrcKbrTestResult._fields_ if f != "sd"}
+        for i, name in enumerate(SD_FIELDS):
+            s = st.sd[i]
+            d[name] = {"count": s.count, "mean": s.mean, "stddev": s.stddev, "min": s.min, "max": s.max}
+        return d
 
     def find_node(self, node: int, key, numRedundantNodes: int, numSiblings: int):
         key = np.ascontiguousarray(key, dtype=np.uint32)
