@@ -93,12 +93,13 @@ typedef struct ovs_params {
     int32_t lookupFinishOnFirstUnchanged;
     int32_t lookupVerifySiblings;       /* false only */
     int32_t lookupMajoritySiblings;     /* false only */
-    int32_t routingType;                /* 0 = "iterative" (only) */
+    int32_t routingType;                /* **.routingType: 0 = "iterative", 1 = "semi-recursive",
+                                           2 = "full-recursive" (recursive: Chord stable rings) */
     int32_t numSiblings;                /* sendToKey numSiblings (1 for KBRTestApp one-way) */
     int32_t useCoordinateBasedDelay;    /* **.udp.useCoordinateBasedDelay = true */
     int32_t simtimeRound;               /* SimTime(double): 1 = round half up, 0 = truncate */
     int32_t testMsgSize;                /* **.kbrTestApp.testMsgSize = 100 B */
-    int32_t _pad0;
+    int32_t recNumRedundantNodes;       /* **.recNumRedundantNodes = 3 (default.ini:386) */
     double  rpcUdpTimeout;              /* **.rpcUdpTimeout = 1.5 s */
     double  lookupTimeout;              /* LOOKUP_TIMEOUT = 10 s (IterativeLookup.h:44) */
     double  jitter;                     /* **.udp.jitter (must be 0 for bit-exact latency) */

@@ -222,6 +222,8 @@ static void params_common(orc_params* p)
     p->respPerNodeBytes = 26;    /* NODEHANDLE_L = 208 bits */
     p->routeBytes = 158 + 28;    /* BASEROUTE_L 424 + BASEAPPDATA_L 40 + testMsgSize 100 B */
     p->kadSeed = 0x4b41444dull;
+    p->routingType = 0;          /* default.ini:392 "iterative" */
+    p->recNumRedundantNodes = 3; /* default.ini:386 */
 }
 void orc_params_chord_default(orc_params* p) { params_common(p); }
 void orc_params_kad_default(orc_params* p)
@@ -1139,6 +1141,65 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
     free(L);
 }
 
+/* ===================================================================== */
+/* 7. Recursive routing of a one-way route message (SEMI_RECURSIVE and   */
+/*    FULL_RECURSIVE behave identically for a one-way KBRTestMessage:    */
+/*    they differ only in how RPC responses travel back).                */
+/*    recordRoute = false, routeMsgAcks = false (default.ini:398, 434).  */
+/* ===================================================================== */
+static void run_recursive(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out, uint32_t* hopseq)
+{
+    const orc_params* p = &net->p;
+    uint32_t cur = S, lastHop = S;      /* routeCtrlInfo->setLastHop(thisNode) at the source (BaseOverlay.cc:1400) */
+    int hopCount = 0;
+    int64_t t = 0;
+    out->responsible = NONE; out->hops = 0; out->one_way_hops = 0; out->latency_ns = -1;
+    for (;;) {
+        int err = 0;
+        if (cur != S) {
+            /* handleBaseOverlayMessage, OVERLAYROUTE (BaseOverlay.cc:907-914): deliver when sibling */
+            if (ov_isSiblingFor(net, cur, cur, key, 1, &err)) break;
+        }
+        /* sendToKey, recursive branch (BaseOverlay.cc:1445-1582) */
+        NVec nextHops;
+        if (ov_findNode(net, cur, key, p->recNumRedundantNodes, p->numSiblings, &nextHops) < 0) {
+            out->status = 5;            /* Chord throws: successor list broken (Chord.cc:615-620) */
+            return;
+        }
+        if (nextHops.size == 0) { out->status = 4; return; }           /* 1449-1461: dropped */
+        if (hopCount >= p->hopCountMax) { out->status = 3; return; }   /* 1464-1488: dropped */
+        const int isSibling = ov_isSiblingFor(net, cur, cur, key, p->numSiblings, &err);
+        uint32_t next = NONE;
+        for (int i = 0; next == NONE && i < nextHops.size; ++i) {      /* 1502-1516 loop detection */
+            const uint32_t h = nextHops.v[i];
+            if ((h == lastHop && h != cur) ||                          /* back to the last hop */
+                (h == S && cur != S) ||                                /* never to the source */
+                (h == cur && !isSibling))                              /* self without being sibling */
+                continue;
+            next = h;
+        }
+        if (next == NONE) { out->status = 4; return; }                 /* 1518-1538: no useful next hop */
+        if (next == cur) {                                             /* 1555-1570: this node is responsible */
+            if (isSibling && !err) break;
+            out->status = 5;
+            return;
+        }
+        /* sendRouteMessage (1107-1146): hopCount + 1, one UDP message from cur */
+        int64_t tx = 0;
+        t += calc_delay(net, cur, next, p->routeBytes, t, &tx);
+        if (hopseq && hopCount < p->hopCountMax) hopseq[hopCount] = next;
+        ++hopCount;
+        lastHop = cur;
+        cur = next;
+    }
+    /* KBRTestApp::deliver -> evaluateData(simTime() - creationTime, hopCount) (KBRTestApp.cc:404-410) */
+    out->status = 0;
+    out->responsible = cur;
+    out->hops = (uint16_t)hopCount;
+    out->one_way_hops = (uint8_t)hopCount;
+    out->latency_ns = t;
+}
+
 uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
                          orc_route_out* out, uint32_t* hop_seq, uint32_t* rpcs_out, int nthreads)
 {
@@ -1151,8 +1212,13 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
 #endif
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         OKey k = ok_from(&keys[i]);
-        run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
-                   rpcs_out ? &rpcs_out[i] : NULL);
+        if (net->p.routingType == 0)
+            run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
+                       rpcs_out ? &rpcs_out[i] : NULL);
+        else {
+            run_recursive(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL);
+            if (rpcs_out) rpcs_out[i] = 0;     /* no FindNodeCalls in recursive routing */
+        }
         total += out[i].hops;
     }
     (void)nthreads;

@@ -68,6 +68,8 @@ typedef struct {
     int32_t respPerNodeBytes;         /* + 26 B per NodeHandle */
     int32_t routeBytes;               /* one-way KBRTestMessage route msg = 186 */
     uint64_t kadSeed;                 /* Kademlia snapshot bucket-sampling seed */
+    int32_t routingType;              /* 0 iterative, 1 semi-recursive, 2 full-recursive (default.ini:392) */
+    int32_t recNumRedundantNodes;     /* default.ini:386 = 3 */
 } orc_params;
 
 void orc_params_chord_default(orc_params* p);

@@ -226,7 +226,7 @@ __device__ __forceinline__ Decision decide_general(const ChordView& V, uint32_t 
 // ---------------------------------------------------------------------------
 // K1: batched one-way lookups
 
-template <bool IDEAL, bool RECORD>
+template <bool IDEAL, bool RECORD, bool REC>
 __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC, LookupConsts LC,
                                                      const K160* __restrict__ qkeys,
                                                      const uint32_t* __restrict__ qsrc, uint64_t nq,
@@ -274,6 +274,41 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
 
         uint8_t status = 0xFF;   // 0xFF = still running
         uint32_t R = NONE;
+        if (REC) {
+            // Recursive one-way route message (BaseOverlay::sendToKey recursive branch,
+            // BaseOverlay.cc:1445-1582; receipt 907-914).  (sx, sy) = the last sender.
+            const bool at_src = local;
+            if (!local) t += DC.msgRoute + coord_ns(sx, sy, cxy.x, cxy.y, DC.round);   // sendRouteMessage
+            local = false;
+            sx = cxy.x; sy = cxy.y;
+            // a forwarded message is delivered on receipt (907-914); at the source sendToKey's
+            // hop-count check precedes the delivery to itself (1464 before 1555)
+            if (d.sib && (!at_src || hops < LC.hopCountMax)) { status = OVS_LOOKUP_OK; R = cur; }
+            else if (d.sib) status = OVS_LOOKUP_HOPMAX;
+            else if (d.broken) status = OVS_LOOKUP_BROKEN;
+            else if (hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;               // 1464-1488
+            else if (d.next == S || d.next == cur) {
+                // loop detection (1502-1516) rejects findNode's first candidate: on a converged
+                // ring this cannot happen (every hop moves strictly towards the key), and the
+                // recursive path is only enabled for converged rings
+                status = OVS_LOOKUP_NO_NEXT;
+            } else {
+                if (RECORD && hops < LC.hopCountMax) hopseq[q * (uint64_t)LC.hopCountMax + hops] = d.next;
+                ++hops;
+                cur = d.next; crec = d.rec;
+            }
+            if (status != 0xFF) {
+                ovs_route_out o;
+                o.hops = (uint16_t)(status == OVS_LOOKUP_OK ? hops : 0);
+                o.status = status;
+                o.responsible = R;
+                o.one_way_hops = (uint8_t)(status == OVS_LOOKUP_OK ? hops : 0);
+                o.latency_ns = status == OVS_LOOKUP_OK ? t : -1;
+                out[q] = o;
+                active = false;
+            }
+            continue;
+        }
         if (local) {
             // IterativeLookup::start (IterativeLookup.cc:157-204): local step, no hop, no delay
             local = false;
@@ -619,17 +654,34 @@ hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint
     return hipGetLastError();
 }
 
-template <bool IDEAL, bool RECORD>
+template <bool IDEAL, bool RECORD, bool REC>
 static int route_blocks_per_cu()
 {
     static int bpc = 0;
     if (bpc == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_route<IDEAL, RECORD>, 256, 0) != hipSuccess || b < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_route<IDEAL, RECORD, REC>, 256, 0) != hipSuccess ||
+            b < 1)
             b = 1;
         bpc = b;
     }
     return bpc;
+}
+
+template <bool IDEAL, bool RECORD, bool REC>
+static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
+                                     const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
+                                     uint32_t* hopseq, int num_cu, hipStream_t s)
+{
+    // persistent grid: every resident wave owns one contiguous slice of the batch
+    const uint64_t waves = (uint64_t)num_cu * route_blocks_per_cu<IDEAL, RECORD, REC>() * 4;   // 4 waves per block
+    uint64_t chunk = (nq + waves - 1) / waves;
+    if (chunk < 1) chunk = 1;
+    const uint64_t need_waves = (nq + chunk - 1) / chunk;
+    const uint64_t blocks = (need_waves + 3) / 4;
+    hipLaunchKernelGGL((k_chord_route<IDEAL, RECORD, REC>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC, qkeys,
+                       qsrc, nq, chunk, out, hopseq);
+    return hipGetLastError();
 }
 
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
@@ -637,22 +689,14 @@ hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts&
                               uint32_t* hopseq, int num_cu, hipStream_t s)
 {
     if (nq == 0) return hipSuccess;
-    // persistent grid: every resident wave owns one contiguous slice of the batch
-    const int bpc = ideal ? (hopseq ? route_blocks_per_cu<true, true>() : route_blocks_per_cu<true, false>())
-                          : route_blocks_per_cu<false, true>();
-    const uint64_t waves = (uint64_t)num_cu * bpc * 4;   // 256 threads = 4 waves per block
-    uint64_t chunk = (nq + waves - 1) / waves;
-    if (chunk < 1) chunk = 1;
-    const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    const uint64_t blocks = (need_waves + 3) / 4;
-    const dim3 g((unsigned)blocks), b(256);
-    if (ideal) {
-        if (hopseq) hipLaunchKernelGGL((k_chord_route<true, true>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);
-        else hipLaunchKernelGGL((k_chord_route<true, false>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);
-    } else {
-        hipLaunchKernelGGL((k_chord_route<false, true>), g, b, 0, s, V, DC, LC, qkeys, qsrc, nq, chunk, out, hopseq);
+    if (LC.recursive) {
+        if (!ideal) return hipErrorNotSupported;
+        return hopseq ? chord_route_launch<true, true, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s)
+                      : chord_route_launch<true, false, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s);
     }
-    return hipGetLastError();
+    if (!ideal) return chord_route_launch<false, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s);
+    return hopseq ? chord_route_launch<true, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s)
+                  : chord_route_launch<true, false, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s);
 }
 
 hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,

@@ -96,6 +96,7 @@ struct LookupConsts {
     int32_t hopCountMax;
     int32_t numSiblings;
     int32_t numRedundantNodes;
+    int32_t recursive;          // routingType semi-/full-recursive: hop-by-hop route message
 };
 
 }  // namespace ovs

@@ -273,10 +273,28 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
     want_bool("lookupFinishOnFirstUnchanged", &p->lookupFinishOnFirstUnchanged);
     want_bool("lookupVerifySiblings", &p->lookupVerifySiblings);
     want_bool("lookupMajoritySiblings", &p->lookupMajoritySiblings);
+    want_int("recNumRedundantNodes", &p->recNumRedundantNodes);
+    // route-message options that change the recursive message format: only their defaults
+    for (const char* opt : {"recordRoute", "routeMsgAcks"}) {
+        int32_t on = 0;
+        if (lookup(ovp + opt, &v)) {
+            if (!to_bool(unquote(v), &on)) bad = opt;
+            else if (on) {
+                set_err(std::string(opt) + " = true not supported (default.ini:398,434 set false)");
+                return OVS_ENOTSUP;
+            }
+        }
+    }
     if (lookup(ovp + "routingType", &v)) {
         const std::string rt = unquote(v);
+        // BaseOverlay::initialize routingType names (BaseOverlay.cc:119-131)
         if (rt == "iterative") p->routingType = 0;
-        else { set_err("routingType \"" + rt + "\" not supported (iterative only)"); return OVS_ENOTSUP; }
+        else if (rt == "semi-recursive") p->routingType = 1;
+        else if (rt == "full-recursive") p->routingType = 2;
+        else {
+            set_err("routingType \"" + rt + "\" not supported (iterative, semi-recursive, full-recursive)");
+            return OVS_ENOTSUP;
+        }
     }
     if (lookup(ovp + "rpcUdpTimeout", &v) && !to_seconds(unquote(v), &p->rpcUdpTimeout)) bad = "rpcUdpTimeout";
     const std::string udp = host + ".udp.";

@@ -120,7 +120,10 @@ DelayConsts delay_consts(const ovs_params& P)
 ovs_status check_common(ovs_ctx* c, const ovs_params& P)
 {
     if (P.keyLength != 160) return fail(c, OVS_ENOTSUP, "keyLength != 160 not supported");
-    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "only routingType = \"iterative\" is implemented");
+    if (P.routingType < 0 || P.routingType > 2)
+        return fail(c, OVS_ENOTSUP, "routingType must be iterative, semi-recursive or full-recursive");
+    if (P.routingType != 0 && P.recNumRedundantNodes < 1)
+        return fail(c, OVS_EINVAL, "recNumRedundantNodes must be >= 1");
     if (P.lookupParallelPaths != 1) return fail(c, OVS_ENOTSUP, "lookupParallelPaths != 1 not supported");
     if (P.lookupVerifySiblings || P.lookupMajoritySiblings)
         return fail(c, OVS_ENOTSUP, "lookupVerifySiblings/lookupMajoritySiblings not supported");
@@ -137,6 +140,13 @@ ovs_status check_chord_route(ovs_ctx* c, const ovs_params& P)
 {
     if (P.lookupMerge) return fail(c, OVS_EINVAL, "Chord doesn't work with iterativeLookupConfig.merge = true!");
     if (P.extendedFingerTable) return fail(c, OVS_ENOTSUP, "extendedFingerTable = true not supported");
+    if (P.routingType != 0) {
+        // recursive: the route message follows findNode's first acceptable candidate hop by hop
+        if (P.numSiblings != 1) return fail(c, OVS_ENOTSUP, "recursive Chord routing implements numSiblings=1");
+        if (!c->ideal)
+            return fail(c, OVS_ENOTSUP, "recursive routing is implemented for converged (ovs_chord_load) rings");
+        return OVS_OK;
+    }
     if (P.lookupRedundantNodes != 1 || P.lookupParallelRpcs != 1 || P.numSiblings != 1)
         return fail(c, OVS_ENOTSUP,
                     "Chord route kernel implements lookupRedundantNodes=1, lookupParallelRpcs=1, numSiblings=1");
@@ -216,6 +226,7 @@ void ovs_params_default(int32_t overlay, ovs_params* p)
     p->useCoordinateBasedDelay = 1;     // default.ini:546
     p->simtimeRound = 1;
     p->testMsgSize = 100;               // default.ini:37
+    p->recNumRedundantNodes = 3;        // default.ini:386
     p->rpcUdpTimeout = 1.5;             // default.ini:483
     p->lookupTimeout = 10.0;            // IterativeLookup.h:44
     p->jitter = 0.0;                    // default.ini:549 has 0.1; bit-exact latency needs 0
@@ -362,7 +373,7 @@ ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, o
     hipStream_t s = (hipStream_t)stream;   // device-pointer call: NULL = the default stream
     if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
     HIPCHK(c, hipMemcpyAsync(c->d_bounds, M.lo, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice, s));
-    LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes};
+    LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes, c->P.routingType != 0};
     HIPCHK(c, launch_chord_shard_step(chord_view(c), delay_consts(c->P), LC, c->d_bounds, (int)nshards, me, in, n_in, out,
                                       out_dest, out_cap, out_count, done, done_cap, done_count, c->num_cu, s));
     return OVS_OK;
@@ -480,6 +491,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         if (st != OVS_OK) return st;
         if (c->ideal && (c->shard_lo != 0 || c->shard_hi != c->n))
             return fail(c, OVS_ESTATE, "context holds one arc of a sharded ring: use ovs_shard_step");
+    } else if (c->P.routingType != 0) {
+        return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
     }
     if (n == 0) return OVS_OK;
     // stage inputs
@@ -512,12 +525,15 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     }
     hipError_t e;
     if (c->overlay == OVS_OVERLAY_CHORD) {
-        LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes};
+        LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes, c->P.routingType != 0};
         if (drpc) {
             // Chord with alpha = 1: one FindNodeCall per hop; filled after the route below
         }
         e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, dk, ds, n, dout, dhop, c->num_cu, s);
-        if (e == hipSuccess && drpc) e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
+        if (e == hipSuccess && drpc) {
+            if (LC.recursive) e = hipMemsetAsync(drpc, 0, sizeof(uint32_t) * n, s);   // no FindNodeCalls
+            else e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
+        }
     } else {
         e = kad_route(c->kad, c->recs, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
                       c->num_cu, s);

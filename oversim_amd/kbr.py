@@ -55,7 +55,7 @@ class Params(C.Structure):
         ("lookupFinishOnFirstUnchanged", C.c_int32), ("lookupVerifySiblings", C.c_int32),
         ("lookupMajoritySiblings", C.c_int32), ("routingType", C.c_int32), ("numSiblings", C.c_int32),
         ("useCoordinateBasedDelay", C.c_int32), ("simtimeRound", C.c_int32), ("testMsgSize", C.c_int32),
-        ("_pad0", C.c_int32), ("rpcUdpTimeout", C.c_double), ("lookupTimeout", C.c_double),
+        ("recNumRedundantNodes", C.c_int32), ("rpcUdpTimeout", C.c_double), ("lookupTimeout", C.c_double),
         ("jitter", C.c_double), ("constantDelay", C.c_double), ("datarate", C.c_double),
         ("accessDelay", C.c_double), ("kadSeed", C.c_uint64),
     ]

@@ -51,6 +51,30 @@ def chord_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: int):
     print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
 
 
+def chord_rec_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: int, hcm: int = 50):
+    """Semi-recursive routing (routingType = semi-recursive, ChordLarge), checked against
+    refmodel.ChordRing.lookup_recursive before writing."""
+    net = W.population(n, seed)
+    k1, s1 = W.lookups(net.ids, m_ids, seed + 1, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m_rand, seed + 2, node_ids=False)
+    keys = np.concatenate([k1, k2])
+    src = np.concatenate([s1, s2])
+    o = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd, routingType=1, hopCountMax=hcm))
+    r = o.route(keys, src, record_hops=True)
+    ring = refmodel.ChordRing(net.ids, net.xy, rnd=bool(rnd))
+    for i in range(len(keys)):
+        m = ring.lookup_recursive(keys[i], int(src[i]), hop_max=hcm)
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+            assert int(r[f][i]) == int(m[f]), (name, i, f, r[f][i], m[f])
+    H = int(r["hops"].max()) + 1
+    np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=keys, src=src,
+                        responsible=r["responsible"], hops=r["hops"], status=r["status"],
+                        one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"],
+                        hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed),
+                        routing_type=np.int32(1), hop_count_max=np.int32(hcm))
+    print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
+
+
 def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
     net = W.population(n, seed)
     k1, s1 = W.lookups(net.ids, m, seed + 1, node_ids=True)
@@ -84,6 +108,10 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
 
 
 if __name__ == "__main__":
+    if "--rec" in sys.argv:
+        chord_rec_case("chord_n1000_semirec", 1000, 0x4213, 2048, 2048, 1)
+        chord_rec_case("chord_n1000_semirec_hcm4", 1000, 0x4214, 512, 512, 0, hcm=4)
+        sys.exit(0)
     chord_case("chord_n1000_round", 1000, 0x4213, 4096, 4096, 1)
     chord_case("chord_n1000_trunc", 1000, 0x4213, 2048, 2048, 0)
     chord_case("chord_n9", 9, 5, 256, 256, 1)

@@ -28,6 +28,7 @@ class OrcParams(C.Structure):
         ("rpcUdpTimeout", C.c_double), ("lookupTimeout", C.c_double), ("datarate", C.c_double),
         ("accessDelay", C.c_double), ("callBytes", C.c_int32), ("respBaseBytes", C.c_int32),
         ("respPerNodeBytes", C.c_int32), ("routeBytes", C.c_int32), ("kadSeed", C.c_uint64),
+        ("routingType", C.c_int32), ("recNumRedundantNodes", C.c_int32),
     ]
 
     def replace(self, **kw) -> "OrcParams":

@@ -152,6 +152,22 @@ class ChordRing:
                 return dict(responsible=0xFFFFFFFF, hops=hops, status=4, one_way_hops=0, latency_ns=-1, hop_seq=seq)
             cur = nxt
 
+    def lookup_recursive(self, kw, S, hop_max=50, route=186):
+        """Semi-recursive one-way route message: greedy forwarding S -> ... -> responsible,
+        one UDP message of `route` bytes per hop (BaseOverlay.cc:1445-1582, 907-914)."""
+        k = to_int(kw)
+        cur, t, hops, seq = S, 0, 0, []
+        while True:
+            sib, nxt = self.decide(cur, k)
+            if sib:
+                return dict(responsible=cur, hops=hops, status=0, one_way_hops=hops, latency_ns=t, hop_seq=seq)
+            if hops >= hop_max:
+                return dict(responsible=0xFFFFFFFF, hops=0, status=3, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+            t += msg_ns(route, self.rnd) + coord_ns(self.xy, cur, nxt, self.rnd)
+            hops += 1
+            seq.append(nxt)
+            cur = nxt
+
 
 # --- Kademlia findNode (Kademlia.cc:357-382, 888-962, 1101-1246) on exported tables --
 class KadTables:

@@ -83,11 +83,35 @@ def test_params_ini_errors():
     with pytest.raises(KbrError):
         Params.from_ini("[General]\n**.overlay*.*.hopCountMax = ${10, 20}\n")
     with pytest.raises(KbrError):
-        Params.from_ini("[General]\n**.overlay*.chord.routingType = \"semi-recursive\"\n")
+        Params.from_ini("[General]\n**.overlay*.chord.routingType = \"source-routing-recursive\"\n")
+    with pytest.raises(KbrError):
+        Params.from_ini("[General]\n**.overlay*.*.recordRoute = true\n")
+    with pytest.raises(KbrError):
+        Params.from_ini("[General]\n**.overlay*.*.routeMsgAcks = true\n")
     with pytest.raises(KbrError):
         Params.from_ini("[General]\n", "NoSuchConfig")
     with pytest.raises(KbrError):
         Params.from_ini("[General]\n**.rpcUdpTimeout = fast\n")
+
+
+def test_params_chordlarge_semi_recursive():
+    """[Config ChordLarge] (omnetpp.ini:75-85) overrides default.ini's iterative Chord routing."""
+    from oversim_amd import Params
+    ini = """
+[Config ChordLarge]
+**.routingType = "semi-recursive"
+**.targetOverlayTerminalNum = 10000
+
+[General]
+**.overlay*.chord.routingType = "iterative"
+**.overlay*.*.recNumRedundantNodes = 3
+**.overlay*.*.recordRoute = false
+**.overlay*.*.routeMsgAcks = false
+"""
+    assert Params.from_ini(ini).routingType == 0
+    p = Params.from_ini(ini, "ChordLarge")
+    assert (p.routingType, p.recNumRedundantNodes) == (1, 3)
+    assert Params.from_ini('[General]\n**.routingType = "full-recursive"\n').routingType == 2
 
 
 def test_reference_default_ini_parses():

@@ -167,3 +167,48 @@ def test_rejects_unsupported(engine: KbrEngine):
         engine.set_params(Params.chord().replace(jitter=0.1))
     with pytest.raises(KbrError):
         engine.chord_load(net.ids[::-1].copy(), net.xy)   # not sorted
+
+
+# ------------------------------------------------------------ semi-recursive routing
+
+@pytest.mark.parametrize("name", ["chord_n1000_semirec", "chord_n1000_semirec_hcm4"])
+def test_recursive_golden_vectors(engine: KbrEngine, name):
+    g = np.load(GOLD / f"{name}.npz")
+    engine.set_params(Params.chord().replace(simtimeRound=int(g["simtime_round"]), routingType=1,
+                                             hopCountMax=int(g["hop_count_max"])))
+    engine.chord_load(g["ids"], g["xy"])
+    r = engine.lookup(g["keys"], g["src"], record_hops=True, count_rpcs=True)
+    _eq(r, {f: g[f] for f in FIELDS} | {"hop_seq": g["hop_seq"]}, name, hop_cols=g["hop_seq"].shape[1])
+    assert not r["rpcs"].any()
+
+
+@pytest.mark.parametrize("rnd,rt,hcm", [(1, 1, 50), (0, 2, 50), (1, 1, 5), (1, 1, 0)])
+def test_recursive_matches_oracle(engine: KbrEngine, rnd, rt, hcm):
+    net = W.population(1 << 16, 77 + rnd)
+    k1, s1 = W.lookups(net.ids, 100_000, 78, node_ids=False)
+    k2, s2 = W.lookups(net.ids, 100_000, 79, node_ids=True)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    engine.set_params(Params.chord().replace(simtimeRound=rnd, routingType=rt, hopCountMax=hcm))
+    engine.chord_load(net.ids, net.xy)
+    r = engine.lookup(keys, src, record_hops=True)
+    o = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd, routingType=rt, hopCountMax=hcm))
+    ref = o.route(keys, src, record_hops=True)
+    _eq(r, ref, f"recursive rnd={rnd} hcm={hcm}", hop_cols=max(hcm, 1))
+    if hcm == 0:
+        assert (r["status"] == 3).all()
+
+
+def test_recursive_rejects_explicit_tables(engine: KbrEngine):
+    from oversim_amd import KbrError
+    g = np.load(GOLD / "chord_n9.npz")
+    engine.set_params(Params.chord())
+    engine.chord_load(g["ids"], g["xy"])
+    fingers = engine.chord_fingers()
+    n = len(g["ids"])
+    pred = (np.arange(n) - 1) % n
+    succ = np.stack([(np.arange(n) + 1 + j) % n for j in range(8)], axis=1).astype(np.uint32)
+    engine.chord_load_tables(g["ids"], g["xy"], pred, succ, np.full(n, 8, np.uint8), fingers,
+                             np.full(n, 160, np.uint8))
+    engine.set_params(Params.chord().replace(routingType=1))
+    with pytest.raises(KbrError):
+        engine.lookup(g["keys"][:4], g["src"][:4])

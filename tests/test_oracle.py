@@ -170,3 +170,47 @@ def test_kademlia_sibling_table_is_xor_closest():
     for c in range(0, 500, 37):
         d = sorted((ids[x] ^ ids[c], x) for x in range(500) if x != c)
         assert [x for _, x in d[:40]] == [int(x) for x in sib[c]]
+
+
+def test_oracle_semi_recursive_matches_refmodel():
+    """Recursive one-way routing (ChordLarge: routingType = semi-recursive): the oracle's
+    full sendToKey restatement (recNumRedundantNodes = 3, loop detection) equals the
+    greedy forwarding walk of the independent model on converged rings."""
+    for n, seed, hcm in ((17, 1, 50), (300, 2, 50), (2500, 3, 50), (2500, 4, 3)):
+        net = W.population(n, seed)
+        k, s = W.lookups(net.ids, 400, seed + 7, node_ids=bool(seed % 2))
+        p = O.chord_params(routingType=1, hopCountMax=hcm)
+        r = O.OracleNet("chord", net.ids, net.xy, p).route(k, s, record_hops=True, count_rpcs=True)
+        assert not r["rpcs"].any()
+        ring = refmodel.ChordRing(net.ids, net.xy)
+        for i in range(len(k)):
+            m = ring.lookup_recursive(k[i], int(s[i]), hop_max=hcm)
+            for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+                assert int(r[f][i]) == int(m[f]), (n, i, f)
+            if m["status"] == 0:
+                assert list(r["hop_seq"][i][:m["hops"]]) == m["hop_seq"]
+
+
+def test_semi_recursive_path_is_iterative_path():
+    """On a converged ring both modes visit the same nodes; only the accounting differs:
+    recursive hop count = iterative responders (+0), latency = sum of per-hop route messages."""
+    net = W.population(3000, 5)
+    k, s = W.lookups(net.ids, 500, 6)
+    it = O.OracleNet("chord", net.ids, net.xy).route(k, s, record_hops=True)
+    rc = O.OracleNet("chord", net.ids, net.xy, O.chord_params(routingType=1)).route(k, s, record_hops=True)
+    ok = (it["status"] == 0) & (rc["status"] == 0)
+    assert ok.mean() > 0.99
+    assert np.array_equal(it["responsible"][ok], rc["responsible"][ok])
+    assert np.array_equal(it["hops"][ok], rc["hops"][ok])
+    assert np.array_equal(it["hop_seq"][ok], rc["hop_seq"][ok])
+
+
+@pytest.mark.parametrize("name", ["chord_n1000_semirec", "chord_n1000_semirec_hcm4"])
+def test_oracle_reproduces_recursive_golden(name):
+    g = np.load(GOLD / f"{name}.npz")
+    p = O.chord_params(simtimeRound=int(g["simtime_round"]), routingType=int(g["routing_type"]),
+                       hopCountMax=int(g["hop_count_max"]))
+    r = O.OracleNet("chord", g["ids"], g["xy"], p).route(g["keys"], g["src"], record_hops=True)
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+        assert np.array_equal(r[f], g[f]), f
+    assert np.array_equal(r["hop_seq"][:, :g["hop_seq"].shape[1]], g["hop_seq"])
