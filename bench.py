@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--workload", choices=["B", "C", "D", "E"], default="C")
     ap.add_argument("--nodes", type=int, default=None, help="override ring size (per GPU for C, total for D/E)")
     ap.add_argument("--lookups", type=int, default=None, help="override lookups per GPU per step")
+    ap.add_argument("--routing", choices=["iterative", "semi-recursive"], default="iterative",
+                    help="Chord routingType (semi-recursive = omnetpp.ini ChordLarge)")
     ap.add_argument("--seed", type=int, default=0xC)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -64,12 +66,13 @@ WL = {
 }
 
 
-def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1) -> dict:
+def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, routing_type: int = 0) -> dict:
     """The oracle (CPU restatement, kind 'port') on a bounded sample of the same workload."""
     sys.path.insert(0, str(ROOT / "tests"))
-    from oracle_lib import OracleNet, kad_params
+    from oracle_lib import OracleNet, chord_params, kad_params
     nthreads = min(os.cpu_count() or 1, 16)
-    o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia" else None)
+    o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia"
+                  else chord_params(routingType=routing_type))
     m = 20000
     t = time.perf_counter()
     o.route(keys[:m], src[:m], record_hops=False, nthreads=nthreads)
@@ -135,6 +138,11 @@ def main():
     n_total = nodes * world if wl["per_gpu_nodes"] else nodes
     m = a.lookups or wl["lookups"]
     kind = wl["overlay"]
+    routing_type = 1 if a.routing == "semi-recursive" else 0
+    if routing_type and kind != "chord":
+        raise SystemExit("--routing semi-recursive applies to the Chord workloads (C, D)")
+    if routing_type:
+        wl["desc"] = wl["desc"].replace("iterative", "semi-recursive")
     stream = torch.cuda.Stream(device=dev)
     sharded = kind == "chord" and world > 1
     small = n_total <= (1 << 22)
@@ -169,7 +177,8 @@ def main():
         ids_np = ids if ids is not None else ids_t.cpu().numpy().view(np.uint32)
         xy_np = xy if xy is not None else xy_t.cpu().numpy()
         comm = dev if backend == "nccl" else torch.device("cpu")
-        sh = ShardedChord(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm)
+        sh = ShardedChord(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
+                          params=Params.chord().replace(routingType=routing_type))
         kname = "k_chord_shard_step"
 
         def step():
@@ -177,7 +186,7 @@ def main():
     else:
         eng = KbrEngine(dev_index)
         if kind == "chord":
-            eng.set_params(Params.chord())
+            eng.set_params(Params.chord().replace(routingType=routing_type))
             eng.chord_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
             kname = "k_chord_route"
         else:
@@ -247,7 +256,7 @@ def main():
         traffic = traffic_from_csv(a.traffic_csv, kname)
         cpu = None
         if world == 1 and not a.no_cpu_baseline and small:
-            cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1))
+            cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type)
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
                "hopCountMax": 50, "parallelism": (f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)"
                                                   if sharded else ("replicas" if world > 1 else "1 GPU")),
@@ -256,7 +265,7 @@ def main():
             cfg.update({"k": 8, "alpha": wl["alpha"], "rpcs_per_s": rpc_all * a.steps / wall_max,
                         "mean_rpcs": rpc_all / max(ok_all, 1)})
         else:
-            cfg.update({"successorListSize": 8})
+            cfg.update({"successorListSize": 8, "routingType": a.routing})
         if sharded:
             cfg.update({"hop_rounds": sh.rounds})
         line = {

@@ -398,6 +398,7 @@ __device__ __forceinline__ void store_lrec(ovs_lookup_rec* __restrict__ p, uint6
     q[2] = make_uint4((uint32_t)(uint64_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)hops | ((uint32_t)local << 16), 0u);
 }
 
+template <bool REC>
 __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayConsts DC, LookupConsts LC,
                                                           const uint64_t* __restrict__ shard_lo, int nsh, int me, const ovs_lookup_rec* __restrict__ in, uint64_t nin,
                                                           uint64_t chunk, ovs_lookup_rec* __restrict__ out,
@@ -445,7 +446,35 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
             const Decision d = decide_ideal(V, cur, crec, K);
             uint8_t status = 0xFF;
             uint32_t R = NONE;
-            if (local) {
+            if (REC) {
+                // recursive route message (same rules as k_chord_route<.., REC>); the hop's
+                // delay was charged when the message was sent
+                const bool at_src = local;
+                local = false;
+                if (d.sib && (!at_src || hops < LC.hopCountMax)) { status = OVS_LOOKUP_OK; R = cur; }
+                else if (d.sib) status = OVS_LOOKUP_HOPMAX;
+                else if (d.broken) status = OVS_LOOKUP_BROKEN;
+                else if (hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;
+                else if (d.next == S || d.next == cur) status = OVS_LOOKUP_NO_NEXT;
+                else {
+                    const double2 nxy = V.xy[d.next];   // coordinates are replicated on every rank
+                    t += DC.msgRoute + coord_ns(cxy.x, cxy.y, nxy.x, nxy.y, DC.round);
+                    ++hops;
+                    cur = d.next;
+                    crec = d.rec;
+                    dest = shard_owner(shard_lo, nsh, cur);
+                    if (dest != me) { emit_out = true; active = false; }
+                }
+                if (status != 0xFF) {
+                    o.hops = (uint16_t)(status == OVS_LOOKUP_OK ? hops : 0);
+                    o.status = status;
+                    o.responsible = R;
+                    o.one_way_hops = (uint8_t)(status == OVS_LOOKUP_OK ? hops : 0);
+                    o.latency_ns = status == OVS_LOOKUP_OK ? t : -1;
+                    emit_done = true;
+                    active = false;
+                }
+            } else if (local) {
                 local = false;
                 if (d.broken) status = OVS_LOOKUP_BROKEN;
                 else if (d.sib) { status = OVS_LOOKUP_OK; R = S; }
@@ -464,7 +493,7 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
                     }
                 }
             }
-            if (status == 0xFF) {
+            if (!REC && status == 0xFF) {
                 if (LC.hopCountMax && hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;
                 else if (d.next == S) status = OVS_LOOKUP_NO_NEXT;
                 else {
@@ -474,7 +503,7 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
                     if (dest != me) { emit_out = true; active = false; }
                 }
             }
-            if (status != 0xFF) {
+            if (!REC && status != 0xFF) {
                 o.hops = (uint16_t)hops;
                 o.status = status;
                 if (status == OVS_LOOKUP_OK) {
@@ -733,12 +762,14 @@ hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t
     return hipGetLastError();
 }
 
+template <bool REC>
 static int shard_blocks_per_cu()
 {
     static int bpc = 0;
     if (bpc == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_shard_step, 256, 0) != hipSuccess || b < 1) b = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_shard_step<REC>, 256, 0) != hipSuccess || b < 1)
+            b = 1;
         bpc = b;
     }
     return bpc;
@@ -751,12 +782,18 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    unsigned long long* done_count, int num_cu, hipStream_t s)
 {
     if (nin == 0) return hipSuccess;
-    const uint64_t waves = (uint64_t)num_cu * shard_blocks_per_cu() * 4;
+    const int bpc = LC.recursive ? shard_blocks_per_cu<true>() : shard_blocks_per_cu<false>();
+    const uint64_t waves = (uint64_t)num_cu * bpc * 4;
     uint64_t chunk = (nin + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
     const uint64_t need_waves = (nin + chunk - 1) / chunk;
-    hipLaunchKernelGGL(k_chord_shard_step, dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, s, V, DC, LC, shard_lo, nsh, me, in,
-                       nin, chunk, out, out_dest, out_cap, out_count, done, done_cap, done_count);
+    const dim3 g((unsigned)((need_waves + 3) / 4)), b(256);
+    if (LC.recursive)
+        hipLaunchKernelGGL(k_chord_shard_step<true>, g, b, 0, s, V, DC, LC, shard_lo, nsh, me, in, nin, chunk, out,
+                           out_dest, out_cap, out_count, done, done_cap, done_count);
+    else
+        hipLaunchKernelGGL(k_chord_shard_step<false>, g, b, 0, s, V, DC, LC, shard_lo, nsh, me, in, nin, chunk, out,
+                           out_dest, out_cap, out_count, done, done_cap, done_count);
     return hipGetLastError();
 }
 

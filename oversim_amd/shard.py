@@ -225,10 +225,10 @@ def done_to_numpy(done_t) -> np.ndarray:
 class ShardedChord:
     """bench.py driver for one rank: ring arc + lookups resident in HBM + RCCL exchange."""
 
-    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None):
+    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None):
         self.bounds = arc_bounds(len(ids), world)
         n = keys_t.shape[0]
-        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(2 * n, 1024))
+        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(2 * n, 1024), params=params)
         self.stepper.reset(world * n + 1024)
         self.stepper.timing = True
         self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)

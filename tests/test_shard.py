@@ -149,23 +149,27 @@ def test_sharded_orchestration_gloo_cpu():
 
 # ---------------------------------------------------------------------------- GPU
 
-def _single_gpu_reference(net, keys, src):
+def _single_gpu_reference(net, keys, src, routing_type=0):
     from oversim_amd import KbrEngine, Params
     with KbrEngine(0) as e:
-        e.set_params(Params.chord())
+        e.set_params(Params.chord().replace(routingType=routing_type))
         e.chord_load(net.ids, net.xy)
         return e.lookup(keys, src)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_shard_step_emulated_on_one_gpu(world):
+@pytest.mark.parametrize("world,rt", [(2, 0), (3, 0), (8, 0), (3, 1), (8, 1)])
+def test_shard_step_emulated_on_one_gpu(world, rt):
+    """rt = routingType: 0 iterative, 1 semi-recursive (ChordLarge)."""
+    from oversim_amd import Params
     from oversim_amd.shard import GpuShardStepper, arc_bounds, done_to_numpy, route_local_shards
     n, m = 1 << 16, 6000
     net = W.population(n, 93)
     bounds = arc_bounds(n, world)
     dev = torch.device("cuda", 0)
-    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m) for r in range(world)]
+    params = Params.chord().replace(routingType=rt)
+    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, params=params)
+                for r in range(world)]
     ks, ss, qb, allk, alls = [], [], [], [], []
     for r in range(world):
         k, s = W.lookups(net.ids, m, 94 + r, node_ids=(r % 2 == 0))
@@ -178,7 +182,7 @@ def test_shard_step_emulated_on_one_gpu(world):
     d = np.concatenate([done_to_numpy(x) for x in dones])
     d = d[np.argsort(d["qid"])]
     assert np.array_equal(d["qid"], np.arange(world * m))
-    ref = _single_gpu_reference(net, np.concatenate(allk), np.concatenate(alls))
+    ref = _single_gpu_reference(net, np.concatenate(allk), np.concatenate(alls), rt)
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
     assert rounds >= 2
