@@ -12,7 +12,7 @@
 // distance with an exact 160-bit fallback on ties.
 #include <hipcub/hipcub.hpp>
 
-#include "kad.hpp"
+#include "kad_dev.hpp"
 
 namespace ovs {
 
@@ -23,64 +23,6 @@ void kad_free(KadTables& t)
     if (t.sibe) hipFree(t.sibe);
     if (t.slots) hipFree(t.slots);
     t.recs = nullptr; t.sib = nullptr; t.sibe = nullptr; t.slots = nullptr; t.total_slots = 0;
-}
-
-// ---------------------------------------------------------------------------
-// helpers
-
-__device__ __forceinline__ uint32_t kbit(const K160& k, int b) { return (k.w[b >> 5] >> (b & 31)) & 1u; }
-
-__device__ __forceinline__ K160 kload(const KeyRec* __restrict__ recs, uint32_t i) { return key_of(load_rec(recs, i)); }
-
-__device__ __forceinline__ K160 kad_key(const KadRec* __restrict__ r, uint32_t i)
-{
-    const uint4* p = reinterpret_cast<const uint4*>(r + i);
-    const uint4 a = p[0];
-    K160 k;
-    k.w[0] = a.x; k.w[1] = a.y; k.w[2] = a.z; k.w[3] = a.w; k.w[4] = r[i].key[4];
-    return k;
-}
-
-__device__ __forceinline__ KadRec kad_rec(const KadRec* __restrict__ r, uint32_t i)
-{
-    const uint4* p = reinterpret_cast<const uint4*>(r + i);
-    const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-    KadRec o;
-    o.key[0] = a.x; o.key[1] = a.y; o.key[2] = a.z; o.key[3] = a.w; o.key[4] = b.x;
-    o.R[0] = b.y; o.R[1] = b.z; o.R[2] = b.w; o.R[3] = c.x; o.R[4] = c.y;
-    o.mask[0] = c.z; o.mask[1] = c.w; o.mask[2] = d.x; o.mask[3] = d.y; o.mask[4] = d.z;
-    o.boff = d.w;
-    return o;
-}
-
-__device__ __forceinline__ K160 as_key(const uint32_t* w)
-{
-    K160 k;
-    k.w[0] = w[0]; k.w[1] = w[1]; k.w[2] = w[2]; k.w[3] = w[3]; k.w[4] = w[4];
-    return k;
-}
-
-// first index in [lo,hi) whose bit b is set; all keys in [lo,hi) share the bits above b
-__device__ uint32_t split_bit(const KeyRec* __restrict__ recs, uint32_t lo, uint32_t hi, int b)
-{
-    while (lo < hi) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        if (kbit(kload(recs, mid), b)) hi = mid; else lo = mid + 1;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
-{
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-// identical to the oracle's kad_hash (bucket sampling of the snapshot rule)
-__device__ __forceinline__ uint64_t kad_hash(uint64_t seed, uint32_t node, uint32_t m, uint32_t j)
-{
-    return splitmix64(seed ^ splitmix64(((uint64_t)node << 32) ^ ((uint64_t)m << 16) ^ (uint64_t)j));
 }
 
 // ---------------------------------------------------------------------------
@@ -169,16 +111,17 @@ __global__ void k_kad_set_boff(KadRec* recs, const uint64_t* off, uint32_t n)
 // builder, pass B: buckets m = 159 .. endIndex, up to k members of T_m minus
 // siblings chosen by Floyd sampling (snapshot rule)
 __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadRec* __restrict__ krec, uint32_t n, int k,
-                              int S5, uint64_t seed, const uint32_t* __restrict__ sib, KadEntry* __restrict__ slots)
+                              int S5, uint64_t seed, const uint32_t* __restrict__ sib, KadEntry* __restrict__ slots,
+                              uint32_t own_lo, uint32_t own_hi)
 {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
+    const uint32_t v = own_lo + blockIdx.x * blockDim.x + threadIdx.x;   // rows of the owned arc
+    if (v >= own_hi) return;
     const KadRec r = krec[v];
     const K160 me = as_key(r.key);
     const K160 R = as_key(r.R);
     if (k_msb(R) < 0) return;
     const int endIndex = k_msb(R);
-    const uint32_t* L = sib + (uint64_t)v * S5;
+    const uint32_t* L = sib + (uint64_t)(v - own_lo) * S5;
     uint32_t lo = 0, hi = n;
     uint32_t chosen[32];
     for (int m = KEYBITS - 1; m >= endIndex; --m) {
@@ -260,264 +203,32 @@ __global__ void k_kad_export(const KadRec* __restrict__ krec, const KadEntry* __
     bcount[t] = (uint8_t)c;
 }
 
-// ---------------------------------------------------------------------------
-// sorted vectors in registers (static indexing only)
-
-// XOR-distance order of node a vs node b to key K: top 64 bits, exact fallback on ties
-__device__ __forceinline__ bool closer(uint64_t da, uint32_t ia, uint64_t db, uint32_t ib, const K160& K,
-                                       const KadRec* __restrict__ recs)
-{
-    if (da != db) return da < db;
-    const K160 xa = k_xor(kad_key(recs, ia), K), xb = k_xor(kad_key(recs, ib), K);
-    return k_lt(xa, xb);
-}
-
-__device__ __forceinline__ uint64_t dist_hi(const K160& x, const K160& K)
-{
-    return ((uint64_t)(x.w[4] ^ K.w[4]) << 32) | (uint64_t)(x.w[3] ^ K.w[3]);
-}
-
-template <int CAP>
-struct SVec {
-    uint32_t idx[CAP];
-    uint64_t d[CAP];
-    uint32_t used;   // bit i: entry i alreadyUsed (LookupVector only)
-    int n;
+struct SendNothing {
+    __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
 };
 
-template <int CAP>
-__device__ __forceinline__ void svec_clear(SVec<CAP>& v)
-{
-    v.n = 0;
-    v.used = 0;
-#pragma unroll
-    for (int i = 0; i < CAP; ++i) { v.idx[i] = NONE; v.d[i] = ~0ull; }
-}
-
-// BaseKeySortedVector::add with a KeyDistanceComparator<KeyXorMetric> (NodeVector.h:381-512):
-// dedupe by key (== by node index), insert before the first farther entry, truncate to cap.
-template <int CAP>
-__device__ __forceinline__ int svec_add(SVec<CAP>& v, int cap, uint32_t x, uint64_t dx, const K160& K,
-                                        const KadRec* __restrict__ recs)
-{
-    bool dup = false;
-    int pos = 0;
-#pragma unroll
-    for (int i = 0; i < CAP; ++i) {
-        if (i < v.n) {
-            dup |= (v.idx[i] == x);
-            pos += (v.idx[i] != x && closer(v.d[i], v.idx[i], dx, x, K, recs)) ? 1 : 0;
-        }
+// the responder's findNode evaluated in place (all tables on this GPU)
+struct LocalFindNode {
+    const KadView& V;
+    const K160& K;
+    int redundant;
+    __device__ __forceinline__ bool ready(int) const { return true; }
+    __device__ __forceinline__ void fill(int, uint32_t r, const KadRec& rr, bool sb, SVec<8>& res) const
+    {
+        kad_find_node1(V, r, rr, K, redundant, sb, res);
     }
-    if (dup || pos >= cap) return -1;
-    const uint32_t lowmask = (1u << pos) - 1u;
-    v.used = ((v.used & lowmask) | ((v.used & ~lowmask) << 1)) & ((1u << cap) - 1u);
-#pragma unroll
-    for (int i = CAP - 1; i >= 0; --i) {
-        if (i > pos) {
-            if (i >= 1) { v.idx[i] = v.idx[i - 1]; v.d[i] = v.d[i - 1]; }
-        } else if (i == pos) {
-            v.idx[i] = x; v.d[i] = dx;
-        }
-    }
-    v.n = v.n + 1 > cap ? cap : v.n + 1;
-    return pos;
-}
-
-// ---------------------------------------------------------------------------
-// Kademlia::isSiblingFor(thisNode, key, 1) (Kademlia.cc:888-962) from the 64 B record
-__device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadRec& r, const K160& K)
-{
-    if (V.nsib < 1) return true;
-    const K160 D = k_xor(as_key(r.key), K);
-    if (V.nsib == V.S5 && k_gt(D, as_key(r.R))) return false;
-    const K160 M = as_key(r.mask);
-    return ((D.w[0] & M.w[0]) | (D.w[1] & M.w[1]) | (D.w[2] & M.w[2]) | (D.w[3] & M.w[3]) | (D.w[4] & M.w[4])) == 0;
-}
-
-// insert up to 8 entries of a contiguous entry array (bucket slot or sibling block); the
-// loads are issued together before the dependent sorted inserts
-template <int CAP>
-__device__ __forceinline__ void add_entries8(SVec<CAP>& res, int cap, const KadEntry* __restrict__ s, int cnt,
-                                             const K160& K, const KadRec* __restrict__ recs)
-{
-    uint32_t ix[8];
-    uint64_t dd[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        if (q < cnt) {
-            const uint2* p = reinterpret_cast<const uint2*>(s + q);
-            const uint2 a = p[0], b = p[1], c = p[2];
-            ix[q] = c.y;
-            dd[q] = ((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(b.y ^ K.w[3]);
-            (void)a;
-        } else {
-            ix[q] = NONE;
-            dd[q] = 0;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-        if (ix[q] != NONE) svec_add(res, cap, ix[q], dd[q], K, recs);
-}
-
-template <int CAP>
-__device__ __forceinline__ void add_slot(SVec<CAP>& res, int cap, const KadView& V, uint32_t slot, const K160& K)
-{
-    const KadEntry* e = V.slots + (uint64_t)slot * V.k;
-    for (int q0 = 0; q0 < V.k; q0 += 8) add_entries8(res, cap, e + q0, min(8, V.k - q0), K, V.recs);
-}
-
-// Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246)
-template <int CAP>
-__device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, const KadRec& r, const K160& K, int numRedundant,
-                               bool sib, SVec<CAP>& res)
-{
-    svec_clear(res);
-    const K160 me = as_key(r.key);
-    if (V.nsib == 0 || sib) {
-        // resultSize = 1 and self is the XOR-closest of siblings + self; with a full table the
-        // key lies below endIndex so bucket msb(D) is all siblings
-        svec_add(res, 1, c, dist_hi(me, K), K, V.recs);
-        return;
-    }
-    const int cap = numRedundant < CAP ? numRedundant : CAP;
-    const K160 D = k_xor(me, K);
-    const int m = k_msb(D);
-    const int endIndex = k_msb(as_key(r.R));
-    auto slot_of = [&](int b) { return r.boff + (uint32_t)(KEYBITS - 1 - b); };
-    if (m >= 0 && m >= endIndex) add_slot(res, cap, V, slot_of(m), K);
-    if (m >= endIndex || res.n < cap) {
-        // nothing below bucket m can beat a full result unless siblings share bucket m
-        if (!(m > endIndex && res.n >= cap)) {
-            for (int b = m - 1; b >= endIndex; --b) add_slot(res, cap, V, slot_of(b), K);
-            const KadEntry* L = V.sibe + (uint64_t)c * V.S5;
-            for (int i = 0; i < V.nsib; i += 8) add_entries8(res, cap, L + i, min(8, V.nsib - i), K, V.recs);
-            svec_add(res, cap, c, dist_hi(me, K), K, V.recs);
-        }
-    }
-    for (int b = m + 1; res.n < cap && b < KEYBITS; ++b)
-        if (b >= endIndex) add_slot(res, cap, V, slot_of(b), K);
-}
-
-// ---------------------------------------------------------------------------
-// K2: batched iterative lookups
-
-constexpr int MAXA = 4;    // lookupParallelRpcs <= 4
-
-struct KadLC {
-    int hopCountMax, numSiblings, redundant, alpha;
-    int strict, visitOnlyOnce, acceptLateSiblings, useAll, merge, newOnResp, newOnTimeout, finishOnFirst;
-    int maxRedundantLocal;   // getMaxNumRedundantNodes() = k
 };
 
-// One in-flight FindNodeCall = one future event: its response arrival or its RPC timeout.
-// Event order: (time, insertion time, insertion sequence); insertion time is kept as the
-// (always < 2^32 ns) gap back from the event time.
-struct Pend {
-    uint32_t node;
-    uint32_t tag;      // step at send (bits 0..15) | insertion sequence (bits 16..30) | timeout (bit 31)
-    int64_t t;         // event time
-    uint32_t dins;     // t - insertion time
-};
-
-// per-lane lookup state (IterativeLookup + its single IterativePathLookup)
-template <int A>
-struct KadLookup {
-    K160 K;
-    uint32_t S;
-    double sx, sy;
-    int64_t now, txf;
-    uint32_t seq;
-    SVec<8> nh;            // LookupVector nextHops (cap redundantNodes), used bits = alreadyUsed
-    Pend p[A];
-    uint32_t pvalid;
-    int step, hops, pending;
-    bool pfinished, psuccess, any_to;
-    uint32_t result, nsent;
-};
-
-// FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
-// SimpleNodeEntry::calcDelay with the source's tx queue)
-template <int A>
-__device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
-                                         uint32_t x)
-{
-    const double2 cxy = V.xy[x];
-    const KadRec rr = kad_rec(V.recs, x);
-    const bool sb = kad_is_sibling1(V, rr, L.K);
-    // the response carries findNode's result: 1 node when x is sibling, else min(redundant, n)
-    const int csz = sb ? 1 : (LC.redundant < (int)V.n ? LC.redundant : (int)V.n);
-    const int64_t cd = coord_ns(L.sx, L.sy, cxy.x, cxy.y, DC.round);
-    const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
-    const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
-    L.txf = newTx;
-    const int64_t d1 = (newTx - L.now) + DC.access2 + cd + bwc;
-    const int64_t bwr = bw_ns(DC.respBase + DC.respPerNode * csz, DC.datarate, DC.round);
-    const int64_t d2 = 2 * bwr + DC.access2 + cd;
-    const int64_t tTo = L.now + DC.rpcTimeout;
-    const int64_t tResp = L.now + d1 + d2;
-    const bool isTo = tTo <= tResp;   // the timeout was scheduled first: it wins ties
-    const uint32_t sTo = L.seq++;
-    const uint32_t sR = L.seq++;
-    const uint32_t tag = (uint32_t)L.step | ((isTo ? sTo : sR) << 16) | (isTo ? 0x80000000u : 0u);
-    int slot = 0;
-#pragma unroll
-    for (int i = A - 1; i >= 0; --i)
-        if (!((L.pvalid >> i) & 1u)) slot = i;
-#pragma unroll
-    for (int i = 0; i < A; ++i) {
-        if (i == slot) {
-            L.p[i].node = x;
-            L.p[i].t = isTo ? tTo : tResp;
-            L.p[i].dins = (uint32_t)(isTo ? DC.rpcTimeout : d2);
-            L.p[i].tag = tag;
-        }
+template <bool RECORD>
+struct HopRecorder {
+    uint32_t* __restrict__ hopseq;
+    uint64_t base;
+    int hcm;
+    __device__ __forceinline__ void operator()(int h, uint32_t r) const
+    {
+        if (RECORD && h < hcm) hopseq[base + h] = r;
     }
-    L.pvalid |= 1u << slot;
-    ++L.nsent;
-}
-
-// IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
-template <int A>
-__device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
-                                              int num)
-{
-    if (L.pfinished) return;
-    if (LC.hopCountMax && L.hops >= LC.hopCountMax) { L.pfinished = true; L.psuccess = false; return; }
-    if (LC.strict) num = min(num, LC.alpha - L.pending);
-    if (num == 0 && L.pending == 0 && !LC.finishOnFirst) num = LC.alpha;
-    for (int i = 0; num > 0 && i < LC.redundant; ++i) {
-        // getNextEntry: first entry not alreadyUsed (no node is ever dead in a stable network)
-        const uint32_t unused = ~L.nh.used & ((1u << L.nh.n) - 1u);
-        if (!unused) break;
-        const int e = __ffs((int)unused) - 1;
-        uint32_t h = NONE;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j == e) h = L.nh.idx[j];
-        // visitOnlyOnce: an unused entry can only be a visited node if it is the source
-        // (responders stay in nextHops as used entries or are evicted for good)
-        if (!LC.visitOnlyOnce || h != L.S) {
-            ++L.pending;
-            --num;
-            kad_send(L, V, DC, LC, h);
-        }
-        L.nh.used |= 1u << e;
-    }
-    if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
-}
-
-template <int A>
-__device__ __forceinline__ void kad_timeoutlike(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
-                                                const KadLC& LC)
-{
-    // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
-    --L.pending;
-    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
-    else if (LC.newOnTimeout) kad_send_rpcs(L, V, DC, LC, 1);
-    else if (L.pending == 0) kad_send_rpcs(L, V, DC, LC, LC.alpha);
-}
+};
 
 template <int A, bool RECORD>
 __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, KadLC LC, const K160* __restrict__ qkeys,
@@ -535,6 +246,7 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
     uint64_t q = 0;
     KadLookup<A> L;
     SVec<8> res;
+    const SendNothing on;
 
     while (true) {
         const uint64_t need = __ballot(!active);
@@ -543,126 +255,21 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
             if (!active && mine < end) {
                 q = mine;
                 active = true;
-                L.K = qkeys[q];
-                L.S = qsrc[q];
-                const double2 sxy = V.xy[L.S];
-                L.sx = sxy.x; L.sy = sxy.y;
-                L.now = 0; L.txf = 0; L.seq = 0;
-                svec_clear(L.nh);
-                L.pvalid = 0;
-                L.step = 0; L.hops = 0; L.pending = 0;
-                L.pfinished = false; L.psuccess = false; L.any_to = false;
-                L.result = NONE;
-                L.nsent = 0;
-                // IterativeLookup::start (IterativeLookup.cc:133-244): local findNode at S
-                const KadRec rs = kad_rec(V.recs, L.S);
-                const bool sb = kad_is_sibling1(V, rs, L.K);
-                kad_find_node1(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res);
-                if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
-                else if (LC.numSiblings != 0 && sb) {
-                    L.result = res.idx[0];
-                    L.pfinished = true; L.psuccess = true;
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        if (j < res.n) svec_add(L.nh, LC.redundant, res.idx[j], res.d[j], L.K, V.recs);
-                    kad_send_rpcs(L, V, DC, LC, LC.alpha);
-                }
+                kad_lookup_init(L, qkeys[q], qsrc[q], V.xy);
+                kad_lookup_start(L, V, DC, LC, res, on);
             }
             cursor += (uint64_t)__popcll(need);
         }
         if (!__any(active)) break;
         if (!active) continue;
 
-        if (!L.pfinished && L.pvalid) {
-            // earliest event
-            int e = -1;
-            int64_t bt = 0, bi = 0;
-            uint32_t bs = 0;
-#pragma unroll
-            for (int i = 0; i < A; ++i) {
-                if ((L.pvalid >> i) & 1u) {
-                    const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
-                    const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
-                    const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
-                    if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
-                }
-            }
-            uint32_t r = 0, tag = 0;
-#pragma unroll
-            for (int i = 0; i < A; ++i)
-                if (i == e) { r = L.p[i].node; tag = L.p[i].tag; }
-            L.pvalid &= ~(1u << e);
-            L.now = bt;
-            const int vr = (int)(tag & 0xFFFFu);
-            if (tag & 0x80000000u) {
-                // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
-                L.any_to = true;
-                kad_timeoutlike(L, V, DC, LC);
-            } else {
-                const KadRec rr = kad_rec(V.recs, r);
-                const bool sb = kad_is_sibling1(V, rr, L.K);
-                const bool acc = (LC.useAll && LC.merge) ? true : (vr == L.step);
-                if (acc || (sb && LC.acceptLateSiblings)) {
-                    // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
-                    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
-                    else {
-                        if (r != L.S) {
-                            if (RECORD && L.hops < LC.hopCountMax)
-                                hopseq[q * (uint64_t)LC.hopCountMax + L.hops] = r;
-                            ++L.hops;
-                        }
-                        ++L.step;
-                        --L.pending;
-                        kad_find_node1(V, r, rr, L.K, LC.redundant, sb, res);
-                        int numNew = 0;
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            if (j < res.n) {
-                                const int pos = svec_add(L.nh, LC.redundant, res.idx[j], res.d[j], L.K, V.recs);
-                                if (pos >= 0 && pos < LC.redundant) ++numNew;
-                            }
-                        }
-                        if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
-                        if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
-                        else {
-                            if (numNew == 0 && LC.newOnResp) numNew = 1;
-                            kad_send_rpcs(L, V, DC, LC, min(numNew, LC.alpha));
-                        }
-                    }
-                } else {
-                    // not accepted: handled as a timeout, its nodes are dropped
-                    kad_timeoutlike(L, V, DC, LC);
-                }
-            }
+        if (!kad_lookup_done(L)) {
+            const LocalFindNode fn{V, L.K, LC.redundant};
+            const HopRecorder<RECORD> rec{hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
+            kad_lookup_event(L, V, DC, LC, res, fn, on, rec);
         }
-        // checkStop (IterativeLookup.cc:295-349): the single path finished, or nothing pending
-        if (L.pfinished || L.pvalid == 0) {
-            ovs_route_out o;
-            o.hops = (uint16_t)L.hops;
-            if (L.pfinished && L.psuccess && L.result != NONE) {
-                o.status = OVS_LOOKUP_OK;
-                o.responsible = L.result;
-                o.one_way_hops = (uint8_t)(L.hops + (L.result != L.S ? 1 : 0));
-                int64_t lat = L.now;
-                if (L.result != L.S) {
-                    // sendRouteMessage through the source's tx queue (SimpleNodeEntry.cc:164-194)
-                    const double2 rxy = V.xy[L.result];
-                    const int64_t bwr = bw_ns(DC.routeBytes, DC.datarate, DC.round);
-                    const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwr;
-                    lat = newTx + DC.access2 + coord_ns(L.sx, L.sy, rxy.x, rxy.y, DC.round) + bwr;
-                }
-                o.latency_ns = lat;
-            } else {
-                o.responsible = NONE;
-                o.one_way_hops = 0;
-                o.latency_ns = -1;
-                if (L.now > DC.lookupTimeout) o.status = OVS_LOOKUP_TIMEOUT;
-                else if (L.any_to) o.status = OVS_LOOKUP_RPC_TIMEOUT;
-                else if (LC.hopCountMax && L.hops >= LC.hopCountMax) o.status = OVS_LOOKUP_HOPMAX;
-                else o.status = OVS_LOOKUP_NO_NEXT;
-            }
-            out[q] = o;
+        if (kad_lookup_done(L)) {
+            out[q] = kad_lookup_output(L, V, DC, LC);
             if (rpcs_out) rpcs_out[q] = L.nsent;
             active = false;
         }
@@ -696,41 +303,61 @@ __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, co
 
 static inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed, KadTables& t, hipStream_t st)
+hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed, KadTables& t, hipStream_t st,
+                     uint32_t lo, uint32_t hi)
 {
     hipError_t e;
     kad_free(t);
-    t.k = k; t.s = s; t.seed = seed;
+    if (hi > n) hi = n;
+    if (lo >= hi) return hipErrorInvalidValue;
+    t.k = k; t.s = s; t.seed = seed; t.lo = lo; t.hi = hi;
     const int S5 = 5 * s;
+    const uint32_t nown = hi - lo;
+    const bool whole = lo == 0 && hi == n;
     uint64_t *rowlen = nullptr, *off = nullptr;
+    uint32_t* sib_all = nullptr;
     void* tmp = nullptr;
     size_t tmpb = 0;
+    auto cleanup = [&]() {
+        if (rowlen) hipFree(rowlen);
+        if (off) hipFree(off);
+        if (tmp) hipFree(tmp);
+        if (sib_all && sib_all != t.sib) hipFree(sib_all);
+    };
+    // node records (key, sibling radius R, mask) for the whole ring: a lookup needs every
+    // responder's isSiblingFor when it sends the call; sibling lists are a build temporary
     if ((e = hipMalloc(&t.recs, sizeof(KadRec) * n)) != hipSuccess) return e;
-    if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)n * S5)) != hipSuccess) return e;
-    if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (n + 1))) != hipSuccess) return e;
-    if ((e = hipMalloc(&off, sizeof(uint64_t) * (n + 1))) != hipSuccess) { hipFree(rowlen); return e; }
-    hipLaunchKernelGGL(k_kad_siblings, dim3(nblk(n, 128)), dim3(128), 0, st, recs, n, S5, t.sib, t.recs, rowlen);
-    hipMemsetAsync(rowlen + n, 0, sizeof(uint64_t), st);
+    if ((e = hipMalloc(&sib_all, sizeof(uint32_t) * (uint64_t)n * S5)) != hipSuccess) return e;
+    if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (n + 1))) != hipSuccess) { cleanup(); return e; }
+    if ((e = hipMalloc(&off, sizeof(uint64_t) * (n + 1))) != hipSuccess) { cleanup(); return e; }
+    hipLaunchKernelGGL(k_kad_siblings, dim3(nblk(n, 128)), dim3(128), 0, st, recs, n, S5, sib_all, t.recs, rowlen);
+    // bucket rows only for the owned arc
+    if (lo) hipMemsetAsync(rowlen, 0, sizeof(uint64_t) * lo, st);
+    hipMemsetAsync(rowlen + hi, 0, sizeof(uint64_t) * (n + 1 - hi), st);
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, rowlen, off, n + 1, st);
-    if ((e = hipMalloc(&tmp, tmpb)) != hipSuccess) { hipFree(rowlen); hipFree(off); return e; }
+    if ((e = hipMalloc(&tmp, tmpb)) != hipSuccess) { cleanup(); return e; }
     hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, rowlen, off, n + 1, st);
     uint64_t total = 0;
     hipMemcpyAsync(&total, off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) { hipFree(rowlen); hipFree(off); hipFree(tmp); return e; }
-    if (total >= 0xFFFFFFFFull) { hipFree(rowlen); hipFree(off); hipFree(tmp); return hipErrorInvalidValue; }
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) { cleanup(); return e; }
+    if (total >= 0xFFFFFFFFull) { cleanup(); return hipErrorInvalidValue; }
     t.total_slots = total;
-    if ((e = hipMalloc(&t.slots, sizeof(KadEntry) * (total + 1) * k)) != hipSuccess) {
-        hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
-    }
+    if ((e = hipMalloc(&t.slots, sizeof(KadEntry) * (total + 1) * k)) != hipSuccess) { cleanup(); return e; }
     hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.recs, off, n);
-    if ((e = hipMalloc(&t.sibe, sizeof(KadEntry) * (uint64_t)n * S5)) != hipSuccess) {
-        hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
+    if (whole) {
+        t.sib = sib_all;
+    } else {
+        if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)nown * S5)) != hipSuccess) { cleanup(); return e; }
+        hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5,
+                       hipMemcpyDeviceToDevice, st);
     }
-    hipLaunchKernelGGL(k_kad_sibentries, dim3(nblk((uint64_t)n * S5, 256)), dim3(256), 0, st, recs, t.sib,
-                       (uint64_t)n * S5, t.sibe);
-    hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.recs, n, k, S5, seed, t.sib, t.slots);
+    if ((e = hipMalloc(&t.sibe, sizeof(KadEntry) * (uint64_t)nown * S5)) != hipSuccess) { cleanup(); return e; }
+    hipLaunchKernelGGL(k_kad_sibentries, dim3(nblk((uint64_t)nown * S5, 256)), dim3(256), 0, st, recs, t.sib,
+                       (uint64_t)nown * S5, t.sibe);
+    hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(nown, 64)), dim3(64), 0, st, recs, t.recs, n, k, S5, seed, t.sib,
+                       t.slots, lo, hi);
     e = hipStreamSynchronize(st);
-    hipFree(rowlen); hipFree(off); hipFree(tmp);
+    cleanup();
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
@@ -758,6 +385,7 @@ static KadView make_view(const KadTables& t, const double2* xy, uint32_t n)
 {
     KadView V{};
     V.recs = t.recs; V.xy = xy; V.sib = t.sib; V.sibe = t.sibe; V.slots = t.slots; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
+    V.lo = t.lo; V.hi = t.hi;
     V.nsib = (int)((uint64_t)(n - 1) < (uint64_t)V.S5 ? n - 1 : (uint32_t)V.S5);
     return V;
 }

@@ -33,6 +33,7 @@ struct KadTables {
     KadEntry* sibe = nullptr;     // n * S5 sibling entries with the member key inline
     KadEntry* slots = nullptr;    // total_slots * k
     uint64_t total_slots = 0;
+    uint32_t lo = 0, hi = 0;      // sib / sibe / bucket rows exist for nodes [lo, hi) (the whole ring unsharded)
     int k = 8, s = 8;
     uint64_t seed = 0;
 };
@@ -47,10 +48,13 @@ struct KadView {
     int k;
     int S5;       // sibling table capacity 5s
     int nsib;     // entries in every sibling table = min(5s, n-1)
+    uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)
 };
 
 void kad_free(KadTables& t);
-hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed, KadTables& t, hipStream_t st);
+// tables for nodes [lo, hi) of the sorted ring (node records for all n)
+hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed, KadTables& t, hipStream_t st,
+                     uint32_t lo = 0, uint32_t hi = 0xFFFFFFFFu);
 hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_t* bucket_count,
                       uint32_t* bucket_nodes, hipStream_t st);
 hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, uint32_t n, const ovs_params& P,

@@ -1,0 +1,251 @@
+// kad_shard.hip -- multi-GPU Kademlia: lookups stay on their home rank, FindNodeCalls
+// are requests to the rank that owns the responder.
+//
+// The sorted ID array is cut into contiguous arcs (= ID prefixes); rank r owns the
+// sibling entries and bucket rows of its arc.  The 64 B node records (key, sibling
+// radius, mask) and the coordinates are replicated, so everything a lookup needs at
+// *send* time -- the responder's isSiblingFor flag, hence the response size and the
+// RTT (IterativeLookup::sendRpc -> SimpleNodeEntry::calcDelay) -- is local.  Only the
+// responder's findNode result (Kademlia.cc:1101-1246) needs the owner's tables: it is
+// requested when the RPC is sent and delivered before the lookup's next round, i.e.
+// before the simulated response event can be processed.
+//
+// Per round (oversim_amd/shard.py drives it):
+//   k_kad_shard_step  : every active lookup processes its events in simulated-time
+//                       order until the earliest one still waits for a findNode result;
+//                       new RPCs append requests (32 B) to the outbox, tagged by owner
+//   all-to-allv       : requests to their owners
+//   k_kad_shard_serve : findNode at the responder -> response (104 B)
+//   all-to-allv       : responses back to the home rank (reverse splits)
+//   k_kad_shard_deliver: results into the lookups' pending-event slots
+// The event processing is the single-GPU state machine (kad_dev.hpp), so the result of
+// every lookup is identical to k_kad_route's.
+#include "kad_dev.hpp"
+#include "kad_shard.hpp"
+
+namespace ovs {
+
+namespace {
+
+__device__ __forceinline__ int kshard_owner(const uint64_t* __restrict__ lo, int nsh, uint32_t c)
+{
+    int r = 0;
+    for (int i = 1; i < nsh; ++i) r += ((uint64_t)c >= lo[i]) ? 1 : 0;
+    return r;
+}
+
+// result slot of pending event `slot` of lookup i
+struct ShardRes {
+    KadRes* __restrict__ res;
+    uint64_t base;
+    __device__ __forceinline__ bool ready(int slot) const { return res[base + slot].ready != 0; }
+    __device__ __forceinline__ void fill(int slot, uint32_t, const KadRec&, bool, SVec<8>& v) const
+    {
+        const KadRes& r = res[base + slot];
+        svec_clear(v);
+        const int n = (int)r.count;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j < n) { v.idx[j] = r.nodes[j]; v.d[j] = r.dist[j]; }
+        }
+        v.n = n;
+    }
+};
+
+// new FindNodeCall: mark its slot pending and queue the request to the responder's owner
+struct ShardSend {
+    KadRes* __restrict__ res;
+    uint64_t base;
+    const K160* K;
+    const uint64_t* __restrict__ shard_lo;
+    int nsh;
+    ovs_kad_req* __restrict__ out;
+    uint32_t* __restrict__ out_dest;
+    uint64_t out_cap;
+    unsigned long long* out_count;
+    __device__ __forceinline__ void operator()(int slot, uint32_t x, bool isTo) const
+    {
+        // a timeout event carries no result
+        res[base + slot].ready = isTo ? 1u : 0u;
+        if (isTo) return;
+        const unsigned long long oi = atomicAdd(out_count, 1ull);
+        if (oi < out_cap) {
+            ovs_kad_req q;
+            for (int w = 0; w < 5; ++w) q.key[w] = K->w[w];
+            q.node = x;
+            q.tag = (uint32_t)(base + slot);
+            q.pad = 0;
+            out[oi] = q;
+            out_dest[oi] = (uint32_t)kshard_owner(shard_lo, nsh, x);
+        }
+    }
+};
+
+struct NoRecord {
+    __device__ __forceinline__ void operator()(int, uint32_t) const {}
+};
+
+template <int A>
+__global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts DC, KadLC LC,
+                                                        KadLookup<A>* __restrict__ st, uint8_t* __restrict__ act,
+                                                        const uint32_t* __restrict__ qids, KadRes* __restrict__ res,
+                                                        uint64_t nlook, const uint64_t* __restrict__ shard_lo, int nsh,
+                                                        ovs_kad_req* __restrict__ out, uint32_t* __restrict__ out_dest,
+                                                        uint64_t out_cap, unsigned long long* out_count,
+                                                        ovs_done_rec* __restrict__ done, uint64_t done_cap,
+                                                        unsigned long long* done_count,
+                                                        unsigned long long* active_count)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlook) return;
+    const uint8_t a = act[i];
+    if (a == 0) return;
+    KadLookup<A> L = st[i];
+    SVec<8> r;
+    ShardSend on{res, i * A, &L.K, shard_lo, nsh, out, out_dest, out_cap, out_count};
+    if (a == 2) kad_lookup_start(L, V, DC, LC, r, on);       // first round: IterativeLookup::start
+    const ShardRes gr{res, i * A};
+    const NoRecord rec;
+    while (!kad_lookup_done(L)) {
+        if (!kad_lookup_event(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
+    }
+    if (kad_lookup_done(L)) {
+        const unsigned long long di = atomicAdd(done_count, 1ull);
+        if (di < done_cap) {
+            ovs_done_rec dr;
+            dr.qid = qids[i];
+            dr.pad = 0;
+            dr.out = kad_lookup_output(L, V, DC, LC);
+            done[di] = dr;
+        }
+        act[i] = 0;
+    } else {
+        st[i] = L;
+        act[i] = 1;
+        atomicAdd(active_count, 1ull);
+    }
+}
+
+template <int A>
+__global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* __restrict__ src, uint64_t n,
+                                 uint32_t qid_base, const double2* __restrict__ xy, KadLookup<A>* __restrict__ st,
+                                 uint8_t* __restrict__ act, uint32_t* __restrict__ qids, KadRes* __restrict__ res)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    KadLookup<A> L;
+    kad_lookup_init(L, keys[i], src[i], xy);
+    st[i] = L;
+    act[i] = 2;
+    qids[i] = qid_base + (uint32_t)i;
+    for (int s = 0; s < A; ++s) res[i * A + s].ready = 1;
+}
+
+// findNode at the responder (owned by this rank) for each received request
+__global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __restrict__ in, uint64_t n,
+                                  ovs_kad_resp* __restrict__ out)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const ovs_kad_req q = in[j];
+    K160 K;
+    for (int w = 0; w < 5; ++w) K.w[w] = q.key[w];
+    ovs_kad_resp o;
+    o.tag = q.tag;
+    if (q.node < V.lo || q.node >= V.hi) {
+        o.count = 0xFFFFFFFFu;    // not this rank's node: the caller mis-routed the request
+        out[j] = o;
+        return;
+    }
+    const KadRec rr = kad_rec(V.recs, q.node);
+    const bool sb = kad_is_sibling1(V, rr, K);
+    SVec<8> r;
+    kad_find_node1(V, q.node, rr, K, LC.redundant, sb, r);
+    o.count = (uint32_t)r.n;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { o.nodes[k] = r.idx[k]; o.dist_hi[k] = r.d[k]; }
+    out[j] = o;
+}
+
+__global__ void k_kad_shard_deliver(const ovs_kad_resp* __restrict__ in, uint64_t n, KadRes* __restrict__ res,
+                                    uint64_t nslots, unsigned long long* bad)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const ovs_kad_resp o = in[j];
+    if (o.tag >= nslots || o.count > 8) { atomicAdd(bad, 1ull); return; }
+    KadRes r;
+    r.count = o.count;
+    r.ready = 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { r.nodes[k] = o.nodes[k]; r.dist[k] = o.dist_hi[k]; }
+    res[o.tag] = r;
+}
+
+inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+size_t kad_lookup_state_bytes(int alpha)
+{
+    switch (alpha) {
+    case 1: return sizeof(KadLookup<1>);
+    case 2: return sizeof(KadLookup<2>);
+    case 3: return sizeof(KadLookup<3>);
+    default: return sizeof(KadLookup<4>);
+    }
+}
+
+hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
+                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+#define KI(a) hipLaunchKernelGGL(k_kad_shard_init<a>, dim3(nblk(n, 256)), dim3(256), 0, s, keys, src, n, qid_base, xy, \
+                                 (KadLookup<a>*)st, act, qids, res)
+    switch (alpha) {
+    case 1: KI(1); break;
+    case 2: KI(2); break;
+    case 3: KI(3); break;
+    default: KI(4); break;
+    }
+#undef KI
+    return hipGetLastError();
+}
+
+hipError_t kad_shard_step(const KadView& V, const DelayConsts& DC, const KadLC& LC, void* st, uint8_t* act,
+                          const uint32_t* qids, KadRes* res, uint64_t nlook, const uint64_t* shard_lo, int nsh,
+                          ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap, unsigned long long* out_count,
+                          ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                          unsigned long long* active_count, hipStream_t s)
+{
+    if (nlook == 0) return hipSuccess;
+#define KS(a) hipLaunchKernelGGL(k_kad_shard_step<a>, dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
+                                 (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, out, out_dest, out_cap, \
+                                 out_count, done, done_cap, done_count, active_count)
+    switch (LC.alpha) {
+    case 1: KS(1); break;
+    case 2: KS(2); break;
+    case 3: KS(3); break;
+    default: KS(4); break;
+    }
+#undef KS
+    return hipGetLastError();
+}
+
+hipError_t kad_shard_serve(const KadView& V, const KadLC& LC, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out,
+                           hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_kad_shard_serve, dim3(nblk(n, 128)), dim3(128), 0, s, V, LC, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t kad_shard_deliver(const ovs_kad_resp* in, uint64_t n, KadRes* res, uint64_t nslots,
+                             unsigned long long* bad, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_kad_shard_deliver, dim3(nblk(n, 256)), dim3(256), 0, s, in, n, res, nslots, bad);
+    return hipGetLastError();
+}
+
+}  // namespace ovs
