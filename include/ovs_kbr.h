@@ -271,6 +271,50 @@ ovs_status  ovs_shard_step(ovs_ctx* ctx, const ovs_lookup_rec* in, uint64_t n_in
                            unsigned long long* done_count, const uint64_t* shard_lo,
                            uint32_t nshards, void* stream);
 
+/* ---- multi-GPU Kademlia ----
+ * The sorted ring is cut into contiguous arcs (ID prefixes); a rank holds the
+ * sibling entries and bucket rows of its arc, while the 64 B node records and
+ * coordinates are replicated.  A lookup stays on the rank of its source; every
+ * FindNodeCall it sends becomes a request to the rank owning the responder, whose
+ * findNode result (Kademlia.cc:1101-1246) comes back before the lookup's next
+ * round -- before the simulated response is processed.  Per round the caller runs
+ * ovs_kad_shard_step, exchanges the requests (all-to-allv by out_dest),
+ * ovs_kad_shard_serve on what it received, sends the responses back with the
+ * reverse splits and hands them to ovs_kad_shard_deliver; it stops when the
+ * sum of *active_count over the ranks is 0.  All buffers are device memory. */
+typedef struct ovs_kad_req {        /* 32 B FindNodeCall */
+    uint32_t key[5];
+    uint32_t node;                  /* responder (global index, on the receiving rank's arc) */
+    uint32_t tag;                   /* opaque to the receiver; returned in the response */
+    uint32_t pad;
+} ovs_kad_req;
+
+typedef struct ovs_kad_resp {       /* 104 B FindNodeResponse */
+    uint32_t tag;
+    uint32_t count;                 /* result size, <= 8 */
+    uint32_t nodes[8];
+    uint64_t dist_hi[8];            /* top 64 bits of (node key XOR lookup key) */
+} ovs_kad_resp;
+
+/* Load arc [lo, hi) of a Kademlia network of n_total nodes (ids/xy of all nodes). */
+ovs_status  ovs_kad_load_shard(ovs_ctx* ctx, const ovs_key160* ids_all_sorted, uint64_t n_total,
+                               const double* xy_all, uint64_t lo, uint64_t hi, uint32_t flags);
+/* Start a batch of lookups whose sources lie on this arc (lookup id = qid_base + i). */
+ovs_status  ovs_kad_shard_begin(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                                uint32_t qid_base, void* stream);
+/* One round for this rank's lookups.  *out_count, *done_count, *active_count are
+ * device counters the kernel increments (the caller zeroes out_count and
+ * active_count before each round).  shard_lo: HOST array of nshards+1 arc bounds. */
+ovs_status  ovs_kad_shard_step(ovs_ctx* ctx, ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap,
+                               unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                               unsigned long long* done_count, unsigned long long* active_count,
+                               const uint64_t* shard_lo, uint32_t nshards, void* stream);
+/* findNode at the (local) responders of n received requests. */
+ovs_status  ovs_kad_shard_serve(ovs_ctx* ctx, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out,
+                                void* stream);
+/* Hand n responses (to this rank's requests) back to the waiting lookups. */
+ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const ovs_kad_resp* in, uint64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

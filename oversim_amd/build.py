@@ -27,7 +27,7 @@ CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
     "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value", "-Wno-bitwise-instead-of-logical",
 ]
-SOURCES = ["chord.hip", "kad.hip", "stats.hip", "ovs_kbr.cpp", "ovs_ini.cpp"]
+SOURCES = ["chord.hip", "kad.hip", "kad_shard.hip", "stats.hip", "ovs_kbr.cpp", "ovs_ini.cpp"]
 
 
 def _newer(target: Path, deps: list[Path]) -> bool:

@@ -381,15 +381,6 @@ hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_
     return e;
 }
 
-static KadView make_view(const KadTables& t, const double2* xy, uint32_t n)
-{
-    KadView V{};
-    V.recs = t.recs; V.xy = xy; V.sib = t.sib; V.sibe = t.sibe; V.slots = t.slots; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
-    V.lo = t.lo; V.hi = t.hi;
-    V.nsib = (int)((uint64_t)(n - 1) < (uint64_t)V.S5 ? n - 1 : (uint32_t)V.S5);
-    return V;
-}
-
 template <int A, bool RECORD>
 static int kad_blocks_per_cu()
 {
@@ -422,25 +413,9 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
 {
     (void)recs;
     if (nq == 0) return hipSuccess;
-    if (P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > MAXA || P.lookupRedundantNodes < 1 ||
-        P.lookupRedundantNodes > 8 || !P.lookupMerge || !P.lookupStrictParallelRpcs || P.numSiblings != 1 || t.k > 8 ||
-        P.hopCountMax > 0x7FFF)
-        return hipErrorNotSupported;
-    KadLC LC{};
-    LC.hopCountMax = P.hopCountMax;
-    LC.numSiblings = P.numSiblings;
-    LC.redundant = P.lookupRedundantNodes;
-    LC.alpha = P.lookupParallelRpcs;
-    LC.strict = P.lookupStrictParallelRpcs;
-    LC.visitOnlyOnce = P.lookupVisitOnlyOnce;
-    LC.acceptLateSiblings = P.lookupAcceptLateSiblings;
-    LC.useAll = P.lookupUseAllParallelResponses;
-    LC.merge = P.lookupMerge;
-    LC.newOnResp = P.lookupNewRpcOnEveryResponse;
-    LC.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
-    LC.finishOnFirst = P.lookupFinishOnFirstUnchanged;
-    LC.maxRedundantLocal = t.k;
-    const KadView V = make_view(t, xy, n);
+    if (!kad_params_supported(P, t)) return hipErrorNotSupported;
+    const KadLC LC = kad_make_lc(P, t);
+    const KadView V = kad_make_view(t, xy, n);
     // strictParallelRpcs: never more than alpha FindNodeCalls in flight (IterativeLookup.cc:1078-1079)
     const int A = P.lookupParallelRpcs;
 #define KL(a) (hopseq ? kad_launch<a, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st) \
@@ -461,7 +436,7 @@ hipError_t kad_find_node(const KadTables& t, const KeyRec* recs, uint32_t n, con
     (void)recs; (void)P;
     if (nq == 0) return hipSuccess;
     if (numSiblings != 1 || numRedundant > 16) return hipErrorNotSupported;
-    const KadView V = make_view(t, nullptr, n);
+    const KadView V = kad_make_view(t, nullptr, n);
     hipLaunchKernelGGL(k_kad_find_node, dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, numRedundant, out_nodes,
                        max_out, out_count, out_sib);
     return hipGetLastError();

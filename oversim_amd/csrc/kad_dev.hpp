@@ -471,4 +471,43 @@ __device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A>& L
     return o;
 }
 
+// ---------------------------------------------------------------------------
+// host helpers shared by the single-GPU and sharded launchers
+
+inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
+{
+    KadView V{};
+    V.recs = t.recs; V.xy = xy; V.sib = t.sib; V.sibe = t.sibe; V.slots = t.slots; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
+    V.lo = t.lo; V.hi = t.hi;
+    V.nsib = (int)((uint64_t)(n - 1) < (uint64_t)V.S5 ? n - 1 : (uint32_t)V.S5);
+    return V;
+}
+
+// the lookup configurations the K2 state machine implements (others: OVS_ENOTSUP)
+inline bool kad_params_supported(const ovs_params& P, const KadTables& t)
+{
+    return P.lookupParallelRpcs >= 1 && P.lookupParallelRpcs <= MAXA && P.lookupRedundantNodes >= 1 &&
+           P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings == 1 &&
+           t.k <= 8 && P.hopCountMax <= 0x7FFF;
+}
+
+inline KadLC kad_make_lc(const ovs_params& P, const KadTables& t)
+{
+    KadLC LC{};
+    LC.hopCountMax = P.hopCountMax;
+    LC.numSiblings = P.numSiblings;
+    LC.redundant = P.lookupRedundantNodes;
+    LC.alpha = P.lookupParallelRpcs;
+    LC.strict = P.lookupStrictParallelRpcs;
+    LC.visitOnlyOnce = P.lookupVisitOnlyOnce;
+    LC.acceptLateSiblings = P.lookupAcceptLateSiblings;
+    LC.useAll = P.lookupUseAllParallelResponses;
+    LC.merge = P.lookupMerge;
+    LC.newOnResp = P.lookupNewRpcOnEveryResponse;
+    LC.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
+    LC.finishOnFirst = P.lookupFinishOnFirstUnchanged;
+    LC.maxRedundantLocal = t.k;
+    return LC;
+}
+
 }  // namespace ovs

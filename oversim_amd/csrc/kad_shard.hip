@@ -186,6 +186,8 @@ inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 
 }  // namespace
 
+bool kad_params_supported_host(const ovs_params& P, const KadTables& t) { return kad_params_supported(P, t); }
+
 size_t kad_lookup_state_bytes(int alpha)
 {
     switch (alpha) {
@@ -212,13 +214,16 @@ hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint
     return hipGetLastError();
 }
 
-hipError_t kad_shard_step(const KadView& V, const DelayConsts& DC, const KadLC& LC, void* st, uint8_t* act,
-                          const uint32_t* qids, KadRes* res, uint64_t nlook, const uint64_t* shard_lo, int nsh,
-                          ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap, unsigned long long* out_count,
-                          ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
-                          unsigned long long* active_count, hipStream_t s)
+hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
+                          const DelayConsts& DC, void* st, uint8_t* act, const uint32_t* qids, KadRes* res,
+                          uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
+                          uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                          unsigned long long* done_count, unsigned long long* active_count, hipStream_t s)
 {
+    if (!kad_params_supported(P, t)) return hipErrorNotSupported;
     if (nlook == 0) return hipSuccess;
+    const KadView V = kad_make_view(t, xy, n);
+    const KadLC LC = kad_make_lc(P, t);
 #define KS(a) hipLaunchKernelGGL(k_kad_shard_step<a>, dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
                                  (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, out, out_dest, out_cap, \
                                  out_count, done, done_cap, done_count, active_count)
@@ -232,11 +237,14 @@ hipError_t kad_shard_step(const KadView& V, const DelayConsts& DC, const KadLC& 
     return hipGetLastError();
 }
 
-hipError_t kad_shard_serve(const KadView& V, const KadLC& LC, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out,
-                           hipStream_t s)
+hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
+                           ovs_kad_resp* out, hipStream_t s)
 {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_kad_shard_serve, dim3(nblk(n, 128)), dim3(128), 0, s, V, LC, in, n, out);
+    if (!kad_params_supported(P, t)) return hipErrorNotSupported;
+    if (nreq == 0) return hipSuccess;
+    const KadView V = kad_make_view(t, nullptr, n);
+    const KadLC LC = kad_make_lc(P, t);
+    hipLaunchKernelGGL(k_kad_shard_serve, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
     return hipGetLastError();
 }
 

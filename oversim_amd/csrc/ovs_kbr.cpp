@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "kad.hpp"
+#include "kad_shard.hpp"
 #include "launch.hpp"
 #include "stats.hpp"
 
@@ -42,6 +43,14 @@ struct ovs_ctx {
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     // kademlia
     KadTables kad{};
+    // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
+    void* kst = nullptr;                 // KadLookup<alpha> state records
+    uint8_t* kact = nullptr;             // 0 done, 1 running, 2 not started
+    uint32_t* kqids = nullptr;
+    KadRes* kres = nullptr;              // alpha findNode result slots per lookup
+    unsigned long long* kbad = nullptr;  // undeliverable responses
+    uint64_t knlook = 0, kcap = 0;
+    int kalpha = 0;
     // scratch for host-pointer calls
     std::vector<void*> scratch;
 };
@@ -74,6 +83,15 @@ void free_tables(ovs_ctx* c)
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
     c->overlay = 0; c->n = 0; c->nfing = 0;
+}
+
+void free_kad_shard(ovs_ctx* c)
+{
+    void* ptrs[] = {c->kst, c->kact, c->kqids, c->kres, c->kbad};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    c->kst = nullptr; c->kact = nullptr; c->kqids = nullptr; c->kres = nullptr; c->kbad = nullptr;
+    c->knlook = 0; c->kcap = 0; c->kalpha = 0;
 }
 
 void free_scratch(ovs_ctx* c)
@@ -273,6 +291,7 @@ void ovs_ctx_destroy(ovs_ctx* c)
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     free_tables(c);
+    free_kad_shard(c);
     free_scratch(c);
     if (c->d_bounds) hipFree(c->d_bounds);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -448,20 +467,115 @@ ovs_status ovs_chord_export_fingers(ovs_ctx* c, uint32_t* out)
     return OVS_OK;
 }
 
-ovs_status ovs_kad_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint32_t flags)
+static ovs_status kad_load_arc(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint64_t lo,
+                               uint64_t hi, uint32_t flags)
 {
     if (!c || !ids || !xy) return OVS_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     free_tables(c);
+    free_kad_shard(c);
     if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
     if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
     if (c->P.k < 1 || c->P.k > 32 || c->P.s < 1 || 5 * c->P.s > 64)
         return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..32 and 5*s <= 64");
+    if (lo >= hi || hi > n) return fail(c, OVS_EINVAL, "arc [lo, hi) must be a non-empty part of [0, n)");
     ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
     if (s != OVS_OK) { free_tables(c); return s; }
-    hipError_t e = kad_build(c->recs, (uint32_t)n, c->P.k, c->P.s, c->P.kadSeed, c->kad, c->stream);
+    hipError_t e = kad_build(c->recs, (uint32_t)n, c->P.k, c->P.s, c->P.kadSeed, c->kad, c->stream, (uint32_t)lo,
+                             (uint32_t)hi);
     if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "kademlia table build"); }
     c->overlay = OVS_OVERLAY_KADEMLIA;
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint32_t flags)
+{
+    return kad_load_arc(c, ids, n, xy, 0, n, flags);
+}
+
+ovs_status ovs_kad_load_shard(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint64_t lo,
+                              uint64_t hi, uint32_t flags)
+{
+    return kad_load_arc(c, ids, n, xy, lo, hi, flags);
+}
+
+ovs_status ovs_kad_shard_begin(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
+                               void* stream)
+{
+    if (!c || (n && (!keys || !src))) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    ovs_status st = check_common(c, c->P);
+    if (st != OVS_OK) return st;
+    if (c->P.routingType != 0) return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
+    if (!kad_params_supported_host(c->P, c->kad)) return fail(c, OVS_ENOTSUP, "lookup configuration not implemented");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int alpha = c->P.lookupParallelRpcs;
+    if (n > c->kcap || alpha != c->kalpha) {
+        free_kad_shard(c);
+        const uint64_t cap = n ? n : 1;
+        HIPCHK(c, hipMalloc(&c->kst, kad_lookup_state_bytes(alpha) * cap));
+        HIPCHK(c, hipMalloc(&c->kact, cap));
+        HIPCHK(c, hipMalloc(&c->kqids, sizeof(uint32_t) * cap));
+        HIPCHK(c, hipMalloc(&c->kres, sizeof(KadRes) * cap * alpha));
+        HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
+        c->kcap = cap;
+        c->kalpha = alpha;
+    }
+    c->knlook = n;
+    HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
+    HIPCHK(c, kad_shard_init(alpha, reinterpret_cast<const K160*>(keys), src, n, qid_base, c->xy, c->kst, c->kact,
+                             c->kqids, c->kres, s));
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap,
+                              unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                              unsigned long long* done_count, unsigned long long* active_count,
+                              const uint64_t* shard_lo, uint32_t nshards, void* stream)
+{
+    if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
+    if (!out || !out_dest || !out_count || !done || !done_count || !active_count) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (c->P.lookupParallelRpcs != c->kalpha && c->knlook)
+        return fail(c, OVS_ESTATE, "lookupParallelRpcs changed since ovs_kad_shard_begin");
+    uint64_t lo_h[MAXSHARDS + 1];
+    for (uint32_t r = 0; r <= nshards; ++r) {
+        lo_h[r] = shard_lo[r];
+        if (r > 0 && shard_lo[r] < shard_lo[r - 1]) return fail(c, OVS_EINVAL, "shard_lo must be non-decreasing");
+    }
+    if (shard_lo[0] != 0 || shard_lo[nshards] != c->n) return fail(c, OVS_EINVAL, "shard_lo must cover [0, n)");
+    bool mine = false;
+    for (uint32_t r = 0; r < nshards; ++r) mine |= shard_lo[r] == c->kad.lo && shard_lo[r + 1] == c->kad.hi;
+    if (!mine) return fail(c, OVS_EINVAL, "this context's arc is not one of shard_lo's arcs");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
+    HIPCHK(c, hipMemcpyAsync(c->d_bounds, lo_h, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice, s));
+    hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kqids,
+                                  c->kres, c->knlook, c->d_bounds, (int)nshards, out, out_dest, out_cap, out_count,
+                                  done, done_cap, done_count, active_count, s);
+    if (e != hipSuccess) return hip_fail(c, e, "kademlia shard step");
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_shard_serve(ovs_ctx* c, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out, void* stream)
+{
+    if (!c || (n && (!in || !out))) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipError_t e = kad_shard_serve(c->kad, (uint32_t)c->n, c->P, in, n, out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(c, e, "kademlia shard serve");
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const ovs_kad_resp* in, uint64_t n, void* stream)
+{
+    if (!c || (n && !in)) return OVS_EINVAL;
+    if (!c->kres) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipError_t e = kad_shard_deliver(in, n, c->kres, c->knlook * (uint64_t)c->kalpha, c->kbad, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(c, e, "kademlia shard deliver");
     return OVS_OK;
 }
 
@@ -469,6 +583,7 @@ ovs_status ovs_kad_export(ovs_ctx* c, uint32_t* siblings, uint8_t* bucket_count,
 {
     if (!c || !siblings || !bucket_count || !bucket_nodes) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "export needs the whole network");
     HIPCHK(c, hipSetDevice(c->device));
     hipError_t e = kad_export(c->kad, (uint32_t)c->n, siblings, bucket_count, bucket_nodes, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia export");
@@ -493,6 +608,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             return fail(c, OVS_ESTATE, "context holds one arc of a sharded ring: use ovs_shard_step");
     } else if (c->P.routingType != 0) {
         return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
+    } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
+        return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: use ovs_kad_shard_step");
     }
     if (n == 0) return OVS_OK;
     // stage inputs

@@ -129,6 +129,12 @@ for _name, _args in {
     "ovs_shard_make_records": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p],
     "ovs_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
+    "ovs_kad_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
+    "ovs_kad_shard_begin": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p],
+    "ovs_kad_shard_step": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
+    "ovs_kad_shard_serve": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p],
+    "ovs_kad_shard_deliver": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
 }.items():
     _f = getattr(lib(), _name)
     _f.argtypes = _args
@@ -139,7 +145,7 @@ for _name, _args in {
 # exchanges
 
 class TorchExchange:
-    """all-to-allv of lookup records over torch.distributed (RCCL on GPUs, gloo on CPU)."""
+    """all-to-allv of fixed-size records over torch.distributed (RCCL on GPUs, gloo on CPU)."""
 
     def __init__(self, world: int, device, group=None):
         import torch
@@ -147,19 +153,31 @@ class TorchExchange:
         self.torch, self.dist, self.world, self.group = torch, dist, world, group
         self.comm_dev = device   # tensors handed to the collective live here
 
-    def exchange(self, send, send_counts):
+    def counts(self, send_counts):
+        """Exchange per-destination counts; returns (send counts, receive counts) as lists."""
         torch, dist = self.torch, self.dist
         sc = send_counts.to(self.comm_dev, dtype=torch.int64)
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
-        total = sc.sum().reshape(1)
-        dist.all_reduce(total, group=self.group)
-        if int(total.item()) == 0:
-            return None
-        rcl, scl = rc.tolist(), sc.tolist()
-        recv = torch.empty((sum(rcl), REC_BYTES), dtype=torch.uint8, device=self.comm_dev)
+        return sc.tolist(), rc.tolist()
+
+    def records(self, send, scl, rcl):
+        """all-to-allv of rows of `send` (uint8, one record per row) with explicit splits."""
+        torch, dist = self.torch, self.dist
+        recv = torch.empty((sum(rcl), send.shape[1]), dtype=torch.uint8, device=self.comm_dev)
         dist.all_to_all_single(recv, send.to(self.comm_dev), rcl, scl, group=self.group)
         return recv
+
+    def total(self, x: int) -> int:
+        t = self.torch.tensor([x], dtype=self.torch.int64, device=self.comm_dev)
+        self.dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def exchange(self, send, send_counts):
+        scl, rcl = self.counts(send_counts)
+        if self.total(sum(scl)) == 0:
+            return None
+        return self.records(send, scl, rcl)
 
 
 def group_by_dest(out, dest, world: int):
@@ -215,6 +233,167 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
         inbox = [torch.cat(b) if b else torch.empty((0, REC_BYTES), dtype=torch.uint8, device=dev) for b in buckets]
         if rounds > max_rounds:
             raise RuntimeError("sharded routing did not terminate")
+    return [s.finished() for s in steppers], rounds
+
+
+# ---------------------------------------------------------------------------
+# Kademlia: lookups stay home, FindNodeCalls are requests to the responder's owner
+
+KAD_REQ_BYTES, KAD_RESP_BYTES = 32, 104
+
+
+class KadShardStepper:
+    """One rank's arc of a Kademlia network on one device (ovs_kad_load_shard + shard kernels)."""
+
+    def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device,
+                 params: Params | None = None):
+        import torch
+        self.torch, self.dev = torch, device
+        self.rank, self.bounds, self.world = rank, [int(b) for b in bounds], len(bounds) - 1
+        self.eng = KbrEngine(device.index if device.index is not None else 0)
+        self.params = params or Params.kademlia()
+        self.eng.set_params(self.params)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        xy = np.ascontiguousarray(xy, dtype=np.float64)
+        st = lib().ovs_kad_load_shard(self.eng._h, ids.ctypes.data_as(C.c_void_p), len(ids),
+                                      xy.ctypes.data_as(C.c_void_p), self.bounds[rank], self.bounds[rank + 1], 0)
+        self.eng._chk(st, "ovs_kad_load_shard")
+        self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
+        self.counters = torch.zeros(3, dtype=torch.int64, device=device)   # out, done, active
+        self.n = 0
+        self.timing = False
+        self.kernel_ms = 0.0
+        self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def _s(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _p(self, t, off=0):
+        return C.c_void_p(t.data_ptr() + off)
+
+    def begin(self, keys_t, src_t, qid_base: int):
+        torch = self.torch
+        n = keys_t.shape[0]
+        self.n = n
+        a = self.params.lookupParallelRpcs
+        # one round sends at most alpha requests per lookup (a request occupies a pending slot
+        # until its result is delivered at the end of the round)
+        self.cap = max(n * a, 1)
+        self.out = torch.empty((self.cap, KAD_REQ_BYTES), dtype=torch.uint8, device=self.dev)
+        self.out_dest = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
+        self.done = torch.empty((max(n, 1), DONE_BYTES), dtype=torch.uint8, device=self.dev)
+        self.counters.zero_()
+        st = lib().ovs_kad_shard_begin(self.eng._h, self._p(keys_t), self._p(src_t), n, qid_base, self._s())
+        self.eng._chk(st, "ovs_kad_shard_begin")
+
+    def step(self):
+        """One round: returns (requests, destination ranks, active lookups on this rank)."""
+        self.counters[0].zero_()
+        self.counters[2].zero_()
+        if self.timing:
+            self._ev[0].record()
+        st = lib().ovs_kad_shard_step(self.eng._h, self._p(self.out), self._p(self.out_dest), self.cap,
+                                      self._p(self.counters), self._p(self.done), self.done.shape[0],
+                                      self._p(self.counters, 8), self._p(self.counters, 16), self._lo, self.world,
+                                      self._s())
+        self.eng._chk(st, "ovs_kad_shard_step")
+        if self.timing:
+            self._ev[1].record()
+        c = self.counters.tolist()
+        if self.timing:
+            self.kernel_ms += self._ev[0].elapsed_time(self._ev[1])
+        if c[0] > self.cap:
+            raise RuntimeError("kademlia request buffer overflow")
+        return self.out[:c[0]], self.out_dest[:c[0]], c[2]
+
+    def serve(self, reqs):
+        n = reqs.shape[0]
+        resp = self.torch.empty((n, KAD_RESP_BYTES), dtype=self.torch.uint8, device=self.dev)
+        if n:
+            if self.timing:
+                self._ev[2].record()
+            st = lib().ovs_kad_shard_serve(self.eng._h, self._p(reqs), n, self._p(resp), self._s())
+            self.eng._chk(st, "ovs_kad_shard_serve")
+            if self.timing:
+                self._ev[3].record()
+                self._ev[3].synchronize()
+                self.kernel_ms += self._ev[2].elapsed_time(self._ev[3])
+        return resp
+
+    def deliver(self, resps):
+        if resps.shape[0]:
+            st = lib().ovs_kad_shard_deliver(self.eng._h, self._p(resps), resps.shape[0], self._s())
+            self.eng._chk(st, "ovs_kad_shard_deliver")
+
+    def finished(self):
+        k = int(self.counters[1].item())
+        if k > self.done.shape[0]:
+            raise RuntimeError("done buffer overflow")
+        return self.done[:k]
+
+
+def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 100_000):
+    """Route this rank's Kademlia lookups; 2 all-to-allv per round (requests, responses)."""
+    stepper.begin(keys_t, src_t, qid_base)
+    rounds = 0
+    while True:
+        rounds += 1
+        out, dest, active = stepper.step()
+        send, counts = group_by_dest(out, dest, exchange.world)
+        scl, rcl = exchange.counts(counts)
+        if exchange.total(sum(scl) + active) == 0:
+            break
+        reqs = exchange.records(send, scl, rcl)
+        resps = stepper.serve(reqs.to(stepper.dev))
+        back = exchange.records(resps, rcl, scl)          # reverse splits: back to the requesters
+        stepper.deliver(back.to(stepper.dev))
+        if rounds > max_rounds:
+            raise RuntimeError("sharded Kademlia routing did not terminate")
+    return stepper.finished(), rounds
+
+
+def route_kad_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_rounds: int = 100_000):
+    """Single-process emulation of W Kademlia ranks (W contexts on one device)."""
+    import torch
+    W = len(steppers)
+    for r in range(W):
+        steppers[r].begin(keys_per_shard[r], src_per_shard[r], qid_bases[r])
+    rounds = 0
+    while True:
+        rounds += 1
+        sends, active = [], 0
+        for r in range(W):
+            out, dest, act = steppers[r].step()
+            active += act
+            send, counts = group_by_dest(out, dest, W)
+            sends.append((send, counts.tolist()))
+        if active == 0 and all(sum(c) == 0 for _, c in sends):
+            break
+        # requests to owners
+        inbox = [[] for _ in range(W)]           # (source rank, rows)
+        for r, (send, counts) in enumerate(sends):
+            off = 0
+            for d, c in enumerate(counts):
+                inbox[d].append((r, send[off:off + c]))
+                off += c
+        replies = [[None] * W for _ in range(W)]  # replies[src][owner]
+        for d in range(W):
+            rows = torch.cat([x for _, x in inbox[d]]) if inbox[d] else None
+            if rows is None or rows.shape[0] == 0:
+                for r, x in inbox[d]:
+                    replies[r][d] = x.new_empty((0, KAD_RESP_BYTES))
+                continue
+            resp = steppers[d].serve(rows)
+            off = 0
+            for r, x in inbox[d]:
+                replies[r][d] = resp[off:off + x.shape[0]]
+                off += x.shape[0]
+        for r in range(W):
+            parts = [x for x in replies[r] if x is not None and x.shape[0]]
+            if parts:
+                steppers[r].deliver(torch.cat(parts))
+        if rounds > max_rounds:
+            raise RuntimeError("sharded Kademlia routing did not terminate")
     return [s.finished() for s in steppers], rounds
 
 

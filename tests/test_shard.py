@@ -228,3 +228,207 @@ def test_two_processes_share_one_gpu_gloo():
     ref = _single_gpu_reference(net, np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res]))
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+
+
+# ------------------------------------------------------------- Kademlia request/response
+
+class FakeKadStepper:
+    """Protocol double for route_kad_sharded: lookup i queries the nodes plan[i] one after the
+    other; each query is a request to the node's owner, answered with a value derived from
+    (node, key) that the requester checks.  Exercises grouping, both all-to-allv directions
+    (reverse splits), delivery by tag and termination -- without a GPU."""
+
+    def __init__(self, bounds, rank, n_nodes, seed):
+        self.bounds, self.rank, self.world = bounds, rank, len(bounds) - 1
+        self.dev = torch.device("cpu")
+        self.rng = np.random.default_rng(seed)
+        self.n_nodes = n_nodes
+        self.served = 0
+
+    def owner(self, c):
+        return int(np.searchsorted(self.bounds, c, side="right") - 1)
+
+    def begin(self, keys_t, src_t, qid_base):
+        n = keys_t.shape[0]
+        self.keys = keys_t.numpy()
+        self.plan = [list(self.rng.integers(0, self.n_nodes, int(self.rng.integers(1, 6)))) for _ in range(n)]
+        self.pos = [0] * n
+        self.waiting = [False] * n
+        self.acc = [0] * n
+        self.qid_base = qid_base
+        self.done = []
+
+    def step(self):
+        out, dest, active = [], [], 0
+        for i in range(len(self.plan)):
+            if self.waiting[i] or self.pos[i] < 0:
+                if self.waiting[i]:
+                    active += 1
+                continue
+            if self.pos[i] == len(self.plan[i]):
+                self.done.append((self.qid_base + i, self.acc[i]))
+                self.pos[i] = -1
+                continue
+            node = int(self.plan[i][self.pos[i]])
+            rec = np.zeros(8, np.uint32)
+            rec[:5] = self.keys[i]
+            rec[5], rec[6] = node, i
+            out.append(rec.view(np.uint8))
+            dest.append(self.owner(node))
+            self.waiting[i] = True
+            active += 1
+        o = torch.from_numpy(np.stack(out)) if out else torch.zeros((0, 32), dtype=torch.uint8)
+        return o, torch.tensor(dest, dtype=torch.int32), active
+
+    def serve(self, reqs):
+        r = reqs.numpy().view(np.uint32).reshape(-1, 8)
+        resp = np.zeros((len(r), 26), np.uint32)
+        for j, q in enumerate(r):
+            assert self.bounds[self.rank] <= q[5] < self.bounds[self.rank + 1], "request at the wrong owner"
+            resp[j, 0] = q[6]
+            resp[j, 1] = (int(q[5]) * 2654435761 + int(q[0])) & 0xFFFFFFFF
+        self.served += len(r)
+        return torch.from_numpy(resp.view(np.uint8).reshape(-1, 104).copy())
+
+    def deliver(self, resps):
+        r = resps.numpy().view(np.uint32).reshape(-1, 26)
+        for q in r:
+            i = int(q[0])
+            node = int(self.plan[i][self.pos[i]])
+            assert q[1] == (node * 2654435761 + int(self.keys[i][0])) & 0xFFFFFFFF, "response for another query"
+            self.acc[i] = (self.acc[i] * 31 + int(q[1])) & 0xFFFFFFFF
+            self.pos[i] += 1
+            self.waiting[i] = False
+
+    def finished(self):
+        return self.done
+
+
+def _expected_acc(keys, plan):
+    acc = 0
+    for node in plan:
+        acc = (acc * 31 + ((int(node) * 2654435761 + int(keys[0])) & 0xFFFFFFFF)) & 0xFFFFFFFF
+    return acc
+
+
+def _kad_cpu_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oversim_amd.shard import TorchExchange, arc_bounds, route_kad_sharded
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_nodes, m = 1000, 200
+    bounds = arc_bounds(n_nodes, world)
+    keys = W.random_keys(m, np.random.default_rng(50 + rank))
+    st = FakeKadStepper(bounds, rank, n_nodes, 60 + rank)
+    done, rounds = route_kad_sharded(st, TorchExchange(world, torch.device("cpu")), torch.from_numpy(keys),
+                                     torch.zeros(m, dtype=torch.int32), rank * m)
+    q.put((rank, done, [list(map(int, p)) for p in st.plan], keys, rounds, st.served))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_kad_request_response_orchestration_gloo_cpu():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kad_cpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total_q = sum(len(pl) for r in res for pl in r[2])
+    assert sum(r[5] for r in res) == total_q                  # every query served exactly once
+    longest = max(len(pl) for r in res for pl in r[2])
+    for rank, done, plan, keys, rounds, _ in res:
+        assert rounds == longest + 1                          # one round per query + the finishing step
+        got = dict(done)
+        assert len(got) == len(plan)
+        for i, p in enumerate(plan):
+            assert got[rank * len(plan) + i] == _expected_acc(keys[i], p)
+
+
+def _kad_reference(net, keys, src, params):
+    from oversim_amd import KbrEngine
+    with KbrEngine(0) as e:
+        e.set_params(params)
+        e.kad_load(net.ids, net.xy)
+        return e.lookup(keys, src, count_rpcs=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,alpha,n", [(2, 1, 15000), (3, 3, 15000), (8, 3, 1 << 16), (4, 2, 1 << 16)])
+def test_kad_shards_emulated_on_one_gpu(world, alpha, n):
+    """W arcs in one process: every lookup's result equals the single-GPU kernel's."""
+    from oversim_amd import Params
+    from oversim_amd.shard import KadShardStepper, arc_bounds, done_to_numpy, route_kad_local_shards
+    m = 4000
+    net = W.population(n, 97)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=alpha)
+    steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params) for r in range(world)]
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s = W.lookups(net.ids, m, 98 + r, node_ids=(r % 2 == 0))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k.view(np.int32)).to(dev))
+        ss.append(torch.from_numpy(s.view(np.int32)).to(dev))
+        qb.append(r * m)
+        allk.append(k); alls.append(s)
+    dones, rounds = route_kad_local_shards(steppers, ks, ss, qb)
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    ref = _kad_reference(net, np.concatenate(allk), np.concatenate(alls), params)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    assert rounds >= 3
+
+
+def _kad_gpu_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oversim_amd import Params
+    from oversim_amd.shard import KadShardStepper, TorchExchange, arc_bounds, done_to_numpy, route_kad_sharded
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, m = 1 << 15, 3000
+    net = W.population(n, 99)
+    bounds = arc_bounds(n, world)
+    k, s = W.lookups(net.ids, m, 100 + rank, node_ids=False)
+    s = (bounds[rank] + s.astype(np.int64) % (bounds[rank + 1] - bounds[rank])).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    st = KadShardStepper(net.ids, net.xy, bounds, rank, dev, params=Params.kademlia())
+    done, rounds = route_kad_sharded(st, TorchExchange(world, torch.device("cpu")),
+                                     torch.from_numpy(k.view(np.int32)).to(dev),
+                                     torch.from_numpy(s.view(np.int32)).to(dev), rank * m)
+    q.put((rank, done_to_numpy(done), k, s))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_kad_two_processes_share_one_gpu_gloo():
+    import torch.multiprocessing as mp
+    from oversim_amd import Params
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kad_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    d = np.concatenate([r[1] for r in res])
+    d = d[np.argsort(d["qid"])]
+    net = W.population(1 << 15, 99)
+    ref = _kad_reference(net, np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res]),
+                         Params.kademlia())
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
