@@ -62,7 +62,7 @@ WL = {
     "B": dict(overlay="kademlia", nodes=15000, per_gpu_nodes=False, lookups=1_000_000, node_ids=True, alpha=1,
               desc="B: Kademlia 15000 nodes (nodes_2d_15000.xml), k=8, alpha=1, 1M node-ID lookups per GPU"),
     "E": dict(overlay="kademlia", nodes=1 << 24, per_gpu_nodes=False, lookups=4_000_000, node_ids=False, alpha=3,
-              desc="E: Kademlia 2^24 nodes, k=8, alpha=3, 4M random-key lookups per GPU (replicas for N>1)"),
+              desc="E: Kademlia 2^24 nodes, k=8, alpha=3, 4M random-key lookups per GPU (ID arcs sharded over GPUs)"),
 }
 
 
@@ -144,7 +144,7 @@ def main():
     if routing_type:
         wl["desc"] = wl["desc"].replace("iterative", "semi-recursive")
     stream = torch.cuda.Stream(device=dev)
-    sharded = kind == "chord" and world > 1
+    sharded = world > 1 and (kind == "chord" or os.environ.get("OVS_KAD_REPLICAS") != "1")
     small = n_total <= (1 << 22)
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
@@ -173,13 +173,18 @@ def main():
 
     # ---- engine
     if sharded:
-        from oversim_amd.shard import ShardedChord
+        from oversim_amd.shard import ShardedChord, ShardedKademlia
         ids_np = ids if ids is not None else ids_t.cpu().numpy().view(np.uint32)
         xy_np = xy if xy is not None else xy_t.cpu().numpy()
         comm = dev if backend == "nccl" else torch.device("cpu")
-        sh = ShardedChord(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
-                          params=Params.chord().replace(routingType=routing_type))
-        kname = "k_chord_shard_step"
+        if kind == "chord":
+            sh = ShardedChord(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
+                              params=Params.chord().replace(routingType=routing_type))
+            kname = "k_chord_shard_step"
+        else:
+            sh = ShardedKademlia(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
+                                 params=Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
+            kname = "k_kad_shard"
 
         def step():
             sh.run()
@@ -227,6 +232,8 @@ def main():
     if sharded:
         hop_total, n_ok = sh.hop_total(), sh.ok_total()
         kern_ms = sh.kernel_ms / max(sh.runs, 1)
+        if kind == "kademlia":
+            rpc_total = sh.served     # FindNodeCalls answered by this rank's tables
     else:
         outs = dout.cpu().numpy().reshape(-1, 16)
         hop_total = int(outs[:, 4:6].copy().view(np.uint16).astype(np.int64).sum())
@@ -258,8 +265,10 @@ def main():
         if world == 1 and not a.no_cpu_baseline and small:
             cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type)
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
-               "hopCountMax": 50, "parallelism": (f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)"
-                                                  if sharded else ("replicas" if world > 1 else "1 GPU")),
+               "hopCountMax": 50,
+               "parallelism": ((f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)" if kind == "chord"
+                                else f"ID arcs over {world} GPUs, FindNodeCall request/response all-to-allv per round")
+                               if sharded else ("replicas" if world > 1 else "1 GPU")),
                "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1)}
         if kind == "kademlia":
             cfg.update({"k": 8, "alpha": wl["alpha"], "rpcs_per_s": rpc_all * a.steps / wall_max,

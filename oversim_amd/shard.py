@@ -261,6 +261,7 @@ class KadShardStepper:
         self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
         self.counters = torch.zeros(3, dtype=torch.int64, device=device)   # out, done, active
         self.n = 0
+        self.served = 0   # FindNodeCalls answered by this rank (requests served)
         self.timing = False
         self.kernel_ms = 0.0
         self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -308,6 +309,7 @@ class KadShardStepper:
 
     def serve(self, reqs):
         n = reqs.shape[0]
+        self.served += n
         resp = self.torch.empty((n, KAD_RESP_BYTES), dtype=self.torch.uint8, device=self.dev)
         if n:
             if self.timing:
@@ -432,3 +434,35 @@ class ShardedChord:
     def ok_total(self) -> int:
         d = done_to_numpy(self._done)
         return int((d["status"] == 0).sum())
+
+
+class ShardedKademlia:
+    """bench.py driver for one rank: Kademlia arc + lookups resident in HBM + request/response exchange."""
+
+    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None):
+        self.bounds = arc_bounds(len(ids), world)
+        self.stepper = KadShardStepper(ids, xy, self.bounds, rank, device, params=params)
+        self.stepper.timing = True
+        self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)
+        self.keys_t, self.src_t = keys_t, src_t
+        self.qid_base = rank * keys_t.shape[0]
+        self._done = None
+        self.rounds = 0
+        self.runs = 0
+        self.kernel_ms = 0.0
+        self.served = 0
+
+    def run(self):
+        self.stepper.kernel_ms = 0.0
+        self.stepper.served = 0
+        self._done, self.rounds = route_kad_sharded(self.stepper, self.exchange, self.keys_t, self.src_t,
+                                                    self.qid_base)
+        self.runs += 1
+        self.kernel_ms += self.stepper.kernel_ms
+        self.served = self.stepper.served
+
+    def hop_total(self) -> int:
+        return int(done_to_numpy(self._done)["hops"].astype(np.int64).sum())
+
+    def ok_total(self) -> int:
+        return int((done_to_numpy(self._done)["status"] == 0).sum())

@@ -24,7 +24,7 @@ def _built():
     yield
 
 
-@pytest.fixture(scope="session")
+@pytest.fixture()
 def engine():
     import torch  # noqa: F401  (device visibility check only)
     from oversim_amd import KbrEngine
