@@ -50,7 +50,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0xC)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-csv", default=None, help="rocprofv3 --pmc counter_collection.csv file(s), comma separated")
+    ap.add_argument("--traffic-csv", default=None,
+                    help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE outputs (counter_collection.csv or run_results.db), "
+                         "comma separated")
     return ap.parse_args()
 
 
@@ -90,21 +92,36 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
 
 def traffic_from_csv(path: str | None, kernel_substr: str):
     """HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs (KB units;
-    gfx950 FETCH_SIZE tallies 128-B requests as 64 B -> x2 on the read side, MI355X_MICROARCH.md §HBM)."""
+    gfx950 FETCH_SIZE tallies 128-B requests as 64 B -> x2 on the read side, MI355X_MICROARCH.md §HBM).
+    Accepts rocprofv3 counter_collection.csv files or its SQLite run_results.db files, comma separated."""
     if not path:
         return None
     import csv
+    import sqlite3
     tot, n = {}, {}
+
+    def add(kernel, counter, value):
+        if kernel_substr not in kernel:
+            return
+        tot[counter] = tot.get(counter, 0.0) + float(value)
+        n[counter] = n.get(counter, 0) + 1
+
     for p in path.split(","):
         if not Path(p).exists():
             continue
-        with open(p) as f:
-            for row in csv.DictReader(f):
-                if kernel_substr not in row.get("Kernel_Name", ""):
-                    continue
-                c = row.get("Counter_Name")
-                tot[c] = tot.get(c, 0.0) + float(row.get("Counter_Value", 0))
-                n[c] = n.get(c, 0) + 1
+        if p.endswith(".db"):
+            c = sqlite3.connect(p)
+            try:
+                for kname, counter, value in c.execute(
+                        "select k.name, e.counter_name, sum(e.counter_value) from pmc_events e join kernels k "
+                        "on k.dispatch_id = e.dispatch_id group by e.dispatch_id, e.counter_name"):
+                    add(kname, counter, value)
+            finally:
+                c.close()
+        else:
+            with open(p) as f:
+                for row in csv.DictReader(f):
+                    add(row.get("Kernel_Name", ""), row.get("Counter_Name"), row.get("Counter_Value", 0))
     if "FETCH_SIZE" not in tot:
         return None
     fetch = 2 * 1024 * tot["FETCH_SIZE"] / n["FETCH_SIZE"]
