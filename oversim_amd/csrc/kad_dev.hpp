@@ -130,6 +130,109 @@ __device__ __forceinline__ int svec_add(SVec<CAP>& v, int cap, uint32_t x, uint6
 }
 
 // ---------------------------------------------------------------------------
+// Sorting networks over 8 (distance, node) pairs.  The findNode result and the LookupVector
+// are "the cap XOR-closest distinct nodes seen" -- BaseKeySortedVector::add applied to a
+// sequence of candidates yields exactly that set in distance order, whatever the order of
+// the adds -- so instead of one insertion per candidate (an 8-step compare + shift each), a
+// block of 8 candidates is sorted with a 19-comparator network and merged into the running
+// top 8 with a bitonic merge (8 min + 12 comparators).  Empty entries are (~0, NONE) and
+// sort last; equal top-64-bit distances fall back to the exact 160-bit compare.
+
+__device__ __forceinline__ bool cand_lt(uint64_t da, uint32_t ia, uint64_t db, uint32_t ib, const K160& K,
+                                        const KadRec* __restrict__ recs)
+{
+    if (da != db) return da < db;
+    if (ia == ib || ia == NONE) return false;
+    if (ib == NONE) return true;
+    const K160 xa = k_xor(kad_key(recs, ia), K), xb = k_xor(kad_key(recs, ib), K);   // rare
+    return k_lt(xa, xb);
+}
+
+struct Blk8 {
+    uint64_t d[8];
+    uint32_t x[8];
+    uint32_t f[8];     // payload flags (LookupVector merge: bit 0 alreadyUsed, bit 1 from the response)
+};
+
+template <bool F>
+__device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, const KadRec* __restrict__ recs)
+{
+    const bool s = cand_lt(b.d[j], b.x[j], b.d[i], b.x[i], K, recs);
+    const uint64_t di = s ? b.d[j] : b.d[i], dj = s ? b.d[i] : b.d[j];
+    const uint32_t xi = s ? b.x[j] : b.x[i], xj = s ? b.x[i] : b.x[j];
+    b.d[i] = di; b.d[j] = dj; b.x[i] = xi; b.x[j] = xj;
+    if (F) {
+        const uint32_t fi = s ? b.f[j] : b.f[i], fj = s ? b.f[i] : b.f[j];
+        b.f[i] = fi; b.f[j] = fj;
+    }
+}
+
+// Batcher odd-even merge sort, 19 comparators
+template <bool F>
+__device__ __forceinline__ void blk_sort8(Blk8& b, const K160& K, const KadRec* __restrict__ recs)
+{
+    blk_ce<F>(b, 0, 1, K, recs); blk_ce<F>(b, 2, 3, K, recs); blk_ce<F>(b, 4, 5, K, recs); blk_ce<F>(b, 6, 7, K, recs);
+    blk_ce<F>(b, 0, 2, K, recs); blk_ce<F>(b, 1, 3, K, recs); blk_ce<F>(b, 4, 6, K, recs); blk_ce<F>(b, 5, 7, K, recs);
+    blk_ce<F>(b, 1, 2, K, recs); blk_ce<F>(b, 5, 6, K, recs);
+    blk_ce<F>(b, 0, 4, K, recs); blk_ce<F>(b, 1, 5, K, recs); blk_ce<F>(b, 2, 6, K, recs); blk_ce<F>(b, 3, 7, K, recs);
+    blk_ce<F>(b, 2, 4, K, recs); blk_ce<F>(b, 3, 5, K, recs);
+    blk_ce<F>(b, 1, 2, K, recs); blk_ce<F>(b, 3, 4, K, recs); blk_ce<F>(b, 5, 6, K, recs);
+}
+
+// a <- the 8 smallest of sorted a and sorted b, sorted
+template <bool F>
+__device__ __forceinline__ void blk_merge_top8(Blk8& a, const Blk8& b, const K160& K, const KadRec* __restrict__ recs)
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const bool s = cand_lt(b.d[7 - i], b.x[7 - i], a.d[i], a.x[i], K, recs);
+        a.d[i] = s ? b.d[7 - i] : a.d[i];
+        a.x[i] = s ? b.x[7 - i] : a.x[i];
+        if (F) a.f[i] = s ? b.f[7 - i] : a.f[i];
+    }
+    // a is bitonic: half-cleaners at distance 4, 2, 1
+    blk_ce<F>(a, 0, 4, K, recs); blk_ce<F>(a, 1, 5, K, recs); blk_ce<F>(a, 2, 6, K, recs); blk_ce<F>(a, 3, 7, K, recs);
+    blk_ce<F>(a, 0, 2, K, recs); blk_ce<F>(a, 1, 3, K, recs); blk_ce<F>(a, 4, 6, K, recs); blk_ce<F>(a, 5, 7, K, recs);
+    blk_ce<F>(a, 0, 1, K, recs); blk_ce<F>(a, 2, 3, K, recs); blk_ce<F>(a, 4, 5, K, recs); blk_ce<F>(a, 6, 7, K, recs);
+}
+
+__device__ __forceinline__ void blk_clear(Blk8& b)
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { b.d[i] = ~0ull; b.x[i] = NONE; b.f[i] = 0; }
+}
+
+// up to 8 entries of a contiguous KadEntry array (bucket slot / sibling block), unsorted
+__device__ __forceinline__ void blk_load(Blk8& b, const KadEntry* __restrict__ s, int cnt, const K160& K)
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (q < cnt) {
+            const uint2* p = reinterpret_cast<const uint2*>(s + q);
+            const uint2 bb = p[1], c = p[2];
+            b.x[q] = c.y;
+            b.d[q] = c.y == NONE ? ~0ull : (((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(bb.y ^ K.w[3]));
+        } else {
+            b.x[q] = NONE;
+            b.d[q] = ~0ull;
+        }
+        b.f[q] = 0;
+    }
+}
+
+// keep the first cap entries; returns how many are non-empty
+__device__ __forceinline__ int blk_trunc(Blk8& b, int cap)
+{
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (i >= cap) { b.x[i] = NONE; b.d[i] = ~0ull; b.f[i] = 0; }
+        n += b.x[i] != NONE ? 1 : 0;
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------------------
 // Kademlia::isSiblingFor(thisNode, key, 1) (Kademlia.cc:888-962) from the 64 B record
 __device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadRec& r, const K160& K)
 {
@@ -173,11 +276,115 @@ __device__ __forceinline__ void add_slot(SVec<CAP>& res, int cap, const KadView&
     for (int q0 = 0; q0 < V.k; q0 += 8) add_entries8(res, cap, e + q0, min(8, V.k - q0), K, V.recs);
 }
 
+// Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246),
+// block form: the candidate sets of the reference's scan (bucket m, then buckets below it with
+// the sibling table and self, then buckets above while the result is short) merged 8 at a time
+__device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const KadRec& r, const K160& K,
+                                                 int numRedundant, bool sib, Blk8& res)
+{
+    blk_clear(res);
+    const K160 me = as_key(r.key);
+    if (V.nsib == 0 || sib) {
+        // resultSize = 1 and self is the XOR-closest of siblings + self (see kad_find_node1)
+        res.x[0] = c;
+        res.d[0] = dist_hi(me, K);
+        return 1;
+    }
+    const int cap = numRedundant < 8 ? numRedundant : 8;
+    const K160 D = k_xor(me, K);
+    const int m = k_msb(D);
+    const int endIndex = k_msb(as_key(r.R));
+    int n = 0;
+    auto add_block = [&](const KadEntry* e, int cnt) {
+        Blk8 b;
+        blk_load(b, e, cnt, K);
+        blk_sort8<false>(b, K, V.recs);
+        blk_merge_top8<false>(res, b, K, V.recs);
+        n = blk_trunc(res, cap);
+    };
+    auto add_slot8 = [&](int bucket) {
+        const KadEntry* e = V.slots + (uint64_t)(r.boff + (uint32_t)(KEYBITS - 1 - bucket)) * V.k;
+        for (int q0 = 0; q0 < V.k; q0 += 8) add_block(e + q0, min(8, V.k - q0));
+    };
+    if (m >= 0 && m >= endIndex) add_slot8(m);
+    if (m >= endIndex || n < cap) {
+        if (!(m > endIndex && n >= cap)) {
+            for (int b = m - 1; b >= endIndex; --b) add_slot8(b);
+            const KadEntry* L = V.sibe + (uint64_t)(c - V.lo) * V.S5;
+            for (int i = 0; i < V.nsib; i += 8) add_block(L + i, min(8, V.nsib - i));
+            Blk8 self;
+            blk_clear(self);
+            self.x[0] = c;
+            self.d[0] = dist_hi(me, K);
+            blk_merge_top8<false>(res, self, K, V.recs);
+            n = blk_trunc(res, cap);
+        }
+    }
+    for (int b = m + 1; n < cap && b < KEYBITS; ++b)
+        if (b >= endIndex) add_slot8(b);
+    return n;
+}
+
+// LookupVector merge (IterativePathLookup::handleResponse's add loop, IterativeLookup.cc:853-870):
+// nh <- the cap closest distinct nodes of nh and the (sorted) response; alreadyUsed flags stay
+// with their nodes.  Returns numNewRpcs: response nodes that entered nh (a response node the
+// reference inserts at a position < cap can never be pushed out again by the later, farther
+// response nodes, so "inserted" and "in the final vector" coincide).
+__device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap, const K160& K,
+                                        const KadRec* __restrict__ recs)
+{
+    Blk8 a, b;
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const bool ina = i < nh.n;
+        a.x[i] = ina ? nh.idx[i] : NONE;
+        a.d[i] = ina ? nh.d[i] : ~0ull;
+        a.f[i] = ina ? ((nh.used >> i) & 1u) : 0u;
+        const bool inb = i < res.n;
+        b.x[i] = inb ? res.idx[i] : NONE;
+        b.d[i] = inb ? res.d[i] : ~0ull;
+        b.f[i] = 2u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        bool dj = false;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dj |= (b.x[j] != NONE && b.x[j] == a.x[i]);
+        if (dj) { b.x[j] = NONE; b.d[j] = ~0ull; }
+        dup |= dj;
+    }
+    if (dup) blk_sort8<true>(b, K, recs);     // holes to the end
+    blk_merge_top8<true>(a, b, K, recs);
+    const int n = blk_trunc(a, cap);
+    int numNew = 0;
+    uint32_t used = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        nh.idx[i] = a.x[i];
+        nh.d[i] = a.d[i];
+        numNew += (a.x[i] != NONE && (a.f[i] & 2u)) ? 1 : 0;
+        used |= (a.x[i] != NONE && (a.f[i] & 1u)) ? (1u << i) : 0u;
+    }
+    nh.used = used;
+    nh.n = n;
+    return numNew;
+}
+
 // Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246)
 template <int CAP>
 __device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, const KadRec& r, const K160& K, int numRedundant,
                                bool sib, SVec<CAP>& res)
 {
+    if constexpr (CAP == 8) {
+        Blk8 b;
+        const int n = kad_find_node_blk(V, c, r, K, numRedundant, sib, b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
+        res.n = n;
+        res.used = 0;
+        return;
+    }
     svec_clear(res);
     const K160 me = as_key(r.key);
     if (V.nsib == 0 || sib) {
@@ -356,9 +563,7 @@ __device__ __forceinline__ void kad_lookup_start(KadLookup<A>& L, const KadView&
         L.result = res.idx[0];
         L.pfinished = true; L.psuccess = true;
     } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j < res.n) svec_add(L.nh, LC.redundant, res.idx[j], res.d[j], L.K, V.recs);
+        nh_merge(L.nh, res, LC.redundant, L.K, V.recs);
         kad_send_rpcs(L, V, DC, LC, LC.alpha, on);
     }
 }
@@ -422,14 +627,7 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     ++L.step;
     --L.pending;
     getres.fill(e, r, rr, sb, res);
-    int numNew = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        if (j < res.n) {
-            const int pos = svec_add(L.nh, LC.redundant, res.idx[j], res.d[j], L.K, V.recs);
-            if (pos >= 0 && pos < LC.redundant) ++numNew;
-        }
-    }
+    int numNew = nh_merge(L.nh, res, LC.redundant, L.K, V.recs);
     if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
     if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
     else {

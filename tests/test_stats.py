@@ -135,7 +135,7 @@ def test_gpu_stats_crafted(engine):
         hist[res["one_way_hops"][i]] += 1
     assert np.array_equal(np.array(list(g.hop_hist)), hist)
     assert (g.hop_count_min, g.hop_count_max) == (2, 5)
-    assert (g.latency_min_ns, g.latency_max_ns) == (1, 3_000_000_000)
+    assert (g.latency_min_ns, g.latency_max_ns) == (7, 3_000_000_000)
 
 
 @pytest.mark.gpu
