@@ -64,7 +64,7 @@ __device__ __forceinline__ uint32_t ring_lower_bound(const KeyRec* __restrict__ 
 
 // finger i of node v = responsible(v + 2^i) (rpcFixfingers answers thisNode, Chord.cc:1228-1270)
 __global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32_t lo, uint32_t cnt,
-                             uint32_t* __restrict__ fingers)
+                             uint2* __restrict__ fingers)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
@@ -73,13 +73,37 @@ __global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32
     const K160 self = key_of(r);
     const K160 s0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
     const int ilo = k_msb(k_sub(s0, self)) + 1;
-    uint32_t* row = fingers + r.aux;
-    for (int i = KEYBITS - 1; i >= ilo; --i)
-        row[KEYBITS - 1 - i] = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
+    uint2* row = fingers + r.aux;
+    for (int i = KEYBITS - 1; i >= ilo; --i) {
+        const uint32_t f = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
+        // entry = {finger, code32 of its distance from v} (decide_compact's finger test)
+        row[KEYBITS - 1 - i] = make_uint2(f, (uint32_t)(k_code64(k_sub(key_of(load_rec(recs, f)), self)) >> 32));
+    }
+}
+
+// NodeRec of every node (ideal ring): key, finger-row offset, coordinates, window codes
+__global__ void k_chord_nodes(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t n, int ns,
+                              NodeRec* __restrict__ nodes)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const KeyRec r = load_rec(recs, v);
+    const K160 C = key_of(r);
+    const K160 P = key_of(load_rec(recs, v == 0 ? n - 1 : v - 1));
+    const K160 S0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
+    const uint32_t sl = v + (uint32_t)ns >= n ? v + (uint32_t)ns - n : v + (uint32_t)ns;
+    const K160 SL = key_of(load_rec(recs, sl));
+    const double2 p = xy[v];
+    const uint64_t cP = k_code64(k_sub(P, C)), cS0 = k_code64(k_sub(S0, C)), cSL = k_code64(k_sub(SL, C));
+    uint4* o = reinterpret_cast<uint4*>(nodes + v);
+    o[0] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+    o[1] = make_uint4(r.w[4], r.aux, (uint32_t)__double2loint(p.x), (uint32_t)__double2hiint(p.x));
+    o[2] = make_uint4((uint32_t)__double2loint(p.y), (uint32_t)__double2hiint(p.y), (uint32_t)cP, (uint32_t)(cP >> 32));
+    o[3] = make_uint4((uint32_t)cS0, (uint32_t)(cS0 >> 32), (uint32_t)cSL, (uint32_t)(cSL >> 32));
 }
 
 // resolved getFinger(pos) for every position (test export)
-__global__ void k_chord_export(const KeyRec* __restrict__ recs, const uint32_t* __restrict__ fingers,
+__global__ void k_chord_export(const KeyRec* __restrict__ recs, const uint2* __restrict__ fingers,
                                uint32_t n, uint32_t* __restrict__ out)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -89,7 +113,7 @@ __global__ void k_chord_export(const KeyRec* __restrict__ recs, const uint32_t* 
     const KeyRec r = load_rec(recs, v);
     const uint32_t s0i = v + 1 == n ? 0 : v + 1;
     const int ilo = k_msb(k_sub(key_of(load_rec(recs, s0i)), key_of(r))) + 1;
-    out[t] = pos >= ilo ? fingers[r.aux + (KEYBITS - 1 - pos)] : s0i;
+    out[t] = pos >= ilo ? fingers[r.aux + (KEYBITS - 1 - pos)].x : s0i;
 }
 
 // ---------------------------------------------------------------------------
@@ -109,66 +133,84 @@ __device__ __forceinline__ uint32_t ring_next(uint32_t i, uint32_t d, uint32_t n
     return j >= n ? j - n : j;
 }
 
-// ideal tables: successor j of c is c+1+j, predecessor c-1
-__device__ __forceinline__ Decision decide_ideal(const ChordView& V, uint32_t c, const KeyRec& crec,
-                                                 const K160& K)
-{
-    Decision d;
-    d.broken = 0; d.sib = 0;
-    const K160 C = key_of(crec);
-    const uint32_t pidx = c == 0 ? V.n - 1 : c - 1;
-    const uint32_t s0 = ring_next(c, 1, V.n);
-    // issue every independent gather of this hop up front
-    const K160 D = k_sub(K, C);
-    const int i0 = k_msb(D);                       // -1 only when K == C (then c is responsible)
-    const uint32_t slot0 = (uint32_t)(KEYBITS - 1 - (i0 < 0 ? KEYBITS - 1 : i0));
-    const uint32_t f0 = V.fingers[crec.aux + slot0];   // in bounds: rows are padded by 160 words
-    const KeyRec P = load_rec(V.recs, pidx);
-    const KeyRec S0 = load_rec(V.recs, s0);
-    const uint32_t slast = ring_next(c, (uint32_t)V.ns, V.n);
-    const KeyRec SL = load_rec(V.recs, slast);
-    const K160 PK = key_of(P), S0K = key_of(S0);
+// Ideal tables, compact layout (NodeRec + coded finger rows).  Successor j of c
+// is c+1+j, the predecessor c-1.  Every ring test is taken relative to c with
+// D = K - c: each interval of Chord.cc:452-457, 583-590, 602-674 becomes a
+// compare of D against a distance from c, decided on the order-preserving codes
+// stored in the node record and the finger rows; an equal code (a tie at the
+// code's precision, e.g. a node-ID key) falls back to the exact keys in recs[].
+struct Hop {
+    uint32_t next;   // next hop (== c when c is responsible), NONE when broken
+    uint8_t sib;     // siblings flag of the FindNodeResponse
+    uint8_t broken;  // Chord::closestPreceedingNode threw
+};
 
-    // isSiblingFor(thisNode, key, 1): key in (pred, self]  (Chord.cc:452-457)
-    if (between_R(K, PK, C)) {
-        d.sib = 1; d.next = c; d.rec = crec;
-        return d;
-    }
-    // key in (self, succ0]  (Chord.cc:583-590)
-    if (between_R(K, C, S0K)) {
-        d.next = s0; d.rec = S0;
-        return d;
-    }
-    // closestPreceedingNode (Chord.cc:602-674)
-    // temp = farthest successor in (self, key]
-    int tj = -1;
-    K160 T;
-    if (between_R(key_of(SL), C, K)) {
-        tj = V.ns - 1; T = key_of(SL);
+__device__ __forceinline__ Hop decide_compact(const ChordView& V, uint32_t c, const NodeRec& R, const K160& K)
+{
+    Hop h;
+    h.sib = 0; h.broken = 0; h.next = NONE;
+    const K160 C = key_of_node(R);
+    const K160 D = k_sub(K, C);
+    const int i0 = k_msb(D);                     // -1 only when K == C
+    // finger entry i0, issued before anything that depends on it (rows are padded by 160 entries)
+    const uint2 f0 = V.frow[R.row + (uint32_t)(KEYBITS - 1 - (i0 < 0 ? KEYBITS - 1 : i0))];
+    if (i0 < 0) { h.sib = 1; h.next = c; return h; }
+    const uint64_t cD = k_code64(D);
+    // isSiblingFor(thisNode, key, 1): K in (pred, C]  <=>  D > pred - C  (Chord.cc:452-457)
+    bool t;
+    if (cD != R.cP) t = cD > R.cP;
+    else t = between_R(K, key_of(load_rec(V.recs, c == 0 ? V.n - 1 : c - 1)), C);
+    if (t) { h.sib = 1; h.next = c; return h; }
+    // K in (C, succ0]  <=>  D <= succ0 - C  (Chord.cc:583-590)
+    const uint32_t s0 = ring_next(c, 1, V.n);
+    if (cD != R.cS0) t = cD < R.cS0;
+    else t = between_R(K, C, key_of(load_rec(V.recs, s0)));
+    if (t) { h.next = s0; return h; }
+    // closestPreceedingNode (Chord.cc:602-674): temp = farthest successor in (C, K]
+    int tj;
+    uint32_t cT;                 // code32 of temp - C
+    bool tIsK = false, gTexact = false;
+    K160 gT;
+    if (cD > R.cSL) {
+        tj = V.ns - 1;
+        cT = (uint32_t)(R.cSL >> 32);
     } else {
-        for (int j = V.ns - 2; j >= 0; --j) {
+        tj = -1;
+        for (int j = V.ns - 1; j >= 0; --j) {
             const K160 SJ = key_of(load_rec(V.recs, ring_next(c, (uint32_t)j + 1, V.n)));
-            if (between_R(SJ, C, K)) { tj = j; T = SJ; break; }
+            if (between_R(SJ, C, K)) { tj = j; gT = k_sub(SJ, C); tIsK = k_eq(SJ, K); break; }
         }
+        if (tj < 0) { h.broken = 1; return h; }
+        gTexact = true;
+        cT = (uint32_t)(k_code64(gT) >> 32);
     }
-    if (tj < 0) { d.broken = 1; d.next = NONE; return d; }
-    // finger scan from i0 down (fingers above i0 lie beyond the key)
-    const int ilo = k_msb(k_sub(S0K, C)) + 1;
+    // finger scan from i0 down (fingers above i0 lie beyond the key):
+    // finger F in [temp, K]  <=>  temp - C <= F - C <= D
+    const uint32_t cD32 = (uint32_t)(cD >> 32);
+    const int ilo = (int)(R.cS0 >> 56);
     for (int i = i0; i >= ilo; --i) {
-        const uint32_t f = (i == i0) ? f0 : V.fingers[crec.aux + (uint32_t)(KEYBITS - 1 - i)];
-        const KeyRec F = load_rec(V.recs, f);
-        if (between_LR(key_of(F), T, K)) { d.next = f; d.rec = F; return d; }
+        const uint2 e = (i == i0) ? f0 : V.frow[R.row + (uint32_t)(KEYBITS - 1 - i)];
+        bool hit;
+        if (e.y != cD32 && e.y != cT) {
+            hit = (e.y < cD32) & (e.y > cT);
+        } else {
+            const K160 dF = k_sub(key_of(load_rec(V.recs, e.x)), C);
+            if (!gTexact) {
+                gT = k_sub(key_of(load_rec(V.recs, ring_next(c, (uint32_t)V.ns, V.n))), C);
+                gTexact = true;
+            }
+            hit = k_le(gT, dF) & k_le(dF, D);
+        }
+        if (hit) { h.next = e.x; return h; }
     }
-    // trivial positions resolve to succ0 (ChordFingerTable.cc:183-184)
-    if (between_LR(S0K, T, K)) { d.next = s0; d.rec = S0; return d; }
-    // no finger: farthest successor in the OPEN interval (self, key) (Chord.cc:653-658)
-    for (int j = V.ns - 1; j >= 0; --j) {
-        const uint32_t sj = ring_next(c, (uint32_t)j + 1, V.n);
-        const KeyRec SJ = (j == V.ns - 1) ? SL : load_rec(V.recs, sj);
-        if (between_open(key_of(SJ), C, K)) { d.next = sj; d.rec = SJ; return d; }
-    }
-    d.broken = 1; d.next = NONE;
-    return d;
+    // trivial positions resolve to succ0 (ChordFingerTable.cc:183-184); succ0 lies in
+    // [temp, K] only when temp is succ0
+    if (tj == 0) { h.next = s0; return h; }
+    // no finger: farthest successor in the OPEN interval (C, K) (Chord.cc:653-658) --
+    // temp itself unless temp == K
+    const int j = tIsK ? tj - 1 : tj;
+    h.next = ring_next(c, (uint32_t)j + 1, V.n);
+    return h;
 }
 
 // general (explicit snapshot) tables: literal restatement incl. unspecified predecessor
@@ -226,6 +268,36 @@ __device__ __forceinline__ Decision decide_general(const ChordView& V, uint32_t 
 // ---------------------------------------------------------------------------
 // K1: batched one-way lookups
 
+// Responder state carried in registers between hops.  Ideal rings: the 64 B
+// NodeRec of the current responder (key, finger-row offset, coordinates, window
+// codes); explicit tables: its 24 B KeyRec (coordinates gathered per hop).
+template <bool IDEAL> struct Responder;
+template <> struct Responder<true> {
+    NodeRec n;
+    __device__ __forceinline__ void load(const ChordView& V, uint32_t c) { n = load_node(V.nodes, c); }
+    __device__ __forceinline__ double2 xy(const ChordView&, uint32_t) const { return make_double2(n.x, n.y); }
+    __device__ __forceinline__ Hop decide(const ChordView& V, uint32_t c, const K160& K) const
+    {
+        return decide_compact(V, c, n, K);
+    }
+    __device__ __forceinline__ void advance(const ChordView& V, const Hop& h) { load(V, h.next); }
+};
+template <> struct Responder<false> {
+    KeyRec r;
+    KeyRec nxt;
+    __device__ __forceinline__ void load(const ChordView& V, uint32_t c) { r = load_rec(V.recs, c); }
+    __device__ __forceinline__ double2 xy(const ChordView& V, uint32_t c) const { return V.xy[c]; }
+    __device__ __forceinline__ Hop decide(const ChordView& V, uint32_t c, const K160& K)
+    {
+        const Decision d = decide_general(V, c, r, K);
+        nxt = d.rec;
+        Hop h;
+        h.next = d.next; h.sib = d.sib; h.broken = d.broken;
+        return h;
+    }
+    __device__ __forceinline__ void advance(const ChordView&, const Hop&) { r = nxt; }
+};
+
 template <bool IDEAL, bool RECORD, bool REC>
 __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC, LookupConsts LC,
                                                      const K160* __restrict__ qkeys,
@@ -243,7 +315,7 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
     uint64_t q = 0;
     uint32_t S = 0, cur = 0;
     K160 K;
-    KeyRec crec;
+    Responder<IDEAL> rs;
     double sx = 0, sy = 0;
     int64_t t = 0;
     int hops = 0;
@@ -258,8 +330,8 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
                 active = true;
                 K = qkeys[q];
                 S = qsrc[q];
-                crec = load_rec(V.recs, S);
-                const double2 sxy = V.xy[S];
+                rs.load(V, S);
+                const double2 sxy = rs.xy(V, S);
                 sx = sxy.x; sy = sxy.y;
                 cur = S; t = 0; hops = 0; local = true;
             }
@@ -268,9 +340,8 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
         if (!__any(active)) break;
         if (!active) continue;
 
-        // responder coordinates are independent of the routing decision: issue first
-        const double2 cxy = V.xy[cur];
-        const Decision d = IDEAL ? decide_ideal(V, cur, crec, K) : decide_general(V, cur, crec, K);
+        const double2 cxy = rs.xy(V, cur);
+        const Hop d = rs.decide(V, cur, K);
 
         uint8_t status = 0xFF;   // 0xFF = still running
         uint32_t R = NONE;
@@ -295,7 +366,8 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
             } else {
                 if (RECORD && hops < LC.hopCountMax) hopseq[q * (uint64_t)LC.hopCountMax + hops] = d.next;
                 ++hops;
-                cur = d.next; crec = d.rec;
+                cur = d.next;
+                rs.advance(V, d);
             }
             if (status != 0xFF) {
                 ovs_route_out o;
@@ -342,7 +414,7 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
                         visited |= hopseq[q * (uint64_t)LC.hopCountMax + h] == d.next;
                 }
                 if (visited) status = OVS_LOOKUP_NO_NEXT;
-                else { cur = d.next; crec = d.rec; }
+                else { cur = d.next; rs.advance(V, d); }
             }
         }
         if (status != 0xFF) {
@@ -415,7 +487,7 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
     bool active = false;
     uint32_t S = 0, cur = 0, qid = 0;
     K160 K;
-    KeyRec crec;
+    NodeRec cn;
     double sx = 0, sy = 0;
     int64_t t = 0;
     int hops = 0;
@@ -430,8 +502,8 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
                 active = true;
                 for (int w = 0; w < 5; ++w) K.w[w] = r.key[w];
                 S = r.src; cur = r.cur; qid = r.qid; t = r.t_ns; hops = r.hops; local = r.local != 0;
-                crec = load_rec(V.recs, cur);
-                const double2 sxy = V.xy[S];
+                cn = load_node(V.nodes, cur);
+                const double2 sxy = V.xy[S];     // source coordinates (replicated on every rank)
                 sx = sxy.x; sy = sxy.y;
             }
             cursor += (uint64_t)__popcll(need);
@@ -442,8 +514,8 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
         int dest = 0;
         ovs_route_out o;
         if (active) {
-            const double2 cxy = V.xy[cur];
-            const Decision d = decide_ideal(V, cur, crec, K);
+            const double2 cxy = make_double2(cn.x, cn.y);
+            const Hop d = decide_compact(V, cur, cn, K);
             uint8_t status = 0xFF;
             uint32_t R = NONE;
             if (REC) {
@@ -461,9 +533,9 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
                     t += DC.msgRoute + coord_ns(cxy.x, cxy.y, nxy.x, nxy.y, DC.round);
                     ++hops;
                     cur = d.next;
-                    crec = d.rec;
                     dest = shard_owner(shard_lo, nsh, cur);
                     if (dest != me) { emit_out = true; active = false; }
+                    else cn = load_node(V.nodes, cur);
                 }
                 if (status != 0xFF) {
                     o.hops = (uint16_t)(status == OVS_LOOKUP_OK ? hops : 0);
@@ -498,9 +570,9 @@ __global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayCons
                 else if (d.next == S) status = OVS_LOOKUP_NO_NEXT;
                 else {
                     cur = d.next;
-                    crec = d.rec;
                     dest = shard_owner(shard_lo, nsh, cur);
                     if (dest != me) { emit_out = true; active = false; }
+                    else cn = load_node(V.nodes, cur);
                 }
             }
             if (!REC && status != 0xFF) {
@@ -572,7 +644,7 @@ __global__ void k_chord_find_node(ChordView V, int ideal, const uint32_t* __rest
     const uint32_t s0 = ssize > 0 ? succ_at(0) : c;
     const int ilo = ideal ? k_msb(k_sub(key_of(load_rec(V.recs, s0)), C)) + 1 : 0;
     auto finger_at = [&](int pos) -> uint32_t {
-        if (ideal) return pos >= ilo ? V.fingers[crec.aux + (uint32_t)(KEYBITS - 1 - pos)] : s0;
+        if (ideal) return pos >= ilo ? V.frow[crec.aux + (uint32_t)(KEYBITS - 1 - pos)].x : s0;
         return V.fres[(uint64_t)c * KEYBITS + pos];
     };
     const bool sib = ideal ? between_R(K, key_of(load_rec(V.recs, c == 0 ? V.n - 1 : c - 1)), C)
@@ -638,7 +710,7 @@ hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hi
     return hipGetLastError();
 }
 
-hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, uint32_t** fingers_out,
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, uint2** fingers_out,
                               uint64_t* nfing_out, hipStream_t s)
 {
     hipError_t e;
@@ -659,12 +731,12 @@ hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi
     hipMemcpyAsync(&total, off + cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     if (total + KEYBITS >= 0xFFFFFFFFull) { hipFree(rowlen); hipFree(off); hipFree(tmp); return hipErrorInvalidValue; }
-    uint32_t* fing = nullptr;
-    // +160 words of padding: the kernel's speculative first-finger read may run past a row
-    if ((e = hipMalloc(&fing, sizeof(uint32_t) * (total + KEYBITS))) != hipSuccess) {
+    uint2* fing = nullptr;
+    // +160 entries of padding: the kernel's speculative first-finger read may run past a row
+    if ((e = hipMalloc(&fing, sizeof(uint2) * (total + KEYBITS))) != hipSuccess) {
         hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
     }
-    hipMemsetAsync(fing, 0, sizeof(uint32_t) * (total + KEYBITS), s);
+    hipMemsetAsync(fing, 0, sizeof(uint2) * (total + KEYBITS), s);
     hipLaunchKernelGGL(k_set_aux, dim3(nblk(cnt, 256)), dim3(256), 0, s, recs, off, lo, cnt);
     hipLaunchKernelGGL(k_chord_fill, dim3(nblk(cnt, 128)), dim3(128), 0, s, recs, n, lo, cnt, fing);
     e = hipStreamSynchronize(s);
@@ -675,7 +747,14 @@ hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi
     return hipGetLastError();
 }
 
-hipError_t launch_chord_export(const KeyRec* recs, const uint32_t* fingers, uint32_t n, uint32_t* out,
+hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chord_nodes, dim3(nblk(n, 256)), dim3(256), 0, s, recs, xy, n, ns, nodes);
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_export(const KeyRec* recs, const uint2* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s)
 {
     const uint64_t tot = (uint64_t)n * KEYBITS;

@@ -65,17 +65,56 @@ __device__ __forceinline__ KeyRec load_rec(const KeyRec* __restrict__ recs, uint
 }
 
 // ---------------------------------------------------------------------------
+// Chord node record of the converged ring: everything one hop at node c reads
+// about c, in one 64 B line.  The ring window (pred, succ0, succ[ns-1]) enters
+// as order-preserving codes of its distances from c (k_code64), so the
+// isSiblingFor / (c, succ0] / temp tests cost no extra gather; an equal code
+// falls back to the exact keys in recs[].
+struct alignas(64) NodeRec {
+    uint32_t w[5];   // node key
+    uint32_t row;    // offset of the node's finger row (valid on the arc that owns the row)
+    double x, y;     // SimpleUnderlay coordinates
+    uint64_t cP;     // k_code64((pred - c) mod 2^160)
+    uint64_t cS0;    // k_code64(succ0 - c);  cS0 >> 56 = i_lo = first non-trivial finger
+    uint64_t cSL;    // k_code64(succ[ns-1] - c), ns = min(successorListSize, n - 1)
+};
+static_assert(sizeof(NodeRec) == 64, "NodeRec is one 64 B line");
+
+__device__ __forceinline__ NodeRec load_node(const NodeRec* __restrict__ p, uint32_t i)
+{
+    const uint4* q = reinterpret_cast<const uint4*>(p + i);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    NodeRec r;
+    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w; r.w[4] = b.x; r.row = b.y;
+    r.x = __hiloint2double((int)b.w, (int)b.z);
+    r.y = __hiloint2double((int)c.y, (int)c.x);
+    r.cP = (uint64_t)c.z | ((uint64_t)c.w << 32);
+    r.cS0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    r.cSL = (uint64_t)d.z | ((uint64_t)d.w << 32);
+    return r;
+}
+
+__device__ __forceinline__ K160 key_of_node(const NodeRec& r)
+{
+    K160 k;
+    for (int i = 0; i < 5; ++i) k.w[i] = r.w[i];
+    return k;
+}
+
 // Chord device view.
-//  recs[n]      : sorted node keys, aux = offset of the node's finger row
+//  recs[n]      : sorted node keys (24 B), aux = offset of the node's finger row
 //  xy[n]        : SimpleUnderlay coordinates (fp64)
-//  fingers[...] : ideal mode -- CSR rows, row(v)[159 - i] = finger i for the
-//                 non-trivial positions i >= i_lo(v) = msb(succ0 - v) + 1
-//                 (trivial positions resolve to succ0, ChordFingerTable.cc:183-184)
+//  nodes[n]     : ideal mode -- NodeRec per node (64 B)
+//  frow[...]    : ideal mode -- CSR rows of {finger index, k_code64(finger - v) >> 32},
+//                 row(v)[159 - i] = finger i for the non-trivial positions
+//                 i >= i_lo(v) = msb(succ0 - v) + 1 (trivial positions resolve to
+//                 succ0, ChordFingerTable.cc:183-184)
 //  general mode : pred[n], succ[n*sls], nsucc[n], fres[n*160] = getFinger(i) resolved
 struct ChordView {
     const KeyRec* __restrict__ recs;
     const double2* __restrict__ xy;
-    const uint32_t* __restrict__ fingers;
+    const NodeRec* __restrict__ nodes;
+    const uint2* __restrict__ frow;
     const uint32_t* __restrict__ pred;
     const uint32_t* __restrict__ succ;
     const uint8_t* __restrict__ nsucc;

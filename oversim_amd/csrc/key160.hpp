@@ -114,6 +114,35 @@ OVS_HD int k_msb(const K160& a)
     return -1;
 }
 
+// word i of a key, 0 above the top word (select chain: no dynamic register indexing)
+OVS_HD uint32_t k_word(const K160& a, int i)
+{
+    return i == 0 ? a.w[0] : i == 1 ? a.w[1] : i == 2 ? a.w[2] : i == 3 ? a.w[3] : i == 4 ? a.w[4] : 0u;
+}
+
+// Order-preserving 64-bit code of a 160-bit value v (a floating-point-like
+// summary used to decide ring-interval tests without the full key):
+//   code(0) = 0;  otherwise code(v) = (msb(v) + 1) << 56 | the 56 bits below msb(v).
+// a < b  =>  code(a) <= code(b);   code(a) < code(b)  =>  a < b.
+// Equal codes decide nothing: callers fall back to the exact 160-bit compare.
+// code(v) >> 32 is the same construction with a 24-bit mantissa.
+OVS_HD uint64_t k_code64(const K160& v)
+{
+    const int e = k_msb(v);
+    if (e < 0) return 0;
+    uint64_t top;   // the 64-bit window of v whose msb is bit e
+    if (e >= 63) {
+        const int s = e - 63, q = s >> 5, r = s & 31;
+        const uint32_t a0 = k_word(v, q), a1 = k_word(v, q + 1), a2 = k_word(v, q + 2);
+        const uint32_t lo = r ? (a0 >> r) | (a1 << (32 - r)) : a0;
+        const uint32_t hi = r ? (a1 >> r) | (a2 << (32 - r)) : a1;
+        top = (uint64_t)lo | ((uint64_t)hi << 32);
+    } else {
+        top = lo64(v) << (63 - e);
+    }
+    return ((uint64_t)(e + 1) << 56) | ((top << 1) >> 8);
+}
+
 // 2^e (OverlayKey::pow2, 704-717)
 OVS_HD K160 k_pow2(int e)
 {

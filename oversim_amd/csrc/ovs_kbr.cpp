@@ -32,8 +32,10 @@ struct ovs_ctx {
     // chord
     KeyRec* recs = nullptr;
     double2* xy = nullptr;
-    uint32_t* fingers = nullptr;
+    uint2* fingers = nullptr;      // ideal finger rows {index, distance code}
     uint64_t nfing = 0;
+    NodeRec* nodes = nullptr;      // ideal node records (built for successorListSize = nodes_ns)
+    int nodes_ns = -1;
     uint32_t* pred = nullptr;
     uint32_t* succ = nullptr;
     uint8_t* nsucc = nullptr;
@@ -76,9 +78,10 @@ ovs_status hip_fail(ovs_ctx* c, hipError_t e, const char* where)
 
 void free_tables(ovs_ctx* c)
 {
-    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres};
+    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres, c->nodes};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    c->nodes = nullptr; c->nodes_ns = -1;
     c->recs = nullptr; c->xy = nullptr; c->fingers = nullptr; c->pred = nullptr;
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
@@ -185,12 +188,25 @@ ovs_status to_device(ovs_ctx* c, const T* src, uint64_t count, bool dev, T** out
 ChordView chord_view(const ovs_ctx* c)
 {
     ChordView V{};
-    V.recs = c->recs; V.xy = c->xy; V.fingers = c->fingers; V.pred = c->pred; V.succ = c->succ;
+    V.recs = c->recs; V.xy = c->xy; V.nodes = c->nodes; V.frow = c->fingers; V.pred = c->pred; V.succ = c->succ;
     V.nsucc = c->nsucc; V.fres = c->fres; V.n = (uint32_t)c->n;
     V.ns = (int)std::min<uint64_t>((uint64_t)c->P.successorListSize, c->n - 1);
     V.sls = c->sls;
     V.numFingerCandidates = c->P.numFingerCandidates;
     return V;
+}
+
+// NodeRec array of an ideal ring for the current successorListSize (rebuilt when it changes)
+ovs_status ensure_nodes(ovs_ctx* c, hipStream_t s)
+{
+    if (!c->ideal || c->overlay != OVS_OVERLAY_CHORD) return OVS_OK;
+    const int ns = (int)std::min<uint64_t>((uint64_t)c->P.successorListSize, c->n - 1);
+    if (c->nodes && c->nodes_ns == ns) return OVS_OK;
+    if (ns < 1) return fail(c, OVS_EINVAL, "successorListSize must be >= 1");
+    if (!c->nodes) HIPCHK(c, hipMalloc(&c->nodes, sizeof(NodeRec) * c->n));
+    HIPCHK(c, launch_chord_nodes(c->recs, c->xy, (uint32_t)c->n, ns, c->nodes, s));
+    c->nodes_ns = ns;
+    return OVS_OK;
 }
 
 // upload sorted ids (+ coordinates) into KeyRec / double2 arrays
@@ -393,6 +409,8 @@ ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, o
     if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
     HIPCHK(c, hipMemcpyAsync(c->d_bounds, M.lo, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice, s));
     LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes, c->P.routingType != 0};
+    st = ensure_nodes(c, s);
+    if (st != OVS_OK) return st;
     HIPCHK(c, launch_chord_shard_step(chord_view(c), delay_consts(c->P), LC, c->d_bounds, (int)nshards, me, in, n_in, out,
                                       out_dest, out_cap, out_count, done, done_cap, done_count, c->num_cu, s));
     return OVS_OK;
@@ -606,6 +624,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         if (st != OVS_OK) return st;
         if (c->ideal && (c->shard_lo != 0 || c->shard_hi != c->n))
             return fail(c, OVS_ESTATE, "context holds one arc of a sharded ring: use ovs_shard_step");
+        st = ensure_nodes(c, s);
+        if (st != OVS_OK) return st;
     } else if (c->P.routingType != 0) {
         return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
     } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
