@@ -62,9 +62,10 @@ __device__ __forceinline__ uint32_t ring_lower_bound(const KeyRec* __restrict__ 
     return lo == n ? 0 : lo;
 }
 
-// finger i of node v = responsible(v + 2^i) (rpcFixfingers answers thisNode, Chord.cc:1228-1270)
+// finger i of node v = responsible(v + 2^i) (rpcFixfingers answers thisNode, Chord.cc:1228-1270);
+// only the index is written here, k_chord_entries completes the entry from the finger's NodeRec
 __global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32_t lo, uint32_t cnt,
-                             uint2* __restrict__ fingers)
+                             FingerEnt* __restrict__ fingers)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
@@ -73,15 +74,12 @@ __global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32
     const K160 self = key_of(r);
     const K160 s0 = key_of(load_rec(recs, v + 1 == n ? 0 : v + 1));
     const int ilo = k_msb(k_sub(s0, self)) + 1;
-    uint2* row = fingers + r.aux;
-    for (int i = KEYBITS - 1; i >= ilo; --i) {
-        const uint32_t f = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
-        // entry = {finger, code32 of its distance from v} (decide_compact's finger test)
-        row[KEYBITS - 1 - i] = make_uint2(f, (uint32_t)(k_code64(k_sub(key_of(load_rec(recs, f)), self)) >> 32));
-    }
+    FingerEnt* row = fingers + r.aux;
+    for (int i = KEYBITS - 1; i >= ilo; --i)
+        row[KEYBITS - 1 - i].idx = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
 }
 
-// NodeRec of every node (ideal ring): key, finger-row offset, coordinates, window codes
+// NodeRec of every node (ideal ring): key, finger-row offset, coordinates, window distances
 __global__ void k_chord_nodes(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t n, int ns,
                               NodeRec* __restrict__ nodes)
 {
@@ -94,16 +92,50 @@ __global__ void k_chord_nodes(const KeyRec* __restrict__ recs, const double2* __
     const uint32_t sl = v + (uint32_t)ns >= n ? v + (uint32_t)ns - n : v + (uint32_t)ns;
     const K160 SL = key_of(load_rec(recs, sl));
     const double2 p = xy[v];
-    const uint64_t cP = k_code64(k_sub(P, C)), cS0 = k_code64(k_sub(S0, C)), cSL = k_code64(k_sub(SL, C));
+    const uint64_t gP = top64(k_sub(P, C)), gS0 = top64(k_sub(S0, C)), gSL = top64(k_sub(SL, C));
     uint4* o = reinterpret_cast<uint4*>(nodes + v);
     o[0] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
     o[1] = make_uint4(r.w[4], r.aux, (uint32_t)__double2loint(p.x), (uint32_t)__double2hiint(p.x));
-    o[2] = make_uint4((uint32_t)__double2loint(p.y), (uint32_t)__double2hiint(p.y), (uint32_t)cP, (uint32_t)(cP >> 32));
-    o[3] = make_uint4((uint32_t)cS0, (uint32_t)(cS0 >> 32), (uint32_t)cSL, (uint32_t)(cSL >> 32));
+    o[2] = make_uint4((uint32_t)__double2loint(p.y), (uint32_t)__double2hiint(p.y), (uint32_t)gS0, (uint32_t)(gS0 >> 32));
+    o[3] = make_uint4((uint32_t)gSL, (uint32_t)(gSL >> 32), (uint32_t)gP, (uint32_t)(gP >> 32));
+}
+
+// WinRec of every node of the arc [lo, lo + cnt): top64 of the distances to successors 0..ns-1
+__global__ void k_chord_win(const KeyRec* __restrict__ recs, uint32_t n, uint32_t lo, uint32_t cnt, int ns,
+                            WinRec* __restrict__ win)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint32_t v = lo + t;
+    const K160 C = key_of(load_rec(recs, v));
+    uint64_t g[8];
+    for (int j = 0; j < 8; ++j) {
+        uint32_t sj = v + (uint32_t)j + 1;
+        while (sj >= n) sj -= n;
+        g[j] = j < ns ? top64(k_sub(key_of(load_rec(recs, sj)), C)) : ~0ull;
+    }
+    uint4* o = reinterpret_cast<uint4*>(win + t);
+    for (int j = 0; j < 4; ++j)
+        o[j] = make_uint4((uint32_t)g[2 * j], (uint32_t)(g[2 * j] >> 32), (uint32_t)g[2 * j + 1], (uint32_t)(g[2 * j + 1] >> 32));
+}
+
+// complete every finger entry from its finger's NodeRec (rerun when the NodeRecs change)
+__global__ void k_chord_entries(const NodeRec* __restrict__ nodes, FingerEnt* __restrict__ ents, uint64_t total)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const uint32_t f = ents[e].idx;
+    const uint4* q = reinterpret_cast<const uint4*>(nodes + f);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    uint4* o = reinterpret_cast<uint4*>(ents + e);
+    o[0] = a;                                     // key
+    o[1] = make_uint4(b.x, f, b.z, b.w);          // key[4], idx, x
+    o[2] = c;                                     // y, gS0
+    o[3] = make_uint4(d.x, d.y, b.y, 0u);         // gSL, the finger's row offset
 }
 
 // resolved getFinger(pos) for every position (test export)
-__global__ void k_chord_export(const KeyRec* __restrict__ recs, const uint2* __restrict__ fingers,
+__global__ void k_chord_export(const KeyRec* __restrict__ recs, const FingerEnt* __restrict__ fingers,
                                uint32_t n, uint32_t* __restrict__ out)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -113,7 +145,7 @@ __global__ void k_chord_export(const KeyRec* __restrict__ recs, const uint2* __r
     const KeyRec r = load_rec(recs, v);
     const uint32_t s0i = v + 1 == n ? 0 : v + 1;
     const int ilo = k_msb(k_sub(key_of(load_rec(recs, s0i)), key_of(r))) + 1;
-    out[t] = pos >= ilo ? fingers[r.aux + (KEYBITS - 1 - pos)].x : s0i;
+    out[t] = pos >= ilo ? fingers[r.aux + (KEYBITS - 1 - pos)].idx : s0i;
 }
 
 // ---------------------------------------------------------------------------
@@ -131,86 +163,6 @@ __device__ __forceinline__ uint32_t ring_next(uint32_t i, uint32_t d, uint32_t n
 {
     uint32_t j = i + d;
     return j >= n ? j - n : j;
-}
-
-// Ideal tables, compact layout (NodeRec + coded finger rows).  Successor j of c
-// is c+1+j, the predecessor c-1.  Every ring test is taken relative to c with
-// D = K - c: each interval of Chord.cc:452-457, 583-590, 602-674 becomes a
-// compare of D against a distance from c, decided on the order-preserving codes
-// stored in the node record and the finger rows; an equal code (a tie at the
-// code's precision, e.g. a node-ID key) falls back to the exact keys in recs[].
-struct Hop {
-    uint32_t next;   // next hop (== c when c is responsible), NONE when broken
-    uint8_t sib;     // siblings flag of the FindNodeResponse
-    uint8_t broken;  // Chord::closestPreceedingNode threw
-};
-
-__device__ __forceinline__ Hop decide_compact(const ChordView& V, uint32_t c, const NodeRec& R, const K160& K)
-{
-    Hop h;
-    h.sib = 0; h.broken = 0; h.next = NONE;
-    const K160 C = key_of_node(R);
-    const K160 D = k_sub(K, C);
-    const int i0 = k_msb(D);                     // -1 only when K == C
-    // finger entry i0, issued before anything that depends on it (rows are padded by 160 entries)
-    const uint2 f0 = V.frow[R.row + (uint32_t)(KEYBITS - 1 - (i0 < 0 ? KEYBITS - 1 : i0))];
-    if (i0 < 0) { h.sib = 1; h.next = c; return h; }
-    const uint64_t cD = k_code64(D);
-    // isSiblingFor(thisNode, key, 1): K in (pred, C]  <=>  D > pred - C  (Chord.cc:452-457)
-    bool t;
-    if (cD != R.cP) t = cD > R.cP;
-    else t = between_R(K, key_of(load_rec(V.recs, c == 0 ? V.n - 1 : c - 1)), C);
-    if (t) { h.sib = 1; h.next = c; return h; }
-    // K in (C, succ0]  <=>  D <= succ0 - C  (Chord.cc:583-590)
-    const uint32_t s0 = ring_next(c, 1, V.n);
-    if (cD != R.cS0) t = cD < R.cS0;
-    else t = between_R(K, C, key_of(load_rec(V.recs, s0)));
-    if (t) { h.next = s0; return h; }
-    // closestPreceedingNode (Chord.cc:602-674): temp = farthest successor in (C, K]
-    int tj;
-    uint32_t cT;                 // code32 of temp - C
-    bool tIsK = false, gTexact = false;
-    K160 gT;
-    if (cD > R.cSL) {
-        tj = V.ns - 1;
-        cT = (uint32_t)(R.cSL >> 32);
-    } else {
-        tj = -1;
-        for (int j = V.ns - 1; j >= 0; --j) {
-            const K160 SJ = key_of(load_rec(V.recs, ring_next(c, (uint32_t)j + 1, V.n)));
-            if (between_R(SJ, C, K)) { tj = j; gT = k_sub(SJ, C); tIsK = k_eq(SJ, K); break; }
-        }
-        if (tj < 0) { h.broken = 1; return h; }
-        gTexact = true;
-        cT = (uint32_t)(k_code64(gT) >> 32);
-    }
-    // finger scan from i0 down (fingers above i0 lie beyond the key):
-    // finger F in [temp, K]  <=>  temp - C <= F - C <= D
-    const uint32_t cD32 = (uint32_t)(cD >> 32);
-    const int ilo = (int)(R.cS0 >> 56);
-    for (int i = i0; i >= ilo; --i) {
-        const uint2 e = (i == i0) ? f0 : V.frow[R.row + (uint32_t)(KEYBITS - 1 - i)];
-        bool hit;
-        if (e.y != cD32 && e.y != cT) {
-            hit = (e.y < cD32) & (e.y > cT);
-        } else {
-            const K160 dF = k_sub(key_of(load_rec(V.recs, e.x)), C);
-            if (!gTexact) {
-                gT = k_sub(key_of(load_rec(V.recs, ring_next(c, (uint32_t)V.ns, V.n))), C);
-                gTexact = true;
-            }
-            hit = k_le(gT, dF) & k_le(dF, D);
-        }
-        if (hit) { h.next = e.x; return h; }
-    }
-    // trivial positions resolve to succ0 (ChordFingerTable.cc:183-184); succ0 lies in
-    // [temp, K] only when temp is succ0
-    if (tj == 0) { h.next = s0; return h; }
-    // no finger: farthest successor in the OPEN interval (C, K) (Chord.cc:653-658) --
-    // temp itself unless temp == K
-    const int j = tIsK ? tj - 1 : tj;
-    h.next = ring_next(c, (uint32_t)j + 1, V.n);
-    return h;
 }
 
 // general (explicit snapshot) tables: literal restatement incl. unspecified predecessor
@@ -268,36 +220,21 @@ __device__ __forceinline__ Decision decide_general(const ChordView& V, uint32_t 
 // ---------------------------------------------------------------------------
 // K1: batched one-way lookups
 
-// Responder state carried in registers between hops.  Ideal rings: the 64 B
-// NodeRec of the current responder (key, finger-row offset, coordinates, window
-// codes); explicit tables: its 24 B KeyRec (coordinates gathered per hop).
+// Responder state carried in registers between hops for explicit (non-converged)
+// tables: its 24 B KeyRec (coordinates gathered per hop).
 template <bool IDEAL> struct Responder;
-template <> struct Responder<true> {
-    NodeRec n;
-    __device__ __forceinline__ void load(const ChordView& V, uint32_t c) { n = load_node(V.nodes, c); }
-    __device__ __forceinline__ double2 xy(const ChordView&, uint32_t) const { return make_double2(n.x, n.y); }
-    __device__ __forceinline__ Hop decide(const ChordView& V, uint32_t c, const K160& K) const
-    {
-        return decide_compact(V, c, n, K);
-    }
-    __device__ __forceinline__ void advance(const ChordView& V, const Hop& h) { load(V, h.next); }
-};
 template <> struct Responder<false> {
     KeyRec r;
-    KeyRec nxt;
     __device__ __forceinline__ void load(const ChordView& V, uint32_t c) { r = load_rec(V.recs, c); }
     __device__ __forceinline__ double2 xy(const ChordView& V, uint32_t c) const { return V.xy[c]; }
-    __device__ __forceinline__ Hop decide(const ChordView& V, uint32_t c, const K160& K)
+    __device__ __forceinline__ Decision decide(const ChordView& V, uint32_t c, const K160& K) const
     {
-        const Decision d = decide_general(V, c, r, K);
-        nxt = d.rec;
-        Hop h;
-        h.next = d.next; h.sib = d.sib; h.broken = d.broken;
-        return h;
+        return decide_general(V, c, r, K);
     }
-    __device__ __forceinline__ void advance(const ChordView&, const Hop&) { r = nxt; }
+    __device__ __forceinline__ void advance(const ChordView&, const Decision& d) { r = d.rec; }
 };
 
+// K1 on explicit (non-converged) tables: literal restatement, full finger scan.
 template <bool IDEAL, bool RECORD, bool REC>
 __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC, LookupConsts LC,
                                                      const K160* __restrict__ qkeys,
@@ -341,7 +278,7 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
         if (!active) continue;
 
         const double2 cxy = rs.xy(V, cur);
-        const Hop d = rs.decide(V, cur, K);
+        const Decision d = rs.decide(V, cur, K);
 
         uint8_t status = 0xFF;   // 0xFF = still running
         uint32_t R = NONE;
@@ -470,143 +407,375 @@ __device__ __forceinline__ void store_lrec(ovs_lookup_rec* __restrict__ p, uint6
     q[2] = make_uint4((uint32_t)(uint64_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)hops | ((uint32_t)local << 16), 0u);
 }
 
-template <bool REC>
-__global__ __launch_bounds__(256) void k_chord_shard_step(ChordView V, DelayConsts DC, LookupConsts LC,
-                                                          const uint64_t* __restrict__ shard_lo, int nsh, int me, const ovs_lookup_rec* __restrict__ in, uint64_t nin,
-                                                          uint64_t chunk, ovs_lookup_rec* __restrict__ out,
-                                                          uint32_t* __restrict__ out_dest, uint64_t out_cap,
-                                                          unsigned long long* out_count, ovs_done_rec* __restrict__ done,
-                                                          uint64_t done_cap, unsigned long long* done_count)
+// ---------------------------------------------------------------------------
+// K1 on a converged ring: the lookup as a per-lane state machine.
+//
+// Every loop iteration a lane consumes the one 64 B line it requested in the
+// previous iteration, advances its lookup, and requests the next line; no lane
+// waits inside an iteration for a second dependent load of its own.  A wave's
+// iteration therefore costs one memory latency however its 64 lanes diverge (a
+// finger probe that misses, a successor hand-off and a lookup start are each one
+// more iteration of that lane only), and the waves of a SIMD overlap their
+// latencies.  Phases (what the pending line is):
+//   FETCH  the lookup's key and source (route) or its 48 B hand-off record (shard)
+//   START  NodeRec of the responder where the lookup starts / arrives from a shard
+//   NODE   NodeRec of a successor chosen as next hop
+//   PROBE  FingerEnt pi of the current responder (whose key/row stay in registers)
+//   WIN    WinRec of the current responder (K inside its successor window)
+// Exact-key fallbacks on top64 ties read recs[] synchronously (rare).
+enum : uint32_t { PH_FETCH = 0, PH_START = 1, PH_NODE = 2, PH_PROBE = 3, PH_WIN = 4 };
+
+// a responder as unpacked from its NodeRec or from the finger entry pointing at it
+struct Hdr {
+    K160 k;
+    uint32_t row;
+    double x, y;
+    uint64_t gS0, gSL;
+};
+
+__device__ __forceinline__ bool k_zero(const K160& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3] | a.w[4]) == 0; }
+
+__device__ __forceinline__ int msb64(uint64_t x) { return 63 - __clzll((long long)x); }
+
+__device__ __forceinline__ uint64_t u64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+// sign of (D - gap) where gap = key(recs[g]) - C and gt = top64(gap): decided on the top
+// 64 bits, exact on a tie
+__device__ __forceinline__ int cmp_gap(const ChordView& V, const K160& D, uint64_t gt, const K160& C, uint32_t g)
+{
+    const uint64_t Dt = top64(D);
+    if (Dt != gt) return Dt < gt ? -1 : 1;
+    const K160 G = k_sub(key_of(load_rec(V.recs, g)), C);
+    return k_lt(D, G) ? -1 : (k_eq(D, G) ? 0 : 1);
+}
+
+struct LaneIO {
+    // single-GPU route (ovs_route_batch)
+    const K160* __restrict__ qkeys;
+    const uint32_t* __restrict__ qsrc;
+    ovs_route_out* __restrict__ out;
+    uint32_t* __restrict__ hopseq;
+    // one hop round of an arc (ovs_shard_step)
+    const ovs_lookup_rec* __restrict__ in;
+    ovs_lookup_rec* __restrict__ sout;
+    uint32_t* __restrict__ sdest;
+    uint64_t scap;
+    unsigned long long* scount;
+    ovs_done_rec* __restrict__ done;
+    uint64_t dcap;
+    unsigned long long* dcount;
+    const uint64_t* __restrict__ shard_lo;
+    int nsh, me;
+    uint64_t n, chunk;
+};
+
+template <bool REC, bool RECORD, bool SHARD>
+__global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    uint64_t cursor = wave * chunk;
-    const uint64_t end = min(cursor + chunk, nin);
+    uint64_t cursor = wave * io.chunk;                    // wave-uniform
+    const uint64_t end = min(cursor + io.chunk, io.n);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int ns = V.ns;
+    const int hcm = LC.hopCountMax;
 
     bool active = false;
-    uint32_t S = 0, cur = 0, qid = 0;
+    uint32_t ph = PH_FETCH;
+    uint64_t q = 0;
+    uint32_t qid = 0;
     K160 K;
-    NodeRec cn;
-    double sx = 0, sy = 0;
+    uint32_t S = 0, cur = 0;
     int64_t t = 0;
     int hops = 0;
-    bool local = false;
+    bool local = true, nsib = false, pend = false;
+    double sx = 0, sy = 0;            // iterative: the source's coordinates; recursive: the last sender's
+    // the responder whose next hop is being determined (PROBE / WIN)
+    K160 C;
+    uint32_t row = 0;
+    uint64_t gSL = 0;
+    int pi = 0, ilo = 0, esl = 0;
+    uint32_t fb = 0;                  // closestPreceedingNode's successor fallback (Chord.cc:653-658)
+    bool gTx = false;                 // temp == K (node-ID key): a finger hits only when it is K
+    const uint4* lp = nullptr;        // the line requested for the next iteration
+    uint4 L0 = make_uint4(0, 0, 0, 0), L1 = L0, L2 = L0, L3 = L0;
 
     while (true) {
+        // ---- refill: lanes without a lookup take the next of the wave's slice
+        bool fresh = false;
         const uint64_t need = __ballot(!active);
         if (need != 0 && cursor < end) {
             const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
             if (!active && mine < end) {
-                const ovs_lookup_rec r = load_lrec(in, mine);
+                q = mine;
                 active = true;
-                for (int w = 0; w < 5; ++w) K.w[w] = r.key[w];
-                S = r.src; cur = r.cur; qid = r.qid; t = r.t_ns; hops = r.hops; local = r.local != 0;
-                cn = load_node(V.nodes, cur);
-                const double2 sxy = V.xy[S];     // source coordinates (replicated on every rank)
-                sx = sxy.x; sy = sxy.y;
+                fresh = true;
+                ph = PH_FETCH;
+                if (SHARD) {
+                    const uint4* r = reinterpret_cast<const uint4*>(io.in + q);
+                    L0 = r[0]; L1 = r[1]; L2 = r[2];
+                } else {
+                    K = io.qkeys[q];
+                    S = io.qsrc[q];
+                }
             }
             cursor += (uint64_t)__popcll(need);
         }
         if (!__any(active)) break;
 
-        bool emit_done = false, emit_out = false;
-        int dest = 0;
-        ovs_route_out o;
-        if (active) {
-            const double2 cxy = make_double2(cn.x, cn.y);
-            const Hop d = decide_compact(V, cur, cn, K);
-            uint8_t status = 0xFF;
+        if (active && !fresh) {
+            bool arrived = false, asib = false, fin = false;
+            uint8_t status = OVS_LOOKUP_OK;
             uint32_t R = NONE;
-            if (REC) {
-                // recursive route message (same rules as k_chord_route<.., REC>); the hop's
-                // delay was charged when the message was sent
-                const bool at_src = local;
-                local = false;
-                if (d.sib && (!at_src || hops < LC.hopCountMax)) { status = OVS_LOOKUP_OK; R = cur; }
-                else if (d.sib) status = OVS_LOOKUP_HOPMAX;
-                else if (d.broken) status = OVS_LOOKUP_BROKEN;
-                else if (hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;
-                else if (d.next == S || d.next == cur) status = OVS_LOOKUP_NO_NEXT;
-                else {
-                    const double2 nxy = V.xy[d.next];   // coordinates are replicated on every rank
-                    t += DC.msgRoute + coord_ns(cxy.x, cxy.y, nxy.x, nxy.y, DC.round);
-                    ++hops;
-                    cur = d.next;
-                    dest = shard_owner(shard_lo, nsh, cur);
-                    if (dest != me) { emit_out = true; active = false; }
-                    else cn = load_node(V.nodes, cur);
-                }
-                if (status != 0xFF) {
-                    o.hops = (uint16_t)(status == OVS_LOOKUP_OK ? hops : 0);
-                    o.status = status;
-                    o.responsible = R;
-                    o.one_way_hops = (uint8_t)(status == OVS_LOOKUP_OK ? hops : 0);
-                    o.latency_ns = status == OVS_LOOKUP_OK ? t : -1;
-                    emit_done = true;
-                    active = false;
-                }
-            } else if (local) {
-                local = false;
-                if (d.broken) status = OVS_LOOKUP_BROKEN;
-                else if (d.sib) { status = OVS_LOOKUP_OK; R = S; }
-            } else {
-                const int64_t cd = coord_ns(sx, sy, cxy.x, cxy.y, DC.round);
-                const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
-                if (rtt >= DC.rpcTimeout) {
-                    status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
+            Hdr A;
+            uint32_t nxt = NONE;      // next hop chosen this iteration ...
+            bool nxt_node = false;    // ... whose header must be read from its NodeRec
+            bool nxt_sib = false;
+            lp = nullptr;
+
+            // ---- consume the pending line
+            if (ph == PH_FETCH) {
+                if (SHARD) {
+                    K.w[0] = L0.x; K.w[1] = L0.y; K.w[2] = L0.z; K.w[3] = L0.w; K.w[4] = L1.x;
+                    S = L1.y; cur = L1.z; qid = L1.w;
+                    t = (int64_t)u64(L2.x, L2.y);
+                    hops = (int)(L2.z & 0xFFFF);
+                    local = ((L2.z >> 16) & 0xFF) != 0;
+                    if (!REC) {
+                        const double2 sxy = V.xy[S];      // coordinates are replicated on every rank
+                        sx = sxy.x; sy = sxy.y;
+                    }
                 } else {
-                    t += rtt;
-                    if (t > DC.lookupTimeout) status = OVS_LOOKUP_TIMEOUT;
-                    else {
-                        ++hops;
-                        if (d.broken) status = OVS_LOOKUP_BROKEN;
-                        else if (d.sib) { status = OVS_LOOKUP_OK; R = cur; }
+                    cur = S; t = 0; hops = 0; local = true;
+                }
+                lp = reinterpret_cast<const uint4*>(V.nodes + cur);
+                ph = PH_START;
+            } else {
+                // the 64 B line: NodeRec and FingerEnt share key, coordinates and window distances
+                A.k.w[0] = L0.x; A.k.w[1] = L0.y; A.k.w[2] = L0.z; A.k.w[3] = L0.w; A.k.w[4] = L1.x;
+                A.x = dbl(L1.z, L1.w);
+                A.y = dbl(L2.x, L2.y);
+                A.gS0 = u64(L2.z, L2.w);
+                A.gSL = u64(L3.x, L3.y);
+                if (ph == PH_START) {
+                    A.row = L1.y;
+                    // isSiblingFor(cur, K, 1): K in (pred, cur]  <=>  D == 0 or D > pred - cur (Chord.cc:452-457)
+                    const K160 D = k_sub(K, A.k);
+                    asib = k_zero(D) || cmp_gap(V, D, u64(L3.z, L3.w), A.k, cur == 0 ? V.n - 1 : cur - 1) > 0;
+                    if (!SHARD && !REC) { sx = A.x; sy = A.y; }
+                    arrived = true;
+                } else if (ph == PH_NODE) {
+                    A.row = L1.y;
+                    asib = nsib;
+                    if (REC && pend) t += DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round);   // to a successor
+                    arrived = true;
+                } else if (ph == PH_PROBE) {
+                    // finger pi of C lies in [temp, K]  <=>  temp - C <= F - C <= D
+                    A.row = L3.z;
+                    const K160 D = k_sub(K, C);
+                    const K160 dF = k_sub(A.k, C);
+                    bool hit = k_le(dF, D);
+                    if (hit) {
+                        if (gTx) hit = k_eq(dF, D);                        // temp == K
+                        else if (pi >= esl) hit = !k_zero(dF);             // 2^pi > temp - C
+                        else hit = cmp_gap(V, dF, gSL, C, ring_next(cur, (uint32_t)ns, V.n)) >= 0;
+                    }
+                    if (hit) {
+                        // a finger short of K is not responsible: (pred F, F] lies inside (C, F]
+                        nxt = L1.y; nxt_sib = k_eq(A.k, K);
+                    } else if (--pi >= ilo) {
+                        lp = reinterpret_cast<const uint4*>(V.frow + (uint64_t)row + (uint32_t)(KEYBITS - 1 - pi));
+                    } else {
+                        nxt = fb; nxt_node = true;       // Chord.cc:653-658 (succ0 via 183-184 when temp == succ0)
+                    }
+                } else {
+                    // PH_WIN: K inside the successor window; temp = farthest s_j <= K (Chord.cc:612-623)
+                    const K160 D = k_sub(K, C);
+                    const uint64_t Dt = top64(D);
+                    const uint64_t g[8] = {u64(L0.x, L0.y), u64(L0.z, L0.w), u64(L1.x, L1.y), u64(L1.z, L1.w),
+                                           u64(L2.x, L2.y), u64(L2.z, L2.w), u64(L3.x, L3.y), u64(L3.z, L3.w)};
+                    int tj = -1;
+                    bool tie = false;
+                    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (j < ns) {
+                            tie |= g[j] == Dt;
+                            if (g[j] < Dt) tj = j;
+                        }
+                    }
+                    bool tIsK = false;
+                    if (tie) {
+                        tj = -1;
+                        for (int j = ns - 1; j >= 0; --j) {
+                            const K160 SJ = key_of(load_rec(V.recs, ring_next(cur, (uint32_t)j + 1, V.n)));
+                            if (between_R(SJ, C, K)) { tj = j; tIsK = k_eq(SJ, K); break; }
+                        }
+                    }
+                    if (tj < 0) {
+                        fin = true; status = OVS_LOOKUP_BROKEN;
+                    } else if (!tIsK) {
+                        // the only node in [temp, K] is temp: every finger that hits is temp and the
+                        // successor fallback is temp too -- the next hop is temp either way
+                        nxt = ring_next(cur, (uint32_t)tj + 1, V.n); nxt_node = true;
+                    } else {
+                        // temp == K: temp if a finger points at it, else s_{tj-1}
+                        gTx = true;
+                        fb = ring_next(cur, (uint32_t)tj, V.n);
+                        pi = k_msb(D);
+                        if (pi >= ilo) {
+                            lp = reinterpret_cast<const uint4*>(V.frow + (uint64_t)row + (uint32_t)(KEYBITS - 1 - pi));
+                            ph = PH_PROBE;
+                        } else {
+                            nxt = fb; nxt_node = true;
+                        }
                     }
                 }
             }
-            if (!REC && status == 0xFF) {
-                if (LC.hopCountMax && hops >= LC.hopCountMax) status = OVS_LOOKUP_HOPMAX;
-                else if (d.next == S) status = OVS_LOOKUP_NO_NEXT;
-                else {
-                    cur = d.next;
-                    dest = shard_owner(shard_lo, nsh, cur);
-                    if (dest != me) { emit_out = true; active = false; }
-                    else cn = load_node(V.nodes, cur);
+
+            // ---- IterativePathLookup::sendRpc / BaseOverlay::sendToKey for a chosen next hop;
+            // returns true when the next responder's header is already in A (finger entry)
+            auto send = [&](uint32_t nx, bool via_node, bool nx_sib) -> bool {
+                if (REC) {
+                    if (nx == S || nx == cur) { fin = true; status = OVS_LOOKUP_NO_NEXT; return false; }  // BaseOverlay.cc:1502-1516
+                    if (RECORD && !SHARD && hops < hcm) io.hopseq[q * (uint64_t)hcm + hops] = nx;
+                    ++hops;
+                } else if (nx == S) {
+                    fin = true; status = OVS_LOOKUP_NO_NEXT; return false;                             // visitOnlyOnce
                 }
+                if (SHARD) {
+                    const int dest = shard_owner(io.shard_lo, io.nsh, nx);
+                    if (dest != io.me) {
+                        // hand the lookup to the owner of its next responder
+                        if (REC) {
+                            const double2 nxy = via_node ? V.xy[nx] : make_double2(A.x, A.y);
+                            t += DC.msgRoute + coord_ns(sx, sy, nxy.x, nxy.y, DC.round);
+                        }
+                        const unsigned long long oi = atomicAdd(io.scount, 1ull);
+                        if (oi < io.scap) {
+                            store_lrec(io.sout, oi, K, S, nx, qid, t, hops, 0);
+                            io.sdest[oi] = (uint32_t)dest;
+                        }
+                        active = false;
+                        lp = nullptr;
+                        return false;
+                    }
+                }
+                cur = nx;
+                if (via_node) {
+                    nsib = nx_sib; pend = REC;
+                    lp = reinterpret_cast<const uint4*>(V.nodes + nx);
+                    ph = PH_NODE;
+                    return false;
+                }
+                if (REC) t += DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round);
+                asib = nx_sib;
+                return true;
+            };
+            if (!fin && nxt != NONE) arrived = send(nxt, nxt_node, nxt_sib);
+
+            // ---- a responder is reached: its FindNodeResponse (iterative) / the route message (recursive)
+            if (arrived) {
+                uint32_t nx2 = NONE;
+                bool nx2_sib = false;
+                if (REC) {
+                    const bool at_src = local;
+                    local = false;
+                    sx = A.x; sy = A.y;
+                    if (asib && (!at_src || hops < hcm)) { fin = true; R = cur; }       // BaseOverlay.cc:907-914
+                    else if (asib || hops >= hcm) { fin = true; status = OVS_LOOKUP_HOPMAX; }   // 1464-1488
+                } else if (local) {
+                    // IterativeLookup::start (IterativeLookup.cc:157-204): local step, no hop, no delay
+                    local = false;
+                    if (asib) { fin = true; R = S; }
+                } else {
+                    // FindNodeCall S->cur, FindNodeResponse cur->S (one NodeHandle)
+                    const int64_t cd = coord_ns(sx, sy, A.x, A.y, DC.round);
+                    const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
+                    if (rtt >= DC.rpcTimeout) {
+                        fin = true;
+                        status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
+                    } else {
+                        t += rtt;
+                        if (t > DC.lookupTimeout) { fin = true; status = OVS_LOOKUP_TIMEOUT; }  // IterativeLookup.cc:808-815
+                        else {
+                            if (RECORD && !SHARD && hops < hcm) io.hopseq[q * (uint64_t)hcm + hops] = cur;
+                            ++hops;
+                            if (asib) { fin = true; R = cur; }                                   // 896-905
+                        }
+                    }
+                }
+                // sendRpc's hop limit (IterativeLookup.cc:1067-1170) is checked before the next hop
+                // is known: equivalent, as findNode cannot throw on a converged ring
+                if (!REC && !fin && hcm && hops >= hcm) { fin = true; status = OVS_LOOKUP_HOPMAX; }
+                if (!fin) {
+                    // findNode at cur for a key it is not responsible for (Chord.cc:583-674)
+                    C = A.k; row = A.row; gSL = A.gSL; gTx = false;
+                    const K160 D = k_sub(K, C);
+                    const uint32_t s0 = ring_next(cur, 1, V.n);
+                    if (cmp_gap(V, D, A.gS0, C, s0) <= 0) {
+                        nx2 = s0; nx2_sib = true;                      // K in (C, succ0] (Chord.cc:583-590)
+                    } else {
+                        ilo = A.gS0 ? 97 + msb64(A.gS0) : k_msb(k_sub(key_of(load_rec(V.recs, s0)), C)) + 1;
+                        esl = gSL ? 97 + msb64(gSL) : 96;
+                        const uint32_t sl = ring_next(cur, (uint32_t)ns, V.n);
+                        const int c = cmp_gap(V, D, gSL, C, sl);
+                        if (c < 0) {
+                            lp = reinterpret_cast<const uint4*>(V.win + (cur - V.lo));   // K inside the window
+                            ph = PH_WIN;
+                        } else {
+                            // temp = succ[ns-1]; fingers from msb(D) down
+                            gTx = c == 0;
+                            fb = gTx ? ring_next(cur, (uint32_t)ns - 1, V.n) : sl;
+                            pi = k_msb(D);
+                            if (pi >= ilo) {
+                                lp = reinterpret_cast<const uint4*>(V.frow + (uint64_t)row + (uint32_t)(KEYBITS - 1 - pi));
+                                ph = PH_PROBE;
+                            } else {
+                                nx2 = fb;
+                            }
+                        }
+                    }
+                }
+                if (!fin && nx2 != NONE) send(nx2, true, nx2_sib);
             }
-            if (!REC && status != 0xFF) {
-                o.hops = (uint16_t)hops;
-                o.status = status;
-                if (status == OVS_LOOKUP_OK) {
+
+            if (fin) {
+                ovs_route_out o;
+                if (REC) {
+                    const bool ok = status == OVS_LOOKUP_OK;
+                    o.hops = (uint16_t)(ok ? hops : 0);
+                    o.one_way_hops = (uint8_t)(ok ? hops : 0);
+                    o.latency_ns = ok ? t : -1;
+                    o.responsible = ok ? R : NONE;
+                } else if (status == OVS_LOOKUP_OK) {
+                    o.hops = (uint16_t)hops;
                     o.responsible = R;
                     o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
-                    o.latency_ns = t + (R != S ? DC.msgRoute + coord_ns(sx, sy, cxy.x, cxy.y, DC.round) : 0);
+                    // sendRouteMessage to result[0] (BaseOverlay.cc:1107-1146); 0 delay to self
+                    o.latency_ns = t + (R != S ? DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round) : 0);
                 } else {
+                    o.hops = (uint16_t)hops;
                     o.responsible = NONE;
                     o.one_way_hops = 0;
                     o.latency_ns = -1;
                 }
-                emit_done = true;
+                o.status = status;
+                if (SHARD) {
+                    const unsigned long long di = atomicAdd(io.dcount, 1ull);
+                    if (di < io.dcap) {
+                        ovs_done_rec dr;
+                        dr.qid = qid; dr.pad = 0; dr.out = o;
+                        io.done[di] = dr;
+                    }
+                } else {
+                    io.out[q] = o;
+                }
                 active = false;
+                lp = nullptr;
             }
         }
-        // append (hipcc turns these per-lane adds into one wave-level atomic per counter)
-        if (emit_done) {
-            const unsigned long long di = atomicAdd(done_count, 1ull);
-            if (di < done_cap) {
-                ovs_done_rec dr;
-                dr.qid = qid; dr.pad = 0; dr.out = o;
-                done[di] = dr;
-            }
-        }
-        if (emit_out) {
-            const unsigned long long oi = atomicAdd(out_count, 1ull);
-            if (oi < out_cap) {
-                store_lrec(out, oi, K, S, cur, qid, t, hops, 0);
-                out_dest[oi] = (uint32_t)dest;
-            }
-        }
+        // ---- request the next line (one 64 B gather per lane)
+        if (active && lp) { L0 = lp[0]; L1 = lp[1]; L2 = lp[2]; L3 = lp[3]; }
     }
 }
 
@@ -644,7 +813,7 @@ __global__ void k_chord_find_node(ChordView V, int ideal, const uint32_t* __rest
     const uint32_t s0 = ssize > 0 ? succ_at(0) : c;
     const int ilo = ideal ? k_msb(k_sub(key_of(load_rec(V.recs, s0)), C)) + 1 : 0;
     auto finger_at = [&](int pos) -> uint32_t {
-        if (ideal) return pos >= ilo ? V.frow[crec.aux + (uint32_t)(KEYBITS - 1 - pos)].x : s0;
+        if (ideal) return pos >= ilo ? V.frow[crec.aux + (uint32_t)(KEYBITS - 1 - pos)].idx : s0;
         return V.fres[(uint64_t)c * KEYBITS + pos];
     };
     const bool sib = ideal ? between_R(K, key_of(load_rec(V.recs, c == 0 ? V.n - 1 : c - 1)), C)
@@ -710,7 +879,7 @@ hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hi
     return hipGetLastError();
 }
 
-hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, uint2** fingers_out,
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, FingerEnt** fingers_out,
                               uint64_t* nfing_out, hipStream_t s)
 {
     hipError_t e;
@@ -731,12 +900,12 @@ hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi
     hipMemcpyAsync(&total, off + cnt, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
     if (total + KEYBITS >= 0xFFFFFFFFull) { hipFree(rowlen); hipFree(off); hipFree(tmp); return hipErrorInvalidValue; }
-    uint2* fing = nullptr;
+    FingerEnt* fing = nullptr;
     // +160 entries of padding: the kernel's speculative first-finger read may run past a row
-    if ((e = hipMalloc(&fing, sizeof(uint2) * (total + KEYBITS))) != hipSuccess) {
+    if ((e = hipMalloc(&fing, sizeof(FingerEnt) * (total + KEYBITS))) != hipSuccess) {
         hipFree(rowlen); hipFree(off); hipFree(tmp); return e;
     }
-    hipMemsetAsync(fing, 0, sizeof(uint2) * (total + KEYBITS), s);
+    hipMemsetAsync(fing, 0, sizeof(FingerEnt) * (total + KEYBITS), s);
     hipLaunchKernelGGL(k_set_aux, dim3(nblk(cnt, 256)), dim3(256), 0, s, recs, off, lo, cnt);
     hipLaunchKernelGGL(k_chord_fill, dim3(nblk(cnt, 128)), dim3(128), 0, s, recs, n, lo, cnt, fing);
     e = hipStreamSynchronize(s);
@@ -747,14 +916,17 @@ hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi
     return hipGetLastError();
 }
 
-hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes, hipStream_t s)
+hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes,
+                              FingerEnt* fingers, uint64_t nfing, WinRec* win, uint32_t lo, uint32_t hi, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_chord_nodes, dim3(nblk(n, 256)), dim3(256), 0, s, recs, xy, n, ns, nodes);
+    if (hi > lo) hipLaunchKernelGGL(k_chord_win, dim3(nblk(hi - lo, 256)), dim3(256), 0, s, recs, n, lo, hi - lo, ns, win);
+    if (nfing) hipLaunchKernelGGL(k_chord_entries, dim3(nblk(nfing, 256)), dim3(256), 0, s, nodes, fingers, nfing);
     return hipGetLastError();
 }
 
-hipError_t launch_chord_export(const KeyRec* recs, const uint2* fingers, uint32_t n, uint32_t* out,
+hipError_t launch_chord_export(const KeyRec* recs, const FingerEnt* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s)
 {
     const uint64_t tot = (uint64_t)n * KEYBITS;
@@ -762,18 +934,32 @@ hipError_t launch_chord_export(const KeyRec* recs, const uint2* fingers, uint32_
     return hipGetLastError();
 }
 
-template <bool IDEAL, bool RECORD, bool REC>
-static int route_blocks_per_cu()
+// occupancy-sized persistent grid: every resident wave owns one contiguous slice of the work
+template <class Kern>
+static uint64_t persistent_chunk(Kern k, int* cache, uint64_t n, int num_cu, uint64_t* blocks)
+{
+    if (*cache == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, 256, 0) != hipSuccess || b < 1) b = 1;
+        *cache = b;
+    }
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)(*cache) * 4;   // 4 waves per block
+    uint64_t chunk = (n + waves - 1) / waves;
+    if (chunk < 1) chunk = 1;
+    const uint64_t need_waves = (n + chunk - 1) / chunk;
+    *blocks = (need_waves + 3) / 4;
+    return chunk;
+}
+
+template <bool REC, bool RECORD, bool SHARD>
+static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC, LaneIO io,
+                               int num_cu, hipStream_t s)
 {
     static int bpc = 0;
-    if (bpc == 0) {
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_route<IDEAL, RECORD, REC>, 256, 0) != hipSuccess ||
-            b < 1)
-            b = 1;
-        bpc = b;
-    }
-    return bpc;
+    uint64_t blocks = 0;
+    io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD>, &bpc, io.n, num_cu, &blocks);
+    hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC, io);
+    return hipGetLastError();
 }
 
 template <bool IDEAL, bool RECORD, bool REC>
@@ -781,15 +967,18 @@ static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, 
                                      const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
                                      uint32_t* hopseq, int num_cu, hipStream_t s)
 {
-    // persistent grid: every resident wave owns one contiguous slice of the batch
-    const uint64_t waves = (uint64_t)num_cu * route_blocks_per_cu<IDEAL, RECORD, REC>() * 4;   // 4 waves per block
-    uint64_t chunk = (nq + waves - 1) / waves;
-    if (chunk < 1) chunk = 1;
-    const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    const uint64_t blocks = (need_waves + 3) / 4;
-    hipLaunchKernelGGL((k_chord_route<IDEAL, RECORD, REC>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC, qkeys,
-                       qsrc, nq, chunk, out, hopseq);
-    return hipGetLastError();
+    if constexpr (IDEAL) {
+        LaneIO io{};
+        io.qkeys = qkeys; io.qsrc = qsrc; io.out = out; io.hopseq = hopseq; io.n = nq;
+        return lanes_launch<REC, RECORD, false>(V, DC, LC, io, num_cu, s);
+    } else {
+        static int bpc = 0;
+        uint64_t blocks = 0;
+        const uint64_t chunk = persistent_chunk(k_chord_route<false, RECORD, REC>, &bpc, nq, num_cu, &blocks);
+        hipLaunchKernelGGL((k_chord_route<false, RECORD, REC>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC,
+                           qkeys, qsrc, nq, chunk, out, hopseq);
+        return hipGetLastError();
+    }
 }
 
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
@@ -841,19 +1030,6 @@ hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t
     return hipGetLastError();
 }
 
-template <bool REC>
-static int shard_blocks_per_cu()
-{
-    static int bpc = 0;
-    if (bpc == 0) {
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_chord_shard_step<REC>, 256, 0) != hipSuccess || b < 1)
-            b = 1;
-        bpc = b;
-    }
-    return bpc;
-}
-
 hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
                                    const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
                                    ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
@@ -861,19 +1037,12 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    unsigned long long* done_count, int num_cu, hipStream_t s)
 {
     if (nin == 0) return hipSuccess;
-    const int bpc = LC.recursive ? shard_blocks_per_cu<true>() : shard_blocks_per_cu<false>();
-    const uint64_t waves = (uint64_t)num_cu * bpc * 4;
-    uint64_t chunk = (nin + waves - 1) / waves;
-    if (chunk < 1) chunk = 1;
-    const uint64_t need_waves = (nin + chunk - 1) / chunk;
-    const dim3 g((unsigned)((need_waves + 3) / 4)), b(256);
-    if (LC.recursive)
-        hipLaunchKernelGGL(k_chord_shard_step<true>, g, b, 0, s, V, DC, LC, shard_lo, nsh, me, in, nin, chunk, out,
-                           out_dest, out_cap, out_count, done, done_cap, done_count);
-    else
-        hipLaunchKernelGGL(k_chord_shard_step<false>, g, b, 0, s, V, DC, LC, shard_lo, nsh, me, in, nin, chunk, out,
-                           out_dest, out_cap, out_count, done, done_cap, done_count);
-    return hipGetLastError();
+    LaneIO io{};
+    io.in = in; io.sout = out; io.sdest = out_dest; io.scap = out_cap; io.scount = out_count;
+    io.done = done; io.dcap = done_cap; io.dcount = done_count;
+    io.shard_lo = shard_lo; io.nsh = nsh; io.me = me; io.n = nin;
+    return LC.recursive ? lanes_launch<true, false, true>(V, DC, LC, io, num_cu, s)
+                        : lanes_launch<false, false, true>(V, DC, LC, io, num_cu, s);
 }
 
 hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,

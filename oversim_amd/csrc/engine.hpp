@@ -65,47 +65,55 @@ __device__ __forceinline__ KeyRec load_rec(const KeyRec* __restrict__ recs, uint
 }
 
 // ---------------------------------------------------------------------------
-// Chord node record of the converged ring: everything one hop at node c reads
-// about c, in one 64 B line.  The ring window (pred, succ0, succ[ns-1]) enters
-// as order-preserving codes of its distances from c (k_code64), so the
-// isSiblingFor / (c, succ0] / temp tests cost no extra gather; an equal code
-// falls back to the exact keys in recs[].
+// Converged-ring (ideal) Chord layout.  A hop at responder c normally reads ONE
+// 64 B line: the finger entry closestPreceedingNode selects carries, besides the
+// finger's index, everything the NEXT hop needs about that finger (key,
+// coordinates, finger-row offset, the distances of its successor window), so
+// the lookup never gathers the next node's record separately.  Ring distances
+// d from a node enter as their top 64 bits (bits 96..159, top64()); a compare of
+// D = K - c against such a distance is decided unless the top bits are equal,
+// and then falls back to the exact keys in recs[] (a tie means K lies within
+// 2^96 of a node: node-ID keys, or adjacent IDs closer than 2^96).
+//
+// NodeRec: per node -- lookup sources, successor hand-offs, shard arrivals.
 struct alignas(64) NodeRec {
     uint32_t w[5];   // node key
     uint32_t row;    // offset of the node's finger row (valid on the arc that owns the row)
     double x, y;     // SimpleUnderlay coordinates
-    uint64_t cP;     // k_code64((pred - c) mod 2^160)
-    uint64_t cS0;    // k_code64(succ0 - c);  cS0 >> 56 = i_lo = first non-trivial finger
-    uint64_t cSL;    // k_code64(succ[ns-1] - c), ns = min(successorListSize, n - 1)
+    uint64_t gS0;    // top64(succ0 - v)
+    uint64_t gSL;    // top64(succ[ns-1] - v), ns = min(successorListSize, n - 1)
+    uint64_t gP;     // top64((pred - v) mod 2^160)
 };
 static_assert(sizeof(NodeRec) == 64, "NodeRec is one 64 B line");
 
-__device__ __forceinline__ NodeRec load_node(const NodeRec* __restrict__ p, uint32_t i)
-{
-    const uint4* q = reinterpret_cast<const uint4*>(p + i);
-    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
-    NodeRec r;
-    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w; r.w[4] = b.x; r.row = b.y;
-    r.x = __hiloint2double((int)b.w, (int)b.z);
-    r.y = __hiloint2double((int)c.y, (int)c.x);
-    r.cP = (uint64_t)c.z | ((uint64_t)c.w << 32);
-    r.cS0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
-    r.cSL = (uint64_t)d.z | ((uint64_t)d.w << 32);
-    return r;
-}
+// FingerEnt: row(v)[159 - i] = finger i of v (non-trivial i >= i_lo(v)).
+struct alignas(64) FingerEnt {
+    uint32_t w[5];   // finger key
+    uint32_t idx;    // finger node index
+    double x, y;     // finger coordinates
+    uint64_t gS0;    // the finger's own window distances (its NodeRec fields)
+    uint64_t gSL;
+    uint32_t row;    // the finger's own row offset
+    uint32_t pad;
+};
+static_assert(sizeof(FingerEnt) == 64, "FingerEnt is one 64 B line");
 
-__device__ __forceinline__ K160 key_of_node(const NodeRec& r)
-{
-    K160 k;
-    for (int i = 0; i < 5; ++i) k.w[i] = r.w[i];
-    return k;
-}
+// WinRec: per node of the arc, top64(succ_j - v) for j = 0..7 (unused slots all-ones);
+// read only when K falls inside the successor window.
+struct alignas(64) WinRec {
+    uint64_t g[8];
+};
+
+__device__ __host__ __forceinline__ uint64_t top64(const K160& a) { return (uint64_t)a.w[3] | ((uint64_t)a.w[4] << 32); }
+
+__device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) { return __hiloint2double((int)hi, (int)lo); }
 
 // Chord device view.
 //  recs[n]      : sorted node keys (24 B), aux = offset of the node's finger row
 //  xy[n]        : SimpleUnderlay coordinates (fp64)
 //  nodes[n]     : ideal mode -- NodeRec per node (64 B)
-//  frow[...]    : ideal mode -- CSR rows of {finger index, k_code64(finger - v) >> 32},
+//  win[hi-lo]   : ideal mode -- WinRec per node of the arc [lo, hi)
+//  frow[...]    : ideal mode -- CSR rows of FingerEnt (64 B),
 //                 row(v)[159 - i] = finger i for the non-trivial positions
 //                 i >= i_lo(v) = msb(succ0 - v) + 1 (trivial positions resolve to
 //                 succ0, ChordFingerTable.cc:183-184)
@@ -114,7 +122,9 @@ struct ChordView {
     const KeyRec* __restrict__ recs;
     const double2* __restrict__ xy;
     const NodeRec* __restrict__ nodes;
-    const uint2* __restrict__ frow;
+    const FingerEnt* __restrict__ frow;
+    const WinRec* __restrict__ win;
+    uint32_t lo;       // ideal: first node of this context's arc (win index base)
     const uint32_t* __restrict__ pred;
     const uint32_t* __restrict__ succ;
     const uint8_t* __restrict__ nsucc;

@@ -5,7 +5,7 @@
 namespace ovs {
 
 hipError_t launch_check_sorted(const KeyRec* recs, uint32_t n, uint32_t* bad, hipStream_t s);
-hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, uint2** fingers_out,
+hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi, FingerEnt** fingers_out,
                               uint64_t* nfing_out, hipStream_t s);
 hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
                                    const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
@@ -14,8 +14,9 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    unsigned long long* done_count, int num_cu, hipStream_t s);
 hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
                                ovs_lookup_rec* out, hipStream_t s);
-hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes, hipStream_t s);
-hipError_t launch_chord_export(const KeyRec* recs, const uint2* fingers, uint32_t n, uint32_t* out,
+hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes,
+                              FingerEnt* fingers, uint64_t nfing, WinRec* win, uint32_t lo, uint32_t hi, hipStream_t s);
+hipError_t launch_chord_export(const KeyRec* recs, const FingerEnt* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s);
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,

@@ -32,9 +32,10 @@ struct ovs_ctx {
     // chord
     KeyRec* recs = nullptr;
     double2* xy = nullptr;
-    uint2* fingers = nullptr;      // ideal finger rows {index, distance code}
+    FingerEnt* fingers = nullptr;  // ideal finger rows (64 B entries)
     uint64_t nfing = 0;
-    NodeRec* nodes = nullptr;      // ideal node records (built for successorListSize = nodes_ns)
+    NodeRec* nodes = nullptr;      // ideal node records + finger entries built for successorListSize = nodes_ns
+    WinRec* win = nullptr;         // ideal successor windows of the arc [shard_lo, shard_hi)
     int nodes_ns = -1;
     uint32_t* pred = nullptr;
     uint32_t* succ = nullptr;
@@ -78,10 +79,10 @@ ovs_status hip_fail(ovs_ctx* c, hipError_t e, const char* where)
 
 void free_tables(ovs_ctx* c)
 {
-    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres, c->nodes};
+    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres, c->nodes, c->win};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    c->nodes = nullptr; c->nodes_ns = -1;
+    c->nodes = nullptr; c->win = nullptr; c->nodes_ns = -1;
     c->recs = nullptr; c->xy = nullptr; c->fingers = nullptr; c->pred = nullptr;
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
@@ -188,7 +189,9 @@ ovs_status to_device(ovs_ctx* c, const T* src, uint64_t count, bool dev, T** out
 ChordView chord_view(const ovs_ctx* c)
 {
     ChordView V{};
-    V.recs = c->recs; V.xy = c->xy; V.nodes = c->nodes; V.frow = c->fingers; V.pred = c->pred; V.succ = c->succ;
+    V.recs = c->recs; V.xy = c->xy; V.nodes = c->nodes; V.frow = c->fingers; V.win = c->win;
+    V.lo = (uint32_t)c->shard_lo;
+    V.pred = c->pred; V.succ = c->succ;
     V.nsucc = c->nsucc; V.fres = c->fres; V.n = (uint32_t)c->n;
     V.ns = (int)std::min<uint64_t>((uint64_t)c->P.successorListSize, c->n - 1);
     V.sls = c->sls;
@@ -204,7 +207,9 @@ ovs_status ensure_nodes(ovs_ctx* c, hipStream_t s)
     if (c->nodes && c->nodes_ns == ns) return OVS_OK;
     if (ns < 1) return fail(c, OVS_EINVAL, "successorListSize must be >= 1");
     if (!c->nodes) HIPCHK(c, hipMalloc(&c->nodes, sizeof(NodeRec) * c->n));
-    HIPCHK(c, launch_chord_nodes(c->recs, c->xy, (uint32_t)c->n, ns, c->nodes, s));
+    if (!c->win) HIPCHK(c, hipMalloc(&c->win, sizeof(WinRec) * (c->shard_hi - c->shard_lo)));
+    HIPCHK(c, launch_chord_nodes(c->recs, c->xy, (uint32_t)c->n, ns, c->nodes, c->fingers, c->nfing, c->win,
+                                 (uint32_t)c->shard_lo, (uint32_t)c->shard_hi, s));
     c->nodes_ns = ns;
     return OVS_OK;
 }

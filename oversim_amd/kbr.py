@@ -25,7 +25,8 @@ from pathlib import Path
 
 import numpy as np
 
-_LIB_PATH = Path(__file__).resolve().parent / "libovs_kbr.so"
+# OVS_LIB selects an experimental build of the same engine (tools/variants.sh); default: the in-tree build
+_LIB_PATH = Path(os.environ.get("OVS_LIB") or Path(__file__).resolve().parent / "libovs_kbr.so")
 
 OVERLAY_CHORD = 1
 OVERLAY_KADEMLIA = 2
