@@ -500,7 +500,15 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
     const uint4* lp = nullptr;        // the line requested for the next iteration
     uint4 L0 = make_uint4(0, 0, 0, 0), L1 = L0, L2 = L0, L3 = L0;
 
+    __shared__ uint4 xbuf[4][256];    // per wave: the 64 gathered lines, 4 chunks each
+    uint4* const xb = xbuf[threadIdx.x >> 6];
+
     while (true) {
+        // ---- gathered lines to their lanes: chunk (lane & 3) of the line of lane 16k + (lane >> 2)
+        // was fetched into Lk; LDS slot 4 * owner + chunk = 64 k + lane (same wave: in order)
+        xb[lane] = L0; xb[64 + lane] = L1; xb[128 + lane] = L2; xb[192 + lane] = L3;
+        L0 = xb[4 * lane]; L1 = xb[4 * lane + 1]; L2 = xb[4 * lane + 2]; L3 = xb[4 * lane + 3];
+
         // ---- refill: lanes without a lookup take the next of the wave's slice
         bool fresh = false;
         const uint64_t need = __ballot(!active);
@@ -512,11 +520,12 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 fresh = true;
                 ph = PH_FETCH;
                 if (SHARD) {
-                    const uint4* r = reinterpret_cast<const uint4*>(io.in + q);
-                    L0 = r[0]; L1 = r[1]; L2 = r[2];
+                    // the 48 B hand-off record comes through the cooperative gather (tag 1: 3 chunks)
+                    lp = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(io.in + q) | 1u);
                 } else {
                     K = io.qkeys[q];
                     S = io.qsrc[q];
+                    lp = nullptr;
                 }
             }
             cursor += (uint64_t)__popcll(need);
@@ -774,8 +783,24 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 lp = nullptr;
             }
         }
-        // ---- request the next line (one 64 B gather per lane)
-        if (active && lp) { L0 = lp[0]; L1 = lp[1]; L2 = lp[2]; L3 = lp[3]; }
+        // ---- request the next line: a cooperative gather, 4 lanes fetch one 64 B line with one
+        // 16 B load each, so one wave instruction touches 16 lines instead of 64 (on HBM-resident
+        // tables this moves 2.3x the lines/s of per-lane 4 x 16 B loads: tools/ubench/gather.hip)
+        {
+            const uint64_t mine = (active && lp) ? reinterpret_cast<uint64_t>(lp) : 0ull;
+            const uint32_t mlo = (uint32_t)mine, mhi = (uint32_t)(mine >> 32);
+            const int ch = lane & 3;
+            uint4 v[4];
+            #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int owner = 16 * k + (lane >> 2);
+                const uint64_t a = (uint64_t)__shfl(mlo, owner) | ((uint64_t)__shfl(mhi, owner) << 32);
+                // tag 1 = a 48 B record: no fourth chunk
+                if (a != 0 && (ch < 3 || !(a & 1))) v[k] = reinterpret_cast<const uint4*>(a & ~(uint64_t)15)[ch];
+                else v[k] = make_uint4(0, 0, 0, 0);
+            }
+            L0 = v[0]; L1 = v[1]; L2 = v[2]; L3 = v[3];
+        }
     }
 }
 
