@@ -33,7 +33,16 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-B_HOP = 512                    # algorithmic bytes per Chord hop
+# measured ceiling of dependent random 64 B line gathers from an HBM-resident table (cooperative
+# 16 B-per-lane loads, tools/ubench/gather.hip, profiles/r01_j_coop/ubench.txt): 3.9e10-4.7e10 lines/s
+GATHER_CEILING_GBS = 2950.0
+# Algorithmic bytes.  Chord, converged-ring layout of this build: every hop reads
+# the responder's 64 B header line (the finger entry that selected it, or its NodeRec), every
+# lookup additionally its source's NodeRec (64 B) and its key/source/result (24 B in, 16 B out).
+# SURVEY.md §8(d) priced 512 B/hop for a 24 B-record layout with separate window, finger and
+# coordinate gathers; that figure is reported beside ("survey_bytes_per_hop"), not used.
+B_HOP, B_LOOKUP = 64, 104
+B_HOP_SURVEY = 512
 B_RPC = 448                    # algorithmic bytes per evaluated Kademlia RPC
 
 
@@ -50,6 +59,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0xC)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (tools/pmc_json.py); default profiles/pmc/<workload>.json when present")
     ap.add_argument("--traffic-csv", default=None,
                     help="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE outputs (counter_collection.csv or run_results.db), "
                          "comma separated")
@@ -88,6 +99,21 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
             "sample": f"oracle/ovs_oracle.c restatement, {m2} of the step's lookups on the same "
                       f"{len(ids)}-node {kind} network, OpenMP {nthreads} threads, {dt:.1f} s",
             "lookups_per_s": m2 / dt}
+
+
+def traffic_from_json(path: str | None, workload: str, kname: str):
+    """HBM bytes per launch of the dominant kernel from a committed PMC summary
+    (profiles/pmc/<workload>.json, written by tools/pmc_json.py from rocprofv3 --pmc FETCH_SIZE and
+    WRITE_SIZE passes of this same workload).  FETCH_SIZE counts the random 64 B line gathers of
+    these kernels at 64 B each -- calibrated on tools/ubench/gather.hip with a known byte count
+    (profiles/r01_j_coop/calib.txt) -- so no x2 correction is applied."""
+    p = Path(path) if path else ROOT / "profiles" / "pmc" / f"{workload}.json"
+    if not p.exists():
+        return None, None
+    d = json.loads(p.read_text())
+    if kname not in d.get("kernel", ""):
+        return None, None
+    return 1024.0 * (d["fetch_kb"] + d["write_kb"]), str(p.relative_to(ROOT) if p.is_absolute() and ROOT in p.parents else p)
 
 
 def traffic_from_csv(path: str | None, kernel_substr: str):
@@ -197,7 +223,7 @@ def main():
         if kind == "chord":
             sh = ShardedChord(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
                               params=Params.chord().replace(routingType=routing_type))
-            kname = "k_chord_shard_step"
+            kname = "k_chord_lanes"
         else:
             sh = ShardedKademlia(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
                                  params=Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
@@ -210,7 +236,7 @@ def main():
         if kind == "chord":
             eng.set_params(Params.chord().replace(routingType=routing_type))
             eng.chord_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
-            kname = "k_chord_route"
+            kname = "k_chord_lanes"
         else:
             eng.set_params(Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
             eng.kad_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
@@ -272,12 +298,17 @@ def main():
 
     if rank == 0:
         value = hop_all * a.steps / wall_max
+        lookups_launch = n_ok
         if kind == "chord":
-            per_launch_bytes, bper = hop_total * B_HOP, B_HOP
+            per_launch_bytes = hop_total * B_HOP + lookups_launch * B_LOOKUP
+            bper = f"{B_HOP} B/hop + {B_LOOKUP} B/lookup"
         else:
-            per_launch_bytes, bper = rpc_total * B_RPC, B_RPC
+            per_launch_bytes, bper = rpc_total * B_RPC, f"{B_RPC} B/RPC"
         achieved = per_launch_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = traffic_from_csv(a.traffic_csv, kname)
+        traffic, traffic_src = (traffic_from_json(a.traffic_json, a.workload, kname) if world == 1 and not sharded
+                                else (None, None))
+        if a.traffic_csv:
+            traffic, traffic_src = traffic_from_csv(a.traffic_csv, kname), a.traffic_csv
         cpu = None
         if world == 1 and not a.no_cpu_baseline and small:
             cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type)
@@ -314,7 +345,9 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": kname, "kernel_ms": kern_ms,
-                "algorithmic_bytes_per_unit": bper, "unit_of_work": "hop" if kind == "chord" else "RPC",
+                "algorithmic_bytes": bper, "unit_of_work": "hop" if kind == "chord" else "RPC",
+                "traffic_source": traffic_src,
+                "gather_ceiling_GBs": GATHER_CEILING_GBS,
             },
             "cpu_baseline": cpu,
         }
