@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 1
+#define OVS_ABI_VERSION 2
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -261,15 +261,18 @@ ovs_status  ovs_chord_load_shard(ovs_ctx* ctx, const ovs_key160* ids_all_sorted,
 ovs_status  ovs_shard_make_records(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
                                    uint64_t n, uint32_t qid_base, ovs_lookup_rec* recs, void* stream);
 /* One hop round: advance every record of `in` while its responder is on this
- * arc.  Records whose next responder is remote are appended to `out` with the
- * owner rank in out_dest; finished lookups are appended to `done`.
- * *out_count and *done_count are device counters incremented by the kernel.
+ * arc.  A record whose next responder lies on arc d != this one is appended to
+ * segment d of `out` (out + d * out_cap records, the send buffer of the
+ * all-to-allv, grouped by destination in the kernel itself) and counted in
+ * out_count[d]; finished lookups are appended to `done` (done_count).
+ * out_count (nshards counters) and done_count are device counters the kernel
+ * increments; the caller zeroes them.  A segment never receives more than
+ * n_in records, so out_cap = n_in is always enough.
  * shard_lo is a HOST array of nshards+1 arc boundaries (sorted-index space). */
 ovs_status  ovs_shard_step(ovs_ctx* ctx, const ovs_lookup_rec* in, uint64_t n_in,
-                           ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
-                           unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                           unsigned long long* done_count, const uint64_t* shard_lo,
-                           uint32_t nshards, void* stream);
+                           ovs_lookup_rec* out, uint64_t out_cap, unsigned long long* out_count,
+                           ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                           const uint64_t* shard_lo, uint32_t nshards, void* stream);
 
 /* ---- multi-GPU Kademlia ----
  * The sorted ring is cut into contiguous arcs (ID prefixes); a rank holds the

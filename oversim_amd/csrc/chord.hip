@@ -457,10 +457,9 @@ struct LaneIO {
     uint32_t* __restrict__ hopseq;
     // one hop round of an arc (ovs_shard_step)
     const ovs_lookup_rec* __restrict__ in;
-    ovs_lookup_rec* __restrict__ sout;
-    uint32_t* __restrict__ sdest;
+    ovs_lookup_rec* __restrict__ sout;     // nsh segments of scap records, one per destination arc
     uint64_t scap;
-    unsigned long long* scount;
+    unsigned long long* scount;            // nsh counters
     ovs_done_rec* __restrict__ done;
     uint64_t dcap;
     unsigned long long* dcount;
@@ -499,6 +498,7 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
     bool gTx = false;                 // temp == K (node-ID key): a finger hits only when it is K
     const uint4* lp = nullptr;        // the line requested for the next iteration
     uint4 L0 = make_uint4(0, 0, 0, 0), L1 = L0, L2 = L0, L3 = L0;
+    int hand = -1;                    // shard: this lane's lookup moves to arc `hand` this iteration
 
     __shared__ uint4 xbuf[4][256];    // per wave: the 64 gathered lines, 4 chunks each
     uint4* const xb = xbuf[threadIdx.x >> 6];
@@ -537,6 +537,7 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
             uint8_t status = OVS_LOOKUP_OK;
             uint32_t R = NONE;
             Hdr A;
+            int emit = -1;            // shard: destination arc of a hand-off made this iteration
             uint32_t nxt = NONE;      // next hop chosen this iteration ...
             bool nxt_node = false;    // ... whose header must be read from its NodeRec
             bool nxt_sib = false;
@@ -659,11 +660,8 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                             const double2 nxy = via_node ? V.xy[nx] : make_double2(A.x, A.y);
                             t += DC.msgRoute + coord_ns(sx, sy, nxy.x, nxy.y, DC.round);
                         }
-                        const unsigned long long oi = atomicAdd(io.scount, 1ull);
-                        if (oi < io.scap) {
-                            store_lrec(io.sout, oi, K, S, nx, qid, t, hops, 0);
-                            io.sdest[oi] = (uint32_t)dest;
-                        }
+                        cur = nx;
+                        emit = dest;
                         active = false;
                         lp = nullptr;
                         return false;
@@ -782,6 +780,24 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 active = false;
                 lp = nullptr;
             }
+            if (SHARD) hand = emit;
+        }
+        if (SHARD) {
+            // ---- hand-offs appended to their destination's segment: one atomic per wave and
+            // destination (ballot + prefix count), so the outbox needs no grouping afterwards
+            for (int d = 0; d < io.nsh; ++d) {
+                const uint64_t mk = __ballot(hand == d);
+                if (mk == 0) continue;
+                const int leader = __ffsll((long long)mk) - 1;
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(io.scount + d, (unsigned long long)__popcll(mk));
+                base = __shfl(base, leader);
+                if (hand == d) {
+                    const unsigned long long oi = base + (unsigned long long)__popcll(mk & lt_mask);
+                    if (oi < io.scap) store_lrec(io.sout + (uint64_t)d * io.scap, oi, K, S, cur, qid, t, hops, 0);
+                }
+            }
+            hand = -1;
         }
         // ---- request the next line: a cooperative gather, 4 lanes fetch one 64 B line with one
         // 16 B load each, so one wave instruction touches 16 lines instead of 64 (on HBM-resident
@@ -1057,13 +1073,13 @@ hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t
 
 hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
                                    const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
-                                   ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
+                                   ovs_lookup_rec* out, uint64_t out_cap,
                                    unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                                    unsigned long long* done_count, int num_cu, hipStream_t s)
 {
     if (nin == 0) return hipSuccess;
     LaneIO io{};
-    io.in = in; io.sout = out; io.sdest = out_dest; io.scap = out_cap; io.scount = out_count;
+    io.in = in; io.sout = out; io.scap = out_cap; io.scount = out_count;
     io.done = done; io.dcap = done_cap; io.dcount = done_count;
     io.shard_lo = shard_lo; io.nsh = nsh; io.me = me; io.n = nin;
     return LC.recursive ? lanes_launch<true, false, true>(V, DC, LC, io, num_cu, s)

@@ -9,7 +9,7 @@ hipError_t launch_chord_build(KeyRec* recs, uint32_t n, uint32_t lo, uint32_t hi
                               uint64_t* nfing_out, hipStream_t s);
 hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
                                    const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
-                                   ovs_lookup_rec* out, uint32_t* out_dest, uint64_t out_cap,
+                                   ovs_lookup_rec* out, uint64_t out_cap,
                                    unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                                    unsigned long long* done_count, int num_cu, hipStream_t s);
 hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,

@@ -387,13 +387,12 @@ ovs_status ovs_shard_make_records(ovs_ctx* c, const ovs_key160* keys, const uint
     return OVS_OK;
 }
 
-ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out,
-                          uint32_t* out_dest, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,
-                          uint64_t done_cap, unsigned long long* done_count, const uint64_t* shard_lo,
-                          uint32_t nshards, void* stream)
+ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out, uint64_t out_cap,
+                          unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                          unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
 {
     if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
-    if (n_in && (!in || !out || !out_dest || !out_count || !done || !done_count)) return OVS_EINVAL;
+    if (n_in && (!in || !out || !out_count || !done || !done_count)) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_CHORD || !c->ideal) return fail(c, OVS_ESTATE, "no Chord ring (shard) loaded");
     ovs_status st = check_common(c, c->P);
     if (st == OVS_OK) st = check_chord_route(c, c->P);
@@ -417,7 +416,7 @@ ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, o
     st = ensure_nodes(c, s);
     if (st != OVS_OK) return st;
     HIPCHK(c, launch_chord_shard_step(chord_view(c), delay_consts(c->P), LC, c->d_bounds, (int)nshards, me, in, n_in, out,
-                                      out_dest, out_cap, out_count, done, done_cap, done_count, c->num_cu, s));
+                                      out_cap, out_count, done, done_cap, done_count, c->num_cu, s));
     return OVS_OK;
 }
 

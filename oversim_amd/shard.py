@@ -3,16 +3,17 @@ lookups handed between ranks every hop round by an all-to-allv.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm, the
 exchange runs over xGMI).  Node keys and coordinates are replicated on every
-rank (24 + 16 B per node), finger rows exist only for the rank's own arc, so a
-lookup is forwarded to the rank that owns its next responder -- the message a
-FindNodeCall would be in OverSim (BaseOverlay.cc:1841-1915).  Per round:
+rank, finger rows exist only for the rank's own arc, so a lookup is forwarded
+to the rank that owns its next responder -- the message a FindNodeCall would be
+in OverSim (BaseOverlay.cc:1841-1915).  Per round:
 
   1. ovs_shard_step advances every inbound record while its responder is
-     local; remote hand-offs go to an outbox tagged with the owner rank,
-     finished lookups to the rank's done buffer;
-  2. the outbox is grouped by destination (stable sort on the tag);
-  3. counts all-to-all, then records all-to-allv (48 B per lookup);
-  4. a 1-element all-reduce decides termination.
+     local; a hand-off is appended by the kernel to the send segment of its
+     destination rank (no grouping pass), finished lookups to the done buffer;
+  2. one all-gather of the per-destination counts gives every rank the whole
+     count matrix (sizes of the all-to-allv and the termination test) -- the
+     round's only host synchronisation;
+  3. one all-to-allv moves the records (48 B per lookup).
 
 The orchestration is independent of the stepper (the HIP kernel here, a CPU
 test double in tests/) and of the exchange (torch.distributed, or an in-process
@@ -63,6 +64,7 @@ class GpuShardStepper:
         self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
         self.cap = 0
         self._ensure(capacity)
+        self.out_count = torch.zeros(self.world, dtype=torch.int64, device=device)
         self.done_count = torch.zeros(1, dtype=torch.int64, device=device)
         self.done = torch.empty((max(capacity, 1), DONE_BYTES), dtype=torch.uint8, device=device)
         self.done_cap = max(capacity, 1)
@@ -72,17 +74,15 @@ class GpuShardStepper:
         self._ev1 = torch.cuda.Event(enable_timing=True)
 
     def _ensure(self, cap: int):
-        torch = self.torch
         if cap <= self.cap:
             return
         self.cap = cap
-        self.out = torch.empty((cap, REC_BYTES), dtype=torch.uint8, device=self.dev)
-        self.out_dest = torch.empty(cap, dtype=torch.int32, device=self.dev)
-        self.out_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        # one send segment of `cap` records per destination rank
+        self.out = self.torch.empty((self.world, cap, REC_BYTES), dtype=self.torch.uint8, device=self.dev)
 
     def _s(self):
         # every kernel of the round runs on torch's current stream, so the torch ops around it
-        # (counter resets, grouping, the collectives) are ordered with it
+        # (counter resets, the collectives) are ordered with it
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
 
     def reset(self, capacity: int):
@@ -100,22 +100,27 @@ class GpuShardStepper:
         return recs
 
     def step(self, inbox):
+        """One round; returns (send segments [world, cap, 48], per-destination counts on the device)."""
         n_in = inbox.shape[0]
         self._ensure(n_in)
         self.out_count.zero_()
         if self.timing:
             self._ev0.record()
         st = lib().ovs_shard_step(self.eng._h, C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(self.out.data_ptr()),
-                                  C.c_void_p(self.out_dest.data_ptr()), self.cap, C.c_void_p(self.out_count.data_ptr()),
+                                  self.cap, C.c_void_p(self.out_count.data_ptr()),
                                   C.c_void_p(self.done.data_ptr()), self.done_cap,
                                   C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
         self.eng._chk(st, "ovs_shard_step")
         if self.timing:
             self._ev1.record()
-        m = int(self.out_count.item())
-        if self.timing:
+            self._timed = True
+        return self.out, self.out_count
+
+    def collect_timing(self):
+        """Add the last step's kernel time (call after the round's host synchronisation)."""
+        if self.timing and getattr(self, "_timed", False):
             self.kernel_ms += self._ev0.elapsed_time(self._ev1)
-        return self.out[:m], self.out_dest[:m]
+            self._timed = False
 
     def finished(self):
         k = int(self.done_count.item())
@@ -127,7 +132,7 @@ class GpuShardStepper:
 for _name, _args in {
     "ovs_chord_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
     "ovs_shard_make_records": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p],
-    "ovs_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+    "ovs_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
     "ovs_kad_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
     "ovs_kad_shard_begin": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p],
@@ -151,7 +156,16 @@ class TorchExchange:
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.world, self.group = torch, dist, world, group
+        self.rank = dist.get_rank(group)
         self.comm_dev = device   # tensors handed to the collective live here
+
+    def count_matrix(self, counts) -> np.ndarray:
+        """All-gather every rank's per-destination counts: M[s, d] = records rank s sends to d."""
+        torch = self.torch
+        c = counts.to(self.comm_dev, dtype=torch.int64).reshape(-1)
+        parts = [torch.empty_like(c) for _ in range(self.world)]
+        self.dist.all_gather(parts, c, group=self.group)
+        return torch.stack(parts).cpu().numpy()
 
     def counts(self, send_counts):
         """Exchange per-destination counts; returns (send counts, receive counts) as lists."""
@@ -181,7 +195,7 @@ class TorchExchange:
 
 
 def group_by_dest(out, dest, world: int):
-    """Stable grouping of the outbox by destination rank (counting sort)."""
+    """Stable grouping of an outbox by destination rank (Kademlia request path)."""
     import torch
     if out.shape[0] == 0:
         return out, torch.zeros(world, dtype=torch.int64, device=out.device)
@@ -191,18 +205,31 @@ def group_by_dest(out, dest, world: int):
     return out.index_select(0, order), counts
 
 
+def _send_buffer(out, row):
+    """The all-to-allv send buffer: destination segments out[d][:row[d]] back to back."""
+    import torch
+    parts = [out[d][: int(k)] for d, k in enumerate(row) if k]
+    if not parts:
+        return out[0][:0]
+    return parts[0] if len(parts) == 1 else torch.cat(parts)
+
+
 def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 10_000):
     """Route one batch of lookups originating on this rank; returns (done records, rounds)."""
     inbox = stepper.make_records(keys_t, src_t, qid_base)
     rounds = 0
+    me = exchange.rank
     while True:
         rounds += 1
-        out, dest = stepper.step(inbox)
-        send, counts = group_by_dest(out, dest, exchange.world)
-        recv = exchange.exchange(send, counts)
-        if recv is None:
+        out, counts = stepper.step(inbox)
+        M = exchange.count_matrix(counts)          # the round's host synchronisation
+        if hasattr(stepper, "collect_timing"):
+            stepper.collect_timing()
+        if int(M.sum()) == 0:
             break
-        inbox = recv if recv.device == out.device else recv.to(out.device)
+        send = _send_buffer(out, M[me])
+        recv = exchange.records(send, M[me].tolist(), M[:, me].tolist())
+        inbox = recv if recv.device == send.device else recv.to(send.device)
         if rounds > max_rounds:
             raise RuntimeError("sharded routing did not terminate")
     return stepper.finished(), rounds
@@ -219,14 +246,14 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
         buckets = [[] for _ in range(W)]
         moved = 0
         for r in range(W):
-            out, dest = steppers[r].step(inbox[r])
-            send, counts = group_by_dest(out, dest, W)
-            off = 0
-            for d, c in enumerate(counts.tolist()):
-                if c:
-                    buckets[d].append(send[off:off + c].clone())
-                    moved += c
-                off += c
+            out, counts = steppers[r].step(inbox[r])
+            row = counts.cpu().tolist()
+            if hasattr(steppers[r], "collect_timing"):
+                steppers[r].collect_timing()
+            for d, k in enumerate(row):
+                if k:
+                    buckets[d].append(out[d][:k].clone())
+                    moved += k
         if moved == 0:
             break
         dev = steppers[0].dev
@@ -409,7 +436,7 @@ class ShardedChord:
     def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None):
         self.bounds = arc_bounds(len(ids), world)
         n = keys_t.shape[0]
-        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(2 * n, 1024), params=params)
+        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(n + n // 4, 1024), params=params)
         self.stepper.reset(world * n + 1024)
         self.stepper.timing = True
         self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)

@@ -91,9 +91,14 @@ class CpuShardStepper:
                     out.append(o)
                     dest.append(self.owner(cur))
                     break
-        o = np.array(out, dtype=self.REC) if out else np.zeros(0, dtype=self.REC)
-        return (torch.from_numpy(o.view(np.uint8).reshape(-1, 48).copy()),
-                torch.tensor(dest, dtype=torch.int32))
+        # per-destination send segments, as the kernel writes them
+        world = len(self.bounds) - 1
+        segs = []
+        for d in range(world):
+            o = [r for r, x in zip(out, dest) if x == d]
+            o = np.array(o, dtype=self.REC) if o else np.zeros(0, dtype=self.REC)
+            segs.append(torch.from_numpy(o.view(np.uint8).reshape(-1, 48).copy()))
+        return segs, torch.tensor([s.shape[0] for s in segs], dtype=torch.int64)
 
     def finished(self):
         d = np.zeros(len(self.done), dtype=self.DONE)
