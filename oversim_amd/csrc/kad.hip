@@ -12,6 +12,8 @@
 // distance with an exact 160-bit fallback on ties.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "kad_dev.hpp"
 
 namespace ovs {
@@ -100,6 +102,16 @@ __global__ void k_kad_sibentries(const KeyRec* __restrict__ recs, const uint32_t
     const K160 k = x == NONE ? K160{{0, 0, 0, 0, 0}} : kload(recs, x);
     for (int w = 0; w < 5; ++w) e.key[w] = k.w[w];
     sibe[i] = e;
+}
+
+// 1 when two node IDs share their top 63 bits (then top-64 XOR distances of distinct nodes can
+// tie and the K2 comparisons need the exact fallback, cand_lt<true>); IDs are sorted, so
+// adjacent pairs suffice
+__global__ void k_kad_prefix_ties(const KeyRec* __restrict__ recs, uint32_t n, uint32_t* flag)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i + 1 >= n) return;
+    if (((top64(kload(recs, i)) ^ top64(kload(recs, i + 1))) >> 1) == 0) atomicOr(flag, 1u);
 }
 
 __global__ void k_kad_set_boff(KadRec* recs, const uint64_t* off, uint32_t n)
@@ -208,6 +220,7 @@ struct SendNothing {
 };
 
 // the responder's findNode evaluated in place (all tables on this GPU)
+template <bool EX>
 struct LocalFindNode {
     const KadView& V;
     const K160& K;
@@ -215,7 +228,7 @@ struct LocalFindNode {
     __device__ __forceinline__ bool ready(int) const { return true; }
     __device__ __forceinline__ void fill(int, uint32_t r, const KadRec& rr, bool sb, SVec<8>& res) const
     {
-        kad_find_node1(V, r, rr, K, redundant, sb, res);
+        kad_find_node1<8, EX>(V, r, rr, K, redundant, sb, res);
     }
 };
 
@@ -230,7 +243,7 @@ struct HopRecorder {
     }
 };
 
-template <int A, bool RECORD>
+template <int A, bool RECORD, bool EX>
 __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, KadLC LC, const K160* __restrict__ qkeys,
                                                    const uint32_t* __restrict__ qsrc, uint64_t nq, uint64_t chunk,
                                                    ovs_route_out* __restrict__ out, uint32_t* __restrict__ hopseq,
@@ -256,7 +269,7 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
                 q = mine;
                 active = true;
                 kad_lookup_init(L, qkeys[q], qsrc[q], V.xy);
-                kad_lookup_start(L, V, DC, LC, res, on);
+                kad_lookup_start<A, EX>(L, V, DC, LC, res, on);
             }
             cursor += (uint64_t)__popcll(need);
         }
@@ -264,9 +277,9 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
         if (!active) continue;
 
         if (!kad_lookup_done(L)) {
-            const LocalFindNode fn{V, L.K, LC.redundant};
+            const LocalFindNode<EX> fn{V, L.K, LC.redundant};
             const HopRecorder<RECORD> rec{hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
-            kad_lookup_event(L, V, DC, LC, res, fn, on, rec);
+            kad_lookup_event<A, EX>(L, V, DC, LC, res, fn, on, rec);
         }
         if (kad_lookup_done(L)) {
             out[q] = kad_lookup_output(L, V, DC, LC);
@@ -356,9 +369,17 @@ hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed
                        (uint64_t)nown * S5, t.sibe);
     hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(nown, 64)), dim3(64), 0, st, recs, t.recs, n, k, S5, seed, t.sib,
                        t.slots, lo, hi);
+    uint32_t* tie = nullptr;
+    uint32_t htie = 1;
+    if ((e = hipMalloc(&tie, sizeof(uint32_t))) != hipSuccess) { cleanup(); return e; }
+    hipMemsetAsync(tie, 0, sizeof(uint32_t), st);
+    if (n > 1) hipLaunchKernelGGL(k_kad_prefix_ties, dim3(nblk(n, 256)), dim3(256), 0, st, recs, n, tie);
+    hipMemcpyAsync(&htie, tie, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
     e = hipStreamSynchronize(st);
+    hipFree(tie);
     cleanup();
     if (e != hipSuccess) return e;
+    t.exact = htie != 0 || getenv("OVS_KAD_EXACT") != nullptr;
     return hipGetLastError();
 }
 
@@ -381,28 +402,28 @@ hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_
     return e;
 }
 
-template <int A, bool RECORD>
+template <int A, bool RECORD, bool EX>
 static int kad_blocks_per_cu()
 {
     static int bpc = 0;
     if (bpc == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD>, 256, 0) != hipSuccess || b < 1) b = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX>, 256, 0) != hipSuccess || b < 1) b = 1;
         bpc = b;
     }
     return bpc;
 }
 
-template <int A, bool RECORD>
+template <int A, bool RECORD, bool EX>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
                              const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
                              int num_cu, hipStream_t st)
 {
-    const uint64_t waves = (uint64_t)num_cu * kad_blocks_per_cu<A, RECORD>() * 4;
+    const uint64_t waves = (uint64_t)num_cu * kad_blocks_per_cu<A, RECORD, EX>() * 4;
     uint64_t chunk = (nq + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
     const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    hipLaunchKernelGGL((k_kad_route<A, RECORD>), dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, st, V, DC, LC,
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX>), dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, st, V, DC, LC,
                        qkeys, qsrc, nq, chunk, out, hopseq, rpcs);
     return hipGetLastError();
 }
@@ -418,8 +439,9 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
     const KadView V = kad_make_view(t, xy, n);
     // strictParallelRpcs: never more than alpha FindNodeCalls in flight (IterativeLookup.cc:1078-1079)
     const int A = P.lookupParallelRpcs;
-#define KL(a) (hopseq ? kad_launch<a, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st) \
-                      : kad_launch<a, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st))
+#define KLX(a, x) (hopseq ? kad_launch<a, true, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st) \
+                          : kad_launch<a, false, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st))
+#define KL(a) (t.exact ? KLX(a, true) : KLX(a, false))
     switch (A) {
     case 1: return KL(1);
     case 2: return KL(2);
@@ -427,6 +449,7 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
     default: return KL(4);
     }
 #undef KL
+#undef KLX
 }
 
 hipError_t kad_find_node(const KadTables& t, const KeyRec* recs, uint32_t n, const ovs_params& P, const uint32_t* node,

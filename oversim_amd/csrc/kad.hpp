@@ -36,6 +36,7 @@ struct KadTables {
     uint32_t lo = 0, hi = 0;      // sib / sibe / bucket rows exist for nodes [lo, hi) (the whole ring unsharded)
     int k = 8, s = 8;
     uint64_t seed = 0;
+    int exact = 1;                // two IDs share their top 63 bits: K2 uses the 160-bit tie fallback
 };
 
 struct KadView {

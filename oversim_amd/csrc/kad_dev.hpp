@@ -77,9 +77,14 @@ __device__ __forceinline__ bool closer(uint64_t da, uint32_t ia, uint64_t db, ui
     return k_lt(xa, xb);
 }
 
+// top 64 bits of the XOR distance, clamped below the empty-entry sentinel ~0 (a real distance
+// of ~0 becomes ~0 - 1: ordered before every empty entry, and with KadView::exact == 0 still
+// unique, as no two node IDs then share their top 63 bits)
+__device__ __forceinline__ uint64_t dclamp(uint64_t d) { return d == ~0ull ? ~0ull - 1 : d; }
+
 __device__ __forceinline__ uint64_t dist_hi(const K160& x, const K160& K)
 {
-    return ((uint64_t)(x.w[4] ^ K.w[4]) << 32) | (uint64_t)(x.w[3] ^ K.w[3]);
+    return dclamp(((uint64_t)(x.w[4] ^ K.w[4]) << 32) | (uint64_t)(x.w[3] ^ K.w[3]));
 }
 
 template <int CAP>
@@ -138,9 +143,18 @@ __device__ __forceinline__ int svec_add(SVec<CAP>& v, int cap, uint32_t x, uint6
 // top 8 with a bitonic merge (8 min + 12 comparators).  Empty entries are (~0, NONE) and
 // sort last; equal top-64-bit distances fall back to the exact 160-bit compare.
 
+// XOR distances of distinct nodes to one key are distinct (XOR is a bijection); their top 64
+// bits can tie only when the two node IDs share their top 64 bits.  EX = false is used when the
+// build found no two IDs sharing their top 63 bits (KadTables::exact == 0): the one 64-bit
+// compare is then exact and branch-free.  EX = true keeps the 160-bit fallback on ties.
+template <bool EX>
 __device__ __forceinline__ bool cand_lt(uint64_t da, uint32_t ia, uint64_t db, uint32_t ib, const K160& K,
                                         const KadRec* __restrict__ recs)
 {
+    if constexpr (!EX) {
+        (void)ia; (void)ib; (void)K; (void)recs;
+        return da < db;
+    }
     if (da != db) return da < db;
     if (ia == ib || ia == NONE) return false;
     if (ib == NONE) return true;
@@ -154,10 +168,10 @@ struct Blk8 {
     uint32_t f[8];     // payload flags (LookupVector merge: bit 0 alreadyUsed, bit 1 from the response)
 };
 
-template <bool F>
+template <bool F, bool EX>
 __device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, const KadRec* __restrict__ recs)
 {
-    const bool s = cand_lt(b.d[j], b.x[j], b.d[i], b.x[i], K, recs);
+    const bool s = cand_lt<EX>(b.d[j], b.x[j], b.d[i], b.x[i], K, recs);
     const uint64_t di = s ? b.d[j] : b.d[i], dj = s ? b.d[i] : b.d[j];
     const uint32_t xi = s ? b.x[j] : b.x[i], xj = s ? b.x[i] : b.x[j];
     b.d[i] = di; b.d[j] = dj; b.x[i] = xi; b.x[j] = xj;
@@ -168,32 +182,32 @@ __device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, con
 }
 
 // Batcher odd-even merge sort, 19 comparators
-template <bool F>
+template <bool F, bool EX>
 __device__ __forceinline__ void blk_sort8(Blk8& b, const K160& K, const KadRec* __restrict__ recs)
 {
-    blk_ce<F>(b, 0, 1, K, recs); blk_ce<F>(b, 2, 3, K, recs); blk_ce<F>(b, 4, 5, K, recs); blk_ce<F>(b, 6, 7, K, recs);
-    blk_ce<F>(b, 0, 2, K, recs); blk_ce<F>(b, 1, 3, K, recs); blk_ce<F>(b, 4, 6, K, recs); blk_ce<F>(b, 5, 7, K, recs);
-    blk_ce<F>(b, 1, 2, K, recs); blk_ce<F>(b, 5, 6, K, recs);
-    blk_ce<F>(b, 0, 4, K, recs); blk_ce<F>(b, 1, 5, K, recs); blk_ce<F>(b, 2, 6, K, recs); blk_ce<F>(b, 3, 7, K, recs);
-    blk_ce<F>(b, 2, 4, K, recs); blk_ce<F>(b, 3, 5, K, recs);
-    blk_ce<F>(b, 1, 2, K, recs); blk_ce<F>(b, 3, 4, K, recs); blk_ce<F>(b, 5, 6, K, recs);
+    blk_ce<F, EX>(b, 0, 1, K, recs); blk_ce<F, EX>(b, 2, 3, K, recs); blk_ce<F, EX>(b, 4, 5, K, recs); blk_ce<F, EX>(b, 6, 7, K, recs);
+    blk_ce<F, EX>(b, 0, 2, K, recs); blk_ce<F, EX>(b, 1, 3, K, recs); blk_ce<F, EX>(b, 4, 6, K, recs); blk_ce<F, EX>(b, 5, 7, K, recs);
+    blk_ce<F, EX>(b, 1, 2, K, recs); blk_ce<F, EX>(b, 5, 6, K, recs);
+    blk_ce<F, EX>(b, 0, 4, K, recs); blk_ce<F, EX>(b, 1, 5, K, recs); blk_ce<F, EX>(b, 2, 6, K, recs); blk_ce<F, EX>(b, 3, 7, K, recs);
+    blk_ce<F, EX>(b, 2, 4, K, recs); blk_ce<F, EX>(b, 3, 5, K, recs);
+    blk_ce<F, EX>(b, 1, 2, K, recs); blk_ce<F, EX>(b, 3, 4, K, recs); blk_ce<F, EX>(b, 5, 6, K, recs);
 }
 
 // a <- the 8 smallest of sorted a and sorted b, sorted
-template <bool F>
+template <bool F, bool EX>
 __device__ __forceinline__ void blk_merge_top8(Blk8& a, const Blk8& b, const K160& K, const KadRec* __restrict__ recs)
 {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const bool s = cand_lt(b.d[7 - i], b.x[7 - i], a.d[i], a.x[i], K, recs);
+        const bool s = cand_lt<EX>(b.d[7 - i], b.x[7 - i], a.d[i], a.x[i], K, recs);
         a.d[i] = s ? b.d[7 - i] : a.d[i];
         a.x[i] = s ? b.x[7 - i] : a.x[i];
         if (F) a.f[i] = s ? b.f[7 - i] : a.f[i];
     }
     // a is bitonic: half-cleaners at distance 4, 2, 1
-    blk_ce<F>(a, 0, 4, K, recs); blk_ce<F>(a, 1, 5, K, recs); blk_ce<F>(a, 2, 6, K, recs); blk_ce<F>(a, 3, 7, K, recs);
-    blk_ce<F>(a, 0, 2, K, recs); blk_ce<F>(a, 1, 3, K, recs); blk_ce<F>(a, 4, 6, K, recs); blk_ce<F>(a, 5, 7, K, recs);
-    blk_ce<F>(a, 0, 1, K, recs); blk_ce<F>(a, 2, 3, K, recs); blk_ce<F>(a, 4, 5, K, recs); blk_ce<F>(a, 6, 7, K, recs);
+    blk_ce<F, EX>(a, 0, 4, K, recs); blk_ce<F, EX>(a, 1, 5, K, recs); blk_ce<F, EX>(a, 2, 6, K, recs); blk_ce<F, EX>(a, 3, 7, K, recs);
+    blk_ce<F, EX>(a, 0, 2, K, recs); blk_ce<F, EX>(a, 1, 3, K, recs); blk_ce<F, EX>(a, 4, 6, K, recs); blk_ce<F, EX>(a, 5, 7, K, recs);
+    blk_ce<F, EX>(a, 0, 1, K, recs); blk_ce<F, EX>(a, 2, 3, K, recs); blk_ce<F, EX>(a, 4, 5, K, recs); blk_ce<F, EX>(a, 6, 7, K, recs);
 }
 
 __device__ __forceinline__ void blk_clear(Blk8& b)
@@ -211,7 +225,7 @@ __device__ __forceinline__ void blk_load(Blk8& b, const KadEntry* __restrict__ s
             const uint2* p = reinterpret_cast<const uint2*>(s + q);
             const uint2 bb = p[1], c = p[2];
             b.x[q] = c.y;
-            b.d[q] = c.y == NONE ? ~0ull : (((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(bb.y ^ K.w[3]));
+            b.d[q] = c.y == NONE ? ~0ull : dclamp(((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(bb.y ^ K.w[3]));
         } else {
             b.x[q] = NONE;
             b.d[q] = ~0ull;
@@ -257,7 +271,7 @@ __device__ __forceinline__ void add_entries8(SVec<CAP>& res, int cap, const KadE
             const uint2* p = reinterpret_cast<const uint2*>(s + q);
             const uint2 a = p[0], b = p[1], c = p[2];
             ix[q] = c.y;
-            dd[q] = ((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(b.y ^ K.w[3]);
+            dd[q] = dclamp(((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(b.y ^ K.w[3]));
             (void)a;
         } else {
             ix[q] = NONE;
@@ -279,6 +293,7 @@ __device__ __forceinline__ void add_slot(SVec<CAP>& res, int cap, const KadView&
 // Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246),
 // block form: the candidate sets of the reference's scan (bucket m, then buckets below it with
 // the sibling table and self, then buckets above while the result is short) merged 8 at a time
+template <bool EX>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const KadRec& r, const K160& K,
                                                  int numRedundant, bool sib, Blk8& res)
 {
@@ -298,8 +313,8 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     auto add_block = [&](const KadEntry* e, int cnt) {
         Blk8 b;
         blk_load(b, e, cnt, K);
-        blk_sort8<false>(b, K, V.recs);
-        blk_merge_top8<false>(res, b, K, V.recs);
+        blk_sort8<false, EX>(b, K, V.recs);
+        blk_merge_top8<false, EX>(res, b, K, V.recs);
         n = blk_trunc(res, cap);
     };
     auto add_slot8 = [&](int bucket) {
@@ -316,7 +331,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
             blk_clear(self);
             self.x[0] = c;
             self.d[0] = dist_hi(me, K);
-            blk_merge_top8<false>(res, self, K, V.recs);
+            blk_merge_top8<false, EX>(res, self, K, V.recs);
             n = blk_trunc(res, cap);
         }
     }
@@ -330,6 +345,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
 // with their nodes.  Returns numNewRpcs: response nodes that entered nh (a response node the
 // reference inserts at a position < cap can never be pushed out again by the later, farther
 // response nodes, so "inserted" and "in the final vector" coincide).
+template <bool EX>
 __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap, const K160& K,
                                         const KadRec* __restrict__ recs)
 {
@@ -354,8 +370,8 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
         if (dj) { b.x[j] = NONE; b.d[j] = ~0ull; }
         dup |= dj;
     }
-    if (dup) blk_sort8<true>(b, K, recs);     // holes to the end
-    blk_merge_top8<true>(a, b, K, recs);
+    if (dup) blk_sort8<true, EX>(b, K, recs);     // holes to the end
+    blk_merge_top8<true, EX>(a, b, K, recs);
     const int n = blk_trunc(a, cap);
     int numNew = 0;
     uint32_t used = 0;
@@ -372,13 +388,13 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
 }
 
 // Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246)
-template <int CAP>
+template <int CAP, bool EX = true>
 __device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, const KadRec& r, const K160& K, int numRedundant,
                                bool sib, SVec<CAP>& res)
 {
     if constexpr (CAP == 8) {
         Blk8 b;
-        const int n = kad_find_node_blk(V, c, r, K, numRedundant, sib, b);
+        const int n = kad_find_node_blk<EX>(V, c, r, K, numRedundant, sib, b);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
         res.n = n;
@@ -551,19 +567,19 @@ __device__ __forceinline__ void kad_timeoutlike(KadLookup<A>& L, const KadView& 
 }
 
 // IterativeLookup::start (IterativeLookup.cc:133-244): local findNode at the source
-template <int A, class OnSend>
+template <int A, bool EX, class OnSend>
 __device__ __forceinline__ void kad_lookup_start(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                  const KadLC& LC, SVec<8>& res, const OnSend& on)
 {
     const KadRec rs = kad_rec(V.recs, L.S);
     const bool sb = kad_is_sibling1(V, rs, L.K);
-    kad_find_node1(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res);
+    kad_find_node1<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res);
     if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
     else if (LC.numSiblings != 0 && sb) {
         L.result = res.idx[0];
         L.pfinished = true; L.psuccess = true;
     } else {
-        nh_merge(L.nh, res, LC.redundant, L.K, V.recs);
+        nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.recs);
         kad_send_rpcs(L, V, DC, LC, LC.alpha, on);
     }
 }
@@ -579,7 +595,7 @@ __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
 // getres.ready(slot) says whether the responder's findNode result is available (always on a
 // single GPU); getres.fill(slot, node, rec, sibling, res) produces it.  Returns false, with the
 // state untouched, when the earliest event is a response whose result has not arrived yet.
-template <int A, class GetRes, class OnSend, class Rec>
+template <int A, bool EX, class GetRes, class OnSend, class Rec>
 __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                  const KadLC& LC, SVec<8>& res, const GetRes& getres,
                                                  const OnSend& on, const Rec& record)
@@ -627,7 +643,7 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     ++L.step;
     --L.pending;
     getres.fill(e, r, rr, sb, res);
-    int numNew = nh_merge(L.nh, res, LC.redundant, L.K, V.recs);
+    int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.recs);
     if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
     if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
     else {

@@ -85,7 +85,7 @@ struct NoRecord {
     __device__ __forceinline__ void operator()(int, uint32_t) const {}
 };
 
-template <int A>
+template <int A, bool EX>
 __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts DC, KadLC LC,
                                                         KadLookup<A>* __restrict__ st, uint8_t* __restrict__ act,
                                                         const uint32_t* __restrict__ qids, KadRes* __restrict__ res,
@@ -103,11 +103,11 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
     KadLookup<A> L = st[i];
     SVec<8> r;
     ShardSend on{res, i * A, &L.K, shard_lo, nsh, out, out_dest, out_cap, out_count};
-    if (a == 2) kad_lookup_start(L, V, DC, LC, r, on);       // first round: IterativeLookup::start
+    if (a == 2) kad_lookup_start<A, EX>(L, V, DC, LC, r, on);   // first round: IterativeLookup::start
     const ShardRes gr{res, i * A};
     const NoRecord rec;
     while (!kad_lookup_done(L)) {
-        if (!kad_lookup_event(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
+        if (!kad_lookup_event<A, EX>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
     }
     if (kad_lookup_done(L)) {
         const unsigned long long di = atomicAdd(done_count, 1ull);
@@ -142,6 +142,7 @@ __global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* 
 }
 
 // findNode at the responder (owned by this rank) for each received request
+template <bool EX>
 __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __restrict__ in, uint64_t n,
                                   ovs_kad_resp* __restrict__ out)
 {
@@ -160,7 +161,7 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
     const KadRec rr = kad_rec(V.recs, q.node);
     const bool sb = kad_is_sibling1(V, rr, K);
     SVec<8> r;
-    kad_find_node1(V, q.node, rr, K, LC.redundant, sb, r);
+    kad_find_node1<8, EX>(V, q.node, rr, K, LC.redundant, sb, r);
     o.count = (uint32_t)r.n;
 #pragma unroll
     for (int k = 0; k < 8; ++k) { o.nodes[k] = r.idx[k]; o.dist_hi[k] = r.d[k]; }
@@ -224,9 +225,10 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     if (nlook == 0) return hipSuccess;
     const KadView V = kad_make_view(t, xy, n);
     const KadLC LC = kad_make_lc(P, t);
-#define KS(a) hipLaunchKernelGGL(k_kad_shard_step<a>, dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
+#define KSX(a, x) hipLaunchKernelGGL((k_kad_shard_step<a, x>), dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
                                  (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, out, out_dest, out_cap, \
                                  out_count, done, done_cap, done_count, active_count)
+#define KS(a) do { if (t.exact) KSX(a, true); else KSX(a, false); } while (0)
     switch (LC.alpha) {
     case 1: KS(1); break;
     case 2: KS(2); break;
@@ -234,6 +236,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     default: KS(4); break;
     }
 #undef KS
+#undef KSX
     return hipGetLastError();
 }
 
@@ -244,7 +247,8 @@ hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, 
     if (nreq == 0) return hipSuccess;
     const KadView V = kad_make_view(t, nullptr, n);
     const KadLC LC = kad_make_lc(P, t);
-    hipLaunchKernelGGL(k_kad_shard_serve, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
+    if (t.exact) hipLaunchKernelGGL(k_kad_shard_serve<true>, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
+    else hipLaunchKernelGGL(k_kad_shard_serve<false>, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
     return hipGetLastError();
 }
 

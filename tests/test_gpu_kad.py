@@ -113,3 +113,42 @@ def test_route_config_b_full_batch(engine: KbrEngine):
     kid = keys.view(np.uint32).reshape(-1, 5)
     assert np.array_equal(net.ids[ok], kid)
     assert np.all(g["rpcs"] == g["hops"])          # alpha = 1: every RPC answered and accepted
+
+
+def _paired_population(n_pairs: int, seed: int):
+    """IDs in pairs that differ only in bit 0: XOR distances of a pair's members to any key tie
+    in their top 64 bits, so the build must select the exact (160-bit fallback) comparator."""
+    base = W.sorted_unique_ids(n_pairs, seed)
+    base[:, 0] &= ~np.uint32(1)
+    ids = np.concatenate([base, base ^ np.array([1, 0, 0, 0, 0], np.uint32)])
+    order = np.lexsort((ids[:, 0], ids[:, 1], ids[:, 2], ids[:, 3], ids[:, 4]))
+    ids = np.ascontiguousarray(ids[order])
+    ids = ids[np.concatenate([[True], np.any(ids[1:] != ids[:-1], axis=1)])]
+    return ids, W.coordinates(len(ids), seed)
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+def test_route_prefix_ties_use_exact_path(engine: KbrEngine, alpha):
+    ids, xy = _paired_population(3000, 0x51)
+    _load(engine, ids, xy, lookupParallelRpcs=alpha)
+    o = OracleNet("kademlia", ids, xy, kad_params(lookupParallelRpcs=alpha))
+    k1, s1 = W.lookups(ids, 8000, 70 + alpha, node_ids=True)
+    k2, s2 = W.lookups(ids, 8000, 80 + alpha, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    g = engine.lookup(keys, src, record_hops=True, count_rpcs=True)
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    _eq(g, r, f"paired ids alpha={alpha}", hop_cols=50, rpcs=True)
+
+
+def test_forced_exact_path_matches_fast_path(monkeypatch):
+    """OVS_KAD_EXACT forces the 160-bit tie fallback; on a tie-free network both comparators agree."""
+    net = W.population(15000, 0x4b41)
+    keys, src = W.lookups(net.ids, 40000, 90, node_ids=True)
+    res = []
+    for force in (False, True):
+        if force:
+            monkeypatch.setenv("OVS_KAD_EXACT", "1")
+        with KbrEngine(0) as e:
+            _load(e, net.ids, net.xy, lookupParallelRpcs=3)
+            res.append(e.lookup(keys, src, record_hops=True, count_rpcs=True))
+    _eq(res[0], res[1], "fast vs exact comparator", hop_cols=50, rpcs=True)
