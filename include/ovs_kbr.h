@@ -231,8 +231,8 @@ ovs_status  ovs_kbrtest_stats_batch(ovs_ctx* ctx, const ovs_route_out* out, cons
                                     uint32_t flags, void* stream);
 
 /* ---- multi-GPU sharding (one process per GPU; the host exchanges records) ----
- * The sorted ring is cut into contiguous arcs, one per rank.  Node keys and
- * coordinates are replicated (24 + 16 B per node); the finger rows -- the bulk
+ * The sorted ring is cut into contiguous arcs, one per rank.  Node keys,
+ * coordinates and 64 B node records are replicated; the finger rows -- the bulk
  * of the routing state -- exist only for the rank's own arc, so a lookup is
  * handed to the rank that owns its next responder.  The exchange of in-flight
  * records between hop rounds is done by the caller (RCCL all-to-allv over xGMI,
