@@ -96,6 +96,36 @@ def test_route_medium_ring(engine: KbrEngine, rnd):
     _eq(g, r, f"2^16 ring rnd={rnd}", hop_cols=50)
 
 
+@pytest.mark.parametrize("sls,hcm", [(1, 50), (2, 50), (3, 6), (8, 4), (5, 0)])
+def test_route_successor_list_and_hop_limit(engine: KbrEngine, sls, hcm):
+    """successorListSize (the window the WinRec / NodeRec distances cover) and hopCountMax
+    variants of the converged-ring kernel against the oracle, node-ID and random keys."""
+    net = W.population(1 << 14, 40 + sls)
+    p = dict(successorListSize=sls, hopCountMax=hcm)
+    engine.set_params(Params.chord().replace(**p))
+    engine.chord_load(net.ids, net.xy)
+    o = OracleNet("chord", net.ids, net.xy, chord_params(**p))
+    k1, s1 = W.lookups(net.ids, 20000, 41 + sls, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 20000, 42 + sls, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    g = engine.lookup(keys, src, record_hops=True)
+    r = o.route(keys, src, record_hops=True)
+    _eq(g, r, f"successorListSize={sls} hopCountMax={hcm}", hop_cols=max(hcm, 1))
+
+
+def test_params_change_rebuilds_node_records(engine: KbrEngine):
+    """successorListSize changed after the load: the node records are rebuilt for it."""
+    net = W.population(5000, 47)
+    engine.set_params(Params.chord())
+    engine.chord_load(net.ids, net.xy)
+    keys, src = W.lookups(net.ids, 20000, 48, node_ids=True)
+    engine.lookup(keys, src)
+    engine.set_params(Params.chord().replace(successorListSize=2))
+    g = engine.lookup(keys, src, record_hops=True)
+    r = OracleNet("chord", net.ids, net.xy, chord_params(successorListSize=2)).route(keys, src, record_hops=True)
+    _eq(g, r, "successorListSize 8 -> 2", hop_cols=50)
+
+
 def test_route_1m_ring_vs_oracle(engine: KbrEngine):
     """Config C ring size (2^20 nodes, random coordinates) on a 200k-lookup sample."""
     net = W.population(1 << 20, 0xC)
