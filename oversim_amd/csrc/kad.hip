@@ -226,9 +226,14 @@ struct LocalFindNode {
     const K160& K;
     int redundant;
     __device__ __forceinline__ bool ready(int) const { return true; }
-    __device__ __forceinline__ void fill(int, uint32_t r, const KadRec& rr, bool sb, SVec<8>& res) const
+    __device__ __forceinline__ void fill(int, uint32_t r, const RespGeo& g, bool sb, SVec<8>& res) const
     {
-        kad_find_node1<8, EX>(V, r, rr, K, redundant, sb, res);
+        Blk8 b;
+        const int n = kad_find_node_blk<EX>(V, r, g, K, redundant, sb, b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
+        res.n = n;
+        res.used = 0;
     }
 };
 

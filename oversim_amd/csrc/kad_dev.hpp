@@ -290,25 +290,40 @@ __device__ __forceinline__ void add_slot(SVec<CAP>& res, int cap, const KadView&
     for (int q0 = 0; q0 < V.k; q0 += 8) add_entries8(res, cap, e + q0, min(8, V.k - q0), K, V.recs);
 }
 
+// What findNode at a responder needs of its 64 B record, captured when the FindNodeCall is sent
+// (the record is read then anyway, for the siblings flag): m = msb(key ^ K) (-1: key == K),
+// endIndex = msb(R), the bucket-row offset.  Its key is re-read only on the rare paths.
+struct RespGeo {
+    int m, endIndex;
+    uint32_t boff;
+};
+
+__device__ __forceinline__ RespGeo resp_geo(const KadRec& r, const K160& K)
+{
+    RespGeo g;
+    g.m = k_msb(k_xor(as_key(r.key), K));
+    g.endIndex = k_msb(as_key(r.R));
+    g.boff = r.boff;
+    return g;
+}
+
 // Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246),
 // block form: the candidate sets of the reference's scan (bucket m, then buckets below it with
 // the sibling table and self, then buckets above while the result is short) merged 8 at a time
 template <bool EX>
-__device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const KadRec& r, const K160& K,
+__device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
                                                  int numRedundant, bool sib, Blk8& res)
 {
     blk_clear(res);
-    const K160 me = as_key(r.key);
     if (V.nsib == 0 || sib) {
         // resultSize = 1 and self is the XOR-closest of siblings + self (see kad_find_node1)
         res.x[0] = c;
-        res.d[0] = dist_hi(me, K);
+        res.d[0] = dist_hi(kad_key(V.recs, c), K);
         return 1;
     }
     const int cap = numRedundant < 8 ? numRedundant : 8;
-    const K160 D = k_xor(me, K);
-    const int m = k_msb(D);
-    const int endIndex = k_msb(as_key(r.R));
+    const int m = g.m;
+    const int endIndex = g.endIndex;
     int n = 0;
     auto add_block = [&](const KadEntry* e, int cnt) {
         Blk8 b;
@@ -318,7 +333,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         n = blk_trunc(res, cap);
     };
     auto add_slot8 = [&](int bucket) {
-        const KadEntry* e = V.slots + (uint64_t)(r.boff + (uint32_t)(KEYBITS - 1 - bucket)) * V.k;
+        const KadEntry* e = V.slots + (uint64_t)(g.boff + (uint32_t)(KEYBITS - 1 - bucket)) * V.k;
         for (int q0 = 0; q0 < V.k; q0 += 8) add_block(e + q0, min(8, V.k - q0));
     };
     if (m >= 0 && m >= endIndex) add_slot8(m);
@@ -330,7 +345,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
             Blk8 self;
             blk_clear(self);
             self.x[0] = c;
-            self.d[0] = dist_hi(me, K);
+            self.d[0] = dist_hi(kad_key(V.recs, c), K);
             blk_merge_top8<false, EX>(res, self, K, V.recs);
             n = blk_trunc(res, cap);
         }
@@ -394,7 +409,7 @@ __device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, con
 {
     if constexpr (CAP == 8) {
         Blk8 b;
-        const int n = kad_find_node_blk<EX>(V, c, r, K, numRedundant, sib, b);
+        const int n = kad_find_node_blk<EX>(V, c, resp_geo(r, K), K, numRedundant, sib, b);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
         res.n = n;
@@ -447,6 +462,8 @@ struct Pend {
     uint32_t tag;      // step at send (bits 0..15) | insertion sequence (bits 16..30) | timeout (bit 31)
     int64_t t;         // event time
     uint32_t dins;     // t - insertion time
+    uint32_t geo;      // responder: m + 1 (bits 0..7) | endIndex + 1 (bits 8..15) | siblings flag (bit 16)
+    uint32_t boff;     // responder's bucket-row offset
 };
 
 // per-lane lookup state (IterativeLookup + its single IterativePathLookup)
@@ -492,6 +509,8 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     const double2 cxy = V.xy[x];
     const KadRec rr = kad_rec(V.recs, x);
     const bool sb = kad_is_sibling1(V, rr, L.K);
+    const RespGeo rg = resp_geo(rr, L.K);
+    const uint32_t geo = (uint32_t)(rg.m + 1) | ((uint32_t)(rg.endIndex + 1) << 8) | (sb ? 0x10000u : 0u);
     // the response carries findNode's result: 1 node when x is sibling, else min(redundant, n)
     const int csz = sb ? 1 : (LC.redundant < (int)V.n ? LC.redundant : (int)V.n);
     const int64_t cd = coord_ns(L.sx, L.sy, cxy.x, cxy.y, DC.round);
@@ -518,6 +537,8 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
             L.p[i].t = isTo ? tTo : tResp;
             L.p[i].dins = (uint32_t)(isTo ? DC.rpcTimeout : d2);
             L.p[i].tag = tag;
+            L.p[i].geo = geo;
+            L.p[i].boff = rg.boff;
         }
     }
     L.pvalid |= 1u << slot;
@@ -593,7 +614,7 @@ __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
 
 // Process the earliest pending event (response or RPC timeout) of a running lookup.
 // getres.ready(slot) says whether the responder's findNode result is available (always on a
-// single GPU); getres.fill(slot, node, rec, sibling, res) produces it.  Returns false, with the
+// single GPU); getres.fill(slot, node, geometry, sibling, res) produces it.  Returns false, with the
 // state untouched, when the earliest event is a response whose result has not arrived yet.
 template <int A, bool EX, class GetRes, class OnSend, class Rec>
 __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
@@ -612,10 +633,10 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
             if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
         }
     }
-    uint32_t r = 0, tag = 0;
+    uint32_t r = 0, tag = 0, geo = 0, boff = 0;
 #pragma unroll
     for (int i = 0; i < A; ++i)
-        if (i == e) { r = L.p[i].node; tag = L.p[i].tag; }
+        if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; }
     if (!(tag & 0x80000000u) && !getres.ready(e)) return false;
     L.pvalid &= ~(1u << e);
     L.now = bt;
@@ -626,8 +647,12 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
         kad_timeoutlike(L, V, DC, LC, on);
         return true;
     }
-    const KadRec rr = kad_rec(V.recs, r);
-    const bool sb = kad_is_sibling1(V, rr, L.K);
+    // the responder's siblings flag and bucket geometry were captured at send (kad_send)
+    const bool sb = (geo & 0x10000u) != 0;
+    RespGeo rg;
+    rg.m = (int)(geo & 0xFFu) - 1;
+    rg.endIndex = (int)((geo >> 8) & 0xFFu) - 1;
+    rg.boff = boff;
     const bool acc = (LC.useAll && LC.merge) ? true : (vr == L.step);
     if (!(acc || (sb && LC.acceptLateSiblings))) {
         // not accepted: handled as a timeout, its nodes are dropped
@@ -642,7 +667,7 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     }
     ++L.step;
     --L.pending;
-    getres.fill(e, r, rr, sb, res);
+    getres.fill(e, r, rg, sb, res);
     int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.recs);
     if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
     if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }

@@ -39,7 +39,7 @@ struct ShardRes {
     KadRes* __restrict__ res;
     uint64_t base;
     __device__ __forceinline__ bool ready(int slot) const { return res[base + slot].ready != 0; }
-    __device__ __forceinline__ void fill(int slot, uint32_t, const KadRec&, bool, SVec<8>& v) const
+    __device__ __forceinline__ void fill(int slot, uint32_t, const RespGeo&, bool, SVec<8>& v) const
     {
         const KadRes& r = res[base + slot];
         svec_clear(v);

@@ -1,0 +1,2 @@
+cd "$GRAFT_REPO_ROOT"; export OVS_SKIP_BUILD=1
+for i in 1 2 3; do timeout -k 10 200 python bench.py --workload B --no-cpu-baseline 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('B', '%.4g'%d['value'], '%.4f ms'%d['roofline']['kernel_ms'])" || exit 1; done
