@@ -158,6 +158,24 @@ ovs_status  ovs_kad_export(ovs_ctx* ctx, uint32_t* siblings, uint8_t* bucket_cou
 /* copy the resolved Chord finger table out: out[n*160] = getFinger(pos) */
 ovs_status  ovs_chord_export_fingers(ovs_ctx* ctx, uint32_t* out);
 
+/* Batched maintenance lookups: one synchronous fixfingers round for the listed
+ * nodes of an explicit-table ring (Chord::handleFixFingersTimerExpired,
+ * Chord.cc:845-875; rpcFixfingers + handleRpcFixfingersResponse, 1228-1270,
+ * extendedFingerTable = false).  At every listed node the trivial fingers
+ * (2^i <= succ0 - n) are removed, the lookups of n + 2^i from n are routed on
+ * the device over the tables as they then are, and finger i is set to each
+ * successful lookup's result.  The reference fires the nodes' timers at
+ * different times; the round fixes all listed nodes at one instant.  Host
+ * buffers; stats may be NULL. */
+typedef struct ovs_fixfingers_stats {
+    uint64_t lookups;        /* FixfingersCalls routed */
+    uint64_t ok;             /* answered (lookup valid) */
+    uint64_t changed;        /* finger entries that changed */
+    uint64_t hops;           /* accepted hops of all lookups */
+} ovs_fixfingers_stats;
+ovs_status  ovs_chord_fix_fingers(ovs_ctx* ctx, const uint32_t* nodes, uint64_t m,
+                                  ovs_fixfingers_stats* stats);
+
 /* Batched iterative lookups: lookup i routes keys[i] from node src[i]
  * (KBRTestApp one-way test: createDestKey -> callRoute -> sendToKey ->
  * IterativeLookup -> sendRouteMessage).  hop_seq may be NULL, else

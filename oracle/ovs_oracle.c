@@ -1226,6 +1226,62 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
 }
 
 /* ======================================================================== */
+/* One synchronous fixfingers round (Chord::handleFixFingersTimerExpired,   */
+/* Chord.cc:845-875; rpcFixfingers / handleRpcFixfingersResponse,           */
+/* Chord.cc:1228-1270, extendedFingerTable = false) for a list of nodes:     */
+/*  1. at every listed node, trivial fingers (2^i <= succ0 - n) are removed   */
+/*     in the order i = 0..159 (they all precede the non-trivial ones);      */
+/*  2. the lookups of n + 2^i from n (iterative, numSiblings = 1) route over */
+/*     the tables as they are then;                                          */
+/*  3. every successful lookup sets finger i to its result (the node that    */
+/*     answers the FixfingersCall).                                          */
+/* The reference runs the timers of different nodes at different times; the */
+/* round fixes all listed nodes at one instant of a frozen snapshot.         */
+/* ======================================================================== */
+uint64_t orc_chord_fix_fingers(orc_net* net, const uint32_t* nodes, uint64_t m, uint64_t* out_ok,
+                               uint64_t* out_changed, int nthreads)
+{
+    if (net->type != NET_CHORD) { set_err("fix_fingers: not a Chord network"); return 0; }
+    uint64_t cap = m * 160, nl = 0;
+    orc_key* keys = (orc_key*)malloc(sizeof(orc_key) * (cap ? cap : 1));
+    uint32_t* src = (uint32_t*)malloc(sizeof(uint32_t) * (cap ? cap : 1));
+    uint16_t* pos = (uint16_t*)malloc(sizeof(uint16_t) * (cap ? cap : 1));
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        const OKey* self = &net->ids[v];
+        OKey gap = ok_sub(net->ids[succ_get(net, v, 0)], self);
+        for (uint32_t i = 0; i < 160; ++i) {
+            OKey off = ok_pow2(i);
+            if (ok_cmp(&off, &gap) > 0) {
+                OKey lk = ok_add(*self, &off);
+                ok_to(&lk, &keys[nl]);
+                src[nl] = v;
+                pos[nl] = (uint16_t)i;
+                ++nl;
+            } else {
+                ft_removeFinger(net, v, i);
+            }
+        }
+    }
+    orc_route_out* out = (orc_route_out*)malloc(sizeof(orc_route_out) * (nl ? nl : 1));
+    uint64_t hops = orc_route_batch(net, keys, src, nl, out, NULL, NULL, nthreads);
+    uint64_t ok = 0, changed = 0;
+    for (uint64_t q = 0; q < nl; ++q) {
+        if (out[q].status != 0) continue;
+        ++ok;
+        const uint32_t v = src[q], i = pos[q];
+        const uint32_t p = 160 - i - 1;
+        const uint32_t before = p < net->fsize[v] ? net->fdeque[(size_t)v * 160 + p] : NONE;
+        if (before != out[q].responsible) ++changed;
+        ft_setFinger(net, v, i, out[q].responsible);
+    }
+    free(keys); free(src); free(pos); free(out);
+    if (out_ok) *out_ok = ok;
+    if (out_changed) *out_changed = changed;
+    return hops;
+}
+
+/* ======================================================================== */
 /* KBRTestApp one-way statistics                                             */
 /* ======================================================================== */
 

@@ -116,6 +116,13 @@ typedef struct {
 uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
                          orc_route_out* out, uint32_t* hop_seq, uint32_t* rpcs_out, int nthreads);
 
+/* One synchronous fixfingers round for nodes[0..m) (Chord.cc:845-875, 1228-1270): trivial
+ * fingers removed, then lookups of n + 2^i routed over the tables, then finger i := result.
+ * Explicit or converged networks.  Returns total hops; *out_ok successful lookups,
+ * *out_changed fingers whose deque entry changed. */
+uint64_t orc_chord_fix_fingers(orc_net* net, const uint32_t* nodes, uint64_t m, uint64_t* out_ok,
+                               uint64_t* out_changed, int nthreads);
+
 /* SimpleNodeEntry::calcDelay for an idle tx queue, in ns (SimpleNodeEntry.cc:155-195) */
 int64_t orc_delay_ns(const orc_net* net, uint32_t a, uint32_t b, int32_t bytes);
 /* float distance (SimpleNodeEntry.cc:145-153) */

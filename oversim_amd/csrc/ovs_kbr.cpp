@@ -42,6 +42,12 @@ struct ovs_ctx {
     uint8_t* nsucc = nullptr;
     uint32_t* fres = nullptr;
     int sls = 0;
+    // explicit tables: host copies for batched maintenance (ovs_chord_fix_fingers)
+    std::vector<K160> h_ids;
+    std::vector<uint32_t> h_deque;      // n * 160 ChordFingerTable deque entries (index p = 159 - pos)
+    std::vector<uint8_t> h_fsize;       // deque sizes
+    std::vector<uint32_t> h_succ0;      // successorList->getSuccessor()
+    std::vector<uint32_t> h_fres;       // n * 160 resolved getFinger(pos)
     uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     // kademlia
@@ -87,6 +93,7 @@ void free_tables(ovs_ctx* c)
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
     c->overlay = 0; c->n = 0; c->nfing = 0;
+    c->h_ids.clear(); c->h_deque.clear(); c->h_fsize.clear(); c->h_succ0.clear(); c->h_fres.clear();
 }
 
 void free_kad_shard(ovs_ctx* c)
@@ -212,6 +219,23 @@ ovs_status ensure_nodes(ovs_ctx* c, hipStream_t s)
                                  (uint32_t)c->shard_lo, (uint32_t)c->shard_hi, s));
     c->nodes_ns = ns;
     return OVS_OK;
+}
+
+// ChordFingerTable::getFinger(pos) of node v from the host deque (ChordFingerTable.cc:174-193)
+void resolve_row(ovs_ctx* c, uint64_t v)
+{
+    const uint32_t* dq = c->h_deque.data() + v * 160;
+    const uint32_t size = c->h_fsize[v];
+    for (int pos = 0; pos < 160; ++pos) {
+        uint32_t p = 160 - pos - 1;
+        uint32_t r;
+        if (p >= size) r = c->h_succ0[v];
+        else {
+            while (dq[p] == 0xFFFFFFFFu && p < size - 1) ++p;
+            r = dq[p] == 0xFFFFFFFFu ? c->h_succ0[v] : dq[p];
+        }
+        c->h_fres[v * 160 + pos] = r;
+    }
 }
 
 // upload sorted ids (+ coordinates) into KeyRec / double2 arrays
@@ -432,29 +456,29 @@ ovs_status ovs_chord_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, 
     ovs_status s = upload_nodes(c, ids, n, xy, false);
     if (s != OVS_OK) { free_tables(c); return s; }
     const int sls = c->P.successorListSize;
-    // resolve ChordFingerTable::getFinger(pos) on the host (ChordFingerTable.cc:174-193)
-    std::vector<uint32_t> fres((size_t)n * 160);
+    // keep the tables on the host too (batched maintenance rewrites them) and resolve
+    // ChordFingerTable::getFinger(pos) there (ChordFingerTable.cc:174-193)
+    c->h_ids.assign(reinterpret_cast<const K160*>(ids), reinterpret_cast<const K160*>(ids) + n);
+    c->h_deque.resize((size_t)n * 160);
+    c->h_fsize.assign(deque_size, deque_size + n);
+    c->h_succ0.resize(n);
+    c->h_fres.resize((size_t)n * 160);
     for (uint64_t v = 0; v < n; ++v) {
-        for (int pos = 0; pos < 160; ++pos) {
-            const uint32_t size = deque_size[v];
-            uint32_t p = 160 - pos - 1;
-            uint32_t r;
-            // deque entry p holds position 159 - p
-            auto entry = [&](uint32_t pp) { return fingers[v * 160 + (159 - pp)]; };
-            if (nsucc[v] == 0) return fail(c, OVS_EINVAL, "empty successor list");
-            if (p >= size) r = succ[v * sls];
-            else {
-                while (entry(p) == 0xFFFFFFFFu && (p < size - 1)) ++p;
-                r = entry(p) == 0xFFFFFFFFu ? succ[v * sls] : entry(p);
-            }
-            if (r >= n) return fail(c, OVS_EINVAL, "finger index out of range");
-            fres[v * 160 + pos] = r;
+        if (nsucc[v] == 0) return fail(c, OVS_EINVAL, "empty successor list");
+        if (deque_size[v] > 160) return fail(c, OVS_EINVAL, "deque_size > 160");
+        for (uint32_t p = 0; p < 160; ++p) {
+            const uint32_t f = fingers[v * 160 + (159 - p)];
+            if (f != 0xFFFFFFFFu && f >= n) return fail(c, OVS_EINVAL, "finger index out of range");
+            c->h_deque[v * 160 + p] = f;
         }
+        c->h_succ0[v] = succ[v * sls];
         if (pred[v] != 0xFFFFFFFFu && pred[v] >= n) return fail(c, OVS_EINVAL, "pred index out of range");
         if (nsucc[v] > sls) return fail(c, OVS_EINVAL, "nsucc > successorListSize");
         for (int j = 0; j < nsucc[v]; ++j)
             if (succ[v * sls + j] >= n) return fail(c, OVS_EINVAL, "successor index out of range");
+        resolve_row(c, v);
     }
+    const std::vector<uint32_t>& fres = c->h_fres;
     HIPCHK(c, hipMalloc(&c->pred, sizeof(uint32_t) * n));
     HIPCHK(c, hipMalloc(&c->succ, sizeof(uint32_t) * n * sls));
     HIPCHK(c, hipMalloc(&c->nsucc, n));
@@ -486,6 +510,78 @@ ovs_status ovs_chord_export_fingers(ovs_ctx* c, uint32_t* out)
     HIPCHK(c, hipMemcpyAsync(out, d, sizeof(uint32_t) * tot, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(d);
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_fix_fingers(ovs_ctx* c, const uint32_t* nodes, uint64_t m, ovs_fixfingers_stats* stats)
+{
+    if (!c || (m && !nodes)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "no Chord network loaded");
+    if (c->ideal)
+        return fail(c, OVS_ESTATE, "fixfingers rounds run on explicit tables (ovs_chord_load_tables); "
+                                   "a converged ring is already their fixed point");
+    const uint64_t n = c->n;
+    for (uint64_t j = 0; j < m; ++j)
+        if (nodes[j] >= n) return fail(c, OVS_EINVAL, "node index out of range");
+    // 1. handleFixFingersTimerExpired (Chord.cc:851-870): trivial fingers removed, lookups for the rest
+    std::vector<ovs_key160> keys;
+    std::vector<uint32_t> src;
+    std::vector<uint8_t> pos;
+    keys.reserve(m * 32); src.reserve(m * 32); pos.reserve(m * 32);
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        const K160 self = c->h_ids[v];
+        const K160 gap = k_sub(c->h_ids[c->h_succ0[v]], self);
+        for (int i = 0; i < 160; ++i) {
+            const K160 off = k_pow2(i);
+            if (k_lt(gap, off)) {                              // offset > successor - thisNode
+                const K160 k = k_add(self, off);
+                ovs_key160 kk;
+                for (int w = 0; w < 5; ++w) kk.w[w] = k.w[w];
+                keys.push_back(kk); src.push_back(v); pos.push_back((uint8_t)i);
+            } else {                                           // ChordFingerTable::removeFinger (154-172)
+                const uint32_t p = 160 - i - 1;
+                uint8_t& size = c->h_fsize[v];
+                if (p >= size) continue;
+                if (p == (uint32_t)size - 1) --size;
+                else c->h_deque[(uint64_t)v * 160 + p] = 0xFFFFFFFFu;
+            }
+        }
+    }
+    auto upload_rows = [&]() -> ovs_status {
+        for (uint64_t j = 0; j < m; ++j) resolve_row(c, nodes[j]);
+        if (m * 8 >= n) {
+            HIPCHK(c, hipMemcpy(c->fres, c->h_fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
+        } else {
+            for (uint64_t j = 0; j < m; ++j)
+                HIPCHK(c, hipMemcpy(c->fres + (uint64_t)nodes[j] * 160, c->h_fres.data() + (uint64_t)nodes[j] * 160,
+                                    sizeof(uint32_t) * 160, hipMemcpyHostToDevice));
+        }
+        return OVS_OK;
+    };
+    ovs_status st = upload_rows();
+    if (st != OVS_OK) return st;
+    // 2. the FixfingersCalls, routed as KBR lookups on the device (sendRouteRpcCall -> sendToKey)
+    std::vector<ovs_route_out> out(keys.size());
+    st = ovs_route_batch(c, keys.data(), src.data(), keys.size(), out.data(), nullptr, nullptr, 0, nullptr);
+    if (st != OVS_OK) return st;
+    // 3. handleRpcFixfingersResponse: finger i := the answering (responsible) node
+    uint64_t ok = 0, changed = 0, hops = 0;
+    for (size_t q = 0; q < out.size(); ++q) {
+        hops += out[q].hops;
+        if (out[q].status != OVS_LOOKUP_OK) continue;
+        ++ok;
+        const uint32_t v = src[q], p = 160 - pos[q] - 1;
+        uint32_t* dq = c->h_deque.data() + (uint64_t)v * 160;
+        uint8_t& size = c->h_fsize[v];
+        const uint32_t before = p < size ? dq[p] : 0xFFFFFFFFu;
+        while (size <= p) dq[size++] = 0xFFFFFFFFu;          // ChordFingerTable::setFinger (66-87)
+        dq[p] = out[q].responsible;
+        changed += before != out[q].responsible;
+    }
+    st = upload_rows();
+    if (st != OVS_OK) return st;
+    if (stats) { stats->lookups = keys.size(); stats->ok = ok; stats->changed = changed; stats->hops = hops; }
     return OVS_OK;
 }
 

@@ -164,6 +164,7 @@ def lib() -> C.CDLL:
         "ovs_delay_batch": ([vp, vp, vp, vp, u64, vp, u32, vp], C.c_int),
         "ovs_sync": ([vp], C.c_int),
         "ovs_kbrtest_stats_batch": ([vp, vp, vp, vp, u64, C.c_double, i32, vp, u32, vp], C.c_int),
+        "ovs_chord_fix_fingers": ([vp, vp, u64, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -282,6 +283,15 @@ class KbrEngine:
         out = np.empty((self.n, 160), dtype=np.uint32)
         self._chk(self._L.ovs_chord_export_fingers(self._h, _ptr(out)), "ovs_chord_export_fingers")
         return out
+
+    def chord_fix_fingers(self, nodes=None) -> dict:
+        """One synchronous fixfingers round on an explicit-table ring (ovs_chord_fix_fingers):
+        the batched maintenance lookups of Chord::handleFixFingersTimerExpired."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        st = (C.c_uint64 * 4)()
+        self._chk(self._L.ovs_chord_fix_fingers(self._h, _ptr(nodes), len(nodes), C.cast(st, C.c_void_p)),
+                  "ovs_chord_fix_fingers")
+        return {"lookups": st[0], "ok": st[1], "changed": st[2], "hops": st[3]}
 
     def kad_tables(self):
         p = self.get_params()

@@ -74,6 +74,7 @@ def lib() -> C.CDLL:
             ("orc_coord_dist", [vp, u32, u32], C.c_float),
             ("orc_last_error", [], C.c_char_p),
             ("orc_kbrtest_stats", [vp, vp, vp, vp, u64, C.c_double, C.c_int, i32, vp], None),
+            ("orc_chord_fix_fingers", [vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.c_int], u64),
         ]:
             f = getattr(L, name)
             f.argtypes = args
@@ -183,6 +184,13 @@ class OracleNet:
         flag = C.c_int(0)
         cnt = lib().orc_find_node(self._h, int(node), _p(key), numRedundantNodes, numSiblings, _p(out), C.byref(flag))
         return list(out[:cnt]), bool(flag.value)
+
+    def chord_fix_fingers(self, nodes=None, nthreads=0) -> dict:
+        """One synchronous fixfingers round (orc_chord_fix_fingers); returns its counters."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        ok, ch = C.c_uint64(0), C.c_uint64(0)
+        hops = lib().orc_chord_fix_fingers(self._h, _p(nodes), len(nodes), C.byref(ok), C.byref(ch), nthreads)
+        return {"hops": int(hops), "ok": ok.value, "changed": ch.value}
 
     def chord_fingers(self) -> np.ndarray:
         out = np.empty((self.n, 160), dtype=np.uint32)

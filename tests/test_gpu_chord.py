@@ -188,6 +188,45 @@ def test_explicit_tables_match_oracle(engine: KbrEngine):
     _eq(g, r, "explicit tables", hop_cols=50)
 
 
+def _broken_tables(n, seed):
+    """A non-converged snapshot: ~30% of finger entries unspecified, deques shrunk, some short
+    successor lists (correct pred/succ0)."""
+    net = W.population(n, seed)
+    rng = np.random.default_rng(seed + 1)
+    fing = OracleNet("chord", net.ids, net.xy).chord_fingers().copy()
+    fing[rng.random(fing.shape) < 0.3] = 0xFFFFFFFF
+    wrong = rng.random(fing.shape) < 0.05                 # stale entries pointing anywhere
+    fing[wrong] = rng.integers(0, n, int(wrong.sum())).astype(np.uint32)
+    deque = rng.integers(100, 161, n).astype(np.uint8)
+    pred = ((np.arange(n) - 1) % n).astype(np.uint32)
+    succ = ((np.arange(n)[:, None] + 1 + np.arange(8)[None, :]) % n).astype(np.uint32)
+    nsucc = np.full(n, 8, dtype=np.uint8)
+    nsucc[rng.integers(0, n, n // 10)] = rng.integers(1, 8, n // 10).astype(np.uint8)
+    return net, dict(pred=pred, succ=succ, nsucc=nsucc, fingers=fing, deque_size=deque)
+
+
+@pytest.mark.parametrize("subset", [False, True])
+def test_fix_fingers_round_matches_oracle(engine: KbrEngine, subset):
+    """Batched maintenance lookups (ovs_chord_fix_fingers) vs the oracle's round: same fingers,
+    same counters; a full round over a ring with correct successors reaches the ideal table."""
+    n = 3000
+    net, t = _broken_tables(n, 61)
+    o = OracleNet("chord", net.ids, net.xy, tables=t)
+    engine.set_params(Params.chord())
+    engine.chord_load_tables(net.ids, net.xy, t["pred"], t["succ"], t["nsucc"], t["fingers"], t["deque_size"])
+    nodes = np.arange(0, n, 3, dtype=np.uint32) if subset else None
+    g = engine.chord_fix_fingers(nodes)
+    r = o.chord_fix_fingers(nodes)
+    assert (g["ok"], g["changed"], g["hops"]) == (r["ok"], r["changed"], r["hops"]), (g, r)
+    assert g["lookups"] == g["ok"] > 0
+    assert np.array_equal(engine.chord_fingers(), o.chord_fingers())
+    if not subset:
+        assert np.array_equal(engine.chord_fingers(), OracleNet("chord", net.ids, net.xy).chord_fingers())
+    keys, src = W.lookups(net.ids, 4000, 62, node_ids=True)
+    _eq(engine.lookup(keys, src, record_hops=True), o.route(keys, src, record_hops=True), "after fixfingers",
+        hop_cols=50)
+
+
 def test_rejects_unsupported(engine: KbrEngine):
     from oversim_amd import KbrError
     net = W.population(100, 26)

@@ -214,3 +214,24 @@ def test_oracle_reproduces_recursive_golden(name):
     for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
         assert np.array_equal(r[f], g[f]), f
     assert np.array_equal(r["hop_seq"][:, :g["hop_seq"].shape[1]], g["hop_seq"])
+
+
+def test_oracle_fix_fingers_round_converges():
+    """The oracle's synchronous fixfingers round (Chord.cc:845-875, 1228-1270) repairs a ring
+    whose successor pointers are right into the converged finger table."""
+    n = 800
+    net = W.population(n, 71)
+    ideal = O.OracleNet("chord", net.ids, net.xy).chord_fingers()
+    rng = np.random.default_rng(72)
+    fing = ideal.copy()
+    fing[rng.random(fing.shape) < 0.4] = 0xFFFFFFFF
+    pred = ((np.arange(n) - 1) % n).astype(np.uint32)
+    succ = ((np.arange(n)[:, None] + 1 + np.arange(8)[None, :]) % n).astype(np.uint32)
+    t = dict(pred=pred, succ=succ, nsucc=np.full(n, 8, np.uint8), fingers=fing,
+             deque_size=rng.integers(120, 161, n).astype(np.uint8))
+    o = O.OracleNet("chord", net.ids, net.xy, tables=t)
+    r = o.chord_fix_fingers()
+    assert r["ok"] > 0 and r["changed"] > 0
+    assert np.array_equal(o.chord_fingers(), ideal)
+    r2 = o.chord_fix_fingers()
+    assert r2["changed"] == 0 and r2["ok"] == r["ok"]
