@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 2
+#define OVS_ABI_VERSION 3
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -184,6 +184,28 @@ ovs_status  ovs_chord_fix_fingers(ovs_ctx* ctx, const uint32_t* nodes, uint64_t 
 ovs_status  ovs_route_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
                             uint64_t n, ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs,
                             uint32_t flags, void* stream);
+
+/* Result of one LookupCall (KBRTestApp lookup test, kbrLookupTest = true:
+ * KBRTestApp.cc:190-206 sends LookupCall{key, numSiblings = getMaxNumSiblings()};
+ * BaseOverlay::lookupRpc, BaseOverlay.cc:1938-1968; the answer is built by
+ * SendToKeyListener::lookupFinished, BaseOverlay.cc:1272-1300). */
+typedef struct ovs_lookup_out {
+    uint32_t num_siblings;  /* LookupResponse siblings array size (getResult().size()); 0 when !isValid */
+    uint16_t hops;          /* LookupResponse hopCount = IterativeLookup::getMinHops() */
+    uint8_t  status;        /* OVS_LOOKUP_* */
+    uint8_t  is_valid;      /* LookupResponse isValid = lookup->isValid() */
+    int64_t  latency_ns;    /* the LookupCall's RTT (an internal RPC: the lookup's duration), ns; -1 when !isValid */
+} ovs_lookup_out;
+
+/* Batched LookupCalls: lookup i resolves keys[i] at node src[i] with
+ * num_siblings siblings (-1 = getMaxNumSiblings(): Chord successorListSize,
+ * Kademlia s; larger than that is OVS_EINVAL like the reference's
+ * "numSiblings too big!").  siblings = n*num_siblings node indices, the
+ * response's sibling vector in order, 0xFFFFFFFF padded.  Iterative routing,
+ * single-context (unsharded) networks. */
+ovs_status  ovs_lookup_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
+                             uint64_t n, int32_t num_siblings, ovs_lookup_out* out,
+                             uint32_t* siblings, uint32_t flags, void* stream);
 
 /* Batched responder step: for each i, findNode(keys[i], numRedundantNodes,
  * numSiblings) evaluated at node[i] and the findNodeRpc siblings flag

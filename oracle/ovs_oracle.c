@@ -1044,13 +1044,17 @@ static int lk_checkStop(Lookup* L)
     return 0;
 }
 
+/* lout != NULL: the lookup answers a LookupCall with numSiblings (KBRTestApp.cc:190-206,
+ * BaseOverlay::lookupRpc 1938-1968) instead of routing the one-way message; the response is
+ * built by SendToKeyListener::lookupFinished (BaseOverlay.cc:1272-1300) and sibs receives the
+ * sibling vector (numSiblings slots, NONE padded). */
 static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out,
-                       uint32_t* hopseq, uint32_t* rpcsOut)
+                       uint32_t* hopseq, uint32_t* rpcsOut, int numSiblings, orc_lookup_out* lout, uint32_t* sibs)
 {
     const orc_params* p = &net->p;
     Lookup* L = (Lookup*)calloc(1, sizeof(Lookup));
     L->net = net; L->key = *key; L->S = S;
-    L->numSiblings = p->numSiblings; L->hopCountMax = p->hopCountMax;
+    L->numSiblings = lout ? numSiblings : p->numSiblings; L->hopCountMax = p->hopCountMax;
     L->hopseq = hopseq;
     L->minHops = 0x7fffffff;
     L->running = 1; L->startTime = 0; L->now = 0; L->txFinished = 0;
@@ -1117,6 +1121,23 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
     /* stop() -> SendToKeyListener::lookupFinished (BaseOverlay.cc:1241-1307) */
     int valid = L->success && L->finished;
     int minHops = (L->minHops == 0x7fffffff) ? 0 : L->minHops;
+    if (lout) {
+        /* LookupResponse: hopCount = getMinHops(), isValid, siblings = getResult() (1274-1286);
+         * the internal LookupCall's RTT is the lookup's duration */
+        lout->hops = (uint16_t)minHops;
+        lout->is_valid = (uint8_t)(valid ? 1 : 0);
+        lout->num_siblings = valid ? (uint32_t)L->nsiblings : 0;
+        lout->latency_ns = valid ? L->now - L->startTime : -1;
+        if (valid) lout->status = 0;
+        else if (L->now > L->startTime + simtime(p->lookupTimeout, p->simtimeRound)) lout->status = 1;
+        else if (L->ndead > 0) lout->status = 2;
+        else if (L->hopCountMax && L->hops >= L->hopCountMax) lout->status = 3;
+        else lout->status = 4;
+        for (int i = 0; i < numSiblings; ++i) sibs[i] = (valid && i < L->nsiblings) ? L->siblings[i] : NONE;
+        free(L->visited);
+        free(L);
+        return;
+    }
     out->hops = (uint16_t)minHops;
     if (valid && L->nsiblings > 0) {
         uint32_t R = L->siblings[0];
@@ -1214,7 +1235,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
         OKey k = ok_from(&keys[i]);
         if (net->p.routingType == 0)
             run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
-                       rpcs_out ? &rpcs_out[i] : NULL);
+                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL);
         else {
             run_recursive(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL);
             if (rpcs_out) rpcs_out[i] = 0;     /* no FindNodeCalls in recursive routing */
@@ -1223,6 +1244,27 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
     }
     (void)nthreads;
     return total;
+}
+
+int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int numSiblings,
+                     orc_lookup_out* out, uint32_t* siblings, int nthreads)
+{
+    const int maxs = net->type == NET_CHORD ? net->p.successorListSize : net->p.s;
+    if (numSiblings < 0) numSiblings = maxs;                              /* BaseOverlay.cc:1942-1944 */
+    if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
+    if (numSiblings < 1 || numSiblings > 16) { set_err("numSiblings must be 1..16"); return -1; }
+    if (net->p.routingType != 0) { set_err("LookupCall: iterative routing only"); return -1; }
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 256) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        OKey k = ok_from(&keys[i]);
+        orc_route_out dummy;
+        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings);
+    }
+    (void)nthreads;
+    return numSiblings;
 }
 
 /* ======================================================================== */

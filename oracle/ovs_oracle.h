@@ -116,6 +116,20 @@ typedef struct {
 uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
                          orc_route_out* out, uint32_t* hop_seq, uint32_t* rpcs_out, int nthreads);
 
+/* ---- batched LookupCalls (KBRTestApp lookup test) */
+typedef struct {
+    uint32_t num_siblings;  /* LookupResponse siblings array size (0 when !isValid) */
+    uint16_t hops;          /* getMinHops() */
+    uint8_t  status;        /* 0 ok, see ovs_kbr.h */
+    uint8_t  is_valid;
+    int64_t  latency_ns;    /* lookup duration; -1 when !isValid */
+} orc_lookup_out;
+
+/* numSiblings < 0 -> getMaxNumSiblings().  siblings = n * numSiblings (NONE padded).
+ * Returns the numSiblings used, -1 on error (orc_last_error). */
+int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int numSiblings,
+                     orc_lookup_out* out, uint32_t* siblings, int nthreads);
+
 /* One synchronous fixfingers round for nodes[0..m) (Chord.cc:845-875, 1228-1270): trivial
  * fingers removed, then lookups of n + 2^i routed over the tables, then finger i := result.
  * Explicit or converged networks.  Returns total hops; *out_ok successful lookups,

@@ -326,7 +326,10 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
         } else {
             // FindNodeCall S->cur, FindNodeResponse cur->S (one NodeHandle)
             const int64_t cd = coord_ns(sx, sy, cxy.x, cxy.y, DC.round);
-            const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
+            // the responsible node answers [cur, succ...] downsized to numSiblings (Chord.cc:573-580)
+            const int64_t mresp = (d.sib && DC.lookupCall)
+                ? resp_ns(DC, min(LC.numSiblings, 1 + (int)V.nsucc[cur])) : DC.msgResp1;
+            const int64_t rtt = DC.msgCall + mresp + 2 * cd;
             if (rtt >= DC.rpcTimeout) {
                 status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
             } else {
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(256) void k_chord_route(ChordView V, DelayConsts DC
                 o.responsible = R;
                 o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
                 // sendRouteMessage to result[0] (BaseOverlay.cc:1107-1146); 0 delay to self
-                o.latency_ns = t + (R != S ? DC.msgRoute + coord_ns(sx, sy, cxy.x, cxy.y, DC.round) : 0);
+                o.latency_ns = t + ((R != S && !DC.lookupCall) ? DC.msgRoute + coord_ns(sx, sy, cxy.x, cxy.y, DC.round) : 0);
             } else {
                 o.responsible = NONE;
                 o.one_way_hops = 0;
@@ -697,7 +700,7 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 } else {
                     // FindNodeCall S->cur, FindNodeResponse cur->S (one NodeHandle)
                     const int64_t cd = coord_ns(sx, sy, A.x, A.y, DC.round);
-                    const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
+                    const int64_t rtt = DC.msgCall + (asib ? DC.msgRespSib : DC.msgResp1) + 2 * cd;
                     if (rtt >= DC.rpcTimeout) {
                         fin = true;
                         status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
@@ -759,7 +762,7 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                     o.responsible = R;
                     o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
                     // sendRouteMessage to result[0] (BaseOverlay.cc:1107-1146); 0 delay to self
-                    o.latency_ns = t + (R != S ? DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round) : 0);
+                    o.latency_ns = t + ((R != S && !DC.lookupCall) ? DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round) : 0);
                 } else {
                     o.hops = (uint16_t)hops;
                     o.responsible = NONE;
@@ -1054,6 +1057,53 @@ __global__ void k_fill_rpcs(const ovs_route_out* __restrict__ out, uint64_t n, u
     // alpha = 1: one FindNodeCall per counted hop, plus the call whose response came too late
     const ovs_route_out o = out[i];
     rpcs[i] = o.hops + ((o.status == OVS_LOOKUP_TIMEOUT || o.status == OVS_LOOKUP_RPC_TIMEOUT) ? 1u : 0u);
+}
+
+// LookupCall results from the lookups' route records, in place (ovs_route_out and ovs_lookup_out
+// share their 16 B slot).  Chord: the sibling vector is the responsible node's findNode answer
+// [R, succ...] downsized to numSiblings (Chord.cc:573-580; IterativeLookup::addSibling pushes it
+// in order, 406-449).  Kademlia: the route kernel has written the answering response's nodes.
+__global__ void k_lookup_finish(ChordView V, int chord, int ideal, int ns, ovs_route_out* __restrict__ io,
+                                uint32_t* __restrict__ sibs, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ovs_route_out r = io[i];
+    const bool ok = r.status == OVS_LOOKUP_OK;
+    uint32_t* row = sibs + i * (uint64_t)ns;
+    uint32_t cnt = 0;
+    if (chord) {
+        if (ok) {
+            const uint32_t R = r.responsible;
+            const int ssize = ideal ? V.ns : (int)V.nsucc[R];
+            const int m = min(ns, 1 + ssize);
+            row[0] = R;
+            for (int j = 1; j < m; ++j)
+                row[j] = ideal ? ring_next(R, (uint32_t)j, V.n) : V.succ[(uint64_t)R * V.sls + (j - 1)];
+            cnt = (uint32_t)m;
+        }
+        for (int j = (int)cnt; j < ns; ++j) row[j] = NONE;
+    } else if (ok) {
+        while (cnt < (uint32_t)ns && row[cnt] != NONE) ++cnt;
+    } else {
+        for (int j = 0; j < ns; ++j) row[j] = NONE;
+    }
+    ovs_lookup_out o;
+    o.num_siblings = ok ? cnt : 0;
+    o.hops = r.hops;
+    o.status = r.status;
+    o.is_valid = ok ? 1 : 0;
+    o.latency_ns = ok ? r.latency_ns : -1;
+    reinterpret_cast<ovs_lookup_out*>(io)[i] = o;
+}
+
+hipError_t launch_lookup_finish(const ChordView& V, bool chord, bool ideal, int ns, ovs_route_out* io,
+                                uint32_t* sibs, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_lookup_finish, dim3(nblk(n, 256)), dim3(256), 0, s, V, chord ? 1 : 0, ideal ? 1 : 0, ns, io,
+                       sibs, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill_rpcs_from_hops(const ovs_route_out* out, uint64_t n, uint32_t* rpcs, hipStream_t s)

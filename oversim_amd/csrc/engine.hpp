@@ -28,7 +28,11 @@ struct DelayConsts {
     int32_t routeBytes;  // one-way route message, 186 B for testMsgSize = 100 B
     double datarate;
     int64_t access2;     // 2*T(accessDelay)
+    int64_t msgRespSib;  // same for the responsible node's FindNodeResponse on a converged Chord ring:
+                         // min(numSiblings, 1 + successors) NodeHandles (== msgResp1 for numSiblings = 1)
+    int32_t lookupCall;  // LookupCall (ovs_lookup_batch): the lookup ends at the last response, no route message
 };
+
 
 // SimTime(double) at scale 1e-9: truncation or round-half-up (recorded in every fixture)
 __device__ __forceinline__ int64_t simtime_ns(double seconds, int round)
@@ -53,6 +57,12 @@ __device__ __forceinline__ int64_t coord_ns(double ax, double ay, double bx, dou
 __device__ __forceinline__ int64_t bw_ns(int32_t bytes, double datarate, int round)
 {
     return simtime_ns(__ddiv_rn((double)((int64_t)bytes * 8), datarate), round);
+}
+
+// 2*T(L*8/datarate) + 2*T(accessDelay) of a FindNodeResponse carrying `nodes` NodeHandles
+__device__ __forceinline__ int64_t resp_ns(const DelayConsts& DC, int nodes)
+{
+    return 2 * bw_ns(DC.respBase + DC.respPerNode * nodes, DC.datarate, DC.round) + DC.access2;
 }
 
 __device__ __forceinline__ KeyRec load_rec(const KeyRec* __restrict__ recs, uint32_t i)

@@ -225,11 +225,12 @@ struct LocalFindNode {
     const KadView& V;
     const K160& K;
     int redundant;
+    int numSiblings;
     __device__ __forceinline__ bool ready(int) const { return true; }
     __device__ __forceinline__ void fill(int, uint32_t r, const RespGeo& g, bool sb, SVec<8>& res) const
     {
         Blk8 b;
-        const int n = kad_find_node_blk<EX>(V, r, g, K, redundant, sb, b);
+        const int n = kad_find_node_blk<EX>(V, r, g, K, redundant, sb, b, numSiblings);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
         res.n = n;
@@ -252,7 +253,7 @@ template <int A, bool RECORD, bool EX>
 __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, KadLC LC, const K160* __restrict__ qkeys,
                                                    const uint32_t* __restrict__ qsrc, uint64_t nq, uint64_t chunk,
                                                    ovs_route_out* __restrict__ out, uint32_t* __restrict__ hopseq,
-                                                   uint32_t* __restrict__ rpcs_out)
+                                                   uint32_t* __restrict__ rpcs_out, uint32_t* __restrict__ sib_out)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -282,21 +283,31 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
         if (!active) continue;
 
         if (!kad_lookup_done(L)) {
-            const LocalFindNode<EX> fn{V, L.K, LC.redundant};
+            const LocalFindNode<EX> fn{V, L.K, LC.redundant, LC.numSiblings};
             const HopRecorder<RECORD> rec{hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
             kad_lookup_event<A, EX>(L, V, DC, LC, res, fn, on, rec);
         }
         if (kad_lookup_done(L)) {
-            out[q] = kad_lookup_output(L, V, DC, LC);
+            const ovs_route_out o = kad_lookup_output(L, V, DC, LC);
+            out[q] = o;
             if (rpcs_out) rpcs_out[q] = L.nsent;
+            if (sib_out) {
+                // LookupCall: the siblings vector = the answering response's nodes (start(): the
+                // local findNode result), pushed in order up to numSiblings (IterativeLookup.cc:406-449)
+                const bool ok = o.status == OVS_LOOKUP_OK;
+                uint32_t* row = sib_out + q * (uint64_t)LC.numSiblings;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j < LC.numSiblings) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
+            }
             active = false;
         }
     }
 }
 
-// batched findNode (general numRedundantNodes <= 16, numSiblings == 1) for the ABI
+// batched findNode (general numRedundantNodes <= 16, 1 <= numSiblings <= 16) for the ABI
 __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, const K160* __restrict__ keys, uint64_t n,
-                                int numRedundant, uint32_t* __restrict__ out_nodes, uint32_t max_out,
+                                int numRedundant, int numSiblings, uint32_t* __restrict__ out_nodes, uint32_t max_out,
                                 uint8_t* __restrict__ out_count, uint8_t* __restrict__ out_sib)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -304,9 +315,9 @@ __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, co
     const uint32_t c = node[i];
     const K160 K = keys[i];
     const KadRec r = kad_rec(V.recs, c);
-    const bool sb = kad_is_sibling1(V, r, K);
+    const bool sb = kad_is_sibling(V, r, c, K, numSiblings);
     SVec<16> res;
-    kad_find_node1(V, c, r, K, numRedundant, sb, res);
+    kad_find_node1(V, c, r, K, numRedundant, sb, res, numSiblings);
     uint32_t* o = out_nodes + i * max_out;
     for (uint32_t j = 0; j < max_out; ++j) o[j] = NONE;
 #pragma unroll
@@ -422,20 +433,20 @@ static int kad_blocks_per_cu()
 template <int A, bool RECORD, bool EX>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
                              const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
-                             int num_cu, hipStream_t st)
+                             uint32_t* sibs, int num_cu, hipStream_t st)
 {
     const uint64_t waves = (uint64_t)num_cu * kad_blocks_per_cu<A, RECORD, EX>() * 4;
     uint64_t chunk = (nq + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
     const uint64_t need_waves = (nq + chunk - 1) / chunk;
     hipLaunchKernelGGL((k_kad_route<A, RECORD, EX>), dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, st, V, DC, LC,
-                       qkeys, qsrc, nq, chunk, out, hopseq, rpcs);
+                       qkeys, qsrc, nq, chunk, out, hopseq, rpcs, sibs);
     return hipGetLastError();
 }
 
 hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, uint32_t n, const ovs_params& P,
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                     uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st)
+                     uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st, uint32_t* sibs)
 {
     (void)recs;
     if (nq == 0) return hipSuccess;
@@ -444,8 +455,8 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
     const KadView V = kad_make_view(t, xy, n);
     // strictParallelRpcs: never more than alpha FindNodeCalls in flight (IterativeLookup.cc:1078-1079)
     const int A = P.lookupParallelRpcs;
-#define KLX(a, x) (hopseq ? kad_launch<a, true, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st) \
-                          : kad_launch<a, false, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, num_cu, st))
+#define KLX(a, x) (hopseq ? kad_launch<a, true, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st) \
+                          : kad_launch<a, false, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st))
 #define KL(a) (t.exact ? KLX(a, true) : KLX(a, false))
     switch (A) {
     case 1: return KL(1);
@@ -463,9 +474,9 @@ hipError_t kad_find_node(const KadTables& t, const KeyRec* recs, uint32_t n, con
 {
     (void)recs; (void)P;
     if (nq == 0) return hipSuccess;
-    if (numSiblings != 1 || numRedundant > 16) return hipErrorNotSupported;
+    if (numSiblings < 1 || numSiblings > 16 || numRedundant > 16) return hipErrorNotSupported;
     const KadView V = kad_make_view(t, nullptr, n);
-    hipLaunchKernelGGL(k_kad_find_node, dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, numRedundant, out_nodes,
+    hipLaunchKernelGGL(k_kad_find_node, dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, numRedundant, numSiblings, out_nodes,
                        max_out, out_count, out_sib);
     return hipGetLastError();
 }

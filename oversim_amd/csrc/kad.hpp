@@ -60,7 +60,8 @@ hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_
                       uint32_t* bucket_nodes, hipStream_t st);
 hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, uint32_t n, const ovs_params& P,
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
-                     ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st);
+                     ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st,
+                     uint32_t* sibs = nullptr);
 hipError_t kad_find_node(const KadTables& t, const KeyRec* recs, uint32_t n, const ovs_params& P,
                          const uint32_t* node, const K160* keys, uint64_t nq, int numRedundant, int numSiblings,
                          uint32_t* out_nodes, uint32_t max_out, uint8_t* out_count, uint8_t* out_sib,

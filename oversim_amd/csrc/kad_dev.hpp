@@ -257,6 +257,31 @@ __device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadRec& 
     return ((D.w[0] & M.w[0]) | (D.w[1] & M.w[1]) | (D.w[2] & M.w[2]) | (D.w[3] & M.w[3]) | (D.w[4] & M.w[4])) == 0;
 }
 
+// Kademlia::isSiblingFor(thisNode = c, key, numSiblings) for numSiblings >= 1 (Kademlia.cc:888-962):
+// c is in the numSiblings XOR-closest of siblings + c.  A sibling x is closer to K than c exactly
+// when bit msb(x ^ c) of D = c ^ K is set (x ^ K = (x ^ c) ^ D differs from D first at that bit),
+// so c qualifies when fewer than numSiblings siblings have their level bit set in D.  The mask
+// (OR of the level bits) decides the common case; the count reads c's sibling row (owned arc).
+__device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadRec& r, uint32_t c, const K160& K,
+                                               int numSiblings)
+{
+    if (numSiblings <= 1) return kad_is_sibling1(V, r, K);
+    if (V.nsib < numSiblings) return true;
+    const K160 me = as_key(r.key);
+    const K160 D = k_xor(me, K);
+    if (V.nsib == V.S5 && k_gt(D, as_key(r.R))) return false;
+    const K160 M = as_key(r.mask);
+    if (((D.w[0] & M.w[0]) | (D.w[1] & M.w[1]) | (D.w[2] & M.w[2]) | (D.w[3] & M.w[3]) | (D.w[4] & M.w[4])) == 0)
+        return true;
+    const KadEntry* L = V.sibe + (uint64_t)(c - V.lo) * V.S5;
+    int closer = 0;
+    for (int i = 0; i < V.nsib; ++i) {
+        const K160 x = as_key(L[i].key);
+        closer += (int)kbit(D, k_msb(k_xor(x, me)));
+    }
+    return closer < numSiblings;
+}
+
 // insert up to 8 entries of a contiguous entry array (bucket slot or sibling block); the
 // loads are issued together before the dependent sorted inserts
 template <int CAP>
@@ -312,16 +337,18 @@ __device__ __forceinline__ RespGeo resp_geo(const KadRec& r, const K160& K)
 // the sibling table and self, then buckets above while the result is short) merged 8 at a time
 template <bool EX>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
-                                                 int numRedundant, bool sib, Blk8& res)
+                                                 int numRedundant, bool sib, Blk8& res, int numSiblings = 1)
 {
     blk_clear(res);
-    if (V.nsib == 0 || sib) {
+    if (V.nsib == 0 || (sib && numSiblings <= 1)) {
         // resultSize = 1 and self is the XOR-closest of siblings + self (see kad_find_node1)
         res.x[0] = c;
         res.d[0] = dist_hi(kad_key(V.recs, c), K);
         return 1;
     }
-    const int cap = numRedundant < 8 ? numRedundant : 8;
+    // resultSize = numSiblings when c is a sibling for K, else numRedundantNodes (Kademlia.cc:1127-1129)
+    const int rs = sib ? numSiblings : numRedundant;
+    const int cap = rs < 8 ? rs : 8;
     const int m = g.m;
     const int endIndex = g.endIndex;
     int n = 0;
@@ -405,11 +432,11 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
 // Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246)
 template <int CAP, bool EX = true>
 __device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, const KadRec& r, const K160& K, int numRedundant,
-                               bool sib, SVec<CAP>& res)
+                               bool sib, SVec<CAP>& res, int numSiblings = 1)
 {
     if constexpr (CAP == 8) {
         Blk8 b;
-        const int n = kad_find_node_blk<EX>(V, c, resp_geo(r, K), K, numRedundant, sib, b);
+        const int n = kad_find_node_blk<EX>(V, c, resp_geo(r, K), K, numRedundant, sib, b, numSiblings);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
         res.n = n;
@@ -418,13 +445,14 @@ __device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, con
     }
     svec_clear(res);
     const K160 me = as_key(r.key);
-    if (V.nsib == 0 || sib) {
+    if (V.nsib == 0 || (sib && numSiblings <= 1)) {
         // resultSize = 1 and self is the XOR-closest of siblings + self; with a full table the
         // key lies below endIndex so bucket msb(D) is all siblings
         svec_add(res, 1, c, dist_hi(me, K), K, V.recs);
         return;
     }
-    const int cap = numRedundant < CAP ? numRedundant : CAP;
+    const int rs = sib ? numSiblings : numRedundant;
+    const int cap = rs < CAP ? rs : CAP;
     const K160 D = k_xor(me, K);
     const int m = k_msb(D);
     const int endIndex = k_msb(as_key(r.R));
@@ -508,11 +536,13 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
 {
     const double2 cxy = V.xy[x];
     const KadRec rr = kad_rec(V.recs, x);
-    const bool sb = kad_is_sibling1(V, rr, L.K);
+    const bool sb = kad_is_sibling(V, rr, x, L.K, LC.numSiblings);
     const RespGeo rg = resp_geo(rr, L.K);
     const uint32_t geo = (uint32_t)(rg.m + 1) | ((uint32_t)(rg.endIndex + 1) << 8) | (sb ? 0x10000u : 0u);
-    // the response carries findNode's result: 1 node when x is sibling, else min(redundant, n)
-    const int csz = sb ? 1 : (LC.redundant < (int)V.n ? LC.redundant : (int)V.n);
+    // the response carries findNode's result: min(numSiblings, n) nodes when x is sibling,
+    // else min(redundant, n)
+    const int rsz = sb ? LC.numSiblings : LC.redundant;
+    const int csz = rsz < (int)V.n ? rsz : (int)V.n;
     const int64_t cd = coord_ns(L.sx, L.sy, cxy.x, cxy.y, DC.round);
     const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
     const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
@@ -593,8 +623,8 @@ __device__ __forceinline__ void kad_lookup_start(KadLookup<A>& L, const KadView&
                                                  const KadLC& LC, SVec<8>& res, const OnSend& on)
 {
     const KadRec rs = kad_rec(V.recs, L.S);
-    const bool sb = kad_is_sibling1(V, rs, L.K);
-    kad_find_node1<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res);
+    const bool sb = kad_is_sibling(V, rs, L.S, L.K, LC.numSiblings);
+    kad_find_node1<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res, LC.numSiblings);
     if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
     else if (LC.numSiblings != 0 && sb) {
         L.result = res.idx[0];
@@ -690,7 +720,7 @@ __device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A>& L
         o.responsible = L.result;
         o.one_way_hops = (uint8_t)(L.hops + (L.result != L.S ? 1 : 0));
         int64_t lat = L.now;
-        if (L.result != L.S) {
+        if (L.result != L.S && !DC.lookupCall) {
             // sendRouteMessage through the source's tx queue (SimpleNodeEntry.cc:164-194)
             const double2 rxy = V.xy[L.result];
             const int64_t bwr = bw_ns(DC.routeBytes, DC.datarate, DC.round);
@@ -726,7 +756,8 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
 inline bool kad_params_supported(const ovs_params& P, const KadTables& t)
 {
     return P.lookupParallelRpcs >= 1 && P.lookupParallelRpcs <= MAXA && P.lookupRedundantNodes >= 1 &&
-           P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings == 1 &&
+           P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings >= 1 &&
+           P.numSiblings <= t.s && P.numSiblings <= 8 &&
            t.k <= 8 && P.hopCountMax <= 0x7FFF;
 }
 

@@ -221,7 +221,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
                           uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                           unsigned long long* done_count, unsigned long long* active_count, hipStream_t s)
 {
-    if (!kad_params_supported(P, t)) return hipErrorNotSupported;
+    if (!kad_params_supported(P, t) || P.numSiblings != 1) return hipErrorNotSupported;
     if (nlook == 0) return hipSuccess;
     const KadView V = kad_make_view(t, xy, n);
     const KadLC LC = kad_make_lc(P, t);
@@ -243,7 +243,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
                            ovs_kad_resp* out, hipStream_t s)
 {
-    if (!kad_params_supported(P, t)) return hipErrorNotSupported;
+    if (!kad_params_supported(P, t) || P.numSiblings != 1) return hipErrorNotSupported;
     if (nreq == 0) return hipSuccess;
     const KadView V = kad_make_view(t, nullptr, n);
     const KadLC LC = kad_make_lc(P, t);

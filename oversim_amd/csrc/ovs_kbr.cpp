@@ -7,6 +7,7 @@
 // stream.  No C++ exception crosses the boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -143,6 +144,8 @@ DelayConsts delay_consts(const ovs_params& P)
     d.rpcTimeout = simtime_host(P.rpcUdpTimeout, P.simtimeRound);
     d.lookupTimeout = simtime_host(P.lookupTimeout, P.simtimeRound);
     d.datarate = P.datarate;
+    d.msgRespSib = d.msgResp1;
+    d.lookupCall = 0;
     return d;
 }
 
@@ -625,7 +628,8 @@ ovs_status ovs_kad_shard_begin(ovs_ctx* c, const ovs_key160* keys, const uint32_
     ovs_status st = check_common(c, c->P);
     if (st != OVS_OK) return st;
     if (c->P.routingType != 0) return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
-    if (!kad_params_supported_host(c->P, c->kad)) return fail(c, OVS_ENOTSUP, "lookup configuration not implemented");
+    if (!kad_params_supported_host(c->P, c->kad) || c->P.numSiblings != 1)
+        return fail(c, OVS_ENOTSUP, "lookup configuration not implemented");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     const int alpha = c->P.lookupParallelRpcs;
@@ -728,6 +732,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         if (st != OVS_OK) return st;
     } else if (c->P.routingType != 0) {
         return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
+    } else if (c->P.numSiblings != 1) {
+        return fail(c, OVS_ENOTSUP, "the one-way route implements numSiblings = 1 (LookupCall: ovs_lookup_batch)");
     } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
         return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: use ovs_kad_shard_step");
     }
@@ -787,6 +793,97 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     }
     if (own_hop) hipFree(dhop);
     if (own_rpc) hipFree(drpc);
+    return OVS_OK;
+}
+
+ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n, int32_t num_siblings,
+                            ovs_lookup_out* out, uint32_t* siblings, uint32_t flags, void* stream)
+{
+    static_assert(sizeof(ovs_lookup_out) == sizeof(ovs_route_out), "lookup results are finished in place");
+    if (!c || (n && (!keys || !src || !out || !siblings))) return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    const bool chord = c->overlay == OVS_OVERLAY_CHORD;
+    // BaseOverlay::lookupRpc: numSiblings < 0 -> getMaxNumSiblings() (Chord.cc getMaxNumSiblings =
+    // successorListSize, Kademlia.cc:347-350 = s); isSiblingFor rejects larger values
+    const int32_t maxs = chord ? c->P.successorListSize : c->P.s;
+    const int32_t ns = num_siblings < 0 ? maxs : num_siblings;
+    if (ns > maxs) return fail(c, OVS_EINVAL, "numSiblings too big!");
+    if (ns == 0) return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup) not implemented");
+    if (ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall implements numSiblings <= 8");
+    ovs_params P = c->P;
+    P.numSiblings = 1;          // the route checks: one-way configuration, numSiblings applied below
+    ovs_status st = check_common(c, P);
+    if (st != OVS_OK) return st;
+    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;
+    if (chord) {
+        st = check_chord_route(c, P);
+        if (st != OVS_OK) return st;
+        if (c->ideal && (c->shard_lo != 0 || c->shard_hi != c->n))
+            return fail(c, OVS_ESTATE, "context holds one arc of a sharded ring: LookupCall needs the whole ring");
+        st = ensure_nodes(c, s);
+        if (st != OVS_OK) return st;
+    } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
+        return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: LookupCall needs the whole network");
+    }
+    if (n == 0) return OVS_OK;
+    P.numSiblings = ns;
+    DelayConsts DC = delay_consts(P);
+    DC.lookupCall = 1;
+    if (chord && c->ideal) {
+        // converged ring: every responsible node answers min(numSiblings, 1 + successors) nodes
+        const int64_t nsucc = std::min<int64_t>(P.successorListSize, (int64_t)c->n - 1);
+        const int nodes = (int)std::min<int64_t>(ns, 1 + nsucc);
+        DC.msgRespSib = 2 * simtime_host((double)((int64_t)(DC.respBase + DC.respPerNode * nodes) * 8) / P.datarate,
+                                         P.simtimeRound) + DC.access2;
+    }
+    K160* dk = nullptr; uint32_t* ds = nullptr; ovs_route_out* dout = nullptr; uint32_t* dsib = nullptr;
+    uint32_t* dhop = nullptr;
+    bool ok_k = false, ok_s = false;
+    if (!dev) {
+        st = to_device(c, reinterpret_cast<const K160*>(keys), n, false, &dk, &ok_k);
+        if (st != OVS_OK) return st;
+        st = to_device(c, src, n, false, &ds, &ok_s);
+        if (st != OVS_OK) { hipFree(dk); return st; }
+        HIPCHK(c, hipMalloc(&dout, sizeof(ovs_route_out) * n));
+        HIPCHK(c, hipMalloc(&dsib, sizeof(uint32_t) * n * ns));
+    } else {
+        dk = const_cast<K160*>(reinterpret_cast<const K160*>(keys));
+        ds = const_cast<uint32_t*>(src);
+        dout = reinterpret_cast<ovs_route_out*>(out);
+        dsib = siblings;
+    }
+    const int H = P.hopCountMax > 0 ? P.hopCountMax : 1;
+    const bool need_hop = chord && !c->ideal;      // visited check on explicit tables
+    if (need_hop) {
+        HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H));
+        HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
+    }
+    hipError_t e;
+    if (chord) {
+        LookupConsts LC{P.hopCountMax, ns, P.lookupRedundantNodes, 0};
+        e = launch_chord_route(chord_view(c), c->ideal, DC, LC, dk, ds, n, dout, dhop, c->num_cu, s);
+    } else {
+        e = kad_route(c->kad, c->recs, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
+                      dsib);
+    }
+    if (e == hipSuccess) e = launch_lookup_finish(chord_view(c), chord, c->ideal, ns, dout, dsib, n, s);
+    if (e != hipSuccess) {
+        if (!dev) { hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib); }
+        if (dhop) hipFree(dhop);
+        return hip_fail(c, e, "lookup kernel");
+    }
+    if (!dev) {
+        HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(ovs_lookup_out) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(siblings, dsib, sizeof(uint32_t) * n * ns, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib);
+    } else if (dhop) {
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    if (dhop) hipFree(dhop);
     return OVS_OK;
 }
 

@@ -2,6 +2,9 @@
 
 Names follow the reference so a test reads like OverSim code:
 
+  KbrEngine.lookupCall(keys, src, numSiblings)
+        -> BaseOverlay::lookupRpc for a batch of KBRTestApp LookupCalls
+           (KBRTestApp.cc:190-206, BaseOverlay.cc:1938-1968, 1272-1300)
   KbrEngine.findNode(node, key, numRedundantNodes, numSiblings)
         -> BaseOverlay::findNode (BaseOverlay.h:693-696; Chord.cc:548-599,
            Kademlia.cc:1101-1246), evaluated at `node`
@@ -100,6 +103,9 @@ class Params(C.Structure):
 ROUTE_OUT_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
                             ("one_way_hops", "u1"), ("latency_ns", "<i8")])
 assert ROUTE_OUT_DTYPE.itemsize == 16
+LOOKUP_OUT_DTYPE = np.dtype([("num_siblings", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                             ("is_valid", "u1"), ("latency_ns", "<i8")])
+assert LOOKUP_OUT_DTYPE.itemsize == 16
 
 class StdDev(C.Structure):
     """ovs_stddev: one cStdDev summary (GlobalStatistics::addStdDev)."""
@@ -165,6 +171,7 @@ def lib() -> C.CDLL:
         "ovs_sync": ([vp], C.c_int),
         "ovs_kbrtest_stats_batch": ([vp, vp, vp, vp, u64, C.c_double, i32, vp, u32, vp], C.c_int),
         "ovs_chord_fix_fingers": ([vp, vp, u64, vp], C.c_int),
+        "ovs_lookup_batch": ([vp, vp, vp, u64, i32, vp, vp, u32, vp], C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -320,6 +327,26 @@ class KbrEngine:
             res["hop_seq"] = hop
         if rpcs is not None:
             res["rpcs"] = rpcs
+        return res
+
+    def lookupCall(self, keys, src, numSiblings: int = -1) -> dict:
+        """Batched LookupCalls (KBRTestApp lookup test; BaseOverlay::lookupRpc, BaseOverlay.cc:1938-1968,
+        answered by SendToKeyListener::lookupFinished, 1272-1300).  numSiblings = -1 is
+        getMaxNumSiblings(), as KBRTestApp sends it.  Returns num_siblings, hops, status, is_valid,
+        latency_ns per lookup and `siblings` (n, numSiblings), NONE padded."""
+        keys = keys_array(keys)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        if len(src) != n:
+            raise ValueError("keys and src differ in length")
+        p = self.get_params()
+        ns = numSiblings if numSiblings >= 0 else (p.successorListSize if p.overlay == OVERLAY_CHORD else p.s)
+        out = np.empty(n, dtype=LOOKUP_OUT_DTYPE)
+        sib = np.empty((n, max(ns, 1)), dtype=np.uint32)
+        self._chk(self._L.ovs_lookup_batch(self._h, _ptr(keys), _ptr(src), n, numSiblings, _ptr(out), _ptr(sib), 0,
+                                           None), "ovs_lookup_batch")
+        res = {f: out[f].copy() for f in LOOKUP_OUT_DTYPE.names}
+        res["siblings"] = sib
         return res
 
     def lookup_device(self, keys_ptr: int, src_ptr: int, n: int, out_ptr: int, stream: int | None = None,

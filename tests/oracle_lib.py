@@ -15,6 +15,9 @@ _SO = ROOT / "oracle" / "_build" / "libovs_oracle.so"
 ROUTE_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
                         ("one_way_hops", "u1"), ("latency_ns", "<i8")])
 
+LOOKUP_DTYPE = np.dtype([("num_siblings", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                         ("is_valid", "u1"), ("latency_ns", "<i8")])
+
 
 class OrcParams(C.Structure):
     _fields_ = [
@@ -75,6 +78,7 @@ def lib() -> C.CDLL:
             ("orc_last_error", [], C.c_char_p),
             ("orc_kbrtest_stats", [vp, vp, vp, vp, u64, C.c_double, C.c_int, i32, vp], None),
             ("orc_chord_fix_fingers", [vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.c_int], u64),
+            ("orc_lookup_batch", [vp, vp, vp, u64, C.c_int, vp, vp, C.c_int], C.c_int),
         ]:
             f = getattr(L, name)
             f.argtypes = args
@@ -160,6 +164,22 @@ class OracleNet:
             res["hop_seq"] = hop
         if rpcs is not None:
             res["rpcs"] = rpcs
+        return res
+
+    def lookup_call(self, keys, src, numSiblings: int = -1, nthreads=0) -> dict:
+        """Batched LookupCalls (orc_lookup_batch); numSiblings = -1 is getMaxNumSiblings()."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        ns = numSiblings if numSiblings >= 0 else (self.params.successorListSize if self.kind == "chord"
+                                                   else self.params.s)
+        out = np.empty(n, dtype=LOOKUP_DTYPE)
+        sib = np.empty((n, max(ns, 1)), dtype=np.uint32)
+        r = lib().orc_lookup_batch(self._h, _p(keys), _p(src), n, numSiblings, _p(out), _p(sib), nthreads)
+        if r < 0:
+            raise ValueError(lib().orc_last_error().decode())
+        res = {f: out[f].copy() for f in LOOKUP_DTYPE.names}
+        res["siblings"] = sib
         return res
 
     def kbrtest_stats(self, result: dict, keys, src, measured_time_s: float, lookupNodeIds: bool = True,

@@ -152,6 +152,39 @@ class ChordRing:
                 return dict(responsible=0xFFFFFFFF, hops=hops, status=4, one_way_hops=0, latency_ns=-1, hop_seq=seq)
             cur = nxt
 
+    def lookup_call(self, kw, S, num_siblings=8, hop_max=50, call=83, resp=87, rpc_to=1.5, lk_to=10.0):
+        """KBRTestApp LookupCall: the same iterative path; the responsible node answers
+        [R, succ...] cut to num_siblings (a bigger FindNodeResponse: 61 B + 26 B per node), the
+        response ends the lookup (no route message) and the siblings vector is that answer."""
+        k = to_int(kw)
+        rnd = self.rnd
+        m = min(num_siblings, 1 + self.ns)
+        resp_sib = 61 + 26 * m
+        sib, nxt = self.decide(S, k)
+        if sib:
+            return dict(siblings=[(S + j) % self.n for j in range(m)], hops=0, status=0, latency_ns=0)
+        t, hops, visited = 0, 0, {S}
+        cur = nxt
+        while True:
+            sib, nxt = self.decide(cur, k)
+            cd = coord_ns(self.xy, S, cur, rnd)
+            rtt = msg_ns(call, rnd) + cd + msg_ns(resp_sib if sib else resp, rnd) + cd
+            if rtt >= simtime(rpc_to, rnd):
+                st = 1 if t + simtime(rpc_to, rnd) > simtime(lk_to, rnd) else 2
+                return dict(siblings=[], hops=hops, status=st, latency_ns=-1)
+            t += rtt
+            if t > simtime(lk_to, rnd):
+                return dict(siblings=[], hops=hops, status=1, latency_ns=-1)
+            hops += 1
+            visited.add(cur)
+            if sib:
+                return dict(siblings=[(cur + j) % self.n for j in range(m)], hops=hops, status=0, latency_ns=t)
+            if hop_max and hops >= hop_max:
+                return dict(siblings=[], hops=hops, status=3, latency_ns=-1)
+            if nxt in visited:
+                return dict(siblings=[], hops=hops, status=4, latency_ns=-1)
+            cur = nxt
+
     def lookup_recursive(self, kw, S, hop_max=50, route=186):
         """Semi-recursive one-way route message: greedy forwarding S -> ... -> responsible,
         one UDP message of `route` bytes per hop (BaseOverlay.cc:1445-1582, 907-914)."""

@@ -1,0 +1,141 @@
+"""GPU parity tests for the LookupCall variant (KBRTestApp lookup test).
+
+KBRTestApp.cc:190-206 sends LookupCall{key, numSiblings = getMaxNumSiblings()} to its own
+overlay; BaseOverlay::lookupRpc (BaseOverlay.cc:1938-1968) runs the iterative lookup with
+that numSiblings and SendToKeyListener::lookupFinished (1272-1300) answers with the sibling
+vector, the hop count and isValid.  The engine (ovs_lookup_batch) must match the oracle
+bit-exactly: sibling vector, its size, hop count, status, validity and int64-ns duration.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oversim_amd import KbrEngine, KbrError, Params, workload as W
+from oracle_lib import OracleNet, chord_params, kad_params
+
+pytestmark = pytest.mark.gpu
+FIELDS = ("num_siblings", "hops", "status", "is_valid", "latency_ns")
+
+
+def _eq(a: dict, b: dict, label: str):
+    for f in FIELDS:
+        x, y = np.asarray(a[f]).astype(np.int64), np.asarray(b[f]).astype(np.int64)
+        bad = np.nonzero(x != y)[0]
+        assert len(bad) == 0, f"{label}: {f} differs at {bad[:8]}: gpu={x[bad[:8]]} ref={y[bad[:8]]}"
+    bad = np.nonzero(np.any(a["siblings"] != b["siblings"], axis=1))[0]
+    assert len(bad) == 0, f"{label}: siblings differ at {bad[:8]}: gpu={a['siblings'][bad[:2]]} ref={b['siblings'][bad[:2]]}"
+
+
+@pytest.mark.parametrize("n,seed", [(2, 1), (6, 2), (9, 3), (1000, 4), (20000, 5)])
+@pytest.mark.parametrize("ns", [-1, 1, 3])
+def test_chord_lookup_call_matches_oracle(engine: KbrEngine, n, seed, ns):
+    net = W.population(n, seed)
+    engine.set_params(Params.chord())
+    engine.chord_load(net.ids, net.xy)
+    o = OracleNet("chord", net.ids, net.xy)
+    k1, s1 = W.lookups(net.ids, 3000, seed + 10, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 3000, seed + 20, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    _eq(engine.lookupCall(keys, src, ns), o.lookup_call(keys, src, ns), f"chord n={n} ns={ns}")
+
+
+@pytest.mark.parametrize("sls", [3, 8])
+def test_chord_lookup_call_successor_list_sizes(engine: KbrEngine, sls):
+    net = W.population(4000, 31)
+    engine.set_params(Params.chord().replace(successorListSize=sls))
+    engine.chord_load(net.ids, net.xy)
+    o = OracleNet("chord", net.ids, net.xy, chord_params(successorListSize=sls))
+    keys, src = W.lookups(net.ids, 5000, 32, node_ids=True)
+    _eq(engine.lookupCall(keys, src), o.lookup_call(keys, src), f"chord sls={sls}")
+
+
+def test_chord_lookup_call_explicit_tables(engine: KbrEngine):
+    """Non-converged tables: short successor lists shrink the answer (Chord.cc:573-580)."""
+    from test_gpu_chord import _broken_tables
+    net, t = _broken_tables(3000, 33)
+    o = OracleNet("chord", net.ids, net.xy, tables=t)
+    engine.set_params(Params.chord())
+    engine.chord_load_tables(net.ids, net.xy, t["pred"], t["succ"], t["nsucc"], t["fingers"], t["deque_size"])
+    keys, src = W.lookups(net.ids, 6000, 34, node_ids=False)
+    g, r = engine.lookupCall(keys, src), o.lookup_call(keys, src)
+    _eq(g, r, "chord explicit")
+    assert len(np.unique(g["num_siblings"][g["is_valid"] == 1])) > 1
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+@pytest.mark.parametrize("ns", [-1, 3, 1])
+def test_kad_lookup_call_matches_oracle(engine: KbrEngine, alpha, ns):
+    net = W.population(15000, 0x4b41)
+    engine.set_params(Params.kademlia().replace(lookupParallelRpcs=alpha))
+    engine.kad_load(net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params(lookupParallelRpcs=alpha))
+    k1, s1 = W.lookups(net.ids, 6000, 40 + alpha, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 3000, 50 + alpha, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    _eq(engine.lookupCall(keys, src, ns), o.lookup_call(keys, src, ns), f"kad alpha={alpha} ns={ns}")
+
+
+@pytest.mark.parametrize("n,seed", [(2, 1), (9, 2), (41, 4)])
+def test_kad_lookup_call_small_networks(engine: KbrEngine, n, seed):
+    net = W.population(n, seed)
+    engine.set_params(Params.kademlia().replace(lookupParallelRpcs=3))
+    engine.kad_load(net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params(lookupParallelRpcs=3))
+    keys, src = W.lookups(net.ids, 2000, seed + 3, node_ids=bool(seed % 2))
+    _eq(engine.lookupCall(keys, src), o.lookup_call(keys, src), f"kad n={n}")
+
+
+def test_kad_find_node_with_siblings_matches_oracle(engine: KbrEngine):
+    """findNode / isSiblingFor at responders with numSiblings = s (the LookupCall's FindNodeCalls)."""
+    net = W.population(15000, 0x4b41)
+    engine.set_params(Params.kademlia())
+    engine.kad_load(net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy)
+    sib, _, _ = engine.kad_tables()
+    rng = np.random.default_rng(44)
+    node = rng.integers(0, 15000, 3000).astype(np.uint32)
+    keys = W.random_keys(3000, rng)
+    keys[:1000] = net.ids[node[:1000]]
+    keys[1000:2000] = net.ids[sib[node[1000:2000], rng.integers(0, 16, 1000)]]
+    for ns in (8, 4, 2):
+        got, cnt, flag = engine.findNode(node, keys, 8, ns, max_out=16)
+        for i in range(len(node)):
+            ref, f = o.find_node(int(node[i]), keys[i], 8, ns)
+            assert list(got[i, :cnt[i]]) == ref, (ns, i)
+            assert bool(flag[i]) == f, (ns, i)
+
+
+def test_lookup_call_rejects(engine: KbrEngine):
+    net = W.population(200, 45)
+    engine.set_params(Params.chord())
+    engine.chord_load(net.ids, net.xy)
+    keys, src = W.lookups(net.ids, 10, 46, node_ids=True)
+    with pytest.raises(KbrError):
+        engine.lookupCall(keys, src, 9)                # numSiblings too big!
+    with pytest.raises(KbrError):
+        engine.lookupCall(keys, src, 0)                # exact-key lookups: not implemented
+    engine.set_params(Params.chord().replace(routingType=1))
+    with pytest.raises(KbrError):
+        engine.lookupCall(keys, src)
+    with KbrEngine(0) as kad:
+        kad.set_params(Params.kademlia().replace(numSiblings=8))
+        kad.kad_load(net.ids, net.xy)
+        with pytest.raises(KbrError):
+            kad.lookup(keys, src)                      # one-way route: numSiblings = 1 only
+
+
+def test_lookup_call_full_batch_properties(engine: KbrEngine):
+    """Config C size (2^20 lookups on a 2^18 ring): all valid, siblings = [R, R+1, ...] and the
+    answer's first node owns the node-ID key."""
+    net = W.population(1 << 18, 47)
+    engine.set_params(Params.chord())
+    engine.chord_load(net.ids, net.xy)
+    keys, src = W.lookups(net.ids, 1 << 20, 48, node_ids=True)
+    g = engine.lookupCall(keys, src)
+    assert np.all(g["is_valid"] == 1) and np.all(g["num_siblings"] == 8)
+    R = g["siblings"][:, 0].astype(np.int64)
+    assert np.array_equal(net.ids[R], keys)
+    assert np.array_equal(g["siblings"], ((R[:, None] + np.arange(8)[None, :]) % (1 << 18)).astype(np.uint32))
+    r = engine.lookup(keys, src)
+    assert np.array_equal(r["hops"], g["hops"])

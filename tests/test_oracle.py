@@ -235,3 +235,94 @@ def test_oracle_fix_fingers_round_converges():
     assert np.array_equal(o.chord_fingers(), ideal)
     r2 = o.chord_fix_fingers()
     assert r2["changed"] == 0 and r2["ok"] == r["ok"]
+
+
+# ------------------------------------------------------------ LookupCall (KBRTestApp lookup test)
+
+@pytest.mark.parametrize("ns", [8, 3, 1])
+def test_oracle_lookup_call_matches_refmodel_chord(ns):
+    """orc_lookup_batch (the full IterativeLookup state machine with numSiblings = ns) vs the
+    refmodel's direct loop: siblings vector, hop count, status, lookup duration."""
+    for n, seed in ((2, 5), (6, 6), (300, 7), (2500, 8)):
+        net = W.population(n, seed)
+        k, s = W.lookups(net.ids, 300, seed + 9, node_ids=bool(seed % 2))
+        r = O.OracleNet("chord", net.ids, net.xy).lookup_call(k, s, ns)
+        ring = refmodel.ChordRing(net.ids, net.xy)
+        for i in range(len(k)):
+            m = ring.lookup_call(k[i], int(s[i]), ns)
+            row = [int(x) for x in r["siblings"][i] if x != 0xFFFFFFFF]
+            assert row == m["siblings"], (n, i)
+            assert int(r["num_siblings"][i]) == len(m["siblings"]), (n, i)
+            for f in ("hops", "status", "latency_ns"):
+                assert int(r[f][i]) == int(m[f]), (n, i, f)
+            assert int(r["is_valid"][i]) == (m["status"] == 0)
+
+
+def test_oracle_lookup_call_chord_relates_to_route():
+    """Same path as the one-way route; the lookup ends at the answering response."""
+    net = W.population(3000, 12)
+    o = O.OracleNet("chord", net.ids, net.xy)
+    k, s = W.lookups(net.ids, 2000, 13, node_ids=True)
+    a = o.route(k, s)
+    b = o.lookup_call(k, s, 1)
+    assert np.array_equal(a["hops"], b["hops"])
+    assert np.array_equal(a["responsible"], b["siblings"][:, 0])
+    local = a["responsible"] == s
+    assert np.all(b["latency_ns"][local] == a["latency_ns"][local])
+    assert np.all(b["latency_ns"][~local] < a["latency_ns"][~local])
+    c = o.lookup_call(k, s, -1)                     # getMaxNumSiblings() = successorListSize
+    assert c["siblings"].shape[1] == 8 and np.all(c["num_siblings"] == 8)
+    assert np.array_equal(c["siblings"], (a["responsible"][:, None] + np.arange(8)[None, :]) % 3000)
+    assert np.all(c["latency_ns"][~local] > b["latency_ns"][~local])   # 7 more NodeHandles in the answer
+    with pytest.raises(ValueError):
+        o.lookup_call(k[:4], s[:4], 9)               # numSiblings too big!
+
+
+@pytest.mark.parametrize("ns", [8, 5, 2])
+def test_oracle_kademlia_sibling_findnode_matches_refmodel(ns):
+    """Kademlia::isSiblingFor / findNode with numSiblings > 1 (the LookupCall's responders)."""
+    net = W.population(1200, 19)
+    o = O.OracleNet("kademlia", net.ids, net.xy)
+    sib, cnt, nodes = o.kad_tables()
+    tab = refmodel.KadTables(net.ids, sib, cnt, nodes)
+    rng = np.random.default_rng(20)
+    nsib = 0
+    for i in range(400):
+        c = int(rng.integers(0, 1200))
+        if i % 3 == 0:
+            key = W.random_keys(1, rng)[0]
+        else:
+            # keys near c: c's own id or a close node's, so that c is often a sibling
+            key = net.ids[int(sib[c][int(rng.integers(0, 12))])] if i % 3 == 1 else net.ids[c]
+        res, flag = o.find_node(c, key, 8, ns)
+        kk = refmodel.to_int(key)
+        assert flag == tab.is_sibling_for(c, kk, ns)
+        assert [int(x) for x in res] == tab.find_node(c, kk, 8, ns)
+        nsib += flag
+    assert 50 < nsib < 400
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+def test_oracle_kademlia_lookup_call_properties(alpha):
+    """Kademlia LookupCall (numSiblings = s): valid lookups return s distinct nodes in XOR order
+    from the answering sibling's view (not always the global s closest: the answer comes from the
+    responder's own tables); node-ID keys find their node first; the lookup needs no more hops
+    than the one-way route (it stops at the first responder in the key's top s)."""
+    net = W.population(2000, 23)
+    p = O.kad_params(lookupParallelRpcs=alpha)
+    o = O.OracleNet("kademlia", net.ids, net.xy, p)
+    k, s = W.lookups(net.ids, 600, 24, node_ids=True)
+    r = o.lookup_call(k, s)
+    a = o.route(k, s)
+    assert np.all(r["is_valid"] == 1) and np.all(r["num_siblings"] == 8)
+    ids = [refmodel.to_int(w) for w in net.ids]
+    exact = 0
+    for i in range(len(k)):
+        kk = refmodel.to_int(k[i])
+        row = [int(x) for x in r["siblings"][i]]
+        d = [ids[x] ^ kk for x in row]
+        assert d == sorted(d) and len(set(row)) == 8, i
+        assert ids[row[0]] == kk, i                                 # node-ID key: its node first
+        exact += row == sorted(range(2000), key=lambda x: ids[x] ^ kk)[:8]
+    assert exact > len(k) // 2
+    assert np.all(r["hops"] <= a["hops"])
