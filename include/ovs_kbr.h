@@ -270,6 +270,43 @@ ovs_status  ovs_kbrtest_stats_batch(ovs_ctx* ctx, const ovs_route_out* out, cons
                                     int32_t lookup_node_ids, ovs_kbrtest_stats* stats,
                                     uint32_t flags, void* stream);
 
+/* ---- KBRTestApp statistics (lookup test, kbrLookupTest = true) ----
+ *   KBRTestApp::handleLookupResponse / RPC timeout  KBRTestApp.cc:315-371
+ *     success = isValid && (!lookupNodeIds || siblings[0] is the node owning the key);
+ *     recordOutVector("KBRTestApp: Lookup Success Latency" / "Lookup Total Latency" /
+ *     "Lookup Hop Count"), failures: "Lookup Total Latency" = failureLatency,
+ *     "Failed Lookup Hop Count"
+ *   KBRTestApp::finishApp                          KBRTestApp.cc:546-557 */
+typedef struct ovs_kbrtest_lookup_stats {
+    uint64_t num_sent;               /* numLookupSent (= lookups in the batch) */
+    uint64_t num_success;            /* numLookupSuccess */
+    uint64_t num_failed;             /* numLookupFailed */
+    uint64_t num_invalid;            /* the failed lookups with isValid == false */
+    uint64_t hop_count_sum;          /* "Lookup Hop Count" over successful lookups */
+    uint64_t failed_hop_count_sum;   /* "Failed Lookup Hop Count" */
+    int64_t  success_latency_sum_ns; /* "Lookup Success Latency" */
+    uint32_t hop_count_min, hop_count_max;
+    int64_t  success_latency_min_ns, success_latency_max_ns;
+    double   hop_count_mean;         /* "Vector: KBRTestApp: Lookup Hop Count.mean" */
+    double   failed_hop_count_mean;  /* "Vector: KBRTestApp: Failed Lookup Hop Count.mean" */
+    double   success_latency_mean_s; /* "Vector: KBRTestApp: Lookup Success Latency.mean" */
+    double   total_latency_mean_s;   /* "Vector: KBRTestApp: Lookup Total Latency.mean" */
+    uint64_t status_count[8];        /* lookups by OVS_LOOKUP_* status */
+    uint64_t hop_hist[64];           /* successful lookups by hop count (63 = 63 or more) */
+    ovs_stddev successful_lookups_per_s;  /* "KBRTestApp: Successful Lookups/s" */
+    ovs_stddev failed_lookups_per_s;      /* "KBRTestApp: Failed Lookups/s" */
+    ovs_stddev success_ratio;             /* "KBRTestApp: Lookup Success Ratio" ((float)s / (float)sent) */
+} ovs_kbrtest_lookup_stats;
+
+/* Reduce a batch of LookupCall results (out/siblings/keys/src as passed to
+ * ovs_lookup_batch; siblings_stride = its num_siblings) to the KBRTestApp lookup
+ * statistics.  failure_latency_s = kbrTestApp.failureLatency (default.ini:41, 10 s). */
+ovs_status  ovs_kbrtest_lookup_stats_batch(ovs_ctx* ctx, const ovs_lookup_out* out, const uint32_t* siblings,
+                                           int32_t siblings_stride, const ovs_key160* keys, const uint32_t* src,
+                                           uint64_t n, double measured_time_s, int32_t lookup_node_ids,
+                                           double failure_latency_s, ovs_kbrtest_lookup_stats* stats,
+                                           uint32_t flags, void* stream);
+
 /* ---- multi-GPU sharding (one process per GPU; the host exchanges records) ----
  * The sorted ring is cut into contiguous arcs, one per rank.  Node keys,
  * coordinates and 64 B node records are replicated; the finger rows -- the bulk

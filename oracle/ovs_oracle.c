@@ -1406,3 +1406,63 @@ void orc_kbrtest_stats(const orc_net* net, const orc_route_out* out, const orc_k
     for (int k = 0; k < 5; ++k) sd_finish(&sd[k], &st->sd[k]);
     free(sent); free(deliv); free(drop);
 }
+
+/* ======================================================================== */
+/* KBRTestApp lookup-test statistics (kbrLookupTest): handleLookupResponse  */
+/* (KBRTestApp.cc:331-371) per LookupResponse in batch order, finishApp      */
+/* (546-557) per node in node order.                                         */
+/* ======================================================================== */
+void orc_kbrtest_lookup_stats(const orc_net* net, const orc_lookup_out* out, const uint32_t* siblings, int stride,
+                              const orc_key* keys, const uint32_t* src, uint64_t n, double T, int lookupNodeIds,
+                              double failureLatency, orc_kbrtest_lookup_result* st)
+{
+    uint64_t* sent = calloc(net->n, sizeof(uint64_t));
+    uint64_t* succ = calloc(net->n, sizeof(uint64_t));
+    uint64_t* fail = calloc(net->n, sizeof(uint64_t));
+    memset(st, 0, sizeof *st);
+    double hopVec = 0, fhopVec = 0, succLatVec = 0, totLatVec = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t s = src[i];
+        if (s < net->n) sent[s]++;                                   /* numLookupSent++ (205) */
+        st->num_sent++;
+        int ok = out[i].is_valid != 0;                               /* msg->getIsValid() (341) */
+        if (ok && lookupNodeIds) {                                   /* 341-344 */
+            OKey k = ok_from(&keys[i]);
+            const uint32_t f = siblings[(size_t)i * stride];
+            ok = out[i].num_siblings > 0 && f < net->n && ok_cmp(&net->ids[f], &k) == 0;
+        }
+        if (ok) {
+            st->num_success++;
+            if (s < net->n) succ[s]++;
+            st->hop_count_sum += out[i].hops;
+            st->success_latency_sum_ns += out[i].latency_ns;
+            succLatVec += (double)out[i].latency_ns * 1e-9;          /* "Lookup Success Latency" */
+            totLatVec += (double)out[i].latency_ns * 1e-9;           /* "Lookup Total Latency" */
+            hopVec += (double)out[i].hops;                           /* "Lookup Hop Count" */
+        } else {
+            st->num_failed++;
+            if (!out[i].is_valid) st->num_invalid++;
+            if (s < net->n) fail[s]++;
+            st->failed_hop_count_sum += out[i].hops;
+            totLatVec += failureLatency;                             /* failureLatency (363-366) */
+            fhopVec += (double)out[i].hops;                          /* "Failed Lookup Hop Count" */
+        }
+    }
+    if (st->num_success) {
+        st->hop_count_mean = hopVec / (double)st->num_success;
+        st->success_latency_mean_s = succLatVec / (double)st->num_success;
+    }
+    if (st->num_failed) st->failed_hop_count_mean = fhopVec / (double)st->num_failed;
+    if (n) st->total_latency_mean_s = totLatVec / (double)n;
+    StdDev sd[3];
+    memset(sd, 0, sizeof sd);
+    if (T >= 0.1) {
+        for (uint32_t c = 0; c < net->n; ++c) {
+            sd_collect(&sd[0], (double)succ[c] / T);                 /* Successful Lookups/s */
+            sd_collect(&sd[1], (double)fail[c] / T);                 /* Failed Lookups/s */
+            if (sent[c] > 0) sd_collect(&sd[2], (double)((float)succ[c] / (float)sent[c]));
+        }
+    }
+    for (int k = 0; k < 3; ++k) sd_finish(&sd[k], &st->sd[k]);
+    free(sent); free(succ); free(fail);
+}

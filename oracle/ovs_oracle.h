@@ -157,6 +157,17 @@ typedef struct {
 void orc_kbrtest_stats(const orc_net* net, const orc_route_out* out, const orc_key* keys, const uint32_t* src,
                        uint64_t n, double measured_time_s, int lookupNodeIds, int32_t testMsgSize,
                        orc_kbrtest_result* st);
+typedef struct {
+    uint64_t num_sent, num_success, num_failed, num_invalid;
+    uint64_t hop_count_sum, failed_hop_count_sum;
+    int64_t  success_latency_sum_ns;
+    double   hop_count_mean, failed_hop_count_mean, success_latency_mean_s, total_latency_mean_s;
+    orc_stddev sd[3];   /* successful lookups/s, failed lookups/s, success ratio */
+} orc_kbrtest_lookup_result;
+/* KBRTestApp lookup-test statistics (KBRTestApp.cc:331-371, 546-557) of orc_lookup_batch output */
+void orc_kbrtest_lookup_stats(const orc_net* net, const orc_lookup_out* out, const uint32_t* siblings, int stride,
+                              const orc_key* keys, const uint32_t* src, uint64_t n, double measured_time_s,
+                              int lookupNodeIds, double failureLatency, orc_kbrtest_lookup_result* st);
 const char* orc_last_error(void);
 
 #ifdef __cplusplus

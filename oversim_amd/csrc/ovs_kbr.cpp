@@ -1065,6 +1065,106 @@ ovs_status ovs_kbrtest_stats_batch(ovs_ctx* c, const ovs_route_out* out, const o
     return OVS_OK;
 }
 
+ovs_status ovs_kbrtest_lookup_stats_batch(ovs_ctx* c, const ovs_lookup_out* out, const uint32_t* siblings,
+                                          int32_t siblings_stride, const ovs_key160* keys, const uint32_t* src,
+                                          uint64_t n, double measured_time_s, int32_t lookup_node_ids,
+                                          double failure_latency_s, ovs_kbrtest_lookup_stats* stats, uint32_t flags,
+                                          void* stream)
+{
+    if (!c || !stats || siblings_stride < 1 || (n && (!out || !src || !siblings || (lookup_node_ids && !keys))))
+        return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (!(measured_time_s >= 0)) return fail(c, OVS_EINVAL, "measured_time_s must be >= 0");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;
+    const ovs_route_out* dout = reinterpret_cast<const ovs_route_out*>(out);
+    const K160* dk = reinterpret_cast<const K160*>(keys);
+    const uint32_t* ds = src;
+    const uint32_t* dsib = siblings;
+    std::vector<void*> owned;
+    auto cleanup = [&]() { for (void* p : owned) hipFree(p); };
+    if (!dev && n) {
+        ovs_route_out* o; K160* k = nullptr; uint32_t* r; uint32_t* f; bool ow;
+        ovs_status st = to_device(c, reinterpret_cast<const ovs_route_out*>(out), n, false, &o, &ow);
+        if (st != OVS_OK) return st;
+        owned.push_back(o);
+        st = to_device(c, src, n, false, &r, &ow);
+        if (st != OVS_OK) { cleanup(); return st; }
+        owned.push_back(r);
+        st = to_device(c, siblings, n * (uint64_t)siblings_stride, false, &f, &ow);
+        if (st != OVS_OK) { cleanup(); return st; }
+        owned.push_back(f);
+        if (lookup_node_ids) {
+            st = to_device(c, reinterpret_cast<const K160*>(keys), n, false, &k, &ow);
+            if (st != OVS_OK) { cleanup(); return st; }
+            owned.push_back(k);
+        }
+        dout = o; dk = k; ds = r; dsib = f;
+    }
+    StatsDev* S = nullptr; uint32_t* counts = nullptr; double* partial = nullptr; double* result = nullptr;
+    const bool okm = hipMalloc(&S, sizeof(StatsDev)) == hipSuccess &&
+                     hipMalloc(&counts, sizeof(uint32_t) * 3 * c->n) == hipSuccess &&
+                     hipMalloc(&partial, sizeof(double) * STATS_NODE_BLOCKS * NSTAT * 5) == hipSuccess &&
+                     hipMalloc(&result, sizeof(double) * NSTAT * 5) == hipSuccess;
+    owned.push_back(S); owned.push_back(counts); owned.push_back(partial); owned.push_back(result);
+    if (!okm) { cleanup(); return fail(c, OVS_ENOMEM, "statistics scratch allocation failed"); }
+    const int rates = measured_time_s >= 0.1;      // GlobalStatistics::MIN_MEASURED (KBRTestApp.cc:502)
+    hipError_t e = launch_stats(dout, dk, ds, c->recs, n, (uint32_t)c->n, lookup_node_ids, measured_time_s, 0, rates,
+                                S, counts, partial, result, c->num_cu, s, dsib ? dsib : src,
+                                (uint64_t)siblings_stride);
+    StatsDev h{};
+    double r[NSTAT * 5];
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, S, sizeof h, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(r, result, sizeof r, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    cleanup();
+    if (e != hipSuccess) return hip_fail(c, e, "statistics kernels");
+
+    ovs_kbrtest_lookup_stats& o = *stats;
+    std::memset(&o, 0, sizeof o);
+    o.num_sent = n;
+    o.num_success = h.delivered;
+    o.num_failed = h.dropped;
+    o.num_invalid = h.failed;
+    o.hop_count_sum = h.hop_sum;
+    o.failed_hop_count_sum = h.fhop_sum;
+    o.success_latency_sum_ns = (int64_t)h.lat_sum;
+    if (h.delivered) {
+        o.hop_count_min = (uint32_t)h.hop_min;
+        o.hop_count_max = (uint32_t)h.hop_max;
+        o.success_latency_min_ns = (int64_t)h.lat_min;
+        o.success_latency_max_ns = (int64_t)h.lat_max;
+        o.hop_count_mean = (double)h.hop_sum / (double)h.delivered;
+        o.success_latency_mean_s = ((double)h.lat_sum / (double)h.delivered) * 1e-9;
+    }
+    if (h.dropped) o.failed_hop_count_mean = (double)h.fhop_sum / (double)h.dropped;
+    if (n) o.total_latency_mean_s = ((double)h.lat_sum * 1e-9 + (double)h.dropped * failure_latency_s) / (double)n;
+    for (int i = 0; i < 8; ++i) o.status_count[i] = h.status[i];
+    for (int i = 0; i < 64; ++i) o.hop_hist[i] = h.hist[i];
+    const int slot[3] = {0, 2, 4};
+    ovs_stddev* sd[3] = {&o.successful_lookups_per_s, &o.failed_lookups_per_s, &o.success_ratio};
+    for (int q = 0; q < 3; ++q) {
+        const int k = slot[q];
+        const double sum = r[k * 5 + 0], sq = r[k * 5 + 1];
+        uint64_t cnt;
+        std::memcpy(&cnt, &r[k * 5 + 4], sizeof cnt);
+        ovs_stddev& d = *sd[q];
+        d.count = cnt;
+        if (!cnt) continue;
+        d.mean = sum / (double)cnt;
+        double var = 0.0;
+        if (cnt > 1) {
+            var = (sq - sum * sum / (double)cnt) / (double)(cnt - 1);
+            if (var < 0) var = 0;
+        }
+        d.stddev = std::sqrt(var);
+        d.min = r[k * 5 + 2];
+        d.max = r[k * 5 + 3];
+    }
+    return OVS_OK;
+}
+
 ovs_status ovs_sync(ovs_ctx* c)
 {
     if (!c) return OVS_EINVAL;

@@ -52,6 +52,11 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
     return v;
 }
 
+// LK = false: one-way test over ovs_route_out (delivered / dropped / failed lookups).
+// LK = true: lookup test over ovs_lookup_out (same 16 B slot: num_siblings, hops, status,
+// is_valid, latency) and the first column of the sibling vectors: delivered = numLookupSuccess,
+// dropped = numLookupFailed, failed = the !isValid part of it (KBRTestApp.cc:331-371).
+template <bool LK>
 __global__ __launch_bounds__(256) void k_stats_lookups(const ovs_route_out* __restrict__ out,
                                                        const K160* __restrict__ keys,
                                                        const uint32_t* __restrict__ src,
@@ -59,7 +64,8 @@ __global__ __launch_bounds__(256) void k_stats_lookups(const ovs_route_out* __re
                                                        int lookup_node_ids, StatsDev* __restrict__ S,
                                                        uint32_t* __restrict__ node_sent,
                                                        uint32_t* __restrict__ node_deliv,
-                                                       uint32_t* __restrict__ node_drop)
+                                                       uint32_t* __restrict__ node_drop,
+                                                       const uint32_t* __restrict__ first, uint64_t first_stride)
 {
     __shared__ uint32_t hist[64];
     __shared__ uint32_t stat[8];
@@ -67,7 +73,7 @@ __global__ __launch_bounds__(256) void k_stats_lookups(const ovs_route_out* __re
     if (threadIdx.x < 8) stat[threadIdx.x] = 0;
     __syncthreads();
 
-    uint64_t deliv = 0, drop = 0, failed = 0, hops = 0, lat = 0;
+    uint64_t deliv = 0, drop = 0, failed = 0, hops = 0, lat = 0, fhops = 0;
     uint64_t hmin = ~0ull, hmax = 0, lmin = ~0ull, lmax = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -76,6 +82,42 @@ __global__ __launch_bounds__(256) void k_stats_lookups(const ovs_route_out* __re
         const bool valid_src = s < nnodes;
         atomicAdd(&stat[o.status & 7], 1u);
         if (valid_src) atomicAdd(&node_sent[s], 1u);
+        if constexpr (LK) {
+            // KBRTestApp::handleLookupResponse: isValid && (!lookupNodeIds || (siblings non-empty,
+            // siblings[0].key == key, siblings[0] == destAddr)) -- unique IDs: the node owning key
+            const bool valid = o.one_way_hops != 0;
+            bool ok = valid;
+            if (ok && lookup_node_ids) {
+                const uint32_t f = o.responsible > 0 ? first[i * first_stride] : NONE;
+                if (f < nnodes) {
+                    const KeyRec r = load_rec(recs, f);
+                    const K160 k = keys[i];
+                    ok = r.w[0] == k.w[0] && r.w[1] == k.w[1] && r.w[2] == k.w[2] && r.w[3] == k.w[3] &&
+                         r.w[4] == k.w[4];
+                } else {
+                    ok = false;
+                }
+            }
+            if (!ok) {
+                ++drop;
+                failed += valid ? 0 : 1;
+                fhops += o.hops;                  // "Failed Lookup Hop Count"
+                if (valid_src) atomicAdd(&node_drop[s], 1u);
+                continue;
+            }
+            ++deliv;
+            if (valid_src) atomicAdd(&node_deliv[s], 1u);
+            const uint64_t h = o.hops;          // "Lookup Hop Count"
+            const uint64_t l = (uint64_t)o.latency_ns;   // "Lookup Success Latency"
+            hops += h;
+            lat += l;
+            hmin = h < hmin ? h : hmin;
+            hmax = h > hmax ? h : hmax;
+            lmin = l < lmin ? l : lmin;
+            lmax = l > lmax ? l : lmax;
+            atomicAdd(&hist[h < 63 ? h : 63], 1u);
+            continue;
+        }
         if (o.status != OVS_LOOKUP_OK) {
             ++failed;
             continue;
@@ -113,6 +155,7 @@ __global__ __launch_bounds__(256) void k_stats_lookups(const ovs_route_out* __re
     failed = wave_sum_u64(failed);
     hops = wave_sum_u64(hops);
     lat = wave_sum_u64(lat);
+    fhops = wave_sum_u64(fhops);
     hmin = wave_min_u64(hmin);
     hmax = wave_max_u64(hmax);
     lmin = wave_min_u64(lmin);
@@ -123,6 +166,7 @@ __global__ __launch_bounds__(256) void k_stats_lookups(const ovs_route_out* __re
         if (failed) atomicAdd(&S->failed, failed);
         if (hops) atomicAdd(&S->hop_sum, hops);
         if (lat) atomicAdd(&S->lat_sum, lat);
+        if (fhops) atomicAdd(&S->fhop_sum, fhops);
         if (hmin != ~0ull) {
             atomicMin(&S->hop_min, hmin);
             atomicMax(&S->hop_max, hmax);
@@ -214,7 +258,7 @@ __device__ void block_reduce_store(Acc (&a)[NSTAT], double* __restrict__ dst)
 __global__ __launch_bounds__(256) void k_stats_nodes(const uint32_t* __restrict__ node_sent,
                                                      const uint32_t* __restrict__ node_deliv,
                                                      const uint32_t* __restrict__ node_drop, uint32_t nnodes,
-                                                     double time_s, uint64_t msg_bytes, int rates,
+                                                     double time_s, uint64_t msg_bytes, int rates, int lk,
                                                      double* __restrict__ partial)
 {
     Acc a[NSTAT];
@@ -223,7 +267,13 @@ __global__ __launch_bounds__(256) void k_stats_nodes(const uint32_t* __restrict_
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nnodes; i += stride) {
         const uint32_t s = node_sent[i], d = node_deliv[i], r = node_drop[i];
-        if (rates) {
+        if (rates && lk) {
+            // KBRTestApp::finishApp, kbrLookupTest (KBRTestApp.cc:546-557): Successful Lookups/s,
+            // Failed Lookups/s, Lookup Success Ratio
+            acc_add(a[0], __ddiv_rn((double)d, time_s));
+            acc_add(a[2], __ddiv_rn((double)r, time_s));
+            if (s > 0) acc_add(a[4], (double)__fdiv_rn((float)d, (float)s));
+        } else if (rates) {
             // KBRTestApp::finishApp (KBRTestApp.cc:503-512): numDelivered / time etc.
             // (the reference divides long / simtime_t; as doubles here)
             acc_add(a[0], __ddiv_rn((double)d, time_s));
@@ -258,8 +308,9 @@ __global__ __launch_bounds__(256) void k_stats_final(const double* __restrict__ 
 hipError_t launch_stats(const ovs_route_out* out, const K160* keys, const uint32_t* src, const KeyRec* recs,
                         uint64_t n, uint32_t nnodes, int lookup_node_ids, double time_s, uint64_t msg_bytes,
                         int rates, StatsDev* S, uint32_t* node_counts, double* partial, double* result,
-                        int num_cu, hipStream_t st)
+                        int num_cu, hipStream_t st, const uint32_t* first, uint64_t first_stride)
 {
+    const bool lk = first != nullptr;
     uint32_t* node_sent = node_counts;
     uint32_t* node_deliv = node_counts + nnodes;
     uint32_t* node_drop = node_counts + 2 * (uint64_t)nnodes;
@@ -274,13 +325,17 @@ hipError_t launch_stats(const ovs_route_out* out, const K160* keys, const uint32
         uint64_t blocks = (n + 255) / 256;
         const uint64_t cap = (uint64_t)num_cu * 8;
         if (blocks > cap) blocks = cap;
-        hipLaunchKernelGGL(k_stats_lookups, dim3((unsigned)blocks), dim3(256), 0, st, out, keys, src, recs, n, nnodes,
-                           lookup_node_ids, S, node_sent, node_deliv, node_drop);
+        if (lk)
+            hipLaunchKernelGGL(k_stats_lookups<true>, dim3((unsigned)blocks), dim3(256), 0, st, out, keys, src, recs, n,
+                               nnodes, lookup_node_ids, S, node_sent, node_deliv, node_drop, first, first_stride);
+        else
+            hipLaunchKernelGGL(k_stats_lookups<false>, dim3((unsigned)blocks), dim3(256), 0, st, out, keys, src, recs, n,
+                               nnodes, lookup_node_ids, S, node_sent, node_deliv, node_drop, first, first_stride);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_stats_nodes, dim3(STATS_NODE_BLOCKS), dim3(256), 0, st, node_sent, node_deliv, node_drop,
-                       nnodes, time_s, msg_bytes, rates, partial);
+                       nnodes, time_s, msg_bytes, rates, lk ? 1 : 0, partial);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(256), 0, st, partial, STATS_NODE_BLOCKS, result);

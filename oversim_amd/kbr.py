@@ -172,6 +172,8 @@ def lib() -> C.CDLL:
         "ovs_kbrtest_stats_batch": ([vp, vp, vp, vp, u64, C.c_double, i32, vp, u32, vp], C.c_int),
         "ovs_chord_fix_fingers": ([vp, vp, u64, vp], C.c_int),
         "ovs_lookup_batch": ([vp, vp, vp, u64, i32, vp, vp, u32, vp], C.c_int),
+        "ovs_kbrtest_lookup_stats_batch": ([vp, vp, vp, i32, vp, vp, u64, C.c_double, i32, C.c_double, vp, u32, vp],
+                                           C.c_int),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -200,6 +202,27 @@ def key_from_int(x: int) -> np.ndarray:
 
 def key_to_int(w) -> int:
     return sum(int(w[i]) << (32 * i) for i in range(5))
+
+
+class KbrTestLookupStats(C.Structure):
+    """ovs_kbrtest_lookup_stats: KBRTestApp lookup-test statistics of a batch (KBRTestApp.cc:331-371, 546-557)."""
+
+    _fields_ = [
+        ("num_sent", C.c_uint64), ("num_success", C.c_uint64), ("num_failed", C.c_uint64),
+        ("num_invalid", C.c_uint64), ("hop_count_sum", C.c_uint64), ("failed_hop_count_sum", C.c_uint64),
+        ("success_latency_sum_ns", C.c_int64), ("hop_count_min", C.c_uint32), ("hop_count_max", C.c_uint32),
+        ("success_latency_min_ns", C.c_int64), ("success_latency_max_ns", C.c_int64),
+        ("hop_count_mean", C.c_double), ("failed_hop_count_mean", C.c_double),
+        ("success_latency_mean_s", C.c_double), ("total_latency_mean_s", C.c_double),
+        ("status_count", C.c_uint64 * 8), ("hop_hist", C.c_uint64 * 64),
+        ("successful_lookups_per_s", StdDev), ("failed_lookups_per_s", StdDev), ("success_ratio", StdDev),
+    ]
+
+    STDDEV_NAMES = {
+        "successful_lookups_per_s": "KBRTestApp: Successful Lookups/s",
+        "failed_lookups_per_s": "KBRTestApp: Failed Lookups/s",
+        "success_ratio": "KBRTestApp: Lookup Success Ratio",
+    }
 
 
 class KbrEngine:
@@ -403,6 +426,22 @@ class KbrEngine:
         self._chk(self._L.ovs_kbrtest_stats_batch(self._h, _ptr(out), _ptr(keys), _ptr(src), len(out),
                                                   float(measured_time_s), int(bool(lookupNodeIds)), C.byref(st),
                                                   0, None), "ovs_kbrtest_stats_batch")
+        return st
+
+    def kbrtest_lookup_stats(self, result: dict, keys, src, measured_time_s: float, lookupNodeIds: bool = True,
+                             failureLatency: float = 10.0) -> KbrTestLookupStats:
+        """Reduce lookupCall() results to the KBRTestApp lookup-test statistics on the device."""
+        out = np.empty(len(result["hops"]), dtype=LOOKUP_OUT_DTYPE)
+        for f in LOOKUP_OUT_DTYPE.names:
+            out[f] = result[f]
+        sib = np.ascontiguousarray(result["siblings"], dtype=np.uint32)
+        keys = keys_array(keys)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        st = KbrTestLookupStats()
+        self._chk(self._L.ovs_kbrtest_lookup_stats_batch(self._h, _ptr(out), _ptr(sib), sib.shape[1], _ptr(keys),
+                                                         _ptr(src), len(out), float(measured_time_s),
+                                                         int(bool(lookupNodeIds)), float(failureLatency),
+                                                         C.byref(st), 0, None), "ovs_kbrtest_lookup_stats_batch")
         return st
 
     def kbrtest_stats_device(self, out_ptr: int, keys_ptr: int, src_ptr: int, n: int, measured_time_s: float,

@@ -19,17 +19,22 @@ from __future__ import annotations
 import datetime as _dt
 from pathlib import Path
 
-from .kbr import KbrTestStats
+from .kbr import KbrTestLookupStats, KbrTestStats
 
 GLOBAL_STATS_MODULE = "SimpleUnderlayNetwork.globalObserver.globalStatistics"
 
 
-def scalars(st: KbrTestStats, sim_time_s: float, output_stddev: bool = False,
-            output_min_max: bool = False) -> list[tuple[str, float]]:
-    """(name, value) pairs in finalizeStatistics order."""
+def scalars(st: KbrTestStats | None, sim_time_s: float, output_stddev: bool = False,
+            output_min_max: bool = False, lookup: KbrTestLookupStats | None = None) -> list[tuple[str, float]]:
+    """(name, value) pairs in finalizeStatistics order: the one-way test (st) and/or the lookup
+    test (lookup) of the same run."""
     out: list[tuple[str, float]] = [("GlobalStatistics: Simulation Time", float(sim_time_s))]
-    sd = sorted((name, getattr(st, field)) for field, name in KbrTestStats.STDDEV_NAMES.items()
-                if getattr(st, field).count > 0)          # addStdDev only called when collected
+    sd = []
+    for obj, names in ((st, KbrTestStats.STDDEV_NAMES), (lookup, KbrTestLookupStats.STDDEV_NAMES)):
+        if obj is not None:
+            sd += [(name, getattr(obj, field)) for field, name in names.items()
+                   if getattr(obj, field).count > 0]       # addStdDev only called when collected
+    sd.sort(key=lambda t: t[0])
     for name, s in sd:                                    # std::map<std::string, cStdDev*> order
         out.append((name + ".mean", s.mean))
         if output_stddev:
@@ -37,10 +42,20 @@ def scalars(st: KbrTestStats, sim_time_s: float, output_stddev: bool = False,
         if output_min_max:
             out.append((name + ".min", s.min))
             out.append((name + ".max", s.max))
-    if st.num_delivered > 0:                              # recordOutVector only on evaluateData
-        vec = sorted([("KBRTestApp: One-way Hop Count", st.hop_count_mean),
-                      ("KBRTestApp: One-way Latency", st.latency_mean_s)])
-        out.extend(("Vector: " + n + ".mean", v) for n, v in vec)
+    vec = []
+    if st is not None and st.num_delivered > 0:           # recordOutVector only on evaluateData
+        vec += [("KBRTestApp: One-way Hop Count", st.hop_count_mean),
+                ("KBRTestApp: One-way Latency", st.latency_mean_s)]
+    if lookup is not None:                                # handleLookupResponse (KBRTestApp.cc:341-369)
+        if lookup.num_success > 0:
+            vec += [("KBRTestApp: Lookup Success Latency", lookup.success_latency_mean_s),
+                    ("KBRTestApp: Lookup Hop Count", lookup.hop_count_mean)]
+        if lookup.num_failed > 0:
+            vec += [("KBRTestApp: Failed Lookup Hop Count", lookup.failed_hop_count_mean)]
+        if lookup.num_sent > 0:
+            vec += [("KBRTestApp: Lookup Total Latency", lookup.total_latency_mean_s)]
+    vec.sort(key=lambda t: t[0])
+    out.extend(("Vector: " + n + ".mean", v) for n, v in vec)
     return out
 
 
@@ -48,9 +63,10 @@ def _q(s: str) -> str:
     return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"' if (" " in s or '"' in s) else s
 
 
-def write_sca(path: str | Path, st: KbrTestStats, sim_time_s: float, config: str = "General",
+def write_sca(path: str | Path, st: KbrTestStats | None, sim_time_s: float, config: str = "General",
               run_number: int = 0, network: str = "SimpleUnderlayNetwork", output_stddev: bool = False,
-              output_min_max: bool = False, module: str = GLOBAL_STATS_MODULE) -> Path:
+              output_min_max: bool = False, module: str = GLOBAL_STATS_MODULE,
+              lookup: KbrTestLookupStats | None = None) -> Path:
     """Write an OMNeT++ 4 scalar file with the batch's KBRTestApp statistics."""
     path = Path(path)
     now = _dt.datetime.now(_dt.timezone.utc).strftime("%Y%m%d-%H:%M:%S")
@@ -58,7 +74,7 @@ def write_sca(path: str | Path, st: KbrTestStats, sim_time_s: float, config: str
     lines = ["version 2", f"run {run_id}", f"attr configname {config}", f"attr datetime {now}",
              f"attr experiment {config}", "attr measurement \"\"", f"attr network {network}",
              "attr replication #0", f"attr runnumber {run_number}", ""]
-    for name, v in scalars(st, sim_time_s, output_stddev, output_min_max):
+    for name, v in scalars(st, sim_time_s, output_stddev, output_min_max, lookup):
         lines.append(f"scalar {module} \t{_q(name)} \t{v!r}")
     path.write_text("\n".join(lines) + "\n")
     return path

@@ -79,6 +79,8 @@ def lib() -> C.CDLL:
             ("orc_kbrtest_stats", [vp, vp, vp, vp, u64, C.c_double, C.c_int, i32, vp], None),
             ("orc_chord_fix_fingers", [vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.c_int], u64),
             ("orc_lookup_batch", [vp, vp, vp, u64, C.c_int, vp, vp, C.c_int], C.c_int),
+            ("orc_kbrtest_lookup_stats", [vp, vp, vp, C.c_int, vp, vp, u64, C.c_double, C.c_int, C.c_double, vp],
+             None),
         ]:
             f = getattr(L, name)
             f.argtypes = args
@@ -97,6 +99,16 @@ class OrcKbrTestResult(C.Structure):
                 ("num_lookup_failed", C.c_uint64), ("hop_count_sum", C.c_uint64), ("latency_sum_ns", C.c_int64),
                 ("hop_count_mean", C.c_double), ("latency_mean_s", C.c_double), ("sd", OrcStdDev * 5)]
 
+
+class OrcKbrTestLookupResult(C.Structure):
+    _fields_ = [("num_sent", C.c_uint64), ("num_success", C.c_uint64), ("num_failed", C.c_uint64),
+                ("num_invalid", C.c_uint64), ("hop_count_sum", C.c_uint64), ("failed_hop_count_sum", C.c_uint64),
+                ("success_latency_sum_ns", C.c_int64), ("hop_count_mean", C.c_double),
+                ("failed_hop_count_mean", C.c_double), ("success_latency_mean_s", C.c_double),
+                ("total_latency_mean_s", C.c_double), ("sd", OrcStdDev * 3)]
+
+
+LOOKUP_SD_FIELDS = ("successful_lookups_per_s", "failed_lookups_per_s", "success_ratio")
 
 SD_FIELDS = ("delivered_msgs_per_s", "delivered_bytes_per_s", "dropped_msgs_per_s", "dropped_bytes_per_s",
              "delivery_ratio")
@@ -194,6 +206,24 @@ class OracleNet:
                                 int(bool(lookupNodeIds)), int(testMsgSize), C.byref(st))
         d = {f: getattr(st, f) for f, _ in OrcKbrTestResult._fields_ if f != "sd"}
         for i, name in enumerate(SD_FIELDS):
+            s = st.sd[i]
+            d[name] = {"count": s.count, "mean": s.mean, "stddev": s.stddev, "min": s.min, "max": s.max}
+        return d
+
+    def kbrtest_lookup_stats(self, result: dict, keys, src, measured_time_s: float, lookupNodeIds: bool = True,
+                             failureLatency: float = 10.0) -> dict:
+        out = np.empty(len(result["hops"]), dtype=LOOKUP_DTYPE)
+        for f in LOOKUP_DTYPE.names:
+            out[f] = result[f]
+        sib = np.ascontiguousarray(result["siblings"], dtype=np.uint32)
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        st = OrcKbrTestLookupResult()
+        lib().orc_kbrtest_lookup_stats(self._h, _p(out), _p(sib), sib.shape[1], _p(keys), _p(src), len(out),
+                                       float(measured_time_s), int(bool(lookupNodeIds)), float(failureLatency),
+                                       C.byref(st))
+        d = {f: getattr(st, f) for f, _ in OrcKbrTestLookupResult._fields_ if f != "sd"}
+        for i, name in enumerate(LOOKUP_SD_FIELDS):
             s = st.sd[i]
             d[name] = {"count": s.count, "mean": s.mean, "stddev": s.stddev, "min": s.min, "max": s.max}
         return d

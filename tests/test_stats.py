@@ -169,3 +169,118 @@ def test_gpu_stats_kademlia_routes(engine):
 
 def test_route_out_dtype_matches_abi():
     assert ROUTE_OUT_DTYPE.itemsize == 16
+
+
+# ---------------------------------------------------------------- lookup test (kbrLookupTest)
+
+def _crafted_lookups():
+    """8 LookupResponses from 3 sources: valid + right node, valid + wrong first sibling, invalid."""
+    g = np.load(GOLD / "chord_n9.npz")
+    ids, xy = g["ids"], g["xy"]
+    src = np.array([0, 0, 0, 1, 1, 2, 2, 2], np.uint32)
+    keys = ids[[3, 4, 5, 6, 7, 8, 1, 2]].copy()
+    first = np.array([3, 4, 0, 6, 0xFFFFFFFF, 8, 1, 5], np.uint32)      # #2 and #7 wrong, #4 invalid
+    sib = np.full((8, 3), 0xFFFFFFFF, np.uint32)
+    sib[:, 0] = first
+    sib[[0, 1, 2, 3, 5, 6, 7], 1] = 7
+    nsib = np.where(first == 0xFFFFFFFF, 0, 2).astype(np.uint32)
+    valid = (first != 0xFFFFFFFF).astype(np.uint8)
+    hops = np.array([2, 3, 1, 4, 6, 2, 5, 1], np.uint16)
+    lat = np.array([100_000_000, 250_000_000, 1, 3_000_000_000, -1, 7, 999, 5], np.int64)
+    res = {"num_siblings": nsib, "hops": hops, "status": np.where(valid == 1, 0, 3).astype(np.uint8),
+           "is_valid": valid, "latency_ns": lat, "siblings": sib}
+    return ids, xy, keys, src, res
+
+
+def test_oracle_lookup_stats_hand_counted():
+    ids, xy, keys, src, res = _crafted_lookups()
+    o = OracleNet("chord", ids, xy, chord_params())
+    st = o.kbrtest_lookup_stats(res, keys, src, 2.0, lookupNodeIds=True, failureLatency=10.0)
+    ok = [0, 1, 3, 5, 6]
+    assert (st["num_sent"], st["num_success"], st["num_failed"], st["num_invalid"]) == (8, 5, 3, 1)
+    assert st["hop_count_sum"] == sum(int(res["hops"][i]) for i in ok)
+    assert st["failed_hop_count_sum"] == 1 + 6 + 1
+    assert st["success_latency_sum_ns"] == sum(int(res["latency_ns"][i]) for i in ok)
+    lat_s = [res["latency_ns"][i] * 1e-9 for i in ok]
+    assert st["success_latency_mean_s"] == pytest.approx(sum(lat_s) / 5, rel=1e-12)
+    assert st["total_latency_mean_s"] == pytest.approx((sum(lat_s) + 3 * 10.0) / 8, rel=1e-12)
+    assert st["failed_hop_count_mean"] == pytest.approx(8 / 3, rel=1e-15)
+    per_node_succ = [2, 1, 2] + [0] * 6
+    per_node_fail = [1, 1, 1] + [0] * 6
+    exp = {"successful_lookups_per_s": _cstddev([v / 2.0 for v in per_node_succ]),
+           "failed_lookups_per_s": _cstddev([v / 2.0 for v in per_node_fail]),
+           "success_ratio": _cstddev([float(np.float32(2) / np.float32(3)), 0.5, float(np.float32(2) / np.float32(3))])}
+    for f in exp:
+        for k in ("count", "mean", "stddev", "min", "max"):
+            assert st[f][k] == pytest.approx(exp[f][k], rel=1e-12, abs=1e-15), (f, k)
+    # lookupNodeIds = false: every valid response counts
+    st2 = o.kbrtest_lookup_stats(res, keys, src, 2.0, lookupNodeIds=False)
+    assert (st2["num_success"], st2["num_failed"], st2["num_invalid"]) == (7, 1, 1)
+
+
+def test_sca_lookup_scalars(tmp_path):
+    from oversim_amd.kbr import KbrTestLookupStats
+    from oversim_amd.stats import read_sca, write_sca
+    lk = KbrTestLookupStats()
+    lk.num_sent, lk.num_success, lk.num_failed = 10, 9, 1
+    lk.hop_count_mean, lk.success_latency_mean_s, lk.total_latency_mean_s = 4.5, 0.25, 1.225
+    lk.failed_hop_count_mean = 7.0
+    lk.success_ratio.count, lk.success_ratio.mean = 100, 0.9
+    sc = read_sca(write_sca(tmp_path / "l.sca", None, 100.0, lookup=lk))
+    assert sc["Vector: KBRTestApp: Lookup Hop Count.mean"] == 4.5
+    assert sc["Vector: KBRTestApp: Lookup Total Latency.mean"] == 1.225
+    assert sc["Vector: KBRTestApp: Failed Lookup Hop Count.mean"] == 7.0
+    assert sc["KBRTestApp: Lookup Success Ratio.mean"] == 0.9
+    assert "KBRTestApp: Successful Lookups/s.mean" not in sc
+
+
+LK_INT = ("num_sent", "num_success", "num_failed", "num_invalid", "hop_count_sum", "failed_hop_count_sum",
+          "success_latency_sum_ns")
+
+
+def _check_lookup(gpu, orc):
+    from oracle_lib import LOOKUP_SD_FIELDS
+    for f in LK_INT:
+        assert int(getattr(gpu, f)) == int(orc[f]), f
+    for f in ("hop_count_mean", "failed_hop_count_mean", "success_latency_mean_s", "total_latency_mean_s"):
+        assert getattr(gpu, f) == pytest.approx(orc[f], rel=1e-12), f
+    for f in LOOKUP_SD_FIELDS:
+        g, o = getattr(gpu, f), orc[f]
+        assert g.count == o["count"], f
+        for k in ("mean", "stddev", "min", "max"):
+            assert getattr(g, k) == pytest.approx(o[k], rel=1e-12, abs=1e-12), (f, k)
+
+
+@pytest.mark.gpu
+def test_gpu_lookup_stats_crafted(engine):
+    from oversim_amd import Params
+    ids, xy, keys, src, res = _crafted_lookups()
+    engine.set_params(Params.chord())
+    engine.chord_load(ids, xy)
+    o = OracleNet("chord", ids, xy, chord_params())
+    for T, nid in ((2.0, True), (2.0, False), (0.05, True)):
+        _check_lookup(engine.kbrtest_lookup_stats(res, keys, src, T, lookupNodeIds=nid),
+                      o.kbrtest_lookup_stats(res, keys, src, T, lookupNodeIds=nid))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlay", ["chord", "kademlia"])
+def test_gpu_lookup_stats_real_lookups(engine, overlay):
+    from oversim_amd import Params
+    net = W.population(15000, 51)
+    keys, src = W.lookups(net.ids, 100_000, 52, node_ids=True)
+    hcm = 4 if overlay == "chord" else 3         # part of the batch fails: every branch is exercised
+    if overlay == "chord":
+        engine.set_params(Params.chord().replace(hopCountMax=hcm))
+        engine.chord_load(net.ids, net.xy)
+        o = OracleNet("chord", net.ids, net.xy, chord_params(hopCountMax=hcm))
+    else:
+        engine.set_params(Params.kademlia().replace(hopCountMax=hcm))
+        engine.kad_load(net.ids, net.xy)
+        o = OracleNet("kademlia", net.ids, net.xy, kad_params(hopCountMax=hcm))
+    r = engine.lookupCall(keys, src)
+    ref = o.lookup_call(keys, src)
+    assert np.array_equal(r["siblings"], ref["siblings"])
+    g = engine.kbrtest_lookup_stats(r, keys, src, 500.0)
+    _check_lookup(g, o.kbrtest_lookup_stats(r, keys, src, 500.0))
+    assert g.num_failed > 0 and g.num_success > 0
