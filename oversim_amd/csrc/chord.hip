@@ -471,7 +471,8 @@ struct LaneIO {
     uint64_t n, chunk;
 };
 
-template <bool REC, bool RECORD, bool SHARD>
+// LKC: a LookupCall batch (ovs_lookup_batch): the responsible node's larger answer, no route message
+template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
 __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
 {
     const int lane = threadIdx.x & 63;
@@ -700,7 +701,7 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 } else {
                     // FindNodeCall S->cur, FindNodeResponse cur->S (one NodeHandle)
                     const int64_t cd = coord_ns(sx, sy, A.x, A.y, DC.round);
-                    const int64_t rtt = DC.msgCall + (asib ? DC.msgRespSib : DC.msgResp1) + 2 * cd;
+                    const int64_t rtt = DC.msgCall + ((LKC && asib) ? DC.msgRespSib : DC.msgResp1) + 2 * cd;
                     if (rtt >= DC.rpcTimeout) {
                         fin = true;
                         status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                     o.responsible = R;
                     o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
                     // sendRouteMessage to result[0] (BaseOverlay.cc:1107-1146); 0 delay to self
-                    o.latency_ns = t + ((R != S && !DC.lookupCall) ? DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round) : 0);
+                    o.latency_ns = t + ((R != S && !LKC) ? DC.msgRoute + coord_ns(sx, sy, A.x, A.y, DC.round) : 0);
                 } else {
                     o.hops = (uint16_t)hops;
                     o.responsible = NONE;
@@ -995,14 +996,15 @@ static uint64_t persistent_chunk(Kern k, int* cache, uint64_t n, int num_cu, uin
     return chunk;
 }
 
-template <bool REC, bool RECORD, bool SHARD>
+template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
 static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC, LaneIO io,
                                int num_cu, hipStream_t s)
 {
     static int bpc = 0;
     uint64_t blocks = 0;
-    io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD>, &bpc, io.n, num_cu, &blocks);
-    hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC, io);
+    io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD, LKC>, &bpc, io.n, num_cu, &blocks);
+    hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD, LKC>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC,
+                       io);
     return hipGetLastError();
 }
 
@@ -1014,6 +1016,10 @@ static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, 
     if constexpr (IDEAL) {
         LaneIO io{};
         io.qkeys = qkeys; io.qsrc = qsrc; io.out = out; io.hopseq = hopseq; io.n = nq;
+        if constexpr (!REC && !RECORD) {
+            if (DC.lookupCall) return lanes_launch<false, false, false, true>(V, DC, LC, io, num_cu, s);
+        }
+        if (DC.lookupCall) return hipErrorNotSupported;
         return lanes_launch<REC, RECORD, false>(V, DC, LC, io, num_cu, s);
     } else {
         static int bpc = 0;
