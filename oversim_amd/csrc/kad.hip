@@ -220,7 +220,7 @@ struct SendNothing {
 };
 
 // the responder's findNode evaluated in place (all tables on this GPU)
-template <bool EX>
+template <bool EX, bool LK>
 struct LocalFindNode {
     const KadView& V;
     const K160& K;
@@ -230,7 +230,7 @@ struct LocalFindNode {
     __device__ __forceinline__ void fill(int, uint32_t r, const RespGeo& g, bool sb, SVec<8>& res) const
     {
         Blk8 b;
-        const int n = kad_find_node_blk<EX>(V, r, g, K, redundant, sb, b, numSiblings);
+        const int n = kad_find_node_blk<EX>(V, r, g, K, redundant, sb, b, LK ? numSiblings : 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
         res.n = n;
@@ -249,7 +249,7 @@ struct HopRecorder {
     }
 };
 
-template <int A, bool RECORD, bool EX>
+template <int A, bool RECORD, bool EX, bool LK>
 __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, KadLC LC, const K160* __restrict__ qkeys,
                                                    const uint32_t* __restrict__ qsrc, uint64_t nq, uint64_t chunk,
                                                    ovs_route_out* __restrict__ out, uint32_t* __restrict__ hopseq,
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
                 q = mine;
                 active = true;
                 kad_lookup_init(L, qkeys[q], qsrc[q], V.xy);
-                kad_lookup_start<A, EX>(L, V, DC, LC, res, on);
+                kad_lookup_start<A, EX, LK>(L, V, DC, LC, res, on);
             }
             cursor += (uint64_t)__popcll(need);
         }
@@ -283,15 +283,15 @@ __global__ __launch_bounds__(256) void k_kad_route(KadView V, DelayConsts DC, Ka
         if (!active) continue;
 
         if (!kad_lookup_done(L)) {
-            const LocalFindNode<EX> fn{V, L.K, LC.redundant, LC.numSiblings};
+            const LocalFindNode<EX, LK> fn{V, L.K, LC.redundant, LC.numSiblings};
             const HopRecorder<RECORD> rec{hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
-            kad_lookup_event<A, EX>(L, V, DC, LC, res, fn, on, rec);
+            kad_lookup_event<A, EX, LK>(L, V, DC, LC, res, fn, on, rec);
         }
         if (kad_lookup_done(L)) {
             const ovs_route_out o = kad_lookup_output(L, V, DC, LC);
             out[q] = o;
             if (rpcs_out) rpcs_out[q] = L.nsent;
-            if (sib_out) {
+            if (LK) {
                 // LookupCall: the siblings vector = the answering response's nodes (start(): the
                 // local findNode result), pushed in order up to numSiblings (IterativeLookup.cc:406-449)
                 const bool ok = o.status == OVS_LOOKUP_OK;
@@ -418,28 +418,29 @@ hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_
     return e;
 }
 
-template <int A, bool RECORD, bool EX>
+template <int A, bool RECORD, bool EX, bool LK>
 static int kad_blocks_per_cu()
 {
     static int bpc = 0;
     if (bpc == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX>, 256, 0) != hipSuccess || b < 1) b = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK>, 256, 0) != hipSuccess || b < 1)
+            b = 1;
         bpc = b;
     }
     return bpc;
 }
 
-template <int A, bool RECORD, bool EX>
+template <int A, bool RECORD, bool EX, bool LK>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
                              const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
                              uint32_t* sibs, int num_cu, hipStream_t st)
 {
-    const uint64_t waves = (uint64_t)num_cu * kad_blocks_per_cu<A, RECORD, EX>() * 4;
+    const uint64_t waves = (uint64_t)num_cu * kad_blocks_per_cu<A, RECORD, EX, LK>() * 4;
     uint64_t chunk = (nq + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
     const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX>), dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, st, V, DC, LC,
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK>), dim3((unsigned)((need_waves + 3) / 4)), dim3(256), 0, st, V, DC, LC,
                        qkeys, qsrc, nq, chunk, out, hopseq, rpcs, sibs);
     return hipGetLastError();
 }
@@ -455,8 +456,11 @@ hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, 
     const KadView V = kad_make_view(t, xy, n);
     // strictParallelRpcs: never more than alpha FindNodeCalls in flight (IterativeLookup.cc:1078-1079)
     const int A = P.lookupParallelRpcs;
-#define KLX(a, x) (hopseq ? kad_launch<a, true, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st) \
-                          : kad_launch<a, false, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st))
+    // LookupCall batches (sibs != nullptr) record no hop sequence
+    if (sibs && hopseq) return hipErrorNotSupported;
+#define KLX(a, x) (sibs     ? kad_launch<a, false, x, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st) \
+                   : hopseq ? kad_launch<a, true, x, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st) \
+                            : kad_launch<a, false, x, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st))
 #define KL(a) (t.exact ? KLX(a, true) : KLX(a, false))
     switch (A) {
     case 1: return KL(1);

@@ -530,18 +530,20 @@ __device__ __forceinline__ void kad_lookup_init(KadLookup<A>& L, const K160& K, 
 // FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
 // SimpleNodeEntry::calcDelay with the source's tx queue).  on(slot, x, isTimeout) is told which
 // pending-event slot the call occupies (the sharded path requests x's findNode result there).
-template <int A, class OnSend>
+// LK: a LookupCall batch (numSiblings = LC.numSiblings); otherwise numSiblings = 1 at compile time
+template <int A, bool LK, class OnSend>
 __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                          uint32_t x, const OnSend& on)
 {
     const double2 cxy = V.xy[x];
     const KadRec rr = kad_rec(V.recs, x);
-    const bool sb = kad_is_sibling(V, rr, x, L.K, LC.numSiblings);
+    const int ns = LK ? LC.numSiblings : 1;
+    const bool sb = kad_is_sibling(V, rr, x, L.K, ns);
     const RespGeo rg = resp_geo(rr, L.K);
     const uint32_t geo = (uint32_t)(rg.m + 1) | ((uint32_t)(rg.endIndex + 1) << 8) | (sb ? 0x10000u : 0u);
     // the response carries findNode's result: min(numSiblings, n) nodes when x is sibling,
     // else min(redundant, n)
-    const int rsz = sb ? LC.numSiblings : LC.redundant;
+    const int rsz = sb ? ns : LC.redundant;
     const int csz = rsz < (int)V.n ? rsz : (int)V.n;
     const int64_t cd = coord_ns(L.sx, L.sy, cxy.x, cxy.y, DC.round);
     const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
@@ -577,7 +579,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
 }
 
 // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
-template <int A, class OnSend>
+template <int A, bool LK, class OnSend>
 __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                               int num, const OnSend& on)
 {
@@ -599,39 +601,40 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
         if (!LC.visitOnlyOnce || h != L.S) {
             ++L.pending;
             --num;
-            kad_send(L, V, DC, LC, h, on);
+            kad_send<A, LK>(L, V, DC, LC, h, on);
         }
         L.nh.used |= 1u << e;
     }
     if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
 }
 
-template <int A, class OnSend>
+template <int A, bool LK, class OnSend>
 __device__ __forceinline__ void kad_timeoutlike(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                 const KadLC& LC, const OnSend& on)
 {
     // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
     --L.pending;
     if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
-    else if (LC.newOnTimeout) kad_send_rpcs(L, V, DC, LC, 1, on);
-    else if (L.pending == 0) kad_send_rpcs(L, V, DC, LC, LC.alpha, on);
+    else if (LC.newOnTimeout) kad_send_rpcs<A, LK>(L, V, DC, LC, 1, on);
+    else if (L.pending == 0) kad_send_rpcs<A, LK>(L, V, DC, LC, LC.alpha, on);
 }
 
 // IterativeLookup::start (IterativeLookup.cc:133-244): local findNode at the source
-template <int A, bool EX, class OnSend>
+template <int A, bool EX, bool LK, class OnSend>
 __device__ __forceinline__ void kad_lookup_start(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                  const KadLC& LC, SVec<8>& res, const OnSend& on)
 {
     const KadRec rs = kad_rec(V.recs, L.S);
-    const bool sb = kad_is_sibling(V, rs, L.S, L.K, LC.numSiblings);
-    kad_find_node1<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res, LC.numSiblings);
+    const int ns = LK ? LC.numSiblings : 1;
+    const bool sb = kad_is_sibling(V, rs, L.S, L.K, ns);
+    kad_find_node1<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res, ns);
     if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
     else if (LC.numSiblings != 0 && sb) {
         L.result = res.idx[0];
         L.pfinished = true; L.psuccess = true;
     } else {
         nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.recs);
-        kad_send_rpcs(L, V, DC, LC, LC.alpha, on);
+        kad_send_rpcs<A, LK>(L, V, DC, LC, LC.alpha, on);
     }
 }
 
@@ -646,7 +649,7 @@ __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
 // getres.ready(slot) says whether the responder's findNode result is available (always on a
 // single GPU); getres.fill(slot, node, geometry, sibling, res) produces it.  Returns false, with the
 // state untouched, when the earliest event is a response whose result has not arrived yet.
-template <int A, bool EX, class GetRes, class OnSend, class Rec>
+template <int A, bool EX, bool LK, class GetRes, class OnSend, class Rec>
 __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                  const KadLC& LC, SVec<8>& res, const GetRes& getres,
                                                  const OnSend& on, const Rec& record)
@@ -674,7 +677,7 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     if (tag & 0x80000000u) {
         // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
         L.any_to = true;
-        kad_timeoutlike(L, V, DC, LC, on);
+        kad_timeoutlike<A, LK>(L, V, DC, LC, on);
         return true;
     }
     // the responder's siblings flag and bucket geometry were captured at send (kad_send)
@@ -686,7 +689,7 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     const bool acc = (LC.useAll && LC.merge) ? true : (vr == L.step);
     if (!(acc || (sb && LC.acceptLateSiblings))) {
         // not accepted: handled as a timeout, its nodes are dropped
-        kad_timeoutlike(L, V, DC, LC, on);
+        kad_timeoutlike<A, LK>(L, V, DC, LC, on);
         return true;
     }
     // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
@@ -703,7 +706,7 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
     else {
         if (numNew == 0 && LC.newOnResp) numNew = 1;
-        kad_send_rpcs(L, V, DC, LC, min(numNew, LC.alpha), on);
+        kad_send_rpcs<A, LK>(L, V, DC, LC, min(numNew, LC.alpha), on);
     }
     return true;
 }

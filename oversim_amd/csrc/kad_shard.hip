@@ -103,11 +103,11 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
     KadLookup<A> L = st[i];
     SVec<8> r;
     ShardSend on{res, i * A, &L.K, shard_lo, nsh, out, out_dest, out_cap, out_count};
-    if (a == 2) kad_lookup_start<A, EX>(L, V, DC, LC, r, on);   // first round: IterativeLookup::start
+    if (a == 2) kad_lookup_start<A, EX, false>(L, V, DC, LC, r, on);   // first round: IterativeLookup::start
     const ShardRes gr{res, i * A};
     const NoRecord rec;
     while (!kad_lookup_done(L)) {
-        if (!kad_lookup_event<A, EX>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
+        if (!kad_lookup_event<A, EX, false>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
     }
     if (kad_lookup_done(L)) {
         const unsigned long long di = atomicAdd(done_count, 1ull);
