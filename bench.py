@@ -67,38 +67,38 @@ def parse():
     return ap.parse_args()
 
 
-WL = {
-    "C": dict(overlay="chord", nodes=1 << 20, per_gpu_nodes=True, lookups=10_000_000, node_ids=False,
-              desc="C: Chord 2^20 nodes per GPU (ring sharded over GPUs), 10M random-key iterative one-way lookups per GPU"),
-    "D": dict(overlay="chord", nodes=1 << 26, per_gpu_nodes=False, lookups=8_000_000, node_ids=False,
-              desc="D: Chord 2^26-node ring sharded over the GPUs, 8M random-key iterative one-way lookups per GPU"),
-    "B": dict(overlay="kademlia", nodes=15000, per_gpu_nodes=False, lookups=1_000_000, node_ids=True, alpha=1,
-              desc="B: Kademlia 15000 nodes (nodes_2d_15000.xml), k=8, alpha=1, 1M node-ID lookups per GPU"),
-    "E": dict(overlay="kademlia", nodes=1 << 24, per_gpu_nodes=False, lookups=4_000_000, node_ids=False, alpha=3,
-              desc="E: Kademlia 2^24 nodes, k=8, alpha=3, 4M random-key lookups per GPU (ID arcs sharded over GPUs)"),
-}
-
-
 def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, routing_type: int = 0) -> dict:
-    """The oracle (CPU restatement, kind 'port') on a bounded sample of the same workload."""
+    """The oracle (CPU restatement, kind 'port', built -O3) on a bounded sample of the same workload,
+    timed on all the host cores this job may use and on one core.  Populations too large for the
+    oracle's stored tables (configs D, E) use its lazy tables (every table entry evaluated per
+    access), which makes that port slower than one holding the tables."""
     sys.path.insert(0, str(ROOT / "tests"))
     from oracle_lib import OracleNet, chord_params, kad_params
-    nthreads = min(os.cpu_count() or 1, 16)
+    nproc = os.cpu_count() or 1
+    # the job's CPU share: OMP_NUM_THREADS on the GPU box (16 per GPU), else every CPU
+    nthreads = max(1, min(nproc, int(os.environ.get("OMP_NUM_THREADS", nproc))))
+    lazy = len(ids) > (1 << 22)
     o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia"
-                  else chord_params(routingType=routing_type))
-    m = 20000
-    t = time.perf_counter()
-    o.route(keys[:m], src[:m], record_hops=False, nthreads=nthreads)
-    dt = time.perf_counter() - t
-    m2 = int(min(len(keys), max(m, m * target_s / max(dt, 1e-6))))
-    t = time.perf_counter()
-    r = o.route(keys[:m2], src[:m2], record_hops=False, nthreads=nthreads)
-    dt = time.perf_counter() - t
-    hops = int(r["hops"].astype(np.int64).sum())
-    return {"value": hops / dt, "unit": "hops/s", "cores": nthreads, "kind": "port",
-            "sample": f"oracle/ovs_oracle.c restatement, {m2} of the step's lookups on the same "
-                      f"{len(ids)}-node {kind} network, OpenMP {nthreads} threads, {dt:.1f} s",
-            "lookups_per_s": m2 / dt}
+                  else chord_params(routingType=routing_type), lazy=lazy)
+
+    def timed(threads: int, budget_s: float):
+        m = 2000
+        t = time.perf_counter()
+        o.route(keys[:m], src[:m], record_hops=False, nthreads=threads)
+        dt = time.perf_counter() - t
+        m2 = int(min(len(keys), max(m, m * budget_s / max(dt, 1e-6))))
+        t = time.perf_counter()
+        r = o.route(keys[:m2], src[:m2], record_hops=False, nthreads=threads)
+        dt = time.perf_counter() - t
+        return int(r["hops"].astype(np.int64).sum()) / dt, m2 / dt, m2, dt
+
+    hps, lps, m_all, dt_all = timed(nthreads, target_s)
+    hps1, lps1, m_one, dt_one = timed(1, target_s / 2)
+    return {"value": hps, "unit": "hops/s", "cores": nthreads, "kind": "port",
+            "sample": f"oracle/ovs_oracle.c restatement (gcc -O3, OpenMP), {m_all} of the step's lookups on the same "
+                      f"{len(ids)}-node {kind} network{' (lazy tables)' if lazy else ''}: {nthreads} threads "
+                      f"{dt_all:.1f} s; 1 thread {m_one} lookups {dt_one:.1f} s",
+            "lookups_per_s": lps, "host_cpus": nproc, "value_1core": hps1, "lookups_per_s_1core": lps1}
 
 
 def traffic_from_json(path: str | None, workload: str, kname: str):
@@ -176,10 +176,7 @@ def main():
 
     from oversim_amd import KbrEngine, Params, workload as W
 
-    wl = dict(WL[a.workload])
-    nodes = a.nodes or wl["nodes"]
-    n_total = nodes * world if wl["per_gpu_nodes"] else nodes
-    m = a.lookups or wl["lookups"]
+    wl = dict(W.WORKLOADS[a.workload])
     kind = wl["overlay"]
     routing_type = 1 if a.routing == "semi-recursive" else 0
     if routing_type and kind != "chord":
@@ -188,31 +185,13 @@ def main():
         wl["desc"] = wl["desc"].replace("iterative", "semi-recursive")
     stream = torch.cuda.Stream(device=dev)
     sharded = world > 1 and (kind == "chord" or os.environ.get("OVS_KAD_REPLICAS") != "1")
-    small = n_total <= (1 << 22)
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
-    if small:
-        ids = W.sorted_unique_ids(n_total, a.seed)
-        xy = W.coordinates(n_total, a.seed, use_file=(kind == "kademlia" and n_total <= 15000))
-        ids_t = torch.from_numpy(ids.view(np.int32)).to(dev)
-        xy_t = torch.from_numpy(xy).to(dev)
-    else:
-        ids_t, xy_t = W.device_population(n_total, a.seed, dev)
-        ids = xy = None
-    if sharded:
-        from oversim_amd.shard import arc_bounds
-        b = arc_bounds(n_total, world)
-        lo, hi = b[rank], b[rank + 1]
-    else:
-        lo, hi = 0, n_total
-    if small:
-        keys, src = W.lookups(ids, m, a.seed + 1000 + rank, node_ids=wl["node_ids"])
-        src = (lo + (src.astype(np.int64) % (hi - lo))).astype(np.uint32)
-        dkeys = torch.from_numpy(keys.view(np.int32)).to(dev)
-        dsrc = torch.from_numpy(src.view(np.int32)).to(dev)
-    else:
-        dkeys, dsrc = W.device_lookups(n_total, m, a.seed + 1000 + rank, dev, lo, hi)
-        keys = src = None
+    I = W.bench_inputs(a.workload, dev, world=world, rank=rank, seed=a.seed, nodes=a.nodes, n_lookups=a.lookups,
+                       sharded=sharded)
+    n_total, m, lo, hi = I["n_total"], I["m"], I["lo"], I["hi"]
+    ids_t, xy_t, dkeys, dsrc = I["ids_t"], I["xy_t"], I["keys_t"], I["src_t"]
+    ids, xy, keys, src = I["ids"], I["xy"], I["keys"], I["src"]
 
     # ---- engine
     if sharded:
@@ -235,10 +214,12 @@ def main():
         eng = KbrEngine(dev_index)
         if kind == "chord":
             eng.set_params(Params.chord().replace(routingType=routing_type))
+            torch.cuda.synchronize()
             eng.chord_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
             kname = "k_chord_lanes"
         else:
             eng.set_params(Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
+            torch.cuda.synchronize()
             eng.kad_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
             kname = "k_kad_route"
         dout = torch.empty((m, 16), dtype=torch.uint8, device=dev)
@@ -310,7 +291,10 @@ def main():
         if a.traffic_csv:
             traffic, traffic_src = traffic_from_csv(a.traffic_csv, kname), a.traffic_csv
         cpu = None
-        if world == 1 and not a.no_cpu_baseline and small:
+        if world == 1 and not a.no_cpu_baseline:
+            if ids is None:       # device-generated population (D, E): the oracle needs host copies
+                ids, xy = ids_t.cpu().numpy().view(np.uint32), xy_t.cpu().numpy()
+                keys, src = dkeys[:1 << 20].cpu().numpy().view(np.uint32), dsrc[:1 << 20].cpu().numpy().view(np.uint32)
             cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type)
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
                "hopCountMax": 50,
@@ -348,6 +332,7 @@ def main():
                 "algorithmic_bytes": bper, "unit_of_work": "hop" if kind == "chord" else "RPC",
                 "traffic_source": traffic_src,
                 "gather_ceiling_GBs": GATHER_CEILING_GBS,
+                "frac_of_gather_ceiling": achieved / GATHER_CEILING_GBS,
             },
             "cpu_baseline": cpu,
         }

@@ -392,8 +392,14 @@ ovs_status  ovs_kad_shard_step(ovs_ctx* ctx, ovs_kad_req* out, uint32_t* out_des
 /* findNode at the (local) responders of n received requests. */
 ovs_status  ovs_kad_shard_serve(ovs_ctx* ctx, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out,
                                 void* stream);
-/* Hand n responses (to this rank's requests) back to the waiting lookups. */
+/* Hand n responses (to this rank's requests) back to the waiting lookups.  A response
+ * with an unknown tag, or one the serving rank could not answer (the request named a
+ * node outside its arc: count 0xFFFFFFFF), is counted as an error; the latter still
+ * completes its slot with an empty result, so the lookup terminates. */
 ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const ovs_kad_resp* in, uint64_t n, void* stream);
+/* Responses counted as errors by ovs_kad_shard_deliver since ovs_kad_shard_begin
+ * (synchronises the device).  The caller fails the batch when it is non-zero. */
+ovs_status  ovs_kad_shard_errors(ovs_ctx* ctx, uint64_t* bad);
 
 #ifdef __cplusplus
 }

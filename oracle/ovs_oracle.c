@@ -30,8 +30,20 @@
 #endif
 
 static __thread char g_err[256];
-const char* orc_last_error(void) { return g_err; }
 static void set_err(const char* m) { snprintf(g_err, sizeof g_err, "%s", m); }
+
+/* A fixed capacity of this restatement was exceeded (e.g. more than MAXRPC RPCs in one lookup).
+ * Never truncated silently: the first breach is recorded here, from any OpenMP thread, and the
+ * batch entry points fail (orc_route_batch returns ORC_FAIL, orc_lookup_batch -1). */
+static volatile int g_cap_fail = 0;
+static char g_cap_msg[256];
+static void cap_error(const char* m)
+{
+    if (__sync_bool_compare_and_swap(&g_cap_fail, 0, 1)) snprintf(g_cap_msg, sizeof g_cap_msg, "capacity exceeded: %s", m);
+}
+const char* orc_last_error(void) { return g_cap_fail ? g_cap_msg : g_err; }
+int orc_cap_failed(void) { return g_cap_fail; }
+void orc_clear_error(void) { g_cap_fail = 0; g_cap_msg[0] = 0; g_err[0] = 0; }
 
 /* ===================================================================== */
 /* 1. OverlayKey (OverlayKey.cc) with keyLength=160 => aSize=3 limbs of   */
@@ -246,6 +258,12 @@ struct orc_net {
     OKey* ids;
     double* xy;
     orc_params p;
+    /* lazy = 1: the tables of the stable state are not stored but evaluated per access by the
+     * same rule that builds them (Chord: pred / successor list / finger i = responsible(n + 2^i);
+     * Kademlia: a node's sibling table and buckets built on first use, kept in a small per-thread
+     * cache).  Used for networks whose stored tables would not fit in memory (configs D, E). */
+    int lazy;
+    uint32_t ns;            /* lazy Chord: successor list length min(successorListSize, n-1) */
     /* Chord */
     uint32_t* pred;         /* n */
     uint32_t* succ;         /* n * sls */
@@ -313,12 +331,35 @@ static void ft_removeFinger(orc_net* net, uint32_t node, uint32_t pos)          
     else if (p == (uint32_t)net->fsize[node] - 1) net->fsize[node]--;
     else net->fdeque[(size_t)node * 160 + p] = NONE;
 }
+/* the successor list, predecessor and finger deque of a node: stored, or (lazy stable ring)
+ * the values orc_chord_build would have stored */
 static uint32_t succ_get(const orc_net* net, uint32_t node, uint32_t pos)
 {
+    if (net->lazy) return (uint32_t)(((uint64_t)node + 1 + pos) % net->n);
     return net->succ[(size_t)node * net->sls + pos];
+}
+static int nsucc_get(const orc_net* net, uint32_t node)
+{
+    return net->lazy ? (int)net->ns : (int)net->nsucc[node];
+}
+static uint32_t pred_get(const orc_net* net, uint32_t node)
+{
+    return net->lazy ? (node + net->n - 1) % net->n : net->pred[node];
 }
 static uint32_t ft_getFinger(const orc_net* net, uint32_t node, uint32_t pos)     /* 174-193 */
 {
+    if (net->lazy) {
+        /* stable state (Chord.cc:845-875): finger pos is set to responsible(n + 2^pos) iff
+         * 2^pos > succ0 - n, else removed; the removed (trivial) ones are exactly the deque
+         * positions p >= size, which getFinger answers with the successor (183-184) */
+        const OKey* self = &net->ids[node];
+        uint32_t s0 = succ_get(net, node, 0);
+        OKey d = ok_sub(net->ids[s0], self);
+        OKey off = ok_pow2(pos);
+        if (ok_cmp(&off, &d) <= 0) return s0;
+        OKey lk = ok_add(*self, &off);
+        return ring_responsible(net, &lk);
+    }
     uint32_t p = 160 - pos - 1;
     const uint32_t* dq = net->fdeque + (size_t)node * 160;
     uint32_t size = net->fsize[node];
@@ -336,13 +377,26 @@ static uint32_t ft_getFinger(const orc_net* net, uint32_t node, uint32_t pos)   
  *    nextFinger = 0..159, trivial fingers (2^i <= succ - self) are removed, the
  *    others set to the node answering rpcFixfingers for self+2^i, i.e. the
  *    responsible node (Chord.cc:1228-1270, non-extended finger table). */
-orc_net* orc_chord_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+static int check_params(const orc_params* p)
+{
+    /* the fixed capacities below (NVec 128 entries, 16 siblings) bound these parameters */
+    if (p->successorListSize < 1 || p->successorListSize > 120) { set_err("successorListSize must be 1..120"); return 0; }
+    if (p->s < 1 || 5 * p->s > 120 || p->k < 1 || p->k > 64) { set_err("kademlia k must be 1..64, 5s <= 120"); return 0; }
+    if (p->numSiblings < 0 || p->numSiblings > 16) { set_err("numSiblings must be 0..16"); return 0; }
+    if (p->lookupRedundantNodes < 1 || p->lookupRedundantNodes > 64) { set_err("lookupRedundantNodes must be 1..64"); return 0; }
+    return 1;
+}
+
+static orc_net* chord_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p, int lazy)
 {
     if (n < 2) { set_err("chord: need at least 2 nodes"); return NULL; }
+    if (!check_params(p)) return NULL;
     orc_net* net = net_alloc(NET_CHORD, ids, n, xy, p);
     if (!net) return NULL;
     uint32_t sls = (uint32_t)p->successorListSize;
     net->sls = sls;
+    net->ns = (n - 1 < sls) ? n - 1 : sls;
+    if (lazy) { net->lazy = 1; return net; }
     net->pred = (uint32_t*)malloc(sizeof(uint32_t) * n);
     net->succ = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sls);
     net->nsucc = (uint8_t*)malloc(n);
@@ -367,11 +421,53 @@ orc_net* orc_chord_build(const orc_key* ids, uint32_t n, const double* xy, const
     return net;
 }
 
+orc_net* orc_chord_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    return chord_build(ids, n, xy, p, 0);
+}
+
+orc_net* orc_chord_build_lazy(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    return chord_build(ids, n, xy, p, 1);
+}
+
+/* store the tables of a lazy stable ring (a fixfingers round rewrites them) */
+static void chord_materialize(orc_net* net)
+{
+    if (!net->lazy) return;
+    uint32_t n = net->n, sls = net->sls;
+    net->pred = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    net->succ = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sls);
+    net->nsucc = (uint8_t*)malloc(n);
+    net->fdeque = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160);
+    net->fsize = (uint8_t*)calloc(n, 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        net->pred[i] = pred_get(net, i);
+        net->nsucc[i] = (uint8_t)net->ns;
+        for (uint32_t j = 0; j < net->ns; ++j) net->succ[(size_t)i * sls + j] = succ_get(net, i, j);
+    }
+    /* deque entries from the lazy rule, then switch over */
+    for (uint32_t i = 0; i < n; ++i) {
+        OKey d = ok_sub(net->ids[succ_get(net, i, 0)], &net->ids[i]);
+        for (uint32_t nf = 0; nf < 160; ++nf) {
+            OKey off = ok_pow2(nf);
+            uint32_t f = ft_getFinger(net, i, nf);
+            uint32_t p = 160 - nf - 1;
+            if (ok_cmp(&off, &d) > 0) {
+                if (net->fsize[i] <= p) net->fsize[i] = (uint8_t)(p + 1);
+                net->fdeque[(size_t)i * 160 + p] = f;
+            }
+        }
+    }
+    net->lazy = 0;
+}
+
 orc_net* orc_chord_build_tables(const orc_key* ids, uint32_t n, const double* xy,
                                 const uint32_t* pred, const uint32_t* succ, const uint8_t* nsucc,
                                 uint32_t succ_stride, const uint32_t* fingers,
                                 const uint8_t* deque_size, const orc_params* p)
 {
+    if (!check_params(p)) return NULL;
     orc_net* net = net_alloc(NET_CHORD, ids, n, xy, p);
     if (!net) return NULL;
     net->sls = succ_stride;
@@ -427,7 +523,11 @@ static int nv_isAddable(const orc_net* net, const NVec* nv, uint32_t e)         
     if (nv->maxSize == 0) return 1;
     return nv->size != nv->maxSize || (nv->metric && nv_compare(net, nv, e, nv->v[nv->size - 1]) <= 0);
 }
-static void nv_push_back(NVec* nv, uint32_t e) { if (nv->size < 128) nv->v[nv->size++] = e; }
+static void nv_push_back(NVec* nv, uint32_t e)
+{
+    if (nv->size < 128) nv->v[nv->size++] = e;
+    else cap_error("NodeVector of 128 entries");
+}
 static int nv_add(const orc_net* net, NVec* nv, uint32_t e)                      /* 432-512 */
 {
     int pos = -1;
@@ -468,9 +568,9 @@ static int chord_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self,
 {
     /* state == READY; numSiblings <= successorListSize asserted by caller */
     if (numSiblings == -1) numSiblings = net->p.successorListSize;
-    uint32_t pred = net->pred[self];
+    uint32_t pred = pred_get(net, self);
     int predUnspec = (pred == NONE);
-    int ssize = net->nsucc[self];
+    int ssize = nsucc_get(net, self);
     if (predUnspec && node == self) {
         int isEmpty = (ssize == 1 && succ_get(net, self, 0) == self) || ssize == 0;
         if (isEmpty || EQ(&net->ids[node], key)) { *err = 0; return 1; }
@@ -498,7 +598,7 @@ static int chord_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self,
 static int chord_closestPreceedingNode(const orc_net* net, uint32_t self, const OKey* key, NVec* out) /* 602-674 */
 {
     uint32_t temp = NONE;
-    int ssize = net->nsucc[self];
+    int ssize = nsucc_get(net, self);
     for (int j = ssize - 1; j >= 0; j--) {
         uint32_t s = succ_get(net, self, (uint32_t)j);
         if (ok_isBetweenR(&net->ids[s], &net->ids[self], key)) { temp = s; break; }
@@ -516,7 +616,7 @@ static int chord_closestPreceedingNode(const orc_net* net, uint32_t self, const 
         if (ok_isBetween(&net->ids[s], &net->ids[self], key)) nv_push_back(out, s);
     }
     if (out->size != 0) return 0;
-    if (net->pred[self] == NONE && succ_get(net, self, 0) == self) { nv_push_back(out, self); return 0; }
+    if (pred_get(net, self) == NONE && succ_get(net, self, 0) == self) { nv_push_back(out, self); return 0; }
     set_err("Error in Chord::closestPreceedingNode()!");
     return -1;
 }
@@ -529,10 +629,10 @@ static int chord_findNode(const orc_net* net, uint32_t self, const OKey* key,
     if (key->isUnspec) { nv_push_back(out, self); return 0; }
     if (chord_isSiblingFor(net, self, self, key, 1, &err)) {
         nv_push_back(out, self);
-        for (int i = 0; i < net->nsucc[self]; i++) nv_push_back(out, succ_get(net, self, (uint32_t)i));
+        for (int i = 0; i < nsucc_get(net, self); i++) nv_push_back(out, succ_get(net, self, (uint32_t)i));
         nv_downsizeTo(out, numSiblings);
     } else if (ok_isBetweenR(key, &net->ids[self], &net->ids[succ_get(net, self, 0)])) {
-        for (int i = 0; i < net->nsucc[self]; i++) nv_push_back(out, succ_get(net, self, (uint32_t)i));
+        for (int i = 0; i < nsucc_get(net, self); i++) nv_push_back(out, succ_get(net, self, (uint32_t)i));
         nv_downsizeTo(out, numRedundantNodes);
     } else {
         if (chord_closestPreceedingNode(net, self, key, out) < 0) return -1;
@@ -553,14 +653,147 @@ static int kad_routingBucketIndex(const orc_net* net, uint32_t self, const OKey*
     return (i / b) * ((1 << b) - 1) + (int)(pow(2, b) - 2);
 }
 
+/* Kademlia snapshot rule (DESIGN.md): sibling table = the min(5s, n-1) XOR-closest
+ * nodes (what routingAdd, Kademlia.cc:537-616, converges to), buckets hold up to k
+ * of the remaining nodes of each subtree, chosen by Floyd sampling driven by
+ * splitmix64(seed, node, bucket, j); bucket order is irrelevant to findNode since
+ * the result NodeVector is XOR-sorted and XOR distances are unique. */
+static uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+static uint64_t kad_hash(uint64_t seed, uint32_t node, uint32_t m, uint32_t j)
+{
+    return splitmix64(seed ^ splitmix64(((uint64_t)node << 32) ^ ((uint64_t)m << 16) ^ (uint64_t)j));
+}
+/* The tables of one node under the snapshot rule: sib[] (its sibling table, XOR-sorted to
+ * self), *nsib, and per bucket m the members bk[m*k ..] (bc[m] of them). */
+static void kad_node_build(const orc_net* net, uint32_t self, uint32_t* sibOut, int* nsibOut, uint8_t* bc,
+                           uint32_t* bk)
+{
+    const orc_params* p = &net->p;
+    int k = p->k, sibCap = 5 * p->s;
+    /* sibling table: walk subtrees m = 0.. upward, gather members, keep 5s closest */
+    /* T_m = [tlo[m], thi[m]): the ids sharing the bits above m with self and differing at bit m
+     * (subtree_range(self, m)), found by one descent over the sorted ids: the ids sharing the
+     * bits above m form one block, split at its first id with bit m set */
+    uint32_t tlo[160], thi[160];
+    {
+        const OKey* me = &net->ids[self];
+        uint32_t lo = 0, hi = net->n;
+        for (int b = 159; b >= 0; --b) {
+            uint32_t a = lo, z = hi;
+            while (a < z) {
+                uint32_t mid = a + (z - a) / 2;
+                if ((net->ids[mid].key[b / 64] >> (b % 64)) & 1) z = mid; else a = mid + 1;
+            }
+            if ((me->key[b / 64] >> (b % 64)) & 1) { tlo[b] = lo; thi[b] = a; lo = a; }
+            else { tlo[b] = a; thi[b] = hi; hi = a; }
+        }
+    }
+    NVec sib; nv_init(&sib, sibCap, 1, &net->ids[self]);
+    int m;
+    for (m = 0; m < 160; ++m) {
+        for (uint32_t x = tlo[m]; x < thi[m]; ++x) nv_add(net, &sib, x);
+        if (nv_isFull(&sib)) break;   /* all later subtrees are farther (XOR >= 2^(m+1)) */
+    }
+    *nsibOut = sib.size;
+    for (int i = 0; i < sibCap; ++i) sibOut[i] = i < sib.size ? sib.v[i] : NONE;
+    /* buckets */
+    for (m = 0; m < 160; ++m) {
+        bc[m] = 0;
+        uint32_t lo = tlo[m], hi = thi[m];
+        if (hi <= lo) continue;
+        /* members not in the sibling table, in ascending id order */
+        uint32_t cnt = hi - lo;
+        uint32_t nsib_in = 0;
+        for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] >= lo && sib.v[s2] < hi) nsib_in++;
+        uint32_t c = cnt - nsib_in;
+        uint32_t* dst = bk + (size_t)m * k;
+        uint32_t chosen[64]; int nch = 0;
+        if (c <= (uint32_t)k) {
+            for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
+        } else {
+            for (uint32_t j = c - (uint32_t)k; j < c; ++j) {       /* Floyd sampling */
+                uint32_t t = (uint32_t)(kad_hash(p->kadSeed, self, (uint32_t)m, j) % (uint64_t)(j + 1));
+                int dup = 0;
+                for (int q = 0; q < nch; ++q) if (chosen[q] == t) { dup = 1; break; }
+                chosen[nch++] = dup ? j : t;
+            }
+            /* ascending member order */
+            for (int a = 1; a < nch; ++a) { uint32_t v = chosen[a]; int q = a - 1; while (q >= 0 && chosen[q] > v) { chosen[q + 1] = chosen[q]; q--; } chosen[q + 1] = v; }
+        }
+        /* map member rank -> node index (skipping siblings) */
+        int out = 0;
+        if (nsib_in == 0) {
+            for (int q = 0; q < nch; ++q) dst[out++] = lo + chosen[q];
+        } else {
+            uint32_t rank = 0; int q = 0;
+            for (uint32_t x = lo; x < hi && q < nch; ++x) {
+                int is_sib = 0;
+                for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] == x) { is_sib = 1; break; }
+                if (is_sib) continue;
+                if (rank == chosen[q]) { dst[out++] = x; q++; }
+                rank++;
+            }
+        }
+        bc[m] = (uint8_t)out;
+    }
+}
+
+/* A node's Kademlia tables: pointers into the stored arrays, or (lazy network) into a
+ * per-thread cache entry built on first use.  Consecutive findNode / isSiblingFor calls of a
+ * lookup are at the same node, so a small direct-mapped cache suffices. */
+typedef struct { const uint32_t* sib; int nsib; const uint8_t* bc; const uint32_t* bk; } KadTab;
+
+#define KCACHE 16
+typedef struct {
+    const orc_net* net;
+    uint32_t node;
+    int nsib;
+    uint32_t sib[128];
+    uint8_t bc[160];
+    uint32_t bk[160 * 64];
+} KadCacheEnt;
+static __thread KadCacheEnt* tl_kcache = NULL;
+
+static KadTab kad_tab(const orc_net* net, uint32_t self)
+{
+    KadTab t;
+    if (!net->lazy) {
+        size_t sibCap = (size_t)5 * net->p.s;
+        t.sib = net->sib + (size_t)self * sibCap;
+        t.nsib = net->nsib[self];
+        t.bc = net->bcount + (size_t)self * 160;
+        t.bk = net->bucket + (size_t)self * 160 * net->p.k;
+        return t;
+    }
+    if (!tl_kcache) {
+        tl_kcache = (KadCacheEnt*)calloc(KCACHE, sizeof(KadCacheEnt));
+        for (int i = 0; i < KCACHE; ++i) tl_kcache[i].net = NULL;
+    }
+    KadCacheEnt* e = &tl_kcache[(self * 2654435761u) >> 28];
+    if (e->net != net || e->node != self) {
+        kad_node_build(net, self, e->sib, &e->nsib, e->bc, e->bk);
+        e->net = net;
+        e->node = self;
+    }
+    t.sib = e->sib; t.nsib = e->nsib; t.bc = e->bc; t.bk = e->bk;
+    return t;
+}
+
 static int kad_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self, const OKey* key,
                             int numSiblings, int* err)                              /* 888-962 */
 {
     int sibCap = 5 * net->p.s;
     if (numSiblings == -1) numSiblings = net->p.s;
     if (numSiblings == 0) { *err = 0; return EQ(&net->ids[node], key); }
-    int nsib = net->nsib[self];
-    const uint32_t* sib = net->sib + (size_t)self * sibCap;
+    KadTab T = kad_tab(net, self);
+    int nsib = T.nsib;
+    const uint32_t* sib = T.sib;
     if (nsib < numSiblings) { *err = 0; return 1; }
     if (nsib == sibCap) {
         OKey a = ok_xor(net->ids[self], key);
@@ -578,19 +811,20 @@ static int kad_findNode(const orc_net* net, uint32_t self, const OKey* key,
                         int numRedundantNodes, int numSiblings, NVec* result)       /* 1101-1246 */
 {
     int err, resultSize;
-    int k = net->p.k, sibCap = 5 * net->p.s;
+    int k = net->p.k;
     if (numSiblings < 0) resultSize = numRedundantNodes;
     else resultSize = kad_isSiblingFor(net, self, self, key, numSiblings, &err) ?
                       (numSiblings ? numSiblings : 1) : numRedundantNodes;
     nv_init(result, resultSize, 1, key);
-    int nsib = net->nsib[self];
-    const uint32_t* sib = net->sib + (size_t)self * sibCap;
+    KadTab T = kad_tab(net, self);
+    int nsib = T.nsib;
+    const uint32_t* sib = T.sib;
     if (nsib == 0) { nv_add(net, result, self); return 0; }
     int mainIndex = kad_routingBucketIndex(net, self, key, 0);
     int startIndex = kad_routingBucketIndex(net, self, key, 1);
     int endIndex = kad_routingBucketIndex(net, self, &net->ids[sib[nsib - 1]], 0);
-    const uint8_t* bc = net->bcount + (size_t)self * 160;
-    const uint32_t* bk = net->bucket + (size_t)self * 160 * k;
+    const uint8_t* bc = T.bc;
+    const uint32_t* bk = T.bk;
     if (mainIndex != -1) {
         for (int i = 0; i < bc[mainIndex]; ++i) nv_add(net, result, bk[(size_t)mainIndex * k + i]);
     }
@@ -607,120 +841,52 @@ static int kad_findNode(const orc_net* net, uint32_t self, const OKey* key,
     return 0;
 }
 
-/* Kademlia snapshot rule (DESIGN.md): sibling table = the min(5s, n-1) XOR-closest
- * nodes (what routingAdd, Kademlia.cc:537-616, converges to), buckets hold up to k
- * of the remaining nodes of each subtree, chosen by Floyd sampling driven by
- * splitmix64(seed, node, bucket, j); bucket order is irrelevant to findNode since
- * the result NodeVector is XOR-sorted and XOR distances are unique. */
-static uint64_t splitmix64(uint64_t x)
-{
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-static uint64_t kad_hash(uint64_t seed, uint32_t node, uint32_t m, uint32_t j)
-{
-    return splitmix64(seed ^ splitmix64(((uint64_t)node << 32) ^ ((uint64_t)m << 16) ^ (uint64_t)j));
-}
-/* index range of ids sharing the top (159-m) bits of `key` with bit m flipped */
-static void subtree_range(const orc_net* net, const OKey* key, int m, uint32_t* lo, uint32_t* hi)
-{
-    /* prefix block: bits > m equal key's, bit m = !key bit m, bits < m free */
-    OKey base = *key;
-    int li = m / 64, bi = m % 64;
-    base.key[li] ^= (uint64_t)1 << bi;
-    /* clear bits below m */
-    for (int i = 0; i < li; ++i) base.key[i] = 0;
-    base.key[li] &= ~(((uint64_t)1 << bi) - 1);
-    OKey top = base;
-    for (int i = 0; i < li; ++i) top.key[i] = ~0ull;
-    top.key[li] |= (((uint64_t)1 << bi) - 1);
-    ok_trim(&top);
-    /* lower_bound(base), upper_bound(top) */
-    uint32_t a = 0, b = net->n;
-    while (a < b) { uint32_t mid = a + (b - a) / 2; if (ok_cmp(&net->ids[mid], &base) < 0) a = mid + 1; else b = mid; }
-    *lo = a;
-    b = net->n;
-    while (a < b) { uint32_t mid = a + (b - a) / 2; if (ok_cmp(&net->ids[mid], &top) <= 0) a = mid + 1; else b = mid; }
-    *hi = a;
-}
-
-orc_net* orc_kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+static orc_net* kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p, int lazy)
 {
     if (p->b != 1) { set_err("kademlia: only b=1 supported"); return NULL; }
+    if (!check_params(p)) return NULL;
     orc_net* net = net_alloc(NET_KAD, ids, n, xy, p);
     if (!net) return NULL;
+    if (lazy) { net->lazy = 1; return net; }
     int k = p->k, sibCap = 5 * p->s;
     net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
     net->nsib = (uint8_t*)calloc(n, 1);
     net->bucket = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160 * k);
     net->bcount = (uint8_t*)calloc((size_t)n * 160, 1);
-    for (uint32_t i = 0; i < (size_t)n * sibCap; ++i) net->sib[i] = NONE;
-    for (uint32_t self = 0; self < n; ++self) {
-        /* sibling table: walk subtrees m = 0.. upward, gather members, keep 5s closest */
-        NVec sib; nv_init(&sib, sibCap, 1, &net->ids[self]);
-        int m;
-        for (m = 0; m < 160; ++m) {
-            uint32_t lo, hi;
-            subtree_range(net, &net->ids[self], m, &lo, &hi);
-            for (uint32_t x = lo; x < hi; ++x) nv_add(net, &sib, x);
-            if (nv_isFull(&sib)) break;   /* all later subtrees are farther (XOR >= 2^(m+1)) */
-        }
-        net->nsib[self] = (uint8_t)sib.size;
-        memcpy(net->sib + (size_t)self * sibCap, sib.v, sizeof(uint32_t) * (size_t)sib.size);
-        /* buckets */
-        for (m = 0; m < 160; ++m) {
-            uint32_t lo, hi;
-            subtree_range(net, &net->ids[self], m, &lo, &hi);
-            if (hi <= lo) continue;
-            /* members not in the sibling table, in ascending id order */
-            uint32_t cnt = hi - lo;
-            uint32_t nsib_in = 0;
-            for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] >= lo && sib.v[s2] < hi) nsib_in++;
-            uint32_t c = cnt - nsib_in;
-            uint32_t* dst = net->bucket + ((size_t)self * 160 + m) * k;
-            uint32_t chosen[64]; int nch = 0;
-            if (c <= (uint32_t)k) {
-                for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
-            } else {
-                for (uint32_t j = c - (uint32_t)k; j < c; ++j) {       /* Floyd sampling */
-                    uint32_t t = (uint32_t)(kad_hash(p->kadSeed, self, (uint32_t)m, j) % (uint64_t)(j + 1));
-                    int dup = 0;
-                    for (int q = 0; q < nch; ++q) if (chosen[q] == t) { dup = 1; break; }
-                    chosen[nch++] = dup ? j : t;
-                }
-                /* ascending member order */
-                for (int a = 1; a < nch; ++a) { uint32_t v = chosen[a]; int q = a - 1; while (q >= 0 && chosen[q] > v) { chosen[q + 1] = chosen[q]; q--; } chosen[q + 1] = v; }
-            }
-            /* map member rank -> node index (skipping siblings) */
-            int out = 0;
-            if (nsib_in == 0) {
-                for (int q = 0; q < nch; ++q) dst[out++] = lo + chosen[q];
-            } else {
-                uint32_t rank = 0; int q = 0;
-                for (uint32_t x = lo; x < hi && q < nch; ++x) {
-                    int is_sib = 0;
-                    for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] == x) { is_sib = 1; break; }
-                    if (is_sib) continue;
-                    if (rank == chosen[q]) { dst[out++] = x; q++; }
-                    rank++;
-                }
-            }
-            net->bcount[(size_t)self * 160 + m] = (uint8_t)out;
-        }
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64)
+#endif
+    for (int64_t self = 0; self < (int64_t)n; ++self) {
+        int ns = 0;
+        kad_node_build(net, (uint32_t)self, net->sib + (size_t)self * sibCap, &ns, net->bcount + (size_t)self * 160,
+                       net->bucket + (size_t)self * 160 * k);
+        net->nsib[self] = (uint8_t)ns;
     }
     return net;
+}
+
+orc_net* orc_kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    return kad_build(ids, n, xy, p, 0);
+}
+
+orc_net* orc_kad_build_lazy(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    return kad_build(ids, n, xy, p, 1);
 }
 
 void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes)
 {
     size_t sc = (size_t)5 * net->p.s, k = (size_t)net->p.k;
-    memcpy(siblings, net->sib, sizeof(uint32_t) * net->n * sc);
-    memcpy(bucket_count, net->bcount, (size_t)net->n * 160);
-    for (size_t i = 0; i < (size_t)net->n * 160; ++i)
-        for (size_t j = 0; j < k; ++j)
-            bucket_nodes[i * k + j] = j < net->bcount[i] ? net->bucket[i * k + j] : NONE;
+    for (uint32_t v = 0; v < net->n; ++v) {
+        KadTab T = kad_tab(net, v);
+        for (size_t i = 0; i < sc; ++i) siblings[(size_t)v * sc + i] = (int)i < T.nsib ? T.sib[i] : NONE;
+        for (size_t m = 0; m < 160; ++m) {
+            bucket_count[(size_t)v * 160 + m] = T.bc[m];
+            for (size_t j = 0; j < k; ++j)
+                bucket_nodes[((size_t)v * 160 + m) * k + j] = j < T.bc[m] ? T.bk[m * k + j] : NONE;
+        }
+    }
 }
 
 /* ---- overlay dispatch ---------------------------------------------------------- */
@@ -893,6 +1059,7 @@ static int path_add(Lookup* L, uint32_t h)                                      
 {
     if (L->net->p.lookupMerge) return lv_add(L, h);
     if (L->nnh < MAXNH) { L->nh[L->nnh].handle = h; L->nh[L->nnh].alreadyUsed = 0; L->nnh++; }
+    else cap_error("more than MAXNH next hops");
     return L->nnh - 1;
 }
 
@@ -904,7 +1071,7 @@ static void lk_addSibling(Lookup* L, uint32_t h)                                
         if (EQ(&L->net->ids[h], &L->key)) { L->siblings[0] = h; L->nsiblings = 1; }
         return;
     }
-    if (L->nsiblings < cap) L->siblings[L->nsiblings++] = h;
+    if (L->nsiblings < cap) L->siblings[L->nsiblings++] = h;   /* cap <= 16 (check_params, orc_lookup_batch) */
 }
 
 /* IterativeLookup::sendRpc (656-689) + BaseRpc::sendRpcCall timeout (BaseRpc.cc:173-253) */
@@ -913,7 +1080,7 @@ static void lk_sendRpc(Lookup* L, uint32_t handle, int rpcId)
     if (L->finished || !L->running) return;
     Rpc* r = lk_findRpc(L, handle);
     if (!r) {
-        if (L->nrpcs == MAXRPC) { set_err("too many rpcs"); return; }
+        if (L->nrpcs == MAXRPC) { cap_error("more than MAXRPC FindNodeCalls in one lookup"); return; }
         r = &L->rpcs[L->nrpcs++];
         memset(r, 0, sizeof *r);
         r->node = handle; r->active = 1;
@@ -1095,6 +1262,7 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
         L->now = bt;
         if (bestIsTimeout) {                 /* handleRpcTimeout 588-654 */
             if (L->ndead < MAXRPC) L->dead[L->ndead++] = r.node;
+            else cap_error("more than MAXRPC dead nodes in one lookup");
             for (int q = 0; q < r.nInfo; ++q) {
                 if (L->pfinished) continue;
                 path_handleTimeout(L);
@@ -1243,7 +1411,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
         total += out[i].hops;
     }
     (void)nthreads;
-    return total;
+    return g_cap_fail ? ORC_FAIL : total;
 }
 
 int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int numSiblings,
@@ -1264,7 +1432,7 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
         run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings);
     }
     (void)nthreads;
-    return numSiblings;
+    return g_cap_fail ? -1 : numSiblings;
 }
 
 /* ======================================================================== */
@@ -1284,6 +1452,7 @@ uint64_t orc_chord_fix_fingers(orc_net* net, const uint32_t* nodes, uint64_t m, 
                                uint64_t* out_changed, int nthreads)
 {
     if (net->type != NET_CHORD) { set_err("fix_fingers: not a Chord network"); return 0; }
+    chord_materialize(net);
     uint64_t cap = m * 160, nl = 0;
     orc_key* keys = (orc_key*)malloc(sizeof(orc_key) * (cap ? cap : 1));
     uint32_t* src = (uint32_t*)malloc(sizeof(uint32_t) * (cap ? cap : 1));

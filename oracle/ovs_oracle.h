@@ -88,6 +88,13 @@ orc_net* orc_chord_build_tables(const orc_key* ids, uint32_t n, const double* xy
                                 const uint8_t* deque_size, const orc_params* p);
 /* Kademlia snapshot (DESIGN.md "Kademlia snapshot rule"). */
 orc_net* orc_kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
+/* The same networks with lazy tables: nothing but ids / coordinates is stored; every table
+ * entry is evaluated on access by the rule the eager builders store (Chord: pred, successor
+ * list, finger i = responsible(n + 2^i); Kademlia: a node's sibling table and buckets, built
+ * on first use into a per-thread cache).  Results are identical; memory is O(n), so samples of
+ * configs D (2^26-node Chord) and E (2^24-node Kademlia) can be checked. */
+orc_net* orc_chord_build_lazy(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
+orc_net* orc_kad_build_lazy(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
 void     orc_net_free(orc_net* net);
 
 /* export the Kademlia snapshot so the GPU builder can be checked:
@@ -112,7 +119,9 @@ typedef struct {
 
 /* hop_seq may be NULL; else n*hopCountMax entries (accepted responders, UINT32_MAX padded).
  * rpcs_out may be NULL; else per-lookup count of FindNodeCalls sent.
- * nthreads<=0 -> all OpenMP threads. Returns total accepted hops. */
+ * nthreads<=0 -> all OpenMP threads. Returns total accepted hops, or ORC_FAIL when a fixed
+ * capacity of the restatement was exceeded (orc_last_error; never a silent truncation). */
+#define ORC_FAIL 0xFFFFFFFFFFFFFFFFull
 uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
                          orc_route_out* out, uint32_t* hop_seq, uint32_t* rpcs_out, int nthreads);
 
@@ -169,6 +178,8 @@ void orc_kbrtest_lookup_stats(const orc_net* net, const orc_lookup_out* out, con
                               const orc_key* keys, const uint32_t* src, uint64_t n, double measured_time_s,
                               int lookupNodeIds, double failureLatency, orc_kbrtest_lookup_result* st);
 const char* orc_last_error(void);
+int orc_cap_failed(void);      /* 1 once a capacity was exceeded (sticky until orc_clear_error) */
+void orc_clear_error(void);
 
 #ifdef __cplusplus
 }

@@ -5,11 +5,18 @@ gfx950 with hipcc and linked into oversim_amd/libovs_kbr.so (a C-ABI shared
 library, include/ovs_kbr.h).  -ffp-contract=off keeps the fp64 delay
 arithmetic bit-identical to the reference's x86-64 build.
 
+Rebuilds are decided by content, not mtime: each object carries a stamp with
+the hash of its source, every header and the flags, and the library embeds
+`ovs_build_id()` = the hash of all engine sources + flags (source_hash()).
+kbr.lib() refuses to load a library whose id differs from the sources next to
+it, so a tested binary is always the one built from the tree it ships with.
+
 Checker: oracle/ is compiled with gcc into oracle/_build/libovs_oracle.so
 (test infrastructure only).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -30,43 +37,76 @@ CFLAGS = [
 SOURCES = ["chord.hip", "kad.hip", "kad_shard.hip", "stats.hip", "ovs_kbr.cpp", "ovs_ini.cpp"]
 
 
-def _newer(target: Path, deps: list[Path]) -> bool:
-    if not target.exists():
-        return True
-    t = target.stat().st_mtime
-    return any(d.stat().st_mtime > t for d in deps)
+def _engine_files() -> list[Path]:
+    return sorted([CSRC / s for s in SOURCES] + list(CSRC.glob("*.hpp")) + [ROOT / "include" / "ovs_kbr.h"])
+
+
+def _digest(files: list[Path], extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    for f in files:
+        h.update(f.relative_to(ROOT).as_posix().encode() + b"\0")
+        h.update(f.read_bytes())
+        h.update(b"\0")
+    return h.hexdigest()[:32]
+
+
+def source_hash() -> str:
+    """Hash of every engine source and header plus the compile flags (= the library's ovs_build_id())."""
+    return _digest(_engine_files(), " ".join(CFLAGS))
+
+
+def _stamp_ok(target: Path, digest: str) -> bool:
+    stamp = target.with_name(target.name + ".stamp")
+    return target.exists() and stamp.exists() and stamp.read_text() == digest
+
+
+def _write_stamp(target: Path, digest: str):
+    target.with_name(target.name + ".stamp").write_text(digest)
 
 
 def build_engine(verbose: bool = False) -> Path:
     OBJ.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.hpp")) + [ROOT / "include" / "ovs_kbr.h"]
+    flags = " ".join(CFLAGS)
     procs = []
     objs = []
     for src in SOURCES:
         s = CSRC / src
         o = OBJ / (src.rsplit(".", 1)[0] + ".o")
         objs.append(o)
-        if not _newer(o, [s] + headers):
+        d = _digest([s] + headers, flags)
+        if _stamp_ok(o, d):
             continue
         cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", str(s), "-o", str(o)]
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        procs.append((cmd, o, d, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     failed = []
-    for cmd, p in procs:
+    for cmd, o, d, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
             failed.append((cmd, out.decode(errors="replace")))
-        elif verbose and out:
-            print(out.decode(errors="replace"))
+        else:
+            _write_stamp(o, d)
+            if verbose and out:
+                print(out.decode(errors="replace"))
     if failed:
         msg = "\n".join(f"$ {' '.join(c)}\n{o}" for c, o in failed)
         raise RuntimeError(f"hipcc failed:\n{msg}")
-    if _newer(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs)]
+    bid = source_hash()
+    if not _stamp_ok(LIB, bid):
+        # the build id: a one-function translation unit linked into the library
+        idsrc = OBJ / "buildid.cpp"
+        idsrc.write_text(f'extern "C" const char* ovs_build_id(void) {{ return "{bid}"; }}\n')
+        idobj = OBJ / "buildid.o"
+        subprocess.run(["g++", "-O2", "-fPIC", "-c", str(idsrc), "-o", str(idobj)], check=True)
+        tmp = LIB.with_name(LIB.name + ".tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(tmp), *map(str, objs), str(idobj)]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        os.replace(tmp, LIB)          # never rewrite a library a running process may have mapped
+        _write_stamp(LIB, bid)
     return LIB
 
 

@@ -438,6 +438,15 @@ struct Hdr {
 
 __device__ __forceinline__ bool k_zero(const K160& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3] | a.w[4]) == 0; }
 
+// orders one wave's LDS stores before its loads of other lanes' slots (and the loads before the
+// next iteration's stores) for the compiler; a wave's LDS instructions execute in issue order
+__device__ __forceinline__ void lds_wave_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int msb64(uint64_t x) { return 63 - __clzll((long long)x); }
 
 __device__ __forceinline__ uint64_t u64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
@@ -509,9 +518,13 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
 
     while (true) {
         // ---- gathered lines to their lanes: chunk (lane & 3) of the line of lane 16k + (lane >> 2)
-        // was fetched into Lk; LDS slot 4 * owner + chunk = 64 k + lane (same wave: in order)
+        // was fetched into Lk; LDS slot 4 * owner + chunk = 64 k + lane.  The reads below take
+        // slots other lanes wrote: the wavefront fences keep the compiler from moving a ds_read
+        // above the ds_write it depends on (the LDS itself executes one wave's ops in order)
         xb[lane] = L0; xb[64 + lane] = L1; xb[128 + lane] = L2; xb[192 + lane] = L3;
+        lds_wave_fence();
         L0 = xb[4 * lane]; L1 = xb[4 * lane + 1]; L2 = xb[4 * lane + 2]; L3 = xb[4 * lane + 3];
+        lds_wave_fence();
 
         // ---- refill: lanes without a lookup take the next of the wave's slice
         bool fresh = false;
@@ -609,7 +622,9 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                     const uint64_t g[8] = {u64(L0.x, L0.y), u64(L0.z, L0.w), u64(L1.x, L1.y), u64(L1.z, L1.w),
                                            u64(L2.x, L2.y), u64(L2.z, L2.w), u64(L3.x, L3.y), u64(L3.z, L3.w)};
                     int tj = -1;
-                    bool tie = false;
+                    // the WinRec holds 8 successor distances: a longer successor list takes the
+                    // exact scan over all ns successors below (Chord.cc:612-623)
+                    bool tie = ns > 8;
                     #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         if (j < ns) {

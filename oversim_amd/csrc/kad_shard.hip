@@ -174,8 +174,19 @@ __global__ void k_kad_shard_deliver(const ovs_kad_resp* __restrict__ in, uint64_
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const ovs_kad_resp o = in[j];
-    if (o.tag >= nslots || o.count > 8) { atomicAdd(bad, 1ull); return; }
+    if (o.tag >= nslots) { atomicAdd(bad, 1ull); return; }
     KadRes r;
+    if (o.count > 8) {
+        // a request the serving rank could not answer (not its node): counted for
+        // ovs_kad_shard_errors, and the slot completes with an empty result so the lookup ends
+        atomicAdd(bad, 1ull);
+        r.count = 0;
+        r.ready = 1;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { r.nodes[k] = NONE; r.dist[k] = ~0ull; }
+        res[o.tag] = r;
+        return;
+    }
     r.count = o.count;
     r.ready = 1;
 #pragma unroll

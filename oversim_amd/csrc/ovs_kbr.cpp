@@ -246,6 +246,10 @@ ovs_status upload_nodes(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const dou
 {
     if (n < 2) return fail(c, OVS_EINVAL, "need at least 2 nodes");
     if (n >= 0xFFFFFFFFull) return fail(c, OVS_EINVAL, "too many nodes for 32-bit node indices");
+    // device inputs may still be being written by work on any of the caller's streams (the load
+    // call takes none to order against): the copies below run on the context's own
+    // non-blocking stream, so wait for the whole device first (loads are not on the hot path)
+    if (dev) HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMalloc(&c->recs, sizeof(KeyRec) * n));
     HIPCHK(c, hipMalloc(&c->xy, sizeof(double2) * n));
     // interleave 20 B keys into 24 B records with a strided 2-D copy
@@ -698,6 +702,19 @@ ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const ovs_kad_resp* in, uint64_t n,
     HIPCHK(c, hipSetDevice(c->device));
     hipError_t e = kad_shard_deliver(in, n, c->kres, c->knlook * (uint64_t)c->kalpha, c->kbad, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard deliver");
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_shard_errors(ovs_ctx* c, uint64_t* bad)
+{
+    if (!c || !bad) return OVS_EINVAL;
+    *bad = 0;
+    if (!c->kbad) return OVS_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    unsigned long long h = 0;
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(&h, c->kbad, sizeof h, hipMemcpyDeviceToHost));
+    *bad = h;
     return OVS_OK;
 }
 

@@ -150,6 +150,15 @@ def lib() -> C.CDLL:
         raise ImportError(f"{_LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
                           "(the MI355X engine has no CPU fallback)")
     L = C.CDLL(str(_LIB_PATH))
+    L.ovs_build_id.argtypes = []
+    L.ovs_build_id.restype = C.c_char_p
+    if not os.environ.get("OVS_LIB"):
+        # the library must be the build of the sources it ships with (oversim_amd/build.py)
+        from .build import source_hash
+        built, want = L.ovs_build_id().decode(), source_hash()
+        if built != want:
+            raise ImportError(f"{_LIB_PATH} is stale (build id {built}, sources {want}): rebuild with "
+                              "`python -m oversim_amd.build`")
     vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32
     sigs = {
         "ovs_abi_version": ([], C.c_int),

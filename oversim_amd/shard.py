@@ -140,6 +140,7 @@ for _name, _args in {
                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
     "ovs_kad_shard_serve": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p],
     "ovs_kad_shard_deliver": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
+    "ovs_kad_shard_errors": [C.c_void_p, C.c_void_p],
 }.items():
     _f = getattr(lib(), _name)
     _f.argtypes = _args
@@ -354,10 +355,19 @@ class KadShardStepper:
             st = lib().ovs_kad_shard_deliver(self.eng._h, self._p(resps), resps.shape[0], self._s())
             self.eng._chk(st, "ovs_kad_shard_deliver")
 
+    def errors(self) -> int:
+        """Responses ovs_kad_shard_deliver could not hand to a lookup (mis-routed requests)."""
+        bad = C.c_uint64(0)
+        self.eng._chk(lib().ovs_kad_shard_errors(self.eng._h, C.byref(bad)), "ovs_kad_shard_errors")
+        return int(bad.value)
+
     def finished(self):
         k = int(self.counters[1].item())
         if k > self.done.shape[0]:
             raise RuntimeError("done buffer overflow")
+        bad = self.errors()
+        if bad:
+            raise RuntimeError(f"{bad} Kademlia responses could not be delivered (request sent to the wrong rank)")
         return self.done[:k]
 
 

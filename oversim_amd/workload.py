@@ -130,3 +130,62 @@ def device_lookups(n_nodes: int, m: int, seed: int, device, src_lo: int = 0, src
     hi = n_nodes if src_hi is None else src_hi
     src = torch.randint(src_lo, hi, (m,), dtype=torch.int64, device=device, generator=g).to(torch.int32)
     return keys.contiguous(), src.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# The bench workloads (BASELINE.json configs B-E), shared by bench.py and the parity tests that
+# check the exact timed path on the exact timed inputs (tests/test_gpu_timed.py).
+
+WORKLOADS = {
+    "C": dict(overlay="chord", nodes=1 << 20, per_gpu_nodes=True, lookups=10_000_000, node_ids=False,
+              desc="C: Chord 2^20 nodes per GPU (ring sharded over GPUs), 10M random-key iterative one-way lookups per GPU"),
+    "D": dict(overlay="chord", nodes=1 << 26, per_gpu_nodes=False, lookups=8_000_000, node_ids=False,
+              desc="D: Chord 2^26-node ring sharded over the GPUs, 8M random-key iterative one-way lookups per GPU"),
+    "B": dict(overlay="kademlia", nodes=15000, per_gpu_nodes=False, lookups=1_000_000, node_ids=True, alpha=1,
+              desc="B: Kademlia 15000 nodes (nodes_2d_15000.xml), k=8, alpha=1, 1M node-ID lookups per GPU"),
+    "E": dict(overlay="kademlia", nodes=1 << 24, per_gpu_nodes=False, lookups=4_000_000, node_ids=False, alpha=3,
+              desc="E: Kademlia 2^24 nodes, k=8, alpha=3, 4M random-key lookups per GPU (ID arcs sharded over GPUs)"),
+}
+
+SMALL_HOST_LIMIT = 1 << 22     # populations up to this size are generated on the host (numpy)
+
+
+def bench_inputs(workload: str, device, world: int = 1, rank: int = 0, seed: int = 0xC, nodes: int | None = None,
+                 n_lookups: int | None = None, sharded: bool | None = None) -> dict:
+    """The population and this rank's lookups of a bench workload, resident on `device`.
+
+    Returns ids_t (n,5) int32 view of the u32 words, xy_t (n,2) f64, keys_t (m,5) int32, src_t (m,)
+    int32 device tensors; ids / xy / keys / src as numpy arrays when the population is generated
+    on the host (n <= SMALL_HOST_LIMIT), else None; n_total, m, lo, hi (this rank's source arc)."""
+    import torch
+    wl = WORKLOADS[workload]
+    n_node = nodes or wl["nodes"]
+    n_total = n_node * world if wl["per_gpu_nodes"] else n_node
+    m = n_lookups or wl["lookups"]
+    kind = wl["overlay"]
+    if sharded is None:
+        sharded = world > 1
+    if sharded:
+        lo, hi = rank * n_total // world, (rank + 1) * n_total // world
+    else:
+        lo, hi = 0, n_total
+    small = n_total <= SMALL_HOST_LIMIT
+    if small:
+        ids = sorted_unique_ids(n_total, seed)
+        xy = coordinates(n_total, seed, use_file=(kind == "kademlia" and n_total <= 15000))
+        ids_t = torch.from_numpy(ids.view(np.int32)).to(device)
+        xy_t = torch.from_numpy(xy).to(device)
+        keys, src = lookups(ids, m, seed + 1000 + rank, node_ids=wl["node_ids"])
+        src = (lo + (src.astype(np.int64) % (hi - lo))).astype(np.uint32)
+        keys_t = torch.from_numpy(keys.view(np.int32)).to(device)
+        src_t = torch.from_numpy(src.view(np.int32)).to(device)
+    else:
+        ids_t, xy_t = device_population(n_total, seed, device)
+        keys_t, src_t = device_lookups(n_total, m, seed + 1000 + rank, device, lo, hi)
+        ids = xy = keys = src = None
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    return dict(ids_t=ids_t, xy_t=xy_t, keys_t=keys_t, src_t=src_t, ids=ids, xy=xy, keys=keys, src=src,
+                n_total=n_total, m=m, lo=lo, hi=hi, kind=kind, alpha=wl.get("alpha", 1), desc=wl["desc"],
+                per_gpu_nodes=wl["per_gpu_nodes"])
+

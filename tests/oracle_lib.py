@@ -12,6 +12,8 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent.parent
 _SO = ROOT / "oracle" / "_build" / "libovs_oracle.so"
 
+ORC_FAIL = 0xFFFFFFFFFFFFFFFF
+
 ROUTE_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
                         ("one_way_hops", "u1"), ("latency_ns", "<i8")])
 
@@ -68,6 +70,10 @@ def lib() -> C.CDLL:
             ("orc_chord_build", [vp, u32, vp, vp], vp),
             ("orc_chord_build_tables", [vp, u32, vp, vp, vp, vp, u32, vp, vp, vp], vp),
             ("orc_kad_build", [vp, u32, vp, vp], vp),
+            ("orc_chord_build_lazy", [vp, u32, vp, vp], vp),
+            ("orc_kad_build_lazy", [vp, u32, vp, vp], vp),
+            ("orc_cap_failed", [], C.c_int),
+            ("orc_clear_error", [], None),
             ("orc_net_free", [vp], None),
             ("orc_kad_export", [vp, vp, vp, vp], None),
             ("orc_chord_export_fingers", [vp, vp], None),
@@ -133,7 +139,10 @@ def kad_params(**kw) -> OrcParams:
 class OracleNet:
     """A network built by the oracle (Chord stable state or Kademlia snapshot)."""
 
-    def __init__(self, kind: str, ids, xy, params: OrcParams | None = None, tables: dict | None = None):
+    def __init__(self, kind: str, ids, xy, params: OrcParams | None = None, tables: dict | None = None,
+                 lazy: bool = False):
+        """lazy: store no tables, evaluate them per access (orc_*_build_lazy) -- same results, O(n)
+        memory, for samples of the 2^26-node Chord (D) and 2^24-node Kademlia (E) networks."""
         self.ids = np.ascontiguousarray(ids, dtype=np.uint32)
         self.xy = np.ascontiguousarray(xy, dtype=np.float64)
         self.kind = kind
@@ -142,7 +151,8 @@ class OracleNet:
         if kind == "chord":
             self.params = params or chord_params()
             if tables is None:
-                h = L.orc_chord_build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+                build = L.orc_chord_build_lazy if lazy else L.orc_chord_build
+                h = build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
             else:
                 t = {k: np.ascontiguousarray(v) for k, v in tables.items()}
                 self._keep = t
@@ -151,7 +161,8 @@ class OracleNet:
                                              _p(t["deque_size"]), C.byref(self.params))
         else:
             self.params = params or kad_params()
-            h = L.orc_kad_build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+            build = L.orc_kad_build_lazy if lazy else L.orc_kad_build
+            h = build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
         if not h:
             raise RuntimeError(f"oracle build failed: {L.orc_last_error().decode()}")
         self._h = C.c_void_p(h)
@@ -170,7 +181,8 @@ class OracleNet:
         H = max(self.params.hopCountMax, 1)
         hop = np.empty((n, H), dtype=np.uint32) if record_hops else None
         rpcs = np.empty(n, dtype=np.uint32) if count_rpcs else None
-        lib().orc_route_batch(self._h, _p(keys), _p(src), n, _p(out), _p(hop), _p(rpcs), nthreads)
+        if lib().orc_route_batch(self._h, _p(keys), _p(src), n, _p(out), _p(hop), _p(rpcs), nthreads) == ORC_FAIL:
+            raise RuntimeError(f"oracle: {lib().orc_last_error().decode()}")
         res = {f: out[f].copy() for f in ROUTE_DTYPE.names}
         if hop is not None:
             res["hop_seq"] = hop

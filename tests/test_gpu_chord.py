@@ -96,10 +96,11 @@ def test_route_medium_ring(engine: KbrEngine, rnd):
     _eq(g, r, f"2^16 ring rnd={rnd}", hop_cols=50)
 
 
-@pytest.mark.parametrize("sls,hcm", [(1, 50), (2, 50), (3, 6), (8, 4), (5, 0)])
+@pytest.mark.parametrize("sls,hcm", [(1, 50), (2, 50), (3, 6), (8, 4), (5, 0), (12, 50), (16, 50)])
 def test_route_successor_list_and_hop_limit(engine: KbrEngine, sls, hcm):
-    """successorListSize (the window the WinRec / NodeRec distances cover) and hopCountMax
-    variants of the converged-ring kernel against the oracle, node-ID and random keys."""
+    """successorListSize (the window the WinRec / NodeRec distances cover; beyond its 8 entries the
+    kernel scans the successors exactly) and hopCountMax variants of the converged-ring kernel
+    against the oracle, node-ID and random keys."""
     net = W.population(1 << 14, 40 + sls)
     p = dict(successorListSize=sls, hopCountMax=hcm)
     engine.set_params(Params.chord().replace(**p))

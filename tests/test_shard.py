@@ -437,3 +437,71 @@ def test_kad_two_processes_share_one_gpu_gloo():
                          Params.kademlia())
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+
+
+# ------------------------------------------------------------- W = 8 at 2^22 nodes vs the oracle
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_chord_w8_large_ring_vs_oracle():
+    """Eight arcs of a 2^22-node ring (one context per arc on one GPU, the in-process exchange):
+    every lookup compared with the CPU oracle itself, not with the single-GPU kernel."""
+    from oversim_amd import Params
+    from oversim_amd.shard import GpuShardStepper, arc_bounds, done_to_numpy, route_local_shards
+    from oracle_lib import OracleNet
+    world, n, m = 8, 1 << 22, 12_500
+    net = W.population(n, 191)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, params=Params.chord())
+                for r in range(world)]
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s = W.lookups(net.ids, m, 192 + r, node_ids=(r % 2 == 0))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k).to(dev)); ss.append(torch.from_numpy(s).to(dev)); qb.append(r * m)
+        allk.append(k); alls.append(s)
+    for st in steppers:
+        st.reset(world * m)
+    dones, rounds = route_local_shards(steppers, ks, ss, qb)
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    ref = OracleNet("chord", net.ids, net.xy, lazy=True).route(np.concatenate(allk), np.concatenate(alls),
+                                                               record_hops=False)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    assert rounds >= 4
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_kad_w8_large_network_vs_oracle():
+    """Eight ID arcs of a 2^22-node Kademlia network, alpha = 3, request/response exchange in one
+    process: every lookup (and its RPC count) compared with the CPU oracle."""
+    from oversim_amd import Params
+    from oversim_amd.shard import KadShardStepper, arc_bounds, done_to_numpy, route_kad_local_shards
+    from oracle_lib import OracleNet, kad_params
+    world, n, m = 8, 1 << 22, 5_000
+    net = W.population(n, 193)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=3)
+    steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params) for r in range(world)]
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s = W.lookups(net.ids, m, 194 + r, node_ids=(r % 2 == 1))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k.view(np.int32)).to(dev))
+        ss.append(torch.from_numpy(s.view(np.int32)).to(dev))
+        qb.append(r * m)
+        allk.append(k); alls.append(s)
+    dones, rounds = route_kad_local_shards(steppers, ks, ss, qb)
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    ref = OracleNet("kademlia", net.ids, net.xy, kad_params(lookupParallelRpcs=3), lazy=True).route(
+        np.concatenate(allk), np.concatenate(alls), record_hops=False)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    assert sum(s.served for s in steppers) > world * m
