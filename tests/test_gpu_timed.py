@@ -76,16 +76,33 @@ def _chord_properties(out, ids, keys, src, label):
     assert np.all(out["latency_ns"] >= out["hops"].astype(np.int64) * 272000), label
 
 
+def _xor_closest(top, ktop):
+    """Index of the XOR-closest node to each key on the top 64 bits: a descent of the binary trie
+    over the sorted ids, taking the key's bit where some node continues the prefix."""
+    lo = np.zeros(len(ktop), dtype=np.int64)
+    hi = np.full(len(ktop), len(top), dtype=np.int64)
+    prefix = np.zeros(len(ktop), dtype=np.uint64)
+    for b in range(63, -1, -1):
+        bit = np.uint64(1) << np.uint64(b)
+        split = np.clip(np.searchsorted(top, prefix | bit, side="left"), lo, hi)
+        want = ((ktop >> np.uint64(b)) & np.uint64(1)).astype(bool)
+        nlo, nhi = np.where(want, split, lo), np.where(want, hi, split)
+        go = nlo < nhi
+        lo, hi = np.where(go, nlo, np.where(want, lo, split)), np.where(go, nhi, np.where(want, split, hi))
+        prefix |= np.where(go == want, bit, np.uint64(0))
+    return lo, hi - lo
+
+
 def _kad_properties(out, ids, keys, label):
     assert np.all(out["status"] == 0), f"{label}: failed lookups {np.bincount(out['status'])}"
-    # the result is the XOR-closest node to the key: one of its two neighbours in sorted order
-    top, ktop = _top64(ids), _top64(keys)
-    pos = np.searchsorted(top, ktop, side="left")
-    lo, hi = np.clip(pos - 1, 0, len(top) - 1), np.clip(pos, 0, len(top) - 1)
-    dlo, dhi = top[lo] ^ ktop, top[hi] ^ ktop
-    clear = dlo != dhi
-    best = np.where(dlo < dhi, lo, hi)
-    assert np.array_equal(out["responsible"][clear], best[clear].astype(np.uint32)), label
+    # the result is the XOR-closest node to the key (isSiblingFor(c, K, 1) holds only there: every
+    # closer node would lie inside c's sibling radius, Kademlia.cc:888-962); checked on a sample
+    # wherever the top 64 bits decide it
+    idx = np.arange(0, len(out), 13)[:300_000]
+    best, nbest = _xor_closest(_top64(ids), _top64(keys[idx]))
+    clear = nbest == 1
+    assert clear.mean() > 0.99
+    assert np.array_equal(out["responsible"][idx][clear], best[clear].astype(np.uint32)), label
 
 
 @pytest.mark.timeout(600)
