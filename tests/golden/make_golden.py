@@ -3,15 +3,17 @@
 Provenance: the reference (trucndt/oversim) needs OMNeT++ 4.x + INET and cannot
 be built in this image, and ships no routing fixtures.  These vectors are
 therefore produced by the CPU restatement in oracle/ (ovs_oracle.c) and, for
-every Chord case, re-derived independently by tests/refmodel.py before being
-written; a disagreement aborts generation.  They freeze the restated
+every case, re-derived independently by tests/refmodel.py before being written (Chord: a direct
+alpha = 1 loop; Kademlia: findNode on its own KadTables and the lookup as a message-level
+discrete-event simulation, KadLookupSim); a disagreement aborts generation.  They freeze the restated
 reference semantics so that regressions of either the oracle or the engine
 are caught.  Inputs (IDs, coordinates, keys, sources) come from the seeded
 generator in oversim_amd/workload.py; coordinates for N <= 15000 are records of
 the reference's simulations/nodes_2d_15000.xml.
 
 Each .npz records the SimTime rounding rule it was generated with.
-Run: python tests/golden/make_golden.py
+Run: python tests/golden/make_golden.py [--kad] [--rec] [--check: verify the committed Kademlia
+vectors instead of rewriting them]
 """
 from __future__ import annotations
 
@@ -96,7 +98,21 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
         fn_out[i, :len(res)] = res
         fn_sib[i] = flag
     r = o.route(k1, s1, record_hops=True, count_rpcs=True)
+    # the lookups restated twice: oracle event list vs refmodel's message-level simulation
+    sim = refmodel.KadLookupSim(tab, net.xy, alpha=alpha, rnd=bool(rnd), k=p.k)
+    for i in range(len(k1)):
+        mm = sim.run(k1[i], int(s1[i]))
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs"):
+            assert int(r[f][i]) == int(mm[f]), (name, i, f, r[f][i], mm[f])
+        assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == mm["hop_seq"], (name, i)
     H = int(r["hops"].max()) + 1
+    if "--check" in sys.argv:
+        g = np.load(HERE / f"{name}.npz")
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs", "fn_out", "fn_sib"):
+            assert np.array_equal(g[f], {**r, "fn_out": fn_out, "fn_sib": fn_sib}[f]), (name, f)
+        assert np.array_equal(g["hop_seq"], r["hop_seq"][:, :H]), name
+        print(name, "committed vectors reproduced")
+        return
     np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=k1, src=s1, alpha=np.int32(alpha),
                         responsible=r["responsible"], hops=r["hops"], status=r["status"],
                         one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"], rpcs=r["rpcs"],
@@ -111,6 +127,10 @@ if __name__ == "__main__":
     if "--rec" in sys.argv:
         chord_rec_case("chord_n1000_semirec", 1000, 0x4213, 2048, 2048, 1)
         chord_rec_case("chord_n1000_semirec_hcm4", 1000, 0x4214, 512, 512, 0, hcm=4)
+        sys.exit(0)
+    if "--check" in sys.argv:
+        kad_case("kad_n2000_a1", 2000, 0x4b41, 2048, 1)
+        kad_case("kad_n2000_a3", 2000, 0x4b41, 2048, 3)
         sys.exit(0)
     chord_case("chord_n1000_round", 1000, 0x4213, 4096, 4096, 1)
     chord_case("chord_n1000_trunc", 1000, 0x4213, 2048, 2048, 0)

@@ -274,3 +274,273 @@ class KadTables:
                 self._sorted_add(res, size, x, key)
             idx += 1
         return res
+
+
+# --- Kademlia iterative lookup as a discrete-event simulation --------------------------------
+class KadLookupSim:
+    """One KBRTestApp lookup over a Kademlia network, restated as OMNeT++ would run it: a future
+    event set ordered by (arrival time, insertion order), every message hop a separate event --
+    overlay -> UDP (zero delay), UDP -> UDP (SimpleNodeEntry::calcDelay with the sender's tx
+    queue), UDP -> overlay (zero delay) -- the RPC timeout scheduled before the call is sent
+    (BaseRpc.cc:256-271), the responder answering when its overlay handles the call
+    (BaseOverlay::findNodeRpc, BaseOverlay.cc:1841-1915).  The lookup itself follows
+    IterativeLookup / IterativePathLookup (IterativeLookup.cc:133-349, 406-449, 488-689,
+    786-1195) with parallelPaths = 1, failedNodeRpcs = false, no verify / majority siblings.
+
+    Independent of oracle/ovs_oracle.c, whose loop computes each response at send time and
+    orders pending events by (time, insertion time, sequence); this one simulates the messages.
+    findNode / isSiblingFor come from KadTables (another independent restatement)."""
+
+    def __init__(self, tables: "KadTables", xy, redundant=8, alpha=3, merge=True, strict=True, visit_once=True,
+                 accept_late_siblings=True, use_all=False, new_on_timeout=False, new_on_response=False,
+                 finish_on_first_unchanged=False, hop_max=50, rnd=True, rpc_timeout=1.5, lookup_timeout=10.0,
+                 datarate=10e6, k=8, call_bytes=83, resp_base=61, resp_node=26, route_bytes=186):
+        self.T, self.xy = tables, xy
+        self.cfg = dict(redundant=redundant, alpha=alpha, merge=merge, strict=strict, visit_once=visit_once,
+                        late=accept_late_siblings, use_all=use_all, new_to=new_on_timeout,
+                        new_resp=new_on_response, first_unch=finish_on_first_unchanged)
+        self.hop_max, self.rnd, self.k = hop_max, rnd, k
+        self.rpc_to, self.lk_to = simtime(rpc_timeout, rnd), simtime(lookup_timeout, rnd)
+        self.datarate = datarate
+        self.call_b, self.resp_b, self.resp_n, self.route_b = call_bytes, resp_base, resp_node, route_bytes
+
+    # SimpleNodeEntry::calcDelay (SimpleNodeEntry.cc:155-195); SimpleUDP: 0 to itself (SimpleUDP.cc:322)
+    def _delay(self, a, b, nbytes):
+        if a == b:
+            return 0
+        bw = simtime(nbytes * 8 / self.datarate, self.rnd)
+        fin = max(self.tx.get(a, 0), self.now) + bw
+        self.tx[a] = fin
+        return (fin - self.now) + coord_ns(self.xy, a, b, self.rnd) + bw
+
+    def _schedule(self, t, kind, data):
+        import heapq
+        self.ins += 1
+        heapq.heappush(self.fes, (t, self.ins, kind, data))
+
+    def _dist(self, x):
+        return self.T.ids[x] ^ self.key
+
+    # LookupVector::add (BaseKeySortedVector::add, NodeVector.h:432-512), entries [node, alreadyUsed]
+    def _nh_add(self, h):
+        cap, nh = self.cfg["redundant"], self.nh
+        if not self.cfg["merge"]:
+            nh.append([h, False])
+            return len(nh) - 1
+        d = self._dist(h)
+        if len(nh) == cap and not d <= self._dist(nh[-1][0]):
+            return -1
+        for i, e in enumerate(nh):
+            if self.T.ids[e[0]] == self.T.ids[h]:
+                return -1
+            if d < self._dist(e[0]):
+                nh.insert(i, [h, False])
+                del nh[cap:]
+                return i
+        nh.append([h, False])
+        return len(nh) - 1
+
+    def _add_sibling(self, h):
+        if len(self.siblings) < max(self.num_siblings, 1):       # parallelPaths 1: push_back if not full
+            self.siblings.append(h)
+
+    def _send_rpcs(self, num):
+        """IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)."""
+        c = self.cfg
+        if self.pfinished:
+            return
+        if self.hop_max and self.hops >= self.hop_max:
+            self.pfinished, self.psuccess = True, False
+            return
+        if c["strict"]:
+            num = min(num, c["alpha"] - self.pending)
+        if num == 0 and self.pending == 0 and not c["first_unch"]:
+            num = c["alpha"]
+        i = 0
+        while num > 0 and i < c["redundant"]:
+            i += 1
+            it = next((e for e in self.nh if not e[1] and e[0] not in self.dead), None)
+            if it is None:
+                break
+            if not c["visit_once"] or it[0] not in self.visited:
+                self.pending += 1
+                num -= 1
+                self._lookup_send(it[0], self.step)
+            it[1] = True
+        if self.pending == 0:
+            self.psuccess, self.pfinished = False, True
+
+    def _lookup_send(self, h, rpc_id):
+        """IterativeLookup::sendRpc (656-689) + BaseRpc::sendRpcCall: timeout first, then the call."""
+        if self.finished or not self.running:
+            return
+        if h not in self.rpcs:
+            self.rpcs[h] = []
+            self.nsent += 1
+            self.live.add(h)
+            self._schedule(self.now + self.rpc_to, "timeout", h)
+            self._schedule(self.now, "call_udp", h)
+        self.rpcs[h].append(rpc_id)
+
+    def _count_finished(self):
+        if self.pfinished and not self.counted:
+            self.counted = True
+            self.finished_paths += 1
+            self.min_hops = min(self.min_hops, self.hops)
+            self.successful_paths += 1 if self.psuccess else 0
+
+    def _path_timeout(self):
+        """IterativePathLookup::handleTimeout (935-1023), failedNodeRpcs = false."""
+        if self.pfinished:
+            return
+        self.pending -= 1
+        if self.now > self.lk_to:
+            self.pfinished, self.psuccess = True, False
+            return
+        if self.cfg["new_to"]:
+            self._send_rpcs(1)
+        elif self.pending == 0:
+            self._send_rpcs(self.cfg["alpha"])
+
+    def _path_response(self, src, closest, sib_flag):
+        """IterativePathLookup::handleResponse (803-921)."""
+        if self.pfinished:
+            return
+        if self.now > self.lk_to:
+            self.pfinished, self.psuccess = True, False
+            return
+        if src != self.S:
+            self.hops += 1
+            self.hop_seq.append(src)
+        self.visited.add(src)
+        self.step += 1
+        self.pending -= 1
+        if closest and not self.cfg["merge"]:
+            self.nh.clear()
+        new = 0
+        for h in closest:
+            pos = self._nh_add(h)
+            if 0 <= pos < self.cfg["redundant"]:
+                new += 1
+            if self.num_siblings and sib_flag:
+                self._add_sibling(h)
+        if sib_flag and closest and self.num_siblings:
+            self.pfinished, self.psuccess = True, True
+            return
+        if new == 0 and self.cfg["new_resp"]:
+            new = 1
+        self._send_rpcs(min(new, self.cfg["alpha"]))
+
+    def _check_stop(self):
+        """IterativeLookup::checkStop (295-349), numSiblings > 0, retries = 0."""
+        if (self.finished_paths == 1 and self.num_siblings > 0) or not self.rpcs:
+            self.success |= self.psuccess or self.successful_paths >= 1
+            self.running = False
+            self.finished = True
+            return True
+        return False
+
+    def run(self, key_words, S, num_siblings=1, lookup_call=False):
+        import heapq
+        self.key = to_int(key_words)
+        self.S, self.num_siblings = S, num_siblings
+        self.fes, self.ins, self.now, self.tx = [], 0, 0, {}
+        self.nh, self.visited, self.dead, self.rpcs, self.live = [], {S}, set(), {}, set()
+        self.siblings, self.hop_seq = [], []
+        self.hops = self.step = self.pending = 0
+        self.pfinished = self.psuccess = self.counted = False
+        self.finished, self.success, self.running = False, False, True
+        self.finished_paths = self.successful_paths = 0
+        self.min_hops, self.nsent = 1 << 30, 0
+        T = self.T
+        # IterativeLookup::start (133-244)
+        nxt = T.find_node(S, self.key, self.k, num_siblings)
+        done = False
+        if not nxt:
+            self.finished, self.success, done = True, False, True
+        elif num_siblings and T.is_sibling_for(S, self.key, num_siblings):
+            for h in nxt:
+                self._add_sibling(h)
+            self.finished = self.success = done = True
+        if not done:
+            for h in nxt:
+                self._nh_add(h)
+            self._send_rpcs(self.cfg["alpha"])
+            done = self._check_stop()
+        resp_of = {}
+        while not done and self.fes:
+            t, _, kind, h = heapq.heappop(self.fes)
+            self.now = t
+            if kind == "call_udp":            # source UDP: the call leaves through the tx queue
+                self._schedule(t + self._delay(S, h, self.call_b), "call_app_at", h)
+            elif kind == "call_app_at":       # responder UDP -> overlay (zero delay)
+                self._schedule(t, "call_rpc", h)
+            elif kind == "call_rpc":          # findNodeRpc at the responder
+                res = T.find_node(h, self.key, self.cfg["redundant"], num_siblings)
+                flag = T.is_sibling_for(h, self.key, num_siblings)
+                resp_of[h] = (res, flag)
+                self._schedule(t, "resp_udp", h)
+            elif kind == "resp_udp":          # responder UDP: response through its tx queue
+                self._schedule(t + self._delay(h, S, self.resp_b + self.resp_n * len(resp_of[h][0])), "resp_app_at", h)
+            elif kind == "resp_app_at":
+                self._schedule(t, "resp_rpc", h)
+            elif kind == "resp_rpc":          # BaseRpc: response before its timeout -> handleRpcResponse
+                if h not in self.live:
+                    continue
+                self.live.discard(h)
+                if self.finished or not self.running or h not in self.rpcs:
+                    continue
+                ids = self.rpcs.pop(h)
+                res, flag = resp_of[h]
+                handled = False
+                for rid in ids:
+                    if self.pfinished:
+                        continue
+                    acc = (self.cfg["use_all"] and self.cfg["merge"]) or rid == self.step
+                    if not handled and (acc or (flag and self.cfg["late"])):
+                        self._path_response(h, res, flag)
+                        handled = True
+                    else:
+                        self._path_timeout()
+                    self._count_finished()
+                done = self._check_stop()
+            elif kind == "timeout":           # BaseRpc timeout -> handleRpcTimeout (588-654)
+                if h not in self.live:
+                    continue
+                self.live.discard(h)
+                if self.finished or not self.running or h not in self.rpcs:
+                    continue
+                ids = self.rpcs.pop(h)
+                self.dead.add(h)
+                for _ in ids:
+                    if self.pfinished:
+                        continue
+                    self._path_timeout()
+                    self._count_finished()
+                done = self._check_stop()
+        if not done:
+            self._check_stop()
+        valid = self.success and self.finished
+        hops = 0 if self.min_hops == 1 << 30 else self.min_hops
+        if lookup_call:
+            return dict(siblings=list(self.siblings) if valid else [], hops=hops, status=self._status(valid),
+                        is_valid=int(valid), latency_ns=self.now if valid else -1, rpcs=self.nsent)
+        if not valid or not self.siblings:
+            return dict(responsible=0xFFFFFFFF, hops=hops, status=self._status(False), one_way_hops=0,
+                        latency_ns=-1, hop_seq=self.hop_seq, rpcs=self.nsent)
+        R = self.siblings[0]
+        # SendToKeyListener::lookupFinished -> sendRouteMessage (BaseOverlay.cc:1107-1146, 1241-1259)
+        lat = self.now + self._delay(S, R, self.route_b)
+        return dict(responsible=R, hops=hops, status=0, one_way_hops=hops + (R != S), latency_ns=lat,
+                    hop_seq=self.hop_seq, rpcs=self.nsent)
+
+    def _status(self, valid):
+        if valid:
+            return 0
+        if self.now > self.lk_to:
+            return 1
+        if self.dead:
+            return 2
+        if self.hop_max and self.hops >= self.hop_max:
+            return 3
+        return 4

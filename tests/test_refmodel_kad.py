@@ -1,0 +1,92 @@
+"""The two independent restatements of the Kademlia iterative lookup agree.
+
+oracle/ovs_oracle.c runs each lookup as a per-lookup event list that evaluates the responder's
+findNode when the call is sent; tests/refmodel.py (KadLookupSim) simulates every message hop
+through an OMNeT++-style future event set and evaluates findNode when the call arrives, on its
+own findNode / isSiblingFor (KadTables).  Both follow IterativeLookup.cc:133-349, 406-449,
+488-689, 786-1195; parameter variations push the alpha > 1 rules the round-1 golden vectors
+rested on a single reading of: accepts(step), late siblings, strictParallelRpcs, numNewRpcs,
+RPC timeouts / dead nodes, LOOKUP_TIMEOUT, same-instant tx serialisation.  CPU only.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import refmodel
+from oversim_amd import workload as W
+from oracle_lib import OracleNet, kad_params
+
+FIELDS = ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs")
+
+VARIANTS = {
+    "a1": dict(lookupParallelRpcs=1),
+    "a2": dict(lookupParallelRpcs=2),
+    "a3": dict(lookupParallelRpcs=3),
+    "a4_r4": dict(lookupParallelRpcs=4, lookupRedundantNodes=4),
+    "a3_useall": dict(lookupParallelRpcs=3, lookupUseAllParallelResponses=1),
+    "a3_nolate": dict(lookupParallelRpcs=3, lookupAcceptLateSiblings=0),
+    "a3_loose": dict(lookupParallelRpcs=3, lookupStrictParallelRpcs=0),
+    "a3_newresp": dict(lookupParallelRpcs=3, lookupNewRpcOnEveryResponse=1),
+    # RPC timeouts fire (RTTs up to ~1.3 s on these coordinates): dead nodes, handleTimeout
+    "a3_rpcto": dict(lookupParallelRpcs=3, rpcUdpTimeout=0.35),
+    "a3_rpcto_newto": dict(lookupParallelRpcs=3, rpcUdpTimeout=0.35, lookupNewRpcOnEveryTimeout=1),
+    "a2_lookupto": dict(lookupParallelRpcs=2, lookupTimeout=0.9),
+    "a3_hcm3": dict(lookupParallelRpcs=3, hopCountMax=3),
+    "a3_first": dict(lookupParallelRpcs=3, lookupFinishOnFirstUnchanged=1),
+    "a3_trunc": dict(lookupParallelRpcs=3, simtimeRound=0),
+}
+
+
+def _sim(o: OracleNet, net, p) -> refmodel.KadLookupSim:
+    sib, cnt, nodes = o.kad_tables()
+    tab = refmodel.KadTables(net.ids, sib, cnt, nodes, k=p.k, s=p.s)
+    return refmodel.KadLookupSim(
+        tab, net.xy, redundant=p.lookupRedundantNodes, alpha=p.lookupParallelRpcs, merge=bool(p.lookupMerge),
+        strict=bool(p.lookupStrictParallelRpcs), visit_once=bool(p.lookupVisitOnlyOnce),
+        accept_late_siblings=bool(p.lookupAcceptLateSiblings), use_all=bool(p.lookupUseAllParallelResponses),
+        new_on_timeout=bool(p.lookupNewRpcOnEveryTimeout), new_on_response=bool(p.lookupNewRpcOnEveryResponse),
+        finish_on_first_unchanged=bool(p.lookupFinishOnFirstUnchanged), hop_max=p.hopCountMax,
+        rnd=bool(p.simtimeRound), rpc_timeout=p.rpcUdpTimeout, lookup_timeout=p.lookupTimeout, k=p.k)
+
+
+@pytest.fixture(scope="module")
+def net():
+    return W.population(1500, 0x4b42)
+
+
+@pytest.mark.parametrize("name", list(VARIANTS))
+def test_one_way_lookups_agree(net, name):
+    p = kad_params(**VARIANTS[name])
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    k1, s1 = W.lookups(net.ids, 200, 11, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 200, 12, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    statuses = set()
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]))
+        for f in FIELDS:
+            assert int(r[f][i]) == int(m[f]), (name, i, f, int(r[f][i]), int(m[f]))
+        assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == m["hop_seq"], (name, i)
+        statuses.add(int(m["status"]))
+    if "rpcto" in name or "lookupto" in name or "hcm" in name:
+        assert statuses != {0}, f"{name}: the variant should exercise a failure path"
+
+
+@pytest.mark.parametrize("alpha,ns", [(1, 8), (3, 8), (3, 3)])
+def test_lookup_calls_agree(net, alpha, ns):
+    """KBRTestApp LookupCalls (numSiblings > 1): sibling vectors, hops, validity, duration."""
+    p = kad_params(lookupParallelRpcs=alpha)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    keys, src = W.lookups(net.ids, 300, 13 + alpha, node_ids=(ns == 8))
+    r = o.lookup_call(keys, src, ns)
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]), num_siblings=ns, lookup_call=True)
+        assert int(r["is_valid"][i]) == m["is_valid"], i
+        assert int(r["hops"][i]) == m["hops"], i
+        assert int(r["latency_ns"][i]) == m["latency_ns"], i
+        assert int(r["num_siblings"][i]) == len(m["siblings"]), i
+        assert [int(x) for x in r["siblings"][i][: len(m["siblings"])]] == m["siblings"], i

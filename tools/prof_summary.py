@@ -23,7 +23,7 @@ def main():
     out = []
     kt = d / "kt" / "run_results.db"
     if kt.exists():
-        out.append("# kernel trace (rocprofv3 --kernel-trace --stats): name, calls, total_ns, avg_ns, pct")
+        out.append("# kernel trace (rocprofv3 --kernel-trace --stats): name, calls, total_us, avg_us, pct (rocprofv3 stats table: microseconds)")
         for name, calls, tot, avg, pct in rows(kt, "select name,total_calls,total_duration,average,percentage "
                                                     "from top_kernels order by total_duration desc"):
             out.append(f"{name[:140]!s},{calls},{tot:.0f},{avg:.0f},{pct:.2f}")
@@ -33,6 +33,19 @@ def main():
         for r in info:
             if ksub in r[0]:
                 out.append(",".join(str(x) for x in (r[0][:100],) + r[1:]))
+        # per-dispatch durations of the kernel, in launch order: the bench's warm-up launches come
+        # first, so the mean of the last `--steps` dispatches is the figure comparable with its
+        # HIP-event kernel_ms
+        cols = [c[1] for c in rows(kt, "pragma table_info(kernels)")]
+        if ksub and "start" in cols and "end" in cols:
+            ds = [(e - s) * 1e-3 for nm, s, e in rows(kt, "select name, start, end from kernels order by start")
+                  if ksub in nm]
+            if ds:
+                out.append("# dispatches of the kernel (us, launch order): " + " ".join(f"{x:.1f}" for x in ds))
+                tail = ds[-5:]
+                out.append(f"# mean of the last {len(tail)} dispatches (us): {sum(tail) / len(tail):.1f}")
+        elif ksub:
+            out.append("# kernels table columns: " + " ".join(cols))
     for p in ("sq", "fetch", "write"):
         db = d / p / "run_results.db"
         if not db.exists():
