@@ -326,3 +326,41 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
     }
     return OVS_OK;
 }
+
+// defaults = the reference's default.ini values (host-only parameter handling, with the binder above)
+extern "C" void ovs_params_default(int32_t overlay, ovs_params* p)
+{
+    std::memset(p, 0, sizeof *p);
+    p->overlay = overlay;
+    p->keyLength = 160;                 // default.ini:393
+    p->hopCountMax = 50;                // default.ini:385
+    p->successorListSize = 8;           // default.ini:174
+    p->extendedFingerTable = 0;         // default.ini:176
+    p->numFingerCandidates = 3;         // default.ini:177
+    p->k = 8; p->s = 8; p->b = 1;       // default.ini:197-199
+    p->lookupParallelPaths = 1;
+    p->lookupStrictParallelRpcs = 1;    // default.ini:425-433
+    p->lookupVisitOnlyOnce = 1;
+    p->lookupAcceptLateSiblings = 1;
+    p->numSiblings = 1;                 // BaseOverlay::route -> sendToKey(..., 1, ...) (BaseOverlay.cc:1357)
+    p->useCoordinateBasedDelay = 1;     // default.ini:546
+    p->simtimeRound = 1;
+    p->testMsgSize = 100;               // default.ini:37
+    p->recNumRedundantNodes = 3;        // default.ini:386
+    p->rpcUdpTimeout = 1.5;             // default.ini:483
+    p->lookupTimeout = 10.0;            // IterativeLookup.h:44
+    p->jitter = 0.0;                    // default.ini:549 has 0.1; bit-exact latency needs 0
+    p->constantDelay = 0.05;            // default.ini:544
+    p->datarate = 10e6;                 // channels.ned simple_ethernetline
+    p->accessDelay = 0.0;
+    p->kadSeed = 0x4b41444dull;
+    if (overlay == OVS_OVERLAY_KADEMLIA) {
+        p->lookupRedundantNodes = 8;    // default.ini:186
+        p->lookupParallelRpcs = 3;      // default.ini:188
+        p->lookupMerge = 1;             // default.ini:189
+    } else {
+        p->lookupRedundantNodes = 1;    // default.ini:423
+        p->lookupParallelRpcs = 1;      // default.ini:425
+        p->lookupMerge = 0;             // default.ini:428
+    }
+}
