@@ -148,9 +148,22 @@ ovs_status  ovs_chord_load_tables(ovs_ctx* ctx, const ovs_key160* ids_sorted, ui
                                   const double* xy, const uint32_t* pred, const uint32_t* succ,
                                   const uint8_t* nsucc, const uint32_t* fingers,
                                   const uint8_t* deque_size, uint32_t flags);
-/* Kademlia snapshot (DESIGN.md "Kademlia snapshot rule"), built on the device. */
+/* Kademlia snapshot (DESIGN.md "Kademlia snapshot rule": the converged tables a stable network
+ * ends up with), built on the device.  Replaces Kademlia's join / routingAdd / bucket refresh
+ * history for a NoChurn network; ovs_kad_load_tables imports the tables of a running one. */
 ovs_status  ovs_kad_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n,
                          const double* xy, uint32_t flags);
+/* Explicit Kademlia tables -- the k-buckets and sibling tables an OverSim node actually holds
+ * (Kademlia::siblingTable / routingTable, Kademlia.cc:179, 432-756; KademliaBucket.h:30-69).
+ * siblings[n*5s]: node v's sibling table (0xFFFFFFFF padded; any order -- the reference keeps it
+ * XOR-sorted, its back() is the farthest); bucket_count[n*160], bucket_nodes[n*160*k]: routing
+ * bucket i of node v (0xFFFFFFFF padded; LRU order, findNode re-sorts by XOR distance).  The
+ * tables must keep routingAdd's invariants: members are other nodes of [0, n), a bucket i holds
+ * only nodes x with msb(x ^ v) = i and at most k of them, no node twice, no node both sibling and
+ * bucket member -- else OVS_EINVAL naming the node.  Host buffers. */
+ovs_status  ovs_kad_load_tables(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n, const double* xy,
+                                const uint32_t* siblings, const uint8_t* bucket_count,
+                                const uint32_t* bucket_nodes, uint32_t flags);
 /* copy the device Kademlia tables out (host buffers): siblings[n*5s],
  * bucket_count[n*160], bucket_nodes[n*160*k] (0xFFFFFFFF padded) */
 ovs_status  ovs_kad_export(ovs_ctx* ctx, uint32_t* siblings, uint8_t* bucket_count,

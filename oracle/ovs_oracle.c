@@ -875,6 +875,42 @@ orc_net* orc_kad_build_lazy(const orc_key* ids, uint32_t n, const double* xy, co
     return kad_build(ids, n, xy, p, 1);
 }
 
+/* Explicit tables (a running network's k-buckets): the sibling table is kept XOR-sorted to the
+ * node as Kademlia::siblingTable is (KademliaBucket with KeyDistanceComparator<KeyXorMetric>,
+ * Kademlia.cc:315-317), so back() is its farthest entry; buckets keep the caller's (LRU) order. */
+orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, const uint32_t* siblings,
+                              const uint8_t* bucket_count, const uint32_t* bucket_nodes, const orc_params* p)
+{
+    if (p->b != 1) { set_err("kademlia: only b=1 supported"); return NULL; }
+    if (!check_params(p)) return NULL;
+    orc_net* net = net_alloc(NET_KAD, ids, n, xy, p);
+    if (!net) return NULL;
+    int k = p->k, sibCap = 5 * p->s;
+    net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
+    net->nsib = (uint8_t*)calloc(n, 1);
+    net->bucket = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160 * k);
+    net->bcount = (uint8_t*)calloc((size_t)n * 160, 1);
+    for (uint32_t v = 0; v < n; ++v) {
+        NVec sib; nv_init(&sib, sibCap, 1, &net->ids[v]);
+        for (int i = 0; i < sibCap; ++i) {
+            uint32_t x = siblings[(size_t)v * sibCap + i];
+            if (x == NONE) continue;
+            if (x >= n) { set_err("sibling index out of range"); orc_net_free(net); return NULL; }
+            nv_add(net, &sib, x);
+        }
+        net->nsib[v] = (uint8_t)sib.size;
+        for (int i = 0; i < sibCap; ++i) net->sib[(size_t)v * sibCap + i] = i < sib.size ? sib.v[i] : NONE;
+        for (int m = 0; m < 160; ++m) {
+            int c = bucket_count[(size_t)v * 160 + m];
+            if (c > k) { set_err("bucket holds more than k entries"); orc_net_free(net); return NULL; }
+            net->bcount[(size_t)v * 160 + m] = (uint8_t)c;
+            for (int q = 0; q < k; ++q)
+                net->bucket[((size_t)v * 160 + m) * k + q] = q < c ? bucket_nodes[((size_t)v * 160 + m) * k + q] : NONE;
+        }
+    }
+    return net;
+}
+
 void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes)
 {
     size_t sc = (size_t)5 * net->p.s, k = (size_t)net->p.k;

@@ -95,6 +95,10 @@ orc_net* orc_kad_build(const orc_key* ids, uint32_t n, const double* xy, const o
  * configs D (2^26-node Chord) and E (2^24-node Kademlia) can be checked. */
 orc_net* orc_chord_build_lazy(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
 orc_net* orc_kad_build_lazy(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
+/* Explicit Kademlia tables: siblings[n*5s] (UINT32_MAX padded, any order: kept XOR-sorted like
+ * Kademlia::siblingTable), bucket_count[n*160], bucket_nodes[n*160*k] (routingTable buckets). */
+orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, const uint32_t* siblings,
+                              const uint8_t* bucket_count, const uint32_t* bucket_nodes, const orc_params* p);
 void     orc_net_free(orc_net* net);
 
 /* export the Kademlia snapshot so the GPU builder can be checked:

@@ -1,70 +1,102 @@
 // kad.hpp -- Kademlia device tables and launchers (internal).
+//
+// Layout (one HBM line = 64 B is the unit every table is cut to):
+//  KadNode nodes[n]   one line per node: everything the *sender* of a FindNodeCall needs of its
+//                     target (key, coordinates, isSiblingFor summary, bucket-row offset), read
+//                     once per RPC when the call is sent
+//  KadX    nodex[n]   the exact sibling radius R and level mask (fallback on summary ties, rare)
+//  KadLine lines[]    bucket rows and sibling rows as lines of 5 entries (top 64 bits of the
+//                     member key + member index); slot of bucket m of node v = ceil(k/5) lines at
+//                     nodes[v].boff + (159 - m) * lps, for m = rowlo(v) .. 159; sibling row of an
+//                     owned node v = ceil(5s/5) lines at sib_base + (v - lo) * sln
+// The reference's structures these hold: Kademlia::siblingTable (a KademliaBucket of 5s entries
+// sorted by XOR distance to this node, Kademlia.cc:179, 315-317) and routingTable[160] (buckets
+// of up to k entries in LRU order, KademliaBucket.h:30-69, filled by routingAdd 432-756).
 #pragma once
 #include "engine.hpp"
 
 namespace ovs {
 
-// 64 B node record of the Kademlia snapshot (one HBM line per responder visit):
-//  key   : node id
-//  R     : key ^ back(siblingTable)  -- the sibling radius; isSiblingFor's
-//          "(self ^ key) > (self ^ back)" test (Kademlia.cc:923-935)
-//  mask  : OR over siblings s of 2^msb(s ^ key) -- with it, "self is the
-//          XOR-closest of siblings + self" is (D & mask) == 0 for D = self ^ lookup key
-//  boff  : first bucket slot of the node's row; slot s <-> bucket m = 159 - s,
-//          for m = 159 .. endIndex = msb(R) (buckets below endIndex are all siblings)
-struct alignas(16) KadRec {
+// meta bits of KadNode
+constexpr uint32_t KMETA_MASK_OUT = 1u << 24;   // level-mask bits below the 64-bit window: exact check
+struct alignas(64) KadNode {
     uint32_t key[5];
+    uint32_t boff;     // first line of the bucket row
+    double x, y;       // SimpleUnderlay coordinates
+    uint64_t rtop;     // top64(R), R = key ^ back(siblingTable) = max over siblings of (s ^ key)
+    uint64_t mwin;     // level mask bits [mlo, mlo + 63], mlo = max(endIndex - 63, 0); level mask =
+                       // OR over siblings s of 2^msb(s ^ key): this node is the XOR-closest of
+                       // siblings + itself to D = key ^ K  <=>  (D & mask) == 0
+    uint32_t meta;     // endIndex + 1 (bits 0-7, 0 = no siblings), rowlo + 1 (8-15, 0 = no row),
+                       // nsib (16-23), KMETA_* flags (24-31)
+    uint32_t spare;
+};
+static_assert(sizeof(KadNode) == 64, "KadNode is one 64 B line");
+
+struct KadX {
     uint32_t R[5];
     uint32_t mask[5];
-    uint32_t boff;
 };
-static_assert(sizeof(KadRec) == 64, "KadRec must be one 64 B line");
 
-// bucket entry with the member's key inline (24 B); a slot holds k entries,
-// NONE idx marks an empty entry (entries are packed at the front)
-struct KadEntry {
-    uint32_t key[5];
-    uint32_t idx;
+constexpr int KLINE = 5;   // entries per line
+struct alignas(64) KadLine {
+    uint64_t top[KLINE];   // top 64 bits (bits 96..159) of the member key; ~0 for an empty entry
+    uint32_t idx[KLINE];   // member node index; NONE for an empty entry (entries packed at the front)
+    uint32_t pad;
 };
+static_assert(sizeof(KadLine) == 64, "KadLine is one 64 B line");
+
+__host__ __device__ __forceinline__ int kad_end(uint32_t meta) { return (int)(meta & 0xFFu) - 1; }
+__host__ __device__ __forceinline__ int kad_rowlo(uint32_t meta) { return (int)((meta >> 8) & 0xFFu) - 1; }
+__host__ __device__ __forceinline__ int kad_nsib(uint32_t meta) { return (int)((meta >> 16) & 0xFFu); }
 
 struct KadTables {
-    KadRec* recs = nullptr;
-    uint32_t* sib = nullptr;      // n * S5 member indices (unordered set), NONE padded
-    KadEntry* sibe = nullptr;     // n * S5 sibling entries with the member key inline
-    KadEntry* slots = nullptr;    // total_slots * k
-    uint64_t total_slots = 0;
-    uint32_t lo = 0, hi = 0;      // sib / sibe / bucket rows exist for nodes [lo, hi) (the whole ring unsharded)
+    KadNode* nodes = nullptr;
+    KadX* nodex = nullptr;
+    KadLine* lines = nullptr;      // bucket rows (rows_lines lines), then the sibling rows of the owned arc
+    uint64_t rows_lines = 0;       // bucket-row lines; sibling rows start here
+    uint32_t* sib = nullptr;       // (hi - lo) * S5 sibling member indices of the owned arc, NONE padded (export)
+    uint32_t lo = 0, hi = 0;       // sibling / bucket rows exist for nodes [lo, hi) (the whole network unsharded)
     int k = 8, s = 8;
     uint64_t seed = 0;
-    int exact = 1;                // two IDs share their top 63 bits: K2 uses the 160-bit tie fallback
+    int exact = 1;                 // two IDs share their top 63 bits: comparisons use the 160-bit tie fallback
+    int snapshot = 1;              // 0: explicit tables (ovs_kad_load_tables)
+    int maybe_short = 0;           // explicit tables: some node may answer fewer than resultSize nodes
 };
 
 struct KadView {
-    const KadRec* __restrict__ recs;
+    const KadNode* __restrict__ nodes;
+    const KadX* __restrict__ nodex;
+    const KadLine* __restrict__ lines;
+    const KadLine* __restrict__ sibl;   // sibling rows of the owned arc
     const double2* __restrict__ xy;
-    const uint32_t* __restrict__ sib;
-    const KadEntry* __restrict__ sibe;
-    const KadEntry* __restrict__ slots;
     uint32_t n;
     int k;
+    int lps;      // lines per bucket slot = ceil(k / 5)
     int S5;       // sibling table capacity 5s
-    int nsib;     // entries in every sibling table = min(5s, n-1)
+    int sln;      // lines per sibling row = ceil(5s / 5)
     uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)
+    int maybe_short;
+    int snapshot;      // tables built by the snapshot rule (ovs_kad_load), not imported
 };
 
 void kad_free(KadTables& t);
-// tables for nodes [lo, hi) of the sorted ring (node records for all n)
-hipError_t kad_build(const KeyRec* recs, uint32_t n, int k, int s, uint64_t seed, KadTables& t, hipStream_t st,
-                     uint32_t lo = 0, uint32_t hi = 0xFFFFFFFFu);
+// snapshot tables for nodes [lo, hi) of the sorted ring (node records for all n)
+hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, uint64_t seed, KadTables& t,
+                     hipStream_t st, uint32_t lo = 0, uint32_t hi = 0xFFFFFFFFu);
+// explicit tables (device copies of the caller's siblings / bucket members); returns
+// hipErrorInvalidValue with *bad_node set when a table breaks the reference's invariants
+hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, const uint32_t* sib,
+                              const uint8_t* bcount, const uint32_t* bnodes, KadTables& t, uint32_t* bad_node,
+                              uint32_t* bad_code, hipStream_t st);
 hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_t* bucket_count,
                       uint32_t* bucket_nodes, hipStream_t st);
-hipError_t kad_route(const KadTables& t, const KeyRec* recs, const double2* xy, uint32_t n, const ovs_params& P,
+hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
                      ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st,
                      uint32_t* sibs = nullptr);
-hipError_t kad_find_node(const KadTables& t, const KeyRec* recs, uint32_t n, const ovs_params& P,
-                         const uint32_t* node, const K160* keys, uint64_t nq, int numRedundant, int numSiblings,
-                         uint32_t* out_nodes, uint32_t max_out, uint8_t* out_count, uint8_t* out_sib,
-                         hipStream_t st);
+hipError_t kad_find_node(const KadTables& t, uint32_t n, const ovs_params& P, const uint32_t* node, const K160* keys,
+                         uint64_t nq, int numRedundant, int numSiblings, uint32_t* out_nodes, uint32_t max_out,
+                         uint8_t* out_count, uint8_t* out_sib, hipStream_t st);
 
 }  // namespace ovs

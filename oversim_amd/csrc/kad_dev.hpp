@@ -1,6 +1,7 @@
-// kad_dev.hpp -- Kademlia device building blocks shared by the single-GPU kernel (kad.hip)
-// and the sharded request/response kernels (kad_shard.hip): record loads, sorted vectors,
-// isSiblingFor / findNode from the snapshot tables, and the IterativePathLookup state machine.
+// kad_dev.hpp -- Kademlia device building blocks shared by the single-GPU kernels (kad.hip)
+// and the sharded request/response kernels (kad_shard.hip): node / line loads, sorted vectors,
+// isSiblingFor / findNode from the tables (kad.hpp), and the IterativePathLookup state machine
+// in its synchronous (one call = one event) form used by the sharded path.
 #pragma once
 #include "kad.hpp"
 
@@ -13,24 +14,43 @@ __device__ __forceinline__ uint32_t kbit(const K160& k, int b) { return (k.w[b >
 
 __device__ __forceinline__ K160 kload(const KeyRec* __restrict__ recs, uint32_t i) { return key_of(load_rec(recs, i)); }
 
-__device__ __forceinline__ K160 kad_key(const KadRec* __restrict__ r, uint32_t i)
+__device__ __forceinline__ K160 node_key(const KadNode* __restrict__ nodes, uint32_t i)
 {
-    const uint4* p = reinterpret_cast<const uint4*>(r + i);
-    const uint4 a = p[0];
+    const uint4* p = reinterpret_cast<const uint4*>(nodes + i);
+    const uint4 a = p[0], b = p[1];
     K160 k;
-    k.w[0] = a.x; k.w[1] = a.y; k.w[2] = a.z; k.w[3] = a.w; k.w[4] = r[i].key[4];
+    k.w[0] = a.x; k.w[1] = a.y; k.w[2] = a.z; k.w[3] = a.w; k.w[4] = b.x;
     return k;
 }
 
-__device__ __forceinline__ KadRec kad_rec(const KadRec* __restrict__ r, uint32_t i)
+__device__ __forceinline__ KadNode load_node(const KadNode* __restrict__ nodes, uint32_t i)
 {
-    const uint4* p = reinterpret_cast<const uint4*>(r + i);
+    const uint4* p = reinterpret_cast<const uint4*>(nodes + i);
     const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-    KadRec o;
+    KadNode o;
     o.key[0] = a.x; o.key[1] = a.y; o.key[2] = a.z; o.key[3] = a.w; o.key[4] = b.x;
-    o.R[0] = b.y; o.R[1] = b.z; o.R[2] = b.w; o.R[3] = c.x; o.R[4] = c.y;
-    o.mask[0] = c.z; o.mask[1] = c.w; o.mask[2] = d.x; o.mask[3] = d.y; o.mask[4] = d.z;
-    o.boff = d.w;
+    o.boff = b.y;
+    o.x = __hiloint2double((int)b.w, (int)b.z);
+    o.y = __hiloint2double((int)c.y, (int)c.x);
+    o.rtop = (uint64_t)c.z | ((uint64_t)c.w << 32);
+    o.mwin = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    o.meta = d.z;
+    o.spare = d.w;
+    return o;
+}
+
+// a KadNode from the four 16 B chunks of its line (the cooperative gather of kad.hip)
+__device__ __forceinline__ KadNode node_from_line(uint4 a, uint4 b, uint4 c, uint4 d)
+{
+    KadNode o;
+    o.key[0] = a.x; o.key[1] = a.y; o.key[2] = a.z; o.key[3] = a.w; o.key[4] = b.x;
+    o.boff = b.y;
+    o.x = __hiloint2double((int)b.w, (int)b.z);
+    o.y = __hiloint2double((int)c.y, (int)c.x);
+    o.rtop = (uint64_t)c.z | ((uint64_t)c.w << 32);
+    o.mwin = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    o.meta = d.z;
+    o.spare = d.w;
     return o;
 }
 
@@ -64,27 +84,35 @@ __device__ __forceinline__ uint64_t kad_hash(uint64_t seed, uint32_t node, uint3
     return splitmix64(seed ^ splitmix64(((uint64_t)node << 32) ^ ((uint64_t)m << 16) ^ (uint64_t)j));
 }
 
-
 // ---------------------------------------------------------------------------
-// sorted vectors in registers (static indexing only)
-
-// XOR-distance order of node a vs node b to key K: top 64 bits, exact fallback on ties
-__device__ __forceinline__ bool closer(uint64_t da, uint32_t ia, uint64_t db, uint32_t ib, const K160& K,
-                                       const KadRec* __restrict__ recs)
-{
-    if (da != db) return da < db;
-    const K160 xa = k_xor(kad_key(recs, ia), K), xb = k_xor(kad_key(recs, ib), K);
-    return k_lt(xa, xb);
-}
+// XOR distances: ordered by their top 64 bits, exact 160-bit fallback on ties
 
 // top 64 bits of the XOR distance, clamped below the empty-entry sentinel ~0 (a real distance
-// of ~0 becomes ~0 - 1: ordered before every empty entry, and with KadView::exact == 0 still
+// of ~0 becomes ~0 - 1: ordered before every empty entry, and with KadTables::exact == 0 still
 // unique, as no two node IDs then share their top 63 bits)
 __device__ __forceinline__ uint64_t dclamp(uint64_t d) { return d == ~0ull ? ~0ull - 1 : d; }
 
-__device__ __forceinline__ uint64_t dist_hi(const K160& x, const K160& K)
+__device__ __forceinline__ uint64_t ktop(const K160& x) { return ((uint64_t)x.w[4] << 32) | (uint64_t)x.w[3]; }
+
+__device__ __forceinline__ uint64_t dist_hi(const K160& x, const K160& K) { return dclamp(ktop(x) ^ ktop(K)); }
+
+// XOR distances of distinct nodes to one key are distinct (XOR is a bijection); their top 64
+// bits can tie only when the two node IDs share their top 64 bits.  EX = false is used when the
+// build found no two IDs sharing their top 63 bits (KadTables::exact == 0): the one 64-bit
+// compare is then exact and branch-free.  EX = true keeps the 160-bit fallback on ties.
+template <bool EX>
+__device__ __forceinline__ bool cand_lt(uint64_t da, uint32_t ia, uint64_t db, uint32_t ib, const K160& K,
+                                        const KadNode* __restrict__ nodes)
 {
-    return dclamp(((uint64_t)(x.w[4] ^ K.w[4]) << 32) | (uint64_t)(x.w[3] ^ K.w[3]));
+    if constexpr (!EX) {
+        (void)ia; (void)ib; (void)K; (void)nodes;
+        return da < db;
+    }
+    if (da != db) return da < db;
+    if (ia == ib || ia == NONE) return false;
+    if (ib == NONE) return true;
+    const K160 xa = k_xor(node_key(nodes, ia), K), xb = k_xor(node_key(nodes, ib), K);   // rare
+    return k_lt(xa, xb);
 }
 
 template <int CAP>
@@ -104,63 +132,13 @@ __device__ __forceinline__ void svec_clear(SVec<CAP>& v)
     for (int i = 0; i < CAP; ++i) { v.idx[i] = NONE; v.d[i] = ~0ull; }
 }
 
-// BaseKeySortedVector::add with a KeyDistanceComparator<KeyXorMetric> (NodeVector.h:381-512):
-// dedupe by key (== by node index), insert before the first farther entry, truncate to cap.
-template <int CAP>
-__device__ __forceinline__ int svec_add(SVec<CAP>& v, int cap, uint32_t x, uint64_t dx, const K160& K,
-                                        const KadRec* __restrict__ recs)
-{
-    bool dup = false;
-    int pos = 0;
-#pragma unroll
-    for (int i = 0; i < CAP; ++i) {
-        if (i < v.n) {
-            dup |= (v.idx[i] == x);
-            pos += (v.idx[i] != x && closer(v.d[i], v.idx[i], dx, x, K, recs)) ? 1 : 0;
-        }
-    }
-    if (dup || pos >= cap) return -1;
-    const uint32_t lowmask = (1u << pos) - 1u;
-    v.used = ((v.used & lowmask) | ((v.used & ~lowmask) << 1)) & ((1u << cap) - 1u);
-#pragma unroll
-    for (int i = CAP - 1; i >= 0; --i) {
-        if (i > pos) {
-            if (i >= 1) { v.idx[i] = v.idx[i - 1]; v.d[i] = v.d[i - 1]; }
-        } else if (i == pos) {
-            v.idx[i] = x; v.d[i] = dx;
-        }
-    }
-    v.n = v.n + 1 > cap ? cap : v.n + 1;
-    return pos;
-}
-
 // ---------------------------------------------------------------------------
 // Sorting networks over 8 (distance, node) pairs.  The findNode result and the LookupVector
-// are "the cap XOR-closest distinct nodes seen" -- BaseKeySortedVector::add applied to a
-// sequence of candidates yields exactly that set in distance order, whatever the order of
-// the adds -- so instead of one insertion per candidate (an 8-step compare + shift each), a
-// block of 8 candidates is sorted with a 19-comparator network and merged into the running
-// top 8 with a bitonic merge (8 min + 12 comparators).  Empty entries are (~0, NONE) and
-// sort last; equal top-64-bit distances fall back to the exact 160-bit compare.
-
-// XOR distances of distinct nodes to one key are distinct (XOR is a bijection); their top 64
-// bits can tie only when the two node IDs share their top 64 bits.  EX = false is used when the
-// build found no two IDs sharing their top 63 bits (KadTables::exact == 0): the one 64-bit
-// compare is then exact and branch-free.  EX = true keeps the 160-bit fallback on ties.
-template <bool EX>
-__device__ __forceinline__ bool cand_lt(uint64_t da, uint32_t ia, uint64_t db, uint32_t ib, const K160& K,
-                                        const KadRec* __restrict__ recs)
-{
-    if constexpr (!EX) {
-        (void)ia; (void)ib; (void)K; (void)recs;
-        return da < db;
-    }
-    if (da != db) return da < db;
-    if (ia == ib || ia == NONE) return false;
-    if (ib == NONE) return true;
-    const K160 xa = k_xor(kad_key(recs, ia), K), xb = k_xor(kad_key(recs, ib), K);   // rare
-    return k_lt(xa, xb);
-}
+// are "the cap XOR-closest distinct nodes seen" -- BaseKeySortedVector::add (NodeVector.h:
+// 381-512) applied to a sequence of candidates yields exactly that set in distance order,
+// whatever the order of the adds -- so a block of candidates is sorted with a 19-comparator
+// network and merged into the running top 8 with a bitonic merge (8 min + 12 comparators).
+// Empty entries are (~0, NONE) and sort last.
 
 struct Blk8 {
     uint64_t d[8];
@@ -169,9 +147,9 @@ struct Blk8 {
 };
 
 template <bool F, bool EX>
-__device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, const KadRec* __restrict__ recs)
+__device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, const KadNode* __restrict__ nodes)
 {
-    const bool s = cand_lt<EX>(b.d[j], b.x[j], b.d[i], b.x[i], K, recs);
+    const bool s = cand_lt<EX>(b.d[j], b.x[j], b.d[i], b.x[i], K, nodes);
     const uint64_t di = s ? b.d[j] : b.d[i], dj = s ? b.d[i] : b.d[j];
     const uint32_t xi = s ? b.x[j] : b.x[i], xj = s ? b.x[i] : b.x[j];
     b.d[i] = di; b.d[j] = dj; b.x[i] = xi; b.x[j] = xj;
@@ -183,31 +161,31 @@ __device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, con
 
 // Batcher odd-even merge sort, 19 comparators
 template <bool F, bool EX>
-__device__ __forceinline__ void blk_sort8(Blk8& b, const K160& K, const KadRec* __restrict__ recs)
+__device__ __forceinline__ void blk_sort8(Blk8& b, const K160& K, const KadNode* __restrict__ nodes)
 {
-    blk_ce<F, EX>(b, 0, 1, K, recs); blk_ce<F, EX>(b, 2, 3, K, recs); blk_ce<F, EX>(b, 4, 5, K, recs); blk_ce<F, EX>(b, 6, 7, K, recs);
-    blk_ce<F, EX>(b, 0, 2, K, recs); blk_ce<F, EX>(b, 1, 3, K, recs); blk_ce<F, EX>(b, 4, 6, K, recs); blk_ce<F, EX>(b, 5, 7, K, recs);
-    blk_ce<F, EX>(b, 1, 2, K, recs); blk_ce<F, EX>(b, 5, 6, K, recs);
-    blk_ce<F, EX>(b, 0, 4, K, recs); blk_ce<F, EX>(b, 1, 5, K, recs); blk_ce<F, EX>(b, 2, 6, K, recs); blk_ce<F, EX>(b, 3, 7, K, recs);
-    blk_ce<F, EX>(b, 2, 4, K, recs); blk_ce<F, EX>(b, 3, 5, K, recs);
-    blk_ce<F, EX>(b, 1, 2, K, recs); blk_ce<F, EX>(b, 3, 4, K, recs); blk_ce<F, EX>(b, 5, 6, K, recs);
+    blk_ce<F, EX>(b, 0, 1, K, nodes); blk_ce<F, EX>(b, 2, 3, K, nodes); blk_ce<F, EX>(b, 4, 5, K, nodes); blk_ce<F, EX>(b, 6, 7, K, nodes);
+    blk_ce<F, EX>(b, 0, 2, K, nodes); blk_ce<F, EX>(b, 1, 3, K, nodes); blk_ce<F, EX>(b, 4, 6, K, nodes); blk_ce<F, EX>(b, 5, 7, K, nodes);
+    blk_ce<F, EX>(b, 1, 2, K, nodes); blk_ce<F, EX>(b, 5, 6, K, nodes);
+    blk_ce<F, EX>(b, 0, 4, K, nodes); blk_ce<F, EX>(b, 1, 5, K, nodes); blk_ce<F, EX>(b, 2, 6, K, nodes); blk_ce<F, EX>(b, 3, 7, K, nodes);
+    blk_ce<F, EX>(b, 2, 4, K, nodes); blk_ce<F, EX>(b, 3, 5, K, nodes);
+    blk_ce<F, EX>(b, 1, 2, K, nodes); blk_ce<F, EX>(b, 3, 4, K, nodes); blk_ce<F, EX>(b, 5, 6, K, nodes);
 }
 
 // a <- the 8 smallest of sorted a and sorted b, sorted
 template <bool F, bool EX>
-__device__ __forceinline__ void blk_merge_top8(Blk8& a, const Blk8& b, const K160& K, const KadRec* __restrict__ recs)
+__device__ __forceinline__ void blk_merge_top8(Blk8& a, const Blk8& b, const K160& K, const KadNode* __restrict__ nodes)
 {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const bool s = cand_lt<EX>(b.d[7 - i], b.x[7 - i], a.d[i], a.x[i], K, recs);
+        const bool s = cand_lt<EX>(b.d[7 - i], b.x[7 - i], a.d[i], a.x[i], K, nodes);
         a.d[i] = s ? b.d[7 - i] : a.d[i];
         a.x[i] = s ? b.x[7 - i] : a.x[i];
         if (F) a.f[i] = s ? b.f[7 - i] : a.f[i];
     }
     // a is bitonic: half-cleaners at distance 4, 2, 1
-    blk_ce<F, EX>(a, 0, 4, K, recs); blk_ce<F, EX>(a, 1, 5, K, recs); blk_ce<F, EX>(a, 2, 6, K, recs); blk_ce<F, EX>(a, 3, 7, K, recs);
-    blk_ce<F, EX>(a, 0, 2, K, recs); blk_ce<F, EX>(a, 1, 3, K, recs); blk_ce<F, EX>(a, 4, 6, K, recs); blk_ce<F, EX>(a, 5, 7, K, recs);
-    blk_ce<F, EX>(a, 0, 1, K, recs); blk_ce<F, EX>(a, 2, 3, K, recs); blk_ce<F, EX>(a, 4, 5, K, recs); blk_ce<F, EX>(a, 6, 7, K, recs);
+    blk_ce<F, EX>(a, 0, 4, K, nodes); blk_ce<F, EX>(a, 1, 5, K, nodes); blk_ce<F, EX>(a, 2, 6, K, nodes); blk_ce<F, EX>(a, 3, 7, K, nodes);
+    blk_ce<F, EX>(a, 0, 2, K, nodes); blk_ce<F, EX>(a, 1, 3, K, nodes); blk_ce<F, EX>(a, 4, 6, K, nodes); blk_ce<F, EX>(a, 5, 7, K, nodes);
+    blk_ce<F, EX>(a, 0, 1, K, nodes); blk_ce<F, EX>(a, 2, 3, K, nodes); blk_ce<F, EX>(a, 4, 5, K, nodes); blk_ce<F, EX>(a, 6, 7, K, nodes);
 }
 
 __device__ __forceinline__ void blk_clear(Blk8& b)
@@ -216,22 +194,25 @@ __device__ __forceinline__ void blk_clear(Blk8& b)
     for (int i = 0; i < 8; ++i) { b.d[i] = ~0ull; b.x[i] = NONE; b.f[i] = 0; }
 }
 
-// up to 8 entries of a contiguous KadEntry array (bucket slot / sibling block), unsorted
-__device__ __forceinline__ void blk_load(Blk8& b, const KadEntry* __restrict__ s, int cnt, const K160& K)
+// the (up to 5) entries of one table line, unsorted, in slots 0..4 of b; returns how many
+__device__ __forceinline__ int blk_load_line(Blk8& b, const KadLine* __restrict__ l, const K160& K)
 {
+    const uint64_t kt = ktop(K);
+    int n = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        if (q < cnt) {
-            const uint2* p = reinterpret_cast<const uint2*>(s + q);
-            const uint2 bb = p[1], c = p[2];
-            b.x[q] = c.y;
-            b.d[q] = c.y == NONE ? ~0ull : dclamp(((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(bb.y ^ K.w[3]));
+        if (q < KLINE) {
+            const uint32_t x = l->idx[q];
+            b.x[q] = x;
+            b.d[q] = x == NONE ? ~0ull : dclamp(l->top[q] ^ kt);
+            n += x != NONE ? 1 : 0;
         } else {
             b.x[q] = NONE;
             b.d[q] = ~0ull;
         }
         b.f[q] = 0;
     }
+    return n;
 }
 
 // keep the first cap entries; returns how many are non-empty
@@ -247,138 +228,144 @@ __device__ __forceinline__ int blk_trunc(Blk8& b, int cap)
 }
 
 // ---------------------------------------------------------------------------
-// Kademlia::isSiblingFor(thisNode, key, 1) (Kademlia.cc:888-962) from the 64 B record
-__device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadRec& r, const K160& K)
+// Kademlia::isSiblingFor (Kademlia.cc:888-962) from the node's line
+
+// D > R, decided on the top 64 bits, exact on a tie
+__device__ __forceinline__ bool beyond_radius(const KadView& V, const KadNode& r, uint32_t c, const K160& D)
 {
-    if (V.nsib < 1) return true;
-    const K160 D = k_xor(as_key(r.key), K);
-    if (V.nsib == V.S5 && k_gt(D, as_key(r.R))) return false;
-    const K160 M = as_key(r.mask);
-    return ((D.w[0] & M.w[0]) | (D.w[1] & M.w[1]) | (D.w[2] & M.w[2]) | (D.w[3] & M.w[3]) | (D.w[4] & M.w[4])) == 0;
+    const uint64_t dt = ktop(D);
+    if (dt != r.rtop) return dt > r.rtop;
+    return k_gt(D, as_key(V.nodex[c].R));
 }
 
-// Kademlia::isSiblingFor(thisNode = c, key, numSiblings) for numSiblings >= 1 (Kademlia.cc:888-962):
-// c is in the numSiblings XOR-closest of siblings + c.  A sibling x is closer to K than c exactly
-// when bit msb(x ^ c) of D = c ^ K is set (x ^ K = (x ^ c) ^ D differs from D first at that bit),
-// so c qualifies when fewer than numSiblings siblings have their level bit set in D.  The mask
-// (OR of the level bits) decides the common case; the count reads c's sibling row (owned arc).
-__device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadRec& r, uint32_t c, const K160& K,
+// (D & levelmask) != 0: some sibling is XOR-closer to the key than the node
+__device__ __forceinline__ bool mask_hits(const KadView& V, const KadNode& r, uint32_t c, const K160& D)
+{
+    if (r.meta & KMETA_MASK_OUT) {
+        const KadX& X = V.nodex[c];
+        return ((D.w[0] & X.mask[0]) | (D.w[1] & X.mask[1]) | (D.w[2] & X.mask[2]) | (D.w[3] & X.mask[3]) |
+                (D.w[4] & X.mask[4])) != 0;
+    }
+    const int end = kad_end(r.meta);
+    const int mlo = end > 63 ? end - 63 : 0;
+    // bits [mlo, mlo + 63] of D
+    const int wi = mlo >> 5, sh = mlo & 31;
+    const uint64_t lo = (uint64_t)D.w[wi] | ((uint64_t)(wi + 1 < 5 ? D.w[wi + 1] : 0u) << 32);
+    const uint64_t hi = wi + 2 < 5 ? (uint64_t)D.w[wi + 2] : 0ull;
+    const uint64_t win = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+    return (win & r.mwin) != 0;
+}
+
+// isSiblingFor(thisNode = c, key, 1): table shorter than 1, or (not beyond a full table's radius
+// and no sibling closer)
+__device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadNode& r, uint32_t c, const K160& K)
+{
+    const int nsib = kad_nsib(r.meta);
+    if (nsib < 1) return true;
+    const K160 D = k_xor(as_key(r.key), K);
+    if (nsib == V.S5 && beyond_radius(V, r, c, D)) return false;
+    return !mask_hits(V, r, c, D);
+}
+
+// isSiblingFor(thisNode = c, key, numSiblings) for numSiblings >= 1: c is in the numSiblings
+// XOR-closest of siblings + c.  A sibling x is closer to K than c exactly when bit msb(x ^ c)
+// of D = c ^ K is set (x ^ K = (x ^ c) ^ D differs from D first at that bit), so c qualifies when
+// fewer than numSiblings siblings have their level bit set in D.  The mask decides the common
+// case; otherwise c's sibling row (owned arc) is counted.
+__device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadNode& r, uint32_t c, const K160& K,
                                                int numSiblings)
 {
-    if (numSiblings <= 1) return kad_is_sibling1(V, r, K);
-    if (V.nsib < numSiblings) return true;
+    if (numSiblings <= 1) return kad_is_sibling1(V, r, c, K);
+    const int nsib = kad_nsib(r.meta);
+    if (nsib < numSiblings) return true;
     const K160 me = as_key(r.key);
     const K160 D = k_xor(me, K);
-    if (V.nsib == V.S5 && k_gt(D, as_key(r.R))) return false;
-    const K160 M = as_key(r.mask);
-    if (((D.w[0] & M.w[0]) | (D.w[1] & M.w[1]) | (D.w[2] & M.w[2]) | (D.w[3] & M.w[3]) | (D.w[4] & M.w[4])) == 0)
-        return true;
-    const KadEntry* L = V.sibe + (uint64_t)(c - V.lo) * V.S5;
+    if (nsib == V.S5 && beyond_radius(V, r, c, D)) return false;
+    if (!mask_hits(V, r, c, D)) return true;
+    const KadLine* L = V.sibl + (uint64_t)(c - V.lo) * V.sln;
     int closer = 0;
-    for (int i = 0; i < V.nsib; ++i) {
-        const K160 x = as_key(L[i].key);
-        closer += (int)kbit(D, k_msb(k_xor(x, me)));
+    for (int i = 0; i < nsib; ++i) {
+        const uint32_t x = L[i / KLINE].idx[i % KLINE];
+        closer += (int)kbit(D, k_msb(k_xor(node_key(V.nodes, x), me)));
     }
     return closer < numSiblings;
 }
 
-// insert up to 8 entries of a contiguous entry array (bucket slot or sibling block); the
-// loads are issued together before the dependent sorted inserts
-template <int CAP>
-__device__ __forceinline__ void add_entries8(SVec<CAP>& res, int cap, const KadEntry* __restrict__ s, int cnt,
-                                             const K160& K, const KadRec* __restrict__ recs)
-{
-    uint32_t ix[8];
-    uint64_t dd[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        if (q < cnt) {
-            const uint2* p = reinterpret_cast<const uint2*>(s + q);
-            const uint2 a = p[0], b = p[1], c = p[2];
-            ix[q] = c.y;
-            dd[q] = dclamp(((uint64_t)(c.x ^ K.w[4]) << 32) | (uint64_t)(b.y ^ K.w[3]));
-            (void)a;
-        } else {
-            ix[q] = NONE;
-            dd[q] = 0;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-        if (ix[q] != NONE) svec_add(res, cap, ix[q], dd[q], K, recs);
-}
-
-template <int CAP>
-__device__ __forceinline__ void add_slot(SVec<CAP>& res, int cap, const KadView& V, uint32_t slot, const K160& K)
-{
-    const KadEntry* e = V.slots + (uint64_t)slot * V.k;
-    for (int q0 = 0; q0 < V.k; q0 += 8) add_entries8(res, cap, e + q0, min(8, V.k - q0), K, V.recs);
-}
-
-// What findNode at a responder needs of its 64 B record, captured when the FindNodeCall is sent
-// (the record is read then anyway, for the siblings flag): m = msb(key ^ K) (-1: key == K),
-// endIndex = msb(R), the bucket-row offset.  Its key is re-read only on the rare paths.
+// What findNode at a responder needs of its line, captured when the FindNodeCall is sent (the
+// line is read then anyway, for the siblings flag and the delay): m = msb(key ^ K) (-1: key == K),
+// endIndex, the lowest stored bucket, the bucket-row offset, the sibling count.
 struct RespGeo {
-    int m, endIndex;
+    int m, endIndex, rowlo, nsib;
     uint32_t boff;
 };
 
-__device__ __forceinline__ RespGeo resp_geo(const KadRec& r, const K160& K)
+__device__ __forceinline__ RespGeo resp_geo(const KadNode& r, const K160& K)
 {
     RespGeo g;
     g.m = k_msb(k_xor(as_key(r.key), K));
-    g.endIndex = k_msb(as_key(r.R));
+    g.endIndex = kad_end(r.meta);
+    g.rowlo = kad_rowlo(r.meta);
+    g.nsib = kad_nsib(r.meta);
     g.boff = r.boff;
     return g;
 }
 
-// Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246),
-// block form: the candidate sets of the reference's scan (bucket m, then buckets below it with
-// the sibling table and self, then buckets above while the result is short) merged 8 at a time
+__device__ __forceinline__ const KadLine* slot_line(const KadView& V, uint32_t boff, int bucket, int j)
+{
+    return V.lines + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - bucket) * V.lps + j;
+}
+
+// Kademlia::findNode(key, numRedundantNodes, numSiblings) at node c (Kademlia.cc:1101-1246),
+// block form: the candidate sets of the reference's scan (bucket m, then buckets m-1..endIndex with
+// the sibling table and self when m >= endIndex or the result is short, then buckets above m while
+// it is short) merged one table line at a time.  Returns the result size.
 template <bool EX>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
                                                  int numRedundant, bool sib, Blk8& res, int numSiblings = 1)
 {
     blk_clear(res);
-    if (V.nsib == 0 || (sib && numSiblings <= 1)) {
-        // resultSize = 1 and self is the XOR-closest of siblings + self (see kad_find_node1)
+    if (g.nsib == 0 || (V.snapshot && sib && numSiblings <= 1)) {
+        // an empty sibling table answers [self]; on snapshot tables a sibling for numSiblings = 1
+        // is the XOR-closest of everything it knows: nothing below the main bucket beats it
+        // 
         res.x[0] = c;
-        res.d[0] = dist_hi(kad_key(V.recs, c), K);
+        res.d[0] = dist_hi(node_key(V.nodes, c), K);
         return 1;
     }
-    // resultSize = numSiblings when c is a sibling for K, else numRedundantNodes (Kademlia.cc:1127-1129)
+    // resultSize = numSiblings when c is a sibling for K, else numRedundantNodes (Kademlia.cc:1127-1131)
     const int rs = sib ? numSiblings : numRedundant;
     const int cap = rs < 8 ? rs : 8;
-    const int m = g.m;
-    const int endIndex = g.endIndex;
-    int n = 0;
-    auto add_block = [&](const KadEntry* e, int cnt) {
+    int n = 0, seen = 0;
+    auto add_line = [&](const KadLine* l) -> int {
         Blk8 b;
-        blk_load(b, e, cnt, K);
-        blk_sort8<false, EX>(b, K, V.recs);
-        blk_merge_top8<false, EX>(res, b, K, V.recs);
-        n = blk_trunc(res, cap);
-    };
-    auto add_slot8 = [&](int bucket) {
-        const KadEntry* e = V.slots + (uint64_t)(g.boff + (uint32_t)(KEYBITS - 1 - bucket)) * V.k;
-        for (int q0 = 0; q0 < V.k; q0 += 8) add_block(e + q0, min(8, V.k - q0));
-    };
-    if (m >= 0 && m >= endIndex) add_slot8(m);
-    if (m >= endIndex || n < cap) {
-        if (!(m > endIndex && n >= cap)) {
-            for (int b = m - 1; b >= endIndex; --b) add_slot8(b);
-            const KadEntry* L = V.sibe + (uint64_t)(c - V.lo) * V.S5;
-            for (int i = 0; i < V.nsib; i += 8) add_block(L + i, min(8, V.nsib - i));
-            Blk8 self;
-            blk_clear(self);
-            self.x[0] = c;
-            self.d[0] = dist_hi(kad_key(V.recs, c), K);
-            blk_merge_top8<false, EX>(res, self, K, V.recs);
+        const int cnt = blk_load_line(b, l, K);
+        if (cnt) {
+            blk_sort8<false, EX>(b, K, V.nodes);
+            blk_merge_top8<false, EX>(res, b, K, V.nodes);
             n = blk_trunc(res, cap);
+            seen += cnt;
         }
+        return cnt;
+    };
+    auto add_slot = [&](int bucket) {
+        if (g.rowlo < 0 || bucket < g.rowlo) return;      // buckets below the stored row are empty
+        for (int j = 0; j < V.lps; ++j)
+            if (add_line(slot_line(V, g.boff, bucket, j)) < KLINE) break;
+    };
+    if (g.m >= 0) add_slot(g.m);
+    if (g.m >= g.endIndex || seen < rs) {
+        for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
+        const KadLine* L = V.sibl + (uint64_t)(c - V.lo) * V.sln;
+        for (int j = 0; j * KLINE < g.nsib; ++j) add_line(L + j);
+        Blk8 self;
+        blk_clear(self);
+        self.x[0] = c;
+        self.d[0] = dist_hi(node_key(V.nodes, c), K);
+        blk_merge_top8<false, EX>(res, self, K, V.nodes);
+        n = blk_trunc(res, cap);
+        seen += 1;
     }
-    for (int b = m + 1; n < cap && b < KEYBITS; ++b)
-        if (b >= endIndex) add_slot8(b);
+    for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);
     return n;
 }
 
@@ -389,7 +376,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
 // response nodes, so "inserted" and "in the final vector" coincide).
 template <bool EX>
 __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap, const K160& K,
-                                        const KadRec* __restrict__ recs)
+                                        const KadNode* __restrict__ nodes)
 {
     Blk8 a, b;
     bool dup = false;
@@ -412,8 +399,8 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
         if (dj) { b.x[j] = NONE; b.d[j] = ~0ull; }
         dup |= dj;
     }
-    if (dup) blk_sort8<true, EX>(b, K, recs);     // holes to the end
-    blk_merge_top8<true, EX>(a, b, K, recs);
+    if (dup) blk_sort8<true, EX>(b, K, nodes);     // holes to the end
+    blk_merge_top8<true, EX>(a, b, K, nodes);
     const int n = blk_trunc(a, cap);
     int numNew = 0;
     uint32_t used = 0;
@@ -429,50 +416,35 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
     return numNew;
 }
 
-// Kademlia::findNode(key, numRedundantNodes, numSiblings=1) at node c (Kademlia.cc:1101-1246)
-template <int CAP, bool EX = true>
-__device__ __forceinline__ void kad_find_node1(const KadView& V, uint32_t c, const KadRec& r, const K160& K, int numRedundant,
-                               bool sib, SVec<CAP>& res, int numSiblings = 1)
+// findNode(key, numRedundantNodes, numSiblings) at node c into a sorted vector
+template <int CAP, bool EX>
+__device__ __forceinline__ void kad_find_node_vec(const KadView& V, uint32_t c, const KadNode& r, const K160& K,
+                                                  int numRedundant, bool sib, SVec<CAP>& res, int numSiblings = 1)
 {
-    if constexpr (CAP == 8) {
-        Blk8 b;
-        const int n = kad_find_node_blk<EX>(V, c, resp_geo(r, K), K, numRedundant, sib, b, numSiblings);
+    static_assert(CAP == 8, "findNode results hold at most 8 nodes");
+    Blk8 b;
+    const int n = kad_find_node_blk<EX>(V, c, resp_geo(r, K), K, numRedundant, sib, b, numSiblings);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
-        res.n = n;
-        res.used = 0;
-        return;
-    }
-    svec_clear(res);
-    const K160 me = as_key(r.key);
-    if (V.nsib == 0 || (sib && numSiblings <= 1)) {
-        // resultSize = 1 and self is the XOR-closest of siblings + self; with a full table the
-        // key lies below endIndex so bucket msb(D) is all siblings
-        svec_add(res, 1, c, dist_hi(me, K), K, V.recs);
-        return;
-    }
-    const int rs = sib ? numSiblings : numRedundant;
-    const int cap = rs < CAP ? rs : CAP;
-    const K160 D = k_xor(me, K);
-    const int m = k_msb(D);
-    const int endIndex = k_msb(as_key(r.R));
-    auto slot_of = [&](int b) { return r.boff + (uint32_t)(KEYBITS - 1 - b); };
-    if (m >= 0 && m >= endIndex) add_slot(res, cap, V, slot_of(m), K);
-    if (m >= endIndex || res.n < cap) {
-        // nothing below bucket m can beat a full result unless siblings share bucket m
-        if (!(m > endIndex && res.n >= cap)) {
-            for (int b = m - 1; b >= endIndex; --b) add_slot(res, cap, V, slot_of(b), K);
-            const KadEntry* L = V.sibe + (uint64_t)(c - V.lo) * V.S5;   // rows of the owned arc
-            for (int i = 0; i < V.nsib; i += 8) add_entries8(res, cap, L + i, min(8, V.nsib - i), K, V.recs);
-            svec_add(res, cap, c, dist_hi(me, K), K, V.recs);
-        }
-    }
-    for (int b = m + 1; res.n < cap && b < KEYBITS; ++b)
-        if (b >= endIndex) add_slot(res, cap, V, slot_of(b), K);
+    for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
+    res.n = n;
+    res.used = 0;
+}
+
+// The FindNodeResponse size of node c (its findNode result size): resultSize, unless explicit
+// tables leave c fewer candidates on its scan (then counted by running the scan)
+template <bool EX>
+__device__ __forceinline__ int kad_response_size(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
+                                                 int rs, bool sib, int numSiblings)
+{
+    if (g.nsib == 0 || (sib && numSiblings <= 1)) return 1;
+    const int full = rs < (int)V.n ? rs : (int)V.n;
+    if (!V.maybe_short || g.nsib + 1 >= rs) return full;
+    Blk8 b;
+    return kad_find_node_blk<EX>(V, c, g, K, rs, false, b, numSiblings);
 }
 
 // ---------------------------------------------------------------------------
-// K2: batched iterative lookups
+// IterativePathLookup, synchronous form (the sharded path, kad_shard.hip)
 
 constexpr int MAXA = 4;    // lookupParallelRpcs <= 4
 
@@ -490,9 +462,26 @@ struct Pend {
     uint32_t tag;      // step at send (bits 0..15) | insertion sequence (bits 16..30) | timeout (bit 31)
     int64_t t;         // event time
     uint32_t dins;     // t - insertion time
-    uint32_t geo;      // responder: m + 1 (bits 0..7) | endIndex + 1 (bits 8..15) | siblings flag (bit 16)
+    uint32_t geo;      // responder: m + 1 (bits 0..7) | endIndex + 1 (8..15) | rowlo + 1 (16..23) | sib (24)
     uint32_t boff;     // responder's bucket-row offset
+    uint32_t nsib;
 };
+
+__device__ __forceinline__ uint32_t pack_geo(const RespGeo& g, bool sb)
+{
+    return (uint32_t)(g.m + 1) | ((uint32_t)(g.endIndex + 1) << 8) | ((uint32_t)(g.rowlo + 1) << 16) | (sb ? 1u << 24 : 0u);
+}
+
+__device__ __forceinline__ RespGeo unpack_geo(uint32_t geo, uint32_t boff, uint32_t nsib)
+{
+    RespGeo g;
+    g.m = (int)(geo & 0xFFu) - 1;
+    g.endIndex = (int)((geo >> 8) & 0xFFu) - 1;
+    g.rowlo = (int)((geo >> 16) & 0xFFu) - 1;
+    g.boff = boff;
+    g.nsib = (int)nsib;
+    return g;
+}
 
 // per-lane lookup state (IterativeLookup + its single IterativePathLookup)
 template <int A>
@@ -530,22 +519,17 @@ __device__ __forceinline__ void kad_lookup_init(KadLookup<A>& L, const K160& K, 
 // FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
 // SimpleNodeEntry::calcDelay with the source's tx queue).  on(slot, x, isTimeout) is told which
 // pending-event slot the call occupies (the sharded path requests x's findNode result there).
-// LK: a LookupCall batch (numSiblings = LC.numSiblings); otherwise numSiblings = 1 at compile time
-template <int A, bool LK, class OnSend>
+template <int A, bool EX, bool LK, class OnSend>
 __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                          uint32_t x, const OnSend& on)
 {
-    const double2 cxy = V.xy[x];
-    const KadRec rr = kad_rec(V.recs, x);
+    const KadNode rr = load_node(V.nodes, x);
     const int ns = LK ? LC.numSiblings : 1;
     const bool sb = kad_is_sibling(V, rr, x, L.K, ns);
     const RespGeo rg = resp_geo(rr, L.K);
-    const uint32_t geo = (uint32_t)(rg.m + 1) | ((uint32_t)(rg.endIndex + 1) << 8) | (sb ? 0x10000u : 0u);
-    // the response carries findNode's result: min(numSiblings, n) nodes when x is sibling,
-    // else min(redundant, n)
-    const int rsz = sb ? ns : LC.redundant;
-    const int csz = rsz < (int)V.n ? rsz : (int)V.n;
-    const int64_t cd = coord_ns(L.sx, L.sy, cxy.x, cxy.y, DC.round);
+    // the response carries findNode's result (Kademlia.cc:1127-1131 resultSize)
+    const int csz = kad_response_size<EX>(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
+    const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
     const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
     const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
     L.txf = newTx;
@@ -569,8 +553,9 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
             L.p[i].t = isTo ? tTo : tResp;
             L.p[i].dins = (uint32_t)(isTo ? DC.rpcTimeout : d2);
             L.p[i].tag = tag;
-            L.p[i].geo = geo;
+            L.p[i].geo = pack_geo(rg, sb);
             L.p[i].boff = rg.boff;
+            L.p[i].nsib = (uint32_t)rg.nsib;
         }
     }
     L.pvalid |= 1u << slot;
@@ -579,7 +564,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
 }
 
 // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
-template <int A, bool LK, class OnSend>
+template <int A, bool EX, bool LK, class OnSend>
 __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                               int num, const OnSend& on)
 {
@@ -588,7 +573,8 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
     if (LC.strict) num = min(num, LC.alpha - L.pending);
     if (num == 0 && L.pending == 0 && !LC.finishOnFirst) num = LC.alpha;
     for (int i = 0; num > 0 && i < LC.redundant; ++i) {
-        // getNextEntry: first entry not alreadyUsed (no node is ever dead in a stable network)
+        // getNextEntry: first entry not alreadyUsed (a node that timed out is dead, but it is
+        // used already: entries leave nextHops for good once evicted)
         const uint32_t unused = ~L.nh.used & ((1u << L.nh.n) - 1u);
         if (!unused) break;
         const int e = __ffs((int)unused) - 1;
@@ -597,26 +583,25 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
         for (int j = 0; j < 8; ++j)
             if (j == e) h = L.nh.idx[j];
         // visitOnlyOnce: an unused entry can only be a visited node if it is the source
-        // (responders stay in nextHops as used entries or are evicted for good)
         if (!LC.visitOnlyOnce || h != L.S) {
             ++L.pending;
             --num;
-            kad_send<A, LK>(L, V, DC, LC, h, on);
+            kad_send<A, EX, LK>(L, V, DC, LC, h, on);
         }
         L.nh.used |= 1u << e;
     }
     if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
 }
 
-template <int A, bool LK, class OnSend>
+template <int A, bool EX, bool LK, class OnSend>
 __device__ __forceinline__ void kad_timeoutlike(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                 const KadLC& LC, const OnSend& on)
 {
     // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
     --L.pending;
     if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
-    else if (LC.newOnTimeout) kad_send_rpcs<A, LK>(L, V, DC, LC, 1, on);
-    else if (L.pending == 0) kad_send_rpcs<A, LK>(L, V, DC, LC, LC.alpha, on);
+    else if (LC.newOnTimeout) kad_send_rpcs<A, EX, LK>(L, V, DC, LC, 1, on);
+    else if (L.pending == 0) kad_send_rpcs<A, EX, LK>(L, V, DC, LC, LC.alpha, on);
 }
 
 // IterativeLookup::start (IterativeLookup.cc:133-244): local findNode at the source
@@ -624,17 +609,17 @@ template <int A, bool EX, bool LK, class OnSend>
 __device__ __forceinline__ void kad_lookup_start(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                  const KadLC& LC, SVec<8>& res, const OnSend& on)
 {
-    const KadRec rs = kad_rec(V.recs, L.S);
+    const KadNode rs = load_node(V.nodes, L.S);
     const int ns = LK ? LC.numSiblings : 1;
     const bool sb = kad_is_sibling(V, rs, L.S, L.K, ns);
-    kad_find_node1<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res, ns);
+    kad_find_node_vec<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res, ns);
     if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
     else if (LC.numSiblings != 0 && sb) {
         L.result = res.idx[0];
         L.pfinished = true; L.psuccess = true;
     } else {
-        nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.recs);
-        kad_send_rpcs<A, LK>(L, V, DC, LC, LC.alpha, on);
+        nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
+        kad_send_rpcs<A, EX, LK>(L, V, DC, LC, LC.alpha, on);
     }
 }
 
@@ -666,10 +651,10 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
             if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
         }
     }
-    uint32_t r = 0, tag = 0, geo = 0, boff = 0;
+    uint32_t r = 0, tag = 0, geo = 0, boff = 0, nsib = 0;
 #pragma unroll
     for (int i = 0; i < A; ++i)
-        if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; }
+        if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; nsib = L.p[i].nsib; }
     if (!(tag & 0x80000000u) && !getres.ready(e)) return false;
     L.pvalid &= ~(1u << e);
     L.now = bt;
@@ -677,19 +662,16 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     if (tag & 0x80000000u) {
         // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
         L.any_to = true;
-        kad_timeoutlike<A, LK>(L, V, DC, LC, on);
+        kad_timeoutlike<A, EX, LK>(L, V, DC, LC, on);
         return true;
     }
     // the responder's siblings flag and bucket geometry were captured at send (kad_send)
-    const bool sb = (geo & 0x10000u) != 0;
-    RespGeo rg;
-    rg.m = (int)(geo & 0xFFu) - 1;
-    rg.endIndex = (int)((geo >> 8) & 0xFFu) - 1;
-    rg.boff = boff;
+    const bool sb = (geo >> 24) & 1u;
+    const RespGeo rg = unpack_geo(geo, boff, nsib);
     const bool acc = (LC.useAll && LC.merge) ? true : (vr == L.step);
     if (!(acc || (sb && LC.acceptLateSiblings))) {
         // not accepted: handled as a timeout, its nodes are dropped
-        kad_timeoutlike<A, LK>(L, V, DC, LC, on);
+        kad_timeoutlike<A, EX, LK>(L, V, DC, LC, on);
         return true;
     }
     // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
@@ -701,12 +683,12 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     ++L.step;
     --L.pending;
     getres.fill(e, r, rg, sb, res);
-    int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.recs);
+    int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
     if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
     if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
     else {
         if (numNew == 0 && LC.newOnResp) numNew = 1;
-        kad_send_rpcs<A, LK>(L, V, DC, LC, min(numNew, LC.alpha), on);
+        kad_send_rpcs<A, EX, LK>(L, V, DC, LC, min(numNew, LC.alpha), on);
     }
     return true;
 }
@@ -749,9 +731,13 @@ __device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A>& L
 inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
 {
     KadView V{};
-    V.recs = t.recs; V.xy = xy; V.sib = t.sib; V.sibe = t.sibe; V.slots = t.slots; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
+    V.nodes = t.nodes; V.nodex = t.nodex; V.lines = t.lines; V.sibl = t.lines ? t.lines + t.rows_lines : nullptr;
+    V.xy = xy; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
+    V.lps = (t.k + KLINE - 1) / KLINE;
+    V.sln = (V.S5 + KLINE - 1) / KLINE;
     V.lo = t.lo; V.hi = t.hi;
-    V.nsib = (int)((uint64_t)(n - 1) < (uint64_t)V.S5 ? n - 1 : (uint32_t)V.S5);
+    V.maybe_short = t.maybe_short;
+    V.snapshot = t.snapshot;
     return V;
 }
 

@@ -158,10 +158,10 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
         out[j] = o;
         return;
     }
-    const KadRec rr = kad_rec(V.recs, q.node);
-    const bool sb = kad_is_sibling1(V, rr, K);
+    const KadNode rr = load_node(V.nodes, q.node);
+    const bool sb = kad_is_sibling1(V, rr, q.node, K);
     SVec<8> r;
-    kad_find_node1<8, EX>(V, q.node, rr, K, LC.redundant, sb, r);
+    kad_find_node_vec<8, EX>(V, q.node, rr, K, LC.redundant, sb, r);
     o.count = (uint32_t)r.n;
 #pragma unroll
     for (int k = 0; k < 8; ++k) { o.nodes[k] = r.idx[k]; o.dist_hi[k] = r.d[k]; }

@@ -569,7 +569,7 @@ static ovs_status kad_load_arc(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     if (lo >= hi || hi > n) return fail(c, OVS_EINVAL, "arc [lo, hi) must be a non-empty part of [0, n)");
     ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
     if (s != OVS_OK) { free_tables(c); return s; }
-    hipError_t e = kad_build(c->recs, (uint32_t)n, c->P.k, c->P.s, c->P.kadSeed, c->kad, c->stream, (uint32_t)lo,
+    hipError_t e = kad_build(c->recs, c->xy, (uint32_t)n, c->P.k, c->P.s, c->P.kadSeed, c->kad, c->stream, (uint32_t)lo,
                              (uint32_t)hi);
     if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "kademlia table build"); }
     c->overlay = OVS_OVERLAY_KADEMLIA;
@@ -579,6 +579,52 @@ static ovs_status kad_load_arc(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
 ovs_status ovs_kad_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint32_t flags)
 {
     return kad_load_arc(c, ids, n, xy, 0, n, flags);
+}
+
+ovs_status ovs_kad_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, const uint32_t* siblings,
+                               const uint8_t* bucket_count, const uint32_t* bucket_nodes, uint32_t flags)
+{
+    if (!c || !ids || !xy || !siblings || !bucket_count || !bucket_nodes) return OVS_EINVAL;
+    if (flags & OVS_DEVICE_PTRS) return fail(c, OVS_ENOTSUP, "explicit tables are taken from host memory");
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    free_kad_shard(c);
+    if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
+    if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
+    if (c->P.k < 1 || c->P.k > 32 || c->P.s < 1 || 5 * c->P.s > 64)
+        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..32 and 5*s <= 64");
+    ovs_status s = upload_nodes(c, ids, n, xy, false);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    const uint64_t S5 = 5ull * (uint64_t)c->P.s, k = (uint64_t)c->P.k;
+    uint32_t *dsib = nullptr, *dbn = nullptr;
+    uint8_t* dbc = nullptr;
+    auto release = [&]() { if (dsib) hipFree(dsib); if (dbn) hipFree(dbn); if (dbc) hipFree(dbc); };
+    if (hipMalloc(&dsib, sizeof(uint32_t) * n * S5) != hipSuccess || hipMalloc(&dbc, n * 160) != hipSuccess ||
+        hipMalloc(&dbn, sizeof(uint32_t) * n * 160 * k) != hipSuccess) {
+        release(); free_tables(c);
+        return fail(c, OVS_ENOMEM, "explicit Kademlia tables: device allocation failed");
+    }
+    hipError_t e = hipMemcpy(dsib, siblings, sizeof(uint32_t) * n * S5, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dbc, bucket_count, n * 160, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dbn, bucket_nodes, sizeof(uint32_t) * n * 160 * k, hipMemcpyHostToDevice);
+    uint32_t bad_node = 0, bad_code = 0;
+    if (e == hipSuccess)
+        e = kad_build_explicit(c->recs, c->xy, (uint32_t)n, c->P.k, c->P.s, dsib, dbc, dbn, c->kad, &bad_node, &bad_code,
+                               c->stream);
+    release();
+    if (e == hipErrorInvalidValue && bad_code) {
+        static const char* why[] = {"", "sibling index out of range or the node itself", "sibling listed twice",
+                                    "bucket holds more than k entries", "bucket member out of range or the node itself",
+                                    "bucket member in the wrong bucket (msb(member ^ node) != bucket index)",
+                                    "bucket member listed twice", "node is both sibling and bucket member"};
+        free_tables(c);
+        char m[192];
+        std::snprintf(m, sizeof m, "explicit Kademlia tables of node %u: %s", bad_node, bad_code < 8 ? why[bad_code] : "?");
+        return fail(c, OVS_EINVAL, m);
+    }
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "explicit Kademlia table build"); }
+    c->overlay = OVS_OVERLAY_KADEMLIA;
+    return OVS_OK;
 }
 
 ovs_status ovs_kad_load_shard(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint64_t lo,
@@ -758,7 +804,7 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             else e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
         }
     } else {
-        e = kad_route(c->kad, c->recs, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
+        e = kad_route(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
                       c->num_cu, s);
     }
     if (e != hipSuccess) return hip_fail(c, e, "route kernel");
@@ -846,7 +892,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         LookupConsts LC{P.hopCountMax, ns, P.lookupRedundantNodes, 0};
         e = launch_chord_route(chord_view(c), c->ideal, DC, LC, dk, ds, n, dout, dhop, c->num_cu, s);
     } else {
-        e = kad_route(c->kad, c->recs, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
+        e = kad_route(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
                       dsib);
     }
     if (e == hipSuccess) e = launch_lookup_finish(chord_view(c), chord, c->ideal, ns, dout, dsib, n, s);
@@ -902,7 +948,7 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
         e = launch_chord_find_node(chord_view(c), c->ideal, dn, dk, n, numRedundantNodes, numSiblings, dout, max_out,
                                    dc, dsb, s);
     else
-        e = kad_find_node(c->kad, c->recs, (uint32_t)c->n, c->P, dn, dk, n, numRedundantNodes, numSiblings, dout,
+        e = kad_find_node(c->kad, (uint32_t)c->n, c->P, dn, dk, n, numRedundantNodes, numSiblings, dout,
                           max_out, dc, dsb, s);
     if (e != hipSuccess) return hip_fail(c, e, "findNode kernel");
     if (!dev) {

@@ -172,6 +172,7 @@ def lib() -> C.CDLL:
         "ovs_chord_load": ([vp, vp, u64, vp, u32], C.c_int),
         "ovs_chord_load_tables": ([vp, vp, u64, vp, vp, vp, vp, vp, vp, u32], C.c_int),
         "ovs_kad_load": ([vp, vp, u64, vp, u32], C.c_int),
+        "ovs_kad_load_tables": ([vp, vp, u64, vp, vp, vp, vp, u32], C.c_int),
         "ovs_kad_export": ([vp, vp, vp, vp], C.c_int),
         "ovs_chord_export_fingers": ([vp, vp], C.c_int),
         "ovs_route_batch": ([vp, vp, vp, u64, vp, vp, vp, u32, vp], C.c_int),
@@ -316,6 +317,16 @@ class KbrEngine:
         ids = keys_array(ids)
         xy = np.ascontiguousarray(xy, dtype=np.float64)
         self._chk(self._L.ovs_kad_load(self._h, _ptr(ids), len(ids), _ptr(xy), 0), "ovs_kad_load")
+        self.n, self.overlay = len(ids), OVERLAY_KADEMLIA
+
+    def kad_load_tables(self, ids, xy, siblings, bucket_count, bucket_nodes):
+        """Explicit Kademlia tables (ovs_kad_load_tables): siblings (n, 5s), bucket_count (n, 160),
+        bucket_nodes (n, 160, k), 0xFFFFFFFF padded -- the k-buckets a running OverSim node holds."""
+        ids = keys_array(ids)
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+                ((xy, np.float64), (siblings, np.uint32), (bucket_count, np.uint8), (bucket_nodes, np.uint32))]
+        self._chk(self._L.ovs_kad_load_tables(self._h, _ptr(ids), len(ids), *[_ptr(a) for a in arrs], 0),
+                  "ovs_kad_load_tables")
         self.n, self.overlay = len(ids), OVERLAY_KADEMLIA
 
     def chord_fingers(self) -> np.ndarray:

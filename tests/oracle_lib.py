@@ -72,6 +72,7 @@ def lib() -> C.CDLL:
             ("orc_kad_build", [vp, u32, vp, vp], vp),
             ("orc_chord_build_lazy", [vp, u32, vp, vp], vp),
             ("orc_kad_build_lazy", [vp, u32, vp, vp], vp),
+            ("orc_kad_build_tables", [vp, u32, vp, vp, vp, vp, vp], vp),
             ("orc_cap_failed", [], C.c_int),
             ("orc_clear_error", [], None),
             ("orc_net_free", [vp], None),
@@ -161,8 +162,15 @@ class OracleNet:
                                              _p(t["deque_size"]), C.byref(self.params))
         else:
             self.params = params or kad_params()
-            build = L.orc_kad_build_lazy if lazy else L.orc_kad_build
-            h = build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+            if tables is None:
+                build = L.orc_kad_build_lazy if lazy else L.orc_kad_build
+                h = build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+            else:
+                t = {k: np.ascontiguousarray(v) for k, v in tables.items()}
+                self._keep = t
+                h = L.orc_kad_build_tables(_p(self.ids), n, _p(self.xy), _p(t["siblings"].astype(np.uint32)),
+                                           _p(t["bucket_count"].astype(np.uint8)),
+                                           _p(t["bucket_nodes"].astype(np.uint32)), C.byref(self.params))
         if not h:
             raise RuntimeError(f"oracle build failed: {L.orc_last_error().decode()}")
         self._h = C.c_void_p(h)
