@@ -15,8 +15,10 @@ Workloads (--workload, default C):
      sharded over the N GPUs (RCCL all-to-allv).  Weak scaling in lookups.
   B  Kademlia, 15 000 nodes (nodes_2d_15000.xml coordinates), k=8, alpha=1,
      1M node-ID lookups per GPU.  N > 1: independent replicas.
-  E  Kademlia, 2^24 nodes, alpha=3, 4M random-key lookups per GPU.  N > 1:
-     replicas (the XOR-prefix sharded exchange is future work).
+  E  Kademlia, 2^24 nodes, alpha=3, 4M random-key lookups per GPU.  N > 1: the
+     ID space is cut into N arcs (prefixes), each GPU owns its arc's tables, and
+     FindNodeCalls are exchanged as request/response all-to-allv rounds
+     (oversim_amd/shard.py).  Weak scaling in lookups.
 """
 from __future__ import annotations
 
@@ -43,7 +45,14 @@ GATHER_CEILING_GBS = 2950.0
 # coordinate gathers; that figure is reported beside ("survey_bytes_per_hop"), not used.
 B_HOP, B_LOOKUP = 64, 104
 B_HOP_SURVEY = 512
-B_RPC = 448                    # algorithmic bytes per evaluated Kademlia RPC
+# Kademlia, this build's layout: every FindNodeCall reads its target's 64 B KadNode line when it is
+# sent and the responder's 96 B bucket block (findNode's main bucket) when its response is
+# processed; every lookup additionally its source's KadNode + block (the local findNode at start)
+# and its key/source/result (24 B in, 16 B out).  Blocks findNode reads beyond the main bucket
+# (short buckets, the sibling zone) are extra, not counted.  SURVEY.md §8(d) priced 448 B/RPC for
+# a 24 B-entry layout; reported beside ("survey_bytes_per_rpc").
+B_RPC, B_KLOOKUP = 160, 200
+B_RPC_SURVEY = 448
 
 
 def parse():
@@ -284,7 +293,8 @@ def main():
             per_launch_bytes = hop_total * B_HOP + lookups_launch * B_LOOKUP
             bper = f"{B_HOP} B/hop + {B_LOOKUP} B/lookup"
         else:
-            per_launch_bytes, bper = rpc_total * B_RPC, f"{B_RPC} B/RPC"
+            per_launch_bytes = rpc_total * B_RPC + lookups_launch * B_KLOOKUP
+            bper = f"{B_RPC} B/RPC + {B_KLOOKUP} B/lookup"
         achieved = per_launch_bytes / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = (traffic_from_json(a.traffic_json, a.workload, kname) if world == 1 and not sharded
                                 else (None, None))
@@ -333,6 +343,7 @@ def main():
                 "traffic_source": traffic_src,
                 "gather_ceiling_GBs": GATHER_CEILING_GBS,
                 "frac_of_gather_ceiling": achieved / GATHER_CEILING_GBS,
+                **({"survey_bytes_per_hop": B_HOP_SURVEY} if kind == "chord" else {"survey_bytes_per_rpc": B_RPC_SURVEY}),
             },
             "cpu_baseline": cpu,
         }

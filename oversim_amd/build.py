@@ -34,7 +34,13 @@ CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
     "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value", "-Wno-bitwise-instead-of-logical",
 ]
-SOURCES = ["chord.hip", "kad.hip", "kad_shard.hip", "stats.hip", "ovs_kbr.cpp", "ovs_ini.cpp"]
+SOURCES = ["chord.hip", "kad.hip", "kad_route.hip", "kad_shard.hip", "stats.hip", "ovs_kbr.cpp", "ovs_ini.cpp"]
+# translation units compiled more than once: (source, object stem, extra flags).  K2 is built per
+# (alpha, exact) pair so its instantiations compile in parallel.
+VARIANTS = {
+    "kad_route.hip": [(f"kad_route_a{a}{'x' if x else ''}", [f"-DOVS_KAD_A={a}", f"-DOVS_KAD_EX={x}"])
+                      for a in (1, 2, 3, 4) for x in (0, 1)],
+}
 
 
 def _engine_files() -> list[Path]:
@@ -70,14 +76,16 @@ def build_engine(verbose: bool = False) -> Path:
     flags = " ".join(CFLAGS)
     procs = []
     objs = []
-    for src in SOURCES:
+    units = [(src, stem, extra) for src in SOURCES
+             for stem, extra in VARIANTS.get(src, [(src.rsplit(".", 1)[0], [])])]
+    for src, stem, extra in units:
         s = CSRC / src
-        o = OBJ / (src.rsplit(".", 1)[0] + ".o")
+        o = OBJ / (stem + ".o")
         objs.append(o)
-        d = _digest([s] + headers, flags)
+        d = _digest([s] + headers, flags + " " + " ".join(extra))
         if _stamp_ok(o, d):
             continue
-        cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", str(s), "-o", str(o)]
+        cmd = [HIPCC, *CFLAGS, *extra, "-x", "hip", "-c", str(s), "-o", str(o)]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((cmd, o, d, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -1,14 +1,14 @@
 // kad.hpp -- Kademlia device tables and launchers (internal).
 //
-// Layout (one HBM line = 64 B is the unit every table is cut to):
-//  KadNode nodes[n]   one line per node: everything the *sender* of a FindNodeCall needs of its
-//                     target (key, coordinates, isSiblingFor summary, bucket-row offset), read
+// Layout:
+//  KadNode nodes[n]   one 64 B line per node: everything the *sender* of a FindNodeCall needs of
+//                     its target (key, coordinates, isSiblingFor summary, bucket-row offset), read
 //                     once per RPC when the call is sent
 //  KadX    nodex[n]   the exact sibling radius R and level mask (fallback on summary ties, rare)
-//  KadLine lines[]    bucket rows and sibling rows as lines of 5 entries (top 64 bits of the
-//                     member key + member index); slot of bucket m of node v = ceil(k/5) lines at
-//                     nodes[v].boff + (159 - m) * lps, for m = rowlo(v) .. 159; sibling row of an
-//                     owned node v = ceil(5s/5) lines at sib_base + (v - lo) * sln
+//  KadBlk  blks[]     bucket rows and sibling rows as 96 B blocks of 8 entries (top 64 bits of the
+//                     member key, member index): bucket m of node v = blks[nodes[v].boff + 159 - m]
+//                     for m = rowlo(v) .. 159 (one block = one k <= 8 bucket, two lines); sibling
+//                     row of an owned node v = ceil(5s/8) blocks at sib_base + (v - lo) * sbn
 // The reference's structures these hold: Kademlia::siblingTable (a KademliaBucket of 5s entries
 // sorted by XOR distance to this node, Kademlia.cc:179, 315-317) and routingTable[160] (buckets
 // of up to k entries in LRU order, KademliaBucket.h:30-69, filled by routingAdd 432-756).
@@ -38,13 +38,12 @@ struct KadX {
     uint32_t mask[5];
 };
 
-constexpr int KLINE = 5;   // entries per line
-struct alignas(64) KadLine {
-    uint64_t top[KLINE];   // top 64 bits (bits 96..159) of the member key; ~0 for an empty entry
-    uint32_t idx[KLINE];   // member node index; NONE for an empty entry (entries packed at the front)
-    uint32_t pad;
+constexpr int KBLK = 8;   // entries per block (= the largest bucket the route kernel takes, k <= 8)
+struct alignas(32) KadBlk {
+    uint64_t top[KBLK];    // top 64 bits (bits 96..159) of the member key; ~0 for an empty entry
+    uint32_t idx[KBLK];    // member node index; NONE for an empty entry (entries packed at the front)
 };
-static_assert(sizeof(KadLine) == 64, "KadLine is one 64 B line");
+static_assert(sizeof(KadBlk) == 96, "KadBlk is 96 B");
 
 __host__ __device__ __forceinline__ int kad_end(uint32_t meta) { return (int)(meta & 0xFFu) - 1; }
 __host__ __device__ __forceinline__ int kad_rowlo(uint32_t meta) { return (int)((meta >> 8) & 0xFFu) - 1; }
@@ -53,8 +52,8 @@ __host__ __device__ __forceinline__ int kad_nsib(uint32_t meta) { return (int)((
 struct KadTables {
     KadNode* nodes = nullptr;
     KadX* nodex = nullptr;
-    KadLine* lines = nullptr;      // bucket rows (rows_lines lines), then the sibling rows of the owned arc
-    uint64_t rows_lines = 0;       // bucket-row lines; sibling rows start here
+    KadBlk* blks = nullptr;        // bucket rows (rows_blks blocks), then the sibling rows of the owned arc
+    uint64_t rows_blks = 0;        // bucket-row blocks; sibling rows start here
     uint32_t* sib = nullptr;       // (hi - lo) * S5 sibling member indices of the owned arc, NONE padded (export)
     uint32_t lo = 0, hi = 0;       // sibling / bucket rows exist for nodes [lo, hi) (the whole network unsharded)
     int k = 8, s = 8;
@@ -67,14 +66,13 @@ struct KadTables {
 struct KadView {
     const KadNode* __restrict__ nodes;
     const KadX* __restrict__ nodex;
-    const KadLine* __restrict__ lines;
-    const KadLine* __restrict__ sibl;   // sibling rows of the owned arc
+    const KadBlk* __restrict__ blks;
+    const KadBlk* __restrict__ sibb;    // sibling rows of the owned arc
     const double2* __restrict__ xy;
     uint32_t n;
     int k;
-    int lps;      // lines per bucket slot = ceil(k / 5)
     int S5;       // sibling table capacity 5s
-    int sln;      // lines per sibling row = ceil(5s / 5)
+    int sbn;      // blocks per sibling row = ceil(5s / 8)
     uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)
     int maybe_short;
     int snapshot;      // tables built by the snapshot rule (ovs_kad_load), not imported

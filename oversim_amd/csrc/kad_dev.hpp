@@ -10,7 +10,18 @@ namespace ovs {
 // ---------------------------------------------------------------------------
 // helpers
 
-__device__ __forceinline__ uint32_t kbit(const K160& k, int b) { return (k.w[b >> 5] >> (b & 31)) & 1u; }
+// word i (0..4, 5+ reads 0) of a key by selects: a dynamic k.w[i] would put the key in scratch
+__device__ __forceinline__ uint32_t kword(const K160& k, int i)
+{
+    uint32_t r = i == 0 ? k.w[0] : 0u;
+    r = i == 1 ? k.w[1] : r;
+    r = i == 2 ? k.w[2] : r;
+    r = i == 3 ? k.w[3] : r;
+    r = i == 4 ? k.w[4] : r;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t kbit(const K160& k, int b) { return (kword(k, b >> 5) >> (b & 31)) & 1u; }
 
 __device__ __forceinline__ K160 kload(const KeyRec* __restrict__ recs, uint32_t i) { return key_of(load_rec(recs, i)); }
 
@@ -194,23 +205,24 @@ __device__ __forceinline__ void blk_clear(Blk8& b)
     for (int i = 0; i < 8; ++i) { b.d[i] = ~0ull; b.x[i] = NONE; b.f[i] = 0; }
 }
 
-// the (up to 5) entries of one table line, unsorted, in slots 0..4 of b; returns how many
-__device__ __forceinline__ int blk_load_line(Blk8& b, const KadLine* __restrict__ l, const K160& K)
+// the (up to 8) entries of one table block, unsorted; returns how many
+__device__ __forceinline__ int blk_load_block(Blk8& b, const KadBlk* __restrict__ blk, const K160& K)
 {
+    const uint4* p = reinterpret_cast<const uint4*>(blk);
+    const uint4 t0 = p[0], t1 = p[1], t2 = p[2], t3 = p[3], i0 = p[4], i1 = p[5];
+    const uint64_t tops[8] = {(uint64_t)t0.x | ((uint64_t)t0.y << 32), (uint64_t)t0.z | ((uint64_t)t0.w << 32),
+                              (uint64_t)t1.x | ((uint64_t)t1.y << 32), (uint64_t)t1.z | ((uint64_t)t1.w << 32),
+                              (uint64_t)t2.x | ((uint64_t)t2.y << 32), (uint64_t)t2.z | ((uint64_t)t2.w << 32),
+                              (uint64_t)t3.x | ((uint64_t)t3.y << 32), (uint64_t)t3.z | ((uint64_t)t3.w << 32)};
+    const uint32_t ids[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
     const uint64_t kt = ktop(K);
     int n = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        if (q < KLINE) {
-            const uint32_t x = l->idx[q];
-            b.x[q] = x;
-            b.d[q] = x == NONE ? ~0ull : dclamp(l->top[q] ^ kt);
-            n += x != NONE ? 1 : 0;
-        } else {
-            b.x[q] = NONE;
-            b.d[q] = ~0ull;
-        }
+        b.x[q] = ids[q];
+        b.d[q] = ids[q] == NONE ? ~0ull : dclamp(tops[q] ^ kt);
         b.f[q] = 0;
+        n += ids[q] != NONE ? 1 : 0;
     }
     return n;
 }
@@ -250,8 +262,8 @@ __device__ __forceinline__ bool mask_hits(const KadView& V, const KadNode& r, ui
     const int mlo = end > 63 ? end - 63 : 0;
     // bits [mlo, mlo + 63] of D
     const int wi = mlo >> 5, sh = mlo & 31;
-    const uint64_t lo = (uint64_t)D.w[wi] | ((uint64_t)(wi + 1 < 5 ? D.w[wi + 1] : 0u) << 32);
-    const uint64_t hi = wi + 2 < 5 ? (uint64_t)D.w[wi + 2] : 0ull;
+    const uint64_t lo = (uint64_t)kword(D, wi) | ((uint64_t)kword(D, wi + 1) << 32);
+    const uint64_t hi = (uint64_t)kword(D, wi + 2);
     const uint64_t win = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
     return (win & r.mwin) != 0;
 }
@@ -282,10 +294,10 @@ __device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadNode& 
     const K160 D = k_xor(me, K);
     if (nsib == V.S5 && beyond_radius(V, r, c, D)) return false;
     if (!mask_hits(V, r, c, D)) return true;
-    const KadLine* L = V.sibl + (uint64_t)(c - V.lo) * V.sln;
+    const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
     int closer = 0;
     for (int i = 0; i < nsib; ++i) {
-        const uint32_t x = L[i / KLINE].idx[i % KLINE];
+        const uint32_t x = L[i / KBLK].idx[i % KBLK];
         closer += (int)kbit(D, k_msb(k_xor(node_key(V.nodes, x), me)));
     }
     return closer < numSiblings;
@@ -310,9 +322,9 @@ __device__ __forceinline__ RespGeo resp_geo(const KadNode& r, const K160& K)
     return g;
 }
 
-__device__ __forceinline__ const KadLine* slot_line(const KadView& V, uint32_t boff, int bucket, int j)
+__device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t boff, int bucket)
 {
-    return V.lines + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - bucket) * V.lps + j;
+    return V.blks + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - bucket);
 }
 
 // Kademlia::findNode(key, numRedundantNodes, numSiblings) at node c (Kademlia.cc:1101-1246),
@@ -336,27 +348,28 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     const int rs = sib ? numSiblings : numRedundant;
     const int cap = rs < 8 ? rs : 8;
     int n = 0, seen = 0;
-    auto add_line = [&](const KadLine* l) -> int {
+    auto add_blk = [&](const KadBlk* blk) {
         Blk8 b;
-        const int cnt = blk_load_line(b, l, K);
+        const int cnt = blk_load_block(b, blk, K);
         if (cnt) {
             blk_sort8<false, EX>(b, K, V.nodes);
             blk_merge_top8<false, EX>(res, b, K, V.nodes);
             n = blk_trunc(res, cap);
             seen += cnt;
         }
-        return cnt;
     };
     auto add_slot = [&](int bucket) {
         if (g.rowlo < 0 || bucket < g.rowlo) return;      // buckets below the stored row are empty
-        for (int j = 0; j < V.lps; ++j)
-            if (add_line(slot_line(V, g.boff, bucket, j)) < KLINE) break;
+        add_blk(slot_blk(V, g.boff, bucket));
     };
     if (g.m >= 0) add_slot(g.m);
-    if (g.m >= g.endIndex || seen < rs) {
+    // Members of bucket m are XOR-closer to K than everything below it (buckets < m, siblings --
+    // all at msb <= endIndex < m from c -- and c itself all differ from K at bit m): once bucket
+    // m fills the result, the rest of the scan cannot change it
+    if ((g.m >= g.endIndex || seen < rs) && !(g.m > g.endIndex && n >= cap)) {
         for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
-        const KadLine* L = V.sibl + (uint64_t)(c - V.lo) * V.sln;
-        for (int j = 0; j * KLINE < g.nsib; ++j) add_line(L + j);
+        const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
+        for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
         Blk8 self;
         blk_clear(self);
         self.x[0] = c;
@@ -367,6 +380,74 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     }
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);
     return n;
+}
+
+// BaseKeySortedVector::add with a KeyDistanceComparator<KeyXorMetric> (NodeVector.h:381-512):
+// dedupe by key (== by node index), insert before the first farther entry, truncate to cap.
+template <int CAP, bool EX>
+__device__ __forceinline__ int svec_add(SVec<CAP>& v, int cap, uint32_t x, uint64_t dx, const K160& K,
+                                        const KadNode* __restrict__ nodes)
+{
+    bool dup = false;
+    int pos = 0;
+#pragma unroll
+    for (int i = 0; i < CAP; ++i) {
+        if (i < v.n) {
+            dup |= (v.idx[i] == x);
+            pos += (v.idx[i] != x && cand_lt<EX>(v.d[i], v.idx[i], dx, x, K, nodes)) ? 1 : 0;
+        }
+    }
+    if (dup || pos >= cap) return -1;
+#pragma unroll
+    for (int i = CAP - 1; i >= 0; --i) {
+        if (i > pos) {
+            if (i >= 1) { v.idx[i] = v.idx[i - 1]; v.d[i] = v.d[i - 1]; }
+        } else if (i == pos) {
+            v.idx[i] = x; v.d[i] = dx;
+        }
+    }
+    v.n = v.n + 1 > cap ? cap : v.n + 1;
+    return pos;
+}
+
+// findNode for results of up to CAP (> 8) nodes, one insertion per candidate: the batch ABI
+// (ovs_find_node_batch accepts numRedundantNodes / numSiblings up to 16); same scan as
+// kad_find_node_blk
+template <int CAP, bool EX>
+__device__ __forceinline__ int kad_find_node_ins(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
+                                                 int numRedundant, bool sib, SVec<CAP>& res, int numSiblings)
+{
+    svec_clear(res);
+    if (g.nsib == 0 || (V.snapshot && sib && numSiblings <= 1)) {
+        svec_add<CAP, EX>(res, 1, c, dist_hi(node_key(V.nodes, c), K), K, V.nodes);
+        return 1;
+    }
+    const int rs = sib ? numSiblings : numRedundant;
+    const int cap = rs < CAP ? rs : CAP;
+    int seen = 0;
+    const uint64_t kt = ktop(K);
+    auto add_blk = [&](const KadBlk* blk) {
+        for (int q = 0; q < KBLK; ++q) {
+            const uint32_t x = blk->idx[q];
+            if (x == NONE) break;
+            svec_add<CAP, EX>(res, cap, x, dclamp(blk->top[q] ^ kt), K, V.nodes);
+            ++seen;
+        }
+    };
+    auto add_slot = [&](int bucket) {
+        if (g.rowlo < 0 || bucket < g.rowlo) return;
+        add_blk(slot_blk(V, g.boff, bucket));
+    };
+    if (g.m >= 0) add_slot(g.m);
+    if ((g.m >= g.endIndex || seen < rs) && !(g.m > g.endIndex && res.n >= cap)) {   // as kad_find_node_blk
+        for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
+        const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
+        for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
+        svec_add<CAP, EX>(res, cap, c, dist_hi(node_key(V.nodes, c), K), K, V.nodes);
+        seen += 1;
+    }
+    for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);
+    return res.n;
 }
 
 // LookupVector merge (IterativePathLookup::handleResponse's add loop, IterativeLookup.cc:853-870):
@@ -430,6 +511,15 @@ __device__ __forceinline__ void kad_find_node_vec(const KadView& V, uint32_t c, 
     res.used = 0;
 }
 
+// The scan of kad_find_node_blk counted: only explicit tables with short sibling tables reach it
+// (inlined: an out-of-line call costs the lookup kernels more registers than the second copy)
+template <bool EX>
+__device__ __forceinline__ int kad_scan_size(KadView V, uint32_t c, RespGeo g, K160 K, int rs, int numSiblings)
+{
+    Blk8 b;
+    return kad_find_node_blk<EX>(V, c, g, K, rs, false, b, numSiblings);
+}
+
 // The FindNodeResponse size of node c (its findNode result size): resultSize, unless explicit
 // tables leave c fewer candidates on its scan (then counted by running the scan)
 template <bool EX>
@@ -439,12 +529,11 @@ __device__ __forceinline__ int kad_response_size(const KadView& V, uint32_t c, c
     if (g.nsib == 0 || (sib && numSiblings <= 1)) return 1;
     const int full = rs < (int)V.n ? rs : (int)V.n;
     if (!V.maybe_short || g.nsib + 1 >= rs) return full;
-    Blk8 b;
-    return kad_find_node_blk<EX>(V, c, g, K, rs, false, b, numSiblings);
+    return kad_scan_size<EX>(V, c, g, K, rs, numSiblings);
 }
 
 // ---------------------------------------------------------------------------
-// IterativePathLookup, synchronous form (the sharded path, kad_shard.hip)
+// IterativePathLookup, one event per call (K2 in kad_route.hip, the sharded path in kad_shard.hip)
 
 constexpr int MAXA = 4;    // lookupParallelRpcs <= 4
 
@@ -463,23 +552,24 @@ struct Pend {
     int64_t t;         // event time
     uint32_t dins;     // t - insertion time
     uint32_t geo;      // responder: m + 1 (bits 0..7) | endIndex + 1 (8..15) | rowlo + 1 (16..23) | sib (24)
+                       // | sibling count (25..31; 5s <= 120)
     uint32_t boff;     // responder's bucket-row offset
-    uint32_t nsib;
 };
 
 __device__ __forceinline__ uint32_t pack_geo(const RespGeo& g, bool sb)
 {
-    return (uint32_t)(g.m + 1) | ((uint32_t)(g.endIndex + 1) << 8) | ((uint32_t)(g.rowlo + 1) << 16) | (sb ? 1u << 24 : 0u);
+    return (uint32_t)(g.m + 1) | ((uint32_t)(g.endIndex + 1) << 8) | ((uint32_t)(g.rowlo + 1) << 16) |
+           (sb ? 1u << 24 : 0u) | ((uint32_t)g.nsib << 25);
 }
 
-__device__ __forceinline__ RespGeo unpack_geo(uint32_t geo, uint32_t boff, uint32_t nsib)
+__device__ __forceinline__ RespGeo unpack_geo(uint32_t geo, uint32_t boff)
 {
     RespGeo g;
     g.m = (int)(geo & 0xFFu) - 1;
     g.endIndex = (int)((geo >> 8) & 0xFFu) - 1;
     g.rowlo = (int)((geo >> 16) & 0xFFu) - 1;
     g.boff = boff;
-    g.nsib = (int)nsib;
+    g.nsib = (int)(geo >> 25);
     return g;
 }
 
@@ -495,7 +585,7 @@ struct KadLookup {
     Pend p[A];
     uint32_t pvalid;
     int step, hops, pending;
-    bool pfinished, psuccess, any_to;
+    bool started, pfinished, psuccess, any_to;
     uint32_t result, nsent;
 };
 
@@ -511,7 +601,7 @@ __device__ __forceinline__ void kad_lookup_init(KadLookup<A>& L, const K160& K, 
     svec_clear(L.nh);
     L.pvalid = 0;
     L.step = 0; L.hops = 0; L.pending = 0;
-    L.pfinished = false; L.psuccess = false; L.any_to = false;
+    L.started = false; L.pfinished = false; L.psuccess = false; L.any_to = false;
     L.result = NONE;
     L.nsent = 0;
 }
@@ -555,7 +645,6 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
             L.p[i].tag = tag;
             L.p[i].geo = pack_geo(rg, sb);
             L.p[i].boff = rg.boff;
-            L.p[i].nsib = (uint32_t)rg.nsib;
         }
     }
     L.pvalid |= 1u << slot;
@@ -593,103 +682,100 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
     if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
 }
 
-template <int A, bool EX, bool LK, class OnSend>
-__device__ __forceinline__ void kad_timeoutlike(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
-                                                const KadLC& LC, const OnSend& on)
-{
-    // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
-    --L.pending;
-    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
-    else if (LC.newOnTimeout) kad_send_rpcs<A, EX, LK>(L, V, DC, LC, 1, on);
-    else if (L.pending == 0) kad_send_rpcs<A, EX, LK>(L, V, DC, LC, LC.alpha, on);
-}
-
-// IterativeLookup::start (IterativeLookup.cc:133-244): local findNode at the source
-template <int A, bool EX, bool LK, class OnSend>
-__device__ __forceinline__ void kad_lookup_start(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
-                                                 const KadLC& LC, SVec<8>& res, const OnSend& on)
-{
-    const KadNode rs = load_node(V.nodes, L.S);
-    const int ns = LK ? LC.numSiblings : 1;
-    const bool sb = kad_is_sibling(V, rs, L.S, L.K, ns);
-    kad_find_node_vec<8, EX>(V, L.S, rs, L.K, LC.maxRedundantLocal, sb, res, ns);
-    if (res.n == 0) { L.pfinished = true; L.psuccess = false; }
-    else if (LC.numSiblings != 0 && sb) {
-        L.result = res.idx[0];
-        L.pfinished = true; L.psuccess = true;
-    } else {
-        nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
-        kad_send_rpcs<A, EX, LK>(L, V, DC, LC, LC.alpha, on);
-    }
-}
-
 // checkStop (IterativeLookup.cc:295-349): the single path finished, or nothing pending
 template <int A>
 __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
 {
-    return L.pfinished || L.pvalid == 0;
+    return L.started && (L.pfinished || L.pvalid == 0);
 }
 
-// Process the earliest pending event (response or RPC timeout) of a running lookup.
-// getres.ready(slot) says whether the responder's findNode result is available (always on a
-// single GPU); getres.fill(slot, node, geometry, sibling, res) produces it.  Returns false, with the
-// state untouched, when the earliest event is a response whose result has not arrived yet.
+// Advance a lookup by one event.  The first call is IterativeLookup::start (IterativeLookup.cc:
+// 133-244): findNode at the source itself.  Every later call processes the earliest pending
+// event, a FindNodeResponse or an RPC timeout.  getres.ready(slot) says whether the responder's
+// findNode result is available (always on a single GPU); getres.fill(slot, node, geometry,
+// sibling, numRedundant, local, res) produces it (local: the source's own findNode at start).
+// Returns false, with the state untouched, when the earliest event is a response whose result
+// has not arrived yet.  Start, responses and timeouts share one findNode, one LookupVector merge
+// and one sendRpc site, so the kernels inline each once.
 template <int A, bool EX, bool LK, class GetRes, class OnSend, class Rec>
 __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
                                                  const KadLC& LC, SVec<8>& res, const GetRes& getres,
                                                  const OnSend& on, const Rec& record)
 {
-    int e = -1;
-    int64_t bt = 0, bi = 0;
-    uint32_t bs = 0;
+    const int ns = LK ? LC.numSiblings : 1;
+    uint32_t r = L.S;
+    RespGeo rg;
+    bool sb = false, resp = true;
+    int e = -1, numR = LC.redundant;
+    const bool start = !L.started;
+    if (start) {
+        L.started = true;
+        const KadNode rn = load_node(V.nodes, L.S);
+        sb = kad_is_sibling(V, rn, L.S, L.K, ns);
+        rg = resp_geo(rn, L.K);
+        numR = LC.maxRedundantLocal;
+    } else {
+        int64_t bt = 0, bi = 0;
+        uint32_t bs = 0;
 #pragma unroll
-    for (int i = 0; i < A; ++i) {
-        if ((L.pvalid >> i) & 1u) {
-            const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
-            const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
-            const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
-            if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
+        for (int i = 0; i < A; ++i) {
+            if ((L.pvalid >> i) & 1u) {
+                const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
+                const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
+                const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
+                if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
+            }
+        }
+        uint32_t tag = 0, geo = 0, boff = 0;
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+            if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; }
+        if (!(tag & 0x80000000u) && !getres.ready(e)) return false;
+        L.pvalid &= ~(1u << e);
+        L.now = bt;
+        if (tag & 0x80000000u) {
+            // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
+            L.any_to = true;
+            resp = false;
+        } else {
+            // the responder's siblings flag and bucket geometry were captured at send (kad_send)
+            sb = (geo >> 24) & 1u;
+            rg = unpack_geo(geo, boff);
+            const bool acc = (LC.useAll && LC.merge) ? true : ((int)(tag & 0xFFFFu) == L.step);
+            // not accepted: handled as a timeout, its nodes are dropped
+            resp = acc || (sb && LC.acceptLateSiblings);
         }
     }
-    uint32_t r = 0, tag = 0, geo = 0, boff = 0, nsib = 0;
-#pragma unroll
-    for (int i = 0; i < A; ++i)
-        if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; nsib = L.p[i].nsib; }
-    if (!(tag & 0x80000000u) && !getres.ready(e)) return false;
-    L.pvalid &= ~(1u << e);
-    L.now = bt;
-    const int vr = (int)(tag & 0xFFFFu);
-    if (tag & 0x80000000u) {
-        // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
-        L.any_to = true;
-        kad_timeoutlike<A, EX, LK>(L, V, DC, LC, on);
-        return true;
-    }
-    // the responder's siblings flag and bucket geometry were captured at send (kad_send)
-    const bool sb = (geo >> 24) & 1u;
-    const RespGeo rg = unpack_geo(geo, boff, nsib);
-    const bool acc = (LC.useAll && LC.merge) ? true : (vr == L.step);
-    if (!(acc || (sb && LC.acceptLateSiblings))) {
-        // not accepted: handled as a timeout, its nodes are dropped
-        kad_timeoutlike<A, EX, LK>(L, V, DC, LC, on);
-        return true;
-    }
-    // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
-    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return true; }
-    if (r != L.S) {
-        record(L.hops, r);
-        ++L.hops;
-    }
-    ++L.step;
-    --L.pending;
-    getres.fill(e, r, rg, sb, res);
-    int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
-    if (LC.numSiblings != 0 && sb && res.n > 0 && L.result == NONE) L.result = res.idx[0];
-    if (sb && res.n != 0 && LC.numSiblings != 0) { L.pfinished = true; L.psuccess = true; }
-    else {
+    int num;
+    if (resp) {
+        if (!start) {
+            // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
+            if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return true; }
+            if (r != L.S) {
+                record(L.hops, r);
+                ++L.hops;
+            }
+            ++L.step;
+            --L.pending;
+        }
+        getres.fill(e, r, rg, sb, numR, start, res);
+        int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
+        if (LC.numSiblings != 0 && sb && res.n > 0) {
+            if (L.result == NONE) L.result = res.idx[0];
+            L.pfinished = true; L.psuccess = true;
+            return true;
+        }
         if (numNew == 0 && LC.newOnResp) numNew = 1;
-        kad_send_rpcs<A, EX, LK>(L, V, DC, LC, min(numNew, LC.alpha), on);
+        num = start ? LC.alpha : min(numNew, LC.alpha);
+    } else {
+        // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
+        --L.pending;
+        if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return true; }
+        if (LC.newOnTimeout) num = 1;
+        else if (L.pending == 0) num = LC.alpha;
+        else return true;
     }
+    kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, on);
     return true;
 }
 
@@ -731,10 +817,9 @@ __device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A>& L
 inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
 {
     KadView V{};
-    V.nodes = t.nodes; V.nodex = t.nodex; V.lines = t.lines; V.sibl = t.lines ? t.lines + t.rows_lines : nullptr;
+    V.nodes = t.nodes; V.nodex = t.nodex; V.blks = t.blks; V.sibb = t.blks ? t.blks + t.rows_blks : nullptr;
     V.xy = xy; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
-    V.lps = (t.k + KLINE - 1) / KLINE;
-    V.sln = (V.S5 + KLINE - 1) / KLINE;
+    V.sbn = (V.S5 + KBLK - 1) / KBLK;
     V.lo = t.lo; V.hi = t.hi;
     V.maybe_short = t.maybe_short;
     V.snapshot = t.snapshot;
@@ -768,5 +853,11 @@ inline KadLC kad_make_lc(const ovs_params& P, const KadTables& t)
     LC.maxRedundantLocal = t.k;
     return LC;
 }
+
+// K2 for one (alpha, exact) pair; instantiated in kad_route.hip (one object per pair)
+template <int A, bool EX>
+hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
+                            const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
+                            uint32_t* sibs, int num_cu, hipStream_t st);
 
 }  // namespace ovs

@@ -35,12 +35,26 @@ __device__ __forceinline__ int kshard_owner(const uint64_t* __restrict__ lo, int
 }
 
 // result slot of pending event `slot` of lookup i
+template <bool EX>
 struct ShardRes {
     KadRes* __restrict__ res;
     uint64_t base;
+    const KadView& V;
+    const K160& K;
     __device__ __forceinline__ bool ready(int slot) const { return res[base + slot].ready != 0; }
-    __device__ __forceinline__ void fill(int slot, uint32_t, const RespGeo&, bool, SVec<8>& v) const
+    __device__ __forceinline__ void fill(int slot, uint32_t c, const RespGeo& g, bool sb, int numR, bool local,
+                                         SVec<8>& v) const
     {
+        if (local) {
+            // IterativeLookup::start: findNode at the source, on its home rank
+            Blk8 b;
+            const int n = kad_find_node_blk<EX>(V, c, g, K, numR, sb, b, 1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { v.idx[i] = b.x[i]; v.d[i] = b.d[i]; }
+            v.n = n;
+            v.used = 0;
+            return;
+        }
         const KadRes& r = res[base + slot];
         svec_clear(v);
         const int n = (int)r.count;
@@ -103,8 +117,7 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
     KadLookup<A> L = st[i];
     SVec<8> r;
     ShardSend on{res, i * A, &L.K, shard_lo, nsh, out, out_dest, out_cap, out_count};
-    if (a == 2) kad_lookup_start<A, EX, false>(L, V, DC, LC, r, on);   // first round: IterativeLookup::start
-    const ShardRes gr{res, i * A};
+    const ShardRes<EX> gr{res, i * A, V, L.K};   // the first event is IterativeLookup::start
     const NoRecord rec;
     while (!kad_lookup_done(L)) {
         if (!kad_lookup_event<A, EX, false>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
@@ -136,7 +149,7 @@ __global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* 
     KadLookup<A> L;
     kad_lookup_init(L, keys[i], src[i], xy);
     st[i] = L;
-    act[i] = 2;
+    act[i] = 1;
     qids[i] = qid_base + (uint32_t)i;
     for (int s = 0; s < A; ++s) res[i * A + s].ready = 1;
 }
