@@ -214,6 +214,12 @@ def key_to_int(w) -> int:
     return sum(int(w[i]) << (32 * i) for i in range(5))
 
 
+class FixFingersStats(C.Structure):
+    """ovs_fixfingers_stats: one fixfingers round (ovs_chord_fix_fingers)."""
+
+    _fields_ = [("lookups", C.c_uint64), ("ok", C.c_uint64), ("changed", C.c_uint64), ("hops", C.c_uint64)]
+
+
 class KbrTestLookupStats(C.Structure):
     """ovs_kbrtest_lookup_stats: KBRTestApp lookup-test statistics of a batch (KBRTestApp.cc:331-371, 546-557)."""
 
@@ -338,10 +344,10 @@ class KbrEngine:
         """One synchronous fixfingers round on an explicit-table ring (ovs_chord_fix_fingers):
         the batched maintenance lookups of Chord::handleFixFingersTimerExpired."""
         nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
-        st = (C.c_uint64 * 4)()
-        self._chk(self._L.ovs_chord_fix_fingers(self._h, _ptr(nodes), len(nodes), C.cast(st, C.c_void_p)),
+        st = FixFingersStats()
+        self._chk(self._L.ovs_chord_fix_fingers(self._h, _ptr(nodes), len(nodes), C.cast(C.byref(st), C.c_void_p)),
                   "ovs_chord_fix_fingers")
-        return {"lookups": st[0], "ok": st[1], "changed": st[2], "hops": st[3]}
+        return {f: getattr(st, f) for f, _ in FixFingersStats._fields_}
 
     def kad_tables(self):
         p = self.get_params()

@@ -267,7 +267,10 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
 # ---------------------------------------------------------------------------
 # Kademlia: lookups stay home, FindNodeCalls are requests to the responder's owner
 
-KAD_REQ_BYTES, KAD_RESP_BYTES = 32, 104
+KAD_REQ_DTYPE = np.dtype([("key", "<u4", 5), ("node", "<u4"), ("tag", "<u4"), ("pad", "<u4")])
+KAD_RESP_DTYPE = np.dtype([("tag", "<u4"), ("count", "<u4"), ("nodes", "<u4", 8), ("dist_hi", "<u8", 8)])
+KAD_REQ_BYTES, KAD_RESP_BYTES = KAD_REQ_DTYPE.itemsize, KAD_RESP_DTYPE.itemsize
+assert (KAD_REQ_BYTES, KAD_RESP_BYTES) == (32, 104)
 
 
 class KadShardStepper:
