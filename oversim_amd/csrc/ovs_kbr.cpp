@@ -220,6 +220,9 @@ ovs_status ensure_nodes(ovs_ctx* c, hipStream_t s)
     if (!c->win) HIPCHK(c, hipMalloc(&c->win, sizeof(WinRec) * (c->shard_hi - c->shard_lo)));
     HIPCHK(c, launch_chord_nodes(c->recs, c->xy, (uint32_t)c->n, ns, c->nodes, c->fingers, c->nfing, c->win,
                                  (uint32_t)c->shard_lo, (uint32_t)c->shard_hi, s));
+    // the records are built once and then read by kernels on any stream (e.g. one stream per
+    // cohort of ovs_shard_step): complete them before any other call can see nodes_ns set
+    HIPCHK(c, hipStreamSynchronize(s));
     c->nodes_ns = ns;
     return OVS_OK;
 }

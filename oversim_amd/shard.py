@@ -13,7 +13,14 @@ in OverSim (BaseOverlay.cc:1841-1915).  Per round:
   2. one all-gather of the per-destination counts gives every rank the whole
      count matrix (sizes of the all-to-allv and the termination test) -- the
      round's only host synchronisation;
-  3. one all-to-allv moves the records (48 B per lookup).
+  3. one all-to-allv moves the records (48 B per lookup): grouped point-to-point
+     sends straight out of the kernel's destination segments into one receive
+     buffer (no packing copy).
+
+The lookups of a rank are split into cohorts (default 2), each with its own HIP
+stream, send segments and counters.  A cohort's kernel, count gather, host wait
+and exchange are ordered on its own stream only, so the exchange of one cohort
+runs while the kernel of the other computes.
 
 The orchestration is independent of the stepper (the HIP kernel here, a CPU
 test double in tests/) and of the exchange (torch.distributed, or an in-process
@@ -62,28 +69,56 @@ class GpuShardStepper:
         self.eng._chk(st, "ovs_chord_load_shard")
         self.n_total = len(ids)
         self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
-        self.cap = 0
-        self._ensure(capacity)
-        self.out_count = torch.zeros(self.world, dtype=torch.int64, device=device)
+        self._cap = {}
+        self._out = {}
+        self._cnt = {}
+        self._ev = {}
+        self._timed = {}
+        self._streams = []
+        self._ensure(0, capacity)
         self.done_count = torch.zeros(1, dtype=torch.int64, device=device)
         self.done = torch.empty((max(capacity, 1), DONE_BYTES), dtype=torch.uint8, device=device)
         self.done_cap = max(capacity, 1)
         self.timing = False
         self.kernel_ms = 0.0
-        self._ev0 = torch.cuda.Event(enable_timing=True)
-        self._ev1 = torch.cuda.Event(enable_timing=True)
 
-    def _ensure(self, cap: int):
-        if cap <= self.cap:
+    def _ensure(self, cohort: int, cap: int):
+        if cap <= self._cap.get(cohort, 0):
             return
-        self.cap = cap
+        self._cap[cohort] = cap
         # one send segment of `cap` records per destination rank
-        self.out = self.torch.empty((self.world, cap, REC_BYTES), dtype=self.torch.uint8, device=self.dev)
+        self._out[cohort] = self.torch.empty((self.world, cap, REC_BYTES), dtype=self.torch.uint8, device=self.dev)
+        if cohort not in self._cnt:
+            self._cnt[cohort] = self.torch.zeros(self.world, dtype=self.torch.int64, device=self.dev)
+            self._ev[cohort] = (self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True))
+
+    @property
+    def cap(self) -> int:
+        return self._cap[0]
 
     def _s(self):
-        # every kernel of the round runs on torch's current stream, so the torch ops around it
-        # (counter resets, the collectives) are ordered with it
+        # every kernel runs on torch's current stream (the cohort's stream inside cohort()), so
+        # the torch ops around it (counter resets, the collectives) are ordered with it
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def begin_cohorts(self, n: int):
+        """n cohort streams, each ordered after the work queued so far (the inputs)."""
+        torch = self.torch
+        while len(self._streams) < n:
+            self._streams.append(torch.cuda.Stream(self.dev))
+        cur = torch.cuda.current_stream(self.dev)
+        for st in self._streams[:n]:
+            st.wait_stream(cur)
+        self._ncoh = n
+
+    def end_cohorts(self):
+        cur = self.torch.cuda.current_stream(self.dev)
+        for st in self._streams[:getattr(self, "_ncoh", 0)]:
+            cur.wait_stream(st)
+
+    def cohort(self, c: int):
+        """Context in which cohort c's kernels and collectives are issued (its own stream)."""
+        return self.torch.cuda.stream(self._streams[c])
 
     def reset(self, capacity: int):
         self.done_count.zero_()
@@ -99,28 +134,32 @@ class GpuShardStepper:
         self.eng._chk(st, "ovs_shard_make_records")
         return recs
 
-    def step(self, inbox):
-        """One round; returns (send segments [world, cap, 48], per-destination counts on the device)."""
+    def step(self, inbox, cohort: int = 0):
+        """One round of a cohort; returns (send segments [world, cap, 48], per-destination counts
+        on the device).  The segments stay valid until the cohort's next step."""
         n_in = inbox.shape[0]
-        self._ensure(n_in)
-        self.out_count.zero_()
+        self._ensure(cohort, n_in)
+        out, cnt = self._out[cohort], self._cnt[cohort]
+        cnt.zero_()
         if self.timing:
-            self._ev0.record()
-        st = lib().ovs_shard_step(self.eng._h, C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(self.out.data_ptr()),
-                                  self.cap, C.c_void_p(self.out_count.data_ptr()),
+            self._ev[cohort][0].record()
+        st = lib().ovs_shard_step(self.eng._h, C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(out.data_ptr()),
+                                  self._cap[cohort], C.c_void_p(cnt.data_ptr()),
                                   C.c_void_p(self.done.data_ptr()), self.done_cap,
                                   C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
         self.eng._chk(st, "ovs_shard_step")
         if self.timing:
-            self._ev1.record()
-            self._timed = True
-        return self.out, self.out_count
+            self._ev[cohort][1].record()
+            self._timed[cohort] = True
+        return out, cnt
 
-    def collect_timing(self):
-        """Add the last step's kernel time (call after the round's host synchronisation)."""
-        if self.timing and getattr(self, "_timed", False):
-            self.kernel_ms += self._ev0.elapsed_time(self._ev1)
-            self._timed = False
+    def collect_timing(self, cohort: int = 0):
+        """Add the cohort's last step kernel time (call after its host synchronisation)."""
+        if self.timing and self._timed.get(cohort):
+            e0, e1 = self._ev[cohort]
+            e1.synchronize()
+            self.kernel_ms += e0.elapsed_time(e1)
+            self._timed[cohort] = False
 
     def finished(self):
         k = int(self.done_count.item())
@@ -162,11 +201,48 @@ class TorchExchange:
 
     def count_matrix(self, counts) -> np.ndarray:
         """All-gather every rank's per-destination counts: M[s, d] = records rank s sends to d."""
+        return self.count_matrix_async(counts)()
+
+    def count_matrix_async(self, counts):
+        """Start the count all-gather on the current stream; returns a callable that waits for
+        it (and only for the work queued on this stream) and gives the matrix."""
         torch = self.torch
         c = counts.to(self.comm_dev, dtype=torch.int64).reshape(-1)
         parts = [torch.empty_like(c) for _ in range(self.world)]
         self.dist.all_gather(parts, c, group=self.group)
-        return torch.stack(parts).cpu().numpy()
+        M = torch.stack(parts)
+        if M.device.type != "cuda":
+            return lambda: M.numpy()
+        host = torch.empty(M.shape, dtype=torch.int64, pin_memory=True)
+        host.copy_(M, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+
+        def wait():
+            ev.synchronize()
+            return host.numpy()
+        return wait
+
+    def segments(self, segs, scl, rcl, row_bytes: int):
+        """all-to-allv of fixed-size records from per-destination segments (segs[d][:scl[d]])
+        into one receive buffer ordered by source rank: grouped point-to-point sends out of
+        the segments, so nothing is packed first."""
+        torch, dist = self.torch, self.dist
+        recv = torch.empty((sum(rcl), row_bytes), dtype=torch.uint8, device=self.comm_dev)
+        ops, off = [], 0
+        for r in range(self.world):
+            if rcl[r] and r != self.rank:
+                ops.append(dist.P2POp(dist.irecv, recv[off:off + rcl[r]], r, group=self.group))
+            elif rcl[r]:
+                recv[off:off + rcl[r]].copy_(segs[r][:rcl[r]])
+            off += rcl[r]
+        for d in range(self.world):
+            if scl[d] and d != self.rank:
+                ops.append(dist.P2POp(dist.isend, segs[d][:scl[d]].to(self.comm_dev), d, group=self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return recv
 
     def counts(self, send_counts):
         """Exchange per-destination counts; returns (send counts, receive counts) as lists."""
@@ -206,34 +282,64 @@ def group_by_dest(out, dest, world: int):
     return out.index_select(0, order), counts
 
 
-def _send_buffer(out, row):
-    """The all-to-allv send buffer: destination segments out[d][:row[d]] back to back."""
-    import torch
-    parts = [out[d][: int(k)] for d, k in enumerate(row) if k]
-    if not parts:
-        return out[0][:0]
-    return parts[0] if len(parts) == 1 else torch.cat(parts)
+def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 10_000, cohorts: int = 2,
+                  min_split: int = 2048):
+    """Route one batch of lookups originating on this rank; returns (done records, rounds).
 
-
-def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 10_000):
-    """Route one batch of lookups originating on this rank; returns (done records, rounds)."""
-    inbox = stepper.make_records(keys_t, src_t, qid_base)
-    rounds = 0
+    The batch is split into `cohorts` contiguous cohorts (one if the stepper has no cohort
+    support or the batch is small).  Every round first issues the step kernel of each live
+    cohort (each on its own stream; the persistent grids run one after the other), then per
+    cohort its count gather, the host wait for it and its exchange.  The collectives share
+    one communicator stream in issue order (gather 0, exchange 0, gather 1, exchange 1), so
+    cohort 0's exchange is in flight while cohort 1's kernel still runs, and cohort 1's while
+    cohort 0's next kernel runs.  Every rank takes the same decisions from the same gathered
+    matrices, so the collectives match across ranks."""
+    n = int(keys_t.shape[0])
+    if not hasattr(stepper, "cohort") or n < min_split * cohorts:
+        cohorts = 1
+    bounds = [c * n // cohorts for c in range(cohorts + 1)]
     me = exchange.rank
-    while True:
+    if hasattr(stepper, "begin_cohorts"):
+        stepper.begin_cohorts(cohorts)
+    ctx = stepper.cohort if hasattr(stepper, "cohort") else (lambda c: _NoCtx())
+    step = (lambda inbox, c: stepper.step(inbox, c)) if hasattr(stepper, "cohort") else (lambda inbox, c: stepper.step(inbox))
+    inbox = []
+    for c in range(cohorts):
+        with ctx(c):
+            inbox.append(stepper.make_records(keys_t[bounds[c]:bounds[c + 1]], src_t[bounds[c]:bounds[c + 1]],
+                                              qid_base + bounds[c]))
+    live = [True] * cohorts
+    rounds = 0
+    while any(live):
         rounds += 1
-        out, counts = stepper.step(inbox)
-        M = exchange.count_matrix(counts)          # the round's host synchronisation
-        if hasattr(stepper, "collect_timing"):
-            stepper.collect_timing()
-        if int(M.sum()) == 0:
-            break
-        send = _send_buffer(out, M[me])
-        recv = exchange.records(send, M[me].tolist(), M[:, me].tolist())
-        inbox = recv if recv.device == send.device else recv.to(send.device)
+        issued = []
+        for c in range(cohorts):
+            if live[c]:
+                with ctx(c):
+                    issued.append((c,) + tuple(step(inbox[c], c)))
+        for c, out, counts in issued:
+            with ctx(c):
+                M = exchange.count_matrix_async(counts)()     # the cohort's round synchronisation
+                if hasattr(stepper, "collect_timing"):
+                    stepper.collect_timing(c) if hasattr(stepper, "cohort") else stepper.collect_timing()
+                if int(M.sum()) == 0:
+                    live[c] = False
+                    continue
+                recv = exchange.segments(out, M[me].tolist(), M[:, me].tolist(), REC_BYTES)
+                inbox[c] = recv if recv.device == stepper.dev else recv.to(stepper.dev)
         if rounds > max_rounds:
             raise RuntimeError("sharded routing did not terminate")
+    if hasattr(stepper, "end_cohorts"):
+        stepper.end_cohorts()
     return stepper.finished(), rounds
+
+
+class _NoCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_rounds: int = 10_000):

@@ -52,7 +52,11 @@ class CpuShardStepper:
     def owner(self, c):
         return int(np.searchsorted(self.bounds, c, side="right") - 1)
 
-    def step(self, inbox):
+    def cohort(self, c):
+        from oversim_amd.shard import _NoCtx
+        return _NoCtx()
+
+    def step(self, inbox, cohort=0):
         recs = inbox.numpy().view(self.REC).ravel()
         out, dest = [], []
         ring = self.ring
@@ -108,7 +112,7 @@ class CpuShardStepper:
         return torch.from_numpy(d.view(np.uint8).reshape(-1, 24).copy())
 
 
-def _cpu_worker(rank, world, port, n, m, q):
+def _cpu_worker(rank, world, port, n, m, q, cohorts=1):
     import torch.distributed as dist
     from oversim_amd.shard import TorchExchange, arc_bounds, done_to_numpy, route_sharded
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -119,19 +123,21 @@ def _cpu_worker(rank, world, port, n, m, q):
     src = (bounds[rank] + src.astype(np.int64) % (bounds[rank + 1] - bounds[rank])).astype(np.uint32)
     st = CpuShardStepper(net.ids, net.xy, bounds, rank)
     done, rounds = route_sharded(st, TorchExchange(world, torch.device("cpu")), torch.from_numpy(keys),
-                                 torch.from_numpy(src), rank * m)
+                                 torch.from_numpy(src), rank * m, cohorts=cohorts, min_split=1)
     q.put((rank, done_to_numpy(done), keys, src, rounds))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_sharded_orchestration_gloo_cpu():
+@pytest.mark.parametrize("world,cohorts", [(2, 1), (2, 2), (3, 3)])
+def test_sharded_orchestration_gloo_cpu(world, cohorts):
+    """cohorts > 1: the lookups of a rank in cohorts whose exchanges interleave (route_sharded)."""
     import torch.multiprocessing as mp
-    world, n, m = 2, 600, 300
+    n, m = 600, 300
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, n, m, q)) for r in range(world)]
+    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, n, m, q, cohorts)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -206,8 +212,9 @@ def _gpu_worker(rank, world, port, q):
     dev = torch.device("cuda", 0)
     st = GpuShardStepper(net.ids, net.xy, bounds, rank, dev, capacity=world * m)
     st.reset(world * m)
+    # two cohorts on two HIP streams (the exchange of one overlaps the kernel of the other)
     done, rounds = route_sharded(st, TorchExchange(world, torch.device("cpu")), torch.from_numpy(k).to(dev),
-                                 torch.from_numpy(s).to(dev), rank * m)
+                                 torch.from_numpy(s).to(dev), rank * m, cohorts=2, min_split=1)
     q.put((rank, done_to_numpy(done), k, s))
     dist.barrier()
     dist.destroy_process_group()
