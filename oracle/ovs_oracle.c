@@ -236,8 +236,22 @@ static void params_common(orc_params* p)
     p->kadSeed = 0x4b41444dull;
     p->routingType = 0;          /* default.ini:392 "iterative" */
     p->recNumRedundantNodes = 3; /* default.ini:386 */
+    p->shiftingBits = 4;         /* default.ini:277 */
+    p->deBruijnListSize = 16;    /* default.ini:276 */
+    p->useOtherLookup = 1;       /* default.ini:279 */
+    p->useSucList = 1;           /* default.ini:280 */
 }
 void orc_params_chord_default(orc_params* p) { params_common(p); }
+void orc_params_koorde_default(orc_params* p)
+{
+    params_common(p);
+    p->successorListSize = 16;   /* default.ini:275 */
+    /* KOORDEFINDNODEEXTMESSAGE_L = KEY_L + STEP_L = 168 bits (ChordMessage.msg:33,55) rides on
+     * every FindNodeCall and FindNodeResponse of a Koorde lookup (IterativeLookup.cc:359-390,
+     * BaseOverlay.cc:1903-1907) */
+    p->callBytes += 21;
+    p->respBaseBytes += 21;
+}
 void orc_params_kad_default(orc_params* p)
 {
     params_common(p);
@@ -249,7 +263,7 @@ void orc_params_kad_default(orc_params* p)
 /* ===================================================================== */
 /* networks                                                              */
 /* ===================================================================== */
-enum { NET_CHORD = 1, NET_KAD = 2 };
+enum { NET_CHORD = 1, NET_KAD = 2, NET_KOORDE = 3 };   /* NET_KOORDE: Chord tables + de Bruijn state */
 #define NONE 0xFFFFFFFFu
 
 struct orc_net {
@@ -276,6 +290,10 @@ struct orc_net {
     uint8_t* nsib;
     uint32_t* bucket;       /* n * 160 * k */
     uint8_t* bcount;        /* n * 160 */
+    /* Koorde: deBruijnNode, deBruijnNodes = kdbNum ring nodes from sorted index kdbStart */
+    uint32_t* kdb;
+    uint32_t* kdbStart;
+    uint8_t* kdbNum;
 };
 
 void orc_net_free(orc_net* net)
@@ -283,7 +301,7 @@ void orc_net_free(orc_net* net)
     if (!net) return;
     free(net->ids); free(net->xy); free(net->pred); free(net->succ); free(net->nsucc);
     free(net->fdeque); free(net->fsize); free(net->sib); free(net->nsib); free(net->bucket);
-    free(net->bcount); free(net);
+    free(net->bcount); free(net->kdb); free(net->kdbStart); free(net->kdbNum); free(net);
 }
 
 static orc_net* net_alloc(int type, const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
@@ -925,20 +943,245 @@ void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_coun
     }
 }
 
+/* ---- Koorde (src/overlay/koorde/Koorde.cc) ------------------------------------ */
+/* OverlayKey::operator<< / operator>> (OverlayKey.cc:386-425): limb shift, then trim() to
+ * keyLength.  The reference shifts with mpn_lshift / mpn_rshift, which GMP defines only for
+ * counts 1..63: a shift whose count is a multiple of 64 (by 0, 64 or 128 bits) is undefined
+ * there and its result depends on the GMP build; this restatement takes the exact shift
+ * (DESIGN.md §Koorde). */
+static OKey ok_shl(OKey a, int n)
+{
+    OKey r; memset(&r, 0, sizeof r);
+    if (n >= 160) return r;
+    for (int i = A_SIZE - 1; i >= 0; --i) {
+        int src = i - n / 64, b = n % 64;
+        uint64_t v = 0;
+        if (src >= 0) v = a.key[src] << b;
+        if (b && src - 1 >= 0) v |= a.key[src - 1] >> (64 - b);
+        r.key[i] = v;
+    }
+    ok_trim(&r);
+    return r;
+}
+static OKey ok_shr(OKey a, int n)
+{
+    OKey r; memset(&r, 0, sizeof r);
+    if (n >= 160) return r;
+    for (int i = 0; i < A_SIZE; ++i) {
+        int src = i + n / 64, b = n % 64;
+        uint64_t v = 0;
+        if (src < A_SIZE) v = a.key[src] >> b;
+        if (b && src + 1 < A_SIZE) v |= a.key[src + 1] << (64 - b);
+        r.key[i] = v;
+    }
+    ok_trim(&r);
+    return r;
+}
+static OKey ok_small(uint32_t v)                                          /* OverlayKey(uint32_t) 73-78 */
+{
+    OKey r; memset(&r, 0, sizeof r);
+    r.key[0] = v;
+    return r;
+}
+
+typedef struct { OKey routeKey; int step; } KExt;   /* KoordeFindNodeExtMessage (ChordMessage.msg:168-172) */
+
+static uint32_t koorde_walkSuccessorList(const orc_net* net, uint32_t self, const OKey* key)   /* 572-582 */
+{
+    int size = nsucc_get(net, self);
+    for (int i = 0; i < size - 1; i++) {
+        uint32_t a = succ_get(net, self, (uint32_t)i), b = succ_get(net, self, (uint32_t)i + 1);
+        if (ok_isBetweenR(key, &net->ids[a], &net->ids[b])) return a;
+    }
+    return succ_get(net, self, (uint32_t)size - 1);
+}
+static uint32_t koorde_db(const orc_net* net, uint32_t self, int i)
+{
+    return (uint32_t)(((uint64_t)net->kdbStart[self] + (uint64_t)i) % net->n);
+}
+static uint32_t koorde_walkDeBruijnList(const orc_net* net, uint32_t self, const OKey* key)   /* 558-570 */
+{
+    int num = net->kdbNum[self];
+    if (num == 0) return NONE;
+    for (int i = 0; i < num - 1; i++) {
+        uint32_t a = koorde_db(net, self, i), b = koorde_db(net, self, i + 1);
+        if (ok_isBetweenR(key, &net->ids[a], &net->ids[b])) return a;
+    }
+    return koorde_db(net, self, num - 1);
+}
+/* Koorde::findStartKey (664-762) without its disabled #if 0 block; -1 = cRuntimeError */
+static int koorde_findStartKey(const orc_net* net, const OKey* startKey, const OKey* endKey, const OKey* destKey,
+                               OKey* out, int* step)
+{
+    if (EQ(startKey, endKey)) { *out = *startKey; return 0; }   /* step is left as it was */
+    OKey diffKey = ok_sub(*endKey, startKey);
+    int nBits = ok_log2(&diffKey);
+    if (nBits < 0) nBits = 0;
+    while ((160 - nBits) % net->p.shiftingBits != 0) nBits--;
+    *step = nBits + 1;
+    OKey newStart = ok_shl(ok_shr(*startKey, nBits), nBits);
+    OKey tmpDest = ok_shr(*destKey, 160 - nBits);
+    OKey newKey = ok_add(tmpDest, &newStart);
+    if (ok_isBetweenR(&newKey, startKey, endKey)) { *out = newKey; return 0; }
+    OKey pw = ok_pow2((uint32_t)nBits);
+    newKey = ok_add(newKey, &pw);
+    if (ok_isBetweenR(&newKey, startKey, endKey)) { *out = newKey; return 0; }
+    set_err("Koorde::findStartKey(): Invalid start key");
+    return -1;
+}
+/* Koorde::findDeBruijnHop (473-556) on a converged ring (deBruijnNode specified) */
+static uint32_t koorde_findDeBruijnHop(const orc_net* net, uint32_t self, const OKey* destKey, KExt* ext,
+                                       int* breakLookup, int* err)
+{
+    const orc_params* p = &net->p;
+    uint32_t s0 = succ_get(net, self, 0);
+    uint32_t dbNode = net->kdb[self];
+    if (ext->routeKey.isUnspec) {
+        int step = ext->step;
+        OKey rk;
+        if (koorde_findStartKey(net, &net->ids[self], &net->ids[s0], destKey, &rk, &step) < 0) { *err = 1; return NONE; }
+        ext->routeKey = rk;
+        ext->step = step;
+    }
+    if (ok_isBetweenR(&ext->routeKey, &net->ids[self], &net->ids[s0])) {
+        if (ext->step > 160) { set_err("Koorde::findDeBruijnHop - Bounding error"); *err = 1; return NONE; }
+        OKey add; memset(&add, 0, sizeof add);
+        for (int i = 0; i < p->shiftingBits; i++) {
+            int pos = 160 - ext->step - i;
+            /* getBit(p) = getBitRange(p, 1): a position below 0 wraps to a huge uint32 -> throws */
+            if (pos < 0) { set_err("OverlayKey::getBitRange(): invalid range"); *err = 1; return NONE; }
+            OKey bit = ok_small(ok_getBitRange(destKey, (uint32_t)pos, 1));
+            add = (i == 0) ? bit : ok_add(ok_shl(add, 1), &bit);
+        }
+        OKey rk = ok_add(ok_shl(ext->routeKey, p->shiftingBits), &add);
+        ext->routeKey = rk;
+        ext->step += p->shiftingBits;
+        if (net->kdbNum[self] > 0) {
+            uint32_t db0 = koorde_db(net, self, 0);
+            if (ok_isBetweenR(&ext->routeKey, &net->ids[dbNode], &net->ids[db0])) return dbNode;
+            return koorde_walkDeBruijnList(net, self, &ext->routeKey);
+        }
+        return dbNode;
+    }
+    *breakLookup = 1;
+    if (p->useSucList) {
+        uint32_t tmp = koorde_walkSuccessorList(net, self, &ext->routeKey);
+        if (ok_isBetween(&net->ids[dbNode], &net->ids[tmp], &ext->routeKey)) return dbNode;
+        return tmp;
+    }
+    return s0;
+}
+/* Koorde::findNode (405-471), state READY; the self-recursion (tmpHandle == thisNode and not
+ * breakLookup) is the loop.  breakLookup is a member flag, but every return of findNode leaves
+ * it false, so each call starts with it false. */
+static int koorde_findNode(const orc_net* net, uint32_t self, const OKey* key, KExt* ext, NVec* out)
+{
+    nv_init(out, 0, 0, NULL);
+    int breakLookup = 0;
+    uint32_t pred = pred_get(net, self), s0 = succ_get(net, self, 0);
+    int size = nsucc_get(net, self);
+    for (;;) {
+        if (ok_isBetweenR(key, &net->ids[pred], &net->ids[self])) { nv_push_back(out, self); return 0; }
+        if (ok_isBetweenR(key, &net->ids[self], &net->ids[s0])) { nv_push_back(out, s0); return 0; }
+        if (net->p.useOtherLookup) {
+            uint32_t tmp = koorde_walkSuccessorList(net, self, key);
+            if (tmp != succ_get(net, self, (uint32_t)size - 1)) { nv_push_back(out, tmp); return 0; }
+        }
+        int err = 0;
+        uint32_t h = koorde_findDeBruijnHop(net, self, key, ext, &breakLookup, &err);
+        if (err) return -1;
+        if (h != self || breakLookup) { nv_push_back(out, h); return 0; }
+    }
+}
+
+/* handleDeBruijnTimerExpired (164-230) once the ring has converged; the DeBruijnCall of its
+ * third case is answered by the node responsible for the call's key (328-367) */
+static void koorde_state(orc_net* net, uint32_t v)
+{
+    const orc_params* p = &net->p;
+    int size = nsucc_get(net, v);
+    OKey lookup = ok_shl(net->ids[v], p->shiftingBits);
+    if (size > 0) {
+        OKey d = ok_sub(net->ids[succ_get(net, v, (uint32_t)size / 2)], &net->ids[v]);
+        lookup = ok_sub(lookup, &d);
+    }
+    uint32_t s0 = succ_get(net, v, 0), pred = pred_get(net, v);
+    if (size == 0 || ok_isBetweenR(&lookup, &net->ids[v], &net->ids[s0])) {
+        int sucNum = size < p->deBruijnListSize ? size : p->deBruijnListSize;
+        net->kdb[v] = v; net->kdbStart[v] = s0; net->kdbNum[v] = (uint8_t)sucNum;
+    } else if (ok_isBetweenR(&lookup, &net->ids[pred], &net->ids[v])) {
+        int sucNum = size;
+        if (sucNum + 1 > p->deBruijnListSize) sucNum = p->deBruijnListSize - 1;
+        net->kdb[v] = pred; net->kdbStart[v] = v; net->kdbNum[v] = (uint8_t)(sucNum + 1);
+    } else {
+        uint32_t R = ring_responsible(net, &lookup);
+        int sucNum = nsucc_get(net, R) + 1;
+        if (sucNum > p->deBruijnListSize) sucNum = p->deBruijnListSize;
+        net->kdb[v] = pred_get(net, R); net->kdbStart[v] = R; net->kdbNum[v] = (uint8_t)sucNum;
+    }
+}
+
+orc_net* orc_koorde_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
+{
+    if (p->shiftingBits < 1 || p->shiftingBits > 32 || p->deBruijnListSize < 1 || p->deBruijnListSize > 255) {
+        set_err("koorde: shiftingBits must be 1..32, deBruijnListSize 1..255");
+        return NULL;
+    }
+    /* the Chord part as lazy stable tables: Koorde's findNode reads only pred and successors */
+    orc_net* net = chord_build(ids, n, xy, p, 1);
+    if (!net) return NULL;
+    net->type = NET_KOORDE;
+    net->kdb = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    net->kdbStart = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    net->kdbNum = (uint8_t*)malloc(n);
+    for (uint32_t v = 0; v < n; ++v) koorde_state(net, v);
+    return net;
+}
+
+void orc_koorde_export(const orc_net* net, uint32_t* db, uint32_t* db_start, uint8_t* db_num)
+{
+    if (net->type != NET_KOORDE) return;
+    memcpy(db, net->kdb, sizeof(uint32_t) * net->n);
+    memcpy(db_start, net->kdbStart, sizeof(uint32_t) * net->n);
+    memcpy(db_num, net->kdbNum, net->n);
+}
+
+uint32_t orc_koorde_find_node(const orc_net* net, uint32_t node, const orc_key* key, orc_key* route_key,
+                              int* has_route_key, int* step)
+{
+    if (net->type != NET_KOORDE) { set_err("not a Koorde network"); return NONE; }
+    OKey k = ok_from(key);
+    KExt e;
+    if (*has_route_key) e.routeKey = ok_from(route_key);
+    else { memset(&e.routeKey, 0, sizeof e.routeKey); e.routeKey.isUnspec = 1; }
+    e.step = *step;
+    NVec v;
+    if (koorde_findNode(net, node, &k, &e, &v) < 0) return NONE;
+    *has_route_key = !e.routeKey.isUnspec;
+    if (!e.routeKey.isUnspec) ok_to(&e.routeKey, route_key);
+    *step = e.step;
+    return v.v[0];
+}
+
 /* ---- overlay dispatch ---------------------------------------------------------- */
 static int ov_findNode(const orc_net* net, uint32_t self, const OKey* key, int nr, int ns, NVec* out)
 {
     if (net->type == NET_CHORD) return chord_findNode(net, self, key, nr, ns, out);
+    if (net->type == NET_KOORDE) {
+        KExt e;   /* a call without an extension: Koorde::findNode attaches a fresh one */
+        memset(&e.routeKey, 0, sizeof e.routeKey); e.routeKey.isUnspec = 1; e.step = 1;
+        return koorde_findNode(net, self, key, &e, out);
+    }
     return kad_findNode(net, self, key, nr, ns, out);
 }
 static int ov_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self, const OKey* key, int ns, int* err)
 {
-    if (net->type == NET_CHORD) return chord_isSiblingFor(net, node, self, key, ns, err);
+    if (net->type != NET_KAD) return chord_isSiblingFor(net, node, self, key, ns, err);   /* Koorde: Chord's */
     return kad_isSiblingFor(net, node, self, key, ns, err);
 }
 static int ov_maxRedundant(const orc_net* net)
 {
-    return net->type == NET_CHORD ? 1 : net->p.k;   /* Chord.cc:416-419 (!extendedFingerTable), Kademlia.cc:352-355 */
+    return net->type != NET_KAD ? 1 : net->p.k;   /* Chord.cc:416-419 (!extendedFingerTable), Kademlia.cc:352-355 */
 }
 
 int orc_find_node(const orc_net* net, uint32_t node, const orc_key* key, int numRedundantNodes,
@@ -1006,6 +1249,8 @@ typedef struct {
     uint64_t seqResp, seqTimeout;
     int nInfo;
     int vrpcId[8];          /* RpcInfoVector (one path) */
+    KExt extIn, extOut;     /* Koorde: the call's findNodeExt, and the one its response carries */
+    int extInPresent;
 } Rpc;
 
 typedef struct {
@@ -1028,6 +1273,9 @@ typedef struct {
     /* outputs */
     uint32_t* hopseq; int nhop;
     uint32_t rpcsSent;
+    /* Koorde: the findNodeExt the next FindNodeCalls carry (sendRpc's argument) */
+    KExt ext; int extPresent;
+    int broken;             /* a findNode threw (cRuntimeError in the reference): status BROKEN */
 } Lookup;
 
 static int lk_getVisited(Lookup* L, uint32_t n)
@@ -1064,7 +1312,7 @@ static int lk_activeRpcs(Lookup* L)
 /* LookupVector comparator: IterativeLookup::compare -> overlay->distance(., key) (IterativeLookup.cc:397-400) */
 static int lv_compare(Lookup* L, uint32_t a, uint32_t b)
 {
-    int metric = L->net->type == NET_CHORD ? 2 : 1;
+    int metric = L->net->type != NET_KAD ? 2 : 1;
     OKey da = metric_dist(metric, &L->net->ids[a], &L->key);
     OKey db = metric_dist(metric, &L->net->ids[b], &L->key);
     return ok_cmp(&da, &db);
@@ -1124,10 +1372,22 @@ static void lk_sendRpc(Lookup* L, uint32_t handle, int rpcId)
         r->tTimeout = L->now + simtime(p->rpcUdpTimeout, p->simtimeRound);
         r->seqTimeout = L->seq++;
         /* the call travels S -> handle, the responder answers at once */
-        int64_t d1 = calc_delay(L->net, L->S, handle, p->callBytes, L->now, &L->txFinished);
+        const int koorde = L->net->type == NET_KOORDE;
+        /* a Koorde call sent without an extension (after a late response) lacks its 21 B */
+        int64_t d1 = calc_delay(L->net, L->S, handle, p->callBytes - ((koorde && !L->extPresent) ? 21 : 0), L->now,
+                                &L->txFinished);
         int64_t tArr = L->now + d1;
         NVec res; int sflag, err;
-        ov_findNode(L->net, handle, &L->key, p->lookupRedundantNodes, L->numSiblings, &res);
+        if (koorde) {
+            r->extIn = L->ext; r->extInPresent = L->extPresent;
+            r->extOut = L->ext;
+            if (!L->extPresent) {   /* Koorde::findNode attaches a fresh extension (421-429) */
+                memset(&r->extOut.routeKey, 0, sizeof r->extOut.routeKey);
+                r->extOut.routeKey.isUnspec = 1; r->extOut.step = 1;
+            }
+            if (koorde_findNode(L->net, handle, &L->key, &r->extOut, &res) < 0) { L->broken = 1; res.size = 0; }
+        } else
+            ov_findNode(L->net, handle, &L->key, p->lookupRedundantNodes, L->numSiblings, &res);
         sflag = ov_isSiblingFor(L->net, handle, handle, &L->key, L->numSiblings, &err);
         (void)sflag;
         int64_t respTx = 0;   /* responder's tx queue idle */
@@ -1263,7 +1523,14 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
     L->running = 1; L->startTime = 0; L->now = 0; L->txFinished = 0;
     /* start() 133-244 */
     NVec nextHops; int err;
-    ov_findNode(net, S, key, ov_maxRedundant(net), L->numSiblings, &nextHops);
+    if (net->type == NET_KOORDE) {
+        /* the local FindNodeCall gets a fresh extension from Koorde::findNode; start() hands it
+         * to the first sendRpc (200-230) */
+        memset(&L->ext.routeKey, 0, sizeof L->ext.routeKey);
+        L->ext.routeKey.isUnspec = 1; L->ext.step = 1; L->extPresent = 1;
+        if (koorde_findNode(net, S, key, &L->ext, &nextHops) < 0) { L->broken = 1; nextHops.size = 0; }
+    } else
+        ov_findNode(net, S, key, ov_maxRedundant(net), L->numSiblings, &nextHops);
     lk_setVisited(L, S);
     if (nextHops.size == 0) {
         L->finished = 1; L->success = 0;
@@ -1271,11 +1538,11 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
         for (int i = 0; i < nextHops.size; i++) lk_addSibling(L, nextHops.v[i]);
         L->success = L->finished = 1;
     }
-    int done = L->finished;
+    int done = L->finished || L->broken;
     if (!done) {
         for (int i = 0; i < nextHops.size; ++i) path_add(L, nextHops.v[i]);
         path_sendRpc(L, p->lookupParallelRpcs);
-        done = lk_checkStop(L);
+        done = L->broken || lk_checkStop(L);
     }
     /* event loop */
     while (!done) {
@@ -1301,26 +1568,50 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
             else cap_error("more than MAXRPC dead nodes in one lookup");
             for (int q = 0; q < r.nInfo; ++q) {
                 if (L->pfinished) continue;
+                L->ext = r.extIn; L->extPresent = r.extInPresent;   /* the timed-out call's extension (965-969) */
                 path_handleTimeout(L);
                 lk_countFinished(L);
             }
         } else {                             /* handleRpcResponse 488-585 */
             NVec res; int sflag, err2;
-            ov_findNode(net, r.node, key, p->lookupRedundantNodes, L->numSiblings, &res);  /* BaseOverlay.cc:1857-1871 */
+            if (net->type == NET_KOORDE) {
+                KExt e = r.extIn;
+                if (!r.extInPresent) { memset(&e.routeKey, 0, sizeof e.routeKey); e.routeKey.isUnspec = 1; e.step = 1; }
+                if (koorde_findNode(net, r.node, key, &e, &res) < 0) res.size = 0;   /* BROKEN was set at send */
+            } else
+                ov_findNode(net, r.node, key, p->lookupRedundantNodes, L->numSiblings, &res);  /* BaseOverlay.cc:1857-1871 */
             sflag = ov_isSiblingFor(net, r.node, r.node, key, L->numSiblings, &err2);
             int rpcHandled = 0;
             for (int q = 0; q < r.nInfo; ++q) {
                 if (L->pfinished) continue;
                 if (!rpcHandled && (path_accepts(L, r.vrpcId[q]) || (sflag && p->lookupAcceptLateSiblings))) {
+                    L->ext = r.extOut; L->extPresent = 1;            /* the response's extension (908-911) */
                     path_handleResponse(L, r.node, &res, sflag);
                     rpcHandled = 1;
                 } else {
+                    L->extPresent = 0;                               /* handleTimeout(NULL, ...): no extension */
                     path_handleTimeout(L);
                 }
                 lk_countFinished(L);
             }
         }
-        done = lk_checkStop(L);
+        done = L->broken || lk_checkStop(L);
+    }
+    if (L->broken) {
+        /* the reference aborts (cRuntimeError) inside a Koorde findNode; the lookup is reported
+         * BROKEN with the hops accepted so far */
+        if (lout) {
+            lout->hops = (uint16_t)L->hops; lout->is_valid = 0; lout->num_siblings = 0; lout->latency_ns = -1;
+            lout->status = 5;
+            for (int i = 0; i < numSiblings; ++i) sibs[i] = NONE;
+        } else {
+            out->hops = (uint16_t)L->hops; out->responsible = NONE; out->status = 5;
+            out->one_way_hops = 0; out->latency_ns = -1;
+            if (rpcsOut) *rpcsOut = L->rpcsSent;
+        }
+        free(L->visited);
+        free(L);
+        return;
     }
     /* stop() -> SendToKeyListener::lookupFinished (BaseOverlay.cc:1241-1307) */
     int valid = L->success && L->finished;
@@ -1430,6 +1721,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
 {
     uint64_t total = 0;
     int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
+    if (net->type == NET_KOORDE && net->p.routingType != 0) { set_err("Koorde: iterative routing only"); return ORC_FAIL; }
     if (hop_seq) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) hop_seq[i] = NONE;
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
@@ -1453,7 +1745,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
 int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int numSiblings,
                      orc_lookup_out* out, uint32_t* siblings, int nthreads)
 {
-    const int maxs = net->type == NET_CHORD ? net->p.successorListSize : net->p.s;
+    const int maxs = net->type != NET_KAD ? net->p.successorListSize : net->p.s;
     if (numSiblings < 0) numSiblings = maxs;                              /* BaseOverlay.cc:1942-1944 */
     if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
     if (numSiblings < 1 || numSiblings > 16) { set_err("numSiblings must be 1..16"); return -1; }

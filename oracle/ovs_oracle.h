@@ -70,10 +70,18 @@ typedef struct {
     uint64_t kadSeed;                 /* Kademlia snapshot bucket-sampling seed */
     int32_t routingType;              /* 0 iterative, 1 semi-recursive, 2 full-recursive (default.ini:392) */
     int32_t recNumRedundantNodes;     /* default.ini:386 = 3 */
+    /* Koorde (Koorde.ned, default.ini:268-291) */
+    int32_t shiftingBits;             /* = 4 */
+    int32_t deBruijnListSize;         /* = 16 */
+    int32_t useOtherLookup;           /* = true */
+    int32_t useSucList;               /* = true */
 } orc_params;
 
 void orc_params_chord_default(orc_params* p);
 void orc_params_kad_default(orc_params* p);
+/* Koorde defaults: successorListSize = deBruijnListSize = 16, shiftingBits = 4, useOtherLookup,
+ * useSucList; FindNodeCall / FindNodeResponse carry the 168-bit KoordeFindNodeExtMessage */
+void orc_params_koorde_default(orc_params* p);
 
 /* ---- networks */
 typedef struct orc_net orc_net;
@@ -99,6 +107,18 @@ orc_net* orc_kad_build_lazy(const orc_key* ids, uint32_t n, const double* xy, co
  * Kademlia::siblingTable), bucket_count[n*160], bucket_nodes[n*160*k] (routingTable buckets). */
 orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, const uint32_t* siblings,
                               const uint8_t* bucket_count, const uint32_t* bucket_nodes, const orc_params* p);
+/* Koorde (Koorde.cc) on the converged Chord ring of the same ids: successor lists of
+ * successorListSize, the de Bruijn pointer and list each node's handleDeBruijnTimerExpired /
+ * DeBruijnCall exchange converges to (Koorde.cc:164-230, 328-390). */
+orc_net* orc_koorde_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p);
+/* de Bruijn state: node db[i], list = the db_num[i] ring nodes from sorted index db_start[i] */
+void     orc_koorde_export(const orc_net* net, uint32_t* db, uint32_t* db_start, uint8_t* db_num);
+/* Koorde::findNode at `node` for key with a KoordeFindNodeExtMessage (route_key, step);
+ * *has_route_key = 0: routeKey unspecified.  Updates route_key / step / has_route_key to the
+ * extension the response carries; returns the next hop, or UINT32_MAX when the reference
+ * throws (findDeBruijnHop bounding error, findStartKey invalid start key). */
+uint32_t orc_koorde_find_node(const orc_net* net, uint32_t node, const orc_key* key, orc_key* route_key,
+                              int* has_route_key, int* step);
 void     orc_net_free(orc_net* net);
 
 /* export the Kademlia snapshot so the GPU builder can be checked:

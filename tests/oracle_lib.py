@@ -34,6 +34,8 @@ class OrcParams(C.Structure):
         ("accessDelay", C.c_double), ("callBytes", C.c_int32), ("respBaseBytes", C.c_int32),
         ("respPerNodeBytes", C.c_int32), ("routeBytes", C.c_int32), ("kadSeed", C.c_uint64),
         ("routingType", C.c_int32), ("recNumRedundantNodes", C.c_int32),
+        ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
+        ("useSucList", C.c_int32),
     ]
 
     def replace(self, **kw) -> "OrcParams":
@@ -67,6 +69,10 @@ def lib() -> C.CDLL:
             ("orc_key_pow2", [u32, vp], None),
             ("orc_params_chord_default", [vp], None),
             ("orc_params_kad_default", [vp], None),
+            ("orc_params_koorde_default", [vp], None),
+            ("orc_koorde_build", [vp, u32, vp, vp], vp),
+            ("orc_koorde_export", [vp, vp, vp, vp], None),
+            ("orc_koorde_find_node", [vp, u32, vp, vp, C.POINTER(C.c_int), C.POINTER(C.c_int)], u32),
             ("orc_chord_build", [vp, u32, vp, vp], vp),
             ("orc_chord_build_tables", [vp, u32, vp, vp, vp, vp, u32, vp, vp, vp], vp),
             ("orc_kad_build", [vp, u32, vp, vp], vp),
@@ -137,8 +143,14 @@ def kad_params(**kw) -> OrcParams:
     return p.replace(**kw) if kw else p
 
 
+def koorde_params(**kw) -> OrcParams:
+    p = OrcParams()
+    lib().orc_params_koorde_default(C.byref(p))
+    return p.replace(**kw) if kw else p
+
+
 class OracleNet:
-    """A network built by the oracle (Chord stable state or Kademlia snapshot)."""
+    """A network built by the oracle (Chord stable state, Kademlia snapshot, converged Koorde)."""
 
     def __init__(self, kind: str, ids, xy, params: OrcParams | None = None, tables: dict | None = None,
                  lazy: bool = False):
@@ -160,6 +172,9 @@ class OracleNet:
                 h = L.orc_chord_build_tables(_p(self.ids), n, _p(self.xy), _p(t["pred"].astype(np.uint32)),
                                              _p(t["succ"]), _p(t["nsucc"]), t["succ"].shape[1], _p(t["fingers"]),
                                              _p(t["deque_size"]), C.byref(self.params))
+        elif kind == "koorde":
+            self.params = params or koorde_params()
+            h = L.orc_koorde_build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
         else:
             self.params = params or kad_params()
             if tables is None:
@@ -203,8 +218,8 @@ class OracleNet:
         keys = np.ascontiguousarray(keys, dtype=np.uint32)
         src = np.ascontiguousarray(src, dtype=np.uint32)
         n = len(keys)
-        ns = numSiblings if numSiblings >= 0 else (self.params.successorListSize if self.kind == "chord"
-                                                   else self.params.s)
+        ns = numSiblings if numSiblings >= 0 else (self.params.s if self.kind == "kademlia"
+                                                   else self.params.successorListSize)
         out = np.empty(n, dtype=LOOKUP_DTYPE)
         sib = np.empty((n, max(ns, 1)), dtype=np.uint32)
         r = lib().orc_lookup_batch(self._h, _p(keys), _p(src), n, numSiblings, _p(out), _p(sib), nthreads)
@@ -273,6 +288,23 @@ class OracleNet:
         nodes = np.empty((self.n, 160, self.params.k), dtype=np.uint32)
         lib().orc_kad_export(self._h, _p(sib), _p(cnt), _p(nodes))
         return sib, cnt, nodes
+
+    def koorde_state(self):
+        """(deBruijnNode, first node of the de Bruijn list, list length) per node."""
+        db = np.empty(self.n, dtype=np.uint32)
+        start = np.empty(self.n, dtype=np.uint32)
+        num = np.empty(self.n, dtype=np.uint8)
+        lib().orc_koorde_export(self._h, _p(db), _p(start), _p(num))
+        return db, start, num
+
+    def koorde_find_node(self, node: int, key, route_key=None, step: int = 1):
+        """Koorde::findNode with a KoordeFindNodeExtMessage (route_key None = unspecified):
+        returns (next hop or None when the reference throws, route_key out, step out)."""
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        rk = np.zeros(5, dtype=np.uint32) if route_key is None else np.array(route_key, dtype=np.uint32)
+        has, st = C.c_int(0 if route_key is None else 1), C.c_int(step)
+        h = lib().orc_koorde_find_node(self._h, int(node), _p(key), _p(rk), C.byref(has), C.byref(st))
+        return (None if h == 0xFFFFFFFF else int(h)), (rk.copy() if has.value else None), st.value
 
     def delay_ns(self, a: int, b: int, nbytes: int) -> int:
         return int(lib().orc_delay_ns(self._h, a, b, nbytes))

@@ -203,6 +203,164 @@ class ChordRing:
 
 
 # --- Kademlia findNode (Kademlia.cc:357-382, 888-962, 1101-1246) on exported tables --
+class KoordeRing:
+    """Second, independent reading of Koorde routing (src/overlay/koorde/Koorde.cc) on a converged
+    ring, in Python integers: walks over the successor / de Bruijn lists are done by clockwise
+    distance instead of the reference's interval loops, the de Bruijn pointer by bisection."""
+
+    M = 1 << 160
+
+    def __init__(self, ids_words, xy, sls=16, dbls=16, shift=4, use_other=True, use_suc=True, rnd=True):
+        self.ids = [to_int(w) for w in ids_words]
+        self.n = len(self.ids)
+        self.xy = xy
+        self.ns = min(sls, self.n - 1)
+        self.dbls, self.shift, self.use_other, self.use_suc, self.rnd = dbls, shift, use_other, use_suc, rnd
+        self.db = []          # (deBruijnNode, [deBruijnNodes])
+        for v in range(self.n):
+            self.db.append(self._debruijn(v))
+
+    def d(self, a, b):
+        """clockwise distance from key a to key b"""
+        return (b - a) % self.M
+
+    def succ(self, v, j):
+        return (v + 1 + j) % self.n
+
+    def responsible(self, k):
+        i = bisect.bisect_left(self.ids, k)
+        return 0 if i == self.n else i
+
+    def _debruijn(self, v):
+        """Koorde.cc:164-230 (+ the DeBruijnCall answer, 328-367) once the ring is stable"""
+        M, me = self.M, self.ids[v]
+        key = (me << self.shift) % M
+        key = (key - (self.ids[self.succ(v, self.ns // 2)] - me)) % M
+        pred = (v - 1) % self.n
+        if 0 < self.d(me, key) <= self.d(me, self.ids[self.succ(v, 0)]):
+            return v, [self.succ(v, j) for j in range(min(self.ns, self.dbls))]
+        if 0 < self.d(self.ids[pred], key) <= self.d(self.ids[pred], me):
+            return pred, [v] + [self.succ(v, j) for j in range(min(self.ns, self.dbls - 1))]
+        R = self.responsible(key)
+        return (R - 1) % self.n, [(R + j) % self.n for j in range(min(self.ns + 1, self.dbls))]
+
+    def _walk(self, nodes, key):
+        """the last of the clockwise-ordered `nodes` strictly before key, or nodes[-1] when key
+        lies beyond them (walkSuccessorList / walkDeBruijnList)"""
+        base = self.ids[nodes[0]]
+        dk = self.d(base, key)
+        if dk == 0 or dk > self.d(base, self.ids[nodes[-1]]):
+            return nodes[-1]
+        best = nodes[0]
+        for x in nodes:
+            if self.d(base, self.ids[x]) < dk:
+                best = x
+        return best
+
+    def _start_key(self, v, dest):
+        me, s0 = self.ids[v], self.ids[self.succ(v, 0)]
+        nb = max(self.d(me, s0).bit_length() - 1, 0)
+        while (160 - nb) % self.shift:
+            nb -= 1
+        key = (dest >> (160 - nb)) + ((me >> nb) << nb)
+        key %= self.M
+        for cand in (key, (key + (1 << nb)) % self.M):
+            if 0 < self.d(me, cand) <= self.d(me, s0):
+                return cand, nb + 1
+        raise ValueError("invalid start key")
+
+    def find_node(self, v, key, ext):
+        """(next hop, ext) for Koorde::findNode at v; ext = [routeKey or None, step]; raises
+        ValueError where the reference throws"""
+        me, M = self.ids[v], self.M
+        pred, s0 = (v - 1) % self.n, self.succ(v, 0)
+        sl = [self.succ(v, j) for j in range(self.ns)]
+        dbn, dbl = self.db[v]
+        while True:
+            if 0 < self.d(self.ids[pred], key) <= self.d(self.ids[pred], me) or key == me:
+                return v, ext
+            if 0 < self.d(me, key) <= self.d(me, self.ids[s0]):
+                return s0, ext
+            if self.use_other:
+                t = self._walk(sl, key)
+                if t != sl[-1]:
+                    return t, ext
+            brk = False
+            if ext[0] is None:
+                ext = list(self._start_key(v, key))
+            rk, step = ext
+            if 0 < self.d(me, rk) <= self.d(me, self.ids[s0]):
+                if step > 160:
+                    raise ValueError("bounding error")
+                for i in range(self.shift):
+                    pos = 160 - step - i
+                    if pos < 0:
+                        raise ValueError("bit position below 0")
+                rk = ((rk << self.shift) % M) + ((key >> (160 - step - self.shift + 1)) & ((1 << self.shift) - 1))
+                rk %= M
+                ext = [rk, step + self.shift]
+                if 0 < self.d(self.ids[dbn], rk) <= self.d(self.ids[dbn], self.ids[dbl[0]]):
+                    h = dbn
+                else:
+                    h = self._walk(dbl, rk)
+            else:
+                brk = True
+                if self.use_suc:
+                    t = self._walk(sl, rk)
+                    a, x = self.ids[t], self.ids[dbn]
+                    # isBetween(x, a, rk): the open arc; a == rk is the whole ring but a
+                    h = dbn if (x != a and (a == rk or self.d(a, x) < self.d(a, rk))) else t
+                else:
+                    h = s0
+            if h != v or brk:
+                return h, ext
+
+    def lookup(self, kw, S, hop_max=50, call=104, resp=108, route=186, rpc_to=1.5, lk_to=10.0):
+        """KBRTestApp one-way lookup, iterative, one path, one RPC in flight (Koorde's
+        lookupRedundantNodes = lookupParallelRpcs = 1, merge off, visitOnlyOnce)"""
+        k = to_int(kw)
+        rnd = self.rnd
+        pred = (S - 1) % self.n
+        if 0 < self.d(self.ids[pred], k) <= self.d(self.ids[pred], self.ids[S]) or k == self.ids[S]:
+            return dict(responsible=S, hops=0, status=0, one_way_hops=0, latency_ns=0, hop_seq=[])
+        try:
+            nxt, ext = self.find_node(S, k, [None, 1])
+        except ValueError:
+            return dict(responsible=0xFFFFFFFF, hops=0, status=5, one_way_hops=0, latency_ns=-1, hop_seq=[])
+        t, hops, seq, visited = 0, 0, [], {S}
+        if nxt in visited:
+            return dict(responsible=0xFFFFFFFF, hops=0, status=4, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+        cur = nxt
+        while True:
+            try:
+                nxt, ext2 = self.find_node(cur, k, list(ext))
+            except ValueError:
+                return dict(responsible=0xFFFFFFFF, hops=hops, status=5, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+            cd = coord_ns(self.xy, S, cur, rnd)
+            rtt = msg_ns(call, rnd) + cd + msg_ns(resp, rnd) + cd
+            if rtt >= simtime(rpc_to, rnd):
+                st = 1 if t + simtime(rpc_to, rnd) > simtime(lk_to, rnd) else 2
+                return dict(responsible=0xFFFFFFFF, hops=hops, status=st, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+            t += rtt
+            if t > simtime(lk_to, rnd):
+                return dict(responsible=0xFFFFFFFF, hops=hops, status=1, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+            hops += 1
+            seq.append(cur)
+            visited.add(cur)
+            p = (cur - 1) % self.n
+            if 0 < self.d(self.ids[p], k) <= self.d(self.ids[p], self.ids[cur]) or k == self.ids[cur]:
+                R = cur
+                lat = t + (msg_ns(route, rnd) + coord_ns(self.xy, S, R, rnd) if R != S else 0)
+                return dict(responsible=R, hops=hops, status=0, one_way_hops=hops + (R != S), latency_ns=lat,
+                            hop_seq=seq)
+            if hop_max and hops >= hop_max:
+                return dict(responsible=0xFFFFFFFF, hops=hops, status=3, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+            if nxt in visited:
+                return dict(responsible=0xFFFFFFFF, hops=hops, status=4, one_way_hops=0, latency_ns=-1, hop_seq=seq)
+            ext = ext2
+            cur = nxt
+
+
 class KadTables:
     def __init__(self, ids_words, sib, bcount, bnodes, k=8, s=8):
         self.ids = [to_int(w) for w in ids_words]
