@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 3
+#define OVS_ABI_VERSION 4
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -63,10 +63,11 @@ enum {
     OVS_LOOKUP_RPC_TIMEOUT = 2,  /* RTT >= rpcUdpTimeout (BaseRpc.cc:191-211) */
     OVS_LOOKUP_HOPMAX = 3,       /* hops >= hopCountMax (IterativeLookup.cc:1074-1086) */
     OVS_LOOKUP_NO_NEXT = 4,      /* no unvisited next hop (IterativeLookup.cc:1147-1168) */
-    OVS_LOOKUP_BROKEN = 5        /* Chord successor list broken (Chord.cc:615-620, 671-672) */
+    OVS_LOOKUP_BROKEN = 5        /* Chord successor list broken (Chord.cc:615-620, 671-672); Koorde::findNode
+                                    throws (Koorde.cc:490-493 bounding error, 756-760 invalid start key) */
 };
 
-enum { OVS_OVERLAY_CHORD = 1, OVS_OVERLAY_KADEMLIA = 2 };
+enum { OVS_OVERLAY_CHORD = 1, OVS_OVERLAY_KADEMLIA = 2, OVS_OVERLAY_KOORDE = 3 };
 
 /* flags */
 #define OVS_DEVICE_PTRS  0x1u   /* buffers are device pointers; call is async on `stream` */
@@ -107,6 +108,10 @@ typedef struct ovs_params {
     double  datarate;                   /* channel datarate, simple_ethernetline = 10 Mbps */
     double  accessDelay;                /* channel delay = 0 ms */
     uint64_t kadSeed;                   /* Kademlia snapshot bucket-sampling seed */
+    int32_t shiftingBits;               /* **.koorde.shiftingBits = 4 */
+    int32_t deBruijnListSize;           /* **.koorde.deBruijnListSize = 16 */
+    int32_t useOtherLookup;             /* **.koorde.useOtherLookup = true */
+    int32_t useSucList;                 /* **.koorde.useSucList = true */
 } ovs_params;
 
 /* Result of one one-way KBR test lookup (KBRTestApp with kbrOneWayTest). */
@@ -164,6 +169,29 @@ ovs_status  ovs_kad_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n,
 ovs_status  ovs_kad_load_tables(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n, const double* xy,
                                 const uint32_t* siblings, const uint8_t* bucket_count,
                                 const uint32_t* bucket_nodes, uint32_t flags);
+/* Koorde (src/overlay/koorde/Koorde.cc, class Koorde : public Chord) on a converged ring: the
+ * Chord ring of ids (predecessor, successorListSize successors) plus every node's de Bruijn
+ * pointer and list as handleDeBruijnTimerExpired / the DeBruijnCall exchange leave them
+ * (Koorde.cc:164-230, 328-390).  Routing goes through ovs_route_batch (Koorde::findNode,
+ * 405-556, for every FindNodeCall of IterativeLookup, iterative routing with
+ * lookupRedundantNodes = lookupParallelRpcs = 1 and merge off -- the Koorde defaults). */
+ovs_status  ovs_koorde_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n, const double* xy,
+                            uint32_t flags);
+/* de Bruijn state per node (host buffers): deBruijnNode, and the deBruijnNodes list as
+ * db_num[i] consecutive ring nodes from sorted index db_start[i] */
+ovs_status  ovs_koorde_export(ovs_ctx* ctx, uint32_t* db_node, uint32_t* db_start, uint8_t* db_num);
+/* KoordeFindNodeExtMessage (ChordMessage.msg:168-172): the route key and step a Koorde
+ * FindNodeCall carries; has_route_key = 0 is an unspecified route key */
+typedef struct ovs_koorde_ext {
+    uint32_t route_key[5];
+    int32_t  step;
+    int32_t  has_route_key;
+} ovs_koorde_ext;
+/* Koorde::findNode at node[i] for keys[i] with the call's extension ext[i], which is replaced by
+ * the one the response carries; next[i] = the single next hop, 0xFFFFFFFF where the reference
+ * throws.  Host buffers. */
+ovs_status  ovs_koorde_find_node_batch(ovs_ctx* ctx, const uint32_t* node, const ovs_key160* keys,
+                                       ovs_koorde_ext* ext, uint32_t* next, uint64_t n);
 /* copy the device Kademlia tables out (host buffers): siblings[n*5s],
  * bucket_count[n*160], bucket_nodes[n*160*k] (0xFFFFFFFF padded) */
 ovs_status  ovs_kad_export(ovs_ctx* ctx, uint32_t* siblings, uint8_t* bucket_count,

@@ -1,0 +1,385 @@
+// koorde.hip -- Koorde routing (src/overlay/koorde/Koorde.cc) for gfx950 (MI355X).
+//
+// K3 k_koorde_route: one lane per lookup running IterativeLookup with Koorde::findNode (one next
+// hop per response; lookupRedundantNodes = lookupParallelRpcs = 1, merge off: a chain of
+// FindNodeCalls).  Every FindNodeCall carries the KoordeFindNodeExtMessage (de Bruijn route key
+// + step) of the response that produced it, and the responder's findNode advances it
+// (IterativeLookup.cc:200-230, 903-920; BaseOverlay.cc:1841-1907).  Per hop the lane reads the
+// responder's key, predecessor and first successor (24 B records of the sorted ring), its
+// KoordeNode (16 B), and walks its successor / de Bruijn lists -- consecutive ring nodes -- by
+// binary search over clockwise distance, which picks the same node as the reference's interval
+// loops (walkSuccessorList 572-582, walkDeBruijnList 558-570).  Finished lanes refill from the
+// wave's slice of the batch (ballot + popcount); the grid is persistent.
+#include "koorde.hpp"
+
+namespace ovs {
+
+void koorde_free(KoordeTables& t)
+{
+    if (t.nd) hipFree(t.nd);
+    t.nd = nullptr;
+    t.n = 0;
+}
+
+namespace {
+
+__device__ __forceinline__ K160 rkey(const KeyRec* __restrict__ recs, uint32_t i) { return key_of(load_rec(recs, i)); }
+
+__device__ __forceinline__ uint32_t ring_add(uint32_t i, uint32_t d, uint32_t n)
+{
+    const uint64_t j = (uint64_t)i + d;
+    return (uint32_t)(j >= n ? j - n : j);
+}
+
+// OverlayKey::operator<< / operator>> (OverlayKey.cc:386-425) with trim() to 160 bits, exact for
+// every count (the reference's mpn shifts are undefined for counts that are multiples of 64:
+// DESIGN.md §Koorde)
+__device__ __forceinline__ K160 k_shl(const K160& a, int n)
+{
+    K160 r;
+    const int q = n >> 5, b = n & 31;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t hi = k_word(a, i - q), lo = (i - q - 1 >= 0) ? k_word(a, i - q - 1) : 0u;
+        r.w[i] = (i - q < 0 || n >= 160) ? 0u : (b ? (hi << b) | (lo >> (32 - b)) : hi);
+    }
+    return r;
+}
+__device__ __forceinline__ K160 k_shr(const K160& a, int n)
+{
+    K160 r;
+    const int q = n >> 5, b = n & 31;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t lo = k_word(a, i + q), hi = k_word(a, i + q + 1);
+        r.w[i] = (n >= 160) ? 0u : (b ? (lo >> b) | (hi << (32 - b)) : lo);
+    }
+    return r;
+}
+
+__device__ __forceinline__ K160 k_small(uint32_t v)
+{
+    K160 r;
+    r.w[0] = v; r.w[1] = 0; r.w[2] = 0; r.w[3] = 0; r.w[4] = 0;
+    return r;
+}
+
+// The node of the `num` consecutive ring nodes from sorted index `first` that the reference's
+// interval loop returns for key: the last one strictly (clockwise) before key if key lies in
+// (a_0, a_{num-1}], else a_{num-1}
+__device__ uint32_t walk_list(const KeyRec* __restrict__ recs, uint32_t n, uint32_t first, int num, const K160& key)
+{
+    const uint32_t last = ring_add(first, (uint32_t)(num - 1), n);
+    if (num <= 1) return last;
+    const K160 a0 = rkey(recs, first);
+    const K160 dk = k_sub(key, a0);
+    const K160 dl = k_sub(rkey(recs, last), a0);
+    const bool zero = (dk.w[0] | dk.w[1] | dk.w[2] | dk.w[3] | dk.w[4]) == 0;
+    if (zero || k_gt(dk, dl)) return last;
+    int lo = 0, hi = num - 1;   // d(a_lo) < dk <= d(a_hi)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t m = ring_add(first, (uint32_t)mid, n);
+        if (k_lt(k_sub(rkey(recs, m), a0), dk)) lo = mid; else hi = mid;
+    }
+    return ring_add(first, (uint32_t)lo, n);
+}
+
+struct KView {
+    const KeyRec* __restrict__ recs;
+    const KoordeNode* __restrict__ nd;
+    uint32_t n;
+    int ns, sb, useOther, useSuc;
+};
+
+// Koorde::findStartKey (664-762); false = cRuntimeError (invalid start key)
+__device__ bool find_start_key(const KView& V, const K160& self, const K160& s0, const K160& dest, K160& out, int& step)
+{
+    if (k_eq(self, s0)) { out = self; return true; }
+    int nBits = k_msb(k_sub(s0, self));
+    if (nBits < 0) nBits = 0;
+    while ((160 - nBits) % V.sb != 0) nBits--;
+    step = nBits + 1;
+    const K160 newStart = k_shl(k_shr(self, nBits), nBits);
+    K160 newKey = k_add(k_shr(dest, 160 - nBits), newStart);
+    if (between_R(newKey, self, s0)) { out = newKey; return true; }
+    newKey = k_add(newKey, k_pow2(nBits));
+    if (between_R(newKey, self, s0)) { out = newKey; return true; }
+    return false;
+}
+
+// Koorde::findNode (405-471) at node c, state READY, with findDeBruijnHop (473-556) inlined;
+// returns the next hop, NONE where the reference throws
+__device__ uint32_t koorde_find_node_dev(const KView& V, uint32_t c, const K160& key, KExt& e)
+{
+    const uint32_t n = V.n;
+    const uint32_t pred = c == 0 ? n - 1 : c - 1;
+    const uint32_t s0 = ring_add(c, 1, n);
+    const uint32_t slast = ring_add(c, (uint32_t)V.ns, n);
+    const K160 me = rkey(V.recs, c);
+    const K160 kp = rkey(V.recs, pred);
+    const K160 ks0 = rkey(V.recs, s0);
+    if (between_R(key, kp, me)) return c;
+    if (between_R(key, me, ks0)) return s0;
+    if (V.useOther) {
+        const uint32_t tmp = walk_list(V.recs, n, s0, V.ns, key);
+        if (tmp != slast) return tmp;
+    }
+    const KoordeNode kn = V.nd[c];
+    const K160 kdb = rkey(V.recs, kn.db);
+    for (int guard = 0; guard < 200; ++guard) {   // the self-recursion: every round adds shiftingBits to step
+        bool brk = false;
+        uint32_t h;
+        if (!e.has) {
+            K160 rk;
+            int step = e.step;
+            if (!find_start_key(V, me, ks0, key, rk, step)) return NONE;
+            e.rk = rk; e.step = step; e.has = 1;
+        }
+        if (between_R(e.rk, me, ks0)) {
+            if (e.step > 160) return NONE;                          // "Bounding error"
+            if (160 - e.step - (V.sb - 1) < 0) return NONE;         // getBit below bit 0: getBitRange throws
+            // the shiftingBits key bits below position 160 - step, most significant first
+            const uint32_t add = (uint32_t)((k_shr(key, 160 - e.step - V.sb + 1).w[0]) & ((1u << V.sb) - 1u));
+            e.rk = k_add(k_shl(e.rk, V.sb), k_small(add));
+            e.step += V.sb;
+            if (kn.dbNum > 0) {
+                if (between_R(e.rk, kdb, rkey(V.recs, kn.dbStart))) h = kn.db;
+                else h = walk_list(V.recs, n, kn.dbStart, (int)kn.dbNum, e.rk);
+            } else {
+                h = kn.db;
+            }
+        } else {
+            brk = true;
+            if (V.useSuc) {
+                const uint32_t tmp = walk_list(V.recs, n, s0, V.ns, e.rk);
+                h = between_open(kdb, rkey(V.recs, tmp), e.rk) ? kn.db : tmp;
+            } else {
+                h = s0;
+            }
+        }
+        if (h != c || brk) return h;
+        // findNode calls itself again with the advanced extension; the key checks above
+        // (predecessor, successor, successor-list walk) give the same answers again
+    }
+    return NONE;
+}
+
+// handleDeBruijnTimerExpired (164-230) on the converged ring; the DeBruijnCall of the third
+// case is answered by the node responsible for its key (328-367)
+__global__ void k_koorde_build(const KeyRec* __restrict__ recs, uint32_t n, int ns, int sb, int dbls,
+                               KoordeNode* __restrict__ nd)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const K160 me = rkey(recs, v);
+    K160 lookup = k_shl(me, sb);
+    if (ns > 0) lookup = k_sub(lookup, k_sub(rkey(recs, ring_add(v, 1 + (uint32_t)(ns / 2), n)), me));
+    const uint32_t s0 = ring_add(v, 1, n), pred = v == 0 ? n - 1 : v - 1;
+    KoordeNode o;
+    o.pad = 0;
+    if (ns == 0 || between_R(lookup, me, rkey(recs, s0))) {
+        o.db = v; o.dbStart = s0; o.dbNum = (uint32_t)min(ns, dbls);
+    } else if (between_R(lookup, rkey(recs, pred), me)) {
+        const int sucNum = ns + 1 > dbls ? dbls - 1 : ns;
+        o.db = pred; o.dbStart = v; o.dbNum = (uint32_t)(sucNum + 1);
+    } else {
+        // responsible(lookup): the first key >= lookup, wrapping to node 0
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            if (k_lt(rkey(recs, mid), lookup)) lo = mid + 1; else hi = mid;
+        }
+        const uint32_t R = lo == n ? 0 : lo;
+        o.db = R == 0 ? n - 1 : R - 1; o.dbStart = R; o.dbNum = (uint32_t)min(ns + 1, dbls);
+    }
+    nd[v] = o;
+}
+
+__global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
+                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
+                                                      uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
+                                                      uint32_t* __restrict__ hopseq, uint32_t* __restrict__ rpcs)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    uint64_t cursor = wave * chunk;
+    const uint64_t end = min(cursor + chunk, nq);
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t H = hcm > 0 ? (uint64_t)hcm : 1ull;
+
+    bool active = false, local = true;
+    uint64_t q = 0;
+    K160 K;
+    uint32_t S = 0, cur = 0;
+    double sx = 0, sy = 0;
+    int64_t t = 0;
+    int hops = 0;
+    KExt e;
+    e.has = 0; e.step = 1;
+    while (true) {
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && cursor < end) {
+            const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
+            if (!active && mine < end) {
+                q = mine;
+                active = true;
+                local = true;
+                K = qkeys[q];
+                S = qsrc[q];
+                const double2 p = xy[S];
+                sx = p.x; sy = p.y;
+                t = 0; hops = 0;
+                // the local FindNodeCall gets a fresh extension (Koorde.cc:421-429)
+                e.has = 0; e.step = 1;
+            }
+            cursor += (uint64_t)__popcll(need);
+        }
+        if (!__any(active)) break;
+        if (!active) continue;
+
+        uint32_t* seq = hopseq + q * H;
+        uint8_t status = OVS_LOOKUP_OK;
+        bool fin = false;
+        uint32_t R = NONE;
+        const uint32_t c = local ? S : cur;
+        const uint32_t pred = c == 0 ? V.n - 1 : c - 1;
+        // isSiblingFor(c, K, 1) (Chord.cc:452-457): K in (pred, c]
+        const bool sib = between_R(K, rkey(V.recs, pred), rkey(V.recs, c));
+        KExt e2 = e;
+        const uint32_t nx = sib ? c : koorde_find_node_dev(V, c, K, e2);
+        if (local) {
+            // IterativeLookup::start (133-244)
+            local = false;
+            if (sib) { fin = true; R = S; }
+            else if (nx == NONE) { fin = true; status = OVS_LOOKUP_BROKEN; }
+            else if (nx == S) { fin = true; status = OVS_LOOKUP_NO_NEXT; }   // visited: nothing to send
+            else { cur = nx; e = e2; }
+        } else if (nx == NONE) {
+            fin = true; status = OVS_LOOKUP_BROKEN;    // the responder's findNode throws
+        } else {
+            // FindNodeCall S -> c and its FindNodeResponse (one NodeHandle), both with the extension
+            const double2 p = xy[c];
+            const int64_t cd = coord_ns(sx, sy, p.x, p.y, DC.round);
+            const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
+            if (rtt >= DC.rpcTimeout) {
+                fin = true;
+                status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
+            } else {
+                t += rtt;
+                if (t > DC.lookupTimeout) { fin = true; status = OVS_LOOKUP_TIMEOUT; }
+                else {
+                    if (hops < (int)H) seq[hops] = c;
+                    ++hops;
+                    if (sib) { fin = true; R = c; }
+                    else if (hcm && hops >= hcm) { fin = true; status = OVS_LOOKUP_HOPMAX; }
+                    else {
+                        // visitOnlyOnce: the next hop must not be the source or an earlier responder
+                        bool seen = nx == S;
+                        for (int i = 0; i < hops && !seen; ++i) seen = seq[i] == nx;
+                        if (seen) { fin = true; status = OVS_LOOKUP_NO_NEXT; }
+                        else { cur = nx; e = e2; }
+                    }
+                }
+            }
+        }
+        if (fin) {
+            ovs_route_out o;
+            o.hops = (uint16_t)hops;
+            o.status = status;
+            if (status == OVS_LOOKUP_OK) {
+                o.responsible = R;
+                o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
+                int64_t lat = t;
+                if (R != S) {
+                    // sendRouteMessage to the result (BaseOverlay.cc:1107-1146)
+                    const double2 p = xy[R];
+                    lat += DC.msgRoute + coord_ns(sx, sy, p.x, p.y, DC.round);
+                }
+                o.latency_ns = lat;
+            } else {
+                o.responsible = NONE;
+                o.one_way_hops = 0;
+                o.latency_ns = -1;
+            }
+            out[q] = o;
+            // FindNodeCalls sent: one per accepted responder, plus a call to c whose response did
+            // not count (its findNode threw, it timed out, or it came after the lookup timeout)
+            const bool lost = c != S && (status == OVS_LOOKUP_BROKEN || status == OVS_LOOKUP_RPC_TIMEOUT ||
+                                         status == OVS_LOOKUP_TIMEOUT);
+            if (rpcs) rpcs[q] = (uint32_t)hops + (lost ? 1u : 0u);
+            active = false;
+        }
+    }
+}
+
+__global__ void k_koorde_find_node(KView V, const uint32_t* __restrict__ node, const K160* __restrict__ keys,
+                                   KExt* __restrict__ ext, uint32_t* __restrict__ next, uint64_t nq)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    KExt e = ext[i];
+    const uint32_t h = koorde_find_node_dev(V, node[i], keys[i], e);
+    next[i] = h;
+    if (h != NONE) ext[i] = e;
+}
+
+inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+KView make_view(const KoordeTables& t, const KeyRec* recs)
+{
+    KView V;
+    V.recs = recs; V.nd = t.nd; V.n = t.n; V.ns = t.ns; V.sb = t.sb; V.useOther = t.useOther; V.useSuc = t.useSuc;
+    return V;
+}
+
+}  // namespace
+
+hipError_t koorde_build(const KeyRec* recs, uint32_t n, int successorListSize, int shiftingBits, int deBruijnListSize,
+                        int useOtherLookup, int useSucList, KoordeTables& t, hipStream_t st)
+{
+    koorde_free(t);
+    if (n < 2 || shiftingBits < 1 || shiftingBits > 32 || deBruijnListSize < 1) return hipErrorInvalidValue;
+    t.n = n;
+    t.ns = (int)std::min<uint64_t>((uint64_t)successorListSize, (uint64_t)n - 1);
+    t.sb = shiftingBits; t.dbls = deBruijnListSize; t.useOther = useOtherLookup; t.useSuc = useSucList;
+    hipError_t e = hipMalloc(&t.nd, sizeof(KoordeNode) * n);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_koorde_build, dim3(nblk(n, 256)), dim3(256), 0, st, recs, n, t.ns, shiftingBits,
+                       deBruijnListSize, t.nd);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(st);
+}
+
+hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2* xy, const DelayConsts& DC,
+                        int hopCountMax, const K160* keys, const uint32_t* src, uint64_t nq, ovs_route_out* out,
+                        uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st)
+{
+    if (nq == 0) return hipSuccess;
+    if (!hopseq) return hipErrorInvalidValue;
+    static int bpc = 0;
+    if (bpc == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_koorde_route, 256, 0) != hipSuccess || b < 1) b = 1;
+        bpc = b;
+    }
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4;
+    uint64_t chunk = (nq + waves - 1) / waves;
+    if (chunk < 1) chunk = 1;
+    const uint64_t blocks = ((nq + chunk - 1) / chunk + 3) / 4;
+    hipLaunchKernelGGL(k_koorde_route, dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC, hopCountMax,
+                       keys, src, nq, chunk, out, hopseq, rpcs);
+    return hipGetLastError();
+}
+
+hipError_t koorde_find_node(const KoordeTables& t, const KeyRec* recs, const uint32_t* node, const K160* keys,
+                            KExt* ext, uint32_t* next, uint64_t nq, hipStream_t st)
+{
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_koorde_find_node, dim3(nblk(nq, 128)), dim3(128), 0, st, make_view(t, recs), node, keys, ext,
+                       next, nq);
+    return hipGetLastError();
+}
+
+}  // namespace ovs

@@ -238,7 +238,8 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         return false;
     };
 
-    const std::string ov = p->overlay == OVS_OVERLAY_KADEMLIA ? "kademlia" : "chord";
+    const std::string ov = p->overlay == OVS_OVERLAY_KADEMLIA ? "kademlia"
+                           : p->overlay == OVS_OVERLAY_KOORDE ? "koorde" : "chord";
     const std::string host = "SimpleUnderlayNetwork.overlayTerminal[0]";
     const std::string ovp = host + ".overlay." + ov + ".";
     std::string v, bad;
@@ -251,10 +252,16 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
     };
     want_int("keyLength", &p->keyLength);
     want_int("hopCountMax", &p->hopCountMax);
-    if (p->overlay == OVS_OVERLAY_CHORD) {
+    if (p->overlay == OVS_OVERLAY_CHORD || p->overlay == OVS_OVERLAY_KOORDE) {
         want_int("successorListSize", &p->successorListSize);
         want_bool("extendedFingerTable", &p->extendedFingerTable);
         want_int("numFingerCandidates", &p->numFingerCandidates);
+        if (p->overlay == OVS_OVERLAY_KOORDE) {   // Koorde.ned, default.ini:268-291
+            want_int("shiftingBits", &p->shiftingBits);
+            want_int("deBruijnListSize", &p->deBruijnListSize);
+            want_bool("useOtherLookup", &p->useOtherLookup);
+            want_bool("useSucList", &p->useSucList);
+        }
     } else {
         want_int("k", &p->k);
         want_int("s", &p->s);
@@ -354,6 +361,11 @@ extern "C" void ovs_params_default(int32_t overlay, ovs_params* p)
     p->datarate = 10e6;                 // channels.ned simple_ethernetline
     p->accessDelay = 0.0;
     p->kadSeed = 0x4b41444dull;
+    p->shiftingBits = 4;                // default.ini:277
+    p->deBruijnListSize = 16;           // default.ini:276
+    p->useOtherLookup = 1;              // default.ini:279
+    p->useSucList = 1;                  // default.ini:280
+    if (overlay == OVS_OVERLAY_KOORDE) p->successorListSize = 16;   // default.ini:275
     if (overlay == OVS_OVERLAY_KADEMLIA) {
         p->lookupRedundantNodes = 8;    // default.ini:186
         p->lookupParallelRpcs = 3;      // default.ini:188

@@ -16,6 +16,7 @@
 
 #include "kad.hpp"
 #include "kad_shard.hpp"
+#include "koorde.hpp"
 #include "launch.hpp"
 #include "stats.hpp"
 
@@ -53,6 +54,8 @@ struct ovs_ctx {
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     // kademlia
     KadTables kad{};
+    // koorde (on the sorted ring in recs / xy)
+    KoordeTables koorde{};
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
     uint8_t* kact = nullptr;             // 0 done, 1 running, 2 not started
@@ -93,6 +96,7 @@ void free_tables(ovs_ctx* c)
     c->recs = nullptr; c->xy = nullptr; c->fingers = nullptr; c->pred = nullptr;
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
+    koorde_free(c->koorde);
     c->overlay = 0; c->n = 0; c->nfing = 0;
     c->h_ids.clear(); c->h_deque.clear(); c->h_fsize.clear(); c->h_succ0.clear(); c->h_fres.clear();
 }
@@ -136,6 +140,13 @@ DelayConsts delay_consts(const ovs_params& P)
     d.access2 = 2 * acc;
     d.callBytes = 83;        // FINDNODECALL_L 440 bits + 28 B
     d.respBase = 61;         // FINDNODERESPONSE_L 264 bits + 28 B
+    if (P.overlay == OVS_OVERLAY_KOORDE) {
+        // every Koorde FindNodeCall / FindNodeResponse carries a KoordeFindNodeExtMessage,
+        // KEY_L + STEP_L = 168 bits (ChordMessage.msg:33,55; IterativeLookup.cc:385-388,
+        // BaseOverlay.cc:1903-1907)
+        d.callBytes += 21;
+        d.respBase += 21;
+    }
     d.respPerNode = 26;      // NODEHANDLE_L 208 bits
     d.routeBytes = route_bytes(P);
     d.msgCall = 2 * bw(d.callBytes) + 2 * acc;
@@ -327,6 +338,11 @@ ovs_status ovs_set_params(ovs_ctx* c, const ovs_params* p)
     if (c->overlay == OVS_OVERLAY_KADEMLIA &&
         (p->k != c->P.k || p->s != c->P.s || p->b != c->P.b || p->kadSeed != c->P.kadSeed))
         return fail(c, OVS_ESTATE, "k/s/b/kadSeed are fixed once a Kademlia network is loaded");
+    if (c->overlay == OVS_OVERLAY_KOORDE &&
+        (p->successorListSize != c->P.successorListSize || p->shiftingBits != c->P.shiftingBits ||
+         p->deBruijnListSize != c->P.deBruijnListSize || p->useOtherLookup != c->P.useOtherLookup ||
+         p->useSucList != c->P.useSucList))
+        return fail(c, OVS_ESTATE, "the Koorde ring parameters are fixed once a Koorde network is loaded");
     c->P = *p;
     return OVS_OK;
 }
@@ -741,6 +757,70 @@ ovs_status ovs_kad_export(ovs_ctx* c, uint32_t* siblings, uint8_t* bucket_count,
     return OVS_OK;
 }
 
+ovs_status ovs_koorde_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, uint32_t flags)
+{
+    if (!c || !ids || !xy) return OVS_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    free_kad_shard(c);
+    if (c->P.overlay != OVS_OVERLAY_KOORDE) return fail(c, OVS_ESTATE, "params.overlay is not Koorde");
+    if (n < 2) return fail(c, OVS_EINVAL, "Koorde needs at least 2 nodes");
+    if (c->P.successorListSize < 1) return fail(c, OVS_EINVAL, "successorListSize must be >= 1");
+    if (c->P.shiftingBits < 1 || c->P.shiftingBits > 16 || c->P.deBruijnListSize < 1 || c->P.deBruijnListSize > 255)
+        return fail(c, OVS_ENOTSUP, "Koorde shiftingBits must be 1..16 and deBruijnListSize 1..255");
+    ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    hipError_t e = koorde_build(c->recs, (uint32_t)n, c->P.successorListSize, c->P.shiftingBits, c->P.deBruijnListSize,
+                                c->P.useOtherLookup, c->P.useSucList, c->koorde, c->stream);
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "koorde build"); }
+    c->overlay = OVS_OVERLAY_KOORDE;
+    return OVS_OK;
+}
+
+ovs_status ovs_koorde_export(ovs_ctx* c, uint32_t* db_node, uint32_t* db_start, uint8_t* db_num)
+{
+    if (!c || !db_node || !db_start || !db_num) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KOORDE) return fail(c, OVS_ESTATE, "no Koorde network loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<KoordeNode> h(c->n);
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->koorde.nd, sizeof(KoordeNode) * c->n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (uint64_t i = 0; i < c->n; ++i) {
+        db_node[i] = h[i].db; db_start[i] = h[i].dbStart; db_num[i] = (uint8_t)h[i].dbNum;
+    }
+    return OVS_OK;
+}
+
+ovs_status ovs_koorde_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key160* keys, ovs_koorde_ext* ext,
+                                      uint32_t* next, uint64_t n)
+{
+    static_assert(sizeof(ovs_koorde_ext) == sizeof(KExt), "ovs_koorde_ext mirrors KExt");
+    if (!c || (n && (!node || !keys || !ext || !next))) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KOORDE) return fail(c, OVS_ESTATE, "no Koorde network loaded");
+    if (n == 0) return OVS_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    for (uint64_t i = 0; i < n; ++i)
+        if (node[i] >= c->n) return fail(c, OVS_EINVAL, "node index out of range");
+    uint32_t *dn = nullptr, *dnext = nullptr;
+    K160* dk = nullptr;
+    KExt* de = nullptr;
+    bool o1, o2;
+    ovs_status st = to_device(c, node, n, false, &dn, &o1);
+    if (st != OVS_OK) return st;
+    st = to_device(c, reinterpret_cast<const K160*>(keys), n, false, &dk, &o2);
+    if (st != OVS_OK) { hipFree(dn); return st; }
+    HIPCHK(c, hipMalloc(&de, sizeof(KExt) * n));
+    HIPCHK(c, hipMalloc(&dnext, sizeof(uint32_t) * n));
+    HIPCHK(c, hipMemcpyAsync(de, ext, sizeof(KExt) * n, hipMemcpyHostToDevice, c->stream));
+    hipError_t e = koorde_find_node(c->koorde, c->recs, dn, dk, de, dnext, n, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "koorde findNode kernel");
+    HIPCHK(c, hipMemcpyAsync(ext, de, sizeof(KExt) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(next, dnext, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(dn); hipFree(dk); hipFree(de); hipFree(dnext);
+    return OVS_OK;
+}
+
 ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                            ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs, uint32_t flags, void* stream)
 {
@@ -759,6 +839,13 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             return fail(c, OVS_ESTATE, "context holds one arc of a sharded ring: use ovs_shard_step");
         st = ensure_nodes(c, s);
         if (st != OVS_OK) return st;
+    } else if (c->overlay == OVS_OVERLAY_KOORDE) {
+        if (c->P.routingType != 0) return fail(c, OVS_ENOTSUP, "Koorde routing is implemented for routingType = iterative");
+        if (c->P.lookupRedundantNodes != 1 || c->P.lookupParallelRpcs != 1 || c->P.lookupMerge ||
+            c->P.numSiblings != 1 || !c->P.lookupVisitOnlyOnce)
+            return fail(c, OVS_ENOTSUP,
+                        "Koorde route kernel implements lookupRedundantNodes=1, lookupParallelRpcs=1, merge off, "
+                        "visitOnlyOnce, numSiblings=1 (the Koorde defaults)");
     } else if (c->P.routingType != 0) {
         return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
     } else if (c->P.numSiblings != 1) {
@@ -782,8 +869,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         ds = const_cast<uint32_t*>(src);
         dout = out;
     }
-    // hop sequence buffer: always needed for explicit Chord tables (visited check) and Kademlia
-    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal);
+    // hop sequence buffer: always needed for explicit Chord tables and Koorde (the visited check)
+    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal) || c->overlay == OVS_OVERLAY_KOORDE;
     bool own_hop = false;
     if (need_hop) {
         if (dev && hop_seq) dhop = hop_seq;
@@ -806,6 +893,9 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             if (LC.recursive) e = hipMemsetAsync(drpc, 0, sizeof(uint32_t) * n, s);   // no FindNodeCalls
             else e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
         }
+    } else if (c->overlay == OVS_OVERLAY_KOORDE) {
+        e = koorde_route(c->koorde, c->recs, c->xy, delay_consts(c->P), c->P.hopCountMax, dk, ds, n, dout, dhop, drpc,
+                         c->num_cu, s);
     } else {
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
                       c->num_cu, s);
@@ -831,6 +921,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     static_assert(sizeof(ovs_lookup_out) == sizeof(ovs_route_out), "lookup results are finished in place");
     if (!c || (n && (!keys || !src || !out || !siblings))) return OVS_EINVAL;
     if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (c->overlay == OVS_OVERLAY_KOORDE)
+        return fail(c, OVS_ENOTSUP, "Koorde: ovs_route_batch and ovs_koorde_find_node_batch only");
     const bool chord = c->overlay == OVS_OVERLAY_CHORD;
     // BaseOverlay::lookupRpc: numSiblings < 0 -> getMaxNumSiblings() (Chord.cc getMaxNumSiblings =
     // successorListSize, Kademlia.cc:347-350 = s); isSiblingFor rejects larger values
@@ -923,6 +1015,8 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
 {
     if (!c || (n && (!node || !keys || !out_nodes || !out_count || !out_sibling)) || max_out == 0) return OVS_EINVAL;
     if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (c->overlay == OVS_OVERLAY_KOORDE)
+        return fail(c, OVS_ENOTSUP, "Koorde: ovs_route_batch and ovs_koorde_find_node_batch only");
     if (numSiblings > (c->overlay == OVS_OVERLAY_CHORD ? c->P.successorListSize : c->P.s))
         return fail(c, OVS_EINVAL, "numSiblings too big!");
     if (numRedundantNodes < 1 || numRedundantNodes > 64) return fail(c, OVS_EINVAL, "numRedundantNodes out of range");

@@ -33,6 +33,7 @@ _LIB_PATH = Path(os.environ.get("OVS_LIB") or Path(__file__).resolve().parent / 
 
 OVERLAY_CHORD = 1
 OVERLAY_KADEMLIA = 2
+OVERLAY_KOORDE = 3
 DEVICE_PTRS = 0x1
 NONE = 0xFFFFFFFF
 
@@ -62,6 +63,8 @@ class Params(C.Structure):
         ("recNumRedundantNodes", C.c_int32), ("rpcUdpTimeout", C.c_double), ("lookupTimeout", C.c_double),
         ("jitter", C.c_double), ("constantDelay", C.c_double), ("datarate", C.c_double),
         ("accessDelay", C.c_double), ("kadSeed", C.c_uint64),
+        ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
+        ("useSucList", C.c_int32),
     ]
 
     @classmethod
@@ -77,6 +80,10 @@ class Params(C.Structure):
     @classmethod
     def kademlia(cls) -> "Params":
         return cls.default(OVERLAY_KADEMLIA)
+
+    @classmethod
+    def koorde(cls) -> "Params":
+        return cls.default(OVERLAY_KOORDE)
 
     @classmethod
     def from_ini(cls, text: str, config: str | None = None, overlay: int = OVERLAY_CHORD,
@@ -103,6 +110,8 @@ class Params(C.Structure):
 ROUTE_OUT_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
                             ("one_way_hops", "u1"), ("latency_ns", "<i8")])
 assert ROUTE_OUT_DTYPE.itemsize == 16
+KOORDE_EXT_DTYPE = np.dtype([("route_key", "<u4", 5), ("step", "<i4"), ("has_route_key", "<i4")])
+assert KOORDE_EXT_DTYPE.itemsize == 28
 LOOKUP_OUT_DTYPE = np.dtype([("num_siblings", "<u4"), ("hops", "<u2"), ("status", "u1"),
                              ("is_valid", "u1"), ("latency_ns", "<i8")])
 assert LOOKUP_OUT_DTYPE.itemsize == 16
@@ -172,6 +181,9 @@ def lib() -> C.CDLL:
         "ovs_chord_load": ([vp, vp, u64, vp, u32], C.c_int),
         "ovs_chord_load_tables": ([vp, vp, u64, vp, vp, vp, vp, vp, vp, u32], C.c_int),
         "ovs_kad_load": ([vp, vp, u64, vp, u32], C.c_int),
+        "ovs_koorde_load": ([vp, vp, u64, vp, u32], C.c_int),
+        "ovs_koorde_export": ([vp, vp, vp, vp], C.c_int),
+        "ovs_koorde_find_node_batch": ([vp, vp, vp, vp, vp, u64], C.c_int),
         "ovs_kad_load_tables": ([vp, vp, u64, vp, vp, vp, vp, u32], C.c_int),
         "ovs_kad_export": ([vp, vp, vp, vp], C.c_int),
         "ovs_chord_export_fingers": ([vp, vp], C.c_int),
@@ -304,6 +316,42 @@ class KbrEngine:
         self._chk(self._L.ovs_chord_load(self._h, C.c_void_p(ids_ptr), n, C.c_void_p(xy_ptr), DEVICE_PTRS),
                   "ovs_chord_load")
         self.n, self.overlay = n, OVERLAY_CHORD
+
+    def koorde_load(self, ids, xy):
+        """Converged Koorde ring (ovs_koorde_load); params.overlay must be OVERLAY_KOORDE."""
+        ids = keys_array(ids)
+        xy = np.ascontiguousarray(xy, dtype=np.float64)
+        self._chk(self._L.ovs_koorde_load(self._h, _ptr(ids), len(ids), _ptr(xy), 0), "ovs_koorde_load")
+        self.n, self.overlay = len(ids), OVERLAY_KOORDE
+
+    def koorde_load_device(self, ids_ptr: int, xy_ptr: int, n: int):
+        self._chk(self._L.ovs_koorde_load(self._h, C.c_void_p(ids_ptr), n, C.c_void_p(xy_ptr), DEVICE_PTRS),
+                  "ovs_koorde_load")
+        self.n, self.overlay = n, OVERLAY_KOORDE
+
+    def koorde_state(self):
+        """(deBruijnNode, first node of the deBruijnNodes list, list length) per node."""
+        db = np.empty(self.n, dtype=np.uint32)
+        start = np.empty(self.n, dtype=np.uint32)
+        num = np.empty(self.n, dtype=np.uint8)
+        self._chk(self._L.ovs_koorde_export(self._h, _ptr(db), _ptr(start), _ptr(num)), "ovs_koorde_export")
+        return db, start, num
+
+    def koorde_find_node(self, node, keys, ext=None):
+        """Koorde::findNode at node[i] for keys[i]; ext = KOORDE_EXT_DTYPE records (None: fresh,
+        unspecified route key, step 1) are advanced in place.  Returns (next hop, NONE where the
+        reference throws; the extensions the responses carry)."""
+        node = np.ascontiguousarray(node, dtype=np.uint32)
+        keys = keys_array(keys)
+        n = len(node)
+        if ext is None:
+            ext = np.zeros(n, dtype=KOORDE_EXT_DTYPE)
+            ext["step"] = 1
+        ext = np.ascontiguousarray(ext, dtype=KOORDE_EXT_DTYPE).copy()
+        nxt = np.empty(n, dtype=np.uint32)
+        self._chk(self._L.ovs_koorde_find_node_batch(self._h, _ptr(node), _ptr(keys), _ptr(ext), _ptr(nxt), n),
+                  "ovs_koorde_find_node_batch")
+        return nxt, ext
 
     def kad_load_device(self, ids_ptr: int, xy_ptr: int, n: int):
         self._chk(self._L.ovs_kad_load(self._h, C.c_void_p(ids_ptr), n, C.c_void_p(xy_ptr), DEVICE_PTRS),

@@ -42,7 +42,11 @@ int main(void)
     F(ovs_params, numSiblings); F(ovs_params, useCoordinateBasedDelay); F(ovs_params, simtimeRound);
     F(ovs_params, testMsgSize); F(ovs_params, recNumRedundantNodes); F(ovs_params, rpcUdpTimeout);
     F(ovs_params, lookupTimeout); F(ovs_params, jitter); F(ovs_params, constantDelay); F(ovs_params, datarate);
-    F(ovs_params, accessDelay); F(ovs_params, kadSeed);
+    F(ovs_params, accessDelay); F(ovs_params, kadSeed); F(ovs_params, shiftingBits);
+    F(ovs_params, deBruijnListSize); F(ovs_params, useOtherLookup); F(ovs_params, useSucList);
+    end();
+    S(ovs_koorde_ext);
+    F(ovs_koorde_ext, route_key); F(ovs_koorde_ext, step); F(ovs_koorde_ext, has_route_key);
     end();
     S(ovs_route_out);
     F(ovs_route_out, responsible); F(ovs_route_out, hops); F(ovs_route_out, status); F(ovs_route_out, one_way_hops);

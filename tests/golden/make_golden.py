@@ -12,8 +12,8 @@ generator in oversim_amd/workload.py; coordinates for N <= 15000 are records of
 the reference's simulations/nodes_2d_15000.xml.
 
 Each .npz records the SimTime rounding rule it was generated with.
-Run: python tests/golden/make_golden.py [--kad] [--rec] [--check: verify the committed Kademlia
-vectors instead of rewriting them]
+Run: python tests/golden/make_golden.py [--kad] [--rec] [--koorde] [--check: with --koorde verify the
+committed Koorde vectors, alone the committed Kademlia vectors, instead of rewriting them]
 """
 from __future__ import annotations
 
@@ -27,7 +27,7 @@ sys.path.insert(0, str(HERE.parent.parent))
 sys.path.insert(0, str(HERE.parent))
 
 from oversim_amd import workload as W  # noqa: E402
-from oracle_lib import OracleNet, chord_params, kad_params  # noqa: E402
+from oracle_lib import OracleNet, chord_params, kad_params, koorde_params  # noqa: E402
 import refmodel  # noqa: E402
 
 
@@ -123,12 +123,51 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
           "status", np.bincount(r["status"]))
 
 
+def koorde_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, **kw):
+    """Koorde one-way lookups (iterative, Koorde defaults unless overridden), checked against
+    refmodel.KoordeRing (a second reading of Koorde.cc) before writing."""
+    net = W.population(n, seed)
+    k1, s1 = W.lookups(net.ids, m_ids, seed + 1, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m_rand, seed + 2, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    p = koorde_params(**kw)
+    o = OracleNet("koorde", net.ids, net.xy, p)
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    ring = refmodel.KoordeRing(net.ids, net.xy, p.successorListSize, p.deBruijnListSize, p.shiftingBits,
+                               bool(p.useOtherLookup), bool(p.useSucList))
+    for i in range(len(keys)):
+        m = ring.lookup(keys[i], int(src[i]))
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+            assert int(r[f][i]) == int(m[f]), (name, i, f, r[f][i], m[f])
+        assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == m["hop_seq"], (name, i)
+    db, dstart, dnum = o.koorde_state()
+    H = int(r["hops"].max()) + 1
+    out = dict(responsible=r["responsible"], hops=r["hops"], status=r["status"], one_way_hops=r["one_way_hops"],
+               latency_ns=r["latency_ns"], rpcs=r["rpcs"], hop_seq=r["hop_seq"][:, :H], db=db, db_start=dstart,
+               db_num=dnum)
+    if "--check" in sys.argv:
+        g = np.load(HERE / f"{name}.npz")
+        for f, v in out.items():
+            assert np.array_equal(g[f], v), (name, f)
+        print(name, "committed vectors reproduced")
+        return
+    np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=keys, src=src, seed=np.int64(seed),
+                        successorListSize=np.int32(p.successorListSize), deBruijnListSize=np.int32(p.deBruijnListSize),
+                        shiftingBits=np.int32(p.shiftingBits), useOtherLookup=np.int32(p.useOtherLookup),
+                        useSucList=np.int32(p.useSucList), **out)
+    print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
+
+
 if __name__ == "__main__":
+    if "--koorde" in sys.argv:   # (with --check: verify instead of writing)
+        koorde_case("koorde_n2000", 2000, 0x4b4f, 1024, 1024)
+        koorde_case("koorde_n2000_sb2_nosuc", 2000, 0x4b50, 512, 512, shiftingBits=2, useSucList=0)
+        sys.exit(0)
     if "--rec" in sys.argv:
         chord_rec_case("chord_n1000_semirec", 1000, 0x4213, 2048, 2048, 1)
         chord_rec_case("chord_n1000_semirec_hcm4", 1000, 0x4214, 512, 512, 0, hcm=4)
         sys.exit(0)
-    if "--check" in sys.argv:
+    if "--check" in sys.argv and "--koorde" not in sys.argv:
         kad_case("kad_n2000_a1", 2000, 0x4b41, 2048, 1)
         kad_case("kad_n2000_a3", 2000, 0x4b41, 2048, 3)
         sys.exit(0)
