@@ -15,6 +15,8 @@ Workloads (--workload, default C):
      sharded over the N GPUs (RCCL all-to-allv).  Weak scaling in lookups.
   B  Kademlia, 15 000 nodes (nodes_2d_15000.xml coordinates), k=8, alpha=1,
      1M node-ID lookups per GPU.  N > 1: independent replicas.
+  K  Koorde, 2^20 nodes, 4M random-key lookups per GPU (not a BASELINE config:
+     the Koorde routing rule).  N > 1: independent replicas.
   E  Kademlia, 2^24 nodes, alpha=3, 4M random-key lookups per GPU.  N > 1: the
      ID space is cut into N arcs (prefixes), each GPU owns its arc's tables, and
      FindNodeCalls are exchanged as request/response all-to-allv rounds
@@ -53,6 +55,10 @@ B_HOP_SURVEY = 512
 # a 24 B-entry layout; reported beside ("survey_bytes_per_rpc").
 B_RPC, B_KLOOKUP = 160, 200
 B_RPC_SURVEY = 448
+# Koorde: a hop reads the responder's ring records (predecessor, itself, first successor: 3 x 24 B),
+# its 16 B KoordeNode and its 16 B coordinates; a lookup its key/source (24 B), the source's
+# coordinates (16 B) and writes 16 B.  The successor / de Bruijn list searches are extra.
+B_KHOP, B_KLOOKUP_K = 104, 56
 
 
 def parse():
@@ -60,7 +66,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["B", "C", "D", "E"], default="C")
+    ap.add_argument("--workload", choices=["B", "C", "D", "E", "K"], default="C")
     ap.add_argument("--nodes", type=int, default=None, help="override ring size (per GPU for C, total for D/E)")
     ap.add_argument("--lookups", type=int, default=None, help="override lookups per GPU per step")
     ap.add_argument("--routing", choices=["iterative", "semi-recursive"], default="iterative",
@@ -82,13 +88,16 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
     oracle's stored tables (configs D, E) use its lazy tables (every table entry evaluated per
     access), which makes that port slower than one holding the tables."""
     sys.path.insert(0, str(ROOT / "tests"))
-    from oracle_lib import OracleNet, chord_params, kad_params
+    from oracle_lib import OracleNet, chord_params, kad_params, koorde_params
     nproc = os.cpu_count() or 1
     # the job's CPU share: OMP_NUM_THREADS on the GPU box (16 per GPU), else every CPU
     nthreads = max(1, min(nproc, int(os.environ.get("OMP_NUM_THREADS", nproc))))
     lazy = len(ids) > (1 << 22)
-    o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia"
-                  else chord_params(routingType=routing_type), lazy=lazy)
+    if kind == "koorde":
+        o = OracleNet(kind, ids, xy, koorde_params())
+    else:
+        o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia"
+                      else chord_params(routingType=routing_type), lazy=lazy)
 
     def timed(threads: int, budget_s: float):
         m = 2000
@@ -193,7 +202,8 @@ def main():
     if routing_type:
         wl["desc"] = wl["desc"].replace("iterative", "semi-recursive")
     stream = torch.cuda.Stream(device=dev)
-    sharded = world > 1 and (kind == "chord" or os.environ.get("OVS_KAD_REPLICAS") != "1")
+    # Koorde runs replicas (its tables are not sharded); Kademlia shards unless OVS_KAD_REPLICAS=1
+    sharded = world > 1 and (kind == "chord" or (kind == "kademlia" and os.environ.get("OVS_KAD_REPLICAS") != "1"))
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
     I = W.bench_inputs(a.workload, dev, world=world, rank=rank, seed=a.seed, nodes=a.nodes, n_lookups=a.lookups,
@@ -226,6 +236,11 @@ def main():
             torch.cuda.synchronize()
             eng.chord_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
             kname = "k_chord_lanes"
+        elif kind == "koorde":
+            eng.set_params(Params.koorde())
+            torch.cuda.synchronize()
+            eng.koorde_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
+            kname = "k_koorde_route"
         else:
             eng.set_params(Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
             torch.cuda.synchronize()
@@ -292,6 +307,9 @@ def main():
         if kind == "chord":
             per_launch_bytes = hop_total * B_HOP + lookups_launch * B_LOOKUP
             bper = f"{B_HOP} B/hop + {B_LOOKUP} B/lookup"
+        elif kind == "koorde":
+            per_launch_bytes = hop_total * B_KHOP + lookups_launch * B_KLOOKUP_K
+            bper = f"{B_KHOP} B/hop + {B_KLOOKUP_K} B/lookup"
         else:
             per_launch_bytes = rpc_total * B_RPC + lookups_launch * B_KLOOKUP
             bper = f"{B_RPC} B/RPC + {B_KLOOKUP} B/lookup"
@@ -315,6 +333,8 @@ def main():
         if kind == "kademlia":
             cfg.update({"k": 8, "alpha": wl["alpha"], "rpcs_per_s": rpc_all * a.steps / wall_max,
                         "mean_rpcs": rpc_all / max(ok_all, 1)})
+        elif kind == "koorde":
+            cfg.update({"successorListSize": 16, "deBruijnListSize": 16, "shiftingBits": 4, "routingType": "iterative"})
         else:
             cfg.update({"successorListSize": 8, "routingType": a.routing})
         if sharded:
@@ -339,11 +359,12 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": kname, "kernel_ms": kern_ms,
-                "algorithmic_bytes": bper, "unit_of_work": "hop" if kind == "chord" else "RPC",
+                "algorithmic_bytes": bper, "unit_of_work": "RPC" if kind == "kademlia" else "hop",
                 "traffic_source": traffic_src,
                 "gather_ceiling_GBs": GATHER_CEILING_GBS,
                 "frac_of_gather_ceiling": achieved / GATHER_CEILING_GBS,
-                **({"survey_bytes_per_hop": B_HOP_SURVEY} if kind == "chord" else {"survey_bytes_per_rpc": B_RPC_SURVEY}),
+                **({"survey_bytes_per_hop": B_HOP_SURVEY} if kind == "chord" else
+                   {"survey_bytes_per_rpc": B_RPC_SURVEY} if kind == "kademlia" else {}),
             },
             "cpu_baseline": cpu,
         }

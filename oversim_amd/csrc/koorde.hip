@@ -64,23 +64,25 @@ __device__ __forceinline__ K160 k_small(uint32_t v)
     return r;
 }
 
-// The node of the `num` consecutive ring nodes from sorted index `first` that the reference's
-// interval loop returns for key: the last one strictly (clockwise) before key if key lies in
-// (a_0, a_{num-1}], else a_{num-1}
-__device__ uint32_t walk_list(const KeyRec* __restrict__ recs, uint32_t n, uint32_t first, int num, const K160& key)
+// The node of the `num` consecutive ring nodes a_0 .. a_{num-1} from sorted index `first` that
+// the reference's interval loop returns for key: the last one strictly (clockwise) before key if
+// key lies in (a_0, a_{num-1}], else a_{num-1}.  Both are a_i with i = #{j >= 1 : d(a_0, a_j) <
+// d(a_0, key)} (the distances grow with j): the largest j with d(a_0, a_j) < d(a_0, key), found
+// by bisection over the ring records.  (A precomputed 128 B window of successor distances per
+// node, one read instead of the dependent probes, measured 1.4x slower on config K: DESIGN.md.)
+__device__ __forceinline__ uint32_t walk_list(const KeyRec* __restrict__ recs, uint32_t n, uint32_t first, int num,
+                                              const K160& key)
 {
-    const uint32_t last = ring_add(first, (uint32_t)(num - 1), n);
-    if (num <= 1) return last;
+    if (num <= 1) return first;
     const K160 a0 = rkey(recs, first);
     const K160 dk = k_sub(key, a0);
-    const K160 dl = k_sub(rkey(recs, last), a0);
-    const bool zero = (dk.w[0] | dk.w[1] | dk.w[2] | dk.w[3] | dk.w[4]) == 0;
-    if (zero || k_gt(dk, dl)) return last;
+    const uint32_t last = ring_add(first, (uint32_t)(num - 1), n);
+    if ((dk.w[0] | dk.w[1] | dk.w[2] | dk.w[3] | dk.w[4]) == 0) return last;
+    if (k_lt(k_sub(rkey(recs, last), a0), dk)) return last;
     int lo = 0, hi = num - 1;   // d(a_lo) < dk <= d(a_hi)
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
-        const uint32_t m = ring_add(first, (uint32_t)mid, n);
-        if (k_lt(k_sub(rkey(recs, m), a0), dk)) lo = mid; else hi = mid;
+        if (k_lt(k_sub(rkey(recs, ring_add(first, (uint32_t)mid, n)), a0), dk)) lo = mid; else hi = mid;
     }
     return ring_add(first, (uint32_t)lo, n);
 }
@@ -196,6 +198,9 @@ __global__ void k_koorde_build(const KeyRec* __restrict__ recs, uint32_t n, int 
     nd[v] = o;
 }
 
+// visitOnlyOnce filter: one bit per node hash; a clear bit proves the node unvisited
+__device__ __forceinline__ uint64_t vis_bit(uint32_t x) { return 1ull << ((x * 0x9E3779B1u) >> 26); }
+
 __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                       uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
@@ -215,6 +220,7 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
     double sx = 0, sy = 0;
     int64_t t = 0;
     int hops = 0;
+    uint64_t vis = 0;
     KExt e;
     e.has = 0; e.step = 1;
     while (true) {
@@ -230,6 +236,7 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
                 const double2 p = xy[S];
                 sx = p.x; sy = p.y;
                 t = 0; hops = 0;
+                vis = vis_bit(S);
                 // the local FindNodeCall gets a fresh extension (Koorde.cc:421-429)
                 e.has = 0; e.step = 1;
             }
@@ -271,12 +278,15 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
                 else {
                     if (hops < (int)H) seq[hops] = c;
                     ++hops;
+                    vis |= vis_bit(c);
                     if (sib) { fin = true; R = c; }
                     else if (hcm && hops >= hcm) { fin = true; status = OVS_LOOKUP_HOPMAX; }
                     else {
                         // visitOnlyOnce: the next hop must not be the source or an earlier responder
+                        // (the responder list is read only when the filter bit is set)
                         bool seen = nx == S;
-                        for (int i = 0; i < hops && !seen; ++i) seen = seq[i] == nx;
+                        if (!seen && (vis & vis_bit(nx)))
+                            for (int i = 0; i < hops && !seen; ++i) seen = seq[i] == nx;
                         if (seen) { fin = true; status = OVS_LOOKUP_NO_NEXT; }
                         else { cur = nx; e = e2; }
                     }

@@ -56,6 +56,8 @@ struct ovs_ctx {
     KadTables kad{};
     // koorde (on the sorted ring in recs / xy)
     KoordeTables koorde{};
+    uint32_t* kvis = nullptr;            // K3's per-lookup responder lists when no hop_seq is asked for
+    uint64_t kvis_cap = 0;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
     uint8_t* kact = nullptr;             // 0 done, 1 running, 2 not started
@@ -97,6 +99,8 @@ void free_tables(ovs_ctx* c)
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
     koorde_free(c->koorde);
+    if (c->kvis) hipFree(c->kvis);
+    c->kvis = nullptr; c->kvis_cap = 0;
     c->overlay = 0; c->n = 0; c->nfing = 0;
     c->h_ids.clear(); c->h_deque.clear(); c->h_fsize.clear(); c->h_succ0.clear(); c->h_fres.clear();
 }
@@ -869,10 +873,20 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         ds = const_cast<uint32_t*>(src);
         dout = out;
     }
-    // hop sequence buffer: always needed for explicit Chord tables and Koorde (the visited check)
-    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal) || c->overlay == OVS_OVERLAY_KOORDE;
+    // hop sequence buffer: always needed for explicit Chord tables and Koorde (the visited check).
+    // Koorde without a hop_seq request uses a context scratch buffer, unpadded: K3 reads back only
+    // the entries a lookup wrote
+    const bool koorde_scratch = c->overlay == OVS_OVERLAY_KOORDE && !hop_seq;
+    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal);
     bool own_hop = false;
-    if (need_hop) {
+    if (koorde_scratch) {
+        if (c->kvis_cap < n * (uint64_t)H) {
+            if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
+            HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * (uint64_t)H));
+            c->kvis_cap = n * (uint64_t)H;
+        }
+        dhop = c->kvis;
+    } else if (need_hop) {
         if (dev && hop_seq) dhop = hop_seq;
         else { HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H)); own_hop = true; }
         HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
