@@ -158,6 +158,14 @@ def lib() -> C.CDLL:
     if not _LIB_PATH.exists():
         raise ImportError(f"{_LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
                           "(the MI355X engine has no CPU fallback)")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64 / libhsa-runtime64 (same
+    # SONAMEs as /opt/rocm's).  Loaded after torch, the engine binds to torch's copies; loaded
+    # before it, torch would map a second runtime and whichever initialises second finds no GPU
+    # (tools/diag/runtime_order.py).  So torch, when installed, is imported first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(_LIB_PATH))
     L.ovs_build_id.argtypes = []
     L.ovs_build_id.restype = C.c_char_p

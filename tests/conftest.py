@@ -26,8 +26,7 @@ def _built():
 
 @pytest.fixture()
 def engine():
-    import torch  # noqa: F401  (device visibility check only)
-    from oversim_amd import KbrEngine
+    from oversim_amd import KbrEngine   # kbr.lib() imports torch first: one HIP runtime
     eng = KbrEngine(0)
     yield eng
     eng.close()
