@@ -100,10 +100,16 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
                       else chord_params(routingType=routing_type), lazy=lazy)
 
     def timed(threads: int, budget_s: float):
+        # calibrate on growing prefixes until one takes a quarter of the budget (a short probe
+        # is dominated by thread start-up and would undersize the sample), then run the sample
         m = 2000
-        t = time.perf_counter()
-        o.route(keys[:m], src[:m], record_hops=False, nthreads=threads)
-        dt = time.perf_counter() - t
+        while True:
+            t = time.perf_counter()
+            o.route(keys[:m], src[:m], record_hops=False, nthreads=threads)
+            dt = time.perf_counter() - t
+            if dt >= 0.25 * budget_s or m >= len(keys):
+                break
+            m = min(len(keys), m * max(2, int(0.25 * budget_s / max(dt, 1e-6))))
         m2 = int(min(len(keys), max(m, m * budget_s / max(dt, 1e-6))))
         t = time.perf_counter()
         r = o.route(keys[:m2], src[:m2], record_hops=False, nthreads=threads)
