@@ -31,6 +31,9 @@ struct DelayConsts {
     int64_t msgRespSib;  // same for the responsible node's FindNodeResponse on a converged Chord ring:
                          // min(numSiblings, 1 + successors) NodeHandles (== msgResp1 for numSiblings = 1)
     int32_t lookupCall;  // LookupCall (ovs_lookup_batch): the lookup ends at the last response, no route message
+    int64_t bwCall;      // T(L*8/datarate) of a FindNodeCall, of the route message, and of a FindNodeResponse
+    int64_t bwRoute;     // with 0..16 NodeHandles: the constant serialisation terms, precomputed on the host
+    int64_t bwResp[17];
 };
 
 

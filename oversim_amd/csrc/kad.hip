@@ -489,7 +489,8 @@ hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ov
 {
     if (nq == 0) return hipSuccess;
     if (!kad_params_supported(P, t)) return hipErrorNotSupported;
-    const KadLC LC = kad_make_lc(P, t);
+    KadLC LC = kad_make_lc(P, t);
+    kad_lc_sizes(LC, DC, n);
     const KadView V = kad_make_view(t, xy, n);
     // strictParallelRpcs: never more than alpha FindNodeCalls in flight (IterativeLookup.cc:1078-1079)
     const int A = P.lookupParallelRpcs;

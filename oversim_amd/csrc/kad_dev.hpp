@@ -353,7 +353,11 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         const int cnt = blk_load_block(b, blk, K);
         if (cnt) {
             blk_sort8<false, EX>(b, K, V.nodes);
-            blk_merge_top8<false, EX>(res, b, K, V.nodes);
+            if (seen == 0) {
+                res = b;          // into an empty result the merge is the sorted block itself
+            } else {
+                blk_merge_top8<false, EX>(res, b, K, V.nodes);
+            }
             n = blk_trunc(res, cap);
             seen += cnt;
         }
@@ -541,6 +545,8 @@ struct KadLC {
     int hopCountMax, numSiblings, redundant, alpha;
     int strict, visitOnlyOnce, acceptLateSiblings, useAll, merge, newOnResp, newOnTimeout, finishOnFirst;
     int maxRedundantLocal;   // getMaxNumRedundantNodes() = k
+    int full;                // a non-sibling's response size min(numRedundantNodes, n) ...
+    int64_t bwFull;          // ... and its serialisation delay
 };
 
 // One in-flight FindNodeCall = one future event: its response arrival or its RPC timeout.
@@ -620,11 +626,14 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     // the response carries findNode's result (Kademlia.cc:1127-1131 resultSize)
     const int csz = kad_response_size<EX>(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
     const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
-    const int64_t bwc = bw_ns(DC.callBytes, DC.datarate, DC.round);
+    const int64_t bwc = DC.bwCall;
     const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
     L.txf = newTx;
     const int64_t d1 = (newTx - L.now) + DC.access2 + cd + bwc;
-    const int64_t bwr = bw_ns(DC.respBase + DC.respPerNode * csz, DC.datarate, DC.round);
+    // the response sizes of a lookup are 1 (a sibling) or resultSize (LC.full) but for short
+    // explicit tables: the constant terms, else T(L*8/datarate) itself
+    const int64_t bwr = csz == 1 ? DC.bwResp[1] : csz == LC.full ? LC.bwFull
+                                                 : bw_ns(DC.respBase + DC.respPerNode * csz, DC.datarate, DC.round);
     const int64_t d2 = 2 * bwr + DC.access2 + cd;
     const int64_t tTo = L.now + DC.rpcTimeout;
     const int64_t tResp = L.now + d1 + d2;
@@ -794,7 +803,7 @@ __device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A>& L
         if (L.result != L.S && !DC.lookupCall) {
             // sendRouteMessage through the source's tx queue (SimpleNodeEntry.cc:164-194)
             const double2 rxy = V.xy[L.result];
-            const int64_t bwr = bw_ns(DC.routeBytes, DC.datarate, DC.round);
+            const int64_t bwr = DC.bwRoute;
             const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwr;
             lat = newTx + DC.access2 + coord_ns(L.sx, L.sy, rxy.x, rxy.y, DC.round) + bwr;
         }
@@ -851,7 +860,17 @@ inline KadLC kad_make_lc(const ovs_params& P, const KadTables& t)
     LC.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
     LC.finishOnFirst = P.lookupFinishOnFirstUnchanged;
     LC.maxRedundantLocal = t.k;
+    LC.full = 0;
+    LC.bwFull = 0;
     return LC;
+}
+
+// the response-size constants of a lookup batch over n nodes (kad_make_lc's caller has DC)
+inline void kad_lc_sizes(KadLC& LC, const DelayConsts& DC, uint32_t n)
+{
+    LC.full = LC.redundant < (int)n ? LC.redundant : (int)n;
+    LC.bwFull = DC.bwResp[LC.full <= 16 ? LC.full : 16];
+    if (LC.full > 16) LC.full = -1;
 }
 
 // K2 for one (alpha, exact) pair; instantiated in kad_route.hip (one object per pair)

@@ -248,7 +248,8 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     if (!kad_params_supported(P, t) || P.numSiblings != 1) return hipErrorNotSupported;
     if (nlook == 0) return hipSuccess;
     const KadView V = kad_make_view(t, xy, n);
-    const KadLC LC = kad_make_lc(P, t);
+    KadLC LC = kad_make_lc(P, t);
+    kad_lc_sizes(LC, DC, n);
 #define KSX(a, x) hipLaunchKernelGGL((k_kad_shard_step<a, x>), dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
                                  (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, out, out_dest, out_cap, \
                                  out_count, done, done_cap, done_count, active_count)

@@ -161,6 +161,9 @@ DelayConsts delay_consts(const ovs_params& P)
     d.datarate = P.datarate;
     d.msgRespSib = d.msgResp1;
     d.lookupCall = 0;
+    d.bwCall = bw(d.callBytes);
+    d.bwRoute = bw(d.routeBytes);
+    for (int i = 0; i <= 16; ++i) d.bwResp[i] = bw(d.respBase + d.respPerNode * i);
     return d;
 }
 
