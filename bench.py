@@ -192,7 +192,8 @@ def main():
     dev_index = local % max(ndev, 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    dist_on = world > 1 or os.environ.get("OVS_BENCH_SHARD") == "1"
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -210,6 +211,9 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     # Koorde runs replicas (its tables are not sharded); Kademlia shards unless OVS_KAD_REPLICAS=1
     sharded = world > 1 and (kind == "chord" or (kind == "kademlia" and os.environ.get("OVS_KAD_REPLICAS") != "1"))
+    # rehearsal knob: the sharded host path (collectives, cohorts) at N = 1
+    if os.environ.get("OVS_BENCH_SHARD") == "1" and kind != "koorde":
+        sharded = True
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
     I = W.bench_inputs(a.workload, dev, world=world, rank=rank, seed=a.seed, nodes=a.nodes, n_lookups=a.lookups,
@@ -375,7 +379,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

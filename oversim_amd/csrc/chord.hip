@@ -478,6 +478,10 @@ struct LaneIO {
     const uint64_t* __restrict__ shard_lo;
     int nsh, me;
     uint64_t n, chunk;
+    // the step's outcome per input record (compact_by_tag sorts them into sout / done)
+    ovs_lookup_rec* __restrict__ stage_hand;
+    ovs_done_rec* __restrict__ stage_done;
+    uint8_t* __restrict__ stag;            // arc of the hand-off, or nsh: finished
 };
 
 // LKC: a LookupCall batch (ovs_lookup_batch): the responsible node's larger answer, no route message
@@ -512,6 +516,8 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
     const uint4* lp = nullptr;        // the line requested for the next iteration
     uint4 L0 = make_uint4(0, 0, 0, 0), L1 = L0, L2 = L0, L3 = L0;
     int hand = -1;                    // shard: this lane's lookup moves to arc `hand` this iteration
+    bool done_now = false;            // shard: this lane's lookup finished this iteration ...
+    ovs_route_out done_o{};           // ... with this result
 
     __shared__ uint4 xbuf[4][256];    // per wave: the 64 gathered lines, 4 chunks each
     uint4* const xb = xbuf[threadIdx.x >> 6];
@@ -787,12 +793,8 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 }
                 o.status = status;
                 if (SHARD) {
-                    const unsigned long long di = atomicAdd(io.dcount, 1ull);
-                    if (di < io.dcap) {
-                        ovs_done_rec dr;
-                        dr.qid = qid; dr.pad = 0; dr.out = o;
-                        io.done[di] = dr;
-                    }
+                    done_o = o;           // appended below, one atomic per wave
+                    done_now = true;
                 } else {
                     io.out[q] = o;
                 }
@@ -802,20 +804,19 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
             if (SHARD) hand = emit;
         }
         if (SHARD) {
-            // ---- hand-offs appended to their destination's segment: one atomic per wave and
-            // destination (ballot + prefix count), so the outbox needs no grouping afterwards
-            for (int d = 0; d < io.nsh; ++d) {
-                const uint64_t mk = __ballot(hand == d);
-                if (mk == 0) continue;
-                const int leader = __ffsll((long long)mk) - 1;
-                unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(io.scount + d, (unsigned long long)__popcll(mk));
-                base = __shfl(base, leader);
-                if (hand == d) {
-                    const unsigned long long oi = base + (unsigned long long)__popcll(mk & lt_mask);
-                    if (oi < io.scap) store_lrec(io.sout + (uint64_t)d * io.scap, oi, K, S, cur, qid, t, hops, 0);
-                }
+            // ---- every input record has exactly one outcome this launch, staged at its own index
+            // (no atomics: compact_by_tag moves them to the per-arc segments and the done buffer)
+            if (done_now) {
+                ovs_done_rec dr;
+                dr.qid = qid; dr.pad = 0; dr.out = done_o;
+                io.stage_done[q] = dr;
+                io.stag[q] = (uint8_t)io.nsh;
             }
+            if (hand >= 0) {
+                store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, 0);
+                io.stag[q] = (uint8_t)hand;
+            }
+            done_now = false;
             hand = -1;
         }
         // ---- request the next line: a cooperative gather, 4 lanes fetch one 64 B line with one
@@ -1146,15 +1147,36 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
                                    ovs_lookup_rec* out, uint64_t out_cap,
                                    unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                                   unsigned long long* done_count, int num_cu, hipStream_t s)
+                                   unsigned long long* done_count, StageBuf& stage, int num_cu, hipStream_t s)
 {
     if (nin == 0) return hipSuccess;
+    if (nsh < 1 || nsh + 1 > CMAX) return hipErrorInvalidValue;
+    // stage: a hand-off record and a done record per input, and its outcome tag
+    const size_t oh = 0, od = oh + sizeof(ovs_lookup_rec) * nin, ot = od + sizeof(ovs_done_rec) * nin;
+    hipError_t e = stage_ensure(stage, ot + nin, s);
+    if (e != hipSuccess) return e;
+    uint8_t* sb = static_cast<uint8_t*>(stage.buf);
     LaneIO io{};
     io.in = in; io.sout = out; io.scap = out_cap; io.scount = out_count;
     io.done = done; io.dcap = done_cap; io.dcount = done_count;
     io.shard_lo = shard_lo; io.nsh = nsh; io.me = me; io.n = nin;
-    return LC.recursive ? lanes_launch<true, false, true>(V, DC, LC, io, num_cu, s)
-                        : lanes_launch<false, false, true>(V, DC, LC, io, num_cu, s);
+    io.stage_hand = reinterpret_cast<ovs_lookup_rec*>(sb + oh);
+    io.stage_done = reinterpret_cast<ovs_done_rec*>(sb + od);
+    io.stag = sb + ot;
+    if ((e = hipMemsetAsync(io.stag, 0xFF, nin, s)) != hipSuccess) return e;
+    e = LC.recursive ? lanes_launch<true, false, true>(V, DC, LC, io, num_cu, s)
+                     : lanes_launch<false, false, true>(V, DC, LC, io, num_cu, s);
+    if (e != hipSuccess) return e;
+    // outcomes to their outputs: class d < nsh = hand-offs to arc d (segment d of out), nsh = done
+    CPlan P{};
+    P.seg.src = sb + oh; P.seg.src_stride = P.seg.rec_bytes = sizeof(ovs_lookup_rec);
+    P.seg.dst = reinterpret_cast<uint8_t*>(out); P.seg.dst_stride = sizeof(ovs_lookup_rec) * out_cap;
+    P.seg.cap = out_cap; P.seg.counter = out_count; P.seg.n = nsh; P.seg.chain = 0;
+    P.nextra = 1;
+    CClass& d = P.extra[0];
+    d.src = sb + od; d.src_stride = d.rec_bytes = sizeof(ovs_done_rec);
+    d.dst = reinterpret_cast<uint8_t*>(done); d.cap = done_cap; d.counter = done_count;
+    return compact_by_tag(io.stag, nin, P, stage.cs, s);
 }
 
 hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,

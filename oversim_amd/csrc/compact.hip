@@ -1,0 +1,172 @@
+// compact.hip -- stable compaction by class tag (compact.hpp): count, scan, scatter.
+#include "compact.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace ovs {
+
+namespace {
+
+constexpr int CT_STEPS = 16;                 // one wave per tile, 16 elements per lane
+constexpr uint64_t CT_TILE = 64 * CT_STEPS;
+
+__device__ __forceinline__ uint8_t tag_at(const uint8_t* __restrict__ tags, uint64_t n, uint64_t e)
+{
+    return e < n ? tags[e] : (uint8_t)0xFF;
+}
+
+// cnt[c * nb + b] = elements of class c in tile b
+__global__ __launch_bounds__(64) void k_compact_count(const uint8_t* __restrict__ tags, uint64_t n, int nclass,
+                                                      uint64_t nb, unsigned long long* __restrict__ cnt)
+{
+    __shared__ unsigned int h[CMAX];
+    const int lane = threadIdx.x;
+    const uint64_t b = blockIdx.x;
+    for (int c = lane; c < nclass; c += 64) h[c] = 0;
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < CT_STEPS; ++k) {
+        const uint8_t t = tag_at(tags, n, b * CT_TILE + (uint64_t)k * 64 + lane);
+        if (t < nclass) atomicAdd(&h[t], 1u);
+    }
+    __syncthreads();
+    for (int c = lane; c < nclass; c += 64) cnt[(uint64_t)c * nb + b] = h[c];
+}
+
+// per class: the position of its first record and the counter updates (one thread, <= CMAX classes)
+__global__ void k_compact_base(CPlan P, int nclass, uint64_t nb, const unsigned long long* __restrict__ scan,
+                               long long* __restrict__ cbase)
+{
+    long long run = 0;
+    unsigned long long* hc = nullptr;
+    for (int c = 0; c < nclass; ++c) {
+        const CClass k = plan_class(P, c);
+        const unsigned long long s0 = scan[(uint64_t)c * nb], s1 = scan[(uint64_t)(c + 1) * nb];
+        if (!k.chain || c == 0) {
+            hc = k.counter;
+            run = hc ? (long long)*hc : 0;
+        }
+        cbase[c] = run - (long long)s0;
+        run += (long long)(s1 - s0);
+        const bool last = c + 1 == nclass || !plan_class(P, c + 1).chain;
+        if (last && hc) *hc = (unsigned long long)run;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_compact_scatter(const uint8_t* __restrict__ tags, uint64_t n, CPlan P,
+                                                        int nclass, uint64_t nb,
+                                                        const unsigned long long* __restrict__ scan,
+                                                        const long long* __restrict__ cbase)
+{
+    __shared__ long long off[CMAX];
+    const int lane = threadIdx.x;
+    const uint64_t b = blockIdx.x;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int c = lane; c < nclass; c += 64) off[c] = cbase[c] + (long long)scan[(uint64_t)c * nb + b];
+    __syncthreads();
+    for (int k = 0; k < CT_STEPS; ++k) {
+        const uint64_t e = b * CT_TILE + (uint64_t)k * 64 + lane;
+        const uint8_t t = tag_at(tags, n, e);
+        const bool mine = t < nclass;
+        uint64_t rem = __ballot(mine);
+        long long pos = -1;
+        // one pass per class present in this group of 64: stable ranks by ballot
+        while (rem) {
+            const int l0 = __ffsll((long long)rem) - 1;
+            const int c = __shfl((int)t, l0);
+            const uint64_t m = __ballot(mine && (int)t == c);
+            const long long o = off[c];
+            if (mine && (int)t == c) pos = o + (long long)__popcll(m & lt);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == l0) off[c] = o + (long long)__popcll(m);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            rem &= ~m;
+        }
+        if (mine) {
+            const CClass C = plan_class(P, t);
+            if (C.dst && pos >= 0 && (uint64_t)pos < C.cap) {
+                const uint2* s = reinterpret_cast<const uint2*>(C.src + e * C.src_stride);
+                uint2* d = reinterpret_cast<uint2*>(C.dst + (uint64_t)pos * C.rec_bytes);
+                for (uint32_t w = 0; w < C.rec_bytes / 8; ++w) d[w] = s[w];
+                if (C.lab) C.lab[pos] = C.label;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void compact_free(CompactScratch& s)
+{
+    if (s.buf) hipFree(s.buf);
+    s.buf = nullptr;
+    s.bytes = 0;
+}
+
+void stage_free(StageBuf& b)
+{
+    if (b.buf) hipFree(b.buf);
+    b.buf = nullptr;
+    b.bytes = 0;
+    compact_free(b.cs);
+}
+
+hipError_t stage_ensure(StageBuf& b, size_t bytes, hipStream_t s)
+{
+    if (bytes <= b.bytes) return hipSuccess;
+    hipError_t e;
+    if (b.buf) {
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        hipFree(b.buf);
+        b.buf = nullptr;
+        b.bytes = 0;
+    }
+    bytes = (bytes + 255) & ~(size_t)255;
+    if ((e = hipMalloc(&b.buf, bytes)) != hipSuccess) return e;
+    b.bytes = bytes;
+    return hipSuccess;
+}
+
+hipError_t compact_by_tag(const uint8_t* tags, uint64_t n, const CPlan& P, CompactScratch& scr, hipStream_t s)
+{
+    const int nclass = P.seg.n + P.nextra;
+    if (nclass < 1 || nclass > CMAX || P.nextra < 0 || P.nextra > 2) return hipErrorInvalidValue;
+    for (int c = 0; c < nclass; ++c) {
+        const CClass k = plan_class(P, c);
+        if (k.dst && (k.rec_bytes % 8 != 0 || k.src_stride % 8 != 0)) return hipErrorInvalidValue;
+    }
+    const uint64_t nb = n ? (n + CT_TILE - 1) / CT_TILE : 1;
+    const uint64_t ncnt = (uint64_t)nclass * nb + 1;
+    size_t tmpb = 0;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, (unsigned long long*)nullptr,
+                                                    (unsigned long long*)nullptr, ncnt, s);
+    if (e != hipSuccess) return e;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_base = 0, o_cnt = o_base + al(sizeof(long long) * CMAX), o_scan = o_cnt + al(8 * ncnt),
+                 o_tmp = o_scan + al(8 * ncnt), need = o_tmp + al(tmpb);
+    if (need > scr.bytes) {
+        // the stream may still use the old buffer
+        if (scr.buf && (e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        compact_free(scr);
+        if ((e = hipMalloc(&scr.buf, need)) != hipSuccess) return e;
+        scr.bytes = need;
+    }
+    uint8_t* base = static_cast<uint8_t*>(scr.buf);
+    long long* cbase = reinterpret_cast<long long*>(base + o_base);
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(base + o_cnt);
+    unsigned long long* scan = reinterpret_cast<unsigned long long*>(base + o_scan);
+    // the trailing entry (0) makes scan[nclass * nb] the grand total
+    if ((e = hipMemsetAsync(cnt + ncnt - 1, 0, 8, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(64), 0, s, tags, n, nclass, nb, cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(base + o_tmp, tmpb, cnt, scan, ncnt, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_compact_base, dim3(1), dim3(1), 0, s, P, nclass, nb, scan, cbase);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_compact_scatter, dim3((unsigned)nb), dim3(64), 0, s, tags, n, P, nclass, nb, scan, cbase);
+    return hipGetLastError();
+}
+
+}  // namespace ovs

@@ -13,7 +13,8 @@
 // Per round (oversim_amd/shard.py drives it):
 //   k_kad_shard_step  : every active lookup processes its events in simulated-time
 //                       order until the earliest one still waits for a findNode result;
-//                       new RPCs append requests (32 B) to the outbox, tagged by owner
+//                       a new RPC stages its request (32 B) in the call's slot, tagged
+//                       by owner; compact_by_tag groups them by owner rank (no atomics)
 //   all-to-allv       : requests to their owners
 //   k_kad_shard_serve : findNode at the responder -> response (104 B)
 //   all-to-allv       : responses back to the home rank (reverse splits)
@@ -66,32 +67,29 @@ struct ShardRes {
     }
 };
 
-// new FindNodeCall: mark its slot pending and queue the request to the responder's owner
+// new FindNodeCall: mark its slot pending and stage the request, tagged with the responder's
+// owner, in the call's own slot (a slot carries at most one request per round: a response
+// cannot be ready in the round it is requested)
 struct ShardSend {
     KadRes* __restrict__ res;
     uint64_t base;
     const K160* K;
     const uint64_t* __restrict__ shard_lo;
     int nsh;
-    ovs_kad_req* __restrict__ out;
-    uint32_t* __restrict__ out_dest;
-    uint64_t out_cap;
-    unsigned long long* out_count;
+    ovs_kad_req* __restrict__ stage;
+    uint8_t* __restrict__ rtag;
     __device__ __forceinline__ void operator()(int slot, uint32_t x, bool isTo) const
     {
         // a timeout event carries no result
         res[base + slot].ready = isTo ? 1u : 0u;
         if (isTo) return;
-        const unsigned long long oi = atomicAdd(out_count, 1ull);
-        if (oi < out_cap) {
-            ovs_kad_req q;
-            for (int w = 0; w < 5; ++w) q.key[w] = K->w[w];
-            q.node = x;
-            q.tag = (uint32_t)(base + slot);
-            q.pad = 0;
-            out[oi] = q;
-            out_dest[oi] = (uint32_t)kshard_owner(shard_lo, nsh, x);
-        }
+        ovs_kad_req q;
+        for (int w = 0; w < 5; ++w) q.key[w] = K->w[w];
+        q.node = x;
+        q.tag = (uint32_t)(base + slot);
+        q.pad = 0;
+        stage[base + slot] = q;
+        rtag[base + slot] = (uint8_t)kshard_owner(shard_lo, nsh, x);
     }
 };
 
@@ -104,38 +102,34 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
                                                         KadLookup<A>* __restrict__ st, uint8_t* __restrict__ act,
                                                         const uint32_t* __restrict__ qids, KadRes* __restrict__ res,
                                                         uint64_t nlook, const uint64_t* __restrict__ shard_lo, int nsh,
-                                                        ovs_kad_req* __restrict__ out, uint32_t* __restrict__ out_dest,
-                                                        uint64_t out_cap, unsigned long long* out_count,
-                                                        ovs_done_rec* __restrict__ done, uint64_t done_cap,
-                                                        unsigned long long* done_count,
-                                                        unsigned long long* active_count)
+                                                        ovs_kad_req* __restrict__ rstage, uint8_t* __restrict__ rtag,
+                                                        ovs_done_rec* __restrict__ dstage, uint8_t* __restrict__ ltag)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nlook) return;
     const uint8_t a = act[i];
-    if (a == 0) return;
+    if (a == 0) return;            // finished in an earlier round: tags stay 0xFF
     KadLookup<A> L = st[i];
     SVec<8> r;
-    ShardSend on{res, i * A, &L.K, shard_lo, nsh, out, out_dest, out_cap, out_count};
+    ShardSend on{res, i * A, &L.K, shard_lo, nsh, rstage, rtag};
     const ShardRes<EX> gr{res, i * A, V, L.K};   // the first event is IterativeLookup::start
     const NoRecord rec;
     while (!kad_lookup_done(L)) {
         if (!kad_lookup_event<A, EX, false>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
     }
+    // the lookup's outcome this round, staged at its own index: finished (class 0, its done
+    // record) or still active (class 1, counted)
     if (kad_lookup_done(L)) {
-        const unsigned long long di = atomicAdd(done_count, 1ull);
-        if (di < done_cap) {
-            ovs_done_rec dr;
-            dr.qid = qids[i];
-            dr.pad = 0;
-            dr.out = kad_lookup_output(L, V, DC, LC);
-            done[di] = dr;
-        }
+        ovs_done_rec dr;
+        dr.qid = qids[i];
+        dr.pad = 0;
+        dr.out = kad_lookup_output(L, V, DC, LC);
+        dstage[i] = dr;
+        ltag[i] = 0;
         act[i] = 0;
     } else {
         st[i] = L;
-        act[i] = 1;
-        atomicAdd(active_count, 1ull);
+        ltag[i] = 1;
     }
 }
 
@@ -243,18 +237,32 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
                           const DelayConsts& DC, void* st, uint8_t* act, const uint32_t* qids, KadRes* res,
                           uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
                           uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                          unsigned long long* done_count, unsigned long long* active_count, hipStream_t s)
+                          unsigned long long* done_count, unsigned long long* active_count, StageBuf& stage,
+                          hipStream_t s)
 {
     if (!kad_params_supported(P, t) || P.numSiblings != 1) return hipErrorNotSupported;
     if (nlook == 0) return hipSuccess;
+    if (nsh < 1 || nsh > MAXSHARDS) return hipErrorInvalidValue;
     const KadView V = kad_make_view(t, xy, n);
     KadLC LC = kad_make_lc(P, t);
     kad_lc_sizes(LC, DC, n);
+    const int A = LC.alpha;
+    // stage: a request per pending-call slot, a done record per lookup, and their tags
+    const uint64_t ns = nlook * (uint64_t)A;
+    const size_t orq = 0, odn = orq + sizeof(ovs_kad_req) * ns, ort = odn + sizeof(ovs_done_rec) * nlook,
+                 olt = ort + ns;
+    hipError_t e = stage_ensure(stage, olt + nlook, s);
+    if (e != hipSuccess) return e;
+    uint8_t* sb = static_cast<uint8_t*>(stage.buf);
+    ovs_kad_req* rstage = reinterpret_cast<ovs_kad_req*>(sb + orq);
+    ovs_done_rec* dstage = reinterpret_cast<ovs_done_rec*>(sb + odn);
+    uint8_t* rtag = sb + ort;
+    uint8_t* ltag = sb + olt;
+    if ((e = hipMemsetAsync(rtag, 0xFF, ns + nlook, s)) != hipSuccess) return e;   // rtag and ltag are adjacent
 #define KSX(a, x) hipLaunchKernelGGL((k_kad_shard_step<a, x>), dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
-                                 (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, out, out_dest, out_cap, \
-                                 out_count, done, done_cap, done_count, active_count)
+                                 (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, rstage, rtag, dstage, ltag)
 #define KS(a) do { if (t.exact) KSX(a, true); else KSX(a, false); } while (0)
-    switch (LC.alpha) {
+    switch (A) {
     case 1: KS(1); break;
     case 2: KS(2); break;
     case 3: KS(3); break;
@@ -262,7 +270,23 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     }
 #undef KS
 #undef KSX
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // requests grouped by owner rank into out (labels in out_dest), after out_count's records
+    CPlan R{};
+    R.seg.src = reinterpret_cast<const uint8_t*>(rstage);
+    R.seg.src_stride = R.seg.rec_bytes = sizeof(ovs_kad_req);
+    R.seg.dst = reinterpret_cast<uint8_t*>(out); R.seg.lab = out_dest; R.seg.counter = out_count;
+    R.seg.cap = out_cap; R.seg.n = nsh; R.seg.chain = 1;
+    if ((e = compact_by_tag(rtag, ns, R, stage.cs, s)) != hipSuccess) return e;
+    // finished lookups appended to done; the still active ones counted
+    CPlan D{};
+    D.seg.n = 0;
+    D.nextra = 2;
+    D.extra[0].src = reinterpret_cast<const uint8_t*>(dstage);
+    D.extra[0].src_stride = D.extra[0].rec_bytes = sizeof(ovs_done_rec);
+    D.extra[0].dst = reinterpret_cast<uint8_t*>(done); D.extra[0].cap = done_cap; D.extra[0].counter = done_count;
+    D.extra[1].counter = active_count;
+    return compact_by_tag(ltag, nlook, D, stage.cs, s);
 }
 
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,

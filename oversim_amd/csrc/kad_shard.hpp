@@ -1,6 +1,7 @@
 // kad_shard.hpp -- multi-GPU Kademlia request/response kernels (internal).
 #pragma once
 #include "kad.hpp"
+#include "compact.hpp"
 
 namespace ovs {
 
@@ -21,7 +22,8 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
                           const DelayConsts& DC, void* st, uint8_t* act, const uint32_t* qids, KadRes* res,
                           uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
                           uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                          unsigned long long* done_count, unsigned long long* active_count, hipStream_t s);
+                          unsigned long long* done_count, unsigned long long* active_count, StageBuf& stage,
+                          hipStream_t s);
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
                            ovs_kad_resp* out, hipStream_t s);
 hipError_t kad_shard_deliver(const ovs_kad_resp* in, uint64_t n, KadRes* res, uint64_t nslots,

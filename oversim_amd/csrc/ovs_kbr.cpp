@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,8 @@ struct ovs_ctx {
     std::vector<uint32_t> h_fres;       // n * 160 resolved getFinger(pos)
     uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
+    std::vector<uint64_t> h_bounds;         // ... as last uploaded (uploaded again only on a change)
+    std::map<hipStream_t, StageBuf> stage;  // shard-step stage records per stream (cohorts)
     // kademlia
     KadTables kad{};
     // koorde (on the sorted ring in recs / xy)
@@ -330,6 +333,10 @@ void ovs_ctx_destroy(ovs_ctx* c)
     free_kad_shard(c);
     free_scratch(c);
     if (c->d_bounds) hipFree(c->d_bounds);
+    for (auto& kv : c->stage) {
+        hipStreamSynchronize(kv.first);
+        stage_free(kv.second);
+    }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -407,6 +414,18 @@ ovs_status ovs_shard_make_records(ovs_ctx* c, const ovs_key160* keys, const uint
     return OVS_OK;
 }
 
+// the arc boundaries on the device: uploaded (synchronously) only when they change, so a step
+// never waits for the host copy of a pageable buffer behind the work queued on its stream
+ovs_status upload_bounds(ovs_ctx* c, const uint64_t* lo, uint32_t nshards)
+{
+    if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
+    if (c->h_bounds.size() == nshards + 1 && std::equal(lo, lo + nshards + 1, c->h_bounds.begin())) return OVS_OK;
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(c->d_bounds, lo, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice));
+    c->h_bounds.assign(lo, lo + nshards + 1);
+    return OVS_OK;
+}
+
 ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out, uint64_t out_cap,
                           unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                           unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
@@ -430,13 +449,13 @@ ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, o
     if (me < 0) return fail(c, OVS_EINVAL, "this context's arc is not one of shard_lo's arcs");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;   // device-pointer call: NULL = the default stream
-    if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
-    HIPCHK(c, hipMemcpyAsync(c->d_bounds, M.lo, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice, s));
+    st = upload_bounds(c, M.lo, nshards);
+    if (st != OVS_OK) return st;
     LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes, c->P.routingType != 0};
     st = ensure_nodes(c, s);
     if (st != OVS_OK) return st;
     HIPCHK(c, launch_chord_shard_step(chord_view(c), delay_consts(c->P), LC, c->d_bounds, (int)nshards, me, in, n_in, out,
-                                      out_cap, out_count, done, done_cap, done_count, c->num_cu, s));
+                                      out_cap, out_count, done, done_cap, done_count, c->stage[s], c->num_cu, s));
     return OVS_OK;
 }
 
@@ -711,11 +730,11 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, 
     if (!mine) return fail(c, OVS_EINVAL, "this context's arc is not one of shard_lo's arcs");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
-    if (!c->d_bounds) HIPCHK(c, hipMalloc(&c->d_bounds, sizeof(uint64_t) * (MAXSHARDS + 1)));
-    HIPCHK(c, hipMemcpyAsync(c->d_bounds, lo_h, sizeof(uint64_t) * (nshards + 1), hipMemcpyHostToDevice, s));
+    ovs_status bst = upload_bounds(c, lo_h, nshards);
+    if (bst != OVS_OK) return bst;
     hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kqids,
                                   c->kres, c->knlook, c->d_bounds, (int)nshards, out, out_dest, out_cap, out_count,
-                                  done, done_cap, done_count, active_count, s);
+                                  done, done_cap, done_count, active_count, c->stage[s], s);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard step");
     return OVS_OK;
 }

@@ -223,25 +223,38 @@ class TorchExchange:
             return host.numpy()
         return wait
 
+    # rows per point-to-point message: a big all-to-allv goes out in pieces of at most 256 MB
+    # (both sides cut a transfer identically, and messages between two ranks match in order)
+    CHUNK_BYTES = 256 << 20
+
+    def _p2p(self, ops, t, peer, send: bool):
+        dist = self.dist
+        step = max(1, self.CHUNK_BYTES // max(1, t.shape[1] if t.dim() > 1 else 1))
+        for a in range(0, t.shape[0], step):
+            ops.append(dist.P2POp(dist.isend if send else dist.irecv, t[a:a + step], peer, group=self.group))
+
+    def _run(self, ops):
+        if ops:
+            for w in self.dist.batch_isend_irecv(ops):
+                w.wait()
+
     def segments(self, segs, scl, rcl, row_bytes: int):
         """all-to-allv of fixed-size records from per-destination segments (segs[d][:scl[d]])
         into one receive buffer ordered by source rank: grouped point-to-point sends out of
-        the segments, so nothing is packed first."""
-        torch, dist = self.torch, self.dist
+        the segments, so nothing is packed first; this rank's own share is a device copy."""
+        torch = self.torch
         recv = torch.empty((sum(rcl), row_bytes), dtype=torch.uint8, device=self.comm_dev)
         ops, off = [], 0
         for r in range(self.world):
             if rcl[r] and r != self.rank:
-                ops.append(dist.P2POp(dist.irecv, recv[off:off + rcl[r]], r, group=self.group))
+                self._p2p(ops, recv[off:off + rcl[r]], r, send=False)
             elif rcl[r]:
                 recv[off:off + rcl[r]].copy_(segs[r][:rcl[r]])
             off += rcl[r]
         for d in range(self.world):
             if scl[d] and d != self.rank:
-                ops.append(dist.P2POp(dist.isend, segs[d][:scl[d]].to(self.comm_dev), d, group=self.group))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+                self._p2p(ops, segs[d][:scl[d]].to(self.comm_dev), d, send=True)
+        self._run(ops)
         return recv
 
     def counts(self, send_counts):
@@ -253,10 +266,25 @@ class TorchExchange:
         return sc.tolist(), rc.tolist()
 
     def records(self, send, scl, rcl):
-        """all-to-allv of rows of `send` (uint8, one record per row) with explicit splits."""
-        torch, dist = self.torch, self.dist
+        """all-to-allv of rows of `send` (uint8, one record per row, grouped by destination rank)
+        with explicit splits: point-to-point pieces to the other ranks, a device copy of this
+        rank's own share (RCCL's all_to_all_single lost records at world size 1 beyond ~1 GB)."""
+        torch = self.torch
+        send = send.to(self.comm_dev)
         recv = torch.empty((sum(rcl), send.shape[1]), dtype=torch.uint8, device=self.comm_dev)
-        dist.all_to_all_single(recv, send.to(self.comm_dev), rcl, scl, group=self.group)
+        ops = []
+        so = np.concatenate([[0], np.cumsum(scl)]).astype(np.int64)
+        ro = np.concatenate([[0], np.cumsum(rcl)]).astype(np.int64)
+        for r in range(self.world):
+            if r == self.rank:
+                if rcl[r]:
+                    recv[ro[r]:ro[r + 1]].copy_(send[so[r]:so[r + 1]])
+                continue
+            if rcl[r]:
+                self._p2p(ops, recv[ro[r]:ro[r + 1]], r, send=False)
+            if scl[r]:
+                self._p2p(ops, send[so[r]:so[r + 1]], r, send=True)
+        self._run(ops)
         return recv
 
     def total(self, x: int) -> int:
@@ -272,14 +300,16 @@ class TorchExchange:
 
 
 def group_by_dest(out, dest, world: int):
-    """Stable grouping of an outbox by destination rank (Kademlia request path)."""
+    """The outbox grouped by destination rank (stable) and its per-destination counts.
+    ovs_kad_shard_step already writes it grouped, which costs one ordered-check here."""
     import torch
     if out.shape[0] == 0:
         return out, torch.zeros(world, dtype=torch.int64, device=out.device)
     d = dest.to(torch.int64)
-    order = torch.argsort(d, stable=True)
-    counts = torch.bincount(d, minlength=world)
-    return out.index_select(0, order), counts
+    if d.shape[0] > 1 and not bool((d[1:] >= d[:-1]).all()):
+        order = torch.argsort(d, stable=True)
+        out, d = out.index_select(0, order), d.index_select(0, order)
+    return out, torch.bincount(d, minlength=world)
 
 
 def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 10_000, cohorts: int = 2,
@@ -480,7 +510,7 @@ class KadShardStepper:
         return self.done[:k]
 
 
-def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 100_000):
+def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 5_000):
     """Route this rank's Kademlia lookups; 2 all-to-allv per round (requests, responses)."""
     stepper.begin(keys_t, src_t, qid_base)
     rounds = 0
@@ -496,7 +526,8 @@ def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_round
         back = exchange.records(resps, rcl, scl)          # reverse splits: back to the requesters
         stepper.deliver(back.to(stepper.dev))
         if rounds > max_rounds:
-            raise RuntimeError("sharded Kademlia routing did not terminate")
+            raise RuntimeError(f"sharded Kademlia routing did not terminate: {active} lookups active, "
+                               f"{sum(scl)} requests sent, {sum(rcl)} received in round {rounds}")
     return stepper.finished(), rounds
 
 

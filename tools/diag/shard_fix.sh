@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/r02x
+export OVS_SKIP_BUILD=1 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29661
+chk() { case $1 in 124|134|137|139) exit $1;; esac; }
+timeout -k 10 150 python tools/diag/chord_shard_speed.py > gpurun_out/r02x/chord.log 2>&1; rc=$?; echo "chord $rc"; tail -n 9 gpurun_out/r02x/chord.log; chk $rc
+timeout -k 10 150 python tools/diag/kad_shard_scale.py --nodes 4194304 --lookups 4000000 --mode nccl > gpurun_out/r02x/kad.log 2>&1; rc=$?; echo "kad $rc"; tail -n 3 gpurun_out/r02x/kad.log; chk $rc
