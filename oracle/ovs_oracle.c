@@ -1238,7 +1238,7 @@ int64_t orc_delay_ns(const orc_net* net, uint32_t a, uint32_t b, int32_t bytes)
 /*    no verify/majority siblings, failedNodeRpcs = false).              */
 /* ===================================================================== */
 #define MAXRPC 256
-#define MAXNH 64
+#define MAXNH 128
 
 typedef struct { uint32_t handle; int alreadyUsed; } LEntry;
 
@@ -1261,7 +1261,7 @@ typedef struct {
     /* lookup */
     int finished, success, running;
     int64_t startTime, now, txFinished;
-    uint32_t siblings[16]; int nsiblings;
+    uint32_t siblings[64]; int nsiblings;
     uint32_t* visited; int nvisited, capVisited;
     uint32_t dead[MAXRPC]; int ndead;
     int finishedPaths, successfulPaths, minHops;
@@ -1276,6 +1276,11 @@ typedef struct {
     /* Koorde: the findNodeExt the next FindNodeCalls carry (sendRpc's argument) */
     KExt ext; int extPresent;
     int broken;             /* a findNode threw (cRuntimeError in the reference): status BROKEN */
+    /* EXHAUSTIVE_ITERATIVE_ROUTING (Kademlia bucket / sibling refresh): R = config.redundantNodes
+     * of this lookup (the refresh sets it to bucketRefreshNodes / siblingRefreshNodes,
+     * Kademlia.cc:1606-1611, 1660-1665), nextHops holds 2R (IterativeLookup.cc:770-778) */
+    int exh, R, nhCap;
+    int64_t* rtts;          /* exhaustive: RTT of every accepted response (hop order) */
 } Lookup;
 
 static int lk_getVisited(Lookup* L, uint32_t n)
@@ -1320,7 +1325,7 @@ static int lv_compare(Lookup* L, uint32_t a, uint32_t b)
 /* LookupVector::add (BaseKeySortedVector::add with LookupEntry, cap = redundantNodes) */
 static int lv_add(Lookup* L, uint32_t h)
 {
-    int maxSize = L->net->p.lookupRedundantNodes;
+    int maxSize = L->nhCap;
     if (!(L->nnh != maxSize || lv_compare(L, h, L->nh[L->nnh - 1].handle) <= 0)) return -1;
     int pos = -1, i;
     if (L->nnh != 0) {
@@ -1355,7 +1360,7 @@ static void lk_addSibling(Lookup* L, uint32_t h)                                
         if (EQ(&L->net->ids[h], &L->key)) { L->siblings[0] = h; L->nsiblings = 1; }
         return;
     }
-    if (L->nsiblings < cap) L->siblings[L->nsiblings++] = h;   /* cap <= 16 (check_params, orc_lookup_batch) */
+    if (L->nsiblings < cap) L->siblings[L->nsiblings++] = h;   /* cap <= 64 (check_params, orc_lookup_batch, orc_kad_exhaustive_batch) */
 }
 
 /* IterativeLookup::sendRpc (656-689) + BaseRpc::sendRpcCall timeout (BaseRpc.cc:173-253) */
@@ -1386,9 +1391,9 @@ static void lk_sendRpc(Lookup* L, uint32_t handle, int rpcId)
                 r->extOut.routeKey.isUnspec = 1; r->extOut.step = 1;
             }
             if (koorde_findNode(L->net, handle, &L->key, &r->extOut, &res) < 0) { L->broken = 1; res.size = 0; }
-        } else
-            ov_findNode(L->net, handle, &L->key, p->lookupRedundantNodes, L->numSiblings, &res);
-        sflag = ov_isSiblingFor(L->net, handle, handle, &L->key, L->numSiblings, &err);
+        } else   /* findNodeRpc: an exhaustive call asks findNode with numSiblings -1 (BaseOverlay.cc:1857-1859) */
+            ov_findNode(L->net, handle, &L->key, L->R, L->exh ? -1 : L->numSiblings, &res);
+        sflag = L->exh ? 0 : ov_isSiblingFor(L->net, handle, handle, &L->key, L->numSiblings, &err);
         (void)sflag;
         int64_t respTx = 0;   /* responder's tx queue idle */
         int64_t d2 = calc_delay(L->net, handle, L->S, p->respBaseBytes + p->respPerNodeBytes * res.size, tArr, &respTx);
@@ -1407,7 +1412,7 @@ static void path_sendRpc(Lookup* L, int num)                                    
     if (L->hopCountMax && (L->hops >= L->hopCountMax)) { L->pfinished = 1; L->psuccess = 0; return; }
     if (p->lookupStrictParallelRpcs) num = num < (p->lookupParallelRpcs - L->pendingRpcs) ? num : (p->lookupParallelRpcs - L->pendingRpcs);
     if ((num == 0) && (L->pendingRpcs == 0) && !p->lookupFinishOnFirstUnchanged) num = p->lookupParallelRpcs;
-    for (int i = 0; num > 0 && i < p->lookupRedundantNodes; i++) {
+    for (int i = 0; num > 0 && i < L->R; i++) {
         LEntry* it = NULL;
         for (int q = 0; q < L->nnh; ++q) {                                       /* getNextEntry 1172-1182 */
             if (L->nh[q].alreadyUsed || lk_getDead(L, L->nh[q].handle)) continue;
@@ -1421,7 +1426,14 @@ static void path_sendRpc(Lookup* L, int num)                                    
         }
         it->alreadyUsed = 1;
     }
-    if (L->pendingRpcs == 0) { L->psuccess = 0; L->pfinished = 1; }
+    if (L->pendingRpcs == 0) {
+        if (L->exh) {   /* exhaustive lookups are always successful: siblings = nextHops[0..R) (1147-1156) */
+            for (int q = 0; q < L->R && q < L->nnh; ++q) lk_addSibling(L, L->nh[q].handle);
+            L->psuccess = 1;
+        } else
+            L->psuccess = 0;
+        L->pfinished = 1;
+    }
 }
 
 static void path_sendNewRpcAfterTimeout(Lookup* L)                               /* 923-933 */
@@ -1430,9 +1442,17 @@ static void path_sendNewRpcAfterTimeout(Lookup* L)                              
     else if (L->pendingRpcs == 0) path_sendRpc(L, L->net->p.lookupParallelRpcs);
 }
 
-static void path_handleTimeout(Lookup* L)                                        /* 935-1023 */
+static void path_handleTimeout(Lookup* L, uint32_t dest)                         /* 935-1023 */
 {
     if (L->pfinished) return;
+    if (L->exh && lk_getDead(L, dest)) {   /* exhaustive: dead nodes leave nextHops (948-957) */
+        for (int q = 0; q < L->nnh; ++q)
+            if (L->nh[q].handle == dest) {
+                memmove(&L->nh[q], &L->nh[q + 1], sizeof(LEntry) * (size_t)(L->nnh - q - 1));
+                L->nnh--;
+                break;
+            }
+    }
     L->pendingRpcs--;
     if (L->now > L->startTime + simtime(L->net->p.lookupTimeout, L->net->p.simtimeRound)) {
         L->pfinished = 1; L->psuccess = 0; return;
@@ -1447,7 +1467,8 @@ static int path_accepts(Lookup* L, int rpcId)                                   
     return rpcId == L->step;
 }
 
-static void path_handleResponse(Lookup* L, uint32_t source, const NVec* closest, int siblingsFlag) /* 803-921 */
+static void path_handleResponse(Lookup* L, uint32_t source, const NVec* closest, int siblingsFlag,
+                                int64_t rtt)                                     /* 803-921 */
 {
     const orc_params* p = &L->net->p;
     if (L->pfinished) return;
@@ -1455,6 +1476,7 @@ static void path_handleResponse(Lookup* L, uint32_t source, const NVec* closest,
     if (source != L->S) {
         L->hops++;
         if (L->hopseq && L->nhop < L->hopCountMax) L->hopseq[L->nhop] = source;
+        if (L->rtts && L->nhop < L->hopCountMax) L->rtts[L->nhop] = rtt;
         L->nhop++;
     }
     lk_setVisited(L, source);
@@ -1465,15 +1487,15 @@ static void path_handleResponse(Lookup* L, uint32_t source, const NVec* closest,
     for (int i = 0; i < closest->size; i++) {
         uint32_t h = closest->v[i];
         int pos = path_add(L, h);
-        if ((pos >= 0) && (pos < p->lookupRedundantNodes)) numNewRpcs++;
+        if ((pos >= 0) && (pos < L->R)) numNewRpcs++;
         if ((L->numSiblings == 0) && EQ(&L->net->ids[h], &L->key)) {
             lk_addSibling(L, h);
             L->pfinished = 1; L->psuccess = 1; return;
-        } else if (L->numSiblings != 0 && siblingsFlag) {
+        } else if (L->numSiblings != 0 && !L->exh && siblingsFlag) {
             lk_addSibling(L, h);
         }
     }
-    if (siblingsFlag && closest->size != 0 && L->numSiblings != 0) { L->pfinished = 1; L->psuccess = 1; return; }
+    if (!L->exh && siblingsFlag && closest->size != 0 && L->numSiblings != 0) { L->pfinished = 1; L->psuccess = 1; return; }
     if ((numNewRpcs == 0) && p->lookupNewRpcOnEveryResponse) numNewRpcs = 1;
     path_sendRpc(L, numNewRpcs < p->lookupParallelRpcs ? numNewRpcs : p->lookupParallelRpcs);
 }
@@ -1512,12 +1534,17 @@ static int lk_checkStop(Lookup* L)
  * built by SendToKeyListener::lookupFinished (BaseOverlay.cc:1272-1300) and sibs receives the
  * sibling vector (numSiblings slots, NONE padded). */
 static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out,
-                       uint32_t* hopseq, uint32_t* rpcsOut, int numSiblings, orc_lookup_out* lout, uint32_t* sibs)
+                       uint32_t* hopseq, uint32_t* rpcsOut, int numSiblings, orc_lookup_out* lout, uint32_t* sibs,
+                       int exhR, int64_t* rtts)
 {
     const orc_params* p = &net->p;
     Lookup* L = (Lookup*)calloc(1, sizeof(Lookup));
     L->net = net; L->key = *key; L->S = S;
     L->numSiblings = lout ? numSiblings : p->numSiblings; L->hopCountMax = p->hopCountMax;
+    L->exh = exhR > 0;
+    L->R = L->exh ? exhR : p->lookupRedundantNodes;
+    L->nhCap = L->exh ? 2 * exhR : p->lookupRedundantNodes;
+    L->rtts = rtts;
     L->hopseq = hopseq;
     L->minHops = 0x7fffffff;
     L->running = 1; L->startTime = 0; L->now = 0; L->txFinished = 0;
@@ -1530,11 +1557,11 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
         L->ext.routeKey.isUnspec = 1; L->ext.step = 1; L->extPresent = 1;
         if (koorde_findNode(net, S, key, &L->ext, &nextHops) < 0) { L->broken = 1; nextHops.size = 0; }
     } else
-        ov_findNode(net, S, key, ov_maxRedundant(net), L->numSiblings, &nextHops);
+        ov_findNode(net, S, key, ov_maxRedundant(net), L->exh ? -1 : L->numSiblings, &nextHops);
     lk_setVisited(L, S);
     if (nextHops.size == 0) {
         L->finished = 1; L->success = 0;
-    } else if (L->numSiblings != 0 && ov_isSiblingFor(net, S, S, key, L->numSiblings, &err)) {
+    } else if (L->numSiblings != 0 && !L->exh && ov_isSiblingFor(net, S, S, key, L->numSiblings, &err)) {
         for (int i = 0; i < nextHops.size; i++) lk_addSibling(L, nextHops.v[i]);
         L->success = L->finished = 1;
     }
@@ -1569,7 +1596,7 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
             for (int q = 0; q < r.nInfo; ++q) {
                 if (L->pfinished) continue;
                 L->ext = r.extIn; L->extPresent = r.extInPresent;   /* the timed-out call's extension (965-969) */
-                path_handleTimeout(L);
+                path_handleTimeout(L, r.node);
                 lk_countFinished(L);
             }
         } else {                             /* handleRpcResponse 488-585 */
@@ -1579,18 +1606,19 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
                 if (!r.extInPresent) { memset(&e.routeKey, 0, sizeof e.routeKey); e.routeKey.isUnspec = 1; e.step = 1; }
                 if (koorde_findNode(net, r.node, key, &e, &res) < 0) res.size = 0;   /* BROKEN was set at send */
             } else
-                ov_findNode(net, r.node, key, p->lookupRedundantNodes, L->numSiblings, &res);  /* BaseOverlay.cc:1857-1871 */
-            sflag = ov_isSiblingFor(net, r.node, r.node, key, L->numSiblings, &err2);
+                ov_findNode(net, r.node, key, L->R, L->exh ? -1 : L->numSiblings, &res);  /* BaseOverlay.cc:1857-1871 */
+            sflag = L->exh ? 0 : ov_isSiblingFor(net, r.node, r.node, key, L->numSiblings, &err2);
             int rpcHandled = 0;
             for (int q = 0; q < r.nInfo; ++q) {
                 if (L->pfinished) continue;
-                if (!rpcHandled && (path_accepts(L, r.vrpcId[q]) || (sflag && p->lookupAcceptLateSiblings))) {
+                if (!rpcHandled && (path_accepts(L, r.vrpcId[q]) || L->exh || (sflag && p->lookupAcceptLateSiblings))) {
                     L->ext = r.extOut; L->extPresent = 1;            /* the response's extension (908-911) */
-                    path_handleResponse(L, r.node, &res, sflag);
+                    path_handleResponse(L, r.node, &res, sflag,
+                                        bt - (r.tTimeout - simtime(p->rpcUdpTimeout, p->simtimeRound)));
                     rpcHandled = 1;
                 } else {
                     L->extPresent = 0;                               /* handleTimeout(NULL, ...): no extension */
-                    path_handleTimeout(L);
+                    path_handleTimeout(L, r.node);
                 }
                 lk_countFinished(L);
             }
@@ -1629,6 +1657,7 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
         else if (L->hopCountMax && L->hops >= L->hopCountMax) lout->status = 3;
         else lout->status = 4;
         for (int i = 0; i < numSiblings; ++i) sibs[i] = (valid && i < L->nsiblings) ? L->siblings[i] : NONE;
+        if (rpcsOut) *rpcsOut = L->rpcsSent;
         free(L->visited);
         free(L);
         return;
@@ -1731,7 +1760,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
         OKey k = ok_from(&keys[i]);
         if (net->p.routingType == 0)
             run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
-                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL);
+                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL, 0, NULL);
         else {
             run_recursive(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL);
             if (rpcs_out) rpcs_out[i] = 0;     /* no FindNodeCalls in recursive routing */
@@ -1757,10 +1786,73 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         OKey k = ok_from(&keys[i]);
         orc_route_out dummy;
-        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings);
+        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings, 0, NULL);
     }
     (void)nthreads;
     return g_cap_fail ? -1 : numSiblings;
+}
+
+/* ======================================================================== */
+/* Kademlia refresh lookups (Kademlia::handleBucketRefreshTimerExpired,      */
+/* Kademlia.cc:1591-1686, exhaustiveRefresh = true, iterative routing).      */
+/* ======================================================================== */
+int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int R,
+                             orc_lookup_out* out, uint32_t* siblings, uint32_t* responders, int64_t* rtts,
+                             uint32_t* rpcs, int nthreads)
+{
+    if (net->type != NET_KAD) { set_err("exhaustive refresh lookups: Kademlia only"); return -1; }
+    if (R < 1 || R > 64) { set_err("redundantNodes of a refresh lookup must be 1..64"); return -1; }
+    if (net->p.routingType != 0) { set_err("exhaustive-iterative: iterative routing only"); return -1; }
+    const int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
+    if (responders) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) responders[i] = NONE;
+    if (rtts) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) rtts[i] = -1;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        OKey k = ok_from(&keys[i]);
+        orc_route_out dummy;
+        /* lookup(key, numSiblings = R, ...) with config.redundantNodes = R (1606-1610, 1660-1664) */
+        run_lookup(net, &k, src[i], &dummy, responders ? responders + (size_t)i * hcm : NULL,
+                   rpcs ? &rpcs[i] : NULL, R, &out[i], siblings + (size_t)i * R, R,
+                   rtts ? rtts + (size_t)i * hcm : NULL);
+    }
+    (void)nthreads;
+    return g_cap_fail ? -1 : R;
+}
+
+uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
+                              orc_key* keys, uint32_t* src, uint64_t cap)
+{
+    uint64_t cnt = 0;
+    if (net->type != NET_KAD) { set_err("bucket refresh: Kademlia only"); return ORC_FAIL; }
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        KadTab T = kad_tab(net, v);
+        if (T.nsib == 0) continue;                       /* if (siblingTable->size()) (1632) */
+        /* siblingTable->front(): the XOR-closest sibling */
+        OKey best = ok_xor(net->ids[v], &net->ids[T.sib[0]]);
+        for (int q = 1; q < T.nsib; ++q) {
+            OKey d = ok_xor(net->ids[v], &net->ids[T.sib[q]]);
+            if (ok_cmp(&d, &best) < 0) best = d;
+        }
+        /* diff = L - b*(sharedPrefixLength(front, b) + 1) = msb(self ^ front) for b = 1 (1636-1637) */
+        const int spl = 159 - ok_log2(&best);
+        const int diff = 160 - (spl + 1);
+        for (int i = 159; i >= diff; --i) {             /* index = i for b = 1 (1639-1642) */
+            if (stale && !((stale[j * 5 + (uint64_t)(i >> 5)] >> (i & 31)) & 1u)) continue;
+            if (cnt < cap) {
+                OKey key = net->ids[v];                  /* thisNode.key ^ (OverlayKey(1) << i) (1647-1648) */
+                OKey bit = ok_pow2((uint32_t)i);
+                key = ok_xor(key, &bit);
+                ok_to(&key, &keys[cnt]);
+                src[cnt] = v;
+            }
+            ++cnt;
+        }
+    }
+    return cnt;
 }
 
 /* ======================================================================== */

@@ -163,6 +163,21 @@ typedef struct {
 int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int numSiblings,
                      orc_lookup_out* out, uint32_t* siblings, int nthreads);
 
+/* Exhaustive-iterative Kademlia lookups (the bucket / sibling refresh of Kademlia.cc:1591-1686 with
+ * exhaustiveRefresh): lookup i of keys[i] from src[i] with numSiblings = config.redundantNodes = R.
+ * out/siblings as orc_lookup_batch (siblings = n*R); responders / rtts (may be NULL) = n*hopCountMax
+ * accepted responders in order and their RTTs in ns (NONE / -1 padded); rpcs (may be NULL) = n
+ * FindNodeCall counts.  Returns R, -1 on error. */
+int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int R,
+                             orc_lookup_out* out, uint32_t* siblings, uint32_t* responders, int64_t* rtts,
+                             uint32_t* rpcs, int nthreads);
+/* The bucket-refresh keys of Kademlia::handleBucketRefreshTimerExpired (Kademlia.cc:1631-1676, b = 1)
+ * for nodes[0..m): self ^ 2^i for i = 159 .. msb(self ^ closest sibling) where bit i of the node's
+ * 160-bit stale mask is set (stale = m*5 words, NULL = every bucket stale).  Writes up to cap
+ * (key, src) pairs, returns how many there are (ORC_FAIL on error). */
+uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
+                              orc_key* keys, uint32_t* src, uint64_t cap);
+
 /* One synchronous fixfingers round for nodes[0..m) (Chord.cc:845-875, 1228-1270): trivial
  * fingers removed, then lookups of n + 2^i routed over the tables, then finger i := result.
  * Explicit or converged networks.  Returns total hops; *out_ok successful lookups,

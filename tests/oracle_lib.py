@@ -92,6 +92,8 @@ def lib() -> C.CDLL:
             ("orc_kbrtest_stats", [vp, vp, vp, vp, u64, C.c_double, C.c_int, i32, vp], None),
             ("orc_chord_fix_fingers", [vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.c_int], u64),
             ("orc_lookup_batch", [vp, vp, vp, u64, C.c_int, vp, vp, C.c_int], C.c_int),
+            ("orc_kad_exhaustive_batch", [vp, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp, C.c_int], C.c_int),
+            ("orc_kad_refresh_keys", [vp, vp, u64, vp, vp, vp, u64], u64),
             ("orc_kbrtest_lookup_stats", [vp, vp, vp, C.c_int, vp, vp, u64, C.c_double, C.c_int, C.c_double, vp],
              None),
         ]:
@@ -228,6 +230,42 @@ class OracleNet:
         res = {f: out[f].copy() for f in LOOKUP_DTYPE.names}
         res["siblings"] = sib
         return res
+
+    def exhaustive(self, keys, src, R: int, record=True, nthreads=0) -> dict:
+        """Exhaustive-iterative refresh lookups (orc_kad_exhaustive_batch) with redundantNodes = R."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        H = max(self.params.hopCountMax, 1)
+        out = np.empty(n, dtype=LOOKUP_DTYPE)
+        sib = np.empty((n, R), dtype=np.uint32)
+        resp = np.empty((n, H), dtype=np.uint32) if record else None
+        rtt = np.empty((n, H), dtype=np.int64) if record else None
+        rpcs = np.empty(n, dtype=np.uint32)
+        r = lib().orc_kad_exhaustive_batch(self._h, _p(keys), _p(src), n, R, _p(out), _p(sib), _p(resp), _p(rtt),
+                                           _p(rpcs), nthreads)
+        if r < 0:
+            raise ValueError(lib().orc_last_error().decode())
+        res = {f: out[f].copy() for f in LOOKUP_DTYPE.names}
+        res["siblings"] = sib
+        res["rpcs"] = rpcs
+        if record:
+            res["responders"] = resp
+            res["rtt_ns"] = rtt
+        return res
+
+    def refresh_keys(self, nodes, stale=None):
+        """Bucket-refresh (key, src) pairs of Kademlia::handleBucketRefreshTimerExpired."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        st = None if stale is None else np.ascontiguousarray(stale, dtype=np.uint32)
+        L = lib()
+        cnt = L.orc_kad_refresh_keys(self._h, _p(nodes), len(nodes), _p(st), None, None, 0)
+        if cnt == ORC_FAIL:
+            raise ValueError(L.orc_last_error().decode())
+        keys = np.zeros((max(cnt, 1), 5), dtype=np.uint32)
+        src = np.zeros(max(cnt, 1), dtype=np.uint32)
+        L.orc_kad_refresh_keys(self._h, _p(nodes), len(nodes), _p(st), _p(keys), _p(src), cnt)
+        return keys[:cnt], src[:cnt]
 
     def kbrtest_stats(self, result: dict, keys, src, measured_time_s: float, lookupNodeIds: bool = True,
                       testMsgSize: int = 100) -> dict:

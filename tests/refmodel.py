@@ -402,7 +402,11 @@ class KadTables:
         return any(self.ids[x] == self.ids[c] for x in res)
 
     def find_node(self, c, key, num_redundant=8, num_siblings=1):
-        size = (num_siblings or 1) if self.is_sibling_for(c, key, num_siblings) else num_redundant
+        # numSiblings < 0: an exhaustive-iterative call, resultSize = numRedundantNodes (Kademlia.cc:1125-1127)
+        if num_siblings < 0:
+            size = num_redundant
+        else:
+            size = (num_siblings or 1) if self.is_sibling_for(c, key, num_siblings) else num_redundant
         res = []
         sib = self.siblings(c)
         if not sib:
@@ -481,7 +485,7 @@ class KadLookupSim:
 
     # LookupVector::add (BaseKeySortedVector::add, NodeVector.h:432-512), entries [node, alreadyUsed]
     def _nh_add(self, h):
-        cap, nh = self.cfg["redundant"], self.nh
+        cap, nh = (2 * self.R if self.exh else self.R), self.nh
         if not self.cfg["merge"]:
             nh.append([h, False])
             return len(nh) - 1
@@ -515,7 +519,7 @@ class KadLookupSim:
         if num == 0 and self.pending == 0 and not c["first_unch"]:
             num = c["alpha"]
         i = 0
-        while num > 0 and i < c["redundant"]:
+        while num > 0 and i < self.R:
             i += 1
             it = next((e for e in self.nh if not e[1] and e[0] not in self.dead), None)
             if it is None:
@@ -526,7 +530,12 @@ class KadLookupSim:
                 self._lookup_send(it[0], self.step)
             it[1] = True
         if self.pending == 0:
-            self.psuccess, self.pfinished = False, True
+            if self.exh:   # exhaustive lookups always succeed: siblings = the first R next hops (1147-1156)
+                for e in self.nh[: self.R]:
+                    self._add_sibling(e[0])
+                self.psuccess, self.pfinished = True, True
+            else:
+                self.psuccess, self.pfinished = False, True
 
     def _lookup_send(self, h, rpc_id):
         """IterativeLookup::sendRpc (656-689) + BaseRpc::sendRpcCall: timeout first, then the call."""
@@ -538,6 +547,7 @@ class KadLookupSim:
             self.live.add(h)
             self._schedule(self.now + self.rpc_to, "timeout", h)
             self._schedule(self.now, "call_udp", h)
+            self.sent_at[h] = self.now
         self.rpcs[h].append(rpc_id)
 
     def _count_finished(self):
@@ -547,10 +557,12 @@ class KadLookupSim:
             self.min_hops = min(self.min_hops, self.hops)
             self.successful_paths += 1 if self.psuccess else 0
 
-    def _path_timeout(self):
+    def _path_timeout(self, dest=None):
         """IterativePathLookup::handleTimeout (935-1023), failedNodeRpcs = false."""
         if self.pfinished:
             return
+        if self.exh and dest in self.dead:   # exhaustive: a dead node leaves nextHops (948-957)
+            self.nh = [e for e in self.nh if e[0] != dest]
         self.pending -= 1
         if self.now > self.lk_to:
             self.pfinished, self.psuccess = True, False
@@ -570,6 +582,7 @@ class KadLookupSim:
         if src != self.S:
             self.hops += 1
             self.hop_seq.append(src)
+            self.rtts.append(self.now - self.sent_at[src])
         self.visited.add(src)
         self.step += 1
         self.pending -= 1
@@ -578,11 +591,11 @@ class KadLookupSim:
         new = 0
         for h in closest:
             pos = self._nh_add(h)
-            if 0 <= pos < self.cfg["redundant"]:
+            if 0 <= pos < self.R:
                 new += 1
-            if self.num_siblings and sib_flag:
+            if self.num_siblings and not self.exh and sib_flag:
                 self._add_sibling(h)
-        if sib_flag and closest and self.num_siblings:
+        if not self.exh and sib_flag and closest and self.num_siblings:
             self.pfinished, self.psuccess = True, True
             return
         if new == 0 and self.cfg["new_resp"]:
@@ -598,9 +611,16 @@ class KadLookupSim:
             return True
         return False
 
-    def run(self, key_words, S, num_siblings=1, lookup_call=False):
+    def run(self, key_words, S, num_siblings=1, lookup_call=False, exhaustive=0):
+        """exhaustive = R > 0: an EXHAUSTIVE_ITERATIVE_ROUTING lookup with config.redundantNodes = R and
+        numSiblings = R (Kademlia's bucket / sibling refresh, Kademlia.cc:1604-1611, 1658-1665)."""
         import heapq
         self.key = to_int(key_words)
+        self.exh = exhaustive
+        self.R = exhaustive if exhaustive else self.cfg["redundant"]
+        if exhaustive:
+            num_siblings, lookup_call = exhaustive, True
+        self.sent_at, self.rtts = {}, []
         self.S, self.num_siblings = S, num_siblings
         self.fes, self.ins, self.now, self.tx = [], 0, 0, {}
         self.nh, self.visited, self.dead, self.rpcs, self.live = [], {S}, set(), {}, set()
@@ -612,11 +632,11 @@ class KadLookupSim:
         self.min_hops, self.nsent = 1 << 30, 0
         T = self.T
         # IterativeLookup::start (133-244)
-        nxt = T.find_node(S, self.key, self.k, num_siblings)
+        nxt = T.find_node(S, self.key, self.k, -1 if self.exh else num_siblings)
         done = False
         if not nxt:
             self.finished, self.success, done = True, False, True
-        elif num_siblings and T.is_sibling_for(S, self.key, num_siblings):
+        elif num_siblings and not self.exh and T.is_sibling_for(S, self.key, num_siblings):
             for h in nxt:
                 self._add_sibling(h)
             self.finished = self.success = done = True
@@ -634,8 +654,9 @@ class KadLookupSim:
             elif kind == "call_app_at":       # responder UDP -> overlay (zero delay)
                 self._schedule(t, "call_rpc", h)
             elif kind == "call_rpc":          # findNodeRpc at the responder
-                res = T.find_node(h, self.key, self.cfg["redundant"], num_siblings)
-                flag = T.is_sibling_for(h, self.key, num_siblings)
+                # findNodeRpc: exhaustive calls ask findNode with numSiblings -1 and set no flag (1857-1871)
+                res = T.find_node(h, self.key, self.R, -1 if self.exh else num_siblings)
+                flag = False if self.exh else T.is_sibling_for(h, self.key, num_siblings)
                 resp_of[h] = (res, flag)
                 self._schedule(t, "resp_udp", h)
             elif kind == "resp_udp":          # responder UDP: response through its tx queue
@@ -655,11 +676,11 @@ class KadLookupSim:
                     if self.pfinished:
                         continue
                     acc = (self.cfg["use_all"] and self.cfg["merge"]) or rid == self.step
-                    if not handled and (acc or (flag and self.cfg["late"])):
+                    if not handled and (acc or self.exh or (flag and self.cfg["late"])):
                         self._path_response(h, res, flag)
                         handled = True
                     else:
-                        self._path_timeout()
+                        self._path_timeout(h)
                     self._count_finished()
                 done = self._check_stop()
             elif kind == "timeout":           # BaseRpc timeout -> handleRpcTimeout (588-654)
@@ -673,7 +694,7 @@ class KadLookupSim:
                 for _ in ids:
                     if self.pfinished:
                         continue
-                    self._path_timeout()
+                    self._path_timeout(h)
                     self._count_finished()
                 done = self._check_stop()
         if not done:
@@ -682,7 +703,8 @@ class KadLookupSim:
         hops = 0 if self.min_hops == 1 << 30 else self.min_hops
         if lookup_call:
             return dict(siblings=list(self.siblings) if valid else [], hops=hops, status=self._status(valid),
-                        is_valid=int(valid), latency_ns=self.now if valid else -1, rpcs=self.nsent)
+                        is_valid=int(valid), latency_ns=self.now if valid else -1, rpcs=self.nsent,
+                        responders=list(self.hop_seq), rtt_ns=list(self.rtts))
         if not valid or not self.siblings:
             return dict(responsible=0xFFFFFFFF, hops=hops, status=self._status(False), one_way_hops=0,
                         latency_ns=-1, hop_seq=self.hop_seq, rpcs=self.nsent)

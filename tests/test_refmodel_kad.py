@@ -90,3 +90,72 @@ def test_lookup_calls_agree(net, alpha, ns):
         assert int(r["latency_ns"][i]) == m["latency_ns"], i
         assert int(r["num_siblings"][i]) == len(m["siblings"]), i
         assert [int(x) for x in r["siblings"][i][: len(m["siblings"])]] == m["siblings"], i
+
+
+REFRESH_VARIANTS = {
+    "a3": dict(lookupParallelRpcs=3),
+    "a1": dict(lookupParallelRpcs=1),
+    "a3_loose": dict(lookupParallelRpcs=3, lookupStrictParallelRpcs=0),
+    # RPC timeouts: dead nodes leave nextHops (IterativeLookup.cc:948-957), evicted nodes re-enter
+    "a3_rpcto": dict(lookupParallelRpcs=3, rpcUdpTimeout=0.35),
+    "a3_rpcto_newto": dict(lookupParallelRpcs=3, rpcUdpTimeout=0.35, lookupNewRpcOnEveryTimeout=1),
+    "a2_lookupto": dict(lookupParallelRpcs=2, lookupTimeout=0.9),
+    "a3_hcm12": dict(lookupParallelRpcs=3, hopCountMax=12),
+}
+
+
+@pytest.mark.parametrize("name", list(REFRESH_VARIANTS))
+@pytest.mark.parametrize("R", [8, 40])
+def test_refresh_lookups_agree(net, name, R):
+    """Exhaustive-iterative refresh lookups (Kademlia.cc:1591-1686): the bucket refresh keys
+    (R = bucketRefreshNodes = 8) and the sibling refresh of the node's own key (R = 5s = 40)."""
+    p = kad_params(**REFRESH_VARIANTS[name])
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    nodes = np.arange(7, len(net.ids), 149, dtype=np.uint32)
+    if R == 8:
+        keys, src = o.refresh_keys(nodes)
+        keys, src = keys[::3], src[::3]
+    else:
+        keys, src = net.ids[nodes], nodes
+    r = o.exhaustive(keys, src, R)
+    statuses, lost = set(), False
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]), exhaustive=R)
+        assert int(r["is_valid"][i]) == m["is_valid"], (name, i)
+        assert int(r["status"][i]) == m["status"], (name, i)
+        assert int(r["hops"][i]) == m["hops"], (name, i)
+        assert int(r["rpcs"][i]) == m["rpcs"], (name, i)
+        assert int(r["latency_ns"][i]) == m["latency_ns"], (name, i)
+        assert int(r["num_siblings"][i]) == len(m["siblings"]), (name, i)
+        assert [int(x) for x in r["siblings"][i][: len(m["siblings"])]] == m["siblings"], (name, i)
+        H = len(m["responders"])
+        assert [int(x) for x in r["responders"][i][:H]] == m["responders"], (name, i)
+        assert [int(x) for x in r["rtt_ns"][i][:H]] == m["rtt_ns"], (name, i)
+        statuses.add(int(m["status"]))
+        lost |= m["rpcs"] > len(m["responders"])
+    if "rpcto" in name:   # exhaustive lookups succeed through dead nodes: timeouts show as lost calls
+        assert lost, f"{name}: the variant should time some FindNodeCalls out"
+    elif "to" in name or "hcm" in name:
+        assert statuses != {0}, f"{name}: the variant should exercise a failure path"
+
+
+def test_refresh_keys_follow_the_timer(net):
+    """handleBucketRefreshTimerExpired's keys: self ^ 2^i for i = 159 .. msb(self ^ closest
+    sibling), filtered by the stale mask."""
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params())
+    sib, _, _ = o.kad_tables()
+    ids = [refmodel.to_int(w) for w in net.ids]
+    nodes = np.array([0, 5, 700, len(ids) - 1], dtype=np.uint32)
+    keys, src = o.refresh_keys(nodes)
+    exp = []
+    for v in nodes:
+        front = min(ids[x] ^ ids[v] for x in sib[v] if x != 0xFFFFFFFF)
+        for i in range(159, front.bit_length() - 2, -1):
+            exp.append((int(v), ids[v] ^ (1 << i)))
+    assert [(int(s), refmodel.to_int(k)) for k, s in zip(keys, src)] == exp
+    stale = np.zeros((len(nodes), 5), dtype=np.uint32)
+    stale[:, 4] = 0x80000000            # only bucket 159
+    keys2, src2 = o.refresh_keys(nodes, stale)
+    assert list(src2) == list(nodes)
+    assert [refmodel.to_int(k) for k in keys2] == [ids[v] ^ (1 << 159) for v in nodes]
