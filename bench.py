@@ -17,6 +17,9 @@ Workloads (--workload, default C):
      1M node-ID lookups per GPU.  N > 1: independent replicas.
   K  Koorde, 2^20 nodes, 4M random-key lookups per GPU (not a BASELINE config:
      the Koorde routing rule).  N > 1: independent replicas.
+  R  Kademlia, 2^20 nodes, alpha=3: the bucket refresh (Kademlia.cc:1591-1686,
+     exhaustiveRefresh) of 2^16 nodes per GPU, ~1.1M exhaustive-iterative
+     lookups with bucketRefreshNodes = 8.  Replicas.
   E  Kademlia, 2^24 nodes, alpha=3, 4M random-key lookups per GPU.  N > 1: the
      ID space is cut into N arcs (prefixes), each GPU owns its arc's tables, and
      FindNodeCalls are exchanged as request/response all-to-allv rounds
@@ -66,7 +69,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["B", "C", "D", "E", "K"], default="C")
+    ap.add_argument("--workload", choices=["B", "C", "D", "E", "K", "R"], default="C")
     ap.add_argument("--nodes", type=int, default=None, help="override ring size (per GPU for C, total for D/E)")
     ap.add_argument("--lookups", type=int, default=None, help="override lookups per GPU per step")
     ap.add_argument("--routing", choices=["iterative", "semi-recursive"], default="iterative",
@@ -82,7 +85,8 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, routing_type: int = 0) -> dict:
+def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, routing_type: int = 0,
+                 refresh_R: int = 0) -> dict:
     """The oracle (CPU restatement, kind 'port', built -O3) on a bounded sample of the same workload,
     timed on all the host cores this job may use and on one core.  Populations too large for the
     oracle's stored tables (configs D, E) use its lazy tables (every table entry evaluated per
@@ -99,20 +103,25 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
         o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia"
                       else chord_params(routingType=routing_type), lazy=lazy)
 
+    def run(m, threads):
+        if refresh_R:
+            return o.exhaustive(keys[:m], src[:m], refresh_R, record=False, nthreads=threads)
+        return o.route(keys[:m], src[:m], record_hops=False, nthreads=threads)
+
     def timed(threads: int, budget_s: float):
         # calibrate on growing prefixes until one takes a quarter of the budget (a short probe
         # is dominated by thread start-up and would undersize the sample), then run the sample
         m = 2000
         while True:
             t = time.perf_counter()
-            o.route(keys[:m], src[:m], record_hops=False, nthreads=threads)
+            run(m, threads)
             dt = time.perf_counter() - t
             if dt >= 0.25 * budget_s or m >= len(keys):
                 break
             m = min(len(keys), m * max(2, int(0.25 * budget_s / max(dt, 1e-6))))
         m2 = int(min(len(keys), max(m, m * budget_s / max(dt, 1e-6))))
         t = time.perf_counter()
-        r = o.route(keys[:m2], src[:m2], record_hops=False, nthreads=threads)
+        r = run(m2, threads)
         dt = time.perf_counter() - t
         return int(r["hops"].astype(np.int64).sum()) / dt, m2 / dt, m2, dt
 
@@ -210,9 +219,11 @@ def main():
         wl["desc"] = wl["desc"].replace("iterative", "semi-recursive")
     stream = torch.cuda.Stream(device=dev)
     # Koorde runs replicas (its tables are not sharded); Kademlia shards unless OVS_KAD_REPLICAS=1
-    sharded = world > 1 and (kind == "chord" or (kind == "kademlia" and os.environ.get("OVS_KAD_REPLICAS") != "1"))
+    refresh = a.workload == "R"
+    sharded = world > 1 and (kind == "chord" or (kind == "kademlia" and not refresh and
+                                                 os.environ.get("OVS_KAD_REPLICAS") != "1"))
     # rehearsal knob: the sharded host path (collectives, cohorts) at N = 1
-    if os.environ.get("OVS_BENCH_SHARD") == "1" and kind != "koorde":
+    if os.environ.get("OVS_BENCH_SHARD") == "1" and kind != "koorde" and not refresh:
         sharded = True
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
@@ -256,10 +267,24 @@ def main():
             torch.cuda.synchronize()
             eng.kad_load_device(ids_t.data_ptr(), xy_t.data_ptr(), n_total)
             kname = "k_kad_route"
+        if refresh:
+            # this rank's share of the refresh round: every bucket refresh of its 2^16 nodes
+            nn = wl["refresh_nodes"]
+            nodes = ((np.arange(nn, dtype=np.int64) * (n_total // nn) + rank) % n_total).astype(np.uint32)
+            keys, src = eng.kad_refresh_keys(nodes)
+            m = len(keys)
+            dkeys = torch.from_numpy(keys.view(np.int32)).to(dev)
+            dsrc = torch.from_numpy(src.view(np.int32)).to(dev)
+            dsib = torch.empty((m, 8), dtype=torch.int32, device=dev)
+            kname = "k_kad_refresh"
         dout = torch.empty((m, 16), dtype=torch.uint8, device=dev)
         drpc = torch.empty(m, dtype=torch.int32, device=dev) if kind == "kademlia" else None
 
         def step():
+            if refresh:
+                eng.kad_refresh_device(dkeys.data_ptr(), dsrc.data_ptr(), m, 8, dout.data_ptr(), dsib.data_ptr(),
+                                       drpc.data_ptr(), stream.cuda_stream)
+                return
             eng.lookup_device(dkeys.data_ptr(), dsrc.data_ptr(), m, dout.data_ptr(), stream.cuda_stream,
                               rpcs_ptr=drpc.data_ptr() if drpc is not None else None)
 
@@ -333,13 +358,17 @@ def main():
             if ids is None:       # device-generated population (D, E): the oracle needs host copies
                 ids, xy = ids_t.cpu().numpy().view(np.uint32), xy_t.cpu().numpy()
                 keys, src = dkeys[:1 << 20].cpu().numpy().view(np.uint32), dsrc[:1 << 20].cpu().numpy().view(np.uint32)
-            cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type)
+            cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type,
+                               refresh_R=8 if refresh else 0)
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
                "hopCountMax": 50,
                "parallelism": ((f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)" if kind == "chord"
                                 else f"ID arcs over {world} GPUs, FindNodeCall request/response all-to-allv per round")
                                if sharded else ("replicas" if world > 1 else "1 GPU")),
                "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1)}
+        if refresh:
+            cfg.update({"refresh_nodes_per_gpu": wl["refresh_nodes"], "bucketRefreshNodes": 8,
+                        "routingType": "exhaustive-iterative"})
         if kind == "kademlia":
             cfg.update({"k": 8, "alpha": wl["alpha"], "rpcs_per_s": rpc_all * a.steps / wall_max,
                         "mean_rpcs": rpc_all / max(ok_all, 1)})

@@ -15,6 +15,7 @@
  *   AbstractLookup::lookup +       src/common/AbstractLookup.h, IterativeLookup.cc:695-723
  *   LookupListener::lookupFinished src/common/LookupListener.h, BaseOverlay.cc:1241-1307
  *   SimpleNodeEntry::calcDelay     src/underlay/simpleunderlay/SimpleNodeEntry.cc:155-195
+ *   Kademlia bucket refresh        src/overlay/kademlia/Kademlia.cc:1591-1686 (exhaustive lookups)
  *   .ini parameter binding         simulations/default.ini (same key names)
  *
  * Plain C: no C++ exceptions cross this boundary, no torch types.  Every call
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 4
+#define OVS_ABI_VERSION 5
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -247,6 +248,36 @@ typedef struct ovs_lookup_out {
 ovs_status  ovs_lookup_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
                              uint64_t n, int32_t num_siblings, ovs_lookup_out* out,
                              uint32_t* siblings, uint32_t flags, void* stream);
+
+/* Batched Kademlia refresh lookups (Kademlia::handleBucketRefreshTimerExpired,
+ * Kademlia.cc:1591-1686, exhaustiveRefresh = true, iterative routing):
+ * lookup i is createLookup(EXHAUSTIVE_ITERATIVE_ROUTING)->lookup(keys[i],
+ * R, hopCountMax) from node src[i] with config.redundantNodes = R
+ * (bucketRefreshNodes = k for a bucket refresh, siblingRefreshNodes = 5s for
+ * the sibling-table refresh of the node's own key; IterativeLookup.cc:
+ * 133-244, 488-585, 714-781, 803-921, 935-1170 with the exhaustive rules).
+ * out / siblings as ovs_lookup_batch (siblings = n*R, the lookup's result:
+ * nextHops[0..R) when it ran out of unqueried nodes).  responders (may be NULL)
+ * = n*hopCountMax node indices, every FindNodeResponse the lookup received in
+ * order -- the nodes Kademlia::handleRpcResponse routingAdd()s with their RTT
+ * (Kademlia.cc:1352-1420) -- 0xFFFFFFFF padded; rtt_ns (may be NULL) their
+ * RTTs, -1 padded; rpcs (may be NULL) = n FindNodeCall counts.  Requires
+ * lookupMerge, lookupStrictParallelRpcs, lookupParallelRpcs <= 4,
+ * 1 <= R <= 64, 1 <= hopCountMax.  Single-context networks. */
+ovs_status  ovs_kad_refresh_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                                  int32_t redundant_nodes, ovs_lookup_out* out, uint32_t* siblings,
+                                  uint32_t* responders, int64_t* rtt_ns, uint32_t* rpcs, uint32_t flags,
+                                  void* stream);
+/* The bucket-refresh lookups of nodes[0..m) (Kademlia.cc:1631-1676, b = 1):
+ * key self ^ 2^i from the node for i = 159 down to msb(self ^ closest sibling)
+ * where bit i of the node's stale mask is set -- stale = m*5 words (bit i of
+ * word i/32: bucket i is NULL or unused for minBucketRefreshInterval), NULL =
+ * every bucket.  Writes up to cap (keys, src) pairs in the reference's order
+ * and sets *count to how many there are (keys/src may be NULL with cap 0 to
+ * size the call).  nodes / stale / keys / src follow `flags`; *count is host. */
+ovs_status  ovs_kad_refresh_keys(ovs_ctx* ctx, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
+                                 ovs_key160* keys, uint32_t* src, uint64_t cap, uint64_t* count,
+                                 uint32_t flags, void* stream);
 
 /* Batched responder step: for each i, findNode(keys[i], numRedundantNodes,
  * numSiblings) evaluated at node[i] and the findNodeRpc siblings flag

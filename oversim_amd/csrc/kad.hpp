@@ -93,6 +93,15 @@ hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ov
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
                      ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st,
                      uint32_t* sibs = nullptr);
+// exhaustive-iterative refresh lookups (K2x, kad_refresh.hip); *capacity_error: a lookup ran past
+// the kernel's fixed capacities (more than 64 timed-out nodes)
+hipError_t kad_refresh(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
+                       int R, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_lookup_out* out,
+                       uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
+                       hipStream_t st, bool* capacity_error);
+// bucket-refresh keys of nodes[0..m) (device buffers); *total = how many (up to cap written)
+hipError_t kad_refresh_keys(const KadTables& t, uint32_t n, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
+                            K160* keys, uint32_t* src, uint64_t cap, uint64_t* total, hipStream_t st);
 hipError_t kad_find_node(const KadTables& t, uint32_t n, const ovs_params& P, const uint32_t* node, const K160* keys,
                          uint64_t nq, int numRedundant, int numSiblings, uint32_t* out_nodes, uint32_t max_out,
                          uint8_t* out_count, uint8_t* out_sib, hipStream_t st);

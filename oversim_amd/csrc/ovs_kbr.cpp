@@ -1044,6 +1044,121 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     return OVS_OK;
 }
 
+ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                                 int32_t R, ovs_lookup_out* out, uint32_t* siblings, uint32_t* responders,
+                                 int64_t* rtt_ns, uint32_t* rpcs, uint32_t flags, void* stream)
+{
+    if (!c || (n && (!keys || !src || !out || !siblings))) return OVS_EINVAL;
+    if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "refresh lookups: Kademlia only");
+    if (c->kad.lo != 0 || c->kad.hi != c->n)
+        return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: refresh lookups need the whole network");
+    if (R < 1 || R > 64) return fail(c, OVS_ENOTSUP, "refresh lookups implement redundantNodes 1..64");
+    const ovs_params& P = c->P;
+    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "refresh lookups: iterative routing (exhaustive-iterative)");
+    if (P.hopCountMax < 1) return fail(c, OVS_ENOTSUP, "refresh lookups need hopCountMax >= 1");
+    if (!P.lookupMerge || !P.lookupStrictParallelRpcs || P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > 4)
+        return fail(c, OVS_ENOTSUP, "refresh lookups implement lookupMerge, strictParallelRpcs, parallelRpcs 1..4");
+    if (P.lookupParallelPaths != 1 || P.lookupVerifySiblings || P.lookupMajoritySiblings || P.jitter != 0.0)
+        return fail(c, OVS_ENOTSUP, "parallelPaths 1, no verify/majority siblings, jitter 0");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;
+    if (n == 0) return OVS_OK;
+    if (!dev)
+        for (uint64_t i = 0; i < n; ++i)
+            if (src[i] >= c->n) return fail(c, OVS_EINVAL, "source index out of range");
+    const uint64_t H = (uint64_t)P.hopCountMax;
+    K160* dk = nullptr; uint32_t* ds = nullptr; ovs_lookup_out* dout = nullptr; uint32_t* dsib = nullptr;
+    uint32_t* dresp = nullptr; int64_t* drtt = nullptr; uint32_t* drpc = nullptr;
+    bool ok_k = false, ok_s = false;
+    ovs_status st = to_device(c, reinterpret_cast<const K160*>(keys), n, dev, &dk, &ok_k);
+    if (st != OVS_OK) return st;
+    st = to_device(c, src, n, dev, &ds, &ok_s);
+    if (st != OVS_OK) { if (ok_k) hipFree(dk); return st; }
+    // the responder list is the lookup's visited set: always present on the device
+    const bool own_resp = !dev || !responders, own_rtt = !dev && rtt_ns, own_rpc = !dev && rpcs;
+    auto cleanup = [&]() {
+        if (ok_k) hipFree(dk);
+        if (ok_s) hipFree(ds);
+        if (!dev) { hipFree(dout); hipFree(dsib); }
+        if (own_resp) hipFree(dresp);
+        if (own_rtt) hipFree(drtt);
+        if (own_rpc) hipFree(drpc);
+    };
+    if (!dev) {
+        HIPCHK(c, hipMalloc(&dout, sizeof(ovs_lookup_out) * n));
+        HIPCHK(c, hipMalloc(&dsib, sizeof(uint32_t) * n * R));
+    } else { dout = out; dsib = siblings; }
+    if (own_resp) HIPCHK(c, hipMalloc(&dresp, sizeof(uint32_t) * n * H));
+    else dresp = responders;
+    if (own_rtt) HIPCHK(c, hipMalloc(&drtt, sizeof(int64_t) * n * H));
+    else drtt = rtt_ns;
+    if (own_rpc) HIPCHK(c, hipMalloc(&drpc, sizeof(uint32_t) * n));
+    else drpc = rpcs;
+    bool cap_err = false;
+    const hipError_t e = kad_refresh(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), R, dk, ds, n, dout, dsib, dresp,
+                                     drtt, drpc, c->num_cu, s, &cap_err);
+    if (e != hipSuccess) { cleanup(); return hip_fail(c, e, "refresh lookup kernel"); }
+    if (cap_err) { cleanup(); return fail(c, OVS_ENOTSUP, "a refresh lookup exceeded the kernel's capacity (64 timed-out nodes)"); }
+    if (!dev) {
+        HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(ovs_lookup_out) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(siblings, dsib, sizeof(uint32_t) * n * R, hipMemcpyDeviceToHost, s));
+        if (responders) HIPCHK(c, hipMemcpyAsync(responders, dresp, sizeof(uint32_t) * n * H, hipMemcpyDeviceToHost, s));
+        if (rtt_ns) HIPCHK(c, hipMemcpyAsync(rtt_ns, drtt, sizeof(int64_t) * n * H, hipMemcpyDeviceToHost, s));
+        if (rpcs) HIPCHK(c, hipMemcpyAsync(rpcs, drpc, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    cleanup();
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_refresh_keys(ovs_ctx* c, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
+                                ovs_key160* keys, uint32_t* src, uint64_t cap, uint64_t* count, uint32_t flags,
+                                void* stream)
+{
+    if (!c || !count || (m && !nodes) || (cap && (!keys || !src))) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "bucket refresh: Kademlia network needed");
+    if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "bucket refresh needs the whole network");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;
+    *count = 0;
+    if (m == 0) return OVS_OK;
+    if (!dev)
+        for (uint64_t i = 0; i < m; ++i)
+            if (nodes[i] >= c->n) return fail(c, OVS_EINVAL, "node index out of range");
+    uint32_t* dn = nullptr; uint32_t* dst = nullptr; K160* dk = nullptr; uint32_t* dsrc = nullptr;
+    bool o1 = false, o2 = false;
+    ovs_status st = to_device(c, nodes, m, dev, &dn, &o1);
+    if (st != OVS_OK) return st;
+    if (stale) {
+        st = to_device(c, stale, m * 5, dev, &dst, &o2);
+        if (st != OVS_OK) { if (o1) hipFree(dn); return st; }
+    }
+    if (cap && !dev) {
+        HIPCHK(c, hipMalloc(&dk, sizeof(K160) * cap));
+        HIPCHK(c, hipMalloc(&dsrc, sizeof(uint32_t) * cap));
+    } else if (cap) {
+        dk = reinterpret_cast<K160*>(keys);
+        dsrc = src;
+    }
+    uint64_t total = 0;
+    const hipError_t e = kad_refresh_keys(c->kad, (uint32_t)c->n, dn, m, dst, dk, dsrc, cap, &total, s);
+    if (e == hipSuccess && cap && !dev) {
+        const uint64_t w = total < cap ? total : cap;
+        HIPCHK(c, hipMemcpyAsync(keys, dk, sizeof(K160) * w, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(src, dsrc, sizeof(uint32_t) * w, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    if (o1) hipFree(dn);
+    if (o2) hipFree(dst);
+    if (cap && !dev) { hipFree(dk); hipFree(dsrc); }
+    if (e != hipSuccess) return hip_fail(c, e, "bucket refresh keys");
+    *count = total;
+    return OVS_OK;
+}
+
 ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key160* keys, uint64_t n,
                                int32_t numRedundantNodes, int32_t numSiblings, uint32_t* out_nodes,
                                uint32_t max_out, uint8_t* out_count, uint8_t* out_sibling, uint32_t flags,

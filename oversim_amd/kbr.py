@@ -202,6 +202,8 @@ def lib() -> C.CDLL:
         "ovs_kbrtest_stats_batch": ([vp, vp, vp, vp, u64, C.c_double, i32, vp, u32, vp], C.c_int),
         "ovs_chord_fix_fingers": ([vp, vp, u64, vp], C.c_int),
         "ovs_lookup_batch": ([vp, vp, vp, u64, i32, vp, vp, u32, vp], C.c_int),
+        "ovs_kad_refresh_batch": ([vp, vp, vp, u64, i32, vp, vp, vp, vp, vp, u32, vp], C.c_int),
+        "ovs_kad_refresh_keys": ([vp, vp, u64, vp, vp, vp, u64, C.POINTER(u64), u32, vp], C.c_int),
         "ovs_kbrtest_lookup_stats_batch": ([vp, vp, vp, i32, vp, vp, u64, C.c_double, i32, C.c_double, vp, u32, vp],
                                            C.c_int),
     }
@@ -453,6 +455,56 @@ class KbrEngine:
         res = {f: out[f].copy() for f in LOOKUP_OUT_DTYPE.names}
         res["siblings"] = sib
         return res
+
+    def kad_refresh(self, keys, src, redundantNodes: int, record: bool = True) -> dict:
+        """Kademlia refresh lookups (ovs_kad_refresh_batch): exhaustive-iterative lookups of keys[i] from
+        src[i] with config.redundantNodes = numSiblings = redundantNodes (Kademlia.cc:1591-1686).
+        Returns the LookupCall fields, `siblings` (n, R), `rpcs`, and with record the responders
+        (n, hopCountMax) and their RTTs in ns, in the order the responses arrived."""
+        keys = keys_array(keys)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        if len(src) != n:
+            raise ValueError("keys and src differ in length")
+        R = int(redundantNodes)
+        H = max(self.get_params().hopCountMax, 1)
+        out = np.empty(n, dtype=LOOKUP_OUT_DTYPE)
+        sib = np.empty((n, max(R, 1)), dtype=np.uint32)
+        resp = np.empty((n, H), dtype=np.uint32) if record else None
+        rtt = np.empty((n, H), dtype=np.int64) if record else None
+        rpcs = np.empty(n, dtype=np.uint32)
+        self._chk(self._L.ovs_kad_refresh_batch(self._h, _ptr(keys), _ptr(src), n, R, _ptr(out), _ptr(sib), _ptr(resp),
+                                                _ptr(rtt), _ptr(rpcs), 0, None), "ovs_kad_refresh_batch")
+        res = {f: out[f].copy() for f in LOOKUP_OUT_DTYPE.names}
+        res["siblings"] = sib
+        res["rpcs"] = rpcs
+        if record:
+            res["responders"] = resp
+            res["rtt_ns"] = rtt
+        return res
+
+    def kad_refresh_device(self, keys_ptr: int, src_ptr: int, n: int, redundantNodes: int, out_ptr: int,
+                           sib_ptr: int, rpcs_ptr: int | None = None, stream: int | None = None):
+        """Device-resident refresh batch (no responder record)."""
+        self._chk(self._L.ovs_kad_refresh_batch(self._h, C.c_void_p(keys_ptr), C.c_void_p(src_ptr), n, redundantNodes,
+                                                C.c_void_p(out_ptr), C.c_void_p(sib_ptr), None, None,
+                                                C.c_void_p(rpcs_ptr) if rpcs_ptr else None, DEVICE_PTRS,
+                                                C.c_void_p(stream) if stream else None), "ovs_kad_refresh_batch")
+
+    def kad_refresh_keys(self, nodes=None, stale=None):
+        """The bucket-refresh (keys, src) of Kademlia::handleBucketRefreshTimerExpired for `nodes`
+        (default: all); stale = (m, 5) uint32 bit masks of the buckets due (None: all)."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        st = None if stale is None else np.ascontiguousarray(stale, dtype=np.uint32)
+        cnt = C.c_uint64(0)
+        self._chk(self._L.ovs_kad_refresh_keys(self._h, _ptr(nodes), len(nodes), _ptr(st), None, None, 0,
+                                               C.byref(cnt), 0, None), "ovs_kad_refresh_keys")
+        total = cnt.value
+        keys = np.zeros((max(total, 1), 5), dtype=np.uint32)
+        src = np.zeros(max(total, 1), dtype=np.uint32)
+        self._chk(self._L.ovs_kad_refresh_keys(self._h, _ptr(nodes), len(nodes), _ptr(st), _ptr(keys), _ptr(src),
+                                               total, C.byref(cnt), 0, None), "ovs_kad_refresh_keys")
+        return keys[:total], src[:total]
 
     def lookup_device(self, keys_ptr: int, src_ptr: int, n: int, out_ptr: int, stream: int | None = None,
                       hop_ptr: int | None = None, rpcs_ptr: int | None = None):

@@ -145,6 +145,10 @@ WORKLOADS = {
               desc="B: Kademlia 15000 nodes (nodes_2d_15000.xml), k=8, alpha=1, 1M node-ID lookups per GPU"),
     "E": dict(overlay="kademlia", nodes=1 << 24, per_gpu_nodes=False, lookups=4_000_000, node_ids=False, alpha=3,
               desc="E: Kademlia 2^24 nodes, k=8, alpha=3, 4M random-key lookups per GPU (ID arcs sharded over GPUs)"),
+    "R": dict(overlay="kademlia", nodes=1 << 20, per_gpu_nodes=False, lookups=0, node_ids=False, alpha=3,
+              refresh_nodes=1 << 16,
+              desc="R: Kademlia 2^20 nodes, k=8, alpha=3, the bucket refresh of 2^16 nodes per GPU "
+                   "(exhaustive-iterative lookups of self ^ 2^i, bucketRefreshNodes = 8; replicas)"),
     "K": dict(overlay="koorde", nodes=1 << 20, per_gpu_nodes=False, lookups=4_000_000, node_ids=False,
               desc="K: Koorde 2^20 nodes (successorListSize = deBruijnListSize = 16, shiftingBits = 4), "
                    "4M random-key iterative one-way lookups per GPU (replicas)"),
