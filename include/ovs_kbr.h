@@ -281,7 +281,9 @@ ovs_status  ovs_kad_refresh_keys(ovs_ctx* ctx, const uint32_t* nodes, uint64_t m
 
 /* Batched responder step: for each i, findNode(keys[i], numRedundantNodes,
  * numSiblings) evaluated at node[i] and the findNodeRpc siblings flag
- * isSiblingFor(node[i], keys[i], numSiblings).  out_nodes has max_out slots per
+ * isSiblingFor(node[i], keys[i], numSiblings).  Kademlia also takes
+ * numSiblings = -1: the FindNodeCall of an exhaustive-iterative lookup
+ * (resultSize = numRedundantNodes, no siblings flag; BaseOverlay.cc:1857-1871).  out_nodes has max_out slots per
  * query (0xFFFFFFFF padded), out_count the result size. */
 ovs_status  ovs_find_node_batch(ovs_ctx* ctx, const uint32_t* node, const ovs_key160* keys,
                                 uint64_t n, int32_t numRedundantNodes, int32_t numSiblings,

@@ -307,7 +307,9 @@ __global__ void k_kad_export(const KadNode* __restrict__ nodes, const KadBlk* __
     bcount[t] = (uint8_t)c;
 }
 
-// batched findNode (numRedundantNodes <= 16, 1 <= numSiblings <= 16) for the ABI
+// batched findNode (numRedundantNodes <= 16, 1 <= numSiblings <= 16, or numSiblings = -1: the call
+// of an exhaustive-iterative lookup, resultSize = numRedundantNodes and no siblings flag,
+// Kademlia.cc:1125-1127, BaseOverlay.cc:1857-1871) for the ABI
 template <bool EX>
 __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, const K160* __restrict__ keys, uint64_t n,
                                 int numRedundant, int numSiblings, uint32_t* __restrict__ out_nodes, uint32_t max_out,
@@ -318,7 +320,7 @@ __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, co
     const uint32_t c = node[i];
     const K160 K = keys[i];
     const KadNode r = load_node(V.nodes, c);
-    const bool sb = kad_is_sibling(V, r, c, K, numSiblings);
+    const bool sb = numSiblings >= 0 && kad_is_sibling(V, r, c, K, numSiblings);
     SVec<16> res;
     const int cnt = kad_find_node_ins<16, EX>(V, c, resp_geo(r, K), K, numRedundant, sb, res, numSiblings);
     uint32_t* o = out_nodes + i * max_out;
@@ -514,7 +516,7 @@ hipError_t kad_find_node(const KadTables& t, uint32_t n, const ovs_params& P, co
 {
     (void)P;
     if (nq == 0) return hipSuccess;
-    if (numSiblings < 1 || numSiblings > 16 || numRedundant > 16) return hipErrorNotSupported;
+    if ((numSiblings < 1 && numSiblings != -1) || numSiblings > 16 || numRedundant > 16) return hipErrorNotSupported;
     const KadView V = kad_make_view(t, nullptr, n);
     if (t.exact)
         hipLaunchKernelGGL(k_kad_find_node<true>, dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, numRedundant,

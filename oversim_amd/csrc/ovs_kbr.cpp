@@ -1171,6 +1171,8 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
     if (numSiblings > (c->overlay == OVS_OVERLAY_CHORD ? c->P.successorListSize : c->P.s))
         return fail(c, OVS_EINVAL, "numSiblings too big!");
     if (numRedundantNodes < 1 || numRedundantNodes > 64) return fail(c, OVS_EINVAL, "numRedundantNodes out of range");
+    if (numSiblings < 0 && (numSiblings != -1 || c->overlay != OVS_OVERLAY_KADEMLIA))
+        return fail(c, OVS_ENOTSUP, "numSiblings -1 (an exhaustive-iterative call) is implemented for Kademlia");
     HIPCHK(c, hipSetDevice(c->device));
     const bool dev = flags & OVS_DEVICE_PTRS;
     hipStream_t s = dev ? (hipStream_t)stream : c->stream;   // NULL = the default stream

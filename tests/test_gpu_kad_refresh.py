@@ -135,3 +135,19 @@ def test_refresh_rejects_unsupported(engine, net):
     engine.set_params(_params(lookupParallelRpcs=3, lookupStrictParallelRpcs=0))
     with pytest.raises(KbrError):
         engine.kad_refresh(keys, src, 8)
+
+
+def test_exhaustive_find_node_calls(engine, net):
+    """findNodeRpc of an exhaustive call: findNode(key, R, -1) -- resultSize R, no sibling flag."""
+    engine.set_params(Params.kademlia())
+    engine.kad_load(net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params())
+    rng = np.random.default_rng(21)
+    node = rng.integers(0, len(net.ids), 300).astype(np.uint32)
+    keys = np.concatenate([W.random_keys(150, rng), net.ids[node[150:]]])
+    for R in (8, 16):
+        got, cnt, sib = engine.findNode(node, keys, R, -1, max_out=16)
+        assert not sib.any()
+        for i in range(len(node)):
+            exp = o.find_node(int(node[i]), keys[i], R, -1)[0]
+            assert list(got[i, :cnt[i]]) == list(exp), (R, i)
