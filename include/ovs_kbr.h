@@ -96,7 +96,8 @@ typedef struct ovs_params {
     int32_t lookupVerifySiblings;       /* false only */
     int32_t lookupMajoritySiblings;     /* false only */
     int32_t routingType;                /* **.routingType: 0 = "iterative", 1 = "semi-recursive",
-                                           2 = "full-recursive" (recursive: Chord stable rings) */
+                                           2 = "full-recursive" (recursive: Chord stable rings),
+                                           3 = "exhaustive-iterative" (Kademlia, BaseOverlay.cc:123-124) */
     int32_t numSiblings;                /* sendToKey numSiblings (1 for KBRTestApp one-way) */
     int32_t useCoordinateBasedDelay;    /* **.udp.useCoordinateBasedDelay = true */
     int32_t simtimeRound;               /* SimTime(double): 1 = round half up, 0 = truncate */

@@ -1752,15 +1752,22 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
     int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
     if (net->type == NET_KOORDE && net->p.routingType != 0) { set_err("Koorde: iterative routing only"); return ORC_FAIL; }
     if (hop_seq) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) hop_seq[i] = NONE;
+    /* routingType "exhaustive-iterative" (BaseOverlay.cc:123-124, 1434-1442): an exhaustive
+     * IterativeLookup with config.redundantNodes = lookupRedundantNodes (Kademlia only here) */
+    const int exh = net->p.routingType == 3 ? net->p.lookupRedundantNodes : 0;
+    if (exh && (net->type != NET_KAD || net->p.numSiblings > exh)) {
+        set_err("exhaustive-iterative: Kademlia, numSiblings <= lookupRedundantNodes (IterativeLookup.cc:714-719)");
+        return ORC_FAIL;
+    }
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 256) reduction(+ : total) num_threads(nthreads)
 #endif
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         OKey k = ok_from(&keys[i]);
-        if (net->p.routingType == 0)
+        if (net->p.routingType == 0 || net->p.routingType == 3)
             run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
-                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL, 0, NULL);
+                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL, exh, NULL);
         else {
             run_recursive(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL);
             if (rpcs_out) rpcs_out[i] = 0;     /* no FindNodeCalls in recursive routing */
@@ -1778,7 +1785,12 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     if (numSiblings < 0) numSiblings = maxs;                              /* BaseOverlay.cc:1942-1944 */
     if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
     if (numSiblings < 1 || numSiblings > 16) { set_err("numSiblings must be 1..16"); return -1; }
-    if (net->p.routingType != 0) { set_err("LookupCall: iterative routing only"); return -1; }
+    if (net->p.routingType != 0 && net->p.routingType != 3) { set_err("LookupCall: iterative routing only"); return -1; }
+    const int exh = net->p.routingType == 3 ? net->p.lookupRedundantNodes : 0;
+    if (exh && (net->type != NET_KAD || numSiblings > exh)) {
+        set_err("exhaustive-iterative: Kademlia, numSiblings <= lookupRedundantNodes (IterativeLookup.cc:714-719)");
+        return -1;
+    }
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 256) num_threads(nthreads)
@@ -1786,7 +1798,8 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         OKey k = ok_from(&keys[i]);
         orc_route_out dummy;
-        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings, 0, NULL);
+        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings, exh,
+                   NULL);
     }
     (void)nthreads;
     return g_cap_fail ? -1 : numSiblings;

@@ -93,12 +93,14 @@ hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ov
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
                      ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st,
                      uint32_t* sibs = nullptr);
-// exhaustive-iterative refresh lookups (K2x, kad_refresh.hip); *capacity_error: a lookup ran past
-// the kernel's fixed capacities (more than 64 timed-out nodes)
-hipError_t kad_refresh(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
-                       int R, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_lookup_out* out,
-                       uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                       hipStream_t st, bool* capacity_error);
+// exhaustive-iterative lookups (K2x, kad_refresh.hip): config.redundantNodes = R, a siblings vector
+// of ns <= R; out = ovs_route_out (oneway: KBRTestApp one-way test) or ovs_lookup_out; responders =
+// the accepted responders in order (= hop_seq); *capacity_error: a lookup ran past the kernel's
+// fixed capacities (more than 64 timed-out nodes)
+hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
+                          int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
+                          uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
+                          hipStream_t st, bool* capacity_error);
 // bucket-refresh keys of nodes[0..m) (device buffers); *total = how many (up to cap written)
 hipError_t kad_refresh_keys(const KadTables& t, uint32_t n, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
                             K160* keys, uint32_t* src, uint64_t cap, uint64_t* total, hipStream_t st);

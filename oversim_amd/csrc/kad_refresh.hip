@@ -30,7 +30,8 @@ constexpr int XMAXA = 4;        // lookupParallelRpcs <= 4 (strictParallelRpcs: 
 constexpr int XMAXDEAD = 64;    // nodes whose RPC timed out, per lookup
 
 struct XCfg {
-    int R, alpha, hcm, k;
+    int R, ns, alpha, hcm, k;      // ns: the siblings vector's size (numSiblings <= R)
+    int oneway;                    // 1: a KBRTestApp one-way lookup (route message to the result)
     int strict, visitOnlyOnce, newOnResp, newOnTimeout, finishOnFirst;
 };
 
@@ -74,7 +75,7 @@ struct XCtx {
     uint64_t lane;
     uint32_t* __restrict__ resp;      // responders of this lookup (hop order), hcm entries
     int64_t* __restrict__ rtt;        // their RTTs (may be null)
-    uint32_t* __restrict__ sib;       // R siblings of this lookup
+    uint32_t* __restrict__ sib;       // ns siblings of this lookup
 
     __device__ __forceinline__ uint64_t at(int j) const { return (uint64_t)j * X.lanes + lane; }
 
@@ -220,8 +221,10 @@ struct XCtx {
             X.nh_used[at(e)] = 1;
         }
         if (L.pending == 0) {
-            // exhaustive lookups are always successful: siblings = nextHops[0..R) (1147-1156)
-            const int m = L.nnh < C.R ? L.nnh : C.R;
+            // exhaustive lookups are always successful: addSibling(nextHops[0..R)) -- push_back while
+            // the numSiblings-sized vector has room (1147-1156, 436-440)
+            int m = L.nnh < C.R ? L.nnh : C.R;
+            m = m < C.ns ? m : C.ns;
             for (int q = 0; q < m; ++q) sib[q] = X.nh_idx[at(q)];
             L.psuccess = true;
             L.pfinished = true;
@@ -378,8 +381,8 @@ __global__ __launch_bounds__(256) void k_kad_refresh(KadView V, DelayConsts DC, 
         L.pfinished = false; L.psuccess = false; L.counted = false; L.any_to = false; L.success = false; L.err = false;
         L.finishedPaths = 0; L.successfulPaths = 0; L.minHops = 0x7FFFFFFF;
         L.pvalid = 0;
-        uint32_t* sib = sib_out + q * (uint64_t)C.R;
-        for (int j = 0; j < C.R; ++j) sib[j] = NONE;
+        uint32_t* sib = sib_out + q * (uint64_t)C.ns;
+        for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
         uint32_t* resp = resp_out + q * (uint64_t)C.hcm;
         int64_t* rtt = rtt_out ? rtt_out + q * (uint64_t)C.hcm : nullptr;
         const XCtx<EX> ctx{V, DC, C, X, lane, resp, rtt, sib};
@@ -392,26 +395,53 @@ __global__ __launch_bounds__(256) void k_kad_refresh(KadView V, DelayConsts DC, 
         // SendToKeyListener / LookupResponse fields (as ovs_lookup_batch): the ovs_lookup_out is
         // written through its ovs_route_out twin (same size; k_lookup_finish's convention)
         const bool valid = L.success && !L.err;
+        const uint8_t fail_status = L.now > DC.lookupTimeout ? OVS_LOOKUP_TIMEOUT
+                                    : L.nd > 0                 ? OVS_LOOKUP_RPC_TIMEOUT
+                                    : (C.hcm && L.hops >= C.hcm) ? OVS_LOOKUP_HOPMAX
+                                                                 : OVS_LOOKUP_NO_NEXT;
+        if (rpcs_out) rpcs_out[q] = L.nsent;
+        if (C.oneway) {
+            // SendToKeyListener::lookupFinished -> sendRouteMessage to getResult()[0] through the
+            // source's tx queue (BaseOverlay.cc:1107-1146, 1241-1259; SimpleNodeEntry.cc:164-194)
+            ovs_route_out o;
+            o.hops = (uint16_t)(L.minHops == 0x7FFFFFFF ? 0 : L.minHops);
+            const uint32_t R0 = sib[0];
+            if (valid && R0 != NONE) {
+                o.status = OVS_LOOKUP_OK;
+                o.responsible = R0;
+                o.one_way_hops = (uint8_t)(o.hops + (R0 != L.S ? 1 : 0));
+                int64_t lat = L.now;
+                if (R0 != L.S) {
+                    const double2 rxy = V.xy[R0];
+                    const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + DC.bwRoute;
+                    lat = newTx + DC.access2 + coord_ns(L.sx, L.sy, rxy.x, rxy.y, DC.round) + DC.bwRoute;
+                }
+                o.latency_ns = lat;
+            } else {
+                o.status = fail_status;
+                o.responsible = NONE;
+                o.one_way_hops = 0;
+                o.latency_ns = -1;
+            }
+            out[q] = o;
+            continue;
+        }
         ovs_lookup_out o;
         o.hops = (uint16_t)(L.minHops == 0x7FFFFFFF ? 0 : L.minHops);
         o.is_valid = valid ? 1 : 0;
         if (valid) {
             int ns = 0;
-            for (int j = 0; j < C.R; ++j) ns += sib[j] != NONE ? 1 : 0;
+            for (int j = 0; j < C.ns; ++j) ns += sib[j] != NONE ? 1 : 0;
             o.num_siblings = (uint32_t)ns;
             o.latency_ns = L.now;
             o.status = OVS_LOOKUP_OK;
         } else {
-            for (int j = 0; j < C.R; ++j) sib[j] = NONE;
+            for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
             o.num_siblings = 0;
             o.latency_ns = -1;
-            if (L.now > DC.lookupTimeout) o.status = OVS_LOOKUP_TIMEOUT;
-            else if (L.nd > 0) o.status = OVS_LOOKUP_RPC_TIMEOUT;
-            else if (C.hcm && L.hops >= C.hcm) o.status = OVS_LOOKUP_HOPMAX;
-            else o.status = OVS_LOOKUP_NO_NEXT;
+            o.status = fail_status;
         }
         reinterpret_cast<ovs_lookup_out*>(out)[q] = o;
-        if (rpcs_out) rpcs_out[q] = L.nsent;
     }
 }
 
@@ -470,19 +500,19 @@ __global__ void k_kad_refresh_fill(KadView V, const uint32_t* __restrict__ nodes
 
 }  // namespace
 
-hipError_t kad_refresh(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
-                       int R, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_lookup_out* out,
-                       uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                       hipStream_t st, bool* capacity_error)
+hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
+                          int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
+                          uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
+                          hipStream_t st, bool* capacity_error)
 {
     *capacity_error = false;
     if (nq == 0) return hipSuccess;
     const int A = P.lookupParallelRpcs;
-    if (A < 1 || A > XMAXA || R < 1 || R > 64 || !P.lookupMerge || !P.lookupStrictParallelRpcs ||
+    if (A < 1 || A > XMAXA || R < 1 || R > 64 || ns < 1 || ns > R || !P.lookupMerge || !P.lookupStrictParallelRpcs ||
         P.hopCountMax < 1 || t.k > 8)
         return hipErrorNotSupported;
     const KadView V = kad_make_view(t, xy, n);
-    XCfg C{R, A, P.hopCountMax, t.k, P.lookupStrictParallelRpcs, P.lookupVisitOnlyOnce,
+    XCfg C{R, ns, oneway ? 1 : 0, A, P.hopCountMax, t.k, P.lookupStrictParallelRpcs, P.lookupVisitOnlyOnce,
            P.lookupNewRpcOnEveryResponse, P.lookupNewRpcOnEveryTimeout, P.lookupFinishOnFirstUnchanged};
     // one lane per lookup, up to 1024 lanes per CU; the scratch is sized for the lanes
     uint64_t lanes = (uint64_t)num_cu * 1024;
@@ -505,7 +535,7 @@ hipError_t kad_refresh(const KadTables& t, const double2* xy, uint32_t n, const 
     X.lanes = lanes;
     hipMemsetAsync(err, 0, 4, st);
     const unsigned blocks = (unsigned)(lanes / 256);
-    ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);
+    ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);   // or ovs_lookup_out (same size)
     if (t.exact)
         hipLaunchKernelGGL(k_kad_refresh<true>, dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, qsrc, nq, o, sibs,
                            responders, rtts, rpcs, err);

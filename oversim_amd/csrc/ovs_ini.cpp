@@ -298,6 +298,7 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         if (rt == "iterative") p->routingType = 0;
         else if (rt == "semi-recursive") p->routingType = 1;
         else if (rt == "full-recursive") p->routingType = 2;
+        else if (rt == "exhaustive-iterative") p->routingType = 3;
         else {
             set_err("routingType \"" + rt + "\" not supported (iterative, semi-recursive, full-recursive)");
             return OVS_ENOTSUP;

@@ -173,9 +173,13 @@ DelayConsts delay_consts(const ovs_params& P)
 ovs_status check_common(ovs_ctx* c, const ovs_params& P)
 {
     if (P.keyLength != 160) return fail(c, OVS_ENOTSUP, "keyLength != 160 not supported");
-    if (P.routingType < 0 || P.routingType > 2)
-        return fail(c, OVS_ENOTSUP, "routingType must be iterative, semi-recursive or full-recursive");
-    if (P.routingType != 0 && P.recNumRedundantNodes < 1)
+    if (P.routingType < 0 || P.routingType > 3)
+        return fail(c, OVS_ENOTSUP, "routingType must be iterative, semi-recursive, full-recursive or exhaustive-iterative");
+    if (P.routingType == 3 && c->overlay != OVS_OVERLAY_KADEMLIA)
+        return fail(c, OVS_ENOTSUP, "exhaustive-iterative routing is implemented for Kademlia");
+    if (P.routingType == 3 && P.numSiblings > P.lookupRedundantNodes)
+        return fail(c, OVS_EINVAL, "With EXHAUSTIVE_ITERATIVE_ROUTING numRedundantNodes must be >= numSiblings!");
+    if ((P.routingType == 1 || P.routingType == 2) && P.recNumRedundantNodes < 1)
         return fail(c, OVS_EINVAL, "recNumRedundantNodes must be >= 1");
     if (P.lookupParallelPaths != 1) return fail(c, OVS_ENOTSUP, "lookupParallelPaths != 1 not supported");
     if (P.lookupVerifySiblings || P.lookupMajoritySiblings)
@@ -872,8 +876,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             return fail(c, OVS_ENOTSUP,
                         "Koorde route kernel implements lookupRedundantNodes=1, lookupParallelRpcs=1, merge off, "
                         "visitOnlyOnce, numSiblings=1 (the Koorde defaults)");
-    } else if (c->P.routingType != 0) {
-        return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
+    } else if (c->P.routingType != 0 && c->P.routingType != 3) {
+        return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative / exhaustive-iterative");
     } else if (c->P.numSiblings != 1) {
         return fail(c, OVS_ENOTSUP, "the one-way route implements numSiblings = 1 (LookupCall: ovs_lookup_batch)");
     } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
@@ -899,7 +903,9 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     // Koorde without a hop_seq request uses a context scratch buffer, unpadded: K3 reads back only
     // the entries a lookup wrote
     const bool koorde_scratch = c->overlay == OVS_OVERLAY_KOORDE && !hop_seq;
-    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal);
+    // exhaustive-iterative Kademlia: the responder list is the lookup's visited set
+    const bool kad_exh = c->overlay == OVS_OVERLAY_KADEMLIA && c->P.routingType == 3;
+    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal) || kad_exh;
     bool own_hop = false;
     if (koorde_scratch) {
         if (c->kvis_cap < n * (uint64_t)H) {
@@ -932,6 +938,16 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     } else if (c->overlay == OVS_OVERLAY_KOORDE) {
         e = koorde_route(c->koorde, c->recs, c->xy, delay_consts(c->P), c->P.hopCountMax, dk, ds, n, dout, dhop, drpc,
                          c->num_cu, s);
+    } else if (kad_exh) {
+        // sendToKey with EXHAUSTIVE_ITERATIVE_ROUTING (BaseOverlay.cc:1434-1442): lookup(key, numSiblings = 1)
+        // with redundantNodes = lookupRedundantNodes, the route message to getResult()[0]
+        uint32_t* dres = nullptr;
+        HIPCHK(c, hipMalloc(&dres, sizeof(uint32_t) * n));
+        bool cap_err = false;
+        e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->P.lookupRedundantNodes, 1, true,
+                           dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err);
+        hipFree(dres);
+        if (e == hipSuccess && cap_err) return fail(c, OVS_ENOTSUP, "a lookup exceeded the kernel's capacity (64 timed-out nodes)");
     } else {
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
                       c->num_cu, s);
@@ -971,7 +987,11 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     P.numSiblings = 1;          // the route checks: one-way configuration, numSiblings applied below
     ovs_status st = check_common(c, P);
     if (st != OVS_OK) return st;
-    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative");
+    const bool kad_exh = !chord && P.routingType == 3;
+    if (P.routingType != 0 && !kad_exh)
+        return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative (Kademlia: also exhaustive-iterative)");
+    if (kad_exh && ns > P.lookupRedundantNodes)
+        return fail(c, OVS_EINVAL, "With EXHAUSTIVE_ITERATIVE_ROUTING numRedundantNodes must be >= numSiblings!");
     HIPCHK(c, hipSetDevice(c->device));
     const bool dev = flags & OVS_DEVICE_PTRS;
     hipStream_t s = dev ? (hipStream_t)stream : c->stream;
@@ -1013,7 +1033,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         dsib = siblings;
     }
     const int H = P.hopCountMax > 0 ? P.hopCountMax : 1;
-    const bool need_hop = chord && !c->ideal;      // visited check on explicit tables
+    const bool need_hop = (chord && !c->ideal) || kad_exh;   // visited check (explicit tables; exhaustive lookups)
     if (need_hop) {
         HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H));
         HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
@@ -1022,11 +1042,17 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     if (chord) {
         LookupConsts LC{P.hopCountMax, ns, P.lookupRedundantNodes, 0};
         e = launch_chord_route(chord_view(c), c->ideal, DC, LC, dk, ds, n, dout, dhop, c->num_cu, s);
+    } else if (kad_exh) {
+        // lookupRpc with EXHAUSTIVE_ITERATIVE_ROUTING: redundantNodes = lookupRedundantNodes, numSiblings = ns
+        bool cap_err = false;
+        e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), P.lookupRedundantNodes, ns, false, dk, ds,
+                           n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err);
+        if (e == hipSuccess && cap_err) e = hipErrorNotSupported;
     } else {
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
                       dsib);
     }
-    if (e == hipSuccess) e = launch_lookup_finish(chord_view(c), chord, c->ideal, ns, dout, dsib, n, s);
+    if (e == hipSuccess && !kad_exh) e = launch_lookup_finish(chord_view(c), chord, c->ideal, ns, dout, dsib, n, s);
     if (e != hipSuccess) {
         if (!dev) { hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib); }
         if (dhop) hipFree(dhop);
@@ -1055,7 +1081,6 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
         return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: refresh lookups need the whole network");
     if (R < 1 || R > 64) return fail(c, OVS_ENOTSUP, "refresh lookups implement redundantNodes 1..64");
     const ovs_params& P = c->P;
-    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "refresh lookups: iterative routing (exhaustive-iterative)");
     if (P.hopCountMax < 1) return fail(c, OVS_ENOTSUP, "refresh lookups need hopCountMax >= 1");
     if (!P.lookupMerge || !P.lookupStrictParallelRpcs || P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > 4)
         return fail(c, OVS_ENOTSUP, "refresh lookups implement lookupMerge, strictParallelRpcs, parallelRpcs 1..4");
@@ -1097,8 +1122,8 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
     if (own_rpc) HIPCHK(c, hipMalloc(&drpc, sizeof(uint32_t) * n));
     else drpc = rpcs;
     bool cap_err = false;
-    const hipError_t e = kad_refresh(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), R, dk, ds, n, dout, dsib, dresp,
-                                     drtt, drpc, c->num_cu, s, &cap_err);
+    const hipError_t e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), R, R, false, dk, ds, n, dout,
+                                        dsib, dresp, drtt, drpc, c->num_cu, s, &cap_err);
     if (e != hipSuccess) { cleanup(); return hip_fail(c, e, "refresh lookup kernel"); }
     if (cap_err) { cleanup(); return fail(c, OVS_ENOTSUP, "a refresh lookup exceeded the kernel's capacity (64 timed-out nodes)"); }
     if (!dev) {

@@ -612,14 +612,13 @@ class KadLookupSim:
         return False
 
     def run(self, key_words, S, num_siblings=1, lookup_call=False, exhaustive=0):
-        """exhaustive = R > 0: an EXHAUSTIVE_ITERATIVE_ROUTING lookup with config.redundantNodes = R and
-        numSiblings = R (Kademlia's bucket / sibling refresh, Kademlia.cc:1604-1611, 1658-1665)."""
+        """exhaustive = R > 0: an EXHAUSTIVE_ITERATIVE_ROUTING lookup with config.redundantNodes = R
+        (Kademlia's bucket / sibling refresh with numSiblings = R, Kademlia.cc:1604-1611, 1658-1665;
+        routingType = "exhaustive-iterative" lookups with R = lookupRedundantNodes)."""
         import heapq
         self.key = to_int(key_words)
         self.exh = exhaustive
         self.R = exhaustive if exhaustive else self.cfg["redundant"]
-        if exhaustive:
-            num_siblings, lookup_call = exhaustive, True
         self.sent_at, self.rtts = {}, []
         self.S, self.num_siblings = S, num_siblings
         self.fes, self.ins, self.now, self.tx = [], 0, 0, {}

@@ -151,3 +151,27 @@ def test_exhaustive_find_node_calls(engine, net):
         for i in range(len(node)):
             exp = o.find_node(int(node[i]), keys[i], R, -1)[0]
             assert list(got[i, :cnt[i]]) == list(exp), (R, i)
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+def test_exhaustive_routing_type(engine, net, alpha):
+    """routingType = "exhaustive-iterative" (BaseOverlay.cc:123-124, 1434-1442) through the one-way
+    route (numSiblings 1: route message to the closest node the lookup found) and LookupCalls
+    (numSiblings = s), both on K2x."""
+    kw = dict(lookupParallelRpcs=alpha, routingType=3)
+    engine.set_params(_params(**kw))
+    engine.kad_load(net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params(**kw))
+    k1, s1 = W.lookups(net.ids, 1500, 77, node_ids=False)
+    k2, s2 = W.lookups(net.ids, 500, 78, node_ids=True)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    r = engine.lookup(keys, src, record_hops=True, count_rpcs=True)
+    e = o.route(keys, src, record_hops=True, count_rpcs=True)
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs"):
+        assert np.array_equal(r[f], e[f]), f
+    assert np.array_equal(r["hop_seq"], e["hop_seq"])
+    c = engine.lookupCall(keys, src, 8)
+    ce = o.lookup_call(keys, src, 8)
+    for f in FIELDS:
+        assert np.array_equal(c[f], ce[f]), f
+    assert np.array_equal(c["siblings"], ce["siblings"])

@@ -121,7 +121,7 @@ def test_refresh_lookups_agree(net, name, R):
     r = o.exhaustive(keys, src, R)
     statuses, lost = set(), False
     for i in range(len(keys)):
-        m = sim.run(keys[i], int(src[i]), exhaustive=R)
+        m = sim.run(keys[i], int(src[i]), num_siblings=R, lookup_call=True, exhaustive=R)
         assert int(r["is_valid"][i]) == m["is_valid"], (name, i)
         assert int(r["status"][i]) == m["status"], (name, i)
         assert int(r["hops"][i]) == m["hops"], (name, i)
@@ -159,3 +159,25 @@ def test_refresh_keys_follow_the_timer(net):
     keys2, src2 = o.refresh_keys(nodes, stale)
     assert list(src2) == list(nodes)
     assert [refmodel.to_int(k) for k in keys2] == [ids[v] ^ (1 << 159) for v in nodes]
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+def test_exhaustive_routing_type_agrees(net, alpha):
+    """routingType = "exhaustive-iterative" (BaseOverlay.cc:1434-1442): one-way lookups (numSiblings 1,
+    the route message to the closest node found) and LookupCalls (numSiblings = s)."""
+    p = kad_params(lookupParallelRpcs=alpha, routingType=3)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    keys, src = W.lookups(net.ids, 150, 41 + alpha, node_ids=False)
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]), exhaustive=8)
+        for f in FIELDS:
+            assert int(r[f][i]) == int(m[f]), (alpha, i, f, int(r[f][i]), int(m[f]))
+        assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == m["hop_seq"], (alpha, i)
+    c = o.lookup_call(keys, src, 8)
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]), num_siblings=8, lookup_call=True, exhaustive=8)
+        assert int(c["is_valid"][i]) == m["is_valid"] and int(c["hops"][i]) == m["hops"], i
+        assert int(c["latency_ns"][i]) == m["latency_ns"], i
+        assert [int(x) for x in c["siblings"][i][: len(m["siblings"])]] == m["siblings"], i
