@@ -116,6 +116,7 @@ struct XCtx {
         const KadNode r = load_node(V.nodes, c);
         const RespGeo g = resp_geo(r, K);
         const int base = slot * C.R;
+        rs = min(rs, slot < C.alpha ? C.R : max(C.R, C.k));   // the slot's capacity (XScratch::res_idx)
         int n = 0;
         const uint64_t kt = ktop(K);
         if (g.nsib == 0) {      // an empty sibling table answers [self]
@@ -512,8 +513,12 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
         P.hopCountMax < 1 || t.k > 8)
         return hipErrorNotSupported;
     const KadView V = kad_make_view(t, xy, n);
-    XCfg C{R, ns, oneway ? 1 : 0, A, P.hopCountMax, t.k, P.lookupStrictParallelRpcs, P.lookupVisitOnlyOnce,
-           P.lookupNewRpcOnEveryResponse, P.lookupNewRpcOnEveryTimeout, P.lookupFinishOnFirstUnchanged};
+    XCfg C;
+    C.R = R; C.ns = ns; C.alpha = A; C.hcm = P.hopCountMax; C.k = t.k;
+    C.oneway = oneway ? 1 : 0;
+    C.strict = P.lookupStrictParallelRpcs; C.visitOnlyOnce = P.lookupVisitOnlyOnce;
+    C.newOnResp = P.lookupNewRpcOnEveryResponse; C.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
+    C.finishOnFirst = P.lookupFinishOnFirstUnchanged;
     // one lane per lookup, up to 1024 lanes per CU; the scratch is sized for the lanes
     uint64_t lanes = (uint64_t)num_cu * 1024;
     if (lanes > nq) lanes = nq;
