@@ -175,7 +175,7 @@ ovs_status check_common(ovs_ctx* c, const ovs_params& P)
     if (P.keyLength != 160) return fail(c, OVS_ENOTSUP, "keyLength != 160 not supported");
     if (P.routingType < 0 || P.routingType > 3)
         return fail(c, OVS_ENOTSUP, "routingType must be iterative, semi-recursive, full-recursive or exhaustive-iterative");
-    if (P.routingType == 3 && c->overlay != OVS_OVERLAY_KADEMLIA)
+    if (P.routingType == 3 && P.overlay != OVS_OVERLAY_KADEMLIA)
         return fail(c, OVS_ENOTSUP, "exhaustive-iterative routing is implemented for Kademlia");
     if (P.routingType == 3 && P.numSiblings > P.lookupRedundantNodes)
         return fail(c, OVS_EINVAL, "With EXHAUSTIVE_ITERATIVE_ROUTING numRedundantNodes must be >= numSiblings!");
