@@ -11,14 +11,18 @@
 //     unqueried next hops: the lookup then succeeds with nextHops[0..R) as its siblings
 //     (1144-1168); hopCountMax and LOOKUP_TIMEOUT still end it unsuccessfully;
 //   * a node whose RPC timed out leaves nextHops (948-957).
-// R reaches 40 (siblingRefreshNodes = 5s), so the vectors do not fit registers: each lane keeps
-// its LookupVector (2R entries) and the findNode results of its <= alpha pending calls in a
-// per-lane scratch slice laid out entry-major (entry j of lane l at j * lanes + l), so lanes that
-// walk their vectors in step touch consecutive addresses.  The responder's findNode is evaluated
-// when the call is sent (the tables do not change during a batch): its size fixes the response's
-// delay, and the result waits in the pending slot's scratch until the response event.  One lane
-// runs one lookup to completion, then takes the next one of the grid-stride loop.
+// R reaches 40 (siblingRefreshNodes = 5s), so the LookupVector (2R entries) does not fit
+// registers: each lane keeps it in a per-lane scratch slice laid out entry-major (entry j of lane l
+// at j * lanes + l), so lanes that walk their vectors in step touch consecutive addresses.  A
+// responder's findNode is evaluated when its response is processed (the tables do not change
+// during a batch) -- with K2's sorting networks for R <= 8, by insertion into scratch beyond; at
+// send time only its size is needed (the response's delay).  The start, responses and timeouts
+// share one findNode / merge / sendRpc site.  One lane runs one lookup to completion, then takes
+// the next one of the grid-stride loop.
 #include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <mutex>
 
 #include "kad_dev.hpp"
 
@@ -32,6 +36,7 @@ constexpr int XMAXDEAD = 64;    // nodes whose RPC timed out, per lookup
 struct XCfg {
     int R, ns, alpha, hcm, k;      // ns: the siblings vector's size (numSiblings <= R)
     int oneway;                    // 1: a KBRTestApp one-way lookup (route message to the result)
+    int64_t bwFull, bwOne;         // T(L*8/datarate) of a FindNodeResponse with R nodes / one node
     int strict, visitOnlyOnce, newOnResp, newOnTimeout, finishOnFirst;
 };
 
@@ -39,7 +44,7 @@ struct XScratch {
     uint32_t* nh_idx;    // [2R][lanes]
     uint64_t* nh_d;      // [2R][lanes]
     uint8_t* nh_used;    // [2R][lanes]
-    uint32_t* res_idx;   // [A * R + max(R, k)][lanes]: findNode results of the pending calls (slot A: the start)
+    uint32_t* res_idx;   // [max(R, k)][lanes]: a findNode result of more than 8 nodes
     uint64_t* res_d;
     uint32_t* dead;      // [XMAXDEAD][lanes]
     uint64_t lanes;
@@ -47,7 +52,6 @@ struct XScratch {
 
 struct XPend {
     uint32_t node, ninfo, seq;
-    int rn;              // findNode result size (scratch slot)
     int64_t t, tins, tsend;
     bool to;
 };
@@ -66,7 +70,15 @@ struct XLookup {
     uint32_t pvalid;
 };
 
-template <bool EX>
+// LookupVector nextHops of 2R <= 16 entries in registers (R <= 8: the bucket refreshes and the
+// exhaustive-iterative lookups of the default configuration)
+struct XRegNh {
+    uint32_t idx[16];
+    uint64_t d[16];
+    uint32_t used;      // bit i: entry i alreadyUsed
+};
+
+template <bool EX, bool REG>
 struct XCtx {
     const KadView& V;
     const DelayConsts& DC;
@@ -80,54 +92,51 @@ struct XCtx {
     __device__ __forceinline__ uint64_t at(int j) const { return (uint64_t)j * X.lanes + lane; }
 
     // --- sorted vectors in scratch (BaseKeySortedVector::add, NodeVector.h:381-512) -----------------
-    // insert x (distance top dx) into the vector at scratch rows [base, base + cap) holding *n
-    // entries; returns the position or -1 (full and farther than the last, or already present)
-    __device__ int vadd(uint32_t* idx, uint64_t* d, uint8_t* used, int base, int cap, int* n, uint32_t x,
-                        uint64_t dx, const K160& K) const
+    // insert x (distance top dx) into the vector at scratch rows [0, cap) holding *n entries;
+    // returns the position or -1 (full and farther than the last, or already present)
+    __device__ __forceinline__ int vadd(uint32_t* idx, uint64_t* d, uint8_t* used, int cap, int* n, uint32_t x,
+                                        uint64_t dx, const K160& K) const
     {
         const int m = *n;
         if (m == cap) {
-            const uint32_t li = idx[at(base + m - 1)];
-            if (li != x && cand_lt<EX>(d[at(base + m - 1)], li, dx, x, K, V.nodes)) return -1;
+            const uint32_t li = idx[at(m - 1)];
+            if (li != x && cand_lt<EX>(d[at(m - 1)], li, dx, x, K, V.nodes)) return -1;
         }
         int pos = m;
         for (int i = 0; i < m; ++i) {
-            const uint32_t ei = idx[at(base + i)];
+            const uint32_t ei = idx[at(i)];
             if (ei == x) return -1;
-            if (cand_lt<EX>(dx, x, d[at(base + i)], ei, K, V.nodes)) { pos = i; break; }
+            if (cand_lt<EX>(dx, x, d[at(i)], ei, K, V.nodes)) { pos = i; break; }
         }
         const int last = m < cap ? m : cap - 1;
         for (int i = last; i > pos; --i) {
-            idx[at(base + i)] = idx[at(base + i - 1)];
-            d[at(base + i)] = d[at(base + i - 1)];
-            if (used) used[at(base + i)] = used[at(base + i - 1)];
+            idx[at(i)] = idx[at(i - 1)];
+            d[at(i)] = d[at(i - 1)];
+            if (used) used[at(i)] = used[at(i - 1)];
         }
-        idx[at(base + pos)] = x;
-        d[at(base + pos)] = dx;
-        if (used) used[at(base + pos)] = 0;
+        idx[at(pos)] = x;
+        d[at(pos)] = dx;
+        if (used) used[at(pos)] = 0;
         *n = m < cap ? m + 1 : cap;
         return pos;
     }
 
-    // Kademlia::findNode(key, numRedundantNodes = rs, numSiblings = -1) at node c into result slot
-    // `slot` (Kademlia.cc:1101-1246; b = 1: startIndex = mainIndex).  Returns the result size.
-    __device__ int find_node(uint32_t c, const K160& K, int rs, int slot) const
+    // Kademlia::findNode(key, numRedundantNodes = rs > 8, numSiblings = -1) at node c into the
+    // scratch result (Kademlia.cc:1101-1246; b = 1: startIndex = mainIndex).  Returns its size.
+    __device__ __forceinline__ int find_node_scratch(uint32_t c, const RespGeo& g, const K160& K, int rs) const
     {
-        const KadNode r = load_node(V.nodes, c);
-        const RespGeo g = resp_geo(r, K);
-        const int base = slot * C.R;
-        rs = min(rs, slot < C.alpha ? C.R : max(C.R, C.k));   // the slot's capacity (XScratch::res_idx)
         int n = 0;
         const uint64_t kt = ktop(K);
+        const uint64_t dself = dist_hi(node_key(V.nodes, c), K);
         if (g.nsib == 0) {      // an empty sibling table answers [self]
-            vadd(X.res_idx, X.res_d, nullptr, base, rs, &n, c, dist_hi(as_key(r.key), K), K);
+            vadd(X.res_idx, X.res_d, nullptr, rs, &n, c, dself, K);
             return n;
         }
         auto add_blk = [&](const KadBlk* blk) {
             for (int q = 0; q < KBLK; ++q) {
                 const uint32_t x = blk->idx[q];
                 if (x == NONE) break;
-                vadd(X.res_idx, X.res_d, nullptr, base, rs, &n, x, dclamp(blk->top[q] ^ kt), K);
+                vadd(X.res_idx, X.res_d, nullptr, rs, &n, x, dclamp(blk->top[q] ^ kt), K);
             }
         };
         auto add_slot = [&](int bucket) {
@@ -139,13 +148,119 @@ struct XCtx {
             for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
             const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
             for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
-            vadd(X.res_idx, X.res_d, nullptr, base, rs, &n, c, dist_hi(as_key(r.key), K), K);
+            vadd(X.res_idx, X.res_d, nullptr, rs, &n, c, dself, K);
         }
         for (int b = g.m + 1; n < rs && b < KEYBITS; ++b) add_slot(b);
         return n;
     }
 
-    __device__ bool is_dead(const XLookup& L, uint32_t x) const
+    // The size of that result without evaluating it: the scan's candidate sets (buckets, sibling
+    // table, self) are disjoint (routingAdd's invariants), so the result holds min(rs, candidates
+    // visited) nodes.  Needed at send time for the response's delay.
+    __device__ __forceinline__ int find_node_size(uint32_t c, const RespGeo& g, int rs) const
+    {
+        if (g.nsib == 0) return 1;
+        const int full = rs < (int)V.n ? rs : (int)V.n;
+        if (!V.maybe_short || g.nsib + 1 >= rs) return full;   // the scan always reaches siblings + self
+        int n = 0;
+        auto cnt_slot = [&](int bucket) {
+            if (g.rowlo < 0 || bucket < g.rowlo) return;
+            const KadBlk* blk = slot_blk(V, g.boff, bucket);
+            for (int q = 0; q < KBLK && blk->idx[q] != NONE; ++q) ++n;
+        };
+        if (g.m >= 0) cnt_slot(g.m);
+        if (g.m >= g.endIndex || n < rs) {
+            for (int b = g.m - 1; b >= g.endIndex; --b) cnt_slot(b);
+            n += g.nsib + 1;
+        }
+        for (int b = g.m + 1; n < rs && b < KEYBITS; ++b) cnt_slot(b);
+        return n < rs ? n : rs;
+    }
+
+    // --- the LookupVector: registers (REG, 2R <= 16) or the lane's scratch ---------------------------
+    __device__ __forceinline__ int nh_add(XLookup& L, XRegNh& H, uint32_t x, uint64_t dx) const
+    {
+        const int cap = 2 * C.R;
+        if constexpr (!REG) return vadd(X.nh_idx, X.nh_d, X.nh_used, cap, &L.nnh, x, dx, L.K);
+        // BaseKeySortedVector::add: position = entries closer than x; rejected if present or if the
+        // vector is full and x is farther than its last entry
+        bool dup = false;
+        int pos = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (i < L.nnh) {
+                dup |= H.idx[i] == x;
+                pos += (H.idx[i] != x && cand_lt<EX>(H.d[i], H.idx[i], dx, x, L.K, V.nodes)) ? 1 : 0;
+            }
+        }
+        if (dup || pos >= cap) return -1;
+#pragma unroll
+        for (int i = 15; i >= 1; --i)
+            if (i > pos) { H.idx[i] = H.idx[i - 1]; H.d[i] = H.d[i - 1]; }
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i == pos) { H.idx[i] = x; H.d[i] = dx; }
+        const uint32_t lo = H.used & ((1u << pos) - 1u);
+        H.used = (lo | ((H.used >> pos) << (pos + 1))) & ((1u << cap) - 1u);
+        L.nnh = L.nnh + 1 > cap ? cap : L.nnh + 1;
+        return pos;
+    }
+
+    __device__ __forceinline__ uint32_t nh_idx(const XRegNh& H, int q) const
+    {
+        if constexpr (!REG) return X.nh_idx[at(q)];
+        uint32_t r = NONE;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i == q) r = H.idx[i];
+        return r;
+    }
+
+    // getNextEntry (IterativeLookup.cc:1172-1182): the first entry neither alreadyUsed nor dead; -1
+    __device__ __forceinline__ int nh_next(const XLookup& L, const XRegNh& H) const
+    {
+        if constexpr (!REG) {
+            for (int q = 0; q < L.nnh; ++q)
+                if (!X.nh_used[at(q)] && !(L.nd && is_dead(L, X.nh_idx[at(q)]))) return q;
+            return -1;
+        }
+        uint32_t cand = ~H.used & ((1u << L.nnh) - 1u);
+        while (cand) {
+            const int e = __ffs((int)cand) - 1;
+            if (!L.nd || !is_dead(L, nh_idx(H, e))) return e;
+            cand &= cand - 1u;
+        }
+        return -1;
+    }
+
+    __device__ __forceinline__ void nh_set_used(XRegNh& H, int e) const
+    {
+        if constexpr (!REG) X.nh_used[at(e)] = 1;
+        else H.used |= 1u << e;
+    }
+
+    __device__ __forceinline__ void nh_remove(XLookup& L, XRegNh& H, uint32_t x) const
+    {
+        int q = -1;
+        for (int i = 0; i < L.nnh && q < 0; ++i)
+            if (nh_idx(H, i) == x) q = i;
+        if (q < 0) return;
+        if constexpr (!REG) {
+            for (int j = q; j + 1 < L.nnh; ++j) {
+                X.nh_idx[at(j)] = X.nh_idx[at(j + 1)];
+                X.nh_d[at(j)] = X.nh_d[at(j + 1)];
+                X.nh_used[at(j)] = X.nh_used[at(j + 1)];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 15; ++j)
+                if (j >= q) { H.idx[j] = H.idx[j + 1]; H.d[j] = H.d[j + 1]; }
+            H.used = (H.used & ((1u << q) - 1u)) | ((H.used >> (q + 1)) << q);
+        }
+        --L.nnh;
+    }
+
+    __device__ __forceinline__ bool is_dead(const XLookup& L, uint32_t x) const
     {
         for (int i = 0; i < L.nd; ++i)
             if (X.dead[at(i)] == x) return true;
@@ -155,7 +270,7 @@ struct XCtx {
     // visited = the source and every responder.  Without a timeout no responder can be an unused
     // next hop (an evicted entry is farther than the vector's last and never re-enters while the
     // vector only shrinks by eviction), so the list is scanned only after one.
-    __device__ bool visited(const XLookup& L, uint32_t x) const
+    __device__ __forceinline__ bool visited(const XLookup& L, uint32_t x) const
     {
         if (x == L.S) return true;
         if (!L.any_to) return false;
@@ -165,122 +280,89 @@ struct XCtx {
     }
 
     // IterativeLookup::sendRpc (656-689) + BaseRpc timeout + SimpleNodeEntry::calcDelay
-    __device__ void lookup_send(XLookup& L, uint32_t x) const
+    __device__ __forceinline__ void lookup_send(XLookup& L, uint32_t x) const
     {
-        for (int i = 0; i < C.alpha; ++i)
-            if (((L.pvalid >> i) & 1u) && L.p[i].node == x) { ++L.p[i].ninfo; return; }   // "RPC already sent"
+        // pending slots are indexed by compile-time constants only (a dynamic index would put the
+        // array in private memory)
+        bool dup = false;
+#pragma unroll
+        for (int i = 0; i < XMAXA; ++i)
+            if (((L.pvalid >> i) & 1u) && L.p[i].node == x) { ++L.p[i].ninfo; dup = true; }   // "RPC already sent"
+        if (dup) return;
         int slot = -1;
-        for (int i = C.alpha - 1; i >= 0; --i)
-            if (!((L.pvalid >> i) & 1u)) slot = i;
+#pragma unroll
+        for (int i = XMAXA - 1; i >= 0; --i)
+            if (i < C.alpha && !((L.pvalid >> i) & 1u)) slot = i;
         if (slot < 0) { L.err = true; return; }
-        const int rn = find_node(x, L.K, C.R, slot);
         int64_t d1 = 0, d2 = 0;
         if (x != L.S) {                         // SimpleUDP delivers to itself without delay
-            const double2 xy = V.xy[x];
-            const int64_t cd = coord_ns(L.sx, L.sy, xy.x, xy.y, DC.round);
+            const KadNode rr = load_node(V.nodes, x);
+            const int rn = find_node_size(x, resp_geo(rr, L.K), C.R);
+            const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
             const int64_t bwc = DC.bwCall;
             const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
             L.txf = newTx;
             d1 = (newTx - L.now) + DC.access2 + cd + bwc;
-            const int64_t bwr = rn <= 16 ? DC.bwResp[rn] : bw_ns(DC.respBase + DC.respPerNode * rn, DC.datarate, DC.round);
+            const int64_t bwr = rn == C.R ? C.bwFull : rn == 1 ? C.bwOne
+                                                              : bw_ns(DC.respBase + DC.respPerNode * rn, DC.datarate, DC.round);
             d2 = 2 * bwr + DC.access2 + cd;
         }
         const int64_t tTo = L.now + DC.rpcTimeout;
         const int64_t tResp = L.now + d1 + d2;
-        XPend& P = L.p[slot];
-        P.node = x;
-        P.ninfo = 1;
-        P.rn = rn;
-        P.tsend = L.now;
-        P.to = tTo <= tResp;                    // the timeout was scheduled first: it wins a tie
+        const bool to = tTo <= tResp;           // the timeout was scheduled first: it wins a tie
         const uint32_t sTo = L.seq++, sR = L.seq++;
-        P.seq = P.to ? sTo : sR;
-        P.t = P.to ? tTo : tResp;
-        P.tins = P.to ? L.now : L.now + d1;
+#pragma unroll
+        for (int i = 0; i < XMAXA; ++i) {
+            if (i != slot) continue;
+            XPend& P = L.p[i];
+            P.node = x;
+            P.ninfo = 1;
+            P.tsend = L.now;
+            P.to = to;
+            P.seq = to ? sTo : sR;
+            P.t = to ? tTo : tResp;
+            P.tins = to ? L.now : L.now + d1;
+        }
         L.pvalid |= 1u << slot;
         ++L.nsent;
     }
 
     // IterativePathLookup::sendRpc (1067-1170), exhaustive
-    __device__ void send_rpcs(XLookup& L, int num) const
+    __device__ __forceinline__ void send_rpcs(XLookup& L, XRegNh& H, int num) const
     {
         if (L.pfinished) return;
         if (C.hcm && L.hops >= C.hcm) { L.pfinished = true; L.psuccess = false; return; }
         if (C.strict) num = min(num, C.alpha - L.pending);
         if (num == 0 && L.pending == 0 && !C.finishOnFirst) num = C.alpha;
         for (int i = 0; num > 0 && i < C.R; ++i) {
-            int e = -1;                          // getNextEntry: not alreadyUsed, not dead (1172-1182)
-            for (int q = 0; q < L.nnh && e < 0; ++q)
-                if (!X.nh_used[at(q)] && !(L.nd && is_dead(L, X.nh_idx[at(q)]))) e = q;
+            const int e = nh_next(L, H);
             if (e < 0) break;
-            const uint32_t h = X.nh_idx[at(e)];
+            const uint32_t h = nh_idx(H, e);
             if (!C.visitOnlyOnce || !visited(L, h)) {
                 ++L.pending;
                 --num;
                 lookup_send(L, h);
             }
-            X.nh_used[at(e)] = 1;
+            nh_set_used(H, e);
         }
         if (L.pending == 0) {
             // exhaustive lookups are always successful: addSibling(nextHops[0..R)) -- push_back while
             // the numSiblings-sized vector has room (1147-1156, 436-440)
             int m = L.nnh < C.R ? L.nnh : C.R;
             m = m < C.ns ? m : C.ns;
-            for (int q = 0; q < m; ++q) sib[q] = X.nh_idx[at(q)];
+            if constexpr (REG) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    if (q < m) sib[q] = H.idx[q];
+            } else {
+                for (int q = 0; q < m; ++q) sib[q] = X.nh_idx[at(q)];
+            }
             L.psuccess = true;
             L.pfinished = true;
         }
     }
 
-    // IterativePathLookup::handleTimeout (935-1023), failedNodeRpcs = false
-    __device__ void path_timeout(XLookup& L, uint32_t dest) const
-    {
-        if (L.pfinished) return;
-        if (L.nd && is_dead(L, dest)) {          // exhaustive: a dead node leaves nextHops (948-957)
-            for (int q = 0; q < L.nnh; ++q)
-                if (X.nh_idx[at(q)] == dest) {
-                    for (int j = q; j + 1 < L.nnh; ++j) {
-                        X.nh_idx[at(j)] = X.nh_idx[at(j + 1)];
-                        X.nh_d[at(j)] = X.nh_d[at(j + 1)];
-                        X.nh_used[at(j)] = X.nh_used[at(j + 1)];
-                    }
-                    --L.nnh;
-                    break;
-                }
-        }
-        --L.pending;
-        if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return; }
-        if (C.newOnTimeout) send_rpcs(L, 1);
-        else if (L.pending == 0) send_rpcs(L, C.alpha);
-    }
-
-    // IterativePathLookup::handleResponse (803-921), exhaustive: no siblings flag
-    __device__ void path_response(XLookup& L, uint32_t src, int slot, int rn, int64_t rt) const
-    {
-        if (L.pfinished) return;
-        if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return; }
-        if (src != L.S) {
-            if (L.nhop < C.hcm) {
-                resp[L.nhop] = src;
-                if (rtt) rtt[L.nhop] = rt;
-            }
-            ++L.nhop;
-            ++L.hops;
-        }
-        ++L.step;
-        --L.pending;
-        int numNew = 0;
-        const int base = slot * C.R;
-        for (int i = 0; i < rn; ++i) {
-            const int pos = vadd(X.nh_idx, X.nh_d, X.nh_used, 0, 2 * C.R, &L.nnh, X.res_idx[at(base + i)],
-                                 X.res_d[at(base + i)], L.K);
-            if (pos >= 0 && pos < C.R) ++numNew;
-        }
-        if (numNew == 0 && C.newOnResp) numNew = 1;
-        send_rpcs(L, min(numNew, C.alpha));
-    }
-
-    __device__ void count_finished(XLookup& L) const
+    __device__ __forceinline__ void count_finished(XLookup& L) const
     {
         if (L.pfinished && !L.counted) {
             L.counted = true;
@@ -290,8 +372,8 @@ struct XCtx {
         }
     }
 
-    // checkStop (295-349), parallelPaths = 1, numSiblings = R > 0
-    __device__ bool check_stop(XLookup& L) const
+    // checkStop (295-349), parallelPaths = 1, numSiblings > 0
+    __device__ __forceinline__ bool check_stop(XLookup& L) const
     {
         if (L.finishedPaths == 1 || L.pvalid == 0) {
             L.success = L.successfulPaths >= 1 || L.psuccess;
@@ -300,67 +382,121 @@ struct XCtx {
         return false;
     }
 
-    __device__ void run(XLookup& L) const
+    // The lookup as one loop with a single findNode, LookupVector merge and sendRpc site (the start,
+    // a response and a timeout each reach them through the same code, so each is inlined once):
+    //   start (IterativeLookup::start 133-244): findNode(key, k, -1) at the source, all into nextHops,
+    //     sendRpc(alpha), checkStop;
+    //   per event (handleRpcResponse 488-585 / handleRpcTimeout 588-654): every RpcInfo of the node in
+    //     turn -- the first of a response is handleResponse (803-921), the others and those of a
+    //     timeout handleTimeout (935-1023) -- each possibly followed by a sendRpc, then checkStop.
+    __device__ __forceinline__ void run(XLookup& L) const
     {
-        // IterativeLookup::start (133-244): the source's own findNode(key, k, -1)
-        const int rn0 = find_node(L.S, L.K, C.k, C.alpha);
-        bool done = false;
-        if (rn0 == 0) {
-            L.success = false;
-            done = true;
-        } else {
-            const int base = C.alpha * C.R;
-            for (int i = 0; i < rn0; ++i)
-                vadd(X.nh_idx, X.nh_d, X.nh_used, 0, 2 * C.R, &L.nnh, X.res_idx[at(base + i)], X.res_d[at(base + i)],
-                     L.K);
-            send_rpcs(L, C.alpha);
-            done = check_stop(L);
-        }
-        while (!done && !L.err) {
-            int e = -1;
-            int64_t bt = 0, bi = 0;
-            uint32_t bs = 0;
-            for (int i = 0; i < C.alpha; ++i) {
-                if (!((L.pvalid >> i) & 1u)) continue;
-                const XPend& P = L.p[i];
-                if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
-                    e = i; bt = P.t; bi = P.tins; bs = P.seq;
+        XRegNh H;
+        H.used = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { H.idx[i] = NONE; H.d[i] = ~0ull; }
+        XPend cur;
+        cur.node = L.S; cur.ninfo = 1; cur.to = false; cur.tsend = 0;
+        bool start = true, handled = false;
+        uint32_t infos = 1;
+        while (!L.err) {
+            int num = -1;
+            if (infos == 0) {
+                if (check_stop(L)) break;
+                // the earliest pending event: (time, insertion time, sequence)
+                int e = -1;
+                int64_t bt = 0, bi = 0;
+                uint32_t bs = 0;
+#pragma unroll
+                for (int i = 0; i < XMAXA; ++i) {
+                    if (!((L.pvalid >> i) & 1u)) continue;
+                    const XPend& P = L.p[i];
+                    if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
+                        e = i; bt = P.t; bi = P.tins; bs = P.seq;
+                    }
                 }
+                if (e < 0) break;
+#pragma unroll
+                for (int i = 0; i < XMAXA; ++i)
+                    if (i == e) cur = L.p[i];
+                L.pvalid &= ~(1u << e);
+                L.now = bt;
+                if (cur.to) {
+                    L.any_to = true;                 // setDead(dest)
+                    if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = cur.node;
+                    else { L.err = true; break; }
+                }
+                infos = cur.ninfo;
+                handled = false;
+                continue;
             }
-            if (e < 0) break;
-            const XPend P = L.p[e];
-            L.pvalid &= ~(1u << e);
-            L.now = bt;
-            if (P.to) {
-                // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (588-654)
-                L.any_to = true;
-                if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = P.node;
-                else L.err = true;
-                for (uint32_t q = 0; q < P.ninfo; ++q) {
-                    if (L.pfinished) continue;
-                    path_timeout(L, P.node);
-                    count_finished(L);
+            --infos;
+            if (!start && L.pfinished) continue;     // "do not handle finished paths"
+            if (start || (!cur.to && !handled)) {
+                handled = true;
+                bool merge = true;
+                if (!start) {
+                    // handleResponse (exhaustive: accepted whatever its step)
+                    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; merge = false; }
+                    else {
+                        if (cur.node != L.S) {
+                            if (L.nhop < C.hcm) {
+                                resp[L.nhop] = cur.node;
+                                if (rtt) rtt[L.nhop] = L.now - cur.tsend;
+                            }
+                            ++L.nhop;
+                            ++L.hops;
+                        }
+                        ++L.step;
+                        --L.pending;
+                    }
+                }
+                if (merge) {
+                    // the responder's findNode (the source's own at the start) into nextHops (2R)
+                    const KadNode rn = load_node(V.nodes, cur.node);
+                    const RespGeo g = resp_geo(rn, L.K);
+                    const int rs = start ? C.k : C.R;
+                    int numNew = 0, cnt = 0;
+                    if (REG || rs <= 8) {
+                        Blk8 b;       // the block form of K2 (sorting networks, kad_dev.hpp)
+                        cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            if (i >= cnt) continue;
+                            const int pos = nh_add(L, H, b.x[i], b.d[i]);
+                            numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
+                        }
+                    } else {
+                        cnt = find_node_scratch(cur.node, g, L.K, rs);
+                        for (int i = 0; i < cnt; ++i) {
+                            const int pos = nh_add(L, H, X.res_idx[at(i)], X.res_d[at(i)]);
+                            numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
+                        }
+                    }
+                    if (start) {
+                        if (cnt == 0) { L.success = false; break; }   // no next hops known
+                        num = C.alpha;
+                    } else {
+                        if (numNew == 0 && C.newOnResp) numNew = 1;
+                        num = min(numNew, C.alpha);
+                    }
                 }
             } else {
-                // handleRpcResponse (488-585): exhaustive lookups accept every response
-                bool handled = false;
-                for (uint32_t q = 0; q < P.ninfo; ++q) {
-                    if (L.pfinished) continue;
-                    if (!handled) {
-                        path_response(L, P.node, e, P.rn, L.now - P.tsend);
-                        handled = true;
-                    } else {
-                        path_timeout(L, P.node);
-                    }
-                    count_finished(L);
-                }
+                // handleTimeout (for a timeout, or a response's further RpcInfos)
+                if (L.nd && is_dead(L, cur.node)) nh_remove(L, H, cur.node);   // exhaustive: dead nodes leave nextHops (948-957)
+                --L.pending;
+                if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
+                else if (C.newOnTimeout) num = 1;
+                else if (L.pending == 0) num = C.alpha;
             }
-            done = check_stop(L);
+            if (num >= 0) send_rpcs(L, H, num);
+            if (!start) count_finished(L);
+            start = false;
         }
     }
 };
 
-template <bool EX>
+template <bool EX, bool REG>
 __global__ __launch_bounds__(256) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C, XScratch X,
                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                      uint64_t nq, ovs_route_out* __restrict__ out,
@@ -386,7 +522,7 @@ __global__ __launch_bounds__(256) void k_kad_refresh(KadView V, DelayConsts DC, 
         for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
         uint32_t* resp = resp_out + q * (uint64_t)C.hcm;
         int64_t* rtt = rtt_out ? rtt_out + q * (uint64_t)C.hcm : nullptr;
-        const XCtx<EX> ctx{V, DC, C, X, lane, resp, rtt, sib};
+        const XCtx<EX, REG> ctx{V, DC, C, X, lane, resp, rtt, sib};
         ctx.run(L);
         if (L.err) atomicOr(err, 1u);
         for (int j = L.nhop; j < C.hcm; ++j) {
@@ -499,6 +635,19 @@ __global__ void k_kad_refresh_fill(KadView V, const uint32_t* __restrict__ nodes
     }
 }
 
+// SimTime(double) on the host (the device's simtime_ns; same IEEE double arithmetic)
+int64_t simtime_ns_host(double seconds, int round)
+{
+    const double x = seconds * 1e9;
+    return round ? (int64_t)std::floor(x + 0.5) : (int64_t)x;
+}
+
+// The lanes' scratch, kept per device between calls (a batch synchronises before it returns; the
+// mutex serialises contexts sharing a device)
+std::mutex g_scratch_mu;
+char* g_scratch[64] = {};
+size_t g_scratch_cap[64] = {};
+
 }  // namespace
 
 hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
@@ -519,15 +668,39 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     C.strict = P.lookupStrictParallelRpcs; C.visitOnlyOnce = P.lookupVisitOnlyOnce;
     C.newOnResp = P.lookupNewRpcOnEveryResponse; C.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
     C.finishOnFirst = P.lookupFinishOnFirstUnchanged;
-    // one lane per lookup, up to 1024 lanes per CU; the scratch is sized for the lanes
-    uint64_t lanes = (uint64_t)num_cu * 1024;
+    C.bwFull = simtime_ns_host((double)((int64_t)(DC.respBase + DC.respPerNode * R) * 8) / P.datarate, P.simtimeRound);
+    C.bwOne = DC.bwResp[1];
+    // 2R <= 16: the LookupVector lives in registers and findNode results in sorting-network blocks
+    const bool reg = R <= 8;
+    // one lane per lookup, as many lanes as are resident at once (occupancy-sized grid); the
+    // scratch is sized for the lanes
+    static int bpc[4] = {0, 0, 0, 0};
+    const int ki = (t.exact ? 2 : 0) + (reg ? 1 : 0);
+    if (bpc[ki] == 0) {
+        int b = 0;
+        hipError_t oe;
+        if (t.exact) oe = reg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<true, true>, 256, 0)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<true, false>, 256, 0);
+        else oe = reg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<false, true>, 256, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<false, false>, 256, 0);
+        bpc[ki] = (oe == hipSuccess && b > 0) ? b : 1;
+    }
+    uint64_t lanes = (uint64_t)num_cu * (uint64_t)bpc[ki] * 256;
     if (lanes > nq) lanes = nq;
     lanes = (lanes + 255) / 256 * 256;
-    const uint64_t nhE = 2ull * R, resE = (uint64_t)A * R + (uint64_t)(R > t.k ? R : t.k);
+    const uint64_t nhE = reg ? 0 : 2ull * R, resE = reg ? 0 : (uint64_t)(R > t.k ? R : t.k);
     const uint64_t bytes = lanes * (nhE * (4 + 8 + 1) + resE * (4 + 8) + XMAXDEAD * 4) + 4;
-    char* buf = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&buf), bytes);
-    if (e != hipSuccess) return e;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
+    if (g_scratch_cap[dev] < bytes) {
+        if (g_scratch[dev]) { hipDeviceSynchronize(); hipFree(g_scratch[dev]); }
+        g_scratch[dev] = nullptr; g_scratch_cap[dev] = 0;
+        if ((e = hipMalloc(reinterpret_cast<void**>(&g_scratch[dev]), bytes)) != hipSuccess) return e;
+        g_scratch_cap[dev] = bytes;
+    }
+    char* buf = g_scratch[dev];
     XScratch X;
     char* p = buf;
     X.nh_d = reinterpret_cast<uint64_t*>(p); p += lanes * nhE * 8;
@@ -541,17 +714,15 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     hipMemsetAsync(err, 0, 4, st);
     const unsigned blocks = (unsigned)(lanes / 256);
     ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);   // or ovs_lookup_out (same size)
-    if (t.exact)
-        hipLaunchKernelGGL(k_kad_refresh<true>, dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, qsrc, nq, o, sibs,
-                           responders, rtts, rpcs, err);
-    else
-        hipLaunchKernelGGL(k_kad_refresh<false>, dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, qsrc, nq, o, sibs,
-                           responders, rtts, rpcs, err);
+#define KRL(ex, rg) hipLaunchKernelGGL((k_kad_refresh<ex, rg>), dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, qsrc, \
+                                       nq, o, sibs, responders, rtts, rpcs, err)
+    if (t.exact) { if (reg) KRL(true, true); else KRL(true, false); }
+    else { if (reg) KRL(false, true); else KRL(false, false); }
+#undef KRL
     e = hipGetLastError();
     uint32_t herr = 0;
     hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st);
     const hipError_t e2 = hipStreamSynchronize(st);
-    hipFree(buf);
     if (e == hipSuccess) e = e2;
     *capacity_error = herr != 0;
     return e;
