@@ -286,8 +286,11 @@ struct XCtx {
         // array in private memory)
         bool dup = false;
 #pragma unroll
-        for (int i = 0; i < XMAXA; ++i)
-            if (((L.pvalid >> i) & 1u) && L.p[i].node == x) { ++L.p[i].ninfo; dup = true; }   // "RPC already sent"
+        for (int i = 0; i < XMAXA; ++i) {
+            const bool me = ((L.pvalid >> i) & 1u) && L.p[i].node == x;   // "RPC already sent"
+            L.p[i].ninfo += me ? 1u : 0u;
+            dup |= me;
+        }
         if (dup) return;
         int slot = -1;
 #pragma unroll
@@ -311,17 +314,19 @@ struct XCtx {
         const int64_t tResp = L.now + d1 + d2;
         const bool to = tTo <= tResp;           // the timeout was scheduled first: it wins a tie
         const uint32_t sTo = L.seq++, sR = L.seq++;
+        // unconditional selects per slot: a guarded store would be folded into one store through a
+        // dynamic index, which moves the pending array to private memory
 #pragma unroll
         for (int i = 0; i < XMAXA; ++i) {
-            if (i != slot) continue;
+            const bool me = i == slot;
             XPend& P = L.p[i];
-            P.node = x;
-            P.ninfo = 1;
-            P.tsend = L.now;
-            P.to = to;
-            P.seq = to ? sTo : sR;
-            P.t = to ? tTo : tResp;
-            P.tins = to ? L.now : L.now + d1;
+            P.node = me ? x : P.node;
+            P.ninfo = me ? 1u : P.ninfo;
+            P.tsend = me ? L.now : P.tsend;
+            P.to = me ? to : P.to;
+            P.seq = me ? (to ? sTo : sR) : P.seq;
+            P.t = me ? (to ? tTo : tResp) : P.t;
+            P.tins = me ? (to ? L.now : L.now + d1) : P.tins;
         }
         L.pvalid |= 1u << slot;
         ++L.nsent;
@@ -417,8 +422,13 @@ struct XCtx {
                 }
                 if (e < 0) break;
 #pragma unroll
-                for (int i = 0; i < XMAXA; ++i)
-                    if (i == e) cur = L.p[i];
+                for (int i = 0; i < XMAXA; ++i) {
+                    const bool me = i == e;
+                    cur.node = me ? L.p[i].node : cur.node;
+                    cur.ninfo = me ? L.p[i].ninfo : cur.ninfo;
+                    cur.tsend = me ? L.p[i].tsend : cur.tsend;
+                    cur.to = me ? L.p[i].to : cur.to;
+                }
                 L.pvalid &= ~(1u << e);
                 L.now = bt;
                 if (cur.to) {
@@ -496,8 +506,13 @@ struct XCtx {
     }
 };
 
+#ifndef OVS_KX_WAVES
+// minimum waves per SIMD the register allocator must allow for the register-vector (R <= 8) form
+#define OVS_KX_WAVES 2
+#endif
+
 template <bool EX, bool REG>
-__global__ __launch_bounds__(256) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C, XScratch X,
+__global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C, XScratch X,
                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                      uint64_t nq, ovs_route_out* __restrict__ out,
                                                      uint32_t* __restrict__ sib_out, uint32_t* __restrict__ resp_out,
