@@ -1561,6 +1561,10 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
     lk_setVisited(L, S);
     if (nextHops.size == 0) {
         L->finished = 1; L->success = 0;
+    } else if (L->numSiblings == 0 && ov_isSiblingFor(net, S, S, key, 0, &err)) {
+        /* an exact-key lookup of the source's own key (start() 171-184) */
+        lk_addSibling(L, S);
+        L->success = L->finished = 1;
     } else if (L->numSiblings != 0 && !L->exh && ov_isSiblingFor(net, S, S, key, L->numSiblings, &err)) {
         for (int i = 0; i < nextHops.size; i++) lk_addSibling(L, nextHops.v[i]);
         L->success = L->finished = 1;
@@ -1631,7 +1635,7 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
         if (lout) {
             lout->hops = (uint16_t)L->hops; lout->is_valid = 0; lout->num_siblings = 0; lout->latency_ns = -1;
             lout->status = 5;
-            for (int i = 0; i < numSiblings; ++i) sibs[i] = NONE;
+            for (int i = 0; i < (numSiblings ? numSiblings : 1); ++i) sibs[i] = NONE;
         } else {
             out->hops = (uint16_t)L->hops; out->responsible = NONE; out->status = 5;
             out->one_way_hops = 0; out->latency_ns = -1;
@@ -1656,7 +1660,7 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
         else if (L->ndead > 0) lout->status = 2;
         else if (L->hopCountMax && L->hops >= L->hopCountMax) lout->status = 3;
         else lout->status = 4;
-        for (int i = 0; i < numSiblings; ++i) sibs[i] = (valid && i < L->nsiblings) ? L->siblings[i] : NONE;
+        for (int i = 0; i < (numSiblings ? numSiblings : 1); ++i) sibs[i] = (valid && i < L->nsiblings) ? L->siblings[i] : NONE;
         if (rpcsOut) *rpcsOut = L->rpcsSent;
         free(L->visited);
         free(L);
@@ -1784,7 +1788,8 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     const int maxs = net->type != NET_KAD ? net->p.successorListSize : net->p.s;
     if (numSiblings < 0) numSiblings = maxs;                              /* BaseOverlay.cc:1942-1944 */
     if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
-    if (numSiblings < 1 || numSiblings > 16) { set_err("numSiblings must be 1..16"); return -1; }
+    if (numSiblings < 0 || numSiblings > 16) { set_err("numSiblings must be 0..16"); return -1; }
+    if (numSiblings == 0 && net->type != NET_KAD) { set_err("numSiblings = 0: Kademlia only"); return -1; }
     if (net->p.routingType != 0 && net->p.routingType != 3) { set_err("LookupCall: iterative routing only"); return -1; }
     const int exh = net->p.routingType == 3 ? net->p.lookupRedundantNodes : 0;
     if (exh && (net->type != NET_KAD || numSiblings > exh)) {
@@ -1798,8 +1803,9 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         OKey k = ok_from(&keys[i]);
         orc_route_out dummy;
-        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i], siblings + (size_t)i * numSiblings, exh,
-                   NULL);
+        /* numSiblings = 0 (an exact-key lookup) keeps a one-slot sibling vector (start() 149) */
+        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i],
+                   siblings + (size_t)i * (numSiblings ? numSiblings : 1), exh, NULL);
     }
     (void)nthreads;
     return g_cap_fail ? -1 : numSiblings;

@@ -287,6 +287,7 @@ __device__ __forceinline__ bool kad_is_sibling1(const KadView& V, const KadNode&
 __device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadNode& r, uint32_t c, const K160& K,
                                                int numSiblings)
 {
+    if (numSiblings == 0) return k_eq(as_key(r.key), K);   // exact-key lookups (Kademlia.cc:913-916)
     if (numSiblings <= 1) return kad_is_sibling1(V, r, c, K);
     const int nsib = kad_nsib(r.meta);
     if (nsib < numSiblings) return true;
@@ -344,8 +345,8 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         res.d[0] = dist_hi(node_key(V.nodes, c), K);
         return 1;
     }
-    // resultSize = numSiblings when c is a sibling for K, else numRedundantNodes (Kademlia.cc:1127-1131)
-    const int rs = sib ? numSiblings : numRedundant;
+    // resultSize = numSiblings (1 for 0) when c is a sibling for K, else numRedundantNodes (Kademlia.cc:1127-1131)
+    const int rs = sib ? (numSiblings ? numSiblings : 1) : numRedundant;
     const int cap = rs < 8 ? rs : 8;
     int n = 0, seen = 0;
     auto add_blk = [&](const KadBlk* blk) {
@@ -426,7 +427,7 @@ __device__ __forceinline__ int kad_find_node_ins(const KadView& V, uint32_t c, c
         svec_add<CAP, EX>(res, 1, c, dist_hi(node_key(V.nodes, c), K), K, V.nodes);
         return 1;
     }
-    const int rs = sib ? numSiblings : numRedundant;
+    const int rs = sib ? (numSiblings ? numSiblings : 1) : numRedundant;
     const int cap = rs < CAP ? rs : CAP;
     int seen = 0;
     const uint64_t kt = ktop(K);
@@ -767,7 +768,19 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
             ++L.step;
             --L.pending;
         }
+        if (LK && ns == 0 && start && sb) {
+            // an exact-key lookup of the source's own key (IterativeLookup::start 171-184)
+            L.result = L.S;
+            L.pfinished = true; L.psuccess = true;
+            return true;
+        }
         getres.fill(e, r, rg, sb, numR, start, res);
+        if (LK && ns == 0 && !start && res.n > 0 && k_eq(node_key(V.nodes, res.idx[0]), L.K)) {
+            // the key's node is in the response (handleResponse 862-870): XOR distance 0, so first
+            L.result = res.idx[0];
+            L.pfinished = true; L.psuccess = true;
+            return true;
+        }
         int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
         if (LC.numSiblings != 0 && sb && res.n > 0) {
             if (L.result == NONE) L.result = res.idx[0];
@@ -839,7 +852,7 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
 inline bool kad_params_supported(const ovs_params& P, const KadTables& t)
 {
     return P.lookupParallelRpcs >= 1 && P.lookupParallelRpcs <= MAXA && P.lookupRedundantNodes >= 1 &&
-           P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings >= 1 &&
+           P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings >= 0 &&
            P.numSiblings <= t.s && P.numSiblings <= 8 &&
            t.k <= 8 && P.hopCountMax <= 0x7FFF;
 }

@@ -102,10 +102,14 @@ __global__ __launch_bounds__(256, OVS_KAD_WAVES) void k_kad_route(KadView V, Del
             if (rpcs_out) rpcs_out[q] = L.nsent;
             if (LK) {
                 const bool ok = o.status == OVS_LOOKUP_OK;
-                uint32_t* row = sib_out + q * (uint64_t)LC.numSiblings;
+                if (LC.numSiblings == 0) {
+                    sib_out[q] = ok ? L.result : NONE;    // the one-slot vector of an exact-key lookup
+                } else {
+                    uint32_t* row = sib_out + q * (uint64_t)LC.numSiblings;
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j < LC.numSiblings) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
+                    for (int j = 0; j < 8; ++j)
+                        if (j < LC.numSiblings) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
+                }
             }
             active = false;
         }

@@ -981,7 +981,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     const int32_t maxs = chord ? c->P.successorListSize : c->P.s;
     const int32_t ns = num_siblings < 0 ? maxs : num_siblings;
     if (ns > maxs) return fail(c, OVS_EINVAL, "numSiblings too big!");
-    if (ns == 0) return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup) not implemented");
+    if (ns == 0 && (chord || c->P.routingType != 0))
+        return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup) is implemented for iterative Kademlia");
     if (ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall implements numSiblings <= 8");
     ovs_params P = c->P;
     P.numSiblings = 1;          // the route checks: one-way configuration, numSiblings applied below
@@ -1007,6 +1008,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     }
     if (n == 0) return OVS_OK;
     P.numSiblings = ns;
+    const int nslots = ns ? ns : 1;      // an exact-key lookup keeps a one-slot sibling vector (IterativeLookup.cc:149)
     DelayConsts DC = delay_consts(P);
     DC.lookupCall = 1;
     if (chord && c->ideal) {
@@ -1025,7 +1027,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         st = to_device(c, src, n, false, &ds, &ok_s);
         if (st != OVS_OK) { hipFree(dk); return st; }
         HIPCHK(c, hipMalloc(&dout, sizeof(ovs_route_out) * n));
-        HIPCHK(c, hipMalloc(&dsib, sizeof(uint32_t) * n * ns));
+        HIPCHK(c, hipMalloc(&dsib, sizeof(uint32_t) * n * nslots));
     } else {
         dk = const_cast<K160*>(reinterpret_cast<const K160*>(keys));
         ds = const_cast<uint32_t*>(src);
@@ -1052,7 +1054,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
                       dsib);
     }
-    if (e == hipSuccess && !kad_exh) e = launch_lookup_finish(chord_view(c), chord, c->ideal, ns, dout, dsib, n, s);
+    if (e == hipSuccess && !kad_exh) e = launch_lookup_finish(chord_view(c), chord, c->ideal, nslots, dout, dsib, n, s);
     if (e != hipSuccess) {
         if (!dev) { hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib); }
         if (dhop) hipFree(dhop);
@@ -1060,7 +1062,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     }
     if (!dev) {
         HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(ovs_lookup_out) * n, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(siblings, dsib, sizeof(uint32_t) * n * ns, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(siblings, dsib, sizeof(uint32_t) * n * nslots, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib);
     } else if (dhop) {

@@ -390,6 +390,8 @@ class KadTables:
         return [int(x) for x in self.sib[c] if x != 0xFFFFFFFF]
 
     def is_sibling_for(self, c, key, num_siblings=1):
+        if num_siblings == 0:                      # exact-key lookups (Kademlia.cc:913-916)
+            return self.ids[c] == key
         sib = self.siblings(c)
         if len(sib) < num_siblings:
             return True
@@ -593,6 +595,10 @@ class KadLookupSim:
             pos = self._nh_add(h)
             if 0 <= pos < self.R:
                 new += 1
+            if self.num_siblings == 0 and self.T.ids[h] == self.key:   # the key's node found (862-870)
+                self.siblings = [h]
+                self.pfinished, self.psuccess = True, True
+                return
             if self.num_siblings and not self.exh and sib_flag:
                 self._add_sibling(h)
         if not self.exh and sib_flag and closest and self.num_siblings:
@@ -604,7 +610,8 @@ class KadLookupSim:
 
     def _check_stop(self):
         """IterativeLookup::checkStop (295-349), numSiblings > 0, retries = 0."""
-        if (self.finished_paths == 1 and self.num_siblings > 0) or not self.rpcs:
+        if (self.successful_paths >= 1 and self.num_siblings == 0 and self.siblings) or \
+                (self.finished_paths == 1 and self.num_siblings > 0) or not self.rpcs:
             self.success |= self.psuccess or self.successful_paths >= 1
             self.running = False
             self.finished = True
@@ -635,6 +642,9 @@ class KadLookupSim:
         done = False
         if not nxt:
             self.finished, self.success, done = True, False, True
+        elif num_siblings == 0 and T.ids[S] == self.key:     # exact-key lookup of the own key (171-184)
+            self.siblings = [S]
+            self.finished = self.success = done = True
         elif num_siblings and not self.exh and T.is_sibling_for(S, self.key, num_siblings):
             for h in nxt:
                 self._add_sibling(h)

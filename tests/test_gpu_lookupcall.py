@@ -114,7 +114,7 @@ def test_lookup_call_rejects(engine: KbrEngine):
     with pytest.raises(KbrError):
         engine.lookupCall(keys, src, 9)                # numSiblings too big!
     with pytest.raises(KbrError):
-        engine.lookupCall(keys, src, 0)                # exact-key lookups: not implemented
+        engine.lookupCall(keys, src, 0)                # exact-key lookups: Kademlia only
     engine.set_params(Params.chord().replace(routingType=1))
     with pytest.raises(KbrError):
         engine.lookupCall(keys, src)
@@ -139,3 +139,27 @@ def test_lookup_call_full_batch_properties(engine: KbrEngine):
     assert np.array_equal(g["siblings"], ((R[:, None] + np.arange(8)[None, :]) % (1 << 18)).astype(np.uint32))
     r = engine.lookup(keys, src)
     assert np.array_equal(r["hops"], g["hops"])
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+def test_kademlia_exact_key_lookup_calls(engine, alpha):
+    """numSiblings = 0 (IterativeLookup.cc:149, 171-184, 313, 862-870): node-ID keys are found, own
+    keys answer at once, random keys fail -- every field as the oracle."""
+    from oversim_amd import workload as W2
+    from oracle_lib import OracleNet as ON, kad_params as kp
+    net = W2.population(3000, 0xE7)
+    p = Params.kademlia()
+    p.lookupParallelRpcs = alpha
+    engine.set_params(p)
+    engine.kad_load(net.ids, net.xy)
+    o = ON("kademlia", net.ids, net.xy, kp(lookupParallelRpcs=alpha))
+    k1, s1 = W2.lookups(net.ids, 3000, 91 + alpha, node_ids=True)
+    k2, s2 = W2.lookups(net.ids, 1000, 95 + alpha, node_ids=False)
+    keys = np.concatenate([k1, k2, net.ids[:64]])
+    src = np.concatenate([s1, s2, np.arange(64, dtype=np.uint32)])
+    r = engine.lookupCall(keys, src, 0)
+    e = o.lookup_call(keys, src, 0)
+    for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+        assert np.array_equal(r[f], e[f]), f
+    assert np.array_equal(r["siblings"], e["siblings"])
+    assert r["is_valid"][:3000].mean() > 0.99 and r["is_valid"][-64:].all() and not r["is_valid"][3000:4000].any()

@@ -181,3 +181,26 @@ def test_exhaustive_routing_type_agrees(net, alpha):
         assert int(c["is_valid"][i]) == m["is_valid"] and int(c["hops"][i]) == m["hops"], i
         assert int(c["latency_ns"][i]) == m["latency_ns"], i
         assert [int(x) for x in c["siblings"][i][: len(m["siblings"])]] == m["siblings"], i
+
+
+@pytest.mark.parametrize("alpha", [1, 3])
+def test_exact_key_lookup_calls_agree(net, alpha):
+    """LookupCalls with numSiblings = 0 (IterativeLookup.cc:149, 171-184, 313, 862-870): the lookup
+    ends at the first response carrying the key's node; keys no node holds fail."""
+    p = kad_params(lookupParallelRpcs=alpha)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    k1, s1 = W.lookups(net.ids, 150, 51 + alpha, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 50, 61 + alpha, node_ids=False)
+    keys, src = np.concatenate([k1, k2, net.ids[:5]]), np.concatenate([s1, s2, np.arange(5, dtype=np.uint32)])
+    r = o.lookup_call(keys, src, 0)
+    valid = 0
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]), num_siblings=0, lookup_call=True)
+        assert int(r["is_valid"][i]) == m["is_valid"], i
+        assert int(r["status"][i]) == m["status"], i
+        assert int(r["hops"][i]) == m["hops"], i
+        assert int(r["latency_ns"][i]) == m["latency_ns"], i
+        assert [int(x) for x in r["siblings"][i][: len(m["siblings"])]] == m["siblings"], i
+        valid += m["is_valid"]
+    assert 150 <= valid < len(keys)      # node-ID keys and own keys found, random keys not
