@@ -119,6 +119,25 @@ def build_engine(verbose: bool = False) -> Path:
     return LIB
 
 
+C_CONSUMER = ROOT / "tests" / "c_consumer"
+
+
+def build_c_consumer(verbose: bool = False) -> Path:
+    """tests/c_consumer/route_batch: a gcc-built C program against include/ovs_kbr.h, linked to the
+    engine library (RUNPATH next to it) -- the ABI as an OverSim-side C/C++ adapter calls it."""
+    src, exe = C_CONSUMER / "route_batch.c", C_CONSUMER / "route_batch"
+    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-I", str(ROOT / "include"), str(src),
+           "-L", str(LIB.parent), "-lovs_kbr", "-Wl,-rpath,$ORIGIN/../../oversim_amd",
+           "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)]
+    d = _digest([src, ROOT / "include" / "ovs_kbr.h"], " ".join(cmd))
+    if not _stamp_ok(exe, d):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        _write_stamp(exe, d)
+    return exe
+
+
 def build_oracle(verbose: bool = False) -> Path:
     cmd = ["make", "-s", "-C", str(ORACLE)]
     if verbose:
@@ -131,6 +150,7 @@ def main() -> int:
     v = "-v" in sys.argv
     print(build_engine(v))
     print(build_oracle(v))
+    print(build_c_consumer(v))
     return 0
 
 
