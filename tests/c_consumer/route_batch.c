@@ -56,7 +56,11 @@ int main(int argc, char** argv)
     uint32_t* src = (uint32_t*)xread(f, sizeof(uint32_t) * m);
     uint32_t ini_len;
     if (fread(&ini_len, 4, 1, f) != 1) return 2;
-    char* ini = (char*)xread(f, ini_len + 1);
+    char* ini = (char*)malloc((size_t)ini_len + 1);
+    if (!ini || fread(ini, 1, ini_len, f) != ini_len) {
+        fprintf(stderr, "route_batch: short input\n");
+        return 2;
+    }
     ini[ini_len] = 0;
     fclose(f);
 
