@@ -219,6 +219,31 @@ typedef struct ovs_fixfingers_stats {
 ovs_status  ovs_chord_fix_fingers(ovs_ctx* ctx, const uint32_t* nodes, uint64_t m,
                                   ovs_fixfingers_stats* stats);
 
+/* One synchronous stabilize round for the listed nodes of an explicit-table
+ * ring (Chord::handleStabilizeTimerExpired -> StabilizeCall, Chord.cc:793-842,
+ * 1055-1104; NotifyCall / rpcNotify / handleRpcNotifyResponse, 1106-1225;
+ * ChordSuccessorList::addSuccessor / updateList / removeOldSuccessors,
+ * ChordSuccessorList.cc:101-194; mergeOptimizationL1-L4 = false, no failed
+ * nodes).  Every listed node v asks its successor s for its predecessor p,
+ * takes p as successor when p lies in (v, s), notifies the successor t, which
+ * makes v its predecessor when v lies in (pred(t), t), and replaces its list
+ * by t and t's successors.  All messages of the round see the tables as they
+ * stand at its start (the reference fires the nodes' timers at different
+ * times); successor-list entries count as settled at the start (newEntry =
+ * false).  Fingers whose resolution falls back to a changed successor follow;
+ * ovs_chord_fix_fingers then repairs the fingers -- alternating the two is the
+ * convergence of a ring after joins.  Host buffers; stats may be NULL. */
+typedef struct ovs_stabilize_stats {
+    uint64_t nodes;          /* nodes that stabilised */
+    uint64_t succ_changed;   /* successors (list position 0) that changed */
+    uint64_t lists_changed;  /* successor lists that changed */
+    uint64_t pred_changed;   /* predecessors set by a NotifyCall */
+} ovs_stabilize_stats;
+ovs_status  ovs_chord_stabilize(ovs_ctx* ctx, const uint32_t* nodes, uint64_t m, ovs_stabilize_stats* stats);
+/* the explicit tables as they now stand (host buffers): pred[n], succ[n*successorListSize]
+ * (0xFFFFFFFF padded), nsucc[n] */
+ovs_status  ovs_chord_export_tables(ovs_ctx* ctx, uint32_t* pred, uint32_t* succ, uint8_t* nsucc);
+
 /* Batched iterative lookups: lookup i routes keys[i] from node src[i]
  * (KBRTestApp one-way test: createDestKey -> callRoute -> sendToKey ->
  * IterativeLookup -> sendRouteMessage).  hop_seq may be NULL, else

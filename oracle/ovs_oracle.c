@@ -1875,6 +1875,116 @@ uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_
 }
 
 /* ======================================================================== */
+/* One synchronous stabilize round (Chord::handleStabilizeTimerExpired,      */
+/* Chord.cc:793-842; rpcStabilize / handleRpcStabilizeResponse 1055-1104;   */
+/* rpcNotify / handleRpcNotifyResponse 1106-1225; mergeOptimizationL1-L4 off, */
+/* no failed nodes).  Every message sees the tables of the round's start.    */
+/* ======================================================================== */
+/* ChordSuccessorList (ChordSuccessorList.cc): a map keyed by succ - (self + 1), newEntry flags */
+typedef struct { OKey key[64]; uint32_t node[64]; int fresh[64]; int size; } SuccMap;
+
+static void sm_add(const orc_net* net, SuccMap* m, uint32_t self, uint32_t x, int resize, int sls)  /* 122-151 */
+{
+    OKey one = ok_small(1);
+    OKey base = ok_add(net->ids[self], &one);
+    OKey k = ok_sub(net->ids[x], &base);
+    int i;
+    for (i = 0; i < m->size; ++i)
+        if (EQ(&m->key[i], &k)) {                       /* successorMap.erase(it) */
+            memmove(&m->key[i], &m->key[i + 1], sizeof(OKey) * (size_t)(m->size - i - 1));
+            memmove(&m->node[i], &m->node[i + 1], sizeof(uint32_t) * (size_t)(m->size - i - 1));
+            memmove(&m->fresh[i], &m->fresh[i + 1], sizeof(int) * (size_t)(m->size - i - 1));
+            m->size--;
+            break;
+        }
+    for (i = 0; i < m->size && ok_cmp(&m->key[i], &k) < 0; ++i) {}
+    if (m->size == 64) { cap_error("successor map over 64 entries"); return; }
+    memmove(&m->key[i + 1], &m->key[i], sizeof(OKey) * (size_t)(m->size - i));
+    memmove(&m->node[i + 1], &m->node[i], sizeof(uint32_t) * (size_t)(m->size - i));
+    memmove(&m->fresh[i + 1], &m->fresh[i], sizeof(int) * (size_t)(m->size - i));
+    m->key[i] = k; m->node[i] = x; m->fresh[i] = 1; m->size++;
+    if (resize && m->size > sls) m->size--;             /* erase the last (farthest) entry */
+}
+
+static void sm_removeOld(const orc_net* net, SuccMap* m, uint32_t self, int sls)                 /* 170-194 */
+{
+    int w = 0;
+    for (int i = 0; i < m->size; ++i) {
+        if (!m->fresh[i]) continue;
+        m->key[w] = m->key[i]; m->node[w] = m->node[i]; m->fresh[w] = 0; ++w;
+    }
+    m->size = w;
+    if (m->size > sls) m->size = sls;
+    if (m->size == 0) sm_add(net, m, self, self, 1, sls);
+}
+
+uint64_t orc_chord_stabilize(orc_net* net, const uint32_t* nodes, uint64_t m, uint64_t* out_succ_changed,
+                             uint64_t* out_pred_changed)
+{
+    if (net->type != NET_CHORD || net->lazy || !net->pred) { set_err("stabilize: explicit Chord tables"); return ORC_FAIL; }
+    const uint32_t n = net->n, sls = net->sls;
+    uint32_t* pred0 = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    uint32_t* succ0 = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sls);
+    uint8_t* nsucc0 = (uint8_t*)malloc(n);
+    memcpy(pred0, net->pred, sizeof(uint32_t) * n);
+    memcpy(succ0, net->succ, sizeof(uint32_t) * (size_t)n * sls);
+    memcpy(nsucc0, net->nsucc, n);
+    uint32_t* tgt = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint64_t lists = 0, sch = 0, pch = 0;
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        SuccMap L; L.size = 0;
+        for (int q = 0; q < nsucc0[v]; ++q) {           /* the list as it stands: entries settled */
+            sm_add(net, &L, v, succ0[(size_t)v * sls + q], 0, (int)sls);
+            L.fresh[L.size - 1] = 0;
+        }
+        for (int q = 0; q < L.size; ++q) L.fresh[q] = 0;
+        /* handleRpcStabilizeResponse: the successor's predecessor */
+        const uint32_t s = L.node[0];
+        const uint32_t p = pred0[s];
+        if (p != NONE && ok_isBetween(&net->ids[p], &net->ids[v], &net->ids[s]))
+            sm_add(net, &L, v, p, 1, (int)sls);
+        /* NotifyCall to successorList->getSuccessor(); its response carries t's list (sucNum) */
+        const uint32_t t = L.node[0];
+        tgt[j] = t;
+        /* handleRpcNotifyResponse -> updateList (101-119) */
+        sm_add(net, &L, v, t, 0, (int)sls);
+        for (uint32_t k = 0; k < nsucc0[t] && k < sls - 1; ++k) {
+            const uint32_t x = succ0[(size_t)t * sls + k];
+            if (ok_isBetweenLR(&net->ids[x], &net->ids[v], &net->ids[t])) continue;
+            sm_add(net, &L, v, x, 0, (int)sls);
+        }
+        sm_removeOld(net, &L, v, (int)sls);
+        int same = L.size == nsucc0[v];
+        for (int q = 0; same && q < L.size; ++q) same = L.node[q] == succ0[(size_t)v * sls + q];
+        lists += !same;
+        sch += L.node[0] != succ0[(size_t)v * sls];
+        for (uint32_t q = 0; q < sls; ++q) net->succ[(size_t)v * sls + q] = (int)q < L.size ? L.node[q] : NONE;
+        net->nsucc[v] = (uint8_t)L.size;
+    }
+    /* rpcNotify (1106-1161), one call after the other in the listed order */
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t t = tgt[j], v = nodes[j];
+        const uint32_t cur = net->pred[t];
+        if (cur == NONE || ok_isBetween(&net->ids[v], &net->ids[cur], &net->ids[t])) {
+            if (cur == NONE || v != cur) net->pred[t] = v;
+        }
+    }
+    for (uint32_t t = 0; t < n; ++t) pch += net->pred[t] != pred0[t];
+    free(pred0); free(succ0); free(nsucc0); free(tgt);
+    if (out_succ_changed) *out_succ_changed = sch;
+    if (out_pred_changed) *out_pred_changed = pch;
+    return g_cap_fail ? ORC_FAIL : lists;
+}
+
+void orc_chord_export_lists(const orc_net* net, uint32_t* pred, uint32_t* succ, uint8_t* nsucc)
+{
+    memcpy(pred, net->pred, sizeof(uint32_t) * net->n);
+    memcpy(succ, net->succ, sizeof(uint32_t) * (size_t)net->n * net->sls);
+    memcpy(nsucc, net->nsucc, net->n);
+}
+
+/* ======================================================================== */
 /* One synchronous fixfingers round (Chord::handleFixFingersTimerExpired,   */
 /* Chord.cc:845-875; rpcFixfingers / handleRpcFixfingersResponse,           */
 /* Chord.cc:1228-1270, extendedFingerTable = false) for a list of nodes:     */

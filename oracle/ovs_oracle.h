@@ -178,6 +178,13 @@ int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint
 uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
                               orc_key* keys, uint32_t* src, uint64_t cap);
 
+/* One synchronous stabilize round for nodes[0..m) on explicit tables (Chord.cc:793-842, 1055-1225,
+ * ChordSuccessorList.cc:101-194): returns the number of successor lists that changed (ORC_FAIL on
+ * error), *succ_changed the successors that changed, *pred_changed the predecessors set. */
+uint64_t orc_chord_stabilize(orc_net* net, const uint32_t* nodes, uint64_t m, uint64_t* succ_changed,
+                             uint64_t* pred_changed);
+void orc_chord_export_lists(const orc_net* net, uint32_t* pred, uint32_t* succ, uint8_t* nsucc);
+
 /* One synchronous fixfingers round for nodes[0..m) (Chord.cc:845-875, 1228-1270): trivial
  * fingers removed, then lookups of n + 2^i routed over the tables, then finger i := result.
  * Explicit or converged networks.  Returns total hops; *out_ok successful lookups,

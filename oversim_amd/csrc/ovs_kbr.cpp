@@ -51,6 +51,9 @@ struct ovs_ctx {
     std::vector<uint8_t> h_fsize;       // deque sizes
     std::vector<uint32_t> h_succ0;      // successorList->getSuccessor()
     std::vector<uint32_t> h_fres;       // n * 160 resolved getFinger(pos)
+    std::vector<uint32_t> h_pred;       // predecessorNode (ovs_chord_stabilize)
+    std::vector<uint32_t> h_succ;       // n * sls successor lists
+    std::vector<uint8_t> h_nsucc;
     uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     std::vector<uint64_t> h_bounds;         // ... as last uploaded (uploaded again only on a change)
@@ -106,6 +109,7 @@ void free_tables(ovs_ctx* c)
     c->kvis = nullptr; c->kvis_cap = 0;
     c->overlay = 0; c->n = 0; c->nfing = 0;
     c->h_ids.clear(); c->h_deque.clear(); c->h_fsize.clear(); c->h_succ0.clear(); c->h_fres.clear();
+    c->h_pred.clear(); c->h_succ.clear(); c->h_nsucc.clear();
 }
 
 void free_kad_shard(ovs_ctx* c)
@@ -497,6 +501,9 @@ ovs_status ovs_chord_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, 
             if (succ[v * sls + j] >= n) return fail(c, OVS_EINVAL, "successor index out of range");
         resolve_row(c, v);
     }
+    c->h_pred.assign(pred, pred + n);
+    c->h_succ.assign(succ, succ + n * sls);
+    c->h_nsucc.assign(nsucc, nsucc + n);
     const std::vector<uint32_t>& fres = c->h_fres;
     HIPCHK(c, hipMalloc(&c->pred, sizeof(uint32_t) * n));
     HIPCHK(c, hipMalloc(&c->succ, sizeof(uint32_t) * n * sls));
@@ -601,6 +608,101 @@ ovs_status ovs_chord_fix_fingers(ovs_ctx* c, const uint32_t* nodes, uint64_t m, 
     st = upload_rows();
     if (st != OVS_OK) return st;
     if (stats) { stats->lookups = keys.size(); stats->ok = ok; stats->changed = changed; stats->hops = hops; }
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_stabilize(ovs_ctx* c, const uint32_t* nodes, uint64_t m, ovs_stabilize_stats* stats)
+{
+    if (!c || (m && !nodes)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "no Chord network loaded");
+    if (c->ideal) return fail(c, OVS_ESTATE, "stabilize rounds run on explicit tables (ovs_chord_load_tables)");
+    const uint64_t n = c->n;
+    const int sls = c->sls;
+    for (uint64_t j = 0; j < m; ++j)
+        if (nodes[j] >= n) return fail(c, OVS_EINVAL, "node index out of range");
+    const std::vector<K160>& id = c->h_ids;
+    // every message of the round sees the tables as they stand at its start (as ovs_chord_fix_fingers)
+    std::vector<uint32_t> nl((size_t)m * sls, 0xFFFFFFFFu), tgt(m);
+    std::vector<uint8_t> nn(m);
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        const uint32_t s = c->h_succ[(size_t)v * sls];
+        // handleRpcStabilizeResponse (Chord.cc:1072-1104): the successor's predecessor p becomes
+        // the successor when p lies in (v, s); NotifyCall to the (new) successor t
+        const uint32_t p = c->h_pred[s];
+        const uint32_t t = (p != 0xFFFFFFFFu && between_open(id[p], id[v], id[s])) ? p : s;
+        tgt[j] = t;
+        // handleRpcNotifyResponse -> ChordSuccessorList::updateList (ChordSuccessorList.cc:101-119):
+        // t, then t's successors outside [v, t], at most successorListSize - 1 of them looked at;
+        // every entry not re-added is dropped (removeOldSuccessors, 170-194)
+        uint32_t* row = nl.data() + (size_t)j * sls;
+        int k = 0;
+        row[k++] = t;
+        const int ts = std::min<int>(c->h_nsucc[t], sls - 1);
+        for (int q = 0; q < ts; ++q) {
+            const uint32_t x = c->h_succ[(size_t)t * sls + q];
+            if (!between_LR(id[x], id[v], id[t])) row[k++] = x;
+        }
+        nn[j] = (uint8_t)k;
+    }
+    // rpcNotify at t (1106-1189): the caller becomes t's predecessor when it lies in (pred, t); over
+    // the round's callers that leaves the one nearest t (every acceptance moves pred closer), if
+    // it is in (pred0, t)
+    std::vector<uint32_t> best(n, 0xFFFFFFFFu);
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t t = tgt[j], v = nodes[j];
+        if (best[t] == 0xFFFFFFFFu || k_lt(k_sub(id[t], id[v]), k_sub(id[t], id[best[t]]))) best[t] = v;
+    }
+    uint64_t pred_changed = 0, succ_changed = 0, lists_changed = 0;
+    std::vector<uint32_t> changed_succ0;
+    for (uint64_t t = 0; t < n; ++t) {
+        const uint32_t b = best[t];
+        if (b == 0xFFFFFFFFu) continue;
+        const uint32_t p0 = c->h_pred[t];
+        if ((p0 == 0xFFFFFFFFu || between_open(id[b], id[p0], id[t])) && b != p0) {
+            c->h_pred[t] = b;
+            ++pred_changed;
+        }
+    }
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        uint32_t* row = c->h_succ.data() + (size_t)v * sls;
+        const bool same = nn[j] == c->h_nsucc[v] && std::equal(row, row + nn[j], nl.data() + (size_t)j * sls);
+        if (!same) ++lists_changed;
+        if (row[0] != nl[(size_t)j * sls]) { ++succ_changed; changed_succ0.push_back(v); }
+        std::copy(nl.data() + (size_t)j * sls, nl.data() + (size_t)(j + 1) * sls, row);
+        c->h_nsucc[v] = nn[j];
+        c->h_succ0[v] = row[0];
+    }
+    // upload: the lists, the predecessors, and the resolved finger rows whose successor changed
+    // (getFinger falls back to the successor, ChordFingerTable.cc:174-193)
+    HIPCHK(c, hipSetDevice(c->device));
+    for (uint32_t v : changed_succ0) resolve_row(c, v);
+    HIPCHK(c, hipMemcpy(c->pred, c->h_pred.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->succ, c->h_succ.data(), sizeof(uint32_t) * n * sls, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->nsucc, c->h_nsucc.data(), n, hipMemcpyHostToDevice));
+    if (changed_succ0.size() * 8 >= n) {
+        HIPCHK(c, hipMemcpy(c->fres, c->h_fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
+    } else {
+        for (uint32_t v : changed_succ0)
+            HIPCHK(c, hipMemcpy(c->fres + (uint64_t)v * 160, c->h_fres.data() + (uint64_t)v * 160,
+                                sizeof(uint32_t) * 160, hipMemcpyHostToDevice));
+    }
+    if (stats) {
+        stats->nodes = m; stats->succ_changed = succ_changed; stats->lists_changed = lists_changed;
+        stats->pred_changed = pred_changed;
+    }
+    return OVS_OK;
+}
+
+ovs_status ovs_chord_export_tables(ovs_ctx* c, uint32_t* pred, uint32_t* succ, uint8_t* nsucc)
+{
+    if (!c || !pred || !succ || !nsucc) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD || c->ideal)
+        return fail(c, OVS_ESTATE, "explicit Chord tables (ovs_chord_load_tables) needed");
+    std::copy(c->h_pred.begin(), c->h_pred.end(), pred);
+    std::copy(c->h_succ.begin(), c->h_succ.end(), succ);
+    std::copy(c->h_nsucc.begin(), c->h_nsucc.end(), nsucc);
     return OVS_OK;
 }
 

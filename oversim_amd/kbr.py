@@ -202,6 +202,8 @@ def lib() -> C.CDLL:
         "ovs_kbrtest_stats_batch": ([vp, vp, vp, vp, u64, C.c_double, i32, vp, u32, vp], C.c_int),
         "ovs_chord_fix_fingers": ([vp, vp, u64, vp], C.c_int),
         "ovs_lookup_batch": ([vp, vp, vp, u64, i32, vp, vp, u32, vp], C.c_int),
+        "ovs_chord_stabilize": ([vp, vp, u64, vp], C.c_int),
+        "ovs_chord_export_tables": ([vp, vp, vp, vp], C.c_int),
         "ovs_kad_refresh_batch": ([vp, vp, vp, u64, i32, vp, vp, vp, vp, vp, u32, vp], C.c_int),
         "ovs_kad_refresh_keys": ([vp, vp, u64, vp, vp, vp, u64, C.POINTER(u64), u32, vp], C.c_int),
         "ovs_kbrtest_lookup_stats_batch": ([vp, vp, vp, i32, vp, vp, u64, C.c_double, i32, C.c_double, vp, u32, vp],
@@ -240,6 +242,13 @@ class FixFingersStats(C.Structure):
     """ovs_fixfingers_stats: one fixfingers round (ovs_chord_fix_fingers)."""
 
     _fields_ = [("lookups", C.c_uint64), ("ok", C.c_uint64), ("changed", C.c_uint64), ("hops", C.c_uint64)]
+
+
+class StabilizeStats(C.Structure):
+    """ovs_stabilize_stats: one stabilize round (ovs_chord_stabilize)."""
+
+    _fields_ = [("nodes", C.c_uint64), ("succ_changed", C.c_uint64), ("lists_changed", C.c_uint64),
+                ("pred_changed", C.c_uint64)]
 
 
 class KbrTestLookupStats(C.Structure):
@@ -406,6 +415,25 @@ class KbrEngine:
         self._chk(self._L.ovs_chord_fix_fingers(self._h, _ptr(nodes), len(nodes), C.cast(C.byref(st), C.c_void_p)),
                   "ovs_chord_fix_fingers")
         return {f: getattr(st, f) for f, _ in FixFingersStats._fields_}
+
+    def chord_stabilize(self, nodes=None) -> dict:
+        """One synchronous stabilize round on an explicit-table ring (ovs_chord_stabilize): successor's
+        predecessor, notify, successor-list update (Chord.cc:793-842, 1055-1225)."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        st = StabilizeStats()
+        self._chk(self._L.ovs_chord_stabilize(self._h, _ptr(nodes), len(nodes), C.cast(C.byref(st), C.c_void_p)),
+                  "ovs_chord_stabilize")
+        return {f: getattr(st, f) for f, _ in StabilizeStats._fields_}
+
+    def chord_tables(self):
+        """(pred, succ (n, successorListSize), nsucc) of an explicit-table ring as they now stand."""
+        sls = self.get_params().successorListSize
+        pred = np.empty(self.n, dtype=np.uint32)
+        succ = np.empty((self.n, sls), dtype=np.uint32)
+        nsucc = np.empty(self.n, dtype=np.uint8)
+        self._chk(self._L.ovs_chord_export_tables(self._h, _ptr(pred), _ptr(succ), _ptr(nsucc)),
+                  "ovs_chord_export_tables")
+        return pred, succ, nsucc
 
     def kad_tables(self):
         p = self.get_params()

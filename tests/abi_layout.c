@@ -60,6 +60,10 @@ int main(void)
     F(ovs_fixfingers_stats, lookups); F(ovs_fixfingers_stats, ok); F(ovs_fixfingers_stats, changed);
     F(ovs_fixfingers_stats, hops);
     end();
+    S(ovs_stabilize_stats);
+    F(ovs_stabilize_stats, nodes); F(ovs_stabilize_stats, succ_changed); F(ovs_stabilize_stats, lists_changed);
+    F(ovs_stabilize_stats, pred_changed);
+    end();
     S(ovs_stddev);
     F(ovs_stddev, count); F(ovs_stddev, mean); F(ovs_stddev, stddev); F(ovs_stddev, min); F(ovs_stddev, max);
     end();

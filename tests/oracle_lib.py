@@ -92,6 +92,8 @@ def lib() -> C.CDLL:
             ("orc_kbrtest_stats", [vp, vp, vp, vp, u64, C.c_double, C.c_int, i32, vp], None),
             ("orc_chord_fix_fingers", [vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.c_int], u64),
             ("orc_lookup_batch", [vp, vp, vp, u64, C.c_int, vp, vp, C.c_int], C.c_int),
+            ("orc_chord_stabilize", [vp, vp, u64, C.POINTER(u64), C.POINTER(u64)], u64),
+            ("orc_chord_export_lists", [vp, vp, vp, vp], None),
             ("orc_kad_exhaustive_batch", [vp, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp, C.c_int], C.c_int),
             ("orc_kad_refresh_keys", [vp, vp, u64, vp, vp, vp, u64], u64),
             ("orc_kbrtest_lookup_stats", [vp, vp, vp, C.c_int, vp, vp, u64, C.c_double, C.c_int, C.c_double, vp],
@@ -314,6 +316,23 @@ class OracleNet:
         ok, ch = C.c_uint64(0), C.c_uint64(0)
         hops = lib().orc_chord_fix_fingers(self._h, _p(nodes), len(nodes), C.byref(ok), C.byref(ch), nthreads)
         return {"hops": int(hops), "ok": ok.value, "changed": ch.value}
+
+    def chord_stabilize(self, nodes=None) -> dict:
+        """One synchronous stabilize round (orc_chord_stabilize) on explicit tables."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        sc, pc = C.c_uint64(0), C.c_uint64(0)
+        r = lib().orc_chord_stabilize(self._h, _p(nodes), len(nodes), C.byref(sc), C.byref(pc))
+        if r == ORC_FAIL:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return {"nodes": len(nodes), "lists_changed": int(r), "succ_changed": sc.value, "pred_changed": pc.value}
+
+    def chord_lists(self):
+        sls = self.params.successorListSize
+        pred = np.empty(self.n, dtype=np.uint32)
+        succ = np.empty((self.n, sls), dtype=np.uint32)
+        nsucc = np.empty(self.n, dtype=np.uint8)
+        lib().orc_chord_export_lists(self._h, _p(pred), _p(succ), _p(nsucc))
+        return pred, succ, nsucc
 
     def chord_fingers(self) -> np.ndarray:
         out = np.empty((self.n, 160), dtype=np.uint32)

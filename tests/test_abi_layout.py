@@ -32,6 +32,7 @@ CTYPES = {
     "ovs_kbrtest_stats": kbr.KbrTestStats,
     "ovs_kbrtest_lookup_stats": kbr.KbrTestLookupStats,
     "ovs_fixfingers_stats": kbr.FixFingersStats,
+    "ovs_stabilize_stats": kbr.StabilizeStats,
 }
 
 DTYPES = {

@@ -282,3 +282,37 @@ def test_recursive_rejects_explicit_tables(engine: KbrEngine):
     engine.set_params(Params.chord().replace(routingType=1))
     with pytest.raises(KbrError):
         engine.lookup(g["keys"][:4], g["src"][:4])
+
+
+def test_stabilize_fixfingers_rounds_converge(engine: KbrEngine):
+    """Multi-round convergence after a batch of joins: synchronous stabilize rounds
+    (ovs_chord_stabilize, Chord.cc:793-842, 1055-1225) alternating with fixfingers rounds, round by
+    round equal to the oracle's (the engine takes each notified node's nearest caller, the oracle
+    applies the NotifyCalls one by one), ending in the stable ring; routing equal throughout."""
+    from test_oracle_stabilize import joined_ring
+    n = 2000
+    net, joined, t = joined_ring(n, 0x57AD)
+    o = OracleNet("chord", net.ids, net.xy, tables=t)
+    engine.set_params(Params.chord())
+    engine.chord_load_tables(net.ids, net.xy, t["pred"], t["succ"], t["nsucc"], t["fingers"], t["deque_size"])
+    keys, src = W.lookups(net.ids, 3000, 0x57AE, node_ids=True)
+    sub = np.arange(0, n, 2, dtype=np.uint32)
+    for rnd in range(12):
+        nodes = sub if rnd == 0 else None                 # a partial round first
+        g, r = engine.chord_stabilize(nodes), o.chord_stabilize(nodes)
+        assert (g["succ_changed"], g["lists_changed"], g["pred_changed"]) == \
+            (r["succ_changed"], r["lists_changed"], r["pred_changed"]), (rnd, g, r)
+        for a, b in zip(engine.chord_tables(), o.chord_lists()):
+            assert np.array_equal(a, b), rnd
+        gf, rf = engine.chord_fix_fingers(), o.chord_fix_fingers()
+        assert (gf["ok"], gf["changed"], gf["hops"]) == (rf["ok"], rf["changed"], rf["hops"]), rnd
+        assert np.array_equal(engine.chord_fingers(), o.chord_fingers()), rnd
+        if rnd in (0, 2):
+            _eq(engine.lookup(keys, src, record_hops=True), o.route(keys, src, record_hops=True), f"round {rnd}",
+                hop_cols=50)
+        if rnd > 0 and g["lists_changed"] == 0 and g["pred_changed"] == 0 and gf["changed"] == 0:
+            break
+    pred, succ, nsucc = engine.chord_tables()
+    assert np.array_equal(pred, (np.arange(n) - 1) % n)
+    assert np.array_equal(succ, (np.arange(n)[:, None] + 1 + np.arange(8)[None, :]) % n)
+    assert np.array_equal(engine.chord_fingers(), OracleNet("chord", net.ids, net.xy).chord_fingers())
