@@ -101,6 +101,8 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
                           int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
                           uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
                           hipStream_t st, bool* capacity_error);
+// free the exhaustive-lookup scratch K2x keeps for `device` between calls (ovs_ctx_destroy)
+void kad_exhaustive_release(int device);
 // bucket-refresh keys of nodes[0..m) (device buffers); *total = how many (up to cap written)
 hipError_t kad_refresh_keys(const KadTables& t, uint32_t n, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
                             K160* keys, uint32_t* src, uint64_t cap, uint64_t* total, hipStream_t st);

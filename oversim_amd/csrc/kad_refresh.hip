@@ -743,6 +743,18 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     return e;
 }
 
+void kad_exhaustive_release(int device)
+{
+    if (device < 0 || device >= 64) return;
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
+    if (g_scratch[device]) {
+        hipDeviceSynchronize();
+        hipFree(g_scratch[device]);
+    }
+    g_scratch[device] = nullptr;
+    g_scratch_cap[device] = 0;
+}
+
 hipError_t kad_refresh_keys(const KadTables& t, uint32_t n, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
                             K160* keys, uint32_t* src, uint64_t cap, uint64_t* total, hipStream_t st)
 {

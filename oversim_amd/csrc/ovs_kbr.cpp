@@ -340,6 +340,7 @@ void ovs_ctx_destroy(ovs_ctx* c)
     free_tables(c);
     free_kad_shard(c);
     free_scratch(c);
+    kad_exhaustive_release(c->device);
     if (c->d_bounds) hipFree(c->d_bounds);
     for (auto& kv : c->stage) {
         hipStreamSynchronize(kv.first);
