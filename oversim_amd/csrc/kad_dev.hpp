@@ -594,8 +594,6 @@ struct KadLookup {
     int step, hops, pending;
     bool started, pfinished, psuccess, any_to;
     uint32_t result, nsent;
-    int snum, si;          // a sendRpc loop in progress (OVS_KAD_DEFER): calls still to send (-1: none),
-                           // entries examined
 };
 
 template <int A>
@@ -613,7 +611,6 @@ __device__ __forceinline__ void kad_lookup_init(KadLookup<A>& L, const K160& K, 
     L.started = false; L.pfinished = false; L.psuccess = false; L.any_to = false;
     L.result = NONE;
     L.nsent = 0;
-    L.snum = -1; L.si = 0;
 }
 
 // FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
@@ -665,48 +662,6 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     on(slot, x, isTo);
 }
 
-#ifndef OVS_KAD_DEFER
-// 1: one FindNodeCall per loop iteration of a lane (the rest of a sendRpc burst follows in the next
-// iterations, at the same simulated instant, before any event), so that a wave would pay for one send
-// per iteration instead of the alpha sends of a lane that just started.  Measured slower (E 3.28e9 ->
-// 2.41e9 hops/s, B unchanged: profiles/r02_n_defer): the extra iterations cost more than the sends.
-#define OVS_KAD_DEFER 0
-#endif
-
-// The loop of IterativePathLookup::sendRpc (IterativeLookup.cc:1102-1168), from where it stands:
-// with OVS_KAD_DEFER up to one FindNodeCall, else to its end; at its end the path fails when
-// nothing is in flight.
-template <int A, bool EX, bool LK, class OnSend>
-__device__ __forceinline__ void kad_send_step(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
-                                              const OnSend& on)
-{
-    bool sent = false;
-    while (!(OVS_KAD_DEFER && sent) && L.snum > 0 && L.si < LC.redundant) {
-        // getNextEntry: first entry not alreadyUsed (a node that timed out is dead, but it is
-        // used already: entries leave nextHops for good once evicted, DESIGN.md §4)
-        const uint32_t unused = ~L.nh.used & ((1u << L.nh.n) - 1u);
-        if (!unused) { L.si = LC.redundant; break; }
-        const int e = __ffs((int)unused) - 1;
-        uint32_t h = NONE;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j == e) h = L.nh.idx[j];
-        ++L.si;
-        // visitOnlyOnce: an unused entry can only be a visited node if it is the source
-        if (!LC.visitOnlyOnce || h != L.S) {
-            ++L.pending;
-            --L.snum;
-            kad_send<A, EX, LK>(L, V, DC, LC, h, on);
-            sent = true;
-        }
-        L.nh.used |= 1u << e;
-    }
-    if (!(L.snum > 0 && L.si < LC.redundant)) {
-        L.snum = -1;
-        if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
-    }
-}
-
 // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
 template <int A, bool EX, bool LK, class OnSend>
 __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
@@ -716,16 +671,32 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
     if (LC.hopCountMax && L.hops >= LC.hopCountMax) { L.pfinished = true; L.psuccess = false; return; }
     if (LC.strict) num = min(num, LC.alpha - L.pending);
     if (num == 0 && L.pending == 0 && !LC.finishOnFirst) num = LC.alpha;
-    L.snum = num;
-    L.si = 0;
-    kad_send_step<A, EX, LK>(L, V, DC, LC, on);
+    for (int i = 0; num > 0 && i < LC.redundant; ++i) {
+        // getNextEntry: first entry not alreadyUsed (a node that timed out is dead, but it is
+        // used already: entries leave nextHops for good once evicted, DESIGN.md §4)
+        const uint32_t unused = ~L.nh.used & ((1u << L.nh.n) - 1u);
+        if (!unused) break;
+        const int e = __ffs((int)unused) - 1;
+        uint32_t h = NONE;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j == e) h = L.nh.idx[j];
+        // visitOnlyOnce: an unused entry can only be a visited node if it is the source
+        if (!LC.visitOnlyOnce || h != L.S) {
+            ++L.pending;
+            --num;
+            kad_send<A, EX, LK>(L, V, DC, LC, h, on);
+        }
+        L.nh.used |= 1u << e;
+    }
+    if (L.pending == 0) { L.psuccess = false; L.pfinished = true; }
 }
 
 // checkStop (IterativeLookup.cc:295-349): the single path finished, or nothing pending
 template <int A>
 __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
 {
-    return L.started && L.snum < 0 && (L.pfinished || L.pvalid == 0);
+    return L.started && (L.pfinished || L.pvalid == 0);
 }
 
 // Advance a lookup by one event.  The first call is IterativeLookup::start (IterativeLookup.cc:
@@ -741,11 +712,6 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
                                                  const KadLC& LC, SVec<8>& res, const GetRes& getres,
                                                  const OnSend& on, const Rec& record)
 {
-    if (L.snum >= 0) {
-        // the rest of a sendRpc burst (same simulated instant, before any event)
-        kad_send_step<A, EX, LK>(L, V, DC, LC, on);
-        return true;
-    }
     const int ns = LK ? LC.numSiblings : 1;
     uint32_t r = L.S;
     RespGeo rg;
