@@ -453,6 +453,21 @@ ovs_status  ovs_shard_step(ovs_ctx* ctx, const ovs_lookup_rec* in, uint64_t n_in
                            ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
                            const uint64_t* shard_lo, uint32_t nshards, void* stream);
 
+/* LookupCalls across arcs (KBRTestApp lookup test on a sharded ring): rounds as
+ * ovs_shard_step, with num_siblings (-1 = successorListSize, at most 8): the
+ * responsible node's FindNodeResponse carries the sibling vector and the lookup
+ * ends there (no route message).  ovs_shard_lookup_finish turns n finished
+ * records (from `done`, any order) into the LookupResponses, in that order:
+ * out[i] and siblings[i * num_siblings] (0xFFFFFFFF padded) for done[i].qid.
+ * The successor lists of a converged ring are replicated, so any rank finishes
+ * any record.  Device buffers. */
+ovs_status  ovs_shard_step_lookup(ovs_ctx* ctx, int32_t num_siblings, const ovs_lookup_rec* in, uint64_t n_in,
+                                  ovs_lookup_rec* out, uint64_t out_cap, unsigned long long* out_count,
+                                  ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                                  const uint64_t* shard_lo, uint32_t nshards, void* stream);
+ovs_status  ovs_shard_lookup_finish(ovs_ctx* ctx, const ovs_done_rec* done, uint64_t n, int32_t num_siblings,
+                                    ovs_lookup_out* out, uint32_t* siblings, void* stream);
+
 /* ---- multi-GPU Kademlia ----
  * The sorted ring is cut into contiguous arcs (ID prefixes); a rank holds the
  * sibling entries and bucket rows of its arc, while the 64 B node records and

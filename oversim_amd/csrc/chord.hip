@@ -1085,14 +1085,12 @@ __global__ void k_fill_rpcs(const ovs_route_out* __restrict__ out, uint64_t n, u
 // share their 16 B slot).  Chord: the sibling vector is the responsible node's findNode answer
 // [R, succ...] downsized to numSiblings (Chord.cc:573-580; IterativeLookup::addSibling pushes it
 // in order, 406-449).  Kademlia: the route kernel has written the answering response's nodes.
-__global__ void k_lookup_finish(ChordView V, int chord, int ideal, int ns, ovs_route_out* __restrict__ io,
-                                uint32_t* __restrict__ sibs, uint64_t n)
+// SendToKeyListener::lookupFinished's LookupResponse (BaseOverlay.cc:1272-1300) of one finished
+// LookupCall from its route record: on Chord the sibling vector is [R, succ(R)...] (Chord.cc:573-580)
+__device__ __forceinline__ ovs_lookup_out lookup_finish_one(const ChordView& V, int chord, int ideal, int ns,
+                                                            const ovs_route_out r, uint32_t* __restrict__ row)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const ovs_route_out r = io[i];
     const bool ok = r.status == OVS_LOOKUP_OK;
-    uint32_t* row = sibs + i * (uint64_t)ns;
     uint32_t cnt = 0;
     if (chord) {
         if (ok) {
@@ -1116,7 +1114,33 @@ __global__ void k_lookup_finish(ChordView V, int chord, int ideal, int ns, ovs_r
     o.status = r.status;
     o.is_valid = ok ? 1 : 0;
     o.latency_ns = ok ? r.latency_ns : -1;
+    return o;
+}
+
+__global__ void k_lookup_finish(ChordView V, int chord, int ideal, int ns, ovs_route_out* __restrict__ io,
+                                uint32_t* __restrict__ sibs, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ovs_lookup_out o = lookup_finish_one(V, chord, ideal, ns, io[i], sibs + i * (uint64_t)ns);
     reinterpret_cast<ovs_lookup_out*>(io)[i] = o;
+}
+
+// the LookupCalls finished across arcs: done records (any order) -> LookupResponses in that order
+__global__ void k_shard_lookup_finish(ChordView V, int ns, const ovs_done_rec* __restrict__ done,
+                                      ovs_lookup_out* __restrict__ out, uint32_t* __restrict__ sibs, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = lookup_finish_one(V, 1, 1, ns, done[i].out, sibs + i * (uint64_t)ns);
+}
+
+hipError_t launch_shard_lookup_finish(const ChordView& V, int ns, const ovs_done_rec* done, ovs_lookup_out* out,
+                                      uint32_t* sibs, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_shard_lookup_finish, dim3(nblk(n, 256)), dim3(256), 0, s, V, ns, done, out, sibs, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_lookup_finish(const ChordView& V, bool chord, bool ideal, int ns, ovs_route_out* io,
@@ -1164,8 +1188,10 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
     io.stage_done = reinterpret_cast<ovs_done_rec*>(sb + od);
     io.stag = sb + ot;
     if ((e = hipMemsetAsync(io.stag, 0xFF, nin, s)) != hipSuccess) return e;
+    // DC.lookupCall: a LookupCall batch (the responsible node's larger answer, no route message)
     e = LC.recursive ? lanes_launch<true, false, true>(V, DC, LC, io, num_cu, s)
-                     : lanes_launch<false, false, true>(V, DC, LC, io, num_cu, s);
+        : DC.lookupCall ? lanes_launch<false, false, true, true>(V, DC, LC, io, num_cu, s)
+                        : lanes_launch<false, false, true>(V, DC, LC, io, num_cu, s);
     if (e != hipSuccess) return e;
     // outcomes to their outputs: class d < nsh = hand-offs to arc d (segment d of out), nsh = done
     CPlan P{};

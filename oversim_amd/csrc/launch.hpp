@@ -25,6 +25,8 @@ hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts&
 hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,
                                   uint64_t n, int numRedundant, int numSiblings, uint32_t* out_nodes,
                                   uint32_t max_out, uint8_t* out_count, uint8_t* out_sib, hipStream_t s);
+hipError_t launch_shard_lookup_finish(const ChordView& V, int ns, const ovs_done_rec* done, ovs_lookup_out* out,
+                                      uint32_t* sibs, uint64_t n, hipStream_t s);
 hipError_t launch_lookup_finish(const ChordView& V, bool chord, bool ideal, int ns, ovs_route_out* io,
                                 uint32_t* sibs, uint64_t n, hipStream_t s);
 hipError_t launch_fill_rpcs_from_hops(const ovs_route_out* out, uint64_t n, uint32_t* rpcs, hipStream_t s);

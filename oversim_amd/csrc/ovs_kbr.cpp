@@ -435,9 +435,10 @@ ovs_status upload_bounds(ovs_ctx* c, const uint64_t* lo, uint32_t nshards)
     return OVS_OK;
 }
 
-ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out, uint64_t out_cap,
-                          unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                          unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
+// ns = 0: one-way routes (ovs_shard_step); ns >= 1: LookupCalls with that many siblings
+static ovs_status shard_step(ovs_ctx* c, int ns, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out,
+                             uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                             unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
 {
     if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
     if (n_in && (!in || !out || !out_count || !done || !done_count)) return OVS_EINVAL;
@@ -460,11 +461,57 @@ ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, o
     hipStream_t s = (hipStream_t)stream;   // device-pointer call: NULL = the default stream
     st = upload_bounds(c, M.lo, nshards);
     if (st != OVS_OK) return st;
-    LookupConsts LC{c->P.hopCountMax, c->P.numSiblings, c->P.lookupRedundantNodes, c->P.routingType != 0};
+    LookupConsts LC{c->P.hopCountMax, ns ? ns : c->P.numSiblings, c->P.lookupRedundantNodes, c->P.routingType != 0};
+    DelayConsts DC = delay_consts(c->P);
+    if (ns) {
+        if (c->P.routingType != 0) return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative");
+        // as ovs_lookup_batch: the responsible node answers min(numSiblings, 1 + successors) nodes
+        DC.lookupCall = 1;
+        const int64_t nsucc = std::min<int64_t>(c->P.successorListSize, (int64_t)c->n - 1);
+        const int nodes = (int)std::min<int64_t>(ns, 1 + nsucc);
+        DC.msgRespSib = 2 * simtime_host((double)((int64_t)(DC.respBase + DC.respPerNode * nodes) * 8) / c->P.datarate,
+                                         c->P.simtimeRound) + DC.access2;
+    }
     st = ensure_nodes(c, s);
     if (st != OVS_OK) return st;
-    HIPCHK(c, launch_chord_shard_step(chord_view(c), delay_consts(c->P), LC, c->d_bounds, (int)nshards, me, in, n_in, out,
-                                      out_cap, out_count, done, done_cap, done_count, c->stage[s], c->num_cu, s));
+    HIPCHK(c, launch_chord_shard_step(chord_view(c), DC, LC, c->d_bounds, (int)nshards, me, in, n_in, out, out_cap,
+                                      out_count, done, done_cap, done_count, c->stage[s], c->num_cu, s));
+    return OVS_OK;
+}
+
+ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out, uint64_t out_cap,
+                          unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                          unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
+{
+    return shard_step(c, 0, in, n_in, out, out_cap, out_count, done, done_cap, done_count, shard_lo, nshards, stream);
+}
+
+static int32_t shard_lookup_ns(ovs_ctx* c, int32_t num_siblings)
+{
+    return num_siblings < 0 ? c->P.successorListSize : num_siblings;
+}
+
+ovs_status ovs_shard_step_lookup(ovs_ctx* c, int32_t num_siblings, const ovs_lookup_rec* in, uint64_t n_in,
+                                 ovs_lookup_rec* out, uint64_t out_cap, unsigned long long* out_count,
+                                 ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                                 const uint64_t* shard_lo, uint32_t nshards, void* stream)
+{
+    if (!c) return OVS_EINVAL;
+    const int32_t ns = shard_lookup_ns(c, num_siblings);
+    if (ns > c->P.successorListSize) return fail(c, OVS_EINVAL, "numSiblings too big!");
+    if (ns < 1 || ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall across arcs implements numSiblings 1..8");
+    return shard_step(c, ns, in, n_in, out, out_cap, out_count, done, done_cap, done_count, shard_lo, nshards, stream);
+}
+
+ovs_status ovs_shard_lookup_finish(ovs_ctx* c, const ovs_done_rec* done, uint64_t n, int32_t num_siblings,
+                                   ovs_lookup_out* out, uint32_t* siblings, void* stream)
+{
+    if (!c || (n && (!done || !out || !siblings))) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD || !c->ideal) return fail(c, OVS_ESTATE, "no Chord ring (shard) loaded");
+    const int32_t ns = shard_lookup_ns(c, num_siblings);
+    if (ns < 1 || ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall across arcs implements numSiblings 1..8");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, launch_shard_lookup_finish(chord_view(c), ns, done, out, siblings, n, (hipStream_t)stream));
     return OVS_OK;
 }
 

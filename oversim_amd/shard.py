@@ -32,7 +32,7 @@ import ctypes as C
 
 import numpy as np
 
-from .kbr import DEVICE_PTRS, KbrEngine, Params, lib
+from .kbr import DEVICE_PTRS, LOOKUP_OUT_DTYPE, KbrEngine, Params, lib
 
 REC_DTYPE = np.dtype([("key", "<u4", 5), ("src", "<u4"), ("cur", "<u4"), ("qid", "<u4"), ("t_ns", "<i8"),
                       ("hops", "<u2"), ("local", "u1"), ("pad", "u1", 5)])
@@ -54,8 +54,11 @@ class GpuShardStepper:
     """One rank's arc on one device: owns the engine context and the device buffers."""
 
     def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device, stream=None,
-                 capacity: int = 1 << 20, params: Params | None = None):
+                 capacity: int = 1 << 20, params: Params | None = None, lookup_siblings: int | None = None):
+        """lookup_siblings: route KBRTestApp LookupCalls with that many siblings (-1 = successorListSize;
+        ovs_shard_step_lookup) instead of one-way messages; finish them with lookup_finish()."""
         import torch
+        self.lookup_siblings = lookup_siblings
         self.torch = torch
         self.dev = device
         self.stream = stream
@@ -143,11 +146,13 @@ class GpuShardStepper:
         cnt.zero_()
         if self.timing:
             self._ev[cohort][0].record()
-        st = lib().ovs_shard_step(self.eng._h, C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(out.data_ptr()),
-                                  self._cap[cohort], C.c_void_p(cnt.data_ptr()),
-                                  C.c_void_p(self.done.data_ptr()), self.done_cap,
-                                  C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
-        self.eng._chk(st, "ovs_shard_step")
+        args = (C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(out.data_ptr()), self._cap[cohort],
+                C.c_void_p(cnt.data_ptr()), C.c_void_p(self.done.data_ptr()), self.done_cap,
+                C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
+        if self.lookup_siblings is None:
+            self.eng._chk(lib().ovs_shard_step(self.eng._h, *args), "ovs_shard_step")
+        else:
+            self.eng._chk(lib().ovs_shard_step_lookup(self.eng._h, self.lookup_siblings, *args), "ovs_shard_step_lookup")
         if self.timing:
             self._ev[cohort][1].record()
             self._timed[cohort] = True
@@ -167,12 +172,32 @@ class GpuShardStepper:
             raise RuntimeError("done buffer overflow")
         return self.done[:k]
 
+    def lookup_finish(self, done):
+        """LookupResponses of finished LookupCall records (ovs_shard_lookup_finish): (qid, ovs_lookup_out
+        records, siblings (n, numSiblings)) as numpy arrays, in the records' order."""
+        torch = self.torch
+        ns = self.lookup_siblings if self.lookup_siblings and self.lookup_siblings > 0 else \
+            self.eng.get_params().successorListSize
+        n = done.shape[0]
+        out = torch.empty((max(n, 1), 16), dtype=torch.uint8, device=self.dev)
+        sib = torch.empty((max(n, 1), ns), dtype=torch.int32, device=self.dev)
+        st = lib().ovs_shard_lookup_finish(self.eng._h, C.c_void_p(done.data_ptr()), n, ns, C.c_void_p(out.data_ptr()),
+                                           C.c_void_p(sib.data_ptr()), self._s())
+        self.eng._chk(st, "ovs_shard_lookup_finish")
+        torch.cuda.synchronize(self.dev)
+        recs = done_to_numpy(done)
+        lo = out[:n].cpu().numpy().reshape(-1).view(LOOKUP_OUT_DTYPE)
+        return recs["qid"].copy(), lo, sib[:n].cpu().numpy().view(np.uint32)
+
 
 for _name, _args in {
     "ovs_chord_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
     "ovs_shard_make_records": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p],
     "ovs_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
+    "ovs_shard_step_lookup": [C.c_void_p, C.c_int32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                              C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
+    "ovs_shard_lookup_finish": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p],
     "ovs_kad_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
     "ovs_kad_shard_begin": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p],
     "ovs_kad_shard_step": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,

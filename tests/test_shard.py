@@ -512,3 +512,42 @@ def test_kad_w8_large_network_vs_oracle():
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
     assert sum(s.served for s in steppers) > world * m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,ns", [(2, 8), (3, 5), (8, 8)])
+def test_shard_lookup_calls_emulated_on_one_gpu(world, ns):
+    """KBRTestApp LookupCalls across W arcs (ovs_shard_step_lookup + ovs_shard_lookup_finish): every
+    LookupResponse equals the single-context ovs_lookup_batch's (itself checked against the oracle)."""
+    from oversim_amd import KbrEngine, Params
+    from oversim_amd.shard import GpuShardStepper, arc_bounds, route_local_shards
+    n, m = 1 << 16, 5000
+    net = W.population(n, 97)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, lookup_siblings=ns)
+                for r in range(world)]
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s = W.lookups(net.ids, m, 98 + r, node_ids=(r % 2 == 1))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k).to(dev)); ss.append(torch.from_numpy(s).to(dev)); qb.append(r * m)
+        allk.append(k); alls.append(s)
+    for st in steppers:
+        st.reset(world * m)
+    dones, rounds = route_local_shards(steppers, ks, ss, qb)
+    parts = [steppers[r].lookup_finish(dones[r]) for r in range(world)]
+    qid = np.concatenate([p[0] for p in parts])
+    lo = np.concatenate([p[1] for p in parts])
+    sib = np.concatenate([p[2] for p in parts])
+    order = np.argsort(qid)
+    assert np.array_equal(qid[order], np.arange(world * m))
+    lo, sib = lo[order], sib[order]
+    with KbrEngine(0) as eng:
+        eng.set_params(Params.chord())
+        eng.chord_load(net.ids, net.xy)
+        ref = eng.lookupCall(np.concatenate(allk), np.concatenate(alls), ns)
+    for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+        assert np.array_equal(lo[f], ref[f]), f
+    assert np.array_equal(sib, ref["siblings"])
+    assert rounds >= 2
