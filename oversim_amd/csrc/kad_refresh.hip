@@ -394,206 +394,274 @@ struct XCtx {
     //   per event (handleRpcResponse 488-585 / handleRpcTimeout 588-654): every RpcInfo of the node in
     //     turn -- the first of a response is handleResponse (803-921), the others and those of a
     //     timeout handleTimeout (935-1023) -- each possibly followed by a sendRpc, then checkStop.
-    __device__ __forceinline__ void run(XLookup& L) const
-    {
+    // the loop state of a lookup between iterations (start, the event in hand, its RpcInfos left)
+    struct Run {
         XRegNh H;
-        H.used = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { H.idx[i] = NONE; H.d[i] = ~0ull; }
         XPend cur;
-        cur.node = L.S; cur.ninfo = 1; cur.to = false; cur.tsend = 0;
-        bool start = true, handled = false;
-        uint32_t infos = 1;
-        while (!L.err) {
-            int num = -1;
-            if (infos == 0) {
-                if (check_stop(L)) break;
-                // the earliest pending event: (time, insertion time, sequence)
-                int e = -1;
-                int64_t bt = 0, bi = 0;
-                uint32_t bs = 0;
+        bool start, handled;
+        uint32_t infos;
+    };
+
+    __device__ __forceinline__ void init(const XLookup& L, Run& R) const
+    {
+        R.H.used = 0;
 #pragma unroll
-                for (int i = 0; i < XMAXA; ++i) {
-                    if (!((L.pvalid >> i) & 1u)) continue;
-                    const XPend& P = L.p[i];
-                    if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
-                        e = i; bt = P.t; bi = P.tins; bs = P.seq;
-                    }
-                }
-                if (e < 0) break;
+        for (int i = 0; i < 16; ++i) { R.H.idx[i] = NONE; R.H.d[i] = ~0ull; }
+        R.cur.node = L.S; R.cur.ninfo = 1; R.cur.to = false; R.cur.tsend = 0;
+        R.cur.seq = 0; R.cur.t = 0; R.cur.tins = 0;
+        R.start = true; R.handled = false;
+        R.infos = 1;
+    }
+
+    // One iteration of the lookup's loop; true when the lookup has ended.  The start, responses
+    // and timeouts share a single findNode, LookupVector merge and sendRpc site:
+    //   start (IterativeLookup::start 133-244): findNode(key, k, -1) at the source, all into nextHops,
+    //     sendRpc(alpha), checkStop;
+    //   per event (handleRpcResponse 488-585 / handleRpcTimeout 588-654): every RpcInfo of the node in
+    //     turn -- the first of a response is handleResponse (803-921), the others and those of a
+    //     timeout handleTimeout (935-1023) -- each possibly followed by a sendRpc, then checkStop.
+    __device__ __forceinline__ bool step(XLookup& L, Run& R) const
+    {
+        XRegNh& H = R.H;
+        XPend& cur = R.cur;
+        if (L.err) return true;
+        int num = -1;
+        if (R.infos == 0) {
+            if (check_stop(L)) return true;
+            // the earliest pending event: (time, insertion time, sequence)
+            int e = -1;
+            int64_t bt = 0, bi = 0;
+            uint32_t bs = 0;
 #pragma unroll
-                for (int i = 0; i < XMAXA; ++i) {
-                    const bool me = i == e;
-                    cur.node = me ? L.p[i].node : cur.node;
-                    cur.ninfo = me ? L.p[i].ninfo : cur.ninfo;
-                    cur.tsend = me ? L.p[i].tsend : cur.tsend;
-                    cur.to = me ? L.p[i].to : cur.to;
+            for (int i = 0; i < XMAXA; ++i) {
+                if (!((L.pvalid >> i) & 1u)) continue;
+                const XPend& P = L.p[i];
+                if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
+                    e = i; bt = P.t; bi = P.tins; bs = P.seq;
                 }
-                L.pvalid &= ~(1u << e);
-                L.now = bt;
-                if (cur.to) {
-                    L.any_to = true;                 // setDead(dest)
-                    if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = cur.node;
-                    else { L.err = true; break; }
-                }
-                infos = cur.ninfo;
-                handled = false;
-                continue;
             }
-            --infos;
-            if (!start && L.pfinished) continue;     // "do not handle finished paths"
-            if (start || (!cur.to && !handled)) {
-                handled = true;
-                bool merge = true;
-                if (!start) {
-                    // handleResponse (exhaustive: accepted whatever its step)
-                    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; merge = false; }
-                    else {
-                        if (cur.node != L.S) {
-                            if (L.nhop < C.hcm) {
-                                resp[L.nhop] = cur.node;
-                                if (rtt) rtt[L.nhop] = L.now - cur.tsend;
-                            }
-                            ++L.nhop;
-                            ++L.hops;
-                        }
-                        ++L.step;
-                        --L.pending;
-                    }
-                }
-                if (merge) {
-                    // the responder's findNode (the source's own at the start) into nextHops (2R)
-                    const KadNode rn = load_node(V.nodes, cur.node);
-                    const RespGeo g = resp_geo(rn, L.K);
-                    const int rs = start ? C.k : C.R;
-                    int numNew = 0, cnt = 0;
-                    if (REG || rs <= 8) {
-                        Blk8 b;       // the block form of K2 (sorting networks, kad_dev.hpp)
-                        cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1);
+            if (e < 0) return true;
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            if (i >= cnt) continue;
-                            const int pos = nh_add(L, H, b.x[i], b.d[i]);
-                            numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
-                        }
-                    } else {
-                        cnt = find_node_scratch(cur.node, g, L.K, rs);
-                        for (int i = 0; i < cnt; ++i) {
-                            const int pos = nh_add(L, H, X.res_idx[at(i)], X.res_d[at(i)]);
-                            numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
-                        }
-                    }
-                    if (start) {
-                        if (cnt == 0) { L.success = false; break; }   // no next hops known
-                        num = C.alpha;
-                    } else {
-                        if (numNew == 0 && C.newOnResp) numNew = 1;
-                        num = min(numNew, C.alpha);
-                    }
-                }
-            } else {
-                // handleTimeout (for a timeout, or a response's further RpcInfos)
-                if (L.nd && is_dead(L, cur.node)) nh_remove(L, H, cur.node);   // exhaustive: dead nodes leave nextHops (948-957)
-                --L.pending;
-                if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
-                else if (C.newOnTimeout) num = 1;
-                else if (L.pending == 0) num = C.alpha;
+            for (int i = 0; i < XMAXA; ++i) {
+                const bool me = i == e;
+                cur.node = me ? L.p[i].node : cur.node;
+                cur.ninfo = me ? L.p[i].ninfo : cur.ninfo;
+                cur.tsend = me ? L.p[i].tsend : cur.tsend;
+                cur.to = me ? L.p[i].to : cur.to;
             }
-            if (num >= 0) send_rpcs(L, H, num);
-            if (!start) count_finished(L);
-            start = false;
+            L.pvalid &= ~(1u << e);
+            L.now = bt;
+            if (cur.to) {
+                L.any_to = true;                 // setDead(dest)
+                if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = cur.node;
+                else { L.err = true; return true; }
+            }
+            R.infos = cur.ninfo;
+            R.handled = false;
+            return false;
         }
+        --R.infos;
+        if (!R.start && L.pfinished) return false;     // "do not handle finished paths"
+        if (R.start || (!cur.to && !R.handled)) {
+            R.handled = true;
+            bool merge = true;
+            if (!R.start) {
+                // handleResponse (exhaustive: accepted whatever its step)
+                if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; merge = false; }
+                else {
+                    if (cur.node != L.S) {
+                        if (L.nhop < C.hcm) {
+                            resp[L.nhop] = cur.node;
+                            if (rtt) rtt[L.nhop] = L.now - cur.tsend;
+                        }
+                        ++L.nhop;
+                        ++L.hops;
+                    }
+                    ++L.step;
+                    --L.pending;
+                }
+            }
+            if (merge) {
+                // the responder's findNode (the source's own at the start) into nextHops (2R)
+                const KadNode rn = load_node(V.nodes, cur.node);
+                const RespGeo g = resp_geo(rn, L.K);
+                const int rs = R.start ? C.k : C.R;
+                int numNew = 0, cnt = 0;
+                if (REG || rs <= 8) {
+                    Blk8 b;       // the block form of K2 (sorting networks, kad_dev.hpp)
+                    cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        if (i >= cnt) continue;
+                        const int pos = nh_add(L, H, b.x[i], b.d[i]);
+                        numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
+                    }
+                } else {
+                    cnt = find_node_scratch(cur.node, g, L.K, rs);
+                    for (int i = 0; i < cnt; ++i) {
+                        const int pos = nh_add(L, H, X.res_idx[at(i)], X.res_d[at(i)]);
+                        numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
+                    }
+                }
+                if (R.start) {
+                    if (cnt == 0) { L.success = false; return true; }   // no next hops known
+                    num = C.alpha;
+                } else {
+                    if (numNew == 0 && C.newOnResp) numNew = 1;
+                    num = min(numNew, C.alpha);
+                }
+            }
+        } else {
+            // handleTimeout (for a timeout, or a response's further RpcInfos)
+            if (L.nd && is_dead(L, cur.node)) nh_remove(L, H, cur.node);   // exhaustive: dead nodes leave nextHops (948-957)
+            --L.pending;
+            if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; }
+            else if (C.newOnTimeout) num = 1;
+            else if (L.pending == 0) num = C.alpha;
+        }
+        if (num >= 0) send_rpcs(L, H, num);
+        if (!R.start) count_finished(L);
+        R.start = false;
+        return false;
     }
 };
+
+
+template <bool EX, bool REG>
+__device__ __forceinline__ void kx_init_lookup(XLookup& L, const KadView& V, const XCfg& C, const K160* __restrict__ qkeys,
+                                               const uint32_t* __restrict__ qsrc, uint32_t* __restrict__ sib_out, uint64_t q)
+{
+    L.K = qkeys[q];
+    L.S = qsrc[q];
+    const double2 sxy = V.xy[L.S];
+    L.sx = sxy.x; L.sy = sxy.y;
+    L.now = 0; L.txf = 0; L.seq = 0; L.nsent = 0;
+    L.nnh = 0; L.nd = 0; L.nhop = 0;
+    L.step = 0; L.hops = 0; L.pending = 0;
+    L.pfinished = false; L.psuccess = false; L.counted = false; L.any_to = false; L.success = false; L.err = false;
+    L.finishedPaths = 0; L.successfulPaths = 0; L.minHops = 0x7FFFFFFF;
+    L.pvalid = 0;
+#pragma unroll
+    for (int i = 0; i < XMAXA; ++i) {
+        L.p[i].node = NONE; L.p[i].ninfo = 0; L.p[i].seq = 0;
+        L.p[i].t = 0; L.p[i].tins = 0; L.p[i].tsend = 0; L.p[i].to = false;
+    }
+    uint32_t* sib = sib_out + q * (uint64_t)C.ns;
+    for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
+}
+
+// SendToKeyListener / LookupResponse fields of a finished lookup (as ovs_lookup_batch; the
+// ovs_lookup_out is written through its ovs_route_out twin, k_lookup_finish's convention), or the
+// one-way route message
+__device__ __forceinline__ void kx_emit(const XLookup& L, const KadView& V, const DelayConsts& DC, const XCfg& C,
+                                        uint64_t q, ovs_route_out* __restrict__ out, uint32_t* __restrict__ sib,
+                                        uint32_t* __restrict__ resp, int64_t* __restrict__ rtt,
+                                        uint32_t* __restrict__ rpcs_out, uint32_t* __restrict__ err)
+{
+    if (L.err) atomicOr(err, 1u);
+    for (int j = L.nhop; j < C.hcm; ++j) {
+        resp[j] = NONE;
+        if (rtt) rtt[j] = -1;
+    }
+    const bool valid = L.success && !L.err;
+    const uint8_t fail_status = L.now > DC.lookupTimeout ? OVS_LOOKUP_TIMEOUT
+                                : L.nd > 0                 ? OVS_LOOKUP_RPC_TIMEOUT
+                                : (C.hcm && L.hops >= C.hcm) ? OVS_LOOKUP_HOPMAX
+                                                             : OVS_LOOKUP_NO_NEXT;
+    if (rpcs_out) rpcs_out[q] = L.nsent;
+    if (C.oneway) {
+        // SendToKeyListener::lookupFinished -> sendRouteMessage to getResult()[0] through the
+        // source's tx queue (BaseOverlay.cc:1107-1146, 1241-1259; SimpleNodeEntry.cc:164-194)
+        ovs_route_out o;
+        o.hops = (uint16_t)(L.minHops == 0x7FFFFFFF ? 0 : L.minHops);
+        const uint32_t R0 = sib[0];
+        if (valid && R0 != NONE) {
+            o.status = OVS_LOOKUP_OK;
+            o.responsible = R0;
+            o.one_way_hops = (uint8_t)(o.hops + (R0 != L.S ? 1 : 0));
+            int64_t lat = L.now;
+            if (R0 != L.S) {
+                const double2 rxy = V.xy[R0];
+                const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + DC.bwRoute;
+                lat = newTx + DC.access2 + coord_ns(L.sx, L.sy, rxy.x, rxy.y, DC.round) + DC.bwRoute;
+            }
+            o.latency_ns = lat;
+        } else {
+            o.status = fail_status;
+            o.responsible = NONE;
+            o.one_way_hops = 0;
+            o.latency_ns = -1;
+        }
+        out[q] = o;
+        return;
+    }
+    ovs_lookup_out o;
+    o.hops = (uint16_t)(L.minHops == 0x7FFFFFFF ? 0 : L.minHops);
+    o.is_valid = valid ? 1 : 0;
+    if (valid) {
+        int ns = 0;
+        for (int j = 0; j < C.ns; ++j) ns += sib[j] != NONE ? 1 : 0;
+        o.num_siblings = (uint32_t)ns;
+        o.latency_ns = L.now;
+        o.status = OVS_LOOKUP_OK;
+    } else {
+        for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
+        o.num_siblings = 0;
+        o.latency_ns = -1;
+        o.status = fail_status;
+    }
+    reinterpret_cast<ovs_lookup_out*>(out)[q] = o;
+}
 
 #ifndef OVS_KX_WAVES
 // minimum waves per SIMD the register allocator must allow for the register-vector (R <= 8) form
 #define OVS_KX_WAVES 2
 #endif
 
+// One lane per lookup, one loop iteration per kernel-loop iteration; a lane whose lookup ended
+// takes the next one of its wave's contiguous slice of the batch (ballot + popcount, no atomics),
+// so a wave does not wait for its longest lookup before its lanes move on (as K2).
 template <bool EX, bool REG>
 __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C, XScratch X,
                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
-                                                     uint64_t nq, ovs_route_out* __restrict__ out,
+                                                     uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
                                                      uint32_t* __restrict__ sib_out, uint32_t* __restrict__ resp_out,
                                                      int64_t* __restrict__ rtt_out, uint32_t* __restrict__ rpcs_out,
                                                      uint32_t* __restrict__ err)
 {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (lane >= X.lanes) return;
-    for (uint64_t q = lane; q < nq; q += X.lanes) {
-        XLookup L;
-        L.K = qkeys[q];
-        L.S = qsrc[q];
-        const double2 sxy = V.xy[L.S];
-        L.sx = sxy.x; L.sy = sxy.y;
-        L.now = 0; L.txf = 0; L.seq = 0; L.nsent = 0;
-        L.nnh = 0; L.nd = 0; L.nhop = 0;
-        L.step = 0; L.hops = 0; L.pending = 0;
-        L.pfinished = false; L.psuccess = false; L.counted = false; L.any_to = false; L.success = false; L.err = false;
-        L.finishedPaths = 0; L.successfulPaths = 0; L.minHops = 0x7FFFFFFF;
-        L.pvalid = 0;
+    const int wl = threadIdx.x & 63;
+    const uint64_t wave = lane >> 6;
+    uint64_t cursor = wave * chunk;
+    const uint64_t end = min(cursor + chunk, nq);
+    const uint64_t lt_mask = (wl == 0) ? 0ull : (~0ull >> (64 - wl));
+    bool active = false;
+    uint64_t q = 0;
+    XLookup L;
+    typename XCtx<EX, REG>::Run R;
+    while (true) {
+        const uint64_t need = __ballot(!active);
+        if (need != 0 && cursor < end) {
+            const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
+            if (!active && mine < end) {
+                q = mine;
+                active = true;
+                kx_init_lookup<EX, REG>(L, V, C, qkeys, qsrc, sib_out, q);
+                const XCtx<EX, REG> c0{V, DC, C, X, lane, nullptr, nullptr, nullptr};
+                c0.init(L, R);
+            }
+            cursor += (uint64_t)__popcll(need);
+        }
+        if (!__any(active)) break;
+        if (!active) continue;
         uint32_t* sib = sib_out + q * (uint64_t)C.ns;
-        for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
         uint32_t* resp = resp_out + q * (uint64_t)C.hcm;
         int64_t* rtt = rtt_out ? rtt_out + q * (uint64_t)C.hcm : nullptr;
         const XCtx<EX, REG> ctx{V, DC, C, X, lane, resp, rtt, sib};
-        ctx.run(L);
-        if (L.err) atomicOr(err, 1u);
-        for (int j = L.nhop; j < C.hcm; ++j) {
-            resp[j] = NONE;
-            if (rtt) rtt[j] = -1;
+        if (ctx.step(L, R)) {
+            kx_emit(L, V, DC, C, q, out, sib, resp, rtt, rpcs_out, err);
+            active = false;
         }
-        // SendToKeyListener / LookupResponse fields (as ovs_lookup_batch): the ovs_lookup_out is
-        // written through its ovs_route_out twin (same size; k_lookup_finish's convention)
-        const bool valid = L.success && !L.err;
-        const uint8_t fail_status = L.now > DC.lookupTimeout ? OVS_LOOKUP_TIMEOUT
-                                    : L.nd > 0                 ? OVS_LOOKUP_RPC_TIMEOUT
-                                    : (C.hcm && L.hops >= C.hcm) ? OVS_LOOKUP_HOPMAX
-                                                                 : OVS_LOOKUP_NO_NEXT;
-        if (rpcs_out) rpcs_out[q] = L.nsent;
-        if (C.oneway) {
-            // SendToKeyListener::lookupFinished -> sendRouteMessage to getResult()[0] through the
-            // source's tx queue (BaseOverlay.cc:1107-1146, 1241-1259; SimpleNodeEntry.cc:164-194)
-            ovs_route_out o;
-            o.hops = (uint16_t)(L.minHops == 0x7FFFFFFF ? 0 : L.minHops);
-            const uint32_t R0 = sib[0];
-            if (valid && R0 != NONE) {
-                o.status = OVS_LOOKUP_OK;
-                o.responsible = R0;
-                o.one_way_hops = (uint8_t)(o.hops + (R0 != L.S ? 1 : 0));
-                int64_t lat = L.now;
-                if (R0 != L.S) {
-                    const double2 rxy = V.xy[R0];
-                    const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + DC.bwRoute;
-                    lat = newTx + DC.access2 + coord_ns(L.sx, L.sy, rxy.x, rxy.y, DC.round) + DC.bwRoute;
-                }
-                o.latency_ns = lat;
-            } else {
-                o.status = fail_status;
-                o.responsible = NONE;
-                o.one_way_hops = 0;
-                o.latency_ns = -1;
-            }
-            out[q] = o;
-            continue;
-        }
-        ovs_lookup_out o;
-        o.hops = (uint16_t)(L.minHops == 0x7FFFFFFF ? 0 : L.minHops);
-        o.is_valid = valid ? 1 : 0;
-        if (valid) {
-            int ns = 0;
-            for (int j = 0; j < C.ns; ++j) ns += sib[j] != NONE ? 1 : 0;
-            o.num_siblings = (uint32_t)ns;
-            o.latency_ns = L.now;
-            o.status = OVS_LOOKUP_OK;
-        } else {
-            for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
-            o.num_siblings = 0;
-            o.latency_ns = -1;
-            o.status = fail_status;
-        }
-        reinterpret_cast<ovs_lookup_out*>(out)[q] = o;
     }
 }
 
@@ -728,9 +796,11 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     X.lanes = lanes;
     hipMemsetAsync(err, 0, 4, st);
     const unsigned blocks = (unsigned)(lanes / 256);
+    const uint64_t waves = lanes / 64;
+    const uint64_t chunk = (nq + waves - 1) / waves;
     ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);   // or ovs_lookup_out (same size)
 #define KRL(ex, rg) hipLaunchKernelGGL((k_kad_refresh<ex, rg>), dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, qsrc, \
-                                       nq, o, sibs, responders, rtts, rpcs, err)
+                                       nq, chunk, o, sibs, responders, rtts, rpcs, err)
     if (t.exact) { if (reg) KRL(true, true); else KRL(true, false); }
     else { if (reg) KRL(false, true); else KRL(false, false); }
 #undef KRL
