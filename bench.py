@@ -202,6 +202,13 @@ def main():
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     dist_on = world > 1 or os.environ.get("OVS_BENCH_SHARD") == "1"
+    # the JSON line is the only stdout of the run: RCCL prints its version banner to fd 1 when the
+    # first communicator comes up, so fd 1 goes to stderr and the line to the saved descriptor
+    json_fd = None
+    if dist_on:
+        sys.stdout.flush()
+        json_fd = os.dup(1)
+        os.dup2(2, 1)
     if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -407,7 +414,10 @@ def main():
             },
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        if json_fd is not None:
+            os.write(json_fd, (json.dumps(line) + "\n").encode())
+        else:
+            print(json.dumps(line), flush=True)
     if dist_on:
         dist.destroy_process_group()
 
