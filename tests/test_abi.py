@@ -112,6 +112,8 @@ def test_params_chordlarge_semi_recursive():
     p = Params.from_ini(ini, "ChordLarge")
     assert (p.routingType, p.recNumRedundantNodes) == (1, 3)
     assert Params.from_ini('[General]\n**.routingType = "full-recursive"\n').routingType == 2
+    # Kademlia's bucket refresh lookups (Kademlia.cc:1483-1487) run exhaustive-iterative
+    assert Params.from_ini('[General]\n**.routingType = "exhaustive-iterative"\n').routingType == 3
 
 
 def test_reference_default_ini_parses():
