@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 5
+#define OVS_ABI_VERSION 6
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -483,7 +483,7 @@ typedef struct ovs_kad_req {        /* 32 B FindNodeCall */
     uint32_t key[5];
     uint32_t node;                  /* responder (global index, on the receiving rank's arc) */
     uint32_t tag;                   /* opaque to the receiver; returned in the response */
-    uint32_t pad;
+    uint32_t pad;                   /* LookupCall: 0x80000000 | numSiblings of findNode; 0 = KBR route */
 } ovs_kad_req;
 
 typedef struct ovs_kad_resp {       /* 104 B FindNodeResponse */
@@ -499,6 +499,17 @@ ovs_status  ovs_kad_load_shard(ovs_ctx* ctx, const ovs_key160* ids_all_sorted, u
 /* Start a batch of lookups whose sources lie on this arc (lookup id = qid_base + i). */
 ovs_status  ovs_kad_shard_begin(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                                 uint32_t qid_base, void* stream);
+/* LookupCalls (KBRTestApp lookup test, BaseOverlay::lookupRpc) on a sharded network:
+ * as ovs_kad_shard_begin, with num_siblings (-1 = s, 0 = exact-key lookup, at most 8;
+ * replaces ovs_lookup_batch's single-GPU LookupCall).  The rounds are the same calls;
+ * each request then carries numSiblings (ovs_kad_req.pad), so the serving rank answers
+ * findNode(key, numRedundantNodes, numSiblings).  A finished lookup's done record holds
+ * its LookupResponse (an ovs_lookup_out in the ovs_route_out slot) and its sibling
+ * vector goes to siblings[(qid - qid_base) * max(num_siblings, 1)], 0xFFFFFFFF padded:
+ * device memory of n rows that stays valid until the batch ends. */
+ovs_status  ovs_kad_shard_begin_lookup(ovs_ctx* ctx, int32_t num_siblings, const ovs_key160* keys,
+                                       const uint32_t* src, uint64_t n, uint32_t qid_base,
+                                       uint32_t* siblings, void* stream);
 /* One round for this rank's lookups.  *out_count, *done_count, *active_count are
  * device counters the kernel increments (the caller zeroes out_count and
  * active_count before each round).  shard_lo: HOST array of nshards+1 arc bounds. */
@@ -514,8 +525,9 @@ ovs_status  ovs_kad_shard_serve(ovs_ctx* ctx, const ovs_kad_req* in, uint64_t n,
  * node outside its arc: count 0xFFFFFFFF), is counted as an error; the latter still
  * completes its slot with an empty result, so the lookup terminates. */
 ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const ovs_kad_resp* in, uint64_t n, void* stream);
-/* Responses counted as errors by ovs_kad_shard_deliver since ovs_kad_shard_begin
- * (synchronises the device).  The caller fails the batch when it is non-zero. */
+/* Errors since ovs_kad_shard_begin: responses ovs_kad_shard_deliver could not hand over,
+ * and lookups whose source lies off this arc (they never run).  Synchronises the
+ * device.  The caller fails the batch when it is non-zero. */
 ovs_status  ovs_kad_shard_errors(ovs_ctx* ctx, uint64_t* bad);
 
 #ifdef __cplusplus

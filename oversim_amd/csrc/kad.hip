@@ -15,7 +15,8 @@ void kad_free(KadTables& t)
     if (t.nodex) hipFree(t.nodex);
     if (t.blks) hipFree(t.blks);
     if (t.sib) hipFree(t.sib);
-    t.nodes = nullptr; t.nodex = nullptr; t.blks = nullptr; t.sib = nullptr; t.rows_blks = 0;
+    if (t.slev) hipFree(t.slev);
+    t.nodes = nullptr; t.nodex = nullptr; t.blks = nullptr; t.sib = nullptr; t.slev = nullptr; t.rows_blks = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -337,6 +338,17 @@ __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, co
 
 static inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
+// the level msb(x ^ v) of every sibling x of every node v (sharded networks, KadTables::slev)
+__global__ void k_kad_sib_levels(const KadNode* __restrict__ nodes, const uint32_t* __restrict__ sib, uint32_t n,
+                                 int S5, uint8_t* __restrict__ slev)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= (uint64_t)n * S5) return;
+    const uint32_t v = (uint32_t)(j / S5);
+    const uint32_t x = sib[j];
+    slev[j] = x == NONE ? 0xFFu : (uint8_t)k_msb(k_xor(as_key(nodes[x].key), as_key(nodes[v].key)));
+}
+
 static hipError_t kad_prefix_flag(const KeyRec* recs, uint32_t n, KadTables& t, hipStream_t st)
 {
     uint32_t* tie = nullptr;
@@ -399,6 +411,11 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5, hipMemcpyDeviceToDevice, st);
     hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(nown, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn, seed,
                        sib_all, t.blks, t.rows_blks, lo, hi);
+    if (lo != 0 || hi != n) {
+        if ((e = hipMalloc(&t.slev, (uint64_t)n * S5)) != hipSuccess) { cleanup(); return e; }
+        hipLaunchKernelGGL(k_kad_sib_levels, dim3(nblk((uint64_t)n * S5, 256)), dim3(256), 0, st, t.nodes, sib_all, n,
+                           S5, t.slev);
+    }
     e = hipStreamSynchronize(st);
     cleanup();
     if (e != hipSuccess) return e;

@@ -9,6 +9,9 @@
 //                     member key, member index): bucket m of node v = blks[nodes[v].boff + 159 - m]
 //                     for m = rowlo(v) .. 159 (one block = one k <= 8 bucket, two lines); sibling
 //                     row of an owned node v = ceil(5s/8) blocks at sib_base + (v - lo) * sbn
+//  uint8_t slev[n*5s] one arc of a sharded network: the level msb(x ^ v) of each sibling x of every
+//                     node v (5s bytes a node), so a LookupCall decides isSiblingFor(numSiblings > 1)
+//                     of any responder on its home rank
 // The reference's structures these hold: Kademlia::siblingTable (a KademliaBucket of 5s entries
 // sorted by XOR distance to this node, Kademlia.cc:179, 315-317) and routingTable[160] (buckets
 // of up to k entries in LRU order, KademliaBucket.h:30-69, filled by routingAdd 432-756).
@@ -55,6 +58,8 @@ struct KadTables {
     KadBlk* blks = nullptr;        // bucket rows (rows_blks blocks), then the sibling rows of the owned arc
     uint64_t rows_blks = 0;        // bucket-row blocks; sibling rows start here
     uint32_t* sib = nullptr;       // (hi - lo) * S5 sibling member indices of the owned arc, NONE padded (export)
+    uint8_t* slev = nullptr;       // sharded networks: n * S5 sibling levels msb(x ^ v), 0xFF padded, for
+                                   // isSiblingFor(numSiblings > 1) of a responder off the owned arc
     uint32_t lo = 0, hi = 0;       // sibling / bucket rows exist for nodes [lo, hi) (the whole network unsharded)
     int k = 8, s = 8;
     uint64_t seed = 0;
@@ -68,6 +73,7 @@ struct KadView {
     const KadX* __restrict__ nodex;
     const KadBlk* __restrict__ blks;
     const KadBlk* __restrict__ sibb;    // sibling rows of the owned arc
+    const uint8_t* __restrict__ slev;   // sibling levels of every node (sharded networks only)
     const double2* __restrict__ xy;
     uint32_t n;
     int k;

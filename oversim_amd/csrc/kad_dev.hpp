@@ -295,8 +295,14 @@ __device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadNode& 
     const K160 D = k_xor(me, K);
     if (nsib == V.S5 && beyond_radius(V, r, c, D)) return false;
     if (!mask_hits(V, r, c, D)) return true;
-    const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
     int closer = 0;
+    if (c < V.lo || c >= V.hi) {
+        // a responder off this rank's arc (sharded LookupCalls): its replicated sibling levels
+        const uint8_t* lv = V.slev + (uint64_t)c * V.S5;
+        for (int i = 0; i < nsib; ++i) closer += (int)kbit(D, lv[i]);
+        return closer < numSiblings;
+    }
+    const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
     for (int i = 0; i < nsib; ++i) {
         const uint32_t x = L[i / KBLK].idx[i % KBLK];
         closer += (int)kbit(D, k_msb(k_xor(node_key(V.nodes, x), me)));
@@ -840,6 +846,7 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
 {
     KadView V{};
     V.nodes = t.nodes; V.nodex = t.nodex; V.blks = t.blks; V.sibb = t.blks ? t.blks + t.rows_blks : nullptr;
+    V.slev = t.slev;
     V.xy = xy; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
     V.sbn = (V.S5 + KBLK - 1) / KBLK;
     V.lo = t.lo; V.hi = t.hi;

@@ -42,6 +42,7 @@ struct ShardRes {
     uint64_t base;
     const KadView& V;
     const K160& K;
+    int ns;        // numSiblings of the lookup's findNode calls (1 for KBR routes)
     __device__ __forceinline__ bool ready(int slot) const { return res[base + slot].ready != 0; }
     __device__ __forceinline__ void fill(int slot, uint32_t c, const RespGeo& g, bool sb, int numR, bool local,
                                          SVec<8>& v) const
@@ -49,7 +50,7 @@ struct ShardRes {
         if (local) {
             // IterativeLookup::start: findNode at the source, on its home rank
             Blk8 b;
-            const int n = kad_find_node_blk<EX>(V, c, g, K, numR, sb, b, 1);
+            const int n = kad_find_node_blk<EX>(V, c, g, K, numR, sb, b, ns);
 #pragma unroll
             for (int i = 0; i < 8; ++i) { v.idx[i] = b.x[i]; v.d[i] = b.d[i]; }
             v.n = n;
@@ -78,6 +79,7 @@ struct ShardSend {
     int nsh;
     ovs_kad_req* __restrict__ stage;
     uint8_t* __restrict__ rtag;
+    uint32_t pad;   // LookupCall: bit 31 | numSiblings (the responder's findNode argument); 0 for KBR routes
     __device__ __forceinline__ void operator()(int slot, uint32_t x, bool isTo) const
     {
         // a timeout event carries no result
@@ -87,7 +89,7 @@ struct ShardSend {
         for (int w = 0; w < 5; ++w) q.key[w] = K->w[w];
         q.node = x;
         q.tag = (uint32_t)(base + slot);
-        q.pad = 0;
+        q.pad = pad;
         stage[base + slot] = q;
         rtag[base + slot] = (uint8_t)kshard_owner(shard_lo, nsh, x);
     }
@@ -97,13 +99,14 @@ struct NoRecord {
     __device__ __forceinline__ void operator()(int, uint32_t) const {}
 };
 
-template <int A, bool EX>
+template <int A, bool EX, bool LK>
 __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts DC, KadLC LC,
                                                         KadLookup<A>* __restrict__ st, uint8_t* __restrict__ act,
                                                         const uint32_t* __restrict__ qids, KadRes* __restrict__ res,
                                                         uint64_t nlook, const uint64_t* __restrict__ shard_lo, int nsh,
                                                         ovs_kad_req* __restrict__ rstage, uint8_t* __restrict__ rtag,
-                                                        ovs_done_rec* __restrict__ dstage, uint8_t* __restrict__ ltag)
+                                                        ovs_done_rec* __restrict__ dstage, uint8_t* __restrict__ ltag,
+                                                        uint32_t* __restrict__ sib_out)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nlook) return;
@@ -111,11 +114,12 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
     if (a == 0) return;            // finished in an earlier round: tags stay 0xFF
     KadLookup<A> L = st[i];
     SVec<8> r;
-    ShardSend on{res, i * A, &L.K, shard_lo, nsh, rstage, rtag};
-    const ShardRes<EX> gr{res, i * A, V, L.K};   // the first event is IterativeLookup::start
+    const int ns = LK ? LC.numSiblings : 1;
+    ShardSend on{res, i * A, &L.K, shard_lo, nsh, rstage, rtag, LK ? (0x80000000u | (uint32_t)ns) : 0u};
+    const ShardRes<EX> gr{res, i * A, V, L.K, ns};   // the first event is IterativeLookup::start
     const NoRecord rec;
     while (!kad_lookup_done(L)) {
-        if (!kad_lookup_event<A, EX, false>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
+        if (!kad_lookup_event<A, EX, LK>(L, V, DC, LC, r, gr, on, rec)) break;   // earliest event still waits
     }
     // the lookup's outcome this round, staged at its own index: finished (class 0, its done
     // record) or still active (class 1, counted)
@@ -124,6 +128,33 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
         dr.qid = qids[i];
         dr.pad = 0;
         dr.out = kad_lookup_output(L, V, DC, LC);
+        if (LK) {
+            // the LookupResponse (BaseOverlay.cc:1272-1300): the answering sibling's findNode
+            // result (an exact-key lookup: the key's node), in the lookup's own sibling row
+            const bool ok = dr.out.status == OVS_LOOKUP_OK;
+            uint32_t cnt = 0;
+            if (ns == 0) {
+                sib_out[i] = ok ? L.result : NONE;
+                cnt = ok ? 1u : 0u;
+            } else {
+                uint32_t* row = sib_out + i * (uint64_t)ns;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (j < ns) {
+                        const bool has = ok && j < r.n;
+                        row[j] = has ? r.idx[j] : NONE;
+                        cnt += has ? 1u : 0u;
+                    }
+                }
+            }
+            ovs_lookup_out lo;
+            lo.num_siblings = cnt;
+            lo.hops = dr.out.hops;
+            lo.status = dr.out.status;
+            lo.is_valid = ok ? 1 : 0;
+            lo.latency_ns = ok ? dr.out.latency_ns : -1;
+            __builtin_memcpy(&dr.out, &lo, sizeof lo);
+        }
         dstage[i] = dr;
         ltag[i] = 0;
         act[i] = 0;
@@ -136,15 +167,24 @@ __global__ __launch_bounds__(256) void k_kad_shard_step(KadView V, DelayConsts D
 template <int A>
 __global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* __restrict__ src, uint64_t n,
                                  uint32_t qid_base, const double2* __restrict__ xy, KadLookup<A>* __restrict__ st,
-                                 uint8_t* __restrict__ act, uint32_t* __restrict__ qids, KadRes* __restrict__ res)
+                                 uint8_t* __restrict__ act, uint32_t* __restrict__ qids, KadRes* __restrict__ res,
+                                 uint32_t lo, uint32_t hi, unsigned long long* bad)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const uint32_t S = src[i];
+    qids[i] = qid_base + (uint32_t)i;
+    if (S < lo || S >= hi) {
+        // the source's own findNode needs its rows: a source off this arc is an error
+        // (ovs_kad_shard_errors), and its lookup never runs
+        act[i] = 0;
+        atomicAdd(bad, 1ull);
+        return;
+    }
     KadLookup<A> L;
-    kad_lookup_init(L, keys[i], src[i], xy);
+    kad_lookup_init(L, keys[i], S, xy);
     st[i] = L;
     act[i] = 1;
-    qids[i] = qid_base + (uint32_t)i;
     for (int s = 0; s < A; ++s) res[i * A + s].ready = 1;
 }
 
@@ -156,6 +196,8 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const ovs_kad_req q = in[j];
+    // a LookupCall's request names its numSiblings (ShardSend); a KBR route's uses 1
+    const int ns = (q.pad & 0x80000000u) ? (int)(q.pad & 0xFFu) : 1;
     K160 K;
     for (int w = 0; w < 5; ++w) K.w[w] = q.key[w];
     ovs_kad_resp o;
@@ -166,9 +208,9 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
         return;
     }
     const KadNode rr = load_node(V.nodes, q.node);
-    const bool sb = kad_is_sibling1(V, rr, q.node, K);
+    const bool sb = kad_is_sibling(V, rr, q.node, K, ns);
     SVec<8> r;
-    kad_find_node_vec<8, EX>(V, q.node, rr, K, LC.redundant, sb, r);
+    kad_find_node_vec<8, EX>(V, q.node, rr, K, LC.redundant, sb, r, ns);
     o.count = (uint32_t)r.n;
 #pragma unroll
     for (int k = 0; k < 8; ++k) { o.nodes[k] = r.idx[k]; o.dist_hi[k] = r.d[k]; }
@@ -218,11 +260,12 @@ size_t kad_lookup_state_bytes(int alpha)
 }
 
 hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
-                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, hipStream_t s)
+                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, uint32_t lo,
+                          uint32_t hi, unsigned long long* bad, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
 #define KI(a) hipLaunchKernelGGL(k_kad_shard_init<a>, dim3(nblk(n, 256)), dim3(256), 0, s, keys, src, n, qid_base, xy, \
-                                 (KadLookup<a>*)st, act, qids, res)
+                                 (KadLookup<a>*)st, act, qids, res, lo, hi, bad)
     switch (alpha) {
     case 1: KI(1); break;
     case 2: KI(2); break;
@@ -237,15 +280,21 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
                           const DelayConsts& DC, void* st, uint8_t* act, const uint32_t* qids, KadRes* res,
                           uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
                           uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                          unsigned long long* done_count, unsigned long long* active_count, StageBuf& stage,
-                          hipStream_t s)
+                          unsigned long long* done_count, unsigned long long* active_count, int lk_ns,
+                          uint32_t* sib_out, StageBuf& stage, hipStream_t s)
 {
-    if (!kad_params_supported(P, t) || P.numSiblings != 1) return hipErrorNotSupported;
+    const bool lk = lk_ns >= 0;
+    ovs_params Q = P;
+    if (lk) Q.numSiblings = lk_ns;
+    if (!kad_params_supported(Q, t) || Q.numSiblings != (lk ? lk_ns : 1) || (lk && !sib_out))
+        return hipErrorNotSupported;
     if (nlook == 0) return hipSuccess;
     if (nsh < 1 || nsh > MAXSHARDS) return hipErrorInvalidValue;
     const KadView V = kad_make_view(t, xy, n);
-    KadLC LC = kad_make_lc(P, t);
-    kad_lc_sizes(LC, DC, n);
+    KadLC LC = kad_make_lc(Q, t);
+    DelayConsts DL = DC;
+    DL.lookupCall = lk ? 1 : 0;     // a LookupCall ends at its last response (no route message)
+    kad_lc_sizes(LC, DL, n);
     const int A = LC.alpha;
     // stage: a request per pending-call slot, a done record per lookup, and their tags
     const uint64_t ns = nlook * (uint64_t)A;
@@ -259,9 +308,11 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     uint8_t* rtag = sb + ort;
     uint8_t* ltag = sb + olt;
     if ((e = hipMemsetAsync(rtag, 0xFF, ns + nlook, s)) != hipSuccess) return e;   // rtag and ltag are adjacent
-#define KSX(a, x) hipLaunchKernelGGL((k_kad_shard_step<a, x>), dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DC, LC, \
-                                 (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, rstage, rtag, dstage, ltag)
-#define KS(a) do { if (t.exact) KSX(a, true); else KSX(a, false); } while (0)
+#define KSX(a, x, l) hipLaunchKernelGGL((k_kad_shard_step<a, x, l>), dim3(nblk(nlook, 256)), dim3(256), 0, s, V, DL, \
+                                    LC, (KadLookup<a>*)st, act, qids, res, nlook, shard_lo, nsh, rstage, rtag, dstage, \
+                                    ltag, sib_out)
+#define KS(a) do { if (t.exact) { if (lk) KSX(a, true, true); else KSX(a, true, false); } \
+                   else { if (lk) KSX(a, false, true); else KSX(a, false, false); } } while (0)
     switch (A) {
     case 1: KS(1); break;
     case 2: KS(2); break;
@@ -292,7 +343,10 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
                            ovs_kad_resp* out, hipStream_t s)
 {
-    if (!kad_params_supported(P, t) || P.numSiblings != 1) return hipErrorNotSupported;
+    // numSiblings travels with each request; the rest of the configuration is the rank's
+    ovs_params Q = P;
+    Q.numSiblings = 1;
+    if (!kad_params_supported(Q, t)) return hipErrorNotSupported;
     if (nreq == 0) return hipSuccess;
     const KadView V = kad_make_view(t, nullptr, n);
     const KadLC LC = kad_make_lc(P, t);

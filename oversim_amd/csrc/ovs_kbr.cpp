@@ -72,6 +72,8 @@ struct ovs_ctx {
     unsigned long long* kbad = nullptr;  // undeliverable responses
     uint64_t knlook = 0, kcap = 0;
     int kalpha = 0;
+    int32_t kns = -1;                    // LookupCall batch: numSiblings (-1: KBR routes)
+    uint32_t* ksib = nullptr;            // ... and the caller's sibling rows
     // scratch for host-pointer calls
     std::vector<void*> scratch;
 };
@@ -832,15 +834,20 @@ ovs_status ovs_kad_load_shard(ovs_ctx* c, const ovs_key160* ids, uint64_t n, con
     return kad_load_arc(c, ids, n, xy, lo, hi, flags);
 }
 
-ovs_status ovs_kad_shard_begin(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
-                               void* stream)
+namespace {
+
+ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const ovs_key160* keys, const uint32_t* src,
+                                uint64_t n, uint32_t qid_base, void* stream)
 {
     if (!c || (n && (!keys || !src))) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
-    ovs_status st = check_common(c, c->P);
+    ovs_params P = c->P;
+    if (lk_ns >= 0) P.numSiblings = 1;     // the route checks; numSiblings is the LookupCall's
+    ovs_status st = check_common(c, P);
     if (st != OVS_OK) return st;
-    if (c->P.routingType != 0) return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
-    if (!kad_params_supported_host(c->P, c->kad) || c->P.numSiblings != 1)
+    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative");
+    if (lk_ns >= 0) P.numSiblings = lk_ns;
+    if (!kad_params_supported_host(P, c->kad) || (lk_ns < 0 && P.numSiblings != 1))
         return fail(c, OVS_ENOTSUP, "lookup configuration not implemented");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
@@ -857,10 +864,32 @@ ovs_status ovs_kad_shard_begin(ovs_ctx* c, const ovs_key160* keys, const uint32_
         c->kalpha = alpha;
     }
     c->knlook = n;
+    c->kns = lk_ns;
+    c->ksib = sib;
     HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
     HIPCHK(c, kad_shard_init(alpha, reinterpret_cast<const K160*>(keys), src, n, qid_base, c->xy, c->kst, c->kact,
-                             c->kqids, c->kres, s));
+                             c->kqids, c->kres, c->kad.lo, c->kad.hi, c->kbad, s));
     return OVS_OK;
+}
+
+}  // namespace
+
+ovs_status ovs_kad_shard_begin(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
+                               void* stream)
+{
+    return kad_shard_begin_impl(c, -1, nullptr, keys, src, n, qid_base, stream);
+}
+
+ovs_status ovs_kad_shard_begin_lookup(ovs_ctx* c, int32_t num_siblings, const ovs_key160* keys, const uint32_t* src,
+                                      uint64_t n, uint32_t qid_base, uint32_t* siblings, void* stream)
+{
+    if (!c || (n && !siblings)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    // BaseOverlay::lookupRpc: numSiblings < 0 -> getMaxNumSiblings() = s (Kademlia.cc:347-350)
+    const int32_t ns = num_siblings < 0 ? c->P.s : num_siblings;
+    if (ns > c->P.s) return fail(c, OVS_EINVAL, "numSiblings too big!");
+    if (ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall implements numSiblings <= 8");
+    return kad_shard_begin_impl(c, ns, siblings, keys, src, n, qid_base, stream);
 }
 
 ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap,
@@ -888,7 +917,7 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, 
     if (bst != OVS_OK) return bst;
     hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kqids,
                                   c->kres, c->knlook, c->d_bounds, (int)nshards, out, out_dest, out_cap, out_count,
-                                  done, done_cap, done_count, active_count, c->stage[s], s);
+                                  done, done_cap, done_count, active_count, c->kns, c->ksib, c->stage[s], s);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard step");
     return OVS_OK;
 }

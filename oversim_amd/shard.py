@@ -200,6 +200,8 @@ for _name, _args in {
     "ovs_shard_lookup_finish": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p],
     "ovs_kad_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
     "ovs_kad_shard_begin": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p],
+    "ovs_kad_shard_begin_lookup": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                   C.c_void_p, C.c_void_p],
     "ovs_kad_shard_step": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
     "ovs_kad_shard_serve": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p],
@@ -438,13 +440,16 @@ class KadShardStepper:
     """One rank's arc of a Kademlia network on one device (ovs_kad_load_shard + shard kernels)."""
 
     def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device,
-                 params: Params | None = None):
+                 params: Params | None = None, lookup_siblings: int | None = None):
+        """lookup_siblings: run KBRTestApp LookupCalls with that many siblings (-1 = s, 0 = exact-key
+        lookup; ovs_kad_shard_begin_lookup) instead of one-way routes; results via lookup_results()."""
         import torch
         self.torch, self.dev = torch, device
         self.rank, self.bounds, self.world = rank, [int(b) for b in bounds], len(bounds) - 1
         self.eng = KbrEngine(device.index if device.index is not None else 0)
         self.params = params or Params.kademlia()
         self.eng.set_params(self.params)
+        self.lookup_siblings = lookup_siblings
         ids = np.ascontiguousarray(ids, dtype=np.uint32)
         xy = np.ascontiguousarray(xy, dtype=np.float64)
         st = lib().ovs_kad_load_shard(self.eng._h, ids.ctypes.data_as(C.c_void_p), len(ids),
@@ -476,8 +481,16 @@ class KadShardStepper:
         self.out_dest = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
         self.done = torch.empty((max(n, 1), DONE_BYTES), dtype=torch.uint8, device=self.dev)
         self.counters.zero_()
-        st = lib().ovs_kad_shard_begin(self.eng._h, self._p(keys_t), self._p(src_t), n, qid_base, self._s())
-        self.eng._chk(st, "ovs_kad_shard_begin")
+        self.qid_base = qid_base
+        if self.lookup_siblings is None:
+            st = lib().ovs_kad_shard_begin(self.eng._h, self._p(keys_t), self._p(src_t), n, qid_base, self._s())
+            self.eng._chk(st, "ovs_kad_shard_begin")
+            return
+        ns = self.lookup_siblings if self.lookup_siblings >= 0 else self.params.s
+        self.sib = torch.empty((max(n, 1), max(ns, 1)), dtype=torch.int32, device=self.dev)
+        st = lib().ovs_kad_shard_begin_lookup(self.eng._h, self.lookup_siblings, self._p(keys_t), self._p(src_t), n,
+                                              qid_base, self._p(self.sib), self._s())
+        self.eng._chk(st, "ovs_kad_shard_begin_lookup")
 
     def step(self):
         """One round: returns (requests, destination ranks, active lookups on this rank)."""
@@ -520,7 +533,7 @@ class KadShardStepper:
             self.eng._chk(st, "ovs_kad_shard_deliver")
 
     def errors(self) -> int:
-        """Responses ovs_kad_shard_deliver could not hand to a lookup (mis-routed requests)."""
+        """ovs_kad_shard_errors: undeliverable responses (mis-routed requests) and sources off this arc."""
         bad = C.c_uint64(0)
         self.eng._chk(lib().ovs_kad_shard_errors(self.eng._h, C.byref(bad)), "ovs_kad_shard_errors")
         return int(bad.value)
@@ -531,8 +544,17 @@ class KadShardStepper:
             raise RuntimeError("done buffer overflow")
         bad = self.errors()
         if bad:
-            raise RuntimeError(f"{bad} Kademlia responses could not be delivered (request sent to the wrong rank)")
+            raise RuntimeError(f"{bad} Kademlia shard errors: responses that could not be delivered (request sent "
+                               "to the wrong rank) or lookups whose source lies off this rank's arc")
         return self.done[:k]
+
+    def lookup_results(self, done):
+        """LookupCall mode: (qid, ovs_lookup_out records, siblings rows) of finished records, in their order."""
+        recs = done_to_numpy(done)
+        qid = recs["qid"].copy()
+        lo = done[:, 8:24].contiguous().cpu().numpy().reshape(-1).view(LOOKUP_OUT_DTYPE)
+        sib = self.sib.cpu().numpy().view(np.uint32)[qid - np.uint32(self.qid_base)]
+        return qid, lo, sib
 
 
 def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 5_000):

@@ -551,3 +551,67 @@ def test_shard_lookup_calls_emulated_on_one_gpu(world, ns):
         assert np.array_equal(lo[f], ref[f]), f
     assert np.array_equal(sib, ref["siblings"])
     assert rounds >= 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,alpha,ns", [(2, 3, 8), (3, 1, 3), (4, 3, 0), (8, 2, -1)])
+def test_kad_shard_lookup_calls_emulated_on_one_gpu(world, alpha, ns):
+    """KBRTestApp LookupCalls on W Kademlia arcs (ovs_kad_shard_begin_lookup): the requests carry
+    numSiblings to the serving rank; every LookupResponse and sibling row equals the single-context
+    ovs_lookup_batch's (itself checked against the oracle in test_gpu_lookupcall.py).  ns = 0 is
+    the exact-key lookup."""
+    from oversim_amd import KbrEngine, Params
+    from oversim_amd.shard import KadShardStepper, arc_bounds, route_kad_local_shards
+    n, m = 1 << 15, 3000
+    net = W.population(n, 97)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=alpha)
+    steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params, lookup_siblings=ns)
+                for r in range(world)]
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s = W.lookups(net.ids, m, 98 + r, node_ids=(ns == 0 or r % 2 == 1))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k.view(np.int32)).to(dev))
+        ss.append(torch.from_numpy(s.view(np.int32)).to(dev))
+        qb.append(r * m)
+        allk.append(k); alls.append(s)
+    dones, rounds = route_kad_local_shards(steppers, ks, ss, qb)
+    parts = [steppers[r].lookup_results(dones[r]) for r in range(world)]
+    qid = np.concatenate([p[0] for p in parts])
+    lo = np.concatenate([p[1] for p in parts])
+    sib = np.concatenate([p[2] for p in parts])
+    order = np.argsort(qid)
+    assert np.array_equal(qid[order], np.arange(world * m))
+    lo, sib = lo[order], sib[order]
+    with KbrEngine(0) as eng:
+        eng.set_params(params)
+        eng.kad_load(net.ids, net.xy)
+        ref = eng.lookupCall(np.concatenate(allk), np.concatenate(alls), ns)
+    for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+        assert np.array_equal(lo[f], ref[f]), f
+    assert np.array_equal(sib, ref["siblings"])
+    assert (lo["is_valid"] == 1).mean() > 0.9
+    assert rounds >= 3
+
+
+@pytest.mark.gpu
+def test_kad_shard_source_off_arc_is_an_error():
+    """A lookup whose source lies on another rank's arc never runs and is reported by
+    ovs_kad_shard_errors (its own findNode needs that rank's rows)."""
+    from oversim_amd.shard import KadShardStepper, arc_bounds, route_kad_local_shards
+    n, world = 1 << 14, 2
+    net = W.population(n, 97)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev) for r in range(world)]
+    k, _ = W.lookups(net.ids, 4, 5, node_ids=False)
+    s_ok = np.full(4, bounds[0], dtype=np.uint32)
+    s_bad = s_ok.copy()
+    s_bad[2] = bounds[1]            # on arc 1, handed to rank 0
+    kt = torch.from_numpy(k.view(np.int32)).to(dev)
+    with pytest.raises(RuntimeError, match="could not be delivered"):
+        route_kad_local_shards(steppers, [kt, kt], [torch.from_numpy(s_bad.view(np.int32)).to(dev),
+                                                    torch.from_numpy((s_ok + bounds[1]).view(np.int32)).to(dev)],
+                               [0, 4])
