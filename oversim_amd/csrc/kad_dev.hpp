@@ -491,7 +491,7 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
         if (dj) { b.x[j] = NONE; b.d[j] = ~0ull; }
         dup |= dj;
     }
-    if (dup) blk_sort8<true, EX>(b, K, nodes);     // holes to the end
+    if (dup) blk_sort8<false, EX>(b, K, nodes);    // holes to the end (every b flag is 2: nothing to carry)
     blk_merge_top8<true, EX>(a, b, K, nodes);
     const int n = blk_trunc(a, cap);
     int numNew = 0;
