@@ -268,9 +268,9 @@ typedef struct ovs_lookup_out {
 /* Batched LookupCalls: lookup i resolves keys[i] at node src[i] with
  * num_siblings siblings (-1 = getMaxNumSiblings(): Chord successorListSize,
  * Kademlia s; larger than that is OVS_EINVAL like the reference's
- * "numSiblings too big!"; 0 = an exact-key lookup, Kademlia: the lookup ends at
- * the first response that carries the key's node, IterativeLookup.cc:171-184,
- * 862-870).  siblings = n*max(num_siblings, 1) node indices, the
+ * "numSiblings too big!"; 0 = an exact-key lookup: the lookup ends at the first
+ * response that carries the key's node, IterativeLookup.cc:171-184, 862-870;
+ * Chord's responsible node answers nothing then, Chord.cc:573-580).  siblings = n*max(num_siblings, 1) node indices, the
  * response's sibling vector in order, 0xFFFFFFFF padded.  Iterative routing,
  * single-context (unsharded) networks. */
 ovs_status  ovs_lookup_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,

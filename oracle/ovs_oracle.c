@@ -1562,9 +1562,11 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
     if (nextHops.size == 0) {
         L->finished = 1; L->success = 0;
     } else if (L->numSiblings == 0 && ov_isSiblingFor(net, S, S, key, 0, &err)) {
-        /* an exact-key lookup of the source's own key (start() 171-184) */
+        /* an exact-key lookup the source is a sibling for (start() 171-184): found if it is the
+         * source's own key */
         lk_addSibling(L, S);
-        L->success = L->finished = 1;
+        L->success = EQ(&net->ids[S], key);
+        L->finished = 1;
     } else if (L->numSiblings != 0 && !L->exh && ov_isSiblingFor(net, S, S, key, L->numSiblings, &err)) {
         for (int i = 0; i < nextHops.size; i++) lk_addSibling(L, nextHops.v[i]);
         L->success = L->finished = 1;
@@ -1789,7 +1791,7 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     if (numSiblings < 0) numSiblings = maxs;                              /* BaseOverlay.cc:1942-1944 */
     if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
     if (numSiblings < 0 || numSiblings > 16) { set_err("numSiblings must be 0..16"); return -1; }
-    if (numSiblings == 0 && net->type != NET_KAD) { set_err("numSiblings = 0: Kademlia only"); return -1; }
+    if (numSiblings == 0 && net->type == NET_KOORDE) { set_err("numSiblings = 0: Chord and Kademlia only"); return -1; }
     if (net->p.routingType != 0 && net->p.routingType != 3) { set_err("LookupCall: iterative routing only"); return -1; }
     const int exh = net->p.routingType == 3 ? net->p.lookupRedundantNodes : 0;
     if (exh && (net->type != NET_KAD || numSiblings > exh)) {

@@ -1143,6 +1143,79 @@ hipError_t launch_shard_lookup_finish(const ChordView& V, int ns, const ovs_done
     return hipGetLastError();
 }
 
+// Chord LookupCalls with numSiblings = 0 (exact-key lookups).  findNode's choice at a node that is
+// not responsible for K does not depend on numSiblings (Chord.cc:548-599), so the lookup follows the
+// chain R1, R2, ... of the same key routed as a one-way lookup; io holds that route, run without
+// RPC / lookup timeouts and with hopCountMax + 1 hops recorded in hopseq (stride H).  Replayed here
+// with the exact-key rules (IterativeLookup.cc:157-184, 803-921, 1067-1170):
+//  * the source responsible: its findNode answers [S, succ...] downsized to 0 -> no next hop, fail;
+//  * response i from a node not responsible for K carries the next hop R(i+1): the lookup succeeds
+//    there when R(i+1)'s key is K (862-870), the LookupResponse holding R(i+1);
+//  * the responsible node answers an empty vector (and no sibling flag counts for numSiblings = 0):
+//    nothing left to ask, fail (HOPMAX when the hop budget is spent, as sendRpc checks that first);
+//  * every call's RTT with the response's real size (0 nodes from the responsible node), with the
+//    RPC / lookup timeouts of k_chord_route and K1.
+__global__ void k_chord_exact_finish(ChordView V, DelayConsts DC, int hcm, const K160* __restrict__ keys,
+                                     const uint32_t* __restrict__ src, const uint32_t* __restrict__ hopseq, int H,
+                                     ovs_route_out* __restrict__ io, uint64_t n)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const ovs_route_out r = io[q];
+    const uint32_t S = src[q];
+    const K160 K = keys[q];
+    const int nrec = min((int)r.hops, H);
+    const int k = r.status == OVS_LOOKUP_OK ? (int)r.hops : -1;   // the responsible node answered response k
+    const double2 sxy = V.xy[S];
+    ovs_route_out o;
+    o.responsible = NONE;
+    o.one_way_hops = 0;
+    o.latency_ns = -1;
+    o.hops = 0;
+    o.status = k == 0 ? (uint8_t)OVS_LOOKUP_NO_NEXT : r.status;   // nothing sent: the start's outcome
+    int64_t t = 0;
+    for (int i = 1; i <= nrec; ++i) {
+        const uint32_t Ri = hopseq[q * (uint64_t)H + (i - 1)];
+        const bool resp = i == k;
+        const double2 rxy = V.xy[Ri];
+        const int64_t cd = coord_ns(sxy.x, sxy.y, rxy.x, rxy.y, DC.round);
+        const int64_t rtt = DC.msgCall + (resp ? resp_ns(DC, 0) : DC.msgResp1) + 2 * cd;
+        if (rtt >= DC.rpcTimeout) {
+            o.status = (t + DC.rpcTimeout > DC.lookupTimeout) ? OVS_LOOKUP_TIMEOUT : OVS_LOOKUP_RPC_TIMEOUT;
+            break;
+        }
+        t += rtt;
+        if (t > DC.lookupTimeout) { o.status = OVS_LOOKUP_TIMEOUT; break; }
+        o.hops = (uint16_t)i;
+        if (i == nrec && r.status == OVS_LOOKUP_BROKEN) { o.status = OVS_LOOKUP_BROKEN; break; }
+        if (resp) { o.status = (hcm && i >= hcm) ? OVS_LOOKUP_HOPMAX : OVS_LOOKUP_NO_NEXT; break; }
+        if (i < nrec) {
+            const uint32_t nx = hopseq[q * (uint64_t)H + i];
+            if (k_eq(key_of(load_rec(V.recs, nx)), K)) {
+                o.status = OVS_LOOKUP_OK;
+                o.responsible = nx;
+                o.one_way_hops = (uint8_t)(i + 1);
+                o.latency_ns = t;
+                break;
+            }
+        }
+        if (hcm && i >= hcm) { o.status = OVS_LOOKUP_HOPMAX; break; }
+        // the route ended after response i without a recorded next hop: its next was visited
+        if (i == nrec) { o.status = r.status; break; }
+    }
+    io[q] = o;
+}
+
+hipError_t launch_chord_exact_finish(const ChordView& V, const DelayConsts& DC, int hcm, const K160* keys,
+                                     const uint32_t* src, const uint32_t* hopseq, int H, ovs_route_out* io,
+                                     uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chord_exact_finish, dim3(nblk(n, 256)), dim3(256), 0, s, V, DC, hcm, keys, src, hopseq, H,
+                       io, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_lookup_finish(const ChordView& V, bool chord, bool ideal, int ns, ovs_route_out* io,
                                 uint32_t* sibs, uint64_t n, hipStream_t s)
 {

@@ -27,6 +27,10 @@ hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t
                                   uint32_t max_out, uint8_t* out_count, uint8_t* out_sib, hipStream_t s);
 hipError_t launch_shard_lookup_finish(const ChordView& V, int ns, const ovs_done_rec* done, ovs_lookup_out* out,
                                       uint32_t* sibs, uint64_t n, hipStream_t s);
+// Chord exact-key LookupCalls (numSiblings = 0) replayed from the recorded one-way chain (chord.hip)
+hipError_t launch_chord_exact_finish(const ChordView& V, const DelayConsts& DC, int hcm, const K160* keys,
+                                     const uint32_t* src, const uint32_t* hopseq, int H, ovs_route_out* io,
+                                     uint64_t n, hipStream_t s);
 hipError_t launch_lookup_finish(const ChordView& V, bool chord, bool ideal, int ns, ovs_route_out* io,
                                 uint32_t* sibs, uint64_t n, hipStream_t s);
 hipError_t launch_fill_rpcs_from_hops(const ovs_route_out* out, uint64_t n, uint32_t* rpcs, hipStream_t s);

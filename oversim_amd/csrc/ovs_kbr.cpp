@@ -1160,8 +1160,10 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     const int32_t maxs = chord ? c->P.successorListSize : c->P.s;
     const int32_t ns = num_siblings < 0 ? maxs : num_siblings;
     if (ns > maxs) return fail(c, OVS_EINVAL, "numSiblings too big!");
-    if (ns == 0 && (chord || c->P.routingType != 0))
-        return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup) is implemented for iterative Kademlia");
+    if (ns == 0 && c->P.routingType != 0)
+        return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup) is implemented for iterative routing");
+    if (ns == 0 && chord && c->P.hopCountMax < 1)
+        return fail(c, OVS_ENOTSUP, "Chord exact-key LookupCalls need hopCountMax >= 1");
     if (ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall implements numSiblings <= 8");
     ovs_params P = c->P;
     P.numSiblings = 1;          // the route checks: one-way configuration, numSiblings applied below
@@ -1213,14 +1215,24 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         dout = reinterpret_cast<ovs_route_out*>(out);
         dsib = siblings;
     }
-    const int H = P.hopCountMax > 0 ? P.hopCountMax : 1;
-    const bool need_hop = (chord && !c->ideal) || kad_exh;   // visited check (explicit tables; exhaustive lookups)
+    // Chord exact-key lookups replay the one-way chain recorded one hop beyond hopCountMax
+    const bool chord_exact = chord && ns == 0;
+    const int H = chord_exact ? P.hopCountMax + 1 : P.hopCountMax > 0 ? P.hopCountMax : 1;
+    const bool need_hop = (chord && !c->ideal) || kad_exh || chord_exact;   // visited check (explicit tables; exhaustive lookups)
     if (need_hop) {
         HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H));
         HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
     }
     hipError_t e;
-    if (chord) {
+    if (chord_exact) {
+        // the chain: a one-way route (numSiblings 1, no LookupCall sizes) without timeouts
+        DelayConsts DR = delay_consts(P);
+        DR.rpcTimeout = DR.lookupTimeout = INT64_MAX / 4;
+        LookupConsts LR{H, 1, P.lookupRedundantNodes, 0};
+        e = launch_chord_route(chord_view(c), c->ideal, DR, LR, dk, ds, n, dout, dhop, c->num_cu, s);
+        if (e == hipSuccess)
+            e = launch_chord_exact_finish(chord_view(c), delay_consts(P), P.hopCountMax, dk, ds, dhop, H, dout, n, s);
+    } else if (chord) {
         LookupConsts LC{P.hopCountMax, ns, P.lookupRedundantNodes, 0};
         e = launch_chord_route(chord_view(c), c->ideal, DC, LC, dk, ds, n, dout, dhop, c->num_cu, s);
     } else if (kad_exh) {

@@ -113,8 +113,9 @@ def test_lookup_call_rejects(engine: KbrEngine):
     keys, src = W.lookups(net.ids, 10, 46, node_ids=True)
     with pytest.raises(KbrError):
         engine.lookupCall(keys, src, 9)                # numSiblings too big!
+    engine.set_params(Params.chord().replace(hopCountMax=0))
     with pytest.raises(KbrError):
-        engine.lookupCall(keys, src, 0)                # exact-key lookups: Kademlia only
+        engine.lookupCall(keys, src, 0)                # Chord exact-key lookups need a hop budget
     engine.set_params(Params.chord().replace(routingType=1))
     with pytest.raises(KbrError):
         engine.lookupCall(keys, src)
@@ -163,3 +164,67 @@ def test_kademlia_exact_key_lookup_calls(engine, alpha):
         assert np.array_equal(r[f], e[f]), f
     assert np.array_equal(r["siblings"], e["siblings"])
     assert r["is_valid"][:3000].mean() > 0.99 and r["is_valid"][-64:].all() and not r["is_valid"][3000:4000].any()
+
+
+def _exact_keys(net, seed, m=3000):
+    """node-ID keys, random keys, every source's own key, and the key of the source's successor
+    (found by the source's own findNode, which the start does not check: the call goes to the key's
+    node, which answers nothing)."""
+    n = len(net.ids)
+    k1, s1 = W.lookups(net.ids, m, seed, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m // 3, seed + 1, node_ids=False)
+    own = np.arange(min(n, 64), dtype=np.uint32)
+    nxt = ((own.astype(np.int64) + 1) % n).astype(np.uint32)
+    keys = np.concatenate([k1, k2, net.ids[own], net.ids[nxt]])
+    src = np.concatenate([s1, s2, own, own])
+    return keys, src
+
+
+@pytest.mark.parametrize("n,seed", [(2, 1), (6, 2), (1000, 4), (20000, 5)])
+@pytest.mark.parametrize("hcm", [50, 3])
+def test_chord_exact_key_lookup_calls(engine: KbrEngine, n, seed, hcm):
+    """numSiblings = 0 on a converged ring (IterativeLookup.cc:157-184, 862-870; Chord.cc:573-580
+    downsizes the responsible node's answer to nothing): a node-ID key is found by the response
+    that names its node, random keys and keys the source is responsible for fail -- every field
+    as the oracle, which runs the literal IterativeLookup."""
+    net = W.population(n, seed)
+    engine.set_params(Params.chord().replace(hopCountMax=hcm))
+    engine.chord_load(net.ids, net.xy)
+    o = OracleNet("chord", net.ids, net.xy, chord_params(hopCountMax=hcm))
+    keys, src = _exact_keys(net, seed + 60)
+    g = engine.lookupCall(keys, src, 0)
+    _eq(g, o.lookup_call(keys, src, 0), f"chord exact n={n} hcm={hcm}")
+    assert g["siblings"].shape == (len(keys), 1)
+    if n >= 1000 and hcm == 50:
+        assert g["is_valid"][:3000].mean() > 0.9 and not g["is_valid"][3000:].any()
+
+
+def test_chord_exact_key_lookup_calls_explicit_tables(engine: KbrEngine):
+    from test_gpu_chord import _broken_tables
+    net, t = _broken_tables(3000, 33)
+    o = OracleNet("chord", net.ids, net.xy, tables=t)
+    engine.set_params(Params.chord())
+    engine.chord_load_tables(net.ids, net.xy, t["pred"], t["succ"], t["nsucc"], t["fingers"], t["deque_size"])
+    keys, src = _exact_keys(net, 35, 6000)
+    g = engine.lookupCall(keys, src, 0)
+    _eq(g, o.lookup_call(keys, src, 0), "chord exact explicit")
+    assert g["is_valid"].any() and not g["is_valid"].all()
+
+
+def test_chord_exact_key_full_batch_properties(engine: KbrEngine):
+    """2^20 node-ID lookups on a 2^18 ring: the exact-key lookup ends one response before the
+    one-way route's last (the response naming the key's node), and fails when the route needed one
+    hop (the source's own findNode named it) or none."""
+    net = W.population(1 << 18, 47)
+    engine.set_params(Params.chord())
+    engine.chord_load(net.ids, net.xy)
+    keys, src = W.lookups(net.ids, 1 << 20, 49, node_ids=True)
+    g = engine.lookupCall(keys, src, 0)
+    r = engine.lookup(keys, src)
+    k = r["hops"].astype(np.int64)
+    ok = k >= 2
+    assert np.array_equal(g["is_valid"] == 1, ok)
+    assert np.array_equal(g["hops"][ok].astype(np.int64), k[ok] - 1)
+    assert np.array_equal(g["hops"][~ok].astype(np.int64), k[~ok])
+    assert np.array_equal(g["siblings"][ok, 0], r["responsible"][ok])
+    assert np.all(g["latency_ns"][ok] < r["latency_ns"][ok])
