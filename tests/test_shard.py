@@ -401,7 +401,7 @@ def test_kad_shards_emulated_on_one_gpu(world, alpha, n):
     assert rounds >= 3
 
 
-def _kad_gpu_worker(rank, world, port, q):
+def _kad_gpu_worker(rank, world, port, q, ns=None):
     import torch.distributed as dist
     from oversim_amd import Params
     from oversim_amd.shard import KadShardStepper, TorchExchange, arc_bounds, done_to_numpy, route_kad_sharded
@@ -410,16 +410,53 @@ def _kad_gpu_worker(rank, world, port, q):
     n, m = 1 << 15, 3000
     net = W.population(n, 99)
     bounds = arc_bounds(n, world)
-    k, s = W.lookups(net.ids, m, 100 + rank, node_ids=False)
+    k, s = W.lookups(net.ids, m, 100 + rank, node_ids=ns is not None)
     s = (bounds[rank] + s.astype(np.int64) % (bounds[rank + 1] - bounds[rank])).astype(np.uint32)
     dev = torch.device("cuda", 0)
-    st = KadShardStepper(net.ids, net.xy, bounds, rank, dev, params=Params.kademlia())
+    st = KadShardStepper(net.ids, net.xy, bounds, rank, dev, params=Params.kademlia(), lookup_siblings=ns)
     done, rounds = route_kad_sharded(st, TorchExchange(world, torch.device("cpu")),
                                      torch.from_numpy(k.view(np.int32)).to(dev),
                                      torch.from_numpy(s.view(np.int32)).to(dev), rank * m)
-    q.put((rank, done_to_numpy(done), k, s))
+    if ns is None:
+        q.put((rank, done_to_numpy(done), k, s))
+    else:
+        q.put((rank, st.lookup_results(done), k, s))
     dist.barrier()
     dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_kad_lookup_calls_two_processes_share_one_gpu_gloo():
+    """Sharded Kademlia LookupCalls (numSiblings = s) with the request/response exchange between two
+    processes: every LookupResponse equals the single-context ovs_lookup_batch's."""
+    import torch.multiprocessing as mp
+    from oversim_amd import KbrEngine, Params
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kad_gpu_worker, args=(r, world, port, q, -1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    qid = np.concatenate([r[1][0] for r in res])
+    lo = np.concatenate([r[1][1] for r in res])
+    sib = np.concatenate([r[1][2] for r in res])
+    order = np.argsort(qid)
+    assert np.array_equal(qid[order], np.arange(world * 3000))
+    lo, sib = lo[order], sib[order]
+    net = W.population(1 << 15, 99)
+    with KbrEngine(0) as eng:
+        eng.set_params(Params.kademlia())
+        eng.kad_load(net.ids, net.xy)
+        ref = eng.lookupCall(np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res]), -1)
+    for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+        assert np.array_equal(lo[f], ref[f]), f
+    assert np.array_equal(sib, ref["siblings"])
+    assert lo["is_valid"].mean() > 0.99
 
 
 @pytest.mark.gpu
