@@ -33,23 +33,27 @@ __global__ __launch_bounds__(64) void k_compact_count(const uint8_t* __restrict_
     for (int c = lane; c < nclass; c += 64) cnt[(uint64_t)c * nb + b] = h[c];
 }
 
-// per class: the position of its first record and the counter updates (one thread, <= CMAX classes)
+// per class: the position of its first record (one thread, <= CMAX classes).  A counter group (a
+// class and the classes chained to it) reserves its records with one atomicAdd on its counter:
+// compactions on other streams may share the counter (the two cohorts of a Chord shard step
+// append to one done buffer), and a plain read-modify-write there let two groups take the same
+// positions.
 __global__ void k_compact_base(CPlan P, int nclass, uint64_t nb, const unsigned long long* __restrict__ scan,
                                long long* __restrict__ cbase)
 {
-    long long run = 0;
-    unsigned long long* hc = nullptr;
-    for (int c = 0; c < nclass; ++c) {
-        const CClass k = plan_class(P, c);
-        const unsigned long long s0 = scan[(uint64_t)c * nb], s1 = scan[(uint64_t)(c + 1) * nb];
-        if (!k.chain || c == 0) {
-            hc = k.counter;
-            run = hc ? (long long)*hc : 0;
+    int c = 0;
+    while (c < nclass) {
+        int e = c + 1;
+        while (e < nclass && plan_class(P, e).chain) ++e;
+        unsigned long long* hc = plan_class(P, c).counter;
+        const unsigned long long g0 = scan[(uint64_t)c * nb], g1 = scan[(uint64_t)e * nb];
+        long long run = hc ? (long long)atomicAdd(hc, g1 - g0) : 0;
+        for (int j = c; j < e; ++j) {
+            const unsigned long long s0 = scan[(uint64_t)j * nb], s1 = scan[(uint64_t)(j + 1) * nb];
+            cbase[j] = run - (long long)s0;
+            run += (long long)(s1 - s0);
         }
-        cbase[c] = run - (long long)s0;
-        run += (long long)(s1 - s0);
-        const bool last = c + 1 == nclass || !plan_class(P, c + 1).chain;
-        if (last && hc) *hc = (unsigned long long)run;
+        c = e;
     }
 }
 

@@ -82,7 +82,16 @@ struct KadView {
     uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)
     int maybe_short;
     int snapshot;      // tables built by the snapshot rule (ovs_kad_load), not imported
+    unsigned long long* err;   // sharded kernels: a table read this arc cannot serve is counted here
+                               // (ovs_kad_shard_errors) instead of made; nullptr on one GPU
 };
+
+// a table access outside the owned arc [lo, hi): counted (sharded kernels), never performed
+__device__ __forceinline__ bool kad_off_arc(const KadView& V, uint32_t c) { return c < V.lo || c >= V.hi; }
+__device__ __forceinline__ void kad_count_error(const KadView& V)
+{
+    if (V.err) atomicAdd(V.err, 1ull);
+}
 
 void kad_free(KadTables& t);
 // snapshot tables for nodes [lo, hi) of the sorted ring (node records for all n)

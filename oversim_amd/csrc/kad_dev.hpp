@@ -296,8 +296,11 @@ __device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadNode& 
     if (nsib == V.S5 && beyond_radius(V, r, c, D)) return false;
     if (!mask_hits(V, r, c, D)) return true;
     int closer = 0;
-    if (c < V.lo || c >= V.hi) {
-        // a responder off this rank's arc (sharded LookupCalls): its replicated sibling levels
+    if (kad_off_arc(V, c)) {
+        // a responder off this rank's arc (sharded LookupCalls): its replicated sibling levels.
+        // Its sibling row lives on its owner only: reading V.sibb at (c - lo) here was the
+        // round-2 illegal-address fault (c < lo wraps to ~2^32 rows), DESIGN.md §6
+        if (!V.slev) { kad_count_error(V); return false; }
         const uint8_t* lv = V.slev + (uint64_t)c * V.S5;
         for (int i = 0; i < nsib; ++i) closer += (int)kbit(D, lv[i]);
         return closer < numSiblings;
@@ -343,6 +346,12 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
                                                  int numRedundant, bool sib, Blk8& res, int numSiblings = 1)
 {
     blk_clear(res);
+    if (V.err && kad_off_arc(V, c)) {
+        // sharded kernels: c's bucket and sibling rows live on its owner only -- counted
+        // (ovs_kad_shard_errors), answered empty
+        kad_count_error(V);
+        return 0;
+    }
     if (g.nsib == 0 || (V.snapshot && sib && numSiblings <= 1)) {
         // an empty sibling table answers [self]; on snapshot tables a sibling for numSiblings = 1
         // is the XOR-closest of everything it knows: nothing below the main bucket beats it

@@ -757,26 +757,27 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     const bool reg = R <= 8;
     // one lane per lookup, as many lanes as are resident at once (occupancy-sized grid); the
     // scratch is sized for the lanes
-    static int bpc[4] = {0, 0, 0, 0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
+    // the occupancy of each instantiation, per device, filled under the scratch mutex
+    static int bpc[64][4] = {};
     const int ki = (t.exact ? 2 : 0) + (reg ? 1 : 0);
-    if (bpc[ki] == 0) {
+    std::unique_lock<std::mutex> lock(g_scratch_mu);
+    if (bpc[dev][ki] == 0) {
         int b = 0;
         hipError_t oe;
         if (t.exact) oe = reg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<true, true>, 256, 0)
                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<true, false>, 256, 0);
         else oe = reg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<false, true>, 256, 0)
                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<false, false>, 256, 0);
-        bpc[ki] = (oe == hipSuccess && b > 0) ? b : 1;
+        bpc[dev][ki] = (oe == hipSuccess && b > 0) ? b : 1;
     }
-    uint64_t lanes = (uint64_t)num_cu * (uint64_t)bpc[ki] * 256;
+    uint64_t lanes = (uint64_t)num_cu * (uint64_t)bpc[dev][ki] * 256;
     if (lanes > nq) lanes = nq;
     lanes = (lanes + 255) / 256 * 256;
     const uint64_t nhE = reg ? 0 : 2ull * R, resE = reg ? 0 : (uint64_t)(R > t.k ? R : t.k);
     const uint64_t bytes = lanes * (nhE * (4 + 8 + 1) + resE * (4 + 8) + XMAXDEAD * 4) + 4;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
-    std::lock_guard<std::mutex> lock(g_scratch_mu);
     if (g_scratch_cap[dev] < bytes) {
         if (g_scratch[dev]) { hipDeviceSynchronize(); hipFree(g_scratch[dev]); }
         g_scratch[dev] = nullptr; g_scratch_cap[dev] = 0;

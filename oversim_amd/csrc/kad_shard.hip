@@ -202,8 +202,10 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
     for (int w = 0; w < 5; ++w) K.w[w] = q.key[w];
     ovs_kad_resp o;
     o.tag = q.tag;
-    if (q.node < V.lo || q.node >= V.hi) {
-        o.count = 0xFFFFFFFFu;    // not this rank's node: the caller mis-routed the request
+    if (kad_off_arc(V, q.node) || ns > 8 || ns > V.S5) {
+        // not this rank's node (the caller mis-routed the request) or a numSiblings the home rank
+        // would have refused: answered as undeliverable, counted by the requester's deliver
+        o.count = 0xFFFFFFFFu;
         out[j] = o;
         return;
     }
@@ -281,7 +283,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
                           uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
                           uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                           unsigned long long* done_count, unsigned long long* active_count, int lk_ns,
-                          uint32_t* sib_out, StageBuf& stage, hipStream_t s)
+                          uint32_t* sib_out, unsigned long long* bad, StageBuf& stage, hipStream_t s)
 {
     const bool lk = lk_ns >= 0;
     ovs_params Q = P;
@@ -290,7 +292,8 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
         return hipErrorNotSupported;
     if (nlook == 0) return hipSuccess;
     if (nsh < 1 || nsh > MAXSHARDS) return hipErrorInvalidValue;
-    const KadView V = kad_make_view(t, xy, n);
+    KadView V = kad_make_view(t, xy, n);
+    V.err = bad;
     KadLC LC = kad_make_lc(Q, t);
     DelayConsts DL = DC;
     DL.lookupCall = lk ? 1 : 0;     // a LookupCall ends at its last response (no route message)
@@ -341,14 +344,15 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
 }
 
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
-                           ovs_kad_resp* out, hipStream_t s)
+                           ovs_kad_resp* out, unsigned long long* bad, hipStream_t s)
 {
     // numSiblings travels with each request; the rest of the configuration is the rank's
     ovs_params Q = P;
     Q.numSiblings = 1;
     if (!kad_params_supported(Q, t)) return hipErrorNotSupported;
     if (nreq == 0) return hipSuccess;
-    const KadView V = kad_make_view(t, nullptr, n);
+    KadView V = kad_make_view(t, nullptr, n);
+    V.err = bad;
     const KadLC LC = kad_make_lc(P, t);
     if (t.exact) hipLaunchKernelGGL(k_kad_shard_serve<true>, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
     else hipLaunchKernelGGL(k_kad_shard_serve<false>, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);

@@ -24,9 +24,10 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
                           uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
                           uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                           unsigned long long* done_count, unsigned long long* active_count, int lk_ns,
-                          uint32_t* sib_out, StageBuf& stage, hipStream_t s);   // lk_ns < 0: KBR routes
+                          uint32_t* sib_out, unsigned long long* bad, StageBuf& stage,
+                          hipStream_t s);   // lk_ns < 0: KBR routes; bad: table reads off the arc
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
-                           ovs_kad_resp* out, hipStream_t s);
+                           ovs_kad_resp* out, unsigned long long* bad, hipStream_t s);
 hipError_t kad_shard_deliver(const ovs_kad_resp* in, uint64_t n, KadRes* res, uint64_t nslots,
                              unsigned long long* bad, hipStream_t s);
 

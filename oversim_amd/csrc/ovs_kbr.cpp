@@ -338,16 +338,15 @@ void ovs_ctx_destroy(ovs_ctx* c)
 {
     if (!c) return;
     hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    // the whole device: work on caller-supplied streams (c->stage keys) ends here too, without
+    // touching those handles, which the caller may already have destroyed
+    hipDeviceSynchronize();
     free_tables(c);
     free_kad_shard(c);
     free_scratch(c);
     kad_exhaustive_release(c->device);
     if (c->d_bounds) hipFree(c->d_bounds);
-    for (auto& kv : c->stage) {
-        hipStreamSynchronize(kv.first);
-        stage_free(kv.second);
-    }
+    for (auto& kv : c->stage) stage_free(kv.second);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -917,7 +916,7 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, 
     if (bst != OVS_OK) return bst;
     hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kqids,
                                   c->kres, c->knlook, c->d_bounds, (int)nshards, out, out_dest, out_cap, out_count,
-                                  done, done_cap, done_count, active_count, c->kns, c->ksib, c->stage[s], s);
+                                  done, done_cap, done_count, active_count, c->kns, c->ksib, c->kbad, c->stage[s], s);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard step");
     return OVS_OK;
 }
@@ -927,7 +926,7 @@ ovs_status ovs_kad_shard_serve(ovs_ctx* c, const ovs_kad_req* in, uint64_t n, ov
     if (!c || (n && (!in || !out))) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
     HIPCHK(c, hipSetDevice(c->device));
-    hipError_t e = kad_shard_serve(c->kad, (uint32_t)c->n, c->P, in, n, out, (hipStream_t)stream);
+    hipError_t e = kad_shard_serve(c->kad, (uint32_t)c->n, c->P, in, n, out, c->kbad, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard serve");
     return OVS_OK;
 }

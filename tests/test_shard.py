@@ -220,6 +220,44 @@ def _gpu_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+class _SelfExchange:
+    """world = 1 exchange (no process group): every record stays on rank 0."""
+    rank, world = 0, 1
+
+    def count_matrix_async(self, counts):
+        M = counts.reshape(1, -1).cpu().numpy()
+        return lambda: M
+
+    def segments(self, segs, scl, rcl, row_bytes):
+        return segs[0][:rcl[0]].clone()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cohorts", [2, 3])
+def test_cohorts_share_the_done_buffer(cohorts):
+    """Cohorts on their own streams append to one done buffer: the compaction reserves each cohort's
+    records with an atomic (a plain read-modify-write of the shared counter let two cohorts take the
+    same positions).  Uneven cohorts, repeated batches: every qid exactly once, equal to
+    the single-GPU route."""
+    from oversim_amd.shard import GpuShardStepper, arc_bounds, done_to_numpy, route_sharded
+    n, m = 1 << 15, 10_007
+    net = W.population(n, 95)
+    k, s = W.lookups(net.ids, m, 77, node_ids=False)
+    dev = torch.device("cuda", 0)
+    st = GpuShardStepper(net.ids, net.xy, arc_bounds(n, 1), 0, dev, capacity=m)
+    ref = _single_gpu_reference(net, k, s)
+    kt, sv = torch.from_numpy(k).to(dev), torch.from_numpy(s).to(dev)
+    for rep in range(6):
+        st.reset(m)
+        done, _ = route_sharded(st, _SelfExchange(), kt, sv, 0, cohorts=cohorts, min_split=1)
+        d = done_to_numpy(done)
+        assert len(d) == m, (rep, len(d))
+        d = d[np.argsort(d["qid"])]
+        assert np.array_equal(d["qid"], np.arange(m)), rep
+        for f in ROUTE_FIELDS:
+            assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), (rep, f)
+
+
 @pytest.mark.gpu
 def test_two_processes_share_one_gpu_gloo():
     import torch.multiprocessing as mp
@@ -652,3 +690,25 @@ def test_kad_shard_source_off_arc_is_an_error():
         route_kad_local_shards(steppers, [kt, kt], [torch.from_numpy(s_bad.view(np.int32)).to(dev),
                                                     torch.from_numpy((s_ok + bounds[1]).view(np.int32)).to(dev)],
                                [0, 4])
+
+
+@pytest.mark.gpu
+def test_kad_serve_refuses_requests_it_cannot_answer():
+    """k_kad_shard_serve answers a request for a node off its arc, or with a numSiblings the home rank
+    would have refused (> min(8, 5s)), as undeliverable (count 0xFFFFFFFF) instead of reading tables it
+    does not hold; the requester's deliver counts it (ovs_kad_shard_errors)."""
+    from oversim_amd.shard import KAD_REQ_DTYPE, KAD_RESP_DTYPE, KadShardStepper, arc_bounds
+    n, world = 1 << 14, 2
+    net = W.population(n, 97)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    st = KadShardStepper(net.ids, net.xy, bounds, 0, dev, lookup_siblings=8)
+    k, _ = W.lookups(net.ids, 3, 5, node_ids=False)
+    q = np.zeros(3, dtype=KAD_REQ_DTYPE)
+    q["key"] = k
+    q["node"] = [5, bounds[1] + 7, 9]                  # on the arc, off the arc, on the arc
+    q["tag"] = [0, 1, 2]
+    q["pad"] = [0x80000000 | 8, 0x80000000 | 8, 0x80000000 | 200]
+    resp = st.serve(torch.from_numpy(q.view(np.uint8).reshape(3, -1).copy()).to(dev))
+    r = resp.cpu().numpy().view(KAD_RESP_DTYPE).ravel()
+    assert r["count"][0] <= 8 and r["count"][1] == 0xFFFFFFFF and r["count"][2] == 0xFFFFFFFF
