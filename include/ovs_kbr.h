@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 6
+#define OVS_ABI_VERSION 7
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -474,11 +474,15 @@ ovs_status  ovs_shard_lookup_finish(ovs_ctx* ctx, const ovs_done_rec* done, uint
  * coordinates are replicated.  A lookup stays on the rank of its source; every
  * FindNodeCall it sends becomes a request to the rank owning the responder, whose
  * findNode result (Kademlia.cc:1101-1246) comes back before the lookup's next
- * round -- before the simulated response is processed.  Per round the caller runs
- * ovs_kad_shard_step, exchanges the requests (all-to-allv by out_dest),
- * ovs_kad_shard_serve on what it received, sends the responses back with the
- * reverse splits and hands them to ovs_kad_shard_deliver; it stops when the
- * sum of *active_count over the ranks is 0.  All buffers are device memory. */
+ * round -- before the simulated response is processed.  A FindNodeCall to a node of
+ * the rank's own arc is answered on the spot (at world size 1 the first round
+ * finishes every lookup).  Per round the caller runs ovs_kad_shard_step, gathers
+ * every rank's out_count[0..nshards) and *active_count (the round's one host
+ * synchronisation), exchanges the requests (all-to-allv of the per-owner
+ * segments), runs ovs_kad_shard_serve on what it received, sends the responses
+ * back with the reverse splits and hands them to ovs_kad_shard_deliver; it stops
+ * when every rank's requests and active lookups are 0.  All buffers are device
+ * memory. */
 typedef struct ovs_kad_req {        /* 32 B FindNodeCall */
     uint32_t key[5];
     uint32_t node;                  /* responder (global index, on the receiving rank's arc) */
@@ -510,13 +514,17 @@ ovs_status  ovs_kad_shard_begin(ovs_ctx* ctx, const ovs_key160* keys, const uint
 ovs_status  ovs_kad_shard_begin_lookup(ovs_ctx* ctx, int32_t num_siblings, const ovs_key160* keys,
                                        const uint32_t* src, uint64_t n, uint32_t qid_base,
                                        uint32_t* siblings, void* stream);
-/* One round for this rank's lookups.  *out_count, *done_count, *active_count are
- * device counters the kernel increments (the caller zeroes out_count and
- * active_count before each round).  shard_lo: HOST array of nshards+1 arc bounds. */
-ovs_status  ovs_kad_shard_step(ovs_ctx* ctx, ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap,
-                               unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                               unsigned long long* done_count, unsigned long long* active_count,
-                               const uint64_t* shard_lo, uint32_t nshards, void* stream);
+/* One round for this rank's lookups (ABI 7).  Requests for rank d go to segment d of
+ * `out` (out + d * out_cap requests; out_cap >= n * lookupParallelRpcs) and are
+ * counted in out_count[d]; finished lookups are appended to `done` (done_count).
+ * out_count[0..nshards) and done_count are device counters the step adds to (the
+ * caller zeroes out_count before each round, done_count once per batch);
+ * *active_count is set to the lookups still running after the round.
+ * shard_lo: HOST array of nshards+1 arc bounds. */
+ovs_status  ovs_kad_shard_step(ovs_ctx* ctx, ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count,
+                               ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                               unsigned long long* active_count, const uint64_t* shard_lo, uint32_t nshards,
+                               void* stream);
 /* findNode at the (local) responders of n received requests. */
 ovs_status  ovs_kad_shard_serve(ovs_ctx* ctx, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out,
                                 void* stream);

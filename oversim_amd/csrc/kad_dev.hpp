@@ -126,6 +126,12 @@ __device__ __forceinline__ bool cand_lt(uint64_t da, uint32_t ia, uint64_t db, u
     return k_lt(xa, xb);
 }
 
+#ifdef OVS_KAD_STATS
+// cost experiment (tools/diag): [0] findNode calls, [1] blocks read, [2] calls in the sibling zone,
+// [3] calls whose main bucket was short, [4] events, [5] sends
+__device__ unsigned long long g_kad_stats[8];
+#endif
+
 template <int CAP>
 struct SVec {
     uint32_t idx[CAP];
@@ -367,6 +373,9 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     auto add_blk = [&](const KadBlk* blk) {
         Blk8 b;
         const int cnt = blk_load_block(b, blk, K);
+#ifdef OVS_KAD_STATS
+        atomicAdd(&g_kad_stats[1], 1ull);
+#endif
         if (cnt) {
             blk_sort8<false, EX>(b, K, V.nodes);
             if (seen == 0) {
@@ -382,7 +391,26 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         if (g.rowlo < 0 || bucket < g.rowlo) return;      // buckets below the stored row are empty
         add_blk(slot_blk(V, g.boff, bucket));
     };
+#ifdef OVS_KAD_STATS
+    atomicAdd(&g_kad_stats[0], 1ull);
+    if (g.m <= g.endIndex) atomicAdd(&g_kad_stats[2], 1ull);
+#endif
     if (g.m >= 0) add_slot(g.m);
+#ifdef OVS_DUP_MAIN
+    if (g.m >= 0 && g.rowlo >= 0 && g.m >= g.rowlo) {   // cost experiment: the main block again
+        K160 K2 = K;
+        asm volatile("" : "+v"(K2.w[0]));
+        Blk8 b2;
+        const int c2 = blk_load_block(b2, slot_blk(V, g.boff, g.m), K2);
+        blk_sort8<false, EX>(b2, K2, V.nodes);
+        uint32_t z = (uint32_t)c2;
+        for (int q = 0; q < 8; ++q) z ^= b2.x[q] ^ (uint32_t)b2.d[q] ^ (uint32_t)(b2.d[q] >> 32);
+        asm volatile("" :: "v"(z));
+    }
+#endif
+#ifdef OVS_KAD_STATS
+    if (g.m > g.endIndex && seen < rs) atomicAdd(&g_kad_stats[3], 1ull);
+#endif
     // Members of bucket m are XOR-closer to K than everything below it (buckets < m, siblings --
     // all at msb <= endIndex < m from c -- and c itself all differ from K at bit m): once bucket
     // m fills the result, the rest of the scan cannot change it
@@ -390,6 +418,23 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
         const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
         for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
+#ifdef OVS_DUP_EXT
+        {   // cost experiment: the sibling-row scan again
+            K160 K2 = K;
+            asm volatile("" : "+v"(K2.w[0]));
+            Blk8 r2;
+            blk_clear(r2);
+            for (int j = 0; j * KBLK < g.nsib; ++j) {
+                Blk8 b2;
+                blk_load_block(b2, L + j, K2);
+                blk_sort8<false, EX>(b2, K2, V.nodes);
+                blk_merge_top8<false, EX>(r2, b2, K2, V.nodes);
+            }
+            uint32_t z = 0;
+            for (int q = 0; q < 8; ++q) z ^= r2.x[q] ^ (uint32_t)r2.d[q] ^ (uint32_t)(r2.d[q] >> 32);
+            asm volatile("" :: "v"(z));
+        }
+#endif
         Blk8 self;
         blk_clear(self);
         self.x[0] = c;
@@ -557,6 +602,7 @@ __device__ __forceinline__ int kad_response_size(const KadView& V, uint32_t c, c
 
 constexpr int MAXA = 4;    // lookupParallelRpcs <= 4
 
+
 struct KadLC {
     int hopCountMax, numSiblings, redundant, alpha;
     int strict, visitOnlyOnce, acceptLateSiblings, useAll, merge, newOnResp, newOnTimeout, finishOnFirst;
@@ -639,6 +685,19 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     const int ns = LK ? LC.numSiblings : 1;
     const bool sb = kad_is_sibling(V, rr, x, L.K, ns);
     const RespGeo rg = resp_geo(rr, L.K);
+#ifdef OVS_DUP_SEND
+    {   // cost experiment: the send's target evaluation (siblings flag, geometry, size, delay) again
+        K160 K2 = L.K;
+        double sx2 = L.sx;
+        asm volatile("" : "+v"(K2.w[0]), "+v"(sx2));
+        const bool sb2 = kad_is_sibling(V, rr, x, K2, ns);
+        const RespGeo rg2 = resp_geo(rr, K2);
+        const int csz2 = kad_response_size<EX>(V, x, rg2, K2, sb2 ? ns : LC.redundant, sb2, ns);
+        const int64_t cd2 = coord_ns(sx2, L.sy, rr.x, rr.y, DC.round);
+        uint32_t z = (uint32_t)csz2 ^ (uint32_t)cd2 ^ (uint32_t)(cd2 >> 32) ^ (sb2 ? 1u : 0u) ^ (uint32_t)rg2.m;
+        asm volatile("" :: "v"(z));
+    }
+#endif
     // the response carries findNode's result (Kademlia.cc:1127-1131 resultSize)
     const int csz = kad_response_size<EX>(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
     const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
@@ -790,12 +849,33 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
             return true;
         }
         getres.fill(e, r, rg, sb, numR, start, res);
+#ifdef OVS_DUP_FIND
+        {   // cost experiment (tools/diag): the responder's findNode evaluated a second time
+            K160 K2 = L.K;
+            asm volatile("" : "+v"(K2.w[0]));
+            Blk8 b2;
+            const int n2 = kad_find_node_blk<EX>(V, r, rg, K2, numR, sb, b2, ns);
+            uint32_t z = (uint32_t)n2;
+            for (int q = 0; q < 8; ++q) z ^= b2.x[q] ^ (uint32_t)b2.d[q] ^ (uint32_t)(b2.d[q] >> 32);
+            asm volatile("" :: "v"(z));
+        }
+#endif
         if (LK && ns == 0 && !start && res.n > 0 && k_eq(node_key(V.nodes, res.idx[0]), L.K)) {
             // the key's node is in the response (handleResponse 862-870): XOR distance 0, so first
             L.result = res.idx[0];
             L.pfinished = true; L.psuccess = true;
             return true;
         }
+#ifdef OVS_DUP_MERGE
+        {   // cost experiment: the LookupVector merge a second time, on a copy
+            SVec<8> nh2 = L.nh;
+            asm volatile("" : "+v"(nh2.idx[0]));
+            const int k2 = nh_merge<EX>(nh2, res, LC.redundant, L.K, V.nodes);
+            uint32_t z = (uint32_t)k2 ^ nh2.used;
+            for (int q = 0; q < 8; ++q) z ^= nh2.idx[q] ^ (uint32_t)nh2.d[q] ^ (uint32_t)(nh2.d[q] >> 32);
+            asm volatile("" :: "v"(z));
+        }
+#endif
         int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
         if (LC.numSiblings != 0 && sb && res.n > 0) {
             if (L.result == NONE) L.result = res.idx[0];
@@ -814,6 +894,316 @@ __device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView&
     }
     kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, on);
     return true;
+}
+
+// ---------------------------------------------------------------------------
+// The same state machine in phases, for kernels that evaluate the sibling-zone findNode
+// cooperatively across the wave (K2 k_kad_route, its shard step):
+//   kad_event_begin      per lane: pick the earliest event, account for it; tells whether a
+//                        findNode result is needed (KEV_FIND), only sends follow (KEV_SENDS),
+//                        the event was handled completely (KEV_HANDLED) or, in the shard step,
+//                        its remote result has not arrived yet (KEV_WAIT: state untouched)
+//   kad_coop_sibzone     whole wave: the findNode scans that need the sibling table
+//   kad_event_after_find per lane: LookupVector merge and the finish rules; the RPCs to send
+//   kad_send_rpcs        per lane: IterativePathLookup::sendRpc
+// A findNode in the sibling zone reads the responder's 5s-entry sibling table (5 blocks at s = 8)
+// plus its own main bucket: one lane doing that alone serialises six block loads and sorts, and
+// one such lane in a wave made every wave iteration pay for it (42 % of K2's time on config E,
+// profiles/r03_dup).  The cooperative form gives each such findNode eight lanes, one block each,
+// and merges the sorted blocks in three butterfly steps.
+
+enum : int { KEV_IDLE = 0, KEV_WAIT = 1, KEV_HANDLED = 2, KEV_FIND = 3, KEV_SENDS = 4 };
+
+struct KadEv {
+    uint32_t r;        // responder (the source itself at start)
+    uint32_t geo;      // its geometry for K and its siblings flag (pack_geo)
+    uint32_t boff;
+    int e;             // pending slot of the event (-1 at start)
+    int numR;          // numRedundantNodes of the findNode
+    int num;           // KEV_SENDS: RPCs to send
+    bool start;
+    __device__ __forceinline__ bool sb() const { return (geo >> 24) & 1u; }
+    __device__ __forceinline__ RespGeo rg() const { return unpack_geo(geo, boff); }
+};
+
+// IterativeLookup::start / handleRpcResponse / handleRpcTimeout up to the findNode
+// (kad_lookup_event's first half).  ready(slot, node): the result of a response event is available.
+template <int A, bool EX, bool LK, class Ready, class Rec>
+__device__ __forceinline__ int kad_event_begin(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
+                                               const KadLC& LC, const Ready& ready, const Rec& record, KadEv& ev)
+{
+    const int ns = LK ? LC.numSiblings : 1;
+    ev.r = L.S;
+    ev.geo = 0;
+    ev.boff = 0;
+    ev.e = -1;
+    ev.numR = LC.redundant;
+    ev.num = 0;
+    ev.start = !L.started;
+    bool resp = true;
+    if (ev.start) {
+        L.started = true;
+        const KadNode rn = load_node(V.nodes, L.S);
+        const RespGeo g = resp_geo(rn, L.K);
+        ev.geo = pack_geo(g, kad_is_sibling(V, rn, L.S, L.K, ns));
+        ev.boff = g.boff;
+        ev.numR = LC.maxRedundantLocal;
+    } else {
+        int e = -1;
+        int64_t bt = 0, bi = 0;
+        uint32_t bs = 0;
+#pragma unroll
+        for (int i = 0; i < A; ++i) {
+            if ((L.pvalid >> i) & 1u) {
+                const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
+                const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
+                const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
+                if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
+            }
+        }
+        uint32_t r = 0, tag = 0, geo = 0, boff = 0;
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+            if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; }
+        if (!(tag & 0x80000000u) && !ready(e, r)) return KEV_WAIT;
+        ev.r = r;
+        ev.e = e;
+        L.pvalid &= ~(1u << e);
+        L.now = bt;
+        if (tag & 0x80000000u) {
+            // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
+            L.any_to = true;
+            resp = false;
+        } else {
+            ev.geo = geo;
+            ev.boff = boff;
+            const bool acc = (LC.useAll && LC.merge) ? true : ((int)(tag & 0xFFFFu) == L.step);
+            resp = acc || (ev.sb() && LC.acceptLateSiblings);
+        }
+    }
+    if (resp) {
+        if (!ev.start) {
+            // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
+            if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return KEV_HANDLED; }
+            if (ev.r != L.S) {
+                record(L.hops, ev.r);
+                ++L.hops;
+            }
+            ++L.step;
+            --L.pending;
+        }
+        if (LK && ns == 0 && ev.start && ev.sb()) {
+            // an exact-key lookup of the source's own key (IterativeLookup::start 171-184)
+            L.result = L.S;
+            L.pfinished = true; L.psuccess = true;
+            return KEV_HANDLED;
+        }
+        return KEV_FIND;
+    }
+    // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
+    --L.pending;
+    if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return KEV_HANDLED; }
+    if (LC.newOnTimeout) ev.num = 1;
+    else if (L.pending == 0) ev.num = LC.alpha;
+    else return KEV_HANDLED;
+    return KEV_SENDS;
+}
+
+// the findNode answer for the response (kad_lookup_event's second half): numNew, the finish rules;
+// returns the RPCs to send, or -1 when the lookup finished
+template <int A, bool EX, bool LK>
+__device__ __forceinline__ int kad_event_after_find(KadLookup<A>& L, const KadView& V, const KadLC& LC, const KadEv& ev,
+                                                    const SVec<8>& res)
+{
+    const int ns = LK ? LC.numSiblings : 1;
+    if (LK && ns == 0 && !ev.start && res.n > 0 && k_eq(node_key(V.nodes, res.idx[0]), L.K)) {
+        // the key's node is in the response (handleResponse 862-870): XOR distance 0, so first
+        L.result = res.idx[0];
+        L.pfinished = true; L.psuccess = true;
+        return -1;
+    }
+    int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
+    if (LC.numSiblings != 0 && ev.sb() && res.n > 0) {
+        if (L.result == NONE) L.result = res.idx[0];
+        L.pfinished = true; L.psuccess = true;
+        return -1;
+    }
+    if (numNew == 0 && LC.newOnResp) numNew = 1;
+    return ev.start ? LC.alpha : min(numNew, LC.alpha);
+}
+
+// Does findNode(K) at c take the cooperative sibling-zone scan?  Kademlia::findNode (Kademlia.cc:
+// 1101-1246) scans the main bucket m and, when m >= endIndex or the result is short, the buckets
+// m-1 .. endIndex, the sibling table and c itself.  In the sibling zone m <= endIndex the buckets
+// below m are empty unless an imported table stores bucket m < endIndex: those (and the [self]
+// answers, the buckets above endIndex, off-arc responders) stay on the per-lane path.
+__device__ __forceinline__ bool kad_find_is_coop(const KadView& V, uint32_t c, const RespGeo& g, bool sib,
+                                                 int numSiblings)
+{
+    if (g.nsib == 0 || (V.snapshot && sib && numSiblings <= 1)) return false;
+    if (V.err && kad_off_arc(V, c)) return false;
+    if (g.m > g.endIndex) return false;
+    const bool stored_below = g.m < g.endIndex && g.rowlo >= 0 && g.m >= g.rowlo;
+    return !stored_below;
+}
+
+// position of the t-th (from 0) set bit of m (m has more than t set bits)
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int t)
+{
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = pos + w >= 64 ? ~0ull : ((1ull << (pos + w)) - 1ull);
+        if (__popcll(m & low) <= t) pos += w;
+    }
+    return pos;
+}
+
+// LDS of the cooperative findNode, per 256-lane block, entry-major (dword k of lane t at [k][t]:
+// a wave's lanes touch consecutive words): the lanes' partial top-8 vectors during the butterfly,
+// and each owner's result until its lane picks it up
+struct CoopLds {
+    uint32_t acc[24][256];
+    uint32_t cnt[256];
+    uint32_t res[24][256];
+    uint32_t rcnt[256];
+};
+
+__device__ __forceinline__ void coop_put(uint32_t (*a)[256], int t, const Blk8& b)
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        a[3 * q][t] = (uint32_t)b.d[q];
+        a[3 * q + 1][t] = (uint32_t)(b.d[q] >> 32);
+        a[3 * q + 2][t] = b.x[q];
+    }
+}
+
+__device__ __forceinline__ void coop_get(const uint32_t (*a)[256], int t, Blk8& b)
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        b.d[q] = (uint64_t)a[3 * q][t] | ((uint64_t)a[3 * q + 1][t] << 32);
+        b.x[q] = a[3 * q + 2][t];
+        b.f[q] = 0;
+    }
+}
+
+// wave-level ordering of LDS writes and reads between lanes of one wave
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Whole wave (uniform control flow): for every lane with want set, the candidates of its sibling-zone
+// findNode -- bucket m if stored, the sibling table blocks, c itself -- merged into the top 8 by XOR
+// distance to K (left in S.res at the lane's slot) and how many candidates there were (S.rcnt).
+// Eight lanes per findNode: lane j of a group loads and sorts item j (and j + 8, ...), the group
+// merges in three butterfly steps through LDS (lanes ^1, ^2, ^4), the leader stores the result for
+// the owner.  Up to 8 findNodes per pass.
+template <bool EX>
+__device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, uint32_t c, uint32_t geo, uint32_t boff,
+                                                 const K160& K, CoopLds& S)
+{
+    const uint64_t tasks = __ballot(want);
+    if (tasks == 0) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int T = __popcll(tasks);
+    const int grp = lane >> 3, j = lane & 7;
+    for (int p = 0; p * 8 < T; ++p) {
+        const int t = p * 8 + grp;
+        const bool live = t < T;
+        const int owner = live ? nth_set_bit(tasks, t) : lane;
+        const uint32_t oc = __shfl(c, owner);
+        const RespGeo og = unpack_geo(__shfl(geo, owner), __shfl(boff, owner));
+        K160 oK;
+#pragma unroll
+        for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
+        const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;
+        const int nsb = (og.nsib + KBLK - 1) / KBLK;
+        const int nitems = live ? nmain + nsb + 1 : 0;
+        auto load_item = [&](int i, Blk8& b) -> int {
+            if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
+            if (i < nmain + nsb)
+                return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(i - nmain), oK);
+            blk_clear(b);
+            b.x[0] = oc;
+            b.d[0] = dist_hi(node_key(V.nodes, oc), oK);
+            return 1;
+        };
+        Blk8 acc;
+        int cnt = 0;
+        if (j < nitems) {
+            cnt = load_item(j, acc);
+            blk_sort8<false, EX>(acc, oK, V.nodes);
+        } else {
+            blk_clear(acc);
+        }
+        for (int i = j + 8; i < nitems; i += 8) {   // more than 8 items: explicit tables with 5s > 48
+            Blk8 b;
+            const int bc = load_item(i, b);
+            blk_sort8<false, EX>(b, oK, V.nodes);
+            blk_merge_top8<false, EX>(acc, b, oK, V.nodes);
+            cnt += bc;
+        }
+        // butterfly: after step w every lane holds the top 8 of its aligned 2w lanes
+#pragma unroll
+        for (int w = 1; w < 8; w <<= 1) {
+            coop_put(S.acc, tid, acc);
+            S.cnt[tid] = (uint32_t)cnt;
+            wave_lds_sync();
+            const int pt = tid ^ w;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint64_t bd = (uint64_t)S.acc[3 * (7 - i)][pt] | ((uint64_t)S.acc[3 * (7 - i) + 1][pt] << 32);
+                const uint32_t bx = S.acc[3 * (7 - i) + 2][pt];
+                const bool s = cand_lt<EX>(bd, bx, acc.d[i], acc.x[i], oK, V.nodes);
+                acc.d[i] = s ? bd : acc.d[i];
+                acc.x[i] = s ? bx : acc.x[i];
+            }
+            cnt += (int)S.cnt[pt];
+            // acc is bitonic: half-cleaners at distance 4, 2, 1
+            blk_ce<false, EX>(acc, 0, 4, oK, V.nodes); blk_ce<false, EX>(acc, 1, 5, oK, V.nodes);
+            blk_ce<false, EX>(acc, 2, 6, oK, V.nodes); blk_ce<false, EX>(acc, 3, 7, oK, V.nodes);
+            blk_ce<false, EX>(acc, 0, 2, oK, V.nodes); blk_ce<false, EX>(acc, 1, 3, oK, V.nodes);
+            blk_ce<false, EX>(acc, 4, 6, oK, V.nodes); blk_ce<false, EX>(acc, 5, 7, oK, V.nodes);
+            blk_ce<false, EX>(acc, 0, 1, oK, V.nodes); blk_ce<false, EX>(acc, 2, 3, oK, V.nodes);
+            blk_ce<false, EX>(acc, 4, 5, oK, V.nodes); blk_ce<false, EX>(acc, 6, 7, oK, V.nodes);
+            wave_lds_sync();
+        }
+        if (live && j == 0) {
+            const int ot = tid - lane + owner;
+            coop_put(S.res, ot, acc);
+            S.rcnt[ot] = (uint32_t)cnt;
+        }
+    }
+    wave_lds_sync();
+}
+
+// the per-lane end of a cooperative findNode: truncation to resultSize, then the buckets above m
+// while the result is short (Kademlia.cc:1233-1242; only tiny networks / short tables get there)
+template <bool EX>
+__device__ __forceinline__ int kad_coop_finish(const KadView& V, const RespGeo& g, const K160& K, int numRedundant,
+                                               bool sib, int numSiblings, Blk8& res, int seen)
+{
+    const int rs = sib ? (numSiblings ? numSiblings : 1) : numRedundant;
+    const int cap = rs < 8 ? rs : 8;
+    int n = blk_trunc(res, cap);
+    for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) {
+        if (g.rowlo < 0 || b < g.rowlo) continue;
+        Blk8 blk;
+        const int cnt = blk_load_block(blk, slot_blk(V, g.boff, b), K);
+        if (cnt) {
+            blk_sort8<false, EX>(blk, K, V.nodes);
+            blk_merge_top8<false, EX>(res, blk, K, V.nodes);
+            n = blk_trunc(res, cap);
+            seen += cnt;
+        }
+    }
+    return n;
 }
 
 // LookupListener::lookupFinished -> KBRTestApp statistics (BaseOverlay.cc:1241-1307)
@@ -901,6 +1291,13 @@ inline void kad_lc_sizes(KadLC& LC, const DelayConsts& DC, uint32_t n)
     LC.bwFull = DC.bwResp[LC.full <= 16 ? LC.full : 16];
     if (LC.full > 16) LC.full = -1;
 }
+
+struct KadShardStepArgs;   // kad_shard.hpp
+
+// the shard-step instantiation of K2 for one (alpha, exact) pair (kad_route.hip)
+template <int A, bool EX>
+hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const KadShardStepArgs& a,
+                                 int num_cu, hipStream_t st);
 
 // K2 for one (alpha, exact) pair; instantiated in kad_route.hip (one object per pair)
 template <int A, bool EX>

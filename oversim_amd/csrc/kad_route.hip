@@ -1,25 +1,34 @@
-// kad_route.hip -- K2, the Kademlia iterative-lookup kernel, for gfx950 (MI355X).
+// kad_route.hip -- K2, the Kademlia iterative-lookup kernel, for gfx950 (MI355X): the single-GPU
+// batch and the shard step of the multi-GPU path (kad_shard.hip) are two instantiations of it.
 //
-// Compiled once per (alpha, exact) pair (build.py: -DOVS_KAD_A, -DOVS_KAD_EX) so the eight
-// heavy instantiation sets build in parallel; kad.hip's kad_route dispatches to them.
+// Compiled once per (alpha, exact) pair (build.py: -DOVS_KAD_A, -DOVS_KAD_EX) so the heavy
+// instantiation sets build in parallel; kad.hip's kad_route and kad_shard.hip dispatch to them.
 //
 // K2 k_kad_route: one lane per lookup running OverSim's IterativePathLookup (IterativeLookup.cc:
 // 760-1195, merge = true, parallel RPCs) against <= alpha pending FindNodeCalls ordered by
 // simulated arrival time (int64 ns).  Each loop iteration processes the lookup's earliest event:
-// a response is the responder's Kademlia::findNode (Kademlia.cc:1101-1246) over its 96 B bucket
-// blocks (one per k <= 8 bucket) merged into the LookupVector, then the sends it triggers (one
-// 64 B KadNode line per target: its key, coordinates and isSiblingFor summary).  Finished lanes
-// refill from the wave's slice of the batch (ballot + popcount); the grid is persistent.
-// (A per-line state machine in the manner of K1 was tried in this round and reverted: the union
-// of the divergent findNode stages every iteration cost 7x the VALU work)
+// a response is the responder's Kademlia::findNode (Kademlia.cc:1101-1246) merged into the
+// LookupVector, then the sends it triggers (one 64 B KadNode line per target: its key,
+// coordinates and isSiblingFor summary).  A findNode outside the sibling zone reads its main
+// bucket's 96 B block on its own lane; the sibling-zone findNodes of the wave's lanes are
+// evaluated together, eight lanes each (kad_coop_sibzone).  Finished lanes refill from the wave's
+// slice of the batch (ballot + popcount); the grid is persistent.
+//
+// Shard step (SHARD = true): the lookups of this rank (their sources lie on its arc) advance
+// while their responders are local; a FindNodeCall to a node on another arc is staged as a
+// request, and a lookup whose earliest event waits for such a result is suspended (state to HBM)
+// until the next round.  At world size 1 every responder is local and the step is the
+// single-GPU batch.
 #include "kad_dev.hpp"
+#include "kad_shard.hpp"
+
+#include <cstdio>
 
 #ifndef OVS_KAD_A
 #error "kad_route.hip is compiled with -DOVS_KAD_A=<alpha> -DOVS_KAD_EX=<0|1> (oversim_amd/build.py)"
 #endif
 #ifndef OVS_KAD_WAVES
-// minimum waves per SIMD the register allocator must allow: 3 (<= 168 VGPRs) costs a few spills
-// and runs E 1.2x faster than the unconstrained 176-188 VGPRs (2 waves); profiles/r02_b_kad
+// minimum waves per SIMD the register allocator must allow (profiles/r02_b_kad: 3 beat 2 and 4)
 #define OVS_KAD_WAVES 3
 #endif
 
@@ -31,21 +40,8 @@ struct SendNothing {
     __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
 };
 
-template <bool EX, bool LK>
-struct LocalFindNode {
-    const KadView& V;
-    const K160& K;
-    int numSiblings;
-    __device__ __forceinline__ bool ready(int) const { return true; }
-    __device__ __forceinline__ void fill(int, uint32_t r, const RespGeo& g, bool sb, int numR, bool, SVec<8>& res) const
-    {
-        Blk8 b;
-        const int n = kad_find_node_blk<EX>(V, r, g, K, numR, sb, b, LK ? numSiblings : 1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
-        res.n = n;
-        res.used = 0;
-    }
+struct AlwaysReady {
+    __device__ __forceinline__ bool operator()(int, uint32_t) const { return true; }
 };
 
 template <bool RECORD>
@@ -59,91 +55,272 @@ struct HopRecorder {
     }
 };
 
-template <int A, bool RECORD, bool EX, bool LK>
-__global__ __launch_bounds__(256, OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC, const K160* __restrict__ qkeys,
-                                                        const uint32_t* __restrict__ qsrc, uint64_t nq, uint64_t chunk,
-                                                        ovs_route_out* __restrict__ out, uint32_t* __restrict__ hopseq,
-                                                        uint32_t* __restrict__ rpcs_out, uint32_t* __restrict__ sib_out)
+// shard step: a response from a node off this arc is ready once its result was delivered
+struct RemoteReady {
+    const KadRes* __restrict__ res;
+    uint64_t base;
+    uint32_t lo, hi;
+    __device__ __forceinline__ bool operator()(int slot, uint32_t r) const
+    {
+        return (r >= lo && r < hi) || res[base + slot].ready != 0;
+    }
+};
+
+// shard step: a FindNodeCall to a node off this arc becomes a request to its owner, staged in the
+// call's slot (a slot carries at most one request per round: a response cannot be ready in the
+// round it is requested)
+struct ShardSend {
+    KadRes* __restrict__ res;
+    uint64_t base;
+    const K160* K;
+    const uint64_t* __restrict__ shard_lo;
+    int nsh;
+    uint32_t lo, hi;
+    ovs_kad_req* __restrict__ stage;
+    uint8_t* __restrict__ rtag;
+    uint32_t pad;   // LookupCall: bit 31 | numSiblings (the responder's findNode argument); 0 for KBR routes
+    __device__ __forceinline__ void operator()(int slot, uint32_t x, bool isTo) const
+    {
+        if (isTo || (x >= lo && x < hi)) return;   // a timeout carries no result; a local findNode runs here
+        res[base + slot].ready = 0u;
+        ovs_kad_req q;
+        for (int w = 0; w < 5; ++w) q.key[w] = K->w[w];
+        q.node = x;
+        q.tag = (uint32_t)(base + slot);
+        q.pad = pad;
+        stage[base + slot] = q;
+        int r = 0;
+        for (int i = 1; i < nsh; ++i) r += ((uint64_t)x >= shard_lo[i]) ? 1 : 0;
+        rtag[base + slot] = (uint8_t)r;
+    }
+};
+
+struct KadRouteIO {
+    const K160* __restrict__ qkeys;
+    const uint32_t* __restrict__ qsrc;
+    uint64_t nq;             // lookups (single GPU) / entries of the round's list (shard step)
+    uint64_t chunk;
+    ovs_route_out* __restrict__ out;
+    uint32_t* __restrict__ hopseq;
+    uint32_t* __restrict__ rpcs_out;
+    uint32_t* __restrict__ sib_out;
+    // shard step
+    void* st;                               // KadLookup<A>[nlook]
+    const uint8_t* __restrict__ act;
+    KadRes* __restrict__ res;
+    const uint64_t* __restrict__ list;      // this round's lookups (indices), *nlist_dev of them
+    const unsigned long long* __restrict__ nlist_dev;
+    const uint32_t* __restrict__ qids;
+    const uint64_t* __restrict__ shard_lo;
+    int nsh;
+    ovs_kad_req* __restrict__ rstage;
+    uint8_t* __restrict__ rtag;
+    ovs_done_rec* __restrict__ dstage;
+    uint8_t* __restrict__ ltag;
+};
+
+template <int A, bool RECORD, bool EX, bool LK, bool SHARD>
+// the shard step runs at 2 waves/SIMD: its HBM state traffic and request staging need the registers
+// (at 3 the exact-compare instantiations spilled in misaligned 96-bit pieces gfx950 rejects)
+__global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
+                                                                            KadRouteIO io)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    uint64_t nq = io.nq, chunk = io.chunk;
+    if (SHARD) {
+        // the round's list length is the previous round's device count (no host round trip)
+        nq = *io.nlist_dev;
+        const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+        chunk = (nq + waves - 1) / waves;
+    }
     uint64_t cursor = wave * chunk;
     const uint64_t end = min(cursor + chunk, nq);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int ns = LK ? LC.numSiblings : 1;
+    KadLookup<A>* st = static_cast<KadLookup<A>*>(io.st);
 
+#ifndef OVS_NOCOOP
+    __shared__ CoopLds lds;
+#else
+    CoopLds& lds = *(CoopLds*)nullptr;    // experiment build: never touched
+#endif
     bool active = false;
+    bool dead = false;     // shard step: a listed lookup that does not run (source off the arc)
     uint64_t q = 0;
     KadLookup<A> L;
-    SVec<8> res;
-    const SendNothing on;
 
     while (true) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && cursor < end) {
             const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
             if (!active && mine < end) {
-                q = mine;
                 active = true;
-                kad_lookup_init(L, qkeys[q], qsrc[q], V.xy);
+                if (SHARD) {
+                    q = io.list[mine];
+                    dead = io.act[q] == 0;
+                    if (!dead) L = st[q];
+                } else {
+                    q = mine;
+                    kad_lookup_init(L, io.qkeys[q], io.qsrc[q], V.xy);
+                }
             }
             cursor += (uint64_t)__popcll(need);
         }
+        // (a `continue` for a wave without work here, instead of the dead flag, made the compiler
+        // spill 240 B of the lookup state per lane)
         if (!__any(active)) break;
-        if (!active) continue;
 
-        if (!kad_lookup_done(L)) {
-            const LocalFindNode<EX, LK> fn{V, L.K, LC.numSiblings};
-            const HopRecorder<RECORD> rec{hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
-            kad_lookup_event<A, EX, LK>(L, V, DC, LC, res, fn, on, rec);
+        // phase 1 (per lane): the earliest event up to its findNode
+        int ph = KEV_IDLE;
+        KadEv ev;
+        ev.r = 0; ev.geo = 0; ev.boff = 0; ev.e = 0; ev.num = 0; ev.numR = 0; ev.start = false;
+        bool coop = false;
+        if (active && !dead && !kad_lookup_done(L)) {
+            const HopRecorder<RECORD> rec{io.hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
+            if (SHARD) {
+                const RemoteReady rd{io.res, q * A, V.lo, V.hi};
+                ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, rd, rec, ev);
+            } else {
+                ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, AlwaysReady{}, rec, ev);
+            }
+            const bool local = !SHARD || (ev.r >= V.lo && ev.r < V.hi);
+            coop = ph == KEV_FIND && local && kad_find_is_coop(V, ev.r, ev.rg(), ev.sb(), ns);
         }
-        if (kad_lookup_done(L)) {
-            const ovs_route_out o = kad_lookup_output(L, V, DC, LC);
-            out[q] = o;
-            if (rpcs_out) rpcs_out[q] = L.nsent;
-            if (LK) {
-                const bool ok = o.status == OVS_LOOKUP_OK;
-                if (LC.numSiblings == 0) {
-                    sib_out[q] = ok ? L.result : NONE;    // the one-slot vector of an exact-key lookup
-                } else {
-                    uint32_t* row = sib_out + q * (uint64_t)LC.numSiblings;
+
+        // phase 2 (whole wave): the sibling-zone findNodes (results in LDS).  The exact-compare
+        // instantiation (networks with IDs sharing their top 63 bits) keeps the per-lane scan: its
+        // tie fallbacks in the cooperative merge made the register allocator emit misaligned
+        // 96-bit spills that gfx950 rejects.
+#ifndef OVS_NOCOOP
+        if constexpr (!EX) kad_coop_sibzone<EX>(V, coop, ev.r, ev.geo, ev.boff, L.K, lds);
+        else coop = false;
+#else
+        coop = false;
+#endif
+
+        // phase 3 (per lane): the rest of the findNode, the LookupVector, the sends
+        if (SHARD && dead) {
+            active = false;
+            dead = false;
+        } else if (active) {
+            SVec<8> res;
+            res.n = 0;
+            res.used = 0;
+            int num = -1;
+            if (ph == KEV_FIND) {
+                int n;
+                Blk8 fb;
+                if (coop) {
+                    coop_get(lds.res, threadIdx.x, fb);
+                    n = kad_coop_finish<EX>(V, ev.rg(), L.K, ev.numR, ev.sb(), ns, fb, (int)lds.rcnt[threadIdx.x]);
+                } else if (SHARD && !(ev.r >= V.lo && ev.r < V.hi)) {
+                    // the owner's answer, delivered by k_kad_shard_deliver
+                    const KadRes& rr = io.res[q * A + ev.e];
+                    n = (int)rr.count;
 #pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        if (j < LC.numSiblings) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
+                    for (int k = 0; k < 8; ++k) { fb.x[k] = k < n ? rr.nodes[k] : NONE; fb.d[k] = k < n ? rr.dist[k] : ~0ull; }
+                } else {
+                    n = kad_find_node_blk<EX>(V, ev.r, ev.rg(), L.K, ev.numR, ev.sb(), fb, ns);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { res.idx[k] = fb.x[k]; res.d[k] = fb.d[k]; }
+                res.n = n;
+                num = kad_event_after_find<A, EX, LK>(L, V, LC, ev, res);
+            } else if (ph == KEV_SENDS) {
+                num = ev.num;
+            }
+            if (num >= 0) {
+                if (SHARD) {
+                    const ShardSend on{io.res, q * A, &L.K, io.shard_lo, io.nsh, V.lo, V.hi, io.rstage, io.rtag,
+                                       LK ? (0x80000000u | (uint32_t)ns) : 0u};
+                    kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, on);
+                } else {
+                    kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, SendNothing{});
                 }
             }
-            active = false;
+            if (kad_lookup_done(L)) {
+                const ovs_route_out o = kad_lookup_output(L, V, DC, LC);
+                const bool ok = o.status == OVS_LOOKUP_OK;
+                if (LK) {
+                    // the LookupResponse's sibling vector: the answering sibling's findNode result
+                    // (an exact-key lookup: the key's node); res is this iteration's answer
+                    if (ns == 0) {
+                        io.sib_out[q] = ok ? L.result : NONE;
+                    } else {
+                        uint32_t* row = io.sib_out + q * (uint64_t)ns;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            if (j < ns) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
+                    }
+                }
+                if (SHARD) {
+                    ovs_done_rec dr;
+                    dr.qid = io.qids[q];
+                    dr.pad = 0;
+                    dr.out = o;
+                    if (LK) {
+                        uint32_t cnt = 0;
+                        if (ns == 0) cnt = ok ? 1u : 0u;
+                        else cnt = ok ? (uint32_t)min(res.n, ns) : 0u;
+                        ovs_lookup_out lo;
+                        lo.num_siblings = cnt;
+                        lo.hops = o.hops;
+                        lo.status = o.status;
+                        lo.is_valid = ok ? 1 : 0;
+                        lo.latency_ns = ok ? o.latency_ns : -1;
+                        __builtin_memcpy(&dr.out, &lo, sizeof lo);
+                    }
+                    io.dstage[q] = dr;
+                    io.ltag[q] = 0;
+                } else {
+                    io.out[q] = o;
+                    if (io.rpcs_out) io.rpcs_out[q] = L.nsent;
+                }
+                active = false;
+            } else if (SHARD && ph == KEV_WAIT) {
+                // the earliest event waits for an owner's answer: suspended until the next round
+                st[q] = L;
+                io.ltag[q] = 1;
+                active = false;
+            }
         }
     }
 }
 
 }  // namespace
 
-template <class Kern>
-static uint64_t kad_chunk(Kern kern, int* cache, uint64_t nq, int num_cu, uint64_t* blocks)
+// persistent grid: as many waves as are resident, each with a contiguous slice of the batch
+template <int A, bool RECORD, bool EX, bool LK, bool SHARD>
+static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, KadRouteIO io, int num_cu,
+                             hipStream_t st)
 {
-    if (*cache == 0) {
+    // occupancy of this instantiation (the same on every gfx950 device; a function-local static is
+    // initialised once, thread-safely)
+    static const int bpc = [] {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 256, 0) != hipSuccess || b < 1) b = 1;
-        *cache = b;
-    }
-    const uint64_t waves = (uint64_t)num_cu * (uint64_t)(*cache) * 4;
-    uint64_t chunk = (nq + waves - 1) / waves;
-    if (chunk < 1) chunk = 1;
-    const uint64_t need_waves = (nq + chunk - 1) / chunk;
-    *blocks = (need_waves + 3) / 4;
-    return chunk;
-}
-
-template <int A, bool RECORD, bool EX, bool LK>
-static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
-                             const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
-                             uint32_t* sibs, int num_cu, hipStream_t st)
-{
-    static int bpc = 0;    // one per instantiation
-    uint64_t blocks = 0;
-    const uint64_t chunk = kad_chunk(k_kad_route<A, RECORD, EX, LK>, &bpc, nq, num_cu, &blocks);
-    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC, qkeys,
-                       qsrc, nq, chunk, out, hopseq, rpcs, sibs);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SHARD>, 256, 0) !=
+                hipSuccess ||
+            b < 1)
+            b = 1;
+        return b;
+    }();
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4;
+    io.chunk = (io.nq + waves - 1) / waves;
+    if (io.chunk < 1) io.chunk = 1;
+    const uint64_t need_waves = (io.nq + io.chunk - 1) / io.chunk;
+    const uint64_t blocks = (need_waves + 3) / 4;
+#ifdef OVS_KAD_STATS
+    unsigned long long z[8] = {};
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kad_stats), z, sizeof z, 0, hipMemcpyHostToDevice, st);
+#endif
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SHARD>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC, io);
+#ifdef OVS_KAD_STATS
+    hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    fprintf(stderr, "kadstats nq=%llu find=%llu blocks=%llu sibzone=%llu shortmain=%llu\n", (unsigned long long)io.nq,
+            z[0], z[1], z[2], z[3]);
+#endif
     return hipGetLastError();
 }
 
@@ -152,14 +329,33 @@ hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC
                             const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
                             uint32_t* sibs, int num_cu, hipStream_t st)
 {
+    KadRouteIO io{};
+    io.qkeys = qkeys; io.qsrc = qsrc; io.nq = nq; io.out = out; io.hopseq = hopseq; io.rpcs_out = rpcs; io.sib_out = sibs;
     // LookupCall batches (sibs != nullptr) record no hop sequence
-    if (sibs) return kad_launch<A, false, EX, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st);
-    if (hopseq) return kad_launch<A, true, EX, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st);
-    return kad_launch<A, false, EX, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st);
+    if (sibs) return kad_launch<A, false, EX, true, false>(V, DC, LC, io, num_cu, st);
+    if (hopseq) return kad_launch<A, true, EX, false, false>(V, DC, LC, io, num_cu, st);
+    return kad_launch<A, false, EX, false, false>(V, DC, LC, io, num_cu, st);
+}
+
+template <int A, bool EX>
+hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const KadShardStepArgs& a,
+                                 int num_cu, hipStream_t st)
+{
+    if (a.nlist_max == 0) return hipSuccess;
+    KadRouteIO io{};
+    io.nq = a.nlist_max;     // sizes the grid; the kernel reads the list length from nlist_dev
+    io.sib_out = a.sib_out;
+    io.st = a.st; io.act = a.act; io.res = a.res; io.list = a.list; io.nlist_dev = a.nlist_dev; io.qids = a.qids;
+    io.shard_lo = a.shard_lo; io.nsh = a.nsh;
+    io.rstage = a.rstage; io.rtag = a.rtag; io.dstage = a.dstage; io.ltag = a.ltag;
+    if (a.sib_out) return kad_launch<A, false, EX, true, true>(V, DC, LC, io, num_cu, st);
+    return kad_launch<A, false, EX, false, true>(V, DC, LC, io, num_cu, st);
 }
 
 template hipError_t kad_route_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
                                                                  const K160*, const uint32_t*, uint64_t, ovs_route_out*,
                                                                  uint32_t*, uint32_t*, uint32_t*, int, hipStream_t);
+template hipError_t kad_shard_step_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
+                                                                      const KadShardStepArgs&, int, hipStream_t);
 
 }  // namespace ovs

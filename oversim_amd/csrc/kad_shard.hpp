@@ -14,18 +14,42 @@ struct KadRes {
 };
 static_assert(sizeof(KadRes) == 104, "KadRes layout");
 
+// what the shard-step instantiation of K2 (kad_route.hip) reads and writes in one round
+struct KadShardStepArgs {
+    void* st;                          // KadLookup<A>[nlook], the suspended lookups
+    const uint8_t* act;                // 1: the lookup runs (its source is on this arc)
+    KadRes* res;                       // nlook * A result slots
+    const uint64_t* list;              // this round's lookups (indices), *nlist_dev of them
+    const unsigned long long* nlist_dev;
+    uint64_t nlist_max;                // sizes the grid (the lookups of the batch)
+    const uint32_t* qids;
+    const uint64_t* shard_lo;          // device copy of the arc bounds
+    int nsh;
+    ovs_kad_req* rstage;               // a request per pending-call slot, tagged by owner in rtag
+    uint8_t* rtag;
+    ovs_done_rec* dstage;              // a done record per lookup; ltag: 0 finished, 1 still active
+    uint8_t* ltag;
+    uint32_t* sib_out;                 // LookupCalls: the sibling rows (nullptr: KBR routes)
+};
+
 size_t kad_lookup_state_bytes(int alpha);
 bool kad_params_supported_host(const ovs_params& P, const KadTables& t);
+// lookups of this rank: state, qids, the round-1 list (indices 0..n-1) and its count; sources off
+// [lo, hi) are counted in *bad and never run
 hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
-                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, uint32_t lo,
-                          uint32_t hi, unsigned long long* bad, hipStream_t s);   // bad: sources off [lo, hi)
+                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, uint64_t* iota,
+                          unsigned long long* nlist, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t s);
+// one round: the list's lookups advance while their responders are local (k_kad_route<.., SHARD>);
+// requests to the owners of the others go to segment d of out (out + d * out_cap, counter
+// out_count[d]); finished lookups are appended to done (done_count); the still active ones form the
+// next list (*nlist_next) and are counted in *active_count.  bad: table reads off the arc.
 hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
-                          const DelayConsts& DC, void* st, uint8_t* act, const uint32_t* qids, KadRes* res,
-                          uint64_t nlook, const uint64_t* shard_lo, int nsh, ovs_kad_req* out, uint32_t* out_dest,
-                          uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                          unsigned long long* done_count, unsigned long long* active_count, int lk_ns,
-                          uint32_t* sib_out, unsigned long long* bad, StageBuf& stage,
-                          hipStream_t s);   // lk_ns < 0: KBR routes; bad: table reads off the arc
+                          const DelayConsts& DC, void* st, const uint8_t* act, const uint32_t* qids, KadRes* res,
+                          uint64_t nlook, const uint64_t* list, const unsigned long long* nlist, const uint64_t* iota,
+                          uint64_t* list_next, unsigned long long* nlist_next, const uint64_t* shard_lo, int nsh,
+                          ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,
+                          uint64_t done_cap, unsigned long long* done_count, unsigned long long* active_count, int lk_ns,
+                          uint32_t* sib_out, unsigned long long* bad, int num_cu, StageBuf& stage, hipStream_t s);
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
                            ovs_kad_resp* out, unsigned long long* bad, hipStream_t s);
 hipError_t kad_shard_deliver(const ovs_kad_resp* in, uint64_t n, KadRes* res, uint64_t nslots,

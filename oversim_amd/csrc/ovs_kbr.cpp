@@ -70,6 +70,10 @@ struct ovs_ctx {
     uint32_t* kqids = nullptr;
     KadRes* kres = nullptr;              // alpha findNode result slots per lookup
     unsigned long long* kbad = nullptr;  // undeliverable responses
+    uint64_t* kiota = nullptr;           // lookup indices 0..n-1: round 1's list, the source of the next lists
+    uint64_t* klist[2] = {nullptr, nullptr};   // ping-pong lists of the still active lookups
+    unsigned long long* knl = nullptr;   // [3]: length of iota (round 1), klist[0], klist[1]
+    int kcur = 0;                        // list of the next round: 0 = iota, 1/2 = klist[0/1]
     uint64_t knlook = 0, kcap = 0;
     int kalpha = 0;
     int32_t kns = -1;                    // LookupCall batch: numSiblings (-1: KBR routes)
@@ -116,10 +120,11 @@ void free_tables(ovs_ctx* c)
 
 void free_kad_shard(ovs_ctx* c)
 {
-    void* ptrs[] = {c->kst, c->kact, c->kqids, c->kres, c->kbad};
+    void* ptrs[] = {c->kst, c->kact, c->kqids, c->kres, c->kbad, c->kiota, c->klist[0], c->klist[1], c->knl};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->kst = nullptr; c->kact = nullptr; c->kqids = nullptr; c->kres = nullptr; c->kbad = nullptr;
+    c->kiota = nullptr; c->klist[0] = c->klist[1] = nullptr; c->knl = nullptr; c->kcur = 0;
     c->knlook = 0; c->kcap = 0; c->kalpha = 0;
 }
 
@@ -859,6 +864,10 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
         HIPCHK(c, hipMalloc(&c->kqids, sizeof(uint32_t) * cap));
         HIPCHK(c, hipMalloc(&c->kres, sizeof(KadRes) * cap * alpha));
         HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
+        HIPCHK(c, hipMalloc(&c->kiota, sizeof(uint64_t) * cap));
+        HIPCHK(c, hipMalloc(&c->klist[0], sizeof(uint64_t) * cap));
+        HIPCHK(c, hipMalloc(&c->klist[1], sizeof(uint64_t) * cap));
+        HIPCHK(c, hipMalloc(&c->knl, sizeof(unsigned long long) * 3));
         c->kcap = cap;
         c->kalpha = alpha;
     }
@@ -866,8 +875,9 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
     c->kns = lk_ns;
     c->ksib = sib;
     HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
+    c->kcur = 0;
     HIPCHK(c, kad_shard_init(alpha, reinterpret_cast<const K160*>(keys), src, n, qid_base, c->xy, c->kst, c->kact,
-                             c->kqids, c->kres, c->kad.lo, c->kad.hi, c->kbad, s));
+                             c->kqids, c->kres, c->kiota, c->knl, c->kad.lo, c->kad.hi, c->kbad, s));
     return OVS_OK;
 }
 
@@ -891,16 +901,18 @@ ovs_status ovs_kad_shard_begin_lookup(ovs_ctx* c, int32_t num_siblings, const ov
     return kad_shard_begin_impl(c, ns, siblings, keys, src, n, qid_base, stream);
 }
 
-ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, uint64_t out_cap,
-                              unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                              unsigned long long* done_count, unsigned long long* active_count,
-                              const uint64_t* shard_lo, uint32_t nshards, void* stream)
+ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count,
+                              ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                              unsigned long long* active_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
 {
     if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
-    if (!out || !out_dest || !out_count || !done || !done_count || !active_count) return OVS_EINVAL;
+    if (!out || !out_count || !done || !done_count || !active_count) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (!c->kst) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
     if (c->P.lookupParallelRpcs != c->kalpha && c->knlook)
         return fail(c, OVS_ESTATE, "lookupParallelRpcs changed since ovs_kad_shard_begin");
+    if (out_cap < c->knlook * (uint64_t)c->kalpha)
+        return fail(c, OVS_EINVAL, "out_cap must hold a request per pending-call slot (n * lookupParallelRpcs)");
     uint64_t lo_h[MAXSHARDS + 1];
     for (uint32_t r = 0; r <= nshards; ++r) {
         lo_h[r] = shard_lo[r];
@@ -914,10 +926,15 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint32_t* out_dest, 
     hipStream_t s = (hipStream_t)stream;
     ovs_status bst = upload_bounds(c, lo_h, nshards);
     if (bst != OVS_OK) return bst;
+    // this round's list: iota in round 1, then the ping-pong lists the previous round compacted
+    const int cur = c->kcur, nxt = cur == 1 ? 2 : 1;
+    const uint64_t* list = cur == 0 ? c->kiota : c->klist[cur - 1];
     hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kqids,
-                                  c->kres, c->knlook, c->d_bounds, (int)nshards, out, out_dest, out_cap, out_count,
-                                  done, done_cap, done_count, active_count, c->kns, c->ksib, c->kbad, c->stage[s], s);
+                                  c->kres, c->knlook, list, c->knl + cur, c->kiota, c->klist[nxt - 1], c->knl + nxt,
+                                  c->d_bounds, (int)nshards, out, out_cap, out_count, done, done_cap, done_count,
+                                  active_count, c->kns, c->ksib, c->kbad, c->num_cu, c->stage[s], s);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard step");
+    c->kcur = nxt;
     return OVS_OK;
 }
 

@@ -202,8 +202,8 @@ for _name, _args in {
     "ovs_kad_shard_begin": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p],
     "ovs_kad_shard_begin_lookup": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                    C.c_void_p, C.c_void_p],
-    "ovs_kad_shard_step": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
-                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
+    "ovs_kad_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                           C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
     "ovs_kad_shard_serve": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p],
     "ovs_kad_shard_deliver": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
     "ovs_kad_shard_errors": [C.c_void_p, C.c_void_p],
@@ -270,7 +270,9 @@ class TorchExchange:
         into one receive buffer ordered by source rank: grouped point-to-point sends out of
         the segments, so nothing is packed first; this rank's own share is a device copy."""
         torch = self.torch
-        recv = torch.empty((sum(rcl), row_bytes), dtype=torch.uint8, device=self.comm_dev)
+        # 0xFF sentinel: a row the exchange never wrote reads as an impossible record (node / cur /
+        # tag 0xFFFFFFFF), which the consuming kernel counts as an error instead of using
+        recv = torch.full((sum(rcl), row_bytes), 0xFF, dtype=torch.uint8, device=self.comm_dev)
         ops, off = [], 0
         for r in range(self.world):
             if rcl[r] and r != self.rank:
@@ -298,7 +300,7 @@ class TorchExchange:
         rank's own share (RCCL's all_to_all_single lost records at world size 1 beyond ~1 GB)."""
         torch = self.torch
         send = send.to(self.comm_dev)
-        recv = torch.empty((sum(rcl), send.shape[1]), dtype=torch.uint8, device=self.comm_dev)
+        recv = torch.full((sum(rcl), send.shape[1]), 0xFF, dtype=torch.uint8, device=self.comm_dev)   # sentinel
         ops = []
         so = np.concatenate([[0], np.cumsum(scl)]).astype(np.int64)
         ro = np.concatenate([[0], np.cumsum(rcl)]).astype(np.int64)
@@ -324,19 +326,6 @@ class TorchExchange:
         if self.total(sum(scl)) == 0:
             return None
         return self.records(send, scl, rcl)
-
-
-def group_by_dest(out, dest, world: int):
-    """The outbox grouped by destination rank (stable) and its per-destination counts.
-    ovs_kad_shard_step already writes it grouped, which costs one ordered-check here."""
-    import torch
-    if out.shape[0] == 0:
-        return out, torch.zeros(world, dtype=torch.int64, device=out.device)
-    d = dest.to(torch.int64)
-    if d.shape[0] > 1 and not bool((d[1:] >= d[:-1]).all()):
-        order = torch.argsort(d, stable=True)
-        out, d = out.index_select(0, order), d.index_select(0, order)
-    return out, torch.bincount(d, minlength=world)
 
 
 def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 10_000, cohorts: int = 2,
@@ -456,12 +445,14 @@ class KadShardStepper:
                                       xy.ctypes.data_as(C.c_void_p), self.bounds[rank], self.bounds[rank + 1], 0)
         self.eng._chk(st, "ovs_kad_load_shard")
         self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
-        self.counters = torch.zeros(3, dtype=torch.int64, device=device)   # out, done, active
+        # counts[0..world): requests per owner rank, counts[world]: lookups still active, counts[world+1]: done
+        self.counts = torch.zeros(self.world + 2, dtype=torch.int64, device=device)
         self.n = 0
         self.served = 0   # FindNodeCalls answered by this rank (requests served)
         self.timing = False
         self.kernel_ms = 0.0
         self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        self._timed = False
 
     def _s(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
@@ -475,12 +466,11 @@ class KadShardStepper:
         self.n = n
         a = self.params.lookupParallelRpcs
         # one round sends at most alpha requests per lookup (a request occupies a pending slot
-        # until its result is delivered at the end of the round)
-        self.cap = max(n * a, 1)
-        self.out = torch.empty((self.cap, KAD_REQ_BYTES), dtype=torch.uint8, device=self.dev)
-        self.out_dest = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
+        # until its result is delivered at the end of the round): a segment per owner rank
+        self.seg_cap = max(n * a, 1)
+        self.out = torch.empty((self.world, self.seg_cap, KAD_REQ_BYTES), dtype=torch.uint8, device=self.dev)
         self.done = torch.empty((max(n, 1), DONE_BYTES), dtype=torch.uint8, device=self.dev)
-        self.counters.zero_()
+        self.counts.zero_()
         self.qid_base = qid_base
         if self.lookup_siblings is None:
             st = lib().ovs_kad_shard_begin(self.eng._h, self._p(keys_t), self._p(src_t), n, qid_base, self._s())
@@ -493,38 +483,35 @@ class KadShardStepper:
         self.eng._chk(st, "ovs_kad_shard_begin_lookup")
 
     def step(self):
-        """One round: returns (requests, destination ranks, active lookups on this rank)."""
-        self.counters[0].zero_()
-        self.counters[2].zero_()
+        """One round, stream-ordered (no host synchronisation): returns (per-owner request segments
+        [world, seg_cap, 32], device counts [world + 2]: requests per owner, active lookups, done)."""
+        self.counts[:self.world].zero_()
         if self.timing:
             self._ev[0].record()
-        st = lib().ovs_kad_shard_step(self.eng._h, self._p(self.out), self._p(self.out_dest), self.cap,
-                                      self._p(self.counters), self._p(self.done), self.done.shape[0],
-                                      self._p(self.counters, 8), self._p(self.counters, 16), self._lo, self.world,
-                                      self._s())
+        W = self.world
+        st = lib().ovs_kad_shard_step(self.eng._h, self._p(self.out), self.seg_cap, self._p(self.counts),
+                                      self._p(self.done), self.done.shape[0], self._p(self.counts, 8 * (W + 1)),
+                                      self._p(self.counts, 8 * W), self._lo, W, self._s())
         self.eng._chk(st, "ovs_kad_shard_step")
         if self.timing:
             self._ev[1].record()
-        c = self.counters.tolist()
-        if self.timing:
+            self._timed = True
+        return self.out, self.counts
+
+    def collect_timing(self):
+        """Add the last step kernel's time (call after the round's host synchronisation)."""
+        if self.timing and self._timed:
+            self._ev[1].synchronize()
             self.kernel_ms += self._ev[0].elapsed_time(self._ev[1])
-        if c[0] > self.cap:
-            raise RuntimeError("kademlia request buffer overflow")
-        return self.out[:c[0]], self.out_dest[:c[0]], c[2]
+            self._timed = False
 
     def serve(self, reqs):
         n = reqs.shape[0]
         self.served += n
         resp = self.torch.empty((n, KAD_RESP_BYTES), dtype=self.torch.uint8, device=self.dev)
         if n:
-            if self.timing:
-                self._ev[2].record()
             st = lib().ovs_kad_shard_serve(self.eng._h, self._p(reqs), n, self._p(resp), self._s())
             self.eng._chk(st, "ovs_kad_shard_serve")
-            if self.timing:
-                self._ev[3].record()
-                self._ev[3].synchronize()
-                self.kernel_ms += self._ev[2].elapsed_time(self._ev[3])
         return resp
 
     def deliver(self, resps):
@@ -533,19 +520,21 @@ class KadShardStepper:
             self.eng._chk(st, "ovs_kad_shard_deliver")
 
     def errors(self) -> int:
-        """ovs_kad_shard_errors: undeliverable responses (mis-routed requests) and sources off this arc."""
+        """ovs_kad_shard_errors: undeliverable responses (mis-routed or lost requests), table reads off
+        this arc, and sources off this rank's arc."""
         bad = C.c_uint64(0)
         self.eng._chk(lib().ovs_kad_shard_errors(self.eng._h, C.byref(bad)), "ovs_kad_shard_errors")
         return int(bad.value)
 
     def finished(self):
-        k = int(self.counters[1].item())
+        k = int(self.counts[self.world + 1].item())
         if k > self.done.shape[0]:
             raise RuntimeError("done buffer overflow")
         bad = self.errors()
         if bad:
             raise RuntimeError(f"{bad} Kademlia shard errors: responses that could not be delivered (request sent "
-                               "to the wrong rank) or lookups whose source lies off this rank's arc")
+                               "to the wrong rank or lost in the exchange), table reads off the arc, or lookups "
+                               "whose source lies off this rank's arc")
         return self.done[:k]
 
     def lookup_results(self, done):
@@ -558,23 +547,29 @@ class KadShardStepper:
 
 
 def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 5_000):
-    """Route this rank's Kademlia lookups; 2 all-to-allv per round (requests, responses)."""
+    """Route this rank's Kademlia lookups.  Per round: the step kernel, ONE host synchronisation (the
+    all-gather of every rank's per-owner request counts and active lookups), then the requests to the
+    owners, their findNode answers and the responses back (2 all-to-allv with the splits the matrix
+    gives) -- all stream-ordered."""
     stepper.begin(keys_t, src_t, qid_base)
+    W, me = exchange.world, exchange.rank
     rounds = 0
     while True:
         rounds += 1
-        out, dest, active = stepper.step()
-        send, counts = group_by_dest(out, dest, exchange.world)
-        scl, rcl = exchange.counts(counts)
-        if exchange.total(sum(scl) + active) == 0:
+        segs, counts = stepper.step()
+        M = exchange.count_matrix_async(counts[:W + 1])()      # M[s, d] requests s -> d, M[s, W] active on s
+        if hasattr(stepper, "collect_timing"):
+            stepper.collect_timing()
+        if int(M.sum()) == 0:
             break
-        reqs = exchange.records(send, scl, rcl)
-        resps = stepper.serve(reqs.to(stepper.dev))
+        scl, rcl = M[me, :W].tolist(), M[:W, me].tolist()
+        reqs = exchange.segments(segs, scl, rcl, KAD_REQ_BYTES)
+        resps = stepper.serve(reqs if reqs.device == stepper.dev else reqs.to(stepper.dev))
         back = exchange.records(resps, rcl, scl)          # reverse splits: back to the requesters
-        stepper.deliver(back.to(stepper.dev))
+        stepper.deliver(back if back.device == stepper.dev else back.to(stepper.dev))
         if rounds > max_rounds:
-            raise RuntimeError(f"sharded Kademlia routing did not terminate: {active} lookups active, "
-                               f"{sum(scl)} requests sent, {sum(rcl)} received in round {rounds}")
+            raise RuntimeError(f"sharded Kademlia routing did not terminate: {int(M[:, W].sum())} lookups active, "
+                               f"{int(M[:, :W].sum())} requests in round {rounds}")
     return stepper.finished(), rounds
 
 
@@ -587,33 +582,27 @@ def route_kad_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, m
     rounds = 0
     while True:
         rounds += 1
-        sends, active = [], 0
+        segs, rows = [], []
         for r in range(W):
-            out, dest, act = steppers[r].step()
-            active += act
-            send, counts = group_by_dest(out, dest, W)
-            sends.append((send, counts.tolist()))
-        if active == 0 and all(sum(c) == 0 for _, c in sends):
+            sg, counts = steppers[r].step()
+            segs.append(sg)
+            rows.append(counts[:W + 1].cpu().numpy().copy())
+        M = np.stack(rows)
+        if int(M.sum()) == 0:
             break
-        # requests to owners
-        inbox = [[] for _ in range(W)]           # (source rank, rows)
-        for r, (send, counts) in enumerate(sends):
-            off = 0
-            for d, c in enumerate(counts):
-                inbox[d].append((r, send[off:off + c]))
-                off += c
-        replies = [[None] * W for _ in range(W)]  # replies[src][owner]
+        # requests to owners, replies back in the requesters' segment order
+        replies = [[None] * W for _ in range(W)]
         for d in range(W):
-            rows = torch.cat([x for _, x in inbox[d]]) if inbox[d] else None
-            if rows is None or rows.shape[0] == 0:
-                for r, x in inbox[d]:
-                    replies[r][d] = x.new_empty((0, KAD_RESP_BYTES))
+            parts = [segs[r][d][:int(M[r, d])] for r in range(W)]
+            rows_d = torch.cat(parts) if parts else None
+            if rows_d is None or rows_d.shape[0] == 0:
                 continue
-            resp = steppers[d].serve(rows)
+            resp = steppers[d].serve(rows_d)
             off = 0
-            for r, x in inbox[d]:
-                replies[r][d] = resp[off:off + x.shape[0]]
-                off += x.shape[0]
+            for r in range(W):
+                k = int(M[r, d])
+                replies[r][d] = resp[off:off + k]
+                off += k
         for r in range(W):
             parts = [x for x in replies[r] if x is not None and x.shape[0]]
             if parts:

@@ -285,8 +285,8 @@ def test_two_processes_share_one_gpu_gloo():
 class FakeKadStepper:
     """Protocol double for route_kad_sharded: lookup i queries the nodes plan[i] one after the
     other; each query is a request to the node's owner, answered with a value derived from
-    (node, key) that the requester checks.  Exercises grouping, both all-to-allv directions
-    (reverse splits), delivery by tag and termination -- without a GPU."""
+    (node, key) that the requester checks.  Exercises the per-owner segments, the count matrix,
+    both all-to-allv directions (reverse splits), delivery by tag and termination -- without a GPU."""
 
     def __init__(self, bounds, rank, n_nodes, seed):
         self.bounds, self.rank, self.world = bounds, rank, len(bounds) - 1
@@ -309,7 +309,8 @@ class FakeKadStepper:
         self.done = []
 
     def step(self):
-        out, dest, active = [], [], 0
+        segs = [[] for _ in range(self.world)]
+        active = 0
         for i in range(len(self.plan)):
             if self.waiting[i] or self.pos[i] < 0:
                 if self.waiting[i]:
@@ -323,12 +324,12 @@ class FakeKadStepper:
             rec = np.zeros(8, np.uint32)
             rec[:5] = self.keys[i]
             rec[5], rec[6] = node, i
-            out.append(rec.view(np.uint8))
-            dest.append(self.owner(node))
+            segs[self.owner(node)].append(rec.view(np.uint8))
             self.waiting[i] = True
             active += 1
-        o = torch.from_numpy(np.stack(out)) if out else torch.zeros((0, 32), dtype=torch.uint8)
-        return o, torch.tensor(dest, dtype=torch.int32), active
+        out = [torch.from_numpy(np.stack(x)) if x else torch.zeros((0, 32), dtype=torch.uint8) for x in segs]
+        counts = torch.tensor([x.shape[0] for x in out] + [active, len(self.done)], dtype=torch.int64)
+        return out, counts
 
     def serve(self, reqs):
         r = reqs.numpy().view(np.uint32).reshape(-1, 8)
