@@ -44,6 +44,16 @@ __device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2*
     const uint64_t win = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
     bool out_bits = false;
     for (int b = 0; b < mlo; ++b) out_bits |= kbit(M, b) != 0;
+    // siblings at levels <= endIndex - k, k = 1..4 (kad_sib_prefix)
+    uint32_t c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    for (int i = 0; i < cnt; ++i) {
+        const int l = k_msb(k_xor(kload(recs, L[i]), me));
+        c1 += l <= end - 1 ? 1u : 0u;
+        c2 += l <= end - 2 ? 1u : 0u;
+        c3 += l <= end - 3 ? 1u : 0u;
+        c4 += l <= end - 4 ? 1u : 0u;
+    }
+    const uint32_t lev = c1 | (c2 << 8) | (c3 << 16) | (c4 << 24);
     const double2 p = xy[v];
     KadNode o;
     for (int i = 0; i < 5; ++i) o.key[i] = me.w[i];
@@ -52,7 +62,7 @@ __device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2*
     o.rtop = ktop(R);
     o.mwin = win;
     o.meta = (uint32_t)(end + 1) | ((uint32_t)(rowlo + 1) << 8) | ((uint32_t)cnt << 16) | (out_bits ? KMETA_MASK_OUT : 0u);
-    o.spare = 0;
+    o.spare = lev;
     out[v] = o;
     KadX x;
     for (int i = 0; i < 5; ++i) { x.R[i] = R.w[i]; x.mask[i] = M.w[i]; }
@@ -146,6 +156,27 @@ __device__ __forceinline__ void put_entry(KadBlk* __restrict__ blks, uint64_t bl
     b->top[q % KBLK] = x == NONE ? ~0ull : ktop(kload(recs, x));
 }
 
+// a node's sibling row: its S5 entries (NONE padded) in ascending level msb(x ^ v), stable -- the
+// siblings at levels <= l are a prefix, so a findNode whose answer lies below 2^(l+1) reads only
+// that prefix's blocks (kad_sib_prefix)
+__device__ void put_sibling_row(KadBlk* __restrict__ blks, uint64_t blk0, int sbn, const uint32_t* L, int S5,
+                                const K160& me, const KeyRec* __restrict__ recs)
+{
+    uint32_t x[64];
+    uint8_t lv[64];
+    int cnt = 0;
+    for (int i = 0; i < S5 && i < 64; ++i) {
+        if (L[i] == NONE) continue;
+        // insertion by level, stable
+        const uint8_t l = (uint8_t)k_msb(k_xor(kload(recs, L[i]), me));
+        int j = cnt++;
+        while (j > 0 && lv[j - 1] > l) { x[j] = x[j - 1]; lv[j] = lv[j - 1]; --j; }
+        x[j] = L[i];
+        lv[j] = l;
+    }
+    for (int q = 0; q < sbn * KBLK; ++q) put_entry(blks, blk0, q, q < cnt ? x[q] : NONE, recs);
+}
+
 // snapshot pass B: buckets m = 159 .. endIndex of the owned nodes, up to k members of T_m minus
 // siblings chosen by Floyd sampling (snapshot rule); sibling rows
 __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __restrict__ nodes, uint32_t n, int k,
@@ -158,7 +189,7 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
     const K160 me = as_key(r.key);
     const uint32_t* L = sib + (uint64_t)v * S5;
     // sibling row
-    for (int q = 0; q < sbn * KBLK; ++q) put_entry(blks, sib_base + (uint64_t)(v - own_lo) * sbn, q, q < S5 ? L[q] : NONE, recs);
+    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, L, S5, me, recs);
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     uint32_t lo = 0, hi = n;
@@ -274,7 +305,7 @@ __global__ void k_kad_explicit_rows(const KeyRec* __restrict__ recs, const KadNo
     if (v >= n) return;
     const KadNode r = nodes[v];
     const uint32_t* L = sib + (uint64_t)v * S5;
-    for (int q = 0; q < sbn * KBLK; ++q) put_entry(blks, sib_base + (uint64_t)v * sbn, q, q < S5 ? L[q] : NONE, recs);
+    put_sibling_row(blks, sib_base + (uint64_t)v * sbn, sbn, L, S5, kload(recs, v), recs);
     const int rowlo = kad_rowlo(r.meta);
     if (rowlo < 0) return;
     for (int m = KEYBITS - 1; m >= rowlo; --m) {

@@ -617,12 +617,32 @@ struct KadLC {
 struct Pend {
     uint32_t node;
     uint32_t tag;      // step at send (bits 0..15) | insertion sequence (bits 16..30) | timeout (bit 31)
-    int64_t t;         // event time
+    int64_t t;         // event time (bits 0..55, ns) | the responder's sibling-row prefix (56..62, kad_sib_prefix)
     uint32_t dins;     // t - insertion time
     uint32_t geo;      // responder: m + 1 (bits 0..7) | endIndex + 1 (8..15) | rowlo + 1 (16..23) | sib (24)
                        // | sibling count (25..31; 5s <= 120)
     uint32_t boff;     // responder's bucket-row offset
 };
+
+constexpr int64_t PEND_TMASK = (1ll << 56) - 1;   // event times stay below 2^56 ns (kad_params_supported)
+
+// How many entries of c's level-sorted sibling row (kad.hip put_sibling_row) a sibling-zone
+// findNode(K) with result capacity cap must read.  A sibling at level l = msb(x ^ c) lies at XOR
+// distance [2^l, 2^(l+1)) from K when l > m = msb(c ^ K), below 2^(m+1) otherwise, and so does c
+// itself: for the smallest l in [m, endIndex) whose siblings at levels <= l plus c reach cap
+// candidates, nothing beyond that prefix of the row can enter the result.  lev = KadNode.spare:
+// byte k-1 = the siblings at levels <= endIndex - k, k = 1..4.
+__device__ __forceinline__ int kad_sib_prefix(const RespGeo& g, uint32_t lev, int cap)
+{
+    int pre = g.nsib;
+    bool found = false;
+#pragma unroll
+    for (int k = 4; k >= 1; --k) {
+        const int c = (int)((lev >> (8 * (k - 1))) & 0xFFu);
+        if (!found && g.endIndex - k >= g.m && c + 1 >= cap) { pre = c; found = true; }
+    }
+    return pre;
+}
 
 __device__ __forceinline__ uint32_t pack_geo(const RespGeo& g, bool sb)
 {
@@ -716,6 +736,8 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     const uint32_t sTo = L.seq++;
     const uint32_t sR = L.seq++;
     const uint32_t tag = (uint32_t)L.step | ((isTo ? sTo : sR) << 16) | (isTo ? 0x80000000u : 0u);
+    const int rcap = min(sb ? (ns ? ns : 1) : LC.redundant, 8);
+    const int64_t pre = rg.m <= rg.endIndex ? (int64_t)kad_sib_prefix(rg, rr.spare, rcap) : 0;
     int slot = 0;
 #pragma unroll
     for (int i = A - 1; i >= 0; --i)
@@ -724,7 +746,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     for (int i = 0; i < A; ++i) {
         if (i == slot) {
             L.p[i].node = x;
-            L.p[i].t = isTo ? tTo : tResp;
+            L.p[i].t = (isTo ? tTo : tResp) | (pre << 56);
             L.p[i].dins = (uint32_t)(isTo ? DC.rpcTimeout : d2);
             L.p[i].tag = tag;
             L.p[i].geo = pack_geo(rg, sb);
@@ -773,131 +795,8 @@ __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
     return L.started && (L.pfinished || L.pvalid == 0);
 }
 
-// Advance a lookup by one event.  The first call is IterativeLookup::start (IterativeLookup.cc:
-// 133-244): findNode at the source itself.  Every later call processes the earliest pending
-// event, a FindNodeResponse or an RPC timeout.  getres.ready(slot) says whether the responder's
-// findNode result is available (always on a single GPU); getres.fill(slot, node, geometry,
-// sibling, numRedundant, local, res) produces it (local: the source's own findNode at start).
-// Returns false, with the state untouched, when the earliest event is a response whose result
-// has not arrived yet.  Start, responses and timeouts share one findNode, one LookupVector merge
-// and one sendRpc site, so the kernels inline each once.
-template <int A, bool EX, bool LK, class GetRes, class OnSend, class Rec>
-__device__ __forceinline__ bool kad_lookup_event(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
-                                                 const KadLC& LC, SVec<8>& res, const GetRes& getres,
-                                                 const OnSend& on, const Rec& record)
-{
-    const int ns = LK ? LC.numSiblings : 1;
-    uint32_t r = L.S;
-    RespGeo rg;
-    bool sb = false, resp = true;
-    int e = -1, numR = LC.redundant;
-    const bool start = !L.started;
-    if (start) {
-        L.started = true;
-        const KadNode rn = load_node(V.nodes, L.S);
-        sb = kad_is_sibling(V, rn, L.S, L.K, ns);
-        rg = resp_geo(rn, L.K);
-        numR = LC.maxRedundantLocal;
-    } else {
-        int64_t bt = 0, bi = 0;
-        uint32_t bs = 0;
-#pragma unroll
-        for (int i = 0; i < A; ++i) {
-            if ((L.pvalid >> i) & 1u) {
-                const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
-                const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
-                const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
-                if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
-            }
-        }
-        uint32_t tag = 0, geo = 0, boff = 0;
-#pragma unroll
-        for (int i = 0; i < A; ++i)
-            if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; }
-        if (!(tag & 0x80000000u) && !getres.ready(e)) return false;
-        L.pvalid &= ~(1u << e);
-        L.now = bt;
-        if (tag & 0x80000000u) {
-            // BaseRpc timeout -> IterativeLookup::handleRpcTimeout (IterativeLookup.cc:588-654)
-            L.any_to = true;
-            resp = false;
-        } else {
-            // the responder's siblings flag and bucket geometry were captured at send (kad_send)
-            sb = (geo >> 24) & 1u;
-            rg = unpack_geo(geo, boff);
-            const bool acc = (LC.useAll && LC.merge) ? true : ((int)(tag & 0xFFFFu) == L.step);
-            // not accepted: handled as a timeout, its nodes are dropped
-            resp = acc || (sb && LC.acceptLateSiblings);
-        }
-    }
-    int num;
-    if (resp) {
-        if (!start) {
-            // IterativePathLookup::handleResponse (IterativeLookup.cc:803-921)
-            if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return true; }
-            if (r != L.S) {
-                record(L.hops, r);
-                ++L.hops;
-            }
-            ++L.step;
-            --L.pending;
-        }
-        if (LK && ns == 0 && start && sb) {
-            // an exact-key lookup of the source's own key (IterativeLookup::start 171-184)
-            L.result = L.S;
-            L.pfinished = true; L.psuccess = true;
-            return true;
-        }
-        getres.fill(e, r, rg, sb, numR, start, res);
-#ifdef OVS_DUP_FIND
-        {   // cost experiment (tools/diag): the responder's findNode evaluated a second time
-            K160 K2 = L.K;
-            asm volatile("" : "+v"(K2.w[0]));
-            Blk8 b2;
-            const int n2 = kad_find_node_blk<EX>(V, r, rg, K2, numR, sb, b2, ns);
-            uint32_t z = (uint32_t)n2;
-            for (int q = 0; q < 8; ++q) z ^= b2.x[q] ^ (uint32_t)b2.d[q] ^ (uint32_t)(b2.d[q] >> 32);
-            asm volatile("" :: "v"(z));
-        }
-#endif
-        if (LK && ns == 0 && !start && res.n > 0 && k_eq(node_key(V.nodes, res.idx[0]), L.K)) {
-            // the key's node is in the response (handleResponse 862-870): XOR distance 0, so first
-            L.result = res.idx[0];
-            L.pfinished = true; L.psuccess = true;
-            return true;
-        }
-#ifdef OVS_DUP_MERGE
-        {   // cost experiment: the LookupVector merge a second time, on a copy
-            SVec<8> nh2 = L.nh;
-            asm volatile("" : "+v"(nh2.idx[0]));
-            const int k2 = nh_merge<EX>(nh2, res, LC.redundant, L.K, V.nodes);
-            uint32_t z = (uint32_t)k2 ^ nh2.used;
-            for (int q = 0; q < 8; ++q) z ^= nh2.idx[q] ^ (uint32_t)nh2.d[q] ^ (uint32_t)(nh2.d[q] >> 32);
-            asm volatile("" :: "v"(z));
-        }
-#endif
-        int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
-        if (LC.numSiblings != 0 && sb && res.n > 0) {
-            if (L.result == NONE) L.result = res.idx[0];
-            L.pfinished = true; L.psuccess = true;
-            return true;
-        }
-        if (numNew == 0 && LC.newOnResp) numNew = 1;
-        num = start ? LC.alpha : min(numNew, LC.alpha);
-    } else {
-        // IterativePathLookup::handleTimeout (IterativeLookup.cc:935-1023), failedNodeRpcs = false
-        --L.pending;
-        if (L.now > DC.lookupTimeout) { L.pfinished = true; L.psuccess = false; return true; }
-        if (LC.newOnTimeout) num = 1;
-        else if (L.pending == 0) num = LC.alpha;
-        else return true;
-    }
-    kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, on);
-    return true;
-}
-
 // ---------------------------------------------------------------------------
-// The same state machine in phases, for kernels that evaluate the sibling-zone findNode
+// The state machine in phases, for kernels that evaluate the sibling-zone findNode
 // cooperatively across the wave (K2 k_kad_route, its shard step):
 //   kad_event_begin      per lane: pick the earliest event, account for it; tells whether a
 //                        findNode result is needed (KEV_FIND), only sends follow (KEV_SENDS),
@@ -921,6 +820,7 @@ struct KadEv {
     int e;             // pending slot of the event (-1 at start)
     int numR;          // numRedundantNodes of the findNode
     int num;           // KEV_SENDS: RPCs to send
+    int pre;           // sibling-row prefix a sibling-zone findNode reads (kad_sib_prefix)
     bool start;
     __device__ __forceinline__ bool sb() const { return (geo >> 24) & 1u; }
     __device__ __forceinline__ RespGeo rg() const { return unpack_geo(geo, boff); }
@@ -939,15 +839,18 @@ __device__ __forceinline__ int kad_event_begin(KadLookup<A>& L, const KadView& V
     ev.e = -1;
     ev.numR = LC.redundant;
     ev.num = 0;
+    ev.pre = 0;
     ev.start = !L.started;
     bool resp = true;
     if (ev.start) {
         L.started = true;
         const KadNode rn = load_node(V.nodes, L.S);
         const RespGeo g = resp_geo(rn, L.K);
-        ev.geo = pack_geo(g, kad_is_sibling(V, rn, L.S, L.K, ns));
+        const bool sb = kad_is_sibling(V, rn, L.S, L.K, ns);
+        ev.geo = pack_geo(g, sb);
         ev.boff = g.boff;
         ev.numR = LC.maxRedundantLocal;
+        ev.pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, min(sb ? (ns ? ns : 1) : ev.numR, 8)) : 0;
     } else {
         int e = -1;
         int64_t bt = 0, bi = 0;
@@ -955,16 +858,22 @@ __device__ __forceinline__ int kad_event_begin(KadLookup<A>& L, const KadView& V
 #pragma unroll
         for (int i = 0; i < A; ++i) {
             if ((L.pvalid >> i) & 1u) {
-                const int64_t ti = L.p[i].t - (int64_t)L.p[i].dins;
+                const int64_t t = L.p[i].t & PEND_TMASK;
+                const int64_t ti = t - (int64_t)L.p[i].dins;
                 const uint32_t si = (L.p[i].tag >> 16) & 0x7FFFu;
-                const bool better = e < 0 || L.p[i].t < bt || (L.p[i].t == bt && (ti < bi || (ti == bi && si < bs)));
-                if (better) { e = i; bt = L.p[i].t; bi = ti; bs = si; }
+                const bool better = e < 0 || t < bt || (t == bt && (ti < bi || (ti == bi && si < bs)));
+                if (better) { e = i; bt = t; bi = ti; bs = si; }
             }
         }
         uint32_t r = 0, tag = 0, geo = 0, boff = 0;
+        int pre = 0;
 #pragma unroll
         for (int i = 0; i < A; ++i)
-            if (i == e) { r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff; }
+            if (i == e) {
+                r = L.p[i].node; tag = L.p[i].tag; geo = L.p[i].geo; boff = L.p[i].boff;
+                pre = (int)((uint64_t)L.p[i].t >> 56);
+            }
+        ev.pre = pre;
         if (!(tag & 0x80000000u) && !ready(e, r)) return KEV_WAIT;
         ev.r = r;
         ev.e = e;
@@ -1022,6 +931,16 @@ __device__ __forceinline__ int kad_event_after_find(KadLookup<A>& L, const KadVi
         L.pfinished = true; L.psuccess = true;
         return -1;
     }
+#ifdef OVS_DUP_MERGE
+    {   // cost experiment: the LookupVector merge a second time, on a copy
+        SVec<8> nh2 = L.nh;
+        asm volatile("" : "+v"(nh2.idx[0]));
+        const int k2 = nh_merge<EX>(nh2, res, LC.redundant, L.K, V.nodes);
+        uint32_t z = (uint32_t)k2 ^ nh2.used;
+        for (int q = 0; q < 8; ++q) z ^= nh2.idx[q] ^ (uint32_t)nh2.d[q] ^ (uint32_t)(nh2.d[q] >> 32);
+        asm volatile("" :: "v"(z));
+    }
+#endif
     int numNew = nh_merge<EX>(L.nh, res, LC.redundant, L.K, V.nodes);
     if (LC.numSiblings != 0 && ev.sb() && res.n > 0) {
         if (L.result == NONE) L.result = res.idx[0];
@@ -1105,25 +1024,31 @@ __device__ __forceinline__ void wave_lds_sync()
 // the owner.  Up to 8 findNodes per pass.
 template <bool EX>
 __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, uint32_t c, uint32_t geo, uint32_t boff,
-                                                 const K160& K, CoopLds& S)
+                                                 int pre, const K160& K, CoopLds& S)
 {
     const uint64_t tasks = __ballot(want);
     if (tasks == 0) return;
+#ifndef OVS_COOP_G
+#define OVS_COOP_G 4
+#endif
+    constexpr int G = OVS_COOP_G;           // lanes per findNode
+    constexpr int LG = G == 8 ? 3 : G == 4 ? 2 : 1;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int T = __popcll(tasks);
-    const int grp = lane >> 3, j = lane & 7;
-    for (int p = 0; p * 8 < T; ++p) {
-        const int t = p * 8 + grp;
+    const int grp = lane >> LG, j = lane & (G - 1);
+    for (int p = 0; p * (64 / G) < T; ++p) {
+        const int t = p * (64 / G) + grp;
         const bool live = t < T;
         const int owner = live ? nth_set_bit(tasks, t) : lane;
         const uint32_t oc = __shfl(c, owner);
         const RespGeo og = unpack_geo(__shfl(geo, owner), __shfl(boff, owner));
+        const int opre = __shfl(pre, owner);
         K160 oK;
 #pragma unroll
         for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
         const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;
-        const int nsb = (og.nsib + KBLK - 1) / KBLK;
+        const int nsb = (opre + KBLK - 1) / KBLK;     // the level-sorted row's prefix that matters
         const int nitems = live ? nmain + nsb + 1 : 0;
         auto load_item = [&](int i, Blk8& b) -> int {
             if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
@@ -1142,7 +1067,7 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
         } else {
             blk_clear(acc);
         }
-        for (int i = j + 8; i < nitems; i += 8) {   // more than 8 items: explicit tables with 5s > 48
+        for (int i = j + G; i < nitems; i += G) {   // more than G items
             Blk8 b;
             const int bc = load_item(i, b);
             blk_sort8<false, EX>(b, oK, V.nodes);
@@ -1151,7 +1076,7 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
         }
         // butterfly: after step w every lane holds the top 8 of its aligned 2w lanes
 #pragma unroll
-        for (int w = 1; w < 8; w <<= 1) {
+        for (int w = 1; w < G; w <<= 1) {
             coop_put(S.acc, tid, acc);
             S.cnt[tid] = (uint32_t)cnt;
             wave_lds_sync();
@@ -1257,7 +1182,9 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
 // the lookup configurations the K2 state machine implements (others: OVS_ENOTSUP)
 inline bool kad_params_supported(const ovs_params& P, const KadTables& t)
 {
-    return P.lookupParallelRpcs >= 1 && P.lookupParallelRpcs <= MAXA && P.lookupRedundantNodes >= 1 &&
+    // event times of a lookup stay below 2^55 ns (Pend packs a 7-bit field above bit 56)
+    const bool times_fit = P.lookupTimeout >= 0 && P.rpcUdpTimeout >= 0 && P.lookupTimeout + 2 * P.rpcUdpTimeout < 3.0e7;
+    return times_fit && P.lookupParallelRpcs >= 1 && P.lookupParallelRpcs <= MAXA && P.lookupRedundantNodes >= 1 &&
            P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings >= 0 &&
            P.numSiblings <= t.s && P.numSiblings <= 8 &&
            t.k <= 8 && P.hopCountMax <= 0x7FFF;

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
         // phase 1 (per lane): the earliest event up to its findNode
         int ph = KEV_IDLE;
         KadEv ev;
-        ev.r = 0; ev.geo = 0; ev.boff = 0; ev.e = 0; ev.num = 0; ev.numR = 0; ev.start = false;
+        ev.r = 0; ev.geo = 0; ev.boff = 0; ev.e = 0; ev.num = 0; ev.numR = 0; ev.pre = 0; ev.start = false;
         bool coop = false;
         if (active && !dead && !kad_lookup_done(L)) {
             const HopRecorder<RECORD> rec{io.hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
@@ -193,8 +193,14 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
         // tie fallbacks in the cooperative merge made the register allocator emit misaligned
         // 96-bit spills that gfx950 rejects.
 #ifndef OVS_NOCOOP
-        if constexpr (!EX) kad_coop_sibzone<EX>(V, coop, ev.r, ev.geo, ev.boff, L.K, lds);
-        else coop = false;
+        if constexpr (!EX) {
+            kad_coop_sibzone<EX>(V, coop, ev.r, ev.geo, ev.boff, ev.pre, L.K, lds);
+#ifdef OVS_DUP_COOP
+            kad_coop_sibzone<EX>(V, coop, ev.r, ev.geo, ev.boff, ev.pre, L.K, lds);   // cost experiment
+#endif
+        } else {
+            coop = false;
+        }
 #else
         coop = false;
 #endif
@@ -213,7 +219,10 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
                 Blk8 fb;
                 if (coop) {
                     coop_get(lds.res, threadIdx.x, fb);
-                    n = kad_coop_finish<EX>(V, ev.rg(), L.K, ev.numR, ev.sb(), ns, fb, (int)lds.rcnt[threadIdx.x]);
+                    // the candidates findNode saw: the row entries past the prefix's blocks count too
+                    const RespGeo g = ev.rg();
+                    const int rd = min(g.nsib, KBLK * ((ev.pre + KBLK - 1) / KBLK));
+                    n = kad_coop_finish<EX>(V, g, L.K, ev.numR, ev.sb(), ns, fb, (int)lds.rcnt[threadIdx.x] + g.nsib - rd);
                 } else if (SHARD && !(ev.r >= V.lo && ev.r < V.hi)) {
                     // the owner's answer, delivered by k_kad_shard_deliver
                     const KadRes& rr = io.res[q * A + ev.e];
@@ -222,6 +231,17 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
                     for (int k = 0; k < 8; ++k) { fb.x[k] = k < n ? rr.nodes[k] : NONE; fb.d[k] = k < n ? rr.dist[k] : ~0ull; }
                 } else {
                     n = kad_find_node_blk<EX>(V, ev.r, ev.rg(), L.K, ev.numR, ev.sb(), fb, ns);
+#ifdef OVS_DUP_LANEFIND
+                    {   // cost experiment: the per-lane findNode again
+                        K160 K2 = L.K;
+                        asm volatile("" : "+v"(K2.w[0]));
+                        Blk8 b2;
+                        const int n2 = kad_find_node_blk<EX>(V, ev.r, ev.rg(), K2, ev.numR, ev.sb(), b2, ns);
+                        uint32_t z = (uint32_t)n2;
+                        for (int k = 0; k < 8; ++k) z ^= b2.x[k] ^ (uint32_t)b2.d[k] ^ (uint32_t)(b2.d[k] >> 32);
+                        asm volatile("" :: "v"(z));
+                    }
+#endif
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) { res.idx[k] = fb.x[k]; res.d[k] = fb.d[k]; }
