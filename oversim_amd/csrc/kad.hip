@@ -72,7 +72,7 @@ __device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2*
 // snapshot pass A: sibling table (the 5s XOR-closest nodes, what routingAdd converges to:
 // Kademlia.cc:537-616) and the node summary; the row length for the owned arc
 __global__ void k_kad_siblings(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t n, int S5,
-                               uint32_t own_lo, uint32_t own_hi, uint32_t* __restrict__ sib,
+                               int bpb, uint32_t own_lo, uint32_t own_hi, uint32_t* __restrict__ sib,
                                KadNode* __restrict__ out, KadX* __restrict__ ox, uint64_t* __restrict__ rowlen)
 {
     const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -129,7 +129,7 @@ __global__ void k_kad_siblings(const KeyRec* __restrict__ recs, const double2* _
         end = cnt > 0 ? k_msb(R) : -1;
     }
     kad_node_summary(recs, xy, v, L, cnt, end, out, ox);
-    rowlen[v] = (v >= own_lo && v < own_hi && end >= 0) ? (uint64_t)(KEYBITS - end) : 0;
+    rowlen[v] = (v >= own_lo && v < own_hi && end >= 0) ? (uint64_t)(KEYBITS - end) * (uint64_t)bpb : 0;
 }
 
 // 1 when two node IDs share their top 63 bits (then top-64 XOR distances of distinct nodes can
@@ -193,12 +193,13 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     uint32_t lo = 0, hi = n;
-    uint32_t chosen[KBLK];
+    uint32_t chosen[KMAX];
+    const int bpb = (k + KBLK - 1) / KBLK;
     for (int m = KEYBITS - 1; m >= endIndex; --m) {
         const uint32_t mid = split_bit(recs, lo, hi, m);
         const uint32_t nb = kbit(me, m);
         const uint32_t flo = nb ? lo : mid, fhi = nb ? mid : hi;
-        const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m);
+        const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
         uint32_t nsin = 0;
         for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
         const uint32_t c = (fhi - flo) - nsin;
@@ -233,7 +234,7 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
                 ++rank;
             }
         }
-        for (int q = outn; q < KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);
+        for (int q = outn; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);
         lo = nb ? mid : lo;
         hi = nb ? hi : mid;
     }
@@ -291,7 +292,7 @@ __global__ void k_kad_explicit_nodes(const KeyRec* __restrict__ recs, const doub
     const int end = cnt > 0 ? k_msb(R) : -1;
     const int rowlo = end < 0 ? lowest : (lowest >= 0 && lowest < end ? lowest : end);
     kad_node_summary(recs, xy, v, L, cnt, rowlo, out, ox);
-    rowlen[v] = rowlo >= 0 ? (uint64_t)(KEYBITS - rowlo) : 0;
+    rowlen[v] = rowlo >= 0 ? (uint64_t)(KEYBITS - rowlo) * (uint64_t)((k + KBLK - 1) / KBLK) : 0;
     if (cnt + 1 < 8) atomicOr(short_flag, 1u);
 }
 
@@ -308,11 +309,12 @@ __global__ void k_kad_explicit_rows(const KeyRec* __restrict__ recs, const KadNo
     put_sibling_row(blks, sib_base + (uint64_t)v * sbn, sbn, L, S5, kload(recs, v), recs);
     const int rowlo = kad_rowlo(r.meta);
     if (rowlo < 0) return;
+    const int bpb = (k + KBLK - 1) / KBLK;
     for (int m = KEYBITS - 1; m >= rowlo; --m) {
-        const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m);
+        const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
         const int c = bcount[(uint64_t)v * KEYBITS + m];
         const uint32_t* B = bnodes + ((uint64_t)v * KEYBITS + m) * k;
-        for (int q = 0; q < KBLK; ++q) put_entry(blks, blk0, q, q < c ? B[q] : NONE, recs);
+        for (int q = 0; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, q < c ? B[q] : NONE, recs);
     }
 }
 
@@ -329,9 +331,10 @@ __global__ void k_kad_export(const KadNode* __restrict__ nodes, const KadBlk* __
     uint32_t* o = bnodes + t * k;
     for (int q = 0; q < k; ++q) o[q] = NONE;
     if (rowlo >= 0 && m >= rowlo) {
-        const KadBlk* b = blks + (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m);
+        const int bpb = (k + KBLK - 1) / KBLK;
+        const KadBlk* b = blks + (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
         for (int q = 0; q < k; ++q) {
-            const uint32_t x = b->idx[q];
+            const uint32_t x = b[q / KBLK].idx[q % KBLK];
             if (x == NONE) break;
             o[c++] = x;
         }
@@ -404,7 +407,9 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     if (hi > n) hi = n;
     if (lo >= hi) return hipErrorInvalidValue;
     t.k = k; t.s = s; t.seed = seed; t.lo = lo; t.hi = hi; t.snapshot = 1; t.maybe_short = 0;
-    if (k < 1 || k > KBLK) return hipErrorNotSupported;
+    if (k < 1 || k > KMAX) return hipErrorNotSupported;
+    const int bpb = (k + KBLK - 1) / KBLK;
+    t.bpb = bpb;
     const int S5 = 5 * s, sbn = (S5 + KBLK - 1) / KBLK;
     const uint32_t nown = hi - lo;
     uint64_t *rowlen = nullptr, *off = nullptr;
@@ -424,7 +429,7 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     if ((e = hipMalloc(&sib_all, sizeof(uint32_t) * (uint64_t)n * S5)) != hipSuccess) return e;
     if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (n + 1))) != hipSuccess) { cleanup(); return e; }
     if ((e = hipMalloc(&off, sizeof(uint64_t) * (n + 1))) != hipSuccess) { cleanup(); return e; }
-    hipLaunchKernelGGL(k_kad_siblings, dim3(nblk(n, 128)), dim3(128), 0, st, recs, xy, n, S5, lo, hi, sib_all,
+    hipLaunchKernelGGL(k_kad_siblings, dim3(nblk(n, 128)), dim3(128), 0, st, recs, xy, n, S5, bpb, lo, hi, sib_all,
                        t.nodes, t.nodex, rowlen);
     hipMemsetAsync(rowlen + n, 0, sizeof(uint64_t), st);
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, rowlen, off, n + 1, st);
@@ -461,7 +466,8 @@ hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n,
     hipError_t e;
     kad_free(t);
     t.k = k; t.s = s; t.seed = 0; t.lo = 0; t.hi = n; t.snapshot = 0;
-    if (k < 1 || k > KBLK) return hipErrorNotSupported;
+    if (k < 1 || k > KMAX) return hipErrorNotSupported;
+    t.bpb = (k + KBLK - 1) / KBLK;
     const int S5 = 5 * s, sbn = (S5 + KBLK - 1) / KBLK;
     uint64_t *rowlen = nullptr, *off = nullptr;
     uint32_t* flags = nullptr;

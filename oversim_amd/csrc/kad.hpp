@@ -6,9 +6,10 @@
 //                     once per RPC when the call is sent
 //  KadX    nodex[n]   the exact sibling radius R and level mask (fallback on summary ties, rare)
 //  KadBlk  blks[]     bucket rows and sibling rows as 96 B blocks of 8 entries (top 64 bits of the
-//                     member key, member index): bucket m of node v = blks[nodes[v].boff + 159 - m]
-//                     for m = rowlo(v) .. 159 (one block = one k <= 8 bucket, two lines); sibling
-//                     row of an owned node v = ceil(5s/8) blocks at sib_base + (v - lo) * sbn
+//                     member key, member index): bucket m of node v = the bpb = ceil(k/8) blocks at
+//                     blks[nodes[v].boff + (159 - m) * bpb] for m = rowlo(v) .. 159 (k <= 8: one block,
+//                     two lines; KademliaLarge's k = 16: two); sibling row of an owned node v =
+//                     ceil(5s/8) blocks at sib_base + (v - lo) * sbn, in ascending level msb(x ^ v)
 //  uint8_t slev[n*5s] one arc of a sharded network: the level msb(x ^ v) of each sibling x of every
 //                     node v (5s bytes a node), so a LookupCall decides isSiblingFor(numSiblings > 1)
 //                     of any responder on its home rank
@@ -41,7 +42,8 @@ struct KadX {
     uint32_t mask[5];
 };
 
-constexpr int KBLK = 8;   // entries per block (= the largest bucket the route kernel takes, k <= 8)
+constexpr int KBLK = 8;   // entries per block; a bucket of k entries takes bpb = ceil(k / 8) blocks (k <= 16)
+constexpr int KMAX = 16;  // largest bucket size k (and findNode result) the engine implements
 struct alignas(32) KadBlk {
     uint64_t top[KBLK];    // top 64 bits (bits 96..159) of the member key; ~0 for an empty entry
     uint32_t idx[KBLK];    // member node index; NONE for an empty entry (entries packed at the front)
@@ -62,6 +64,7 @@ struct KadTables {
                                    // isSiblingFor(numSiblings > 1) of a responder off the owned arc
     uint32_t lo = 0, hi = 0;       // sibling / bucket rows exist for nodes [lo, hi) (the whole network unsharded)
     int k = 8, s = 8;
+    int bpb = 1;                   // blocks per bucket, ceil(k / 8)
     uint64_t seed = 0;
     int exact = 1;                 // two IDs share their top 63 bits: comparisons use the 160-bit tie fallback
     int snapshot = 1;              // 0: explicit tables (ovs_kad_load_tables)
@@ -77,6 +80,7 @@ struct KadView {
     const double2* __restrict__ xy;
     uint32_t n;
     int k;
+    int bpb;      // blocks per bucket
     int S5;       // sibling table capacity 5s
     int sbn;      // blocks per sibling row = ceil(5s / 8)
     uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)

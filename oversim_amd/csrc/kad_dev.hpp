@@ -157,14 +157,16 @@ __device__ __forceinline__ void svec_clear(SVec<CAP>& v)
 // network and merged into the running top 8 with a bitonic merge (8 min + 12 comparators).
 // Empty entries are (~0, NONE) and sort last.
 
-struct Blk8 {
-    uint64_t d[8];
-    uint32_t x[8];
-    uint32_t f[8];     // payload flags (LookupVector merge: bit 0 alreadyUsed, bit 1 from the response)
+template <int C>
+struct BlkN {
+    uint64_t d[C];
+    uint32_t x[C];
+    uint32_t f[C];     // payload flags (LookupVector merge: bit 0 alreadyUsed, bit 1 from the response)
 };
+using Blk8 = BlkN<8>;
 
-template <bool F, bool EX>
-__device__ __forceinline__ void blk_ce(Blk8& b, int i, int j, const K160& K, const KadNode* __restrict__ nodes)
+template <bool F, bool EX, int C>
+__device__ __forceinline__ void blk_ce(BlkN<C>& b, int i, int j, const K160& K, const KadNode* __restrict__ nodes)
 {
     const bool s = cand_lt<EX>(b.d[j], b.x[j], b.d[i], b.x[i], K, nodes);
     const uint64_t di = s ? b.d[j] : b.d[i], dj = s ? b.d[i] : b.d[j];
@@ -188,27 +190,55 @@ __device__ __forceinline__ void blk_sort8(Blk8& b, const K160& K, const KadNode*
     blk_ce<F, EX>(b, 1, 2, K, nodes); blk_ce<F, EX>(b, 3, 4, K, nodes); blk_ce<F, EX>(b, 5, 6, K, nodes);
 }
 
-// a <- the 8 smallest of sorted a and sorted b, sorted
+// a <- the C smallest of sorted a (C entries) and sorted b (CB <= C entries, as if padded with empty
+// ones), sorted: a against reversed b is bitonic, then half-cleaners at C/2 .. 1
+template <bool F, bool EX, int C, int CB>
+__device__ __forceinline__ void blk_merge_top(BlkN<C>& a, const BlkN<CB>& b, const K160& K,
+                                              const KadNode* __restrict__ nodes)
+{
+    static_assert(CB <= C, "merge a smaller block into a larger vector");
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+        const int j = C - 1 - i;
+        if (j < CB) {
+            const bool s = cand_lt<EX>(b.d[j], b.x[j], a.d[i], a.x[i], K, nodes);
+            a.d[i] = s ? b.d[j] : a.d[i];
+            a.x[i] = s ? b.x[j] : a.x[i];
+            if (F) a.f[i] = s ? b.f[j] : a.f[i];
+        }
+    }
+#pragma unroll
+    for (int w = C / 2; w >= 1; w >>= 1) {
+#pragma unroll
+        for (int i = 0; i < C; ++i)
+            if ((i & w) == 0) blk_ce<F, EX>(a, i, i + w, K, nodes);
+    }
+}
+
+// a <- the 8 smallest of sorted a and sorted b, sorted (8 min + 12 comparators)
 template <bool F, bool EX>
 __device__ __forceinline__ void blk_merge_top8(Blk8& a, const Blk8& b, const K160& K, const KadNode* __restrict__ nodes)
 {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const bool s = cand_lt<EX>(b.d[7 - i], b.x[7 - i], a.d[i], a.x[i], K, nodes);
-        a.d[i] = s ? b.d[7 - i] : a.d[i];
-        a.x[i] = s ? b.x[7 - i] : a.x[i];
-        if (F) a.f[i] = s ? b.f[7 - i] : a.f[i];
-    }
-    // a is bitonic: half-cleaners at distance 4, 2, 1
-    blk_ce<F, EX>(a, 0, 4, K, nodes); blk_ce<F, EX>(a, 1, 5, K, nodes); blk_ce<F, EX>(a, 2, 6, K, nodes); blk_ce<F, EX>(a, 3, 7, K, nodes);
-    blk_ce<F, EX>(a, 0, 2, K, nodes); blk_ce<F, EX>(a, 1, 3, K, nodes); blk_ce<F, EX>(a, 4, 6, K, nodes); blk_ce<F, EX>(a, 5, 7, K, nodes);
-    blk_ce<F, EX>(a, 0, 1, K, nodes); blk_ce<F, EX>(a, 2, 3, K, nodes); blk_ce<F, EX>(a, 4, 5, K, nodes); blk_ce<F, EX>(a, 6, 7, K, nodes);
+    blk_merge_top<F, EX, 8, 8>(a, b, K, nodes);
 }
 
-__device__ __forceinline__ void blk_clear(Blk8& b)
+template <int C>
+__device__ __forceinline__ void blk_clear(BlkN<C>& b)
 {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { b.d[i] = ~0ull; b.x[i] = NONE; b.f[i] = 0; }
+    for (int i = 0; i < C; ++i) { b.d[i] = ~0ull; b.x[i] = NONE; b.f[i] = 0; }
+}
+
+// a <- sorted 8-block b (the rest of a empty)
+template <int C>
+__device__ __forceinline__ void blk_assign(BlkN<C>& a, const Blk8& b)
+{
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+        a.d[i] = i < 8 ? b.d[i < 8 ? i : 0] : ~0ull;
+        a.x[i] = i < 8 ? b.x[i < 8 ? i : 0] : NONE;
+        a.f[i] = i < 8 ? b.f[i < 8 ? i : 0] : 0u;
+    }
 }
 
 // the (up to 8) entries of one table block, unsorted; returns how many
@@ -234,11 +264,12 @@ __device__ __forceinline__ int blk_load_block(Blk8& b, const KadBlk* __restrict_
 }
 
 // keep the first cap entries; returns how many are non-empty
-__device__ __forceinline__ int blk_trunc(Blk8& b, int cap)
+template <int C>
+__device__ __forceinline__ int blk_trunc(BlkN<C>& b, int cap)
 {
     int n = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < C; ++i) {
         if (i >= cap) { b.x[i] = NONE; b.d[i] = ~0ull; b.f[i] = 0; }
         n += b.x[i] != NONE ? 1 : 0;
     }
@@ -338,18 +369,19 @@ __device__ __forceinline__ RespGeo resp_geo(const KadNode& r, const K160& K)
     return g;
 }
 
+// the first of the V.bpb blocks of bucket `bucket` of a node whose row starts at boff
 __device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t boff, int bucket)
 {
-    return V.blks + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - bucket);
+    return V.blks + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - bucket) * (uint64_t)V.bpb;
 }
 
 // Kademlia::findNode(key, numRedundantNodes, numSiblings) at node c (Kademlia.cc:1101-1246),
 // block form: the candidate sets of the reference's scan (bucket m, then buckets m-1..endIndex with
 // the sibling table and self when m >= endIndex or the result is short, then buckets above m while
-// it is short) merged one table line at a time.  Returns the result size.
-template <bool EX>
+// it is short) merged one table block at a time into the top C.  Returns the result size.
+template <bool EX, int C = 8>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
-                                                 int numRedundant, bool sib, Blk8& res, int numSiblings = 1)
+                                                 int numRedundant, bool sib, BlkN<C>& res, int numSiblings = 1)
 {
     blk_clear(res);
     if (V.err && kad_off_arc(V, c)) {
@@ -368,49 +400,25 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     }
     // resultSize = numSiblings (1 for 0) when c is a sibling for K, else numRedundantNodes (Kademlia.cc:1127-1131)
     const int rs = sib ? (numSiblings ? numSiblings : 1) : numRedundant;
-    const int cap = rs < 8 ? rs : 8;
+    const int cap = rs < C ? rs : C;
     int n = 0, seen = 0;
     auto add_blk = [&](const KadBlk* blk) {
         Blk8 b;
         const int cnt = blk_load_block(b, blk, K);
-#ifdef OVS_KAD_STATS
-        atomicAdd(&g_kad_stats[1], 1ull);
-#endif
         if (cnt) {
             blk_sort8<false, EX>(b, K, V.nodes);
-            if (seen == 0) {
-                res = b;          // into an empty result the merge is the sorted block itself
-            } else {
-                blk_merge_top8<false, EX>(res, b, K, V.nodes);
-            }
+            if (seen == 0) blk_assign(res, b);       // into an empty result the merge is the sorted block itself
+            else blk_merge_top<false, EX, C, 8>(res, b, K, V.nodes);
             n = blk_trunc(res, cap);
             seen += cnt;
         }
     };
     auto add_slot = [&](int bucket) {
         if (g.rowlo < 0 || bucket < g.rowlo) return;      // buckets below the stored row are empty
-        add_blk(slot_blk(V, g.boff, bucket));
+        const KadBlk* blk = slot_blk(V, g.boff, bucket);
+        for (int j = 0; j < V.bpb; ++j) add_blk(blk + j);
     };
-#ifdef OVS_KAD_STATS
-    atomicAdd(&g_kad_stats[0], 1ull);
-    if (g.m <= g.endIndex) atomicAdd(&g_kad_stats[2], 1ull);
-#endif
     if (g.m >= 0) add_slot(g.m);
-#ifdef OVS_DUP_MAIN
-    if (g.m >= 0 && g.rowlo >= 0 && g.m >= g.rowlo) {   // cost experiment: the main block again
-        K160 K2 = K;
-        asm volatile("" : "+v"(K2.w[0]));
-        Blk8 b2;
-        const int c2 = blk_load_block(b2, slot_blk(V, g.boff, g.m), K2);
-        blk_sort8<false, EX>(b2, K2, V.nodes);
-        uint32_t z = (uint32_t)c2;
-        for (int q = 0; q < 8; ++q) z ^= b2.x[q] ^ (uint32_t)b2.d[q] ^ (uint32_t)(b2.d[q] >> 32);
-        asm volatile("" :: "v"(z));
-    }
-#endif
-#ifdef OVS_KAD_STATS
-    if (g.m > g.endIndex && seen < rs) atomicAdd(&g_kad_stats[3], 1ull);
-#endif
     // Members of bucket m are XOR-closer to K than everything below it (buckets < m, siblings --
     // all at msb <= endIndex < m from c -- and c itself all differ from K at bit m): once bucket
     // m fills the result, the rest of the scan cannot change it
@@ -418,28 +426,11 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
         const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
         for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
-#ifdef OVS_DUP_EXT
-        {   // cost experiment: the sibling-row scan again
-            K160 K2 = K;
-            asm volatile("" : "+v"(K2.w[0]));
-            Blk8 r2;
-            blk_clear(r2);
-            for (int j = 0; j * KBLK < g.nsib; ++j) {
-                Blk8 b2;
-                blk_load_block(b2, L + j, K2);
-                blk_sort8<false, EX>(b2, K2, V.nodes);
-                blk_merge_top8<false, EX>(r2, b2, K2, V.nodes);
-            }
-            uint32_t z = 0;
-            for (int q = 0; q < 8; ++q) z ^= r2.x[q] ^ (uint32_t)r2.d[q] ^ (uint32_t)(r2.d[q] >> 32);
-            asm volatile("" :: "v"(z));
-        }
-#endif
         Blk8 self;
         blk_clear(self);
         self.x[0] = c;
         self.d[0] = dist_hi(node_key(V.nodes, c), K);
-        blk_merge_top8<false, EX>(res, self, K, V.nodes);
+        blk_merge_top<false, EX, C, 8>(res, self, K, V.nodes);
         n = blk_trunc(res, cap);
         seen += 1;
     }
@@ -475,7 +466,7 @@ __device__ __forceinline__ int svec_add(SVec<CAP>& v, int cap, uint32_t x, uint6
     return pos;
 }
 
-// findNode for results of up to CAP (> 8) nodes, one insertion per candidate: the batch ABI
+// findNode for results of up to CAP nodes, one insertion per candidate: the batch ABI
 // (ovs_find_node_batch accepts numRedundantNodes / numSiblings up to 16); same scan as
 // kad_find_node_blk
 template <int CAP, bool EX>
@@ -501,7 +492,8 @@ __device__ __forceinline__ int kad_find_node_ins(const KadView& V, uint32_t c, c
     };
     auto add_slot = [&](int bucket) {
         if (g.rowlo < 0 || bucket < g.rowlo) return;
-        add_blk(slot_blk(V, g.boff, bucket));
+        const KadBlk* blk = slot_blk(V, g.boff, bucket);
+        for (int j = 0; j < V.bpb; ++j) add_blk(blk + j);
     };
     if (g.m >= 0) add_slot(g.m);
     if ((g.m >= g.endIndex || seen < rs) && !(g.m > g.endIndex && res.n >= cap)) {   // as kad_find_node_blk
@@ -520,14 +512,14 @@ __device__ __forceinline__ int kad_find_node_ins(const KadView& V, uint32_t c, c
 // with their nodes.  Returns numNewRpcs: response nodes that entered nh (a response node the
 // reference inserts at a position < cap can never be pushed out again by the later, farther
 // response nodes, so "inserted" and "in the final vector" coincide).
-template <bool EX>
-__device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap, const K160& K,
+template <bool EX, int C>
+__device__ __forceinline__ int nh_merge(SVec<C>& nh, const SVec<C>& res, int cap, const K160& K,
                                         const KadNode* __restrict__ nodes)
 {
-    Blk8 a, b;
+    BlkN<C> a, b;
     bool dup = false;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < C; ++i) {
         const bool ina = i < nh.n;
         a.x[i] = ina ? nh.idx[i] : NONE;
         a.d[i] = ina ? nh.d[i] : ~0ull;
@@ -538,20 +530,31 @@ __device__ __forceinline__ int nh_merge(SVec<8>& nh, const SVec<8>& res, int cap
         b.f[i] = 2u;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < C; ++j) {
         bool dj = false;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dj |= (b.x[j] != NONE && b.x[j] == a.x[i]);
+        for (int i = 0; i < C; ++i) dj |= (b.x[j] != NONE && b.x[j] == a.x[i]);
         if (dj) { b.x[j] = NONE; b.d[j] = ~0ull; }
         dup |= dj;
     }
-    if (dup) blk_sort8<false, EX>(b, K, nodes);    // holes to the end (every b flag is 2: nothing to carry)
-    blk_merge_top8<true, EX>(a, b, K, nodes);
+    if (dup) {
+        // holes to the end (every b flag is 2: nothing to carry)
+        if constexpr (C == 8) {
+            blk_sort8<false, EX>(b, K, nodes);
+        } else {
+            // a sorted vector with holes stays sorted when the holes move back one place at a time
+#pragma unroll
+            for (int r = 0; r < C; ++r)
+#pragma unroll
+                for (int i = r & 1; i + 1 < C; i += 2) blk_ce<false, EX>(b, i, i + 1, K, nodes);
+        }
+    }
+    blk_merge_top<true, EX, C, C>(a, b, K, nodes);
     const int n = blk_trunc(a, cap);
     int numNew = 0;
     uint32_t used = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < C; ++i) {
         nh.idx[i] = a.x[i];
         nh.d[i] = a.d[i];
         numNew += (a.x[i] != NONE && (a.f[i] & 2u)) ? 1 : 0;
@@ -567,34 +570,33 @@ template <int CAP, bool EX>
 __device__ __forceinline__ void kad_find_node_vec(const KadView& V, uint32_t c, const KadNode& r, const K160& K,
                                                   int numRedundant, bool sib, SVec<CAP>& res, int numSiblings = 1)
 {
-    static_assert(CAP == 8, "findNode results hold at most 8 nodes");
-    Blk8 b;
-    const int n = kad_find_node_blk<EX>(V, c, resp_geo(r, K), K, numRedundant, sib, b, numSiblings);
+    BlkN<CAP> b;
+    const int n = kad_find_node_blk<EX, CAP>(V, c, resp_geo(r, K), K, numRedundant, sib, b, numSiblings);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
+    for (int i = 0; i < CAP; ++i) { res.idx[i] = b.x[i]; res.d[i] = b.d[i]; }
     res.n = n;
     res.used = 0;
 }
 
 // The scan of kad_find_node_blk counted: only explicit tables with short sibling tables reach it
 // (inlined: an out-of-line call costs the lookup kernels more registers than the second copy)
-template <bool EX>
+template <bool EX, int C>
 __device__ __forceinline__ int kad_scan_size(KadView V, uint32_t c, RespGeo g, K160 K, int rs, int numSiblings)
 {
-    Blk8 b;
-    return kad_find_node_blk<EX>(V, c, g, K, rs, false, b, numSiblings);
+    BlkN<C> b;
+    return kad_find_node_blk<EX, C>(V, c, g, K, rs, false, b, numSiblings);
 }
 
 // The FindNodeResponse size of node c (its findNode result size): resultSize, unless explicit
 // tables leave c fewer candidates on its scan (then counted by running the scan)
-template <bool EX>
+template <bool EX, int C = 8>
 __device__ __forceinline__ int kad_response_size(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
                                                  int rs, bool sib, int numSiblings)
 {
     if (g.nsib == 0 || (sib && numSiblings <= 1)) return 1;
     const int full = rs < (int)V.n ? rs : (int)V.n;
     if (!V.maybe_short || g.nsib + 1 >= rs) return full;
-    return kad_scan_size<EX>(V, c, g, K, rs, numSiblings);
+    return kad_scan_size<EX, C>(V, c, g, K, rs, numSiblings);
 }
 
 // ---------------------------------------------------------------------------
@@ -661,15 +663,16 @@ __device__ __forceinline__ RespGeo unpack_geo(uint32_t geo, uint32_t boff)
     return g;
 }
 
-// per-lane lookup state (IterativeLookup + its single IterativePathLookup)
-template <int A>
+// per-lane lookup state (IterativeLookup + its single IterativePathLookup); C = the LookupVector's and
+// findNode's capacity (8; 16 for KademliaLarge's k = lookupRedundantNodes = 16)
+template <int A, int C = 8>
 struct KadLookup {
     K160 K;
     uint32_t S;
     double sx, sy;
     int64_t now, txf;
     uint32_t seq;
-    SVec<8> nh;            // LookupVector nextHops (cap redundantNodes), used bits = alreadyUsed
+    SVec<C> nh;            // LookupVector nextHops (cap redundantNodes), used bits = alreadyUsed
     Pend p[A];
     uint32_t pvalid;
     int step, hops, pending;
@@ -677,8 +680,8 @@ struct KadLookup {
     uint32_t result, nsent;
 };
 
-template <int A>
-__device__ __forceinline__ void kad_lookup_init(KadLookup<A>& L, const K160& K, uint32_t S,
+template <int A, int C>
+__device__ __forceinline__ void kad_lookup_init(KadLookup<A, C>& L, const K160& K, uint32_t S,
                                                 const double2* __restrict__ xy)
 {
     L.K = K;
@@ -697,8 +700,8 @@ __device__ __forceinline__ void kad_lookup_init(KadLookup<A>& L, const K160& K, 
 // FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
 // SimpleNodeEntry::calcDelay with the source's tx queue).  on(slot, x, isTimeout) is told which
 // pending-event slot the call occupies (the sharded path requests x's findNode result there).
-template <int A, bool EX, bool LK, class OnSend>
-__device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
+template <int A, bool EX, bool LK, class OnSend, int C>
+__device__ __forceinline__ void kad_send(KadLookup<A, C>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                          uint32_t x, const OnSend& on)
 {
     const KadNode rr = load_node(V.nodes, x);
@@ -719,7 +722,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     }
 #endif
     // the response carries findNode's result (Kademlia.cc:1127-1131 resultSize)
-    const int csz = kad_response_size<EX>(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
+    const int csz = kad_response_size<EX, C>(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
     const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
     const int64_t bwc = DC.bwCall;
     const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
@@ -736,7 +739,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
     const uint32_t sTo = L.seq++;
     const uint32_t sR = L.seq++;
     const uint32_t tag = (uint32_t)L.step | ((isTo ? sTo : sR) << 16) | (isTo ? 0x80000000u : 0u);
-    const int rcap = min(sb ? (ns ? ns : 1) : LC.redundant, 8);
+    const int rcap = min(sb ? (ns ? ns : 1) : LC.redundant, C);
     const int64_t pre = rg.m <= rg.endIndex ? (int64_t)kad_sib_prefix(rg, rr.spare, rcap) : 0;
     int slot = 0;
 #pragma unroll
@@ -759,8 +762,8 @@ __device__ __forceinline__ void kad_send(KadLookup<A>& L, const KadView& V, cons
 }
 
 // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
-template <int A, bool EX, bool LK, class OnSend>
-__device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
+template <int A, bool EX, bool LK, class OnSend, int C>
+__device__ __forceinline__ void kad_send_rpcs(KadLookup<A, C>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                               int num, const OnSend& on)
 {
     if (L.pfinished) return;
@@ -775,7 +778,7 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
         const int e = __ffs((int)unused) - 1;
         uint32_t h = NONE;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < C; ++j)
             if (j == e) h = L.nh.idx[j];
         // visitOnlyOnce: an unused entry can only be a visited node if it is the source
         if (!LC.visitOnlyOnce || h != L.S) {
@@ -789,8 +792,8 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A>& L, const KadView& V,
 }
 
 // checkStop (IterativeLookup.cc:295-349): the single path finished, or nothing pending
-template <int A>
-__device__ __forceinline__ bool kad_lookup_done(const KadLookup<A>& L)
+template <int A, int C>
+__device__ __forceinline__ bool kad_lookup_done(const KadLookup<A, C>& L)
 {
     return L.started && (L.pfinished || L.pvalid == 0);
 }
@@ -828,8 +831,8 @@ struct KadEv {
 
 // IterativeLookup::start / handleRpcResponse / handleRpcTimeout up to the findNode
 // (kad_lookup_event's first half).  ready(slot, node): the result of a response event is available.
-template <int A, bool EX, bool LK, class Ready, class Rec>
-__device__ __forceinline__ int kad_event_begin(KadLookup<A>& L, const KadView& V, const DelayConsts& DC,
+template <int A, bool EX, bool LK, class Ready, class Rec, int C>
+__device__ __forceinline__ int kad_event_begin(KadLookup<A, C>& L, const KadView& V, const DelayConsts& DC,
                                                const KadLC& LC, const Ready& ready, const Rec& record, KadEv& ev)
 {
     const int ns = LK ? LC.numSiblings : 1;
@@ -850,7 +853,7 @@ __device__ __forceinline__ int kad_event_begin(KadLookup<A>& L, const KadView& V
         ev.geo = pack_geo(g, sb);
         ev.boff = g.boff;
         ev.numR = LC.maxRedundantLocal;
-        ev.pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, min(sb ? (ns ? ns : 1) : ev.numR, 8)) : 0;
+        ev.pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, min(sb ? (ns ? ns : 1) : ev.numR, C)) : 0;
     } else {
         int e = -1;
         int64_t bt = 0, bi = 0;
@@ -920,9 +923,9 @@ __device__ __forceinline__ int kad_event_begin(KadLookup<A>& L, const KadView& V
 
 // the findNode answer for the response (kad_lookup_event's second half): numNew, the finish rules;
 // returns the RPCs to send, or -1 when the lookup finished
-template <int A, bool EX, bool LK>
-__device__ __forceinline__ int kad_event_after_find(KadLookup<A>& L, const KadView& V, const KadLC& LC, const KadEv& ev,
-                                                    const SVec<8>& res)
+template <int A, bool EX, bool LK, int C>
+__device__ __forceinline__ int kad_event_after_find(KadLookup<A, C>& L, const KadView& V, const KadLC& LC, const KadEv& ev,
+                                                    const SVec<C>& res)
 {
     const int ns = LK ? LC.numSiblings : 1;
     if (LK && ns == 0 && !ev.start && res.n > 0 && k_eq(node_key(V.nodes, res.idx[0]), L.K)) {
@@ -933,11 +936,11 @@ __device__ __forceinline__ int kad_event_after_find(KadLookup<A>& L, const KadVi
     }
 #ifdef OVS_DUP_MERGE
     {   // cost experiment: the LookupVector merge a second time, on a copy
-        SVec<8> nh2 = L.nh;
+        SVec<C> nh2 = L.nh;
         asm volatile("" : "+v"(nh2.idx[0]));
         const int k2 = nh_merge<EX>(nh2, res, LC.redundant, L.K, V.nodes);
         uint32_t z = (uint32_t)k2 ^ nh2.used;
-        for (int q = 0; q < 8; ++q) z ^= nh2.idx[q] ^ (uint32_t)nh2.d[q] ^ (uint32_t)(nh2.d[q] >> 32);
+        for (int q = 0; q < C; ++q) z ^= nh2.idx[q] ^ (uint32_t)nh2.d[q] ^ (uint32_t)(nh2.d[q] >> 32);
         asm volatile("" :: "v"(z));
     }
 #endif
@@ -1047,11 +1050,11 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
         K160 oK;
 #pragma unroll
         for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
-        const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;
+        const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? V.bpb : 0;
         const int nsb = (opre + KBLK - 1) / KBLK;     // the level-sorted row's prefix that matters
         const int nitems = live ? nmain + nsb + 1 : 0;
         auto load_item = [&](int i, Blk8& b) -> int {
-            if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
+            if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m) + i, oK);
             if (i < nmain + nsb)
                 return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(i - nmain), oK);
             blk_clear(b);
@@ -1110,30 +1113,32 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
 
 // the per-lane end of a cooperative findNode: truncation to resultSize, then the buckets above m
 // while the result is short (Kademlia.cc:1233-1242; only tiny networks / short tables get there)
-template <bool EX>
+template <bool EX, int C>
 __device__ __forceinline__ int kad_coop_finish(const KadView& V, const RespGeo& g, const K160& K, int numRedundant,
-                                               bool sib, int numSiblings, Blk8& res, int seen)
+                                               bool sib, int numSiblings, BlkN<C>& res, int seen)
 {
     const int rs = sib ? (numSiblings ? numSiblings : 1) : numRedundant;
-    const int cap = rs < 8 ? rs : 8;
+    const int cap = rs < C ? rs : C;
     int n = blk_trunc(res, cap);
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) {
         if (g.rowlo < 0 || b < g.rowlo) continue;
-        Blk8 blk;
-        const int cnt = blk_load_block(blk, slot_blk(V, g.boff, b), K);
-        if (cnt) {
-            blk_sort8<false, EX>(blk, K, V.nodes);
-            blk_merge_top8<false, EX>(res, blk, K, V.nodes);
-            n = blk_trunc(res, cap);
-            seen += cnt;
+        for (int j = 0; j < V.bpb; ++j) {
+            Blk8 blk;
+            const int cnt = blk_load_block(blk, slot_blk(V, g.boff, b) + j, K);
+            if (cnt) {
+                blk_sort8<false, EX>(blk, K, V.nodes);
+                blk_merge_top<false, EX, C, 8>(res, blk, K, V.nodes);
+                n = blk_trunc(res, cap);
+                seen += cnt;
+            }
         }
     }
     return n;
 }
 
 // LookupListener::lookupFinished -> KBRTestApp statistics (BaseOverlay.cc:1241-1307)
-template <int A>
-__device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A>& L, const KadView& V,
+template <int A, int C>
+__device__ __forceinline__ ovs_route_out kad_lookup_output(const KadLookup<A, C>& L, const KadView& V,
                                                            const DelayConsts& DC, const KadLC& LC)
 {
     ovs_route_out o;
@@ -1171,7 +1176,7 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
     KadView V{};
     V.nodes = t.nodes; V.nodex = t.nodex; V.blks = t.blks; V.sibb = t.blks ? t.blks + t.rows_blks : nullptr;
     V.slev = t.slev;
-    V.xy = xy; V.n = n; V.k = t.k; V.S5 = 5 * t.s;
+    V.xy = xy; V.n = n; V.k = t.k; V.bpb = t.bpb; V.S5 = 5 * t.s;
     V.sbn = (V.S5 + KBLK - 1) / KBLK;
     V.lo = t.lo; V.hi = t.hi;
     V.maybe_short = t.maybe_short;
@@ -1185,9 +1190,9 @@ inline bool kad_params_supported(const ovs_params& P, const KadTables& t)
     // event times of a lookup stay below 2^55 ns (Pend packs a 7-bit field above bit 56)
     const bool times_fit = P.lookupTimeout >= 0 && P.rpcUdpTimeout >= 0 && P.lookupTimeout + 2 * P.rpcUdpTimeout < 3.0e7;
     return times_fit && P.lookupParallelRpcs >= 1 && P.lookupParallelRpcs <= MAXA && P.lookupRedundantNodes >= 1 &&
-           P.lookupRedundantNodes <= 8 && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings >= 0 &&
+           P.lookupRedundantNodes <= KMAX && P.lookupMerge && P.lookupStrictParallelRpcs && P.numSiblings >= 0 &&
            P.numSiblings <= t.s && P.numSiblings <= 8 &&
-           t.k <= 8 && P.hopCountMax <= 0x7FFF;
+           t.k <= KMAX && P.hopCountMax <= 0x7FFF;
 }
 
 inline KadLC kad_make_lc(const ovs_params& P, const KadTables& t)

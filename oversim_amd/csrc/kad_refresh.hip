@@ -141,7 +141,8 @@ struct XCtx {
         };
         auto add_slot = [&](int bucket) {
             if (g.rowlo < 0 || bucket < g.rowlo) return;   // buckets below the stored row are empty
-            add_blk(slot_blk(V, g.boff, bucket));
+            const KadBlk* blk = slot_blk(V, g.boff, bucket);
+            for (int j = 0; j < V.bpb; ++j) add_blk(blk + j);
         };
         if (g.m >= 0) add_slot(g.m);
         if (g.m >= g.endIndex || n < rs) {
@@ -166,7 +167,7 @@ struct XCtx {
         auto cnt_slot = [&](int bucket) {
             if (g.rowlo < 0 || bucket < g.rowlo) return;
             const KadBlk* blk = slot_blk(V, g.boff, bucket);
-            for (int q = 0; q < KBLK && blk->idx[q] != NONE; ++q) ++n;
+            for (int q = 0; q < V.bpb * KBLK && blk[q / KBLK].idx[q % KBLK] != NONE; ++q) ++n;
         };
         if (g.m >= 0) cnt_slot(g.m);
         if (g.m >= g.endIndex || n < rs) {
@@ -742,7 +743,7 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     if (nq == 0) return hipSuccess;
     const int A = P.lookupParallelRpcs;
     if (A < 1 || A > XMAXA || R < 1 || R > 64 || ns < 1 || ns > R || !P.lookupMerge || !P.lookupStrictParallelRpcs ||
-        P.hopCountMax < 1 || t.k > 8)
+        P.hopCountMax < 1 || t.k > KMAX)
         return hipErrorNotSupported;
     const KadView V = kad_make_view(t, xy, n);
     XCfg C;

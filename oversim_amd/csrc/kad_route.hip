@@ -119,10 +119,10 @@ struct KadRouteIO {
     uint8_t* __restrict__ ltag;
 };
 
-template <int A, bool RECORD, bool EX, bool LK, bool SHARD>
+template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C>
 // the shard step runs at 2 waves/SIMD: its HBM state traffic and request staging need the registers
 // (at 3 the exact-compare instantiations spilled in misaligned 96-bit pieces gfx950 rejects)
-__global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
+__global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
                                                                             KadRouteIO io)
 {
     const int lane = threadIdx.x & 63;
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
     const uint64_t end = min(cursor + chunk, nq);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int ns = LK ? LC.numSiblings : 1;
-    KadLookup<A>* st = static_cast<KadLookup<A>*>(io.st);
+    KadLookup<A, C>* st = static_cast<KadLookup<A, C>*>(io.st);
 
 #ifndef OVS_NOCOOP
     __shared__ CoopLds lds;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
     bool active = false;
     bool dead = false;     // shard step: a listed lookup that does not run (source off the arc)
     uint64_t q = 0;
-    KadLookup<A> L;
+    KadLookup<A, C> L;
 
     while (true) {
         const uint64_t need = __ballot(!active);
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
         // tie fallbacks in the cooperative merge made the register allocator emit misaligned
         // 96-bit spills that gfx950 rejects.
 #ifndef OVS_NOCOOP
-        if constexpr (!EX) {
+        if constexpr (!EX && C == 8) {
             kad_coop_sibzone<EX>(V, coop, ev.r, ev.geo, ev.boff, ev.pre, L.K, lds);
 #ifdef OVS_DUP_COOP
             kad_coop_sibzone<EX>(V, coop, ev.r, ev.geo, ev.boff, ev.pre, L.K, lds);   // cost experiment
@@ -210,15 +210,15 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
             active = false;
             dead = false;
         } else if (active) {
-            SVec<8> res;
+            SVec<C> res;
             res.n = 0;
             res.used = 0;
             int num = -1;
             if (ph == KEV_FIND) {
                 int n;
-                Blk8 fb;
+                BlkN<C> fb;
                 if (coop) {
-                    coop_get(lds.res, threadIdx.x, fb);
+                    if constexpr (C == 8) coop_get(lds.res, threadIdx.x, fb);
                     // the candidates findNode saw: the row entries past the prefix's blocks count too
                     const RespGeo g = ev.rg();
                     const int rd = min(g.nsib, KBLK * ((ev.pre + KBLK - 1) / KBLK));
@@ -228,23 +228,26 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
                     const KadRes& rr = io.res[q * A + ev.e];
                     n = (int)rr.count;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) { fb.x[k] = k < n ? rr.nodes[k] : NONE; fb.d[k] = k < n ? rr.dist[k] : ~0ull; }
+                    for (int k = 0; k < C; ++k) {
+                        fb.x[k] = k < n ? rr.nodes[k < 8 ? k : 0] : NONE;
+                        fb.d[k] = k < n ? rr.dist[k < 8 ? k : 0] : ~0ull;
+                    }
                 } else {
-                    n = kad_find_node_blk<EX>(V, ev.r, ev.rg(), L.K, ev.numR, ev.sb(), fb, ns);
+                    n = kad_find_node_blk<EX, C>(V, ev.r, ev.rg(), L.K, ev.numR, ev.sb(), fb, ns);
 #ifdef OVS_DUP_LANEFIND
                     {   // cost experiment: the per-lane findNode again
                         K160 K2 = L.K;
                         asm volatile("" : "+v"(K2.w[0]));
-                        Blk8 b2;
-                        const int n2 = kad_find_node_blk<EX>(V, ev.r, ev.rg(), K2, ev.numR, ev.sb(), b2, ns);
+                        BlkN<C> b2;
+                        const int n2 = kad_find_node_blk<EX, C>(V, ev.r, ev.rg(), K2, ev.numR, ev.sb(), b2, ns);
                         uint32_t z = (uint32_t)n2;
-                        for (int k = 0; k < 8; ++k) z ^= b2.x[k] ^ (uint32_t)b2.d[k] ^ (uint32_t)(b2.d[k] >> 32);
+                        for (int k = 0; k < C; ++k) z ^= b2.x[k] ^ (uint32_t)b2.d[k] ^ (uint32_t)(b2.d[k] >> 32);
                         asm volatile("" :: "v"(z));
                     }
 #endif
                 }
 #pragma unroll
-                for (int k = 0; k < 8; ++k) { res.idx[k] = fb.x[k]; res.d[k] = fb.d[k]; }
+                for (int k = 0; k < C; ++k) { res.idx[k] = fb.x[k]; res.d[k] = fb.d[k]; }
                 res.n = n;
                 num = kad_event_after_find<A, EX, LK>(L, V, LC, ev, res);
             } else if (ph == KEV_SENDS) {
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(256, SHARD ? 2 : OVS_KAD_WAVES) void k_kad_route(Ka
 }  // namespace
 
 // persistent grid: as many waves as are resident, each with a contiguous slice of the batch
-template <int A, bool RECORD, bool EX, bool LK, bool SHARD>
+template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C = 8>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, KadRouteIO io, int num_cu,
                              hipStream_t st)
 {
@@ -319,7 +322,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     // initialised once, thread-safely)
     static const int bpc = [] {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SHARD>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SHARD, C>, 256, 0) !=
                 hipSuccess ||
             b < 1)
             b = 1;
@@ -334,7 +337,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kad_stats), z, sizeof z, 0, hipMemcpyHostToDevice, st);
 #endif
-    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SHARD>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC, io);
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SHARD, C>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC, io);
 #ifdef OVS_KAD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
@@ -351,7 +354,13 @@ hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC
 {
     KadRouteIO io{};
     io.qkeys = qkeys; io.qsrc = qsrc; io.nq = nq; io.out = out; io.hopseq = hopseq; io.rpcs_out = rpcs; io.sib_out = sibs;
-    // LookupCall batches (sibs != nullptr) record no hop sequence
+    // LookupCall batches (sibs != nullptr) record no hop sequence.  KademliaLarge (k or
+    // lookupRedundantNodes above 8) takes the 16-entry LookupVector / findNode instantiation.
+    if (LC.redundant > 8 || LC.maxRedundantLocal > 8) {
+        if (sibs) return kad_launch<A, false, EX, true, false, 16>(V, DC, LC, io, num_cu, st);
+        if (hopseq) return kad_launch<A, true, EX, false, false, 16>(V, DC, LC, io, num_cu, st);
+        return kad_launch<A, false, EX, false, false, 16>(V, DC, LC, io, num_cu, st);
+    }
     if (sibs) return kad_launch<A, false, EX, true, false>(V, DC, LC, io, num_cu, st);
     if (hopseq) return kad_launch<A, true, EX, false, false>(V, DC, LC, io, num_cu, st);
     return kad_launch<A, false, EX, false, false>(V, DC, LC, io, num_cu, st);

@@ -132,7 +132,14 @@ hipError_t kad_shard_step_dispatch(int A, const KadView& V, const DelayConsts& D
 
 }  // namespace
 
-bool kad_params_supported_host(const ovs_params& P, const KadTables& t) { return kad_params_supported(P, t); }
+// the sharded path exchanges findNode results of at most 8 nodes (KadRes, ovs_kad_resp): k and
+// lookupRedundantNodes <= 8
+static bool kad_shard_params_supported(const ovs_params& P, const KadTables& t)
+{
+    return kad_params_supported(P, t) && P.lookupRedundantNodes <= 8 && t.k <= 8;
+}
+
+bool kad_params_supported_host(const ovs_params& P, const KadTables& t) { return kad_shard_params_supported(P, t); }
 
 size_t kad_lookup_state_bytes(int alpha)
 {
@@ -172,7 +179,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     const bool lk = lk_ns >= 0;
     ovs_params Q = P;
     if (lk) Q.numSiblings = lk_ns;
-    if (!kad_params_supported(Q, t) || Q.numSiblings != (lk ? lk_ns : 1) || (lk && !sib_out))
+    if (!kad_shard_params_supported(Q, t) || Q.numSiblings != (lk ? lk_ns : 1) || (lk && !sib_out))
         return hipErrorNotSupported;
     if (nsh < 1 || nsh > MAXSHARDS) return hipErrorInvalidValue;
     hipError_t e;
@@ -232,7 +239,7 @@ hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, 
     // numSiblings travels with each request; the rest of the configuration is the rank's
     ovs_params Q = P;
     Q.numSiblings = 1;
-    if (!kad_params_supported(Q, t)) return hipErrorNotSupported;
+    if (!kad_shard_params_supported(Q, t)) return hipErrorNotSupported;
     if (nreq == 0) return hipSuccess;
     KadView V = kad_make_view(t, nullptr, n);
     V.err = bad;

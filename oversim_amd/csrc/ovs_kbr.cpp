@@ -769,8 +769,8 @@ static ovs_status kad_load_arc(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     free_kad_shard(c);
     if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
     if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
-    if (c->P.k < 1 || c->P.k > 8 || c->P.s < 1 || 5 * c->P.s > 64)
-        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..8 (one 96 B bucket block) and 5*s <= 64");
+    if (c->P.k < 1 || c->P.k > KMAX || c->P.s < 1 || 5 * c->P.s > 64)
+        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..16 (two 96 B bucket blocks) and 5*s <= 64");
     if (lo >= hi || hi > n) return fail(c, OVS_EINVAL, "arc [lo, hi) must be a non-empty part of [0, n)");
     ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
     if (s != OVS_OK) { free_tables(c); return s; }
@@ -796,8 +796,8 @@ ovs_status ovs_kad_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     free_kad_shard(c);
     if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
     if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
-    if (c->P.k < 1 || c->P.k > 8 || c->P.s < 1 || 5 * c->P.s > 64)
-        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..8 (one 96 B bucket block) and 5*s <= 64");
+    if (c->P.k < 1 || c->P.k > KMAX || c->P.s < 1 || 5 * c->P.s > 64)
+        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..16 (two 96 B bucket blocks) and 5*s <= 64");
     ovs_status s = upload_nodes(c, ids, n, xy, false);
     if (s != OVS_OK) { free_tables(c); return s; }
     const uint64_t S5 = 5ull * (uint64_t)c->P.s, k = (uint64_t)c->P.k;

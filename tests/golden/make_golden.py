@@ -77,10 +77,12 @@ def chord_rec_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: i
     print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
 
 
-def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
+def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1, **kw):
+    """kw: further Kademlia parameters ([Config KademliaLarge]: k = lookupRedundantNodes = 16)."""
     net = W.population(n, seed)
     k1, s1 = W.lookups(net.ids, m, seed + 1, node_ids=True)
-    p = kad_params(lookupParallelRpcs=alpha, simtimeRound=rnd)
+    p = kad_params(lookupParallelRpcs=alpha, simtimeRound=rnd, **kw)
+    R = p.lookupRedundantNodes
     o = OracleNet("kademlia", net.ids, net.xy, p)
     sib, cnt, nodes = o.kad_tables()
     # findNode restated twice: oracle vs refmodel on the oracle's own snapshot
@@ -88,18 +90,18 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
     rng = np.random.default_rng(seed + 3)
     fn_node = rng.integers(0, n, 512).astype(np.uint32)
     fn_key = np.concatenate([W.random_keys(256, rng), net.ids[rng.integers(0, n, 256)]])
-    fn_out = np.full((512, 8), 0xFFFFFFFF, dtype=np.uint32)
+    fn_out = np.full((512, max(R, 8)), 0xFFFFFFFF, dtype=np.uint32)
     fn_sib = np.zeros(512, dtype=np.uint8)
     for i in range(512):
-        res, flag = o.find_node(int(fn_node[i]), fn_key[i], 8, 1)
-        ref = tab.find_node(int(fn_node[i]), refmodel.to_int(fn_key[i]), 8, 1)
+        res, flag = o.find_node(int(fn_node[i]), fn_key[i], R, 1)
+        ref = tab.find_node(int(fn_node[i]), refmodel.to_int(fn_key[i]), R, 1)
         assert [int(x) for x in res] == ref, (name, i, res, ref)
         assert flag == tab.is_sibling_for(int(fn_node[i]), refmodel.to_int(fn_key[i]), 1)
         fn_out[i, :len(res)] = res
         fn_sib[i] = flag
     r = o.route(k1, s1, record_hops=True, count_rpcs=True)
     # the lookups restated twice: oracle event list vs refmodel's message-level simulation
-    sim = refmodel.KadLookupSim(tab, net.xy, alpha=alpha, rnd=bool(rnd), k=p.k)
+    sim = refmodel.KadLookupSim(tab, net.xy, redundant=R, alpha=alpha, rnd=bool(rnd), k=p.k)
     for i in range(len(k1)):
         mm = sim.run(k1[i], int(s1[i]))
         for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs"):
@@ -118,7 +120,7 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1):
                         one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"], rpcs=r["rpcs"],
                         hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed),
                         kad_seed=np.uint64(p.kadSeed), fn_node=fn_node, fn_key=fn_key, fn_out=fn_out,
-                        fn_sib=fn_sib)
+                        fn_sib=fn_sib, k=np.int32(p.k), s=np.int32(p.s), redundant=np.int32(R))
     print(name, "lookups", len(k1), "mean hops", r["hops"].mean(), "rpcs", r["rpcs"].mean(),
           "status", np.bincount(r["status"]))
 
@@ -166,6 +168,10 @@ if __name__ == "__main__":
     if "--rec" in sys.argv:
         chord_rec_case("chord_n1000_semirec", 1000, 0x4213, 2048, 2048, 1)
         chord_rec_case("chord_n1000_semirec_hcm4", 1000, 0x4214, 512, 512, 0, hcm=4)
+        sys.exit(0)
+    if "--large" in sys.argv:   # [Config KademliaLarge] (omnetpp.ini:113-126), 1000 nodes as configured
+        kad_case("kad_n1000_large", 1000, 0x4b4c, 2048, 1, k=16, lookupRedundantNodes=16, s=8)
+        kad_case("kad_n1000_large_a3", 1000, 0x4b4d, 1024, 3, k=16, lookupRedundantNodes=16, s=8)
         sys.exit(0)
     if "--check" in sys.argv and "--koorde" not in sys.argv:
         kad_case("kad_n2000_a1", 2000, 0x4b41, 2048, 1)

@@ -136,3 +136,31 @@ def test_workload_ids_sorted_unique():
     assert xy.shape == (5000, 2) and np.all(np.abs(xy) < 400)
     xy2 = W.coordinates(20000, 3)
     assert np.all(np.abs(xy2) <= 75)
+
+
+def test_params_kademlia_large():
+    """[Config KademliaLarge] (omnetpp.ini:113-126) binds k = 16, lookupRedundantNodes = 16, s = 8,
+    alpha = 1 over default.ini (omnetpp.ini ends with `include ./default.ini`: textual inclusion).
+    The engine takes these tables (two 96 B blocks per bucket) since round 3."""
+    from oversim_amd import OVERLAY_KADEMLIA, Params
+    ini = """
+[Config KademliaLarge]
+**.overlayType = "oversim.overlay.kademlia.KademliaModules"
+**.overlay.kademlia.lookupRedundantNodes = 16
+**.overlay.kademlia.s = 8
+**.overlay.kademlia.k = 16
+**.overlay.kademlia.lookupMerge = true
+**.overlay.kademlia.lookupParallelPaths = 1
+**.overlay.kademlia.lookupParallelRpcs = 1
+
+[General]
+**.overlay*.kademlia.lookupParallelRpcs = 3
+"""
+    p = Params.from_ini(ini, "KademliaLarge", overlay=OVERLAY_KADEMLIA)
+    assert (p.k, p.s, p.lookupRedundantNodes, p.lookupParallelRpcs, p.lookupMerge) == (16, 8, 16, 1, 1)
+    ref = Path("/root/reference/simulations")
+    if (ref / "omnetpp.ini").exists():
+        text = (ref / "omnetpp.ini").read_text().replace("include ./default.ini", (ref / "default.ini").read_text())
+        q = Params.from_ini(text, "KademliaLarge", overlay=OVERLAY_KADEMLIA)
+        assert (q.k, q.s, q.lookupRedundantNodes, q.lookupParallelRpcs) == (16, 8, 16, 1)
+        assert q.lookupMerge == 1 and q.hopCountMax == 50

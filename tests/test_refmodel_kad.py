@@ -204,3 +204,51 @@ def test_exact_key_lookup_calls_agree(net, alpha):
         assert [int(x) for x in r["siblings"][i][: len(m["siblings"])]] == m["siblings"], i
         valid += m["is_valid"]
     assert 150 <= valid < len(keys)      # node-ID keys and own keys found, random keys not
+
+
+# [Config KademliaLarge] (omnetpp.ini:113-126): k = 16, lookupRedundantNodes = 16, s = 8, alpha = 1
+LARGE_VARIANTS = {
+    "large_a1": dict(k=16, lookupRedundantNodes=16, lookupParallelRpcs=1),
+    "large_a3": dict(k=16, lookupRedundantNodes=16, lookupParallelRpcs=3),
+    "k16_r8_a3": dict(k=16, lookupRedundantNodes=8, lookupParallelRpcs=3),
+    "k12_r12_a2": dict(k=12, lookupRedundantNodes=12, lookupParallelRpcs=2),
+}
+
+
+@pytest.mark.parametrize("name", list(LARGE_VARIANTS))
+def test_kademlia_large_lookups_agree(net, name):
+    """16-entry buckets and LookupVectors: the two readings agree on one-way lookups and LookupCalls."""
+    p = kad_params(**LARGE_VARIANTS[name])
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    k1, s1 = W.lookups(net.ids, 150, 21, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 150, 22, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    r = o.route(keys, src, record_hops=True, count_rpcs=True)
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]))
+        for f in FIELDS:
+            assert int(r[f][i]) == int(m[f]), (name, i, f, int(r[f][i]), int(m[f]))
+        assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == m["hop_seq"], (name, i)
+    lc = o.lookup_call(k1, s1, 8)
+    for i in range(len(k1)):
+        m = sim.run(k1[i], int(s1[i]), num_siblings=8, lookup_call=True)
+        assert int(lc["is_valid"][i]) == m["is_valid"] and int(lc["hops"][i]) == m["hops"], (name, i)
+        assert int(lc["latency_ns"][i]) == m["latency_ns"], (name, i)
+        assert [int(x) for x in lc["siblings"][i][: len(m["siblings"])]] == m["siblings"], (name, i)
+
+
+def test_kademlia_large_refresh_agrees(net):
+    """Bucket refresh with bucketRefreshNodes = k = 16 (exhaustive-iterative, R = 16)."""
+    p = kad_params(k=16, lookupRedundantNodes=16, lookupParallelRpcs=3)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sim = _sim(o, net, p)
+    nodes = np.arange(3, len(net.ids), 211, dtype=np.uint32)
+    keys, src = o.refresh_keys(nodes)
+    keys, src = keys[::4], src[::4]
+    r = o.exhaustive(keys, src, 16)
+    for i in range(len(keys)):
+        m = sim.run(keys[i], int(src[i]), num_siblings=16, lookup_call=True, exhaustive=16)
+        assert int(r["status"][i]) == m["status"] and int(r["hops"][i]) == m["hops"], i
+        assert int(r["rpcs"][i]) == m["rpcs"] and int(r["latency_ns"][i]) == m["latency_ns"], i
+        assert [int(x) for x in r["siblings"][i][: len(m["siblings"])]] == m["siblings"], i
