@@ -755,7 +755,8 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     C.bwFull = simtime_ns_host((double)((int64_t)(DC.respBase + DC.respPerNode * R) * 8) / P.datarate, P.simtimeRound);
     C.bwOne = DC.bwResp[1];
     // 2R <= 16: the LookupVector lives in registers and findNode results in sorting-network blocks
-    const bool reg = R <= 8;
+    // (the start's own findNode answers k nodes: k = 16, KademliaLarge, takes the scratch form)
+    const bool reg = R <= 8 && t.k <= 8;
     // one lane per lookup, as many lanes as are resident at once (occupancy-sized grid); the
     // scratch is sized for the lanes
     int dev = 0;
