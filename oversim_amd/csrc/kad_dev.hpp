@@ -416,7 +416,10 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     auto add_slot = [&](int bucket) {
         if (g.rowlo < 0 || bucket < g.rowlo) return;      // buckets below the stored row are empty
         const KadBlk* blk = slot_blk(V, g.boff, bucket);
-        for (int j = 0; j < V.bpb; ++j) add_blk(blk + j);
+        // the 8-entry instantiations run only on tables with k <= 8 (one block per bucket; the
+        // launchers pick C = 16 otherwise)
+        if constexpr (C == 8) add_blk(blk);
+        else for (int j = 0; j < V.bpb; ++j) add_blk(blk + j);
     };
     if (g.m >= 0) add_slot(g.m);
     // Members of bucket m are XOR-closer to K than everything below it (buckets < m, siblings --
@@ -1050,11 +1053,11 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
         K160 oK;
 #pragma unroll
         for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
-        const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? V.bpb : 0;
+        const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;   // k <= 8: one block
         const int nsb = (opre + KBLK - 1) / KBLK;     // the level-sorted row's prefix that matters
         const int nitems = live ? nmain + nsb + 1 : 0;
         auto load_item = [&](int i, Blk8& b) -> int {
-            if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m) + i, oK);
+            if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
             if (i < nmain + nsb)
                 return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(i - nmain), oK);
             blk_clear(b);
@@ -1122,7 +1125,7 @@ __device__ __forceinline__ int kad_coop_finish(const KadView& V, const RespGeo& 
     int n = blk_trunc(res, cap);
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) {
         if (g.rowlo < 0 || b < g.rowlo) continue;
-        for (int j = 0; j < V.bpb; ++j) {
+        for (int j = 0; j < (C == 8 ? 1 : V.bpb); ++j) {
             Blk8 blk;
             const int cnt = blk_load_block(blk, slot_blk(V, g.boff, b) + j, K);
             if (cnt) {
