@@ -253,7 +253,7 @@ def main():
         else:
             sh = ShardedKademlia(rank, world, ids_np, xy_np, dkeys, dsrc, dev, comm_dev=comm,
                                  params=Params.kademlia().replace(lookupParallelRpcs=wl["alpha"]))
-            kname = "k_kad_shard"
+            kname = "k_kad_route"     # its shard-step instantiation
 
         def step():
             sh.run()

@@ -1,0 +1,89 @@
+"""The sharded kernels at the full sizes of configs D and E, W = 8 arcs emulated in one process on
+one GPU (eight contexts, the in-process exchange): every lookup of a sample of the batch is
+compared with the lazy-table CPU oracle, and the whole batch with the single-context kernel where
+the tables fit twice.  D: Chord 2^26 nodes (8 arcs of 2^23, ~25 GB per arc context); E: Kademlia
+2^24 nodes, alpha = 3 (8 arcs of 2^21)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oversim_amd import Params, workload as W
+
+pytestmark = pytest.mark.gpu
+ROUTE_FIELDS = ("responsible", "hops", "status", "one_way_hops", "latency_ns")
+
+
+def _split(net, bounds, m, seed, node_ids):
+    dev = torch.device("cuda", 0)
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(len(bounds) - 1):
+        k, s = W.lookups(net.ids, m, seed + r, node_ids=node_ids(r))
+        s = (bounds[r] + s.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k.view(np.int32)).to(dev))
+        ss.append(torch.from_numpy(s.view(np.int32)).to(dev))
+        qb.append(r * m)
+        allk.append(k); alls.append(s)
+    return ks, ss, qb, np.concatenate(allk), np.concatenate(alls)
+
+
+@pytest.mark.timeout(900)
+def test_kad_w8_config_e_full_size():
+    """Config E at full size: 2^24 nodes, alpha = 3, 8 arcs, 250k lookups per arc; a 4000-lookup
+    sample against the lazy oracle (RPC counts too), the whole batch against the single context."""
+    from oversim_amd import KbrEngine
+    from oversim_amd.shard import KadShardStepper, arc_bounds, done_to_numpy, route_kad_local_shards
+    from oracle_lib import OracleNet, kad_params
+    world, n, m = 8, 1 << 24, 250_000
+    net = W.population(n, 0xE24)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=3)
+    ks, ss, qb, allk, alls = _split(net, bounds, m, 0xE30, lambda r: r % 4 == 1)
+    steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params) for r in range(world)]
+    dones, rounds = route_kad_local_shards(steppers, ks, ss, qb)
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    assert rounds >= 4
+    del steppers, dones
+    torch.cuda.empty_cache()
+    with KbrEngine(0) as e:
+        e.set_params(params)
+        e.kad_load(net.ids, net.xy)
+        ref = e.lookup(allk, alls)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    pick = np.random.default_rng(1).choice(world * m, 4000, replace=False)
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params(lookupParallelRpcs=3), lazy=True)
+    r = o.route(allk[pick], alls[pick], record_hops=False)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f][pick].astype(np.int64), r[f].astype(np.int64)), f
+
+
+@pytest.mark.timeout(1200)
+def test_chord_w8_config_d_full_size():
+    """Config D at full size: a 2^26-node ring in 8 arcs (one context each, ~25 GB per arc), 125k
+    lookups per arc through the sharded K1; a 3000-lookup sample against the lazy oracle."""
+    from oversim_amd.shard import GpuShardStepper, arc_bounds, done_to_numpy, route_local_shards
+    from oracle_lib import OracleNet
+    world, n, m = 8, 1 << 26, 125_000
+    net = W.population(n, 0xD26)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    ks, ss, qb, allk, alls = _split(net, bounds, m, 0xD30, lambda r: r % 2 == 0)
+    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, params=Params.chord())
+                for r in range(world)]
+    for st in steppers:
+        st.reset(world * m)
+    dones, rounds = route_local_shards(steppers, ks, ss, qb)
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    assert rounds >= 4
+    pick = np.random.default_rng(2).choice(world * m, 3000, replace=False)
+    o = OracleNet("chord", net.ids, net.xy, lazy=True)
+    r = o.route(allk[pick], alls[pick], record_hops=False)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f][pick].astype(np.int64), r[f].astype(np.int64)), f
