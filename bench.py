@@ -323,7 +323,7 @@ def main():
         hop_total, n_ok = sh.hop_total(), sh.ok_total()
         kern_ms = sh.kernel_ms / max(sh.runs, 1)
         if kind == "kademlia":
-            rpc_total = sh.served     # FindNodeCalls answered by this rank's tables
+            rpc_total = sh.rpc_total()     # FindNodeCalls of this rank's lookups (done records)
     else:
         outs = dout.cpu().numpy().reshape(-1, 16)
         hop_total = int(outs[:, 4:6].copy().view(np.uint16).astype(np.int64).sum())

@@ -429,7 +429,7 @@ typedef struct ovs_lookup_rec {     /* 48 B in-flight lookup */
 
 typedef struct ovs_done_rec {       /* 24 B finished lookup */
     uint32_t qid;
-    uint32_t pad;
+    uint32_t pad;                   /* Kademlia shard step: the lookup's FindNodeCalls; 0 otherwise */
     ovs_route_out out;
 } ovs_done_rec;
 

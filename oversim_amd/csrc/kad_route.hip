@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                 if (SHARD) {
                     ovs_done_rec dr;
                     dr.qid = io.qids[q];
-                    dr.pad = 0;
+                    dr.pad = L.nsent;     // the lookup's FindNodeCalls (local and remote)
                     dr.out = o;
                     if (LK) {
                         uint32_t cnt = 0;

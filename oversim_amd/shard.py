@@ -679,3 +679,7 @@ class ShardedKademlia:
 
     def ok_total(self) -> int:
         return int((done_to_numpy(self._done)["status"] == 0).sum())
+
+    def rpc_total(self) -> int:
+        """FindNodeCalls of this rank's lookups (the done records carry each lookup's count)."""
+        return int(done_to_numpy(self._done)["pad"].astype(np.int64).sum())
