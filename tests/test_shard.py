@@ -437,6 +437,7 @@ def test_kad_shards_emulated_on_one_gpu(world, alpha, n):
     ref = _kad_reference(net, np.concatenate(allk), np.concatenate(alls), params)
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    assert np.array_equal(d["pad"].astype(np.int64), ref["rpcs"].astype(np.int64))   # FindNodeCalls per lookup
     assert rounds >= 3
 
 
