@@ -7,6 +7,9 @@ path over one batch of synthetic lookups already resident in HBM.  rank 0
 prints ONE JSON line.
 
 Workloads (--workload, default C):
+  A  Chord, 1000 nodes (nodes_2d_15000.xml coordinates), successorListSize 8,
+     100k node-ID one-way lookups per GPU, seed 0x4213 (BASELINE.md §2 config
+     A, the reference's own CPU-sized case).  N > 1: independent replicas.
   C  Chord, 2^20 ring nodes per GPU (random coordinates, fieldSize 150), 10M
      uniform random-key one-way lookups per GPU.  N > 1: the N x 2^20 ring is
      sharded over the GPUs and in-flight lookups are exchanged every hop round
@@ -69,12 +72,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["B", "C", "D", "E", "K", "R"], default="C")
+    ap.add_argument("--workload", choices=["A", "B", "C", "D", "E", "K", "R"], default="C")
     ap.add_argument("--nodes", type=int, default=None, help="override ring size (per GPU for C, total for D/E)")
     ap.add_argument("--lookups", type=int, default=None, help="override lookups per GPU per step")
     ap.add_argument("--routing", choices=["iterative", "semi-recursive"], default="iterative",
                     help="Chord routingType (semi-recursive = omnetpp.ini ChordLarge)")
-    ap.add_argument("--seed", type=int, default=0xC)
+    ap.add_argument("--seed", type=int, default=None, help="population seed (default: the workload's, 0xC)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
@@ -227,10 +230,10 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     # Koorde runs replicas (its tables are not sharded); Kademlia shards unless OVS_KAD_REPLICAS=1
     refresh = a.workload == "R"
-    sharded = world > 1 and (kind == "chord" or (kind == "kademlia" and not refresh and
+    sharded = world > 1 and ((kind == "chord" and a.workload != "A") or (kind == "kademlia" and not refresh and
                                                  os.environ.get("OVS_KAD_REPLICAS") != "1"))
     # rehearsal knob: the sharded host path (collectives, cohorts) at N = 1
-    if os.environ.get("OVS_BENCH_SHARD") == "1" and kind != "koorde" and not refresh:
+    if os.environ.get("OVS_BENCH_SHARD") == "1" and kind != "koorde" and not refresh and a.workload != "A":
         sharded = True
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
@@ -372,7 +375,8 @@ def main():
                "parallelism": ((f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)" if kind == "chord"
                                 else f"ID arcs over {world} GPUs, FindNodeCall request/response all-to-allv per round")
                                if sharded else ("replicas" if world > 1 else "1 GPU")),
-               "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1)}
+               "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1),
+               "seed": hex(I["seed"])}
         if refresh:
             cfg.update({"refresh_nodes_per_gpu": wl["refresh_nodes"], "bucketRefreshNodes": 8,
                         "routingType": "exhaustive-iterative"})

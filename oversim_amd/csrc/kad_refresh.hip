@@ -488,8 +488,11 @@ struct XCtx {
                 const RespGeo g = resp_geo(rn, L.K);
                 const int rs = R.start ? C.k : C.R;
                 int numNew = 0, cnt = 0;
-                if (REG || rs <= 8) {
-                    Blk8 b;       // the block form of K2 (sorting networks, kad_dev.hpp)
+                if (REG || (rs <= 8 && V.bpb == 1)) {
+                    // the block form of K2 (sorting networks, kad_dev.hpp): its 8-entry instantiation
+                    // reads one block per bucket, so only on tables with k <= 8 (a k = 16 table's
+                    // bucket refresh, R = 8, scans both blocks of each bucket below)
+                    Blk8 b;
                     cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {

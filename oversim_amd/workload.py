@@ -133,10 +133,14 @@ def device_lookups(n_nodes: int, m: int, seed: int, device, src_lo: int = 0, src
 
 
 # ---------------------------------------------------------------------------
-# The bench workloads (BASELINE.json configs B-E), shared by bench.py and the parity tests that
+# The bench workloads (BASELINE.json configs A-E), shared by bench.py and the parity tests that
 # check the exact timed path on the exact timed inputs (tests/test_gpu_timed.py).
 
 WORKLOADS = {
+    "A": dict(overlay="chord", nodes=1000, per_gpu_nodes=False, lookups=100_000, node_ids=True, file_coords=True,
+              seed=0x4213,
+              desc="A: Chord 1000 nodes (nodes_2d_15000.xml), successorListSize 8, 100k node-ID iterative one-way "
+                   "lookups per GPU, seed 0x4213 (replicas)"),
     "C": dict(overlay="chord", nodes=1 << 20, per_gpu_nodes=True, lookups=10_000_000, node_ids=False,
               desc="C: Chord 2^20 nodes per GPU (ring sharded over GPUs), 10M random-key iterative one-way lookups per GPU"),
     "D": dict(overlay="chord", nodes=1 << 26, per_gpu_nodes=False, lookups=8_000_000, node_ids=False,
@@ -157,7 +161,7 @@ WORKLOADS = {
 SMALL_HOST_LIMIT = 1 << 22     # populations up to this size are generated on the host (numpy)
 
 
-def bench_inputs(workload: str, device, world: int = 1, rank: int = 0, seed: int = 0xC, nodes: int | None = None,
+def bench_inputs(workload: str, device, world: int = 1, rank: int = 0, seed: int | None = None, nodes: int | None = None,
                  n_lookups: int | None = None, sharded: bool | None = None) -> dict:
     """The population and this rank's lookups of a bench workload, resident on `device`.
 
@@ -166,6 +170,8 @@ def bench_inputs(workload: str, device, world: int = 1, rank: int = 0, seed: int
     on the host (n <= SMALL_HOST_LIMIT), else None; n_total, m, lo, hi (this rank's source arc)."""
     import torch
     wl = WORKLOADS[workload]
+    if seed is None:
+        seed = wl.get("seed", 0xC)
     n_node = nodes or wl["nodes"]
     n_total = n_node * world if wl["per_gpu_nodes"] else n_node
     m = n_lookups or wl["lookups"]
@@ -179,7 +185,7 @@ def bench_inputs(workload: str, device, world: int = 1, rank: int = 0, seed: int
     small = n_total <= SMALL_HOST_LIMIT
     if small:
         ids = sorted_unique_ids(n_total, seed)
-        xy = coordinates(n_total, seed, use_file=(kind == "kademlia" and n_total <= 15000))
+        xy = coordinates(n_total, seed, use_file=wl.get("file_coords", kind == "kademlia" and n_total <= 15000))
         ids_t = torch.from_numpy(ids.view(np.int32)).to(device)
         xy_t = torch.from_numpy(xy).to(device)
         keys, src = lookups(ids, m, seed + 1000 + rank, node_ids=wl["node_ids"])
@@ -193,6 +199,6 @@ def bench_inputs(workload: str, device, world: int = 1, rank: int = 0, seed: int
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     return dict(ids_t=ids_t, xy_t=xy_t, keys_t=keys_t, src_t=src_t, ids=ids, xy=xy, keys=keys, src=src,
-                n_total=n_total, m=m, lo=lo, hi=hi, kind=kind, alpha=wl.get("alpha", 1), desc=wl["desc"],
+                n_total=n_total, m=m, lo=lo, hi=hi, kind=kind, seed=seed, alpha=wl.get("alpha", 1), desc=wl["desc"],
                 per_gpu_nodes=wl["per_gpu_nodes"])
 

@@ -105,6 +105,25 @@ def _kad_properties(out, ids, keys, label):
     assert np.array_equal(out["responsible"][idx][clear], best[clear].astype(np.uint32)), label
 
 
+@pytest.mark.timeout(300)
+def test_timed_path_config_a():
+    """Config A: Chord 1000 nodes on nodes_2d_15000.xml coordinates, 100k node-ID
+    lookups, seed 0x4213 -- the whole batch against the oracle."""
+    dev = torch.device("cuda", 0)
+    I = W.bench_inputs("A", dev)
+    assert I["seed"] == 0x4213 and I["n_total"] == 1000 and I["m"] == 100_000
+    with KbrEngine(0) as eng:
+        eng.set_params(Params.chord())
+        eng.chord_load_device(I["ids_t"].data_ptr(), I["xy_t"].data_ptr(), I["n_total"])
+        out, _ = _route_device(eng, I, rpcs=False)
+    ids, xy, keys, src = _host_inputs(I)
+    assert np.all(out["status"] == 0)
+    assert np.array_equal(ids[out["responsible"]], keys)     # node-ID keys end at the key's node
+    idx = np.arange(I["m"])
+    ref = OracleNet("chord", ids, xy).route(keys, src, record_hops=False)
+    _check_sample(out, None, ref, idx, "A")
+
+
 @pytest.mark.timeout(600)
 def test_timed_path_config_c():
     """Config C (the default bench line): 2^20-node ring, the full 10M-lookup batch."""

@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -2 $O/smoke.log
 timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
 cat $O/bench_default.json
-for w in D B E K R; do
+for w in A D B E K R; do
   timeout -k 10 400 python -u bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
   cat $O/bench_$w.json
 done
