@@ -223,6 +223,20 @@ typedef struct {
 void orc_kbrtest_lookup_stats(const orc_net* net, const orc_lookup_out* out, const uint32_t* siblings, int stride,
                               const orc_key* keys, const uint32_t* src, uint64_t n, double measured_time_s,
                               int lookupNodeIds, double failureLatency, orc_kbrtest_lookup_result* st);
+/* EpiChord::findNode (EpiChord.cc:517-629) at node `self` on one routing snapshot
+ * (ovs_oracle_epichord.c): succ/pred = the successor / predecessor list entries closest first
+ * (nsucc/npred of them), lists_full bit 0 / bit 1 = successorList / predecessorList->isFull()
+ * (else thisNode ends the list), listSize = successorListSize; the live finger cache as ncache
+ * (node, lastUpdate ns, ttl ns) entries in any order.  src = the FindNodeCall's source
+ * (UINT32_MAX: a local call, msg == NULL), now = simTime() in ns, cacheTTL in ns.  Writes the
+ * next hops and their lastUpdates (the EpiChordFindNodeExtMessage) to out/out_last (cap slots).
+ * Returns the count; -1 where the reference throws "Failed to find node", -2 where it
+ * dereferences an empty finger cache (undefined), -3 bad input, -4 cap too small. */
+int orc_epichord_find_node(const orc_key* ids, uint32_t n, uint32_t self, const uint32_t* succ, int nsucc,
+                           const uint32_t* pred, int npred, int lists_full, int listSize, const uint32_t* cnode,
+                           const int64_t* clast, const int64_t* cttl, int ncache, const orc_key* key, uint32_t src,
+                           int64_t now, int64_t cacheTTL, int numRedundantNodes, uint32_t* out, int64_t* out_last,
+                           int cap);
 const char* orc_last_error(void);
 int orc_cap_failed(void);      /* 1 once a capacity was exceeded (sticky until orc_clear_error) */
 void orc_clear_error(void);

@@ -96,6 +96,8 @@ def lib() -> C.CDLL:
             ("orc_chord_export_lists", [vp, vp, vp, vp], None),
             ("orc_kad_exhaustive_batch", [vp, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp, C.c_int], C.c_int),
             ("orc_kad_refresh_keys", [vp, vp, u64, vp, vp, vp, u64], u64),
+            ("orc_epichord_find_node", [vp, u32, u32, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp,
+                                        C.c_int, vp, u32, C.c_int64, C.c_int64, C.c_int, vp, vp, C.c_int], C.c_int),
             ("orc_kbrtest_lookup_stats", [vp, vp, vp, C.c_int, vp, vp, u64, C.c_double, C.c_int, C.c_double, vp],
              None),
         ]:
@@ -365,3 +367,27 @@ class OracleNet:
 
     def delay_ns(self, a: int, b: int, nbytes: int) -> int:
         return int(lib().orc_delay_ns(self._h, a, b, nbytes))
+
+
+def epichord_find_node(snap: dict, node: int, key, src: int, now: int, R: int, cap: int = 32):
+    """orc_epichord_find_node on a tests/epichord_snap.py snapshot: (status, nodes, lastUpdates);
+    status = the count, -1 the reference throws, -2 it dereferences an empty cache."""
+    L = lib()
+    o0, o1 = int(snap["cache_off"][node]), int(snap["cache_off"][node + 1])
+    cn = np.ascontiguousarray(snap["cache_node"][o0:o1])
+    cl = np.ascontiguousarray(snap["cache_last"][o0:o1])
+    ct = np.ascontiguousarray(snap["cache_ttl"][o0:o1])
+    succ = np.ascontiguousarray(snap["succ"][node])
+    pred = np.ascontiguousarray(snap["pred"][node])
+    k = np.ascontiguousarray(np.asarray(key, dtype=np.uint32).reshape(5))
+    out = np.full(cap, 0xFFFFFFFF, dtype=np.uint32)
+    last = np.full(cap, -1, dtype=np.int64)
+    ids = np.ascontiguousarray(snap["ids"], dtype=np.uint32)
+    r = L.orc_epichord_find_node(_p(ids), snap["n"], int(node), _p(succ), int(snap["nsucc"][node]), _p(pred),
+                                 int(snap["npred"][node]), int(snap["full"][node]), snap["L"], _p(cn), _p(cl), _p(ct),
+                                 o1 - o0, _p(k), int(src), int(now), int(snap["cache_ttl_param"]), int(R), _p(out),
+                                 _p(last), cap)
+    if r == -3 or r == -4:
+        raise ValueError(f"orc_epichord_find_node: bad input ({r})")
+    m = max(r, 0)
+    return r, out[:m].copy(), last[:m].copy()

@@ -733,3 +733,116 @@ class KadLookupSim:
         if self.hop_max and self.hops >= self.hop_max:
             return 3
         return 4
+
+
+# --- EpiChord::findNode on one routing snapshot ---------------------------------
+def epichord_find_node(keys, self_i, succ, pred, full_bits, list_size, cache, key, src, now, cache_ttl, R):
+    """EpiChord.cc:517-629 served by node self_i, written from the reference independently of
+    oracle/ovs_oracle_epichord.c: Python ints, the finger cache as a dict node -> [lastUpdate, ttl],
+    the node lists as plain Python lists ordered by ring offset, and findBestHops as a walk over the
+    live nodes sorted by clockwise distance from self + 1 (EpiChordFingerCache.cc:309-356).
+
+    keys: list of int node keys; succ / pred: node indices closest first; full_bits: bit 0 / 1 =
+    successorList / predecessorList->isFull(); cache: {node: (lastUpdate, ttl)}; src None = a local
+    call.  Returns (status, [(node, lastUpdate)]): status 0 ok, -1 the reference throws, -2 it
+    dereferences an empty cache."""
+    me = keys[self_i]
+    cache = {x: [lu, ttl] for x, (lu, ttl) in cache.items()}
+
+    def off_fwd(x):      # succ map key + 1
+        return (keys[x] - me) % M
+
+    def off_bwd(x):
+        return (me - keys[x]) % M
+
+    # nodeMaps: real entries, plus thisNode (offset 0 -> key M - 1, the largest) when not full
+    lists = {"succ": [list(succ), not (full_bits & 1), off_fwd], "pred": [list(pred), not (full_bits & 2), off_bwd]}
+
+    def upd(x, lu, ttl):                 # EpiChordFingerCache::updateFinger 79-127
+        if x is None or x == self_i:
+            return
+        if x in cache:
+            e = cache[x]
+            e[0] = max(e[0], lu)
+            if e[1] > 0 and (ttl > e[1] or ttl == 0):
+                e[1] = ttl
+        else:
+            cache[x] = [lu, ttl]
+
+    def last_of(name):                   # getNode(getSize() - 1)
+        ent, has_self, _ = lists[name]
+        return self_i if has_self else ent[-1]
+
+    def add(name, x):                    # EpiChordNodeList::addNode(x, resize = true) 108-161
+        ent, has_self, off = lists[name]
+        if x not in ent:
+            ent.append(x)
+            ent.sort(key=off)
+        upd(x, now, 0)
+        if len(ent) + (1 if has_self else 0) > list_size:
+            if has_self:                 # thisNode has the largest offset: it goes first
+                lists[name][1] = False
+            else:
+                gone = ent.pop()
+                if gone in cache:        # setFingerTTL(gone) with the cache's ttl
+                    cache[gone][1] = cache_ttl
+
+    excl = {self_i}
+    if src is not None:
+        excl.add(src)
+        upd(src, now, cache_ttl)         # receiveNewNode 1178-1209, direct
+        for name, inside in (("succ", lambda x: between(keys[x], me, keys[last_of("succ")])),
+                             ("pred", lambda x: between(keys[x], keys[last_of("pred")], me))):
+            ent, has_self, _ = lists[name]
+            contains = src in ent or (has_self and src == self_i)
+            if not contains and (has_self or inside(src)):
+                add(name, src)
+    s_ent, p_ent = lists["succ"][0], lists["pred"][0]
+    succ0 = s_ent[0] if s_ent else self_i
+    pred0 = p_ent[0] if p_ent else self_i
+    out = []
+    if not p_ent:
+        sib = (not s_ent) or key == me
+    else:
+        sib = between_r(key, keys[pred0], me)
+    if sib:
+        out.append((self_i, now))
+        if p_ent:
+            out.append((pred0, cache[pred0][0] if pred0 in cache else now))
+        if s_ent:
+            out.append((succ0, cache[succ0][0] if succ0 in cache else now))
+        return 0, out
+    if src is None:
+        def rd(a, b):
+            return min((a - b) % M, (b - a) % M)
+        choice = pred0 if rd(keys[pred0], key) < rd(keys[succ0], key) else succ0
+    elif between(me, keys[src], key):
+        choice = succ0
+    else:
+        choice = pred0
+    if choice in cache:
+        out.append((choice, cache[choice][0]))
+        excl.add(choice)
+    live = sorted((x for x, (lu, ttl) in cache.items() if not (ttl > 0 and lu + ttl < now)),
+                  key=lambda x: (keys[x] - me - 1) % M)
+    if not live:
+        return -2, out
+    target = (key - me - 1) % M
+    pos = next((i for i, x in enumerate(live) if (keys[x] - me - 1) % M >= target), 0)
+    # forward to the first live node not excluded (at most once round the ring)
+    for step in range(len(live)):
+        j = (pos + step) % len(live)
+        if live[j] not in excl:
+            break
+    else:
+        return (0 if out else -1), out
+    # then backwards from it, R nodes not excluded, at most once round
+    taken = 0
+    for step in range(len(live)):
+        x = live[(j - step) % len(live)]
+        if taken >= R:
+            break
+        if x not in excl:
+            out.append((x, cache[x][0]))
+            taken += 1
+    return (0 if out else -1), out
