@@ -16,6 +16,7 @@
  *   LookupListener::lookupFinished src/common/LookupListener.h, BaseOverlay.cc:1241-1307
  *   SimpleNodeEntry::calcDelay     src/underlay/simpleunderlay/SimpleNodeEntry.cc:155-195
  *   Kademlia bucket refresh        src/overlay/kademlia/Kademlia.cc:1591-1686 (exhaustive lookups)
+ *   EpiChord::findNode             src/overlay/epichord/EpiChord.cc:517-629 (per call, on a snapshot)
  *   .ini parameter binding         simulations/default.ini (same key names)
  *
  * Plain C: no C++ exceptions cross this boundary, no torch types.  Every call
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 7
+#define OVS_ABI_VERSION 8
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -68,7 +69,7 @@ enum {
                                     throws (Koorde.cc:490-493 bounding error, 756-760 invalid start key) */
 };
 
-enum { OVS_OVERLAY_CHORD = 1, OVS_OVERLAY_KADEMLIA = 2, OVS_OVERLAY_KOORDE = 3 };
+enum { OVS_OVERLAY_CHORD = 1, OVS_OVERLAY_KADEMLIA = 2, OVS_OVERLAY_KOORDE = 3, OVS_OVERLAY_EPICHORD = 4 };
 
 /* flags */
 #define OVS_DEVICE_PTRS  0x1u   /* buffers are device pointers; call is async on `stream` */
@@ -114,6 +115,8 @@ typedef struct ovs_params {
     int32_t deBruijnListSize;           /* **.koorde.deBruijnListSize = 16 */
     int32_t useOtherLookup;             /* **.koorde.useOtherLookup = true */
     int32_t useSucList;                 /* **.koorde.useSucList = true */
+    int32_t pad0;
+    double  cacheTTL;                   /* **.epichord.cacheTTL = 120 s (ABI 8) */
 } ovs_params;
 
 /* Result of one one-way KBR test lookup (KBRTestApp with kbrOneWayTest). */
@@ -194,6 +197,39 @@ typedef struct ovs_koorde_ext {
  * throws.  Host buffers. */
 ovs_status  ovs_koorde_find_node_batch(ovs_ctx* ctx, const uint32_t* node, const ovs_key160* keys,
                                        ovs_koorde_ext* ext, uint32_t* next, uint64_t n);
+/* EpiChord (src/overlay/epichord/): one snapshot of every node's routing state, for
+ * ovs_epichord_find_node_batch.  EpiChord's finger cache is rewritten by every message a node
+ * sends or receives (EpiChord.cc:546-553, 754-780), so the engine does not route EpiChord lookups
+ * in batches; it answers findNode calls exactly against a given state.  Per node v:
+ * succ[v*L ..] / pred[v*L ..] (L = successorListSize <= 16): the EpiChordNodeList entries closest
+ * first, nsucc[v] / npred[v] of them; lists_full[v] bit 0 / bit 1 = successorList /
+ * predecessorList->isFull() (when clear, thisNode ends the list, so it has fewer than L entries);
+ * the live finger cache (EpiChordFingerCache::liveCache) as cache_node / cache_last_ns (lastUpdate)
+ * / cache_ttl_ns (ttl, 0 = never expires) entries cache_off[v] .. cache_off[v+1], any order, each
+ * node at most once and never v itself.  The dead cache is not needed: a FindNodeCall's source is
+ * heard from directly, which removes it from the dead cache before anything reads it.  Host
+ * buffers; params.overlay must be OVS_OVERLAY_EPICHORD. */
+ovs_status  ovs_epichord_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n, const double* xy,
+                              const uint32_t* succ, const uint8_t* nsucc, const uint32_t* pred,
+                              const uint8_t* npred, const uint8_t* lists_full, const uint64_t* cache_off,
+                              const uint32_t* cache_node, const int64_t* cache_last_ns,
+                              const int64_t* cache_ttl_ns, uint32_t flags);
+/* EpiChord::findNode(keys[i], numRedundantNodes, 1, FindNodeCall from src[i]) at node[i] at
+ * simulated time now_ns[i], each call on the loaded snapshot with the side effects the reference
+ * applies before it answers (the source enters the finger cache and, where it fits, the node lists,
+ * whose resize may put an evicted member under cacheTTL; EpiChord.cc:1178-1209).  src[i] =
+ * 0xFFFFFFFF is a local call (msg == NULL).  out_nodes / out_last_ns: max_out slots per call
+ * (max_out >= max(3, 1 + numRedundantNodes), 0xFFFFFFFF / -1 padded): the next hops and the
+ * lastUpdates the EpiChordFindNodeExtMessage carries; out_count the count; out_status 0 =
+ * answered, 1 = the reference throws "Failed to find node" (613-614), 2 = the reference
+ * dereferences an empty finger cache (EpiChordFingerCache.cc:317-322, undefined), 3 = node or
+ * source index outside the network (device-pointer calls; host calls return OVS_EINVAL).  Buffers
+ * follow `flags`. */
+ovs_status  ovs_epichord_find_node_batch(ovs_ctx* ctx, const uint32_t* node, const ovs_key160* keys,
+                                         const uint32_t* src, const int64_t* now_ns, uint64_t n,
+                                         int32_t numRedundantNodes, uint32_t* out_nodes, int64_t* out_last_ns,
+                                         uint32_t max_out, uint8_t* out_count, uint8_t* out_status,
+                                         uint32_t flags, void* stream);
 /* copy the device Kademlia tables out (host buffers): siblings[n*5s],
  * bucket_count[n*160], bucket_nodes[n*160*k] (0xFFFFFFFF padded) */
 ovs_status  ovs_kad_export(ovs_ctx* ctx, uint32_t* siblings, uint8_t* bucket_count,

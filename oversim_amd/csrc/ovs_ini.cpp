@@ -239,7 +239,8 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
     };
 
     const std::string ov = p->overlay == OVS_OVERLAY_KADEMLIA ? "kademlia"
-                           : p->overlay == OVS_OVERLAY_KOORDE ? "koorde" : "chord";
+                           : p->overlay == OVS_OVERLAY_KOORDE ? "koorde"
+                           : p->overlay == OVS_OVERLAY_EPICHORD ? "epichord" : "chord";
     const std::string host = "SimpleUnderlayNetwork.overlayTerminal[0]";
     const std::string ovp = host + ".overlay." + ov + ".";
     std::string v, bad;
@@ -262,6 +263,9 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
             want_bool("useOtherLookup", &p->useOtherLookup);
             want_bool("useSucList", &p->useSucList);
         }
+    } else if (p->overlay == OVS_OVERLAY_EPICHORD) {   // EpiChord.ned, default.ini:145-164
+        want_int("successorListSize", &p->successorListSize);
+        if (lookup(ovp + "cacheTTL", &v) && !to_seconds(unquote(v), &p->cacheTTL)) bad = "cacheTTL";
     } else {
         want_int("k", &p->k);
         want_int("s", &p->s);
@@ -366,11 +370,17 @@ extern "C" void ovs_params_default(int32_t overlay, ovs_params* p)
     p->deBruijnListSize = 16;           // default.ini:276
     p->useOtherLookup = 1;              // default.ini:279
     p->useSucList = 1;                  // default.ini:280
+    p->cacheTTL = 120.0;                // default.ini:158
     if (overlay == OVS_OVERLAY_KOORDE) p->successorListSize = 16;   // default.ini:275
+    if (overlay == OVS_OVERLAY_EPICHORD) p->successorListSize = 4;  // default.ini:159
     if (overlay == OVS_OVERLAY_KADEMLIA) {
         p->lookupRedundantNodes = 8;    // default.ini:186
         p->lookupParallelRpcs = 3;      // default.ini:188
         p->lookupMerge = 1;             // default.ini:189
+    } else if (overlay == OVS_OVERLAY_EPICHORD) {
+        p->lookupRedundantNodes = 3;    // default.ini:146
+        p->lookupParallelRpcs = 1;      // default.ini:148
+        p->lookupMerge = 1;             // default.ini:149
     } else {
         p->lookupRedundantNodes = 1;    // default.ini:423
         p->lookupParallelRpcs = 1;      // default.ini:425

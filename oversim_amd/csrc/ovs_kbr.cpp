@@ -13,8 +13,10 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
+#include "epichord.hpp"
 #include "kad.hpp"
 #include "kad_shard.hpp"
 #include "koorde.hpp"
@@ -62,6 +64,8 @@ struct ovs_ctx {
     KadTables kad{};
     // koorde (on the sorted ring in recs / xy)
     KoordeTables koorde{};
+    // epichord routing snapshot (ovs_epichord_load)
+    EpiTables epi{};
     uint32_t* kvis = nullptr;            // K3's per-lookup responder lists when no hop_seq is asked for
     uint64_t kvis_cap = 0;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
@@ -111,6 +115,7 @@ void free_tables(ovs_ctx* c)
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
     koorde_free(c->koorde);
+    epichord_free(c->epi);
     if (c->kvis) hipFree(c->kvis);
     c->kvis = nullptr; c->kvis_cap = 0;
     c->overlay = 0; c->n = 0; c->nfing = 0;
@@ -372,6 +377,8 @@ ovs_status ovs_set_params(ovs_ctx* c, const ovs_params* p)
          p->deBruijnListSize != c->P.deBruijnListSize || p->useOtherLookup != c->P.useOtherLookup ||
          p->useSucList != c->P.useSucList))
         return fail(c, OVS_ESTATE, "the Koorde ring parameters are fixed once a Koorde network is loaded");
+    if (c->overlay == OVS_OVERLAY_EPICHORD && p->successorListSize != c->P.successorListSize)
+        return fail(c, OVS_ESTATE, "successorListSize is fixed once an EpiChord snapshot is loaded");
     c->P = *p;
     return OVS_OK;
 }
@@ -1046,11 +1053,166 @@ ovs_status ovs_koorde_find_node_batch(ovs_ctx* c, const uint32_t* node, const ov
     return OVS_OK;
 }
 
+ovs_status ovs_epichord_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy, const uint32_t* succ,
+                             const uint8_t* nsucc, const uint32_t* pred, const uint8_t* npred, const uint8_t* lists_full,
+                             const uint64_t* cache_off, const uint32_t* cache_node, const int64_t* cache_last_ns,
+                             const int64_t* cache_ttl_ns, uint32_t flags)
+{
+    if (!c || !ids || !xy || !succ || !nsucc || !pred || !npred || !lists_full || !cache_off) return OVS_EINVAL;
+    if (flags & OVS_DEVICE_PTRS) return fail(c, OVS_ENOTSUP, "ovs_epichord_load takes host buffers");
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    free_kad_shard(c);
+    if (c->P.overlay != OVS_OVERLAY_EPICHORD) return fail(c, OVS_ESTATE, "params.overlay is not EpiChord");
+    const int L = c->P.successorListSize;
+    if (L < 1 || L > EPI_MAXL) return fail(c, OVS_ENOTSUP, "EpiChord successorListSize must be 1..16");
+    if (!(c->P.cacheTTL >= 0)) return fail(c, OVS_EINVAL, "cacheTTL must be >= 0");
+    if (n < 2 || n >= 0xFFFFFFFFull) return fail(c, OVS_EINVAL, "node count out of range");
+    const K160* keys = reinterpret_cast<const K160*>(ids);
+    for (uint64_t v = 1; v < n; ++v)
+        if (!k_lt(keys[v - 1], keys[v])) return fail(c, OVS_EINVAL, "node ids must be sorted ascending and unique");
+    const K160 one{{1, 0, 0, 0, 0}}, zero{{0, 0, 0, 0, 0}};
+    auto node_err = [&](uint64_t v, const char* what) {
+        return fail(c, OVS_EINVAL, "EpiChord snapshot, node " + std::to_string(v) + ": " + what);
+    };
+    std::vector<uint32_t> meta(n);
+    for (uint64_t v = 0; v < n; ++v) {
+        const int ns = nsucc[v], np = npred[v], full = lists_full[v] & 3;
+        const int cnt[2] = {ns, np};
+        const uint32_t* lst[2] = {succ + v * L, pred + v * L};
+        for (int l = 0; l < 2; ++l) {
+            // EpiChordNodeList (EpiChordNodeList.cc:56-161): thisNode stays in the map (last) until
+            // the list holds nodeListSize other nodes; isFull() is its absence
+            const bool isfull = (full >> l) & 1;
+            if (cnt[l] > L) return node_err(v, "more list entries than successorListSize");
+            if (isfull ? cnt[l] == 0 : cnt[l] == L) return node_err(v, "isFull() inconsistent with the list length");
+            K160 prev{};
+            for (int i = 0; i < cnt[l]; ++i) {
+                const uint32_t x = lst[l][i];
+                if (x >= n || x == v) return node_err(v, "list entry is not another node");
+                K160 off = k_sub(keys[x], keys[v]);
+                if (l == 1) off = k_sub(zero, off);
+                if (i && !k_lt(prev, off)) return node_err(v, "list entries not closest first / repeated");
+                prev = off;
+            }
+        }
+        meta[v] = (uint32_t)ns | ((uint32_t)np << 8) | ((uint32_t)full << 16);
+    }
+    if (cache_off[0] != 0) return fail(c, OVS_EINVAL, "cache_off[0] must be 0");
+    const uint64_t E = cache_off[n];
+    if (E && (!cache_node || !cache_last_ns || !cache_ttl_ns)) return OVS_EINVAL;
+    std::vector<uint32_t> cn(E);
+    std::vector<int64_t> cl(E), ct(E);
+    std::vector<uint64_t> perm;
+    std::vector<K160> sums;
+    for (uint64_t v = 0; v < n; ++v) {
+        const uint64_t a = cache_off[v], b = cache_off[v + 1];
+        if (b < a || b > E) return node_err(v, "cache_off not monotone");
+        // liveCache order: x - (thisNode + 1) (EpiChordFingerCache.cc:85, 117-126)
+        const K160 base = k_add(keys[v], one);
+        perm.resize(b - a);
+        sums.resize(b - a);
+        for (uint64_t i = a; i < b; ++i) {
+            const uint32_t x = cache_node[i];
+            if (x >= n || x == v) return node_err(v, "cache entry is not another node");
+            if (cache_ttl_ns[i] < 0) return node_err(v, "negative cache ttl");
+            perm[i - a] = i;
+            sums[i - a] = k_sub(keys[x], base);
+        }
+        std::sort(perm.begin(), perm.end(), [&](uint64_t p, uint64_t q) { return k_lt(sums[p - a], sums[q - a]); });
+        for (uint64_t i = 0; i < b - a; ++i) {
+            const uint64_t j = perm[i];
+            if (i && cache_node[j] == cn[a + i - 1]) return node_err(v, "a node twice in the finger cache");
+            cn[a + i] = cache_node[j]; cl[a + i] = cache_last_ns[j]; ct[a + i] = cache_ttl_ns[j];
+        }
+    }
+    ovs_status st = upload_nodes(c, ids, n, xy, false);
+    if (st != OVS_OK) { free_tables(c); return st; }
+    EpiTables& T = c->epi;
+    T.n = (uint32_t)n;
+    T.L = L;
+    T.nent = E;
+    auto up = [&](auto** d, const auto* h, uint64_t cnt) -> hipError_t {
+        using TT = std::remove_pointer_t<std::remove_reference_t<decltype(*d)>>;
+        hipError_t e = hipMalloc((void**)d, sizeof(TT) * (cnt ? cnt : 1));
+        if (e == hipSuccess && cnt) e = hipMemcpyAsync(*d, h, sizeof(TT) * cnt, hipMemcpyHostToDevice, c->stream);
+        return e;
+    };
+    hipError_t e = up(&T.succ, succ, n * L);
+    if (e == hipSuccess) e = up(&T.pred, pred, n * L);
+    if (e == hipSuccess) e = up(&T.meta, meta.data(), n);
+    if (e == hipSuccess) e = up(&T.coff, cache_off, n + 1);
+    if (e == hipSuccess) e = up(&T.cnode, cn.data(), E);
+    if (e == hipSuccess) e = up(&T.clast, cl.data(), E);
+    if (e == hipSuccess) e = up(&T.cttl, ct.data(), E);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "EpiChord snapshot upload"); }
+    c->overlay = OVS_OVERLAY_EPICHORD;
+    return OVS_OK;
+}
+
+ovs_status ovs_epichord_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key160* keys, const uint32_t* src,
+                                        const int64_t* now_ns, uint64_t n, int32_t numRedundantNodes,
+                                        uint32_t* out_nodes, int64_t* out_last_ns, uint32_t max_out, uint8_t* out_count,
+                                        uint8_t* out_status, uint32_t flags, void* stream)
+{
+    if (!c || (n && (!node || !keys || !src || !now_ns || !out_nodes || !out_last_ns || !out_count || !out_status)))
+        return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_EPICHORD) return fail(c, OVS_ESTATE, "no EpiChord snapshot loaded");
+    if (numRedundantNodes < 0 || numRedundantNodes > EPI_MAXR)
+        return fail(c, OVS_EINVAL, "numRedundantNodes must be 0..32");
+    if (max_out < 3 || max_out < (uint32_t)(1 + numRedundantNodes))
+        return fail(c, OVS_EINVAL, "max_out must be >= max(3, 1 + numRedundantNodes)");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool dev = flags & OVS_DEVICE_PTRS;
+    hipStream_t s = dev ? (hipStream_t)stream : c->stream;
+    if (n == 0) return OVS_OK;
+    if (!dev) {
+        for (uint64_t i = 0; i < n; ++i)
+            if (node[i] >= c->n || (src[i] != NONE && src[i] >= c->n))
+                return fail(c, OVS_EINVAL, "node / source index out of range");
+    }
+    uint32_t *dn = nullptr, *dsrc = nullptr, *dout = nullptr;
+    K160* dk = nullptr;
+    int64_t *dnow = nullptr, *dlast = nullptr;
+    uint8_t *dc = nullptr, *dst = nullptr;
+    bool o1, o2, o3, o4;
+    ovs_status st = to_device(c, node, n, dev, &dn, &o1);
+    if (st == OVS_OK) st = to_device(c, reinterpret_cast<const K160*>(keys), n, dev, &dk, &o2);
+    if (st == OVS_OK) st = to_device(c, src, n, dev, &dsrc, &o3);
+    if (st == OVS_OK) st = to_device(c, now_ns, n, dev, &dnow, &o4);
+    if (st != OVS_OK) return st;
+    if (!dev) {
+        HIPCHK(c, hipMalloc(&dout, sizeof(uint32_t) * n * max_out));
+        HIPCHK(c, hipMalloc(&dlast, sizeof(int64_t) * n * max_out));
+        HIPCHK(c, hipMalloc(&dc, n));
+        HIPCHK(c, hipMalloc(&dst, n));
+    } else {
+        dout = out_nodes; dlast = out_last_ns; dc = out_count; dst = out_status;
+    }
+    const int64_t ttl = simtime_host(c->P.cacheTTL, c->P.simtimeRound);
+    hipError_t e = epichord_find_node(c->epi, c->recs, dn, dk, dsrc, dnow, n, numRedundantNodes, ttl, dout, dlast,
+                                      max_out, dc, dst, s);
+    if (e != hipSuccess) return hip_fail(c, e, "EpiChord findNode kernel");
+    if (!dev) {
+        HIPCHK(c, hipMemcpyAsync(out_nodes, dout, sizeof(uint32_t) * n * max_out, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(out_last_ns, dlast, sizeof(int64_t) * n * max_out, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(out_count, dc, n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(out_status, dst, n, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        hipFree(dn); hipFree(dk); hipFree(dsrc); hipFree(dnow); hipFree(dout); hipFree(dlast); hipFree(dc); hipFree(dst);
+    }
+    return OVS_OK;
+}
+
 ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                            ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs, uint32_t flags, void* stream)
 {
     if (!c || (!keys && n) || (!src && n) || (!out && n)) return OVS_EINVAL;
     if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
+    if (c->overlay == OVS_OVERLAY_EPICHORD)
+        return fail(c, OVS_ENOTSUP, "EpiChord lookups rewrite the caches they route over (DESIGN.md §9): "
+                                    "ovs_epichord_find_node_batch only");
     ovs_status st = check_common(c, c->P);
     if (st != OVS_OK) return st;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1170,6 +1332,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
     if (c->overlay == OVS_OVERLAY_KOORDE)
         return fail(c, OVS_ENOTSUP, "Koorde: ovs_route_batch and ovs_koorde_find_node_batch only");
+    if (c->overlay == OVS_OVERLAY_EPICHORD)
+        return fail(c, OVS_ENOTSUP, "EpiChord: ovs_epichord_find_node_batch only");
     const bool chord = c->overlay == OVS_OVERLAY_CHORD;
     // BaseOverlay::lookupRpc: numSiblings < 0 -> getMaxNumSiblings() (Chord.cc getMaxNumSiblings =
     // successorListSize, Kademlia.cc:347-350 = s); isSiblingFor rejects larger values
@@ -1402,6 +1566,8 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
     if (!c->overlay) return fail(c, OVS_ESTATE, "no network loaded");
     if (c->overlay == OVS_OVERLAY_KOORDE)
         return fail(c, OVS_ENOTSUP, "Koorde: ovs_route_batch and ovs_koorde_find_node_batch only");
+    if (c->overlay == OVS_OVERLAY_EPICHORD)
+        return fail(c, OVS_ENOTSUP, "EpiChord: ovs_epichord_find_node_batch only");
     if (numSiblings > (c->overlay == OVS_OVERLAY_CHORD ? c->P.successorListSize : c->P.s))
         return fail(c, OVS_EINVAL, "numSiblings too big!");
     if (numRedundantNodes < 1 || numRedundantNodes > 64) return fail(c, OVS_EINVAL, "numRedundantNodes out of range");

@@ -34,6 +34,7 @@ _LIB_PATH = Path(os.environ.get("OVS_LIB") or Path(__file__).resolve().parent / 
 OVERLAY_CHORD = 1
 OVERLAY_KADEMLIA = 2
 OVERLAY_KOORDE = 3
+OVERLAY_EPICHORD = 4
 DEVICE_PTRS = 0x1
 NONE = 0xFFFFFFFF
 
@@ -64,7 +65,7 @@ class Params(C.Structure):
         ("jitter", C.c_double), ("constantDelay", C.c_double), ("datarate", C.c_double),
         ("accessDelay", C.c_double), ("kadSeed", C.c_uint64),
         ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
-        ("useSucList", C.c_int32),
+        ("useSucList", C.c_int32), ("pad0", C.c_int32), ("cacheTTL", C.c_double),
     ]
 
     @classmethod
@@ -84,6 +85,10 @@ class Params(C.Structure):
     @classmethod
     def koorde(cls) -> "Params":
         return cls.default(OVERLAY_KOORDE)
+
+    @classmethod
+    def epichord(cls) -> "Params":
+        return cls.default(OVERLAY_EPICHORD)
 
     @classmethod
     def from_ini(cls, text: str, config: str | None = None, overlay: int = OVERLAY_CHORD,
@@ -193,6 +198,8 @@ def lib() -> C.CDLL:
         "ovs_koorde_export": ([vp, vp, vp, vp], C.c_int),
         "ovs_koorde_find_node_batch": ([vp, vp, vp, vp, vp, u64], C.c_int),
         "ovs_kad_load_tables": ([vp, vp, u64, vp, vp, vp, vp, u32], C.c_int),
+        "ovs_epichord_load": ([vp, vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32], C.c_int),
+        "ovs_epichord_find_node_batch": ([vp, vp, vp, vp, vp, u64, i32, vp, vp, u32, vp, vp, u32, vp], C.c_int),
         "ovs_kad_export": ([vp, vp, vp, vp], C.c_int),
         "ovs_chord_export_fingers": ([vp, vp], C.c_int),
         "ovs_route_batch": ([vp, vp, vp, u64, vp, vp, vp, u32, vp], C.c_int),
@@ -371,6 +378,38 @@ class KbrEngine:
         self._chk(self._L.ovs_koorde_find_node_batch(self._h, _ptr(node), _ptr(keys), _ptr(ext), _ptr(nxt), n),
                   "ovs_koorde_find_node_batch")
         return nxt, ext
+
+    def epichord_load(self, ids, xy, succ, nsucc, pred, npred, lists_full, cache_off, cache_node, cache_last_ns,
+                      cache_ttl_ns):
+        """One EpiChord routing snapshot (ovs_epichord_load): successor / predecessor lists (n, L) closest
+        first with their lengths and isFull() bits, the live finger caches as CSR rows (node, lastUpdate,
+        ttl in ns).  params.overlay must be OVERLAY_EPICHORD."""
+        ids = keys_array(ids)
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+                ((xy, np.float64), (succ, np.uint32), (nsucc, np.uint8), (pred, np.uint32), (npred, np.uint8),
+                 (lists_full, np.uint8), (cache_off, np.uint64), (cache_node, np.uint32),
+                 (cache_last_ns, np.int64), (cache_ttl_ns, np.int64))]
+        self._chk(self._L.ovs_epichord_load(self._h, _ptr(ids), len(ids), *[_ptr(a) for a in arrs], 0),
+                  "ovs_epichord_load")
+        self.n, self.overlay = len(ids), OVERLAY_EPICHORD
+
+    def epichord_find_node(self, node, keys, src, now_ns, numRedundantNodes: int, max_out: int | None = None):
+        """EpiChord::findNode per call (ovs_epichord_find_node_batch): src NONE = a local call.  Returns
+        (nodes (n, max_out), lastUpdates (n, max_out), count, status)."""
+        node = np.ascontiguousarray(node, dtype=np.uint32)
+        keys = keys_array(keys)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        now = np.ascontiguousarray(now_ns, dtype=np.int64)
+        n = len(node)
+        mo = max_out or max(3, 1 + numRedundantNodes)
+        out = np.empty((n, mo), dtype=np.uint32)
+        last = np.empty((n, mo), dtype=np.int64)
+        cnt = np.empty(n, dtype=np.uint8)
+        st = np.empty(n, dtype=np.uint8)
+        self._chk(self._L.ovs_epichord_find_node_batch(self._h, _ptr(node), _ptr(keys), _ptr(src), _ptr(now), n,
+                                                       numRedundantNodes, _ptr(out), _ptr(last), mo, _ptr(cnt),
+                                                       _ptr(st), 0, None), "ovs_epichord_find_node_batch")
+        return out, last, cnt, st
 
     def kad_load_device(self, ids_ptr: int, xy_ptr: int, n: int):
         self._chk(self._L.ovs_kad_load(self._h, C.c_void_p(ids_ptr), n, C.c_void_p(xy_ptr), DEVICE_PTRS),

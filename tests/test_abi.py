@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 15
     for s in sorted(syms):
         assert hasattr(L, s), f"{s} declared in include/ but not exported"
-    assert L.ovs_abi_version() == 7
+    assert L.ovs_abi_version() == 8
 
 
 def test_params_default_matches_default_ini():
@@ -37,6 +37,23 @@ def test_params_default_matches_default_ini():
     assert p.rpcUdpTimeout == 1.5 and p.lookupTimeout == 10.0 and p.datarate == 10e6
     k = Params.kademlia()
     assert (k.k, k.s, k.b, k.lookupRedundantNodes, k.lookupParallelRpcs, k.lookupMerge) == (8, 8, 1, 8, 3, 1)
+    e = Params.epichord()    # default.ini:145-164
+    assert (e.successorListSize, e.cacheTTL, e.lookupRedundantNodes, e.lookupParallelRpcs, e.lookupMerge) == \
+        (4, 120.0, 3, 1, 1)
+
+
+def test_epichord_params_from_ini():
+    """**.overlay*.epichord.* keys bind for the EpiChord overlay (EpiChord.ned names)."""
+    from oversim_amd import Params
+    from oversim_amd.kbr import OVERLAY_EPICHORD
+    ini = """
+[General]
+**.overlay*.epichord.cacheTTL = 60s
+**.overlay*.epichord.successorListSize = 6
+**.overlay*.chord.successorListSize = 8
+"""
+    p = Params.from_ini(ini, overlay=OVERLAY_EPICHORD)
+    assert (p.successorListSize, p.cacheTTL) == (6, 60.0)
 
 
 def test_params_from_reference_default_ini_text():
