@@ -18,6 +18,8 @@
 #include "engine.hpp"
 #include "launch.hpp"
 
+#include <cstdio>
+
 namespace ovs {
 
 // ---------------------------------------------------------------------------
@@ -484,6 +486,12 @@ struct LaneIO {
     uint8_t* __restrict__ stag;            // arc of the hand-off, or nsh: finished
 };
 
+#ifdef OVS_CHORD_STATS
+// lines consumed by kind: [0] FETCH, [1] START, [2] NODE, [3] first probe of a hop, [4] a further probe
+// (the finger at msb(D) overshot K), [5] WIN
+__device__ unsigned long long g_k1_stats[8];
+#endif
+
 // LKC: a LookupCall batch (ovs_lookup_batch): the responsible node's larger answer, no route message
 template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
 __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
@@ -566,6 +574,16 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
             bool nxt_sib = false;
             lp = nullptr;
 
+#ifdef OVS_CHORD_STATS
+            {   // line accounting (diagnostic build, tools/diag): which kind of line each lane consumes
+                const K160 Dd = k_sub(K, C);
+                const bool reprobe = ph == PH_PROBE && !gTx && pi < k_msb(Dd);
+                const uint64_t b[6] = {__ballot(ph == PH_FETCH), __ballot(ph == PH_START), __ballot(ph == PH_NODE),
+                                       __ballot(ph == PH_PROBE && !reprobe), __ballot(reprobe), __ballot(ph == PH_WIN)};
+                if (lane == __ffsll((long long)__ballot(1)) - 1)
+                    for (int k = 0; k < 6; ++k) atomicAdd(&g_k1_stats[k], (unsigned long long)__popcll(b[k]));
+            }
+#endif
             // ---- consume the pending line
             if (ph == PH_FETCH) {
                 if (SHARD) {
@@ -1019,8 +1037,18 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
     static int bpc = 0;
     uint64_t blocks = 0;
     io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD, LKC>, &bpc, io.n, num_cu, &blocks);
+#ifdef OVS_CHORD_STATS
+    unsigned long long z[8] = {};
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_k1_stats), z, sizeof z, 0, hipMemcpyHostToDevice, s);
+#endif
     hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD, LKC>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC,
                        io);
+#ifdef OVS_CHORD_STATS
+    hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_k1_stats), sizeof z, 0, hipMemcpyDeviceToHost, s);
+    hipStreamSynchronize(s);
+    fprintf(stderr, "k1stats n=%llu fetch=%llu start=%llu node=%llu probe1=%llu reprobe=%llu win=%llu\n",
+            (unsigned long long)io.n, z[0], z[1], z[2], z[3], z[4], z[5]);
+#endif
     return hipGetLastError();
 }
 

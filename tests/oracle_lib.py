@@ -369,10 +369,11 @@ class OracleNet:
         return int(lib().orc_delay_ns(self._h, a, b, nbytes))
 
 
-def epichord_find_node(snap: dict, node: int, key, src: int, now: int, R: int, cap: int = 32):
+def epichord_find_node(snap: dict, node: int, key, src: int, now: int, R: int, cap: int | None = None):
     """orc_epichord_find_node on a tests/epichord_snap.py snapshot: (status, nodes, lastUpdates);
     status = the count, -1 the reference throws, -2 it dereferences an empty cache."""
     L = lib()
+    cap = cap or max(3, 1 + R)
     o0, o1 = int(snap["cache_off"][node]), int(snap["cache_off"][node + 1])
     cn = np.ascontiguousarray(snap["cache_node"][o0:o1])
     cl = np.ascontiguousarray(snap["cache_last"][o0:o1])
