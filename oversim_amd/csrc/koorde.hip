@@ -12,12 +12,16 @@
 // wave's slice of the batch (ballot + popcount); the grid is persistent.
 #include "koorde.hpp"
 
+#include <cstdlib>
+
 namespace ovs {
 
 void koorde_free(KoordeTables& t)
 {
     if (t.nd) hipFree(t.nd);
+    if (t.rec) hipFree(t.rec);
     t.nd = nullptr;
+    t.rec = nullptr;
     t.n = 0;
 }
 
@@ -90,6 +94,7 @@ __device__ __forceinline__ uint32_t walk_list(const KeyRec* __restrict__ recs, u
 struct KView {
     const KeyRec* __restrict__ recs;
     const KoordeNode* __restrict__ nd;
+    const KoordeRec* __restrict__ rec;
     uint32_t n;
     int ns, sb, useOther, useSuc;
 };
@@ -167,6 +172,190 @@ __device__ uint32_t koorde_find_node_dev(const KView& V, uint32_t c, const K160&
     return NONE;
 }
 
+// ---------------------------------------------------------------------------
+// Record form (KoordeRec): the same findNode with every ring distance the reference compares
+// decided from the 32-bit codes of the responder's record, the exact keys read only on a code tie.
+// A hop then reads the responder's 128 B record and, on the de Bruijn step, the record of the de
+// Bruijn list's first node: two dependent loads instead of the list bisections' chain of probes.
+
+__device__ __forceinline__ uint32_t code32(const K160& v) { return (uint32_t)(k_code64(v) >> 32); }
+
+struct KRec {
+    K160 k;
+    uint32_t cP, db, dbStart, dbNum;
+    double x, y;
+    uint32_t sum[KREC_LIST];
+};
+
+__device__ __forceinline__ KRec load_krec(const KoordeRec* __restrict__ rec, uint32_t i)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(rec + i);
+    uint4 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = p[j];
+    KRec r;
+    r.k.w[0] = q[0].x; r.k.w[1] = q[0].y; r.k.w[2] = q[0].z; r.k.w[3] = q[0].w; r.k.w[4] = q[1].x;
+    r.cP = q[1].y; r.db = q[1].z; r.dbStart = q[1].w; r.dbNum = q[2].x;
+    r.x = __hiloint2double((int)q[2].w, (int)q[2].z);
+    r.y = __hiloint2double((int)q[3].y, (int)q[3].x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        r.sum[4 * j] = q[4 + j].x; r.sum[4 * j + 1] = q[4 + j].y; r.sum[4 * j + 2] = q[4 + j].z; r.sum[4 * j + 3] = q[4 + j].w;
+    }
+    return r;
+}
+
+// sign of (exact value e) against the value whose code is c: -1 / +1 decided, 0 = code tie
+__device__ __forceinline__ int code_cmp(const K160& e, uint32_t c)
+{
+    const uint32_t ce = code32(e);
+    return ce < c ? -1 : (ce > c ? 1 : 0);
+}
+
+// x in (pred(v), v] of the node v of record R: (v - x) < (v - pred) (isBetweenR, pred != v)
+__device__ __forceinline__ bool in_pred_r(const KView& V, const KRec& R, uint32_t v, const K160& x)
+{
+    const int s = code_cmp(k_sub(R.k, x), R.cP);
+    if (s) return s < 0;
+    return between_R(x, rkey(V.recs, v == 0 ? V.n - 1 : v - 1), R.k);
+}
+
+// x in (v, succ0(v)]: 0 < (x - v) <= (succ0 - v)
+__device__ __forceinline__ bool in_succ_r(const KView& V, const KRec& R, uint32_t v, const K160& x)
+{
+    const K160 d = k_sub(x, R.k);
+    if ((d.w[0] | d.w[1] | d.w[2] | d.w[3] | d.w[4]) == 0) return false;
+    const int s = code_cmp(d, R.sum[0]);
+    if (s) return s < 0;
+    return between_R(x, R.k, rkey(V.recs, ring_add(v, 1, V.n)));
+}
+
+// walk_list over the `num` consecutive nodes from a0 (the node of record A) for a key at exact
+// distance dk = key - a0 from a0 (dk != 0): a_cnt, cnt = #{j in 1..num-1 : d(a0, a_j) < dk};
+// a code tie takes the exact walk
+__device__ __forceinline__ uint32_t walk_rec(const KView& V, const KRec& A, uint32_t a0, int num, const K160& dk,
+                                             const K160& key)
+{
+    if (num <= 1) return a0;
+    const uint32_t ck = code32(dk);
+    int cnt = 0;
+    bool tie = false;
+#pragma unroll
+    for (int j = 1; j < KREC_LIST; ++j) {
+        if (j < num) {
+            cnt += A.sum[j - 1] < ck ? 1 : 0;
+            tie |= A.sum[j - 1] == ck;
+        }
+    }
+    if (tie) return walk_list(V.recs, V.n, a0, num, key);
+    return ring_add(a0, (uint32_t)cnt, V.n);
+}
+
+// Koorde::findNode (405-471) at node c with record R, K not in (pred c, c] (the caller's siblings
+// check); the structure of koorde_find_node_dev with record decisions
+__device__ uint32_t koorde_find_node_rec(const KView& V, uint32_t c, const KRec& R, const K160& key, KExt& e)
+{
+    const uint32_t n = V.n;
+    const uint32_t s0 = ring_add(c, 1, n);
+    const uint32_t slast = ring_add(c, (uint32_t)V.ns, n);
+    const K160& me = R.k;
+    if (in_pred_r(V, R, c, key)) return c;
+    if (in_succ_r(V, R, c, key)) return s0;
+    // the successor-list walk (walkSuccessorList 572-582) from s0: with key beyond s0,
+    // d(s0, s_j) < d(s0, key) <=> d(c, s_j) < d(c, key), i.e. the record's codes from index 1
+    auto succ_walk = [&](const K160& x) -> uint32_t {
+        const K160 d = k_sub(x, me);
+        if ((d.w[0] | d.w[1] | d.w[2] | d.w[3] | d.w[4]) == 0) return slast;   // x == c: d(s0, c) is the largest
+        if (V.ns <= 1) return s0;
+        const uint32_t ck = code32(d);
+        int cnt = 0;
+        bool tie = false;
+#pragma unroll
+        for (int j = 1; j < KREC_LIST; ++j) {
+            if (j < V.ns) {
+                cnt += R.sum[j] < ck ? 1 : 0;
+                tie |= R.sum[j] == ck;
+            }
+        }
+        if (tie) return walk_list(V.recs, n, s0, V.ns, x);
+        return ring_add(s0, (uint32_t)cnt, n);
+    };
+    if (V.useOther) {
+        const uint32_t tmp = succ_walk(key);
+        if (tmp != slast) return tmp;
+    }
+    const uint32_t db = R.db, dbStart = R.dbStart;
+    const int dbNum = (int)R.dbNum;
+    bool haveB = false;
+    KRec B;
+    for (int guard = 0; guard < 200; ++guard) {   // the self-recursion, as koorde_find_node_dev
+        bool brk = false;
+        uint32_t h;
+        if (!e.has) {
+            // findStartKey (664-762): nBits = msb(succ0 - c) from the record's code
+            int nBits = (int)(R.sum[0] >> 24) - 1;
+            if (nBits < 0) nBits = 0;
+            while ((160 - nBits) % V.sb != 0) nBits--;
+            const int step = nBits + 1;
+            const K160 newStart = k_shl(k_shr(me, nBits), nBits);
+            K160 newKey = k_add(k_shr(key, 160 - nBits), newStart);
+            if (!in_succ_r(V, R, c, newKey)) {
+                newKey = k_add(newKey, k_pow2(nBits));
+                if (!in_succ_r(V, R, c, newKey)) return NONE;    // invalid start key
+            }
+            e.rk = newKey; e.step = step; e.has = 1;
+        }
+        if (in_succ_r(V, R, c, e.rk)) {
+            if (e.step > 160) return NONE;
+            if (160 - e.step - (V.sb - 1) < 0) return NONE;
+            const uint32_t add = (uint32_t)((k_shr(key, 160 - e.step - V.sb + 1).w[0]) & ((1u << V.sb) - 1u));
+            e.rk = k_add(k_shl(e.rk, V.sb), k_small(add));
+            e.step += V.sb;
+            if (dbNum > 0) {
+                if (!haveB) { B = load_krec(V.rec, dbStart); haveB = true; }
+                // rk in (db, dbStart]: db is dbStart's ring predecessor (k_koorde_build)
+                if (in_pred_r(V, B, dbStart, e.rk)) {
+                    h = db;
+                } else {
+                    const K160 dk = k_sub(e.rk, B.k);
+                    h = ((dk.w[0] | dk.w[1] | dk.w[2] | dk.w[3] | dk.w[4]) == 0) ? ring_add(dbStart, (uint32_t)(dbNum - 1), n)
+                                                                                : walk_rec(V, B, dbStart, dbNum, dk, e.rk);
+                }
+            } else {
+                h = db;
+            }
+        } else {
+            brk = true;
+            if (V.useSuc) {
+                const uint32_t tmp = succ_walk(e.rk);
+                h = between_open(rkey(V.recs, db), rkey(V.recs, tmp), e.rk) ? db : tmp;
+            } else {
+                h = s0;
+            }
+        }
+        if (h != c || brk) return h;
+    }
+    return NONE;
+}
+
+// the records (after k_koorde_build)
+__global__ void k_koorde_rec(const KeyRec* __restrict__ recs, const double2* __restrict__ xy,
+                             const KoordeNode* __restrict__ nd, uint32_t n, KoordeRec* __restrict__ out)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const K160 me = rkey(recs, v);
+    KoordeRec r;
+    for (int i = 0; i < 5; ++i) r.w[i] = me.w[i];
+    r.cP = code32(k_sub(me, rkey(recs, v == 0 ? n - 1 : v - 1)));
+    const KoordeNode k = nd[v];
+    r.db = k.db; r.dbStart = k.dbStart; r.dbNum = k.dbNum;
+    r.pad0 = 0; r.pad1[0] = r.pad1[1] = 0;
+    r.x = xy[v].x; r.y = xy[v].y;
+    for (int j = 1; j <= KREC_LIST; ++j) r.sum[j - 1] = code32(k_sub(rkey(recs, (uint32_t)(((uint64_t)v + j) % n)), me));
+    out[v] = r;
+}
+
 // handleDeBruijnTimerExpired (164-230) on the converged ring; the DeBruijnCall of the third
 // case is answered by the node responsible for its key (328-367)
 __global__ void k_koorde_build(const KeyRec* __restrict__ recs, uint32_t n, int ns, int sb, int dbls,
@@ -201,6 +390,8 @@ __global__ void k_koorde_build(const KeyRec* __restrict__ recs, uint32_t n, int 
 // visitOnlyOnce filter: one bit per node hash; a clear bit proves the node unvisited
 __device__ __forceinline__ uint64_t vis_bit(uint32_t x) { return 1ull << ((x * 0x9E3779B1u) >> 26); }
 
+// KR: the record form (KoordeRec), else the list walks on recs[]
+template <bool KR>
 __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                       uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
@@ -252,9 +443,21 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
         const uint32_t c = local ? S : cur;
         const uint32_t pred = c == 0 ? V.n - 1 : c - 1;
         // isSiblingFor(c, K, 1) (Chord.cc:452-457): K in (pred, c]
-        const bool sib = between_R(K, rkey(V.recs, pred), rkey(V.recs, c));
         KExt e2 = e;
-        const uint32_t nx = sib ? c : koorde_find_node_dev(V, c, K, e2);
+        bool sib;
+        uint32_t nx;
+        double cx, cy;
+        if constexpr (KR) {
+            const KRec Rc = load_krec(V.rec, c);
+            sib = in_pred_r(V, Rc, c, K);
+            nx = sib ? c : koorde_find_node_rec(V, c, Rc, K, e2);
+            cx = Rc.x; cy = Rc.y;
+        } else {
+            sib = between_R(K, rkey(V.recs, pred), rkey(V.recs, c));
+            nx = sib ? c : koorde_find_node_dev(V, c, K, e2);
+            const double2 p = xy[c];
+            cx = p.x; cy = p.y;
+        }
         if (local) {
             // IterativeLookup::start (133-244)
             local = false;
@@ -266,8 +469,7 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
             fin = true; status = OVS_LOOKUP_BROKEN;    // the responder's findNode throws
         } else {
             // FindNodeCall S -> c and its FindNodeResponse (one NodeHandle), both with the extension
-            const double2 p = xy[c];
-            const int64_t cd = coord_ns(sx, sy, p.x, p.y, DC.round);
+            const int64_t cd = coord_ns(sx, sy, cx, cy, DC.round);
             const int64_t rtt = DC.msgCall + DC.msgResp1 + 2 * cd;
             if (rtt >= DC.rpcTimeout) {
                 fin = true;
@@ -302,9 +504,8 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
                 o.one_way_hops = (uint8_t)(hops + (R != S ? 1 : 0));
                 int64_t lat = t;
                 if (R != S) {
-                    // sendRouteMessage to the result (BaseOverlay.cc:1107-1146)
-                    const double2 p = xy[R];
-                    lat += DC.msgRoute + coord_ns(sx, sy, p.x, p.y, DC.round);
+                    // sendRouteMessage to the result (BaseOverlay.cc:1107-1146): R is this iteration's c
+                    lat += DC.msgRoute + coord_ns(sx, sy, cx, cy, DC.round);
                 }
                 o.latency_ns = lat;
             } else {
@@ -323,13 +524,17 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
     }
 }
 
+template <bool KR>
 __global__ void k_koorde_find_node(KView V, const uint32_t* __restrict__ node, const K160* __restrict__ keys,
                                    KExt* __restrict__ ext, uint32_t* __restrict__ next, uint64_t nq)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nq) return;
     KExt e = ext[i];
-    const uint32_t h = koorde_find_node_dev(V, node[i], keys[i], e);
+    const uint32_t c = node[i];
+    uint32_t h;
+    if constexpr (KR) h = koorde_find_node_rec(V, c, load_krec(V.rec, c), keys[i], e);
+    else h = koorde_find_node_dev(V, c, keys[i], e);
     next[i] = h;
     if (h != NONE) ext[i] = e;
 }
@@ -339,14 +544,14 @@ inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b
 KView make_view(const KoordeTables& t, const KeyRec* recs)
 {
     KView V;
-    V.recs = recs; V.nd = t.nd; V.n = t.n; V.ns = t.ns; V.sb = t.sb; V.useOther = t.useOther; V.useSuc = t.useSuc;
+    V.recs = recs; V.nd = t.nd; V.rec = t.rec; V.n = t.n; V.ns = t.ns; V.sb = t.sb; V.useOther = t.useOther; V.useSuc = t.useSuc;
     return V;
 }
 
 }  // namespace
 
-hipError_t koorde_build(const KeyRec* recs, uint32_t n, int successorListSize, int shiftingBits, int deBruijnListSize,
-                        int useOtherLookup, int useSucList, KoordeTables& t, hipStream_t st)
+hipError_t koorde_build(const KeyRec* recs, const double2* xy, uint32_t n, int successorListSize, int shiftingBits,
+                        int deBruijnListSize, int useOtherLookup, int useSucList, KoordeTables& t, hipStream_t st)
 {
     koorde_free(t);
     if (n < 2 || shiftingBits < 1 || shiftingBits > 32 || deBruijnListSize < 1) return hipErrorInvalidValue;
@@ -359,6 +564,14 @@ hipError_t koorde_build(const KeyRec* recs, uint32_t n, int successorListSize, i
                        deBruijnListSize, t.nd);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // the record form covers successor / de Bruijn lists of up to 16 nodes (the Koorde defaults)
+    if (t.ns <= KREC_LIST && deBruijnListSize <= KREC_LIST && !getenv("OVS_KOORDE_NOREC")) {
+        e = hipMalloc(&t.rec, sizeof(KoordeRec) * n);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_koorde_rec, dim3(nblk(n, 256)), dim3(256), 0, st, recs, xy, t.nd, n, t.rec);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     return hipStreamSynchronize(st);
 }
 
@@ -368,18 +581,26 @@ hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2
 {
     if (nq == 0) return hipSuccess;
     if (!hopseq) return hipErrorInvalidValue;
-    static int bpc = 0;
-    if (bpc == 0) {
+    static int bpc[2] = {0, 0};
+    const int kr = t.rec ? 1 : 0;
+    if (bpc[kr] == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_koorde_route, 256, 0) != hipSuccess || b < 1) b = 1;
-        bpc = b;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kr ? k_koorde_route<true> : k_koorde_route<false>, 256, 0) !=
+                hipSuccess ||
+            b < 1)
+            b = 1;
+        bpc[kr] = b;
     }
-    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4;
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc[kr] * 4;
     uint64_t chunk = (nq + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
     const uint64_t blocks = ((nq + chunk - 1) / chunk + 3) / 4;
-    hipLaunchKernelGGL(k_koorde_route, dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC, hopCountMax,
-                       keys, src, nq, chunk, out, hopseq, rpcs);
+    if (kr)
+        hipLaunchKernelGGL(k_koorde_route<true>, dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC,
+                           hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs);
+    else
+        hipLaunchKernelGGL(k_koorde_route<false>, dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC,
+                           hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs);
     return hipGetLastError();
 }
 
@@ -387,8 +608,12 @@ hipError_t koorde_find_node(const KoordeTables& t, const KeyRec* recs, const uin
                             KExt* ext, uint32_t* next, uint64_t nq, hipStream_t st)
 {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_koorde_find_node, dim3(nblk(nq, 128)), dim3(128), 0, st, make_view(t, recs), node, keys, ext,
-                       next, nq);
+    if (t.rec)
+        hipLaunchKernelGGL(k_koorde_find_node<true>, dim3(nblk(nq, 128)), dim3(128), 0, st, make_view(t, recs), node, keys,
+                           ext, next, nq);
+    else
+        hipLaunchKernelGGL(k_koorde_find_node<false>, dim3(nblk(nq, 128)), dim3(128), 0, st, make_view(t, recs), node,
+                           keys, ext, next, nq);
     return hipGetLastError();
 }
 

@@ -1002,7 +1002,7 @@ ovs_status ovs_koorde_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const 
         return fail(c, OVS_ENOTSUP, "Koorde shiftingBits must be 1..16 and deBruijnListSize 1..255");
     ovs_status s = upload_nodes(c, ids, n, xy, flags & OVS_DEVICE_PTRS);
     if (s != OVS_OK) { free_tables(c); return s; }
-    hipError_t e = koorde_build(c->recs, (uint32_t)n, c->P.successorListSize, c->P.shiftingBits, c->P.deBruijnListSize,
+    hipError_t e = koorde_build(c->recs, c->xy, (uint32_t)n, c->P.successorListSize, c->P.shiftingBits, c->P.deBruijnListSize,
                                 c->P.useOtherLookup, c->P.useSucList, c->koorde, c->stream);
     if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "koorde build"); }
     c->overlay = OVS_OVERLAY_KOORDE;
