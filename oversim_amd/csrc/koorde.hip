@@ -180,29 +180,85 @@ __device__ uint32_t koorde_find_node_dev(const KView& V, uint32_t c, const K160&
 
 __device__ __forceinline__ uint32_t code32(const K160& v) { return (uint32_t)(k_code64(v) >> 32); }
 
+// the first line of a record (and its first successor-distance code)
 struct KRec {
     K160 k;
     uint32_t cP, db, dbStart, dbNum;
     double x, y;
-    uint32_t sum[KREC_LIST];
+    uint32_t s0;         // sum[0] = code(succ0 - v)
 };
 
-__device__ __forceinline__ KRec load_krec(const KoordeRec* __restrict__ rec, uint32_t i)
+// the record's second line (the 16 successor-distance codes), where the walks read it: in LDS for
+// the responder's own record (its codes are needed again after the de Bruijn record arrives), in
+// registers for the de Bruijn list's first node (used at once)
+struct CodesLds {
+    uint4 (*a)[256];
+    int t;
+    __device__ __forceinline__ uint4 get(int c) const { return a[c][t]; }
+};
+struct CodesReg {
+    uint4 q[4];
+    __device__ __forceinline__ uint4 get(int c) const { return q[c]; }
+};
+
+// one record: the 8 chunks are requested together (one memory round trip)
+template <class Codes>
+__device__ __forceinline__ KRec load_krec(const KoordeRec* __restrict__ rec, uint32_t i, Codes& codes);
+
+__device__ __forceinline__ KRec krec_head(uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint4 q4)
+{
+    KRec r;
+    r.k.w[0] = q0.x; r.k.w[1] = q0.y; r.k.w[2] = q0.z; r.k.w[3] = q0.w; r.k.w[4] = q1.x;
+    r.cP = q1.y; r.db = q1.z; r.dbStart = q1.w; r.dbNum = q2.x;
+    r.x = __hiloint2double((int)q2.w, (int)q2.z);
+    r.y = __hiloint2double((int)q3.y, (int)q3.x);
+    r.s0 = q4.x;
+    return r;
+}
+
+template <>
+__device__ __forceinline__ KRec load_krec<CodesLds>(const KoordeRec* __restrict__ rec, uint32_t i, CodesLds& codes)
 {
     const uint4* p = reinterpret_cast<const uint4*>(rec + i);
     uint4 q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) q[j] = p[j];
-    KRec r;
-    r.k.w[0] = q[0].x; r.k.w[1] = q[0].y; r.k.w[2] = q[0].z; r.k.w[3] = q[0].w; r.k.w[4] = q[1].x;
-    r.cP = q[1].y; r.db = q[1].z; r.dbStart = q[1].w; r.dbNum = q[2].x;
-    r.x = __hiloint2double((int)q[2].w, (int)q[2].z);
-    r.y = __hiloint2double((int)q[3].y, (int)q[3].x);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        r.sum[4 * j] = q[4 + j].x; r.sum[4 * j + 1] = q[4 + j].y; r.sum[4 * j + 2] = q[4 + j].z; r.sum[4 * j + 3] = q[4 + j].w;
+    for (int c = 0; c < 4; ++c) codes.a[c][codes.t] = q[4 + c];
+    return krec_head(q[0], q[1], q[2], q[3], q[4]);
+}
+
+template <>
+__device__ __forceinline__ KRec load_krec<CodesReg>(const KoordeRec* __restrict__ rec, uint32_t i, CodesReg& codes)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(rec + i);
+    uint4 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = p[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) codes.q[c] = q[4 + c];
+    return krec_head(q[0], q[1], q[2], q[3], q[4]);
+}
+
+// #{i in [lo, hi) : sum[i] < ck}; tie: some sum[i] == ck
+template <class Codes>
+__device__ __forceinline__ int count_codes(const Codes& codes, int lo, int hi, uint32_t ck, bool& tie)
+{
+    int cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint4 q = codes.get(c);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * c + j;
+            if (i >= lo && i < hi) {
+                cnt += w[j] < ck ? 1 : 0;
+                tie |= w[j] == ck;
+            }
+        }
     }
-    return r;
+    return cnt;
 }
 
 // sign of (exact value e) against the value whose code is c: -1 / +1 decided, 0 = code tie
@@ -225,58 +281,29 @@ __device__ __forceinline__ bool in_succ_r(const KView& V, const KRec& R, uint32_
 {
     const K160 d = k_sub(x, R.k);
     if ((d.w[0] | d.w[1] | d.w[2] | d.w[3] | d.w[4]) == 0) return false;
-    const int s = code_cmp(d, R.sum[0]);
+    const int s = code_cmp(d, R.s0);
     if (s) return s < 0;
     return between_R(x, R.k, rkey(V.recs, ring_add(v, 1, V.n)));
 }
 
-// walk_list over the `num` consecutive nodes from a0 (the node of record A) for a key at exact
-// distance dk = key - a0 from a0 (dk != 0): a_cnt, cnt = #{j in 1..num-1 : d(a0, a_j) < dk};
-// a code tie takes the exact walk
-__device__ __forceinline__ uint32_t walk_rec(const KView& V, const KRec& A, uint32_t a0, int num, const K160& dk,
-                                             const K160& key)
-{
-    if (num <= 1) return a0;
-    const uint32_t ck = code32(dk);
-    int cnt = 0;
-    bool tie = false;
-#pragma unroll
-    for (int j = 1; j < KREC_LIST; ++j) {
-        if (j < num) {
-            cnt += A.sum[j - 1] < ck ? 1 : 0;
-            tie |= A.sum[j - 1] == ck;
-        }
-    }
-    if (tie) return walk_list(V.recs, V.n, a0, num, key);
-    return ring_add(a0, (uint32_t)cnt, V.n);
-}
-
-// Koorde::findNode (405-471) at node c with record R, K not in (pred c, c] (the caller's siblings
-// check); the structure of koorde_find_node_dev with record decisions
-__device__ uint32_t koorde_find_node_rec(const KView& V, uint32_t c, const KRec& R, const K160& key, KExt& e)
+// Koorde::findNode (405-471) at node c with record R: the structure of koorde_find_node_dev with
+// record decisions.  The extension e is advanced in place (the caller drops it when the hop ends
+// the lookup).
+__device__ uint32_t koorde_find_node_rec(const KView& V, uint32_t c, const KRec& R, const CodesLds& RC, const K160& key,
+                                         KExt& e)
 {
     const uint32_t n = V.n;
     const uint32_t s0 = ring_add(c, 1, n);
     const uint32_t slast = ring_add(c, (uint32_t)V.ns, n);
-    const K160& me = R.k;
     if (in_pred_r(V, R, c, key)) return c;
     if (in_succ_r(V, R, c, key)) return s0;
-    // the successor-list walk (walkSuccessorList 572-582) from s0: with key beyond s0,
-    // d(s0, s_j) < d(s0, key) <=> d(c, s_j) < d(c, key), i.e. the record's codes from index 1
+    // the successor-list walk (walkSuccessorList 572-582) from s0: with x beyond s0,
+    // d(s0, s_j) < d(s0, x) <=> d(c, s_j) < d(c, x), i.e. the record's codes sum[1 .. ns-1]
     auto succ_walk = [&](const K160& x) -> uint32_t {
-        const K160 d = k_sub(x, me);
+        const K160 d = k_sub(x, R.k);
         if ((d.w[0] | d.w[1] | d.w[2] | d.w[3] | d.w[4]) == 0) return slast;   // x == c: d(s0, c) is the largest
-        if (V.ns <= 1) return s0;
-        const uint32_t ck = code32(d);
-        int cnt = 0;
         bool tie = false;
-#pragma unroll
-        for (int j = 1; j < KREC_LIST; ++j) {
-            if (j < V.ns) {
-                cnt += R.sum[j] < ck ? 1 : 0;
-                tie |= R.sum[j] == ck;
-            }
-        }
+        const int cnt = count_codes(RC, 1, V.ns, code32(d), tie);
         if (tie) return walk_list(V.recs, n, s0, V.ns, x);
         return ring_add(s0, (uint32_t)cnt, n);
     };
@@ -286,18 +313,16 @@ __device__ uint32_t koorde_find_node_rec(const KView& V, uint32_t c, const KRec&
     }
     const uint32_t db = R.db, dbStart = R.dbStart;
     const int dbNum = (int)R.dbNum;
-    bool haveB = false;
-    KRec B;
     for (int guard = 0; guard < 200; ++guard) {   // the self-recursion, as koorde_find_node_dev
         bool brk = false;
         uint32_t h;
         if (!e.has) {
             // findStartKey (664-762): nBits = msb(succ0 - c) from the record's code
-            int nBits = (int)(R.sum[0] >> 24) - 1;
+            int nBits = (int)(R.s0 >> 24) - 1;
             if (nBits < 0) nBits = 0;
             while ((160 - nBits) % V.sb != 0) nBits--;
             const int step = nBits + 1;
-            const K160 newStart = k_shl(k_shr(me, nBits), nBits);
+            const K160 newStart = k_shl(k_shr(R.k, nBits), nBits);
             K160 newKey = k_add(k_shr(key, 160 - nBits), newStart);
             if (!in_succ_r(V, R, c, newKey)) {
                 newKey = k_add(newKey, k_pow2(nBits));
@@ -312,14 +337,21 @@ __device__ uint32_t koorde_find_node_rec(const KView& V, uint32_t c, const KRec&
             e.rk = k_add(k_shl(e.rk, V.sb), k_small(add));
             e.step += V.sb;
             if (dbNum > 0) {
-                if (!haveB) { B = load_krec(V.rec, dbStart); haveB = true; }
+                CodesReg BC;
+                const KRec B = load_krec(V.rec, dbStart, BC);
                 // rk in (db, dbStart]: db is dbStart's ring predecessor (k_koorde_build)
                 if (in_pred_r(V, B, dbStart, e.rk)) {
                     h = db;
                 } else {
+                    // walkDeBruijnList (558-570) over dbStart's codes sum[0 .. dbNum-2]
                     const K160 dk = k_sub(e.rk, B.k);
-                    h = ((dk.w[0] | dk.w[1] | dk.w[2] | dk.w[3] | dk.w[4]) == 0) ? ring_add(dbStart, (uint32_t)(dbNum - 1), n)
-                                                                                : walk_rec(V, B, dbStart, dbNum, dk, e.rk);
+                    if ((dk.w[0] | dk.w[1] | dk.w[2] | dk.w[3] | dk.w[4]) == 0 || dbNum <= 1) {
+                        h = dbNum <= 1 ? dbStart : ring_add(dbStart, (uint32_t)(dbNum - 1), n);
+                    } else {
+                        bool tie = false;
+                        const int cnt = count_codes(BC, 0, dbNum - 1, code32(dk), tie);
+                        h = tie ? walk_list(V.recs, n, dbStart, dbNum, e.rk) : ring_add(dbStart, (uint32_t)cnt, n);
+                    }
                 }
             } else {
                 h = db;
@@ -390,9 +422,13 @@ __global__ void k_koorde_build(const KeyRec* __restrict__ recs, uint32_t n, int 
 // visitOnlyOnce filter: one bit per node hash; a clear bit proves the node unvisited
 __device__ __forceinline__ uint64_t vis_bit(uint32_t x) { return 1ull << ((x * 0x9E3779B1u) >> 26); }
 
-// KR: the record form (KoordeRec), else the list walks on recs[]
+#ifndef OVS_KOORDE_WAVES
+#define OVS_KOORDE_WAVES 1
+#endif
+// KR: the record form (KoordeRec), else the list walks on recs[].  OVS_KOORDE_WAVES: minimum waves
+// per SIMD the record form's register allocation must allow
 template <bool KR>
-__global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
+__global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                       uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
                                                       uint32_t* __restrict__ hopseq, uint32_t* __restrict__ rpcs)
@@ -407,6 +443,8 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
     bool active = false, local = true;
     uint64_t q = 0;
     K160 K;
+    __shared__ uint4 rcodes[4][256];            // the responder record's codes, per lane (record form)
+    CodesLds RC{rcodes, (int)threadIdx.x};
     uint32_t S = 0, cur = 0;
     double sx = 0, sy = 0;
     int64_t t = 0;
@@ -443,16 +481,20 @@ __global__ __launch_bounds__(256) void k_koorde_route(KView V, const double2* __
         const uint32_t c = local ? S : cur;
         const uint32_t pred = c == 0 ? V.n - 1 : c - 1;
         // isSiblingFor(c, K, 1) (Chord.cc:452-457): K in (pred, c]
-        KExt e2 = e;
+        KExt e2;
         bool sib;
         uint32_t nx;
         double cx, cy;
         if constexpr (KR) {
-            const KRec Rc = load_krec(V.rec, c);
+            // the extension advances in place: every outcome that does not take nx as the next
+            // hop ends the lookup
+            const KRec Rc = load_krec(V.rec, c, RC);
             sib = in_pred_r(V, Rc, c, K);
-            nx = sib ? c : koorde_find_node_rec(V, c, Rc, K, e2);
+            nx = sib ? c : koorde_find_node_rec(V, c, Rc, RC, K, e);
             cx = Rc.x; cy = Rc.y;
+            e2 = e;
         } else {
+            e2 = e;
             sib = between_R(K, rkey(V.recs, pred), rkey(V.recs, c));
             nx = sib ? c : koorde_find_node_dev(V, c, K, e2);
             const double2 p = xy[c];
@@ -533,7 +575,12 @@ __global__ void k_koorde_find_node(KView V, const uint32_t* __restrict__ node, c
     KExt e = ext[i];
     const uint32_t c = node[i];
     uint32_t h;
-    if constexpr (KR) h = koorde_find_node_rec(V, c, load_krec(V.rec, c), keys[i], e);
+    if constexpr (KR) {
+        __shared__ uint4 rcodes[4][256];      // 128-thread blocks use the first half of each row
+        CodesLds RC{rcodes, (int)threadIdx.x};
+        const KRec R = load_krec(V.rec, c, RC);
+        h = koorde_find_node_rec(V, c, R, RC, keys[i], e);
+    }
     else h = koorde_find_node_dev(V, c, keys[i], e);
     next[i] = h;
     if (h != NONE) ext[i] = e;
