@@ -592,15 +592,22 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                     t = (int64_t)u64(L2.x, L2.y);
                     hops = (int)(L2.z & 0xFFFF);
                     local = ((L2.z >> 16) & 0xFF) != 0;
-                    if (!REC) {
+                    if (S >= V.n || cur >= V.n) {
+                        // a row the exchange never wrote (receive buffers are 0xFF-filled) or a corrupted
+                        // record: finished as BROKEN with its qid (0xFFFFFFFF for the sentinel), which
+                        // the host's completeness check reports -- never a table read
+                        fin = true; status = OVS_LOOKUP_BROKEN;
+                    } else if (!REC) {
                         const double2 sxy = V.xy[S];      // coordinates are replicated on every rank
                         sx = sxy.x; sy = sxy.y;
                     }
                 } else {
                     cur = S; t = 0; hops = 0; local = true;
                 }
-                lp = reinterpret_cast<const uint4*>(V.nodes + cur);
-                ph = PH_START;
+                if (!fin) {
+                    lp = reinterpret_cast<const uint4*>(V.nodes + cur);
+                    ph = PH_START;
+                }
             } else {
                 // the 64 B line: NodeRec and FingerEnt share key, coordinates and window distances
                 A.k.w[0] = L0.x; A.k.w[1] = L0.y; A.k.w[2] = L0.z; A.k.w[3] = L0.w; A.k.w[4] = L1.x;

@@ -379,9 +379,12 @@ __device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t bof
 // block form: the candidate sets of the reference's scan (bucket m, then buckets m-1..endIndex with
 // the sibling table and self when m >= endIndex or the result is short, then buckets above m while
 // it is short) merged one table block at a time into the top C.  Returns the result size.
+// pre >= 0 (a findNode in the sibling zone, m <= endIndex): only the first pre entries of c's
+// level-sorted sibling row can enter the result (kad_sib_prefix); the rest are counted, not read.
 template <bool EX, int C = 8>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
-                                                 int numRedundant, bool sib, BlkN<C>& res, int numSiblings = 1)
+                                                 int numRedundant, bool sib, BlkN<C>& res, int numSiblings = 1,
+                                                 int pre = -1)
 {
     blk_clear(res);
     if (V.err && kad_off_arc(V, c)) {
@@ -428,7 +431,9 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     if ((g.m >= g.endIndex || seen < rs) && !(g.m > g.endIndex && n >= cap)) {
         for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
         const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
-        for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
+        const int rd = pre < 0 ? g.nsib : min(g.nsib, KBLK * ((pre + KBLK - 1) / KBLK));
+        for (int j = 0; j * KBLK < rd; ++j) add_blk(L + j);
+        seen += g.nsib - rd;
         Blk8 self;
         blk_clear(self);
         self.x[0] = c;

@@ -493,7 +493,9 @@ struct XCtx {
                     // reads one block per bucket, so only on tables with k <= 8 (a k = 16 table's
                     // bucket refresh, R = 8, scans both blocks of each bucket below)
                     Blk8 b;
-                    cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1);
+                    // in the sibling zone only the level-sorted row's prefix can enter the answer
+                    const int pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, rs < 8 ? rs : 8) : -1;
+                    cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1, pre);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         if (i >= cnt) continue;

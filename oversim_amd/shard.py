@@ -377,7 +377,28 @@ def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: i
             raise RuntimeError("sharded routing did not terminate")
     if hasattr(stepper, "end_cohorts"):
         stepper.end_cohorts()
-    return stepper.finished(), rounds
+    done = stepper.finished()
+    # Chord lookups finish on whichever rank holds them last: the batch is complete when the ranks'
+    # finished records add up to their lookups (one small all-reduce per batch)
+    check_complete(done, n, "sharded Chord", exchange=exchange)
+    return done, rounds
+
+
+def check_complete(done, n: int, what: str, exchange=None):
+    """No finished record came from an exchange row that was never written (the 0xFF sentinel reads
+    as qid 0xFFFFFFFF, status BROKEN), and the finished records match the lookups -- this rank's
+    (exchange None: a rank finishes exactly its own lookups) or all ranks' together.  A short
+    transfer surfaces here, not as lost lookups."""
+    k = len(done)
+    if k and hasattr(done, "dim") and done.dim() == 2:     # device records (test doubles hand lists)
+        sent = int((done[:, :4] == 0xFF).all(dim=1).sum().item())
+        if sent:
+            raise RuntimeError(f"{what}: {sent} finished records from unwritten or corrupt exchange rows")
+    have, want = k, n
+    if exchange is not None and hasattr(exchange, "total"):
+        have, want = exchange.total(k), exchange.total(n)
+    if have != want:
+        raise RuntimeError(f"{what}: {have} finished records for {want} lookups")
 
 
 class _NoCtx:
@@ -570,7 +591,9 @@ def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_round
         if rounds > max_rounds:
             raise RuntimeError(f"sharded Kademlia routing did not terminate: {int(M[:, W].sum())} lookups active, "
                                f"{int(M[:, :W].sum())} requests in round {rounds}")
-    return stepper.finished(), rounds
+    done = stepper.finished()
+    check_complete(done, int(keys_t.shape[0]), "sharded Kademlia")
+    return done, rounds
 
 
 def route_kad_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_rounds: int = 100_000):

@@ -714,3 +714,18 @@ def test_kad_serve_refuses_requests_it_cannot_answer():
     resp = st.serve(torch.from_numpy(q.view(np.uint8).reshape(3, -1).copy()).to(dev))
     r = resp.cpu().numpy().view(KAD_RESP_DTYPE).ravel()
     assert r["count"][0] <= 8 and r["count"][1] == 0xFFFFFFFF and r["count"][2] == 0xFFFFFFFF
+
+
+def test_check_complete_reports_unwritten_rows_and_missing_records():
+    """A finished record read from an exchange row nobody wrote (the 0xFF sentinel) or a record count
+    that does not match the batch raises, instead of passing as lost lookups."""
+    import torch
+    from oversim_amd.shard import DONE_BYTES, check_complete
+    ok = torch.zeros((5, DONE_BYTES), dtype=torch.uint8)
+    check_complete(ok, 5, "t")
+    bad = ok.clone()
+    bad[2] = 0xFF
+    with pytest.raises(RuntimeError, match="unwritten"):
+        check_complete(bad, 5, "t")
+    with pytest.raises(RuntimeError, match="4 finished records for 5"):
+        check_complete(ok[:4], 5, "t")
