@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define OVS_HD __host__ __device__ __forceinline__
 #else
 #define OVS_HD inline

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "epichord.hpp"
+#include "host_tables.hpp"
 #include "kad.hpp"
 #include "kad_shard.hpp"
 #include "koorde.hpp"
@@ -47,15 +48,8 @@ struct ovs_ctx {
     uint8_t* nsucc = nullptr;
     uint32_t* fres = nullptr;
     int sls = 0;
-    // explicit tables: host copies for batched maintenance (ovs_chord_fix_fingers)
-    std::vector<K160> h_ids;
-    std::vector<uint32_t> h_deque;      // n * 160 ChordFingerTable deque entries (index p = 159 - pos)
-    std::vector<uint8_t> h_fsize;       // deque sizes
-    std::vector<uint32_t> h_succ0;      // successorList->getSuccessor()
-    std::vector<uint32_t> h_fres;       // n * 160 resolved getFinger(pos)
-    std::vector<uint32_t> h_pred;       // predecessorNode (ovs_chord_stabilize)
-    std::vector<uint32_t> h_succ;       // n * sls successor lists
-    std::vector<uint8_t> h_nsucc;
+    // explicit tables: host copies for batched maintenance (ovs_chord_fix_fingers / _stabilize)
+    ChordHost ch;
     uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     std::vector<uint64_t> h_bounds;         // ... as last uploaded (uploaded again only on a change)
@@ -119,8 +113,7 @@ void free_tables(ovs_ctx* c)
     if (c->kvis) hipFree(c->kvis);
     c->kvis = nullptr; c->kvis_cap = 0;
     c->overlay = 0; c->n = 0; c->nfing = 0;
-    c->h_ids.clear(); c->h_deque.clear(); c->h_fsize.clear(); c->h_succ0.clear(); c->h_fres.clear();
-    c->h_pred.clear(); c->h_succ.clear(); c->h_nsucc.clear();
+    c->ch.clear();
 }
 
 void free_kad_shard(ovs_ctx* c)
@@ -266,23 +259,6 @@ ovs_status ensure_nodes(ovs_ctx* c, hipStream_t s)
     HIPCHK(c, hipStreamSynchronize(s));
     c->nodes_ns = ns;
     return OVS_OK;
-}
-
-// ChordFingerTable::getFinger(pos) of node v from the host deque (ChordFingerTable.cc:174-193)
-void resolve_row(ovs_ctx* c, uint64_t v)
-{
-    const uint32_t* dq = c->h_deque.data() + v * 160;
-    const uint32_t size = c->h_fsize[v];
-    for (int pos = 0; pos < 160; ++pos) {
-        uint32_t p = 160 - pos - 1;
-        uint32_t r;
-        if (p >= size) r = c->h_succ0[v];
-        else {
-            while (dq[p] == 0xFFFFFFFFu && p < size - 1) ++p;
-            r = dq[p] == 0xFFFFFFFFu ? c->h_succ0[v] : dq[p];
-        }
-        c->h_fres[v * 160 + pos] = r;
-    }
 }
 
 // upload sorted ids (+ coordinates) into KeyRec / double2 arrays
@@ -542,30 +518,12 @@ ovs_status ovs_chord_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, 
     const int sls = c->P.successorListSize;
     // keep the tables on the host too (batched maintenance rewrites them) and resolve
     // ChordFingerTable::getFinger(pos) there (ChordFingerTable.cc:174-193)
-    c->h_ids.assign(reinterpret_cast<const K160*>(ids), reinterpret_cast<const K160*>(ids) + n);
-    c->h_deque.resize((size_t)n * 160);
-    c->h_fsize.assign(deque_size, deque_size + n);
-    c->h_succ0.resize(n);
-    c->h_fres.resize((size_t)n * 160);
-    for (uint64_t v = 0; v < n; ++v) {
-        if (nsucc[v] == 0) return fail(c, OVS_EINVAL, "empty successor list");
-        if (deque_size[v] > 160) return fail(c, OVS_EINVAL, "deque_size > 160");
-        for (uint32_t p = 0; p < 160; ++p) {
-            const uint32_t f = fingers[v * 160 + (159 - p)];
-            if (f != 0xFFFFFFFFu && f >= n) return fail(c, OVS_EINVAL, "finger index out of range");
-            c->h_deque[v * 160 + p] = f;
-        }
-        c->h_succ0[v] = succ[v * sls];
-        if (pred[v] != 0xFFFFFFFFu && pred[v] >= n) return fail(c, OVS_EINVAL, "pred index out of range");
-        if (nsucc[v] > sls) return fail(c, OVS_EINVAL, "nsucc > successorListSize");
-        for (int j = 0; j < nsucc[v]; ++j)
-            if (succ[v * sls + j] >= n) return fail(c, OVS_EINVAL, "successor index out of range");
-        resolve_row(c, v);
+    std::string err;
+    if (!c->ch.import(reinterpret_cast<const K160*>(ids), n, pred, succ, nsucc, fingers, deque_size, sls, &err)) {
+        free_tables(c);
+        return fail(c, OVS_EINVAL, err);
     }
-    c->h_pred.assign(pred, pred + n);
-    c->h_succ.assign(succ, succ + n * sls);
-    c->h_nsucc.assign(nsucc, nsucc + n);
-    const std::vector<uint32_t>& fres = c->h_fres;
+    const std::vector<uint32_t>& fres = c->ch.fres;
     HIPCHK(c, hipMalloc(&c->pred, sizeof(uint32_t) * n));
     HIPCHK(c, hipMalloc(&c->succ, sizeof(uint32_t) * n * sls));
     HIPCHK(c, hipMalloc(&c->nsucc, n));
@@ -611,37 +569,20 @@ ovs_status ovs_chord_fix_fingers(ovs_ctx* c, const uint32_t* nodes, uint64_t m, 
     for (uint64_t j = 0; j < m; ++j)
         if (nodes[j] >= n) return fail(c, OVS_EINVAL, "node index out of range");
     // 1. handleFixFingersTimerExpired (Chord.cc:851-870): trivial fingers removed, lookups for the rest
-    std::vector<ovs_key160> keys;
+    std::vector<K160> kk;
     std::vector<uint32_t> src;
     std::vector<uint8_t> pos;
-    keys.reserve(m * 32); src.reserve(m * 32); pos.reserve(m * 32);
-    for (uint64_t j = 0; j < m; ++j) {
-        const uint32_t v = nodes[j];
-        const K160 self = c->h_ids[v];
-        const K160 gap = k_sub(c->h_ids[c->h_succ0[v]], self);
-        for (int i = 0; i < 160; ++i) {
-            const K160 off = k_pow2(i);
-            if (k_lt(gap, off)) {                              // offset > successor - thisNode
-                const K160 k = k_add(self, off);
-                ovs_key160 kk;
-                for (int w = 0; w < 5; ++w) kk.w[w] = k.w[w];
-                keys.push_back(kk); src.push_back(v); pos.push_back((uint8_t)i);
-            } else {                                           // ChordFingerTable::removeFinger (154-172)
-                const uint32_t p = 160 - i - 1;
-                uint8_t& size = c->h_fsize[v];
-                if (p >= size) continue;
-                if (p == (uint32_t)size - 1) --size;
-                else c->h_deque[(uint64_t)v * 160 + p] = 0xFFFFFFFFu;
-            }
-        }
-    }
+    kk.reserve(m * 32); src.reserve(m * 32); pos.reserve(m * 32);
+    c->ch.fix_fingers_plan(nodes, m, &kk, &src, &pos);
+    std::vector<ovs_key160> keys(kk.size());
+    for (size_t q = 0; q < kk.size(); ++q)
+        for (int w = 0; w < 5; ++w) keys[q].w[w] = kk[q].w[w];
     auto upload_rows = [&]() -> ovs_status {
-        for (uint64_t j = 0; j < m; ++j) resolve_row(c, nodes[j]);
         if (m * 8 >= n) {
-            HIPCHK(c, hipMemcpy(c->fres, c->h_fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
+            HIPCHK(c, hipMemcpy(c->fres, c->ch.fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
         } else {
             for (uint64_t j = 0; j < m; ++j)
-                HIPCHK(c, hipMemcpy(c->fres + (uint64_t)nodes[j] * 160, c->h_fres.data() + (uint64_t)nodes[j] * 160,
+                HIPCHK(c, hipMemcpy(c->fres + (uint64_t)nodes[j] * 160, c->ch.fres.data() + (uint64_t)nodes[j] * 160,
                                     sizeof(uint32_t) * 160, hipMemcpyHostToDevice));
         }
         return OVS_OK;
@@ -653,19 +594,17 @@ ovs_status ovs_chord_fix_fingers(ovs_ctx* c, const uint32_t* nodes, uint64_t m, 
     st = ovs_route_batch(c, keys.data(), src.data(), keys.size(), out.data(), nullptr, nullptr, 0, nullptr);
     if (st != OVS_OK) return st;
     // 3. handleRpcFixfingersResponse: finger i := the answering (responsible) node
-    uint64_t ok = 0, changed = 0, hops = 0;
+    uint64_t ok = 0, hops = 0;
+    std::vector<uint32_t> resp(out.size());
+    std::vector<uint8_t> okv(out.size());
     for (size_t q = 0; q < out.size(); ++q) {
         hops += out[q].hops;
-        if (out[q].status != OVS_LOOKUP_OK) continue;
-        ++ok;
-        const uint32_t v = src[q], p = 160 - pos[q] - 1;
-        uint32_t* dq = c->h_deque.data() + (uint64_t)v * 160;
-        uint8_t& size = c->h_fsize[v];
-        const uint32_t before = p < size ? dq[p] : 0xFFFFFFFFu;
-        while (size <= p) dq[size++] = 0xFFFFFFFFu;          // ChordFingerTable::setFinger (66-87)
-        dq[p] = out[q].responsible;
-        changed += before != out[q].responsible;
+        okv[q] = out[q].status == OVS_LOOKUP_OK;
+        resp[q] = out[q].responsible;
+        ok += okv[q];
     }
+    const uint64_t changed = c->ch.fix_fingers_apply(src, pos, resp, okv);
+    for (uint64_t j = 0; j < m; ++j) c->ch.resolve_row(nodes[j]);
     st = upload_rows();
     if (st != OVS_OK) return st;
     if (stats) { stats->lookups = keys.size(); stats->ok = ok; stats->changed = changed; stats->hops = hops; }
@@ -681,72 +620,20 @@ ovs_status ovs_chord_stabilize(ovs_ctx* c, const uint32_t* nodes, uint64_t m, ov
     const int sls = c->sls;
     for (uint64_t j = 0; j < m; ++j)
         if (nodes[j] >= n) return fail(c, OVS_EINVAL, "node index out of range");
-    const std::vector<K160>& id = c->h_ids;
-    // every message of the round sees the tables as they stand at its start (as ovs_chord_fix_fingers)
-    std::vector<uint32_t> nl((size_t)m * sls, 0xFFFFFFFFu), tgt(m);
-    std::vector<uint8_t> nn(m);
-    for (uint64_t j = 0; j < m; ++j) {
-        const uint32_t v = nodes[j];
-        const uint32_t s = c->h_succ[(size_t)v * sls];
-        // handleRpcStabilizeResponse (Chord.cc:1072-1104): the successor's predecessor p becomes
-        // the successor when p lies in (v, s); NotifyCall to the (new) successor t
-        const uint32_t p = c->h_pred[s];
-        const uint32_t t = (p != 0xFFFFFFFFu && between_open(id[p], id[v], id[s])) ? p : s;
-        tgt[j] = t;
-        // handleRpcNotifyResponse -> ChordSuccessorList::updateList (ChordSuccessorList.cc:101-119):
-        // t, then t's successors outside [v, t], at most successorListSize - 1 of them looked at;
-        // every entry not re-added is dropped (removeOldSuccessors, 170-194)
-        uint32_t* row = nl.data() + (size_t)j * sls;
-        int k = 0;
-        row[k++] = t;
-        const int ts = std::min<int>(c->h_nsucc[t], sls - 1);
-        for (int q = 0; q < ts; ++q) {
-            const uint32_t x = c->h_succ[(size_t)t * sls + q];
-            if (!between_LR(id[x], id[v], id[t])) row[k++] = x;
-        }
-        nn[j] = (uint8_t)k;
-    }
-    // rpcNotify at t (1106-1189): the caller becomes t's predecessor when it lies in (pred, t); over
-    // the round's callers that leaves the one nearest t (every acceptance moves pred closer), if
-    // it is in (pred0, t)
-    std::vector<uint32_t> best(n, 0xFFFFFFFFu);
-    for (uint64_t j = 0; j < m; ++j) {
-        const uint32_t t = tgt[j], v = nodes[j];
-        if (best[t] == 0xFFFFFFFFu || k_lt(k_sub(id[t], id[v]), k_sub(id[t], id[best[t]]))) best[t] = v;
-    }
     uint64_t pred_changed = 0, succ_changed = 0, lists_changed = 0;
     std::vector<uint32_t> changed_succ0;
-    for (uint64_t t = 0; t < n; ++t) {
-        const uint32_t b = best[t];
-        if (b == 0xFFFFFFFFu) continue;
-        const uint32_t p0 = c->h_pred[t];
-        if ((p0 == 0xFFFFFFFFu || between_open(id[b], id[p0], id[t])) && b != p0) {
-            c->h_pred[t] = b;
-            ++pred_changed;
-        }
-    }
-    for (uint64_t j = 0; j < m; ++j) {
-        const uint32_t v = nodes[j];
-        uint32_t* row = c->h_succ.data() + (size_t)v * sls;
-        const bool same = nn[j] == c->h_nsucc[v] && std::equal(row, row + nn[j], nl.data() + (size_t)j * sls);
-        if (!same) ++lists_changed;
-        if (row[0] != nl[(size_t)j * sls]) { ++succ_changed; changed_succ0.push_back(v); }
-        std::copy(nl.data() + (size_t)j * sls, nl.data() + (size_t)(j + 1) * sls, row);
-        c->h_nsucc[v] = nn[j];
-        c->h_succ0[v] = row[0];
-    }
+    c->ch.stabilize(nodes, m, &succ_changed, &lists_changed, &pred_changed, &changed_succ0);
     // upload: the lists, the predecessors, and the resolved finger rows whose successor changed
     // (getFinger falls back to the successor, ChordFingerTable.cc:174-193)
     HIPCHK(c, hipSetDevice(c->device));
-    for (uint32_t v : changed_succ0) resolve_row(c, v);
-    HIPCHK(c, hipMemcpy(c->pred, c->h_pred.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->succ, c->h_succ.data(), sizeof(uint32_t) * n * sls, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->nsucc, c->h_nsucc.data(), n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->pred, c->ch.pred.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->succ, c->ch.succ.data(), sizeof(uint32_t) * n * sls, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->nsucc, c->ch.nsucc.data(), n, hipMemcpyHostToDevice));
     if (changed_succ0.size() * 8 >= n) {
-        HIPCHK(c, hipMemcpy(c->fres, c->h_fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->fres, c->ch.fres.data(), sizeof(uint32_t) * n * 160, hipMemcpyHostToDevice));
     } else {
         for (uint32_t v : changed_succ0)
-            HIPCHK(c, hipMemcpy(c->fres + (uint64_t)v * 160, c->h_fres.data() + (uint64_t)v * 160,
+            HIPCHK(c, hipMemcpy(c->fres + (uint64_t)v * 160, c->ch.fres.data() + (uint64_t)v * 160,
                                 sizeof(uint32_t) * 160, hipMemcpyHostToDevice));
     }
     if (stats) {
@@ -761,9 +648,9 @@ ovs_status ovs_chord_export_tables(ovs_ctx* c, uint32_t* pred, uint32_t* succ, u
     if (!c || !pred || !succ || !nsucc) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_CHORD || c->ideal)
         return fail(c, OVS_ESTATE, "explicit Chord tables (ovs_chord_load_tables) needed");
-    std::copy(c->h_pred.begin(), c->h_pred.end(), pred);
-    std::copy(c->h_succ.begin(), c->h_succ.end(), succ);
-    std::copy(c->h_nsucc.begin(), c->h_nsucc.end(), nsucc);
+    std::copy(c->ch.pred.begin(), c->ch.pred.end(), pred);
+    std::copy(c->ch.succ.begin(), c->ch.succ.end(), succ);
+    std::copy(c->ch.nsucc.begin(), c->ch.nsucc.end(), nsucc);
     return OVS_OK;
 }
 
@@ -1068,64 +955,13 @@ ovs_status ovs_epichord_load(ovs_ctx* c, const ovs_key160* ids, uint64_t n, cons
     if (L < 1 || L > EPI_MAXL) return fail(c, OVS_ENOTSUP, "EpiChord successorListSize must be 1..16");
     if (!(c->P.cacheTTL >= 0)) return fail(c, OVS_EINVAL, "cacheTTL must be >= 0");
     if (n < 2 || n >= 0xFFFFFFFFull) return fail(c, OVS_EINVAL, "node count out of range");
-    const K160* keys = reinterpret_cast<const K160*>(ids);
-    for (uint64_t v = 1; v < n; ++v)
-        if (!k_lt(keys[v - 1], keys[v])) return fail(c, OVS_EINVAL, "node ids must be sorted ascending and unique");
-    const K160 one{{1, 0, 0, 0, 0}}, zero{{0, 0, 0, 0, 0}};
-    auto node_err = [&](uint64_t v, const char* what) {
-        return fail(c, OVS_EINVAL, "EpiChord snapshot, node " + std::to_string(v) + ": " + what);
-    };
-    std::vector<uint32_t> meta(n);
-    for (uint64_t v = 0; v < n; ++v) {
-        const int ns = nsucc[v], np = npred[v], full = lists_full[v] & 3;
-        const int cnt[2] = {ns, np};
-        const uint32_t* lst[2] = {succ + v * L, pred + v * L};
-        for (int l = 0; l < 2; ++l) {
-            // EpiChordNodeList (EpiChordNodeList.cc:56-161): thisNode stays in the map (last) until
-            // the list holds nodeListSize other nodes; isFull() is its absence
-            const bool isfull = (full >> l) & 1;
-            if (cnt[l] > L) return node_err(v, "more list entries than successorListSize");
-            if (isfull ? cnt[l] == 0 : cnt[l] == L) return node_err(v, "isFull() inconsistent with the list length");
-            K160 prev{};
-            for (int i = 0; i < cnt[l]; ++i) {
-                const uint32_t x = lst[l][i];
-                if (x >= n || x == v) return node_err(v, "list entry is not another node");
-                K160 off = k_sub(keys[x], keys[v]);
-                if (l == 1) off = k_sub(zero, off);
-                if (i && !k_lt(prev, off)) return node_err(v, "list entries not closest first / repeated");
-                prev = off;
-            }
-        }
-        meta[v] = (uint32_t)ns | ((uint32_t)np << 8) | ((uint32_t)full << 16);
-    }
-    if (cache_off[0] != 0) return fail(c, OVS_EINVAL, "cache_off[0] must be 0");
+    std::vector<uint32_t> meta, cn;
+    std::vector<int64_t> cl, ct;
+    std::string err;
+    if (!epichord_prepare(reinterpret_cast<const K160*>(ids), n, L, succ, nsucc, pred, npred, lists_full, cache_off,
+                          cache_node, cache_last_ns, cache_ttl_ns, &meta, &cn, &cl, &ct, &err))
+        return fail(c, OVS_EINVAL, err);
     const uint64_t E = cache_off[n];
-    if (E && (!cache_node || !cache_last_ns || !cache_ttl_ns)) return OVS_EINVAL;
-    std::vector<uint32_t> cn(E);
-    std::vector<int64_t> cl(E), ct(E);
-    std::vector<uint64_t> perm;
-    std::vector<K160> sums;
-    for (uint64_t v = 0; v < n; ++v) {
-        const uint64_t a = cache_off[v], b = cache_off[v + 1];
-        if (b < a || b > E) return node_err(v, "cache_off not monotone");
-        // liveCache order: x - (thisNode + 1) (EpiChordFingerCache.cc:85, 117-126)
-        const K160 base = k_add(keys[v], one);
-        perm.resize(b - a);
-        sums.resize(b - a);
-        for (uint64_t i = a; i < b; ++i) {
-            const uint32_t x = cache_node[i];
-            if (x >= n || x == v) return node_err(v, "cache entry is not another node");
-            if (cache_ttl_ns[i] < 0) return node_err(v, "negative cache ttl");
-            perm[i - a] = i;
-            sums[i - a] = k_sub(keys[x], base);
-        }
-        std::sort(perm.begin(), perm.end(), [&](uint64_t p, uint64_t q) { return k_lt(sums[p - a], sums[q - a]); });
-        for (uint64_t i = 0; i < b - a; ++i) {
-            const uint64_t j = perm[i];
-            if (i && cache_node[j] == cn[a + i - 1]) return node_err(v, "a node twice in the finger cache");
-            cn[a + i] = cache_node[j]; cl[a + i] = cache_last_ns[j]; ct[a + i] = cache_ttl_ns[j];
-        }
-    }
     ovs_status st = upload_nodes(c, ids, n, xy, false);
     if (st != OVS_OK) { free_tables(c); return st; }
     EpiTables& T = c->epi;

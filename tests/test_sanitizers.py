@@ -39,3 +39,25 @@ def test_oracle_and_ini_binder_clean_under_asan_ubsan(tmp_path):
                OMP_NUM_THREADS="2")
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and "clean" in r.stdout, r.stdout[-3000:] + r.stderr[-6000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_host_table_bookkeeping_clean_under_asan_ubsan(tmp_path):
+    """The C ABI's host-side table code (oversim_amd/csrc/host_tables.cpp: explicit Chord tables, the
+    fixfingers and stabilize rounds' updates, EpiChord snapshot validation and ordering) built with
+    plain g++ under ASan/UBSan -Werror and driven through a converging ring and broken inputs
+    (tests/host_tables_driver.cpp)."""
+    inc = ["-I", str(ROOT / "oversim_amd" / "csrc")]
+    objs = []
+    for src, o in ((ROOT / "oversim_amd" / "csrc" / "host_tables.cpp", "ht.o"),
+                   (ROOT / "tests" / "host_tables_driver.cpp", "drv.o")):
+        c = ["g++", "-std=c++17", *SAN, *WARN, *inc, "-c", str(src), "-o", str(tmp_path / o)]
+        r = subprocess.run(c, capture_output=True, text=True)
+        assert r.returncode == 0, f"{' '.join(c)}\n{r.stdout}{r.stderr}"
+        objs.append(str(tmp_path / o))
+    exe = tmp_path / "host_tables_driver"
+    r = subprocess.run(["g++", *SAN, *objs, "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0 and "clean" in r.stdout, r.stdout[-3000:] + r.stderr[-6000:]
