@@ -156,21 +156,24 @@ __device__ __forceinline__ void put_entry(KadBlk* __restrict__ blks, uint64_t bl
     b->top[q % KBLK] = x == NONE ? ~0ull : ktop(kload(recs, x));
 }
 
-// a node's sibling row: its S5 entries (NONE padded) in ascending level msb(x ^ v), stable -- the
-// siblings at levels <= l are a prefix, so a findNode whose answer lies below 2^(l+1) reads only
-// that prefix's blocks (kad_sib_prefix)
+// a node's sibling row: the node itself, then its S5 siblings (NONE padded) in ascending level
+// msb(x ^ v), stable -- the node and its siblings at levels <= l are a prefix, so a findNode whose
+// answer lies below 2^(l+1) reads only that prefix's blocks (kad_sib_prefix), and the node itself --
+// a candidate of every sibling-zone findNode (Kademlia.cc:1207-1211) -- comes with the first block
 __device__ void put_sibling_row(KadBlk* __restrict__ blks, uint64_t blk0, int sbn, const uint32_t* L, int S5,
-                                const K160& me, const KeyRec* __restrict__ recs)
+                                uint32_t self, const K160& me, const KeyRec* __restrict__ recs)
 {
-    uint32_t x[64];
-    uint8_t lv[64];
-    int cnt = 0;
+    uint32_t x[65];
+    uint8_t lv[65];
+    x[0] = self;
+    lv[0] = 0;
+    int cnt = 1;
     for (int i = 0; i < S5 && i < 64; ++i) {
         if (L[i] == NONE) continue;
         // insertion by level, stable
         const uint8_t l = (uint8_t)k_msb(k_xor(kload(recs, L[i]), me));
         int j = cnt++;
-        while (j > 0 && lv[j - 1] > l) { x[j] = x[j - 1]; lv[j] = lv[j - 1]; --j; }
+        while (j > 1 && lv[j - 1] > l) { x[j] = x[j - 1]; lv[j] = lv[j - 1]; --j; }
         x[j] = L[i];
         lv[j] = l;
     }
@@ -189,7 +192,7 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
     const K160 me = as_key(r.key);
     const uint32_t* L = sib + (uint64_t)v * S5;
     // sibling row
-    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, L, S5, me, recs);
+    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, L, S5, v, me, recs);
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     uint32_t lo = 0, hi = n;
@@ -306,7 +309,7 @@ __global__ void k_kad_explicit_rows(const KeyRec* __restrict__ recs, const KadNo
     if (v >= n) return;
     const KadNode r = nodes[v];
     const uint32_t* L = sib + (uint64_t)v * S5;
-    put_sibling_row(blks, sib_base + (uint64_t)v * sbn, sbn, L, S5, kload(recs, v), recs);
+    put_sibling_row(blks, sib_base + (uint64_t)v * sbn, sbn, L, S5, v, kload(recs, v), recs);
     const int rowlo = kad_rowlo(r.meta);
     if (rowlo < 0) return;
     const int bpb = (k + KBLK - 1) / KBLK;
@@ -410,7 +413,7 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     if (k < 1 || k > KMAX) return hipErrorNotSupported;
     const int bpb = (k + KBLK - 1) / KBLK;
     t.bpb = bpb;
-    const int S5 = 5 * s, sbn = (S5 + KBLK - 1) / KBLK;
+    const int S5 = 5 * s, sbn = (S5 + 1 + KBLK - 1) / KBLK;   // the node + its siblings
     const uint32_t nown = hi - lo;
     uint64_t *rowlen = nullptr, *off = nullptr;
     uint32_t* sib_all = nullptr;
@@ -468,7 +471,7 @@ hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n,
     t.k = k; t.s = s; t.seed = 0; t.lo = 0; t.hi = n; t.snapshot = 0;
     if (k < 1 || k > KMAX) return hipErrorNotSupported;
     t.bpb = (k + KBLK - 1) / KBLK;
-    const int S5 = 5 * s, sbn = (S5 + KBLK - 1) / KBLK;
+    const int S5 = 5 * s, sbn = (S5 + 1 + KBLK - 1) / KBLK;   // the node + its siblings
     uint64_t *rowlen = nullptr, *off = nullptr;
     uint32_t* flags = nullptr;
     void* tmp = nullptr;

@@ -343,7 +343,7 @@ __device__ __forceinline__ bool kad_is_sibling(const KadView& V, const KadNode& 
         return closer < numSiblings;
     }
     const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
-    for (int i = 0; i < nsib; ++i) {
+    for (int i = 1; i <= nsib; ++i) {           // row entry 0 is c itself
         const uint32_t x = L[i / KBLK].idx[i % KBLK];
         closer += (int)kbit(D, k_msb(k_xor(node_key(V.nodes, x), me)));
     }
@@ -369,6 +369,10 @@ __device__ __forceinline__ RespGeo resp_geo(const KadNode& r, const K160& K)
     return g;
 }
 
+// entries of a sibling row (c itself + its siblings by level) read for a prefix of pre siblings:
+// whole blocks
+__device__ __forceinline__ int kad_row_read(int pre) { return KBLK * ((pre + 1 + KBLK - 1) / KBLK); }
+
 // the first of the V.bpb blocks of bucket `bucket` of a node whose row starts at boff
 __device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t boff, int bucket)
 {
@@ -379,8 +383,8 @@ __device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t bof
 // block form: the candidate sets of the reference's scan (bucket m, then buckets m-1..endIndex with
 // the sibling table and self when m >= endIndex or the result is short, then buckets above m while
 // it is short) merged one table block at a time into the top C.  Returns the result size.
-// pre >= 0 (a findNode in the sibling zone, m <= endIndex): only the first pre entries of c's
-// level-sorted sibling row can enter the result (kad_sib_prefix); the rest are counted, not read.
+// pre >= 0 (a findNode in the sibling zone, m <= endIndex): only c and the first pre siblings of c's
+// level-sorted row can enter the result (kad_sib_prefix); the rest are counted, not read.
 template <bool EX, int C = 8>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
                                                  int numRedundant, bool sib, BlkN<C>& res, int numSiblings = 1,
@@ -430,17 +434,12 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     // m fills the result, the rest of the scan cannot change it
     if ((g.m >= g.endIndex || seen < rs) && !(g.m > g.endIndex && n >= cap)) {
         for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
+        // the row: c itself, then its siblings by level (put_sibling_row)
         const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
-        const int rd = pre < 0 ? g.nsib : min(g.nsib, KBLK * ((pre + KBLK - 1) / KBLK));
+        const int tot = g.nsib + 1;
+        const int rd = pre < 0 ? tot : min(tot, kad_row_read(pre));
         for (int j = 0; j * KBLK < rd; ++j) add_blk(L + j);
-        seen += g.nsib - rd;
-        Blk8 self;
-        blk_clear(self);
-        self.x[0] = c;
-        self.d[0] = dist_hi(node_key(V.nodes, c), K);
-        blk_merge_top<false, EX, C, 8>(res, self, K, V.nodes);
-        n = blk_trunc(res, cap);
-        seen += 1;
+        seen += tot - rd;
     }
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);
     return n;
@@ -506,10 +505,8 @@ __device__ __forceinline__ int kad_find_node_ins(const KadView& V, uint32_t c, c
     if (g.m >= 0) add_slot(g.m);
     if ((g.m >= g.endIndex || seen < rs) && !(g.m > g.endIndex && res.n >= cap)) {   // as kad_find_node_blk
         for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
-        const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
-        for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
-        svec_add<CAP, EX>(res, cap, c, dist_hi(node_key(V.nodes, c), K), K, V.nodes);
-        seen += 1;
+        const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;   // c itself, then its siblings
+        for (int j = 0; j * KBLK < g.nsib + 1; ++j) add_blk(L + j);
     }
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);
     return res.n;
@@ -967,14 +964,17 @@ __device__ __forceinline__ int kad_event_after_find(KadLookup<A, C>& L, const Ka
 // m-1 .. endIndex, the sibling table and c itself.  In the sibling zone m <= endIndex the buckets
 // below m are empty unless an imported table stores bucket m < endIndex: those (and the [self]
 // answers, the buckets above endIndex, off-arc responders) stay on the per-lane path.
+// A scan of one block (no main bucket, the row prefix within the first block) stays on the lane.
 __device__ __forceinline__ bool kad_find_is_coop(const KadView& V, uint32_t c, const RespGeo& g, bool sib,
-                                                 int numSiblings)
+                                                 int numSiblings, int pre)
 {
     if (g.nsib == 0 || (V.snapshot && sib && numSiblings <= 1)) return false;
     if (V.err && kad_off_arc(V, c)) return false;
     if (g.m > g.endIndex) return false;
     const bool stored_below = g.m < g.endIndex && g.rowlo >= 0 && g.m >= g.rowlo;
-    return !stored_below;
+    if (stored_below) return false;
+    const int nmain = g.m >= 0 && g.rowlo >= 0 && g.m >= g.rowlo ? 1 : 0;
+    return nmain + kad_row_read(pre) / KBLK >= 2;
 }
 
 // position of the t-th (from 0) set bit of m (m has more than t set bits)
@@ -1028,7 +1028,7 @@ __device__ __forceinline__ void wave_lds_sync()
 }
 
 // Whole wave (uniform control flow): for every lane with want set, the candidates of its sibling-zone
-// findNode -- bucket m if stored, the sibling table blocks, c itself -- merged into the top 8 by XOR
+// findNode -- bucket m if stored, the row blocks (c itself, then the siblings) -- merged into the top 8 by XOR
 // distance to K (left in S.res at the lane's slot) and how many candidates there were (S.rcnt).
 // Eight lanes per findNode: lane j of a group loads and sorts item j (and j + 8, ...), the group
 // merges in three butterfly steps through LDS (lanes ^1, ^2, ^4), the leader stores the result for
@@ -1059,16 +1059,11 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
 #pragma unroll
         for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
         const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;   // k <= 8: one block
-        const int nsb = (opre + KBLK - 1) / KBLK;     // the level-sorted row's prefix that matters
-        const int nitems = live ? nmain + nsb + 1 : 0;
+        const int nsb = kad_row_read(opre) / KBLK;    // the row's prefix that matters (c first)
+        const int nitems = live ? nmain + nsb : 0;
         auto load_item = [&](int i, Blk8& b) -> int {
             if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
-            if (i < nmain + nsb)
-                return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(i - nmain), oK);
-            blk_clear(b);
-            b.x[0] = oc;
-            b.d[0] = dist_hi(node_key(V.nodes, oc), oK);
-            return 1;
+            return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(i - nmain), oK);
         };
         Blk8 acc;
         int cnt = 0;
@@ -1185,7 +1180,7 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
     V.nodes = t.nodes; V.nodex = t.nodex; V.blks = t.blks; V.sibb = t.blks ? t.blks + t.rows_blks : nullptr;
     V.slev = t.slev;
     V.xy = xy; V.n = n; V.k = t.k; V.bpb = t.bpb; V.S5 = 5 * t.s;
-    V.sbn = (V.S5 + KBLK - 1) / KBLK;
+    V.sbn = (V.S5 + 1 + KBLK - 1) / KBLK;     // c itself + its siblings
     V.lo = t.lo; V.hi = t.hi;
     V.maybe_short = t.maybe_short;
     V.snapshot = t.snapshot;

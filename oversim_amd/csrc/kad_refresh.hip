@@ -147,9 +147,8 @@ struct XCtx {
         if (g.m >= 0) add_slot(g.m);
         if (g.m >= g.endIndex || n < rs) {
             for (int b = g.m - 1; b >= g.endIndex; --b) add_slot(b);
-            const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
-            for (int j = 0; j * KBLK < g.nsib; ++j) add_blk(L + j);
-            vadd(X.res_idx, X.res_d, nullptr, rs, &n, c, dself, K);
+            const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;     // c itself, then its siblings
+            for (int j = 0; j * KBLK < g.nsib + 1; ++j) add_blk(L + j);
         }
         for (int b = g.m + 1; n < rs && b < KEYBITS; ++b) add_slot(b);
         return n;
