@@ -119,7 +119,9 @@ struct KadRouteIO {
     uint8_t* __restrict__ ltag;
 };
 
-template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C>
+// SH: explicit tables with short sibling tables (KadTables::maybe_short): a send may have to count
+// the responder's scan (kad_response_size); snapshot tables never do
+template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C, bool SH>
 // the shard step runs at 2 waves/SIMD: its HBM state traffic and request staging need the registers
 // (at 3 the exact-compare instantiations spilled in misaligned 96-bit pieces gfx950 rejects)
 __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
@@ -260,9 +262,9 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                 if (SHARD) {
                     const ShardSend on{io.res, q * A, &L.K, io.shard_lo, io.nsh, V.lo, V.hi, io.rstage, io.rtag,
                                        LK ? (0x80000000u | (uint32_t)ns) : 0u};
-                    kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, on);
+                    kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, on);
                 } else {
-                    kad_send_rpcs<A, EX, LK>(L, V, DC, LC, num, SendNothing{});
+                    kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, SendNothing{});
                 }
             }
             if (kad_lookup_done(L)) {
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
 }  // namespace
 
 // persistent grid: as many waves as are resident, each with a contiguous slice of the batch
-template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C = 8>
+template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C = 8, bool SH = true>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, KadRouteIO io, int num_cu,
                              hipStream_t st)
 {
@@ -325,7 +327,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     // initialised once, thread-safely)
     static const int bpc = [] {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SHARD, C>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SHARD, C, SH>, 256, 0) !=
                 hipSuccess ||
             b < 1)
             b = 1;
@@ -340,7 +342,8 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kad_stats), z, sizeof z, 0, hipMemcpyHostToDevice, st);
 #endif
-    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SHARD, C>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC, io);
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SHARD, C, SH>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC,
+                       io);
 #ifdef OVS_KAD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
@@ -364,9 +367,14 @@ hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC
         if (hopseq) return kad_launch<A, true, EX, false, false, 16>(V, DC, LC, io, num_cu, st);
         return kad_launch<A, false, EX, false, false, 16>(V, DC, LC, io, num_cu, st);
     }
-    if (sibs) return kad_launch<A, false, EX, true, false>(V, DC, LC, io, num_cu, st);
-    if (hopseq) return kad_launch<A, true, EX, false, false>(V, DC, LC, io, num_cu, st);
-    return kad_launch<A, false, EX, false, false>(V, DC, LC, io, num_cu, st);
+    if (V.maybe_short) {
+        if (sibs) return kad_launch<A, false, EX, true, false, 8, true>(V, DC, LC, io, num_cu, st);
+        if (hopseq) return kad_launch<A, true, EX, false, false, 8, true>(V, DC, LC, io, num_cu, st);
+        return kad_launch<A, false, EX, false, false, 8, true>(V, DC, LC, io, num_cu, st);
+    }
+    if (sibs) return kad_launch<A, false, EX, true, false, 8, false>(V, DC, LC, io, num_cu, st);
+    if (hopseq) return kad_launch<A, true, EX, false, false, 8, false>(V, DC, LC, io, num_cu, st);
+    return kad_launch<A, false, EX, false, false, 8, false>(V, DC, LC, io, num_cu, st);
 }
 
 template <int A, bool EX>
@@ -380,8 +388,10 @@ hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const 
     io.st = a.st; io.act = a.act; io.res = a.res; io.list = a.list; io.nlist_dev = a.nlist_dev; io.qids = a.qids;
     io.shard_lo = a.shard_lo; io.nsh = a.nsh;
     io.rstage = a.rstage; io.rtag = a.rtag; io.dstage = a.dstage; io.ltag = a.ltag;
-    if (a.sib_out) return kad_launch<A, false, EX, true, true>(V, DC, LC, io, num_cu, st);
-    return kad_launch<A, false, EX, false, true>(V, DC, LC, io, num_cu, st);
+    // sharded networks are snapshot builds: never short
+    if (V.maybe_short) return hipErrorNotSupported;
+    if (a.sib_out) return kad_launch<A, false, EX, true, true, 8, false>(V, DC, LC, io, num_cu, st);
+    return kad_launch<A, false, EX, false, true, 8, false>(V, DC, LC, io, num_cu, st);
 }
 
 template hipError_t kad_route_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
