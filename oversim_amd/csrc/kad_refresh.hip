@@ -206,6 +206,50 @@ struct XCtx {
         return pos;
     }
 
+    // The register LookupVector's add loop over one sorted findNode block (handleResponse 853-870),
+    // as a merge: nextHops <- the 2R closest distinct nodes of nextHops and the block, alreadyUsed
+    // flags travelling with their nodes.  The adds run in the block's (distance) order, so a block
+    // node's insertion position is its position in the merged vector; returns how many entered at a
+    // position < R (numNewRpcs).
+    __device__ __forceinline__ int nh_merge_blk(XLookup& L, XRegNh& H, const Blk8& r, int cnt) const
+    {
+        const int cap = 2 * C.R;
+        BlkN<16> a;
+        Blk8 b;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const bool in = i < L.nnh;
+            a.x[i] = in ? H.idx[i] : NONE;
+            a.d[i] = in ? H.d[i] : ~0ull;
+            a.f[i] = in ? ((H.used >> i) & 1u) : 0u;
+        }
+        bool dup = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            bool dj = j >= cnt;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dj |= r.x[j] == a.x[i];
+            dup |= j < cnt && dj;
+            b.x[j] = dj ? NONE : r.x[j];
+            b.d[j] = dj ? ~0ull : r.d[j];
+            b.f[j] = 2u;
+        }
+        if (dup) blk_sort8<false, EX>(b, L.K, V.nodes);     // the nodes already present leave holes: to the end
+        blk_merge_top<true, EX, 16, 8>(a, b, L.K, V.nodes);
+        L.nnh = blk_trunc(a, cap);
+        int numNew = 0;
+        uint32_t used = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            H.idx[i] = a.x[i];
+            H.d[i] = a.d[i];
+            numNew += (i < C.R && a.x[i] != NONE && (a.f[i] & 2u)) ? 1 : 0;
+            used |= (a.x[i] != NONE && (a.f[i] & 1u)) ? (1u << i) : 0u;
+        }
+        H.used = used;
+        return numNew;
+    }
+
     __device__ __forceinline__ uint32_t nh_idx(const XRegNh& H, int q) const
     {
         if constexpr (!REG) return X.nh_idx[at(q)];
@@ -413,53 +457,60 @@ struct XCtx {
         R.infos = 1;
     }
 
-    // One iteration of the lookup's loop; true when the lookup has ended.  The start, responses
-    // and timeouts share a single findNode, LookupVector merge and sendRpc site:
-    //   start (IterativeLookup::start 133-244): findNode(key, k, -1) at the source, all into nextHops,
-    //     sendRpc(alpha), checkStop;
-    //   per event (handleRpcResponse 488-585 / handleRpcTimeout 588-654): every RpcInfo of the node in
-    //     turn -- the first of a response is handleResponse (803-921), the others and those of a
-    //     timeout handleTimeout (935-1023) -- each possibly followed by a sendRpc, then checkStop.
+    // the next event of the lookup (after checkStop): the earliest pending one by (time, insertion
+    // time, sequence); true when the lookup has ended
+    __device__ __forceinline__ bool pick(XLookup& L, Run& R) const
+    {
+        XPend& cur = R.cur;
+        if (check_stop(L)) return true;
+        int e = -1;
+        int64_t bt = 0, bi = 0;
+        uint32_t bs = 0;
+#pragma unroll
+        for (int i = 0; i < XMAXA; ++i) {
+            if (!((L.pvalid >> i) & 1u)) continue;
+            const XPend& P = L.p[i];
+            if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
+                e = i; bt = P.t; bi = P.tins; bs = P.seq;
+            }
+        }
+        if (e < 0) return true;
+#pragma unroll
+        for (int i = 0; i < XMAXA; ++i) {
+            const bool me = i == e;
+            cur.node = me ? L.p[i].node : cur.node;
+            cur.ninfo = me ? L.p[i].ninfo : cur.ninfo;
+            cur.tsend = me ? L.p[i].tsend : cur.tsend;
+            cur.to = me ? L.p[i].to : cur.to;
+        }
+        L.pvalid &= ~(1u << e);
+        L.now = bt;
+        if (cur.to) {
+            L.any_to = true;                 // setDead(dest)
+            if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = cur.node;
+            else { L.err = true; return true; }
+        }
+        R.infos = cur.ninfo;
+        R.handled = false;
+        return false;
+    }
+
+    // One iteration of the lookup's loop: one RpcInfo of the event in hand, then -- when that was
+    // its last -- checkStop and the pick of the next event, in the same iteration (a wave's lanes
+    // do not split its iterations between picking and handling); true when the lookup has ended.
     __device__ __forceinline__ bool step(XLookup& L, Run& R) const
+    {
+        if (L.err) return true;
+        if (handle(L, R)) return true;
+        return R.infos == 0 ? pick(L, R) : false;
+    }
+
+    // one RpcInfo of the event in hand; true when the lookup has ended
+    __device__ __forceinline__ bool handle(XLookup& L, Run& R) const
     {
         XRegNh& H = R.H;
         XPend& cur = R.cur;
-        if (L.err) return true;
         int num = -1;
-        if (R.infos == 0) {
-            if (check_stop(L)) return true;
-            // the earliest pending event: (time, insertion time, sequence)
-            int e = -1;
-            int64_t bt = 0, bi = 0;
-            uint32_t bs = 0;
-#pragma unroll
-            for (int i = 0; i < XMAXA; ++i) {
-                if (!((L.pvalid >> i) & 1u)) continue;
-                const XPend& P = L.p[i];
-                if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
-                    e = i; bt = P.t; bi = P.tins; bs = P.seq;
-                }
-            }
-            if (e < 0) return true;
-#pragma unroll
-            for (int i = 0; i < XMAXA; ++i) {
-                const bool me = i == e;
-                cur.node = me ? L.p[i].node : cur.node;
-                cur.ninfo = me ? L.p[i].ninfo : cur.ninfo;
-                cur.tsend = me ? L.p[i].tsend : cur.tsend;
-                cur.to = me ? L.p[i].to : cur.to;
-            }
-            L.pvalid &= ~(1u << e);
-            L.now = bt;
-            if (cur.to) {
-                L.any_to = true;                 // setDead(dest)
-                if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = cur.node;
-                else { L.err = true; return true; }
-            }
-            R.infos = cur.ninfo;
-            R.handled = false;
-            return false;
-        }
         --R.infos;
         if (!R.start && L.pfinished) return false;     // "do not handle finished paths"
         if (R.start || (!cur.to && !R.handled)) {
@@ -495,11 +546,12 @@ struct XCtx {
                     // in the sibling zone only the level-sorted row's prefix can enter the answer
                     const int pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, rs < 8 ? rs : 8) : -1;
                     cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1, pre);
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        if (i >= cnt) continue;
-                        const int pos = nh_add(L, H, b.x[i], b.d[i]);
-                        numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
+                    if constexpr (REG) numNew = nh_merge_blk(L, H, b, cnt);
+                    else {
+                        for (int i = 0; i < cnt; ++i) {
+                            const int pos = nh_add(L, H, b.x[i], b.d[i]);
+                            numNew += (pos >= 0 && pos < C.R) ? 1 : 0;
+                        }
                     }
                 } else {
                     cnt = find_node_scratch(cur.node, g, L.K, rs);
