@@ -385,10 +385,12 @@ __device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t bof
 // it is short) merged one table block at a time into the top C.  Returns the result size.
 // pre >= 0 (a findNode in the sibling zone, m <= endIndex): only c and the first pre siblings of c's
 // level-sorted row can enter the result (kad_sib_prefix); the rest are counted, not read.
+// r0 > 0: the entries before row entry r0 cannot enter the result either (kad_sib_range: the
+// siblings at level m alone fill it); they are counted, not read.
 template <bool EX, int C = 8>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
                                                  int numRedundant, bool sib, BlkN<C>& res, int numSiblings = 1,
-                                                 int pre = -1)
+                                                 int pre = -1, int r0 = 0)
 {
     blk_clear(res);
     if (V.err && kad_off_arc(V, c)) {
@@ -438,8 +440,9 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         const KadBlk* L = V.sibb + (uint64_t)(c - V.lo) * V.sbn;
         const int tot = g.nsib + 1;
         const int rd = pre < 0 ? tot : min(tot, kad_row_read(pre));
-        for (int j = 0; j * KBLK < rd; ++j) add_blk(L + j);
-        seen += tot - rd;
+        const int j0 = r0 / KBLK;
+        for (int j = j0; j * KBLK < rd; ++j) add_blk(L + j);
+        seen += tot - (rd - j0 * KBLK);
     }
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);
     return n;
@@ -631,7 +634,7 @@ struct KadLC {
 struct Pend {
     uint32_t node;
     uint32_t tag;      // step at send (bits 0..15) | insertion sequence (bits 16..30) | timeout (bit 31)
-    int64_t t;         // event time (bits 0..55, ns) | the responder's sibling-row prefix (56..62, kad_sib_prefix)
+    int64_t t;         // event time (bits 0..55, ns) | the responder's sibling-row blocks (56..63, kad_row_blocks)
     uint32_t dins;     // t - insertion time
     uint32_t geo;      // responder: m + 1 (bits 0..7) | endIndex + 1 (8..15) | rowlo + 1 (16..23) | sib (24)
                        // | sibling count (25..31; 5s <= 120)
@@ -657,6 +660,32 @@ __device__ __forceinline__ int kad_sib_prefix(const RespGeo& g, uint32_t lev, in
     }
     return pre;
 }
+
+// The row range a sibling-zone findNode with result capacity cap must read: (first entry, prefix
+// as kad_sib_prefix).  The siblings at level m = msb(c ^ K) lie below 2^m from K -- closer than c
+// and every other sibling -- so when m is one of the four levels endIndex .. endIndex - 3 whose
+// counts KadNode.spare carries and that level alone holds cap siblings, they are the only row
+// entries that can enter the result (row entries 1 + count(levels < m) .. count(levels <= m)).
+__device__ __forceinline__ int2 kad_sib_range(const RespGeo& g, uint32_t lev, int cap)
+{
+    const int k = g.endIndex - g.m;
+    if (k >= 0 && k <= 3) {
+        const int hi = k == 0 ? g.nsib : (int)((lev >> (8 * (k - 1))) & 0xFFu);   // siblings at levels <= m
+        const int lo = (int)((lev >> (8 * k)) & 0xFFu);                            // at levels < m
+        if (hi - lo >= cap) return make_int2(1 + lo, hi);
+    }
+    return make_int2(0, kad_sib_prefix(g, lev, cap));
+}
+
+// kad_sib_range at block granularity, in one byte (Pend.t bits 56..63): the first row block to
+// read (bits 0..3) and the last (4..7); rows hold at most 121 entries = 16 blocks
+__device__ __forceinline__ int kad_row_blocks(const RespGeo& g, uint32_t lev, int cap)
+{
+    const int2 r = kad_sib_range(g, lev, cap);
+    return (r.x / KBLK) | ((r.y / KBLK) << 4);
+}
+__device__ __forceinline__ int rb_pre(int rb) { return (rb >> 4) * KBLK; }   // a prefix through the last block
+__device__ __forceinline__ int rb_r0(int rb) { return (rb & 15) * KBLK; }    // the first block's first entry
 
 __device__ __forceinline__ uint32_t pack_geo(const RespGeo& g, bool sb)
 {
@@ -752,7 +781,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A, C>& L, const KadView& V, c
     const uint32_t sR = L.seq++;
     const uint32_t tag = (uint32_t)L.step | ((isTo ? sTo : sR) << 16) | (isTo ? 0x80000000u : 0u);
     const int rcap = min(sb ? (ns ? ns : 1) : LC.redundant, C);
-    const int64_t pre = rg.m <= rg.endIndex ? (int64_t)kad_sib_prefix(rg, rr.spare, rcap) : 0;
+    const int64_t pre = rg.m <= rg.endIndex ? (int64_t)kad_row_blocks(rg, rr.spare, rcap) : 0;
     int slot = 0;
 #pragma unroll
     for (int i = A - 1; i >= 0; --i)
@@ -835,7 +864,7 @@ struct KadEv {
     int e;             // pending slot of the event (-1 at start)
     int numR;          // numRedundantNodes of the findNode
     int num;           // KEV_SENDS: RPCs to send
-    int pre;           // sibling-row prefix a sibling-zone findNode reads (kad_sib_prefix)
+    int pre;           // the sibling-row blocks a sibling-zone findNode reads (kad_row_blocks)
     bool start;
     __device__ __forceinline__ bool sb() const { return (geo >> 24) & 1u; }
     __device__ __forceinline__ RespGeo rg() const { return unpack_geo(geo, boff); }
@@ -865,7 +894,7 @@ __device__ __forceinline__ int kad_event_begin(KadLookup<A, C>& L, const KadView
         ev.geo = pack_geo(g, sb);
         ev.boff = g.boff;
         ev.numR = LC.maxRedundantLocal;
-        ev.pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, min(sb ? (ns ? ns : 1) : ev.numR, C)) : 0;
+        ev.pre = g.m <= g.endIndex ? kad_row_blocks(g, rn.spare, min(sb ? (ns ? ns : 1) : ev.numR, C)) : 0;
     } else {
         int e = -1;
         int64_t bt = 0, bi = 0;
@@ -973,7 +1002,7 @@ __device__ __forceinline__ int kad_event_after_find(KadLookup<A, C>& L, const Ka
 // answers, the buckets above endIndex, off-arc responders) stay on the per-lane path.
 // A scan of one block (no main bucket, the row prefix within the first block) stays on the lane.
 __device__ __forceinline__ bool kad_find_is_coop(const KadView& V, uint32_t c, const RespGeo& g, bool sib,
-                                                 int numSiblings, int pre)
+                                                 int numSiblings, int pre, int r0 = 0)
 {
     if (g.nsib == 0 || (V.snapshot && sib && numSiblings <= 1)) return false;
     if (V.err && kad_off_arc(V, c)) return false;
@@ -981,7 +1010,7 @@ __device__ __forceinline__ bool kad_find_is_coop(const KadView& V, uint32_t c, c
     const bool stored_below = g.m < g.endIndex && g.rowlo >= 0 && g.m >= g.rowlo;
     if (stored_below) return false;
     const int nmain = g.m >= 0 && g.rowlo >= 0 && g.m >= g.rowlo ? 1 : 0;
-    return nmain + kad_row_read(pre) / KBLK >= 2;
+    return nmain + kad_row_read(pre) / KBLK - r0 / KBLK >= 2;
 }
 
 // position of the t-th (from 0) set bit of m (m has more than t set bits)
@@ -1035,14 +1064,14 @@ __device__ __forceinline__ void wave_lds_sync()
 }
 
 // Whole wave (uniform control flow): for every lane with want set, the candidates of its sibling-zone
-// findNode -- bucket m if stored, the row blocks (c itself, then the siblings) -- merged into the top 8 by XOR
-// distance to K (left in S.res at the lane's slot) and how many candidates there were (S.rcnt).
-// Eight lanes per findNode: lane j of a group loads and sorts item j (and j + 8, ...), the group
-// merges in three butterfly steps through LDS (lanes ^1, ^2, ^4), the leader stores the result for
-// the owner.  Up to 8 findNodes per pass.
+// findNode -- bucket m if stored, the row blocks rb names (kad_row_blocks) -- merged into the top 8
+// by XOR distance to K (left in S.res at the lane's slot) and how many candidates there were
+// (S.rcnt).  G lanes per findNode (OVS_COOP_G, 4): lane j of a group loads and sorts item j (and
+// j + G, ...), the group merges in log2 G butterfly steps through LDS, the leader stores the result
+// for the owner.  64 / G findNodes per pass.
 template <bool EX>
 __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, uint32_t c, uint32_t geo, uint32_t boff,
-                                                 int pre, const K160& K, CoopLds& S)
+                                                 int rb, const K160& K, CoopLds& S)
 {
     const uint64_t tasks = __ballot(want);
     if (tasks == 0) return;
@@ -1061,16 +1090,16 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
         const int owner = live ? nth_set_bit(tasks, t) : lane;
         const uint32_t oc = __shfl(c, owner);
         const RespGeo og = unpack_geo(__shfl(geo, owner), __shfl(boff, owner));
-        const int opre = __shfl(pre, owner);
+        const int orb = __shfl(rb, owner);
         K160 oK;
 #pragma unroll
         for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
         const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;   // k <= 8: one block
-        const int nsb = kad_row_read(opre) / KBLK;    // the row's prefix that matters (c first)
+        const int j0 = orb & 15, nsb = (orb >> 4) - j0 + 1;   // the row blocks that matter (kad_row_blocks)
         const int nitems = live ? nmain + nsb : 0;
         auto load_item = [&](int i, Blk8& b) -> int {
             if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
-            return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(i - nmain), oK);
+            return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(j0 + i - nmain), oK);
         };
         Blk8 acc;
         int cnt = 0;

@@ -544,8 +544,8 @@ struct XCtx {
                     // bucket refresh, R = 8, scans both blocks of each bucket below)
                     Blk8 b;
                     // in the sibling zone only the level-sorted row's prefix can enter the answer
-                    const int pre = g.m <= g.endIndex ? kad_sib_prefix(g, rn.spare, rs < 8 ? rs : 8) : -1;
-                    cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1, pre);
+                    const int2 rr = g.m <= g.endIndex ? kad_sib_range(g, rn.spare, rs < 8 ? rs : 8) : make_int2(0, -1);
+                    cnt = kad_find_node_blk<EX>(V, cur.node, g, L.K, rs, false, b, 1, rr.y, rr.x);
                     if constexpr (REG) numNew = nh_merge_blk(L, H, b, cnt);
                     else {
                         for (int i = 0; i < cnt; ++i) {

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                 ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, AlwaysReady{}, rec, ev);
             }
             const bool local = !SHARD || (ev.r >= V.lo && ev.r < V.hi);
-            coop = ph == KEV_FIND && local && kad_find_is_coop(V, ev.r, ev.rg(), ev.sb(), ns, ev.pre);
+            coop = ph == KEV_FIND && local && kad_find_is_coop(V, ev.r, ev.rg(), ev.sb(), ns, rb_pre(ev.pre), rb_r0(ev.pre));
         }
 
         // phase 2 (whole wave): the sibling-zone findNodes (results in LDS).  The exact-compare
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                     if constexpr (C == 8) coop_get(lds.res, threadIdx.x, fb);
                     // the candidates findNode saw: the row entries past the prefix's blocks count too
                     const RespGeo g = ev.rg();
-                    const int tot = g.nsib + 1, rd = min(tot, kad_row_read(ev.pre));
+                    const int tot = g.nsib + 1, rd = min(tot, kad_row_read(rb_pre(ev.pre))) - rb_r0(ev.pre);
                     n = kad_coop_finish<EX>(V, g, L.K, ev.numR, ev.sb(), ns, fb, (int)lds.rcnt[threadIdx.x] + tot - rd);
                 } else if (SHARD && !(ev.r >= V.lo && ev.r < V.hi)) {
                     // the owner's answer, delivered by k_kad_shard_deliver
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                     // in the sibling zone only c and the row prefix can enter the answer (ev.pre)
                     const RespGeo g = ev.rg();
                     n = kad_find_node_blk<EX, C>(V, ev.r, g, L.K, ev.numR, ev.sb(), fb, ns,
-                                                 g.m <= g.endIndex ? ev.pre : -1);
+                                                 g.m <= g.endIndex ? rb_pre(ev.pre) : -1, rb_r0(ev.pre));
 #ifdef OVS_DUP_LANEFIND
                     {   // cost experiment: the per-lane findNode again
                         K160 K2 = L.K;
