@@ -244,7 +244,8 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                         K160 K2 = L.K;
                         asm volatile("" : "+v"(K2.w[0]));
                         BlkN<C> b2;
-                        const int n2 = kad_find_node_blk<EX, C>(V, ev.r, ev.rg(), K2, ev.numR, ev.sb(), b2, ns);
+                        const int n2 = kad_find_node_blk<EX, C>(V, ev.r, g, K2, ev.numR, ev.sb(), b2, ns,
+                                                                g.m <= g.endIndex ? rb_pre(ev.pre) : -1, rb_r0(ev.pre));
                         uint32_t z = (uint32_t)n2;
                         for (int k = 0; k < C; ++k) z ^= b2.x[k] ^ (uint32_t)b2.d[k] ^ (uint32_t)(b2.d[k] >> 32);
                         asm volatile("" :: "v"(z));
