@@ -127,8 +127,7 @@ __device__ __forceinline__ bool cand_lt(uint64_t da, uint32_t ia, uint64_t db, u
 }
 
 #ifdef OVS_KAD_STATS
-// cost experiment (tools/diag): [0] findNode calls, [1] blocks read, [2] calls in the sibling zone,
-// [3] calls whose main bucket was short, [4] events, [5] sends
+// cost experiment (-DOVS_KAD_STATS builds): lane occupancy of K2's phases (kad_route.hip)
 __device__ unsigned long long g_kad_stats[8];
 #endif
 

@@ -180,16 +180,41 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
         bool coop = false;
         if (active && !dead && !kad_lookup_done(L)) {
             const HopRecorder<RECORD> rec{io.hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
-            if (SHARD) {
-                const RemoteReady rd{io.res, q * A, V.lo, V.hi};
-                ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, rd, rec, ev);
-            } else {
-                ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, AlwaysReady{}, rec, ev);
+            // An event that only accounts (a response of an older step, a timeout with calls still
+            // pending) leaves the lane idle through the findNode, merge and send phases: the lane
+            // takes its next event in the same iteration instead (at most A pending events).  With
+            // α = 3 these are ~40 % of the events (most parallel responses arrive a step late).
+#ifndef OVS_KAD_ONE_EVENT
+            for (int r = 0; r < A; ++r) {
+#endif
+                if (SHARD) {
+                    const RemoteReady rd{io.res, q * A, V.lo, V.hi};
+                    ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, rd, rec, ev);
+                } else {
+                    ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, AlwaysReady{}, rec, ev);
+                }
+#ifndef OVS_KAD_ONE_EVENT
+                if (ph != KEV_HANDLED || kad_lookup_done(L)) break;
             }
+#endif
             const bool local = !SHARD || (ev.r >= V.lo && ev.r < V.hi);
             coop = ph == KEV_FIND && local && kad_find_is_coop(V, ev.r, ev.rg(), ev.sb(), ns, rb_pre(ev.pre), rb_r0(ev.pre));
         }
 
+#ifdef OVS_KAD_STATS
+        {   // lane occupancy of the phases (cost experiment): [0] wave iterations, [1] active lanes,
+            // [2] per-lane findNodes, [3] cooperative findNodes, [4] send-only events
+            const uint64_t act = __ballot(active), lf = __ballot(active && ph == KEV_FIND && !coop);
+            const uint64_t cp = __ballot(coop), se = __ballot(active && ph == KEV_SENDS);
+            if ((threadIdx.x & 63) == 0) {
+                atomicAdd(&g_kad_stats[0], 1ull);
+                atomicAdd(&g_kad_stats[1], (unsigned long long)__popcll(act));
+                atomicAdd(&g_kad_stats[2], (unsigned long long)__popcll(lf));
+                atomicAdd(&g_kad_stats[3], (unsigned long long)__popcll(cp));
+                atomicAdd(&g_kad_stats[4], (unsigned long long)__popcll(se));
+            }
+        }
+#endif
         // phase 2 (whole wave): the sibling-zone findNodes (results in LDS).  The exact-compare
         // instantiation (networks with IDs sharing their top 63 bits) keeps the per-lane scan: its
         // tie fallbacks in the cooperative merge made the register allocator emit misaligned
@@ -259,6 +284,17 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
             } else if (ph == KEV_SENDS) {
                 num = ev.num;
             }
+#ifdef OVS_KAD_STATS
+            {   // [5] lanes sending, [6] the wave's send-loop trips (max num), [7] sends wanted
+                const uint64_t t1 = __ballot(num >= 1), t2 = __ballot(num >= 2), t3 = __ballot(num >= 3);
+                const uint64_t all = __ballot(true);
+                if ((int)(threadIdx.x & 63) == __ffsll((long long)all) - 1) {
+                    atomicAdd(&g_kad_stats[5], (unsigned long long)__popcll(t1));
+                    atomicAdd(&g_kad_stats[6], (unsigned long long)((t1 != 0) + (t2 != 0) + (t3 != 0)));
+                    atomicAdd(&g_kad_stats[7], (unsigned long long)(__popcll(t1) + __popcll(t2) + __popcll(t3)));
+                }
+            }
+#endif
             if (num >= 0) {
                 if (SHARD) {
                     const ShardSend on{io.res, q * A, &L.K, io.shard_lo, io.nsh, V.lo, V.hi, io.rstage, io.rtag,
@@ -348,8 +384,8 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
 #ifdef OVS_KAD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
-    fprintf(stderr, "kadstats nq=%llu find=%llu blocks=%llu sibzone=%llu shortmain=%llu\n", (unsigned long long)io.nq,
-            z[0], z[1], z[2], z[3]);
+    fprintf(stderr, "kadstats nq=%llu iters=%llu active=%llu lanefind=%llu coop=%llu sendonly=%llu sending=%llu sendtrips=%llu sends=%llu\n",
+            (unsigned long long)io.nq, z[0], z[1], z[2], z[3], z[4], z[5], z[6], z[7]);
 #endif
     return hipGetLastError();
 }
