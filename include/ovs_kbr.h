@@ -551,7 +551,8 @@ ovs_status  ovs_kad_shard_begin_lookup(ovs_ctx* ctx, int32_t num_siblings, const
                                        const uint32_t* src, uint64_t n, uint32_t qid_base,
                                        uint32_t* siblings, void* stream);
 /* One round for this rank's lookups (ABI 7).  Requests for rank d go to segment d of
- * `out` (out + d * out_cap requests; out_cap >= n * lookupParallelRpcs) and are
+ * `out` (out + d * out_cap requests; out_cap >= n * lookupParallelRpcs, n * 8 when
+ * lookupParallelRpcs is 5..8: a lookup owns 1, 2, 3, 4 or 8 pending-call slots) and are
  * counted in out_count[d]; finished lookups are appended to `done` (done_count).
  * out_count[0..nshards) and done_count are device counters the step adds to (the
  * caller zeroes out_count before each round, done_count once per batch);

@@ -37,10 +37,11 @@ CFLAGS = [
 SOURCES = ["chord.hip", "compact.hip", "epichord.hip", "kad.hip", "kad_refresh.hip", "kad_route.hip", "kad_shard.hip", "koorde.hip", "stats.hip", "ovs_kbr.cpp",
            "ovs_ini.cpp", "host_tables.cpp"]
 # translation units compiled more than once: (source, object stem, extra flags).  K2 is built per
-# (alpha, exact) pair so its instantiations compile in parallel.
+# (alpha, exact) pair so its instantiations compile in parallel; A = 8 serves alpha 5..8 (A is the
+# pending-call capacity, the lookup's alpha is a runtime parameter).
 VARIANTS = {
     "kad_route.hip": [(f"kad_route_a{a}{'x' if x else ''}", [f"-DOVS_KAD_A={a}", f"-DOVS_KAD_EX={x}"])
-                      for a in (1, 2, 3, 4) for x in (0, 1)],
+                      for a in (1, 2, 3, 4, 8) for x in (0, 1)],
 }
 
 

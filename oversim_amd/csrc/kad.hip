@@ -561,7 +561,8 @@ hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ov
     case 1: return KL(1);
     case 2: return KL(2);
     case 3: return KL(3);
-    default: return KL(4);
+    case 4: return KL(4);
+    default: return KL(8);     // 5..8: A is the pending-call capacity (kad_params_supported)
     }
 #undef KL
 #undef KLX

@@ -21,6 +21,12 @@
 
 namespace ovs {
 
+// lookupParallelRpcs <= 8 (maidsafe.ini:18-19 sets 8).  Pending-call slots of a lookup with
+// lookupParallelRpcs = alpha: the K2 instantiation's capacity A (alpha 5..8 run on the A = 8
+// objects); the slots a sharded lookup owns follow A, not alpha.
+constexpr int KAD_MAX_ALPHA = 8;
+inline int kad_pend_slots(int alpha) { return alpha <= 4 ? alpha : KAD_MAX_ALPHA; }
+
 // meta bits of KadNode
 constexpr uint32_t KMETA_MASK_OUT = 1u << 24;   // level-mask bits below the 64-bit window: exact check
 struct alignas(64) KadNode {

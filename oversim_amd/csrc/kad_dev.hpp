@@ -616,7 +616,8 @@ __device__ __forceinline__ int kad_response_size(const KadView& V, uint32_t c, c
 // ---------------------------------------------------------------------------
 // IterativePathLookup, one event per call (K2 in kad_route.hip, the sharded path in kad_shard.hip)
 
-constexpr int MAXA = 4;    // lookupParallelRpcs <= 4
+constexpr int MAXA = 8;    // lookupParallelRpcs <= 8 (maidsafe.ini:18-19 sets 8); K2 objects for A = 1..4 and 8
+static_assert(MAXA == KAD_MAX_ALPHA, "kad.hpp's kad_pend_slots assumes the A = 8 objects");
 
 
 struct KadLC {

@@ -30,7 +30,8 @@ namespace ovs {
 
 namespace {
 
-constexpr int XMAXA = 4;        // lookupParallelRpcs <= 4 (strictParallelRpcs: <= alpha calls in flight)
+// pending-call slots (strictParallelRpcs: <= alpha calls in flight): 4, or 8 for lookupParallelRpcs
+// 5..8 (maidsafe.ini:18-19) -- a template parameter XA of the lookup state and the kernel
 constexpr int XMAXDEAD = 64;    // nodes whose RPC timed out, per lookup
 
 struct XCfg {
@@ -56,6 +57,7 @@ struct XPend {
     bool to;
 };
 
+template <int XA>
 struct XLookup {
     K160 K;
     uint32_t S;
@@ -66,7 +68,7 @@ struct XLookup {
     int step, hops, pending;
     bool pfinished, psuccess, counted, any_to, success, err;
     int finishedPaths, successfulPaths, minHops;
-    XPend p[XMAXA];
+    XPend p[XA];
     uint32_t pvalid;
 };
 
@@ -78,8 +80,9 @@ struct XRegNh {
     uint32_t used;      // bit i: entry i alreadyUsed
 };
 
-template <bool EX, bool REG>
+template <bool EX, bool REG, int XA>
 struct XCtx {
+    using XL = XLookup<XA>;
     const KadView& V;
     const DelayConsts& DC;
     const XCfg& C;
@@ -178,7 +181,7 @@ struct XCtx {
     }
 
     // --- the LookupVector: registers (REG, 2R <= 16) or the lane's scratch ---------------------------
-    __device__ __forceinline__ int nh_add(XLookup& L, XRegNh& H, uint32_t x, uint64_t dx) const
+    __device__ __forceinline__ int nh_add(XL& L, XRegNh& H, uint32_t x, uint64_t dx) const
     {
         const int cap = 2 * C.R;
         if constexpr (!REG) return vadd(X.nh_idx, X.nh_d, X.nh_used, cap, &L.nnh, x, dx, L.K);
@@ -211,7 +214,7 @@ struct XCtx {
     // flags travelling with their nodes.  The adds run in the block's (distance) order, so a block
     // node's insertion position is its position in the merged vector; returns how many entered at a
     // position < R (numNewRpcs).
-    __device__ __forceinline__ int nh_merge_blk(XLookup& L, XRegNh& H, const Blk8& r, int cnt) const
+    __device__ __forceinline__ int nh_merge_blk(XL& L, XRegNh& H, const Blk8& r, int cnt) const
     {
         const int cap = 2 * C.R;
         BlkN<16> a;
@@ -261,7 +264,7 @@ struct XCtx {
     }
 
     // getNextEntry (IterativeLookup.cc:1172-1182): the first entry neither alreadyUsed nor dead; -1
-    __device__ __forceinline__ int nh_next(const XLookup& L, const XRegNh& H) const
+    __device__ __forceinline__ int nh_next(const XL& L, const XRegNh& H) const
     {
         if constexpr (!REG) {
             for (int q = 0; q < L.nnh; ++q)
@@ -283,7 +286,7 @@ struct XCtx {
         else H.used |= 1u << e;
     }
 
-    __device__ __forceinline__ void nh_remove(XLookup& L, XRegNh& H, uint32_t x) const
+    __device__ __forceinline__ void nh_remove(XL& L, XRegNh& H, uint32_t x) const
     {
         int q = -1;
         for (int i = 0; i < L.nnh && q < 0; ++i)
@@ -304,7 +307,7 @@ struct XCtx {
         --L.nnh;
     }
 
-    __device__ __forceinline__ bool is_dead(const XLookup& L, uint32_t x) const
+    __device__ __forceinline__ bool is_dead(const XL& L, uint32_t x) const
     {
         for (int i = 0; i < L.nd; ++i)
             if (X.dead[at(i)] == x) return true;
@@ -314,7 +317,7 @@ struct XCtx {
     // visited = the source and every responder.  Without a timeout no responder can be an unused
     // next hop (an evicted entry is farther than the vector's last and never re-enters while the
     // vector only shrinks by eviction), so the list is scanned only after one.
-    __device__ __forceinline__ bool visited(const XLookup& L, uint32_t x) const
+    __device__ __forceinline__ bool visited(const XL& L, uint32_t x) const
     {
         if (x == L.S) return true;
         if (!L.any_to) return false;
@@ -324,13 +327,13 @@ struct XCtx {
     }
 
     // IterativeLookup::sendRpc (656-689) + BaseRpc timeout + SimpleNodeEntry::calcDelay
-    __device__ __forceinline__ void lookup_send(XLookup& L, uint32_t x) const
+    __device__ __forceinline__ void lookup_send(XL& L, uint32_t x) const
     {
         // pending slots are indexed by compile-time constants only (a dynamic index would put the
         // array in private memory)
         bool dup = false;
 #pragma unroll
-        for (int i = 0; i < XMAXA; ++i) {
+        for (int i = 0; i < XA; ++i) {
             const bool me = ((L.pvalid >> i) & 1u) && L.p[i].node == x;   // "RPC already sent"
             L.p[i].ninfo += me ? 1u : 0u;
             dup |= me;
@@ -338,7 +341,7 @@ struct XCtx {
         if (dup) return;
         int slot = -1;
 #pragma unroll
-        for (int i = XMAXA - 1; i >= 0; --i)
+        for (int i = XA - 1; i >= 0; --i)
             if (i < C.alpha && !((L.pvalid >> i) & 1u)) slot = i;
         if (slot < 0) { L.err = true; return; }
         int64_t d1 = 0, d2 = 0;
@@ -361,7 +364,7 @@ struct XCtx {
         // unconditional selects per slot: a guarded store would be folded into one store through a
         // dynamic index, which moves the pending array to private memory
 #pragma unroll
-        for (int i = 0; i < XMAXA; ++i) {
+        for (int i = 0; i < XA; ++i) {
             const bool me = i == slot;
             XPend& P = L.p[i];
             P.node = me ? x : P.node;
@@ -377,7 +380,7 @@ struct XCtx {
     }
 
     // IterativePathLookup::sendRpc (1067-1170), exhaustive
-    __device__ __forceinline__ void send_rpcs(XLookup& L, XRegNh& H, int num) const
+    __device__ __forceinline__ void send_rpcs(XL& L, XRegNh& H, int num) const
     {
         if (L.pfinished) return;
         if (C.hcm && L.hops >= C.hcm) { L.pfinished = true; L.psuccess = false; return; }
@@ -411,7 +414,7 @@ struct XCtx {
         }
     }
 
-    __device__ __forceinline__ void count_finished(XLookup& L) const
+    __device__ __forceinline__ void count_finished(XL& L) const
     {
         if (L.pfinished && !L.counted) {
             L.counted = true;
@@ -422,7 +425,7 @@ struct XCtx {
     }
 
     // checkStop (295-349), parallelPaths = 1, numSiblings > 0
-    __device__ __forceinline__ bool check_stop(XLookup& L) const
+    __device__ __forceinline__ bool check_stop(XL& L) const
     {
         if (L.finishedPaths == 1 || L.pvalid == 0) {
             L.success = L.successfulPaths >= 1 || L.psuccess;
@@ -446,7 +449,7 @@ struct XCtx {
         uint32_t infos;
     };
 
-    __device__ __forceinline__ void init(const XLookup& L, Run& R) const
+    __device__ __forceinline__ void init(const XL& L, Run& R) const
     {
         R.H.used = 0;
 #pragma unroll
@@ -459,7 +462,7 @@ struct XCtx {
 
     // the next event of the lookup (after checkStop): the earliest pending one by (time, insertion
     // time, sequence); true when the lookup has ended
-    __device__ __forceinline__ bool pick(XLookup& L, Run& R) const
+    __device__ __forceinline__ bool pick(XL& L, Run& R) const
     {
         XPend& cur = R.cur;
         if (check_stop(L)) return true;
@@ -467,7 +470,7 @@ struct XCtx {
         int64_t bt = 0, bi = 0;
         uint32_t bs = 0;
 #pragma unroll
-        for (int i = 0; i < XMAXA; ++i) {
+        for (int i = 0; i < XA; ++i) {
             if (!((L.pvalid >> i) & 1u)) continue;
             const XPend& P = L.p[i];
             if (e < 0 || P.t < bt || (P.t == bt && (P.tins < bi || (P.tins == bi && P.seq < bs)))) {
@@ -476,7 +479,7 @@ struct XCtx {
         }
         if (e < 0) return true;
 #pragma unroll
-        for (int i = 0; i < XMAXA; ++i) {
+        for (int i = 0; i < XA; ++i) {
             const bool me = i == e;
             cur.node = me ? L.p[i].node : cur.node;
             cur.ninfo = me ? L.p[i].ninfo : cur.ninfo;
@@ -498,7 +501,7 @@ struct XCtx {
     // One iteration of the lookup's loop: one RpcInfo of the event in hand, then -- when that was
     // its last -- checkStop and the pick of the next event, in the same iteration (a wave's lanes
     // do not split its iterations between picking and handling); true when the lookup has ended.
-    __device__ __forceinline__ bool step(XLookup& L, Run& R) const
+    __device__ __forceinline__ bool step(XL& L, Run& R) const
     {
         if (L.err) return true;
         if (handle(L, R)) return true;
@@ -506,7 +509,7 @@ struct XCtx {
     }
 
     // one RpcInfo of the event in hand; true when the lookup has ended
-    __device__ __forceinline__ bool handle(XLookup& L, Run& R) const
+    __device__ __forceinline__ bool handle(XL& L, Run& R) const
     {
         XRegNh& H = R.H;
         XPend& cur = R.cur;
@@ -584,8 +587,8 @@ struct XCtx {
 };
 
 
-template <bool EX, bool REG>
-__device__ __forceinline__ void kx_init_lookup(XLookup& L, const KadView& V, const XCfg& C, const K160* __restrict__ qkeys,
+template <bool EX, bool REG, int XA>
+__device__ __forceinline__ void kx_init_lookup(XLookup<XA>& L, const KadView& V, const XCfg& C, const K160* __restrict__ qkeys,
                                                const uint32_t* __restrict__ qsrc, uint32_t* __restrict__ sib_out, uint64_t q)
 {
     L.K = qkeys[q];
@@ -599,7 +602,7 @@ __device__ __forceinline__ void kx_init_lookup(XLookup& L, const KadView& V, con
     L.finishedPaths = 0; L.successfulPaths = 0; L.minHops = 0x7FFFFFFF;
     L.pvalid = 0;
 #pragma unroll
-    for (int i = 0; i < XMAXA; ++i) {
+    for (int i = 0; i < XA; ++i) {
         L.p[i].node = NONE; L.p[i].ninfo = 0; L.p[i].seq = 0;
         L.p[i].t = 0; L.p[i].tins = 0; L.p[i].tsend = 0; L.p[i].to = false;
     }
@@ -610,7 +613,8 @@ __device__ __forceinline__ void kx_init_lookup(XLookup& L, const KadView& V, con
 // SendToKeyListener / LookupResponse fields of a finished lookup (as ovs_lookup_batch; the
 // ovs_lookup_out is written through its ovs_route_out twin, k_lookup_finish's convention), or the
 // one-way route message
-__device__ __forceinline__ void kx_emit(const XLookup& L, const KadView& V, const DelayConsts& DC, const XCfg& C,
+template <int XA>
+__device__ __forceinline__ void kx_emit(const XLookup<XA>& L, const KadView& V, const DelayConsts& DC, const XCfg& C,
                                         uint64_t q, ovs_route_out* __restrict__ out, uint32_t* __restrict__ sib,
                                         uint32_t* __restrict__ resp, int64_t* __restrict__ rtt,
                                         uint32_t* __restrict__ rpcs_out, uint32_t* __restrict__ err)
@@ -678,7 +682,7 @@ __device__ __forceinline__ void kx_emit(const XLookup& L, const KadView& V, cons
 // One lane per lookup, one loop iteration per kernel-loop iteration; a lane whose lookup ended
 // takes the next one of its wave's contiguous slice of the batch (ballot + popcount, no atomics),
 // so a wave does not wait for its longest lookup before its lanes move on (as K2).
-template <bool EX, bool REG>
+template <bool EX, bool REG, int XA>
 __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C, XScratch X,
                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                      uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
@@ -694,8 +698,8 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     const uint64_t lt_mask = (wl == 0) ? 0ull : (~0ull >> (64 - wl));
     bool active = false;
     uint64_t q = 0;
-    XLookup L;
-    typename XCtx<EX, REG>::Run R;
+    XLookup<XA> L;
+    typename XCtx<EX, REG, XA>::Run R;
     while (true) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && cursor < end) {
@@ -704,7 +708,7 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
                 q = mine;
                 active = true;
                 kx_init_lookup<EX, REG>(L, V, C, qkeys, qsrc, sib_out, q);
-                const XCtx<EX, REG> c0{V, DC, C, X, lane, nullptr, nullptr, nullptr};
+                const XCtx<EX, REG, XA> c0{V, DC, C, X, lane, nullptr, nullptr, nullptr};
                 c0.init(L, R);
             }
             cursor += (uint64_t)__popcll(need);
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
         uint32_t* sib = sib_out + q * (uint64_t)C.ns;
         uint32_t* resp = resp_out + q * (uint64_t)C.hcm;
         int64_t* rtt = rtt_out ? rtt_out + q * (uint64_t)C.hcm : nullptr;
-        const XCtx<EX, REG> ctx{V, DC, C, X, lane, resp, rtt, sib};
+        const XCtx<EX, REG, XA> ctx{V, DC, C, X, lane, resp, rtt, sib};
         if (ctx.step(L, R)) {
             kx_emit(L, V, DC, C, q, out, sib, resp, rtt, rpcs_out, err);
             active = false;
@@ -798,7 +802,7 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     *capacity_error = false;
     if (nq == 0) return hipSuccess;
     const int A = P.lookupParallelRpcs;
-    if (A < 1 || A > XMAXA || R < 1 || R > 64 || ns < 1 || ns > R || !P.lookupMerge || !P.lookupStrictParallelRpcs ||
+    if (A < 1 || A > KAD_MAX_ALPHA || R < 1 || R > 64 || ns < 1 || ns > R || !P.lookupMerge || !P.lookupStrictParallelRpcs ||
         P.hopCountMax < 1 || t.k > KMAX)
         return hipErrorNotSupported;
     const KadView V = kad_make_view(t, xy, n);
@@ -819,16 +823,22 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
     // the occupancy of each instantiation, per device, filled under the scratch mutex
-    static int bpc[64][4] = {};
-    const int ki = (t.exact ? 2 : 0) + (reg ? 1 : 0);
+    static int bpc[64][8] = {};
+    const bool a8 = A > 4;     // the 8-slot instantiations serve lookupParallelRpcs 5..8
+    const int ki = (t.exact ? 2 : 0) + (reg ? 1 : 0) + (a8 ? 4 : 0);
     std::unique_lock<std::mutex> lock(g_scratch_mu);
     if (bpc[dev][ki] == 0) {
         int b = 0;
         hipError_t oe;
-        if (t.exact) oe = reg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<true, true>, 256, 0)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<true, false>, 256, 0);
-        else oe = reg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<false, true>, 256, 0)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<false, false>, 256, 0);
+#define KOCC(ex, rg, xa) hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<ex, rg, xa>, 256, 0)
+        if (a8) {
+            if (t.exact) oe = reg ? KOCC(true, true, 8) : KOCC(true, false, 8);
+            else oe = reg ? KOCC(false, true, 8) : KOCC(false, false, 8);
+        } else {
+            if (t.exact) oe = reg ? KOCC(true, true, 4) : KOCC(true, false, 4);
+            else oe = reg ? KOCC(false, true, 4) : KOCC(false, false, 4);
+        }
+#undef KOCC
         bpc[dev][ki] = (oe == hipSuccess && b > 0) ? b : 1;
     }
     uint64_t lanes = (uint64_t)num_cu * (uint64_t)bpc[dev][ki] * 256;
@@ -858,10 +868,15 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     const uint64_t waves = lanes / 64;
     const uint64_t chunk = (nq + waves - 1) / waves;
     ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);   // or ovs_lookup_out (same size)
-#define KRL(ex, rg) hipLaunchKernelGGL((k_kad_refresh<ex, rg>), dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, qsrc, \
-                                       nq, chunk, o, sibs, responders, rtts, rpcs, err)
-    if (t.exact) { if (reg) KRL(true, true); else KRL(true, false); }
-    else { if (reg) KRL(false, true); else KRL(false, false); }
+#define KRL(ex, rg, xa) hipLaunchKernelGGL((k_kad_refresh<ex, rg, xa>), dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, \
+                                           qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err)
+    if (a8) {
+        if (t.exact) { if (reg) KRL(true, true, 8); else KRL(true, false, 8); }
+        else { if (reg) KRL(false, true, 8); else KRL(false, false, 8); }
+    } else {
+        if (t.exact) { if (reg) KRL(true, true, 4); else KRL(true, false, 4); }
+        else { if (reg) KRL(false, true, 4); else KRL(false, false, 4); }
+    }
 #undef KRL
     e = hipGetLastError();
     uint32_t herr = 0;

@@ -126,7 +126,8 @@ hipError_t kad_shard_step_dispatch(int A, const KadView& V, const DelayConsts& D
     case 1: return kad_shard_step_launch<1, EX>(V, DC, LC, a, num_cu, s);
     case 2: return kad_shard_step_launch<2, EX>(V, DC, LC, a, num_cu, s);
     case 3: return kad_shard_step_launch<3, EX>(V, DC, LC, a, num_cu, s);
-    default: return kad_shard_step_launch<4, EX>(V, DC, LC, a, num_cu, s);
+    case 4: return kad_shard_step_launch<4, EX>(V, DC, LC, a, num_cu, s);
+    default: return kad_shard_step_launch<8, EX>(V, DC, LC, a, num_cu, s);
     }
 }
 
@@ -147,7 +148,8 @@ size_t kad_lookup_state_bytes(int alpha)
     case 1: return sizeof(KadLookup<1>);
     case 2: return sizeof(KadLookup<2>);
     case 3: return sizeof(KadLookup<3>);
-    default: return sizeof(KadLookup<4>);
+    case 4: return sizeof(KadLookup<4>);
+    default: return sizeof(KadLookup<8>);
     }
 }
 
@@ -162,7 +164,8 @@ hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint
     case 1: KI(1); break;
     case 2: KI(2); break;
     case 3: KI(3); break;
-    default: KI(4); break;
+    case 4: KI(4); break;
+    default: KI(8); break;
     }
 #undef KI
     return hipGetLastError();
@@ -191,7 +194,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     DelayConsts DL = DC;
     DL.lookupCall = lk ? 1 : 0;     // a LookupCall ends at its last response (no route message)
     kad_lc_sizes(LC, DL, n);
-    const int A = LC.alpha;
+    const int A = kad_pend_slots(LC.alpha);
     // stage: a request per pending-call slot, a done record per lookup, and their tags
     const uint64_t nslot = nlook * (uint64_t)A;
     const size_t orq = 0, odn = orq + sizeof(ovs_kad_req) * nslot, ort = odn + sizeof(ovs_done_rec) * nlook,

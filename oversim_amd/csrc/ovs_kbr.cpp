@@ -756,7 +756,7 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
         HIPCHK(c, hipMalloc(&c->kst, kad_lookup_state_bytes(alpha) * cap));
         HIPCHK(c, hipMalloc(&c->kact, cap));
         HIPCHK(c, hipMalloc(&c->kqids, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->kres, sizeof(KadRes) * cap * alpha));
+        HIPCHK(c, hipMalloc(&c->kres, sizeof(KadRes) * cap * kad_pend_slots(alpha)));
         HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
         HIPCHK(c, hipMalloc(&c->kiota, sizeof(uint64_t) * cap));
         HIPCHK(c, hipMalloc(&c->klist[0], sizeof(uint64_t) * cap));
@@ -805,8 +805,9 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint64_t out_cap, un
     if (!c->kst) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
     if (c->P.lookupParallelRpcs != c->kalpha && c->knlook)
         return fail(c, OVS_ESTATE, "lookupParallelRpcs changed since ovs_kad_shard_begin");
-    if (out_cap < c->knlook * (uint64_t)c->kalpha)
-        return fail(c, OVS_EINVAL, "out_cap must hold a request per pending-call slot (n * lookupParallelRpcs)");
+    if (out_cap < c->knlook * (uint64_t)kad_pend_slots(c->kalpha))
+        return fail(c, OVS_EINVAL, "out_cap must hold a request per pending-call slot "
+                                   "(n * lookupParallelRpcs; n * 8 for lookupParallelRpcs 5..8)");
     uint64_t lo_h[MAXSHARDS + 1];
     for (uint32_t r = 0; r <= nshards; ++r) {
         lo_h[r] = shard_lo[r];
@@ -847,7 +848,7 @@ ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const ovs_kad_resp* in, uint64_t n,
     if (!c || (n && !in)) return OVS_EINVAL;
     if (!c->kres) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
     HIPCHK(c, hipSetDevice(c->device));
-    hipError_t e = kad_shard_deliver(in, n, c->kres, c->knlook * (uint64_t)c->kalpha, c->kbad, (hipStream_t)stream);
+    hipError_t e = kad_shard_deliver(in, n, c->kres, c->knlook * (uint64_t)kad_pend_slots(c->kalpha), c->kbad, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard deliver");
     return OVS_OK;
 }
@@ -1291,8 +1292,8 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
     if (R < 1 || R > 64) return fail(c, OVS_ENOTSUP, "refresh lookups implement redundantNodes 1..64");
     const ovs_params& P = c->P;
     if (P.hopCountMax < 1) return fail(c, OVS_ENOTSUP, "refresh lookups need hopCountMax >= 1");
-    if (!P.lookupMerge || !P.lookupStrictParallelRpcs || P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > 4)
-        return fail(c, OVS_ENOTSUP, "refresh lookups implement lookupMerge, strictParallelRpcs, parallelRpcs 1..4");
+    if (!P.lookupMerge || !P.lookupStrictParallelRpcs || P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > KAD_MAX_ALPHA)
+        return fail(c, OVS_ENOTSUP, "refresh lookups implement lookupMerge, strictParallelRpcs, parallelRpcs 1..8");
     if (P.lookupParallelPaths != 1 || P.lookupVerifySiblings || P.lookupMajoritySiblings || P.jitter != 0.0)
         return fail(c, OVS_ENOTSUP, "parallelPaths 1, no verify/majority siblings, jitter 0");
     HIPCHK(c, hipSetDevice(c->device));

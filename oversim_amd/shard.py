@@ -486,6 +486,7 @@ class KadShardStepper:
         n = keys_t.shape[0]
         self.n = n
         a = self.params.lookupParallelRpcs
+        a = a if a <= 4 else 8      # pending-call slots: the K2 instantiation's capacity (kad_pend_slots)
         # one round sends at most alpha requests per lookup (a request occupies a pending slot
         # until its result is delivered at the end of the round): a segment per owner rank
         self.seg_cap = max(n * a, 1)

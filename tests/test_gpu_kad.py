@@ -75,7 +75,7 @@ def test_find_node_matches_oracle(engine: KbrEngine):
             assert bool(sib[i]) == flag, (nr, i)
 
 
-@pytest.mark.parametrize("alpha", [1, 2, 3])
+@pytest.mark.parametrize("alpha", [1, 2, 3, 4, 5, 8])
 def test_route_config_b(engine: KbrEngine, alpha):
     """Config B: 15000 nodes (nodes_2d_15000 coordinates), node-ID keys."""
     net = W.population(15000, 0x4b41)

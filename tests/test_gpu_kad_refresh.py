@@ -68,6 +68,9 @@ VARIANTS = {
     "a3_hcm12": dict(lookupParallelRpcs=3, hopCountMax=12),
     "a3_newresp": dict(lookupParallelRpcs=3, lookupNewRpcOnEveryResponse=1),
     "a3_trunc": dict(lookupParallelRpcs=3, simtimeRound=0),
+    # the 8-slot instantiations (lookupParallelRpcs 5..8; maidsafe.ini:18-19 sets 8)
+    "a8": dict(lookupParallelRpcs=8),
+    "a6_rpcto": dict(lookupParallelRpcs=6, rpcUdpTimeout=0.35),
 }
 
 

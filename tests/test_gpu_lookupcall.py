@@ -63,7 +63,7 @@ def test_chord_lookup_call_explicit_tables(engine: KbrEngine):
     assert len(np.unique(g["num_siblings"][g["is_valid"] == 1])) > 1
 
 
-@pytest.mark.parametrize("alpha", [1, 3])
+@pytest.mark.parametrize("alpha", [1, 3, 8])
 @pytest.mark.parametrize("ns", [-1, 3, 1])
 def test_kad_lookup_call_matches_oracle(engine: KbrEngine, alpha, ns):
     net = W.population(15000, 0x4b41)

@@ -35,6 +35,11 @@ VARIANTS = {
     "a3_hcm3": dict(lookupParallelRpcs=3, hopCountMax=3),
     "a3_first": dict(lookupParallelRpcs=3, lookupFinishOnFirstUnchanged=1),
     "a3_trunc": dict(lookupParallelRpcs=3, simtimeRound=0),
+    # the fork's own Kademlia configuration: lookupParallelRpcs = lookupRedundantNodes = 8
+    # (maidsafe.ini:18-19), and one alpha between 4 and 8
+    "a8_maidsafe": dict(lookupParallelRpcs=8, lookupRedundantNodes=8),
+    "a5": dict(lookupParallelRpcs=5),
+    "a8_rpcto": dict(lookupParallelRpcs=8, rpcUdpTimeout=0.35),
 }
 
 
@@ -101,6 +106,7 @@ REFRESH_VARIANTS = {
     "a3_rpcto_newto": dict(lookupParallelRpcs=3, rpcUdpTimeout=0.35, lookupNewRpcOnEveryTimeout=1),
     "a2_lookupto": dict(lookupParallelRpcs=2, lookupTimeout=0.9),
     "a3_hcm12": dict(lookupParallelRpcs=3, hopCountMax=12),
+    "a8": dict(lookupParallelRpcs=8),
 }
 
 

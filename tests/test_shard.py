@@ -411,7 +411,8 @@ def _kad_reference(net, keys, src, params):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,alpha,n", [(2, 1, 15000), (3, 3, 15000), (8, 3, 1 << 16), (4, 2, 1 << 16)])
+@pytest.mark.parametrize("world,alpha,n", [(2, 1, 15000), (3, 3, 15000), (8, 3, 1 << 16), (4, 2, 1 << 16), (3, 8, 15000),
+                                           (2, 5, 15000)])
 def test_kad_shards_emulated_on_one_gpu(world, alpha, n):
     """W arcs in one process: every lookup's result equals the single-GPU kernel's."""
     from oversim_amd import Params
