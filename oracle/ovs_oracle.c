@@ -288,8 +288,13 @@ struct orc_net {
     /* Kademlia */
     uint32_t* sib;          /* n * 5s, sorted by XOR to self */
     uint8_t* nsib;
-    uint32_t* bucket;       /* n * 160 * k */
+    uint32_t* bucket;       /* n * 160 * k (snapshot builds) */
     uint8_t* bcount;        /* n * 160 */
+    /* explicit (mutable) tables: bucket (v, m) is a growable array in LRU order (KademliaBucket,
+     * push_back / erase in routingAdd), bdyn[v * 160 + m] with bdcnt entries of bdcap */
+    uint32_t** bdyn;
+    uint16_t* bdcnt;
+    uint16_t* bdcap;
     /* Koorde: deBruijnNode, deBruijnNodes = kdbNum ring nodes from sorted index kdbStart */
     uint32_t* kdb;
     uint32_t* kdbStart;
@@ -301,7 +306,10 @@ void orc_net_free(orc_net* net)
     if (!net) return;
     free(net->ids); free(net->xy); free(net->pred); free(net->succ); free(net->nsucc);
     free(net->fdeque); free(net->fsize); free(net->sib); free(net->nsib); free(net->bucket);
-    free(net->bcount); free(net->kdb); free(net->kdbStart); free(net->kdbNum); free(net);
+    free(net->bcount); free(net->kdb); free(net->kdbStart); free(net->kdbNum);
+    if (net->bdyn) for (size_t i = 0; i < (size_t)net->n * 160; ++i) free(net->bdyn[i]);
+    free(net->bdyn); free(net->bdcnt); free(net->bdcap);
+    free(net);
 }
 
 static orc_net* net_alloc(int type, const orc_key* ids, uint32_t n, const double* xy, const orc_params* p)
@@ -762,10 +770,43 @@ static void kad_node_build(const orc_net* net, uint32_t self, uint32_t* sibOut, 
     }
 }
 
+/* explicit tables: growable bucket arrays */
+static void kad_dyn_alloc(orc_net* net)
+{
+    net->bdyn = (uint32_t**)calloc((size_t)net->n * 160, sizeof(uint32_t*));
+    net->bdcnt = (uint16_t*)calloc((size_t)net->n * 160, sizeof(uint16_t));
+    net->bdcap = (uint16_t*)calloc((size_t)net->n * 160, sizeof(uint16_t));
+}
+static void kad_dyn_push(orc_net* net, uint32_t v, int m, uint32_t x)       /* KademliaBucket::push_back */
+{
+    const size_t i = (size_t)v * 160 + (size_t)m;
+    if (net->bdcnt[i] == net->bdcap[i]) {
+        if (net->bdcap[i] >= 32768) { cap_error("bucket over 32768 entries"); return; }
+        net->bdcap[i] = (uint16_t)(net->bdcap[i] ? 2 * net->bdcap[i] : 8);
+        net->bdyn[i] = (uint32_t*)realloc(net->bdyn[i], sizeof(uint32_t) * net->bdcap[i]);
+    }
+    net->bdyn[i][net->bdcnt[i]++] = x;
+}
+static void kad_dyn_erase(orc_net* net, uint32_t v, int m, int pos)        /* bucket->erase(i) */
+{
+    const size_t i = (size_t)v * 160 + (size_t)m;
+    memmove(&net->bdyn[i][pos], &net->bdyn[i][pos + 1], sizeof(uint32_t) * (size_t)(net->bdcnt[i] - pos - 1));
+    net->bdcnt[i]--;
+}
+
 /* A node's Kademlia tables: pointers into the stored arrays, or (lazy network) into a
  * per-thread cache entry built on first use.  Consecutive findNode / isSiblingFor calls of a
  * lookup are at the same node, so a small direct-mapped cache suffices. */
-typedef struct { const uint32_t* sib; int nsib; const uint8_t* bc; const uint32_t* bk; } KadTab;
+typedef struct {
+    const uint32_t* sib; int nsib;
+    const uint8_t* bc; const uint32_t* bk; int k;      /* snapshot layout: bucket m = bk[m*k ..], bc[m] */
+    uint32_t* const* bd; const uint16_t* bdc;           /* explicit tables: bucket m = bd[m][0 .. bdc[m]) */
+} KadTab;
+static inline int kt_count(const KadTab* T, int m) { return T->bd ? (int)T->bdc[m] : (int)T->bc[m]; }
+static inline const uint32_t* kt_members(const KadTab* T, int m)
+{
+    return T->bd ? T->bd[m] : T->bk + (size_t)m * (size_t)T->k;
+}
 
 #define KCACHE 16
 typedef struct {
@@ -781,12 +822,19 @@ static __thread KadCacheEnt* tl_kcache = NULL;
 static KadTab kad_tab(const orc_net* net, uint32_t self)
 {
     KadTab t;
+    memset(&t, 0, sizeof t);
+    t.k = net->p.k;
     if (!net->lazy) {
         size_t sibCap = (size_t)5 * net->p.s;
         t.sib = net->sib + (size_t)self * sibCap;
         t.nsib = net->nsib[self];
-        t.bc = net->bcount + (size_t)self * 160;
-        t.bk = net->bucket + (size_t)self * 160 * net->p.k;
+        if (net->bdyn) {
+            t.bd = net->bdyn + (size_t)self * 160;
+            t.bdc = net->bdcnt + (size_t)self * 160;
+        } else {
+            t.bc = net->bcount + (size_t)self * 160;
+            t.bk = net->bucket + (size_t)self * 160 * net->p.k;
+        }
         return t;
     }
     if (!tl_kcache) {
@@ -841,21 +889,24 @@ static int kad_findNode(const orc_net* net, uint32_t self, const OKey* key,
     int mainIndex = kad_routingBucketIndex(net, self, key, 0);
     int startIndex = kad_routingBucketIndex(net, self, key, 1);
     int endIndex = kad_routingBucketIndex(net, self, &net->ids[sib[nsib - 1]], 0);
-    const uint8_t* bc = T.bc;
-    const uint32_t* bk = T.bk;
+    (void)k;
     if (mainIndex != -1) {
-        for (int i = 0; i < bc[mainIndex]; ++i) nv_add(net, result, bk[(size_t)mainIndex * k + i]);
+        const uint32_t* bk = kt_members(&T, mainIndex);
+        for (int i = 0; i < kt_count(&T, mainIndex); ++i) nv_add(net, result, bk[i]);
     }
     if (startIndex >= endIndex || !nv_isFull(result)) {
         for (int index = startIndex; index >= endIndex; --index) {
             if (index == mainIndex) continue;
-            for (int i = 0; i < bc[index]; ++i) nv_add(net, result, bk[(size_t)index * k + i]);
+            const uint32_t* bk = kt_members(&T, index);
+            for (int i = 0; i < kt_count(&T, index); ++i) nv_add(net, result, bk[i]);
         }
         for (int i = 0; i < nsib; ++i) nv_add(net, result, sib[i]);
         nv_add(net, result, self);
     }
-    for (int index = mainIndex + 1; !nv_isFull(result) && index < 160; ++index)
-        for (int i = 0; i < bc[index]; ++i) nv_add(net, result, bk[(size_t)index * k + i]);
+    for (int index = mainIndex + 1; !nv_isFull(result) && index < 160; ++index) {
+        const uint32_t* bk = kt_members(&T, index);
+        for (int i = 0; i < kt_count(&T, index); ++i) nv_add(net, result, bk[i]);
+    }
     return 0;
 }
 
@@ -906,8 +957,7 @@ orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, 
     int k = p->k, sibCap = 5 * p->s;
     net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
     net->nsib = (uint8_t*)calloc(n, 1);
-    net->bucket = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160 * k);
-    net->bcount = (uint8_t*)calloc((size_t)n * 160, 1);
+    kad_dyn_alloc(net);
     for (uint32_t v = 0; v < n; ++v) {
         NVec sib; nv_init(&sib, sibCap, 1, &net->ids[v]);
         for (int i = 0; i < sibCap; ++i) {
@@ -921,9 +971,11 @@ orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, 
         for (int m = 0; m < 160; ++m) {
             int c = bucket_count[(size_t)v * 160 + m];
             if (c > k) { set_err("bucket holds more than k entries"); orc_net_free(net); return NULL; }
-            net->bcount[(size_t)v * 160 + m] = (uint8_t)c;
-            for (int q = 0; q < k; ++q)
-                net->bucket[((size_t)v * 160 + m) * k + q] = q < c ? bucket_nodes[((size_t)v * 160 + m) * k + q] : NONE;
+            for (int q = 0; q < c; ++q) {
+                uint32_t x = bucket_nodes[((size_t)v * 160 + m) * k + q];
+                if (x >= n) { set_err("bucket member index out of range"); orc_net_free(net); return NULL; }
+                kad_dyn_push(net, v, m, x);
+            }
         }
     }
     return net;
@@ -936,9 +988,12 @@ void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_coun
         KadTab T = kad_tab(net, v);
         for (size_t i = 0; i < sc; ++i) siblings[(size_t)v * sc + i] = (int)i < T.nsib ? T.sib[i] : NONE;
         for (size_t m = 0; m < 160; ++m) {
-            bucket_count[(size_t)v * 160 + m] = T.bc[m];
+            const int c = kt_count(&T, (int)m);
+            const uint32_t* bk = kt_members(&T, (int)m);
+            if (c > (int)k) cap_error("orc_kad_export: a bucket holds more than k entries (use orc_kad_export_csr)");
+            bucket_count[(size_t)v * 160 + m] = (uint8_t)(c < (int)k ? c : (int)k);
             for (size_t j = 0; j < k; ++j)
-                bucket_nodes[((size_t)v * 160 + m) * k + j] = j < T.bc[m] ? T.bk[m * k + j] : NONE;
+                bucket_nodes[((size_t)v * 160 + m) * k + j] = (int)j < c ? bk[j] : NONE;
         }
     }
 }
@@ -1281,6 +1336,10 @@ typedef struct {
      * Kademlia.cc:1606-1611, 1660-1665), nextHops holds 2R (IterativeLookup.cc:770-778) */
     int exh, R, nhCap;
     int64_t* rtts;          /* exhaustive: RTT of every accepted response (hop order) */
+    int64_t* tarrs;         /* ... the time the response reached the source (maintenance rounds) */
+    uint32_t* cnode;        /* every FindNodeCall sent (maintenance rounds): its destination ... */
+    int64_t* ctime;         /* ... and the time it reached it; ccap slots */
+    int ncall, ccap;
 } Lookup;
 
 static int lk_getVisited(Lookup* L, uint32_t n)
@@ -1399,6 +1458,10 @@ static void lk_sendRpc(Lookup* L, uint32_t handle, int rpcId)
         int64_t d2 = calc_delay(L->net, handle, L->S, p->respBaseBytes + p->respPerNodeBytes * res.size, tArr, &respTx);
         r->tResp = tArr + d2;
         r->tIns = tArr;
+        if (L->cnode) {
+            if (L->ncall < L->ccap) { L->cnode[L->ncall] = handle; L->ctime[L->ncall] = tArr; ++L->ncall; }
+            else cap_error("more FindNodeCalls than the call-record capacity");
+        }
         r->seqResp = L->seq++;
         L->rpcsSent++;
     }
@@ -1477,6 +1540,7 @@ static void path_handleResponse(Lookup* L, uint32_t source, const NVec* closest,
         L->hops++;
         if (L->hopseq && L->nhop < L->hopCountMax) L->hopseq[L->nhop] = source;
         if (L->rtts && L->nhop < L->hopCountMax) L->rtts[L->nhop] = rtt;
+        if (L->tarrs && L->nhop < L->hopCountMax) L->tarrs[L->nhop] = L->now;
         L->nhop++;
     }
     lk_setVisited(L, source);
@@ -1535,7 +1599,7 @@ static int lk_checkStop(Lookup* L)
  * sibling vector (numSiblings slots, NONE padded). */
 static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out,
                        uint32_t* hopseq, uint32_t* rpcsOut, int numSiblings, orc_lookup_out* lout, uint32_t* sibs,
-                       int exhR, int64_t* rtts)
+                       int exhR, int64_t* rtts, int64_t* tarrs, uint32_t* cnode, int64_t* ctime, int ccap)
 {
     const orc_params* p = &net->p;
     Lookup* L = (Lookup*)calloc(1, sizeof(Lookup));
@@ -1545,6 +1609,8 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
     L->R = L->exh ? exhR : p->lookupRedundantNodes;
     L->nhCap = L->exh ? 2 * exhR : p->lookupRedundantNodes;
     L->rtts = rtts;
+    L->tarrs = tarrs;
+    L->cnode = cnode; L->ctime = ctime; L->ccap = ccap;
     L->hopseq = hopseq;
     L->minHops = 0x7fffffff;
     L->running = 1; L->startTime = 0; L->now = 0; L->txFinished = 0;
@@ -1773,7 +1839,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
         OKey k = ok_from(&keys[i]);
         if (net->p.routingType == 0 || net->p.routingType == 3)
             run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
-                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL, exh, NULL);
+                       rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL, exh, NULL, NULL, NULL, NULL, 0);
         else {
             run_recursive(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL);
             if (rpcs_out) rpcs_out[i] = 0;     /* no FindNodeCalls in recursive routing */
@@ -1807,7 +1873,7 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
         orc_route_out dummy;
         /* numSiblings = 0 (an exact-key lookup) keeps a one-slot sibling vector (start() 149) */
         run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i],
-                   siblings + (size_t)i * (numSiblings ? numSiblings : 1), exh, NULL);
+                   siblings + (size_t)i * (numSiblings ? numSiblings : 1), exh, NULL, NULL, NULL, NULL, 0);
     }
     (void)nthreads;
     return g_cap_fail ? -1 : numSiblings;
@@ -1817,9 +1883,10 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
 /* Kademlia refresh lookups (Kademlia::handleBucketRefreshTimerExpired,      */
 /* Kademlia.cc:1591-1686, exhaustiveRefresh = true, iterative routing).      */
 /* ======================================================================== */
-int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int R,
-                             orc_lookup_out* out, uint32_t* siblings, uint32_t* responders, int64_t* rtts,
-                             uint32_t* rpcs, int nthreads)
+int orc_kad_exhaustive_batch_t(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int R,
+                               orc_lookup_out* out, uint32_t* siblings, uint32_t* responders, int64_t* rtts,
+                               int64_t* tarrs, uint32_t* cnode, int64_t* ctime, int ccap, uint32_t* rpcs,
+                               int nthreads)
 {
     if (net->type != NET_KAD) { set_err("exhaustive refresh lookups: Kademlia only"); return -1; }
     if (R < 1 || R > 64) { set_err("redundantNodes of a refresh lookup must be 1..64"); return -1; }
@@ -1827,6 +1894,8 @@ int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint
     const int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
     if (responders) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) responders[i] = NONE;
     if (rtts) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) rtts[i] = -1;
+    if (tarrs) for (uint64_t i = 0; i < n * (uint64_t)hcm; ++i) tarrs[i] = -1;
+    if (cnode) for (uint64_t i = 0; i < n * (uint64_t)ccap; ++i) { cnode[i] = NONE; ctime[i] = -1; }
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
@@ -1837,10 +1906,19 @@ int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint
         /* lookup(key, numSiblings = R, ...) with config.redundantNodes = R (1606-1610, 1660-1664) */
         run_lookup(net, &k, src[i], &dummy, responders ? responders + (size_t)i * hcm : NULL,
                    rpcs ? &rpcs[i] : NULL, R, &out[i], siblings + (size_t)i * R, R,
-                   rtts ? rtts + (size_t)i * hcm : NULL);
+                   rtts ? rtts + (size_t)i * hcm : NULL, tarrs ? tarrs + (size_t)i * hcm : NULL,
+                   cnode ? cnode + (size_t)i * ccap : NULL, ctime ? ctime + (size_t)i * ccap : NULL, ccap);
     }
     (void)nthreads;
     return g_cap_fail ? -1 : R;
+}
+
+int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int R,
+                             orc_lookup_out* out, uint32_t* siblings, uint32_t* responders, int64_t* rtts,
+                             uint32_t* rpcs, int nthreads)
+{
+    return orc_kad_exhaustive_batch_t(net, keys, src, n, R, out, siblings, responders, rtts, NULL, NULL, NULL, 0,
+                                      rpcs, nthreads);
 }
 
 uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
@@ -1874,6 +1952,267 @@ uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_
         }
     }
     return cnt;
+}
+
+/* ======================================================================== */
+/* Kademlia maintenance: routingAdd and one synchronous refresh round.       */
+/* ======================================================================== */
+/* Kademlia::routingAdd (Kademlia.cc:432-756) on explicit tables, with the default
+ * secureMaintenance = false, pingNewSiblings = false, activePing = false and
+ * proximityNeighborSelection = false (default.ini:191, 201, 219-221), bucketType "kademlia"
+ * (routingBucketSize = k, 384-411).  The replacement cache (729-745) and its pings never change
+ * a table's membership without RPC timeouts, so a rejected add is only counted.  rtt / lastSeen
+ * are not modelled (nothing in routing reads them).  Returns routingAdd's result. */
+static int kad_routingAdd(orc_net* net, uint32_t self, uint32_t h, int isAlive, orc_kad_round_stats* st)
+{
+    if (h == self) return 0;                                          /* 437-439 */
+    const int sibCap = 5 * net->p.s;
+    uint32_t* sib = net->sib + (size_t)self * sibCap;
+    const int nsib = net->nsib[self];
+    for (int i = 0; i < nsib; ++i)                                    /* already a sibling: 454-481 */
+        if (sib[i] == h) { if (isAlive) st->refreshed++; return 1; }
+    const int bi = kad_routingBucketIndex(net, self, &net->ids[h], 0);
+    {
+        const size_t bx = (size_t)self * 160 + (size_t)bi;
+        for (int i = 0; i < net->bdcnt[bx]; ++i)                      /* already in a bucket: 483-535 */
+            if (net->bdyn[bx][i] == h) {
+                if (isAlive) {                                        /* erase + push_back (514-517) */
+                    kad_dyn_erase(net, self, bi, i);
+                    kad_dyn_push(net, self, bi, h);
+                    st->refreshed++;
+                }
+                return 1;
+            }
+    }
+    int result = 0;
+    uint32_t cur = h;
+    NVec sv; nv_init(&sv, sibCap, 1, &net->ids[self]);               /* siblingTable, XOR to self */
+    for (int i = 0; i < nsib; ++i) sv.v[i] = sib[i];
+    sv.size = nsib;
+    if (nv_isAddable(net, &sv, h)) {                                  /* 537-616 */
+        if (nv_isFull(&sv)) {
+            const uint32_t old = sv.v[sv.size - 1];                   /* preempted handle (579) */
+            nv_add(net, &sv, h);
+            cur = old;
+            result = 1;
+            st->sib_changes++;
+        } else {
+            nv_add(net, &sv, h);
+            for (int i = 0; i < sv.size; ++i) sib[i] = sv.v[i];
+            net->nsib[self] = (uint8_t)sv.size;
+            st->sib_changes++;
+            return 1;
+        }
+        for (int i = 0; i < sv.size; ++i) sib[i] = sv.v[i];
+        net->nsib[self] = (uint8_t)sv.size;
+    }
+    const int b2 = kad_routingBucketIndex(net, self, &net->ids[cur], 0);   /* routingBucket(.., true) 619 */
+    const size_t bx2 = (size_t)self * 160 + (size_t)b2;
+    if (net->bdcnt[bx2] < net->p.k) {                                 /* !bucket->isFull() 665-701 */
+        kad_dyn_push(net, self, b2, cur);
+        st->bucket_changes++;
+        return 1;
+    }
+    if (cur != h) st->lost++;            /* a preempted sibling whose bucket is full leaves the tables */
+    else if (isAlive) st->replacement++; /* replacement cache (729-745) */
+    return result;
+}
+
+/* FindNodeCalls a lookup can send: at most alpha pending, a new one per response or timeout,
+ * responses bounded by hopCountMax (sendRpc stops there); timeouts add one each, bounded by the
+ * MAXRPC calls of the restatement */
+static int kad_call_cap(const orc_net* net)
+{
+    const int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
+    return 2 * hcm + 2 * net->p.lookupParallelRpcs + 16;
+}
+
+int orc_kad_routing_add(orc_net* net, uint32_t v, uint32_t x, int isAlive)
+{
+    orc_kad_round_stats st; memset(&st, 0, sizeof st);
+    if (net->type != NET_KAD || net->lazy || !net->bdyn || v >= net->n || x >= net->n) { set_err("routing_add: explicit Kademlia tables"); return -1; }
+    return kad_routingAdd(net, v, x, isAlive, &st);
+}
+
+/* one routingAdd event of a round at one node */
+typedef struct { int64_t t; int kind; uint32_t task, idx; } KEvt;
+
+static int kevt_cmp(const void* a, const void* b)
+{
+    const KEvt* x = (const KEvt*)a; const KEvt* y = (const KEvt*)b;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    if (x->kind != y->kind) return x->kind < y->kind ? -1 : 1;
+    if (x->task != y->task) return x->task < y->task ? -1 : 1;
+    if (x->idx != y->idx) return x->idx < y->idx ? -1 : 1;
+    return 0;
+}
+
+uint64_t orc_kad_maintenance_round(orc_net* net, const uint32_t* nodes, uint64_t m, const uint8_t* flags,
+                                   const uint32_t* stale, orc_kad_round_stats* st, int nthreads)
+{
+    orc_kad_round_stats z; memset(&z, 0, sizeof z);
+    if (st) *st = z; else st = &z;
+    if (net->type != NET_KAD || net->lazy || !net->bdyn) { set_err("maintenance round: explicit Kademlia tables"); return ORC_FAIL; }
+    if (net->p.routingType != 0) { set_err("maintenance round: iterative routing"); return ORC_FAIL; }
+    const int hcm = net->p.hopCountMax > 0 ? net->p.hopCountMax : 1;
+    /* the round's tasks, per listed node in list order (handleBucketRefreshTimerExpired,
+     * Kademlia.cc:1591-1686, exhaustiveRefresh): flags bit 0 = the sibling-table refresh, a lookup
+     * of the node's own key with siblingRefreshNodes = 5s (1604-1611); bit 1 = the bucket
+     * refreshes of the stale buckets with bucketRefreshNodes = lookupRedundantNodes (1631-1676) */
+    const int Rs = 5 * net->p.s, Rb = net->p.lookupRedundantNodes;
+    uint64_t cap = 0;
+    for (uint64_t j = 0; j < m; ++j) cap += 1 + 160;
+    orc_key* keys = (orc_key*)malloc(sizeof(orc_key) * cap);
+    uint32_t* src = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    int* tR = (int*)malloc(sizeof(int) * cap);
+    uint64_t nt = 0;
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        if (v >= net->n) { set_err("maintenance round: node index out of range"); free(keys); free(src); free(tR); return ORC_FAIL; }
+        const uint8_t f = flags ? flags[j] : 3;
+        if (f & 1) { ok_to(&net->ids[v], &keys[nt]); src[nt] = v; tR[nt] = Rs; ++nt; }
+        if (f & 2) {
+            const uint64_t c = orc_kad_refresh_keys(net, &v, 1, stale ? stale + j * 5 : NULL, keys + nt, src + nt, 160);
+            for (uint64_t q = 0; q < c; ++q) tR[nt + q] = Rb;
+            nt += c;
+        }
+    }
+    st->lookups = nt;
+    /* the lookups, all on the round-start tables (grouped by R, task order kept); every lookup's
+     * FindNodeCalls (destination, arrival) and accepted responses (responder, arrival) */
+    const int ccap = kad_call_cap(net);
+    uint32_t* resp = (uint32_t*)malloc(sizeof(uint32_t) * nt * (size_t)hcm);
+    int64_t* tarr = (int64_t*)malloc(sizeof(int64_t) * nt * (size_t)hcm);
+    uint32_t* cnode = (uint32_t*)malloc(sizeof(uint32_t) * nt * (size_t)ccap);
+    int64_t* ctime = (int64_t*)malloc(sizeof(int64_t) * nt * (size_t)ccap);
+    uint32_t* rpcs = (uint32_t*)malloc(sizeof(uint32_t) * (nt ? nt : 1));
+    orc_lookup_out* out = (orc_lookup_out*)malloc(sizeof(orc_lookup_out) * (nt ? nt : 1));
+    for (int g = 0; g < 2; ++g) {
+        const int R = g == 0 ? Rs : Rb;
+        uint64_t cnt = 0;
+        for (uint64_t t = 0; t < nt; ++t) cnt += tR[t] == R && (g == 0 || Rs != Rb);
+        if (cnt == 0) continue;
+        uint64_t* ix = (uint64_t*)malloc(sizeof(uint64_t) * cnt);
+        orc_key* gk = (orc_key*)malloc(sizeof(orc_key) * cnt);
+        uint32_t* gs = (uint32_t*)malloc(sizeof(uint32_t) * cnt);
+        uint64_t c = 0;
+        for (uint64_t t = 0; t < nt; ++t)
+            if (tR[t] == R && (g == 0 || Rs != Rb)) { ix[c] = t; gk[c] = keys[t]; gs[c] = src[t]; ++c; }
+        uint32_t* gsib = (uint32_t*)malloc(sizeof(uint32_t) * cnt * (size_t)R);
+        uint32_t* gresp = (uint32_t*)malloc(sizeof(uint32_t) * cnt * (size_t)hcm);
+        int64_t* gta = (int64_t*)malloc(sizeof(int64_t) * cnt * (size_t)hcm);
+        uint32_t* gcn = (uint32_t*)malloc(sizeof(uint32_t) * cnt * (size_t)ccap);
+        int64_t* gct = (int64_t*)malloc(sizeof(int64_t) * cnt * (size_t)ccap);
+        uint32_t* grp = (uint32_t*)malloc(sizeof(uint32_t) * cnt);
+        orc_lookup_out* go = (orc_lookup_out*)malloc(sizeof(orc_lookup_out) * cnt);
+        const int rr = orc_kad_exhaustive_batch_t(net, gk, gs, cnt, R, go, gsib, gresp, NULL, gta, gcn, gct, ccap, grp,
+                                                  nthreads);
+        for (uint64_t q = 0; q < cnt; ++q) {
+            const uint64_t t = ix[q];
+            memcpy(resp + t * hcm, gresp + q * hcm, sizeof(uint32_t) * (size_t)hcm);
+            memcpy(tarr + t * hcm, gta + q * hcm, sizeof(int64_t) * (size_t)hcm);
+            memcpy(cnode + t * ccap, gcn + q * ccap, sizeof(uint32_t) * (size_t)ccap);
+            memcpy(ctime + t * ccap, gct + q * ccap, sizeof(int64_t) * (size_t)ccap);
+            rpcs[t] = grp[q]; out[t] = go[q];
+        }
+        free(ix); free(gk); free(gs); free(gsib); free(gresp); free(gta); free(gcn); free(gct); free(grp); free(go);
+        if (rr < 0) { free(keys); free(src); free(tR); free(resp); free(tarr); free(cnode); free(ctime); free(rpcs); free(out); return ORC_FAIL; }
+    }
+    /* the responses' contents: findNode(key, R, -1) at each responder on the round-start tables
+     * (BaseOverlay::findNodeRpc, BaseOverlay.cc:1841-1915); CSR over (task, responder) */
+    uint64_t* roff = (uint64_t*)malloc(sizeof(uint64_t) * (nt * (size_t)hcm + 1));
+    uint64_t tot = 0;
+    for (uint64_t t = 0; t < nt; ++t) {
+        int nr = 0;
+        for (int i = 0; i < hcm && resp[t * hcm + i] != NONE; ++i) ++nr;
+        if (out[t].status != 0) st->failed++;
+        st->responses += (uint64_t)nr;
+        for (int i = 0; i < hcm; ++i) { roff[t * hcm + i] = tot; tot += resp[t * hcm + i] != NONE ? (uint64_t)tR[t] : 0; }
+    }
+    roff[nt * hcm] = tot;
+    uint32_t* rnodes = (uint32_t*)malloc(sizeof(uint32_t) * (tot ? tot : 1));
+    uint8_t* rcnt = (uint8_t*)calloc(nt * (size_t)hcm + 1, 1);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads > 0 ? nthreads : omp_get_max_threads())
+#endif
+    for (int64_t t = 0; t < (int64_t)nt; ++t) {
+        OKey k = ok_from(&keys[t]);
+        for (int i = 0; i < hcm && resp[t * hcm + i] != NONE; ++i) {
+            NVec res;
+            kad_findNode(net, resp[t * hcm + i], &k, tR[t], -1, &res);
+            rcnt[t * hcm + i] = (uint8_t)res.size;
+            for (int q = 0; q < res.size; ++q) rnodes[roff[t * hcm + i] + q] = res.v[q];
+        }
+    }
+    /* the routingAdd events per node: every FindNodeCall reaching its destination x adds its
+     * source there (Kademlia::handleRpcCall, 1328-1349: routingAdd(src, true)) -- also the calls
+     * whose response the lookup never handled (IterativeLookup::stop cancels only the RPC state,
+     * 256-261); every FindNodeResponse the lookup handled adds, at the source, the nodes it carries,
+     * not alive, then the responder, alive (handleRpcResponse, 1352-1420).  Each node applies its
+     * events in simulated-time order -- every refresh lookup of the round starts at its instant 0
+     * -- ties by (kind: calls first, task, index). */
+    uint64_t* ecnt = (uint64_t*)calloc((size_t)net->n + 1, sizeof(uint64_t));
+    for (uint64_t t = 0; t < nt; ++t) {
+        for (int i = 0; i < ccap && cnode[t * ccap + i] != NONE; ++i) ecnt[cnode[t * ccap + i]]++;
+        for (int i = 0; i < hcm && resp[t * hcm + i] != NONE; ++i) ecnt[src[t]]++;
+    }
+    uint64_t* eoff = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)net->n + 1));
+    uint64_t acc = 0;
+    for (uint32_t v = 0; v < net->n; ++v) { eoff[v] = acc; acc += ecnt[v]; ecnt[v] = 0; }
+    eoff[net->n] = acc;
+    KEvt* ev = (KEvt*)malloc(sizeof(KEvt) * (acc ? acc : 1));
+    for (uint64_t t = 0; t < nt; ++t) {
+        for (int i = 0; i < ccap && cnode[t * ccap + i] != NONE; ++i) {
+            const uint32_t x = cnode[t * ccap + i];
+            KEvt a = {ctime[t * ccap + i], 0, (uint32_t)t, (uint32_t)i};
+            ev[eoff[x] + ecnt[x]++] = a;
+        }
+        for (int i = 0; i < hcm && resp[t * hcm + i] != NONE; ++i) {
+            const uint32_t v = src[t];
+            KEvt b = {tarr[t * hcm + i], 1, (uint32_t)t, (uint32_t)i};
+            ev[eoff[v] + ecnt[v]++] = b;
+        }
+    }
+    for (uint32_t v = 0; v < net->n; ++v) {
+        KEvt* e = ev + eoff[v];
+        const uint64_t ne = eoff[v + 1] - eoff[v];
+        qsort(e, ne, sizeof(KEvt), kevt_cmp);
+        for (uint64_t q = 0; q < ne; ++q) {
+            const uint64_t t = e[q].task, i = e[q].idx;
+            if (e[q].kind == 0) {
+                kad_routingAdd(net, v, src[t], 1, st);
+            } else {
+                const uint64_t ri = t * hcm + i;
+                for (int c = 0; c < rcnt[ri]; ++c) kad_routingAdd(net, v, rnodes[roff[ri] + c], 0, st);
+                kad_routingAdd(net, v, resp[ri], 1, st);
+            }
+        }
+    }
+    free(keys); free(src); free(tR); free(resp); free(tarr); free(cnode); free(ctime); free(rpcs); free(out);
+    free(roff); free(rnodes); free(rcnt); free(ecnt); free(eoff); free(ev);
+    if (g_cap_fail) return ORC_FAIL;
+    return st->sib_changes + st->bucket_changes + st->lost;
+}
+
+/* explicit tables in CSR form (buckets of any size): siblings[n*5s]; bucket_off[n*160+1];
+ * bucket_nodes[bucket_off[n*160]] in LRU order.  orc_kad_export_csr with bucket_nodes = NULL
+ * only fills bucket_off (the size query). */
+void orc_kad_export_csr(const orc_net* net, uint32_t* siblings, uint64_t* bucket_off, uint32_t* bucket_nodes)
+{
+    const size_t sc = (size_t)5 * net->p.s;
+    uint64_t o = 0;
+    for (uint32_t v = 0; v < net->n; ++v) {
+        KadTab T = kad_tab(net, v);
+        if (siblings) for (size_t i = 0; i < sc; ++i) siblings[(size_t)v * sc + i] = (int)i < T.nsib ? T.sib[i] : NONE;
+        for (int mm = 0; mm < 160; ++mm) {
+            bucket_off[(size_t)v * 160 + mm] = o;
+            const int c = kt_count(&T, mm);
+            const uint32_t* bk = kt_members(&T, mm);
+            if (bucket_nodes) for (int j = 0; j < c; ++j) bucket_nodes[o + j] = bk[j];
+            o += (uint64_t)c;
+        }
+    }
+    bucket_off[(size_t)net->n * 160] = o;
 }
 
 /* ======================================================================== */

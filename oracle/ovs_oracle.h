@@ -178,6 +178,44 @@ int orc_kad_exhaustive_batch(const orc_net* net, const orc_key* keys, const uint
 uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_t m, const uint32_t* stale,
                               orc_key* keys, uint32_t* src, uint64_t cap);
 
+/* orc_kad_exhaustive_batch plus, per accepted response, the time it reached the source (tarrs,
+ * hopCountMax slots, -1 padded), and every FindNodeCall the lookup sent: its destination (cnode,
+ * ccap slots, NONE padded) and the time it reached it (ctime), ns from the lookup's start. */
+int orc_kad_exhaustive_batch_t(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n, int R,
+                               orc_lookup_out* out, uint32_t* siblings, uint32_t* responders, int64_t* rtts,
+                               int64_t* tarrs, uint32_t* cnode, int64_t* ctime, int ccap, uint32_t* rpcs,
+                               int nthreads);
+
+/* One synchronous Kademlia maintenance round on explicit tables (orc_kad_build_tables): for the
+ * listed nodes, handleBucketRefreshTimerExpired's exhaustive-iterative refresh lookups
+ * (Kademlia.cc:1591-1686; flags[j] bit 0 = the sibling-table refresh of the node's own key with
+ * 5s redundant nodes, bit 1 = the bucket refreshes of the buckets stale[j*5..] marks (NULL = all)
+ * with lookupRedundantNodes; flags NULL = both) all routed on the round-start tables; then every
+ * node applies Kademlia::routingAdd (432-756) for the FindNodeCalls that reached it (handleRpcCall,
+ * 1328-1349; every call sent, answered or not) and the FindNodeResponses its lookups handled
+ * (handleRpcResponse, 1352-1420: the carried nodes not alive, then the responder alive) in
+ * simulated-time order, every lookup of the round starting at instant 0 (ties: calls first, then
+ * task and index order).  Returns the membership changes
+ * (sibling insertions + bucket insertions + preempted siblings lost), ORC_FAIL on error. */
+typedef struct {
+    uint64_t lookups;        /* refresh lookups routed */
+    uint64_t failed;         /* lookups that did not end successfully (hopCountMax, timeouts) */
+    uint64_t responses;      /* FindNodeResponses applied */
+    uint64_t sib_changes;    /* handles inserted into a sibling table */
+    uint64_t bucket_changes; /* handles inserted into a bucket */
+    uint64_t lost;           /* preempted siblings whose bucket was full */
+    uint64_t replacement;    /* alive handles a full bucket turned away (replacement cache) */
+    uint64_t refreshed;      /* alive handles already known (LRU move / sibling refresh) */
+} orc_kad_round_stats;
+uint64_t orc_kad_maintenance_round(orc_net* net, const uint32_t* nodes, uint64_t m, const uint8_t* flags,
+                                   const uint32_t* stale, orc_kad_round_stats* st, int nthreads);
+/* Kademlia::routingAdd(x, isAlive) at node v on explicit tables (the rules the round applies);
+ * returns its result, -1 on error */
+int orc_kad_routing_add(orc_net* net, uint32_t v, uint32_t x, int isAlive);
+/* explicit / snapshot tables in CSR form: siblings[n*5s] (NONE padded), bucket_off[n*160+1],
+ * bucket_nodes[bucket_off[n*160]] (each bucket in LRU order); bucket_nodes NULL = size query */
+void orc_kad_export_csr(const orc_net* net, uint32_t* siblings, uint64_t* bucket_off, uint32_t* bucket_nodes);
+
 /* One synchronous stabilize round for nodes[0..m) on explicit tables (Chord.cc:793-842, 1055-1225,
  * ChordSuccessorList.cc:101-194): returns the number of successor lists that changed (ORC_FAIL on
  * error), *succ_changed the successors that changed, *pred_changed the predecessors set. */

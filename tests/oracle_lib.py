@@ -96,6 +96,11 @@ def lib() -> C.CDLL:
             ("orc_chord_export_lists", [vp, vp, vp, vp], None),
             ("orc_kad_exhaustive_batch", [vp, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp, C.c_int], C.c_int),
             ("orc_kad_refresh_keys", [vp, vp, u64, vp, vp, vp, u64], u64),
+            ("orc_kad_exhaustive_batch_t", [vp, vp, vp, u64, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp,
+                                            C.c_int], C.c_int),
+            ("orc_kad_maintenance_round", [vp, vp, u64, vp, vp, vp, C.c_int], u64),
+            ("orc_kad_export_csr", [vp, vp, vp, vp], None),
+            ("orc_kad_routing_add", [vp, u32, u32, C.c_int], C.c_int),
             ("orc_epichord_find_node", [vp, u32, u32, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp,
                                         C.c_int, vp, u32, C.c_int64, C.c_int64, C.c_int, vp, vp, C.c_int], C.c_int),
             ("orc_kbrtest_lookup_stats", [vp, vp, vp, C.c_int, vp, vp, u64, C.c_double, C.c_int, C.c_double, vp],
@@ -106,6 +111,11 @@ def lib() -> C.CDLL:
             f.restype = res
         _L = L
     return _L
+
+
+class OrcKadRoundStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("lookups", "failed", "responses", "sib_changes", "bucket_changes", "lost",
+                                           "replacement", "refreshed")]
 
 
 class OrcStdDev(C.Structure):
@@ -257,6 +267,59 @@ class OracleNet:
             res["responders"] = resp
             res["rtt_ns"] = rtt
         return res
+
+    def exhaustive_times(self, keys, src, R: int, ccap: int | None = None, nthreads=0) -> dict:
+        """exhaustive() plus each accepted response's arrival at the source (tarr_ns) and every
+        FindNodeCall sent (call_node, call_ns: its arrival at the destination), ns from the
+        lookup's start (orc_kad_exhaustive_batch_t)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        src = np.ascontiguousarray(src, dtype=np.uint32)
+        n = len(keys)
+        H = max(self.params.hopCountMax, 1)
+        ccap = ccap or (2 * H + 2 * self.params.lookupParallelRpcs + 16)
+        out = np.empty(n, dtype=LOOKUP_DTYPE)
+        sib = np.empty((n, R), dtype=np.uint32)
+        resp = np.empty((n, H), dtype=np.uint32)
+        rtt, ta = (np.empty((n, H), dtype=np.int64) for _ in range(2))
+        cn = np.empty((n, ccap), dtype=np.uint32)
+        ct = np.empty((n, ccap), dtype=np.int64)
+        rpcs = np.empty(n, dtype=np.uint32)
+        r = lib().orc_kad_exhaustive_batch_t(self._h, _p(keys), _p(src), n, R, _p(out), _p(sib), _p(resp), _p(rtt),
+                                             _p(ta), _p(cn), _p(ct), ccap, _p(rpcs), nthreads)
+        if r < 0:
+            raise ValueError(lib().orc_last_error().decode())
+        res = {f: out[f].copy() for f in LOOKUP_DTYPE.names}
+        res.update(siblings=sib, rpcs=rpcs, responders=resp, rtt_ns=rtt, tarr_ns=ta, call_node=cn, call_ns=ct)
+        return res
+
+    def maintenance_round(self, nodes=None, flags=None, stale=None, nthreads=0) -> dict:
+        """One synchronous Kademlia maintenance round (orc_kad_maintenance_round) on explicit tables:
+        the listed nodes' refresh lookups, then routingAdd at every node; returns its counters."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        fl = None if flags is None else np.ascontiguousarray(np.broadcast_to(flags, nodes.shape), dtype=np.uint8)
+        st = None if stale is None else np.ascontiguousarray(stale, dtype=np.uint32)
+        stats = OrcKadRoundStats()
+        r = lib().orc_kad_maintenance_round(self._h, _p(nodes), len(nodes), _p(fl), _p(st), C.byref(stats), nthreads)
+        if r == ORC_FAIL:
+            raise RuntimeError(lib().orc_last_error().decode())
+        d = {f: getattr(stats, f) for f, _ in OrcKadRoundStats._fields_}
+        d["changes"] = int(r)
+        return d
+
+    def routing_add(self, v: int, x: int, alive: bool = True) -> int:
+        r = lib().orc_kad_routing_add(self._h, int(v), int(x), int(bool(alive)))
+        if r < 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return r
+
+    def kad_tables_csr(self):
+        """(siblings[n, 5s], bucket_off[n*160+1], bucket_nodes) -- buckets of any size, LRU order."""
+        sib = np.empty((self.n, 5 * self.params.s), dtype=np.uint32)
+        off = np.empty(self.n * 160 + 1, dtype=np.uint64)
+        lib().orc_kad_export_csr(self._h, _p(sib), _p(off), None)
+        nodes = np.empty(max(int(off[-1]), 1), dtype=np.uint32)
+        lib().orc_kad_export_csr(self._h, _p(sib), _p(off), _p(nodes))
+        return sib, off, nodes[: int(off[-1])]
 
     def refresh_keys(self, nodes, stale=None):
         """Bucket-refresh (key, src) pairs of Kademlia::handleBucketRefreshTimerExpired."""

@@ -585,6 +585,7 @@ class KadLookupSim:
             self.hops += 1
             self.hop_seq.append(src)
             self.rtts.append(self.now - self.sent_at[src])
+            self.arrivals.append(self.now)
         self.visited.add(src)
         self.step += 1
         self.pending -= 1
@@ -626,7 +627,7 @@ class KadLookupSim:
         self.key = to_int(key_words)
         self.exh = exhaustive
         self.R = exhaustive if exhaustive else self.cfg["redundant"]
-        self.sent_at, self.rtts = {}, []
+        self.sent_at, self.rtts, self.arrivals, self.calls = {}, [], [], []
         self.S, self.num_siblings = S, num_siblings
         self.fes, self.ins, self.now, self.tx = [], 0, 0, {}
         self.nh, self.visited, self.dead, self.rpcs, self.live = [], {S}, set(), {}, set()
@@ -659,7 +660,9 @@ class KadLookupSim:
             t, _, kind, h = heapq.heappop(self.fes)
             self.now = t
             if kind == "call_udp":            # source UDP: the call leaves through the tx queue
-                self._schedule(t + self._delay(S, h, self.call_b), "call_app_at", h)
+                ta = t + self._delay(S, h, self.call_b)
+                self.calls.append((h, ta))
+                self._schedule(ta, "call_app_at", h)
             elif kind == "call_app_at":       # responder UDP -> overlay (zero delay)
                 self._schedule(t, "call_rpc", h)
             elif kind == "call_rpc":          # findNodeRpc at the responder
@@ -708,12 +711,21 @@ class KadLookupSim:
                 done = self._check_stop()
         if not done:
             self._check_stop()
+        # calls still leaving the source's UDP when the lookup ended reach their destination anyway
+        # (IterativeLookup::stop cancels the RPC state, not the message; IterativeLookup.cc:256-261)
+        now_end = self.now
+        for t, _, kind, h in sorted(self.fes):
+            if kind == "call_udp":
+                self.now = t
+                self.calls.append((h, t + self._delay(S, h, self.call_b)))
+        self.now = now_end
         valid = self.success and self.finished
         hops = 0 if self.min_hops == 1 << 30 else self.min_hops
         if lookup_call:
             return dict(siblings=list(self.siblings) if valid else [], hops=hops, status=self._status(valid),
                         is_valid=int(valid), latency_ns=self.now if valid else -1, rpcs=self.nsent,
-                        responders=list(self.hop_seq), rtt_ns=list(self.rtts))
+                        responders=list(self.hop_seq), rtt_ns=list(self.rtts), tarr_ns=list(self.arrivals),
+                        calls=list(self.calls))
         if not valid or not self.siblings:
             return dict(responsible=0xFFFFFFFF, hops=hops, status=self._status(False), one_way_hops=0,
                         latency_ns=-1, hop_seq=self.hop_seq, rpcs=self.nsent)
@@ -733,6 +745,113 @@ class KadLookupSim:
         if self.hop_max and self.hops >= self.hop_max:
             return 3
         return 4
+
+
+# --- Kademlia maintenance: routingAdd and a synchronous refresh round -------------------------
+class KadMaint:
+    """A network's Kademlia tables as a running OverSim node keeps them, written from the reference
+    independently of oracle/ovs_oracle.c: per node the sibling table as a Python list kept sorted by
+    XOR distance to the node (KademliaBucket with its comparator, Kademlia.cc:179, 315-317) and the
+    routing buckets as a dict bucket index -> list in LRU order (push_back / erase, 432-756)."""
+
+    def __init__(self, ids_words, sib, bcount, bnodes, k=8, s=8):
+        self.ids = [to_int(w) for w in ids_words]
+        self.k, self.s = k, s
+        n = len(self.ids)
+        self.sib = []
+        self.bk = []
+        for v in range(n):
+            mine = [int(x) for x in sib[v] if x != 0xFFFFFFFF]
+            self.sib.append(sorted(mine, key=lambda x: self.ids[x] ^ self.ids[v]))
+            self.bk.append({m: [int(x) for x in bnodes[v][m][: bcount[v][m]]] for m in range(160) if bcount[v][m]})
+
+    def arrays(self):
+        n, S5 = len(self.ids), 5 * self.s
+        sib = [[0xFFFFFFFF] * S5 for _ in range(n)]
+        cnt = [[0] * 160 for _ in range(n)]
+        nodes = [[[0xFFFFFFFF] * self.k for _ in range(160)] for _ in range(n)]
+        for v in range(n):
+            for i, x in enumerate(self.sib[v]):
+                sib[v][i] = x
+            for m, lst in self.bk[v].items():
+                cnt[v][m] = len(lst)
+                for j, x in enumerate(lst):
+                    nodes[v][m][j] = x
+        return sib, cnt, nodes
+
+    def routing_add(self, v, h, alive):
+        """Kademlia::routingAdd (Kademlia.cc:432-756): secureMaintenance, pingNewSiblings, activePing
+        and proximityNeighborSelection off, bucketType kademlia (k per bucket).  Returns its result."""
+        if h == v:
+            return False
+        me = self.ids[v]
+        sib = self.sib[v]
+        if h in sib:
+            return True
+        b = (self.ids[h] ^ me).bit_length() - 1
+        bucket = self.bk[v].get(b)
+        if bucket is not None and h in bucket:
+            if alive:
+                bucket.remove(h)
+                bucket.append(h)
+            return True
+        cap = 5 * self.s
+        d = self.ids[h] ^ me
+        result = False
+        if len(sib) < cap or d <= (self.ids[sib[-1]] ^ me):      # siblingTable->isAddable
+            pos = next((i for i, x in enumerate(sib) if d < (self.ids[x] ^ me)), len(sib))
+            sib.insert(pos, h)
+            if len(sib) <= cap:
+                return True
+            h = sib.pop()                                        # preempted: goes to its bucket
+            result = True
+        b = (self.ids[h] ^ me).bit_length() - 1
+        bucket = self.bk[v].setdefault(b, [])
+        if len(bucket) < self.k:
+            bucket.append(h)
+            return True
+        return result
+
+    def refresh_keys(self, v):
+        """handleBucketRefreshTimerExpired's bucket keys (Kademlia.cc:1631-1676, b = 1)."""
+        if not self.sib[v]:
+            return []
+        me = self.ids[v]
+        front = self.ids[self.sib[v][0]] ^ me
+        return [me ^ (1 << i) for i in range(159, front.bit_length() - 2, -1)]
+
+    def round(self, xy, nodes, flags, lookup_cfg, R_bucket=8):
+        """One synchronous maintenance round: the listed nodes' exhaustive refresh lookups on the
+        round-start tables (KadLookupSim), then at every node the routingAdds of the calls that reached
+        it and of its handled responses (carried nodes not alive, then the responder alive), in
+        simulated-time order with ties (calls first, task, index)."""
+        sib, cnt, nod = self.arrays()
+        T = KadTables.__new__(KadTables)            # the round-start tables, as findNode reads them
+        T.ids, T.sib, T.bcount, T.bnodes, T.k, T.s = self.ids, sib, cnt, nod, self.k, self.s
+        sim = KadLookupSim(T, xy, k=self.k, **lookup_cfg)
+        tasks = []
+        for v, f in zip(nodes, flags):
+            if f & 1:
+                tasks.append((v, self.ids[v], 5 * self.s))
+            if f & 2:
+                tasks += [(v, key, R_bucket) for key in self.refresh_keys(v)]
+        events = {}
+        for t, (v, key, R) in enumerate(tasks):
+            words = [(key >> (32 * i)) & 0xFFFFFFFF for i in range(5)]
+            m = sim.run(words, v, num_siblings=R, lookup_call=True, exhaustive=R)
+            for i, (x, tc) in enumerate(m["calls"]):
+                events.setdefault(x, []).append((tc, 0, t, i, v, None))
+            for i, (x, ta) in enumerate(zip(m["responders"], m["tarr_ns"])):
+                events.setdefault(v, []).append((ta, 1, t, i, x, T.find_node(x, key, R, -1)))
+        for v, ev in events.items():
+            for _, kind, _, _, x, carried in sorted(ev, key=lambda e: e[:4]):
+                if kind == 0:
+                    self.routing_add(v, x, True)
+                else:
+                    for c in carried:
+                        self.routing_add(v, c, False)
+                    self.routing_add(v, x, True)
+        return len(tasks)
 
 
 # --- EpiChord::findNode on one routing snapshot ---------------------------------
