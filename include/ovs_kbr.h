@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 8
+#define OVS_ABI_VERSION 9
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -332,6 +332,32 @@ ovs_status  ovs_kad_refresh_batch(ovs_ctx* ctx, const ovs_key160* keys, const ui
                                   int32_t redundant_nodes, ovs_lookup_out* out, uint32_t* siblings,
                                   uint32_t* responders, int64_t* rtt_ns, uint32_t* rpcs, uint32_t flags,
                                   void* stream);
+/* One synchronous Kademlia maintenance round (ABI 9; replaces the bucket / sibling refresh
+ * timers and Kademlia::routingAdd, Kademlia.cc:432-756, 1328-1420, 1591-1686, for a NoChurn
+ * network).  For nodes[0..m): flags[j] bit 0 = the sibling-table refresh (an exhaustive-iterative
+ * lookup of the node's own key with siblingRefreshNodes = 5s), bit 1 = the bucket refreshes of the
+ * buckets stale[j*5..] marks (NULL = all; key self ^ 2^i, bucketRefreshNodes =
+ * lookupRedundantNodes); flags NULL = both.  All lookups run on the device over the tables of the
+ * round's start; then every node applies routingAdd, on the host, for each FindNodeCall that
+ * reached it (handleRpcCall: the caller, alive) and each FindNodeResponse its lookups handled
+ * (handleRpcResponse: the carried nodes, not alive, then the responder, alive) in simulated-time
+ * order -- every lookup of the round starts at its instant 0; ties: calls first, then lookup and
+ * message order -- with secureMaintenance, pingNewSiblings, activePing and PNS off (the
+ * defaults) and bucketType "kademlia".  The device tables are rebuilt from the result.  Needs the
+ * whole network in this context (ovs_kad_load or ovs_kad_load_tables); nodes / flags / stale are
+ * host buffers; stats may be NULL. */
+typedef struct ovs_kad_round_stats {
+    uint64_t lookups;        /* refresh lookups routed */
+    uint64_t failed;         /* lookups that did not end successfully (hopCountMax, timeouts) */
+    uint64_t responses;      /* FindNodeResponses applied */
+    uint64_t sib_changes;    /* handles inserted into a sibling table */
+    uint64_t bucket_changes; /* handles inserted into a bucket */
+    uint64_t lost;           /* preempted siblings whose bucket was full */
+    uint64_t replacement;    /* alive handles a full bucket turned away (replacement cache) */
+    uint64_t refreshed;      /* alive handles already known (LRU move / sibling refresh) */
+} ovs_kad_round_stats;
+ovs_status  ovs_kad_maintenance_round(ovs_ctx* ctx, const uint32_t* nodes, uint64_t m, const uint8_t* flags,
+                                      const uint32_t* stale, ovs_kad_round_stats* stats);
 /* The bucket-refresh lookups of nodes[0..m) (Kademlia.cc:1631-1676, b = 1):
  * key self ^ 2^i from the node for i = 159 down to msb(self ^ closest sibling)
  * where bit i of the node's stale mask is set -- stale = m*5 words (bit i of

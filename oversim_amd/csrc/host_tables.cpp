@@ -164,6 +164,156 @@ void ChordHost::stabilize(const uint32_t* nodes, uint64_t m, uint64_t* succ_chan
     for (uint32_t v : *changed_succ0) resolve_row(v);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Kademlia maintenance
+
+void KadHost::clear()
+{
+    ids.clear(); sib.clear(); bk.clear();
+    k = s = 0;
+}
+
+void KadHost::import(const K160* keys, uint64_t n, int k_in, int s_in, const uint32_t* siblings,
+                     const uint8_t* bucket_count, const uint32_t* bucket_nodes)
+{
+    clear();
+    k = k_in; s = s_in;
+    ids.assign(keys, keys + n);
+    sib.assign(n, {});
+    bk.assign(n * 160, {});
+    const uint64_t S5 = 5ull * (uint64_t)s;
+    for (uint64_t v = 0; v < n; ++v) {
+        std::vector<uint32_t>& L = sib[v];
+        for (uint64_t i = 0; i < S5; ++i)
+            if (siblings[v * S5 + i] != 0xFFFFFFFFu) L.push_back(siblings[v * S5 + i]);
+        const K160 me = ids[v];
+        std::sort(L.begin(), L.end(), [&](uint32_t a, uint32_t b) { return k_lt(k_xor(ids[a], me), k_xor(ids[b], me)); });
+        for (int m = 0; m < 160; ++m) {
+            const uint64_t bi = v * 160 + (uint64_t)m;
+            bk[bi].assign(bucket_nodes + bi * (uint64_t)k, bucket_nodes + bi * (uint64_t)k + bucket_count[bi]);
+        }
+    }
+}
+
+bool KadHost::export_k(uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes) const
+{
+    const uint64_t S5 = 5ull * (uint64_t)s, nn = n();
+    bool ok = true;
+    for (uint64_t v = 0; v < nn; ++v) {
+        for (uint64_t i = 0; i < S5; ++i) siblings[v * S5 + i] = i < sib[v].size() ? sib[v][i] : 0xFFFFFFFFu;
+        for (int m = 0; m < 160; ++m) {
+            const uint64_t bi = v * 160 + (uint64_t)m;
+            const std::vector<uint32_t>& B = bk[bi];
+            ok &= B.size() <= (size_t)k;
+            bucket_count[bi] = (uint8_t)std::min(B.size(), (size_t)k);
+            for (int q = 0; q < k; ++q) bucket_nodes[bi * (uint64_t)k + q] = (size_t)q < B.size() ? B[q] : 0xFFFFFFFFu;
+        }
+    }
+    return ok;
+}
+
+bool KadHost::routing_add(uint32_t v, uint32_t h, bool alive, KadRoundCount* st)
+{
+    if (h == v) return false;                                     // 437-439
+    const K160 me = ids[v];
+    std::vector<uint32_t>& S = sib[v];
+    for (uint32_t x : S)                                          // already a sibling (454-481)
+        if (x == h) { if (alive) st->refreshed++; return true; }
+    const K160 dh = k_xor(ids[h], me);
+    std::vector<uint32_t>& B = bk[(uint64_t)v * 160 + (uint64_t)k_msb(dh)];
+    for (size_t i = 0; i < B.size(); ++i)                         // already in its bucket (483-535)
+        if (B[i] == h) {
+            if (alive) {                                          // erase, re-add to the tail (514-517)
+                B.erase(B.begin() + (long)i);
+                B.push_back(h);
+                st->refreshed++;
+            }
+            return true;
+        }
+    bool result = false;
+    uint32_t cur = h;
+    const size_t cap = 5u * (size_t)s;
+    // siblingTable->isAddable: room, or closer than back() (NodeVector.h:381-399)
+    if (S.size() < cap || !k_lt(k_xor(ids[S.back()], me), dh)) {    // 537-616
+        size_t pos = 0;
+        while (pos < S.size() && !k_lt(dh, k_xor(ids[S[pos]], me))) ++pos;
+        S.insert(S.begin() + (long)pos, h);
+        st->sib_changes++;
+        if (S.size() <= cap) return true;                         // simply added
+        cur = S.back();                                           // the preempted handle goes on
+        S.pop_back();
+        result = true;
+    }
+    std::vector<uint32_t>& B2 = bk[(uint64_t)v * 160 + (uint64_t)k_msb(k_xor(ids[cur], me))];
+    if (B2.size() < (size_t)k) {                                  // !bucket->isFull() (665-701)
+        B2.push_back(cur);
+        st->bucket_changes++;
+        return true;
+    }
+    if (cur != h) st->lost++;             // a preempted sibling whose bucket is full leaves the tables
+    else if (alive) st->replacement++;    // replacement cache (729-745): membership unchanged
+    return result;
+}
+
+void KadHost::refresh_plan(const uint32_t* nodes, uint64_t m, const uint8_t* flags, const uint32_t* stale, int Rs,
+                           int Rb, std::vector<K160>* keys, std::vector<uint32_t>* src, std::vector<int>* R) const
+{
+    for (uint64_t j = 0; j < m; ++j) {
+        const uint32_t v = nodes[j];
+        const uint8_t f = flags ? flags[j] : 3;
+        const K160 me = ids[v];
+        if (f & 1) { keys->push_back(me); src->push_back(v); R->push_back(Rs); }
+        if (!(f & 2) || sib[v].empty()) continue;                 // if (siblingTable->size()) (1632)
+        // diff = L - (sharedPrefixLength(front) + 1) = msb(self ^ front) for b = 1 (1636-1637)
+        const int diff = k_msb(k_xor(ids[sib[v][0]], me));
+        for (int i = 159; i >= diff; --i) {
+            if (stale && !((stale[j * 5 + (uint64_t)(i >> 5)] >> (i & 31)) & 1u)) continue;
+            K160 key = me;
+            key.w[i >> 5] ^= 1u << (i & 31);                      // self ^ (OverlayKey(1) << i) (1647-1648)
+            keys->push_back(key); src->push_back(v); R->push_back(Rb);
+        }
+    }
+}
+
+void KadHost::apply_round(const std::vector<KadRoundLookup>& lk, KadRoundCount* st)
+{
+    struct Ev { int64_t t; uint32_t kind, task, idx; };
+    const uint64_t nn = n();
+    std::vector<uint64_t> off(nn + 1, 0);
+    for (const KadRoundLookup& L : lk) {
+        for (int i = 0; i < L.ncall; ++i) off[L.cnode[i] + 1]++;
+        off[L.src + 1] += (uint64_t)L.nresp;
+        st->responses += (uint64_t)L.nresp;
+    }
+    for (uint64_t v = 0; v < nn; ++v) off[v + 1] += off[v];
+    std::vector<Ev> ev(off[nn]);
+    std::vector<uint64_t> fill(off.begin(), off.end() - 1);
+    for (size_t t = 0; t < lk.size(); ++t) {
+        const KadRoundLookup& L = lk[t];
+        for (int i = 0; i < L.ncall; ++i) ev[fill[L.cnode[i]]++] = Ev{L.ctime[i], 0u, (uint32_t)t, (uint32_t)i};
+        for (int i = 0; i < L.nresp; ++i) ev[fill[L.src]++] = Ev{L.tarr[i], 1u, (uint32_t)t, (uint32_t)i};
+    }
+    for (uint64_t v = 0; v < nn; ++v) {
+        Ev* b = ev.data() + off[v];
+        Ev* e = ev.data() + off[v + 1];
+        std::sort(b, e, [](const Ev& x, const Ev& y) {
+            if (x.t != y.t) return x.t < y.t;
+            if (x.kind != y.kind) return x.kind < y.kind;
+            if (x.task != y.task) return x.task < y.task;
+            return x.idx < y.idx;
+        });
+        for (Ev* q = b; q < e; ++q) {
+            const KadRoundLookup& L = lk[q->task];
+            if (q->kind == 0) {
+                routing_add((uint32_t)v, L.src, true, st);
+            } else {
+                for (int c = 0; c < L.ncarried[q->idx]; ++c) routing_add((uint32_t)v, L.carried[q->idx][c], false, st);
+                routing_add((uint32_t)v, L.resp[q->idx], true, st);
+            }
+        }
+    }
+}
+
 bool epichord_prepare(const K160* keys, uint64_t n, int L, const uint32_t* succ, const uint8_t* nsucc,
                       const uint32_t* pred, const uint8_t* npred, const uint8_t* lists_full, const uint64_t* cache_off,
                       const uint32_t* cache_node, const int64_t* cache_last, const int64_t* cache_ttl,

@@ -47,6 +47,56 @@ struct ChordHost {
                    uint64_t* pred_changed, std::vector<uint32_t>* changed_succ0);
 };
 
+// Counters of a Kademlia maintenance round (ovs_kad_round_stats' twin)
+struct KadRoundCount {
+    uint64_t lookups = 0, failed = 0, responses = 0, sib_changes = 0, bucket_changes = 0, lost = 0, replacement = 0,
+             refreshed = 0;
+};
+
+// What one refresh lookup of a maintenance round produced (device results copied to the host):
+// the FindNodeCalls it sent (destination, arrival there), the responses it handled (responder,
+// arrival at the source) and each response's carried nodes (findNode(key, R, -1) at the responder).
+struct KadRoundLookup {
+    uint32_t src;
+    const uint32_t* cnode; const int64_t* ctime; int ncall;
+    const uint32_t* resp; const int64_t* tarr; int nresp;
+    const uint32_t* const* carried; const uint8_t* ncarried;   // per response
+};
+
+// Explicit Kademlia tables as the host keeps them between maintenance rounds: per node the sibling
+// table sorted by XOR distance to the node (Kademlia::siblingTable, a KademliaBucket with
+// KeyDistanceComparator<KeyXorMetric>, Kademlia.cc:179, 315-317) and the routing buckets in LRU
+// order (KademliaBucket push_back / erase in routingAdd, 432-756).
+struct KadHost {
+    std::vector<K160> ids;
+    int k = 0, s = 0;
+    std::vector<std::vector<uint32_t>> sib;    // n
+    std::vector<std::vector<uint32_t>> bk;     // n * 160
+
+    uint64_t n() const { return ids.size(); }
+    void clear();
+    // import siblings[n*5s] (any order) and bucket_count[n*160] / bucket_nodes[n*160*k] (LRU
+    // order); the device builder validates the invariants, this keeps a copy
+    void import(const K160* keys, uint64_t n, int k, int s, const uint32_t* siblings, const uint8_t* bucket_count,
+                const uint32_t* bucket_nodes);
+    // the k-stride arrays ovs_kad_load_tables takes (siblings XOR-sorted); false when a bucket holds
+    // more than k entries
+    bool export_k(uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes) const;
+    // Kademlia::routingAdd (Kademlia.cc:432-756) at node v: secureMaintenance, pingNewSiblings,
+    // activePing and proximityNeighborSelection off, bucketType "kademlia"; returns its result
+    bool routing_add(uint32_t v, uint32_t h, bool alive, KadRoundCount* st);
+    // a round's refresh lookups (handleBucketRefreshTimerExpired, 1591-1686) for nodes[0..m): per
+    // node, flags bit 0 the sibling refresh (own key, Rs), bit 1 the bucket refreshes of the buckets
+    // stale[j*5..] marks (NULL = all; key self ^ 2^i, i = 159 .. msb(self ^ front), Rb)
+    void refresh_plan(const uint32_t* nodes, uint64_t m, const uint8_t* flags, const uint32_t* stale, int Rs, int Rb,
+                      std::vector<K160>* keys, std::vector<uint32_t>* src, std::vector<int>* R) const;
+    // apply a round's routingAdd events: at every node, in simulated-time order (ties: calls first,
+    // then lookup and index order), a call reaching it adds its source alive (handleRpcCall,
+    // 1328-1349), a handled response adds the carried nodes not alive, then the responder alive
+    // (handleRpcResponse, 1352-1420)
+    void apply_round(const std::vector<KadRoundLookup>& lk, KadRoundCount* st);
+};
+
 // An EpiChord snapshot (ovs_epichord_load): validates the lists and the finger caches and returns the
 // per-node meta words and the cache rows sorted in liveCache map order (x - (v + 1)); false with
 // *err naming the node on an inconsistent snapshot.

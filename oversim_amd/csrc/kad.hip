@@ -345,10 +345,11 @@ __global__ void k_kad_export(const KadNode* __restrict__ nodes, const KadBlk* __
     bcount[t] = (uint8_t)c;
 }
 
-// batched findNode (numRedundantNodes <= 16, 1 <= numSiblings <= 16, or numSiblings = -1: the call
+// batched findNode (numRedundantNodes <= CAP, 1 <= numSiblings <= CAP, or numSiblings = -1: the call
 // of an exhaustive-iterative lookup, resultSize = numRedundantNodes and no siblings flag,
-// Kademlia.cc:1125-1127, BaseOverlay.cc:1857-1871) for the ABI
-template <bool EX>
+// Kademlia.cc:1125-1127, BaseOverlay.cc:1857-1871) for the ABI.  CAP = 64: the responses of the
+// sibling-table refresh (siblingRefreshNodes = 5s = 40) in maintenance rounds.
+template <bool EX, int CAP>
 __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, const K160* __restrict__ keys, uint64_t n,
                                 int numRedundant, int numSiblings, uint32_t* __restrict__ out_nodes, uint32_t max_out,
                                 uint8_t* __restrict__ out_count, uint8_t* __restrict__ out_sib)
@@ -359,12 +360,12 @@ __global__ void k_kad_find_node(KadView V, const uint32_t* __restrict__ node, co
     const K160 K = keys[i];
     const KadNode r = load_node(V.nodes, c);
     const bool sb = numSiblings >= 0 && kad_is_sibling(V, r, c, K, numSiblings);
-    SVec<16> res;
-    const int cnt = kad_find_node_ins<16, EX>(V, c, resp_geo(r, K), K, numRedundant, sb, res, numSiblings);
+    SVec<CAP> res;
+    const int cnt = kad_find_node_ins<CAP, EX>(V, c, resp_geo(r, K), K, numRedundant, sb, res, numSiblings);
     uint32_t* o = out_nodes + i * max_out;
     for (uint32_t j = 0; j < max_out; ++j) o[j] = NONE;
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
+    for (int j = 0; j < CAP; ++j)
         if (j < cnt && (uint32_t)j < max_out) o[j] = res.idx[j];
     out_count[i] = (uint8_t)(cnt < (int)max_out ? cnt : (int)max_out);
     out_sib[i] = sb ? 1 : 0;
@@ -574,14 +575,14 @@ hipError_t kad_find_node(const KadTables& t, uint32_t n, const ovs_params& P, co
 {
     (void)P;
     if (nq == 0) return hipSuccess;
-    if ((numSiblings < 1 && numSiblings != -1) || numSiblings > 16 || numRedundant > 16) return hipErrorNotSupported;
+    if ((numSiblings < 1 && numSiblings != -1) || numSiblings > 64 || numRedundant > 64) return hipErrorNotSupported;
     const KadView V = kad_make_view(t, nullptr, n);
-    if (t.exact)
-        hipLaunchKernelGGL(k_kad_find_node<true>, dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, numRedundant,
-                           numSiblings, out_nodes, max_out, out_count, out_sib);
-    else
-        hipLaunchKernelGGL(k_kad_find_node<false>, dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, numRedundant,
-                           numSiblings, out_nodes, max_out, out_count, out_sib);
+    const bool wide = numSiblings > 16 || numRedundant > 16;
+#define KFN(ex, cap) hipLaunchKernelGGL((k_kad_find_node<ex, cap>), dim3(nblk(nq, 128)), dim3(128), 0, st, V, node, keys, nq, \
+                                        numRedundant, numSiblings, out_nodes, max_out, out_count, out_sib)
+    if (t.exact) { if (wide) KFN(true, 64); else KFN(true, 16); }
+    else { if (wide) KFN(false, 64); else KFN(false, 16); }
+#undef KFN
     return hipGetLastError();
 }
 

@@ -122,10 +122,19 @@ hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ov
 // of ns <= R; out = ovs_route_out (oneway: KBRTestApp one-way test) or ovs_lookup_out; responders =
 // the accepted responders in order (= hop_seq); *capacity_error: a lookup ran past the kernel's
 // fixed capacities (more than 64 timed-out nodes)
+// trace: (maintenance rounds) per accepted response its arrival at the source (tarr, hopCountMax
+// per lookup), per FindNodeCall sent its destination and arrival there (cnode / ctime, ccap per
+// lookup; a lookup sending more is a capacity error)
+struct KadExhTrace {
+    int64_t* tarr;
+    uint32_t* cnode;
+    int64_t* ctime;
+    int ccap;
+};
 hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
                           int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
                           uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                          hipStream_t st, bool* capacity_error);
+                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace = nullptr);
 // free the exhaustive-lookup scratch K2x keeps for `device` between calls (ovs_ctx_destroy)
 void kad_exhaustive_release(int device);
 // bucket-refresh keys of nodes[0..m) (device buffers); *total = how many (up to cap written)

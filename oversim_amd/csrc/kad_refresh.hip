@@ -80,7 +80,17 @@ struct XRegNh {
     uint32_t used;      // bit i: entry i alreadyUsed
 };
 
-template <bool EX, bool REG, int XA>
+// Maintenance-round trace (TR instantiations, kad_maintenance_round): per accepted response its
+// arrival at the source; per FindNodeCall sent its destination and its arrival there -- the events
+// at which Kademlia::handleRpcCall / handleRpcResponse run routingAdd (Kademlia.cc:1328-1420).
+struct XTrace {
+    int64_t* tarr;       // [nq][hcm]
+    uint32_t* cnode;     // [nq][ccap]
+    int64_t* ctime;      // [nq][ccap]
+    int ccap;
+};
+
+template <bool EX, bool REG, int XA, bool TR = false>
 struct XCtx {
     using XL = XLookup<XA>;
     const KadView& V;
@@ -91,6 +101,10 @@ struct XCtx {
     uint32_t* __restrict__ resp;      // responders of this lookup (hop order), hcm entries
     int64_t* __restrict__ rtt;        // their RTTs (may be null)
     uint32_t* __restrict__ sib;       // ns siblings of this lookup
+    int64_t* __restrict__ tarr = nullptr;    // TR: response arrivals (hop order)
+    uint32_t* __restrict__ cn = nullptr;     // TR: calls sent: destination ...
+    int64_t* __restrict__ ct = nullptr;      // ... and its arrival there
+    int ccap = 0;
 
     __device__ __forceinline__ uint64_t at(int j) const { return (uint64_t)j * X.lanes + lane; }
 
@@ -357,6 +371,11 @@ struct XCtx {
                                                               : bw_ns(DC.respBase + DC.respPerNode * rn, DC.datarate, DC.round);
             d2 = 2 * bwr + DC.access2 + cd;
         }
+        if constexpr (TR) {
+            // the call reaches x at now + d1 whatever happens to its response
+            if ((int)L.nsent < ccap) { cn[L.nsent] = x; ct[L.nsent] = L.now + d1; }
+            else L.err = true;
+        }
         const int64_t tTo = L.now + DC.rpcTimeout;
         const int64_t tResp = L.now + d1 + d2;
         const bool to = tTo <= tResp;           // the timeout was scheduled first: it wins a tie
@@ -527,6 +546,7 @@ struct XCtx {
                         if (L.nhop < C.hcm) {
                             resp[L.nhop] = cur.node;
                             if (rtt) rtt[L.nhop] = L.now - cur.tsend;
+                            if constexpr (TR) tarr[L.nhop] = L.now;
                         }
                         ++L.nhop;
                         ++L.hops;
@@ -682,13 +702,13 @@ __device__ __forceinline__ void kx_emit(const XLookup<XA>& L, const KadView& V, 
 // One lane per lookup, one loop iteration per kernel-loop iteration; a lane whose lookup ended
 // takes the next one of its wave's contiguous slice of the batch (ballot + popcount, no atomics),
 // so a wave does not wait for its longest lookup before its lanes move on (as K2).
-template <bool EX, bool REG, int XA>
+template <bool EX, bool REG, int XA, bool TR>
 __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C, XScratch X,
                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                      uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
                                                      uint32_t* __restrict__ sib_out, uint32_t* __restrict__ resp_out,
                                                      int64_t* __restrict__ rtt_out, uint32_t* __restrict__ rpcs_out,
-                                                     uint32_t* __restrict__ err)
+                                                     uint32_t* __restrict__ err, XTrace T)
 {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int wl = threadIdx.x & 63;
@@ -699,7 +719,7 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     bool active = false;
     uint64_t q = 0;
     XLookup<XA> L;
-    typename XCtx<EX, REG, XA>::Run R;
+    typename XCtx<EX, REG, XA, TR>::Run R;
     while (true) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && cursor < end) {
@@ -708,7 +728,7 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
                 q = mine;
                 active = true;
                 kx_init_lookup<EX, REG>(L, V, C, qkeys, qsrc, sib_out, q);
-                const XCtx<EX, REG, XA> c0{V, DC, C, X, lane, nullptr, nullptr, nullptr};
+                const XCtx<EX, REG, XA, TR> c0{V, DC, C, X, lane, nullptr, nullptr, nullptr};
                 c0.init(L, R);
             }
             cursor += (uint64_t)__popcll(need);
@@ -718,9 +738,19 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
         uint32_t* sib = sib_out + q * (uint64_t)C.ns;
         uint32_t* resp = resp_out + q * (uint64_t)C.hcm;
         int64_t* rtt = rtt_out ? rtt_out + q * (uint64_t)C.hcm : nullptr;
-        const XCtx<EX, REG, XA> ctx{V, DC, C, X, lane, resp, rtt, sib};
+        XCtx<EX, REG, XA, TR> ctx{V, DC, C, X, lane, resp, rtt, sib};
+        if constexpr (TR) {
+            ctx.tarr = T.tarr + q * (uint64_t)C.hcm;
+            ctx.cn = T.cnode + q * (uint64_t)T.ccap;
+            ctx.ct = T.ctime + q * (uint64_t)T.ccap;
+            ctx.ccap = T.ccap;
+        }
         if (ctx.step(L, R)) {
             kx_emit(L, V, DC, C, q, out, sib, resp, rtt, rpcs_out, err);
+            if constexpr (TR) {
+                for (int j = L.nhop; j < C.hcm; ++j) ctx.tarr[j] = -1;
+                for (int j = (int)L.nsent; j < T.ccap; ++j) { ctx.cn[j] = NONE; ctx.ct[j] = -1; }
+            }
             active = false;
         }
     }
@@ -797,7 +827,7 @@ size_t g_scratch_cap[64] = {};
 hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
                           int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
                           uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                          hipStream_t st, bool* capacity_error)
+                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace)
 {
     *capacity_error = false;
     if (nq == 0) return hipSuccess;
@@ -823,14 +853,16 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
     // the occupancy of each instantiation, per device, filled under the scratch mutex
-    static int bpc[64][8] = {};
+    static int bpc[64][16] = {};
     const bool a8 = A > 4;     // the 8-slot instantiations serve lookupParallelRpcs 5..8
-    const int ki = (t.exact ? 2 : 0) + (reg ? 1 : 0) + (a8 ? 4 : 0);
+    const bool tr = trace != nullptr;
+    const int ki = (t.exact ? 2 : 0) + (reg ? 1 : 0) + (a8 ? 4 : 0) + (tr ? 8 : 0);
     std::unique_lock<std::mutex> lock(g_scratch_mu);
     if (bpc[dev][ki] == 0) {
         int b = 0;
         hipError_t oe;
-#define KOCC(ex, rg, xa) hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<ex, rg, xa>, 256, 0)
+#define KOCC(ex, rg, xa) (tr ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<ex, rg, xa, true>, 256, 0) \
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_refresh<ex, rg, xa, false>, 256, 0))
         if (a8) {
             if (t.exact) oe = reg ? KOCC(true, true, 8) : KOCC(true, false, 8);
             else oe = reg ? KOCC(false, true, 8) : KOCC(false, false, 8);
@@ -868,8 +900,15 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     const uint64_t waves = lanes / 64;
     const uint64_t chunk = (nq + waves - 1) / waves;
     ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);   // or ovs_lookup_out (same size)
-#define KRL(ex, rg, xa) hipLaunchKernelGGL((k_kad_refresh<ex, rg, xa>), dim3(blocks), dim3(256), 0, st, V, DC, C, X, qkeys, \
-                                           qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err)
+    XTrace T{};
+    if (tr) { T.tarr = trace->tarr; T.cnode = trace->cnode; T.ctime = trace->ctime; T.ccap = trace->ccap; }
+#define KRL(ex, rg, xa)                                                                                                 \
+    do {                                                                                                                \
+        if (tr) hipLaunchKernelGGL((k_kad_refresh<ex, rg, xa, true>), dim3(blocks), dim3(256), 0, st, V, DC, C, X,    \
+                                   qkeys, qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err, T);                  \
+        else hipLaunchKernelGGL((k_kad_refresh<ex, rg, xa, false>), dim3(blocks), dim3(256), 0, st, V, DC, C, X,      \
+                                qkeys, qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err, T);                     \
+    } while (0)
     if (a8) {
         if (t.exact) { if (reg) KRL(true, true, 8); else KRL(true, false, 8); }
         else { if (reg) KRL(false, true, 8); else KRL(false, false, 8); }

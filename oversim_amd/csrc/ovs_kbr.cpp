@@ -50,6 +50,8 @@ struct ovs_ctx {
     int sls = 0;
     // explicit tables: host copies for batched maintenance (ovs_chord_fix_fingers / _stabilize)
     ChordHost ch;
+    // explicit Kademlia tables: host copy for maintenance rounds (ovs_kad_maintenance_round)
+    KadHost kh;
     uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     std::vector<uint64_t> h_bounds;         // ... as last uploaded (uploaded again only on a change)
@@ -114,6 +116,7 @@ void free_tables(ovs_ctx* c)
     c->kvis = nullptr; c->kvis_cap = 0;
     c->overlay = 0; c->n = 0; c->nfing = 0;
     c->ch.clear();
+    c->kh.clear();
 }
 
 void free_kad_shard(ovs_ctx* c)
@@ -723,6 +726,7 @@ ovs_status ovs_kad_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     }
     if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "explicit Kademlia table build"); }
     c->overlay = OVS_OVERLAY_KADEMLIA;
+    c->kh.import(reinterpret_cast<const K160*>(ids), n, c->P.k, c->P.s, siblings, bucket_count, bucket_nodes);
     return OVS_OK;
 }
 
@@ -1345,6 +1349,218 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
         HIPCHK(c, hipStreamSynchronize(s));
     }
     cleanup();
+    return OVS_OK;
+}
+
+extern "C++" {
+namespace {
+
+// rebuild the device tables of a whole-network Kademlia context from its host copy
+ovs_status kad_upload_host_tables(ovs_ctx* c)
+{
+    const uint64_t n = c->n, S5 = 5ull * (uint64_t)c->P.s, k = (uint64_t)c->P.k;
+    std::vector<uint32_t> hs(n * S5), hn(n * 160 * k);
+    std::vector<uint8_t> hc(n * 160);
+    if (!c->kh.export_k(hs.data(), hc.data(), hn.data()))
+        return fail(c, OVS_ENOTSUP, "a bucket outgrew k (bucketType kademlia keeps k per bucket)");
+    uint32_t *dsib = nullptr, *dbn = nullptr;
+    uint8_t* dbc = nullptr;
+    auto release = [&]() { if (dsib) hipFree(dsib); if (dbn) hipFree(dbn); if (dbc) hipFree(dbc); };
+    if (hipMalloc(&dsib, sizeof(uint32_t) * n * S5) != hipSuccess || hipMalloc(&dbc, n * 160) != hipSuccess ||
+        hipMalloc(&dbn, sizeof(uint32_t) * n * 160 * k) != hipSuccess) {
+        release();
+        return fail(c, OVS_ENOMEM, "maintenance round: device allocation failed");
+    }
+    hipError_t e = hipMemcpy(dsib, hs.data(), sizeof(uint32_t) * n * S5, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dbc, hc.data(), n * 160, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dbn, hn.data(), sizeof(uint32_t) * n * 160 * k, hipMemcpyHostToDevice);
+    uint32_t bad_node = 0, bad_code = 0;
+    if (e == hipSuccess) {
+        kad_free(c->kad);
+        e = kad_build_explicit(c->recs, c->xy, (uint32_t)n, c->P.k, c->P.s, dsib, dbc, dbn, c->kad, &bad_node, &bad_code,
+                               c->stream);
+    }
+    release();
+    if (e == hipErrorInvalidValue && bad_code) {
+        char m[160];
+        std::snprintf(m, sizeof m, "maintenance round broke a table invariant at node %u (code %u)", bad_node, bad_code);
+        return fail(c, OVS_EDEVICE, m);
+    }
+    if (e != hipSuccess) return hip_fail(c, e, "maintenance round: table rebuild");
+    return OVS_OK;
+}
+
+// device buffers of a round, freed on every path
+struct DevBufs {
+    std::vector<void*> p;
+    template <class T>
+    hipError_t get(T** out, uint64_t count)
+    {
+        *out = nullptr;
+        const hipError_t e = hipMalloc(out, sizeof(T) * (count ? count : 1));
+        if (e == hipSuccess) p.push_back(*out);
+        return e;
+    }
+    ~DevBufs() { for (void* q : p) hipFree(q); }
+};
+
+}  // namespace
+}  // extern "C++"
+
+ovs_status ovs_kad_maintenance_round(ovs_ctx* c, const uint32_t* nodes, uint64_t m, const uint8_t* flags,
+                                     const uint32_t* stale, ovs_kad_round_stats* stats)
+{
+    if (!c || (m && !nodes)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "maintenance rounds need the whole network");
+    const ovs_params& P = c->P;
+    if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "maintenance rounds run iterative refresh lookups");
+    if (P.hopCountMax < 1) return fail(c, OVS_ENOTSUP, "refresh lookups need hopCountMax >= 1");
+    if (!P.lookupMerge || !P.lookupStrictParallelRpcs || P.lookupParallelRpcs < 1 || P.lookupParallelRpcs > KAD_MAX_ALPHA)
+        return fail(c, OVS_ENOTSUP, "refresh lookups implement lookupMerge, strictParallelRpcs, parallelRpcs 1..8");
+    if (P.lookupParallelPaths != 1 || P.lookupVerifySiblings || P.lookupMajoritySiblings || P.jitter != 0.0)
+        return fail(c, OVS_ENOTSUP, "parallelPaths 1, no verify/majority siblings, jitter 0");
+    const int Rs = 5 * P.s, Rb = P.lookupRedundantNodes;
+    if (Rs > 64 || Rb > 64) return fail(c, OVS_ENOTSUP, "refresh lookups implement redundantNodes 1..64");
+    for (uint64_t j = 0; j < m; ++j)
+        if (nodes[j] >= c->n) return fail(c, OVS_EINVAL, "node index out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (c->kh.n() != c->n) {
+        // a snapshot network (ovs_kad_load): its tables become the host copy
+        const uint64_t n = c->n, S5 = 5ull * (uint64_t)P.s, k = (uint64_t)P.k;
+        std::vector<uint32_t> hs(n * S5), hn(n * 160 * k);
+        std::vector<uint8_t> hc(n * 160);
+        const hipError_t e = kad_export(c->kad, (uint32_t)n, hs.data(), hc.data(), hn.data(), s);
+        if (e != hipSuccess) return hip_fail(c, e, "maintenance round: table export");
+        std::vector<K160> ids(n);
+        std::vector<KeyRec> recs(n);
+        HIPCHK(c, hipMemcpy(recs.data(), c->recs, sizeof(KeyRec) * n, hipMemcpyDeviceToHost));
+        for (uint64_t v = 0; v < n; ++v) ids[v] = key_of(recs[v]);
+        c->kh.import(ids.data(), n, P.k, P.s, hs.data(), hc.data(), hn.data());
+    }
+    KadRoundCount cnt;
+    std::vector<K160> keys;
+    std::vector<uint32_t> src;
+    std::vector<int> R;
+    c->kh.refresh_plan(nodes, m, flags, stale, Rs, Rb, &keys, &src, &R);
+    const uint64_t nt = keys.size(), H = (uint64_t)P.hopCountMax;
+    const int ccap = 2 * P.hopCountMax + 2 * P.lookupParallelRpcs + 16;
+    cnt.lookups = nt;
+    // host results of every lookup
+    std::vector<uint32_t> resp(nt * H), cnode(nt * (uint64_t)ccap);
+    std::vector<int64_t> tarr(nt * H), ctime(nt * (uint64_t)ccap);
+    std::vector<ovs_lookup_out> outv(nt);
+    const DelayConsts DC = delay_consts(P);
+    for (int g = 0; g < 2 && nt; ++g) {
+        const int Rg = g == 0 ? Rs : Rb;
+        if (g == 1 && Rb == Rs) break;
+        std::vector<uint64_t> ix;
+        for (uint64_t t = 0; t < nt; ++t)
+            if (R[t] == Rg) ix.push_back(t);
+        if (ix.empty()) continue;
+        const uint64_t ng = ix.size();
+        std::vector<K160> gk(ng);
+        std::vector<uint32_t> gs(ng);
+        for (uint64_t q = 0; q < ng; ++q) { gk[q] = keys[ix[q]]; gs[q] = src[ix[q]]; }
+        DevBufs d;
+        K160* dk; uint32_t *ds, *dsib, *dresp, *drpc, *dcn; ovs_lookup_out* dout; int64_t *dta, *dct;
+        HIPCHK(c, d.get(&dk, ng)); HIPCHK(c, d.get(&ds, ng)); HIPCHK(c, d.get(&dsib, ng * (uint64_t)Rg));
+        HIPCHK(c, d.get(&dresp, ng * H)); HIPCHK(c, d.get(&drpc, ng)); HIPCHK(c, d.get(&dout, ng));
+        HIPCHK(c, d.get(&dta, ng * H)); HIPCHK(c, d.get(&dcn, ng * (uint64_t)ccap)); HIPCHK(c, d.get(&dct, ng * (uint64_t)ccap));
+        HIPCHK(c, hipMemcpyAsync(dk, gk.data(), sizeof(K160) * ng, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(ds, gs.data(), sizeof(uint32_t) * ng, hipMemcpyHostToDevice, s));
+        const KadExhTrace tr{dta, dcn, dct, ccap};
+        bool cap_err = false;
+        const hipError_t e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, DC, Rg, Rg, false, dk, ds, ng, dout, dsib,
+                                            dresp, nullptr, drpc, c->num_cu, s, &cap_err, &tr);
+        if (e != hipSuccess) return hip_fail(c, e, "maintenance round: refresh lookups");
+        if (cap_err) return fail(c, OVS_ENOTSUP, "a refresh lookup exceeded the kernel's capacity");
+        std::vector<uint32_t> hr(ng * H), hc(ng * (uint64_t)ccap);
+        std::vector<int64_t> hta(ng * H), hct(ng * (uint64_t)ccap);
+        std::vector<ovs_lookup_out> ho(ng);
+        HIPCHK(c, hipMemcpyAsync(hr.data(), dresp, sizeof(uint32_t) * ng * H, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(hta.data(), dta, sizeof(int64_t) * ng * H, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(hc.data(), dcn, sizeof(uint32_t) * ng * ccap, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(hct.data(), dct, sizeof(int64_t) * ng * ccap, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(ho.data(), dout, sizeof(ovs_lookup_out) * ng, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        for (uint64_t q = 0; q < ng; ++q) {
+            const uint64_t t = ix[q];
+            std::copy(hr.begin() + q * H, hr.begin() + (q + 1) * H, resp.begin() + t * H);
+            std::copy(hta.begin() + q * H, hta.begin() + (q + 1) * H, tarr.begin() + t * H);
+            std::copy(hc.begin() + q * ccap, hc.begin() + (q + 1) * ccap, cnode.begin() + t * ccap);
+            std::copy(hct.begin() + q * ccap, hct.begin() + (q + 1) * ccap, ctime.begin() + t * ccap);
+            outv[t] = ho[q];
+        }
+    }
+    // the carried nodes of every handled response: findNode(key, R, -1) at the responder on the
+    // round-start tables (BaseOverlay::findNodeRpc, BaseOverlay.cc:1841-1915), on the device
+    std::vector<uint64_t> pair_off(nt * H + 1, 0);
+    std::vector<uint32_t> carried;
+    std::vector<uint8_t> ncarried(nt * H, 0);
+    std::vector<int> nresp(nt, 0), ncall(nt, 0);
+    for (uint64_t t = 0; t < nt; ++t) {
+        while (nresp[t] < (int)H && resp[t * H + nresp[t]] != 0xFFFFFFFFu) ++nresp[t];
+        while (ncall[t] < ccap && cnode[t * ccap + ncall[t]] != 0xFFFFFFFFu) ++ncall[t];
+        if (outv[t].status != OVS_LOOKUP_OK) cnt.failed++;
+    }
+    std::vector<uint64_t> roff(nt * H, 0);
+    {
+        uint64_t tot = 0;
+        for (uint64_t t = 0; t < nt; ++t)
+            for (int i = 0; i < nresp[t]; ++i) { roff[t * H + i] = tot; tot += (uint64_t)R[t]; }
+        carried.assign(tot ? tot : 1, 0xFFFFFFFFu);
+        for (int g = 0; g < 2; ++g) {
+            const int Rg = g == 0 ? Rs : Rb;
+            if (g == 1 && Rb == Rs) break;
+            std::vector<uint32_t> pn;
+            std::vector<K160> pk;
+            std::vector<uint64_t> pri;
+            for (uint64_t t = 0; t < nt; ++t)
+                if (R[t] == Rg)
+                    for (int i = 0; i < nresp[t]; ++i) { pn.push_back(resp[t * H + i]); pk.push_back(keys[t]); pri.push_back(t * H + i); }
+            const uint64_t np = pn.size();
+            if (np == 0) continue;
+            DevBufs d;
+            uint32_t *dn, *dout; K160* dk; uint8_t *dcount, *dsb;
+            HIPCHK(c, d.get(&dn, np)); HIPCHK(c, d.get(&dk, np)); HIPCHK(c, d.get(&dout, np * (uint64_t)Rg));
+            HIPCHK(c, d.get(&dcount, np)); HIPCHK(c, d.get(&dsb, np));
+            HIPCHK(c, hipMemcpyAsync(dn, pn.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, s));
+            HIPCHK(c, hipMemcpyAsync(dk, pk.data(), sizeof(K160) * np, hipMemcpyHostToDevice, s));
+            const hipError_t e = kad_find_node(c->kad, (uint32_t)c->n, P, dn, dk, np, Rg, -1, dout, (uint32_t)Rg, dcount,
+                                               dsb, s);
+            if (e != hipSuccess) return hip_fail(c, e, "maintenance round: findNode of the responses");
+            std::vector<uint32_t> ho(np * (uint64_t)Rg);
+            std::vector<uint8_t> hcount(np);
+            HIPCHK(c, hipMemcpyAsync(ho.data(), dout, sizeof(uint32_t) * np * Rg, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(hcount.data(), dcount, np, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            for (uint64_t q = 0; q < np; ++q) {
+                ncarried[pri[q]] = hcount[q];
+                std::copy(ho.begin() + q * Rg, ho.begin() + q * Rg + hcount[q], carried.begin() + roff[pri[q]]);
+            }
+        }
+    }
+    std::vector<const uint32_t*> cptr(nt * H, nullptr);
+    for (uint64_t t = 0; t < nt; ++t)
+        for (int i = 0; i < nresp[t]; ++i) cptr[t * H + i] = carried.data() + roff[t * H + i];
+    std::vector<KadRoundLookup> lk(nt);
+    for (uint64_t t = 0; t < nt; ++t) {
+        KadRoundLookup& L = lk[t];
+        L.src = src[t];
+        L.cnode = cnode.data() + t * ccap; L.ctime = ctime.data() + t * ccap; L.ncall = ncall[t];
+        L.resp = resp.data() + t * H; L.tarr = tarr.data() + t * H; L.nresp = nresp[t];
+        L.carried = cptr.data() + t * H; L.ncarried = ncarried.data() + t * H;
+    }
+    c->kh.apply_round(lk, &cnt);
+    const ovs_status us = kad_upload_host_tables(c);
+    if (us != OVS_OK) return us;
+    if (stats) {
+        stats->lookups = cnt.lookups; stats->failed = cnt.failed; stats->responses = cnt.responses;
+        stats->sib_changes = cnt.sib_changes; stats->bucket_changes = cnt.bucket_changes; stats->lost = cnt.lost;
+        stats->replacement = cnt.replacement; stats->refreshed = cnt.refreshed;
+    }
     return OVS_OK;
 }
 

@@ -213,6 +213,7 @@ def lib() -> C.CDLL:
         "ovs_chord_export_tables": ([vp, vp, vp, vp], C.c_int),
         "ovs_kad_refresh_batch": ([vp, vp, vp, u64, i32, vp, vp, vp, vp, vp, u32, vp], C.c_int),
         "ovs_kad_refresh_keys": ([vp, vp, u64, vp, vp, vp, u64, C.POINTER(u64), u32, vp], C.c_int),
+        "ovs_kad_maintenance_round": ([vp, vp, u64, vp, vp, vp], C.c_int),
         "ovs_kbrtest_lookup_stats_batch": ([vp, vp, vp, i32, vp, vp, u64, C.c_double, i32, C.c_double, vp, u32, vp],
                                            C.c_int),
     }
@@ -256,6 +257,13 @@ class StabilizeStats(C.Structure):
 
     _fields_ = [("nodes", C.c_uint64), ("succ_changed", C.c_uint64), ("lists_changed", C.c_uint64),
                 ("pred_changed", C.c_uint64)]
+
+
+class KadRoundStats(C.Structure):
+    """ovs_kad_round_stats: one Kademlia maintenance round (ovs_kad_maintenance_round)."""
+
+    _fields_ = [(f, C.c_uint64) for f in ("lookups", "failed", "responses", "sib_changes", "bucket_changes", "lost",
+                                           "replacement", "refreshed")]
 
 
 class KbrTestLookupStats(C.Structure):
@@ -463,6 +471,21 @@ class KbrEngine:
         self._chk(self._L.ovs_chord_stabilize(self._h, _ptr(nodes), len(nodes), C.cast(C.byref(st), C.c_void_p)),
                   "ovs_chord_stabilize")
         return {f: getattr(st, f) for f, _ in StabilizeStats._fields_}
+
+    def kad_maintenance_round(self, nodes=None, flags=None, stale=None) -> dict:
+        """One synchronous Kademlia maintenance round (ovs_kad_maintenance_round): the listed nodes'
+        refresh lookups on the device (flags bit 0 sibling refresh, bit 1 bucket refreshes; None =
+        both), then Kademlia::routingAdd for every call and response on the host; returns the counters
+        plus "changes" (membership changes)."""
+        nodes = np.arange(self.n, dtype=np.uint32) if nodes is None else np.ascontiguousarray(nodes, np.uint32)
+        fl = None if flags is None else np.ascontiguousarray(np.broadcast_to(flags, nodes.shape), dtype=np.uint8)
+        stl = None if stale is None else np.ascontiguousarray(stale, dtype=np.uint32)
+        st = KadRoundStats()
+        self._chk(self._L.ovs_kad_maintenance_round(self._h, _ptr(nodes), len(nodes), _ptr(fl), _ptr(stl),
+                                                    C.cast(C.byref(st), C.c_void_p)), "ovs_kad_maintenance_round")
+        d = {f: getattr(st, f) for f, _ in KadRoundStats._fields_}
+        d["changes"] = d["sib_changes"] + d["bucket_changes"] + d["lost"]
+        return d
 
     def chord_tables(self):
         """(pred, succ (n, successorListSize), nsucc) of an explicit-table ring as they now stand."""

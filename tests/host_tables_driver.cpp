@@ -171,10 +171,104 @@ static void epichord_snapshots()
     }
 }
 
+// routingAdd's invariants on every node: siblings XOR-sorted, at most 5s of them; every bucket member
+// in its own bucket msb(x ^ v), at most k; no node twice, never v itself
+static void kad_check(const KadHost& h)
+{
+    const uint64_t n = h.n();
+    std::vector<uint32_t> seen(n, 0xFFFFFFFFu);
+    for (uint64_t v = 0; v < n; ++v) {
+        const std::vector<uint32_t>& S = h.sib[v];
+        CHECK(S.size() <= 5u * (size_t)h.s);
+        for (size_t i = 0; i < S.size(); ++i) {
+            CHECK(S[i] < n && S[i] != v && seen[S[i]] != v);
+            seen[S[i]] = (uint32_t)v;
+            if (i) CHECK(k_lt(k_xor(h.ids[S[i - 1]], h.ids[v]), k_xor(h.ids[S[i]], h.ids[v])));
+        }
+        for (int m = 0; m < 160; ++m) {
+            const std::vector<uint32_t>& B = h.bk[v * 160 + (uint64_t)m];
+            CHECK(B.size() <= (size_t)h.k);
+            for (uint32_t x : B) {
+                CHECK(x < n && x != v && seen[x] != v);
+                seen[x] = (uint32_t)v;
+                CHECK(k_msb(k_xor(h.ids[x], h.ids[v])) == m);
+            }
+        }
+    }
+}
+
+// Kademlia maintenance bookkeeping: routingAdd from empty tables (sibling insertions, preemption
+// into buckets, full buckets, LRU moves), the refresh plan, and a round of synthetic events
+static void kad_maintenance()
+{
+    const uint64_t n = 400;
+    const int k = 4, s = 2;
+    std::vector<K160> id = sorted_keys(n);
+    std::vector<uint32_t> sib(n * 5 * s, 0xFFFFFFFFu), bn(n * 160 * k, 0xFFFFFFFFu);
+    std::vector<uint8_t> bc(n * 160, 0);
+    KadHost h;
+    h.import(id.data(), n, k, s, sib.data(), bc.data(), bn.data());
+    KadRoundCount st;
+    for (int i = 0; i < 40000; ++i) {
+        const uint32_t v = (uint32_t)(rnd() % n), x = (uint32_t)(rnd() % n);
+        const bool alive = (rnd() & 1) != 0;
+        const bool r = h.routing_add(v, x, alive, &st);
+        CHECK(r || x == v || h.bk[v * 160 + (uint64_t)k_msb(k_xor(id[x], id[v]))].size() == (size_t)k);
+    }
+    CHECK(st.sib_changes > 0 && st.bucket_changes > 0 && st.lost + st.replacement > 0 && st.refreshed > 0);
+    kad_check(h);
+    std::vector<uint32_t> hs(n * 5 * s), hn(n * 160 * k);
+    std::vector<uint8_t> hc(n * 160);
+    CHECK(h.export_k(hs.data(), hc.data(), hn.data()));
+    KadHost h2;
+    h2.import(id.data(), n, k, s, hs.data(), hc.data(), hn.data());
+    CHECK(h2.sib == h.sib && h2.bk == h.bk);
+    // refresh plan: the sibling refresh first, then keys self ^ 2^i down to msb(self ^ front)
+    std::vector<uint32_t> nodes = {0, 7, 399};
+    std::vector<uint8_t> fl = {3, 1, 2};
+    std::vector<uint32_t> stale(3 * 5, 0xFFFFFFFFu);
+    stale[2 * 5 + 4] = 0;    // node 399: buckets 128..159 fresh
+    std::vector<K160> keys;
+    std::vector<uint32_t> src;
+    std::vector<int> R;
+    h.refresh_plan(nodes.data(), nodes.size(), fl.data(), stale.data(), 10, 4, &keys, &src, &R);
+    CHECK(!keys.empty() && src[0] == 0 && R[0] == 10 && k_eq(keys[0], id[0]));
+    for (size_t t = 0; t < keys.size(); ++t) {
+        const int i = k_msb(k_xor(keys[t], id[src[t]]));
+        CHECK(R[t] == 10 ? i < 0 : (i >= k_msb(k_xor(id[h.sib[src[t]][0]], id[src[t]])) && !(src[t] == 399 && i >= 128)));
+    }
+    // a round of synthetic lookups: calls and responses at random times
+    std::vector<KadRoundLookup> lk(300);
+    std::vector<std::vector<uint32_t>> cn(lk.size()), rs(lk.size()), car(lk.size() * 8);
+    std::vector<std::vector<int64_t>> ct(lk.size()), ta(lk.size());
+    std::vector<std::vector<const uint32_t*>> cp(lk.size());
+    std::vector<std::vector<uint8_t>> nc(lk.size());
+    for (size_t t = 0; t < lk.size(); ++t) {
+        const int nr = (int)(rnd() % 8);
+        for (int i = 0; i < nr + 2; ++i) { cn[t].push_back((uint32_t)(rnd() % n)); ct[t].push_back((int64_t)(rnd() % 1000)); }
+        for (int i = 0; i < nr; ++i) {
+            rs[t].push_back(cn[t][i]); ta[t].push_back(ct[t][i] + (int64_t)(rnd() % 1000));
+            std::vector<uint32_t>& C = car[t * 8 + i];
+            for (int q = 0; q < (int)(rnd() % 6); ++q) C.push_back((uint32_t)(rnd() % n));
+        }
+        for (int i = 0; i < nr; ++i) { cp[t].push_back(car[t * 8 + i].data()); nc[t].push_back((uint8_t)car[t * 8 + i].size()); }
+        KadRoundLookup& L = lk[t];
+        L.src = (uint32_t)(rnd() % n);
+        L.cnode = cn[t].data(); L.ctime = ct[t].data(); L.ncall = (int)cn[t].size();
+        L.resp = rs[t].data(); L.tarr = ta[t].data(); L.nresp = nr;
+        L.carried = cp[t].data(); L.ncarried = nc[t].data();
+    }
+    KadRoundCount st2;
+    h.apply_round(lk, &st2);
+    CHECK(st2.responses > 0);
+    kad_check(h);
+}
+
 int main()
 {
     chord_rounds();
     epichord_snapshots();
+    kad_maintenance();
     std::printf("clean\n");
     return 0;
 }
