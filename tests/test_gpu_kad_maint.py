@@ -115,5 +115,7 @@ def test_snapshot_is_a_fixed_point(engine):
     st = engine.kad_maintenance_round()
     assert st["changes"] == 0 and st["lookups"] > 10 * len(net.ids)
     after = engine.kad_tables()
-    assert np.array_equal(before[0], after[0])
+    # the snapshot build stores sibling tables in index order, the round's rebuild XOR-sorted
+    assert np.array_equal(np.sort(before[0], axis=1), np.sort(after[0], axis=1))
+    assert np.array_equal(before[1], after[1])
     assert all(np.array_equal(np.sort(a, axis=-1), np.sort(b, axis=-1)) for a, b in zip(before[2], after[2]))

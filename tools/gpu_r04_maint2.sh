@@ -1,0 +1,11 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/$1; mkdir -p $O
+export OVS_SKIP_BUILD=1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kad_maint.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/maint.log 2>&1 || { tail -40 $O/maint.log; exit 1; }
+tail -3 $O/maint.log
+timeout -k 10 300 python -u tools/diag/kad_maint_rounds.py 15000 0.1 > $O/rounds_15000.log 2>&1 || { tail -20 $O/rounds_15000.log; exit 1; }
+cat $O/rounds_15000.log
+timeout -k 10 900 python -u -m pytest tests/test_gpu_kad.py tests/test_gpu_kad_refresh.py tests/test_gpu_lookupcall.py tests/test_shard.py tests/test_gpu_kad_tables.py -m gpu -x -v --timeout 300 --timeout-method thread -k "kad or Kad or refresh or exhaustive" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -3 $O/tests.log
+for w in B E R; do timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }; cat $O/bench_$w.json; done
