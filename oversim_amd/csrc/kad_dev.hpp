@@ -852,8 +852,8 @@ __device__ __forceinline__ bool kad_lookup_done(const KadLookup<A, C>& L)
 // A findNode in the sibling zone reads the responder's 5s-entry sibling table (5 blocks at s = 8)
 // plus its own main bucket: one lane doing that alone serialises six block loads and sorts, and
 // one such lane in a wave made every wave iteration pay for it (42 % of K2's time on config E,
-// profiles/r03_dup).  The cooperative form gives each such findNode eight lanes, one block each,
-// and merges the sorted blocks in three butterfly steps.
+// profiles/r03_dup).  The cooperative form gives each such findNode four lanes (OVS_COOP_G), a block
+// each per pass, and merges the sorted blocks in two butterfly steps.
 
 enum : int { KEV_IDLE = 0, KEV_WAIT = 1, KEV_HANDLED = 2, KEV_FIND = 3, KEV_SENDS = 4 };
 

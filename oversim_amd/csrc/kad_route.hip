@@ -11,7 +11,7 @@
 // LookupVector, then the sends it triggers (one 64 B KadNode line per target: its key,
 // coordinates and isSiblingFor summary).  A findNode outside the sibling zone reads its main
 // bucket's 96 B block on its own lane; the sibling-zone findNodes of the wave's lanes are
-// evaluated together, eight lanes each (kad_coop_sibzone).  Finished lanes refill from the wave's
+// evaluated together, four lanes each (kad_coop_sibzone, OVS_COOP_G).  Finished lanes refill from the wave's
 // slice of the batch (ballot + popcount); the grid is persistent.
 //
 // Shard step (SHARD = true): the lookups of this rank (their sources lie on its arc) advance

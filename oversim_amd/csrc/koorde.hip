@@ -425,9 +425,15 @@ __device__ __forceinline__ uint64_t vis_bit(uint32_t x) { return 1ull << ((x * 0
 #ifndef OVS_KOORDE_WAVES
 #define OVS_KOORDE_WAVES 1
 #endif
-// KR: the record form (KoordeRec), else the list walks on recs[].  OVS_KOORDE_WAVES: minimum waves
-// per SIMD the record form's register allocation must allow
-template <bool KR>
+// the first KVL responders of a lookup whose hop sequence nobody asked for stay in LDS (the
+// visitOnlyOnce list, read only when the filter bit is set): one dword per hop written to HBM had
+// been 1.6 GB of scattered 32 B sectors per launch on config K, 17 % of its traffic
+constexpr int KVL = 16;
+
+// KR: the record form (KoordeRec), else the list walks on recs[].  RECORD: hopseq is the caller's
+// hop sequence (every responder written); otherwise it is scratch for responders past the first
+// KVL.  OVS_KOORDE_WAVES: minimum waves per SIMD the record form's register allocation must allow
+template <bool KR, bool RECORD>
 __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                       uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
@@ -445,6 +451,8 @@ __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route
     K160 K;
     __shared__ uint4 rcodes[4][256];            // the responder record's codes, per lane (record form)
     CodesLds RC{rcodes, (int)threadIdx.x};
+    __shared__ uint32_t vlist[RECORD ? 1 : KVL][256];   // the lane's first KVL responders (!RECORD)
+    const int tid = (int)threadIdx.x;
     uint32_t S = 0, cur = 0;
     double sx = 0, sy = 0;
     int64_t t = 0;
@@ -520,7 +528,10 @@ __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route
                 t += rtt;
                 if (t > DC.lookupTimeout) { fin = true; status = OVS_LOOKUP_TIMEOUT; }
                 else {
-                    if (hops < (int)H) seq[hops] = c;
+                    if (hops < (int)H) {
+                        if (RECORD || hops >= KVL) seq[hops] = c;
+                        else vlist[RECORD ? 0 : hops][tid] = c;
+                    }
                     ++hops;
                     vis |= vis_bit(c);
                     if (sib) { fin = true; R = c; }
@@ -530,7 +541,8 @@ __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route
                         // (the responder list is read only when the filter bit is set)
                         bool seen = nx == S;
                         if (!seen && (vis & vis_bit(nx)))
-                            for (int i = 0; i < hops && !seen; ++i) seen = seq[i] == nx;
+                            for (int i = 0; i < hops && !seen; ++i)
+                                seen = (RECORD || i >= KVL ? seq[i] : vlist[RECORD ? 0 : i][tid]) == nx;
                         if (seen) { fin = true; status = OVS_LOOKUP_NO_NEXT; }
                         else { cur = nx; e = e2; }
                     }
@@ -612,7 +624,12 @@ hipError_t koorde_build(const KeyRec* recs, const double2* xy, uint32_t n, int s
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     // the record form covers successor / de Bruijn lists of up to 16 nodes (the Koorde defaults)
-    if (t.ns <= KREC_LIST && deBruijnListSize <= KREC_LIST && !getenv("OVS_KOORDE_NOREC")) {
+#ifdef OVS_KOORDE_NOREC
+    const bool rec_form = false;      // diagnostic build: the list form only
+#else
+    const bool rec_form = true;
+#endif
+    if (rec_form && t.ns <= KREC_LIST && deBruijnListSize <= KREC_LIST) {
         e = hipMalloc(&t.rec, sizeof(KoordeRec) * n);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_koorde_rec, dim3(nblk(n, 256)), dim3(256), 0, st, recs, xy, t.nd, n, t.rec);
@@ -624,30 +641,33 @@ hipError_t koorde_build(const KeyRec* recs, const double2* xy, uint32_t n, int s
 
 hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2* xy, const DelayConsts& DC,
                         int hopCountMax, const K160* keys, const uint32_t* src, uint64_t nq, ovs_route_out* out,
-                        uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st)
+                        uint32_t* hopseq, bool record, uint32_t* rpcs, int num_cu, hipStream_t st)
 {
     if (nq == 0) return hipSuccess;
     if (!hopseq) return hipErrorInvalidValue;
-    static int bpc[2] = {0, 0};
+    static int bpc[4] = {0, 0, 0, 0};
     const int kr = t.rec ? 1 : 0;
-    if (bpc[kr] == 0) {
+    const int ki = kr + (record ? 2 : 0);
+#define KRT(a, b) k_koorde_route<a, b>
+    if (bpc[ki] == 0) {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kr ? k_koorde_route<true> : k_koorde_route<false>, 256, 0) !=
-                hipSuccess ||
-            b < 1)
-            b = 1;
-        bpc[kr] = b;
+        const hipError_t oe =
+            kr ? (record ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, KRT(true, true), 256, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, KRT(true, false), 256, 0))
+               : (record ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, KRT(false, true), 256, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, KRT(false, false), 256, 0));
+        bpc[ki] = (oe == hipSuccess && b > 0) ? b : 1;
     }
-    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc[kr] * 4;
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc[ki] * 4;
     uint64_t chunk = (nq + waves - 1) / waves;
     if (chunk < 1) chunk = 1;
     const uint64_t blocks = ((nq + chunk - 1) / chunk + 3) / 4;
-    if (kr)
-        hipLaunchKernelGGL(k_koorde_route<true>, dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC,
-                           hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs);
-    else
-        hipLaunchKernelGGL(k_koorde_route<false>, dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC,
-                           hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs);
+#define KRL(a, b) hipLaunchKernelGGL((KRT(a, b)), dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC, \
+                                     hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs)
+    if (kr) { if (record) KRL(true, true); else KRL(true, false); }
+    else { if (record) KRL(false, true); else KRL(false, false); }
+#undef KRL
+#undef KRT
     return hipGetLastError();
 }
 

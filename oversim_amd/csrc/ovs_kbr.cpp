@@ -233,6 +233,21 @@ ovs_status to_device(ovs_ctx* c, const T* src, uint64_t count, bool dev, T** out
     return OVS_OK;
 }
 
+// device buffers of one call, freed on every path (early returns included)
+struct DevBufs {
+    std::vector<void*> p;
+    template <class T>
+    hipError_t get(T** out, uint64_t count)
+    {
+        *out = nullptr;
+        const hipError_t e = hipMalloc(out, sizeof(T) * (count ? count : 1));
+        if (e == hipSuccess) p.push_back(*out);
+        return e;
+    }
+    void own(void* q, bool owned) { if (owned && q) p.push_back(q); }
+    ~DevBufs() { for (void* q : p) hipFree(q); }
+};
+
 ChordView chord_view(const ovs_ctx* c)
 {
     ChordView V{};
@@ -327,9 +342,10 @@ void ovs_ctx_destroy(ovs_ctx* c)
 {
     if (!c) return;
     hipSetDevice(c->device);
-    // the whole device: work on caller-supplied streams (c->stage keys) ends here too, without
-    // touching those handles, which the caller may already have destroyed
-    hipDeviceSynchronize();
+    // this context's own stream; work the caller queued on its streams (c->stage keys, which the
+    // caller may already have destroyed) is ordered before the frees below by hipFree itself, so
+    // destroy waits for no other context's or communicator's work
+    if (c->stream) hipStreamSynchronize(c->stream);
     free_tables(c);
     free_kad_shard(c);
     free_scratch(c);
@@ -1017,17 +1033,19 @@ ovs_status ovs_epichord_find_node_batch(ovs_ctx* c, const uint32_t* node, const 
     K160* dk = nullptr;
     int64_t *dnow = nullptr, *dlast = nullptr;
     uint8_t *dc = nullptr, *dst = nullptr;
-    bool o1, o2, o3, o4;
+    bool o1 = false, o2 = false, o3 = false, o4 = false;
+    DevBufs own;          // the temporaries of a host-buffer call, freed on every path
     ovs_status st = to_device(c, node, n, dev, &dn, &o1);
-    if (st == OVS_OK) st = to_device(c, reinterpret_cast<const K160*>(keys), n, dev, &dk, &o2);
-    if (st == OVS_OK) st = to_device(c, src, n, dev, &dsrc, &o3);
-    if (st == OVS_OK) st = to_device(c, now_ns, n, dev, &dnow, &o4);
+    own.own(dn, o1);
+    if (st == OVS_OK) { st = to_device(c, reinterpret_cast<const K160*>(keys), n, dev, &dk, &o2); own.own(dk, o2); }
+    if (st == OVS_OK) { st = to_device(c, src, n, dev, &dsrc, &o3); own.own(dsrc, o3); }
+    if (st == OVS_OK) { st = to_device(c, now_ns, n, dev, &dnow, &o4); own.own(dnow, o4); }
     if (st != OVS_OK) return st;
     if (!dev) {
-        HIPCHK(c, hipMalloc(&dout, sizeof(uint32_t) * n * max_out));
-        HIPCHK(c, hipMalloc(&dlast, sizeof(int64_t) * n * max_out));
-        HIPCHK(c, hipMalloc(&dc, n));
-        HIPCHK(c, hipMalloc(&dst, n));
+        HIPCHK(c, own.get(&dout, n * max_out));
+        HIPCHK(c, own.get(&dlast, n * max_out));
+        HIPCHK(c, own.get(&dc, n));
+        HIPCHK(c, own.get(&dst, n));
     } else {
         dout = out_nodes; dlast = out_last_ns; dc = out_count; dst = out_status;
     }
@@ -1041,7 +1059,6 @@ ovs_status ovs_epichord_find_node_batch(ovs_ctx* c, const uint32_t* node, const 
         HIPCHK(c, hipMemcpyAsync(out_count, dc, n, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(out_status, dst, n, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        hipFree(dn); hipFree(dk); hipFree(dsrc); hipFree(dnow); hipFree(dout); hipFree(dlast); hipFree(dc); hipFree(dst);
     }
     return OVS_OK;
 }
@@ -1134,8 +1151,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             else e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
         }
     } else if (c->overlay == OVS_OVERLAY_KOORDE) {
-        e = koorde_route(c->koorde, c->recs, c->xy, delay_consts(c->P), c->P.hopCountMax, dk, ds, n, dout, dhop, drpc,
-                         c->num_cu, s);
+        e = koorde_route(c->koorde, c->recs, c->xy, delay_consts(c->P), c->P.hopCountMax, dk, ds, n, dout, dhop,
+                         !koorde_scratch, drpc, c->num_cu, s);
     } else if (kad_exh) {
         // sendToKey with EXHAUSTIVE_ITERATIVE_ROUTING (BaseOverlay.cc:1434-1442): lookup(key, numSiblings = 1)
         // with redundantNodes = lookupRedundantNodes, the route message to getResult()[0]
@@ -1389,20 +1406,6 @@ ovs_status kad_upload_host_tables(ovs_ctx* c)
     if (e != hipSuccess) return hip_fail(c, e, "maintenance round: table rebuild");
     return OVS_OK;
 }
-
-// device buffers of a round, freed on every path
-struct DevBufs {
-    std::vector<void*> p;
-    template <class T>
-    hipError_t get(T** out, uint64_t count)
-    {
-        *out = nullptr;
-        const hipError_t e = hipMalloc(out, sizeof(T) * (count ? count : 1));
-        if (e == hipSuccess) p.push_back(*out);
-        return e;
-    }
-    ~DevBufs() { for (void* q : p) hipFree(q); }
-};
 
 }  // namespace
 }  // extern "C++"
