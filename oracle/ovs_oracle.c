@@ -240,6 +240,9 @@ static void params_common(orc_params* p)
     p->deBruijnListSize = 16;    /* default.ini:276 */
     p->useOtherLookup = 1;       /* default.ini:279 */
     p->useSucList = 1;           /* default.ini:280 */
+    p->bucketType = 0;           /* default.ini:209 "kademlia" */
+    p->globalNodeLimit = 1000;   /* default.ini:210 */
+    p->extraNodesFinalBucket = 0;/* default.ini:211 (0 = key length) */
 }
 void orc_params_chord_default(orc_params* p) { params_common(p); }
 void orc_params_koorde_default(orc_params* p)
@@ -288,10 +291,13 @@ struct orc_net {
     /* Kademlia */
     uint32_t* sib;          /* n * 5s, sorted by XOR to self */
     uint8_t* nsib;
-    uint32_t* bucket;       /* n * 160 * k (snapshot builds) */
-    uint8_t* bcount;        /* n * 160 */
+    int nb;                 /* numBuckets = (2^b - 1) * (160 / b) (Kademlia.cc:176) */
+    int bks;                /* snapshot builds: slots per bucket (the largest routingBucketSize) */
+    uint32_t* bucket;       /* n * nb * bks (snapshot builds) */
+    uint8_t* bcount;        /* n * nb */
+    uint32_t* rts;          /* explicit tables: currentRoutingTableSize per node (bucket entries) */
     /* explicit (mutable) tables: bucket (v, m) is a growable array in LRU order (KademliaBucket,
-     * push_back / erase in routingAdd), bdyn[v * 160 + m] with bdcnt entries of bdcap */
+     * push_back / erase in routingAdd), bdyn[v * nb + m] with bdcnt entries of bdcap */
     uint32_t** bdyn;
     uint16_t* bdcnt;
     uint16_t* bdcap;
@@ -307,8 +313,8 @@ void orc_net_free(orc_net* net)
     free(net->ids); free(net->xy); free(net->pred); free(net->succ); free(net->nsucc);
     free(net->fdeque); free(net->fsize); free(net->sib); free(net->nsib); free(net->bucket);
     free(net->bcount); free(net->kdb); free(net->kdbStart); free(net->kdbNum);
-    if (net->bdyn) for (size_t i = 0; i < (size_t)net->n * 160; ++i) free(net->bdyn[i]);
-    free(net->bdyn); free(net->bdcnt); free(net->bdcap);
+    if (net->bdyn) for (size_t i = 0; i < (size_t)net->n * (size_t)net->nb; ++i) free(net->bdyn[i]);
+    free(net->bdyn); free(net->bdcnt); free(net->bdcap); free(net->rts);
     free(net);
 }
 
@@ -668,6 +674,27 @@ static int chord_findNode(const orc_net* net, uint32_t self, const OKey* key,
 }
 
 /* ---- Kademlia (Kademlia.cc) -------------------------------------------------- */
+int orc_kad_num_buckets(const orc_params* p)                                  /* Kademlia.cc:176 */
+{
+    return (int)(((1L << p->b) - 1L) * (160 / p->b));
+}
+
+int orc_kad_bucket_size(const orc_params* p, int index)                       /* 384-411 */
+{
+    if (p->bucketType == 1) return 0;                     /* NKADEMLIA: no maximum per bucket */
+    if (p->bucketType == 2) {                             /* NR128: the final buckets hold more */
+        const int extra = p->extraNodesFinalBucket == 0 ? 160 : p->extraNodesFinalBucket;   /* 146-148 */
+        const int limit = (int)(log((double)extra) / log(2.0));
+        int offset = limit - (160 - (index + 1));
+        if (offset > 0) {
+            offset = (int)pow(2, offset);
+            if (offset > p->k) return offset;
+        }
+        return p->k;
+    }
+    return p->k;
+}
+
 static int kad_routingBucketIndex(const orc_net* net, uint32_t self, const OKey* key, int firstOnLayer) /* 357-382 */
 {
     int b = net->p.b;
@@ -696,20 +723,26 @@ static uint64_t kad_hash(uint64_t seed, uint32_t node, uint32_t m, uint32_t j)
     return splitmix64(seed ^ splitmix64(((uint64_t)node << 32) ^ ((uint64_t)m << 16) ^ (uint64_t)j));
 }
 /* The tables of one node under the snapshot rule: sib[] (its sibling table, XOR-sorted to
- * self), *nsib, and per bucket m the members bk[m*k ..] (bc[m] of them). */
+ * self), *nsib, and per bucket index m (0 .. nb-1) the members bk[m*bks ..] (bc[m] of them): up to
+ * routingBucketSize(m) of the bucket's subtree minus the siblings.  For b > 1 bucket
+ * (layer L, digit d) holds the ids that share self's bits above the digit at bit i = L*b + 160 % b
+ * and whose digit there is self's ^ d (routingBucketIndex, Kademlia.cc:357-382). */
 static void kad_node_build(const orc_net* net, uint32_t self, uint32_t* sibOut, int* nsibOut, uint8_t* bc,
                            uint32_t* bk)
 {
     const orc_params* p = &net->p;
-    int k = p->k, sibCap = 5 * p->s;
+    int sibCap = 5 * p->s;
+    const int B = p->b, per = (1 << B) - 1, bks = net->bks;
     /* sibling table: walk subtrees m = 0.. upward, gather members, keep 5s closest */
     /* T_m = [tlo[m], thi[m]): the ids sharing the bits above m with self and differing at bit m
      * (subtree_range(self, m)), found by one descent over the sorted ids: the ids sharing the
      * bits above m form one block, split at its first id with bit m set */
     uint32_t tlo[160], thi[160];
+    uint32_t slo[161], shi[161];     /* S[b'] = the ids sharing bits b' .. 159 with self */
     {
         const OKey* me = &net->ids[self];
         uint32_t lo = 0, hi = net->n;
+        slo[160] = lo; shi[160] = hi;
         for (int b = 159; b >= 0; --b) {
             uint32_t a = lo, z = hi;
             while (a < z) {
@@ -718,6 +751,7 @@ static void kad_node_build(const orc_net* net, uint32_t self, uint32_t* sibOut, 
             }
             if ((me->key[b / 64] >> (b % 64)) & 1) { tlo[b] = lo; thi[b] = a; lo = a; }
             else { tlo[b] = a; thi[b] = hi; hi = a; }
+            slo[b] = lo; shi[b] = hi;
         }
     }
     NVec sib; nv_init(&sib, sibCap, 1, &net->ids[self]);
@@ -729,17 +763,36 @@ static void kad_node_build(const orc_net* net, uint32_t self, uint32_t* sibOut, 
     *nsibOut = sib.size;
     for (int i = 0; i < sibCap; ++i) sibOut[i] = i < sib.size ? sib.v[i] : NONE;
     /* buckets */
-    for (m = 0; m < 160; ++m) {
+    for (m = 0; m < net->nb; ++m) {
         bc[m] = 0;
-        uint32_t lo = tlo[m], hi = thi[m];
+        uint32_t lo, hi;
+        if (B == 1) { lo = tlo[m]; hi = thi[m]; }
+        else {
+            /* index m = layer L * (2^b - 1) + digit d - 1; the digit sits at bits i .. i+b-1 */
+            const int L = m / per, d = m % per + 1, i = L * B + 160 % B;
+            const uint32_t want = ok_getBitRange(&net->ids[self], (uint32_t)i, (uint32_t)B) ^ (uint32_t)d;
+            uint32_t a = slo[i + B], z = shi[i + B];
+            while (a < z) {               /* first id of the block whose digit >= want */
+                uint32_t mid = a + (z - a) / 2;
+                if (ok_getBitRange(&net->ids[mid], (uint32_t)i, (uint32_t)B) < want) a = mid + 1; else z = mid;
+            }
+            lo = a; z = shi[i + B];
+            while (a < z) {               /* ... and > want */
+                uint32_t mid = a + (z - a) / 2;
+                if (ok_getBitRange(&net->ids[mid], (uint32_t)i, (uint32_t)B) <= want) a = mid + 1; else z = mid;
+            }
+            hi = a;
+        }
         if (hi <= lo) continue;
+        const int k = orc_kad_bucket_size(p, m);
+        if (k <= 0 || k > bks) { cap_error("snapshot tables need a bounded bucketType (kademlia / nr128)"); return; }
         /* members not in the sibling table, in ascending id order */
         uint32_t cnt = hi - lo;
         uint32_t nsib_in = 0;
         for (int s2 = 0; s2 < sib.size; ++s2) if (sib.v[s2] >= lo && sib.v[s2] < hi) nsib_in++;
         uint32_t c = cnt - nsib_in;
-        uint32_t* dst = bk + (size_t)m * k;
-        uint32_t chosen[64]; int nch = 0;
+        uint32_t* dst = bk + (size_t)m * bks;
+        uint32_t chosen[256]; int nch = 0;
         if (c <= (uint32_t)k) {
             for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
         } else {
@@ -773,13 +826,14 @@ static void kad_node_build(const orc_net* net, uint32_t self, uint32_t* sibOut, 
 /* explicit tables: growable bucket arrays */
 static void kad_dyn_alloc(orc_net* net)
 {
-    net->bdyn = (uint32_t**)calloc((size_t)net->n * 160, sizeof(uint32_t*));
-    net->bdcnt = (uint16_t*)calloc((size_t)net->n * 160, sizeof(uint16_t));
-    net->bdcap = (uint16_t*)calloc((size_t)net->n * 160, sizeof(uint16_t));
+    net->bdyn = (uint32_t**)calloc((size_t)net->n * (size_t)net->nb, sizeof(uint32_t*));
+    net->bdcnt = (uint16_t*)calloc((size_t)net->n * (size_t)net->nb, sizeof(uint16_t));
+    net->bdcap = (uint16_t*)calloc((size_t)net->n * (size_t)net->nb, sizeof(uint16_t));
+    net->rts = (uint32_t*)calloc((size_t)net->n, sizeof(uint32_t));
 }
 static void kad_dyn_push(orc_net* net, uint32_t v, int m, uint32_t x)       /* KademliaBucket::push_back */
 {
-    const size_t i = (size_t)v * 160 + (size_t)m;
+    const size_t i = (size_t)v * (size_t)net->nb + (size_t)m;
     if (net->bdcnt[i] == net->bdcap[i]) {
         if (net->bdcap[i] >= 32768) { cap_error("bucket over 32768 entries"); return; }
         net->bdcap[i] = (uint16_t)(net->bdcap[i] ? 2 * net->bdcap[i] : 8);
@@ -789,7 +843,7 @@ static void kad_dyn_push(orc_net* net, uint32_t v, int m, uint32_t x)       /* K
 }
 static void kad_dyn_erase(orc_net* net, uint32_t v, int m, int pos)        /* bucket->erase(i) */
 {
-    const size_t i = (size_t)v * 160 + (size_t)m;
+    const size_t i = (size_t)v * (size_t)net->nb + (size_t)m;
     memmove(&net->bdyn[i][pos], &net->bdyn[i][pos + 1], sizeof(uint32_t) * (size_t)(net->bdcnt[i] - pos - 1));
     net->bdcnt[i]--;
 }
@@ -799,7 +853,7 @@ static void kad_dyn_erase(orc_net* net, uint32_t v, int m, int pos)        /* bu
  * lookup are at the same node, so a small direct-mapped cache suffices. */
 typedef struct {
     const uint32_t* sib; int nsib;
-    const uint8_t* bc; const uint32_t* bk; int k;      /* snapshot layout: bucket m = bk[m*k ..], bc[m] */
+    const uint8_t* bc; const uint32_t* bk; int k;      /* snapshot layout: bucket m = bk[m*k ..], bc[m] (k = bks) */
     uint32_t* const* bd; const uint16_t* bdc;           /* explicit tables: bucket m = bd[m][0 .. bdc[m]) */
 } KadTab;
 static inline int kt_count(const KadTab* T, int m) { return T->bd ? (int)T->bdc[m] : (int)T->bc[m]; }
@@ -823,17 +877,17 @@ static KadTab kad_tab(const orc_net* net, uint32_t self)
 {
     KadTab t;
     memset(&t, 0, sizeof t);
-    t.k = net->p.k;
+    t.k = net->bks;
     if (!net->lazy) {
         size_t sibCap = (size_t)5 * net->p.s;
         t.sib = net->sib + (size_t)self * sibCap;
         t.nsib = net->nsib[self];
         if (net->bdyn) {
-            t.bd = net->bdyn + (size_t)self * 160;
-            t.bdc = net->bdcnt + (size_t)self * 160;
+            t.bd = net->bdyn + (size_t)self * (size_t)net->nb;
+            t.bdc = net->bdcnt + (size_t)self * (size_t)net->nb;
         } else {
-            t.bc = net->bcount + (size_t)self * 160;
-            t.bk = net->bucket + (size_t)self * 160 * net->p.k;
+            t.bc = net->bcount + (size_t)self * (size_t)net->nb;
+            t.bk = net->bucket + (size_t)self * (size_t)net->nb * (size_t)net->bks;
         }
         return t;
     }
@@ -903,34 +957,67 @@ static int kad_findNode(const orc_net* net, uint32_t self, const OKey* key,
         for (int i = 0; i < nsib; ++i) nv_add(net, result, sib[i]);
         nv_add(net, result, self);
     }
-    for (int index = mainIndex + 1; !nv_isFull(result) && index < 160; ++index) {
+    for (int index = mainIndex + 1; !nv_isFull(result) && index < net->nb; ++index) {
         const uint32_t* bk = kt_members(&T, index);
         for (int i = 0; i < kt_count(&T, index); ++i) nv_add(net, result, bk[i]);
     }
     return 0;
 }
 
+/* Kademlia parameters the restatement covers: b = 1..5 (numBuckets <= 992), the three bucketTypes */
+static int kad_check(const orc_params* p)
+{
+    if (p->b < 1 || p->b > 5) { set_err("kademlia: b must be 1..5"); return 0; }
+    if (p->bucketType < 0 || p->bucketType > 2) { set_err("kademlia: bucketType must be 0..2"); return 0; }
+    if (p->bucketType == 1 && p->globalNodeLimit < 0) { set_err("kademlia: globalNodeLimit < 0"); return 0; }
+    /* routingBucketSize (384-411) counts indices as if b = 1 (offset = limit - (160 - (index + 1))):
+     * for b > 1 the indices 160 .. numBuckets-1 get sizes 2^8 .. 2^30 and then (int)pow(2, >= 31),
+     * undefined behaviour -- not a configuration the restatement follows */
+    if (p->bucketType == 2 && p->b != 1) { set_err("kademlia: nr128 buckets need b = 1"); return 0; }
+    if (p->bucketType == 2 && (p->extraNodesFinalBucket < 0 || p->extraNodesFinalBucket > 511)) {
+        set_err("kademlia: extraNodesFinalBucket must be 0..511"); return 0;
+    }
+    return check_params(p);
+}
+static void kad_net_init(orc_net* net)
+{
+    net->nb = orc_kad_num_buckets(&net->p);
+    int mx = 0;
+    for (int m = 0; m < net->nb; ++m) {
+        const int c = orc_kad_bucket_size(&net->p, m);
+        mx = c > mx ? c : mx;
+    }
+    net->bks = mx;        /* 0: unbounded buckets (nkademlia) -- explicit tables only */
+}
+
 static orc_net* kad_build(const orc_key* ids, uint32_t n, const double* xy, const orc_params* p, int lazy)
 {
-    if (p->b != 1) { set_err("kademlia: only b=1 supported"); return NULL; }
-    if (!check_params(p)) return NULL;
+    if (!kad_check(p)) return NULL;
+    if (p->bucketType == 1) { set_err("kademlia: nkademlia tables are order-dependent: explicit tables only"); return NULL; }
     orc_net* net = net_alloc(NET_KAD, ids, n, xy, p);
     if (!net) return NULL;
-    if (lazy) { net->lazy = 1; return net; }
-    int k = p->k, sibCap = 5 * p->s;
+    kad_net_init(net);
+    if (lazy) {
+        if (net->nb != 160 || net->bks > 64) { set_err("lazy kademlia tables: b = 1, buckets of <= 64"); orc_net_free(net); return NULL; }
+        net->lazy = 1;
+        return net;
+    }
+    const int sibCap = 5 * p->s;
+    const size_t nb = (size_t)net->nb, bks = (size_t)net->bks;
     net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
     net->nsib = (uint8_t*)calloc(n, 1);
-    net->bucket = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * 160 * k);
-    net->bcount = (uint8_t*)calloc((size_t)n * 160, 1);
+    net->bucket = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * nb * bks);
+    net->bcount = (uint8_t*)calloc((size_t)n * nb, 1);
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 64)
 #endif
     for (int64_t self = 0; self < (int64_t)n; ++self) {
         int ns = 0;
-        kad_node_build(net, (uint32_t)self, net->sib + (size_t)self * sibCap, &ns, net->bcount + (size_t)self * 160,
-                       net->bucket + (size_t)self * 160 * k);
+        kad_node_build(net, (uint32_t)self, net->sib + (size_t)self * sibCap, &ns, net->bcount + (size_t)self * nb,
+                       net->bucket + (size_t)self * nb * bks);
         net->nsib[self] = (uint8_t)ns;
     }
+    if (g_cap_fail) { orc_net_free(net); return NULL; }
     return net;
 }
 
@@ -950,10 +1037,11 @@ orc_net* orc_kad_build_lazy(const orc_key* ids, uint32_t n, const double* xy, co
 orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, const uint32_t* siblings,
                               const uint8_t* bucket_count, const uint32_t* bucket_nodes, const orc_params* p)
 {
-    if (p->b != 1) { set_err("kademlia: only b=1 supported"); return NULL; }
-    if (!check_params(p)) return NULL;
+    if (p->b != 1) { set_err("kademlia: k-stride tables are b = 1 (orc_kad_build_tables_csr for b > 1)"); return NULL; }
+    if (!kad_check(p)) return NULL;
     orc_net* net = net_alloc(NET_KAD, ids, n, xy, p);
     if (!net) return NULL;
+    kad_net_init(net);
     int k = p->k, sibCap = 5 * p->s;
     net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
     net->nsib = (uint8_t*)calloc(n, 1);
@@ -975,6 +1063,44 @@ orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, 
                 uint32_t x = bucket_nodes[((size_t)v * 160 + m) * k + q];
                 if (x >= n) { set_err("bucket member index out of range"); orc_net_free(net); return NULL; }
                 kad_dyn_push(net, v, m, x);
+                net->rts[v]++;
+            }
+        }
+    }
+    return net;
+}
+
+orc_net* orc_kad_build_tables_csr(const orc_key* ids, uint32_t n, const double* xy, const uint32_t* siblings,
+                                  const uint64_t* bucket_off, const uint32_t* bucket_nodes, const orc_params* p)
+{
+    if (!kad_check(p)) return NULL;
+    orc_net* net = net_alloc(NET_KAD, ids, n, xy, p);
+    if (!net) return NULL;
+    kad_net_init(net);
+    const int sibCap = 5 * p->s, nb = net->nb;
+    net->sib = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sibCap);
+    net->nsib = (uint8_t*)calloc(n, 1);
+    kad_dyn_alloc(net);
+    for (uint32_t v = 0; v < n; ++v) {
+        NVec sib; nv_init(&sib, sibCap, 1, &net->ids[v]);
+        for (int i = 0; i < sibCap; ++i) {
+            uint32_t x = siblings[(size_t)v * sibCap + i];
+            if (x == NONE) continue;
+            if (x >= n) { set_err("sibling index out of range"); orc_net_free(net); return NULL; }
+            nv_add(net, &sib, x);
+        }
+        net->nsib[v] = (uint8_t)sib.size;
+        for (int i = 0; i < sibCap; ++i) net->sib[(size_t)v * sibCap + i] = i < sib.size ? sib.v[i] : NONE;
+        for (int m = 0; m < nb; ++m) {
+            const size_t bi = (size_t)v * nb + (size_t)m;
+            const int cap = orc_kad_bucket_size(p, m);
+            if (cap && bucket_off[bi + 1] - bucket_off[bi] > (uint64_t)cap) {
+                set_err("a bucket holds more than routingBucketSize entries"); orc_net_free(net); return NULL;
+            }
+            for (uint64_t q = bucket_off[bi]; q < bucket_off[bi + 1]; ++q) {
+                if (bucket_nodes[q] >= n) { set_err("bucket member index out of range"); orc_net_free(net); return NULL; }
+                kad_dyn_push(net, v, m, bucket_nodes[q]);
+                net->rts[v]++;
             }
         }
     }
@@ -984,6 +1110,7 @@ orc_net* orc_kad_build_tables(const orc_key* ids, uint32_t n, const double* xy, 
 void orc_kad_export(const orc_net* net, uint32_t* siblings, uint8_t* bucket_count, uint32_t* bucket_nodes)
 {
     size_t sc = (size_t)5 * net->p.s, k = (size_t)net->p.k;
+    if (net->nb != 160) { cap_error("orc_kad_export: b > 1 (use orc_kad_export_csr)"); return; }
     for (uint32_t v = 0; v < net->n; ++v) {
         KadTab T = kad_tab(net, v);
         for (size_t i = 0; i < sc; ++i) siblings[(size_t)v * sc + i] = (int)i < T.nsib ? T.sib[i] : NONE;
@@ -1930,25 +2057,37 @@ uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_
         const uint32_t v = nodes[j];
         KadTab T = kad_tab(net, v);
         if (T.nsib == 0) continue;                       /* if (siblingTable->size()) (1632) */
-        /* siblingTable->front(): the XOR-closest sibling */
-        OKey best = ok_xor(net->ids[v], &net->ids[T.sib[0]]);
-        for (int q = 1; q < T.nsib; ++q) {
-            OKey d = ok_xor(net->ids[v], &net->ids[T.sib[q]]);
-            if (ok_cmp(&d, &best) < 0) best = d;
-        }
-        /* diff = L - b*(sharedPrefixLength(front, b) + 1) = msb(self ^ front) for b = 1 (1636-1637) */
-        const int spl = 159 - ok_log2(&best);
-        const int diff = 160 - (spl + 1);
-        for (int i = 159; i >= diff; --i) {             /* index = i for b = 1 (1639-1642) */
-            if (stale && !((stale[j * 5 + (uint64_t)(i >> 5)] >> (i & 31)) & 1u)) continue;
-            if (cnt < cap) {
-                OKey key = net->ids[v];                  /* thisNode.key ^ (OverlayKey(1) << i) (1647-1648) */
-                OKey bit = ok_pow2((uint32_t)i);
-                key = ok_xor(key, &bit);
-                ok_to(&key, &keys[cnt]);
-                src[cnt] = v;
+        /* diff = L - b*(sharedPrefixLength(front, b) + 1) (1636-1637) */
+        const int B = net->p.b, per = (1 << B) - 1;
+        orc_key me, fr;
+        ok_to(&net->ids[v], &me);
+        {
+            /* the front: the XOR-closest sibling */
+            uint32_t f = T.sib[0];
+            for (int q = 1; q < T.nsib; ++q) {
+                OKey d1 = ok_xor(net->ids[v], &net->ids[T.sib[q]]), d0 = ok_xor(net->ids[v], &net->ids[f]);
+                if (ok_cmp(&d1, &d0) < 0) f = T.sib[q];
             }
-            ++cnt;
+            ok_to(&net->ids[f], &fr);
+        }
+        const int spl = (int)orc_key_shared_prefix(&me, &fr, (uint32_t)B);
+        const int diff = 160 - B * (spl + 1);
+        const uint64_t sw = ((uint64_t)net->nb + 31) / 32;      /* stale mask words per node */
+        for (int i = 160 - B; i >= diff; i -= B) {               /* 1639-1676 */
+            for (int d = 0; d < per; ++d) {
+                const int index = (i / B) * per + d;
+                if (index < 0) continue;
+                if (stale && !((stale[j * sw + (uint64_t)(index >> 5)] >> (index & 31)) & 1u)) continue;
+                if (cnt < cap) {
+                    /* thisNode.key ^ (OverlayKey(d + 1) << i) (1647-1648) */
+                    OKey key = net->ids[v];
+                    for (int bit = 0; bit < B; ++bit)
+                        if (((d + 1) >> bit) & 1) { OKey pw = ok_pow2((uint32_t)(i + bit)); key = ok_xor(key, &pw); }
+                    ok_to(&key, &keys[cnt]);
+                    src[cnt] = v;
+                }
+                ++cnt;
+            }
         }
     }
     return cnt;
@@ -1959,8 +2098,8 @@ uint64_t orc_kad_refresh_keys(const orc_net* net, const uint32_t* nodes, uint64_
 /* ======================================================================== */
 /* Kademlia::routingAdd (Kademlia.cc:432-756) on explicit tables, with the default
  * secureMaintenance = false, pingNewSiblings = false, activePing = false and
- * proximityNeighborSelection = false (default.ini:191, 201, 219-221), bucketType "kademlia"
- * (routingBucketSize = k, 384-411).  The replacement cache (729-745) and its pings never change
+ * proximityNeighborSelection = false (default.ini:191, 201, 219-221), any bucketType
+ * (routingBucketSize, 384-411; the nkademlia branch 620-664 with currentRoutingTableSize).  The replacement cache (729-745) and its pings never change
  * a table's membership without RPC timeouts, so a rejected add is only counted.  rtt / lastSeen
  * are not modelled (nothing in routing reads them).  Returns routingAdd's result. */
 static int kad_routingAdd(orc_net* net, uint32_t self, uint32_t h, int isAlive, orc_kad_round_stats* st)
@@ -1972,8 +2111,8 @@ static int kad_routingAdd(orc_net* net, uint32_t self, uint32_t h, int isAlive, 
     for (int i = 0; i < nsib; ++i)                                    /* already a sibling: 454-481 */
         if (sib[i] == h) { if (isAlive) st->refreshed++; return 1; }
     const int bi = kad_routingBucketIndex(net, self, &net->ids[h], 0);
-    {
-        const size_t bx = (size_t)self * 160 + (size_t)bi;
+    if (bi >= 0) {                                                    /* routingBucket(key, false) */
+        const size_t bx = (size_t)self * (size_t)net->nb + (size_t)bi;
         for (int i = 0; i < net->bdcnt[bx]; ++i)                      /* already in a bucket: 483-535 */
             if (net->bdyn[bx][i] == h) {
                 if (isAlive) {                                        /* erase + push_back (514-517) */
@@ -2007,9 +2146,23 @@ static int kad_routingAdd(orc_net* net, uint32_t self, uint32_t h, int isAlive, 
         net->nsib[self] = (uint8_t)sv.size;
     }
     const int b2 = kad_routingBucketIndex(net, self, &net->ids[cur], 0);   /* routingBucket(.., true) 619 */
-    const size_t bx2 = (size_t)self * 160 + (size_t)b2;
-    if (net->bdcnt[bx2] < net->p.k) {                                 /* !bucket->isFull() 665-701 */
+    if (b2 < 0) { cap_error("routingAdd: bucket index -1 (the reference dereferences a NULL bucket)"); return result; }
+    const size_t bx2 = (size_t)self * (size_t)net->nb + (size_t)b2;
+    if (net->p.bucketType == 1) {                                     /* NKADEMLIA (620-664) */
+        if (net->bdcnt[bx2] >= net->p.k && (int64_t)net->rts[self] >= (int64_t)net->p.globalNodeLimit) {
+            if (cur != h) st->lost++;
+            else if (isAlive) st->replacement++;
+            return 0;
+        }
         kad_dyn_push(net, self, b2, cur);
+        net->rts[self]++;
+        st->bucket_changes++;
+        return 1;
+    }
+    const int cap = orc_kad_bucket_size(&net->p, b2);
+    if (net->bdcnt[bx2] < cap) {                                      /* !bucket->isFull() 665-701 */
+        kad_dyn_push(net, self, b2, cur);
+        net->rts[self]++;
         st->bucket_changes++;
         return 1;
     }
@@ -2061,7 +2214,7 @@ uint64_t orc_kad_maintenance_round(orc_net* net, const uint32_t* nodes, uint64_t
      * refreshes of the stale buckets with bucketRefreshNodes = lookupRedundantNodes (1631-1676) */
     const int Rs = 5 * net->p.s, Rb = net->p.lookupRedundantNodes;
     uint64_t cap = 0;
-    for (uint64_t j = 0; j < m; ++j) cap += 1 + 160;
+    for (uint64_t j = 0; j < m; ++j) cap += 1 + (uint64_t)net->nb;
     orc_key* keys = (orc_key*)malloc(sizeof(orc_key) * cap);
     uint32_t* src = (uint32_t*)malloc(sizeof(uint32_t) * cap);
     int* tR = (int*)malloc(sizeof(int) * cap);
@@ -2072,7 +2225,9 @@ uint64_t orc_kad_maintenance_round(orc_net* net, const uint32_t* nodes, uint64_t
         const uint8_t f = flags ? flags[j] : 3;
         if (f & 1) { ok_to(&net->ids[v], &keys[nt]); src[nt] = v; tR[nt] = Rs; ++nt; }
         if (f & 2) {
-            const uint64_t c = orc_kad_refresh_keys(net, &v, 1, stale ? stale + j * 5 : NULL, keys + nt, src + nt, 160);
+            const uint64_t sw = ((uint64_t)net->nb + 31) / 32;
+            const uint64_t c = orc_kad_refresh_keys(net, &v, 1, stale ? stale + j * sw : NULL, keys + nt, src + nt,
+                                                    (uint64_t)net->nb);
             for (uint64_t q = 0; q < c; ++q) tR[nt + q] = Rb;
             nt += c;
         }
@@ -2204,15 +2359,15 @@ void orc_kad_export_csr(const orc_net* net, uint32_t* siblings, uint64_t* bucket
     for (uint32_t v = 0; v < net->n; ++v) {
         KadTab T = kad_tab(net, v);
         if (siblings) for (size_t i = 0; i < sc; ++i) siblings[(size_t)v * sc + i] = (int)i < T.nsib ? T.sib[i] : NONE;
-        for (int mm = 0; mm < 160; ++mm) {
-            bucket_off[(size_t)v * 160 + mm] = o;
+        for (int mm = 0; mm < net->nb; ++mm) {
+            bucket_off[(size_t)v * (size_t)net->nb + mm] = o;
             const int c = kt_count(&T, mm);
             const uint32_t* bk = kt_members(&T, mm);
             if (bucket_nodes) for (int j = 0; j < c; ++j) bucket_nodes[o + j] = bk[j];
             o += (uint64_t)c;
         }
     }
-    bucket_off[(size_t)net->n * 160] = o;
+    bucket_off[(size_t)net->n * (size_t)net->nb] = o;
 }
 
 /* ======================================================================== */

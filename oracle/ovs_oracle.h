@@ -75,6 +75,13 @@ typedef struct {
     int32_t deBruijnListSize;         /* = 16 */
     int32_t useOtherLookup;           /* = true */
     int32_t useSucList;               /* = true */
+    /* the fork's Kademlia bucket variants (Kademlia.cc:135-151, 384-411; default.ini:209-211):
+     * bucketType 0 "kademlia" (k per bucket), 1 "nkademlia" (buckets unbounded while the table
+     * holds fewer than globalNodeLimit entries), 2 "nr128" (the top buckets hold up to 2^offset,
+     * offset from extraNodesFinalBucket, 0 = keyLength) */
+    int32_t bucketType;
+    int32_t globalNodeLimit;          /* = 1000 */
+    int32_t extraNodesFinalBucket;    /* = 0 */
 } orc_params;
 
 void orc_params_chord_default(orc_params* p);
@@ -212,9 +219,16 @@ uint64_t orc_kad_maintenance_round(orc_net* net, const uint32_t* nodes, uint64_t
 /* Kademlia::routingAdd(x, isAlive) at node v on explicit tables (the rules the round applies);
  * returns its result, -1 on error */
 int orc_kad_routing_add(orc_net* net, uint32_t v, uint32_t x, int isAlive);
-/* explicit / snapshot tables in CSR form: siblings[n*5s] (NONE padded), bucket_off[n*160+1],
- * bucket_nodes[bucket_off[n*160]] (each bucket in LRU order); bucket_nodes NULL = size query */
+/* explicit / snapshot tables in CSR form: siblings[n*5s] (NONE padded), bucket_off[n*NB+1],
+ * bucket_nodes[bucket_off[n*NB]] (each bucket in LRU order); NB = numBuckets = (2^b - 1) * (160 / b)
+ * (Kademlia.cc:176); bucket_nodes NULL = size query */
 void orc_kad_export_csr(const orc_net* net, uint32_t* siblings, uint64_t* bucket_off, uint32_t* bucket_nodes);
+/* explicit tables of any b and bucket sizes in that CSR form (buckets in LRU order) */
+orc_net* orc_kad_build_tables_csr(const orc_key* ids, uint32_t n, const double* xy, const uint32_t* siblings,
+                                  const uint64_t* bucket_off, const uint32_t* bucket_nodes, const orc_params* p);
+/* Kademlia::routingBucketSize(index) (Kademlia.cc:384-411): 0 = unbounded */
+int orc_kad_bucket_size(const orc_params* p, int index);
+int orc_kad_num_buckets(const orc_params* p);
 
 /* One synchronous stabilize round for nodes[0..m) on explicit tables (Chord.cc:793-842, 1055-1225,
  * ChordSuccessorList.cc:101-194): returns the number of successor lists that changed (ORC_FAIL on

@@ -36,6 +36,7 @@ class OrcParams(C.Structure):
         ("routingType", C.c_int32), ("recNumRedundantNodes", C.c_int32),
         ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
         ("useSucList", C.c_int32),
+        ("bucketType", C.c_int32), ("globalNodeLimit", C.c_int32), ("extraNodesFinalBucket", C.c_int32),
     ]
 
     def replace(self, **kw) -> "OrcParams":
@@ -101,6 +102,9 @@ def lib() -> C.CDLL:
             ("orc_kad_maintenance_round", [vp, vp, u64, vp, vp, vp, C.c_int], u64),
             ("orc_kad_export_csr", [vp, vp, vp, vp], None),
             ("orc_kad_routing_add", [vp, u32, u32, C.c_int], C.c_int),
+            ("orc_kad_build_tables_csr", [vp, u32, vp, vp, vp, vp, vp], vp),
+            ("orc_kad_bucket_size", [vp, C.c_int], C.c_int),
+            ("orc_kad_num_buckets", [vp], C.c_int),
             ("orc_epichord_find_node", [vp, u32, u32, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp,
                                         C.c_int, vp, u32, C.c_int64, C.c_int64, C.c_int, vp, vp, C.c_int], C.c_int),
             ("orc_kbrtest_lookup_stats", [vp, vp, vp, C.c_int, vp, vp, u64, C.c_double, C.c_int, C.c_double, vp],
@@ -196,6 +200,14 @@ class OracleNet:
             if tables is None:
                 build = L.orc_kad_build_lazy if lazy else L.orc_kad_build
                 h = build(_p(self.ids), n, _p(self.xy), C.byref(self.params))
+            elif "bucket_off" in tables:       # CSR tables: any b, any bucket size
+                t = {k: np.ascontiguousarray(v) for k, v in tables.items()}
+                t["siblings"] = t["siblings"].astype(np.uint32)
+                t["bucket_off"] = t["bucket_off"].astype(np.uint64)
+                t["bucket_nodes"] = np.ascontiguousarray(t["bucket_nodes"].astype(np.uint32))
+                self._keep = t
+                h = L.orc_kad_build_tables_csr(_p(self.ids), n, _p(self.xy), _p(t["siblings"]), _p(t["bucket_off"]),
+                                               _p(t["bucket_nodes"]), C.byref(self.params))
             else:
                 t = {k: np.ascontiguousarray(v) for k, v in tables.items()}
                 self._keep = t
@@ -312,10 +324,14 @@ class OracleNet:
             raise RuntimeError(lib().orc_last_error().decode())
         return r
 
+    def num_buckets(self) -> int:
+        return int(lib().orc_kad_num_buckets(C.byref(self.params)))
+
     def kad_tables_csr(self):
-        """(siblings[n, 5s], bucket_off[n*160+1], bucket_nodes) -- buckets of any size, LRU order."""
+        """(siblings[n, 5s], bucket_off[n*NB+1], bucket_nodes) -- buckets of any size, LRU order;
+        NB = numBuckets = (2^b - 1) * (160 / b)."""
         sib = np.empty((self.n, 5 * self.params.s), dtype=np.uint32)
-        off = np.empty(self.n * 160 + 1, dtype=np.uint64)
+        off = np.empty(self.n * self.num_buckets() + 1, dtype=np.uint64)
         lib().orc_kad_export_csr(self._h, _p(sib), _p(off), None)
         nodes = np.empty(max(int(off[-1]), 1), dtype=np.uint32)
         lib().orc_kad_export_csr(self._h, _p(sib), _p(off), _p(nodes))

@@ -361,11 +361,44 @@ class KoordeRing:
             cur = nxt
 
 
+def kad_num_buckets(b: int) -> int:
+    """numBuckets = ((2^b) - 1) * (keylength / b) (Kademlia.cc:176)."""
+    return ((1 << b) - 1) * (160 // b)
+
+
+def kad_bucket_index(delta: int, b: int, first_on_layer: bool = False) -> int:
+    """Kademlia::routingBucketIndex of a key whose XOR distance to the node is delta (357-382): the
+    highest b-bit digit (positions 160-b, 160-2b, ... >= 0) that is not zero."""
+    i = 160 - b
+    while i >= 0 and (delta >> i) & ((1 << b) - 1) == 0:
+        i -= b
+    if i < 0:
+        return -1
+    per = (1 << b) - 1
+    return (i // b) * per + (per - 1 if first_on_layer else ((delta >> i) & per) - 1)
+
+
+def kad_bucket_size(index: int, k: int, bucket_type: int = 0, extra: int = 0) -> int:
+    """Kademlia::routingBucketSize (384-411); 0 = unbounded (nkademlia)."""
+    if bucket_type == 1:
+        return 0
+    if bucket_type == 2:
+        import math
+        limit = int(math.log(extra or 160) / math.log(2))
+        off = limit - (160 - (index + 1))
+        if off > 0 and 2 ** off > k:
+            return 2 ** off
+    return k
+
+
 class KadTables:
-    def __init__(self, ids_words, sib, bcount, bnodes, k=8, s=8):
+    def __init__(self, ids_words, sib, bcount, bnodes, k=8, s=8, b=1, buckets=None):
+        """buckets: per node a dict bucket index -> members (any b / size); else the k-stride
+        bcount / bnodes arrays (b = 1)."""
         self.ids = [to_int(w) for w in ids_words]
         self.sib, self.bcount, self.bnodes = sib, bcount, bnodes
-        self.k, self.s = k, s
+        self.k, self.s, self.b = k, s, b
+        self.buckets = buckets
 
     def _sorted_add(self, vec, cap, node, key):
         # BaseKeySortedVector::add with KeyXorMetric (NodeVector.h:432-512)
@@ -382,9 +415,8 @@ class KadTables:
         vec.append(node)          # only reached when not full
         return len(vec) - 1
 
-    def bucket_index(self, c, key):
-        d = key ^ self.ids[c]
-        return d.bit_length() - 1 if d else -1
+    def bucket_index(self, c, key, first=False):
+        return kad_bucket_index(key ^ self.ids[c], self.b, first)
 
     def siblings(self, c):
         return [int(x) for x in self.sib[c] if x != 0xFFFFFFFF]
@@ -414,10 +446,12 @@ class KadTables:
         if not sib:
             return [c]
         main = self.bucket_index(c, key)
-        start = main
+        start = self.bucket_index(c, key, True)
         end = self.bucket_index(c, self.ids[sib[-1]])
 
         def bucket(m):
+            if self.buckets is not None:
+                return list(self.buckets[c].get(m, ()))
             return [int(x) for x in self.bnodes[c][m][: self.bcount[c][m]]]
 
         if main != -1:
@@ -433,7 +467,7 @@ class KadTables:
                 self._sorted_add(res, size, x, key)
             self._sorted_add(res, size, c, key)
         idx = main + 1
-        while len(res) < size and idx < 160:
+        while len(res) < size and idx < kad_num_buckets(self.b):
             for x in bucket(idx):
                 self._sorted_add(res, size, x, key)
             idx += 1
@@ -754,16 +788,30 @@ class KadMaint:
     XOR distance to the node (KademliaBucket with its comparator, Kademlia.cc:179, 315-317) and the
     routing buckets as a dict bucket index -> list in LRU order (push_back / erase, 432-756)."""
 
-    def __init__(self, ids_words, sib, bcount, bnodes, k=8, s=8):
+    def __init__(self, ids_words, sib, bcount=None, bnodes=None, k=8, s=8, b=1, bucket_type=0, node_limit=1000,
+                 extra=0, bucket_off=None, bucket_nodes=None):
+        """k-stride bcount / bnodes (b = 1) or CSR bucket_off / bucket_nodes (any b)."""
         self.ids = [to_int(w) for w in ids_words]
-        self.k, self.s = k, s
+        self.ids_words = ids_words
+        self.k, self.s, self.b = k, s, b
+        self.bucket_type, self.node_limit, self.extra = bucket_type, node_limit, extra
+        self.nb = kad_num_buckets(b)
         n = len(self.ids)
         self.sib = []
         self.bk = []
         for v in range(n):
             mine = [int(x) for x in sib[v] if x != 0xFFFFFFFF]
             self.sib.append(sorted(mine, key=lambda x: self.ids[x] ^ self.ids[v]))
-            self.bk.append({m: [int(x) for x in bnodes[v][m][: bcount[v][m]]] for m in range(160) if bcount[v][m]})
+            if bucket_off is not None:
+                row = {}
+                for m in range(self.nb):
+                    o0, o1 = int(bucket_off[v * self.nb + m]), int(bucket_off[v * self.nb + m + 1])
+                    if o1 > o0:
+                        row[m] = [int(x) for x in bucket_nodes[o0:o1]]
+                self.bk.append(row)
+            else:
+                self.bk.append({m: [int(x) for x in bnodes[v][m][: bcount[v][m]]] for m in range(160) if bcount[v][m]})
+        self.rts = [sum(len(x) for x in row.values()) for row in self.bk]   # currentRoutingTableSize
 
     def arrays(self):
         n, S5 = len(self.ids), 5 * self.s
@@ -779,16 +827,28 @@ class KadMaint:
                     nodes[v][m][j] = x
         return sib, cnt, nodes
 
+    def csr(self):
+        """(siblings rows, bucket_off, bucket_nodes) as orc_kad_export_csr lays them out."""
+        S5 = 5 * self.s
+        sib = [list(x) + [0xFFFFFFFF] * (S5 - len(x)) for x in self.sib]
+        off, nodes = [0], []
+        for row in self.bk:
+            for m in range(self.nb):
+                nodes += row.get(m, [])
+                off.append(len(nodes))
+        return sib, off, nodes
+
     def routing_add(self, v, h, alive):
         """Kademlia::routingAdd (Kademlia.cc:432-756): secureMaintenance, pingNewSiblings, activePing
-        and proximityNeighborSelection off, bucketType kademlia (k per bucket).  Returns its result."""
+        and proximityNeighborSelection off; every bucketType (routingBucketSize 384-411, the nkademlia
+        branch 620-664).  Returns its result."""
         if h == v:
             return False
         me = self.ids[v]
         sib = self.sib[v]
         if h in sib:
             return True
-        b = (self.ids[h] ^ me).bit_length() - 1
+        b = kad_bucket_index(self.ids[h] ^ me, self.b)
         bucket = self.bk[v].get(b)
         if bucket is not None and h in bucket:
             if alive:
@@ -805,29 +865,46 @@ class KadMaint:
                 return True
             h = sib.pop()                                        # preempted: goes to its bucket
             result = True
-        b = (self.ids[h] ^ me).bit_length() - 1
+        b = kad_bucket_index(self.ids[h] ^ me, self.b)
+        assert b >= 0, "bucket index -1: the reference dereferences a NULL bucket"
         bucket = self.bk[v].setdefault(b, [])
-        if len(bucket) < self.k:
+        if self.bucket_type == 1:                 # nkademlia (620-664): a global table limit
+            if len(bucket) >= self.k and self.rts[v] >= self.node_limit:
+                return False
             bucket.append(h)
+            self.rts[v] += 1
+            return True
+        if len(bucket) < kad_bucket_size(b, self.k, self.bucket_type, self.extra):
+            bucket.append(h)
+            self.rts[v] += 1
             return True
         return result
 
     def refresh_keys(self, v):
-        """handleBucketRefreshTimerExpired's bucket keys (Kademlia.cc:1631-1676, b = 1)."""
+        """handleBucketRefreshTimerExpired's bucket keys (Kademlia.cc:1631-1676): self ^ ((d+1) << i)
+        for the digits i = 160-b .. diff and d = 0 .. 2^b-2, diff = 160 - b*(shared digits + 1)."""
         if not self.sib[v]:
             return []
         me = self.ids[v]
         front = self.ids[self.sib[v][0]] ^ me
-        return [me ^ (1 << i) for i in range(159, front.bit_length() - 2, -1)]
+        shared_bits = 160 - front.bit_length()
+        diff = 160 - self.b * (shared_bits // self.b + 1)
+        out = []
+        for i in range(160 - self.b, diff - 1, -self.b):
+            for d in range((1 << self.b) - 1):
+                out.append(me ^ ((d + 1) << i))
+        return out
 
     def round(self, xy, nodes, flags, lookup_cfg, R_bucket=8):
         """One synchronous maintenance round: the listed nodes' exhaustive refresh lookups on the
         round-start tables (KadLookupSim), then at every node the routingAdds of the calls that reached
         it and of its handled responses (carried nodes not alive, then the responder alive), in
         simulated-time order with ties (calls first, task, index)."""
-        sib, cnt, nod = self.arrays()
         T = KadTables.__new__(KadTables)            # the round-start tables, as findNode reads them
-        T.ids, T.sib, T.bcount, T.bnodes, T.k, T.s = self.ids, sib, cnt, nod, self.k, self.s
+        T.ids, T.k, T.s, T.b = self.ids, self.k, self.s, self.b
+        T.sib = [list(x) + [0xFFFFFFFF] * (5 * self.s - len(x)) for x in self.sib]
+        T.buckets = [{m: list(l) for m, l in row.items()} for row in self.bk]
+        T.bcount = T.bnodes = None
         sim = KadLookupSim(T, xy, k=self.k, **lookup_cfg)
         tasks = []
         for v, f in zip(nodes, flags):
