@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 9
+#define OVS_ABI_VERSION 10
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -82,7 +82,8 @@ typedef struct ovs_params {
     int32_t successorListSize;          /* **.chord.successorListSize = 8 */
     int32_t extendedFingerTable;        /* **.chord.extendedFingerTable = false (only false) */
     int32_t numFingerCandidates;        /* **.chord.numFingerCandidates = 3 */
-    int32_t k, s, b;                    /* **.kademlia.k/s/b = 8/8/1 (b = 1 only) */
+    int32_t k, s, b;                    /* **.kademlia.k/s/b = 8/8/1 (b 2..5, bucketType != kademlia:
+                                           tables through ovs_kad_load_tables_csr) */
     int32_t lookupRedundantNodes;
     int32_t lookupParallelPaths;        /* 1 only */
     int32_t lookupParallelRpcs;
@@ -115,8 +116,11 @@ typedef struct ovs_params {
     int32_t deBruijnListSize;           /* **.koorde.deBruijnListSize = 16 */
     int32_t useOtherLookup;             /* **.koorde.useOtherLookup = true */
     int32_t useSucList;                 /* **.koorde.useSucList = true */
-    int32_t pad0;
+    int32_t bucketType;                 /* **.kademlia.bucketType: 0 = "kademlia", 1 = "nkademlia",
+                                           2 = "nr128" (Kademlia.cc:135-151; ABI 10, formerly padding) */
     double  cacheTTL;                   /* **.epichord.cacheTTL = 120 s (ABI 8) */
+    int32_t globalNodeLimit;            /* **.kademlia.globalNodeLimit = 1000 (nkademlia; ABI 10) */
+    int32_t extraNodesFinalBucket;      /* **.kademlia.extraNodesFinalBucket = 0 (nr128; 0 = keyLength) */
 } ovs_params;
 
 /* Result of one one-way KBR test lookup (KBRTestApp with kbrOneWayTest). */
@@ -174,6 +178,27 @@ ovs_status  ovs_kad_load(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n,
 ovs_status  ovs_kad_load_tables(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n, const double* xy,
                                 const uint32_t* siblings, const uint8_t* bucket_count,
                                 const uint32_t* bucket_nodes, uint32_t flags);
+/* Kademlia variants (ABI 10) through explicit tables in CSR form: b = 1..5 (numBuckets =
+ * (2^b - 1) * (160 / b); routingBucketIndex's b-bit digits, Kademlia.cc:176, 357-382) and
+ * bucketType "nr128" (b = 1: bigger final buckets, routingBucketSize 384-411) or "nkademlia" (no
+ * per-bucket maximum, 620-664), as params.b / params.bucketType say.  siblings[n*5s] as for
+ * ovs_kad_load_tables; bucket i of node v = bucket_nodes[bucket_off[v*nb + i] ..
+ * bucket_off[v*nb + i + 1]) in LRU order, nb = ovs_kad_num_buckets(params), bucket_off[0] = 0.
+ * The tables must keep routingAdd's invariants: members are other nodes of [0, n) whose
+ * routingBucketIndex is the bucket's, at most routingBucketSize(i) of them (kademlia / nr128), no
+ * node twice, none both sibling and member -- else OVS_EINVAL naming the node.  One-way routes and
+ * LookupCalls (iterative routing) and ovs_find_node_batch run on these tables (kernel K2g);
+ * exhaustive-iterative routing, refresh batches and maintenance rounds take the 160-bucket
+ * kademlia tables only (OVS_ENOTSUP).  Host buffers. */
+int32_t     ovs_kad_num_buckets(const ovs_params* p);   /* -1 when b is outside 1..5 */
+ovs_status  ovs_kad_load_tables_csr(ovs_ctx* ctx, const ovs_key160* ids_sorted, uint64_t n, const double* xy,
+                                    const uint32_t* siblings, const uint64_t* bucket_off,
+                                    const uint32_t* bucket_nodes, uint32_t flags);
+/* The loaded Kademlia tables in CSR form (host buffers): siblings[n*5s] (0xFFFFFFFF padded),
+ * bucket_off[n*nb + 1], up to cap bucket members; *total = how many there are (cap 0 sizes the
+ * call; bucket_nodes may then be NULL).  Any loaded whole network (ovs_kad_load, _tables, _csr). */
+ovs_status  ovs_kad_export_csr(ovs_ctx* ctx, uint32_t* siblings, uint64_t* bucket_off, uint32_t* bucket_nodes,
+                               uint64_t cap, uint64_t* total);
 /* Koorde (src/overlay/koorde/Koorde.cc, class Koorde : public Chord) on a converged ring: the
  * Chord ring of ids (predecessor, successorListSize successors) plus every node's de Bruijn
  * pointer and list as handleDeBruijnTimerExpired / the DeBruijnCall exchange leave them
@@ -326,7 +351,7 @@ ovs_status  ovs_lookup_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_
  * order -- the nodes Kademlia::handleRpcResponse routingAdd()s with their RTT
  * (Kademlia.cc:1352-1420) -- 0xFFFFFFFF padded; rtt_ns (may be NULL) their
  * RTTs, -1 padded; rpcs (may be NULL) = n FindNodeCall counts.  Requires
- * lookupMerge, lookupStrictParallelRpcs, lookupParallelRpcs <= 4,
+ * lookupMerge, lookupStrictParallelRpcs, lookupParallelRpcs <= 8,
  * 1 <= R <= 64, 1 <= hopCountMax.  Single-context networks. */
 ovs_status  ovs_kad_refresh_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                                   int32_t redundant_nodes, ovs_lookup_out* out, uint32_t* siblings,

@@ -16,7 +16,13 @@ void kad_free(KadTables& t)
     if (t.blks) hipFree(t.blks);
     if (t.sib) hipFree(t.sib);
     if (t.slev) hipFree(t.slev);
+    if (t.goff) hipFree(t.goff);
+    if (t.gtop) hipFree(t.gtop);
+    if (t.gidx) hipFree(t.gidx);
+    if (t.gend) hipFree(t.gend);
     t.nodes = nullptr; t.nodex = nullptr; t.blks = nullptr; t.sib = nullptr; t.slev = nullptr; t.rows_blks = 0;
+    t.goff = nullptr; t.gtop = nullptr; t.gidx = nullptr; t.gend = nullptr; t.gtotal = 0;
+    t.general = 0; t.b = 1; t.nb = KEYBITS;
 }
 
 // ---------------------------------------------------------------------------
@@ -321,6 +327,66 @@ __global__ void k_kad_explicit_rows(const KeyRec* __restrict__ recs, const KadNo
     }
 }
 
+// general tables (CSR buckets), pass A: routingAdd's invariants under b and the bucket sizes
+// (codes as k_kad_explicit_nodes; 3 = more than routingBucketSize(i), 5 = routingBucketIndex of the
+// member is not the bucket's), the node summary, the bucket index of the farthest sibling
+__global__ void k_kad_general_nodes(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t n, int S5,
+                                    int b, int nb, const int* __restrict__ caps, uint32_t* __restrict__ sib,
+                                    const uint32_t* __restrict__ off, const uint32_t* __restrict__ members,
+                                    KadNode* __restrict__ out, KadX* __restrict__ ox, int16_t* __restrict__ gend,
+                                    uint32_t* err, uint32_t* short_flag)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const K160 me = kload(recs, v);
+    uint32_t* L = sib + (uint64_t)v * S5;
+    int cnt = 0;
+    for (int i = 0; i < S5; ++i) {
+        const uint32_t x = L[i];
+        if (x == NONE) continue;
+        L[cnt++] = x;
+    }
+    for (int i = cnt; i < S5; ++i) L[i] = NONE;
+    uint32_t code = 0;
+    for (int i = 0; i < cnt && !code; ++i) {
+        if (L[i] >= n || L[i] == v) code = 1;
+        for (int j = 0; j < i && !code; ++j) if (L[j] == L[i]) code = 2;
+    }
+    for (int m = 0; m < nb && !code; ++m) {
+        const uint32_t a = off[(uint64_t)v * nb + m], z = off[(uint64_t)v * nb + m + 1];
+        if (z < a) { code = 3; break; }
+        if (caps[m] > 0 && z - a > (uint32_t)caps[m]) { code = 3; break; }
+        for (uint32_t q = a; q < z && !code; ++q) {
+            const uint32_t x = members[q];
+            if (x >= n || x == v) { code = 4; break; }
+            if (kad_bucket_index(k_xor(kload(recs, x), me), b, false) != m) { code = 5; break; }
+            for (uint32_t j = a; j < q; ++j) if (members[j] == x) code = 6;
+            for (int i = 0; i < cnt; ++i) if (L[i] == x) code = 7;
+        }
+    }
+    if (code) {
+        if (atomicCAS(err, NONE, v) == NONE) err[1] = code;
+        return;
+    }
+    K160 R{};
+    for (int i = 0; i < 5; ++i) R.w[i] = 0;
+    for (int i = 0; i < cnt; ++i) {
+        const K160 d = k_xor(kload(recs, L[i]), me);
+        if (k_gt(d, R)) R = d;
+    }
+    // no 160-bucket rows: rowlo = -1
+    kad_node_summary(recs, xy, v, L, cnt, -1, out, ox);
+    gend[v] = (int16_t)(cnt > 0 ? kad_bucket_index(R, b, false) : -1);
+    if (cnt + 1 < 8) atomicOr(short_flag, 1u);
+}
+
+__global__ void k_kad_general_tops(const KeyRec* __restrict__ recs, const uint32_t* __restrict__ members, uint64_t total,
+                                   uint64_t* __restrict__ tops)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < total) tops[e] = ktop(kload(recs, members[e]));
+}
+
 __global__ void k_kad_export(const KadNode* __restrict__ nodes, const KadBlk* __restrict__ blks, uint32_t n, int k,
                              uint8_t* __restrict__ bcount, uint32_t* __restrict__ bnodes)
 {
@@ -517,6 +583,67 @@ hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n,
     hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, 0u, n);
     hipLaunchKernelGGL(k_kad_explicit_rows, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn,
                        t.sib, bcount, bnodes, t.blks, t.rows_blks);
+    e = hipStreamSynchronize(st);
+    cleanup();
+    if (e != hipSuccess) return e;
+    if ((e = kad_prefix_flag(recs, n, t, st)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t kad_build_general(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, int b, const int* caps,
+                             const uint32_t* sib, const uint32_t* off, const uint32_t* members, uint64_t total,
+                             KadTables& t, uint32_t* bad_node, uint32_t* bad_code, hipStream_t st)
+{
+    hipError_t e;
+    kad_free(t);
+    t.k = k; t.s = s; t.seed = 0; t.lo = 0; t.hi = n; t.snapshot = 0; t.general = 1;
+    t.b = b; t.nb = (int)(((1 << b) - 1) * (KEYBITS / b));
+    if (k < 1 || k > KMAX || b < 1 || b > 5) return hipErrorNotSupported;
+    t.bpb = (k + KBLK - 1) / KBLK;
+    const int S5 = 5 * s, sbn = (S5 + 1 + KBLK - 1) / KBLK;
+    const uint64_t dir = (uint64_t)n * t.nb + 1;
+    uint32_t* flags = nullptr;
+    int* dcaps = nullptr;
+    auto cleanup = [&]() {
+        if (flags) hipFree(flags);
+        if (dcaps) hipFree(dcaps);
+    };
+    if ((e = hipMalloc(&t.nodes, sizeof(KadNode) * n)) != hipSuccess) return e;
+    if ((e = hipMalloc(&t.nodex, sizeof(KadX) * n)) != hipSuccess) return e;
+    if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)n * S5)) != hipSuccess) return e;
+    if ((e = hipMalloc(&t.goff, sizeof(uint32_t) * dir)) != hipSuccess) return e;
+    if ((e = hipMalloc(&t.gidx, sizeof(uint32_t) * (total ? total : 1))) != hipSuccess) return e;
+    if ((e = hipMalloc(&t.gtop, sizeof(uint64_t) * (total ? total : 1))) != hipSuccess) return e;
+    if ((e = hipMalloc(&t.gend, sizeof(int16_t) * n)) != hipSuccess) return e;
+    if ((e = hipMalloc(&flags, sizeof(uint32_t) * 3)) != hipSuccess) { cleanup(); return e; }
+    if ((e = hipMalloc(&dcaps, sizeof(int) * t.nb)) != hipSuccess) { cleanup(); return e; }
+    t.gtotal = total;
+    hipMemcpyAsync(t.sib, sib, sizeof(uint32_t) * (uint64_t)n * S5, hipMemcpyDeviceToDevice, st);
+    hipMemcpyAsync(t.goff, off, sizeof(uint32_t) * dir, hipMemcpyDeviceToDevice, st);
+    if (total) hipMemcpyAsync(t.gidx, members, sizeof(uint32_t) * total, hipMemcpyDeviceToDevice, st);
+    hipMemcpyAsync(dcaps, caps, sizeof(int) * t.nb, hipMemcpyHostToDevice, st);
+    const uint32_t init[3] = {NONE, 0u, 0u};
+    hipMemcpyAsync(flags, init, sizeof init, hipMemcpyHostToDevice, st);
+    hipLaunchKernelGGL(k_kad_general_nodes, dim3(nblk(n, 128)), dim3(128), 0, st, recs, xy, n, S5, b, t.nb, dcaps, t.sib,
+                       t.goff, t.gidx, t.nodes, t.nodex, t.gend, flags, flags + 2);
+    uint32_t hf[3] = {0, 0, 0};
+    hipMemcpyAsync(hf, flags, sizeof hf, hipMemcpyDeviceToHost, st);
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) { cleanup(); return e; }
+    if (hf[0] != NONE) {
+        *bad_node = hf[0];
+        *bad_code = hf[1];
+        cleanup();
+        return hipErrorInvalidValue;
+    }
+    t.maybe_short = hf[2] != 0;
+    if (total)
+        hipLaunchKernelGGL(k_kad_general_tops, dim3(nblk(total, 256)), dim3(256), 0, st, recs, t.gidx, total, t.gtop);
+    // the sibling rows (level-sorted, the node first) as blocks: isSiblingFor(numSiblings > 1) and
+    // findNode's sibling part read them as on the 160-bucket tables; no bucket rows (rowlo = -1)
+    t.rows_blks = 0;
+    if ((e = hipMalloc(&t.blks, sizeof(KadBlk) * ((uint64_t)n * sbn + 1))) != hipSuccess) { cleanup(); return e; }
+    hipLaunchKernelGGL(k_kad_explicit_rows, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn, t.sib,
+                       (const uint8_t*)nullptr, (const uint32_t*)nullptr, t.blks, (uint64_t)0);
     e = hipStreamSynchronize(st);
     cleanup();
     if (e != hipSuccess) return e;

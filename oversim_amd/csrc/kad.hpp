@@ -75,6 +75,24 @@ struct KadTables {
     int exact = 1;                 // two IDs share their top 63 bits: comparisons use the 160-bit tie fallback
     int snapshot = 1;              // 0: explicit tables (ovs_kad_load_tables)
     int maybe_short = 0;           // explicit tables: some node may answer fewer than resultSize nodes
+    // general tables (ovs_kad_load_tables_csr: b > 1, bucketType nr128 / nkademlia): the buckets in
+    // CSR form instead of the 160 bucket rows (blks then holds the sibling rows only)
+    int general = 0;
+    int b = 1, nb = KEYBITS;       // digit width, numBuckets
+    uint32_t* goff = nullptr;      // n * nb + 1 member offsets (bucket i of node v: [goff[v*nb+i], goff[v*nb+i+1]))
+    uint64_t* gtop = nullptr;      // per member: top 64 bits of its key
+    uint32_t* gidx = nullptr;      // per member: node index (LRU order within a bucket)
+    int16_t* gend = nullptr;       // per node: routingBucketIndex of its farthest sibling (-1: none)
+    uint64_t gtotal = 0;           // members
+};
+
+// the general-table view of K2g and the batched findNode (kad_general.hip)
+struct KadGenView {
+    const uint32_t* __restrict__ goff;
+    const uint64_t* __restrict__ gtop;
+    const uint32_t* __restrict__ gidx;
+    const int16_t* __restrict__ gend;
+    int b, nb;
 };
 
 struct KadView {
@@ -114,6 +132,19 @@ hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n,
                               uint32_t* bad_code, hipStream_t st);
 hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_t* bucket_count,
                       uint32_t* bucket_nodes, hipStream_t st);
+// general tables from CSR (device copies of the caller's arrays: sib n*5s, off n*nb+1 (< 2^32
+// members), nodes); caps[nb] = routingBucketSize per bucket index (0: unbounded, nkademlia).
+// hipErrorInvalidValue with *bad_node / *bad_code when a table breaks routingAdd's invariants.
+hipError_t kad_build_general(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, int b, const int* caps,
+                             const uint32_t* sib, const uint32_t* off, const uint32_t* nodes, uint64_t total,
+                             KadTables& t, uint32_t* bad_node, uint32_t* bad_code, hipStream_t st);
+// K2g (kad_general.hip): one-way routes (sibs == nullptr) or LookupCalls over general tables
+hipError_t kad_route_general(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
+                             const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
+                             ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, hipStream_t st, uint32_t* sibs);
+hipError_t kad_find_node_general(const KadTables& t, uint32_t n, const uint32_t* node, const K160* keys, uint64_t nq,
+                                 int numRedundant, int numSiblings, uint32_t* out_nodes, uint32_t max_out,
+                                 uint8_t* out_count, uint8_t* out_sib, hipStream_t st);
 hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
                      ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st,

@@ -25,6 +25,21 @@ __device__ __forceinline__ uint32_t kbit(const K160& k, int b) { return (kword(k
 
 __device__ __forceinline__ K160 kload(const KeyRec* __restrict__ recs, uint32_t i) { return key_of(load_rec(recs, i)); }
 
+// Kademlia::routingBucketIndex (Kademlia.cc:357-382) of the XOR distance D for digit width b: the
+// b-bit digits sit at bits i = 160 % b + j * b (the bits below 160 % b belong to none); the highest
+// nonzero digit d, at i, gives bucket (i / b) * (2^b - 1) + d - 1 (firstOnLayer: + 2^b - 2, the
+// layer's last); -1 when every digit is zero
+__device__ __forceinline__ int kad_bucket_index(const K160& D, int b, bool first)
+{
+    const int m = k_msb(D);
+    const int r = KEYBITS % b;
+    if (m < r) return -1;
+    const int i = r + ((m - r) / b) * b;
+    const uint64_t win = (uint64_t)kword(D, i >> 5) | ((uint64_t)kword(D, (i >> 5) + 1) << 32);
+    const int d = (int)((win >> (i & 31)) & ((1u << b) - 1u));
+    return (i / b) * ((1 << b) - 1) + (first ? (1 << b) - 2 : d - 1);
+}
+
 __device__ __forceinline__ K160 node_key(const KadNode* __restrict__ nodes, uint32_t i)
 {
     const uint4* p = reinterpret_cast<const uint4*>(nodes + i);
@@ -738,12 +753,23 @@ __device__ __forceinline__ void kad_lookup_init(KadLookup<A, C>& L, const K160& 
     L.nsent = 0;
 }
 
+// The FindNodeResponse size of a call's target on the 160-bucket tables (kad_response_size); the
+// general tables (K2g, kad_general.hip) bring their own
+template <bool EX, int C, bool SHORT>
+struct KadBlkSizer {
+    __device__ __forceinline__ int operator()(const KadView& V, uint32_t x, const RespGeo& g, const K160& K, int rs,
+                                              bool sib, int ns) const
+    {
+        return kad_response_size<EX, C, SHORT>(V, x, g, K, rs, sib, ns);
+    }
+};
+
 // FindNodeCall from the source to x at `now` (IterativeLookup::sendRpc 656-689, BaseRpc timeout,
 // SimpleNodeEntry::calcDelay with the source's tx queue).  on(slot, x, isTimeout) is told which
 // pending-event slot the call occupies (the sharded path requests x's findNode result there).
-template <int A, bool EX, bool LK, bool SHORT, class OnSend, int C>
+template <int A, bool EX, bool LK, bool SHORT, class OnSend, int C, class Sizer = KadBlkSizer<EX, C, SHORT>>
 __device__ __forceinline__ void kad_send(KadLookup<A, C>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
-                                         uint32_t x, const OnSend& on)
+                                         uint32_t x, const OnSend& on, const Sizer& size = Sizer{})
 {
     const KadNode rr = load_node(V.nodes, x);
     const int ns = LK ? LC.numSiblings : 1;
@@ -763,7 +789,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A, C>& L, const KadView& V, c
     }
 #endif
     // the response carries findNode's result (Kademlia.cc:1127-1131 resultSize)
-    const int csz = kad_response_size<EX, C, SHORT>(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
+    const int csz = size(V, x, rg, L.K, sb ? ns : LC.redundant, sb, ns);
     const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
     const int64_t bwc = DC.bwCall;
     const int64_t newTx = (L.txf > L.now ? L.txf : L.now) + bwc;
@@ -803,9 +829,9 @@ __device__ __forceinline__ void kad_send(KadLookup<A, C>& L, const KadView& V, c
 }
 
 // IterativePathLookup::sendRpc (IterativeLookup.cc:1067-1170)
-template <int A, bool EX, bool LK, bool SHORT, class OnSend, int C>
+template <int A, bool EX, bool LK, bool SHORT, class OnSend, int C, class Sizer = KadBlkSizer<EX, C, SHORT>>
 __device__ __forceinline__ void kad_send_rpcs(KadLookup<A, C>& L, const KadView& V, const DelayConsts& DC, const KadLC& LC,
-                                              int num, const OnSend& on)
+                                              int num, const OnSend& on, const Sizer& size = Sizer{})
 {
     if (L.pfinished) return;
     if (LC.hopCountMax && L.hops >= LC.hopCountMax) { L.pfinished = true; L.psuccess = false; return; }
@@ -825,7 +851,7 @@ __device__ __forceinline__ void kad_send_rpcs(KadLookup<A, C>& L, const KadView&
         if (!LC.visitOnlyOnce || h != L.S) {
             ++L.pending;
             --num;
-            kad_send<A, EX, LK, SHORT>(L, V, DC, LC, h, on);
+            kad_send<A, EX, LK, SHORT>(L, V, DC, LC, h, on, size);
         }
         L.nh.used |= 1u << e;
     }

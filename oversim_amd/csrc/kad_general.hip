@@ -1,0 +1,222 @@
+// kad_general.hip -- K2g: Kademlia lookups over the general tables (ovs_kad_load_tables_csr) for
+// gfx950 (MI355X): b > 1 (routingBucketIndex's b-bit digits, numBuckets = (2^b - 1) * (160 / b),
+// Kademlia.cc:176, 357-382) and the fork's bucketType variants nr128 / nkademlia
+// (routingBucketSize 384-411, routingAdd 620-664), whose buckets may hold far more than the 16
+// entries K2's two 96 B blocks carry.
+//
+// The lookup state machine is K2's (kad_dev.hpp: kad_event_begin / kad_event_after_find /
+// kad_send_rpcs -- IterativeLookup.cc:133-1195 with merge, parallel RPCs, int64-ns event order);
+// only Kademlia::findNode (Kademlia.cc:1101-1246) differs: it walks the CSR buckets in the
+// reference's order -- the main bucket, then (main bucket at or above the sibling zone, or a short
+// result) the buckets startIndex .. endIndex other than the main one, the sibling table and the
+// node itself, then the buckets above the main one while the result is short -- inserting each
+// member into the XOR-sorted result by its top-64 distance (exact compare on ties, cand_lt<EX>).
+// One lane per lookup, to completion: a variant path, not the tuned K2 (no cooperative
+// sibling-zone pass, no persistent refill); parity first (tests/test_gpu_kad_general.py).
+#include "kad_dev.hpp"
+
+namespace ovs {
+
+namespace {
+
+struct GSendNothing {
+    __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
+};
+
+struct GAlwaysReady {
+    __device__ __forceinline__ bool operator()(int, uint32_t) const { return true; }
+};
+
+template <bool RECORD>
+struct GHopRecorder {
+    uint32_t* __restrict__ hopseq;
+    uint64_t base;
+    int hcm;
+    __device__ __forceinline__ void operator()(int h, uint32_t r) const
+    {
+        if (RECORD && h < hcm) hopseq[base + h] = r;
+    }
+};
+
+// Kademlia::findNode(K, numRedundantNodes, numSiblings) at node c (nsib siblings) over the general
+// tables; numSiblings = -1: an exhaustive-iterative call (resultSize = numRedundantNodes, no
+// siblings flag).  Returns the result size.
+template <bool EX, int C>
+__device__ int kadg_find_node(const KadView& V, const KadGenView& G, uint32_t c, int nsib, const K160& K,
+                              int numRedundant, bool sib, int numSiblings, SVec<C>& res)
+{
+    svec_clear(res);
+    const K160 me = node_key(V.nodes, c);
+    if (nsib == 0) {                       // an empty sibling table answers [self] (Kademlia.cc:1133-1137)
+        svec_add<C, EX>(res, 1, c, dist_hi(me, K), K, V.nodes);
+        return 1;
+    }
+    // resultSize (Kademlia.cc:1125-1131)
+    const int rs = numSiblings < 0 ? numRedundant : sib ? (numSiblings ? numSiblings : 1) : numRedundant;
+    const int cap = rs < C ? rs : C;
+    const K160 D = k_xor(me, K);
+    const int mainI = kad_bucket_index(D, G.b, false);
+    const int startI = kad_bucket_index(D, G.b, true);
+    const int endI = G.gend[c];
+    const uint64_t kt = ktop(K);
+    const uint64_t row = (uint64_t)c * (uint64_t)G.nb;
+    auto add_bucket = [&](int m) {
+        const uint32_t a = G.goff[row + m], z = G.goff[row + m + 1];
+        for (uint32_t e = a; e < z; ++e) svec_add<C, EX>(res, cap, G.gidx[e], dclamp(G.gtop[e] ^ kt), K, V.nodes);
+    };
+    if (mainI >= 0) add_bucket(mainI);
+    if (startI >= endI || res.n < cap) {
+        for (int m = startI; m >= endI && m >= 0; --m)
+            if (m != mainI) add_bucket(m);
+        const KadBlk* Lr = V.sibb + (uint64_t)c * V.sbn;     // c itself, then its siblings
+        for (int i = 0; i <= nsib; ++i) {
+            const KadBlk& bk = Lr[i / KBLK];
+            svec_add<C, EX>(res, cap, bk.idx[i % KBLK], dclamp(bk.top[i % KBLK] ^ kt), K, V.nodes);
+        }
+    }
+    for (int m = mainI + 1; res.n < cap && m < G.nb; ++m) add_bucket(m);
+    return res.n;
+}
+
+// the FindNodeResponse size of a call's target: resultSize unless the target's scan sees fewer
+// candidates, which needs a sibling table shorter than resultSize - 1 (then the scan is counted)
+template <bool EX, int C>
+struct KadGenSizer {
+    KadGenView G;
+    __device__ __forceinline__ int operator()(const KadView& V, uint32_t x, const RespGeo& g, const K160& K, int rs,
+                                              bool sib, int ns) const
+    {
+        if (g.nsib == 0 || (sib && ns <= 1)) return 1;
+        const int full = rs < (int)V.n ? rs : (int)V.n;
+        if (g.nsib + 1 >= rs) return full;
+        SVec<C> r;
+        return kadg_find_node<EX, C>(V, G, x, g.nsib, K, rs, sib, ns, r);
+    }
+};
+
+template <bool RECORD, bool EX, bool LK, int C>
+__global__ __launch_bounds__(128) void k_kadg_route(KadView V, KadGenView G, DelayConsts DC, KadLC LC,
+                                                    const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
+                                                    uint64_t nq, ovs_route_out* __restrict__ out,
+                                                    uint32_t* __restrict__ hopseq, uint32_t* __restrict__ rpcs_out,
+                                                    uint32_t* __restrict__ sib_out)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    constexpr int A = KAD_MAX_ALPHA;     // slots; strictParallelRpcs keeps alpha of them in use
+    const int ns = LK ? LC.numSiblings : 1;
+    KadLookup<A, C> L;
+    kad_lookup_init(L, qkeys[q], qsrc[q], V.xy);
+    const GHopRecorder<RECORD> rec{hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
+    const KadGenSizer<EX, C> size{G};
+    SVec<C> res;
+    res.n = 0;
+    res.used = 0;
+    while (!kad_lookup_done(L)) {
+        KadEv ev;
+        ev.r = 0; ev.geo = 0; ev.boff = 0; ev.e = 0; ev.num = 0; ev.numR = 0; ev.pre = 0; ev.start = false;
+        const int ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, GAlwaysReady{}, rec, ev);
+        res.n = 0;
+        res.used = 0;
+        int num = -1;
+        if (ph == KEV_FIND) {
+            kadg_find_node<EX, C>(V, G, ev.r, ev.rg().nsib, L.K, ev.numR, ev.sb(), ns, res);
+            num = kad_event_after_find<A, EX, LK>(L, V, LC, ev, res);
+        } else if (ph == KEV_SENDS) {
+            num = ev.num;
+        }
+        if (num >= 0) kad_send_rpcs<A, EX, LK, true>(L, V, DC, LC, num, GSendNothing{}, size);
+    }
+    const ovs_route_out o = kad_lookup_output(L, V, DC, LC);
+    const bool ok = o.status == OVS_LOOKUP_OK;
+    if (LK) {
+        // the LookupResponse's sibling vector: the answering sibling's findNode result (K2's rule)
+        if (ns == 0) {
+            sib_out[q] = ok ? L.result : NONE;
+        } else {
+            uint32_t* row = sib_out + q * (uint64_t)ns;
+            for (int j = 0; j < ns && j < 8; ++j) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
+        }
+    }
+    out[q] = o;
+    if (rpcs_out) rpcs_out[q] = L.nsent;
+}
+
+template <bool EX, int CAP>
+__global__ void k_kadg_find_node(KadView V, KadGenView G, const uint32_t* __restrict__ node,
+                                 const K160* __restrict__ keys, uint64_t n, int numRedundant, int numSiblings,
+                                 uint32_t* __restrict__ out_nodes, uint32_t max_out, uint8_t* __restrict__ out_count,
+                                 uint8_t* __restrict__ out_sib)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = node[i];
+    const K160 K = keys[i];
+    const KadNode r = load_node(V.nodes, c);
+    const bool sb = numSiblings >= 0 && kad_is_sibling(V, r, c, K, numSiblings);
+    SVec<CAP> res;
+    const int cnt = kadg_find_node<EX, CAP>(V, G, c, kad_nsib(r.meta), K, numRedundant, sb, numSiblings, res);
+    uint32_t* o = out_nodes + i * max_out;
+    for (uint32_t j = 0; j < max_out; ++j) o[j] = NONE;
+#pragma unroll
+    for (int j = 0; j < CAP; ++j)
+        if (j < cnt && (uint32_t)j < max_out) o[j] = res.idx[j];
+    out_count[i] = (uint8_t)(cnt < (int)max_out ? cnt : (int)max_out);
+    out_sib[i] = sb ? 1 : 0;
+}
+
+inline unsigned gblocks(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+inline KadGenView gen_view(const KadTables& t) { return KadGenView{t.goff, t.gtop, t.gidx, t.gend, t.b, t.nb}; }
+
+}  // namespace
+
+hipError_t kad_route_general(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
+                             const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
+                             ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, hipStream_t st, uint32_t* sibs)
+{
+    if (nq == 0) return hipSuccess;
+    if (!t.general || !kad_params_supported(P, t)) return hipErrorNotSupported;
+    if (sibs && hopseq) return hipErrorNotSupported;
+    KadLC LC = kad_make_lc(P, t);
+    kad_lc_sizes(LC, DC, n);
+    const KadView V = kad_make_view(t, xy, n);
+    const KadGenView G = gen_view(t);
+    const bool wide = LC.redundant > 8 || LC.maxRedundantLocal > 8;
+    const dim3 grid(gblocks(nq, 128)), blk(128);
+#define KG(rec, ex, lk, c) hipLaunchKernelGGL((k_kadg_route<rec, ex, lk, c>), grid, blk, 0, st, V, G, DC, LC, qkeys, qsrc, nq, \
+                                              out, hopseq, rpcs, sibs)
+#define KGC(rec, lk, c) do { if (t.exact) KG(rec, true, lk, c); else KG(rec, false, lk, c); } while (0)
+    if (wide) {
+        if (sibs) KGC(false, true, 16);
+        else if (hopseq) KGC(true, false, 16);
+        else KGC(false, false, 16);
+    } else {
+        if (sibs) KGC(false, true, 8);
+        else if (hopseq) KGC(true, false, 8);
+        else KGC(false, false, 8);
+    }
+#undef KGC
+#undef KG
+    return hipGetLastError();
+}
+
+hipError_t kad_find_node_general(const KadTables& t, uint32_t n, const uint32_t* node, const K160* keys, uint64_t nq,
+                                 int numRedundant, int numSiblings, uint32_t* out_nodes, uint32_t max_out,
+                                 uint8_t* out_count, uint8_t* out_sib, hipStream_t st)
+{
+    if (nq == 0) return hipSuccess;
+    if (!t.general) return hipErrorNotSupported;
+    if ((numSiblings < 1 && numSiblings != -1) || numSiblings > 64 || numRedundant > 64) return hipErrorNotSupported;
+    const KadView V = kad_make_view(t, nullptr, n);
+    const KadGenView G = gen_view(t);
+    const bool wide = numSiblings > 16 || numRedundant > 16;
+#define KFN(ex, cap) hipLaunchKernelGGL((k_kadg_find_node<ex, cap>), dim3(gblocks(nq, 128)), dim3(128), 0, st, V, G, node, keys, \
+                                        nq, numRedundant, numSiblings, out_nodes, max_out, out_count, out_sib)
+    if (t.exact) { if (wide) KFN(true, 64); else KFN(true, 16); }
+    else { if (wide) KFN(false, 64); else KFN(false, 16); }
+#undef KFN
+    return hipGetLastError();
+}
+
+}  // namespace ovs

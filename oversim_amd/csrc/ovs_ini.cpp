@@ -270,6 +270,16 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         want_int("k", &p->k);
         want_int("s", &p->s);
         want_int("b", &p->b);
+        want_int("globalNodeLimit", &p->globalNodeLimit);
+        want_int("extraNodesFinalBucket", &p->extraNodesFinalBucket);
+        if (lookup(ovp + "bucketType", &v)) {
+            // Kademlia::initializeOverlay (Kademlia.cc:135-151)
+            const std::string bt = unquote(v);
+            if (bt == "kademlia") p->bucketType = 0;
+            else if (bt == "nkademlia") p->bucketType = 1;
+            else if (bt == "nr128") p->bucketType = 2;
+            else bad = "bucketType";
+        }
     }
     want_int("lookupRedundantNodes", &p->lookupRedundantNodes);
     want_int("lookupParallelPaths", &p->lookupParallelPaths);
@@ -371,6 +381,9 @@ extern "C" void ovs_params_default(int32_t overlay, ovs_params* p)
     p->useOtherLookup = 1;              // default.ini:279
     p->useSucList = 1;                  // default.ini:280
     p->cacheTTL = 120.0;                // default.ini:158
+    p->bucketType = 0;                  // default.ini:209 "kademlia"
+    p->globalNodeLimit = 1000;          // default.ini:210
+    p->extraNodesFinalBucket = 0;       // default.ini:211
     if (overlay == OVS_OVERLAY_KOORDE) p->successorListSize = 16;   // default.ini:275
     if (overlay == OVS_OVERLAY_EPICHORD) p->successorListSize = 4;  // default.ini:159
     if (overlay == OVS_OVERLAY_KADEMLIA) {

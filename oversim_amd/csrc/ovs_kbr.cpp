@@ -365,8 +365,10 @@ ovs_status ovs_set_params(ovs_ctx* c, const ovs_params* p)
     if (s != OVS_OK) return s;
     if (c->overlay && p->overlay != c->overlay) return fail(c, OVS_ESTATE, "overlay type differs from loaded network");
     if (c->overlay == OVS_OVERLAY_KADEMLIA &&
-        (p->k != c->P.k || p->s != c->P.s || p->b != c->P.b || p->kadSeed != c->P.kadSeed))
-        return fail(c, OVS_ESTATE, "k/s/b/kadSeed are fixed once a Kademlia network is loaded");
+        (p->k != c->P.k || p->s != c->P.s || p->b != c->P.b || p->kadSeed != c->P.kadSeed ||
+         p->bucketType != c->P.bucketType || p->extraNodesFinalBucket != c->P.extraNodesFinalBucket ||
+         p->globalNodeLimit != c->P.globalNodeLimit))
+        return fail(c, OVS_ESTATE, "k/s/b/kadSeed/bucketType are fixed once a Kademlia network is loaded");
     if (c->overlay == OVS_OVERLAY_KOORDE &&
         (p->successorListSize != c->P.successorListSize || p->shiftingBits != c->P.shiftingBits ||
          p->deBruijnListSize != c->P.deBruijnListSize || p->useOtherLookup != c->P.useOtherLookup ||
@@ -681,7 +683,9 @@ static ovs_status kad_load_arc(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     free_tables(c);
     free_kad_shard(c);
     if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
-    if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
+    if (c->P.b != 1 || c->P.bucketType != 0)
+        return fail(c, OVS_ENOTSUP, "the snapshot rule builds b = 1 kademlia tables: other b / bucketType through "
+                                    "ovs_kad_load_tables_csr");
     if (c->P.k < 1 || c->P.k > KMAX || c->P.s < 1 || 5 * c->P.s > 64)
         return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..16 (two 96 B bucket blocks) and 5*s <= 64");
     if (lo >= hi || hi > n) return fail(c, OVS_EINVAL, "arc [lo, hi) must be a non-empty part of [0, n)");
@@ -708,7 +712,9 @@ ovs_status ovs_kad_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     free_tables(c);
     free_kad_shard(c);
     if (c->P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
-    if (c->P.b != 1) return fail(c, OVS_ENOTSUP, "Kademlia b != 1 not supported");
+    if (c->P.b != 1 || c->P.bucketType != 0)
+        return fail(c, OVS_ENOTSUP, "k-stride tables hold b = 1 kademlia buckets: other b / bucketType through "
+                                    "ovs_kad_load_tables_csr");
     if (c->P.k < 1 || c->P.k > KMAX || c->P.s < 1 || 5 * c->P.s > 64)
         return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..16 (two 96 B bucket blocks) and 5*s <= 64");
     ovs_status s = upload_nodes(c, ids, n, xy, false);
@@ -743,6 +749,132 @@ ovs_status ovs_kad_load_tables(ovs_ctx* c, const ovs_key160* ids, uint64_t n, co
     if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "explicit Kademlia table build"); }
     c->overlay = OVS_OVERLAY_KADEMLIA;
     c->kh.import(reinterpret_cast<const K160*>(ids), n, c->P.k, c->P.s, siblings, bucket_count, bucket_nodes);
+    return OVS_OK;
+}
+
+// Kademlia::routingBucketSize (Kademlia.cc:384-411); 0 = no maximum (nkademlia)
+static int kad_bucket_size_host(const ovs_params& P, int index)
+{
+    if (P.bucketType == 1) return 0;
+    if (P.bucketType == 2) {
+        const int extra = P.extraNodesFinalBucket == 0 ? KEYBITS : P.extraNodesFinalBucket;   // 146-148
+        const int limit = (int)(std::log((double)extra) / std::log(2.0));
+        int offset = limit - (KEYBITS - (index + 1));
+        if (offset > 0) {
+            offset = 1 << offset;
+            if (offset > P.k) return offset;
+        }
+    }
+    return P.k;
+}
+
+int32_t ovs_kad_num_buckets(const ovs_params* p)
+{
+    if (!p || p->b < 1 || p->b > 5) return -1;
+    return ((1 << p->b) - 1) * (KEYBITS / p->b);      // Kademlia.cc:176
+}
+
+ovs_status ovs_kad_load_tables_csr(ovs_ctx* c, const ovs_key160* ids, uint64_t n, const double* xy,
+                                   const uint32_t* siblings, const uint64_t* bucket_off, const uint32_t* bucket_nodes,
+                                   uint32_t flags)
+{
+    if (!c || !ids || !xy || !siblings || !bucket_off) return OVS_EINVAL;
+    if (flags & OVS_DEVICE_PTRS) return fail(c, OVS_ENOTSUP, "explicit tables are taken from host memory");
+    HIPCHK(c, hipSetDevice(c->device));
+    free_tables(c);
+    free_kad_shard(c);
+    const ovs_params& P = c->P;
+    if (P.overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "params.overlay is not Kademlia");
+    if (P.b < 1 || P.b > 5) return fail(c, OVS_ENOTSUP, "Kademlia b must be 1..5 (numBuckets <= 992)");
+    if (P.bucketType < 0 || P.bucketType > 2) return fail(c, OVS_EINVAL, "bucketType must be 0..2 (kademlia, nkademlia, nr128)");
+    // routingBucketSize counts indices as if b = 1 (Kademlia.cc:400-406): for b > 1 the indices past
+    // 159 get sizes 2^8 .. 2^30 and then (int)pow(2, >= 31) -- undefined, not followed
+    if (P.bucketType == 2 && P.b != 1) return fail(c, OVS_ENOTSUP, "nr128 buckets need b = 1");
+    if (P.bucketType == 2 && (P.extraNodesFinalBucket < 0 || P.extraNodesFinalBucket > 511))
+        return fail(c, OVS_ENOTSUP, "nr128: extraNodesFinalBucket must be 0..511");
+    if (P.k < 1 || P.k > KMAX || P.s < 1 || 5 * P.s > 64)
+        return fail(c, OVS_ENOTSUP, "Kademlia k must be 1..16 and 5*s <= 64");
+    if (n == 0 || n >= 0xFFFFFFFFull) return fail(c, OVS_EINVAL, "network size out of range");
+    const int nb = ovs_kad_num_buckets(&P);
+    const uint64_t dir = n * (uint64_t)nb;
+    if (bucket_off[0] != 0) return fail(c, OVS_EINVAL, "bucket_off[0] must be 0");
+    for (uint64_t j = 0; j < dir; ++j)
+        if (bucket_off[j + 1] < bucket_off[j]) return fail(c, OVS_EINVAL, "bucket_off must not decrease");
+    const uint64_t total = bucket_off[dir];
+    if (total >= 0xFFFFFFFFull) return fail(c, OVS_ENOTSUP, "more than 2^32 - 1 bucket members");
+    if (total && !bucket_nodes) return fail(c, OVS_EINVAL, "bucket_nodes is NULL");
+    ovs_status s = upload_nodes(c, ids, n, xy, false);
+    if (s != OVS_OK) { free_tables(c); return s; }
+    const uint64_t S5 = 5ull * (uint64_t)P.s;
+    std::vector<uint32_t> off32(dir + 1);
+    for (uint64_t j = 0; j <= dir; ++j) off32[j] = (uint32_t)bucket_off[j];
+    std::vector<int> caps(nb);
+    for (int m = 0; m < nb; ++m) caps[m] = kad_bucket_size_host(P, m);
+    DevBufs d;
+    uint32_t *dsib = nullptr, *doff = nullptr, *dmem = nullptr;
+    if (d.get(&dsib, n * S5) != hipSuccess || d.get(&doff, dir + 1) != hipSuccess || d.get(&dmem, total) != hipSuccess) {
+        free_tables(c);
+        return fail(c, OVS_ENOMEM, "CSR Kademlia tables: device allocation failed");
+    }
+    hipError_t e = hipMemcpy(dsib, siblings, sizeof(uint32_t) * n * S5, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(doff, off32.data(), sizeof(uint32_t) * (dir + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess && total) e = hipMemcpy(dmem, bucket_nodes, sizeof(uint32_t) * total, hipMemcpyHostToDevice);
+    uint32_t bad_node = 0, bad_code = 0;
+    if (e == hipSuccess)
+        e = kad_build_general(c->recs, c->xy, (uint32_t)n, P.k, P.s, P.b, caps.data(), dsib, doff, dmem, total, c->kad,
+                              &bad_node, &bad_code, c->stream);
+    if (e == hipErrorInvalidValue && bad_code) {
+        static const char* why[] = {"", "sibling index out of range or the node itself", "sibling listed twice",
+                                    "bucket holds more than routingBucketSize(i) entries",
+                                    "bucket member out of range or the node itself",
+                                    "bucket member in the wrong bucket (routingBucketIndex(member) != bucket index)",
+                                    "bucket member listed twice", "node is both sibling and bucket member"};
+        free_tables(c);
+        char m[192];
+        std::snprintf(m, sizeof m, "CSR Kademlia tables of node %u: %s", bad_node, bad_code < 8 ? why[bad_code] : "?");
+        return fail(c, OVS_EINVAL, m);
+    }
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "CSR Kademlia table build"); }
+    c->overlay = OVS_OVERLAY_KADEMLIA;
+    return OVS_OK;
+}
+
+ovs_status ovs_kad_export_csr(ovs_ctx* c, uint32_t* siblings, uint64_t* bucket_off, uint32_t* bucket_nodes, uint64_t cap,
+                              uint64_t* total)
+{
+    if (!c || !siblings || !bucket_off || !total || (cap && !bucket_nodes)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "export needs the whole network");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t n = c->n, S5 = 5ull * (uint64_t)c->P.s;
+    const KadTables& t = c->kad;
+    if (t.general) {
+        const uint64_t dir = n * (uint64_t)t.nb;
+        std::vector<uint32_t> off32(dir + 1);
+        HIPCHK(c, hipMemcpyAsync(siblings, t.sib, sizeof(uint32_t) * n * S5, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(off32.data(), t.goff, sizeof(uint32_t) * (dir + 1), hipMemcpyDeviceToHost, c->stream));
+        const uint64_t ncopy = std::min<uint64_t>(cap, t.gtotal);
+        if (ncopy)
+            HIPCHK(c, hipMemcpyAsync(bucket_nodes, t.gidx, sizeof(uint32_t) * ncopy, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (uint64_t j = 0; j <= dir; ++j) bucket_off[j] = off32[j];
+        *total = t.gtotal;
+        return OVS_OK;
+    }
+    // the 160-bucket tables, converted
+    const uint64_t k = (uint64_t)t.k;
+    std::vector<uint8_t> bc(n * KEYBITS);
+    std::vector<uint32_t> bn(n * KEYBITS * k);
+    hipError_t e = kad_export(t, (uint32_t)n, siblings, bc.data(), bn.data(), c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "kademlia export");
+    uint64_t w = 0;
+    bucket_off[0] = 0;
+    for (uint64_t j = 0; j < n * KEYBITS; ++j) {
+        for (uint64_t q = 0; q < bc[j]; ++q, ++w)
+            if (w < cap) bucket_nodes[w] = bn[j * k + q];
+        bucket_off[j + 1] = w;
+    }
+    *total = w;
     return OVS_OK;
 }
 
@@ -891,6 +1023,7 @@ ovs_status ovs_kad_export(ovs_ctx* c, uint32_t* siblings, uint8_t* bucket_count,
     if (!c || !siblings || !bucket_count || !bucket_nodes) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
     if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "export needs the whole network");
+    if (c->kad.general) return fail(c, OVS_ENOTSUP, "CSR tables: ovs_kad_export_csr");
     HIPCHK(c, hipSetDevice(c->device));
     hipError_t e = kad_export(c->kad, (uint32_t)c->n, siblings, bucket_count, bucket_nodes, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia export");
@@ -1093,6 +1226,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
                         "visitOnlyOnce, numSiblings=1 (the Koorde defaults)");
     } else if (c->P.routingType != 0 && c->P.routingType != 3) {
         return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative / exhaustive-iterative");
+    } else if (c->kad.general && c->P.routingType != 0) {
+        return fail(c, OVS_ENOTSUP, "CSR (b > 1 / nr128 / nkademlia) tables route with routingType = iterative");
     } else if (c->P.numSiblings != 1) {
         return fail(c, OVS_ENOTSUP, "the one-way route implements numSiblings = 1 (LookupCall: ovs_lookup_batch)");
     } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
@@ -1163,6 +1298,9 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
                            dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err);
         hipFree(dres);
         if (e == hipSuccess && cap_err) return fail(c, OVS_ENOTSUP, "a lookup exceeded the kernel's capacity (64 timed-out nodes)");
+    } else if (c->kad.general) {
+        e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc, s,
+                              nullptr);
     } else {
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
                       c->num_cu, s);
@@ -1210,6 +1348,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     const bool kad_exh = !chord && P.routingType == 3;
     if (P.routingType != 0 && !kad_exh)
         return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative (Kademlia: also exhaustive-iterative)");
+    if (kad_exh && c->kad.general)
+        return fail(c, OVS_ENOTSUP, "CSR (b > 1 / nr128 / nkademlia) tables: LookupCalls with routingType = iterative");
     if (kad_exh && ns > P.lookupRedundantNodes)
         return fail(c, OVS_EINVAL, "With EXHAUSTIVE_ITERATIVE_ROUTING numRedundantNodes must be >= numSiblings!");
     HIPCHK(c, hipSetDevice(c->device));
@@ -1279,6 +1419,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), P.lookupRedundantNodes, ns, false, dk, ds,
                            n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err);
         if (e == hipSuccess && cap_err) e = hipErrorNotSupported;
+    } else if (c->kad.general) {
+        e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, s, dsib);
     } else {
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
                       dsib);
@@ -1310,6 +1452,7 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "refresh lookups: Kademlia only");
     if (c->kad.lo != 0 || c->kad.hi != c->n)
         return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: refresh lookups need the whole network");
+    if (c->kad.general) return fail(c, OVS_ENOTSUP, "refresh lookups run on the 160-bucket kademlia tables");
     if (R < 1 || R > 64) return fail(c, OVS_ENOTSUP, "refresh lookups implement redundantNodes 1..64");
     const ovs_params& P = c->P;
     if (P.hopCountMax < 1) return fail(c, OVS_ENOTSUP, "refresh lookups need hopCountMax >= 1");
@@ -1416,6 +1559,7 @@ ovs_status ovs_kad_maintenance_round(ovs_ctx* c, const uint32_t* nodes, uint64_t
     if (!c || (m && !nodes)) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
     if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "maintenance rounds need the whole network");
+    if (c->kad.general) return fail(c, OVS_ENOTSUP, "maintenance rounds run on the 160-bucket kademlia tables");
     const ovs_params& P = c->P;
     if (P.routingType != 0) return fail(c, OVS_ENOTSUP, "maintenance rounds run iterative refresh lookups");
     if (P.hopCountMax < 1) return fail(c, OVS_ENOTSUP, "refresh lookups need hopCountMax >= 1");
@@ -1574,6 +1718,7 @@ ovs_status ovs_kad_refresh_keys(ovs_ctx* c, const uint32_t* nodes, uint64_t m, c
     if (!c || !count || (m && !nodes) || (cap && (!keys || !src))) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "bucket refresh: Kademlia network needed");
     if (c->kad.lo != 0 || c->kad.hi != c->n) return fail(c, OVS_ESTATE, "bucket refresh needs the whole network");
+    if (c->kad.general) return fail(c, OVS_ENOTSUP, "refresh keys are generated for the 160-bucket kademlia tables");
     HIPCHK(c, hipSetDevice(c->device));
     const bool dev = flags & OVS_DEVICE_PTRS;
     hipStream_t s = dev ? (hipStream_t)stream : c->stream;
@@ -1653,6 +1798,9 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
     if (c->overlay == OVS_OVERLAY_CHORD)
         e = launch_chord_find_node(chord_view(c), c->ideal, dn, dk, n, numRedundantNodes, numSiblings, dout, max_out,
                                    dc, dsb, s);
+    else if (c->kad.general)
+        e = kad_find_node_general(c->kad, (uint32_t)c->n, dn, dk, n, numRedundantNodes, numSiblings, dout, max_out, dc,
+                                  dsb, s);
     else
         e = kad_find_node(c->kad, (uint32_t)c->n, c->P, dn, dk, n, numRedundantNodes, numSiblings, dout,
                           max_out, dc, dsb, s);

@@ -65,7 +65,8 @@ class Params(C.Structure):
         ("jitter", C.c_double), ("constantDelay", C.c_double), ("datarate", C.c_double),
         ("accessDelay", C.c_double), ("kadSeed", C.c_uint64),
         ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
-        ("useSucList", C.c_int32), ("pad0", C.c_int32), ("cacheTTL", C.c_double),
+        ("useSucList", C.c_int32), ("bucketType", C.c_int32), ("cacheTTL", C.c_double),
+        ("globalNodeLimit", C.c_int32), ("extraNodesFinalBucket", C.c_int32),
     ]
 
     @classmethod
@@ -198,6 +199,9 @@ def lib() -> C.CDLL:
         "ovs_koorde_export": ([vp, vp, vp, vp], C.c_int),
         "ovs_koorde_find_node_batch": ([vp, vp, vp, vp, vp, u64], C.c_int),
         "ovs_kad_load_tables": ([vp, vp, u64, vp, vp, vp, vp, u32], C.c_int),
+        "ovs_kad_num_buckets": ([vp], i32),
+        "ovs_kad_load_tables_csr": ([vp, vp, u64, vp, vp, vp, vp, u32], C.c_int),
+        "ovs_kad_export_csr": ([vp, vp, vp, vp, u64, C.POINTER(u64)], C.c_int),
         "ovs_epichord_load": ([vp, vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32], C.c_int),
         "ovs_epichord_find_node_batch": ([vp, vp, vp, vp, vp, u64, i32, vp, vp, u32, vp, vp, u32, vp], C.c_int),
         "ovs_kad_export": ([vp, vp, vp, vp], C.c_int),
@@ -448,6 +452,33 @@ class KbrEngine:
         self._chk(self._L.ovs_kad_load_tables(self._h, _ptr(ids), len(ids), *[_ptr(a) for a in arrs], 0),
                   "ovs_kad_load_tables")
         self.n, self.overlay = len(ids), OVERLAY_KADEMLIA
+
+    def kad_load_tables_csr(self, ids, xy, siblings, bucket_off, bucket_nodes):
+        """Kademlia tables in CSR form (ovs_kad_load_tables_csr): any b / bucketType of the current
+        params -- siblings (n, 5s), bucket_off (n * numBuckets + 1) uint64, bucket_nodes (LRU order)."""
+        ids = keys_array(ids)
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+                ((xy, np.float64), (siblings, np.uint32), (bucket_off, np.uint64), (bucket_nodes, np.uint32))]
+        self._chk(self._L.ovs_kad_load_tables_csr(self._h, _ptr(ids), len(ids), *[_ptr(a) for a in arrs], 0),
+                  "ovs_kad_load_tables_csr")
+        self.n, self.overlay = len(ids), OVERLAY_KADEMLIA
+
+    def kad_num_buckets(self) -> int:
+        p = self.get_params()
+        return int(self._L.ovs_kad_num_buckets(C.byref(p)))
+
+    def kad_tables_csr(self):
+        """(siblings (n, 5s), bucket_off (n * numBuckets + 1), bucket_nodes) of the loaded tables."""
+        p = self.get_params()
+        nb = self.kad_num_buckets()
+        sib = np.empty((self.n, 5 * p.s), dtype=np.uint32)
+        off = np.empty(self.n * nb + 1, dtype=np.uint64)
+        tot = C.c_uint64(0)
+        self._chk(self._L.ovs_kad_export_csr(self._h, _ptr(sib), _ptr(off), None, 0, C.byref(tot)), "ovs_kad_export_csr")
+        nodes = np.empty(max(int(tot.value), 1), dtype=np.uint32)
+        self._chk(self._L.ovs_kad_export_csr(self._h, _ptr(sib), _ptr(off), _ptr(nodes), len(nodes), C.byref(tot)),
+                  "ovs_kad_export_csr")
+        return sib, off, nodes[:int(tot.value)]
 
     def chord_fingers(self) -> np.ndarray:
         out = np.empty((self.n, 160), dtype=np.uint32)
