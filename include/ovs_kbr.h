@@ -65,8 +65,9 @@ enum {
     OVS_LOOKUP_RPC_TIMEOUT = 2,  /* RTT >= rpcUdpTimeout (BaseRpc.cc:191-211) */
     OVS_LOOKUP_HOPMAX = 3,       /* hops >= hopCountMax (IterativeLookup.cc:1074-1086) */
     OVS_LOOKUP_NO_NEXT = 4,      /* no unvisited next hop (IterativeLookup.cc:1147-1168) */
-    OVS_LOOKUP_BROKEN = 5        /* Chord successor list broken (Chord.cc:615-620, 671-672); Koorde::findNode
+    OVS_LOOKUP_BROKEN = 5,       /* Chord successor list broken (Chord.cc:615-620, 671-672); Koorde::findNode
                                     throws (Koorde.cc:490-493 bounding error, 756-760 invalid start key) */
+    OVS_LOOKUP_INVALID = 6       /* recursive LookupCall answered without the siblings flag (RecursiveLookup.cc:120-139) */
 };
 
 enum { OVS_OVERLAY_CHORD = 1, OVS_OVERLAY_KADEMLIA = 2, OVS_OVERLAY_KOORDE = 3, OVS_OVERLAY_EPICHORD = 4 };
@@ -121,6 +122,7 @@ typedef struct ovs_params {
     double  cacheTTL;                   /* **.epichord.cacheTTL = 120 s (ABI 8) */
     int32_t globalNodeLimit;            /* **.kademlia.globalNodeLimit = 1000 (nkademlia; ABI 10) */
     int32_t extraNodesFinalBucket;      /* **.kademlia.extraNodesFinalBucket = 0 (nr128; 0 = keyLength) */
+    double  rpcKeyTimeout;              /* **.rpcKeyTimeout = 10 s: routed RPCs (recursive LookupCalls; ABI 10) */
 } ovs_params;
 
 /* Result of one one-way KBR test lookup (KBRTestApp with kbrOneWayTest). */

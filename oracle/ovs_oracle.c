@@ -243,6 +243,7 @@ static void params_common(orc_params* p)
     p->bucketType = 0;           /* default.ini:209 "kademlia" */
     p->globalNodeLimit = 1000;   /* default.ini:210 */
     p->extraNodesFinalBucket = 0;/* default.ini:211 (0 = key length) */
+    p->rpcKeyTimeout = 10.0;     /* default.ini:484 */
 }
 void orc_params_chord_default(orc_params* p) { params_common(p); }
 void orc_params_koorde_default(orc_params* p)
@@ -1886,62 +1887,155 @@ static void run_lookup(const orc_net* net, const OKey* key, uint32_t S, orc_rout
 }
 
 /* ===================================================================== */
-/* 7. Recursive routing of a one-way route message (SEMI_RECURSIVE and   */
-/*    FULL_RECURSIVE behave identically for a one-way KBRTestMessage:    */
-/*    they differ only in how RPC responses travel back).                */
-/*    recordRoute = false, routeMsgAcks = false (default.ini:398, 434).  */
+/* 7. Recursive routing (SEMI_RECURSIVE / FULL_RECURSIVE).  recordRoute =  */
+/*    false, routeMsgAcks = false (default.ini:398, 434).  A one-way      */
+/*    KBRTestMessage travels the same way under both: they differ only in */
+/*    how an RPC response travels back (BaseOverlay.cc:1802-1818).        */
 /* ===================================================================== */
-static void run_recursive(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out, uint32_t* hopseq)
+typedef struct {
+    uint32_t node;     /* the node the message was delivered to */
+    int hops;          /* route hops */
+    int status;        /* 0 delivered, else OVS_LOOKUP_* of the drop */
+    int64_t t;         /* delivery time */
+    int64_t tx;        /* the delivering node's tx queue (busy until) after its R/Kademlia hook */
+} RecEnd;
+
+/* the KademliaRoutingInfoMessage of R/Kademlia's hook at node x (Kademlia.cc:1031-1045):
+ * findNode(key, k, s) nodes, KADEMLIAROUTINGINFO_L = TYPE_L + NODEHANDLE_L + KEY_L + n *
+ * MARKEDNODEHANDLE_L = 376 + 216 n bits (KademliaMessage.msg:27-37), + UDP/IP 28 B */
+static int32_t kad_info_bytes(const orc_net* net, uint32_t x, const OKey* key)
+{
+    NVec v;
+    kad_findNode(net, x, key, net->p.k, net->p.s, &v);
+    return 47 + 27 * v.size + 28;
+}
+
+/* One BaseRouteMessage from `from` (its srcNode) towards key, leaving `from` at t0 with from's
+ * tx queue busy until tx0.  nsFrom: numSiblings of the first sendToKey (the route RPC of a
+ * LookupCall passes the call's own, BaseOverlay.cc:1764-1775); forwarding hops use 1 (1003).
+ * At every node: delivery when sibling (907-914, not at the source), findNode(key,
+ * recNumRedundantNodes, numSiblings), drop on an empty result or hopCountMax (1449-1488),
+ * loop detection (1497-1521), local delivery when the first usable candidate is the node itself
+ * (1555-1570), else sendRouteMessage (1107-1146) with the node's queue idle on arrival.
+ * R/Kademlia (recursiveRoutingHook, Kademlia.cc:1022-1057, altRecMode = false): every node the
+ * message reaches other than its srcNode first sends a KademliaRoutingInfoMessage to the srcNode
+ * -- at a forwarding hop before sendRouteMessage (BaseOverlay.cc:1577-1579), at the delivering
+ * node before the message is handled (978-984) -- so that message leaves the node's queue first.
+ * Its routingAdd calls change tables the batch holds fixed. */
+static RecEnd rec_route(const orc_net* net, const OKey* key, uint32_t from, int nsFrom, int32_t bytes, int64_t t0,
+                        int64_t tx0, uint32_t* hopseq)
 {
     const orc_params* p = &net->p;
-    uint32_t cur = S, lastHop = S;      /* routeCtrlInfo->setLastHop(thisNode) at the source (BaseOverlay.cc:1400) */
+    const int hook = net->type == NET_KAD;
+    RecEnd e;
+    e.node = NONE; e.hops = 0; e.status = 0; e.t = t0; e.tx = tx0;
+    uint32_t cur = from, lastHop = from;   /* routeCtrlInfo->setLastHop(thisNode) (BaseOverlay.cc:1400) */
     int hopCount = 0;
-    int64_t t = 0;
-    out->responsible = NONE; out->hops = 0; out->one_way_hops = 0; out->latency_ns = -1;
+    int64_t t = t0, tx = tx0;
     for (;;) {
         int err = 0;
-        if (cur != S) {
-            /* handleBaseOverlayMessage, OVERLAYROUTE (BaseOverlay.cc:907-914): deliver when sibling */
-            if (ov_isSiblingFor(net, cur, cur, key, 1, &err)) break;
+        const int ns = cur == from ? nsFrom : 1;
+        if (cur != from) {
+            tx = 0;
+            if (ov_isSiblingFor(net, cur, cur, key, 1, &err)) {
+                if (hook) calc_delay(net, cur, from, kad_info_bytes(net, cur, key), t, &tx);
+                break;
+            }
         }
-        /* sendToKey, recursive branch (BaseOverlay.cc:1445-1582) */
         NVec nextHops;
-        if (ov_findNode(net, cur, key, p->recNumRedundantNodes, p->numSiblings, &nextHops) < 0) {
-            out->status = 5;            /* Chord throws: successor list broken (Chord.cc:615-620) */
-            return;
+        if (ov_findNode(net, cur, key, p->recNumRedundantNodes, ns, &nextHops) < 0) {
+            e.status = 5;               /* Chord throws: successor list broken (Chord.cc:615-620) */
+            return e;
         }
-        if (nextHops.size == 0) { out->status = 4; return; }           /* 1449-1461: dropped */
-        if (hopCount >= p->hopCountMax) { out->status = 3; return; }   /* 1464-1488: dropped */
-        const int isSibling = ov_isSiblingFor(net, cur, cur, key, p->numSiblings, &err);
+        if (nextHops.size == 0) { e.status = 4; return e; }            /* 1449-1461: dropped */
+        if (hopCount >= p->hopCountMax) { e.status = 3; return e; }    /* 1464-1488: dropped */
+        const int isSibling = ov_isSiblingFor(net, cur, cur, key, ns, &err);
         uint32_t next = NONE;
         for (int i = 0; next == NONE && i < nextHops.size; ++i) {      /* 1502-1516 loop detection */
             const uint32_t h = nextHops.v[i];
             if ((h == lastHop && h != cur) ||                          /* back to the last hop */
-                (h == S && cur != S) ||                                /* never to the source */
+                (h == from && cur != from) ||                          /* never to the source */
                 (h == cur && !isSibling))                              /* self without being sibling */
                 continue;
             next = h;
         }
-        if (next == NONE) { out->status = 4; return; }                 /* 1518-1538: no useful next hop */
+        if (next == NONE) { e.status = 4; return e; }                  /* 1518-1538: no useful next hop */
         if (next == cur) {                                             /* 1555-1570: this node is responsible */
             if (isSibling && !err) break;
-            out->status = 5;
-            return;
+            e.status = 5;
+            return e;
         }
-        /* sendRouteMessage (1107-1146): hopCount + 1, one UDP message from cur */
-        int64_t tx = 0;
-        t += calc_delay(net, cur, next, p->routeBytes, t, &tx);
+        if (hook && cur != from) calc_delay(net, cur, from, kad_info_bytes(net, cur, key), t, &tx);
+        t += calc_delay(net, cur, next, bytes, t, &tx);
         if (hopseq && hopCount < p->hopCountMax) hopseq[hopCount] = next;
         ++hopCount;
         lastHop = cur;
         cur = next;
     }
-    /* KBRTestApp::deliver -> evaluateData(simTime() - creationTime, hopCount) (KBRTestApp.cc:404-410) */
+    e.node = cur; e.hops = hopCount; e.t = t; e.tx = tx;
+    return e;
+}
+
+/* a one-way KBRTestMessage: sendToKey(key, msg, numSiblings = 1) (BaseOverlay.cc:1357) ->
+ * KBRTestApp::deliver -> evaluateData(simTime() - creationTime, hopCount) (KBRTestApp.cc:404-410) */
+static void run_recursive(const orc_net* net, const OKey* key, uint32_t S, orc_route_out* out, uint32_t* hopseq)
+{
+    const RecEnd e = rec_route(net, key, S, net->p.numSiblings, net->p.routeBytes, 0, 0, hopseq);
+    out->responsible = NONE; out->hops = 0; out->one_way_hops = 0; out->latency_ns = -1;
+    out->status = (uint8_t)e.status;
+    if (e.status) return;
+    out->responsible = e.node;
+    out->hops = (uint16_t)e.hops;
+    out->one_way_hops = (uint8_t)e.hops;
+    out->latency_ns = e.t;
+}
+
+/* A LookupCall with recursive routing: BaseOverlay::lookupRpc -> RecursiveLookup::lookup
+ * (BaseOverlay.cc:1938-1969, RecursiveLookup.cc:52-70): FindNodeCall{key, numRedundantNodes =
+ * lookupRedundantNodes (BaseOverlay.cc:162), numSiblings} routed as a route RPC (136 B: BASEROUTE_L
+ * 424 + FINDNODECALL_L 440 bits + UDP/IP); the delivering node D answers findNodeRpc (1841-1915):
+ * findNode(key, numRedundantNodes, numSiblings) and the flag isSiblingFor(D, key, numSiblings).
+ * The response (internalSendRpcResponse, 1779-1822): semi-recursive -> UDP from D to the source;
+ * full-recursive -> routed from D to the source's key (numSiblings 1), lost when it ends at another
+ * node; D = the source -> zero delay (SimpleUDP.cc:322).  RecursiveLookup::handleRpcResponse
+ * (RecursiveLookup.cc:120-139): valid = flag && nodes; siblings = the response's nodes; hops =
+ * getMinHops() = 0.  A lost or dropped call times out after rpcKeyTimeout (BaseRpc.cc:201-205) and
+ * is resent once (lookupRpc passes retries = 1; the nonce stays, so a late first response still
+ * counts): it fails from 2 * rpcKeyTimeout on.  Statuses: the drop's (3 / 4 / 5), 2 for a lost
+ * response or a response after 2 * rpcKeyTimeout, 6 for an answer without the siblings flag. */
+static void run_recursive_call(const orc_net* net, const OKey* key, uint32_t S, int numSiblings, orc_lookup_out* out,
+                               uint32_t* sib)
+{
+    const orc_params* p = &net->p;
+    const int nslots = numSiblings ? numSiblings : 1;
+    for (int i = 0; i < nslots; ++i) sib[i] = NONE;
+    out->num_siblings = 0; out->hops = 0; out->is_valid = 0; out->latency_ns = -1;
+    const RecEnd d = rec_route(net, key, S, numSiblings, 53 + 55 + 28, 0, 0, NULL);
+    if (d.status) { out->status = (uint8_t)d.status; return; }
+    NVec res;
+    int err = 0;
+    if (ov_findNode(net, d.node, key, p->lookupRedundantNodes, numSiblings, &res) < 0) res.size = 0;
+    const int flag = ov_isSiblingFor(net, d.node, d.node, key, numSiblings, &err);
+    int64_t T = d.t;
+    if (d.node != S) {
+        const int32_t resp = p->respBaseBytes + p->respPerNodeBytes * res.size;
+        if (p->routingType == 1) {
+            int64_t tx = d.tx;
+            T += calc_delay(net, d.node, S, resp, d.t, &tx);
+        } else {
+            const RecEnd r = rec_route(net, &net->ids[S], d.node, 1, 53 + resp, d.t, d.tx, NULL);
+            if (r.status || r.node != S) { out->status = 2; return; }
+            T = r.t;
+        }
+    }
+    if (T >= 2 * simtime(p->rpcKeyTimeout, p->simtimeRound)) { out->status = 2; return; }
+    if (!flag || res.size == 0) { out->status = 6; return; }
+    const int cnt = res.size < nslots ? res.size : nslots;
+    for (int i = 0; i < cnt; ++i) sib[i] = res.v[i];
+    out->num_siblings = (uint32_t)res.size;
     out->status = 0;
-    out->responsible = cur;
-    out->hops = (uint16_t)hopCount;
-    out->one_way_hops = (uint8_t)hopCount;
-    out->latency_ns = t;
+    out->is_valid = 1;
+    out->latency_ns = T;
 }
 
 uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t* src, uint64_t n,
@@ -1985,7 +2079,8 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
     if (numSiblings < 0 || numSiblings > 16) { set_err("numSiblings must be 0..16"); return -1; }
     if (numSiblings == 0 && net->type == NET_KOORDE) { set_err("numSiblings = 0: Chord and Kademlia only"); return -1; }
-    if (net->p.routingType != 0 && net->p.routingType != 3) { set_err("LookupCall: iterative routing only"); return -1; }
+    if (net->p.routingType < 0 || net->p.routingType > 3) { set_err("LookupCall: routingType 0..3"); return -1; }
+    if (net->type == NET_KOORDE && net->p.routingType != 0) { set_err("Koorde: iterative routing only"); return -1; }
     const int exh = net->p.routingType == 3 ? net->p.lookupRedundantNodes : 0;
     if (exh && (net->type != NET_KAD || numSiblings > exh)) {
         set_err("exhaustive-iterative: Kademlia, numSiblings <= lookupRedundantNodes (IterativeLookup.cc:714-719)");
@@ -1999,8 +2094,11 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
         OKey k = ok_from(&keys[i]);
         orc_route_out dummy;
         /* numSiblings = 0 (an exact-key lookup) keeps a one-slot sibling vector (start() 149) */
-        run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i],
-                   siblings + (size_t)i * (numSiblings ? numSiblings : 1), exh, NULL, NULL, NULL, NULL, 0);
+        if (net->p.routingType == 1 || net->p.routingType == 2)
+            run_recursive_call(net, &k, src[i], numSiblings, &out[i], siblings + (size_t)i * (numSiblings ? numSiblings : 1));
+        else
+            run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i],
+                       siblings + (size_t)i * (numSiblings ? numSiblings : 1), exh, NULL, NULL, NULL, NULL, 0);
     }
     (void)nthreads;
     return g_cap_fail ? -1 : numSiblings;

@@ -82,6 +82,7 @@ typedef struct {
     int32_t bucketType;
     int32_t globalNodeLimit;          /* = 1000 */
     int32_t extraNodesFinalBucket;    /* = 0 */
+    double  rpcKeyTimeout;            /* default.ini:484 = 10 s: a routed RPC (recursive LookupCalls) */
 } orc_params;
 
 void orc_params_chord_default(orc_params* p);

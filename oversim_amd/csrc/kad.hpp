@@ -142,6 +142,13 @@ hipError_t kad_build_general(const KeyRec* recs, const double2* xy, uint32_t n, 
 hipError_t kad_route_general(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
                              const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
                              ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, hipStream_t st, uint32_t* sibs);
+// recursive routing (R/Kademlia, kad_general.hip) over either table form: one-way routes (sibs ==
+// nullptr; hopseq optional) or LookupCalls with numSiblings lookup_ns (semi- / full-recursive
+// response as P.routingType says); key_timeout = rpcKeyTimeout in ns
+hipError_t kad_route_recursive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
+                               const DelayConsts& DC, int64_t key_timeout, int lookup_ns, const K160* qkeys,
+                               const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* sibs,
+                               hipStream_t st);
 hipError_t kad_find_node_general(const KadTables& t, uint32_t n, const uint32_t* node, const K160* keys, uint64_t nq,
                                  int numRedundant, int numSiblings, uint32_t* out_nodes, uint32_t max_out,
                                  uint8_t* out_count, uint8_t* out_sib, hipStream_t st);

@@ -165,6 +165,164 @@ __global__ void k_kadg_find_node(KadView V, KadGenView G, const uint32_t* __rest
     out_sib[i] = sb ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Recursive routing (R/Kademlia): semi- / full-recursive one-way routes and LookupCalls over either
+// table form.  One lane per message, hop by hop: BaseOverlay::sendToKey / handleBaseOverlayMessage
+// (BaseOverlay.cc:880-1004, 1380-1582) with Kademlia::recursiveRoutingHook (Kademlia.cc:1022-1057,
+// altRecMode off): every node the message reaches other than its source first sends the source a
+// KademliaRoutingInfoMessage (findNode(key, k, s) nodes, 47 + 27 n + 28 B), which leaves the
+// node's tx queue ahead of the route message.  LookupCalls: RecursiveLookup (RecursiveLookup.cc:
+// 52-139) -- a routed FindNodeCall (136 B), findNodeRpc at the delivering node, the response back
+// by UDP (semi) or routed to the source's key (full).  oracle: rec_route / run_recursive_call.
+
+constexpr int KREC_C = 16;     // result capacity: recNumRedundantNodes, lookupRedundantNodes, k, s <= 16
+
+struct KadRecCfg {
+    int hcm, recR, R, k, s;
+    int64_t keyTimeout2;       // 2 * rpcKeyTimeout (the call is resent once)
+};
+
+template <bool GEN, bool EX>
+__device__ __forceinline__ int krec_find(const KadView& V, const KadGenView& G, uint32_t c, const KadNode& r,
+                                         const K160& K, int numRedundant, bool sib, int ns, SVec<KREC_C>& res)
+{
+    if constexpr (GEN) return kadg_find_node<EX, KREC_C>(V, G, c, kad_nsib(r.meta), K, numRedundant, sib, ns, res);
+    else return kad_find_node_ins<KREC_C, EX>(V, c, resp_geo(r, K), K, numRedundant, sib, res, ns);
+}
+
+struct KRecEnd {
+    uint32_t node;
+    int hops, status;
+    int64_t t, tx;
+};
+
+// one BaseRouteMessage from `from` towards K, leaving at t0 with from's queue busy until tx0;
+// bwMsg = its serialisation time; nsFrom = numSiblings of the first sendToKey
+template <bool GEN, bool EX, bool RECORD>
+__device__ KRecEnd krec_walk(const KadView& V, const KadGenView& G, const DelayConsts& DC, const KadRecCfg& RC,
+                             const K160& K, uint32_t from, int nsFrom, int64_t bwMsg, int64_t t0, int64_t tx0,
+                             uint32_t* __restrict__ hopseq)
+{
+    KRecEnd e;
+    e.node = NONE; e.hops = 0; e.status = 0; e.t = t0; e.tx = tx0;
+    uint32_t cur = from, last = from;
+    int hops = 0;
+    int64_t t = t0, tx = tx0;
+    SVec<KREC_C> res;
+    // the hook's KademliaRoutingInfoMessage at node c: tx queue busy for its serialisation first
+    auto info = [&](uint32_t c, const KadNode& r) {
+        const bool sbs = kad_is_sibling(V, r, c, K, RC.s);
+        const int n = krec_find<GEN, EX>(V, G, c, r, K, RC.k, sbs, RC.s, res);
+        tx = (tx > t ? tx : t) + bw_ns(47 + 27 * n + 28, DC.datarate, DC.round);
+    };
+    for (;;) {
+        const KadNode r = load_node(V.nodes, cur);
+        const int ns = cur == from ? nsFrom : 1;
+        if (cur != from) {
+            tx = 0;                                   // a node's queue is idle when the message arrives
+            if (kad_is_sibling(V, r, cur, K, 1)) {    // delivery (BaseOverlay.cc:907-914), hook first
+                info(cur, r);
+                break;
+            }
+        }
+        const bool sb = kad_is_sibling(V, r, cur, K, ns);
+        const int n = krec_find<GEN, EX>(V, G, cur, r, K, RC.recR, sb, ns, res);
+        if (n == 0) { e.status = OVS_LOOKUP_NO_NEXT; return e; }           // 1449-1461
+        if (hops >= RC.hcm) { e.status = OVS_LOOKUP_HOPMAX; return e; }     // 1464-1488
+        uint32_t next = NONE;
+        for (int i = 0; i < KREC_C && next == NONE; ++i) {                   // loop detection 1502-1516
+            if (i >= n) break;
+            const uint32_t h = res.idx[i];
+            if ((h == last && h != cur) || (h == from && cur != from) || (h == cur && !sb)) continue;
+            next = h;
+        }
+        if (next == NONE) { e.status = OVS_LOOKUP_NO_NEXT; return e; }
+        if (next == cur) break;                                              // 1555-1570: responsible
+        if (cur != from) info(cur, r);
+        // sendRouteMessage (1107-1146) through the node's queue
+        const double2 b = V.xy[next];
+        const int64_t newTx = (tx > t ? tx : t) + bwMsg;
+        tx = newTx;
+        t = newTx + DC.access2 + coord_ns(r.x, r.y, b.x, b.y, DC.round) + bwMsg;
+        if (RECORD && hops < RC.hcm) hopseq[hops] = next;
+        ++hops;
+        last = cur;
+        cur = next;
+    }
+    e.node = cur; e.hops = hops; e.t = t; e.tx = tx;
+    return e;
+}
+
+// MODE 0: one-way route, 1: one-way route with the hop sequence, 2 / 3: LookupCall with a
+// semi- / full-recursive response
+template <bool GEN, bool EX, int MODE>
+__global__ __launch_bounds__(128) void k_kad_recursive(KadView V, KadGenView G, DelayConsts DC, KadRecCfg RC, int ns,
+                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
+                                                       uint64_t nq, ovs_route_out* __restrict__ out,
+                                                       uint32_t* __restrict__ hopseq, uint32_t* __restrict__ sib_out)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const K160 K = qkeys[q];
+    const uint32_t S = qsrc[q];
+    ovs_route_out o;
+    o.responsible = NONE; o.hops = 0; o.one_way_hops = 0; o.latency_ns = -1; o.status = 0;
+    if constexpr (MODE <= 1) {
+        const KRecEnd e = krec_walk<GEN, EX, MODE == 1>(V, G, DC, RC, K, S, 1, DC.bwRoute, 0, 0,
+                                                        hopseq + q * (uint64_t)RC.hcm);
+        o.status = (uint8_t)e.status;
+        if (!e.status) {
+            o.responsible = e.node;
+            o.hops = (uint16_t)e.hops;
+            o.one_way_hops = (uint8_t)e.hops;
+            o.latency_ns = e.t;
+        }
+    } else {
+        const int nslots = ns ? ns : 1;
+        uint32_t* row = sib_out + q * (uint64_t)nslots;
+        for (int j = 0; j < nslots; ++j) row[j] = NONE;
+        // the routed FindNodeCall: BASEROUTE_L 424 + FINDNODECALL_L 440 bits + UDP/IP 28 B
+        const KRecEnd d = krec_walk<GEN, EX, false>(V, G, DC, RC, K, S, ns, bw_ns(53 + 55 + 28, DC.datarate, DC.round),
+                                                    0, 0, nullptr);
+        o.status = (uint8_t)d.status;
+        if (!d.status) {
+            // findNodeRpc at D (BaseOverlay.cc:1841-1915)
+            const KadNode rd = load_node(V.nodes, d.node);
+            const bool flag = kad_is_sibling(V, rd, d.node, K, ns);
+            SVec<KREC_C> res;
+            const int n = krec_find<GEN, EX>(V, G, d.node, rd, K, RC.R, flag, ns, res);
+            int64_t T = d.t;
+            bool lost = false;
+            if (d.node != S) {
+                const int32_t rb = DC.respBase + DC.respPerNode * n;
+                const double2 sxy = V.xy[S];
+                if (MODE == 2) {          // semi-recursive: UDP straight back (1807-1813)
+                    const int64_t bwr = bw_ns(rb, DC.datarate, DC.round);
+                    const int64_t newTx = (d.tx > d.t ? d.tx : d.t) + bwr;
+                    T = newTx + DC.access2 + coord_ns(rd.x, rd.y, sxy.x, sxy.y, DC.round) + bwr;
+                } else {                  // full-recursive: routed to the source's key (1814-1818)
+                    const K160 KS = node_key(V.nodes, S);
+                    const KRecEnd b = krec_walk<GEN, EX, false>(V, G, DC, RC, KS, d.node, 1,
+                                                                bw_ns(53 + rb, DC.datarate, DC.round), d.t, d.tx, nullptr);
+                    lost = b.status != 0 || b.node != S;
+                    T = b.t;
+                }
+            }
+            if (lost || T >= RC.keyTimeout2) {
+                o.status = OVS_LOOKUP_RPC_TIMEOUT;
+            } else if (!flag || n == 0) {
+                o.status = OVS_LOOKUP_INVALID;
+            } else {
+                for (int j = 0; j < KREC_C; ++j)
+                    if (j < n && j < nslots) row[j] = res.idx[j];
+                o.responsible = d.node;
+                o.latency_ns = T;     // hops: RecursiveLookup::getMinHops() = 0
+            }
+        }
+    }
+    out[q] = o;
+}
+
 inline unsigned gblocks(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 inline KadGenView gen_view(const KadTables& t) { return KadGenView{t.goff, t.gtop, t.gidx, t.gend, t.b, t.nb}; }
@@ -216,6 +374,34 @@ hipError_t kad_find_node_general(const KadTables& t, uint32_t n, const uint32_t*
     if (t.exact) { if (wide) KFN(true, 64); else KFN(true, 16); }
     else { if (wide) KFN(false, 64); else KFN(false, 16); }
 #undef KFN
+    return hipGetLastError();
+}
+
+hipError_t kad_route_recursive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
+                               const DelayConsts& DC, int64_t key_timeout, int lookup_ns, const K160* qkeys,
+                               const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* sibs,
+                               hipStream_t st)
+{
+    if (nq == 0) return hipSuccess;
+    if (P.routingType != 1 && P.routingType != 2) return hipErrorNotSupported;
+    if (P.recNumRedundantNodes < 1 || P.recNumRedundantNodes > KREC_C || P.lookupRedundantNodes < 1 ||
+        P.lookupRedundantNodes > KREC_C || t.k > KREC_C || t.s > KREC_C || P.hopCountMax < 0)
+        return hipErrorNotSupported;
+    const KadView V = kad_make_view(t, xy, n);
+    const KadGenView G = gen_view(t);
+    KadRecCfg RC;
+    RC.hcm = P.hopCountMax; RC.recR = P.recNumRedundantNodes; RC.R = P.lookupRedundantNodes; RC.k = t.k; RC.s = t.s;
+    RC.keyTimeout2 = 2 * key_timeout;
+    const dim3 grid(gblocks(nq, 128)), blk(128);
+    const int mode = sibs ? (P.routingType == 1 ? 2 : 3) : (hopseq ? 1 : 0);
+#define KR(gen, ex, m) hipLaunchKernelGGL((k_kad_recursive<gen, ex, m>), grid, blk, 0, st, V, G, DC, RC, lookup_ns, qkeys, qsrc, \
+                                          nq, out, hopseq, sibs)
+#define KRM(gen, ex) do { switch (mode) { case 0: KR(gen, ex, 0); break; case 1: KR(gen, ex, 1); break; \
+                                          case 2: KR(gen, ex, 2); break; default: KR(gen, ex, 3); } } while (0)
+    if (t.general) { if (t.exact) KRM(true, true); else KRM(true, false); }
+    else { if (t.exact) KRM(false, true); else KRM(false, false); }
+#undef KRM
+#undef KR
     return hipGetLastError();
 }
 

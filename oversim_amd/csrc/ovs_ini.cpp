@@ -319,6 +319,7 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         }
     }
     if (lookup(ovp + "rpcUdpTimeout", &v) && !to_seconds(unquote(v), &p->rpcUdpTimeout)) bad = "rpcUdpTimeout";
+    if (lookup(ovp + "rpcKeyTimeout", &v) && !to_seconds(unquote(v), &p->rpcKeyTimeout)) bad = "rpcKeyTimeout";
     const std::string udp = host + ".udp.";
     if (lookup(udp + "jitter", &v)) {
         double x; std::string u;
@@ -384,6 +385,7 @@ extern "C" void ovs_params_default(int32_t overlay, ovs_params* p)
     p->bucketType = 0;                  // default.ini:209 "kademlia"
     p->globalNodeLimit = 1000;          // default.ini:210
     p->extraNodesFinalBucket = 0;       // default.ini:211
+    p->rpcKeyTimeout = 10.0;            // default.ini:484
     if (overlay == OVS_OVERLAY_KOORDE) p->successorListSize = 16;   // default.ini:275
     if (overlay == OVS_OVERLAY_EPICHORD) p->successorListSize = 4;  // default.ini:159
     if (overlay == OVS_OVERLAY_KADEMLIA) {

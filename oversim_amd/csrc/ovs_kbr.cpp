@@ -193,6 +193,10 @@ ovs_status check_common(ovs_ctx* c, const ovs_params& P)
         return fail(c, OVS_EINVAL, "With EXHAUSTIVE_ITERATIVE_ROUTING numRedundantNodes must be >= numSiblings!");
     if ((P.routingType == 1 || P.routingType == 2) && P.recNumRedundantNodes < 1)
         return fail(c, OVS_EINVAL, "recNumRedundantNodes must be >= 1");
+    if ((P.routingType == 1 || P.routingType == 2) && P.overlay == OVS_OVERLAY_KADEMLIA &&
+        (P.recNumRedundantNodes > 16 || P.lookupRedundantNodes > 16 || !(P.rpcKeyTimeout >= 0)))
+        return fail(c, OVS_ENOTSUP, "recursive Kademlia implements recNumRedundantNodes, lookupRedundantNodes <= 16 "
+                                    "and rpcKeyTimeout >= 0");
     if (P.lookupParallelPaths != 1) return fail(c, OVS_ENOTSUP, "lookupParallelPaths != 1 not supported");
     if (P.lookupVerifySiblings || P.lookupMajoritySiblings)
         return fail(c, OVS_ENOTSUP, "lookupVerifySiblings/lookupMajoritySiblings not supported");
@@ -1224,10 +1228,11 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             return fail(c, OVS_ENOTSUP,
                         "Koorde route kernel implements lookupRedundantNodes=1, lookupParallelRpcs=1, merge off, "
                         "visitOnlyOnce, numSiblings=1 (the Koorde defaults)");
-    } else if (c->P.routingType != 0 && c->P.routingType != 3) {
-        return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative / exhaustive-iterative");
-    } else if (c->kad.general && c->P.routingType != 0) {
-        return fail(c, OVS_ENOTSUP, "CSR (b > 1 / nr128 / nkademlia) tables route with routingType = iterative");
+    } else if (c->P.routingType < 0 || c->P.routingType > 3) {
+        return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative / semi-recursive / "
+                                    "full-recursive / exhaustive-iterative");
+    } else if (c->kad.general && c->P.routingType == 3) {
+        return fail(c, OVS_ENOTSUP, "CSR (b > 1 / nr128 / nkademlia) tables: routingType iterative or recursive");
     } else if (c->P.numSiblings != 1) {
         return fail(c, OVS_ENOTSUP, "the one-way route implements numSiblings = 1 (LookupCall: ovs_lookup_batch)");
     } else if (c->kad.lo != 0 || c->kad.hi != c->n) {
@@ -1298,6 +1303,11 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
                            dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err);
         hipFree(dres);
         if (e == hipSuccess && cap_err) return fail(c, OVS_ENOTSUP, "a lookup exceeded the kernel's capacity (64 timed-out nodes)");
+    } else if (c->P.routingType == 1 || c->P.routingType == 2) {
+        // R/Kademlia: recursive routing with Kademlia's recursiveRoutingHook (kad_general.hip)
+        e = kad_route_recursive(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P),
+                                simtime_host(c->P.rpcKeyTimeout, c->P.simtimeRound), 1, dk, ds, n, dout, dhop, nullptr, s);
+        if (e == hipSuccess && drpc) e = hipMemsetAsync(drpc, 0, sizeof(uint32_t) * n, s);   // no FindNodeCalls
     } else if (c->kad.general) {
         e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc, s,
                               nullptr);
@@ -1336,8 +1346,10 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     const int32_t maxs = chord ? c->P.successorListSize : c->P.s;
     const int32_t ns = num_siblings < 0 ? maxs : num_siblings;
     if (ns > maxs) return fail(c, OVS_EINVAL, "numSiblings too big!");
-    if (ns == 0 && c->P.routingType != 0)
-        return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup) is implemented for iterative routing");
+    if (ns == 0 && c->P.routingType == 3)
+        return fail(c, OVS_ENOTSUP, "LookupCall with numSiblings = 0 (exact-key lookup): iterative or recursive routing");
+    if (ns == 0 && chord && c->P.routingType != 0)
+        return fail(c, OVS_ENOTSUP, "Chord LookupCall with numSiblings = 0 (exact-key lookup): iterative routing");
     if (ns == 0 && chord && c->P.hopCountMax < 1)
         return fail(c, OVS_ENOTSUP, "Chord exact-key LookupCalls need hopCountMax >= 1");
     if (ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall implements numSiblings <= 8");
@@ -1346,8 +1358,10 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     ovs_status st = check_common(c, P);
     if (st != OVS_OK) return st;
     const bool kad_exh = !chord && P.routingType == 3;
-    if (P.routingType != 0 && !kad_exh)
-        return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative (Kademlia: also exhaustive-iterative)");
+    const bool kad_rec = !chord && (P.routingType == 1 || P.routingType == 2);
+    if (P.routingType != 0 && !kad_exh && !kad_rec)
+        return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative (Kademlia: also recursive and "
+                                    "exhaustive-iterative)");
     if (kad_exh && c->kad.general)
         return fail(c, OVS_ENOTSUP, "CSR (b > 1 / nr128 / nkademlia) tables: LookupCalls with routingType = iterative");
     if (kad_exh && ns > P.lookupRedundantNodes)
@@ -1419,6 +1433,11 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), P.lookupRedundantNodes, ns, false, dk, ds,
                            n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err);
         if (e == hipSuccess && cap_err) e = hipErrorNotSupported;
+    } else if (kad_rec) {
+        // RecursiveLookup (RecursiveLookup.cc:52-139): a routed FindNodeCall, the response back by UDP
+        // (semi-recursive) or routed to the source's key (full-recursive)
+        e = kad_route_recursive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P),
+                                simtime_host(P.rpcKeyTimeout, P.simtimeRound), ns, dk, ds, n, dout, nullptr, dsib, s);
     } else if (c->kad.general) {
         e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, s, dsib);
     } else {

@@ -39,7 +39,7 @@ DEVICE_PTRS = 0x1
 NONE = 0xFFFFFFFF
 
 STATUS = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "ESTATE", 5: "ENOTSUP"}
-LOOKUP_STATUS = {0: "OK", 1: "TIMEOUT", 2: "RPC_TIMEOUT", 3: "HOPMAX", 4: "NO_NEXT", 5: "BROKEN"}
+LOOKUP_STATUS = {0: "OK", 1: "TIMEOUT", 2: "RPC_TIMEOUT", 3: "HOPMAX", 4: "NO_NEXT", 5: "BROKEN", 6: "INVALID"}
 
 
 class KbrError(RuntimeError):
@@ -66,7 +66,7 @@ class Params(C.Structure):
         ("accessDelay", C.c_double), ("kadSeed", C.c_uint64),
         ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
         ("useSucList", C.c_int32), ("bucketType", C.c_int32), ("cacheTTL", C.c_double),
-        ("globalNodeLimit", C.c_int32), ("extraNodesFinalBucket", C.c_int32),
+        ("globalNodeLimit", C.c_int32), ("extraNodesFinalBucket", C.c_int32), ("rpcKeyTimeout", C.c_double),
     ]
 
     @classmethod

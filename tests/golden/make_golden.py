@@ -12,7 +12,7 @@ generator in oversim_amd/workload.py; coordinates for N <= 15000 are records of
 the reference's simulations/nodes_2d_15000.xml.
 
 Each .npz records the SimTime rounding rule it was generated with.
-Run: python tests/golden/make_golden.py [--kad] [--rec] [--koorde] [--check: with --koorde verify the
+Run: python tests/golden/make_golden.py [--kad] [--rec] [--kadrec] [--koorde] [--check: with --koorde verify the
 committed Koorde vectors, alone the committed Kademlia vectors, instead of rewriting them]
 """
 from __future__ import annotations
@@ -160,7 +160,58 @@ def koorde_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, **kw):
     print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
 
 
+def kad_rec_case(name: str, n: int, seed: int, m: int, rnd: int = 1, hcm: int = 50, **kw):
+    """R/Kademlia: recursive one-way routes (semi- and full-recursive route a KBRTestMessage the same
+    way) and recursive LookupCalls (numSiblings 1, s, 0; semi- and full-recursive responses) over
+    the snapshot tables, checked against refmodel.KadRecursiveSim before writing."""
+    net = W.population(n, seed)
+    k1, s1 = W.lookups(net.ids, m // 2, seed + 1, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m // 2, seed + 2, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    out = {}
+    for rt in (1, 2):
+        p = kad_params(routingType=rt, simtimeRound=rnd, hopCountMax=hcm, **kw)
+        o = OracleNet("kademlia", net.ids, net.xy, p)
+        sib, cnt, nodes = o.kad_tables()
+        sim = refmodel.KadRecursiveSim(refmodel.KadTables(net.ids, sib, cnt, nodes, k=p.k, s=p.s), net.xy, k=p.k,
+                                       s=p.s, rec_redundant=p.recNumRedundantNodes, redundant=p.lookupRedundantNodes,
+                                       hop_max=hcm, rnd=bool(rnd))
+        if rt == 1:
+            r = o.route(keys, src, record_hops=True)
+            for i in range(len(keys)):
+                mm = sim.route(keys[i], int(src[i]))
+                for f in ("responsible", "hops", "status", "latency_ns"):
+                    assert int(r[f][i]) == int(mm[f]), (name, i, f, r[f][i], mm[f])
+                assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == mm["hop_seq"], (name, i)
+            H = int(r["hops"].max()) + 1
+            out.update(responsible=r["responsible"], hops=r["hops"], status=r["status"],
+                       one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"], hop_seq=r["hop_seq"][:, :H])
+        for ns in (1, p.s, 0):
+            lc = o.lookup_call(keys, src, ns)
+            for i in range(len(keys)):
+                mm = sim.lookup_call(keys[i], int(src[i]), ns, full=(rt == 2))
+                for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+                    assert int(lc[f][i]) == int(mm[f]), (name, rt, ns, i, f, lc[f][i], mm[f])
+                assert [int(x) for x in lc["siblings"][i] if x != 0xFFFFFFFF] == mm["siblings"][:max(ns, 1)], (name, i)
+            for f in ("num_siblings", "status", "is_valid", "latency_ns", "siblings"):
+                out[f"lc{rt}_ns{ns}_{f}"] = np.asarray(lc[f])
+    if "--check" in sys.argv:
+        g = np.load(HERE / f"{name}.npz")
+        for f, v in out.items():
+            assert np.array_equal(g[f], v), (name, f)
+        print(name, "committed vectors reproduced")
+        return
+    np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=keys, src=src, seed=np.int64(seed),
+                        simtime_round=np.int32(rnd), hop_count_max=np.int32(hcm), **out)
+    print(name, "lookups", len(keys), "mean hops", out["hops"].mean(), "status", np.bincount(out["status"]),
+          "lookup-call valid", out["lc1_ns8_is_valid"].mean(), out["lc2_ns8_is_valid"].mean())
+
+
 if __name__ == "__main__":
+    if "--kadrec" in sys.argv:   # (with --check: verify instead of writing)
+        kad_rec_case("kad_n2000_rec", 2000, 0x4b52, 2048)
+        kad_rec_case("kad_n1000_rec_hcm3", 1000, 0x4b53, 1024, rnd=0, hcm=3)
+        sys.exit(0)
     if "--koorde" in sys.argv:   # (with --check: verify instead of writing)
         koorde_case("koorde_n2000", 2000, 0x4b4f, 1024, 1024)
         koorde_case("koorde_n2000_sb2_nosuc", 2000, 0x4b50, 512, 512, shiftingBits=2, useSucList=0)

@@ -1042,3 +1042,103 @@ def epichord_find_node(keys, self_i, succ, pred, full_bits, list_size, cache, ke
             out.append((x, cache[x][0]))
             taken += 1
     return (0 if out else -1), out
+
+
+# --- recursive routing over Kademlia tables (R/Kademlia) -------------------------------------
+class KadRecursiveSim:
+    """Recursive (semi / full) routing of one message over Kademlia tables, read from
+    BaseOverlay::sendToKey / handleBaseOverlayMessage (BaseOverlay.cc:880-1004, 1380-1582) and
+    Kademlia::recursiveRoutingHook (Kademlia.cc:1022-1057, altRecMode off): a route message carries
+    its source and last hop; every node it reaches other than its source first sends a
+    KademliaRoutingInfoMessage (findNode(key, k, s) nodes, 47 + 27 n + 28 B) to the source, which
+    occupies the node's tx queue ahead of whatever the node sends next.  LookupCalls go through
+    RecursiveLookup (RecursiveLookup.cc:52-139): a routed FindNodeCall, answered by findNodeRpc at
+    the delivering node, the response sent back by UDP (semi) or routed to the source's key
+    (full).  Independent of the oracle's rec_route; findNode / isSiblingFor from KadTables."""
+
+    ROUTE_HDR = 53          # BASEROUTE_L 424 bits
+    CALL = 55               # FINDNODECALL_L 440 bits
+
+    def __init__(self, tables: "KadTables", xy, k=8, s=8, rec_redundant=3, redundant=8, hop_max=50, rnd=True,
+                 datarate=10e6, route_bytes=186, resp_base=61, resp_node=26, key_timeout=10.0):
+        self.T, self.xy, self.k, self.s = tables, xy, k, s
+        self.recR, self.R, self.hop_max, self.rnd, self.datarate = rec_redundant, redundant, hop_max, rnd, datarate
+        self.route_b, self.resp_b, self.resp_n = route_bytes, resp_base, resp_node
+        self.key_to = simtime(key_timeout, rnd)
+
+    def _send(self, q, a, b, nbytes, now):
+        """SimpleNodeEntry::calcDelay with node a's queue q[a]; the arrival time at b."""
+        if a == b:
+            return now
+        bw = simtime(nbytes * 8 / self.datarate, self.rnd)
+        fin = max(q.get(a, 0), now) + bw
+        q[a] = fin
+        return fin + coord_ns(self.xy, a, b, self.rnd) + bw
+
+    def _info(self, x, key):
+        return 47 + 27 * len(self.T.find_node(x, key, self.k, self.s)) + 28
+
+    def walk(self, key, src, ns_src, nbytes, now=0, q=None):
+        """(delivered node or None, hops, time, status, queues, hop list)."""
+        q = {} if q is None else q
+        msg = dict(src=src, last=src, hops=0)
+        node, t, path = src, now, []
+        while True:
+            ns = ns_src if node == src else 1
+            if node != src:
+                q.pop(node, None)                      # the queue is idle when the message arrives
+                if self.T.is_sibling_for(node, key, 1):
+                    self._send(q, node, src, self._info(node, key), t)   # the hook, then delivery
+                    return node, msg["hops"], t, 0, q, path
+            hops = self.T.find_node(node, key, self.recR, ns)
+            if not hops:
+                return None, 0, t, 4, q, path
+            if msg["hops"] >= self.hop_max:
+                return None, 0, t, 3, q, path
+            sib = self.T.is_sibling_for(node, key, ns)
+            nxt = None
+            for h in hops:
+                if (h == msg["last"] and h != node) or (h == src and node != src) or (h == node and not sib):
+                    continue
+                nxt = h
+                break
+            if nxt is None:
+                return None, 0, t, 4, q, path
+            if nxt == node:
+                return node, msg["hops"], t, 0, q, path
+            if node != src:
+                self._send(q, node, src, self._info(node, key), t)
+            t = self._send(q, node, nxt, nbytes, t)
+            msg["hops"] += 1
+            msg["last"] = node
+            path.append(nxt)
+            node = nxt
+
+    def route(self, key, src):
+        key = to_int(key) if not isinstance(key, int) else key
+        d, hops, t, st, _, path = self.walk(key, src, 1, self.route_b)
+        if st:
+            return dict(responsible=0xFFFFFFFF, hops=0, status=st, latency_ns=-1, hop_seq=path)
+        return dict(responsible=d, hops=hops, status=0, latency_ns=t, hop_seq=path)
+
+    def lookup_call(self, key, src, ns, full=False):
+        key = to_int(key) if not isinstance(key, int) else key
+        d, _, t, st, q, _ = self.walk(key, src, ns, self.ROUTE_HDR + self.CALL + 28)
+        fail = dict(num_siblings=0, hops=0, is_valid=0, latency_ns=-1, siblings=[])
+        if st:
+            return dict(fail, status=st)
+        res = self.T.find_node(d, key, self.R, ns)
+        flag = self.T.is_sibling_for(d, key, ns)
+        if d != src:
+            nbytes = self.resp_b + self.resp_n * len(res)
+            if not full:
+                t = self._send(q, d, src, nbytes, t)
+            else:
+                back, _, t, st2, _, _ = self.walk(self.T.ids[src], d, 1, self.ROUTE_HDR + nbytes, t, {d: q.get(d, 0)})
+                if st2 or back != src:
+                    return dict(fail, status=2)
+        if t >= 2 * self.key_to:
+            return dict(fail, status=2)
+        if not flag or not res:
+            return dict(fail, status=6)
+        return dict(num_siblings=len(res), hops=0, status=0, is_valid=1, latency_ns=t, siblings=list(res))
