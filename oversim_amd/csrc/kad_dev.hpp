@@ -736,6 +736,87 @@ struct KadLookup {
     uint32_t result, nsent;
 };
 
+// A suspended lookup (the sharded step) in HBM, structure of arrays: word w of lookup q at
+// base[w * stride + q], so a wave's lanes touch consecutive words (one 256 B line per word per
+// wave).  Written and read field by field: copying the aggregate made the compiler keep the whole
+// record addressable, which spilled the step kernel (r04: 0.6 ms at config E, W = 1, for a path
+// that never runs there).
+template <int A, int C>
+struct KadStateWords {
+    static constexpr int value = 5 + 1 + 4 + 4 + 1 + 3 * C + 2 + 7 * A + 4 + 3;
+};
+
+template <int A, int C>
+__device__ __forceinline__ void kad_state_put(uint32_t* __restrict__ base, uint64_t stride, uint64_t q,
+                                              const KadLookup<A, C>& L)
+{
+    int w = 0;
+    auto put = [&](uint32_t v) { base[(uint64_t)(w++) * stride + q] = v; };
+    auto put64 = [&](uint64_t v) { put((uint32_t)v); put((uint32_t)(v >> 32)); };
+#pragma unroll
+    for (int k = 0; k < 5; ++k) put(L.K.w[k]);
+    put(L.S);
+    put64((uint64_t)__double_as_longlong(L.sx));
+    put64((uint64_t)__double_as_longlong(L.sy));
+    put64((uint64_t)L.now);
+    put64((uint64_t)L.txf);
+    put(L.seq);
+#pragma unroll
+    for (int i = 0; i < C; ++i) put(L.nh.idx[i]);
+#pragma unroll
+    for (int i = 0; i < C; ++i) put64(L.nh.d[i]);
+    put(L.nh.used);
+    put((uint32_t)L.nh.n);
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+        put(L.p[i].node); put(L.p[i].tag); put64((uint64_t)L.p[i].t); put(L.p[i].dins); put(L.p[i].geo);
+        put(L.p[i].boff);
+    }
+    put(L.pvalid);
+    put((uint32_t)L.step);
+    put((uint32_t)L.hops);
+    put((uint32_t)L.pending);
+    put((L.started ? 1u : 0u) | (L.pfinished ? 2u : 0u) | (L.psuccess ? 4u : 0u) | (L.any_to ? 8u : 0u));
+    put(L.result);
+    put(L.nsent);
+}
+
+template <int A, int C>
+__device__ __forceinline__ void kad_state_get(KadLookup<A, C>& L, const uint32_t* __restrict__ base, uint64_t stride,
+                                              uint64_t q)
+{
+    int w = 0;
+    auto get = [&]() -> uint32_t { return base[(uint64_t)(w++) * stride + q]; };
+    auto get64 = [&]() -> uint64_t { const uint64_t lo = get(); return lo | ((uint64_t)get() << 32); };
+#pragma unroll
+    for (int k = 0; k < 5; ++k) L.K.w[k] = get();
+    L.S = get();
+    L.sx = __longlong_as_double((long long)get64());
+    L.sy = __longlong_as_double((long long)get64());
+    L.now = (int64_t)get64();
+    L.txf = (int64_t)get64();
+    L.seq = get();
+#pragma unroll
+    for (int i = 0; i < C; ++i) L.nh.idx[i] = get();
+#pragma unroll
+    for (int i = 0; i < C; ++i) L.nh.d[i] = get64();
+    L.nh.used = get();
+    L.nh.n = (int)get();
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+        L.p[i].node = get(); L.p[i].tag = get(); L.p[i].t = (int64_t)get64(); L.p[i].dins = get(); L.p[i].geo = get();
+        L.p[i].boff = get();
+    }
+    L.pvalid = get();
+    L.step = (int)get();
+    L.hops = (int)get();
+    L.pending = (int)get();
+    const uint32_t f = get();
+    L.started = f & 1u; L.pfinished = f & 2u; L.psuccess = f & 4u; L.any_to = f & 8u;
+    L.result = get();
+    L.nsent = get();
+}
+
 template <int A, int C>
 __device__ __forceinline__ void kad_lookup_init(KadLookup<A, C>& L, const K160& K, uint32_t S,
                                                 const double2* __restrict__ xy)

@@ -105,8 +105,9 @@ struct KadRouteIO {
     uint32_t* __restrict__ rpcs_out;
     uint32_t* __restrict__ sib_out;
     // shard step
-    void* st;                               // KadLookup<A>[nlook]
-    const uint8_t* __restrict__ act;
+    void* st;                               // suspended lookups, KadStateWords<A, C> words each (SoA)
+    uint64_t sstride;                       // their word stride (the batch's lookups)
+    uint8_t* __restrict__ act;               // 2 not started, 1 suspended in st, 0 never runs
     KadRes* __restrict__ res;
     const uint64_t* __restrict__ list;      // this round's lookups (indices), *nlist_dev of them
     const unsigned long long* __restrict__ nlist_dev;
@@ -122,9 +123,10 @@ struct KadRouteIO {
 // SH: explicit tables with short sibling tables (KadTables::maybe_short): a send may have to count
 // the responder's scan (kad_response_size); snapshot tables never do
 template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C, bool SH>
-// the shard step runs at 2 waves/SIMD: its HBM state traffic and request staging need the registers
-// (at 3 the exact-compare instantiations spilled in misaligned 96-bit pieces gfx950 rejects)
-__global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
+// the shard step's exact-compare and LookupCall instantiations run at 2 waves/SIMD: their HBM state
+// traffic and request staging need the registers (at 3 the exact-compare ones spilled in misaligned
+// 96-bit pieces gfx950 rejects, the LookupCall one 109 VGPRs); the one-way route step keeps K2's 3
+__global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
                                                                             KadRouteIO io)
 {
     const int lane = threadIdx.x & 63;
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
     const uint64_t end = min(cursor + chunk, nq);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int ns = LK ? LC.numSiblings : 1;
-    KadLookup<A, C>* st = static_cast<KadLookup<A, C>*>(io.st);
+    uint32_t* st = static_cast<uint32_t*>(io.st);
 
 #ifndef OVS_NOCOOP
     __shared__ CoopLds lds;
@@ -160,8 +162,14 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                 active = true;
                 if (SHARD) {
                     q = io.list[mine];
-                    dead = io.act[q] == 0;
-                    if (!dead) L = st[q];
+                    const uint8_t a = io.act[q];
+                    dead = a == 0;
+#if !defined(OVS_SHARD_NOSUSPEND) && !defined(OVS_SHARD_NOLOAD)
+                    if (a == 2) kad_lookup_init(L, io.qkeys[q], io.qsrc[q], V.xy);   // first visit
+                    else if (a == 1) kad_state_get(L, st, io.sstride, q);
+#else
+                    if (a) kad_lookup_init(L, io.qkeys[q], io.qsrc[q], V.xy);   // cost experiment (W = 1 only)
+#endif
                 } else {
                     q = mine;
                     kad_lookup_init(L, io.qkeys[q], io.qsrc[q], V.xy);
@@ -250,6 +258,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                     const RespGeo g = ev.rg();
                     const int tot = g.nsib + 1, rd = min(tot, kad_row_read(rb_pre(ev.pre))) - rb_r0(ev.pre);
                     n = kad_coop_finish<EX>(V, g, L.K, ev.numR, ev.sb(), ns, fb, (int)lds.rcnt[threadIdx.x] + tot - rd);
+#ifndef OVS_SHARD_NOREMOTE
                 } else if (SHARD && !(ev.r >= V.lo && ev.r < V.hi)) {
                     // the owner's answer, delivered by k_kad_shard_deliver
                     const KadRes& rr = io.res[q * A + ev.e];
@@ -259,6 +268,7 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                         fb.x[k] = k < n ? rr.nodes[k < 8 ? k : 0] : NONE;
                         fb.d[k] = k < n ? rr.dist[k < 8 ? k : 0] : ~0ull;
                     }
+#endif
                 } else {
                     // in the sibling zone only c and the row prefix can enter the answer (ev.pre)
                     const RespGeo g = ev.rg();
@@ -345,7 +355,10 @@ __global__ __launch_bounds__(256, (SHARD || C > 8) ? 2 : OVS_KAD_WAVES) void k_k
                 active = false;
             } else if (SHARD && ph == KEV_WAIT) {
                 // the earliest event waits for an owner's answer: suspended until the next round
-                st[q] = L;
+#if !defined(OVS_SHARD_NOSUSPEND) && !defined(OVS_SHARD_NOSTORE)
+                kad_state_put(st, io.sstride, q, L);
+#endif
+                io.act[q] = 1;
                 io.ltag[q] = 1;
                 active = false;
             }
@@ -422,7 +435,7 @@ hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const 
     KadRouteIO io{};
     io.nq = a.nlist_max;     // sizes the grid; the kernel reads the list length from nlist_dev
     io.sib_out = a.sib_out;
-    io.st = a.st; io.act = a.act; io.res = a.res; io.list = a.list; io.nlist_dev = a.nlist_dev; io.qids = a.qids;
+    io.st = a.st; io.sstride = a.nlist_max; io.act = a.act; io.qkeys = a.qkeys; io.qsrc = a.qsrc; io.res = a.res; io.list = a.list; io.nlist_dev = a.nlist_dev; io.qids = a.qids;
     io.shard_lo = a.shard_lo; io.nsh = a.nsh;
     io.rstage = a.rstage; io.rtag = a.rtag; io.dstage = a.dstage; io.ltag = a.ltag;
     // sharded networks are snapshot builds: never short

@@ -31,12 +31,13 @@ namespace ovs {
 
 namespace {
 
-template <int A>
+// a lookup's state record is written only when it first suspends: round 1 starts every lookup
+// from its key and source (act = 2), so at world size 1 no state crosses HBM at all.  A result
+// slot's ready flag is read only after the send that requested it cleared it: nothing to initialise.
 __global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* __restrict__ src, uint64_t n,
-                                 uint32_t qid_base, const double2* __restrict__ xy, KadLookup<A>* __restrict__ st,
-                                 uint8_t* __restrict__ act, uint32_t* __restrict__ qids, KadRes* __restrict__ res,
-                                 uint64_t* __restrict__ iota, unsigned long long* nlist, uint32_t lo, uint32_t hi,
-                                 unsigned long long* bad)
+                                 uint32_t qid_base, K160* __restrict__ qkeys, uint32_t* __restrict__ qsrc,
+                                 uint8_t* __restrict__ act, uint32_t* __restrict__ qids, uint64_t* __restrict__ iota,
+                                 unsigned long long* nlist, uint32_t lo, uint32_t hi, unsigned long long* bad)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *nlist = n;        // round 1 visits every lookup of the batch
@@ -44,18 +45,13 @@ __global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* 
     const uint32_t S = src[i];
     qids[i] = qid_base + (uint32_t)i;
     iota[i] = i;
-    if (S < lo || S >= hi) {
-        // the source's own findNode needs its rows: a source off this arc is an error
-        // (ovs_kad_shard_errors), and its lookup never runs
-        act[i] = 0;
-        atomicAdd(bad, 1ull);
-        return;
-    }
-    KadLookup<A> L;
-    kad_lookup_init(L, keys[i], S, xy);
-    st[i] = L;
-    act[i] = 1;
-    for (int s = 0; s < A; ++s) res[i * A + s].ready = 1;
+    qkeys[i] = keys[i];
+    qsrc[i] = S;
+    // the source's own findNode needs its rows: a source off this arc is an error
+    // (ovs_kad_shard_errors), and its lookup never runs
+    const bool off = S < lo || S >= hi;
+    act[i] = off ? 0 : 2;
+    if (off) atomicAdd(bad, 1ull);
 }
 
 // findNode at the responder (owned by this rank) for each received request
@@ -145,34 +141,27 @@ bool kad_params_supported_host(const ovs_params& P, const KadTables& t) { return
 size_t kad_lookup_state_bytes(int alpha)
 {
     switch (alpha) {
-    case 1: return sizeof(KadLookup<1>);
-    case 2: return sizeof(KadLookup<2>);
-    case 3: return sizeof(KadLookup<3>);
-    case 4: return sizeof(KadLookup<4>);
-    default: return sizeof(KadLookup<8>);
+    case 1: return 4 * KadStateWords<1, 8>::value;
+    case 2: return 4 * KadStateWords<2, 8>::value;
+    case 3: return 4 * KadStateWords<3, 8>::value;
+    case 4: return 4 * KadStateWords<4, 8>::value;
+    default: return 4 * KadStateWords<8, 8>::value;
     }
 }
 
-hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
-                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, uint64_t* iota,
-                          unsigned long long* nlist, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t s)
+hipError_t kad_shard_init(const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base, K160* qkeys,
+                          uint32_t* qsrc, uint8_t* act, uint32_t* qids, uint64_t* iota, unsigned long long* nlist,
+                          uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t s)
 {
     const uint64_t g = n ? n : 1;
-#define KI(a) hipLaunchKernelGGL(k_kad_shard_init<a>, dim3(nblk(g, 256)), dim3(256), 0, s, keys, src, n, qid_base, xy, \
-                                 (KadLookup<a>*)st, act, qids, res, iota, nlist, lo, hi, bad)
-    switch (alpha) {
-    case 1: KI(1); break;
-    case 2: KI(2); break;
-    case 3: KI(3); break;
-    case 4: KI(4); break;
-    default: KI(8); break;
-    }
-#undef KI
+    hipLaunchKernelGGL(k_kad_shard_init, dim3(nblk(g, 256)), dim3(256), 0, s, keys, src, n, qid_base, qkeys, qsrc, act,
+                       qids, iota, nlist, lo, hi, bad);
     return hipGetLastError();
 }
 
 hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
-                          const DelayConsts& DC, void* st, const uint8_t* act, const uint32_t* qids, KadRes* res,
+                          const DelayConsts& DC, void* st, uint8_t* act, const K160* qkeys, const uint32_t* qsrc,
+                          const uint32_t* qids, KadRes* res,
                           uint64_t nlook, const uint64_t* list, const unsigned long long* nlist, const uint64_t* iota,
                           uint64_t* list_next, unsigned long long* nlist_next, const uint64_t* shard_lo, int nsh,
                           ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,
@@ -202,7 +191,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
     if ((e = stage_ensure(stage, olt + nlook, s)) != hipSuccess) return e;
     uint8_t* sb = static_cast<uint8_t*>(stage.buf);
     KadShardStepArgs a{};
-    a.st = st; a.act = act; a.res = res; a.list = list; a.nlist_dev = nlist; a.nlist_max = nlook; a.qids = qids;
+    a.st = st; a.act = act; a.qkeys = qkeys; a.qsrc = qsrc; a.res = res; a.list = list; a.nlist_dev = nlist; a.nlist_max = nlook; a.qids = qids;
     a.shard_lo = shard_lo; a.nsh = nsh;
     a.rstage = reinterpret_cast<ovs_kad_req*>(sb + orq);
     a.dstage = reinterpret_cast<ovs_done_rec*>(sb + odn);

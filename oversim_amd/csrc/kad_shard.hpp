@@ -16,8 +16,10 @@ static_assert(sizeof(KadRes) == 104, "KadRes layout");
 
 // what the shard-step instantiation of K2 (kad_route.hip) reads and writes in one round
 struct KadShardStepArgs {
-    void* st;                          // KadLookup<A>[nlook], the suspended lookups
-    const uint8_t* act;                // 1: the lookup runs (its source is on this arc)
+    void* st;                          // the suspended lookups: KadStateWords words each, stride nlist_max (SoA)
+    uint8_t* act;                      // 2: not started, 1: suspended in st, 0: never runs (source off the arc)
+    const K160* qkeys;                 // the batch's keys and sources (a lookup starts from them in the
+    const uint32_t* qsrc;              // round that first visits it: no state record before its first suspend)
     KadRes* res;                       // nlook * A result slots
     const uint64_t* list;              // this round's lookups (indices), *nlist_dev of them
     const unsigned long long* nlist_dev;
@@ -34,17 +36,18 @@ struct KadShardStepArgs {
 
 size_t kad_lookup_state_bytes(int alpha);
 bool kad_params_supported_host(const ovs_params& P, const KadTables& t);
-// lookups of this rank: state, qids, the round-1 list (indices 0..n-1) and its count; sources off
-// [lo, hi) are counted in *bad and never run
-hipError_t kad_shard_init(int alpha, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
-                          const double2* xy, void* st, uint8_t* act, uint32_t* qids, KadRes* res, uint64_t* iota,
-                          unsigned long long* nlist, uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t s);
+// lookups of this rank: their keys and sources (copied to qkeys / qsrc), act = 2 (not started), qids,
+// the round-1 list (indices 0..n-1) and its count; sources off [lo, hi) are counted in *bad and never run
+hipError_t kad_shard_init(const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base, K160* qkeys,
+                          uint32_t* qsrc, uint8_t* act, uint32_t* qids, uint64_t* iota, unsigned long long* nlist,
+                          uint32_t lo, uint32_t hi, unsigned long long* bad, hipStream_t s);
 // one round: the list's lookups advance while their responders are local (k_kad_route<.., SHARD>);
 // requests to the owners of the others go to segment d of out (out + d * out_cap, counter
 // out_count[d]); finished lookups are appended to done (done_count); the still active ones form the
 // next list (*nlist_next) and are counted in *active_count.  bad: table reads off the arc.
 hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
-                          const DelayConsts& DC, void* st, const uint8_t* act, const uint32_t* qids, KadRes* res,
+                          const DelayConsts& DC, void* st, uint8_t* act, const K160* qkeys, const uint32_t* qsrc,
+                          const uint32_t* qids, KadRes* res,
                           uint64_t nlook, const uint64_t* list, const unsigned long long* nlist, const uint64_t* iota,
                           uint64_t* list_next, unsigned long long* nlist_next, const uint64_t* shard_lo, int nsh,
                           ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,

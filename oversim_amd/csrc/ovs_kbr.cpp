@@ -66,7 +66,9 @@ struct ovs_ctx {
     uint64_t kvis_cap = 0;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
-    uint8_t* kact = nullptr;             // 0 done, 1 running, 2 not started
+    uint8_t* kact = nullptr;             // 0 never runs, 1 suspended in kst, 2 not started
+    K160* kkeys = nullptr;               // the batch's keys and sources (a lookup starts from them)
+    uint32_t* ksrc = nullptr;
     uint32_t* kqids = nullptr;
     KadRes* kres = nullptr;              // alpha findNode result slots per lookup
     unsigned long long* kbad = nullptr;  // undeliverable responses
@@ -121,10 +123,12 @@ void free_tables(ovs_ctx* c)
 
 void free_kad_shard(ovs_ctx* c)
 {
-    void* ptrs[] = {c->kst, c->kact, c->kqids, c->kres, c->kbad, c->kiota, c->klist[0], c->klist[1], c->knl};
+    void* ptrs[] = {c->kst, c->kact, c->kqids, c->kres, c->kbad, c->kiota, c->klist[0], c->klist[1], c->knl,
+                    c->kkeys, c->ksrc};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->kst = nullptr; c->kact = nullptr; c->kqids = nullptr; c->kres = nullptr; c->kbad = nullptr;
+    c->kkeys = nullptr; c->ksrc = nullptr;
     c->kiota = nullptr; c->klist[0] = c->klist[1] = nullptr; c->knl = nullptr; c->kcur = 0;
     c->knlook = 0; c->kcap = 0; c->kalpha = 0;
 }
@@ -911,6 +915,8 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
         const uint64_t cap = n ? n : 1;
         HIPCHK(c, hipMalloc(&c->kst, kad_lookup_state_bytes(alpha) * cap));
         HIPCHK(c, hipMalloc(&c->kact, cap));
+        HIPCHK(c, hipMalloc(&c->kkeys, sizeof(K160) * cap));
+        HIPCHK(c, hipMalloc(&c->ksrc, sizeof(uint32_t) * cap));
         HIPCHK(c, hipMalloc(&c->kqids, sizeof(uint32_t) * cap));
         HIPCHK(c, hipMalloc(&c->kres, sizeof(KadRes) * cap * kad_pend_slots(alpha)));
         HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
@@ -926,8 +932,8 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
     c->ksib = sib;
     HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
     c->kcur = 0;
-    HIPCHK(c, kad_shard_init(alpha, reinterpret_cast<const K160*>(keys), src, n, qid_base, c->xy, c->kst, c->kact,
-                             c->kqids, c->kres, c->kiota, c->knl, c->kad.lo, c->kad.hi, c->kbad, s));
+    HIPCHK(c, kad_shard_init(reinterpret_cast<const K160*>(keys), src, n, qid_base, c->kkeys, c->ksrc, c->kact,
+                             c->kqids, c->kiota, c->knl, c->kad.lo, c->kad.hi, c->kbad, s));
     return OVS_OK;
 }
 
@@ -980,7 +986,8 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint64_t out_cap, un
     // this round's list: iota in round 1, then the ping-pong lists the previous round compacted
     const int cur = c->kcur, nxt = cur == 1 ? 2 : 1;
     const uint64_t* list = cur == 0 ? c->kiota : c->klist[cur - 1];
-    hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kqids,
+    hipError_t e = kad_shard_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->kst, c->kact, c->kkeys,
+                                  c->ksrc, c->kqids,
                                   c->kres, c->knlook, list, c->knl + cur, c->kiota, c->klist[nxt - 1], c->knl + nxt,
                                   c->d_bounds, (int)nshards, out, out_cap, out_count, done, done_cap, done_count,
                                   active_count, c->kns, c->ksib, c->kbad, c->num_cu, c->stage[s], s);

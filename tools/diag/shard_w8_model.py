@@ -1,0 +1,137 @@
+"""W = 8 cost model of the sharded paths, emulated on one GPU (eight engine contexts, one per arc,
+the in-process exchange of oversim_amd.shard): per round and per arc the step kernel time, the
+serve / deliver kernel times (Kademlia), the records each arc sends to the others and the active
+lookups -- the inputs of DESIGN.md §6's per-rank estimate for a real 8-GPU node.
+
+usage: python tools/diag/shard_w8_model.py --workload E [--lookups-per-rank M] [--world 8]
+Prints one JSON line per round and a summary line."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np
+import torch
+
+from oversim_amd import Params, workload as W
+from oversim_amd.shard import (KAD_REQ_BYTES, KAD_RESP_BYTES, REC_BYTES, GpuShardStepper, KadShardStepper, arc_bounds,
+                               done_to_numpy)
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", choices=["D", "E"], required=True)
+ap.add_argument("--lookups-per-rank", type=int, default=0)
+ap.add_argument("--world", type=int, default=8)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+Wn = a.world
+wl = W.WORKLOADS[a.workload]
+m = a.lookups_per_rank or wl["lookups"]
+inputs = [W.bench_inputs(a.workload, dev, world=Wn, rank=r, n_lookups=m, sharded=True) for r in range(Wn)]
+I0 = inputs[0]
+n = I0["n_total"]
+ids = I0["ids"] if I0["ids"] is not None else I0["ids_t"].cpu().numpy().view(np.uint32)
+xy = I0["xy"] if I0["xy"] is not None else I0["xy_t"].cpu().numpy()
+bounds = arc_bounds(n, Wn)
+kad = a.workload == "E"
+params = Params.kademlia().replace(lookupParallelRpcs=wl.get("alpha", 3)) if kad else Params.chord()
+
+
+def ev():
+    return torch.cuda.Event(enable_timing=True)
+
+
+t_start = time.time()
+if kad:
+    steppers = [KadShardStepper(ids, xy, bounds, r, dev, params=params) for r in range(Wn)]
+    for r in range(Wn):
+        steppers[r].begin(inputs[r]["keys_t"], inputs[r]["src_t"], r * m)
+else:
+    steppers = [GpuShardStepper(ids, xy, bounds, r, dev, capacity=Wn * m, params=params) for r in range(Wn)]
+    for st in steppers:
+        st.reset(Wn * m)
+    inbox = [steppers[r].make_records(inputs[r]["keys_t"], inputs[r]["src_t"], r * m) for r in range(Wn)]
+torch.cuda.synchronize()
+print(json.dumps(dict(workload=a.workload, world=Wn, nodes=n, lookups_per_rank=m, setup_s=round(time.time() - t_start, 1))),
+      flush=True)
+rounds, tot = 0, dict(step_ms=np.zeros(Wn), serve_ms=np.zeros(Wn), deliver_ms=np.zeros(Wn), sent=np.zeros(Wn))
+while True:
+    rounds += 1
+    segs, rows, kms = [], [], []
+    for r in range(Wn):
+        e0, e1 = ev(), ev()
+        e0.record()
+        if kad:
+            sg, counts = steppers[r].step()
+        else:
+            sg, counts = steppers[r].step(inbox[r])
+        e1.record()
+        segs.append(sg)
+        rows.append(counts[:Wn + 1].cpu().numpy().copy() if kad else counts[:Wn].cpu().numpy().copy())
+        kms.append((e0, e1))
+    torch.cuda.synchronize()
+    step_ms = np.array([x.elapsed_time(y) for x, y in kms])
+    M = np.stack(rows)
+    if int(M.sum()) == 0:
+        break
+    serve_ms, deliver_ms = np.zeros(Wn), np.zeros(Wn)
+    if kad:
+        replies = [[None] * Wn for _ in range(Wn)]
+        for d in range(Wn):
+            parts = [segs[r][d][:int(M[r, d])] for r in range(Wn)]
+            rows_d = torch.cat(parts)
+            if rows_d.shape[0] == 0:
+                continue
+            e0, e1 = ev(), ev()
+            e0.record()
+            resp = steppers[d].serve(rows_d)
+            e1.record()
+            torch.cuda.synchronize()
+            serve_ms[d] = e0.elapsed_time(e1)
+            off = 0
+            for r in range(Wn):
+                k = int(M[r, d])
+                replies[r][d] = resp[off:off + k]
+                off += k
+        for r in range(Wn):
+            parts = [x for x in replies[r] if x is not None and x.shape[0]]
+            if parts:
+                e0, e1 = ev(), ev()
+                e0.record()
+                steppers[r].deliver(torch.cat(parts))
+                e1.record()
+                torch.cuda.synchronize()
+                deliver_ms[r] = e0.elapsed_time(e1)
+        # remote requests out (32 B) and their responses back (104 B), per requesting arc
+        remote = np.array([int(M[r, :Wn].sum() - M[r, r]) for r in range(Wn)])
+        bytes_out = remote * (KAD_REQ_BYTES + KAD_RESP_BYTES)
+    else:
+        new_inbox = []
+        for d in range(Wn):
+            parts = [segs[r][d][:int(M[r, d])] for r in range(Wn)]
+            new_inbox.append(torch.cat(parts) if parts else segs[d][d][:0])
+        inbox = new_inbox
+        remote = np.array([int(M[r, :Wn].sum() - M[r, r]) for r in range(Wn)])
+        bytes_out = remote * REC_BYTES
+    tot["step_ms"] += step_ms
+    tot["serve_ms"] += serve_ms
+    tot["deliver_ms"] += deliver_ms
+    tot["sent"] += bytes_out
+    print(json.dumps(dict(round=rounds, step_ms_max=round(float(step_ms.max()), 3), step_ms_mean=round(float(step_ms.mean()), 3),
+                          serve_ms_max=round(float(serve_ms.max()), 3), deliver_ms_max=round(float(deliver_ms.max()), 3),
+                          remote_records=[int(x) for x in remote], bytes_out_max=int(bytes_out.max()),
+                          active=int(M[:, Wn].sum()) if kad else None)), flush=True)
+    if rounds > 5000:
+        raise RuntimeError("did not terminate")
+torch.cuda.synchronize()
+dn = [done_to_numpy(s.finished()) for s in steppers]
+d = np.concatenate(dn)
+print(json.dumps(dict(summary=True, workload=a.workload, world=Wn, rounds=rounds, lookups=int(len(d)),
+                      ok=int((d["status"] == 0).sum()), mean_hops=float(d["hops"].mean()),
+                      step_ms_per_rank=[round(float(x), 3) for x in tot["step_ms"]],
+                      serve_ms_per_rank=[round(float(x), 3) for x in tot["serve_ms"]],
+                      deliver_ms_per_rank=[round(float(x), 3) for x in tot["deliver_ms"]],
+                      bytes_out_per_rank=[int(x) for x in tot["sent"]], wall_s=round(time.time() - t_start, 1))),
+      flush=True)
