@@ -586,6 +586,16 @@ typedef struct ovs_kad_resp {       /* 104 B FindNodeResponse */
     uint64_t dist_hi[8];            /* top 64 bits of (node key XOR lookup key) */
 } ovs_kad_resp;
 
+/* The FindNodeResponse record of KademliaLarge networks (k or lookupRedundantNodes 9..16,
+ * omnetpp.ini:113-126): ovs_kad_shard_serve writes and ovs_kad_shard_deliver reads these when
+ * ovs_kad_shard_resp_bytes(ctx) says 200 (ABI 10). */
+typedef struct ovs_kad_resp16 {     /* 200 B */
+    uint32_t tag;
+    uint32_t count;                 /* result size, <= 16 */
+    uint32_t nodes[16];
+    uint64_t dist_hi[16];
+} ovs_kad_resp16;
+
 /* Load arc [lo, hi) of a Kademlia network of n_total nodes (ids/xy of all nodes). */
 ovs_status  ovs_kad_load_shard(ovs_ctx* ctx, const ovs_key160* ids_all_sorted, uint64_t n_total,
                                const double* xy_all, uint64_t lo, uint64_t hi, uint32_t flags);
@@ -615,14 +625,18 @@ ovs_status  ovs_kad_shard_step(ovs_ctx* ctx, ovs_kad_req* out, uint64_t out_cap,
                                ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
                                unsigned long long* active_count, const uint64_t* shard_lo, uint32_t nshards,
                                void* stream);
-/* findNode at the (local) responders of n received requests. */
-ovs_status  ovs_kad_shard_serve(ovs_ctx* ctx, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out,
+/* Bytes of this context's response records: 104 (ovs_kad_resp) when k and lookupRedundantNodes
+ * are <= 8, else 200 (ovs_kad_resp16); -1 without a Kademlia network. */
+int32_t     ovs_kad_shard_resp_bytes(const ovs_ctx* ctx);
+/* findNode at the (local) responders of n received requests; out = n response records of
+ * ovs_kad_shard_resp_bytes(ctx) bytes. */
+ovs_status  ovs_kad_shard_serve(ovs_ctx* ctx, const ovs_kad_req* in, uint64_t n, void* out,
                                 void* stream);
 /* Hand n responses (to this rank's requests) back to the waiting lookups.  A response
  * with an unknown tag, or one the serving rank could not answer (the request named a
  * node outside its arc: count 0xFFFFFFFF), is counted as an error; the latter still
  * completes its slot with an empty result, so the lookup terminates. */
-ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const ovs_kad_resp* in, uint64_t n, void* stream);
+ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const void* in, uint64_t n, void* stream);
 /* Errors since ovs_kad_shard_begin: responses ovs_kad_shard_deliver could not hand over,
  * and lookups whose source lies off this arc (they never run).  Synchronises the
  * device.  The caller fails the batch when it is non-zero. */

@@ -56,8 +56,9 @@ struct HopRecorder {
 };
 
 // shard step: a response from a node off this arc is ready once its result was delivered
+template <int C>
 struct RemoteReady {
-    const KadRes* __restrict__ res;
+    const KadResN<C>* __restrict__ res;
     uint64_t base;
     uint32_t lo, hi;
     __device__ __forceinline__ bool operator()(int slot, uint32_t r) const
@@ -69,8 +70,9 @@ struct RemoteReady {
 // shard step: a FindNodeCall to a node off this arc becomes a request to its owner, staged in the
 // call's slot (a slot carries at most one request per round: a response cannot be ready in the
 // round it is requested)
+template <int C>
 struct ShardSend {
-    KadRes* __restrict__ res;
+    KadResN<C>* __restrict__ res;
     uint64_t base;
     const K160* K;
     const uint64_t* __restrict__ shard_lo;
@@ -108,7 +110,7 @@ struct KadRouteIO {
     void* st;                               // suspended lookups, KadStateWords<A, C> words each (SoA)
     uint64_t sstride;                       // their word stride (the batch's lookups)
     uint8_t* __restrict__ act;               // 2 not started, 1 suspended in st, 0 never runs
-    KadRes* __restrict__ res;
+    void* res;                               // KadResN<C>[nlook * A]
     const uint64_t* __restrict__ list;      // this round's lookups (indices), *nlist_dev of them
     const unsigned long long* __restrict__ nlist_dev;
     const uint32_t* __restrict__ qids;
@@ -196,7 +198,7 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
             for (int r = 0; r < A; ++r) {
 #endif
                 if (SHARD) {
-                    const RemoteReady rd{io.res, q * A, V.lo, V.hi};
+                    const RemoteReady<C> rd{static_cast<const KadResN<C>*>(io.res), q * A, V.lo, V.hi};
                     ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, rd, rec, ev);
                 } else {
                     ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, AlwaysReady{}, rec, ev);
@@ -261,12 +263,12 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
 #ifndef OVS_SHARD_NOREMOTE
                 } else if (SHARD && !(ev.r >= V.lo && ev.r < V.hi)) {
                     // the owner's answer, delivered by k_kad_shard_deliver
-                    const KadRes& rr = io.res[q * A + ev.e];
+                    const KadResN<C>& rr = static_cast<const KadResN<C>*>(io.res)[q * A + ev.e];
                     n = (int)rr.count;
 #pragma unroll
                     for (int k = 0; k < C; ++k) {
-                        fb.x[k] = k < n ? rr.nodes[k < 8 ? k : 0] : NONE;
-                        fb.d[k] = k < n ? rr.dist[k < 8 ? k : 0] : ~0ull;
+                        fb.x[k] = k < n ? rr.nodes[k] : NONE;
+                        fb.d[k] = k < n ? rr.dist[k] : ~0ull;
                     }
 #endif
                 } else {
@@ -307,8 +309,8 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
 #endif
             if (num >= 0) {
                 if (SHARD) {
-                    const ShardSend on{io.res, q * A, &L.K, io.shard_lo, io.nsh, V.lo, V.hi, io.rstage, io.rtag,
-                                       LK ? (0x80000000u | (uint32_t)ns) : 0u};
+                    const ShardSend<C> on{static_cast<KadResN<C>*>(io.res), q * A, &L.K, io.shard_lo, io.nsh, V.lo,
+                                          V.hi, io.rstage, io.rtag, LK ? (0x80000000u | (uint32_t)ns) : 0u};
                     kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, on);
                 } else {
                     kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, SendNothing{});
@@ -438,8 +440,13 @@ hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const 
     io.st = a.st; io.sstride = a.nlist_max; io.act = a.act; io.qkeys = a.qkeys; io.qsrc = a.qsrc; io.res = a.res; io.list = a.list; io.nlist_dev = a.nlist_dev; io.qids = a.qids;
     io.shard_lo = a.shard_lo; io.nsh = a.nsh;
     io.rstage = a.rstage; io.rtag = a.rtag; io.dstage = a.dstage; io.ltag = a.ltag;
-    // sharded networks are snapshot builds: never short
+    // sharded networks are snapshot builds: never short.  KademliaLarge (k or lookupRedundantNodes
+    // above 8) takes the 16-entry instantiation, its results travel as ovs_kad_resp16
     if (V.maybe_short) return hipErrorNotSupported;
+    if (LC.redundant > 8 || LC.maxRedundantLocal > 8) {
+        if (a.sib_out) return kad_launch<A, false, EX, true, true, 16, false>(V, DC, LC, io, num_cu, st);
+        return kad_launch<A, false, EX, false, true, 16, false>(V, DC, LC, io, num_cu, st);
+    }
     if (a.sib_out) return kad_launch<A, false, EX, true, true, 8, false>(V, DC, LC, io, num_cu, st);
     return kad_launch<A, false, EX, false, true, 8, false>(V, DC, LC, io, num_cu, st);
 }

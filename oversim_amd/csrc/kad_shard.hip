@@ -55,9 +55,9 @@ __global__ void k_kad_shard_init(const K160* __restrict__ keys, const uint32_t* 
 }
 
 // findNode at the responder (owned by this rank) for each received request
-template <bool EX>
+template <bool EX, int C>
 __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __restrict__ in, uint64_t n,
-                                  ovs_kad_resp* __restrict__ out)
+                                  typename KadWire<C>::type* __restrict__ out)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
@@ -66,7 +66,7 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
     const int ns = (q.pad & 0x80000000u) ? (int)(q.pad & 0xFFu) : 1;
     K160 K;
     for (int w = 0; w < 5; ++w) K.w[w] = q.key[w];
-    ovs_kad_resp o;
+    typename KadWire<C>::type o;
     o.tag = q.tag;
     if (kad_off_arc(V, q.node) || ns > 8 || ns > V.S5) {
         // not this rank's node (the caller mis-routed the request, or the record was never written:
@@ -78,37 +78,38 @@ __global__ void k_kad_shard_serve(KadView V, KadLC LC, const ovs_kad_req* __rest
     }
     const KadNode rr = load_node(V.nodes, q.node);
     const bool sb = kad_is_sibling(V, rr, q.node, K, ns);
-    SVec<8> r;
-    kad_find_node_vec<8, EX>(V, q.node, rr, K, LC.redundant, sb, r, ns);
+    SVec<C> r;
+    kad_find_node_vec<C, EX>(V, q.node, rr, K, LC.redundant, sb, r, ns);
     o.count = (uint32_t)r.n;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { o.nodes[k] = r.idx[k]; o.dist_hi[k] = r.d[k]; }
+    for (int k = 0; k < C; ++k) { o.nodes[k] = r.idx[k]; o.dist_hi[k] = r.d[k]; }
     out[j] = o;
 }
 
-__global__ void k_kad_shard_deliver(const ovs_kad_resp* __restrict__ in, uint64_t n, KadRes* __restrict__ res,
-                                    uint64_t nslots, unsigned long long* bad)
+template <int C>
+__global__ void k_kad_shard_deliver(const typename KadWire<C>::type* __restrict__ in, uint64_t n,
+                                    KadResN<C>* __restrict__ res, uint64_t nslots, unsigned long long* bad)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    const ovs_kad_resp o = in[j];
+    const typename KadWire<C>::type o = in[j];
     if (o.tag >= nslots) { atomicAdd(bad, 1ull); return; }
-    KadRes r;
-    if (o.count > 8) {
+    KadResN<C> r;
+    if (o.count > (uint32_t)C) {
         // a request the serving rank could not answer (not its node): counted for
         // ovs_kad_shard_errors, and the slot completes with an empty result so the lookup ends
         atomicAdd(bad, 1ull);
         r.count = 0;
         r.ready = 1;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { r.nodes[k] = NONE; r.dist[k] = ~0ull; }
+        for (int k = 0; k < C; ++k) { r.nodes[k] = NONE; r.dist[k] = ~0ull; }
         res[o.tag] = r;
         return;
     }
     r.count = o.count;
     r.ready = 1;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { r.nodes[k] = o.nodes[k]; r.dist[k] = o.dist_hi[k]; }
+    for (int k = 0; k < C; ++k) { r.nodes[k] = o.nodes[k]; r.dist[k] = o.dist_hi[k]; }
     res[o.tag] = r;
 }
 
@@ -129,24 +130,20 @@ hipError_t kad_shard_step_dispatch(int A, const KadView& V, const DelayConsts& D
 
 }  // namespace
 
-// the sharded path exchanges findNode results of at most 8 nodes (KadRes, ovs_kad_resp): k and
-// lookupRedundantNodes <= 8
+// the sharded path exchanges findNode results of up to 8 nodes (ovs_kad_resp), or 16 for
+// KademliaLarge (ovs_kad_resp16): k and lookupRedundantNodes <= 16 (kad_params_supported)
 static bool kad_shard_params_supported(const ovs_params& P, const KadTables& t)
 {
-    return kad_params_supported(P, t) && P.lookupRedundantNodes <= 8 && t.k <= 8;
+    return kad_params_supported(P, t) && P.lookupRedundantNodes <= 16 && t.k <= 16;
 }
 
 bool kad_params_supported_host(const ovs_params& P, const KadTables& t) { return kad_shard_params_supported(P, t); }
 
-size_t kad_lookup_state_bytes(int alpha)
+size_t kad_lookup_state_bytes(int alpha, int cap)
 {
-    switch (alpha) {
-    case 1: return 4 * KadStateWords<1, 8>::value;
-    case 2: return 4 * KadStateWords<2, 8>::value;
-    case 3: return 4 * KadStateWords<3, 8>::value;
-    case 4: return 4 * KadStateWords<4, 8>::value;
-    default: return 4 * KadStateWords<8, 8>::value;
-    }
+    const int A = kad_pend_slots(alpha);
+    return cap > 8 ? 4 * (size_t)(KadStateWords<1, 16>::value + 7 * (A - 1))
+                   : 4 * (size_t)(KadStateWords<1, 8>::value + 7 * (A - 1));
 }
 
 hipError_t kad_shard_init(const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base, K160* qkeys,
@@ -161,7 +158,7 @@ hipError_t kad_shard_init(const K160* keys, const uint32_t* src, uint64_t n, uin
 
 hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
                           const DelayConsts& DC, void* st, uint8_t* act, const K160* qkeys, const uint32_t* qsrc,
-                          const uint32_t* qids, KadRes* res,
+                          const uint32_t* qids, void* res,
                           uint64_t nlook, const uint64_t* list, const unsigned long long* nlist, const uint64_t* iota,
                           uint64_t* list_next, unsigned long long* nlist_next, const uint64_t* shard_lo, int nsh,
                           ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,
@@ -226,7 +223,7 @@ hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, con
 }
 
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
-                           ovs_kad_resp* out, unsigned long long* bad, hipStream_t s)
+                           void* out, unsigned long long* bad, hipStream_t s)
 {
     // numSiblings travels with each request; the rest of the configuration is the rank's
     ovs_params Q = P;
@@ -236,16 +233,24 @@ hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, 
     KadView V = kad_make_view(t, nullptr, n);
     V.err = bad;
     const KadLC LC = kad_make_lc(P, t);
-    if (t.exact) hipLaunchKernelGGL(k_kad_shard_serve<true>, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
-    else hipLaunchKernelGGL(k_kad_shard_serve<false>, dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, out);
+#define KS(ex, c) hipLaunchKernelGGL((k_kad_shard_serve<ex, c>), dim3(nblk(nreq, 128)), dim3(128), 0, s, V, LC, in, nreq, \
+                                     static_cast<KadWire<c>::type*>(out))
+    if (kad_shard_cap(P, t) > 8) { if (t.exact) KS(true, 16); else KS(false, 16); }
+    else { if (t.exact) KS(true, 8); else KS(false, 8); }
+#undef KS
     return hipGetLastError();
 }
 
-hipError_t kad_shard_deliver(const ovs_kad_resp* in, uint64_t n, KadRes* res, uint64_t nslots,
-                             unsigned long long* bad, hipStream_t s)
+hipError_t kad_shard_deliver(int cap, const void* in, uint64_t n, void* res, uint64_t nslots, unsigned long long* bad,
+                             hipStream_t s)
 {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_kad_shard_deliver, dim3(nblk(n, 256)), dim3(256), 0, s, in, n, res, nslots, bad);
+    if (cap > 8)
+        hipLaunchKernelGGL(k_kad_shard_deliver<16>, dim3(nblk(n, 256)), dim3(256), 0, s,
+                           static_cast<const ovs_kad_resp16*>(in), n, static_cast<KadResN<16>*>(res), nslots, bad);
+    else
+        hipLaunchKernelGGL(k_kad_shard_deliver<8>, dim3(nblk(n, 256)), dim3(256), 0, s,
+                           static_cast<const ovs_kad_resp*>(in), n, static_cast<KadResN<8>*>(res), nslots, bad);
     return hipGetLastError();
 }
 

@@ -5,14 +5,26 @@
 
 namespace ovs {
 
-// findNode result slot of one pending FindNodeCall of a lookup (home rank)
-struct KadRes {
-    uint32_t count;      // result size (<= 8)
+// findNode result slot of one pending FindNodeCall of a lookup (home rank); C = the findNode
+// capacity of the network (8; 16 for KademliaLarge)
+template <int C>
+struct KadResN {
+    uint32_t count;      // result size (<= C)
     uint32_t ready;      // 0 = requested, not delivered yet
-    uint32_t nodes[8];
-    uint64_t dist[8];    // top 64 bits of node XOR key
+    uint32_t nodes[C];
+    uint64_t dist[C];    // top 64 bits of node XOR key
 };
-static_assert(sizeof(KadRes) == 104, "KadRes layout");
+using KadRes = KadResN<8>;
+static_assert(sizeof(KadResN<8>) == 104 && sizeof(KadResN<16>) == 200, "KadRes layout");
+// the response record on the wire: ovs_kad_resp (C = 8) / ovs_kad_resp16
+template <int C> struct KadWire;
+template <> struct KadWire<8> { using type = ovs_kad_resp; };
+template <> struct KadWire<16> { using type = ovs_kad_resp16; };
+// the network's findNode capacity on the shard path: 16 when k or lookupRedundantNodes exceed 8
+inline int kad_shard_cap(const ovs_params& P, const KadTables& t)
+{
+    return (P.lookupRedundantNodes > 8 || t.k > 8) ? 16 : 8;
+}
 
 // what the shard-step instantiation of K2 (kad_route.hip) reads and writes in one round
 struct KadShardStepArgs {
@@ -20,7 +32,7 @@ struct KadShardStepArgs {
     uint8_t* act;                      // 2: not started, 1: suspended in st, 0: never runs (source off the arc)
     const K160* qkeys;                 // the batch's keys and sources (a lookup starts from them in the
     const uint32_t* qsrc;              // round that first visits it: no state record before its first suspend)
-    KadRes* res;                       // nlook * A result slots
+    void* res;                         // nlook * A result slots (KadResN<C>)
     const uint64_t* list;              // this round's lookups (indices), *nlist_dev of them
     const unsigned long long* nlist_dev;
     uint64_t nlist_max;                // sizes the grid (the lookups of the batch)
@@ -34,7 +46,7 @@ struct KadShardStepArgs {
     uint32_t* sib_out;                 // LookupCalls: the sibling rows (nullptr: KBR routes)
 };
 
-size_t kad_lookup_state_bytes(int alpha);
+size_t kad_lookup_state_bytes(int alpha, int cap);
 bool kad_params_supported_host(const ovs_params& P, const KadTables& t);
 // lookups of this rank: their keys and sources (copied to qkeys / qsrc), act = 2 (not started), qids,
 // the round-1 list (indices 0..n-1) and its count; sources off [lo, hi) are counted in *bad and never run
@@ -47,15 +59,16 @@ hipError_t kad_shard_init(const K160* keys, const uint32_t* src, uint64_t n, uin
 // next list (*nlist_next) and are counted in *active_count.  bad: table reads off the arc.
 hipError_t kad_shard_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
                           const DelayConsts& DC, void* st, uint8_t* act, const K160* qkeys, const uint32_t* qsrc,
-                          const uint32_t* qids, KadRes* res,
+                          const uint32_t* qids, void* res,
                           uint64_t nlook, const uint64_t* list, const unsigned long long* nlist, const uint64_t* iota,
                           uint64_t* list_next, unsigned long long* nlist_next, const uint64_t* shard_lo, int nsh,
                           ovs_kad_req* out, uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done,
                           uint64_t done_cap, unsigned long long* done_count, unsigned long long* active_count, int lk_ns,
                           uint32_t* sib_out, unsigned long long* bad, int num_cu, StageBuf& stage, hipStream_t s);
 hipError_t kad_shard_serve(const KadTables& t, uint32_t n, const ovs_params& P, const ovs_kad_req* in, uint64_t nreq,
-                           ovs_kad_resp* out, unsigned long long* bad, hipStream_t s);
-hipError_t kad_shard_deliver(const ovs_kad_resp* in, uint64_t n, KadRes* res, uint64_t nslots,
-                             unsigned long long* bad, hipStream_t s);
+                           void* out, unsigned long long* bad, hipStream_t s);
+// cap: the network's findNode capacity (kad_shard_cap): the record types of in / res
+hipError_t kad_shard_deliver(int cap, const void* in, uint64_t n, void* res, uint64_t nslots, unsigned long long* bad,
+                             hipStream_t s);
 
 }  // namespace ovs

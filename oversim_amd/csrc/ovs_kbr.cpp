@@ -70,7 +70,7 @@ struct ovs_ctx {
     K160* kkeys = nullptr;               // the batch's keys and sources (a lookup starts from them)
     uint32_t* ksrc = nullptr;
     uint32_t* kqids = nullptr;
-    KadRes* kres = nullptr;              // alpha findNode result slots per lookup
+    void* kres = nullptr;                // alpha findNode result slots per lookup (KadResN<kfcap>)
     unsigned long long* kbad = nullptr;  // undeliverable responses
     uint64_t* kiota = nullptr;           // lookup indices 0..n-1: round 1's list, the source of the next lists
     uint64_t* klist[2] = {nullptr, nullptr};   // ping-pong lists of the still active lookups
@@ -78,6 +78,7 @@ struct ovs_ctx {
     int kcur = 0;                        // list of the next round: 0 = iota, 1/2 = klist[0/1]
     uint64_t knlook = 0, kcap = 0;
     int kalpha = 0;
+    int kfcap = 8;                       // findNode capacity of the shard records (8; 16 KademliaLarge)
     int32_t kns = -1;                    // LookupCall batch: numSiblings (-1: KBR routes)
     uint32_t* ksib = nullptr;            // ... and the caller's sibling rows
     // scratch for host-pointer calls
@@ -910,15 +911,16 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     const int alpha = c->P.lookupParallelRpcs;
-    if (n > c->kcap || alpha != c->kalpha) {
+    const int fcap = kad_shard_cap(P, c->kad);
+    if (n > c->kcap || alpha != c->kalpha || fcap != c->kfcap) {
         free_kad_shard(c);
         const uint64_t cap = n ? n : 1;
-        HIPCHK(c, hipMalloc(&c->kst, kad_lookup_state_bytes(alpha) * cap));
+        HIPCHK(c, hipMalloc(&c->kst, kad_lookup_state_bytes(alpha, fcap) * cap));
         HIPCHK(c, hipMalloc(&c->kact, cap));
         HIPCHK(c, hipMalloc(&c->kkeys, sizeof(K160) * cap));
         HIPCHK(c, hipMalloc(&c->ksrc, sizeof(uint32_t) * cap));
         HIPCHK(c, hipMalloc(&c->kqids, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->kres, sizeof(KadRes) * cap * kad_pend_slots(alpha)));
+        HIPCHK(c, hipMalloc(&c->kres, (fcap > 8 ? sizeof(KadResN<16>) : sizeof(KadResN<8>)) * cap * kad_pend_slots(alpha)));
         HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
         HIPCHK(c, hipMalloc(&c->kiota, sizeof(uint64_t) * cap));
         HIPCHK(c, hipMalloc(&c->klist[0], sizeof(uint64_t) * cap));
@@ -926,6 +928,7 @@ ovs_status kad_shard_begin_impl(ovs_ctx* c, int32_t lk_ns, uint32_t* sib, const 
         HIPCHK(c, hipMalloc(&c->knl, sizeof(unsigned long long) * 3));
         c->kcap = cap;
         c->kalpha = alpha;
+        c->kfcap = fcap;
     }
     c->knlook = n;
     c->kns = lk_ns;
@@ -996,7 +999,13 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint64_t out_cap, un
     return OVS_OK;
 }
 
-ovs_status ovs_kad_shard_serve(ovs_ctx* c, const ovs_kad_req* in, uint64_t n, ovs_kad_resp* out, void* stream)
+int32_t ovs_kad_shard_resp_bytes(const ovs_ctx* c)
+{
+    if (!c || c->overlay != OVS_OVERLAY_KADEMLIA) return -1;
+    return kad_shard_cap(c->P, c->kad) > 8 ? (int32_t)sizeof(ovs_kad_resp16) : (int32_t)sizeof(ovs_kad_resp);
+}
+
+ovs_status ovs_kad_shard_serve(ovs_ctx* c, const ovs_kad_req* in, uint64_t n, void* out, void* stream)
 {
     if (!c || (n && (!in || !out))) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
@@ -1006,12 +1015,13 @@ ovs_status ovs_kad_shard_serve(ovs_ctx* c, const ovs_kad_req* in, uint64_t n, ov
     return OVS_OK;
 }
 
-ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const ovs_kad_resp* in, uint64_t n, void* stream)
+ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const void* in, uint64_t n, void* stream)
 {
     if (!c || (n && !in)) return OVS_EINVAL;
     if (!c->kres) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
     HIPCHK(c, hipSetDevice(c->device));
-    hipError_t e = kad_shard_deliver(in, n, c->kres, c->knlook * (uint64_t)kad_pend_slots(c->kalpha), c->kbad, (hipStream_t)stream);
+    hipError_t e = kad_shard_deliver(c->kfcap, in, n, c->kres, c->knlook * (uint64_t)kad_pend_slots(c->kalpha), c->kbad,
+                                     (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard deliver");
     return OVS_OK;
 }

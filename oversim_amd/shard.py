@@ -207,6 +207,7 @@ for _name, _args in {
     "ovs_kad_shard_serve": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p],
     "ovs_kad_shard_deliver": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
     "ovs_kad_shard_errors": [C.c_void_p, C.c_void_p],
+    "ovs_kad_shard_resp_bytes": [C.c_void_p],
 }.items():
     _f = getattr(lib(), _name)
     _f.argtypes = _args
@@ -444,8 +445,10 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
 
 KAD_REQ_DTYPE = np.dtype([("key", "<u4", 5), ("node", "<u4"), ("tag", "<u4"), ("pad", "<u4")])
 KAD_RESP_DTYPE = np.dtype([("tag", "<u4"), ("count", "<u4"), ("nodes", "<u4", 8), ("dist_hi", "<u8", 8)])
+# KademliaLarge (k or lookupRedundantNodes above 8): ovs_kad_resp16
+KAD_RESP16_DTYPE = np.dtype([("tag", "<u4"), ("count", "<u4"), ("nodes", "<u4", 16), ("dist_hi", "<u8", 16)])
 KAD_REQ_BYTES, KAD_RESP_BYTES = KAD_REQ_DTYPE.itemsize, KAD_RESP_DTYPE.itemsize
-assert (KAD_REQ_BYTES, KAD_RESP_BYTES) == (32, 104)
+assert (KAD_REQ_BYTES, KAD_RESP_BYTES, KAD_RESP16_DTYPE.itemsize) == (32, 104, 200)
 
 
 class KadShardStepper:
@@ -476,6 +479,8 @@ class KadShardStepper:
         self.kernel_ms = 0.0
         self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         self._timed = False
+        # response records: 104 B, or 200 B (ovs_kad_resp16) for KademliaLarge
+        self.resp_bytes = int(lib().ovs_kad_shard_resp_bytes(self.eng._h))
 
     def _s(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
@@ -532,7 +537,7 @@ class KadShardStepper:
     def serve(self, reqs):
         n = reqs.shape[0]
         self.served += n
-        resp = self.torch.empty((n, KAD_RESP_BYTES), dtype=self.torch.uint8, device=self.dev)
+        resp = self.torch.empty((n, self.resp_bytes), dtype=self.torch.uint8, device=self.dev)
         if n:
             st = lib().ovs_kad_shard_serve(self.eng._h, self._p(reqs), n, self._p(resp), self._s())
             self.eng._chk(st, "ovs_kad_shard_serve")

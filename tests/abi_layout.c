@@ -104,6 +104,9 @@ int main(void)
     S(ovs_kad_resp);
     F(ovs_kad_resp, tag); F(ovs_kad_resp, count); F(ovs_kad_resp, nodes); F(ovs_kad_resp, dist_hi);
     end();
+    S(ovs_kad_resp16);
+    F(ovs_kad_resp16, tag); F(ovs_kad_resp16, count); F(ovs_kad_resp16, nodes); F(ovs_kad_resp16, dist_hi);
+    end();
     printf("}\n");
     return 0;
 }

@@ -41,6 +41,7 @@ DTYPES = {
     "ovs_lookup_rec": shard.REC_DTYPE,
     "ovs_kad_req": shard.KAD_REQ_DTYPE,
     "ovs_kad_resp": shard.KAD_RESP_DTYPE,
+    "ovs_kad_resp16": shard.KAD_RESP16_DTYPE,
     "ovs_koorde_ext": kbr.KOORDE_EXT_DTYPE,
 }
 

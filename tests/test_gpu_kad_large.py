@@ -143,13 +143,47 @@ def test_refresh_k16(engine: KbrEngine):
         assert np.array_equal(r["responders"], e["responders"]) and np.array_equal(r["rtt_ns"], e["rtt_ns"]), R
 
 
-def test_sharded_path_refuses_k16():
-    """The sharded request/response path exchanges findNode answers of at most 8 nodes."""
+@pytest.mark.parametrize("world,alpha,ns", [(2, 3, None), (4, 1, None), (4, 3, 8), (3, 3, 0)])
+def test_sharded_k16_matches_single_context(engine: KbrEngine, world, alpha, ns):
+    """KademliaLarge on W arcs (W contexts on one GPU, the in-process exchange): findNode answers of
+    up to 16 nodes travel as ovs_kad_resp16 records; every lookup (one-way or LookupCall) equals the
+    single-context K2's."""
     import torch
-    from oversim_amd.shard import KadShardStepper, arc_bounds
-    net = W.population(2000, 5)
-    st = KadShardStepper(net.ids, net.xy, arc_bounds(2000, 2), 0, torch.device("cuda", 0),
-                         params=Params.kademlia().replace(**LARGE))
-    k, s = W.lookups(net.ids, 10, 6, node_ids=True)
-    with pytest.raises(KbrError, match="not implemented"):
-        st.begin(torch.from_numpy(k.view(np.int32)).cuda(), torch.from_numpy(np.zeros(10, np.int32)).cuda(), 0)
+    from oversim_amd.shard import KadShardStepper, arc_bounds, done_to_numpy, route_kad_local_shards
+    n, m = 6000, 1500
+    net = W.population(n, 0x16A + world)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=alpha, **LARGE)
+    ks, ss, qb, allk, alls = [], [], [], [], []
+    for r in range(world):
+        k, s0 = W.lookups(net.ids, m, 0x170 + r, node_ids=(r % 2 == 0))
+        s0 = (bounds[r] + s0.astype(np.int64) % (bounds[r + 1] - bounds[r])).astype(np.uint32)
+        ks.append(torch.from_numpy(k.view(np.int32)).to(dev))
+        ss.append(torch.from_numpy(s0.view(np.int32)).to(dev))
+        qb.append(r * m)
+        allk.append(k); alls.append(s0)
+    allk, alls = np.concatenate(allk), np.concatenate(alls)
+    steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params, lookup_siblings=ns)
+                for r in range(world)]
+    assert all(st.resp_bytes == 200 for st in steppers)
+    dones, rounds = route_kad_local_shards(steppers, ks, ss, qb)
+    assert rounds >= 2
+    engine.set_params(params)
+    engine.kad_load(net.ids, net.xy)
+    if ns is None:
+        d = np.concatenate([done_to_numpy(x) for x in dones])
+        d = d[np.argsort(d["qid"])]
+        assert np.array_equal(d["qid"], np.arange(world * m))
+        ref = engine.lookup(allk, alls, count_rpcs=True)
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+            assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+        assert np.array_equal(d["pad"].astype(np.int64), ref["rpcs"].astype(np.int64))
+    else:
+        ref = engine.lookupCall(allk, alls, ns)
+        for r in range(world):
+            qid, lo, sib = steppers[r].lookup_results(dones[r])
+            for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+                assert np.array_equal(lo[f].astype(np.int64), np.asarray(ref[f])[qid].astype(np.int64)), (r, f)
+            nsl = max(ns, 1)
+            assert np.array_equal(sib[:, :nsl], np.asarray(ref["siblings"])[qid][:, :nsl])
