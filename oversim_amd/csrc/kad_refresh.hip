@@ -37,6 +37,7 @@ constexpr int XMAXDEAD = 64;    // nodes whose RPC timed out, per lookup
 struct XCfg {
     int R, ns, alpha, hcm, k;      // ns: the siblings vector's size (numSiblings <= R)
     int oneway;                    // 1: a KBRTestApp one-way lookup (route message to the result)
+    int pad;                       // 1: responder / RTT rows padded to hopCountMax (NONE / -1)
     int64_t bwFull, bwOne;         // T(L*8/datarate) of a FindNodeResponse with R nodes / one node
     int strict, visitOnlyOnce, newOnResp, newOnTimeout, finishOnFirst;
 };
@@ -640,10 +641,11 @@ __device__ __forceinline__ void kx_emit(const XLookup<XA>& L, const KadView& V, 
                                         uint32_t* __restrict__ rpcs_out, uint32_t* __restrict__ err)
 {
     if (L.err) atomicOr(err, 1u);
-    for (int j = L.nhop; j < C.hcm; ++j) {
-        resp[j] = NONE;
-        if (rtt) rtt[j] = -1;
-    }
+    if (C.pad)
+        for (int j = L.nhop; j < C.hcm; ++j) {
+            resp[j] = NONE;
+            if (rtt) rtt[j] = -1;
+        }
     const bool valid = L.success && !L.err;
     const uint8_t fail_status = L.now > DC.lookupTimeout ? OVS_LOOKUP_TIMEOUT
                                 : L.nd > 0                 ? OVS_LOOKUP_RPC_TIMEOUT
@@ -827,7 +829,7 @@ size_t g_scratch_cap[64] = {};
 hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
                           int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
                           uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace)
+                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace, bool pad)
 {
     *capacity_error = false;
     if (nq == 0) return hipSuccess;
@@ -839,6 +841,7 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     XCfg C;
     C.R = R; C.ns = ns; C.alpha = A; C.hcm = P.hopCountMax; C.k = t.k;
     C.oneway = oneway ? 1 : 0;
+    C.pad = pad ? 1 : 0;
     C.strict = P.lookupStrictParallelRpcs; C.visitOnlyOnce = P.lookupVisitOnlyOnce;
     C.newOnResp = P.lookupNewRpcOnEveryResponse; C.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
     C.finishOnFirst = P.lookupFinishOnFirstUnchanged;

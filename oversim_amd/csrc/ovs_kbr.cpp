@@ -1316,8 +1316,9 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         uint32_t* dres = nullptr;
         HIPCHK(c, hipMalloc(&dres, sizeof(uint32_t) * n));
         bool cap_err = false;
+        // dhop was filled with NONE above: the kernel leaves the rows unpadded
         e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->P.lookupRedundantNodes, 1, true,
-                           dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err);
+                           dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err, nullptr, false);
         hipFree(dres);
         if (e == hipSuccess && cap_err) return fail(c, OVS_ENOTSUP, "a lookup exceeded the kernel's capacity (64 timed-out nodes)");
     } else if (c->P.routingType == 1 || c->P.routingType == 2) {
@@ -1448,7 +1449,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         // lookupRpc with EXHAUSTIVE_ITERATIVE_ROUTING: redundantNodes = lookupRedundantNodes, numSiblings = ns
         bool cap_err = false;
         e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), P.lookupRedundantNodes, ns, false, dk, ds,
-                           n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err);
+                           n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err, nullptr, false);
         if (e == hipSuccess && cap_err) e = hipErrorNotSupported;
     } else if (kad_rec) {
         // RecursiveLookup (RecursiveLookup.cc:52-139): a routed FindNodeCall, the response back by UDP
@@ -1533,7 +1534,8 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
     else drpc = rpcs;
     bool cap_err = false;
     const hipError_t e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), R, R, false, dk, ds, n, dout,
-                                        dsib, dresp, drtt, drpc, c->num_cu, s, &cap_err);
+                                        dsib, dresp, drtt, drpc, c->num_cu, s, &cap_err, nullptr,
+                                        responders != nullptr /* else the internal visited lists: no padding */);
     if (e != hipSuccess) { cleanup(); return hip_fail(c, e, "refresh lookup kernel"); }
     if (cap_err) { cleanup(); return fail(c, OVS_ENOTSUP, "a refresh lookup exceeded the kernel's capacity (64 timed-out nodes)"); }
     if (!dev) {
