@@ -554,6 +554,15 @@ ovs_status  ovs_shard_step_lookup(ovs_ctx* ctx, int32_t num_siblings, const ovs_
                                   ovs_lookup_rec* out, uint64_t out_cap, unsigned long long* out_count,
                                   ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
                                   const uint64_t* shard_lo, uint32_t nshards, void* stream);
+/* The first round of a batch straight from its keys and sources (device memory, ABI 10): the same
+ * as ovs_shard_make_records followed by ovs_shard_step / ovs_shard_step_lookup on those records,
+ * without writing and reading them (lookup i has qid qid_base + i).  num_siblings 0: one-way KBR
+ * routes (ovs_shard_step); otherwise LookupCalls with that many siblings (-1 = successorListSize). */
+ovs_status  ovs_shard_step_keys(ovs_ctx* ctx, int32_t num_siblings, const ovs_key160* keys, const uint32_t* src,
+                                uint64_t n, uint32_t qid_base, ovs_lookup_rec* out, uint64_t out_cap,
+                                unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                                unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards,
+                                void* stream);
 ovs_status  ovs_shard_lookup_finish(ovs_ctx* ctx, const ovs_done_rec* done, uint64_t n, int32_t num_siblings,
                                     ovs_lookup_out* out, uint32_t* siblings, void* stream);
 

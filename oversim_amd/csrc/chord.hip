@@ -471,6 +471,9 @@ struct LaneIO {
     uint32_t* __restrict__ hopseq;
     // one hop round of an arc (ovs_shard_step)
     const ovs_lookup_rec* __restrict__ in;
+    const K160* __restrict__ fkeys;        // a batch's first round straight from its keys and sources
+    const uint32_t* __restrict__ fsrc;     // (ovs_shard_step_keys; in == nullptr): lookup q has qid fqid + q
+    uint32_t fqid;
     ovs_lookup_rec* __restrict__ sout;     // nsh segments of scap records, one per destination arc
     uint64_t scap;
     unsigned long long* scount;            // nsh counters
@@ -550,7 +553,13 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
                 active = true;
                 fresh = true;
                 ph = PH_FETCH;
-                if (SHARD) {
+                if (SHARD && io.fkeys) {
+                    // a batch's first round: no record, the lookup starts from its key and source
+                    K = io.fkeys[q];
+                    S = io.fsrc[q];
+                    qid = io.fqid + (uint32_t)q;
+                    lp = nullptr;
+                } else if (SHARD) {
                     // the 48 B hand-off record comes through the cooperative gather (tag 1: 3 chunks)
                     lp = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(io.in + q) | 1u);
                 } else {
@@ -587,11 +596,15 @@ __global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC
             // ---- consume the pending line
             if (ph == PH_FETCH) {
                 if (SHARD) {
-                    K.w[0] = L0.x; K.w[1] = L0.y; K.w[2] = L0.z; K.w[3] = L0.w; K.w[4] = L1.x;
-                    S = L1.y; cur = L1.z; qid = L1.w;
-                    t = (int64_t)u64(L2.x, L2.y);
-                    hops = (int)(L2.z & 0xFFFF);
-                    local = ((L2.z >> 16) & 0xFF) != 0;
+                    if (io.fkeys) {
+                        cur = S; t = 0; hops = 0; local = true;
+                    } else {
+                        K.w[0] = L0.x; K.w[1] = L0.y; K.w[2] = L0.z; K.w[3] = L0.w; K.w[4] = L1.x;
+                        S = L1.y; cur = L1.z; qid = L1.w;
+                        t = (int64_t)u64(L2.x, L2.y);
+                        hops = (int)(L2.z & 0xFFFF);
+                        local = ((L2.z >> 16) & 0xFF) != 0;
+                    }
                     if (S >= V.n || cur >= V.n) {
                         // a row the exchange never wrote (receive buffers are 0xFF-filled) or a corrupted
                         // record: finished as BROKEN with its qid (0xFFFFFFFF for the sentinel), which
@@ -1279,7 +1292,8 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    const uint64_t* shard_lo, int nsh, int me, const ovs_lookup_rec* in, uint64_t nin,
                                    ovs_lookup_rec* out, uint64_t out_cap,
                                    unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                                   unsigned long long* done_count, StageBuf& stage, int num_cu, hipStream_t s)
+                                   unsigned long long* done_count, StageBuf& stage, int num_cu, hipStream_t s,
+                                   const K160* fkeys, const uint32_t* fsrc, uint32_t fqid)
 {
     if (nin == 0) return hipSuccess;
     if (nsh < 1 || nsh + 1 > CMAX) return hipErrorInvalidValue;
@@ -1290,6 +1304,7 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
     uint8_t* sb = static_cast<uint8_t*>(stage.buf);
     LaneIO io{};
     io.in = in; io.sout = out; io.scap = out_cap; io.scount = out_count;
+    io.fkeys = fkeys; io.fsrc = fsrc; io.fqid = fqid;
     io.done = done; io.dcap = done_cap; io.dcount = done_count;
     io.shard_lo = shard_lo; io.nsh = nsh; io.me = me; io.n = nin;
     io.stage_hand = reinterpret_cast<ovs_lookup_rec*>(sb + oh);

@@ -457,10 +457,11 @@ ovs_status upload_bounds(ovs_ctx* c, const uint64_t* lo, uint32_t nshards)
 // ns = 0: one-way routes (ovs_shard_step); ns >= 1: LookupCalls with that many siblings
 static ovs_status shard_step(ovs_ctx* c, int ns, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out,
                              uint64_t out_cap, unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
-                             unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream)
+                             unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards, void* stream,
+                             const ovs_key160* fkeys = nullptr, const uint32_t* fsrc = nullptr, uint32_t fqid = 0)
 {
     if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
-    if (n_in && (!in || !out || !out_count || !done || !done_count)) return OVS_EINVAL;
+    if (n_in && ((!in && !(fkeys && fsrc)) || !out || !out_count || !done || !done_count)) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_CHORD || !c->ideal) return fail(c, OVS_ESTATE, "no Chord ring (shard) loaded");
     ovs_status st = check_common(c, c->P);
     if (st == OVS_OK) st = check_chord_route(c, c->P);
@@ -494,8 +495,25 @@ static ovs_status shard_step(ovs_ctx* c, int ns, const ovs_lookup_rec* in, uint6
     st = ensure_nodes(c, s);
     if (st != OVS_OK) return st;
     HIPCHK(c, launch_chord_shard_step(chord_view(c), DC, LC, c->d_bounds, (int)nshards, me, in, n_in, out, out_cap,
-                                      out_count, done, done_cap, done_count, c->stage[s], c->num_cu, s));
+                                      out_count, done, done_cap, done_count, c->stage[s], c->num_cu, s,
+                                      reinterpret_cast<const K160*>(fkeys), fsrc, fqid));
     return OVS_OK;
+}
+
+ovs_status ovs_shard_step_keys(ovs_ctx* c, int32_t num_siblings, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                               uint32_t qid_base, ovs_lookup_rec* out, uint64_t out_cap, unsigned long long* out_count,
+                               ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                               const uint64_t* shard_lo, uint32_t nshards, void* stream)
+{
+    if (!c || (n && (!keys || !src))) return OVS_EINVAL;
+    int32_t ns = 0;
+    if (num_siblings != 0) {
+        ns = num_siblings < 0 ? c->P.successorListSize : num_siblings;
+        if (ns > c->P.successorListSize) return fail(c, OVS_EINVAL, "numSiblings too big!");
+        if (ns < 1 || ns > 8) return fail(c, OVS_ENOTSUP, "LookupCall across arcs implements numSiblings 1..8");
+    }
+    return shard_step(c, ns, nullptr, n, out, out_cap, out_count, done, done_cap, done_count, shard_lo, nshards, stream,
+                      keys, src, qid_base);
 }
 
 ovs_status ovs_shard_step(ovs_ctx* c, const ovs_lookup_rec* in, uint64_t n_in, ovs_lookup_rec* out, uint64_t out_cap,

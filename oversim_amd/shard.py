@@ -50,6 +50,15 @@ def arc_bounds(n_total: int, world: int) -> list[int]:
 # ---------------------------------------------------------------------------
 # steppers
 
+class FreshBatch:
+    """A batch's first-round inbox: its keys and sources, not yet records (GpuShardStepper.first_batch)."""
+
+    def __init__(self, keys, src, qid_base: int):
+        self.keys, self.src, self.qid_base = keys, src, int(qid_base)
+        self.shape = (int(keys.shape[0]), REC_BYTES)
+        self.device = keys.device
+
+
 class GpuShardStepper:
     """One rank's arc on one device: owns the engine context and the device buffers."""
 
@@ -137,6 +146,11 @@ class GpuShardStepper:
         self.eng._chk(st, "ovs_shard_make_records")
         return recs
 
+    def first_batch(self, keys_t, src_t, qid_base: int):
+        """A batch's first-round inbox without records: step() runs it through ovs_shard_step_keys,
+        which starts every lookup from its key and source (no 48 B record written and read back)."""
+        return FreshBatch(keys_t, src_t, qid_base)
+
     def step(self, inbox, cohort: int = 0):
         """One round of a cohort; returns (send segments [world, cap, 48], per-destination counts
         on the device).  The segments stay valid until the cohort's next step."""
@@ -146,9 +160,19 @@ class GpuShardStepper:
         cnt.zero_()
         if self.timing:
             self._ev[cohort][0].record()
-        args = (C.c_void_p(inbox.data_ptr()), n_in, C.c_void_p(out.data_ptr()), self._cap[cohort],
-                C.c_void_p(cnt.data_ptr()), C.c_void_p(self.done.data_ptr()), self.done_cap,
-                C.c_void_p(self.done_count.data_ptr()), self._lo, self.world, self._s())
+        tail = (C.c_void_p(out.data_ptr()), self._cap[cohort], C.c_void_p(cnt.data_ptr()),
+                C.c_void_p(self.done.data_ptr()), self.done_cap, C.c_void_p(self.done_count.data_ptr()), self._lo,
+                self.world, self._s())
+        if isinstance(inbox, FreshBatch):
+            ns = 0 if self.lookup_siblings is None else self.lookup_siblings
+            self.eng._chk(lib().ovs_shard_step_keys(self.eng._h, ns, C.c_void_p(inbox.keys.data_ptr()),
+                                                    C.c_void_p(inbox.src.data_ptr()), n_in, inbox.qid_base, *tail),
+                          "ovs_shard_step_keys")
+            if self.timing:
+                self._ev[cohort][1].record()
+                self._timed[cohort] = True
+            return out, cnt
+        args = (C.c_void_p(inbox.data_ptr()), n_in) + tail
         if self.lookup_siblings is None:
             self.eng._chk(lib().ovs_shard_step(self.eng._h, *args), "ovs_shard_step")
         else:
@@ -198,6 +222,9 @@ for _name, _args in {
     "ovs_shard_step_lookup": [C.c_void_p, C.c_int32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                               C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
     "ovs_shard_lookup_finish": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p],
+    "ovs_shard_step_keys": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
+                            C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
+                            C.c_void_p],
     "ovs_kad_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
     "ovs_kad_shard_begin": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p],
     "ovs_kad_shard_begin_lookup": [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
@@ -351,10 +378,10 @@ def route_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: i
     ctx = stepper.cohort if hasattr(stepper, "cohort") else (lambda c: _NoCtx())
     step = (lambda inbox, c: stepper.step(inbox, c)) if hasattr(stepper, "cohort") else (lambda inbox, c: stepper.step(inbox))
     inbox = []
+    first = getattr(stepper, "first_batch", stepper.make_records)
     for c in range(cohorts):
         with ctx(c):
-            inbox.append(stepper.make_records(keys_t[bounds[c]:bounds[c + 1]], src_t[bounds[c]:bounds[c + 1]],
-                                              qid_base + bounds[c]))
+            inbox.append(first(keys_t[bounds[c]:bounds[c + 1]], src_t[bounds[c]:bounds[c + 1]], qid_base + bounds[c]))
     live = [True] * cohorts
     rounds = 0
     while any(live):
@@ -394,7 +421,13 @@ def check_complete(done, n: int, what: str, exchange=None, sentinel: bool = True
     ovs_kad_shard_errors instead)."""
     k = len(done)
     if sentinel and k and hasattr(done, "dim") and done.dim() == 2:     # device records (test doubles hand lists)
-        sent = int((done[:, :4] == 0xFF).all(dim=1).sum().item())
+        # the qid word of a sentinel record is 0xFFFFFFFF: one strided compare + any over the qid column
+        # (the byte-wise all() over (n, 4) cost 0.3 ms per 10M records)
+        if done.shape[1] % 4 == 0 and done.is_contiguous():
+            import torch
+            sent = int((done.view(torch.int32)[:, 0] == -1).sum().item())
+        else:
+            sent = int((done[:, :4] == 0xFF).all(dim=1).sum().item())
         if sent:
             raise RuntimeError(f"{what}: {sent} finished records from unwritten or corrupt exchange rows")
     have, want = k, n
@@ -416,7 +449,8 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
     """Single-process emulation of W ranks (e.g. W contexts on one GPU): the exchange is a concatenation."""
     import torch
     W = len(steppers)
-    inbox = [steppers[r].make_records(keys_per_shard[r], src_per_shard[r], qid_bases[r]) for r in range(W)]
+    inbox = [getattr(steppers[r], "first_batch", steppers[r].make_records)(keys_per_shard[r], src_per_shard[r], qid_bases[r])
+             for r in range(W)]
     rounds = 0
     while True:
         rounds += 1
