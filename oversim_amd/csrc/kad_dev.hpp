@@ -236,6 +236,26 @@ __device__ __forceinline__ void blk_merge_top8(Blk8& a, const Blk8& b, const K16
     blk_merge_top<F, EX, 8, 8>(a, b, K, nodes);
 }
 
+// a <- the C smallest of sorted a and the single entry (d, x): its position is the count of entries
+// closer, the entries from there on move down one (the last drops) -- what blk_merge_top computes
+// for a block holding one entry, in C compares and selects instead of C min + (C/2)log2(C) comparators
+// (no payload flags: the findNode blocks)
+template <bool EX, int C>
+__device__ __forceinline__ void blk_insert1(BlkN<C>& a, uint64_t d, uint32_t x, const K160& K,
+                                            const KadNode* __restrict__ nodes)
+{
+    bool lt[C];
+#pragma unroll
+    for (int i = 0; i < C; ++i) lt[i] = cand_lt<EX>(d, x, a.d[i], a.x[i], K, nodes);   // x goes before entry i
+#pragma unroll
+    for (int i = C - 1; i >= 0; --i) {
+        const bool here = lt[i] && (i == 0 || !lt[i - 1]);
+        const bool down = i > 0 && lt[i - 1];
+        a.d[i] = down ? a.d[i > 0 ? i - 1 : 0] : here ? d : a.d[i];
+        a.x[i] = down ? a.x[i > 0 ? i - 1 : 0] : here ? x : a.x[i];
+    }
+}
+
 template <int C>
 __device__ __forceinline__ void blk_clear(BlkN<C>& b)
 {
@@ -429,8 +449,16 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         Blk8 b;
         const int cnt = blk_load_block(b, blk, K);
         if (cnt) {
-            blk_sort8<false, EX>(b, K, V.nodes);
+            // a block holding one entry at its start (a sibling row's last block: 9 entries at s = 8)
+            // is sorted and enters the result by one insertion
+#ifdef OVS_KAD_NO_INSERT1
+            const bool one = false;                  // A/B: the round-3 sort + merge for every block
+#else
+            const bool one = cnt == 1 && b.x[0] != NONE;
+#endif
+            if (!one) blk_sort8<false, EX>(b, K, V.nodes);
             if (seen == 0) blk_assign(res, b);       // into an empty result the merge is the sorted block itself
+            else if (one) blk_insert1<EX, C>(res, b.d[0], b.x[0], K, V.nodes);
             else blk_merge_top<false, EX, C, 8>(res, b, K, V.nodes);
             n = blk_trunc(res, cap);
             seen += cnt;

@@ -20,7 +20,7 @@ from oversim_amd.shard import (KAD_REQ_BYTES, KAD_RESP_BYTES, REC_BYTES, GpuShar
                                done_to_numpy)
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--workload", choices=["D", "E"], required=True)
+ap.add_argument("--workload", choices=["C", "D", "E"], required=True)
 ap.add_argument("--lookups-per-rank", type=int, default=0)
 ap.add_argument("--world", type=int, default=8)
 a = ap.parse_args()
@@ -49,10 +49,12 @@ if kad:
     for r in range(Wn):
         steppers[r].begin(inputs[r]["keys_t"], inputs[r]["src_t"], r * m)
 else:
-    steppers = [GpuShardStepper(ids, xy, bounds, r, dev, capacity=Wn * m, params=params) for r in range(Wn)]
+    # send segments of 1.25 m records per destination (a round's inbox is about m; step() grows them)
+    steppers = [GpuShardStepper(ids, xy, bounds, r, dev, capacity=m + m // 4, params=params) for r in range(Wn)]
     for st in steppers:
         st.reset(Wn * m)
-    inbox = [steppers[r].make_records(inputs[r]["keys_t"], inputs[r]["src_t"], r * m) for r in range(Wn)]
+    # the first round starts from the keys (ovs_shard_step_keys), as route_sharded
+    inbox = [steppers[r].first_batch(inputs[r]["keys_t"], inputs[r]["src_t"], r * m) for r in range(Wn)]
 torch.cuda.synchronize()
 print(json.dumps(dict(workload=a.workload, world=Wn, nodes=n, lookups_per_rank=m, setup_s=round(time.time() - t_start, 1))),
       flush=True)
