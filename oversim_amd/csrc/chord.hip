@@ -496,8 +496,13 @@ __device__ unsigned long long g_k1_stats[8];
 #endif
 
 // LKC: a LookupCall batch (ovs_lookup_batch): the responsible node's larger answer, no route message
+// minimum waves per SIMD: every instantiation at the single-GPU route's 5 (its 89 VGPRs); the shard
+// step's outcome staging had taken it to 98 VGPRs = 4 waves/SIMD
+#ifndef OVS_K1_WAVES
+#define OVS_K1_WAVES 5
+#endif
 template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
-__global__ __launch_bounds__(256) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
+__global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
