@@ -81,7 +81,12 @@ typedef struct ovs_params {
     int32_t keyLength;                  /* **.keyLength = 160 (only 160 supported) */
     int32_t hopCountMax;                /* **.hopCountMax = 50 */
     int32_t successorListSize;          /* **.chord.successorListSize = 8 */
-    int32_t extendedFingerTable;        /* **.chord.extendedFingerTable = false (only false) */
+    int32_t extendedFingerTable;        /* **.chord.extendedFingerTable = false.  true: Chord on a converged
+                                           ring (ovs_chord_load / _load_shard) when no FindNodeCall can time
+                                           out -- largest RTT from the coordinates' bounding box below
+                                           rpcUdpTimeout -- where its routes equal the non-extended ones;
+                                           refused otherwise, and for findNode answers of > 1 node and
+                                           maintenance rounds (OVS_ENOTSUP) */
     int32_t numFingerCandidates;        /* **.chord.numFingerCandidates = 3 */
     int32_t k, s, b;                    /* **.kademlia.k/s/b = 8/8/1 (b 2..5, bucketType != kademlia:
                                            tables through ovs_kad_load_tables_csr) */

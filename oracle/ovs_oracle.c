@@ -417,6 +417,9 @@ static int check_params(const orc_params* p)
     if (p->s < 1 || 5 * p->s > 120 || p->k < 1 || p->k > 64) { set_err("kademlia k must be 1..64, 5s <= 120"); return 0; }
     if (p->numSiblings < 0 || p->numSiblings > 16) { set_err("numSiblings must be 0..16"); return 0; }
     if (p->lookupRedundantNodes < 1 || p->lookupRedundantNodes > 64) { set_err("lookupRedundantNodes must be 1..64"); return 0; }
+    if (p->extendedFingerTable && (p->numFingerCandidates < 1 || p->numFingerCandidates > 64)) {
+        set_err("numFingerCandidates must be 1..64"); return 0;
+    }
     return 1;
 }
 
@@ -501,6 +504,9 @@ orc_net* orc_chord_build_tables(const orc_key* ids, uint32_t n, const double* xy
                                 const uint8_t* deque_size, const orc_params* p)
 {
     if (!check_params(p)) return NULL;
+    if (p->extendedFingerTable) {
+        set_err("extendedFingerTable: explicit tables carry no finger candidate lists"); return NULL;
+    }
     orc_net* net = net_alloc(NET_CHORD, ids, n, xy, p);
     if (!net) return NULL;
     net->sls = succ_stride;
@@ -628,6 +634,39 @@ static int chord_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self,
     return 0;
 }
 
+/* finger pos of a stable ring is trivial (2^pos <= succ0 - node): removed from the deque, which
+ * getFinger answers with the successor (Chord.cc:845-875, ChordFingerTable.cc:174-193) */
+static int ft_trivial(const orc_net* net, uint32_t node, uint32_t pos)
+{
+    if (net->lazy) {
+        OKey d = ok_sub(net->ids[succ_get(net, node, 0)], &net->ids[node]);
+        OKey off = ok_pow2(pos);
+        return ok_cmp(&off, &d) <= 0;
+    }
+    return 160 - pos - 1 >= net->fsize[node];
+}
+
+/* ChordFingerTable::getFinger(pos, key) with extendedFingerTable (ChordFingerTable.cc:195-228) on
+ * a stable ring: entry pos holds the FixfingersResponse of its finger f -- f, then f's first
+ * min(successorListSize, numFingerCandidates) successors (Chord::rpcFixfingers 1228-1251) --
+ * inserted in that order under the one key MAXTIME up to this node (handleRpcFixfingersResponse
+ * 1268-1287; no proximity routing); the answer keeps the candidates that do not reach past the
+ * key (!key.isBetweenLR(f, c)), else f.  A trivial position answers the successor. */
+static int chord_getFinger_ext(const orc_net* net, uint32_t self, uint32_t pos, const OKey* key, NVec* out)
+{
+    if (ft_trivial(net, self, pos)) { nv_push_back(out, succ_get(net, self, 0)); return 0; }
+    const uint32_t f = ft_getFinger(net, self, pos);
+    const int nf = nsucc_get(net, f);
+    const int m = nf < net->p.numFingerCandidates ? nf : net->p.numFingerCandidates;
+    for (int j = -1; j < m; ++j) {
+        const uint32_t c = j < 0 ? f : succ_get(net, f, (uint32_t)j);
+        if (c == self) break;
+        if (!ok_isBetweenLR(key, &net->ids[f], &net->ids[c])) nv_push_back(out, c);
+    }
+    if (out->size == 0) nv_push_back(out, f);
+    return 0;
+}
+
 static int chord_closestPreceedingNode(const orc_net* net, uint32_t self, const OKey* key, NVec* out) /* 602-674 */
 {
     uint32_t temp = NONE;
@@ -639,7 +678,8 @@ static int chord_closestPreceedingNode(const orc_net* net, uint32_t self, const 
     if (temp == NONE) { set_err("Chord::closestPreceedingNode(): Successor list broken"); return -1; }
     for (int i = 160 - 1; i >= 0; i--) {
         uint32_t f = ft_getFinger(net, self, (uint32_t)i);
-        if (ok_isBetweenLR(&net->ids[f], &net->ids[temp], key)) {   /* !extendedFingerTable */
+        if (ok_isBetweenLR(&net->ids[f], &net->ids[temp], key)) {
+            if (net->p.extendedFingerTable) return chord_getFinger_ext(net, self, (uint32_t)i, key, out);
             nv_push_back(out, f);
             return 0;
         }
@@ -1364,7 +1404,8 @@ static int ov_isSiblingFor(const orc_net* net, uint32_t node, uint32_t self, con
 }
 static int ov_maxRedundant(const orc_net* net)
 {
-    return net->type != NET_KAD ? 1 : net->p.k;   /* Chord.cc:416-419 (!extendedFingerTable), Kademlia.cc:352-355 */
+    if (net->type == NET_CHORD && net->p.extendedFingerTable) return net->p.numFingerCandidates;   /* Chord.cc:416-419 */
+    return net->type != NET_KAD ? 1 : net->p.k;   /* Chord.cc:416-419, Kademlia.cc:352-355 */
 }
 
 int orc_find_node(const orc_net* net, uint32_t node, const orc_key* key, int numRedundantNodes,
@@ -2516,6 +2557,7 @@ uint64_t orc_chord_stabilize(orc_net* net, const uint32_t* nodes, uint64_t m, ui
                              uint64_t* out_pred_changed)
 {
     if (net->type != NET_CHORD || net->lazy || !net->pred) { set_err("stabilize: explicit Chord tables"); return ORC_FAIL; }
+    if (net->p.extendedFingerTable) { set_err("stabilize: extendedFingerTable rounds not restated"); return ORC_FAIL; }
     const uint32_t n = net->n, sls = net->sls;
     uint32_t* pred0 = (uint32_t*)malloc(sizeof(uint32_t) * n);
     uint32_t* succ0 = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n * sls);
@@ -2595,6 +2637,7 @@ uint64_t orc_chord_fix_fingers(orc_net* net, const uint32_t* nodes, uint64_t m, 
                                uint64_t* out_changed, int nthreads)
 {
     if (net->type != NET_CHORD) { set_err("fix_fingers: not a Chord network"); return 0; }
+    if (net->p.extendedFingerTable) { set_err("fix_fingers: extendedFingerTable rounds not restated"); return 0; }
     chord_materialize(net);
     uint64_t cap = m * 160, nl = 0;
     orc_key* keys = (orc_key*)malloc(sizeof(orc_key) * (cap ? cap : 1));

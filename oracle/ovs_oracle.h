@@ -83,6 +83,10 @@ typedef struct {
     int32_t globalNodeLimit;          /* = 1000 */
     int32_t extraNodesFinalBucket;    /* = 0 */
     double  rpcKeyTimeout;            /* default.ini:484 = 10 s: a routed RPC (recursive LookupCalls) */
+    /* Chord.ned extendedFingerTable (default.ini:176 = false): finger entries hold the finger's
+     * FixfingersResponse candidates, getMaxNumRedundantNodes() = numFingerCandidates.  Stable
+     * (orc_chord_build / _lazy) rings only: explicit tables do not carry the candidate lists */
+    int32_t extendedFingerTable;
 } orc_params;
 
 void orc_params_chord_default(orc_params* p);

@@ -1333,6 +1333,36 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
     return compact_by_tag(io.stag, nin, P, stage.cs, s);
 }
 
+__global__ __launch_bounds__(256) void k_xy_bbox(const double2* __restrict__ xy, uint64_t n, double* __restrict__ out)
+{
+    __shared__ double sh[4][256];
+    double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const double2 p = xy[i];
+        x0 = fmin(x0, p.x); x1 = fmax(x1, p.x); y0 = fmin(y0, p.y); y1 = fmax(y1, p.y);
+    }
+    sh[0][threadIdx.x] = x0; sh[1][threadIdx.x] = x1; sh[2][threadIdx.x] = y0; sh[3][threadIdx.x] = y1;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            sh[0][threadIdx.x] = fmin(sh[0][threadIdx.x], sh[0][threadIdx.x + w]);
+            sh[1][threadIdx.x] = fmax(sh[1][threadIdx.x], sh[1][threadIdx.x + w]);
+            sh[2][threadIdx.x] = fmin(sh[2][threadIdx.x], sh[2][threadIdx.x + w]);
+            sh[3][threadIdx.x] = fmax(sh[3][threadIdx.x], sh[3][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) out[4 * blockIdx.x + threadIdx.x] = sh[threadIdx.x][0];
+}
+
+hipError_t launch_xy_bbox(const double2* xy, uint64_t n, double* out, int* blocks, hipStream_t s)
+{
+    const uint64_t b = nblk(n, 256);
+    *blocks = (int)(b < 256 ? (b ? b : 1) : 256);
+    hipLaunchKernelGGL(k_xy_bbox, dim3((unsigned)*blocks), dim3(256), 0, s, xy, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
                                ovs_lookup_rec* out, hipStream_t s)
 {

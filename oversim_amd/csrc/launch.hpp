@@ -35,6 +35,9 @@ hipError_t launch_chord_exact_finish(const ChordView& V, const DelayConsts& DC, 
 hipError_t launch_lookup_finish(const ChordView& V, bool chord, bool ideal, int ns, ovs_route_out* io,
                                 uint32_t* sibs, uint64_t n, hipStream_t s);
 hipError_t launch_fill_rpcs_from_hops(const ovs_route_out* out, uint64_t n, uint32_t* rpcs, hipStream_t s);
+// per-block min / max of the coordinates (x0, x1, y0, y1 per block into out[4 * blocks], blocks <= 256):
+// the bounding box that bounds every coordinate delay (extendedFingerTable's acceptance, ovs_kbr.cpp)
+hipError_t launch_xy_bbox(const double2* xy, uint64_t n, double* out, int* blocks, hipStream_t s);
 hipError_t launch_delay(const double2* xy, const DelayConsts& DC, const uint32_t* a, const uint32_t* b,
                         const int32_t* bytes, uint64_t n, int64_t* out, hipStream_t s);
 

@@ -56,6 +56,8 @@ struct ovs_ctx {
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     std::vector<uint64_t> h_bounds;         // ... as last uploaded (uploaded again only on a change)
     std::map<hipStream_t, StageBuf> stage;  // shard-step stage records per stream (cohorts)
+    bool bbox_ok = false;                   // the coordinates' bounding box (x0, x1, y0, y1), computed
+    double bbox[4] = {0, 0, 0, 0};          // on first use (extendedFingerTable's acceptance rule)
     // kademlia
     KadTables kad{};
     // koorde (on the sorted ring in recs / xy)
@@ -118,6 +120,7 @@ void free_tables(ovs_ctx* c)
     if (c->kvis) hipFree(c->kvis);
     c->kvis = nullptr; c->kvis_cap = 0;
     c->overlay = 0; c->n = 0; c->nfing = 0;
+    c->bbox_ok = false;
     c->ch.clear();
     c->kh.clear();
 }
@@ -202,6 +205,10 @@ ovs_status check_common(ovs_ctx* c, const ovs_params& P)
         (P.recNumRedundantNodes > 16 || P.lookupRedundantNodes > 16 || !(P.rpcKeyTimeout >= 0)))
         return fail(c, OVS_ENOTSUP, "recursive Kademlia implements recNumRedundantNodes, lookupRedundantNodes <= 16 "
                                     "and rpcKeyTimeout >= 0");
+    if (P.extendedFingerTable && P.overlay != OVS_OVERLAY_CHORD)
+        return fail(c, OVS_ENOTSUP, "extendedFingerTable is implemented for Chord");
+    if (P.extendedFingerTable && (P.numFingerCandidates < 1 || P.numFingerCandidates > 64))
+        return fail(c, OVS_EINVAL, "numFingerCandidates must be 1..64");
     if (P.lookupParallelPaths != 1) return fail(c, OVS_ENOTSUP, "lookupParallelPaths != 1 not supported");
     if (P.lookupVerifySiblings || P.lookupMajoritySiblings)
         return fail(c, OVS_ENOTSUP, "lookupVerifySiblings/lookupMajoritySiblings not supported");
@@ -214,10 +221,65 @@ ovs_status check_common(ovs_ctx* c, const ovs_params& P)
     return OVS_OK;
 }
 
+// coordDelay of the farthest pair the bounding box admits (host copy of engine.hpp coord_ns: the
+// same IEEE operations; every step is monotone in |dx|, |dy|, so no pair of nodes exceeds it)
+int64_t coord_ns_host(double dx, double dy, int round)
+{
+    const double s2 = dx * dx + dy * dy;
+    const float f = (float)std::sqrt(s2);
+    return simtime_host(0.001 * (double)f, round);
+}
+
+// extendedFingerTable (Chord.cc:416-419, 627-641; ChordFingerTable.cc:195-228) changes a lookup only
+// through its start: IterativeLookup::start takes numFingerCandidates nodes from the source's
+// findNode, the first of them the non-extended choice, and with lookupMerge = false the first
+// response replaces them (IterativeLookup.cc:840-846) while every later FindNodeCall asks for one
+// node -- so routes differ only when a first FindNodeCall times out (the reference then tries the
+// next candidate).  Accepted when no call can: the largest RTT the coordinates' bounding box admits
+// (call + the largest response + twice the farthest coordinate delay) is below rpcUdpTimeout
+// (the oracle restates the candidates, tests/test_oracle_extended.py).
+ovs_status check_extended_fingers(ovs_ctx* c, const ovs_params& P)
+{
+    if (!c->ideal)
+        return fail(c, OVS_ENOTSUP, "extendedFingerTable: explicit tables carry no finger candidate lists");
+    if (P.routingType != 0) return OVS_OK;     // recursive routes: route messages, no RPC timeouts
+    if (!c->bbox_ok) {
+        if (!c->xy || c->n == 0) return fail(c, OVS_ESTATE, "no network loaded");
+        double* d = nullptr;
+        HIPCHK(c, hipMalloc(&d, sizeof(double) * 4 * 256));
+        int blocks = 0;
+        double h[4 * 256];
+        hipError_t e = launch_xy_bbox(c->xy, c->n, d, &blocks, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(double) * 4 * blocks, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        hipFree(d);
+        if (e != hipSuccess) return hip_fail(c, e, "coordinate bounding box");
+        c->bbox[0] = h[0]; c->bbox[1] = h[1]; c->bbox[2] = h[2]; c->bbox[3] = h[3];
+        for (int b = 1; b < blocks; ++b) {
+            c->bbox[0] = std::min(c->bbox[0], h[4 * b]); c->bbox[1] = std::max(c->bbox[1], h[4 * b + 1]);
+            c->bbox[2] = std::min(c->bbox[2], h[4 * b + 2]); c->bbox[3] = std::max(c->bbox[3], h[4 * b + 3]);
+        }
+        c->bbox_ok = true;
+    }
+    const DelayConsts DC = delay_consts(P);
+    const int64_t cd = coord_ns_host(c->bbox[1] - c->bbox[0], c->bbox[3] - c->bbox[2], P.simtimeRound);
+    const int64_t resp = 2 * simtime_host((double)((int64_t)(DC.respBase + DC.respPerNode * (1 + P.successorListSize)) * 8) /
+                                              P.datarate, P.simtimeRound) + DC.access2;
+    const int64_t rtt = DC.msgCall + std::max(resp, DC.msgResp1) + 2 * cd;
+    if (rtt >= DC.rpcTimeout)
+        return fail(c, OVS_ENOTSUP,
+                    "extendedFingerTable: a FindNodeCall could time out (largest RTT " + std::to_string(rtt) +
+                        " ns >= rpcUdpTimeout), where the extended table's next start candidate would be tried");
+    return OVS_OK;
+}
+
 ovs_status check_chord_route(ovs_ctx* c, const ovs_params& P)
 {
     if (P.lookupMerge) return fail(c, OVS_EINVAL, "Chord doesn't work with iterativeLookupConfig.merge = true!");
-    if (P.extendedFingerTable) return fail(c, OVS_ENOTSUP, "extendedFingerTable = true not supported");
+    if (P.extendedFingerTable) {
+        const ovs_status st = check_extended_fingers(c, P);
+        if (st != OVS_OK) return st;
+    }
     if (P.routingType != 0) {
         // recursive: the route message follows findNode's first acceptable candidate hop by hop
         if (P.numSiblings != 1) return fail(c, OVS_ENOTSUP, "recursive Chord routing implements numSiblings=1");
@@ -613,6 +675,8 @@ ovs_status ovs_chord_fix_fingers(ovs_ctx* c, const uint32_t* nodes, uint64_t m, 
     if (c->ideal)
         return fail(c, OVS_ESTATE, "fixfingers rounds run on explicit tables (ovs_chord_load_tables); "
                                    "a converged ring is already their fixed point");
+    if (c->P.extendedFingerTable)
+        return fail(c, OVS_ENOTSUP, "extendedFingerTable: maintenance rounds keep one node per finger");
     const uint64_t n = c->n;
     for (uint64_t j = 0; j < m; ++j)
         if (nodes[j] >= n) return fail(c, OVS_EINVAL, "node index out of range");
@@ -664,6 +728,8 @@ ovs_status ovs_chord_stabilize(ovs_ctx* c, const uint32_t* nodes, uint64_t m, ov
     if (!c || (m && !nodes)) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_CHORD) return fail(c, OVS_ESTATE, "no Chord network loaded");
     if (c->ideal) return fail(c, OVS_ESTATE, "stabilize rounds run on explicit tables (ovs_chord_load_tables)");
+    if (c->P.extendedFingerTable)
+        return fail(c, OVS_ENOTSUP, "extendedFingerTable: maintenance rounds keep one node per finger");
     const uint64_t n = c->n;
     const int sls = c->sls;
     for (uint64_t j = 0; j < m; ++j)
@@ -1828,6 +1894,9 @@ ovs_status ovs_find_node_batch(ovs_ctx* c, const uint32_t* node, const ovs_key16
     if (numSiblings > (c->overlay == OVS_OVERLAY_CHORD ? c->P.successorListSize : c->P.s))
         return fail(c, OVS_EINVAL, "numSiblings too big!");
     if (numRedundantNodes < 1 || numRedundantNodes > 64) return fail(c, OVS_EINVAL, "numRedundantNodes out of range");
+    if (c->overlay == OVS_OVERLAY_CHORD && c->P.extendedFingerTable && numRedundantNodes > 1)
+        return fail(c, OVS_ENOTSUP, "extendedFingerTable: findNode answers of more than one node (finger candidate "
+                                    "lists) are not implemented");
     if (numSiblings < 0 && (numSiblings != -1 || c->overlay != OVS_OVERLAY_KADEMLIA))
         return fail(c, OVS_ENOTSUP, "numSiblings -1 (an exhaustive-iterative call) is implemented for Kademlia");
     HIPCHK(c, hipSetDevice(c->device));

@@ -316,3 +316,59 @@ def test_stabilize_fixfingers_rounds_converge(engine: KbrEngine):
     assert np.array_equal(pred, (np.arange(n) - 1) % n)
     assert np.array_equal(succ, (np.arange(n)[:, None] + 1 + np.arange(8)[None, :]) % n)
     assert np.array_equal(engine.chord_fingers(), OracleNet("chord", net.ids, net.xy).chord_fingers())
+
+
+# ------------------------------------------------------------ extendedFingerTable (Chord.cc:416-419, 627-641)
+
+@pytest.mark.parametrize("nfc,rt", [(3, 0), (1, 0), (8, 0), (3, 1)])
+def test_extended_finger_table_matches_oracle(engine: KbrEngine, nfc, rt):
+    """With no FindNodeCall able to time out (150 x 150 coordinate field: RTT <= ~0.43 s against
+    rpcUdpTimeout 1.5 s), the engine routes with extendedFingerTable = true and equals the oracle,
+    which restates the finger candidate lists (tests/test_oracle_extended.py)."""
+    net = W.population(1 << 14, 41)
+    p = Params.chord().replace(extendedFingerTable=1, numFingerCandidates=nfc, routingType=rt)
+    engine.set_params(p)
+    engine.chord_load(net.ids, net.xy)
+    o = OracleNet("chord", net.ids, net.xy, chord_params(extendedFingerTable=1, numFingerCandidates=nfc, routingType=rt))
+    k1, s1 = W.lookups(net.ids, 3000, 42, node_ids=True)
+    k2, s2 = W.lookups(net.ids, 3000, 43, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    _eq(engine.lookup(keys, src, record_hops=True), o.route(keys, src, record_hops=True), f"extended nfc={nfc} rt={rt}",
+        hop_cols=50)
+    if rt == 0:
+        g, r = engine.lookupCall(keys, src), o.lookup_call(keys, src)
+        for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+            assert np.array_equal(np.asarray(g[f]).astype(np.int64), np.asarray(r[f]).astype(np.int64)), f
+
+
+def test_extended_finger_table_refusals(engine: KbrEngine):
+    """Refused where the extended table would route differently or answer lists the engine does not
+    build: a FindNodeCall that could time out (the next start candidate would be tried), findNode
+    answers of more than one node, explicit tables."""
+    from oversim_amd import KbrError
+    net = W.population(2000, 44)
+    k, s = W.lookups(net.ids, 500, 45, node_ids=False)
+    engine.set_params(Params.chord().replace(extendedFingerTable=1, rpcUdpTimeout=0.25))
+    engine.chord_load(net.ids, net.xy)
+    with pytest.raises(KbrError, match="time out"):
+        engine.lookup(k, s)
+    # recursive routes carry no RPC timeout: accepted, equal to the oracle
+    engine.set_params(Params.chord().replace(extendedFingerTable=1, rpcUdpTimeout=0.25, routingType=1))
+    o = OracleNet("chord", net.ids, net.xy, chord_params(extendedFingerTable=1, rpcUdpTimeout=0.25, routingType=1))
+    _eq(engine.lookup(k, s, record_hops=True), o.route(k, s, record_hops=True), "extended recursive", hop_cols=50)
+    engine.set_params(Params.chord().replace(extendedFingerTable=1))
+    nodes, cnt, sib = engine.findNode(s[:10], k[:10], 1, 1)          # one node: the non-extended finger
+    o1 = OracleNet("chord", net.ids, net.xy, chord_params(extendedFingerTable=1))
+    for i in range(10):
+        assert list(nodes[i, :cnt[i]]) == o1.find_node(int(s[i]), k[i], 1, 1)[0]
+    with pytest.raises(KbrError, match="extendedFingerTable"):
+        engine.findNode(s[:10], k[:10], 3, 1)
+    fingers = OracleNet("chord", net.ids, net.xy).chord_fingers()
+    n = len(net.ids)
+    engine.set_params(Params.chord())
+    engine.chord_load_tables(net.ids, net.xy, ((np.arange(n) - 1) % n).astype(np.uint32),
+                             ((np.arange(n)[:, None] + 1 + np.arange(8)[None, :]) % n).astype(np.uint32),
+                             np.full(n, 8, np.uint8), fingers, np.full(n, 160, np.uint8))
+    engine.set_params(Params.chord().replace(extendedFingerTable=1))
+    with pytest.raises(KbrError, match="explicit tables"):
+        engine.lookup(k, s)
