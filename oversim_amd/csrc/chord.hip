@@ -576,6 +576,12 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
             cursor += (uint64_t)__popcll(need);
         }
         if (!__any(active)) break;
+#ifdef OVS_CHORD_STATS
+        {   // [6] wave iterations, [7] lanes that consume a line in them (diagnostic build)
+            const uint64_t w = __ballot(active && !fresh);
+            if (lane == 0) { atomicAdd(&g_k1_stats[6], 1ull); atomicAdd(&g_k1_stats[7], (unsigned long long)__popcll(w)); }
+        }
+#endif
 
         if (active && !fresh) {
             bool arrived = false, asib = false, fin = false;
@@ -1071,8 +1077,9 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
 #ifdef OVS_CHORD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_k1_stats), sizeof z, 0, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
-    fprintf(stderr, "k1stats n=%llu fetch=%llu start=%llu node=%llu probe1=%llu reprobe=%llu win=%llu\n",
-            (unsigned long long)io.n, z[0], z[1], z[2], z[3], z[4], z[5]);
+    fprintf(stderr, "k1stats n=%llu fetch=%llu start=%llu node=%llu probe1=%llu reprobe=%llu win=%llu "
+            "wave_iters=%llu busy_lanes=%llu\n",
+            (unsigned long long)io.n, z[0], z[1], z[2], z[3], z[4], z[5], z[6], z[7]);
 #endif
     return hipGetLastError();
 }
