@@ -169,16 +169,17 @@ def _single_gpu_reference(net, keys, src, routing_type=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,rt", [(2, 0), (3, 0), (8, 0), (3, 1), (8, 1)])
-def test_shard_step_emulated_on_one_gpu(world, rt):
-    """rt = routingType: 0 iterative, 1 semi-recursive (ChordLarge)."""
+@pytest.mark.parametrize("world,rt,ext", [(2, 0, 0), (3, 0, 0), (8, 0, 0), (3, 1, 0), (8, 1, 0), (3, 0, 1)])
+def test_shard_step_emulated_on_one_gpu(world, rt, ext):
+    """rt = routingType: 0 iterative, 1 semi-recursive (ChordLarge).  ext: the arcs route with
+    extendedFingerTable = true (no call can time out on this field: equal to the plain table)."""
     from oversim_amd import Params
     from oversim_amd.shard import GpuShardStepper, arc_bounds, done_to_numpy, route_local_shards
     n, m = 1 << 16, 6000
     net = W.population(n, 93)
     bounds = arc_bounds(n, world)
     dev = torch.device("cuda", 0)
-    params = Params.chord().replace(routingType=rt)
+    params = Params.chord().replace(routingType=rt, extendedFingerTable=ext)
     steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, params=params)
                 for r in range(world)]
     ks, ss, qb, allk, alls = [], [], [], [], []
