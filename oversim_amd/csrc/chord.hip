@@ -538,6 +538,26 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
     __shared__ uint4 xbuf[4][256];    // per wave: the 64 gathered lines, 4 chunks each
     uint4* const xb = xbuf[threadIdx.x >> 6];
 
+    // Lookups started from their key and source (the single-GPU route): the sources of the wave's
+    // next 64 candidates are preloaded one per lane, so a refilled lane has its source at once and
+    // requests its source's NodeRec in the refill iteration itself (its key is loaded there too,
+    // used from the next iteration on) -- one iteration per lookup fewer than requesting the line
+    // in a PH_FETCH iteration after the refill.
+#ifdef OVS_K1_NO_PRELOAD
+    constexpr bool pre_ok = false;    // A/B build: the PH_FETCH iteration for every lookup
+#else
+    // (the shard step keeps the PH_FETCH iteration: its staging leaves no register for the
+    // preloaded source at 5 waves/SIMD -- 20 B of spills)
+    constexpr bool pre_ok = !SHARD;
+#endif
+    const K160* const pkeys = SHARD ? io.fkeys : io.qkeys;
+    const uint32_t* const psrc = SHARD ? io.fsrc : io.qsrc;
+    uint32_t pS = 0;
+    auto preload = [&](uint64_t from) {
+        if (pre_ok && from + (uint64_t)lane < end) pS = psrc[from + lane];
+    };
+    preload(cursor);
+
     while (true) {
         // ---- gathered lines to their lanes: chunk (lane & 3) of the line of lane 16k + (lane >> 2)
         // was fetched into Lk; LDS slot 4 * owner + chunk = 64 k + lane.  The reads below take
@@ -551,7 +571,30 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
         // ---- refill: lanes without a lookup take the next of the wave's slice
         bool fresh = false;
         const uint64_t need = __ballot(!active);
-        if (need != 0 && cursor < end) {
+        if (need != 0 && cursor < end && pre_ok) {
+            const int rank = __popcll(need & lt_mask);
+            const uint64_t mine = cursor + (uint64_t)rank;
+            const uint32_t s0 = __shfl(pS, rank);
+            if (!active && mine < end) {
+                q = mine;
+                active = true;
+                fresh = true;
+                K = pkeys[q];
+                S = s0;
+                if (SHARD) qid = io.fqid + (uint32_t)q;
+                if (S < V.n) {
+                    // what PH_FETCH does for a lookup at its source, and the source's line requested now
+                    cur = S; t = 0; hops = 0; local = true;
+                    lp = reinterpret_cast<const uint4*>(V.nodes + cur);
+                    ph = PH_START;
+                } else {
+                    ph = PH_FETCH;        // a source outside the ring: PH_FETCH reports it
+                    lp = nullptr;
+                }
+            }
+            cursor += (uint64_t)__popcll(need);
+            preload(cursor);
+        } else if (need != 0 && cursor < end) {
             const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
             if (!active && mine < end) {
                 q = mine;
@@ -644,7 +687,9 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                     // isSiblingFor(cur, K, 1): K in (pred, cur]  <=>  D == 0 or D > pred - cur (Chord.cc:452-457)
                     const K160 D = k_sub(K, A.k);
                     asib = k_zero(D) || cmp_gap(V, D, u64(L3.z, L3.w), A.k, cur == 0 ? V.n - 1 : cur - 1) > 0;
-                    if (!SHARD && !REC) { sx = A.x; sy = A.y; }
+                    // the source's own line (a lookup that left its source never comes back to START
+                    // in one launch; a shard record's START is its responder's: coordinates from FETCH)
+                    if (!REC && (!SHARD || local)) { sx = A.x; sy = A.y; }
                     arrived = true;
                 } else if (ph == PH_NODE) {
                     A.row = L1.y;
