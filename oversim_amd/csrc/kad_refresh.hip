@@ -610,10 +610,10 @@ struct XCtx {
 
 template <bool EX, bool REG, int XA>
 __device__ __forceinline__ void kx_init_lookup(XLookup<XA>& L, const KadView& V, const XCfg& C, const K160* __restrict__ qkeys,
-                                               const uint32_t* __restrict__ qsrc, uint32_t* __restrict__ sib_out, uint64_t q)
+                                               uint32_t S, uint32_t* __restrict__ sib_out, uint64_t q)
 {
     L.K = qkeys[q];
-    L.S = qsrc[q];
+    L.S = S;
     const double2 sxy = V.xy[L.S];
     L.sx = sxy.x; L.sy = sxy.y;
     L.now = 0; L.txf = 0; L.seq = 0; L.nsent = 0;
@@ -722,18 +722,31 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     uint64_t q = 0;
     XLookup<XA> L;
     typename XCtx<EX, REG, XA, TR>::Run R;
+    // the sources of the wave's next 64 lookups, preloaded one per lane: a refilled lane's first
+    // loads (its coordinates, its own KadNode and rows for the start's findNode) wait for nothing
+    // loaded in the same iteration
+#ifdef OVS_KX_NO_PRELOAD
+    constexpr bool pre_ok = false;    // A/B build
+#else
+    constexpr bool pre_ok = true;
+#endif
+    uint32_t pS = 0;
+    if (pre_ok && cursor + (uint64_t)wl < end) pS = qsrc[cursor + wl];
     while (true) {
         const uint64_t need = __ballot(!active);
         if (need != 0 && cursor < end) {
-            const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
+            const int rank = __popcll(need & lt_mask);
+            const uint64_t mine = cursor + (uint64_t)rank;
+            const uint32_t ps = pre_ok ? (uint32_t)__shfl((int)pS, rank) : 0u;
             if (!active && mine < end) {
                 q = mine;
                 active = true;
-                kx_init_lookup<EX, REG>(L, V, C, qkeys, qsrc, sib_out, q);
+                kx_init_lookup<EX, REG>(L, V, C, qkeys, pre_ok ? ps : qsrc[q], sib_out, q);
                 const XCtx<EX, REG, XA, TR> c0{V, DC, C, X, lane, nullptr, nullptr, nullptr};
                 c0.init(L, R);
             }
             cursor += (uint64_t)__popcll(need);
+            if (pre_ok && cursor + (uint64_t)wl < end) pS = qsrc[cursor + wl];
         }
         if (!__any(active)) break;
         if (!active) continue;
