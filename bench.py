@@ -370,10 +370,11 @@ def main():
                 keys, src = dkeys[:1 << 20].cpu().numpy().view(np.uint32), dsrc[:1 << 20].cpu().numpy().view(np.uint32)
             cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type,
                                refresh_R=8 if refresh else 0)
+        xname = "RCCL" if backend == "nccl" else f"{backend} (rehearsal)"
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
                "hopCountMax": 50,
-               "parallelism": ((f"ring sharded over {world} GPUs (RCCL all-to-allv per hop round)" if kind == "chord"
-                                else f"ID arcs over {world} GPUs, FindNodeCall request/response all-to-allv per round")
+               "parallelism": ((f"ring sharded over {world} GPUs ({xname} all-to-allv per hop round)" if kind == "chord"
+                                else f"ID arcs over {world} GPUs, FindNodeCall request/response {xname} all-to-allv per round")
                                if sharded else ("replicas" if world > 1 else "1 GPU")),
                "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1),
                "seed": hex(I["seed"])}
