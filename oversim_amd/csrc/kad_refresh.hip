@@ -889,7 +889,11 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
 #undef KOCC
         bpc[dev][ki] = (oe == hipSuccess && b > 0) ? b : 1;
     }
-    uint64_t lanes = (uint64_t)num_cu * (uint64_t)bpc[dev][ki] * 256;
+#ifndef OVS_KX_OVERSUB
+#define OVS_KX_OVERSUB 1
+#endif
+    // OVS_KX_OVERSUB > 1 (A/B builds): that many lanes per resident slot, each wave a shorter slice
+    uint64_t lanes = (uint64_t)num_cu * (uint64_t)bpc[dev][ki] * 256 * OVS_KX_OVERSUB;
     if (lanes > nq) lanes = nq;
     lanes = (lanes + 255) / 256 * 256;
     const uint64_t nhE = reg ? 0 : 2ull * R, resE = reg ? 0 : (uint64_t)(R > t.k ? R : t.k);

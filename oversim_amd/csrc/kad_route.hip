@@ -385,7 +385,11 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
             b = 1;
         return b;
     }();
-    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4;
+#ifndef OVS_KAD_OVERSUB
+#define OVS_KAD_OVERSUB 1
+#endif
+    // OVS_KAD_OVERSUB > 1 (A/B builds): that many waves per resident slot, each with a shorter slice
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4 * (SHARD ? 1 : OVS_KAD_OVERSUB);
     io.chunk = (io.nq + waves - 1) / waves;
     if (io.chunk < 1) io.chunk = 1;
     const uint64_t need_waves = (io.nq + io.chunk - 1) / io.chunk;
