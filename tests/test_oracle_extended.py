@@ -26,14 +26,17 @@ def _route(net, p, k, s, lazy=False):
     return O.OracleNet("chord", net.ids, net.xy, p, lazy=lazy).route(k, s, record_hops=True)
 
 
-@pytest.mark.parametrize("n,seed,node_ids", [(17, 1, True), (300, 2, False), (2500, 3, True)])
-def test_extended_equals_plain_without_timeouts(n, seed, node_ids):
-    """rpcUdpTimeout 1.5 s against at most ~0.4 s of RTT on the 150 x 150 field: no call times out."""
+@pytest.mark.parametrize("n,seed,node_ids,sls", [(2, 4, True, 8), (3, 5, False, 8), (5, 6, True, 2), (17, 1, True, 8),
+                                                 (300, 2, False, 8), (300, 7, True, 3), (2500, 3, True, 8)])
+def test_extended_equals_plain_without_timeouts(n, seed, node_ids, sls):
+    """rpcUdpTimeout 1.5 s against at most ~0.4 s of RTT on the 150 x 150 field: no call times out.
+    Tiny rings (a finger's candidate list stops at the asking node) and numFingerCandidates above the
+    successor list size (the FixfingersResponse carries min(sls, nfc) successors) included."""
     net = W.population(n, seed)
     k, s = W.lookups(net.ids, 1500, seed + 7, node_ids=node_ids)
-    a = _route(net, O.chord_params(), k, s)
-    for nfc in (1, 3, 8):
-        b = _route(net, O.chord_params(extendedFingerTable=1, numFingerCandidates=nfc), k, s)
+    a = _route(net, O.chord_params(successorListSize=sls), k, s)
+    for nfc in (1, 3, 8, 12):
+        b = _route(net, O.chord_params(successorListSize=sls, extendedFingerTable=1, numFingerCandidates=nfc), k, s)
         for f in FIELDS:
             assert np.array_equal(a[f], b[f]), (n, nfc, f)
         assert np.array_equal(a["hop_seq"], b["hop_seq"]), (n, nfc)
@@ -88,3 +91,82 @@ def test_extended_refused_on_explicit_tables():
     O.OracleNet("chord", net.ids, net.xy, tables=tables)         # accepted without the extended table
     with pytest.raises(RuntimeError, match="extendedFingerTable"):
         O.OracleNet("chord", net.ids, net.xy, O.chord_params(extendedFingerTable=1), tables=tables)
+
+
+# ---- a second reading of the extended findNode, straight from the reference's code paths ----------
+M160 = 1 << 160
+
+
+def _between(x, a, b, lo_closed, hi_closed):
+    """OverlayKey::isBetween / R / L / LR (OverlayKey.cc:587-644), literally."""
+    if not lo_closed and not hi_closed:
+        if x == a:
+            return False
+        return a < x < b if a < b else (x > a or x < b)
+    if a == b and x == a:
+        return True
+    lo = (lambda: x >= a) if lo_closed else (lambda: x > a)
+    hi = (lambda: x <= b) if hi_closed else (lambda: x < b)
+    return (lo() and hi()) if a <= b else (lo() or hi())
+
+
+def _find_node_ext(ids, node, key, nfc, sls):
+    """Chord::findNode(key, nfc, 1) with extendedFingerTable on the stable ring (Chord.cc:548-599,
+    600-674; ChordFingerTable.cc:195-228; the finger entries as handleRpcFixfingersResponse stores
+    them, 1268-1287)."""
+    n = len(ids)
+    ns = min(sls, n - 1)
+    me = ids[node]
+    succ = [(node + 1 + j) % n for j in range(ns)]
+    pred = ids[(node - 1) % n]
+    if _between(key, pred, me, False, True):                  # isSiblingFor(thisNode, key, 1)
+        return [node]
+    if _between(key, me, ids[succ[0]], False, True):           # key in (me, succ0]
+        return succ[:nfc]
+    temp = None
+    for s in reversed(succ):                                   # closestPreceedingNode 604-611
+        if _between(ids[s], me, key, False, True):
+            temp = s
+            break
+    d0 = (ids[succ[0]] - me) % M160
+    for i in range(159, -1, -1):
+        trivial = (1 << i) <= d0
+        if trivial:
+            f = succ[0]
+        else:
+            lk = (me + (1 << i)) % M160
+            f = next((j for j in range(n) if ids[j] >= lk), 0)   # responsible(me + 2^i)
+        if _between(ids[f], ids[temp], key, True, True):
+            if trivial:
+                return [succ[0]]
+            out = []
+            for j in range(-1, min(min(sls, n - 1), nfc)):
+                c = f if j < 0 else (f + 1 + j) % n
+                if c == node:
+                    break
+                if not _between(key, ids[f], ids[c], True, True):
+                    out.append(c)
+            return (out or [f])[:nfc]
+    out = []
+    for s in reversed(succ):
+        if len(out) > nfc:
+            break
+        if _between(ids[s], me, key, False, False):
+            out.append(s)
+    return out[:nfc]
+
+
+@pytest.mark.parametrize("n,seed,sls", [(3, 11, 8), (40, 12, 4), (500, 13, 8)])
+def test_extended_find_node_matches_second_reading(n, seed, sls):
+    from oversim_amd.kbr import key_to_int
+    net = W.population(n, seed)
+    ids = [key_to_int(net.ids[i]) for i in range(n)]
+    rng = np.random.default_rng(seed)
+    for nfc in (1, 3, 6):
+        o = O.OracleNet("chord", net.ids, net.xy, O.chord_params(successorListSize=sls, extendedFingerTable=1,
+                                                                numFingerCandidates=nfc))
+        keys, _ = W.lookups(net.ids, 120, seed + nfc, node_ids=False)
+        nodes = rng.integers(0, n, len(keys))
+        for i in range(len(keys)):
+            got, _ = o.find_node(int(nodes[i]), keys[i], nfc, 1)
+            assert got == _find_node_ext(ids, int(nodes[i]), key_to_int(keys[i]), nfc, sls), (n, nfc, i)
