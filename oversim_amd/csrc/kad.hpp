@@ -172,9 +172,12 @@ struct KadExhTrace {
 hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
                           int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
                           uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace = nullptr, bool pad = true);
+                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace = nullptr, bool pad = true,
+                          bool internal_resp = false);
 // pad = false: the responder / RTT rows are left unwritten past a lookup's responders (the caller
 // filled them, or reads only the lookup's hops entries -- the internal visited lists)
+// internal_resp: nobody reads the responder rows (they are the lookups' visited sets): the first
+// KXVL responders of a lookup stay in LDS (kad_refresh.hip)
 // free the exhaustive-lookup scratch K2x keeps for `device` between calls (ovs_ctx_destroy)
 void kad_exhaustive_release(int device);
 // bucket-refresh keys of nodes[0..m) (device buffers); *total = how many (up to cap written)

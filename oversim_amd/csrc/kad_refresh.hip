@@ -33,11 +33,16 @@ namespace {
 // pending-call slots (strictParallelRpcs: <= alpha calls in flight): 4, or 8 for lookupParallelRpcs
 // 5..8 (maidsafe.ini:18-19) -- a template parameter XA of the lookup state and the kernel
 constexpr int XMAXDEAD = 64;    // nodes whose RPC timed out, per lookup
+// responders of a lookup kept in the lane's LDS column when the caller asked for none (the visited
+// set, read only after a timeout): scattered 4 B stores to HBM had been ~0.8 GB of partial-sector
+// writes per launch on workload R; responders past KXVL go to the HBM row
+constexpr int KXVL = 32;
 
 struct XCfg {
     int R, ns, alpha, hcm, k;      // ns: the siblings vector's size (numSiblings <= R)
     int oneway;                    // 1: a KBRTestApp one-way lookup (route message to the result)
     int pad;                       // 1: responder / RTT rows padded to hopCountMax (NONE / -1)
+    int lvis;                      // 1: nobody reads the responder rows -- the first KXVL stay in LDS
     int64_t bwFull, bwOne;         // T(L*8/datarate) of a FindNodeResponse with R nodes / one node
     int strict, visitOnlyOnce, newOnResp, newOnTimeout, finishOnFirst;
 };
@@ -102,6 +107,7 @@ struct XCtx {
     uint32_t* __restrict__ resp;      // responders of this lookup (hop order), hcm entries
     int64_t* __restrict__ rtt;        // their RTTs (may be null)
     uint32_t* __restrict__ sib;       // ns siblings of this lookup
+    uint32_t (*vis)[256] = nullptr;   // C.lvis: the lane's LDS column of its first KXVL responders
     int64_t* __restrict__ tarr = nullptr;    // TR: response arrivals (hop order)
     uint32_t* __restrict__ cn = nullptr;     // TR: calls sent: destination ...
     int64_t* __restrict__ ct = nullptr;      // ... and its arrival there
@@ -336,8 +342,9 @@ struct XCtx {
     {
         if (x == L.S) return true;
         if (!L.any_to) return false;
+        const int t = (int)(threadIdx.x);
         for (int i = 0; i < L.nhop; ++i)
-            if (resp[i] == x) return true;
+            if ((C.lvis && i < KXVL ? vis[i][t] : resp[i]) == x) return true;
         return false;
     }
 
@@ -545,7 +552,8 @@ struct XCtx {
                 else {
                     if (cur.node != L.S) {
                         if (L.nhop < C.hcm) {
-                            resp[L.nhop] = cur.node;
+                            if (C.lvis && L.nhop < KXVL) vis[L.nhop][threadIdx.x] = cur.node;
+                            else resp[L.nhop] = cur.node;
                             if (rtt) rtt[L.nhop] = L.now - cur.tsend;
                             if constexpr (TR) tarr[L.nhop] = L.now;
                         }
@@ -722,6 +730,7 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     uint64_t q = 0;
     XLookup<XA> L;
     typename XCtx<EX, REG, XA, TR>::Run R;
+    __shared__ uint32_t kxvis[KXVL][256];
     // the sources of the wave's next 64 lookups, preloaded one per lane: a refilled lane's first
     // loads (its coordinates, its own KadNode and rows for the start's findNode) wait for nothing
     // loaded in the same iteration
@@ -754,6 +763,7 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
         uint32_t* resp = resp_out + q * (uint64_t)C.hcm;
         int64_t* rtt = rtt_out ? rtt_out + q * (uint64_t)C.hcm : nullptr;
         XCtx<EX, REG, XA, TR> ctx{V, DC, C, X, lane, resp, rtt, sib};
+        ctx.vis = kxvis;
         if constexpr (TR) {
             ctx.tarr = T.tarr + q * (uint64_t)C.hcm;
             ctx.cn = T.cnode + q * (uint64_t)T.ccap;
@@ -842,7 +852,7 @@ size_t g_scratch_cap[64] = {};
 hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
                           int R, int ns, bool oneway, const K160* qkeys, const uint32_t* qsrc, uint64_t nq, void* out,
                           uint32_t* sibs, uint32_t* responders, int64_t* rtts, uint32_t* rpcs, int num_cu,
-                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace, bool pad)
+                          hipStream_t st, bool* capacity_error, const KadExhTrace* trace, bool pad, bool internal_resp)
 {
     *capacity_error = false;
     if (nq == 0) return hipSuccess;
@@ -855,6 +865,11 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     C.R = R; C.ns = ns; C.alpha = A; C.hcm = P.hopCountMax; C.k = t.k;
     C.oneway = oneway ? 1 : 0;
     C.pad = pad ? 1 : 0;
+#ifdef OVS_KX_NO_LVIS
+    C.lvis = 0;                       // A/B build: every responder to the HBM row
+#else
+    C.lvis = internal_resp && !trace ? 1 : 0;
+#endif
     C.strict = P.lookupStrictParallelRpcs; C.visitOnlyOnce = P.lookupVisitOnlyOnce;
     C.newOnResp = P.lookupNewRpcOnEveryResponse; C.newOnTimeout = P.lookupNewRpcOnEveryTimeout;
     C.finishOnFirst = P.lookupFinishOnFirstUnchanged;

@@ -1619,7 +1619,8 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
     bool cap_err = false;
     const hipError_t e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), R, R, false, dk, ds, n, dout,
                                         dsib, dresp, drtt, drpc, c->num_cu, s, &cap_err, nullptr,
-                                        responders != nullptr /* else the internal visited lists: no padding */);
+                                        responders != nullptr /* else the internal visited lists: no padding */,
+                                        responders == nullptr /* ... and their first entries in LDS */);
     if (e != hipSuccess) { cleanup(); return hip_fail(c, e, "refresh lookup kernel"); }
     if (cap_err) { cleanup(); return fail(c, OVS_ENOTSUP, "a refresh lookup exceeded the kernel's capacity (64 timed-out nodes)"); }
     if (!dev) {
