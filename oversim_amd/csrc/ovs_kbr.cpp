@@ -64,7 +64,7 @@ struct ovs_ctx {
     KoordeTables koorde{};
     // epichord routing snapshot (ovs_epichord_load)
     EpiTables epi{};
-    uint32_t* kvis = nullptr;            // K3's per-lookup responder lists when no hop_seq is asked for
+    uint32_t* kvis = nullptr;            // internal visited lists (K3 without hop_seq, K2x without responders)
     uint64_t kvis_cap = 0;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
@@ -1596,8 +1596,11 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
     if (st != OVS_OK) return st;
     st = to_device(c, src, n, dev, &ds, &ok_s);
     if (st != OVS_OK) { if (ok_k) hipFree(dk); return st; }
-    // the responder list is the lookup's visited set: always present on the device
-    const bool own_resp = !dev || !responders, own_rtt = !dev && rtt_ns, own_rpc = !dev && rpcs;
+    // the responder list is the lookup's visited set: always present on the device -- when the
+    // caller asked for none, in the context's cached buffer (as K3's; a per-call hipMalloc / hipFree
+    // of n * hopCountMax entries had put an allocation and a device synchronisation into every call)
+    const bool internal_resp = !responders;
+    const bool own_resp = !dev && responders, own_rtt = !dev && rtt_ns, own_rpc = !dev && rpcs;
     auto cleanup = [&]() {
         if (ok_k) hipFree(dk);
         if (ok_s) hipFree(ds);
@@ -1610,8 +1613,18 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
         HIPCHK(c, hipMalloc(&dout, sizeof(ovs_lookup_out) * n));
         HIPCHK(c, hipMalloc(&dsib, sizeof(uint32_t) * n * R));
     } else { dout = out; dsib = siblings; }
-    if (own_resp) HIPCHK(c, hipMalloc(&dresp, sizeof(uint32_t) * n * H));
-    else dresp = responders;
+    if (internal_resp) {
+        if (c->kvis_cap < n * H) {
+            if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
+            HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * H));
+            c->kvis_cap = n * H;
+        }
+        dresp = c->kvis;
+    } else if (own_resp) {
+        HIPCHK(c, hipMalloc(&dresp, sizeof(uint32_t) * n * H));
+    } else {
+        dresp = responders;
+    }
     if (own_rtt) HIPCHK(c, hipMalloc(&drtt, sizeof(int64_t) * n * H));
     else drtt = rtt_ns;
     if (own_rpc) HIPCHK(c, hipMalloc(&drpc, sizeof(uint32_t) * n));
