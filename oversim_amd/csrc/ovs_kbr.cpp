@@ -1371,8 +1371,21 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         }
         dhop = c->kvis;
     } else if (need_hop) {
-        if (dev && hop_seq) dhop = hop_seq;
-        else { HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H)); own_hop = true; }
+        if (dev && hop_seq) {
+            dhop = hop_seq;
+        } else if (!hop_seq) {
+            // an internal hop list (explicit Chord tables, exhaustive Kademlia: the visited sets) in the
+            // context's cached buffer, not a per-call allocation
+            if (c->kvis_cap < n * (uint64_t)H) {
+                if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
+                HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * (uint64_t)H));
+                c->kvis_cap = n * (uint64_t)H;
+            }
+            dhop = c->kvis;
+        } else {
+            HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H));
+            own_hop = true;
+        }
         HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
     }
     bool own_rpc = false;
@@ -1402,7 +1415,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         bool cap_err = false;
         // dhop was filled with NONE above: the kernel leaves the rows unpadded
         e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), c->P.lookupRedundantNodes, 1, true,
-                           dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err, nullptr, false);
+                           dk, ds, n, dout, dres, dhop, nullptr, drpc, c->num_cu, s, &cap_err, nullptr, false,
+                           hop_seq == nullptr /* nobody reads the visited sets: their first entries in LDS */);
         hipFree(dres);
         if (e == hipSuccess && cap_err) return fail(c, OVS_ENOTSUP, "a lookup exceeded the kernel's capacity (64 timed-out nodes)");
     } else if (c->P.routingType == 1 || c->P.routingType == 2) {
@@ -1514,7 +1528,13 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     const int H = chord_exact ? P.hopCountMax + 1 : P.hopCountMax > 0 ? P.hopCountMax : 1;
     const bool need_hop = (chord && !c->ideal) || kad_exh || chord_exact;   // visited check (explicit tables; exhaustive lookups)
     if (need_hop) {
-        HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H));
+        // internal (a LookupCall records no hop sequence): the context's cached buffer
+        if (c->kvis_cap < n * (uint64_t)H) {
+            if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
+            HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * (uint64_t)H));
+            c->kvis_cap = n * (uint64_t)H;
+        }
+        dhop = c->kvis;
         HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
     }
     hipError_t e;
@@ -1533,7 +1553,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         // lookupRpc with EXHAUSTIVE_ITERATIVE_ROUTING: redundantNodes = lookupRedundantNodes, numSiblings = ns
         bool cap_err = false;
         e = kad_exhaustive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P), P.lookupRedundantNodes, ns, false, dk, ds,
-                           n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err, nullptr, false);
+                           n, dout, dsib, dhop, nullptr, nullptr, c->num_cu, s, &cap_err, nullptr, false,
+                           true /* a LookupCall records no hop sequence: the visited sets' first entries in LDS */);
         if (e == hipSuccess && cap_err) e = hipErrorNotSupported;
     } else if (kad_rec) {
         // RecursiveLookup (RecursiveLookup.cc:52-139): a routed FindNodeCall, the response back by UDP
@@ -1549,7 +1570,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     if (e == hipSuccess && !kad_exh) e = launch_lookup_finish(chord_view(c), chord, c->ideal, nslots, dout, dsib, n, s);
     if (e != hipSuccess) {
         if (!dev) { hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib); }
-        if (dhop) hipFree(dhop);
+        /* dhop: the context's cached buffer */
         return hip_fail(c, e, "lookup kernel");
     }
     if (!dev) {
@@ -1560,7 +1581,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     } else if (dhop) {
         HIPCHK(c, hipStreamSynchronize(s));
     }
-    if (dhop) hipFree(dhop);
+    /* dhop: the context's cached buffer */
     return OVS_OK;
 }
 
