@@ -42,15 +42,22 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+# the 16 B per-lookup result records (include/ovs_kbr.h ovs_route_out / ovs_lookup_out)
+ROUTE_DTYPE = np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                        ("one_way_hops", "u1"), ("latency_ns", "<i8")])
+LOOKUP_DTYPE = np.dtype([("num_siblings", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                         ("is_valid", "u1"), ("latency_ns", "<i8")])
+
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 # measured ceiling of dependent random 64 B line gathers from an HBM-resident table (cooperative
 # 16 B-per-lane loads, tools/ubench/gather.hip, profiles/r01_j_coop/ubench.txt): 3.9e10-4.7e10 lines/s
 GATHER_CEILING_GBS = 2950.0
+GATHER_CEILING_LINES = 4.6e10
 # Algorithmic bytes.  Chord, converged-ring layout of this build: every hop reads
 # the responder's 64 B header line (the finger entry that selected it, or its NodeRec), every
 # lookup additionally its source's NodeRec (64 B) and its key/source/result (24 B in, 16 B out).
 # SURVEY.md §8(d) priced 512 B/hop for a 24 B-record layout with separate window, finger and
-# coordinate gathers; that figure is reported beside ("survey_bytes_per_hop"), not used.
+# coordinate gathers; that figure is reported beside ("survey_model", with the fraction it would imply), not used.
 B_HOP, B_LOOKUP = 64, 104
 B_HOP_SURVEY = 512
 # Kademlia, this build's layout: every FindNodeCall reads its target's 64 B KadNode line when it is
@@ -58,13 +65,24 @@ B_HOP_SURVEY = 512
 # processed; every lookup additionally its source's KadNode + block (the local findNode at start)
 # and its key/source/result (24 B in, 16 B out).  Blocks findNode reads beyond the main bucket
 # (short buckets, the sibling zone) are extra, not counted.  SURVEY.md §8(d) priced 448 B/RPC for
-# a 24 B-entry layout; reported beside ("survey_bytes_per_rpc").
+# a 24 B-entry layout; reported beside ("survey_model").
 B_RPC, B_KLOOKUP = 160, 200
 B_RPC_SURVEY = 448
 # Koorde: a hop reads the responder's ring records (predecessor, itself, first successor: 3 x 24 B),
 # its 16 B KoordeNode and its 16 B coordinates; a lookup its key/source (24 B), the source's
 # coordinates (16 B) and writes 16 B.  The successor / de Bruijn list searches are extra.
 B_KHOP, B_KLOOKUP_K = 104, 56
+
+
+def survey_model(kind, hops, rpcs, lookups, kern_ms) -> dict:
+    """SURVEY.md §8(d) priced the path for a 24 B-record layout with separate window / finger /
+    coordinate gathers (512 B/hop, 448 B/RPC).  This layout moves a fraction of that,
+    so the survey model's implied fraction is printed for reference only: above 1 it is physically
+    impossible and shows the model is superseded, not that the kernel beats HBM."""
+    b = B_HOP_SURVEY * hops if kind == "chord" else B_RPC_SURVEY * (rpcs or 0)
+    f = b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    return {"bytes_per_unit": B_HOP_SURVEY if kind == "chord" else B_RPC_SURVEY, "implied_frac": f,
+            "note": "SURVEY §8(d) layout model, superseded by this build's layout (DESIGN.md §5); not the roofline"}
 
 
 def parse():
@@ -109,7 +127,7 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
     def run(m, threads):
         if refresh_R:
             return o.exhaustive(keys[:m], src[:m], refresh_R, record=False, nthreads=threads)
-        return o.route(keys[:m], src[:m], record_hops=False, nthreads=threads)
+        return o.route(keys[:m], src[:m], record_hops=False, count_rpcs=kind == "kademlia", nthreads=threads)
 
     def timed(threads: int, budget_s: float):
         # calibrate on growing prefixes until one takes a quarter of the budget (a short probe
@@ -126,15 +144,42 @@ def cpu_baseline(kind, ids, xy, keys, src, target_s: float, alpha: int = 1, rout
         t = time.perf_counter()
         r = run(m2, threads)
         dt = time.perf_counter() - t
-        return int(r["hops"].astype(np.int64).sum()) / dt, m2 / dt, m2, dt
+        return int(r["hops"].astype(np.int64).sum()) / dt, m2 / dt, m2, dt, r
 
-    hps, lps, m_all, dt_all = timed(nthreads, target_s)
-    hps1, lps1, m_one, dt_one = timed(1, target_s / 2)
+    hps, lps, m_all, dt_all, res = timed(nthreads, target_s)
+    hps1, lps1, m_one, dt_one, _ = timed(1, target_s / 2)
     return {"value": hps, "unit": "hops/s", "cores": nthreads, "kind": "port",
             "sample": f"oracle/ovs_oracle.c restatement (gcc -O3, OpenMP), {m_all} of the step's lookups on the same "
                       f"{len(ids)}-node {kind} network{' (lazy tables)' if lazy else ''}: {nthreads} threads "
                       f"{dt_all:.1f} s; 1 thread {m_one} lookups {dt_one:.1f} s",
-            "lookups_per_s": lps, "host_cpus": nproc, "value_1core": hps1, "lookups_per_s_1core": lps1}
+            "lookups_per_s": lps, "host_cpus": nproc, "value_1core": hps1, "lookups_per_s_1core": lps1}, res
+
+
+# output fields the parity check compares, per result kind (the oracle's record dtypes, tests/oracle_lib.py):
+# one-way route -> ovs_route_out (IterativeLookup getResult()[0] / getMinHops(), BaseOverlay.cc:1241-1307 +
+# the route message's latency); refresh lookups -> ovs_lookup_out + the R-node result + FindNodeCall counts
+ROUTE_FIELDS = ("responsible", "hops", "status", "one_way_hops", "latency_ns")
+LOOKUP_FIELDS = ("num_siblings", "hops", "status", "is_valid", "latency_ns")
+
+
+def parity_check(gpu: dict, orc: dict, m: int, fields) -> dict:
+    """Field-by-field comparison of the step's GPU results with the CPU oracle's on the first m lookups of
+    the same batch (the lookups cpu_baseline() ran).  Every field must be equal (bit-exact contract,
+    latency in int64 ns)."""
+    bad = np.zeros(m, dtype=bool)
+    per = {}
+    for f in fields:
+        a, b = np.asarray(gpu[f])[:m], np.asarray(orc[f])[:m]
+        d = a != b
+        if d.ndim > 1:
+            d = d.reshape(m, -1).any(axis=1)
+        per[f] = int(d.sum())
+        bad |= d
+    out = {"checked": int(m), "mismatches": int(bad.sum()), "fields": list(fields),
+           "per_field": per, "reference": "oracle/ovs_oracle.c (CPU restatement, the cpu_baseline run's own results)"}
+    if bad.any():
+        out["first_mismatch"] = int(np.argmax(bad))
+    return out
 
 
 def traffic_from_json(path: str | None, workload: str, kname: str):
@@ -322,17 +367,26 @@ def main():
 
     # ---- work of one step (identical every step: same inputs)
     rpc_total = None
+    gres = None          # the last step's per-lookup results, in batch order (for the parity check)
     if sharded:
         hop_total, n_ok = sh.hop_total(), sh.ok_total()
         kern_ms = sh.kernel_ms / max(sh.runs, 1)
         if kind == "kademlia":
             rpc_total = sh.rpc_total()     # FindNodeCalls of this rank's lookups (done records)
+        if world == 1:
+            gres = sh.results_by_qid()
     else:
         outs = dout.cpu().numpy().reshape(-1, 16)
         hop_total = int(outs[:, 4:6].copy().view(np.uint16).astype(np.int64).sum())
         n_ok = int((outs[:, 6] == 0).sum())
+        rec = outs.reshape(-1).view(LOOKUP_DTYPE if refresh else ROUTE_DTYPE)
+        gres = {f: rec[f] for f in rec.dtype.names}
         if drpc is not None:
-            rpc_total = int(drpc.cpu().numpy().astype(np.int64).sum())
+            rpcs_np = drpc.cpu().numpy().view(np.uint32)
+            rpc_total = int(rpcs_np.astype(np.int64).sum())
+            gres["rpcs"] = rpcs_np
+        if refresh:
+            gres["siblings"] = dsib.cpu().numpy().view(np.uint32)
         kern_ms = step_ms
 
     t = torch.tensor([wall, float(hop_total), float(n_ok), float(rpc_total or 0)], dtype=torch.float64, device=dev)
@@ -364,12 +418,23 @@ def main():
         if a.traffic_csv:
             traffic, traffic_src = traffic_from_csv(a.traffic_csv, kname), a.traffic_csv
         cpu = None
+        parity = None
         if world == 1 and not a.no_cpu_baseline:
             if ids is None:       # device-generated population (D, E): the oracle needs host copies
                 ids, xy = ids_t.cpu().numpy().view(np.uint32), xy_t.cpu().numpy()
                 keys, src = dkeys[:1 << 20].cpu().numpy().view(np.uint32), dsrc[:1 << 20].cpu().numpy().view(np.uint32)
-            cpu = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type,
-                               refresh_R=8 if refresh else 0)
+            cpu, orc = cpu_baseline(kind, ids, xy, keys, src, a.cpu_seconds, wl.get("alpha", 1), routing_type,
+                                    refresh_R=8 if refresh else 0)
+            if gres is not None:
+                # the bench checks its own output: the oracle results the baseline just computed against
+                # the GPU's on the same lookups, field by field
+                mchk = len(orc["hops"])
+                if refresh:
+                    fields = LOOKUP_FIELDS + ("siblings", "rpcs")
+                else:
+                    fields = ROUTE_FIELDS + (("rpcs",) if kind == "kademlia" and "rpcs" in gres else ())
+                parity = parity_check(gres, orc, mchk, fields)
+                parity["of_batch"] = int(m)
         xname = "RCCL" if backend == "nccl" else f"{backend} (rehearsal)"
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
                "hopCountMax": 50,
@@ -389,7 +454,11 @@ def main():
         else:
             cfg.update({"successorListSize": 8, "routingType": a.routing})
         if sharded:
-            cfg.update({"hop_rounds": sh.rounds})
+            cfg.update({"hop_rounds": sh.rounds,
+                        "round_loop": "C++ (ovs_shard_route_batch)" if getattr(sh, "native", False) else "python",
+                        "shard_stats_rank0": getattr(sh, "stats", None)})
+            if kind == "chord":
+                cfg["replicated_top_levels"] = sh.stepper.top_levels
         line = {
             "metric": "routed lookup hops/sec (whole node)",
             "value": value,
@@ -412,12 +481,19 @@ def main():
                 "kernel": kname, "kernel_ms": kern_ms,
                 "algorithmic_bytes": bper, "unit_of_work": "RPC" if kind == "kademlia" else "hop",
                 "traffic_source": traffic_src,
+                # the PMC bytes per launch over this run's kernel time: what HBM actually delivered
+                "frac_counter": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                # 64 B lines per second the kernel fetched, beside the measured ceiling of dependent
+                # random 64 B gathers (tools/ubench/gather.hip: 4.6e10-4.8e10 lines/s)
+                "lines_per_s": (traffic / 64.0 / (kern_ms * 1e-3)) if traffic else None,
+                "gather_ceiling_lines_per_s": GATHER_CEILING_LINES,
                 "gather_ceiling_GBs": GATHER_CEILING_GBS,
                 "frac_of_gather_ceiling": achieved / GATHER_CEILING_GBS,
-                **({"survey_bytes_per_hop": B_HOP_SURVEY} if kind == "chord" else
-                   {"survey_bytes_per_rpc": B_RPC_SURVEY} if kind == "kademlia" else {}),
+                **({"survey_model": survey_model(kind, hop_total, rpc_total, lookups_launch, kern_ms)}
+                   if kind in ("chord", "kademlia") else {}),
             },
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         if json_fd is not None:
             os.write(json_fd, (json.dumps(line) + "\n").encode())

@@ -32,6 +32,12 @@
  * context's device and the call is asynchronous on `stream` (NULL = the HIP
  * default stream, as everywhere in HIP).  Host-pointer calls are synchronous
  * and run on the context's own stream.
+ * Context scratch: internal visited / hop lists (explicit-table Chord,
+ * exhaustive Kademlia, Koorde without hop_seq, refresh batches without
+ * responders) live in one buffer the context caches.  Every call that uses it
+ * makes its stream wait for the previous user's launch (an event), so
+ * device-pointer calls on different streams stay correct and asynchronous;
+ * they serialise on the device through that buffer.
  */
 #ifndef OVS_KBR_H
 #define OVS_KBR_H
@@ -42,7 +48,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 10
+#define OVS_ABI_VERSION 11
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -517,7 +523,9 @@ typedef struct ovs_lookup_rec {     /* 48 B in-flight lookup */
     uint32_t qid;                   /* caller's lookup id */
     int64_t  t_ns;                  /* simulated time since lookup start */
     uint16_t hops;
-    uint8_t  local;                 /* 1: the source's local step (no hop, no delay) is pending */
+    uint8_t  local;                 /* 1: the source's local step (no hop, no delay) is pending;
+                                       2: `cur` was reached (its response accounted) on another rank,
+                                          only its findNode decision is pending (replicated levels) */
     uint8_t  pad[5];
 } ovs_lookup_rec;
 
@@ -530,6 +538,16 @@ typedef struct ovs_done_rec {       /* 24 B finished lookup */
 /* Load arc [lo, hi) of a Chord ring of n_total nodes (ids/xy of the whole ring). */
 ovs_status  ovs_chord_load_shard(ovs_ctx* ctx, const ovs_key160* ids_all_sorted, uint64_t n_total,
                                  const double* xy_all, uint64_t lo, uint64_t hi, uint32_t flags);
+/* Replicate the top `top_levels` finger levels (fingers 159 .. 160 - top_levels) of EVERY node of
+ * the ring on this arc's context (ABI 11; 64 B per node and level: 2^26 nodes x 4 levels = 17 GB).
+ * A lookup's first hops are its long jumps, and they are the ones whose responders lie on other
+ * arcs: a responder off this arc whose next finger probe falls in the replicated levels is decided
+ * here, from the same finger the owner's row holds (Chord.cc:602-674, ChordFingerTable.cc:174-193),
+ * so the lookup crosses to another arc about once instead of once per long hop.  A decision that
+ * needs the owner's rows after all (a finger below the replicated levels, the successor window) is
+ * handed to the owner as a record with local = 2.  0 = none (the default). */
+ovs_status  ovs_chord_shard_replicate(ovs_ctx* ctx, int32_t top_levels);
+int32_t     ovs_chord_shard_levels(const ovs_ctx* ctx);
 /* Initial records for lookups whose sources lie on this arc: qid = qid_base + i. */
 ovs_status  ovs_shard_make_records(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
                                    uint64_t n, uint32_t qid_base, ovs_lookup_rec* recs, void* stream);
@@ -655,6 +673,84 @@ ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const void* in, uint64_t n, void
  * and lookups whose source lies off this arc (they never run).  Synchronises the
  * device.  The caller fails the batch when it is non-zero. */
 ovs_status  ovs_kad_shard_errors(ovs_ctx* ctx, uint64_t* bad);
+
+/* ---------------------------------------------------------------------------
+ * Sharded routing behind the ABI (ABI 11): the whole multi-GPU batch in one call.
+ *
+ * Replaces BaseOverlay::sendToKey's iterative branch (src/common/BaseOverlay.cc:1367-1442) for a
+ * network whose tables are split over the ranks (one context per GPU, one process or thread per
+ * rank).  The round loop -- step kernels, the per-round count all-gather, the all-to-allv of the
+ * records, the completeness check -- runs in C++ inside the library; every rank calls the entry
+ * point collectively with the same exchange.  The exchange is a table of callbacks:
+ * ovs_exchange_rccl_create fills it with RCCL over xGMI (ncclSend / ncclRecv groups, one
+ * communicator, collectives serialised on one communicator stream); ovs_exchange_local_create with
+ * W ranks that are threads of one process (contexts on one or more devices, device-to-device
+ * copies); a caller may plug its own (tests: gloo through Python callbacks).  All callbacks are
+ * collective and are called in the same order on every rank; they return 0 on success. */
+typedef struct ovs_exchange {
+    void* user;
+    uint32_t rank, world;
+    /* every rank contributes n host int64 (host_send); on return host_recv[world * n] (rank-major)
+     * holds all contributions -- the round's count matrix, the loop's one host synchronisation */
+    int (*allgather_i64)(void* user, const int64_t* host_send, uint32_t n, int64_t* host_recv);
+    /* all-to-allv of row_bytes-sized rows in DEVICE memory: the rows for rank d are send[d]
+     * (send_rows[d] of them); the rows from rank s land at recv + recv_off[s] * row_bytes
+     * (recv_rows[s] of them).  Ordered after the work queued on `stream`; work queued on `stream`
+     * afterwards sees the received rows (the callback may return before the transfer ends) */
+    int (*alltoallv)(void* user, const void* const* send, const uint64_t* send_rows, void* recv,
+                     const uint64_t* recv_off, const uint64_t* recv_rows, uint32_t row_bytes, void* stream);
+    /* element-wise sum over the ranks of n host int64, in place */
+    int (*allreduce_sum_i64)(void* user, int64_t* values, uint32_t n);
+    /* releases `user` (ovs_exchange_destroy); may be NULL */
+    void (*destroy)(void* user);
+} ovs_exchange;
+
+/* RCCL exchange for rank `rank` of `world` on HIP device `device`.  unique_id: the 128 bytes
+ * ovs_rccl_unique_id produced on rank 0 and the caller distributed (as ncclGetUniqueId's).  RCCL is
+ * loaded at run time (the process's librccl.so.1 when one is loaded, else /opt/rocm's). */
+ovs_status  ovs_rccl_unique_id(void* unique_id_128);
+ovs_status  ovs_exchange_rccl_create(int device, uint32_t rank, uint32_t world, const void* unique_id_128,
+                                     ovs_exchange* out);
+/* W in-process ranks (threads): fills out[0..world), one exchange per rank */
+ovs_status  ovs_exchange_local_create(uint32_t world, ovs_exchange* out);
+void        ovs_exchange_destroy(ovs_exchange* ex);
+/* The last RCCL / exchange error text of this thread (ovs_exchange_* calls have no context) */
+const char* ovs_exchange_last_error(void);
+
+typedef struct ovs_shard_route_stats {
+    uint32_t rounds;         /* hop rounds (Chord) / request rounds (Kademlia) of the batch */
+    uint32_t cohorts;
+    uint64_t sent;           /* records this rank sent to other ranks (hand-offs / FindNodeCalls) */
+    uint64_t sent_bytes;     /* ... and their bytes, responses included (Kademlia) */
+    uint64_t done;           /* lookups that finished on this rank */
+    double   step_ms;        /* step kernels incl. compaction (HIP events), summed over rounds */
+    double   exchange_ms;    /* host wall time inside the exchange callbacks */
+    double   total_ms;       /* host wall time of the call */
+} ovs_shard_route_stats;
+
+/* Route one batch of Chord lookups whose sources lie on this context's arc (ovs_chord_load_shard;
+ * lookup i has qid qid_base + i).  shard_lo: HOST array of world + 1 arc bounds (every rank's).
+ * num_siblings 0: one-way KBR routes; otherwise LookupCalls with that many siblings (-1 =
+ * successorListSize; finish them with ovs_shard_lookup_finish).  keys / src / done are DEVICE
+ * buffers; a lookup finishes on whichever rank holds it last, so done_cap must hold every record
+ * that can finish here (the total over all ranks is always enough); *n_done = records in done.
+ * cohorts (1..4, 0 = 2): the batch is split so one cohort's exchange overlaps another's kernel.
+ * The call returns when the batch is complete on every rank: it fails (OVS_EDEVICE) when the
+ * records finished on all ranks do not add up to the lookups started, or when a finished record came
+ * from an exchange row nobody wrote (receive buffers are 0xFF-filled).  stats may be NULL. */
+ovs_status  ovs_shard_route_batch(ovs_ctx* ctx, const ovs_exchange* ex, const uint64_t* shard_lo,
+                                  int32_t num_siblings, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                                  uint32_t qid_base, ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done,
+                                  uint32_t cohorts, ovs_shard_route_stats* stats, void* stream);
+/* The same for Kademlia (ovs_kad_load_shard; the lookups stay on this rank, FindNodeCalls and their
+ * responses are exchanged): num_siblings < -1 ... -2: one-way KBR routes; -1 / 0..8: LookupCalls
+ * (as ovs_kad_shard_begin_lookup; siblings = n rows of max(num_siblings, 1), device memory).
+ * done receives exactly this rank's n lookups (done_cap >= n); done[i].pad = its FindNodeCalls. */
+ovs_status  ovs_kad_shard_route_batch(ovs_ctx* ctx, const ovs_exchange* ex, const uint64_t* shard_lo,
+                                      int32_t num_siblings, const ovs_key160* keys, const uint32_t* src, uint64_t n,
+                                      uint32_t qid_base, ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done,
+                                      uint32_t* siblings, ovs_shard_route_stats* stats, void* stream);
+#define OVS_KAD_ONEWAY (-2)
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,7 @@ CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
     "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value", "-Wno-bitwise-instead-of-logical",
 ]
-SOURCES = ["chord.hip", "compact.hip", "epichord.hip", "kad.hip", "kad_general.hip", "kad_refresh.hip", "kad_route.hip", "kad_shard.hip", "koorde.hip", "stats.hip", "ovs_kbr.cpp",
+SOURCES = ["chord.hip", "compact.hip", "epichord.hip", "kad.hip", "kad_general.hip", "kad_refresh.hip", "kad_route.hip", "kad_shard.hip", "koorde.hip", "stats.hip", "ovs_kbr.cpp", "shard_route.cpp",
            "ovs_ini.cpp", "host_tables.cpp"]
 # translation units compiled more than once: (source, object stem, extra flags).  K2 is built per
 # (alpha, exact) pair so its instantiations compile in parallel; A = 8 serves alpha 5..8 (A is the
@@ -136,6 +136,19 @@ def build_c_consumer(verbose: bool = False) -> Path:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         _write_stamp(exe, d)
+    # the sharded route from C: W ranks as pthreads over the library's in-process exchange (device
+    # buffers through the HIP runtime API, which is C)
+    src2, exe2 = C_CONSUMER / "sharded_route.c", C_CONSUMER / "sharded_route"
+    cmd2 = ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I", str(ROOT / "include"),
+            "-I", "/opt/rocm/include", str(src2), "-L", str(LIB.parent), "-lovs_kbr", "-L", "/opt/rocm/lib", "-lamdhip64",
+            "-lpthread", "-Wl,-rpath,$ORIGIN/../../oversim_amd", "-Wl,-rpath,/opt/rocm/lib",
+            "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe2)]
+    d2 = _digest([src2, ROOT / "include" / "ovs_kbr.h"], " ".join(cmd2))
+    if not _stamp_ok(exe2, d2):
+        if verbose:
+            print(" ".join(cmd2), flush=True)
+        subprocess.run(cmd2, check=True)
+        _write_stamp(exe2, d2)
     return exe
 
 

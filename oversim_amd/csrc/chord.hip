@@ -81,6 +81,20 @@ __global__ void k_chord_fill(const KeyRec* __restrict__ recs, uint32_t n, uint32
         row[KEYBITS - 1 - i].idx = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
 }
 
+// replicated top levels of a sharded ring: finger i = responsible(v + 2^i) of EVERY node v for the
+// top L levels (i = 159 .. 160 - L), ftop[v * L + (159 - i)]; k_chord_entries completes the entries
+// from the fingers' NodeRecs.  A trivial position (2^i <= succ0 - v, tiny rings) resolves to succ0,
+// which is what the lower bound gives there, and is never probed (pi >= ilo is checked first)
+__global__ void k_chord_top(const KeyRec* __restrict__ recs, uint32_t n, int L, FingerEnt* __restrict__ ftop)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n * (uint32_t)L) return;
+    const uint32_t v = (uint32_t)(t / (uint32_t)L);
+    const int i = KEYBITS - 1 - (int)(t % (uint32_t)L);
+    const K160 self = key_of(load_rec(recs, v));
+    ftop[t].idx = ring_lower_bound(recs, n, k_add(self, k_pow2(i)));
+}
+
 // NodeRec of every node (ideal ring): key, finger-row offset, coordinates, window distances
 __global__ void k_chord_nodes(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t n, int ns,
                               NodeRec* __restrict__ nodes)
@@ -532,6 +546,12 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
     const uint4* lp = nullptr;        // the line requested for the next iteration
     uint4 L0 = make_uint4(0, 0, 0, 0), L1 = L0, L2 = L0, L3 = L0;
     int hand = -1;                    // shard: this lane's lookup moves to arc `hand` this iteration
+    // shard with replicated top finger levels (V.ftl > 0): `remote` -- the current responder lies off
+    // this arc and is being decided from the replicated levels; `redo` -- the record arrived as a
+    // responder already reached whose decision needs its owner's rows (record local byte 2);
+    // `hl` -- the local byte of the record this lane hands off
+    bool remote = false, redo = false;
+    uint32_t hl = 0;
     bool done_now = false;            // shard: this lane's lookup finished this iteration ...
     ovs_route_out done_o{};           // ... with this result
 
@@ -601,6 +621,7 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                 active = true;
                 fresh = true;
                 ph = PH_FETCH;
+                remote = false; redo = false;
                 if (SHARD && io.fkeys) {
                     // a batch's first round: no record, the lookup starts from its key and source
                     K = io.fkeys[q];
@@ -626,6 +647,13 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
         }
 #endif
 
+        // finger pi of the current responder: its own row on this arc, or the replicated top levels
+        // of an off-arc responder (pi >= 160 - V.ftl there, checked by the callers)
+        auto fptr = [&](int p) -> const uint4* {
+            if (SHARD && remote)
+                return reinterpret_cast<const uint4*>(V.ftop + (uint64_t)cur * (uint32_t)V.ftl + (uint32_t)(KEYBITS - 1 - p));
+            return reinterpret_cast<const uint4*>(V.frow + (uint64_t)row + (uint32_t)(KEYBITS - 1 - p));
+        };
         if (active && !fresh) {
             bool arrived = false, asib = false, fin = false;
             uint8_t status = OVS_LOOKUP_OK;
@@ -636,6 +664,15 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
             bool nxt_node = false;    // ... whose header must be read from its NodeRec
             bool nxt_sib = false;
             lp = nullptr;
+            // an off-arc responder whose decision needs its owner's rows (a finger below the
+            // replicated levels, or its successor window): the lookup goes to the owner as a
+            // responder already reached (its response accounted here), which decides there
+            auto redo_hand = [&]() {
+                emit = shard_owner(io.shard_lo, io.nsh, cur);
+                hl = 2;
+                active = false;
+                lp = nullptr;
+            };
 
 #ifdef OVS_CHORD_STATS
             {   // line accounting (diagnostic build, tools/diag): which kind of line each lane consumes
@@ -657,7 +694,9 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                         S = L1.y; cur = L1.z; qid = L1.w;
                         t = (int64_t)u64(L2.x, L2.y);
                         hops = (int)(L2.z & 0xFFFF);
-                        local = ((L2.z >> 16) & 0xFF) != 0;
+                        const uint32_t lb = (L2.z >> 16) & 0xFF;
+                        local = lb == 1;
+                        redo = lb == 2;
                     }
                     if (S >= V.n || cur >= V.n) {
                         // a row the exchange never wrote (receive buffers are 0xFF-filled) or a corrupted
@@ -711,7 +750,8 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                         // a finger short of K is not responsible: (pred F, F] lies inside (C, F]
                         nxt = L1.y; nxt_sib = k_eq(A.k, K);
                     } else if (--pi >= ilo) {
-                        lp = reinterpret_cast<const uint4*>(V.frow + (uint64_t)row + (uint32_t)(KEYBITS - 1 - pi));
+                        if (SHARD && remote && pi < KEYBITS - V.ftl) redo_hand();
+                        else lp = fptr(pi);
                     } else {
                         nxt = fb; nxt_node = true;       // Chord.cc:653-658 (succ0 via 183-184 when temp == succ0)
                     }
@@ -773,7 +813,14 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                 }
                 if (SHARD) {
                     const int dest = shard_owner(io.shard_lo, io.nsh, nx);
-                    if (dest != io.me) {
+                    remote = false;
+                    // an off-arc responder reached through a finger entry (its header in A) whose first
+                    // probe lies in the replicated top levels -- or which is the key's node, decided
+                    // without a probe -- is decided here instead of on its owner
+                    if (dest != io.me && V.ftl > 0 && !via_node &&
+                        (nx_sib || k_msb(k_sub(K, A.k)) >= KEYBITS - V.ftl))
+                        remote = true;
+                    else if (dest != io.me) {
                         // hand the lookup to the owner of its next responder
                         if (REC) {
                             const double2 nxy = via_node ? V.xy[nx] : make_double2(A.x, A.y);
@@ -781,6 +828,7 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                         }
                         cur = nx;
                         emit = dest;
+                        hl = 0;
                         active = false;
                         lp = nullptr;
                         return false;
@@ -803,7 +851,13 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
             if (arrived) {
                 uint32_t nx2 = NONE;
                 bool nx2_sib = false;
-                if (REC) {
+                if (SHARD && redo) {
+                    // a responder reached on another rank, which accounted for its response (or route
+                    // message) and handed its decision here (record local byte 2)
+                    redo = false;
+                    local = false;
+                    if (REC) { sx = A.x; sy = A.y; }
+                } else if (REC) {
                     const bool at_src = local;
                     local = false;
                     sx = A.x; sy = A.y;
@@ -846,16 +900,24 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                         const uint32_t sl = ring_next(cur, (uint32_t)ns, V.n);
                         const int c = cmp_gap(V, D, gSL, C, sl);
                         if (c < 0) {
-                            lp = reinterpret_cast<const uint4*>(V.win + (cur - V.lo));   // K inside the window
-                            ph = PH_WIN;
+                            if (SHARD && remote) {
+                                redo_hand();                       // the window exists on the owner only
+                            } else {
+                                lp = reinterpret_cast<const uint4*>(V.win + (cur - V.lo));   // K inside the window
+                                ph = PH_WIN;
+                            }
                         } else {
                             // temp = succ[ns-1]; fingers from msb(D) down
                             gTx = c == 0;
                             fb = gTx ? ring_next(cur, (uint32_t)ns - 1, V.n) : sl;
                             pi = k_msb(D);
                             if (pi >= ilo) {
-                                lp = reinterpret_cast<const uint4*>(V.frow + (uint64_t)row + (uint32_t)(KEYBITS - 1 - pi));
-                                ph = PH_PROBE;
+                                if (SHARD && remote && pi < KEYBITS - V.ftl) {
+                                    redo_hand();
+                                } else {
+                                    lp = fptr(pi);
+                                    ph = PH_PROBE;
+                                }
                             } else {
                                 nx2 = fb;
                             }
@@ -907,7 +969,7 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                 io.stag[q] = (uint8_t)io.nsh;
             }
             if (hand >= 0) {
-                store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, 0);
+                store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, (int)hl);
                 io.stag[q] = (uint8_t)hand;
             }
             done_now = false;
@@ -1078,6 +1140,21 @@ hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n,
     hipLaunchKernelGGL(k_chord_nodes, dim3(nblk(n, 256)), dim3(256), 0, s, recs, xy, n, ns, nodes);
     if (hi > lo) hipLaunchKernelGGL(k_chord_win, dim3(nblk(hi - lo, 256)), dim3(256), 0, s, recs, n, lo, hi - lo, ns, win);
     if (nfing) hipLaunchKernelGGL(k_chord_entries, dim3(nblk(nfing, 256)), dim3(256), 0, s, nodes, fingers, nfing);
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_top(const KeyRec* recs, uint32_t n, int L, FingerEnt* ftop, hipStream_t s)
+{
+    const uint64_t tot = (uint64_t)n * (uint32_t)L;
+    if (tot == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chord_top, dim3(nblk(tot, 256)), dim3(256), 0, s, recs, n, L, ftop);
+    return hipGetLastError();
+}
+
+hipError_t launch_chord_entries(const NodeRec* nodes, FingerEnt* ents, uint64_t total, hipStream_t s)
+{
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chord_entries, dim3(nblk(total, 256)), dim3(256), 0, s, nodes, ents, total);
     return hipGetLastError();
 }
 

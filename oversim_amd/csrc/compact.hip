@@ -173,4 +173,22 @@ hipError_t compact_by_tag(const uint8_t* tags, uint64_t n, const CPlan& P, Compa
     return hipGetLastError();
 }
 
+// finished records whose qid word is 0xFFFFFFFF: rows of an exchange receive buffer nobody wrote
+// (0xFF-filled), which the step kernel finishes as BROKEN instead of routing
+__global__ void k_count_sentinel(const ovs_done_rec* __restrict__ done, uint64_t n, unsigned long long* out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool hit = i < n && done[i].qid == 0xFFFFFFFFu;
+    const uint64_t b = __ballot(hit);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+}
+
+hipError_t count_sentinel_records(const ovs_done_rec* done, uint64_t n, unsigned long long* out, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess || n == 0) return e;
+    hipLaunchKernelGGL(k_count_sentinel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, done, n, out);
+    return hipGetLastError();
+}
+
 }  // namespace ovs

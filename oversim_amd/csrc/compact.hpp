@@ -77,6 +77,9 @@ hipError_t stage_ensure(StageBuf& b, size_t bytes, hipStream_t s);
 
 // tags[i] < the plan's class count selects the class of element i (other values: no output);
 // stream-ordered, no host synchronisation
+// out = the finished records of done[0, n) with qid 0xFFFFFFFF (exchange rows nobody wrote)
+hipError_t count_sentinel_records(const ovs_done_rec* done, uint64_t n, unsigned long long* out, hipStream_t s);
+
 hipError_t compact_by_tag(const uint8_t* tags, uint64_t n, const CPlan& plan, CompactScratch& scr, hipStream_t s);
 
 }  // namespace ovs

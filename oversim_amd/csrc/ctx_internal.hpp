@@ -1,0 +1,24 @@
+// ctx_internal.hpp -- what the host layers outside ovs_kbr.cpp may use of a context (internal).
+//
+// The sharded round loop (shard_route.cpp) drives a context through the public ABI; these give it
+// the context's device, its error slot, cohort streams the context owns (the shard step keeps its
+// stage records per stream, so the streams must live as long as the context) and one cached
+// scratch object the context frees with itself.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/ovs_kbr.h"
+
+namespace ovs {
+
+int ctx_device(const ovs_ctx* c);
+ovs_status ctx_fail(ovs_ctx* c, ovs_status s, const std::string& msg);
+// cohort stream i (0..3) of the context, created non-blocking on first use
+hipStream_t ctx_cohort_stream(ovs_ctx* c, int i);
+// the context's slot for the round loop's cached buffers, released with `release` at destroy
+void* ctx_route_scratch(ovs_ctx* c);
+void ctx_set_route_scratch(ovs_ctx* c, void* p, void (*release)(void*));
+
+}  // namespace ovs

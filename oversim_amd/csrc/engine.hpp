@@ -146,6 +146,11 @@ struct ChordView {
     int32_t ns;        // ideal: min(successorListSize, n-1)
     int32_t sls;       // successor list stride (general)
     int32_t numFingerCandidates;
+    // sharded rings (ovs_chord_shard_replicate): the top `ftl` finger levels of EVERY node,
+    // ftop[v * ftl + (159 - i)] = finger i of v for i >= 160 - ftl, so a lookup's first hops --
+    // the long jumps that cross arcs -- are decided on the rank that holds the lookup
+    const FingerEnt* __restrict__ ftop;
+    int32_t ftl;
 };
 
 constexpr int MAXSHARDS = 64;

@@ -730,7 +730,9 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     uint64_t q = 0;
     XLookup<XA> L;
     typename XCtx<EX, REG, XA, TR>::Run R;
-    __shared__ uint32_t kxvis[KXVL][256];
+    // the LDS visited set (C.lvis) is never used by the trace instantiations (kad_exhaustive sets
+    // lvis only without a trace): they reserve one row instead of 32 KB
+    __shared__ uint32_t kxvis[TR ? 1 : KXVL][256];
     // the sources of the wave's next 64 lookups, preloaded one per lane: a refilled lane's first
     // loads (its coordinates, its own KadNode and rows for the start's findNode) wait for nothing
     // loaded in the same iteration

@@ -18,6 +18,9 @@ hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint3
                                ovs_lookup_rec* out, hipStream_t s);
 hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes,
                               FingerEnt* fingers, uint64_t nfing, WinRec* win, uint32_t lo, uint32_t hi, hipStream_t s);
+// replicated top finger levels of a sharded ring (finger indices; launch_chord_entries completes them)
+hipError_t launch_chord_top(const KeyRec* recs, uint32_t n, int L, FingerEnt* ftop, hipStream_t s);
+hipError_t launch_chord_entries(const NodeRec* nodes, FingerEnt* ents, uint64_t total, hipStream_t s);
 hipError_t launch_chord_export(const KeyRec* recs, const FingerEnt* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s);
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,

@@ -10,12 +10,14 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
 #include <type_traits>
 #include <vector>
 
+#include "ctx_internal.hpp"
 #include "epichord.hpp"
 #include "host_tables.hpp"
 #include "kad.hpp"
@@ -53,6 +55,8 @@ struct ovs_ctx {
     // explicit Kademlia tables: host copy for maintenance rounds (ovs_kad_maintenance_round)
     KadHost kh;
     uint64_t shard_lo = 0, shard_hi = 0;   // finger rows exist for [shard_lo, shard_hi)
+    FingerEnt* ftop = nullptr;              // replicated top finger levels of every node (ovs_chord_shard_replicate)
+    int ftl = 0;
     uint64_t* d_bounds = nullptr;           // device copy of the arc boundaries (MAXSHARDS + 1)
     std::vector<uint64_t> h_bounds;         // ... as last uploaded (uploaded again only on a change)
     std::map<hipStream_t, StageBuf> stage;  // shard-step stage records per stream (cohorts)
@@ -66,6 +70,8 @@ struct ovs_ctx {
     EpiTables epi{};
     uint32_t* kvis = nullptr;            // internal visited lists (K3 without hop_seq, K2x without responders)
     uint64_t kvis_cap = 0;
+    hipEvent_t kvis_ev = nullptr;        // recorded after the last launch that used kvis (kvis_acquire)
+    bool kvis_used = false;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
     uint8_t* kact = nullptr;             // 0 never runs, 1 suspended in kst, 2 not started
@@ -85,7 +91,39 @@ struct ovs_ctx {
     uint32_t* ksib = nullptr;            // ... and the caller's sibling rows
     // scratch for host-pointer calls
     std::vector<void*> scratch;
+    // the sharded round loop (shard_route.cpp): cohort streams and cached buffers
+    hipStream_t cohort[4] = {nullptr, nullptr, nullptr, nullptr};
+    void* route_scratch = nullptr;
+    void (*route_scratch_release)(void*) = nullptr;
 };
+
+namespace ovs {
+
+int ctx_device(const ovs_ctx* c) { return c->device; }
+
+ovs_status ctx_fail(ovs_ctx* c, ovs_status s, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return s;
+}
+
+hipStream_t ctx_cohort_stream(ovs_ctx* c, int i)
+{
+    if (i < 0 || i >= 4) return nullptr;
+    if (!c->cohort[i] && hipStreamCreateWithFlags(&c->cohort[i], hipStreamNonBlocking) != hipSuccess)
+        c->cohort[i] = nullptr;
+    return c->cohort[i];
+}
+
+void* ctx_route_scratch(ovs_ctx* c) { return c->route_scratch; }
+
+void ctx_set_route_scratch(ovs_ctx* c, void* p, void (*release)(void*))
+{
+    c->route_scratch = p;
+    c->route_scratch_release = release;
+}
+
+}  // namespace ovs
 
 namespace {
 
@@ -93,6 +131,12 @@ ovs_status fail(ovs_ctx* c, ovs_status s, const std::string& m)
 {
     if (c) c->err = m;
     return s;
+}
+
+bool fault_injected(const char* what)
+{
+    const char* f = std::getenv("OVS_FAULT_INJECT");
+    return f && std::strcmp(f, what) == 0;
 }
 
 ovs_status hip_fail(ovs_ctx* c, hipError_t e, const char* where)
@@ -108,17 +152,17 @@ ovs_status hip_fail(ovs_ctx* c, hipError_t e, const char* where)
 
 void free_tables(ovs_ctx* c)
 {
-    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres, c->nodes, c->win};
+    void* ptrs[] = {c->recs, c->xy, c->fingers, c->pred, c->succ, c->nsucc, c->fres, c->nodes, c->win, c->ftop};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    c->nodes = nullptr; c->win = nullptr; c->nodes_ns = -1;
+    c->nodes = nullptr; c->win = nullptr; c->nodes_ns = -1; c->ftop = nullptr; c->ftl = 0;
     c->recs = nullptr; c->xy = nullptr; c->fingers = nullptr; c->pred = nullptr;
     c->succ = nullptr; c->nsucc = nullptr; c->fres = nullptr;
     kad_free(c->kad);
     koorde_free(c->koorde);
     epichord_free(c->epi);
-    if (c->kvis) hipFree(c->kvis);
-    c->kvis = nullptr; c->kvis_cap = 0;
+    if (c->kvis) hipFree(c->kvis);      // hipFree waits for the launches that use it
+    c->kvis = nullptr; c->kvis_cap = 0; c->kvis_used = false;
     c->overlay = 0; c->n = 0; c->nfing = 0;
     c->bbox_ok = false;
     c->ch.clear();
@@ -135,6 +179,42 @@ void free_kad_shard(ovs_ctx* c)
     c->kkeys = nullptr; c->ksrc = nullptr;
     c->kiota = nullptr; c->klist[0] = c->klist[1] = nullptr; c->knl = nullptr; c->kcur = 0;
     c->knlook = 0; c->kcap = 0; c->kalpha = 0;
+}
+
+// The context's cached scratch for internal visited / hop lists (kvis) is one buffer shared by every
+// call on the context.  A call on stream s first waits for the last launch that used it (kvis_ev, on
+// whichever stream that was) and records its own use after its launch (kvis_release), so calls on
+// different streams -- device-pointer calls return while their kernels run -- never rewrite each
+// other's rows.  Growing the buffer waits for that last use only, not for the whole device.
+ovs_status kvis_acquire(ovs_ctx* c, uint64_t need, hipStream_t s, uint32_t** out)
+{
+    if (!c->kvis_ev) {
+        const hipError_t e = hipEventCreateWithFlags(&c->kvis_ev, hipEventDisableTiming);
+        if (e != hipSuccess) { c->kvis_ev = nullptr; return fail(c, OVS_EDEVICE, std::string("kvis event: ") + hipGetErrorString(e)); }
+    }
+    if (c->kvis_cap < need) {
+        if (c->kvis) {
+            if (c->kvis_used) {
+                const hipError_t e = hipEventSynchronize(c->kvis_ev);
+                if (e != hipSuccess) return fail(c, OVS_EDEVICE, std::string("kvis wait: ") + hipGetErrorString(e));
+            }
+            hipFree(c->kvis);
+            c->kvis = nullptr; c->kvis_cap = 0; c->kvis_used = false;
+        }
+        const hipError_t e = hipMalloc(&c->kvis, sizeof(uint32_t) * need);
+        if (e != hipSuccess) { c->kvis = nullptr; return fail(c, OVS_ENOMEM, "kvis allocation"); }
+        c->kvis_cap = need;
+    } else if (c->kvis_used) {
+        const hipError_t e = hipStreamWaitEvent(s, c->kvis_ev, 0);
+        if (e != hipSuccess) return fail(c, OVS_EDEVICE, std::string("kvis stream wait: ") + hipGetErrorString(e));
+    }
+    *out = c->kvis;
+    return OVS_OK;
+}
+
+void kvis_release(ovs_ctx* c, hipStream_t s)
+{
+    if (c->kvis_ev && hipEventRecord(c->kvis_ev, s) == hipSuccess) c->kvis_used = true;
 }
 
 void free_scratch(ovs_ctx* c)
@@ -329,6 +409,7 @@ ChordView chord_view(const ovs_ctx* c)
     V.ns = (int)std::min<uint64_t>((uint64_t)c->P.successorListSize, c->n - 1);
     V.sls = c->sls;
     V.numFingerCandidates = c->P.numFingerCandidates;
+    V.ftop = c->ftop; V.ftl = c->ftop ? c->ftl : 0;
     return V;
 }
 
@@ -343,6 +424,8 @@ ovs_status ensure_nodes(ovs_ctx* c, hipStream_t s)
     if (!c->win) HIPCHK(c, hipMalloc(&c->win, sizeof(WinRec) * (c->shard_hi - c->shard_lo)));
     HIPCHK(c, launch_chord_nodes(c->recs, c->xy, (uint32_t)c->n, ns, c->nodes, c->fingers, c->nfing, c->win,
                                  (uint32_t)c->shard_lo, (uint32_t)c->shard_hi, s));
+    // the replicated top levels carry their fingers' window distances too
+    if (c->ftop) HIPCHK(c, launch_chord_entries(c->nodes, c->ftop, c->n * (uint64_t)c->ftl, s));
     // the records are built once and then read by kernels on any stream (e.g. one stream per
     // cohort of ovs_shard_step): complete them before any other call can see nodes_ns set
     HIPCHK(c, hipStreamSynchronize(s));
@@ -422,7 +505,11 @@ void ovs_ctx_destroy(ovs_ctx* c)
     free_scratch(c);
     kad_exhaustive_release(c->device);
     if (c->d_bounds) hipFree(c->d_bounds);
+    if (c->kvis_ev) hipEventDestroy(c->kvis_ev);
+    if (c->route_scratch && c->route_scratch_release) c->route_scratch_release(c->route_scratch);
     for (auto& kv : c->stage) stage_free(kv.second);
+    for (hipStream_t cs : c->cohort)
+        if (cs) hipStreamDestroy(cs);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -492,6 +579,27 @@ ovs_status ovs_chord_load_shard(ovs_ctx* c, const ovs_key160* ids, uint64_t n, c
     c->shard_lo = lo; c->shard_hi = hi;
     return OVS_OK;
 }
+
+ovs_status ovs_chord_shard_replicate(ovs_ctx* c, int32_t top_levels)
+{
+    if (!c) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_CHORD || !c->ideal) return fail(c, OVS_ESTATE, "no Chord ring (shard) loaded");
+    if (top_levels < 0 || top_levels > 32) return fail(c, OVS_EINVAL, "top_levels must be 0..32");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());        // kernels of earlier steps may still read the old levels
+    if (c->ftop) hipFree(c->ftop);
+    c->ftop = nullptr; c->ftl = 0;
+    if (top_levels == 0) return OVS_OK;
+    const uint64_t tot = c->n * (uint64_t)top_levels;
+    HIPCHK(c, hipMalloc(&c->ftop, sizeof(FingerEnt) * tot));
+    c->ftl = top_levels;
+    HIPCHK(c, launch_chord_top(c->recs, (uint32_t)c->n, top_levels, c->ftop, c->stream));
+    if (c->nodes) HIPCHK(c, launch_chord_entries(c->nodes, c->ftop, tot, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return OVS_OK;
+}
+
+int32_t ovs_chord_shard_levels(const ovs_ctx* c) { return c && c->ftop ? c->ftl : 0; }
 
 ovs_status ovs_shard_make_records(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                                   uint32_t qid_base, ovs_lookup_rec* recs, void* stream)
@@ -1054,6 +1162,8 @@ ovs_status ovs_kad_shard_step(ovs_ctx* c, ovs_kad_req* out, uint64_t out_cap, un
     if (!c->kst) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
     if (c->P.lookupParallelRpcs != c->kalpha && c->knlook)
         return fail(c, OVS_ESTATE, "lookupParallelRpcs changed since ovs_kad_shard_begin");
+    if (kad_shard_cap(c->P, c->kad) != c->kfcap && c->knlook)
+        return fail(c, OVS_ESTATE, "lookupRedundantNodes / k changed the findNode capacity since ovs_kad_shard_begin");
     if (out_cap < c->knlook * (uint64_t)kad_pend_slots(c->kalpha))
         return fail(c, OVS_EINVAL, "out_cap must hold a request per pending-call slot "
                                    "(n * lookupParallelRpcs; n * 8 for lookupParallelRpcs 5..8)");
@@ -1093,6 +1203,8 @@ ovs_status ovs_kad_shard_serve(ovs_ctx* c, const ovs_kad_req* in, uint64_t n, vo
 {
     if (!c || (n && (!in || !out))) return OVS_EINVAL;
     if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (c->kst && c->knlook && kad_shard_cap(c->P, c->kad) != c->kfcap)
+        return fail(c, OVS_ESTATE, "lookupRedundantNodes / k changed the findNode capacity since ovs_kad_shard_begin");
     HIPCHK(c, hipSetDevice(c->device));
     hipError_t e = kad_shard_serve(c->kad, (uint32_t)c->n, c->P, in, n, out, c->kbad, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia shard serve");
@@ -1103,6 +1215,9 @@ ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const void* in, uint64_t n, void* s
 {
     if (!c || (n && !in)) return OVS_EINVAL;
     if (!c->kres) return fail(c, OVS_ESTATE, "no lookups started (ovs_kad_shard_begin)");
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    if (c->knlook && kad_shard_cap(c->P, c->kad) != c->kfcap)
+        return fail(c, OVS_ESTATE, "lookupRedundantNodes / k changed the findNode capacity since ovs_kad_shard_begin");
     HIPCHK(c, hipSetDevice(c->device));
     hipError_t e = kad_shard_deliver(c->kfcap, in, n, c->kres, c->knlook * (uint64_t)kad_pend_slots(c->kalpha), c->kbad,
                                      (hipStream_t)stream);
@@ -1364,24 +1479,20 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal) || kad_exh;
     bool own_hop = false;
     if (koorde_scratch) {
-        if (c->kvis_cap < n * (uint64_t)H) {
-            if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
-            HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * (uint64_t)H));
-            c->kvis_cap = n * (uint64_t)H;
+        {
+            const ovs_status ks = kvis_acquire(c, n * (uint64_t)H, s, &dhop);
+            if (ks != OVS_OK) return ks;
         }
-        dhop = c->kvis;
     } else if (need_hop) {
         if (dev && hop_seq) {
             dhop = hop_seq;
         } else if (!hop_seq) {
             // an internal hop list (explicit Chord tables, exhaustive Kademlia: the visited sets) in the
             // context's cached buffer, not a per-call allocation
-            if (c->kvis_cap < n * (uint64_t)H) {
-                if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
-                HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * (uint64_t)H));
-                c->kvis_cap = n * (uint64_t)H;
+            {
+                const ovs_status ks = kvis_acquire(c, n * (uint64_t)H, s, &dhop);
+                if (ks != OVS_OK) return ks;
             }
-            dhop = c->kvis;
         } else {
             HIPCHK(c, hipMalloc(&dhop, sizeof(uint32_t) * n * H));
             own_hop = true;
@@ -1431,6 +1542,7 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
                       c->num_cu, s);
     }
+    if (dhop && dhop == c->kvis) kvis_release(c, s);
     if (e != hipSuccess) return hip_fail(c, e, "route kernel");
     if (!dev) {
         HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(ovs_route_out) * n, hipMemcpyDeviceToHost, s));
@@ -1529,12 +1641,10 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     const bool need_hop = (chord && !c->ideal) || kad_exh || chord_exact;   // visited check (explicit tables; exhaustive lookups)
     if (need_hop) {
         // internal (a LookupCall records no hop sequence): the context's cached buffer
-        if (c->kvis_cap < n * (uint64_t)H) {
-            if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
-            HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * (uint64_t)H));
-            c->kvis_cap = n * (uint64_t)H;
+        {
+            const ovs_status ks = kvis_acquire(c, n * (uint64_t)H, s, &dhop);
+            if (ks != OVS_OK) return ks;
         }
-        dhop = c->kvis;
         HIPCHK(c, hipMemsetAsync(dhop, 0xFF, sizeof(uint32_t) * n * H, s));
     }
     hipError_t e;
@@ -1568,6 +1678,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
                       dsib);
     }
     if (e == hipSuccess && !kad_exh) e = launch_lookup_finish(chord_view(c), chord, c->ideal, nslots, dout, dsib, n, s);
+    if (dhop && dhop == c->kvis) kvis_release(c, s);
     if (e != hipSuccess) {
         if (!dev) { hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib); }
         /* dhop: the context's cached buffer */
@@ -1578,10 +1689,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         HIPCHK(c, hipMemcpyAsync(siblings, dsib, sizeof(uint32_t) * n * nslots, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         hipFree(dk); hipFree(ds); hipFree(dout); hipFree(dsib);
-    } else if (dhop) {
-        HIPCHK(c, hipStreamSynchronize(s));
     }
-    /* dhop: the context's cached buffer */
+    /* dhop: the context's cached buffer, ordered by kvis_ev: a device-pointer call stays asynchronous */
     return OVS_OK;
 }
 
@@ -1635,12 +1744,10 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
         HIPCHK(c, hipMalloc(&dsib, sizeof(uint32_t) * n * R));
     } else { dout = out; dsib = siblings; }
     if (internal_resp) {
-        if (c->kvis_cap < n * H) {
-            if (c->kvis) { HIPCHK(c, hipDeviceSynchronize()); hipFree(c->kvis); c->kvis = nullptr; c->kvis_cap = 0; }
-            HIPCHK(c, hipMalloc(&c->kvis, sizeof(uint32_t) * n * H));
-            c->kvis_cap = n * H;
+        {
+            const ovs_status ks = kvis_acquire(c, n * H, s, &dresp);
+            if (ks != OVS_OK) return ks;
         }
-        dresp = c->kvis;
     } else if (own_resp) {
         HIPCHK(c, hipMalloc(&dresp, sizeof(uint32_t) * n * H));
     } else {
@@ -1655,6 +1762,7 @@ ovs_status ovs_kad_refresh_batch(ovs_ctx* c, const ovs_key160* keys, const uint3
                                         dsib, dresp, drtt, drpc, c->num_cu, s, &cap_err, nullptr,
                                         responders != nullptr /* else the internal visited lists: no padding */,
                                         responders == nullptr /* ... and their first entries in LDS */);
+    if (internal_resp) kvis_release(c, s);
     if (e != hipSuccess) { cleanup(); return hip_fail(c, e, "refresh lookup kernel"); }
     if (cap_err) { cleanup(); return fail(c, OVS_ENOTSUP, "a refresh lookup exceeded the kernel's capacity (64 timed-out nodes)"); }
     if (!dev) {
@@ -1678,8 +1786,10 @@ ovs_status kad_upload_host_tables(ovs_ctx* c)
     const uint64_t n = c->n, S5 = 5ull * (uint64_t)c->P.s, k = (uint64_t)c->P.k;
     std::vector<uint32_t> hs(n * S5), hn(n * 160 * k);
     std::vector<uint8_t> hc(n * 160);
-    if (!c->kh.export_k(hs.data(), hc.data(), hn.data()))
+    if (!c->kh.export_k(hs.data(), hc.data(), hn.data())) {
+        free_tables(c);    // the host copy was changed by the round: the device tables no longer match it
         return fail(c, OVS_ENOTSUP, "a bucket outgrew k (bucketType kademlia keeps k per bucket)");
+    }
     uint32_t *dsib = nullptr, *dbn = nullptr;
     uint8_t* dbc = nullptr;
     auto release = [&]() { if (dsib) hipFree(dsib); if (dbn) hipFree(dbn); if (dbc) hipFree(dbc); };
@@ -1692,12 +1802,26 @@ ovs_status kad_upload_host_tables(ovs_ctx* c)
     if (e == hipSuccess) e = hipMemcpy(dbc, hc.data(), n * 160, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dbn, hn.data(), sizeof(uint32_t) * n * 160 * k, hipMemcpyHostToDevice);
     uint32_t bad_node = 0, bad_code = 0;
+    // build into a temporary and swap it in only on success: a failed rebuild must leave the context
+    // either with its previous tables or with none (free_tables below), never with null or half-built
+    // tables that a later route would launch on
+    KadTables nt{};
+    if (e == hipSuccess)
+        e = kad_build_explicit(c->recs, c->xy, (uint32_t)n, c->P.k, c->P.s, dsib, dbc, dbn, nt, &bad_node, &bad_code,
+                               c->stream);
+    // test hook: OVS_FAULT_INJECT=kad_rebuild makes the rebuild report a broken invariant
+    // (tests/test_gpu_kad_maint.py::test_failed_rebuild_leaves_no_tables)
+    if (e == hipSuccess && fault_injected("kad_rebuild")) { e = hipErrorInvalidValue; bad_code = 99; }
+    release();
     if (e == hipSuccess) {
         kad_free(c->kad);
-        e = kad_build_explicit(c->recs, c->xy, (uint32_t)n, c->P.k, c->P.s, dsib, dbc, dbn, c->kad, &bad_node, &bad_code,
-                               c->stream);
+        c->kad = nt;
+    } else {
+        kad_free(nt);
+        // the host copy has already been changed by the round: the old device tables no longer
+        // describe it, so the context drops its network (later calls fail with OVS_ESTATE)
+        free_tables(c);
     }
-    release();
     if (e == hipErrorInvalidValue && bad_code) {
         char m[160];
         std::snprintf(m, sizeof m, "maintenance round broke a table invariant at node %u (code %u)", bad_node, bad_code);

@@ -47,6 +47,15 @@ def arc_bounds(n_total: int, world: int) -> list[int]:
     return [r * n_total // world for r in range(world + 1)]
 
 
+def default_top_levels(world: int) -> int:
+    """Replicated top finger levels for W arcs: the log2(W) levels whose jumps span arcs, plus 3 more
+    levels after which a lookup is within 2^(157 - log2 W) of its key, so it crosses to another arc
+    about once (at the boundary of its key's arc with probability ~1/8).  64 B per node and level."""
+    if world <= 1:
+        return 0
+    return min(32, int(np.ceil(np.log2(world))) + 3)
+
+
 # ---------------------------------------------------------------------------
 # steppers
 
@@ -63,9 +72,12 @@ class GpuShardStepper:
     """One rank's arc on one device: owns the engine context and the device buffers."""
 
     def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device, stream=None,
-                 capacity: int = 1 << 20, params: Params | None = None, lookup_siblings: int | None = None):
+                 capacity: int = 1 << 20, params: Params | None = None, lookup_siblings: int | None = None,
+                 top_levels: int | None = None):
         """lookup_siblings: route KBRTestApp LookupCalls with that many siblings (-1 = successorListSize;
-        ovs_shard_step_lookup) instead of one-way messages; finish them with lookup_finish()."""
+        ovs_shard_step_lookup) instead of one-way messages; finish them with lookup_finish().
+        top_levels: replicate that many top finger levels of every node (ovs_chord_shard_replicate;
+        None = default_top_levels(world)), so a lookup's long first hops are decided at home."""
         import torch
         self.lookup_siblings = lookup_siblings
         self.torch = torch
@@ -79,6 +91,9 @@ class GpuShardStepper:
         st = lib().ovs_chord_load_shard(self.eng._h, ids.ctypes.data_as(C.c_void_p), len(ids),
                                         xy.ctypes.data_as(C.c_void_p), self.bounds[rank], self.bounds[rank + 1], 0)
         self.eng._chk(st, "ovs_chord_load_shard")
+        self.top_levels = default_top_levels(self.world) if top_levels is None else int(top_levels)
+        if self.top_levels:
+            self.eng._chk(lib().ovs_chord_shard_replicate(self.eng._h, self.top_levels), "ovs_chord_shard_replicate")
         self.n_total = len(ids)
         self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
         self._cap = {}
@@ -216,6 +231,7 @@ class GpuShardStepper:
 
 for _name, _args in {
     "ovs_chord_load_shard": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32],
+    "ovs_chord_shard_replicate": [C.c_void_p, C.c_int32],
     "ovs_shard_make_records": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p],
     "ovs_shard_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p],
@@ -235,14 +251,220 @@ for _name, _args in {
     "ovs_kad_shard_deliver": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
     "ovs_kad_shard_errors": [C.c_void_p, C.c_void_p],
     "ovs_kad_shard_resp_bytes": [C.c_void_p],
+    "ovs_rccl_unique_id": [C.c_void_p],
+    "ovs_exchange_rccl_create": [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p],
+    "ovs_exchange_local_create": [C.c_uint32, C.c_void_p],
+    "ovs_shard_route_batch": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64,
+                              C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p],
+    "ovs_kad_shard_route_batch": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_uint64,
+                                  C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
 }.items():
     _f = getattr(lib(), _name)
     _f.argtypes = _args
     _f.restype = C.c_int
+lib().ovs_exchange_destroy.argtypes = [C.c_void_p]
+lib().ovs_exchange_destroy.restype = None
+lib().ovs_exchange_last_error.argtypes = []
+lib().ovs_exchange_last_error.restype = C.c_char_p
+lib().ovs_chord_shard_levels.argtypes = [C.c_void_p]
+lib().ovs_chord_shard_levels.restype = C.c_int32
 
 
 # ---------------------------------------------------------------------------
-# exchanges
+# the round loop behind the C ABI (ovs_shard_route_batch / ovs_kad_shard_route_batch) and its exchanges
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_uint32, C.POINTER(C.c_int64))
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_void_p,
+                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_uint32)
+DESTROY_FN = C.CFUNCTYPE(None, C.c_void_p)
+
+
+class Exchange(C.Structure):
+    """ovs_exchange (include/ovs_kbr.h): the collective callbacks the native round loop runs over."""
+    _fields_ = [("user", C.c_void_p), ("rank", C.c_uint32), ("world", C.c_uint32),
+                ("allgather_i64", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN),
+                ("allreduce_sum_i64", ALLREDUCE_FN), ("destroy", DESTROY_FN)]
+
+
+class RouteStats(C.Structure):
+    """ovs_shard_route_stats."""
+    _fields_ = [("rounds", C.c_uint32), ("cohorts", C.c_uint32), ("sent", C.c_uint64), ("sent_bytes", C.c_uint64),
+                ("done", C.c_uint64), ("step_ms", C.c_double), ("exchange_ms", C.c_double), ("total_ms", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+def _exchange_error(what: str, st: int):
+    msg = lib().ovs_exchange_last_error()
+    raise RuntimeError(f"{what}: status {st}: {msg.decode() if msg else ''}")
+
+
+def rccl_exchange(rank: int, world: int, device_index: int, unique_id: bytes) -> Exchange:
+    """The library's RCCL exchange (ovs_exchange_rccl_create); unique_id from rccl_unique_id() on rank 0."""
+    ex = Exchange()
+    buf = C.create_string_buffer(bytes(unique_id), 128)
+    st = lib().ovs_exchange_rccl_create(device_index, rank, world, buf, C.byref(ex))
+    if st != 0:
+        _exchange_error("ovs_exchange_rccl_create", st)
+    return ex
+
+
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    st = lib().ovs_rccl_unique_id(buf)
+    if st != 0:
+        _exchange_error("ovs_rccl_unique_id", st)
+    return buf.raw
+
+
+def rccl_exchange_from_torch(device_index: int) -> Exchange:
+    """An RCCL exchange for every rank of torch.distributed's default group (rank 0's unique id
+    broadcast through the group)."""
+    import torch.distributed as dist
+    obj = [rccl_unique_id() if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return rccl_exchange(dist.get_rank(), dist.get_world_size(), device_index, obj[0])
+
+
+def local_exchanges(world: int) -> list:
+    """W in-process ranks (threads): one exchange per rank (ovs_exchange_local_create)."""
+    arr = (Exchange * world)()
+    st = lib().ovs_exchange_local_create(world, arr)
+    if st != 0:
+        _exchange_error("ovs_exchange_local_create", st)
+    return [arr[r] for r in range(world)]
+
+
+def destroy_exchange(ex: Exchange):
+    lib().ovs_exchange_destroy(C.byref(ex))
+
+
+class _DevBytes:
+    """A device byte range as a torch tensor (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(ptr), False),
+                                         "version": 2, "strides": None}
+
+
+class CallbackExchange:
+    """An ovs_exchange whose callbacks run torch.distributed collectives (gloo on CPU tensors): the
+    native round loop over a Python-side process group -- how the tests drive it with gloo, and how
+    a caller could plug any transport in."""
+
+    def __init__(self, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group, self.dev = torch, dist, group, device
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self._cb = (ALLGATHER_FN(self._allgather), ALLTOALLV_FN(self._alltoallv), ALLREDUCE_FN(self._allreduce),
+                    DESTROY_FN())
+        self.ex = Exchange(None, self.rank, self.world, *self._cb)
+        self.ex._owner = self          # keeps the callbacks alive with the table
+        self.error = None
+
+    def _guard(self, f, *a):
+        try:
+            f(*a)
+            return 0
+        except Exception as e:       # a Python exception must not unwind through C frames
+            self.error = e
+            return 1
+
+    def _allgather(self, user, send, n, recv):
+        def run():
+            torch = self.torch
+            t = torch.tensor([send[i] for i in range(n)], dtype=torch.int64)
+            parts = [torch.empty_like(t) for _ in range(self.world)]
+            self.dist.all_gather(parts, t, group=self.group)
+            flat = torch.cat(parts).tolist()
+            for i, v in enumerate(flat):
+                recv[i] = v
+        return self._guard(run)
+
+    def _allreduce(self, user, vals, n):
+        def run():
+            t = self.torch.tensor([vals[i] for i in range(n)], dtype=self.torch.int64)
+            self.dist.all_reduce(t, group=self.group)
+            for i, v in enumerate(t.tolist()):
+                vals[i] = v
+        return self._guard(run)
+
+    def _alltoallv(self, user, send, send_rows, recv, recv_off, recv_rows, row_bytes, stream):
+        def run():
+            torch, dist = self.torch, self.dist
+            torch.cuda.ExternalStream(stream, device=self.dev).synchronize()    # the segments are complete
+            ops, host_recv = [], {}
+            for r in range(self.world):
+                ns, nr = int(send_rows[r]) * row_bytes, int(recv_rows[r]) * row_bytes
+                if r == self.rank:
+                    if nr:
+                        dst = torch.as_tensor(_DevBytes(recv + int(recv_off[r]) * row_bytes, nr), device=self.dev)
+                        dst.copy_(torch.as_tensor(_DevBytes(send[r], ns), device=self.dev))
+                    continue
+                if ns:
+                    ops.append(dist.P2POp(dist.isend, torch.as_tensor(_DevBytes(send[r], ns), device=self.dev).cpu(),
+                                          r, group=self.group))
+                if nr:
+                    host_recv[r] = torch.empty(nr, dtype=torch.uint8)
+                    ops.append(dist.P2POp(dist.irecv, host_recv[r], r, group=self.group))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            for r, t in host_recv.items():
+                torch.as_tensor(_DevBytes(recv + int(recv_off[r]) * row_bytes, t.numel()), device=self.dev).copy_(t)
+            torch.cuda.synchronize(self.dev)
+        return self._guard(run)
+
+
+def native_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, cohorts: int = 2, num_siblings: int = 0,
+                 stream=None) -> tuple:
+    """Route this rank's Chord batch through ovs_shard_route_batch (the round loop in C++);
+    returns (done records [k, 24] uint8 on the device, RouteStats)."""
+    torch = stepper.torch
+    n = int(keys_t.shape[0])
+    bounds = (C.c_uint64 * (stepper.world + 1))(*stepper.bounds)
+    nd = C.c_uint64(0)
+    stats = RouteStats()
+    s = stream if stream is not None else torch.cuda.current_stream(stepper.dev).cuda_stream
+    st = lib().ovs_shard_route_batch(stepper.eng._h, C.byref(ex), bounds, num_siblings, C.c_void_p(keys_t.data_ptr()),
+                                     C.c_void_p(src_t.data_ptr()), n, qid_base, C.c_void_p(stepper.done.data_ptr()),
+                                     stepper.done_cap, C.byref(nd), cohorts, C.byref(stats), C.c_void_p(s))
+    if st != 0 and isinstance(getattr(ex, "_owner", None), CallbackExchange) and ex._owner.error:
+        raise RuntimeError(f"exchange callback failed: {ex._owner.error!r}")
+    stepper.eng._chk(st, "ovs_shard_route_batch")
+    return stepper.done[:nd.value], stats
+
+
+def native_kad_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, num_siblings: int = -2,
+                     stream=None) -> tuple:
+    """Route this rank's Kademlia batch through ovs_kad_shard_route_batch; returns (done [n, 24], RouteStats)."""
+    torch = stepper.torch
+    n = int(keys_t.shape[0])
+    bounds = (C.c_uint64 * (stepper.world + 1))(*stepper.bounds)
+    stepper.n = n
+    stepper.done = torch.empty((max(n, 1), DONE_BYTES), dtype=torch.uint8, device=stepper.dev)
+    sib = None
+    if num_siblings >= -1:
+        ns = num_siblings if num_siblings >= 0 else stepper.params.s
+        stepper.sib = torch.empty((max(n, 1), max(ns, 1)), dtype=torch.int32, device=stepper.dev)
+        sib = C.c_void_p(stepper.sib.data_ptr())
+        stepper.qid_base = qid_base
+    nd = C.c_uint64(0)
+    stats = RouteStats()
+    s = stream if stream is not None else torch.cuda.current_stream(stepper.dev).cuda_stream
+    st = lib().ovs_kad_shard_route_batch(stepper.eng._h, C.byref(ex), bounds, num_siblings,
+                                         C.c_void_p(keys_t.data_ptr()), C.c_void_p(src_t.data_ptr()), n, qid_base,
+                                         C.c_void_p(stepper.done.data_ptr()), stepper.done.shape[0], C.byref(nd), sib,
+                                         C.byref(stats), C.c_void_p(s))
+    stepper.eng._chk(st, "ovs_kad_shard_route_batch")
+    return stepper.done[:nd.value], stats
+
+
+# ---------------------------------------------------------------------------
+# exchanges of the Python round loop (route_sharded / route_kad_sharded)
 
 class TorchExchange:
     """all-to-allv of fixed-size records over torch.distributed (RCCL on GPUs, gloo on CPU)."""
@@ -681,33 +903,61 @@ def done_to_numpy(done_t) -> np.ndarray:
     return done_t.cpu().numpy().view(DONE_DTYPE).ravel()
 
 
-class ShardedChord:
-    """bench.py driver for one rank: ring arc + lookups resident in HBM + RCCL exchange."""
+def bench_exchange(device, comm_dev):
+    """The native loop's exchange for a bench rank: the library's RCCL exchange when the process group
+    is RCCL (comm_dev on the GPU), else torch.distributed callbacks (gloo rehearsal)."""
+    if comm_dev is not None and getattr(comm_dev, "type", "cuda") == "cuda":
+        return rccl_exchange_from_torch(device.index if device.index is not None else 0)
+    return CallbackExchange(device).ex
 
-    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None):
+
+class ShardedChord:
+    """bench.py driver for one rank: ring arc + lookups resident in HBM + RCCL exchange.  The round loop
+    runs in C++ behind the ABI (ovs_shard_route_batch) unless OVS_SHARD_PYLOOP=1 (the Python loop,
+    route_sharded, over torch.distributed)."""
+
+    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None, top_levels=None,
+                 native=None):
+        import os
         self.bounds = arc_bounds(len(ids), world)
         n = keys_t.shape[0]
-        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(n + n // 4, 1024), params=params)
+        self.stepper = GpuShardStepper(ids, xy, self.bounds, rank, device, capacity=max(n + n // 4, 1024), params=params,
+                                       top_levels=top_levels)
         self.stepper.reset(world * n + 1024)
         self.stepper.timing = True
-        self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)
+        self.native = (os.environ.get("OVS_SHARD_PYLOOP") != "1") if native is None else native
+        if self.native:
+            self.ex = bench_exchange(device, comm_dev)
+        else:
+            self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)
         self.keys_t, self.src_t = keys_t, src_t
         self.qid_base = rank * n
         self._done = None
         self.rounds = 0
         self.runs = 0
         self.kernel_ms = 0.0
+        self.stats = None
 
     def run(self):
         self.stepper.reset(self.stepper.done_cap)
         self.stepper.kernel_ms = 0.0
-        self._done, self.rounds = route_sharded(self.stepper, self.exchange, self.keys_t, self.src_t, self.qid_base)
+        if self.native:
+            self._done, st = native_route(self.stepper, self.ex, self.keys_t, self.src_t, self.qid_base, cohorts=2)
+            self.rounds = st.rounds
+            self.stats = st.as_dict()
+            self.kernel_ms += st.step_ms
+        else:
+            self._done, self.rounds = route_sharded(self.stepper, self.exchange, self.keys_t, self.src_t, self.qid_base)
+            self.kernel_ms += self.stepper.kernel_ms
         self.runs += 1
-        self.kernel_ms += self.stepper.kernel_ms
 
     def hop_total(self) -> int:
         d = done_to_numpy(self._done)
         return int(d["hops"].astype(np.int64).sum())
+
+    def results_by_qid(self) -> dict:
+        """This rank's finished records in batch order (qid - qid_base), as ovs_route_out fields."""
+        return _results_by_qid(self._done, self.qid_base, self.keys_t.shape[0], rpcs=False)
 
     def ok_total(self) -> int:
         d = done_to_numpy(self._done)
@@ -715,13 +965,20 @@ class ShardedChord:
 
 
 class ShardedKademlia:
-    """bench.py driver for one rank: Kademlia arc + lookups resident in HBM + request/response exchange."""
+    """bench.py driver for one rank: Kademlia arc + lookups resident in HBM + request/response exchange
+    (the round loop in C++, ovs_kad_shard_route_batch, unless OVS_SHARD_PYLOOP=1)."""
 
-    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None):
+    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None, native=None):
+        import os
         self.bounds = arc_bounds(len(ids), world)
         self.stepper = KadShardStepper(ids, xy, self.bounds, rank, device, params=params)
         self.stepper.timing = True
-        self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)
+        self.native = (os.environ.get("OVS_SHARD_PYLOOP") != "1") if native is None else native
+        if self.native:
+            self.ex = bench_exchange(device, comm_dev)
+        else:
+            self.exchange = TorchExchange(world, comm_dev if comm_dev is not None else device)
+        self.stats = None
         self.keys_t, self.src_t = keys_t, src_t
         self.qid_base = rank * keys_t.shape[0]
         self._done = None
@@ -733,11 +990,17 @@ class ShardedKademlia:
     def run(self):
         self.stepper.kernel_ms = 0.0
         self.stepper.served = 0
-        self._done, self.rounds = route_kad_sharded(self.stepper, self.exchange, self.keys_t, self.src_t,
-                                                    self.qid_base)
+        if self.native:
+            self._done, st = native_kad_route(self.stepper, self.ex, self.keys_t, self.src_t, self.qid_base)
+            self.rounds = st.rounds
+            self.stats = st.as_dict()
+            self.kernel_ms += st.step_ms
+        else:
+            self._done, self.rounds = route_kad_sharded(self.stepper, self.exchange, self.keys_t, self.src_t,
+                                                        self.qid_base)
+            self.kernel_ms += self.stepper.kernel_ms
+            self.served = self.stepper.served
         self.runs += 1
-        self.kernel_ms += self.stepper.kernel_ms
-        self.served = self.stepper.served
 
     def hop_total(self) -> int:
         return int(done_to_numpy(self._done)["hops"].astype(np.int64).sum())
@@ -748,3 +1011,24 @@ class ShardedKademlia:
     def rpc_total(self) -> int:
         """FindNodeCalls of this rank's lookups (the done records carry each lookup's count)."""
         return int(done_to_numpy(self._done)["pad"].astype(np.int64).sum())
+
+    def results_by_qid(self) -> dict:
+        """This rank's finished records in batch order, as ovs_route_out fields plus the RPC counts."""
+        return _results_by_qid(self._done, self.qid_base, self.keys_t.shape[0], rpcs=True)
+
+
+def _results_by_qid(done_t, qid_base: int, n: int, rpcs: bool) -> dict:
+    d = done_to_numpy(done_t)
+    i = d["qid"].astype(np.int64) - int(qid_base)
+    if len(d) != n or i.min(initial=0) < 0 or i.max(initial=-1) >= n:
+        raise RuntimeError(f"finished records do not cover the batch ({len(d)} for {n})")
+    out = {}
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+        a = np.empty(n, dtype=d[f].dtype)
+        a[i] = d[f]
+        out[f] = a
+    if rpcs:
+        a = np.empty(n, dtype=np.uint32)
+        a[i] = d["pad"]
+        out["rpcs"] = a
+    return out

@@ -63,3 +63,44 @@ def test_c_consumer_matches_oracle(tmp_path, overlay):
     for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
         assert np.array_equal(lo[f], c[f]), f
     assert np.array_equal(sib, c["siblings"])
+
+
+EXE2 = ROOT / "tests" / "c_consumer" / "sharded_route"
+
+
+@pytest.mark.parametrize("overlay,world,top", [(kbr.OVERLAY_CHORD, 3, 6), (kbr.OVERLAY_CHORD, 4, 0),
+                                               (kbr.OVERLAY_KADEMLIA, 3, 0)])
+def test_c_consumer_sharded_route(tmp_path, overlay, world, top):
+    """The multi-GPU route from C: tests/c_consumer/sharded_route runs W ranks as
+    pthreads, one context per arc, over the library's in-process exchange through
+    ovs_shard_route_batch / ovs_kad_shard_route_batch -- the round loop in C++ behind the ABI -- and
+    its results equal ovs_route_batch on the whole network and the oracle."""
+    assert EXE2.exists(), "tests/c_consumer/sharded_route missing: run __graft_entry__.build()"
+    net = W.population(20000, 0xC5 + overlay + world)
+    keys, src = W.lookups(net.ids, 6000, 0xC6 + overlay, node_ids=(world % 2 == 1))
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    with open(fin, "wb") as f:
+        f.write(struct.pack("<IQQ", overlay, len(net.ids), len(keys)))
+        for a in (net.ids.astype("<u4"), net.xy.astype("<f8"), keys.astype("<u4"), src.astype("<u4")):
+            f.write(np.ascontiguousarray(a).tobytes())
+        f.write(struct.pack("<Ii", world, top))
+    subprocess.run([str(EXE2), str(fin), str(fout)], check=True, timeout=300)
+    raw = fout.read_bytes()
+    m = len(keys)
+    sh = np.frombuffer(raw, dtype=kbr.ROUTE_OUT_DTYPE, count=m)
+    off = sh.nbytes
+    rpcs = np.frombuffer(raw, dtype="<u4", count=m, offset=off)
+    off += rpcs.nbytes
+    ref = np.frombuffer(raw, dtype=kbr.ROUTE_OUT_DTYPE, count=m, offset=off)
+    rounds = struct.unpack_from("<I", raw, off + ref.nbytes)[0]
+    assert rounds >= 2
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+        assert np.array_equal(sh[f], ref[f]), f
+    if overlay == kbr.OVERLAY_CHORD:
+        e = OracleNet("chord", net.ids, net.xy, chord_params()).route(keys, src, record_hops=False)
+    else:
+        e = OracleNet("kademlia", net.ids, net.xy, kad_params(lookupParallelRpcs=3)).route(keys, src, record_hops=False,
+                                                                                          count_rpcs=True)
+        assert np.array_equal(rpcs, e["rpcs"])
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+        assert np.array_equal(sh[f], e[f]), f

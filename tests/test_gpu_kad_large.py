@@ -187,3 +187,31 @@ def test_sharded_k16_matches_single_context(engine: KbrEngine, world, alpha, ns)
                 assert np.array_equal(lo[f].astype(np.int64), np.asarray(ref[f])[qid].astype(np.int64)), (r, f)
             nsl = max(ns, 1)
             assert np.array_equal(sib[:, :nsl], np.asarray(ref["siblings"])[qid][:, :nsl])
+
+
+def test_shard_refuses_capacity_change_mid_batch():
+    """ADVICE r04: the shard buffers are sized for the findNode capacity fixed at begin (8 here);
+    moving lookupRedundantNodes across 8 between begin and step must be refused (OVS_ESTATE) by
+    step, serve and deliver, not run a 16-wide layout in 8-wide buffers."""
+    import torch
+    from oversim_amd.shard import KadShardStepper, arc_bounds
+    n, m = 3000, 256
+    net = W.population(n, 0x16F)
+    bounds = arc_bounds(n, 2)
+    dev = torch.device("cuda", 0)
+    st = KadShardStepper(net.ids, net.xy, bounds, 0, dev, params=Params.kademlia())
+    k, s0 = W.lookups(net.ids, m, 0x171, node_ids=True)
+    s0 = (s0.astype(np.int64) % bounds[1]).astype(np.uint32)
+    st.begin(torch.from_numpy(k.view(np.int32)).to(dev), torch.from_numpy(s0.view(np.int32)).to(dev), 0)
+    st.eng.set_params(Params.kademlia().replace(lookupRedundantNodes=16))
+    with pytest.raises(KbrError, match="capacity"):
+        st.step()
+    req = torch.zeros((4, 32), dtype=torch.uint8, device=dev)
+    with pytest.raises(KbrError, match="capacity"):
+        st.serve(req)
+    with pytest.raises(KbrError, match="capacity"):
+        st.deliver(torch.zeros((4, 104), dtype=torch.uint8, device=dev))
+    # back to the begin-time capacity: the batch runs
+    st.eng.set_params(Params.kademlia())
+    st.step()
+    torch.cuda.synchronize()

@@ -119,3 +119,25 @@ def test_snapshot_is_a_fixed_point(engine):
     assert np.array_equal(np.sort(before[0], axis=1), np.sort(after[0], axis=1))
     assert np.array_equal(before[1], after[1])
     assert all(np.array_equal(np.sort(a, axis=-1), np.sort(b, axis=-1)) for a, b in zip(before[2], after[2]))
+
+
+def test_failed_rebuild_leaves_no_tables(engine, monkeypatch):
+    """a maintenance round whose table rebuild fails (forced here through the
+    OVS_FAULT_INJECT test hook) must not leave the context routing on null or half-built device
+    tables: the round reports the error, and every later call fails with OVS_ESTATE instead of
+    launching a kernel."""
+    from oversim_amd.kbr import KbrError
+    net = W.population(2000, 0x4b79)
+    tabs, join = partial_join(net.ids, net.xy, 0.1, 17)
+    engine.set_params(Params.kademlia())
+    engine.kad_load_tables(net.ids, net.xy, tabs["siblings"], tabs["bucket_count"], tabs["bucket_nodes"])
+    monkeypatch.setenv("OVS_FAULT_INJECT", "kad_rebuild")
+    with pytest.raises(KbrError, match="invariant"):
+        engine.kad_maintenance_round(join, 1)
+    monkeypatch.delenv("OVS_FAULT_INJECT")
+    keys, src = W.lookups(net.ids, 256, 5, node_ids=True)
+    with pytest.raises(KbrError, match="ESTATE|no network"):
+        engine.lookup(keys, src)
+    # the context is usable again after a reload
+    engine.kad_load(net.ids, net.xy)
+    assert np.all(engine.lookup(keys, src)["status"] == 0)

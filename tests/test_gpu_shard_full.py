@@ -73,7 +73,10 @@ def test_chord_w8_config_d_full_size():
     bounds = arc_bounds(n, world)
     dev = torch.device("cuda", 0)
     ks, ss, qb, allk, alls = _split(net, bounds, m, 0xD30, lambda r: r % 2 == 0)
-    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, params=Params.chord())
+    # top_levels = 0: eight contexts on ONE GPU cannot also hold eight copies of replicated top finger
+    # levels of 2^26 nodes (4.3 GB per level each); a real rank holds one
+    steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=world * m, params=Params.chord(),
+                                top_levels=0)
                 for r in range(world)]
     for st in steppers:
         st.reset(world * m)

@@ -23,6 +23,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", choices=["C", "D", "E"], required=True)
 ap.add_argument("--lookups-per-rank", type=int, default=0)
 ap.add_argument("--world", type=int, default=8)
+ap.add_argument("--top-levels", type=int, default=None, help="Chord: replicated top finger levels (default: shard.default_top_levels)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -50,7 +51,8 @@ if kad:
         steppers[r].begin(inputs[r]["keys_t"], inputs[r]["src_t"], r * m)
 else:
     # send segments of 1.25 m records per destination (a round's inbox is about m; step() grows them)
-    steppers = [GpuShardStepper(ids, xy, bounds, r, dev, capacity=m + m // 4, params=params) for r in range(Wn)]
+    steppers = [GpuShardStepper(ids, xy, bounds, r, dev, capacity=m + m // 4, params=params, top_levels=a.top_levels)
+                for r in range(Wn)]
     for st in steppers:
         st.reset(Wn * m)
     # the first round starts from the keys (ovs_shard_step_keys), as route_sharded
@@ -130,6 +132,26 @@ while True:
 torch.cuda.synchronize()
 dn = [done_to_numpy(s.finished()) for s in steppers]
 d = np.concatenate(dn)
+if not kad and os.environ.get("OVS_MODEL_CHECK", "1") == "1":
+    # every lookup against the single-context route of the same ring (the parity the tests assert)
+    from oversim_amd import KbrEngine
+    del steppers
+    torch.cuda.empty_cache()
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(Wn * m))
+    with KbrEngine(0) as e:
+        e.set_params(params)
+        e.chord_load_device(inputs[0]["ids_t"].data_ptr(), inputs[0]["xy_t"].data_ptr(), n)
+        kk = torch.cat([I["keys_t"] for I in inputs]); ss = torch.cat([I["src_t"] for I in inputs])
+        out = torch.empty((kk.shape[0], 16), dtype=torch.uint8, device=dev)
+        e.lookup_device(kk.data_ptr(), ss.data_ptr(), kk.shape[0], out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ref = out.cpu().numpy().reshape(-1).view(np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
+                                                           ("one_way_hops", "u1"), ("latency_ns", "<i8")]))
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+        bad = int((d[f].astype(np.int64) != ref[f].astype(np.int64)).sum())
+        assert bad == 0, f"{f}: {bad} lookups differ from the single-context route"
+    print(json.dumps(dict(check="sharded == single-context route", lookups=int(len(d)))), flush=True)
 print(json.dumps(dict(summary=True, workload=a.workload, world=Wn, rounds=rounds, lookups=int(len(d)),
                       ok=int((d["status"] == 0).sum()), mean_hops=float(d["hops"].mean()),
                       step_ms_per_rank=[round(float(x), 3) for x in tot["step_ms"]],
