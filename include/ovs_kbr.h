@@ -674,6 +674,30 @@ ovs_status  ovs_kad_shard_deliver(ovs_ctx* ctx, const void* in, uint64_t n, void
  * device.  The caller fails the batch when it is non-zero. */
 ovs_status  ovs_kad_shard_errors(ovs_ctx* ctx, uint64_t* bad);
 
+/* Kademlia lookups that MIGRATE (ABI 11).  Under the XOR-prefix partition a lookup's late
+ * FindNodeCalls all go to nodes within 2^(160 - log2 W) of its key, i.e. to the key's own arc, and
+ * its early ones to nodes anywhere.  ovs_kad_shard_replicate keeps the top `top_levels` buckets of
+ * EVERY node on every rank (96 B per node and level): a findNode whose answer is a full main bucket
+ * among them (the long first hops) is answered on any rank, and a lookup whose next findNode needs
+ * another arc's rows moves there as one record (ovs_kad_shard_rec_bytes bytes: its whole
+ * IterativeLookup state) instead of exchanging a request and a response per call -- on prefix arcs
+ * it moves at most once, to its key's arc.  Rebuilds the arc's tables; 0 = none.  The results are
+ * the single-context K2's (the same event order, findNode answers and delays). */
+ovs_status  ovs_kad_shard_replicate(ovs_ctx* ctx, int32_t top_levels);
+int32_t     ovs_kad_shard_levels(const ovs_ctx* ctx);
+int32_t     ovs_kad_shard_rec_bytes(const ovs_ctx* ctx);
+/* One migration round (one-way KBR routes): advance the lookups of `in` (n_in records of
+ * ovs_kad_shard_rec_bytes bytes) -- or, in a batch's first round (in == NULL), n_in lookups from
+ * fkeys / fsrc with ids fqid + i -- until each finishes (appended to done, done_count) or needs
+ * another rank's rows (appended to segment d of out: out + d * out_cap records, out_count[d]).
+ * A segment never receives more than n_in records.  Lookups finish on whichever rank holds them
+ * last.  shard_lo: HOST array of nshards + 1 arc bounds; errors via ovs_kad_shard_errors. */
+ovs_status  ovs_kad_shard_mig_step(ovs_ctx* ctx, const void* in, uint64_t n_in, const ovs_key160* fkeys,
+                                   const uint32_t* fsrc, uint32_t fqid, void* out, uint64_t out_cap,
+                                   unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                                   unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards,
+                                   void* stream);
+
 /* ---------------------------------------------------------------------------
  * Sharded routing behind the ABI (ABI 11): the whole multi-GPU batch in one call.
  *
@@ -742,10 +766,13 @@ ovs_status  ovs_shard_route_batch(ovs_ctx* ctx, const ovs_exchange* ex, const ui
                                   int32_t num_siblings, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                                   uint32_t qid_base, ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done,
                                   uint32_t cohorts, ovs_shard_route_stats* stats, void* stream);
-/* The same for Kademlia (ovs_kad_load_shard; the lookups stay on this rank, FindNodeCalls and their
- * responses are exchanged): num_siblings < -1 ... -2: one-way KBR routes; -1 / 0..8: LookupCalls
- * (as ovs_kad_shard_begin_lookup; siblings = n rows of max(num_siblings, 1), device memory).
- * done receives exactly this rank's n lookups (done_cap >= n); done[i].pad = its FindNodeCalls. */
+/* The same for Kademlia (ovs_kad_load_shard): num_siblings OVS_KAD_ONEWAY: one-way KBR routes;
+ * -1 / 0..8: LookupCalls (as ovs_kad_shard_begin_lookup; siblings = n rows of max(num_siblings, 1),
+ * device memory).  One-way routes on a context with replicated top buckets (ovs_kad_shard_replicate)
+ * MIGRATE (ovs_kad_shard_mig_step rounds; a lookup finishes on any rank, so done_cap must hold every
+ * record that can finish here, as for Chord); otherwise the lookups stay home and FindNodeCalls and
+ * their responses are exchanged (done receives exactly this rank's n lookups, done_cap >= n).
+ * done[i].pad = the lookup's FindNodeCalls. */
 ovs_status  ovs_kad_shard_route_batch(ovs_ctx* ctx, const ovs_exchange* ex, const uint64_t* shard_lo,
                                       int32_t num_siblings, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                                       uint32_t qid_base, ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done,

@@ -23,6 +23,7 @@ void kad_free(KadTables& t)
     t.nodes = nullptr; t.nodex = nullptr; t.blks = nullptr; t.sib = nullptr; t.slev = nullptr; t.rows_blks = 0;
     t.goff = nullptr; t.gtop = nullptr; t.gidx = nullptr; t.gend = nullptr; t.gtotal = 0;
     t.general = 0; t.b = 1; t.nb = KEYBITS;
+    t.tl = 0; t.tend = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -148,10 +149,10 @@ __global__ void k_kad_prefix_ties(const KeyRec* __restrict__ recs, uint32_t n, u
     if (((top64(kload(recs, i)) ^ top64(kload(recs, i + 1))) >> 1) == 0) atomicOr(flag, 1u);
 }
 
-__global__ void k_kad_set_boff(KadNode* nodes, const uint64_t* off, uint32_t lo, uint32_t hi)
+__global__ void k_kad_set_boff(KadNode* nodes, const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t base)
 {
     const uint32_t v = lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < hi) nodes[v].boff = (uint32_t)off[v];
+    if (v < hi) nodes[v].boff = (uint32_t)(base + off[v]);
 }
 
 __device__ __forceinline__ void put_entry(KadBlk* __restrict__ blks, uint64_t blk0, int q, uint32_t x,
@@ -186,6 +187,52 @@ __device__ void put_sibling_row(KadBlk* __restrict__ blks, uint64_t blk0, int sb
     for (int q = 0; q < sbn * KBLK; ++q) put_entry(blks, blk0, q, q < cnt ? x[q] : NONE, recs);
 }
 
+// bucket m of node v under the snapshot rule: up to k members of T_m = [flo, fhi) (the nodes at
+// msb(x ^ v) = m) minus v's siblings L, chosen by Floyd sampling with kad_hash(seed, v, m, j)
+// (DESIGN.md §4), written in ascending index order to the bpb blocks at blk0.  Returns the members.
+__device__ int kad_bucket_fill(const KeyRec* __restrict__ recs, uint32_t v, int m, uint32_t flo, uint32_t fhi,
+                               const uint32_t* L, int S5, int k, uint64_t seed, KadBlk* __restrict__ blks, uint64_t blk0)
+{
+    uint32_t chosen[KMAX];
+    const int bpb = (k + KBLK - 1) / KBLK;
+    uint32_t nsin = 0;
+    for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
+    const uint32_t c = (fhi - flo) - nsin;
+    int nch = 0;
+    if (c <= (uint32_t)k) {
+        for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
+    } else {
+        for (uint32_t j = c - (uint32_t)k; j < c; ++j) {
+            const uint32_t t = (uint32_t)(kad_hash(seed, v, (uint32_t)m, j) % (uint64_t)(j + 1));
+            bool dup = false;
+            for (int q = 0; q < nch; ++q) dup |= (chosen[q] == t);
+            chosen[nch++] = dup ? j : t;
+        }
+        for (int a = 1; a < nch; ++a) {
+            const uint32_t x = chosen[a];
+            int q = a - 1;
+            while (q >= 0 && chosen[q] > x) { chosen[q + 1] = chosen[q]; --q; }
+            chosen[q + 1] = x;
+        }
+    }
+    int outn = 0;
+    if (nsin == 0) {
+        for (int q = 0; q < nch; ++q) put_entry(blks, blk0, outn++, flo + chosen[q], recs);
+    } else {
+        uint32_t rank = 0;
+        int q = 0;
+        for (uint32_t x = flo; x < fhi && q < nch; ++x) {
+            bool is_sib = false;
+            for (int i = 0; i < S5; ++i) is_sib |= (L[i] == x);
+            if (is_sib) continue;
+            if (rank == chosen[q]) { put_entry(blks, blk0, outn++, x, recs); ++q; }
+            ++rank;
+        }
+    }
+    for (int q = outn; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);
+    return outn;
+}
+
 // snapshot pass B: buckets m = 159 .. endIndex of the owned nodes, up to k members of T_m minus
 // siblings chosen by Floyd sampling (snapshot rule); sibling rows
 __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __restrict__ nodes, uint32_t n, int k,
@@ -202,51 +249,50 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     uint32_t lo = 0, hi = n;
-    uint32_t chosen[KMAX];
     const int bpb = (k + KBLK - 1) / KBLK;
     for (int m = KEYBITS - 1; m >= endIndex; --m) {
         const uint32_t mid = split_bit(recs, lo, hi, m);
         const uint32_t nb = kbit(me, m);
         const uint32_t flo = nb ? lo : mid, fhi = nb ? mid : hi;
         const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
-        uint32_t nsin = 0;
-        for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
-        const uint32_t c = (fhi - flo) - nsin;
-        int nch = 0;
-        if (c <= (uint32_t)k) {
-            for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
-        } else {
-            for (uint32_t j = c - (uint32_t)k; j < c; ++j) {
-                const uint32_t t = (uint32_t)(kad_hash(seed, v, (uint32_t)m, j) % (uint64_t)(j + 1));
-                bool dup = false;
-                for (int q = 0; q < nch; ++q) dup |= (chosen[q] == t);
-                chosen[nch++] = dup ? j : t;
-            }
-            for (int a = 1; a < nch; ++a) {
-                const uint32_t x = chosen[a];
-                int q = a - 1;
-                while (q >= 0 && chosen[q] > x) { chosen[q + 1] = chosen[q]; --q; }
-                chosen[q + 1] = x;
-            }
-        }
-        int outn = 0;
-        if (nsin == 0) {
-            for (int q = 0; q < nch; ++q) put_entry(blks, blk0, outn++, flo + chosen[q], recs);
-        } else {
-            uint32_t rank = 0;
-            int q = 0;
-            for (uint32_t x = flo; x < fhi && q < nch; ++x) {
-                bool is_sib = false;
-                for (int i = 0; i < S5; ++i) is_sib |= (L[i] == x);
-                if (is_sib) continue;
-                if (rank == chosen[q]) { put_entry(blks, blk0, outn++, x, recs); ++q; }
-                ++rank;
-            }
-        }
-        for (int q = outn; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);
+        kad_bucket_fill(recs, v, m, flo, fhi, L, S5, k, seed, blks, blk0);
         lo = nb ? mid : lo;
         hi = nb ? hi : mid;
     }
+}
+
+// sharded networks (KadTables::tl > 0): the top tl buckets m = 159 .. 160 - tl of EVERY node, at
+// blks[(v * tl + (159 - m)) * bpb] -- the same members its owner's row holds (the same snapshot rule),
+// so findNode(K) at any node whose main bucket m is one of them, lies above its sibling zone and is
+// full can be answered on any rank (the kernels' virtual row offset v * tl * bpb).  The node line
+// records which of them are full (KMETA_TOPFULL bits), which decides that at send time.
+__global__ void k_kad_top_buckets(const KeyRec* __restrict__ recs, KadNode* __restrict__ nodes, uint32_t n, int k,
+                                  int S5, uint64_t seed, const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks,
+                                  int tl)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const K160 me = kload(recs, v);
+    const uint32_t* L = sib + (uint64_t)v * S5;
+    const int endIndex = kad_end(nodes[v].meta);
+    const int bpb = (k + KBLK - 1) / KBLK;
+    uint32_t lo = 0, hi = n, full = 0;
+    for (int m = KEYBITS - 1; m >= KEYBITS - tl; --m) {
+        const uint32_t mid = split_bit(recs, lo, hi, m);
+        const uint32_t nb = kbit(me, m);
+        const uint32_t flo = nb ? lo : mid, fhi = nb ? mid : hi;
+        const int j = KEYBITS - 1 - m;
+        const uint64_t blk0 = ((uint64_t)v * (uint32_t)tl + (uint32_t)j) * (uint64_t)bpb;
+        if (m >= endIndex) {
+            const int cnt = kad_bucket_fill(recs, v, m, flo, fhi, L, S5, k, seed, blks, blk0);
+            if (cnt >= k && m > endIndex) full |= 1u << j;
+        } else {
+            for (int q = 0; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);
+        }
+        lo = nb ? mid : lo;
+        hi = nb ? hi : mid;
+    }
+    nodes[v].meta = (nodes[v].meta & ~KMETA_TOPFULL_ALL) | (full << KMETA_TOPFULL_SHIFT);
 }
 
 // explicit tables, pass A: validate a node's tables against the invariants OverSim's routingAdd
@@ -470,7 +516,7 @@ static hipError_t kad_prefix_flag(const KeyRec* recs, uint32_t n, KadTables& t, 
 }
 
 hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, uint64_t seed, KadTables& t,
-                     hipStream_t st, uint32_t lo, uint32_t hi)
+                     hipStream_t st, uint32_t lo, uint32_t hi, int tl)
 {
     hipError_t e;
     kad_free(t);
@@ -478,6 +524,7 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     if (lo >= hi) return hipErrorInvalidValue;
     t.k = k; t.s = s; t.seed = seed; t.lo = lo; t.hi = hi; t.snapshot = 1; t.maybe_short = 0;
     if (k < 1 || k > KMAX) return hipErrorNotSupported;
+    if (tl < 0 || tl > KTOP_MAX) return hipErrorInvalidValue;
     const int bpb = (k + KBLK - 1) / KBLK;
     t.bpb = bpb;
     const int S5 = 5 * s, sbn = (S5 + 1 + KBLK - 1) / KBLK;   // the node + its siblings
@@ -508,15 +555,23 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     uint64_t total = 0;
     hipMemcpyAsync(&total, off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
     if ((e = hipStreamSynchronize(st)) != hipSuccess) { cleanup(); return e; }
-    if (total >= 0xFFFFFFFFull) { cleanup(); return hipErrorInvalidValue; }
-    t.rows_blks = total;
-    const uint64_t nblks = total + (uint64_t)nown * sbn + 1;
+    // the replicated top buckets of every node come first (the same offsets on every rank), then
+    // the owned rows, then the owned sibling rows
+    const uint64_t tend = (uint64_t)n * (uint32_t)tl * (uint32_t)bpb;
+    if (total + tend >= 0xFFFFFFFFull) { cleanup(); return hipErrorInvalidValue; }
+    t.tl = tl;
+    t.tend = tend;
+    t.rows_blks = tend + total;
+    const uint64_t nblks = t.rows_blks + (uint64_t)nown * sbn + 1;
     if ((e = hipMalloc(&t.blks, sizeof(KadBlk) * nblks)) != hipSuccess) { cleanup(); return e; }
-    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(nown, 256)), dim3(256), 0, st, t.nodes, off, lo, hi);
+    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(nown, 256)), dim3(256), 0, st, t.nodes, off, lo, hi, tend);
     if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)nown * S5)) != hipSuccess) { cleanup(); return e; }
     hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5, hipMemcpyDeviceToDevice, st);
     hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(nown, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn, seed,
                        sib_all, t.blks, t.rows_blks, lo, hi);
+    if (tl > 0)
+        hipLaunchKernelGGL(k_kad_top_buckets, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, seed, sib_all,
+                           t.blks, tl);
     if (lo != 0 || hi != n) {
         if ((e = hipMalloc(&t.slev, (uint64_t)n * S5)) != hipSuccess) { cleanup(); return e; }
         hipLaunchKernelGGL(k_kad_sib_levels, dim3(nblk((uint64_t)n * S5, 256)), dim3(256), 0, st, t.nodes, sib_all, n,
@@ -580,7 +635,7 @@ hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n,
     if (total >= 0xFFFFFFFFull) { cleanup(); return hipErrorInvalidValue; }
     t.rows_blks = total;
     if ((e = hipMalloc(&t.blks, sizeof(KadBlk) * (total + (uint64_t)n * sbn + 1))) != hipSuccess) { cleanup(); return e; }
-    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, 0u, n);
+    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, 0u, n, 0ull);
     hipLaunchKernelGGL(k_kad_explicit_rows, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn,
                        t.sib, bcount, bnodes, t.blks, t.rows_blks);
     e = hipStreamSynchronize(st);

@@ -29,6 +29,12 @@ inline int kad_pend_slots(int alpha) { return alpha <= 4 ? alpha : KAD_MAX_ALPHA
 
 // meta bits of KadNode
 constexpr uint32_t KMETA_MASK_OUT = 1u << 24;   // level-mask bits below the 64-bit window: exact check
+// sharded networks with replicated top buckets (KadTables::tl): bit 25 + j set when the node's
+// bucket 159 - j (j < tl <= KTOP_MAX) holds k members and lies above its sibling zone -- then
+// findNode there is that bucket's XOR-closest, answerable from the replicated block on any rank
+constexpr int KTOP_MAX = 7;
+constexpr int KMETA_TOPFULL_SHIFT = 25;
+constexpr uint32_t KMETA_TOPFULL_ALL = 0x7Fu << KMETA_TOPFULL_SHIFT;
 struct alignas(64) KadNode {
     uint32_t key[5];
     uint32_t boff;     // first line of the bucket row
@@ -84,6 +90,11 @@ struct KadTables {
     uint32_t* gidx = nullptr;      // per member: node index (LRU order within a bucket)
     int16_t* gend = nullptr;       // per node: routingBucketIndex of its farthest sibling (-1: none)
     uint64_t gtotal = 0;           // members
+    // sharded networks: the top tl buckets of EVERY node replicated at the front of blks (tend
+    // blocks: bucket 159 - j of v at (v * tl + j) * bpb), so a responder off the owned arc whose
+    // findNode is its full main bucket there is answered on this rank (Kademlia migration, §6)
+    int tl = 0;
+    uint64_t tend = 0;
 };
 
 // the general-table view of K2g and the batched findNode (kad_general.hip)
@@ -108,6 +119,8 @@ struct KadView {
     int S5;       // sibling table capacity 5s
     int sbn;      // blocks per sibling row = ceil(5s / 8)
     uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)
+    int tl;            // replicated top buckets (KadTables::tl) ...
+    uint32_t tend;     // ... in blocks [0, tend): a row offset below tend is a replicated (virtual) row
     int maybe_short;
     int snapshot;      // tables built by the snapshot rule (ovs_kad_load), not imported
     unsigned long long* err;   // sharded kernels: a table read this arc cannot serve is counted here
@@ -124,7 +137,7 @@ __device__ __forceinline__ void kad_count_error(const KadView& V)
 void kad_free(KadTables& t);
 // snapshot tables for nodes [lo, hi) of the sorted ring (node records for all n)
 hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, uint64_t seed, KadTables& t,
-                     hipStream_t st, uint32_t lo = 0, uint32_t hi = 0xFFFFFFFFu);
+                     hipStream_t st, uint32_t lo = 0, uint32_t hi = 0xFFFFFFFFu, int tl = 0);
 // explicit tables (device copies of the caller's siblings / bucket members); returns
 // hipErrorInvalidValue with *bad_node set when a table breaks the reference's invariants
 hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n, int k, int s, const uint32_t* sib,

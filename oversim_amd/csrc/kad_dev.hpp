@@ -427,9 +427,10 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
                                                  int pre = -1, int r0 = 0)
 {
     blk_clear(res);
-    if (V.err && kad_off_arc(V, c)) {
+    if (V.err && kad_off_arc(V, c) && g.boff >= V.tend) {
         // sharded kernels: c's bucket and sibling rows live on its owner only -- counted
-        // (ovs_kad_shard_errors), answered empty
+        // (ovs_kad_shard_errors), answered empty.  (A row offset below V.tend names c's replicated
+        // top buckets, which every rank holds.)
         kad_count_error(V);
         return 0;
     }
@@ -845,6 +846,104 @@ __device__ __forceinline__ void kad_state_get(KadLookup<A, C>& L, const uint32_t
     L.nsent = get();
 }
 
+// A migrating lookup (the sharded step's migration mode, kad_route.hip): its state as one record of
+// KadRecWords words -- the lookup id, then the KadStateWords fields -- written and read with 16 B
+// accesses (a lane's record is contiguous; the exchange moves records between ranks as rows).
+template <int A, int C>
+struct KadRecWords {
+    static constexpr int value = (1 + KadStateWords<A, C>::value + 3) / 4 * 4;
+};
+
+// (fields are streamed through 16 B chunks -- a whole record held in registers spilled the step)
+template <int A, int C>
+__device__ __forceinline__ void kad_rec_put(uint32_t* __restrict__ rec, uint32_t qid, const KadLookup<A, C>& L)
+{
+    constexpr int RW = KadRecWords<A, C>::value;
+    uint4* o = reinterpret_cast<uint4*>(rec);
+    uint32_t b[4] = {0u, 0u, 0u, 0u};
+    int i = 0;
+    auto put = [&](uint32_t v) {
+        b[i & 3] = v;
+        if ((i & 3) == 3) o[i >> 2] = make_uint4(b[0], b[1], b[2], b[3]);
+        ++i;
+    };
+    auto put64 = [&](uint64_t v) { put((uint32_t)v); put((uint32_t)(v >> 32)); };
+    put(qid);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) put(L.K.w[k]);
+    put(L.S);
+    put64((uint64_t)__double_as_longlong(L.sx));
+    put64((uint64_t)__double_as_longlong(L.sy));
+    put64((uint64_t)L.now);
+    put64((uint64_t)L.txf);
+    put(L.seq);
+#pragma unroll
+    for (int k = 0; k < C; ++k) put(L.nh.idx[k]);
+#pragma unroll
+    for (int k = 0; k < C; ++k) put64(L.nh.d[k]);
+    put(L.nh.used);
+    put((uint32_t)L.nh.n);
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+        put(L.p[k].node); put(L.p[k].tag); put64((uint64_t)L.p[k].t); put(L.p[k].dins); put(L.p[k].geo);
+        put(L.p[k].boff);
+    }
+    put(L.pvalid);
+    put((uint32_t)L.step);
+    put((uint32_t)L.hops);
+    put((uint32_t)L.pending);
+    put((L.started ? 1u : 0u) | (L.pfinished ? 2u : 0u) | (L.psuccess ? 4u : 0u) | (L.any_to ? 8u : 0u));
+    put(L.result);
+    put(L.nsent);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (i < RW) put(0u);
+}
+
+template <int A, int C>
+__device__ __forceinline__ uint32_t kad_rec_get(KadLookup<A, C>& L, const uint32_t* __restrict__ rec)
+{
+    const uint4* in = reinterpret_cast<const uint4*>(rec);
+    uint4 b = make_uint4(0, 0, 0, 0);
+    int i = 0;
+    auto get = [&]() -> uint32_t {
+        if ((i & 3) == 0) b = in[i >> 2];
+        const int j = i & 3;
+        ++i;
+        return j == 0 ? b.x : j == 1 ? b.y : j == 2 ? b.z : b.w;
+    };
+    auto get64 = [&]() -> uint64_t { const uint64_t lo = get(); return lo | ((uint64_t)get() << 32); };
+    const uint32_t qid = get();
+#pragma unroll
+    for (int k = 0; k < 5; ++k) L.K.w[k] = get();
+    L.S = get();
+    L.sx = __longlong_as_double((long long)get64());
+    L.sy = __longlong_as_double((long long)get64());
+    L.now = (int64_t)get64();
+    L.txf = (int64_t)get64();
+    L.seq = get();
+#pragma unroll
+    for (int k = 0; k < C; ++k) L.nh.idx[k] = get();
+#pragma unroll
+    for (int k = 0; k < C; ++k) L.nh.d[k] = get64();
+    L.nh.used = get();
+    L.nh.n = (int)get();
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+        L.p[k].node = get(); L.p[k].tag = get(); L.p[k].t = (int64_t)get64(); L.p[k].dins = get(); L.p[k].geo = get();
+        L.p[k].boff = get();
+    }
+    L.pvalid = get();
+    L.step = (int)get();
+    L.hops = (int)get();
+    L.pending = (int)get();
+    const uint32_t f = get();
+    L.started = f & 1u; L.pfinished = f & 2u; L.psuccess = f & 4u; L.any_to = f & 8u;
+    L.result = get();
+    L.nsent = get();
+    return qid;
+}
+
 template <int A, int C>
 __device__ __forceinline__ void kad_lookup_init(KadLookup<A, C>& L, const K160& K, uint32_t S,
                                                 const double2* __restrict__ xy)
@@ -929,7 +1028,7 @@ __device__ __forceinline__ void kad_send(KadLookup<A, C>& L, const KadView& V, c
             L.p[i].dins = (uint32_t)(isTo ? DC.rpcTimeout : d2);
             L.p[i].tag = tag;
             L.p[i].geo = pack_geo(rg, sb);
-            L.p[i].boff = rg.boff;
+            L.p[i].boff = on.boff(x, rr, rg, sb);    // the row findNode will read (OnSend::boff)
         }
     }
     L.pvalid |= 1u << slot;
@@ -1006,7 +1105,8 @@ struct KadEv {
 };
 
 // IterativeLookup::start / handleRpcResponse / handleRpcTimeout up to the findNode
-// (kad_lookup_event's first half).  ready(slot, node): the result of a response event is available.
+// (kad_lookup_event's first half).  ready(slot, node, row offset): the result of a response event is
+// available (on KEV_WAIT, ev.r names the responder it waits for).
 template <int A, bool EX, bool LK, class Ready, class Rec, int C>
 __device__ __forceinline__ int kad_event_begin(KadLookup<A, C>& L, const KadView& V, const DelayConsts& DC,
                                                const KadLC& LC, const Ready& ready, const Rec& record, KadEv& ev)
@@ -1053,7 +1153,7 @@ __device__ __forceinline__ int kad_event_begin(KadLookup<A, C>& L, const KadView
                 pre = (int)((uint64_t)L.p[i].t >> 56);
             }
         ev.pre = pre;
-        if (!(tag & 0x80000000u) && !ready(e, r)) return KEV_WAIT;
+        if (!(tag & 0x80000000u) && !ready(e, r, boff)) { ev.r = r; return KEV_WAIT; }
         ev.r = r;
         ev.e = e;
         L.pvalid &= ~(1u << e);
@@ -1353,6 +1453,7 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
     V.xy = xy; V.n = n; V.k = t.k; V.bpb = t.bpb; V.S5 = 5 * t.s;
     V.sbn = (V.S5 + 1 + KBLK - 1) / KBLK;     // c itself + its siblings
     V.lo = t.lo; V.hi = t.hi;
+    V.tl = t.tl; V.tend = (uint32_t)t.tend;
     V.maybe_short = t.maybe_short;
     V.snapshot = t.snapshot;
     return V;
@@ -1399,6 +1500,12 @@ inline void kad_lc_sizes(KadLC& LC, const DelayConsts& DC, uint32_t n)
 }
 
 struct KadShardStepArgs;   // kad_shard.hpp
+struct KadMigStepArgs;
+
+// the migration-step instantiation of K2 for one (alpha, exact) pair (kad_route.hip)
+template <int A, bool EX>
+hipError_t kad_mig_step_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const KadMigStepArgs& a,
+                               int num_cu, hipStream_t st);
 
 // the shard-step instantiation of K2 for one (alpha, exact) pair (kad_route.hip)
 template <int A, bool EX>

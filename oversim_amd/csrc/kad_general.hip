@@ -21,10 +21,11 @@ namespace {
 
 struct GSendNothing {
     __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
+    __device__ __forceinline__ uint32_t boff(uint32_t, const KadNode&, const RespGeo& g, bool) const { return g.boff; }
 };
 
 struct GAlwaysReady {
-    __device__ __forceinline__ bool operator()(int, uint32_t) const { return true; }
+    __device__ __forceinline__ bool operator()(int, uint32_t, uint32_t) const { return true; }
 };
 
 template <bool RECORD>

@@ -31,6 +31,11 @@
 // minimum waves per SIMD the register allocator must allow (profiles/r02_b_kad: 3 beat 2 and 4)
 #define OVS_KAD_WAVES 3
 #endif
+#ifndef OVS_KAD_MIG2
+// the migration step (SM = 2) runs at 2 waves/SIMD: at 3 its record load / store spilled 34 VGPRs
+// (186 VGPRs at 2, no spill); -DOVS_KAD_MIG2=-1 builds it at OVS_KAD_WAVES (A/B)
+#define OVS_KAD_MIG2 2
+#endif
 
 namespace ovs {
 
@@ -38,10 +43,11 @@ namespace {
 
 struct SendNothing {
     __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
+    __device__ __forceinline__ uint32_t boff(uint32_t, const KadNode&, const RespGeo& g, bool) const { return g.boff; }
 };
 
 struct AlwaysReady {
-    __device__ __forceinline__ bool operator()(int, uint32_t) const { return true; }
+    __device__ __forceinline__ bool operator()(int, uint32_t, uint32_t) const { return true; }
 };
 
 template <bool RECORD>
@@ -61,9 +67,40 @@ struct RemoteReady {
     const KadResN<C>* __restrict__ res;
     uint64_t base;
     uint32_t lo, hi;
-    __device__ __forceinline__ bool operator()(int slot, uint32_t r) const
+    __device__ __forceinline__ bool operator()(int slot, uint32_t r, uint32_t) const
     {
         return (r >= lo && r < hi) || res[base + slot].ready != 0;
+    }
+};
+
+// migration step: a response is processed here when its responder is on this arc or its findNode
+// reads the responder's replicated top bucket (a row offset below tend, MigSend)
+struct MigReady {
+    uint32_t lo, hi, tend;
+    __device__ __forceinline__ bool operator()(int, uint32_t r, uint32_t boff) const
+    {
+        return (r >= lo && r < hi) || boff < tend;
+    }
+};
+
+// migration step: at send time the target's line says whether its findNode can be answered on any
+// rank -- the [self] answer of a sibling (snapshot tables, numSiblings 1) or of an empty sibling
+// table, or the full main bucket m above its sibling zone among the replicated top buckets
+// (KMETA_TOPFULL): then the call's row offset names the replicated row (x * tl * bpb; the [self]
+// answers read none), else the owner's row (valid on the owner, where the lookup then moves)
+struct MigSend {
+    int tl, bpb;
+    bool full_ok;      // lookupRedundantNodes <= k: a full main bucket alone is the answer
+    __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
+    __device__ __forceinline__ uint32_t boff(uint32_t x, const KadNode& rr, const RespGeo& g, bool sb) const
+    {
+        if (tl > 0) {
+            if (sb || g.nsib == 0) return 0u;
+            const int j = KEYBITS - 1 - g.m;
+            if (full_ok && g.m > g.endIndex && j < tl && ((rr.meta >> (KMETA_TOPFULL_SHIFT + j)) & 1u))
+                return x * (uint32_t)(tl * bpb);
+        }
+        return g.boff;
     }
 };
 
@@ -81,6 +118,7 @@ struct ShardSend {
     ovs_kad_req* __restrict__ stage;
     uint8_t* __restrict__ rtag;
     uint32_t pad;   // LookupCall: bit 31 | numSiblings (the responder's findNode argument); 0 for KBR routes
+    __device__ __forceinline__ uint32_t boff(uint32_t, const KadNode&, const RespGeo& g, bool) const { return g.boff; }
     __device__ __forceinline__ void operator()(int slot, uint32_t x, bool isTo) const
     {
         if (isTo || (x >= lo && x < hi)) return;   // a timeout carries no result; a local findNode runs here
@@ -120,17 +158,32 @@ struct KadRouteIO {
     uint8_t* __restrict__ rtag;
     ovs_done_rec* __restrict__ dstage;
     uint8_t* __restrict__ ltag;
+    // migration step (SM = 2): this round's input -- migrated lookup records (min, nq of them) or,
+    // in a batch's first round, keys and sources (qkeys / qsrc, lookup q has id fqid + q); per input
+    // one outcome at its own index: a record moving to rank mtag[q] (mstage) or a done record
+    // (dstage, mtag[q] = nsh)
+    const uint32_t* __restrict__ min;
+    uint32_t fqid;
+    uint32_t* __restrict__ mstage;
+    uint8_t* __restrict__ mtag;
+    int me;
+    int tl, bpb, full_ok;
 };
 
 // SH: explicit tables with short sibling tables (KadTables::maybe_short): a send may have to count
 // the responder's scan (kad_response_size); snapshot tables never do
-template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C, bool SH>
+// SM: 0 single GPU; 1 shard step, request/response (lookups stay home, remote findNodes answered by
+// their owners); 2 shard step, migration (a lookup moves to the rank whose rows its next findNode
+// needs; the replicated top buckets answer the long first hops anywhere)
+template <int A, bool RECORD, bool EX, bool LK, int SM, int C, bool SH>
 // the shard step's exact-compare and LookupCall instantiations run at 2 waves/SIMD: their HBM state
 // traffic and request staging need the registers (at 3 the exact-compare ones spilled in misaligned
 // 96-bit pieces gfx950 rejects, the LookupCall one 109 VGPRs); the one-way route step keeps K2's 3
-__global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
+__global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_MIG2) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
                                                                             KadRouteIO io)
 {
+    constexpr bool SHARD = SM == 1;
+    constexpr bool MIG = SM == 2;
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     uint64_t nq = io.nq, chunk = io.chunk;
@@ -153,7 +206,9 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
 #endif
     bool active = false;
     bool dead = false;     // shard step: a listed lookup that does not run (source off the arc)
+    bool go = false;       // migration step: a fresh lookup whose source lies off this arc moves at once
     uint64_t q = 0;
+    uint32_t qid = 0;
     KadLookup<A, C> L;
 
     while (true) {
@@ -162,7 +217,17 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
             const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
             if (!active && mine < end) {
                 active = true;
-                if (SHARD) {
+                if (MIG) {
+                    q = mine;
+                    if (io.min) {
+                        qid = kad_rec_get(L, io.min + q * (uint64_t)KadRecWords<A, C>::value);
+                    } else {
+                        qid = io.fqid + (uint32_t)q;
+                        kad_lookup_init(L, io.qkeys[q], io.qsrc[q], V.xy);
+                        // the start is the source's own findNode: its rows are on its owner
+                        go = L.S < V.lo || L.S >= V.hi;
+                    }
+                } else if (SHARD) {
                     q = io.list[mine];
                     const uint8_t a = io.act[q];
                     dead = a == 0;
@@ -188,7 +253,7 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
         KadEv ev;
         ev.r = 0; ev.geo = 0; ev.boff = 0; ev.e = 0; ev.num = 0; ev.numR = 0; ev.pre = 0; ev.start = false;
         bool coop = false;
-        if (active && !dead && !kad_lookup_done(L)) {
+        if (active && !dead && !go && !kad_lookup_done(L)) {
             const HopRecorder<RECORD> rec{io.hopseq, q * (uint64_t)LC.hopCountMax, LC.hopCountMax};
             // An event that only accounts (a response of an older step, a timeout with calls still
             // pending) leaves the lane idle through the findNode, merge and send phases: the lane
@@ -200,6 +265,8 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
                 if (SHARD) {
                     const RemoteReady<C> rd{static_cast<const KadResN<C>*>(io.res), q * A, V.lo, V.hi};
                     ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, rd, rec, ev);
+                } else if (MIG) {
+                    ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, MigReady{V.lo, V.hi, V.tend}, rec, ev);
                 } else {
                     ph = kad_event_begin<A, EX, LK>(L, V, DC, LC, AlwaysReady{}, rec, ev);
                 }
@@ -207,7 +274,7 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
                 if (ph != KEV_HANDLED || kad_lookup_done(L)) break;
             }
 #endif
-            const bool local = !SHARD || (ev.r >= V.lo && ev.r < V.hi);
+            const bool local = !SM || (ev.r >= V.lo && ev.r < V.hi);
             coop = ph == KEV_FIND && local && kad_find_is_coop(V, ev.r, ev.rg(), ev.sb(), ns, rb_pre(ev.pre), rb_r0(ev.pre));
         }
 
@@ -246,6 +313,14 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
         if (SHARD && dead) {
             active = false;
             dead = false;
+        } else if (MIG && active && go) {
+            // a fresh lookup whose source lies off this arc: to the source's owner before it starts
+            kad_rec_put(io.mstage + q * (uint64_t)KadRecWords<A, C>::value, qid, L);
+            int r = 0;
+            for (int i = 1; i < io.nsh; ++i) r += ((uint64_t)L.S >= io.shard_lo[i]) ? 1 : 0;
+            io.mtag[q] = (uint8_t)r;
+            active = false;
+            go = false;
         } else if (active) {
             SVec<C> res;
             res.n = 0;
@@ -312,6 +387,8 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
                     const ShardSend<C> on{static_cast<KadResN<C>*>(io.res), q * A, &L.K, io.shard_lo, io.nsh, V.lo,
                                           V.hi, io.rstage, io.rtag, LK ? (0x80000000u | (uint32_t)ns) : 0u};
                     kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, on);
+                } else if (MIG) {
+                    kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, MigSend{io.tl, io.bpb, io.full_ok != 0});
                 } else {
                     kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, SendNothing{});
                 }
@@ -331,7 +408,14 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
                             if (j < ns) row[j] = (ok && j < res.n) ? res.idx[j] : NONE;
                     }
                 }
-                if (SHARD) {
+                if (MIG) {
+                    ovs_done_rec dr;
+                    dr.qid = qid;
+                    dr.pad = L.nsent;
+                    dr.out = o;
+                    io.dstage[q] = dr;
+                    io.mtag[q] = (uint8_t)io.nsh;
+                } else if (SHARD) {
                     ovs_done_rec dr;
                     dr.qid = io.qids[q];
                     dr.pad = L.nsent;     // the lookup's FindNodeCalls (local and remote)
@@ -355,6 +439,14 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
                     if (io.rpcs_out) io.rpcs_out[q] = L.nsent;
                 }
                 active = false;
+            } else if (MIG && ph == KEV_WAIT) {
+                // the earliest event needs the rows of a responder off this arc: the lookup moves to
+                // that responder's owner (its record staged at its input index, compacted by rank)
+                kad_rec_put(io.mstage + q * (uint64_t)KadRecWords<A, C>::value, qid, L);
+                int r = 0;
+                for (int i = 1; i < io.nsh; ++i) r += ((uint64_t)ev.r >= io.shard_lo[i]) ? 1 : 0;
+                io.mtag[q] = (uint8_t)r;
+                active = false;
             } else if (SHARD && ph == KEV_WAIT) {
                 // the earliest event waits for an owner's answer: suspended until the next round
 #if !defined(OVS_SHARD_NOSUSPEND) && !defined(OVS_SHARD_NOSTORE)
@@ -371,7 +463,7 @@ __global__ __launch_bounds__(256, ((SHARD && (EX || LK)) || C > 8) ? 2 : OVS_KAD
 }  // namespace
 
 // persistent grid: as many waves as are resident, each with a contiguous slice of the batch
-template <int A, bool RECORD, bool EX, bool LK, bool SHARD, int C = 8, bool SH = true>
+template <int A, bool RECORD, bool EX, bool LK, int SM, int C = 8, bool SH = true>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, KadRouteIO io, int num_cu,
                              hipStream_t st)
 {
@@ -379,7 +471,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     // initialised once, thread-safely)
     static const int bpc = [] {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SHARD, C, SH>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SM, C, SH>, 256, 0) !=
                 hipSuccess ||
             b < 1)
             b = 1;
@@ -389,7 +481,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
 #define OVS_KAD_OVERSUB 1
 #endif
     // OVS_KAD_OVERSUB > 1 (A/B builds): that many waves per resident slot, each with a shorter slice
-    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4 * (SHARD ? 1 : OVS_KAD_OVERSUB);
+    const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc * 4 * (SM ? 1 : OVS_KAD_OVERSUB);
     io.chunk = (io.nq + waves - 1) / waves;
     if (io.chunk < 1) io.chunk = 1;
     const uint64_t need_waves = (io.nq + io.chunk - 1) / io.chunk;
@@ -398,7 +490,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kad_stats), z, sizeof z, 0, hipMemcpyHostToDevice, st);
 #endif
-    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SHARD, C, SH>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC,
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SM, C, SH>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC,
                        io);
 #ifdef OVS_KAD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
@@ -419,18 +511,18 @@ hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC
     // LookupCall batches (sibs != nullptr) record no hop sequence.  KademliaLarge (k or
     // lookupRedundantNodes above 8) takes the 16-entry LookupVector / findNode instantiation.
     if (LC.redundant > 8 || LC.maxRedundantLocal > 8) {
-        if (sibs) return kad_launch<A, false, EX, true, false, 16>(V, DC, LC, io, num_cu, st);
-        if (hopseq) return kad_launch<A, true, EX, false, false, 16>(V, DC, LC, io, num_cu, st);
-        return kad_launch<A, false, EX, false, false, 16>(V, DC, LC, io, num_cu, st);
+        if (sibs) return kad_launch<A, false, EX, true, 0, 16>(V, DC, LC, io, num_cu, st);
+        if (hopseq) return kad_launch<A, true, EX, false, 0, 16>(V, DC, LC, io, num_cu, st);
+        return kad_launch<A, false, EX, false, 0, 16>(V, DC, LC, io, num_cu, st);
     }
     if (V.maybe_short) {
-        if (sibs) return kad_launch<A, false, EX, true, false, 8, true>(V, DC, LC, io, num_cu, st);
-        if (hopseq) return kad_launch<A, true, EX, false, false, 8, true>(V, DC, LC, io, num_cu, st);
-        return kad_launch<A, false, EX, false, false, 8, true>(V, DC, LC, io, num_cu, st);
+        if (sibs) return kad_launch<A, false, EX, true, 0, 8, true>(V, DC, LC, io, num_cu, st);
+        if (hopseq) return kad_launch<A, true, EX, false, 0, 8, true>(V, DC, LC, io, num_cu, st);
+        return kad_launch<A, false, EX, false, 0, 8, true>(V, DC, LC, io, num_cu, st);
     }
-    if (sibs) return kad_launch<A, false, EX, true, false, 8, false>(V, DC, LC, io, num_cu, st);
-    if (hopseq) return kad_launch<A, true, EX, false, false, 8, false>(V, DC, LC, io, num_cu, st);
-    return kad_launch<A, false, EX, false, false, 8, false>(V, DC, LC, io, num_cu, st);
+    if (sibs) return kad_launch<A, false, EX, true, 0, 8, false>(V, DC, LC, io, num_cu, st);
+    if (hopseq) return kad_launch<A, true, EX, false, 0, 8, false>(V, DC, LC, io, num_cu, st);
+    return kad_launch<A, false, EX, false, 0, 8, false>(V, DC, LC, io, num_cu, st);
 }
 
 template <int A, bool EX>
@@ -448,13 +540,31 @@ hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const 
     // above 8) takes the 16-entry instantiation, its results travel as ovs_kad_resp16
     if (V.maybe_short) return hipErrorNotSupported;
     if (LC.redundant > 8 || LC.maxRedundantLocal > 8) {
-        if (a.sib_out) return kad_launch<A, false, EX, true, true, 16, false>(V, DC, LC, io, num_cu, st);
-        return kad_launch<A, false, EX, false, true, 16, false>(V, DC, LC, io, num_cu, st);
+        if (a.sib_out) return kad_launch<A, false, EX, true, 1, 16, false>(V, DC, LC, io, num_cu, st);
+        return kad_launch<A, false, EX, false, 1, 16, false>(V, DC, LC, io, num_cu, st);
     }
-    if (a.sib_out) return kad_launch<A, false, EX, true, true, 8, false>(V, DC, LC, io, num_cu, st);
-    return kad_launch<A, false, EX, false, true, 8, false>(V, DC, LC, io, num_cu, st);
+    if (a.sib_out) return kad_launch<A, false, EX, true, 1, 8, false>(V, DC, LC, io, num_cu, st);
+    return kad_launch<A, false, EX, false, 1, 8, false>(V, DC, LC, io, num_cu, st);
 }
 
+template <int A, bool EX>
+hipError_t kad_mig_step_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const KadMigStepArgs& a,
+                               int num_cu, hipStream_t st)
+{
+    if (a.nin == 0) return hipSuccess;
+    KadRouteIO io{};
+    io.nq = a.nin;
+    io.qkeys = a.fkeys; io.qsrc = a.fsrc; io.fqid = a.fqid; io.min = a.in;
+    io.shard_lo = a.shard_lo; io.nsh = a.nsh; io.me = a.me;
+    io.mstage = a.mstage; io.mtag = a.mtag; io.dstage = a.dstage;
+    io.tl = V.tl; io.bpb = V.bpb; io.full_ok = LC.redundant <= V.k ? 1 : 0;
+    // one-way routes on snapshot tables, findNode results of up to 8 nodes (kad_mig_supported)
+    if (V.maybe_short || LC.redundant > 8 || LC.maxRedundantLocal > 8) return hipErrorNotSupported;
+    return kad_launch<A, false, EX, false, 2, 8, false>(V, DC, LC, io, num_cu, st);
+}
+
+template hipError_t kad_mig_step_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
+                                                                    const KadMigStepArgs&, int, hipStream_t);
 template hipError_t kad_route_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
                                                                  const K160*, const uint32_t*, uint64_t, ovs_route_out*,
                                                                  uint32_t*, uint32_t*, uint32_t*, int, hipStream_t);

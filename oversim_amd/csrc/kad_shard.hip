@@ -116,6 +116,19 @@ __global__ void k_kad_shard_deliver(const typename KadWire<C>::type* __restrict_
 inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 template <bool EX>
+hipError_t kad_mig_step_dispatch(int A, const KadView& V, const DelayConsts& DC, const KadLC& LC, const KadMigStepArgs& a,
+                                 int num_cu, hipStream_t s)
+{
+    switch (A) {
+    case 1: return kad_mig_step_launch<1, EX>(V, DC, LC, a, num_cu, s);
+    case 2: return kad_mig_step_launch<2, EX>(V, DC, LC, a, num_cu, s);
+    case 3: return kad_mig_step_launch<3, EX>(V, DC, LC, a, num_cu, s);
+    case 4: return kad_mig_step_launch<4, EX>(V, DC, LC, a, num_cu, s);
+    default: return kad_mig_step_launch<8, EX>(V, DC, LC, a, num_cu, s);
+    }
+}
+
+template <bool EX>
 hipError_t kad_shard_step_dispatch(int A, const KadView& V, const DelayConsts& DC, const KadLC& LC,
                                    const KadShardStepArgs& a, int num_cu, hipStream_t s)
 {
@@ -144,6 +157,68 @@ size_t kad_lookup_state_bytes(int alpha, int cap)
     const int A = kad_pend_slots(alpha);
     return cap > 8 ? 4 * (size_t)(KadStateWords<1, 16>::value + 7 * (A - 1))
                    : 4 * (size_t)(KadStateWords<1, 8>::value + 7 * (A - 1));
+}
+
+uint32_t kad_rec_bytes(int alpha)
+{
+    switch (kad_pend_slots(alpha)) {
+    case 1: return 4u * KadRecWords<1, 8>::value;
+    case 2: return 4u * KadRecWords<2, 8>::value;
+    case 3: return 4u * KadRecWords<3, 8>::value;
+    case 4: return 4u * KadRecWords<4, 8>::value;
+    default: return 4u * KadRecWords<8, 8>::value;
+    }
+}
+
+bool kad_mig_supported(const ovs_params& P, const KadTables& t)
+{
+    return kad_params_supported(P, t) && P.lookupRedundantNodes <= 8 && t.k <= 8 && t.snapshot && !t.maybe_short &&
+           P.numSiblings == 1 && P.routingType == 0;
+}
+
+hipError_t kad_mig_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
+                        const void* in, uint64_t nin, const K160* fkeys, const uint32_t* fsrc, uint32_t fqid,
+                        const uint64_t* shard_lo, int nsh, int me, void* out, uint64_t out_cap,
+                        unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                        unsigned long long* done_count, unsigned long long* bad, int num_cu, StageBuf& stage,
+                        hipStream_t s)
+{
+    if (!kad_mig_supported(P, t)) return hipErrorNotSupported;
+    if (nsh < 1 || nsh + 1 > CMAX) return hipErrorInvalidValue;
+    if (nin == 0) return hipSuccess;
+    const uint32_t RB = kad_rec_bytes(P.lookupParallelRpcs);
+    // stage: a record and a done record per input, and its outcome tag
+    const size_t om = 0, od = om + (size_t)RB * nin, ot = od + sizeof(ovs_done_rec) * nin;
+    hipError_t e = stage_ensure(stage, ot + nin, s);
+    if (e != hipSuccess) return e;
+    uint8_t* sb = static_cast<uint8_t*>(stage.buf);
+    KadView V = kad_make_view(t, xy, n);
+    V.err = bad;
+    KadLC LC = kad_make_lc(P, t);
+    DelayConsts DL = DC;
+    DL.lookupCall = 0;
+    kad_lc_sizes(LC, DL, n);
+    KadMigStepArgs a{};
+    a.in = static_cast<const uint32_t*>(in);
+    a.fkeys = fkeys; a.fsrc = fsrc; a.fqid = fqid; a.nin = nin;
+    a.shard_lo = shard_lo; a.nsh = nsh; a.me = me;
+    a.mstage = reinterpret_cast<uint32_t*>(sb + om);
+    a.dstage = reinterpret_cast<ovs_done_rec*>(sb + od);
+    a.mtag = sb + ot;
+    if ((e = hipMemsetAsync(a.mtag, 0xFF, nin, s)) != hipSuccess) return e;
+    const int A = kad_pend_slots(LC.alpha);
+    e = t.exact ? kad_mig_step_dispatch<true>(A, V, DL, LC, a, num_cu, s)
+                : kad_mig_step_dispatch<false>(A, V, DL, LC, a, num_cu, s);
+    if (e != hipSuccess) return e;
+    CPlan Pl{};
+    Pl.seg.src = sb + om; Pl.seg.src_stride = Pl.seg.rec_bytes = RB;
+    Pl.seg.dst = static_cast<uint8_t*>(out); Pl.seg.dst_stride = (uint64_t)RB * out_cap;
+    Pl.seg.cap = out_cap; Pl.seg.counter = out_count; Pl.seg.n = nsh; Pl.seg.chain = 0;
+    Pl.nextra = 1;
+    CClass& d = Pl.extra[0];
+    d.src = sb + od; d.src_stride = d.rec_bytes = sizeof(ovs_done_rec);
+    d.dst = reinterpret_cast<uint8_t*>(done); d.cap = done_cap; d.counter = done_count;
+    return compact_by_tag(a.mtag, nin, Pl, stage.cs, s);
 }
 
 hipError_t kad_shard_init(const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base, K160* qkeys,

@@ -46,7 +46,36 @@ struct KadShardStepArgs {
     uint32_t* sib_out;                 // LookupCalls: the sibling rows (nullptr: KBR routes)
 };
 
+// the migration step (k_kad_route<.., SM = 2>): one round over migrated lookup records or a batch's
+// keys; every input gets one outcome at its own index -- a record moving to rank mtag[q] (mstage,
+// KadRecWords words each) or a done record (dstage, mtag[q] = nsh)
+struct KadMigStepArgs {
+    const uint32_t* in;                // nin migrated records, or nullptr: the batch's first round ...
+    const K160* fkeys;                 // ... from its keys and sources (lookup q has id fqid + q)
+    const uint32_t* fsrc;
+    uint32_t fqid;
+    uint64_t nin;
+    const uint64_t* shard_lo;          // device copy of the arc bounds
+    int nsh, me;
+    uint32_t* mstage;
+    uint8_t* mtag;
+    ovs_done_rec* dstage;
+};
+
 size_t kad_lookup_state_bytes(int alpha, int cap);
+// bytes of a migrating lookup record (KadRecWords) for lookupParallelRpcs alpha
+uint32_t kad_rec_bytes(int alpha);
+// does the migration step implement these parameters (one-way KBR routes on snapshot tables, findNode
+// results of up to 8 nodes)
+bool kad_mig_supported(const ovs_params& P, const KadTables& t);
+// one migration round: the outcomes compacted by tag into per-rank segments of out (out + d * out_cap
+// records, counter out_count[d]) and the done buffer (done_count)
+hipError_t kad_mig_step(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
+                        const void* in, uint64_t nin, const K160* fkeys, const uint32_t* fsrc, uint32_t fqid,
+                        const uint64_t* shard_lo, int nsh, int me, void* out, uint64_t out_cap,
+                        unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                        unsigned long long* done_count, unsigned long long* bad, int num_cu, StageBuf& stage,
+                        hipStream_t s);
 bool kad_params_supported_host(const ovs_params& P, const KadTables& t);
 // lookups of this rank: their keys and sources (copied to qkeys / qsrc), act = 2 (not started), qids,
 // the round-1 list (indices 0..n-1) and its count; sources off [lo, hi) are counted in *bad and never run

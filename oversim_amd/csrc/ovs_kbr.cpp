@@ -1225,6 +1225,72 @@ ovs_status ovs_kad_shard_deliver(ovs_ctx* c, const void* in, uint64_t n, void* s
     return OVS_OK;
 }
 
+ovs_status ovs_kad_shard_replicate(ovs_ctx* c, int32_t top_levels)
+{
+    if (!c) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA || !c->kad.snapshot || c->kad.general)
+        return fail(c, OVS_ESTATE, "no Kademlia snapshot network (ovs_kad_load_shard) loaded");
+    if (top_levels < 0 || top_levels > KTOP_MAX) return fail(c, OVS_EINVAL, "top_levels must be 0..7");
+    if (c->kad.tl == top_levels) return OVS_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());      // kernels of earlier rounds may still read the tables
+    const uint32_t lo = c->kad.lo, hi = c->kad.hi;
+    hipError_t e = kad_build(c->recs, c->xy, (uint32_t)c->n, c->P.k, c->P.s, c->P.kadSeed, c->kad, c->stream, lo, hi,
+                             top_levels);
+    if (e != hipSuccess) { free_tables(c); return hip_fail(c, e, "kademlia table rebuild (replicated top buckets)"); }
+    return OVS_OK;
+}
+
+int32_t ovs_kad_shard_levels(const ovs_ctx* c)
+{
+    return c && c->overlay == OVS_OVERLAY_KADEMLIA ? c->kad.tl : 0;
+}
+
+int32_t ovs_kad_shard_rec_bytes(const ovs_ctx* c)
+{
+    if (!c || c->overlay != OVS_OVERLAY_KADEMLIA) return -1;
+    return (int32_t)kad_rec_bytes(c->P.lookupParallelRpcs);
+}
+
+ovs_status ovs_kad_shard_mig_step(ovs_ctx* c, const void* in, uint64_t n_in, const ovs_key160* fkeys, const uint32_t* fsrc,
+                                  uint32_t fqid, void* out, uint64_t out_cap, unsigned long long* out_count,
+                                  ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
+                                  const uint64_t* shard_lo, uint32_t nshards, void* stream)
+{
+    if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
+    if (n_in && ((!in && !(fkeys && fsrc)) || !out || !out_count || !done || !done_count)) return OVS_EINVAL;
+    if (c->overlay != OVS_OVERLAY_KADEMLIA) return fail(c, OVS_ESTATE, "no Kademlia network loaded");
+    ovs_status st = check_common(c, c->P);
+    if (st != OVS_OK) return st;
+    if (!kad_mig_supported(c->P, c->kad))
+        return fail(c, OVS_ENOTSUP, "the migration step implements one-way iterative KBR routes on snapshot tables with "
+                                    "k and lookupRedundantNodes <= 8");
+    uint64_t lo_h[MAXSHARDS + 1];
+    int me = -1;
+    for (uint32_t r = 0; r <= nshards; ++r) {
+        lo_h[r] = shard_lo[r];
+        if (r > 0 && shard_lo[r] < shard_lo[r - 1]) return fail(c, OVS_EINVAL, "shard_lo must be non-decreasing");
+    }
+    if (shard_lo[0] != 0 || shard_lo[nshards] != c->n) return fail(c, OVS_EINVAL, "shard_lo must cover [0, n)");
+    for (uint32_t r = 0; r < nshards; ++r)
+        if (shard_lo[r] == c->kad.lo && shard_lo[r + 1] == c->kad.hi) me = (int)r;
+    if (me < 0) return fail(c, OVS_EINVAL, "this context's arc is not one of shard_lo's arcs");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    ovs_status bst = upload_bounds(c, lo_h, nshards);
+    if (bst != OVS_OK) return bst;
+    if (!c->kbad) {
+        HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
+        HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
+    }
+    if (!in) HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));   // a batch's first round
+    hipError_t e = kad_mig_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), in, n_in,
+                                reinterpret_cast<const K160*>(fkeys), fsrc, fqid, c->d_bounds, (int)nshards, me, out,
+                                out_cap, out_count, done, done_cap, done_count, c->kbad, c->num_cu, c->stage[s], s);
+    if (e != hipSuccess) return hip_fail(c, e, "kademlia migration step");
+    return OVS_OK;
+}
+
 ovs_status ovs_kad_shard_errors(ovs_ctx* c, uint64_t* bad)
 {
     if (!c || !bad) return OVS_EINVAL;

@@ -12,8 +12,10 @@
 //      (0xFF-filled first: a row nobody wrote finishes as a sentinel record the end check counts),
 //      then the cohort's next step is queued behind it on the cohort stream, so one cohort's
 //      exchange overlaps the other cohort's kernel.
-// Kademlia (lookups stay home): step -> count all-gather -> requests all-to-allv -> serve ->
-// responses all-to-allv (reverse splits) -> deliver.
+// Kademlia one-way routes over replicated top buckets take the same loop with migrating lookup
+// records (ovs_kad_shard_mig_step); otherwise (LookupCalls, no replicated buckets) the lookups stay
+// home: step -> count all-gather -> requests all-to-allv -> serve -> responses all-to-allv (reverse
+// splits) -> deliver.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -160,16 +162,18 @@ ovs_status check_totals(ovs_ctx* c, const ovs_exchange* ex, int64_t have, int64_
 }  // namespace
 
 // ===========================================================================
-extern "C" {
 
-ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint64_t* shard_lo, int32_t num_siblings,
-                                 const ovs_key160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
-                                 ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done, uint32_t cohorts,
-                                 ovs_shard_route_stats* stats, void* stream)
+namespace {
+
+// the record loop of a batch whose lookups move between ranks (Chord hand-offs, Kademlia migration):
+// step(k, first, in, nin, b0, out, cap, cnt, stream) runs one round of cohort k -- a batch's first
+// round from keys[b0, b0 + nin) (first = true), else over nin received records -- appending
+// hand-offs to segment d of out and finished lookups to done (the shared counter dcnt)
+template <class Step>
+ovs_status route_records(ovs_ctx* c, const ovs_exchange* ex, uint64_t n, uint32_t RB, const Step& step,
+                         ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done, uint32_t cohorts,
+                         ovs_shard_route_stats* stats, void* stream, const char* what)
 {
-    if (!c || !n_done || (n && (!keys || !src)) || !done) return OVS_EINVAL;
-    ovs_status st = check_exchange(c, ex, shard_lo);
-    if (st != OVS_OK) return st;
     const double t_start = now_ms();
     double xms = 0, kms = 0;
     const uint32_t W = ex->world, me = ex->rank;
@@ -189,14 +193,12 @@ ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint6
     RCHK(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long), s0));
     // every cohort stream starts after the caller's stream (inputs, the counter reset)
     RCHK(hipEventRecord(mk_event(&R->ev, false), s0));
-    const int32_t ns = num_siblings;
     uint64_t nin[4] = {0, 0, 0, 0}, cap[4] = {0, 0, 0, 0};
     bool live[4] = {false, false, false, false};
-    std::vector<int64_t> M((size_t)W * W), mine(W);
+    std::vector<int64_t> M((size_t)W * W);
     std::vector<uint64_t> scl(W), rcl(W), roff(W);
     std::vector<const void*> sendp(W);
     uint64_t sent = 0, sent_bytes = 0;
-    constexpr uint32_t RB = sizeof(ovs_lookup_rec);
     auto issue = [&](int k, bool first, uint64_t b0) -> ovs_status {
         CohortBufs& B = R->coh[k];
         // a segment receives at most the step's input records
@@ -207,22 +209,13 @@ ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint6
         cap[k] = B.out.cap / ((size_t)W * RB);
         RCHK(hipMemsetAsync(B.cnt.p, 0, sizeof(unsigned long long) * W, cs[k]));
         RCHK(hipEventRecord(mk_event(&B.e0, true), cs[k]));
-        auto* out = static_cast<ovs_lookup_rec*>(B.out.p);
-        auto* cnt = static_cast<unsigned long long*>(B.cnt.p);
-        ovs_status s;
-        if (first)
-            s = ovs_shard_step_keys(c, ns, keys + b0, src + b0, nin[k], qid_base + (uint32_t)b0, out, cap[k], cnt, done,
-                                    done_cap, dcnt, shard_lo, W, cs[k]);
-        else if (ns == 0)
-            s = ovs_shard_step(c, static_cast<const ovs_lookup_rec*>(B.recv.p), nin[k], out, cap[k], cnt, done, done_cap,
-                               dcnt, shard_lo, W, cs[k]);
-        else
-            s = ovs_shard_step_lookup(c, ns, static_cast<const ovs_lookup_rec*>(B.recv.p), nin[k], out, cap[k], cnt,
-                                      done, done_cap, dcnt, shard_lo, W, cs[k]);
+        const ovs_status s = step(k, first, first ? nullptr : B.recv.p, nin[k], b0, B.out.p, cap[k],
+                                  static_cast<unsigned long long*>(B.cnt.p), dcnt, cs[k]);
         if (s != OVS_OK) return s;
         RCHK(hipEventRecord(mk_event(&B.e1, true), cs[k]));
         return OVS_OK;
     };
+    ovs_status st;
     for (int k = 0; k < nc; ++k) {
         RCHK(hipStreamWaitEvent(cs[k], R->ev, 0));
         const uint64_t b0 = (uint64_t)k * n / nc, b1 = (uint64_t)(k + 1) * n / nc;
@@ -249,14 +242,14 @@ ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint6
             if (tot == 0) { live[k] = false; continue; }
             any = true;
             uint64_t tin = 0;
-            for (uint32_t s = 0; s < W; ++s) {
-                scl[s] = (uint64_t)M[(size_t)me * W + s];
-                rcl[s] = (uint64_t)M[(size_t)s * W + me];
-                roff[s] = tin;
-                tin += rcl[s];
-                if (s != me) { sent += scl[s]; sent_bytes += scl[s] * RB; }
-                sendp[s] = static_cast<const uint8_t*>(B.out.p) + (size_t)s * cap[k] * RB;
-                if (scl[s] > cap[k]) return ctx_fail(c, OVS_EDEVICE, "shard route: a segment overflowed");
+            for (uint32_t r = 0; r < W; ++r) {
+                scl[r] = (uint64_t)M[(size_t)me * W + r];
+                rcl[r] = (uint64_t)M[(size_t)r * W + me];
+                roff[r] = tin;
+                tin += rcl[r];
+                if (r != me) { sent += scl[r]; sent_bytes += scl[r] * RB; }
+                sendp[r] = static_cast<const uint8_t*>(B.out.p) + (size_t)r * cap[k] * RB;
+                if (scl[r] > cap[k]) return ctx_fail(c, OVS_EDEVICE, "shard route: a segment overflowed");
             }
             if (ensure(B.recv, std::max<size_t>((size_t)tin * RB, RB), cs[k]) != hipSuccess)
                 return ctx_fail(c, OVS_ENOMEM, "shard route: receive buffer");
@@ -269,7 +262,7 @@ ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint6
             if (st != OVS_OK) return st;
         }
         if (!any) break;
-        if (++rounds > 10000) return ctx_fail(c, OVS_EDEVICE, "sharded routing did not terminate");
+        if (++rounds > 10000) return ctx_fail(c, OVS_EDEVICE, std::string(what) + " did not terminate");
     }
     // the caller's stream continues after every cohort
     R->cev.resize(std::max<size_t>(R->cev.size(), (size_t)nc), nullptr);
@@ -285,7 +278,7 @@ ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint6
     RCHK(count_sentinel_records(done, hd, static_cast<unsigned long long*>(R->sentinel.p), s0));
     RCHK(hipMemcpyAsync(&hs, R->sentinel.p, sizeof hs, hipMemcpyDeviceToHost, s0));
     RCHK(hipStreamSynchronize(s0));
-    st = check_totals(c, ex, (int64_t)hd, (int64_t)n, (int64_t)hs, xms, "sharded Chord");
+    st = check_totals(c, ex, (int64_t)hd, (int64_t)n, (int64_t)hs, xms, what);
     if (st != OVS_OK) return st;
     *n_done = hd;
     if (stats) {
@@ -301,6 +294,34 @@ ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint6
     return OVS_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+ovs_status ovs_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint64_t* shard_lo, int32_t num_siblings,
+                                 const ovs_key160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
+                                 ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done, uint32_t cohorts,
+                                 ovs_shard_route_stats* stats, void* stream)
+{
+    if (!c || !n_done || (n && (!keys || !src)) || !done) return OVS_EINVAL;
+    ovs_status st = check_exchange(c, ex, shard_lo);
+    if (st != OVS_OK) return st;
+    const uint32_t W = ex->world;
+    const int32_t ns = num_siblings;
+    auto step = [&](int, bool first, const void* in, uint64_t nin, uint64_t b0, void* out, uint64_t cap,
+                    unsigned long long* cnt, unsigned long long* dcnt, hipStream_t s) -> ovs_status {
+        auto* o = static_cast<ovs_lookup_rec*>(out);
+        if (first)
+            return ovs_shard_step_keys(c, ns, keys + b0, src + b0, nin, qid_base + (uint32_t)b0, o, cap, cnt, done,
+                                       done_cap, dcnt, shard_lo, W, s);
+        const auto* r = static_cast<const ovs_lookup_rec*>(in);
+        if (ns == 0) return ovs_shard_step(c, r, nin, o, cap, cnt, done, done_cap, dcnt, shard_lo, W, s);
+        return ovs_shard_step_lookup(c, ns, r, nin, o, cap, cnt, done, done_cap, dcnt, shard_lo, W, s);
+    };
+    return route_records(c, ex, n, (uint32_t)sizeof(ovs_lookup_rec), step, done, done_cap, n_done, cohorts,
+                         stats, stream, "sharded Chord");
+}
+
 ovs_status ovs_kad_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const uint64_t* shard_lo,
                                      int32_t num_siblings, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                                      uint32_t qid_base, ovs_done_rec* done, uint64_t done_cap, uint64_t* n_done,
@@ -309,6 +330,31 @@ ovs_status ovs_kad_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const u
     if (!c || !n_done || (n && (!keys || !src)) || !done) return OVS_EINVAL;
     ovs_status st = check_exchange(c, ex, shard_lo);
     if (st != OVS_OK) return st;
+    if (num_siblings < -1 && ovs_kad_shard_levels(c) > 0) {
+        // one-way routes over replicated top buckets: the lookups migrate (ovs_kad_shard_mig_step)
+        const int32_t rb = ovs_kad_shard_rec_bytes(c);
+        if (rb <= 0) return ctx_fail(c, OVS_ESTATE, "no Kademlia network loaded");
+        const uint32_t W = ex->world;
+        auto step = [&](int, bool first, const void* in, uint64_t nin, uint64_t b0, void* out, uint64_t cap,
+                        unsigned long long* cnt, unsigned long long* dcnt, hipStream_t s) -> ovs_status {
+            return ovs_kad_shard_mig_step(c, first ? nullptr : in, nin, first ? keys + b0 : nullptr,
+                                          first ? src + b0 : nullptr, qid_base + (uint32_t)b0, out, cap, cnt, done,
+                                          done_cap, dcnt, shard_lo, W, s);
+        };
+        // one cohort: the migration step's records are large and a round's exchange is short
+        st = route_records(c, ex, n, (uint32_t)rb, step, done, done_cap, n_done, 1, stats, stream,
+                           "sharded Kademlia (migration)");
+        if (st != OVS_OK) return st;
+        uint64_t bad = 0;
+        if ((st = ovs_kad_shard_errors(c, &bad)) != OVS_OK) return st;
+        int64_t v[1] = {(int64_t)bad};
+        double xms = 0;
+        XCHK(ex->allreduce_sum_i64(ex->user, v, 1), "allreduce");
+        if (stats) stats->exchange_ms += xms;
+        if (v[0] != 0)
+            return ctx_fail(c, OVS_EDEVICE, std::to_string(v[0]) + " Kademlia shard errors (table reads off an arc)");
+        return OVS_OK;
+    }
     if (done_cap < n) return ctx_fail(c, OVS_EINVAL, "done_cap must hold the batch (Kademlia lookups finish at home)");
     const double t_start = now_ms();
     double xms = 0, kms = 0;

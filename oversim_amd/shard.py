@@ -47,6 +47,16 @@ def arc_bounds(n_total: int, world: int) -> list[int]:
     return [r * n_total // world for r in range(world + 1)]
 
 
+def prefix_bounds(ids: np.ndarray, world: int) -> list[int]:
+    """Arcs cut at key prefixes (the XOR-prefix partition of SURVEY §8e): arc r holds the IDs whose top
+    bits lie in [r * 2^160 / W, (r + 1) * 2^160 / W) -- for W a power of two exactly the IDs sharing
+    their top log2(W) bits.  Bounds as indices into the sorted ID array."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint32).reshape(-1, 5)
+    top = (ids[:, 4].astype(np.uint64) << np.uint64(32)) | ids[:, 3].astype(np.uint64)   # the top 64 bits
+    cuts = [int(np.searchsorted(top, np.uint64((r << 64) // world), side="left")) for r in range(1, world)]
+    return [0] + cuts + [len(ids)]
+
+
 def default_top_levels(world: int) -> int:
     """Replicated top finger levels for W arcs: the log2(W) levels whose jumps span arcs, plus 3 more
     levels after which a lookup is within 2^(157 - log2 W) of its key, so it crosses to another arc
@@ -251,6 +261,10 @@ for _name, _args in {
     "ovs_kad_shard_deliver": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p],
     "ovs_kad_shard_errors": [C.c_void_p, C.c_void_p],
     "ovs_kad_shard_resp_bytes": [C.c_void_p],
+    "ovs_kad_shard_replicate": [C.c_void_p, C.c_int32],
+    "ovs_kad_shard_mig_step": [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                               C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
+                               C.c_void_p],
     "ovs_rccl_unique_id": [C.c_void_p],
     "ovs_exchange_rccl_create": [C.c_int, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p],
     "ovs_exchange_local_create": [C.c_uint32, C.c_void_p],
@@ -268,6 +282,10 @@ lib().ovs_exchange_last_error.argtypes = []
 lib().ovs_exchange_last_error.restype = C.c_char_p
 lib().ovs_chord_shard_levels.argtypes = [C.c_void_p]
 lib().ovs_chord_shard_levels.restype = C.c_int32
+lib().ovs_kad_shard_levels.argtypes = [C.c_void_p]
+lib().ovs_kad_shard_levels.restype = C.c_int32
+lib().ovs_kad_shard_rec_bytes.argtypes = [C.c_void_p]
+lib().ovs_kad_shard_rec_bytes.restype = C.c_int32
 
 
 # ---------------------------------------------------------------------------
@@ -370,7 +388,10 @@ class CallbackExchange:
             f(*a)
             return 0
         except Exception as e:       # a Python exception must not unwind through C frames
+            import sys
+            import traceback
             self.error = e
+            traceback.print_exc(file=sys.stderr)
             return 1
 
     def _allgather(self, user, send, n, recv):
@@ -445,7 +466,11 @@ def native_kad_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, num_si
     n = int(keys_t.shape[0])
     bounds = (C.c_uint64 * (stepper.world + 1))(*stepper.bounds)
     stepper.n = n
-    stepper.done = torch.empty((max(n, 1), DONE_BYTES), dtype=torch.uint8, device=stepper.dev)
+    # migrating lookups (replicated top buckets, one-way routes) finish on any rank: room for all of
+    # them (every rank's batch is the same size here, as in bench.py and the tests)
+    rows = n * stepper.world if (num_siblings < -1 and getattr(stepper, "top_levels", 0)) else n
+    if getattr(stepper, "done", None) is None or stepper.done.shape[0] < max(rows, 1):
+        stepper.done = torch.empty((max(rows, 1), DONE_BYTES), dtype=torch.uint8, device=stepper.dev)
     sib = None
     if num_siblings >= -1:
         ns = num_siblings if num_siblings >= 0 else stepper.params.s
@@ -459,6 +484,8 @@ def native_kad_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, num_si
                                          C.c_void_p(keys_t.data_ptr()), C.c_void_p(src_t.data_ptr()), n, qid_base,
                                          C.c_void_p(stepper.done.data_ptr()), stepper.done.shape[0], C.byref(nd), sib,
                                          C.byref(stats), C.c_void_p(s))
+    if st != 0 and isinstance(getattr(ex, "_owner", None), CallbackExchange) and ex._owner.error:
+        raise RuntimeError(f"exchange callback failed: {ex._owner.error!r}")
     stepper.eng._chk(st, "ovs_kad_shard_route_batch")
     return stepper.done[:nd.value], stats
 
@@ -690,7 +717,8 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
         if moved == 0:
             break
         dev = steppers[0].dev
-        inbox = [torch.cat(b) if b else torch.empty((0, REC_BYTES), dtype=torch.uint8, device=dev) for b in buckets]
+        rb = getattr(steppers[0], "rec_bytes", REC_BYTES)
+        inbox = [torch.cat(b) if b else torch.empty((0, rb), dtype=torch.uint8, device=dev) for b in buckets]
         if rounds > max_rounds:
             raise RuntimeError("sharded routing did not terminate")
     return [s.finished() for s in steppers], rounds
@@ -711,9 +739,11 @@ class KadShardStepper:
     """One rank's arc of a Kademlia network on one device (ovs_kad_load_shard + shard kernels)."""
 
     def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device,
-                 params: Params | None = None, lookup_siblings: int | None = None):
+                 params: Params | None = None, lookup_siblings: int | None = None, top_levels: int = 0):
         """lookup_siblings: run KBRTestApp LookupCalls with that many siblings (-1 = s, 0 = exact-key
-        lookup; ovs_kad_shard_begin_lookup) instead of one-way routes; results via lookup_results()."""
+        lookup; ovs_kad_shard_begin_lookup) instead of one-way routes; results via lookup_results().
+        top_levels: replicate the top buckets of every node (ovs_kad_shard_replicate) -- one-way
+        routes through the native loop then migrate (KadMigStepper is the Python stepper of that mode)."""
         import torch
         self.torch, self.dev = torch, device
         self.rank, self.bounds, self.world = rank, [int(b) for b in bounds], len(bounds) - 1
@@ -726,6 +756,9 @@ class KadShardStepper:
         st = lib().ovs_kad_load_shard(self.eng._h, ids.ctypes.data_as(C.c_void_p), len(ids),
                                       xy.ctypes.data_as(C.c_void_p), self.bounds[rank], self.bounds[rank + 1], 0)
         self.eng._chk(st, "ovs_kad_load_shard")
+        self.top_levels = int(top_levels)
+        if self.top_levels:
+            self.eng._chk(lib().ovs_kad_shard_replicate(self.eng._h, self.top_levels), "ovs_kad_shard_replicate")
         self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
         # counts[0..world): requests per owner rank, counts[world]: lookups still active, counts[world+1]: done
         self.counts = torch.zeros(self.world + 2, dtype=torch.int64, device=device)
@@ -829,6 +862,82 @@ class KadShardStepper:
         lo = done[:, 8:24].contiguous().cpu().numpy().reshape(-1).view(LOOKUP_OUT_DTYPE)
         sib = self.sib.cpu().numpy().view(np.uint32)[qid - np.uint32(self.qid_base)]
         return qid, lo, sib
+
+
+class KadMigStepper:
+    """One rank's arc of a Kademlia network whose one-way lookups MIGRATE (ovs_kad_shard_mig_step): the
+    stepper interface of GpuShardStepper (first_batch / step / finished), so route_local_shards and
+    route_sharded drive it; records are ovs_kad_shard_rec_bytes bytes."""
+
+    def __init__(self, ids: np.ndarray, xy: np.ndarray, bounds: list[int], rank: int, device,
+                 params: Params | None = None, top_levels: int = 3, capacity: int = 1 << 16):
+        import torch
+        self.torch, self.dev = torch, device
+        self.rank, self.bounds, self.world = rank, [int(b) for b in bounds], len(bounds) - 1
+        self.eng = KbrEngine(device.index if device.index is not None else 0)
+        self.params = params or Params.kademlia()
+        self.eng.set_params(self.params)
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        xy = np.ascontiguousarray(xy, dtype=np.float64)
+        st = lib().ovs_kad_load_shard(self.eng._h, ids.ctypes.data_as(C.c_void_p), len(ids),
+                                      xy.ctypes.data_as(C.c_void_p), self.bounds[rank], self.bounds[rank + 1], 0)
+        self.eng._chk(st, "ovs_kad_load_shard")
+        self.top_levels = int(top_levels)
+        self.eng._chk(lib().ovs_kad_shard_replicate(self.eng._h, self.top_levels), "ovs_kad_shard_replicate")
+        self.rec_bytes = int(lib().ovs_kad_shard_rec_bytes(self.eng._h))
+        self._lo = (C.c_uint64 * (self.world + 1))(*self.bounds)
+        self._cap = 0
+        self.cnt = torch.zeros(self.world, dtype=torch.int64, device=device)
+        self.done_count = torch.zeros(1, dtype=torch.int64, device=device)
+        self.done = torch.empty((max(capacity, 1), DONE_BYTES), dtype=torch.uint8, device=device)
+        self.done_cap = max(capacity, 1)
+        self.timing = False
+        self.kernel_ms = 0.0
+
+    def reset(self, capacity: int):
+        self.done_count.zero_()
+        if capacity > self.done_cap:
+            self.done = self.torch.empty((capacity, DONE_BYTES), dtype=self.torch.uint8, device=self.dev)
+            self.done_cap = capacity
+
+    def first_batch(self, keys_t, src_t, qid_base: int):
+        return FreshBatch(keys_t, src_t, qid_base)
+
+    def _s(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def step(self, inbox):
+        torch = self.torch
+        n_in = inbox.shape[0]
+        if n_in > self._cap:
+            self._cap = n_in
+            self.out = torch.empty((self.world, max(n_in, 1), self.rec_bytes), dtype=torch.uint8, device=self.dev)
+        self.cnt.zero_()
+        p = lambda t: C.c_void_p(t.data_ptr())
+        if isinstance(inbox, FreshBatch):
+            st = lib().ovs_kad_shard_mig_step(self.eng._h, None, n_in, p(inbox.keys), p(inbox.src), inbox.qid_base,
+                                              p(self.out), self._cap, p(self.cnt), p(self.done), self.done_cap,
+                                              p(self.done_count), self._lo, self.world, self._s())
+        else:
+            st = lib().ovs_kad_shard_mig_step(self.eng._h, p(inbox), n_in, None, None, 0, p(self.out), self._cap,
+                                              p(self.cnt), p(self.done), self.done_cap, p(self.done_count), self._lo,
+                                              self.world, self._s())
+        self.eng._chk(st, "ovs_kad_shard_mig_step")
+        return self.out, self.cnt
+
+    def errors(self) -> int:
+        bad = C.c_uint64(0)
+        self.eng._chk(lib().ovs_kad_shard_errors(self.eng._h, C.byref(bad)), "ovs_kad_shard_errors")
+        return int(bad.value)
+
+    def finished(self):
+        k = int(self.done_count.item())
+        if k > self.done_cap:
+            raise RuntimeError("done buffer overflow")
+        bad = self.errors()
+        if bad:
+            raise RuntimeError(f"{bad} Kademlia shard errors (table reads off the arc)")
+        return self.done[:k]
 
 
 def route_kad_sharded(stepper, exchange, keys_t, src_t, qid_base: int, max_rounds: int = 5_000):

@@ -757,7 +757,8 @@ def _native_inputs(net, bounds, world, m, seed, node_ids=lambda r: r % 2 == 0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,world,top", [("chord", 3, None), ("chord", 4, 0), ("chord", 2, 8), ("kademlia", 3, None)])
+@pytest.mark.parametrize("kind,world,top", [("chord", 3, None), ("chord", 4, 0), ("chord", 2, 8), ("kademlia", 3, 0),
+                                            ("kademlia", 3, 3), ("kademlia", 8, 2)])
 def test_native_round_loop_threads(kind, world, top):
     """ovs_shard_route_batch / ovs_kad_shard_route_batch with W ranks as threads of this process (one
     context per arc on one GPU, ovs_exchange_local_create): equal to the single-context route."""
@@ -776,7 +777,9 @@ def test_native_round_loop_threads(kind, world, top):
             st.reset(world * m)
     else:
         params = Params.kademlia().replace(lookupParallelRpcs=3)
-        steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params) for r in range(world)]
+        # top > 0: replicated top buckets, the lookups migrate (ovs_kad_shard_mig_step rounds)
+        steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params, top_levels=top or 0)
+                    for r in range(world)]
     exs = local_exchanges(world)
     res, errs = [None] * world, []
 
@@ -848,6 +851,15 @@ def test_native_round_loop_rccl_world1(kind):
 
 
 def _native_gloo_worker(rank, world, port, q, kind):
+    import traceback
+    try:
+        _native_gloo_body(rank, world, port, q, kind)
+    except BaseException:       # noqa: BLE001 -- reported to the parent, which stops the other rank
+        q.put(("error", rank, traceback.format_exc()))
+        raise
+
+
+def _native_gloo_body(rank, world, port, q, kind):
     import torch.distributed as dist
     from oversim_amd import Params
     from oversim_amd.shard import (CallbackExchange, GpuShardStepper, KadShardStepper, arc_bounds, done_to_numpy,
@@ -888,7 +900,18 @@ def test_native_round_loop_gloo_two_processes(kind):
     procs = [ctx.Process(target=_native_gloo_worker, args=(r, world, port, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda x: x[0])
+    res = []
+    try:
+        for _ in range(world):
+            x = q.get(timeout=150)
+            if x[0] == "error":
+                pytest.fail(f"rank {x[1]} failed:\n{x[2]}")
+            res.append(x)
+    finally:
+        if len(res) < world:
+            for p in procs:       # the surviving rank waits in a collective: stop our own children
+                p.kill()
+    res.sort(key=lambda x: x[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -899,5 +922,61 @@ def test_native_round_loop_gloo_two_processes(kind):
     net = W.population(1 << 14, 0x5E)
     keys, src = np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res])
     ref = _single_gpu_reference(net, keys, src) if kind == "chord" else _kad_reference(net, keys, src, Params.kademlia())
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+
+
+# ------------------------------------------------- Kademlia lookups that migrate (ABI 11)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,alpha,n,top", [(2, 3, 1 << 16, 3), (8, 3, 1 << 16, 3), (3, 1, 15000, 2), (4, 8, 1 << 16, 4),
+                                               (3, 3, 15000, 0), (8, 2, 3000, 7), (5, 3, 1 << 16, 1)])
+def test_kad_migration_emulated_on_one_gpu(world, alpha, n, top):
+    """Kademlia one-way lookups that move between arcs (ovs_kad_shard_mig_step; W contexts on one GPU,
+    the in-process exchange): the top `top` buckets of every node replicated, a lookup moved as one
+    record to the owner of the rows its next findNode needs.  Every lookup -- responsible node, hops,
+    status, latency and its FindNodeCall count -- equals the single-context K2's, including networks
+    whose top buckets are not full (3000 nodes, 7 levels) and no replication at all (top 0)."""
+    from oversim_amd import Params
+    from oversim_amd.shard import KadMigStepper, arc_bounds, done_to_numpy, route_local_shards
+    m = 4000
+    net = W.population(n, 0x7A + world + alpha)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=alpha)
+    steppers = [KadMigStepper(net.ids, net.xy, bounds, r, dev, params=params, top_levels=top, capacity=world * m)
+                for r in range(world)]
+    ks, ss, allk, alls = _native_inputs(net, bounds, world, m, 0x7B, node_ids=lambda r: r % 2 == 1)
+    dones, rounds = route_local_shards(steppers, ks, ss, [r * m for r in range(world)])
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    assert np.array_equal(d["qid"], np.arange(world * m))
+    ref = _kad_reference(net, allk, alls, params)
+    for f in ROUTE_FIELDS:
+        assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
+    assert np.array_equal(d["pad"].astype(np.int64), ref["rpcs"].astype(np.int64))
+    assert rounds >= 2
+
+
+@pytest.mark.gpu
+def test_kad_migration_moves_once_on_prefix_arcs():
+    """On arcs cut at key prefixes (W = 8: the top three ID bits) with 3 replicated levels, every
+    findNode a lookup needs is either answerable from the replicated top buckets or on its key's arc:
+    a lookup moves at most once, so every round after the second is empty."""
+    from oversim_amd import Params
+    from oversim_amd.shard import KadMigStepper, done_to_numpy, route_local_shards, prefix_bounds
+    world, n, m = 8, 1 << 16, 4000
+    net = W.population(n, 0x7C)
+    bounds = prefix_bounds(net.ids, world)
+    dev = torch.device("cuda", 0)
+    params = Params.kademlia().replace(lookupParallelRpcs=3)
+    steppers = [KadMigStepper(net.ids, net.xy, bounds, r, dev, params=params, top_levels=3, capacity=world * m)
+                for r in range(world)]
+    ks, ss, allk, alls = _native_inputs(net, bounds, world, m, 0x7D, node_ids=lambda r: False)
+    dones, rounds = route_local_shards(steppers, ks, ss, [r * m for r in range(world)])
+    assert rounds <= 2, rounds          # round 1 at home, round 2 at the key's arc, nothing left after
+    d = np.concatenate([done_to_numpy(x) for x in dones])
+    d = d[np.argsort(d["qid"])]
+    ref = _kad_reference(net, allk, alls, params)
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f

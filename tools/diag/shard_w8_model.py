@@ -16,14 +16,16 @@ import numpy as np
 import torch
 
 from oversim_amd import Params, workload as W
-from oversim_amd.shard import (KAD_REQ_BYTES, KAD_RESP_BYTES, REC_BYTES, GpuShardStepper, KadShardStepper, arc_bounds,
-                               done_to_numpy)
+from oversim_amd.shard import (KAD_REQ_BYTES, KAD_RESP_BYTES, REC_BYTES, GpuShardStepper, KadMigStepper, KadShardStepper,
+                               arc_bounds, done_to_numpy, prefix_bounds)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", choices=["C", "D", "E"], required=True)
 ap.add_argument("--lookups-per-rank", type=int, default=0)
 ap.add_argument("--world", type=int, default=8)
-ap.add_argument("--top-levels", type=int, default=None, help="Chord: replicated top finger levels (default: shard.default_top_levels)")
+ap.add_argument("--top-levels", type=int, default=None,
+                help="replicated top finger levels (Chord; default shard.default_top_levels) / buckets (Kademlia --mig; default 3)")
+ap.add_argument("--mig", action="store_true", help="Kademlia: migrating lookups over replicated top buckets, prefix arcs")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -35,8 +37,14 @@ I0 = inputs[0]
 n = I0["n_total"]
 ids = I0["ids"] if I0["ids"] is not None else I0["ids_t"].cpu().numpy().view(np.uint32)
 xy = I0["xy"] if I0["xy"] is not None else I0["xy_t"].cpu().numpy()
-bounds = arc_bounds(n, Wn)
 kad = a.workload == "E"
+mig = kad and a.mig
+bounds = prefix_bounds(ids, Wn) if mig else arc_bounds(n, Wn)
+if mig:
+    # the lookups' sources must lie on their rank's prefix arc: remap them into it
+    for r, I in enumerate(inputs):
+        lo_, hi_ = bounds[r], bounds[r + 1]
+        I["src_t"] = (lo_ + (I["src_t"].to(torch.int64) % (hi_ - lo_))).to(torch.int32).contiguous()
 params = Params.kademlia().replace(lookupParallelRpcs=wl.get("alpha", 3)) if kad else Params.chord()
 
 
@@ -45,7 +53,12 @@ def ev():
 
 
 t_start = time.time()
-if kad:
+if mig:
+    tl = 3 if a.top_levels is None else a.top_levels
+    steppers = [KadMigStepper(ids, xy, bounds, r, dev, params=params, top_levels=tl, capacity=Wn * m) for r in range(Wn)]
+    inbox = [steppers[r].first_batch(inputs[r]["keys_t"], inputs[r]["src_t"], r * m) for r in range(Wn)]
+    kad = False          # the record loop below (as Chord's)
+elif kad:
     steppers = [KadShardStepper(ids, xy, bounds, r, dev, params=params) for r in range(Wn)]
     for r in range(Wn):
         steppers[r].begin(inputs[r]["keys_t"], inputs[r]["src_t"], r * m)
@@ -118,7 +131,7 @@ while True:
             new_inbox.append(torch.cat(parts) if parts else segs[d][d][:0])
         inbox = new_inbox
         remote = np.array([int(M[r, :Wn].sum() - M[r, r]) for r in range(Wn)])
-        bytes_out = remote * REC_BYTES
+        bytes_out = remote * getattr(steppers[0], "rec_bytes", REC_BYTES)
     tot["step_ms"] += step_ms
     tot["serve_ms"] += serve_ms
     tot["deliver_ms"] += deliver_ms
@@ -132,7 +145,7 @@ while True:
 torch.cuda.synchronize()
 dn = [done_to_numpy(s.finished()) for s in steppers]
 d = np.concatenate(dn)
-if not kad and os.environ.get("OVS_MODEL_CHECK", "1") == "1":
+if (not kad or mig) and os.environ.get("OVS_MODEL_CHECK", "1") == "1":
     # every lookup against the single-context route of the same ring (the parity the tests assert)
     from oversim_amd import KbrEngine
     del steppers
@@ -141,16 +154,24 @@ if not kad and os.environ.get("OVS_MODEL_CHECK", "1") == "1":
     assert np.array_equal(d["qid"], np.arange(Wn * m))
     with KbrEngine(0) as e:
         e.set_params(params)
-        e.chord_load_device(inputs[0]["ids_t"].data_ptr(), inputs[0]["xy_t"].data_ptr(), n)
+        if mig:
+            e.kad_load_device(inputs[0]["ids_t"].data_ptr(), inputs[0]["xy_t"].data_ptr(), n)
+        else:
+            e.chord_load_device(inputs[0]["ids_t"].data_ptr(), inputs[0]["xy_t"].data_ptr(), n)
         kk = torch.cat([I["keys_t"] for I in inputs]); ss = torch.cat([I["src_t"] for I in inputs])
         out = torch.empty((kk.shape[0], 16), dtype=torch.uint8, device=dev)
-        e.lookup_device(kk.data_ptr(), ss.data_ptr(), kk.shape[0], out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        rp = torch.empty(kk.shape[0], dtype=torch.int32, device=dev) if mig else None
+        e.lookup_device(kk.data_ptr(), ss.data_ptr(), kk.shape[0], out.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                        rpcs_ptr=rp.data_ptr() if mig else None)
         torch.cuda.synchronize()
         ref = out.cpu().numpy().reshape(-1).view(np.dtype([("responsible", "<u4"), ("hops", "<u2"), ("status", "u1"),
                                                            ("one_way_hops", "u1"), ("latency_ns", "<i8")]))
     for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
         bad = int((d[f].astype(np.int64) != ref[f].astype(np.int64)).sum())
         assert bad == 0, f"{f}: {bad} lookups differ from the single-context route"
+    if mig:
+        bad = int((d["pad"].astype(np.int64) != rp.cpu().numpy().astype(np.int64)).sum())
+        assert bad == 0, f"rpcs: {bad} lookups differ from the single-context route"
     print(json.dumps(dict(check="sharded == single-context route", lookups=int(len(d)))), flush=True)
 print(json.dumps(dict(summary=True, workload=a.workload, world=Wn, rounds=rounds, lookups=int(len(d)),
                       ok=int((d["status"] == 0).sum()), mean_hops=float(d["hops"].mean()),

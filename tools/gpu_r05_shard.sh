@@ -5,7 +5,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$1; shift; mkdir -p $O
 export OVS_SKIP_BUILD=1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread \
   -k "native or c_consumer or emulated or failed_rebuild or capacity_change or cohorts or two_processes" \
   > $O/shard_tests.log 2>&1 || { tail -40 $O/shard_tests.log; exit 1; }
 tail -3 $O/shard_tests.log
