@@ -1963,19 +1963,35 @@ static int32_t kad_info_bytes(const orc_net* net, uint32_t x, const OKey* key)
  * -- at a forwarding hop before sendRouteMessage (BaseOverlay.cc:1577-1579), at the delivering
  * node before the message is handled (978-984) -- so that message leaves the node's queue first.
  * Its routingAdd calls change tables the batch holds fixed. */
-static RecEnd rec_route(const orc_net* net, const OKey* key, uint32_t from, int nsFrom, int32_t bytes, int64_t t0,
-                        int64_t tx0, uint32_t* hopseq)
+/* routingType "source-routing-recursive" (RECURSIVE_SOURCE_ROUTING, BaseOverlay.cc:129-130): every
+ * node a route message reaches appends its sender to the message's visitedHops (888-897), and the
+ * loop detection of the forwarding node also skips every visited hop (1502-1516).  The message's
+ * length is set once, when sendToKey creates it (1398: BASEROUTE_L with empty visited / next-hop
+ * arrays) and is not updated as visitedHops grows, so the per-hop delays equal semi-recursive
+ * routing's.  visited: the senders in arrival order (visited[0] = the source), nvis of them. */
+#define REC_MAXVIS 256
+static RecEnd rec_route_v(const orc_net* net, const OKey* key, uint32_t from, int nsFrom, int32_t bytes, int64_t t0,
+                          int64_t tx0, uint32_t* hopseq, uint32_t* visited, int* nvis)
 {
     const orc_params* p = &net->p;
     const int hook = net->type == NET_KAD;
+    const int srcroute = p->routingType == 4;
     RecEnd e;
     e.node = NONE; e.hops = 0; e.status = 0; e.t = t0; e.tx = tx0;
     uint32_t cur = from, lastHop = from;   /* routeCtrlInfo->setLastHop(thisNode) (BaseOverlay.cc:1400) */
-    int hopCount = 0;
+    int hopCount = 0, nv = 0;
     int64_t t = t0, tx = tx0;
+    if (nvis) *nvis = 0;
     for (;;) {
         int err = 0;
         const int ns = cur == from ? nsFrom : 1;
+        if (cur != from && srcroute) {
+            /* receipt: the sender joins visitedHops (BaseOverlay.cc:888-897) */
+            if (nv >= REC_MAXVIS) { cap_error("source route longer than 256 hops"); e.status = 3; return e; }
+            if (visited) visited[nv] = lastHop;
+            ++nv;
+            if (nvis) *nvis = nv;
+        }
         if (cur != from) {
             tx = 0;
             if (ov_isSiblingFor(net, cur, cur, key, 1, &err)) {
@@ -1998,6 +2014,11 @@ static RecEnd rec_route(const orc_net* net, const OKey* key, uint32_t from, int 
                 (h == from && cur != from) ||                          /* never to the source */
                 (h == cur && !isSibling))                              /* self without being sibling */
                 continue;
+            if (srcroute && visited) {                                 /* a visited hop (source routing) */
+                int seen = 0;
+                for (int j = 0; j < nv && !seen; ++j) seen = visited[j] == h;
+                if (seen) continue;
+            }
             next = h;
         }
         if (next == NONE) { e.status = 4; return e; }                  /* 1518-1538: no useful next hop */
@@ -2015,6 +2036,38 @@ static RecEnd rec_route(const orc_net* net, const OKey* key, uint32_t from, int 
     }
     e.node = cur; e.hops = hopCount; e.t = t; e.tx = tx;
     return e;
+}
+
+static RecEnd rec_route(const orc_net* net, const OKey* key, uint32_t from, int nsFrom, int32_t bytes, int64_t t0,
+                        int64_t tx0, uint32_t* hopseq)
+{
+    uint32_t vis[REC_MAXVIS];
+    int nv = 0;
+    return rec_route_v(net, key, from, nsFrom, bytes, t0, tx0, hopseq, vis, &nv);
+}
+
+/* A source-routed message from `from` along route[0 .. nroute) (sendToKey with a sourceRoute,
+ * BaseOverlay.cc:1419-1431; each hop pops itself off nextHops and forwards to the next, 888-905,
+ * 1003), delivered at the last node.  No findNode, no hop limit.  R/Kademlia: every node it reaches
+ * other than its srcNode (`from`) first sends the srcNode a KademliaRoutingInfoMessage about the
+ * message's destKey (Kademlia.cc:1022-1057) -- forwarding nodes before sendRouteMessage, so the
+ * message waits for that one's serialisation.  Returns the delivery time. */
+static int64_t src_route(const orc_net* net, const OKey* destKey, uint32_t from, const uint32_t* route, int nroute,
+                         int32_t bytes, int64_t t0, int64_t tx0)
+{
+    const int hook = net->type == NET_KAD;
+    uint32_t cur = from;
+    int64_t t = t0, tx = tx0;
+    for (int i = 0; i < nroute; ++i) {
+        const uint32_t next = route[i];
+        if (cur != from) {
+            tx = 0;
+            if (hook) calc_delay(net, cur, from, kad_info_bytes(net, cur, destKey), t, &tx);
+        }
+        t += calc_delay(net, cur, next, bytes, t, &tx);
+        cur = next;
+    }
+    return t;
 }
 
 /* a one-way KBRTestMessage: sendToKey(key, msg, numSiblings = 1) (BaseOverlay.cc:1357) ->
@@ -2051,7 +2104,9 @@ static void run_recursive_call(const orc_net* net, const OKey* key, uint32_t S, 
     const int nslots = numSiblings ? numSiblings : 1;
     for (int i = 0; i < nslots; ++i) sib[i] = NONE;
     out->num_siblings = 0; out->hops = 0; out->is_valid = 0; out->latency_ns = -1;
-    const RecEnd d = rec_route(net, key, S, numSiblings, 53 + 55 + 28, 0, 0, NULL);
+    uint32_t dvis[REC_MAXVIS];
+    int dv = 0;
+    const RecEnd d = rec_route_v(net, key, S, numSiblings, 53 + 55 + 28, 0, 0, NULL, dvis, &dv);
     if (d.status) { out->status = (uint8_t)d.status; return; }
     NVec res;
     int err = 0;
@@ -2063,6 +2118,13 @@ static void run_recursive_call(const orc_net* net, const OKey* key, uint32_t S, 
         if (p->routingType == 1) {
             int64_t tx = d.tx;
             T += calc_delay(net, d.node, S, resp, d.t, &tx);
+        } else if (p->routingType == 4) {
+            /* source routing: the response goes back along the call's recorded route, reversed
+             * (BaseRpc.cc:575-588: sourceRoute = visitedHops from the last to the first, sent with
+             * ROUTE_TRANSPORT and RECURSIVE_SOURCE_ROUTING), a 53 B route header + the response */
+            uint32_t rev[REC_MAXVIS];
+            for (int i = 0; i < dv; ++i) rev[i] = dvis[dv - 1 - i];
+            T = src_route(net, &net->ids[S], d.node, rev, dv, 53 + resp, d.t, d.tx);
         } else {
             const RecEnd r = rec_route(net, &net->ids[S], d.node, 1, 53 + resp, d.t, d.tx, NULL);
             if (r.status || r.node != S) { out->status = 2; return; }
@@ -2099,7 +2161,7 @@ uint64_t orc_route_batch(const orc_net* net, const orc_key* keys, const uint32_t
 #endif
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         OKey k = ok_from(&keys[i]);
-        if (net->p.routingType == 0 || net->p.routingType == 3)
+        if (net->p.routingType == 0 || net->p.routingType == 3)    /* 1, 2, 4: recursive */
             run_lookup(net, &k, src[i], &out[i], hop_seq ? hop_seq + (size_t)i * hcm : NULL,
                        rpcs_out ? &rpcs_out[i] : NULL, 0, NULL, NULL, exh, NULL, NULL, NULL, NULL, 0);
         else {
@@ -2120,7 +2182,7 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
     if (numSiblings > maxs) { set_err("numSiblings too big!"); return -1; }
     if (numSiblings < 0 || numSiblings > 16) { set_err("numSiblings must be 0..16"); return -1; }
     if (numSiblings == 0 && net->type == NET_KOORDE) { set_err("numSiblings = 0: Chord and Kademlia only"); return -1; }
-    if (net->p.routingType < 0 || net->p.routingType > 3) { set_err("LookupCall: routingType 0..3"); return -1; }
+    if (net->p.routingType < 0 || net->p.routingType > 4) { set_err("LookupCall: routingType 0..4"); return -1; }
     if (net->type == NET_KOORDE && net->p.routingType != 0) { set_err("Koorde: iterative routing only"); return -1; }
     const int exh = net->p.routingType == 3 ? net->p.lookupRedundantNodes : 0;
     if (exh && (net->type != NET_KAD || numSiblings > exh)) {
@@ -2135,7 +2197,7 @@ int orc_lookup_batch(const orc_net* net, const orc_key* keys, const uint32_t* sr
         OKey k = ok_from(&keys[i]);
         orc_route_out dummy;
         /* numSiblings = 0 (an exact-key lookup) keeps a one-slot sibling vector (start() 149) */
-        if (net->p.routingType == 1 || net->p.routingType == 2)
+        if (net->p.routingType == 1 || net->p.routingType == 2 || net->p.routingType == 4)
             run_recursive_call(net, &k, src[i], numSiblings, &out[i], siblings + (size_t)i * (numSiblings ? numSiblings : 1));
         else
             run_lookup(net, &k, src[i], &dummy, NULL, NULL, numSiblings, &out[i],

@@ -68,7 +68,7 @@ typedef struct {
     int32_t respPerNodeBytes;         /* + 26 B per NodeHandle */
     int32_t routeBytes;               /* one-way KBRTestMessage route msg = 186 */
     uint64_t kadSeed;                 /* Kademlia snapshot bucket-sampling seed */
-    int32_t routingType;              /* 0 iterative, 1 semi-recursive, 2 full-recursive (default.ini:392) */
+    int32_t routingType;              /* 0 iterative, 1 semi-recursive, 2 full-recursive, 3 exhaustive-iterative, 4 source-routing-recursive (default.ini:392) */
     int32_t recNumRedundantNodes;     /* default.ini:386 = 3 */
     /* Koorde (Koorde.ned, default.ini:268-291) */
     int32_t shiftingBits;             /* = 4 */

@@ -190,13 +190,21 @@ __device__ void put_sibling_row(KadBlk* __restrict__ blks, uint64_t blk0, int sb
 // bucket m of node v under the snapshot rule: up to k members of T_m = [flo, fhi) (the nodes at
 // msb(x ^ v) = m) minus v's siblings L, chosen by Floyd sampling with kad_hash(seed, v, m, j)
 // (DESIGN.md §4), written in ascending index order to the bpb blocks at blk0.  Returns the members.
+// Siblings lie at levels <= endIndex (the farthest one's level), so only the bucket m = endIndex can
+// hold any: may_sib = false skips the sibling scans for the buckets above it.  L (S5 entries) is read
+// with stride ls (the builders stage it in LDS).
 __device__ int kad_bucket_fill(const KeyRec* __restrict__ recs, uint32_t v, int m, uint32_t flo, uint32_t fhi,
-                               const uint32_t* L, int S5, int k, uint64_t seed, KadBlk* __restrict__ blks, uint64_t blk0)
+                               const uint32_t* L, int ls, int S5, int k, uint64_t seed, KadBlk* __restrict__ blks,
+                               uint64_t blk0, bool may_sib)
 {
     uint32_t chosen[KMAX];
     const int bpb = (k + KBLK - 1) / KBLK;
     uint32_t nsin = 0;
-    for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
+    if (may_sib)
+        for (int i = 0; i < S5; ++i) {
+            const uint32_t x = L[i * ls];
+            nsin += (x != NONE && x >= flo && x < fhi) ? 1u : 0u;
+        }
     const uint32_t c = (fhi - flo) - nsin;
     int nch = 0;
     if (c <= (uint32_t)k) {
@@ -223,7 +231,7 @@ __device__ int kad_bucket_fill(const KeyRec* __restrict__ recs, uint32_t v, int 
         int q = 0;
         for (uint32_t x = flo; x < fhi && q < nch; ++x) {
             bool is_sib = false;
-            for (int i = 0; i < S5; ++i) is_sib |= (L[i] == x);
+            for (int i = 0; i < S5; ++i) is_sib |= (L[i * ls] == x);
             if (is_sib) continue;
             if (rank == chosen[q]) { put_entry(blks, blk0, outn++, x, recs); ++q; }
             ++rank;
@@ -240,12 +248,17 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
                               KadBlk* __restrict__ blks, uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
 {
     const uint32_t v = own_lo + blockIdx.x * blockDim.x + threadIdx.x;   // rows of the owned arc
+    // the thread's sibling list staged in LDS (stride 64: thread t's entry i at [i][t]), read by the
+    // sibling-row sort and the endIndex bucket's scans instead of from HBM
+    __shared__ uint32_t lsib[64][64];
     if (v >= own_hi) return;
     const KadNode r = nodes[v];
     const K160 me = as_key(r.key);
-    const uint32_t* L = sib + (uint64_t)v * S5;
+    const uint32_t* G = sib + (uint64_t)v * S5;
+    for (int i = 0; i < S5; ++i) lsib[i][threadIdx.x] = G[i];
+    const uint32_t* L = &lsib[0][threadIdx.x];
     // sibling row
-    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, L, S5, v, me, recs);
+    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, G, S5, v, me, recs);
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     uint32_t lo = 0, hi = n;
@@ -255,7 +268,7 @@ __global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __
         const uint32_t nb = kbit(me, m);
         const uint32_t flo = nb ? lo : mid, fhi = nb ? mid : hi;
         const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
-        kad_bucket_fill(recs, v, m, flo, fhi, L, S5, k, seed, blks, blk0);
+        kad_bucket_fill(recs, v, m, flo, fhi, L, 64, S5, k, seed, blks, blk0, m == endIndex);
         lo = nb ? mid : lo;
         hi = nb ? hi : mid;
     }
@@ -284,7 +297,7 @@ __global__ void k_kad_top_buckets(const KeyRec* __restrict__ recs, KadNode* __re
         const int j = KEYBITS - 1 - m;
         const uint64_t blk0 = ((uint64_t)v * (uint32_t)tl + (uint32_t)j) * (uint64_t)bpb;
         if (m >= endIndex) {
-            const int cnt = kad_bucket_fill(recs, v, m, flo, fhi, L, S5, k, seed, blks, blk0);
+            const int cnt = kad_bucket_fill(recs, v, m, flo, fhi, L, 1, S5, k, seed, blks, blk0, m == endIndex);
             if (cnt >= k && m > endIndex) full |= 1u << j;
         } else {
             for (int q = 0; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);

@@ -198,8 +198,12 @@ struct KRecEnd {
 };
 
 // one BaseRouteMessage from `from` towards K, leaving at t0 with from's queue busy until tx0;
-// bwMsg = its serialisation time; nsFrom = numSiblings of the first sendToKey
-template <bool GEN, bool EX, bool RECORD>
+// bwMsg = its serialisation time; nsFrom = numSiblings of the first sendToKey.
+// SRC (routingType source-routing-recursive): the message records its senders (visitedHops,
+// BaseOverlay.cc:888-897) -- `from`, then the hop list hopseq[0 .. hops-2], which SRC always records --
+// and the loop detection skips every one of them (1502-1516); the message's length stays the one set
+// when it was created (1398), so the delays are semi-recursive's.
+template <bool GEN, bool EX, bool RECORD, bool SRC = false>
 __device__ KRecEnd krec_walk(const KadView& V, const KadGenView& G, const DelayConsts& DC, const KadRecCfg& RC,
                              const K160& K, uint32_t from, int nsFrom, int64_t bwMsg, int64_t t0, int64_t tx0,
                              uint32_t* __restrict__ hopseq)
@@ -235,6 +239,11 @@ __device__ KRecEnd krec_walk(const KadView& V, const KadGenView& G, const DelayC
             if (i >= n) break;
             const uint32_t h = res.idx[i];
             if ((h == last && h != cur) || (h == from && cur != from) || (h == cur && !sb)) continue;
+            if (SRC) {
+                bool seen = false;
+                for (int j = 0; j + 1 < hops && !seen; ++j) seen = hopseq[j] == h;
+                if (seen) continue;
+            }
             next = h;
         }
         if (next == NONE) { e.status = OVS_LOOKUP_NO_NEXT; return e; }
@@ -245,7 +254,7 @@ __device__ KRecEnd krec_walk(const KadView& V, const KadGenView& G, const DelayC
         const int64_t newTx = (tx > t ? tx : t) + bwMsg;
         tx = newTx;
         t = newTx + DC.access2 + coord_ns(r.x, r.y, b.x, b.y, DC.round) + bwMsg;
-        if (RECORD && hops < RC.hcm) hopseq[hops] = next;
+        if ((RECORD || SRC) && hops < RC.hcm) hopseq[hops] = next;
         ++hops;
         last = cur;
         cur = next;
@@ -255,7 +264,9 @@ __device__ KRecEnd krec_walk(const KadView& V, const KadGenView& G, const DelayC
 }
 
 // MODE 0: one-way route, 1: one-way route with the hop sequence, 2 / 3: LookupCall with a
-// semi- / full-recursive response
+// semi- / full-recursive response; source-routing-recursive: 4 one-way route (the hop list in hopseq:
+// the caller's or the context's scratch), 5 LookupCall whose response goes back along the call's
+// visited hops reversed (BaseRpc.cc:575-588), the R/Kademlia hook at every node on the way
 template <bool GEN, bool EX, int MODE>
 __global__ __launch_bounds__(128) void k_kad_recursive(KadView V, KadGenView G, DelayConsts DC, KadRecCfg RC, int ns,
                                                        const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
@@ -268,9 +279,9 @@ __global__ __launch_bounds__(128) void k_kad_recursive(KadView V, KadGenView G, 
     const uint32_t S = qsrc[q];
     ovs_route_out o;
     o.responsible = NONE; o.hops = 0; o.one_way_hops = 0; o.latency_ns = -1; o.status = 0;
-    if constexpr (MODE <= 1) {
-        const KRecEnd e = krec_walk<GEN, EX, MODE == 1>(V, G, DC, RC, K, S, 1, DC.bwRoute, 0, 0,
-                                                        hopseq + q * (uint64_t)RC.hcm);
+    if constexpr (MODE <= 1 || MODE == 4) {
+        const KRecEnd e = krec_walk<GEN, EX, MODE == 1, MODE == 4>(V, G, DC, RC, K, S, 1, DC.bwRoute, 0, 0,
+                                                                   hopseq + q * (uint64_t)RC.hcm);
         o.status = (uint8_t)e.status;
         if (!e.status) {
             o.responsible = e.node;
@@ -283,8 +294,9 @@ __global__ __launch_bounds__(128) void k_kad_recursive(KadView V, KadGenView G, 
         uint32_t* row = sib_out + q * (uint64_t)nslots;
         for (int j = 0; j < nslots; ++j) row[j] = NONE;
         // the routed FindNodeCall: BASEROUTE_L 424 + FINDNODECALL_L 440 bits + UDP/IP 28 B
-        const KRecEnd d = krec_walk<GEN, EX, false>(V, G, DC, RC, K, S, ns, bw_ns(53 + 55 + 28, DC.datarate, DC.round),
-                                                    0, 0, nullptr);
+        uint32_t* vl = MODE == 5 ? hopseq + q * (uint64_t)RC.hcm : nullptr;   // its hops (source routing)
+        const KRecEnd d = krec_walk<GEN, EX, false, MODE == 5>(V, G, DC, RC, K, S, ns,
+                                                               bw_ns(53 + 55 + 28, DC.datarate, DC.round), 0, 0, vl);
         o.status = (uint8_t)d.status;
         if (!d.status) {
             // findNodeRpc at D (BaseOverlay.cc:1841-1915)
@@ -301,6 +313,29 @@ __global__ __launch_bounds__(128) void k_kad_recursive(KadView V, KadGenView G, 
                     const int64_t bwr = bw_ns(rb, DC.datarate, DC.round);
                     const int64_t newTx = (d.tx > d.t ? d.tx : d.t) + bwr;
                     T = newTx + DC.access2 + coord_ns(rd.x, rd.y, sxy.x, sxy.y, DC.round) + bwr;
+                } else if (MODE == 5) {   // source routing: the senders reversed, h_{k-1} .. h_1, S
+                    const K160 KS = node_key(V.nodes, S);
+                    const int64_t bwm = bw_ns(53 + rb, DC.datarate, DC.round);
+                    uint32_t cur = d.node;
+                    int64_t t = d.t, tx = d.tx;
+                    SVec<KREC_C> ires;
+                    for (int i = d.hops - 2; i >= -1; --i) {
+                        const uint32_t nx = i >= 0 ? vl[i] : S;
+                        const KadNode rc = load_node(V.nodes, cur);
+                        if (cur != d.node) {
+                            // the node's queue is idle on arrival; R/Kademlia's hook toward the
+                            // response's source (D) leaves it first (Kademlia.cc:1022-1057)
+                            const bool sbs = kad_is_sibling(V, rc, cur, KS, RC.s);
+                            const int ni = krec_find<GEN, EX>(V, G, cur, rc, KS, RC.k, sbs, RC.s, ires);
+                            tx = t + bw_ns(47 + 27 * ni + 28, DC.datarate, DC.round);
+                        }
+                        const double2 b = V.xy[nx];
+                        const int64_t newTx = (tx > t ? tx : t) + bwm;
+                        tx = newTx;
+                        t = newTx + DC.access2 + coord_ns(rc.x, rc.y, b.x, b.y, DC.round) + bwm;
+                        cur = nx;
+                    }
+                    T = t;
                 } else {                  // full-recursive: routed to the source's key (1814-1818)
                     const K160 KS = node_key(V.nodes, S);
                     const KRecEnd b = krec_walk<GEN, EX, false>(V, G, DC, RC, KS, d.node, 1,
@@ -384,7 +419,8 @@ hipError_t kad_route_recursive(const KadTables& t, const double2* xy, uint32_t n
                                hipStream_t st)
 {
     if (nq == 0) return hipSuccess;
-    if (P.routingType != 1 && P.routingType != 2) return hipErrorNotSupported;
+    if (P.routingType != 1 && P.routingType != 2 && P.routingType != 4) return hipErrorNotSupported;
+    if (P.routingType == 4 && !hopseq) return hipErrorInvalidValue;   // source routing keeps the hop lists
     if (P.recNumRedundantNodes < 1 || P.recNumRedundantNodes > KREC_C || P.lookupRedundantNodes < 1 ||
         P.lookupRedundantNodes > KREC_C || t.k > KREC_C || t.s > KREC_C || P.hopCountMax < 0)
         return hipErrorNotSupported;
@@ -394,11 +430,12 @@ hipError_t kad_route_recursive(const KadTables& t, const double2* xy, uint32_t n
     RC.hcm = P.hopCountMax; RC.recR = P.recNumRedundantNodes; RC.R = P.lookupRedundantNodes; RC.k = t.k; RC.s = t.s;
     RC.keyTimeout2 = 2 * key_timeout;
     const dim3 grid(gblocks(nq, 128)), blk(128);
-    const int mode = sibs ? (P.routingType == 1 ? 2 : 3) : (hopseq ? 1 : 0);
+    const int mode = P.routingType == 4 ? (sibs ? 5 : 4) : sibs ? (P.routingType == 1 ? 2 : 3) : (hopseq ? 1 : 0);
 #define KR(gen, ex, m) hipLaunchKernelGGL((k_kad_recursive<gen, ex, m>), grid, blk, 0, st, V, G, DC, RC, lookup_ns, qkeys, qsrc, \
                                           nq, out, hopseq, sibs)
 #define KRM(gen, ex) do { switch (mode) { case 0: KR(gen, ex, 0); break; case 1: KR(gen, ex, 1); break; \
-                                          case 2: KR(gen, ex, 2); break; default: KR(gen, ex, 3); } } while (0)
+                                          case 2: KR(gen, ex, 2); break; case 3: KR(gen, ex, 3); break; \
+                                          case 4: KR(gen, ex, 4); break; default: KR(gen, ex, 5); } } while (0)
     if (t.general) { if (t.exact) KRM(true, true); else KRM(true, false); }
     else { if (t.exact) KRM(false, true); else KRM(false, false); }
 #undef KRM

@@ -313,8 +313,10 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         else if (rt == "semi-recursive") p->routingType = 1;
         else if (rt == "full-recursive") p->routingType = 2;
         else if (rt == "exhaustive-iterative") p->routingType = 3;
+        else if (rt == "source-routing-recursive") p->routingType = 4;
         else {
-            set_err("routingType \"" + rt + "\" not supported (iterative, semi-recursive, full-recursive)");
+            set_err("routingType \"" + rt + "\" not supported (iterative, semi-recursive, full-recursive, "
+                    "exhaustive-iterative, source-routing-recursive)");
             return OVS_ENOTSUP;
         }
     }

@@ -273,15 +273,17 @@ DelayConsts delay_consts(const ovs_params& P)
 ovs_status check_common(ovs_ctx* c, const ovs_params& P)
 {
     if (P.keyLength != 160) return fail(c, OVS_ENOTSUP, "keyLength != 160 not supported");
-    if (P.routingType < 0 || P.routingType > 3)
-        return fail(c, OVS_ENOTSUP, "routingType must be iterative, semi-recursive, full-recursive or exhaustive-iterative");
+    if (P.routingType < 0 || P.routingType > 4)
+        return fail(c, OVS_ENOTSUP, "routingType must be iterative, semi-recursive, full-recursive, exhaustive-iterative "
+                                    "or source-routing-recursive");
+    const bool rec = P.routingType == 1 || P.routingType == 2 || P.routingType == 4;
     if (P.routingType == 3 && P.overlay != OVS_OVERLAY_KADEMLIA)
         return fail(c, OVS_ENOTSUP, "exhaustive-iterative routing is implemented for Kademlia");
     if (P.routingType == 3 && P.numSiblings > P.lookupRedundantNodes)
         return fail(c, OVS_EINVAL, "With EXHAUSTIVE_ITERATIVE_ROUTING numRedundantNodes must be >= numSiblings!");
-    if ((P.routingType == 1 || P.routingType == 2) && P.recNumRedundantNodes < 1)
+    if (rec && P.recNumRedundantNodes < 1)
         return fail(c, OVS_EINVAL, "recNumRedundantNodes must be >= 1");
-    if ((P.routingType == 1 || P.routingType == 2) && P.overlay == OVS_OVERLAY_KADEMLIA &&
+    if (rec && P.overlay == OVS_OVERLAY_KADEMLIA &&
         (P.recNumRedundantNodes > 16 || P.lookupRedundantNodes > 16 || !(P.rpcKeyTimeout >= 0)))
         return fail(c, OVS_ENOTSUP, "recursive Kademlia implements recNumRedundantNodes, lookupRedundantNodes <= 16 "
                                     "and rpcKeyTimeout >= 0");
@@ -1510,9 +1512,9 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             return fail(c, OVS_ENOTSUP,
                         "Koorde route kernel implements lookupRedundantNodes=1, lookupParallelRpcs=1, merge off, "
                         "visitOnlyOnce, numSiblings=1 (the Koorde defaults)");
-    } else if (c->P.routingType < 0 || c->P.routingType > 3) {
+    } else if (c->P.routingType < 0 || c->P.routingType > 4) {
         return fail(c, OVS_ENOTSUP, "Kademlia routing is implemented for routingType = iterative / semi-recursive / "
-                                    "full-recursive / exhaustive-iterative");
+                                    "full-recursive / exhaustive-iterative / source-routing-recursive");
     } else if (c->kad.general && c->P.routingType == 3) {
         return fail(c, OVS_ENOTSUP, "CSR (b > 1 / nr128 / nkademlia) tables: routingType iterative or recursive");
     } else if (c->P.numSiblings != 1) {
@@ -1542,7 +1544,9 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
     const bool koorde_scratch = c->overlay == OVS_OVERLAY_KOORDE && !hop_seq;
     // exhaustive-iterative Kademlia: the responder list is the lookup's visited set
     const bool kad_exh = c->overlay == OVS_OVERLAY_KADEMLIA && c->P.routingType == 3;
-    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal) || kad_exh;
+    // source-routing-recursive Kademlia: the hop list is the message's visitedHops
+    const bool kad_src = c->overlay == OVS_OVERLAY_KADEMLIA && c->P.routingType == 4;
+    const bool need_hop = hop_seq || (c->overlay == OVS_OVERLAY_CHORD && !c->ideal) || kad_exh || kad_src;
     bool own_hop = false;
     if (koorde_scratch) {
         {
@@ -1596,7 +1600,7 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
                            hop_seq == nullptr /* nobody reads the visited sets: their first entries in LDS */);
         hipFree(dres);
         if (e == hipSuccess && cap_err) return fail(c, OVS_ENOTSUP, "a lookup exceeded the kernel's capacity (64 timed-out nodes)");
-    } else if (c->P.routingType == 1 || c->P.routingType == 2) {
+    } else if (c->P.routingType == 1 || c->P.routingType == 2 || kad_src) {
         // R/Kademlia: recursive routing with Kademlia's recursiveRoutingHook (kad_general.hip)
         e = kad_route_recursive(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P),
                                 simtime_host(c->P.rpcKeyTimeout, c->P.simtimeRound), 1, dk, ds, n, dout, dhop, nullptr, s);
@@ -1652,7 +1656,7 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     ovs_status st = check_common(c, P);
     if (st != OVS_OK) return st;
     const bool kad_exh = !chord && P.routingType == 3;
-    const bool kad_rec = !chord && (P.routingType == 1 || P.routingType == 2);
+    const bool kad_rec = !chord && (P.routingType == 1 || P.routingType == 2 || P.routingType == 4);
     if (P.routingType != 0 && !kad_exh && !kad_rec)
         return fail(c, OVS_ENOTSUP, "LookupCall is implemented for routingType = iterative (Kademlia: also recursive and "
                                     "exhaustive-iterative)");
@@ -1704,7 +1708,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     // Chord exact-key lookups replay the one-way chain recorded one hop beyond hopCountMax
     const bool chord_exact = chord && ns == 0;
     const int H = chord_exact ? P.hopCountMax + 1 : P.hopCountMax > 0 ? P.hopCountMax : 1;
-    const bool need_hop = (chord && !c->ideal) || kad_exh || chord_exact;   // visited check (explicit tables; exhaustive lookups)
+    // visited check (explicit tables; exhaustive lookups; source routing: the call's route, reversed by the response)
+    const bool need_hop = (chord && !c->ideal) || kad_exh || chord_exact || (kad_rec && P.routingType == 4);
     if (need_hop) {
         // internal (a LookupCall records no hop sequence): the context's cached buffer
         {
@@ -1734,9 +1739,11 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         if (e == hipSuccess && cap_err) e = hipErrorNotSupported;
     } else if (kad_rec) {
         // RecursiveLookup (RecursiveLookup.cc:52-139): a routed FindNodeCall, the response back by UDP
-        // (semi-recursive) or routed to the source's key (full-recursive)
+        // (semi-recursive), routed to the source's key (full-recursive) or along the call's route
+        // reversed (source-routing-recursive)
         e = kad_route_recursive(c->kad, c->xy, (uint32_t)c->n, P, delay_consts(P),
-                                simtime_host(P.rpcKeyTimeout, P.simtimeRound), ns, dk, ds, n, dout, nullptr, dsib, s);
+                                simtime_host(P.rpcKeyTimeout, P.simtimeRound), ns, dk, ds, n, dout,
+                                P.routingType == 4 ? dhop : nullptr, dsib, s);
     } else if (c->kad.general) {
         e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, s, dsib);
     } else {

@@ -207,7 +207,81 @@ def kad_rec_case(name: str, n: int, seed: int, m: int, rnd: int = 1, hcm: int = 
           "lookup-call valid", out["lc1_ns8_is_valid"].mean(), out["lc2_ns8_is_valid"].mean())
 
 
+def src_route_case(name: str, n_chord: int, n_kad: int, seed: int, m: int, rnd: int = 1):
+    """routingType = "source-routing-recursive" (BaseOverlay.cc:129-130; verify.ini [Config ChordSource]).
+    One-way routes on Chord and Kademlia: the route message records its senders and skips them in the
+    loop detection, its length stays the one set at creation (BaseOverlay.cc:888-897, 1398, 1502-1516),
+    so on converged rings and snapshot tables the routes equal semi-recursive ones -- the oracle is
+    checked against its own semi-recursive routes and against refmodel.  Kademlia LookupCalls: the
+    response travels back along the call's recorded route, reversed (BaseRpc.cc:575-588), with the
+    R/Kademlia hook at every node on the way -- oracle vs refmodel.KadRecursiveSim(source_routing)."""
+    out = {}
+    # Chord
+    net = W.population(n_chord, seed)
+    k1, s1 = W.lookups(net.ids, m // 2, seed + 1, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m // 2, seed + 2, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    r4 = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd, routingType=4)).route(keys, src, record_hops=True)
+    r1 = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd, routingType=1)).route(keys, src, record_hops=True)
+    ring = refmodel.ChordRing(net.ids, net.xy, rnd=bool(rnd))
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "hop_seq"):
+        assert np.array_equal(r4[f], r1[f]), (name, "chord: source routing differs from semi-recursive", f)
+    for i in range(len(keys)):
+        mm = ring.lookup_recursive(keys[i], int(src[i]))
+        for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
+            assert int(r4[f][i]) == int(mm[f]), (name, i, f, r4[f][i], mm[f])
+    H = int(r4["hops"].max()) + 1
+    out.update(chord_ids=net.ids, chord_xy=net.xy, chord_keys=keys, chord_src=src,
+               **{f"chord_{f}": r4[f] for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns")},
+               chord_hop_seq=r4["hop_seq"][:, :H])
+    # Kademlia
+    net = W.population(n_kad, seed + 10)
+    k1, s1 = W.lookups(net.ids, m // 2, seed + 11, node_ids=True)
+    k2, s2 = W.lookups(net.ids, m // 2, seed + 12, node_ids=False)
+    keys, src = np.concatenate([k1, k2]), np.concatenate([s1, s2])
+    p = kad_params(routingType=4, simtimeRound=rnd)
+    o = OracleNet("kademlia", net.ids, net.xy, p)
+    sib, cnt, nodes = o.kad_tables()
+    sim = refmodel.KadRecursiveSim(refmodel.KadTables(net.ids, sib, cnt, nodes, k=p.k, s=p.s), net.xy, k=p.k, s=p.s,
+                                   rec_redundant=p.recNumRedundantNodes, redundant=p.lookupRedundantNodes, rnd=bool(rnd))
+    r = o.route(keys, src, record_hops=True)
+    r1 = OracleNet("kademlia", net.ids, net.xy, kad_params(routingType=1, simtimeRound=rnd)).route(keys, src,
+                                                                                                   record_hops=True)
+    for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "hop_seq"):
+        assert np.array_equal(r[f], r1[f]), (name, "kademlia: source routing differs from semi-recursive", f)
+    for i in range(len(keys)):
+        mm = sim.route(keys[i], int(src[i]), source_routing=True)
+        for f in ("responsible", "hops", "status", "latency_ns"):
+            assert int(r[f][i]) == int(mm[f]), (name, i, f, r[f][i], mm[f])
+    H = int(r["hops"].max()) + 1
+    out.update(kad_ids=net.ids, kad_xy=net.xy, kad_keys=keys, kad_src=src,
+               **{f"kad_{f}": r[f] for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns")},
+               kad_hop_seq=r["hop_seq"][:, :H])
+    for ns in (1, p.s, 0):
+        lc = o.lookup_call(keys, src, ns)
+        for i in range(len(keys)):
+            mm = sim.lookup_call(keys[i], int(src[i]), ns, source_routing=True)
+            for f in ("num_siblings", "hops", "status", "is_valid", "latency_ns"):
+                assert int(lc[f][i]) == int(mm[f]), (name, ns, i, f, lc[f][i], mm[f])
+            assert [int(x) for x in lc["siblings"][i] if x != 0xFFFFFFFF] == mm["siblings"][:max(ns, 1)], (name, i)
+        for f in ("num_siblings", "status", "is_valid", "latency_ns", "siblings"):
+            out[f"kad_lc_ns{ns}_{f}"] = np.asarray(lc[f])
+    if "--check" in sys.argv:
+        g = np.load(HERE / f"{name}.npz")
+        for f, v in out.items():
+            assert np.array_equal(g[f], v), (name, f)
+        print(name, "committed vectors reproduced")
+        return
+    np.savez_compressed(HERE / f"{name}.npz", seed=np.int64(seed), simtime_round=np.int32(rnd),
+                        routing_type=np.int32(4), **out)
+    print(name, "chord mean hops", out["chord_hops"].mean(), "kad mean hops", out["kad_hops"].mean(),
+          "lookup-call valid", out["kad_lc_ns8_is_valid"].mean())
+
+
 if __name__ == "__main__":
+    if "--srcroute" in sys.argv:   # (with --check: verify instead of writing)
+        src_route_case("srcroute_n2000", 1000, 2000, 0x5C0, 2048)
+        sys.exit(0)
     if "--kadrec" in sys.argv:   # (with --check: verify instead of writing)
         kad_rec_case("kad_n2000_rec", 2000, 0x4b52, 2048)
         kad_rec_case("kad_n1000_rec_hcm3", 1000, 0x4b53, 1024, rnd=0, hcm=3)

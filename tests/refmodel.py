@@ -1078,14 +1078,19 @@ class KadRecursiveSim:
     def _info(self, x, key):
         return 47 + 27 * len(self.T.find_node(x, key, self.k, self.s)) + 28
 
-    def walk(self, key, src, ns_src, nbytes, now=0, q=None):
-        """(delivered node or None, hops, time, status, queues, hop list)."""
+    def walk(self, key, src, ns_src, nbytes, now=0, q=None, source_routing=False):
+        """(delivered node or None, hops, time, status, queues, hop list).  source_routing: the
+        message records its senders (visitedHops, BaseOverlay.cc:888-897) and the forwarding nodes
+        skip them too (1502-1516); its length stays the one set at creation (1398)."""
         q = {} if q is None else q
-        msg = dict(src=src, last=src, hops=0)
+        msg = dict(src=src, last=src, hops=0, visited=[])
         node, t, path = src, now, []
+        self.visited = msg["visited"]
         while True:
             ns = ns_src if node == src else 1
             if node != src:
+                if source_routing:
+                    msg["visited"].append(msg["last"])
                 q.pop(node, None)                      # the queue is idle when the message arrives
                 if self.T.is_sibling_for(node, key, 1):
                     self._send(q, node, src, self._info(node, key), t)   # the hook, then delivery
@@ -1099,6 +1104,8 @@ class KadRecursiveSim:
             nxt = None
             for h in hops:
                 if (h == msg["last"] and h != node) or (h == src and node != src) or (h == node and not sib):
+                    continue
+                if h in msg["visited"]:
                     continue
                 nxt = h
                 break
@@ -1114,16 +1121,17 @@ class KadRecursiveSim:
             path.append(nxt)
             node = nxt
 
-    def route(self, key, src):
+    def route(self, key, src, source_routing=False):
         key = to_int(key) if not isinstance(key, int) else key
-        d, hops, t, st, _, path = self.walk(key, src, 1, self.route_b)
+        d, hops, t, st, _, path = self.walk(key, src, 1, self.route_b, source_routing=source_routing)
         if st:
             return dict(responsible=0xFFFFFFFF, hops=0, status=st, latency_ns=-1, hop_seq=path)
         return dict(responsible=d, hops=hops, status=0, latency_ns=t, hop_seq=path)
 
-    def lookup_call(self, key, src, ns, full=False):
+    def lookup_call(self, key, src, ns, full=False, source_routing=False):
         key = to_int(key) if not isinstance(key, int) else key
-        d, _, t, st, q, _ = self.walk(key, src, ns, self.ROUTE_HDR + self.CALL + 28)
+        d, _, t, st, q, _ = self.walk(key, src, ns, self.ROUTE_HDR + self.CALL + 28, source_routing=source_routing)
+        visited = list(self.visited)
         fail = dict(num_siblings=0, hops=0, is_valid=0, latency_ns=-1, siblings=[])
         if st:
             return dict(fail, status=st)
@@ -1131,7 +1139,18 @@ class KadRecursiveSim:
         flag = self.T.is_sibling_for(d, key, ns)
         if d != src:
             nbytes = self.resp_b + self.resp_n * len(res)
-            if not full:
+            if source_routing:
+                # BaseRpc::internalSendRpcResponse (BaseRpc.cc:575-588): back along the visited hops,
+                # last first; every node but the response's source (d) runs the hook toward d first
+                skey = self.T.ids[src]
+                node = d
+                for nxt in reversed(visited):
+                    if node != d:
+                        q.pop(node, None)
+                        self._send(q, node, d, self._info(node, skey), t)
+                    t = self._send(q, node, nxt, self.ROUTE_HDR + nbytes, t)
+                    node = nxt
+            elif not full:
                 t = self._send(q, d, src, nbytes, t)
             else:
                 back, _, t, st2, _, _ = self.walk(self.T.ids[src], d, 1, self.ROUTE_HDR + nbytes, t, {d: q.get(d, 0)})

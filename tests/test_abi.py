@@ -100,7 +100,7 @@ def test_params_ini_errors():
     with pytest.raises(KbrError):
         Params.from_ini("[General]\n**.overlay*.*.hopCountMax = ${10, 20}\n")
     with pytest.raises(KbrError):
-        Params.from_ini("[General]\n**.overlay*.chord.routingType = \"source-routing-recursive\"\n")
+        Params.from_ini("[General]\n**.overlay*.chord.routingType = \"hop-by-hop\"\n")
     with pytest.raises(KbrError):
         Params.from_ini("[General]\n**.overlay*.*.recordRoute = true\n")
     with pytest.raises(KbrError):
@@ -131,6 +131,8 @@ def test_params_chordlarge_semi_recursive():
     assert Params.from_ini('[General]\n**.routingType = "full-recursive"\n').routingType == 2
     # Kademlia's bucket refresh lookups (Kademlia.cc:1483-1487) run exhaustive-iterative
     assert Params.from_ini('[General]\n**.routingType = "exhaustive-iterative"\n').routingType == 3
+    # verify.ini [Config ChordSource]
+    assert Params.from_ini('[General]\n**.routingType = "source-routing-recursive"\n').routingType == 4
 
 
 def test_reference_default_ini_parses():
