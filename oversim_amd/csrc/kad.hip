@@ -149,10 +149,13 @@ __global__ void k_kad_prefix_ties(const KeyRec* __restrict__ recs, uint32_t n, u
     if (((top64(kload(recs, i)) ^ top64(kload(recs, i + 1))) >> 1) == 0) atomicOr(flag, 1u);
 }
 
-__global__ void k_kad_set_boff(KadNode* nodes, const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t base)
+// row offsets of the owned nodes; an off-arc node's row exists on its owner only: NONE (>= every
+// replicated-region end, so a sharded kernel can never read a row through it)
+__global__ void k_kad_set_boff(KadNode* nodes, const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t base,
+                               uint32_t n)
 {
-    const uint32_t v = lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < hi) nodes[v].boff = (uint32_t)(base + off[v]);
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < n) nodes[v].boff = (v >= lo && v < hi) ? (uint32_t)(base + off[v]) : NONE;
 }
 
 __device__ __forceinline__ void put_entry(KadBlk* __restrict__ blks, uint64_t blk0, int q, uint32_t x,
@@ -241,37 +244,162 @@ __device__ int kad_bucket_fill(const KeyRec* __restrict__ recs, uint32_t v, int 
     return outn;
 }
 
-// snapshot pass B: buckets m = 159 .. endIndex of the owned nodes, up to k members of T_m minus
-// siblings chosen by Floyd sampling (snapshot rule); sibling rows
-__global__ void k_kad_buckets(const KeyRec* __restrict__ recs, const KadNode* __restrict__ nodes, uint32_t n, int k,
-                              int S5, int sbn, uint64_t seed, const uint32_t* __restrict__ sib,
-                              KadBlk* __restrict__ blks, uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
+// top 64 key bits (96..159) of every node: the bucket builder's searches and member tops read this
+// 8 B array (128 MB at 2^24 nodes, resident in the MALL) instead of the 24 B key records
+__global__ void k_kad_tops(const KeyRec* __restrict__ recs, uint32_t n, uint64_t* __restrict__ tops)
 {
-    const uint32_t v = own_lo + blockIdx.x * blockDim.x + threadIdx.x;   // rows of the owned arc
-    // the thread's sibling list staged in LDS (stride 64: thread t's entry i at [i][t]), read by the
-    // sibling-row sort and the endIndex bucket's scans instead of from HBM
-    __shared__ uint32_t lsib[64][64];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) tops[i] = ktop(kload(recs, i));
+}
+
+// first x in [lo, hi) whose key bits m..159 are >= Q's (upper: > Q's); keys sorted ascending, so the
+// prefix is monotone.  m >= 96: the prefix lies in the top 64 bits (tops); below, the full keys.
+__device__ uint32_t kad_prefix_bound(const KeyRec* __restrict__ recs, const uint64_t* __restrict__ tops, uint32_t lo,
+                                     uint32_t hi, int m, const K160& Q, bool upper)
+{
+    if (m >= 96) {
+        const int sh = m - 96;
+        const uint64_t q = ktop(Q) >> sh;
+        while (lo < hi) {
+            const uint32_t mid = lo + ((hi - lo) >> 1);
+            const uint64_t p = tops[mid] >> sh;
+            if (upper ? p <= q : p < q) lo = mid + 1; else hi = mid;
+        }
+        return lo;
+    }
+    K160 qm = Q;
+#pragma unroll
+    for (int w = 0; w < 5; ++w) {
+        const int b0 = 32 * w;
+        qm.w[w] = b0 + 32 <= m ? 0u : b0 >= m ? qm.w[w] : qm.w[w] & (~0u << (m - b0));
+    }
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        K160 x = kload(recs, mid);
+#pragma unroll
+        for (int w = 0; w < 5; ++w) {
+            const int b0 = 32 * w;
+            x.w[w] = b0 + 32 <= m ? 0u : b0 >= m ? x.w[w] : x.w[w] & (~0u << (m - b0));
+        }
+        if (upper ? k_le(x, qm) : k_lt(x, qm)) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+constexpr int KB_LANES = 32;   // k_kad_bucket_rows: lanes per node, lane j builds buckets m = 159 - j - 32 i
+
+// snapshot pass B: bucket m = 159 .. endIndex of every owned node -- up to k members of T_m (the
+// nodes at msb(x ^ v) = m, one contiguous index range [flo, fhi) of the sorted keys) minus the
+// node's siblings, chosen by Floyd sampling with kad_hash(seed, v, m, j) (snapshot rule, DESIGN.md
+// §4), in ascending index order.  One lane per (node, bucket): consecutive lanes write consecutive
+// KadBlks of the row, so every store is a coalesced run; T_m comes from two prefix searches over
+// the whole sorted array (their top levels are shared by every lane and stay in the caches), and
+// the c-th non-sibling member is found without scanning T_m.  Only bucket endIndex can hold
+// siblings (siblings lie at levels <= endIndex).  Same blocks as kad_bucket_fill (k_kad_top_buckets).
+template <int KC>
+__global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restrict__ recs,
+                                                          const uint64_t* __restrict__ tops,
+                                                          const KadNode* __restrict__ nodes, uint32_t n, int k, int S5,
+                                                          uint64_t seed, const uint32_t* __restrict__ sib,
+                                                          KadBlk* __restrict__ blks, uint32_t own_lo, uint32_t own_hi)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t v = own_lo + (uint32_t)(g / KB_LANES);
+    const int lane = (int)(g % KB_LANES);
     if (v >= own_hi) return;
     const KadNode r = nodes[v];
-    const K160 me = as_key(r.key);
-    const uint32_t* G = sib + (uint64_t)v * S5;
-    for (int i = 0; i < S5; ++i) lsib[i][threadIdx.x] = G[i];
-    const uint32_t* L = &lsib[0][threadIdx.x];
-    // sibling row
-    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, G, S5, v, me, recs);
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
-    uint32_t lo = 0, hi = n;
+    const K160 me = as_key(r.key);
     const int bpb = (k + KBLK - 1) / KBLK;
-    for (int m = KEYBITS - 1; m >= endIndex; --m) {
-        const uint32_t mid = split_bit(recs, lo, hi, m);
-        const uint32_t nb = kbit(me, m);
-        const uint32_t flo = nb ? lo : mid, fhi = nb ? mid : hi;
-        const uint64_t blk0 = (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
-        kad_bucket_fill(recs, v, m, flo, fhi, L, 64, S5, k, seed, blks, blk0, m == endIndex);
-        lo = nb ? mid : lo;
-        hi = nb ? hi : mid;
+    const uint32_t* L = sib + (uint64_t)v * S5;
+    for (int m = KEYBITS - 1 - lane; m >= endIndex; m -= KB_LANES) {
+        // T_m: the prefix of bits m..159 equal to the node's with bit m flipped
+        K160 Q = me;
+#pragma unroll
+        for (int w = 0; w < 5; ++w) Q.w[w] ^= (m >> 5) == w ? 1u << (m & 31) : 0u;   // selects: no scratch
+        const bool below = kbit(me, m) != 0;     // T_m lies below v in the sorted order
+        const uint32_t flo = kad_prefix_bound(recs, tops, below ? 0u : v + 1, below ? v : n, m, Q, false);
+        const uint32_t fhi = kad_prefix_bound(recs, tops, flo, below ? v : n, m, Q, true);
+        uint32_t nsin = 0;
+        if (m == endIndex)
+            for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
+        const uint32_t c = (fhi - flo) - nsin;
+        // Floyd sampling of min(k, c) ranks out of c, then ascending
+        uint32_t ch[KC];
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+            uint32_t t = NONE;
+            if (i < k && (uint32_t)i < c) {
+                if (c <= (uint32_t)k) {
+                    t = (uint32_t)i;
+                } else {
+                    const uint32_t j = c - (uint32_t)k + (uint32_t)i;
+                    t = (uint32_t)(kad_hash(seed, v, (uint32_t)m, j) % (uint64_t)(j + 1));
+                    bool dup = false;
+#pragma unroll
+                    for (int q = 0; q < i; ++q) dup |= ch[q] == t;
+                    t = dup ? j : t;
+                }
+            }
+            ch[i] = t;
+        }
+#pragma unroll
+        for (int a = 0; a < KC; ++a)          // odd-even transposition sort (NONE = the largest)
+#pragma unroll
+            for (int b = a & 1; b + 1 < KC; b += 2) {
+                const uint32_t x = ch[b], y = ch[b + 1];
+                ch[b] = x < y ? x : y;
+                ch[b + 1] = x < y ? y : x;
+            }
+        // rank -> node: flo + rank, stepped over the siblings inside T_m (least fixed point of
+        // x = flo + rank + #{siblings in [flo, x]})
+        if (nsin) {
+#pragma unroll
+            for (int q = 0; q < KC; ++q) {
+                if (ch[q] == NONE) continue;
+                const uint32_t base = flo + ch[q];
+                uint32_t x = base;
+                for (;;) {
+                    uint32_t cs = 0;
+                    for (int i = 0; i < S5; ++i) cs += (L[i] != NONE && L[i] >= flo && L[i] <= x) ? 1u : 0u;
+                    if (base + cs == x) break;
+                    x = base + cs;
+                }
+                ch[q] = x;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < KC; ++q) ch[q] = ch[q] == NONE ? NONE : flo + ch[q];
+        }
+        uint64_t tp[KC];
+#pragma unroll
+        for (int q = 0; q < KC; ++q) tp[q] = ch[q] == NONE ? ~0ull : tops[ch[q]];
+        KadBlk* B = blks + (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
+#pragma unroll
+        for (int b = 0; b < KC / KBLK; ++b) {
+            if (b >= bpb) break;
+            uint4* d = reinterpret_cast<uint4*>(B + b);
+#pragma unroll
+            for (int q = 0; q < KBLK; q += 2) {
+                const uint64_t t0 = tp[b * KBLK + q], t1 = tp[b * KBLK + q + 1];
+                d[q / 2] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+            }
+            d[4] = make_uint4(ch[b * KBLK], ch[b * KBLK + 1], ch[b * KBLK + 2], ch[b * KBLK + 3]);
+            d[5] = make_uint4(ch[b * KBLK + 4], ch[b * KBLK + 5], ch[b * KBLK + 6], ch[b * KBLK + 7]);
+        }
     }
+}
+
+// the owned nodes' sibling rows
+__global__ void k_kad_sib_rows(const KeyRec* __restrict__ recs, const KadNode* __restrict__ nodes, int S5, int sbn,
+                               const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks, uint64_t sib_base,
+                               uint32_t own_lo, uint32_t own_hi)
+{
+    const uint32_t v = own_lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= own_hi) return;
+    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, sib + (uint64_t)v * S5, S5, v,
+                    as_key(nodes[v].key), recs);
 }
 
 // sharded networks (KadTables::tl > 0): the top tl buckets m = 159 .. 160 - tl of EVERY node, at
@@ -577,11 +705,26 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     t.rows_blks = tend + total;
     const uint64_t nblks = t.rows_blks + (uint64_t)nown * sbn + 1;
     if ((e = hipMalloc(&t.blks, sizeof(KadBlk) * nblks)) != hipSuccess) { cleanup(); return e; }
-    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(nown, 256)), dim3(256), 0, st, t.nodes, off, lo, hi, tend);
+    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, lo, hi, tend, n);
     if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)nown * S5)) != hipSuccess) { cleanup(); return e; }
     hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5, hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(k_kad_buckets, dim3(nblk(nown, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn, seed,
-                       sib_all, t.blks, t.rows_blks, lo, hi);
+    hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, 128)), dim3(128), 0, st, recs, t.nodes, S5, sbn, sib_all,
+                       t.blks, t.rows_blks, lo, hi);
+    {
+        uint64_t* tops = nullptr;
+        if ((e = hipMalloc(&tops, sizeof(uint64_t) * n)) != hipSuccess) { cleanup(); return e; }
+        hipLaunchKernelGGL(k_kad_tops, dim3(nblk(n, 256)), dim3(256), 0, st, recs, n, tops);
+        const dim3 grid((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256));
+        if (k <= KBLK)
+            hipLaunchKernelGGL(k_kad_bucket_rows<KBLK>, grid, dim3(256), 0, st, recs, tops, t.nodes, n, k, S5, seed,
+                               sib_all, t.blks, lo, hi);
+        else
+            hipLaunchKernelGGL(k_kad_bucket_rows<2 * KBLK>, grid, dim3(256), 0, st, recs, tops, t.nodes, n, k, S5,
+                               seed, sib_all, t.blks, lo, hi);
+        e = hipStreamSynchronize(st);
+        hipFree(tops);
+        if (e != hipSuccess) { cleanup(); return e; }
+    }
     if (tl > 0)
         hipLaunchKernelGGL(k_kad_top_buckets, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, seed, sib_all,
                            t.blks, tl);
@@ -648,7 +791,7 @@ hipError_t kad_build_explicit(const KeyRec* recs, const double2* xy, uint32_t n,
     if (total >= 0xFFFFFFFFull) { cleanup(); return hipErrorInvalidValue; }
     t.rows_blks = total;
     if ((e = hipMalloc(&t.blks, sizeof(KadBlk) * (total + (uint64_t)n * sbn + 1))) != hipSuccess) { cleanup(); return e; }
-    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, 0u, n, 0ull);
+    hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, 0u, n, 0ull, n);
     hipLaunchKernelGGL(k_kad_explicit_rows, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, sbn,
                        t.sib, bcount, bnodes, t.blks, t.rows_blks);
     e = hipStreamSynchronize(st);

@@ -91,6 +91,7 @@ struct MigReady {
 struct MigSend {
     int tl, bpb;
     bool full_ok;      // lookupRedundantNodes <= k: a full main bucket alone is the answer
+    uint32_t lo, hi;   // this rank's arc
     __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
     __device__ __forceinline__ uint32_t boff(uint32_t x, const KadNode& rr, const RespGeo& g, bool sb) const
     {
@@ -100,7 +101,10 @@ struct MigSend {
             if (full_ok && g.m > g.endIndex && j < tl && ((rr.meta >> (KMETA_TOPFULL_SHIFT + j)) & 1u))
                 return x * (uint32_t)(tl * bpb);
         }
-        return g.boff;
+        // the owner's row: valid on the owner only.  Off this arc the call names no row here (NONE
+        // >= tend: MigReady holds the lookup until it has moved to the owner, which re-reads the
+        // responder's own line, and kad_find_node_blk never reads a row through it)
+        return (x >= lo && x < hi) ? g.boff : NONE;
     }
 };
 
@@ -275,6 +279,9 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
             }
 #endif
             const bool local = !SM || (ev.r >= V.lo && ev.r < V.hi);
+            // migration step: a call sent from another rank names no row of this one (MigSend:
+            // NONE); its responder's row here is the responder's own line's
+            if (MIG && ph == KEV_FIND && local && ev.boff >= V.tend) ev.boff = V.nodes[ev.r].boff;
             coop = ph == KEV_FIND && local && kad_find_is_coop(V, ev.r, ev.rg(), ev.sb(), ns, rb_pre(ev.pre), rb_r0(ev.pre));
         }
 
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
                                           V.hi, io.rstage, io.rtag, LK ? (0x80000000u | (uint32_t)ns) : 0u};
                     kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, on);
                 } else if (MIG) {
-                    kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, MigSend{io.tl, io.bpb, io.full_ok != 0});
+                    kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, MigSend{io.tl, io.bpb, io.full_ok != 0, V.lo, V.hi});
                 } else {
                     kad_send_rpcs<A, EX, LK, SH>(L, V, DC, LC, num, SendNothing{});
                 }

@@ -416,7 +416,11 @@ class CallbackExchange:
     def _alltoallv(self, user, send, send_rows, recv, recv_off, recv_rows, row_bytes, stream):
         def run():
             torch, dist = self.torch, self.dist
-            torch.cuda.ExternalStream(stream, device=self.dev).synchronize()    # the segments are complete
+            # the segments are complete (stream NULL: the device's default stream)
+            if stream:
+                torch.cuda.ExternalStream(stream, device=self.dev).synchronize()
+            else:
+                torch.cuda.synchronize(self.dev)
             ops, host_recv = [], {}
             for r in range(self.world):
                 ns, nr = int(send_rows[r]) * row_bytes, int(recv_rows[r]) * row_bytes
@@ -698,8 +702,9 @@ def route_local_shards(steppers, keys_per_shard, src_per_shard, qid_bases, max_r
     """Single-process emulation of W ranks (e.g. W contexts on one GPU): the exchange is a concatenation."""
     import torch
     W = len(steppers)
-    inbox = [getattr(steppers[r], "first_batch", steppers[r].make_records)(keys_per_shard[r], src_per_shard[r], qid_bases[r])
-             for r in range(W)]
+    def first(st):      # a stepper that starts from the keys, else the records of make_records
+        return st.first_batch if hasattr(st, "first_batch") else st.make_records
+    inbox = [first(steppers[r])(keys_per_shard[r], src_per_shard[r], qid_bases[r]) for r in range(W)]
     rounds = 0
     while True:
         rounds += 1
