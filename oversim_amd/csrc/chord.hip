@@ -515,8 +515,14 @@ __device__ unsigned long long g_k1_stats[8];
 #ifndef OVS_K1_WAVES
 #define OVS_K1_WAVES 5
 #endif
+// the shard step: 5 waves as well, with its outcomes staged where they are decided (held to the end
+// of the iteration they had taken it to 107 VGPRs: at 5 waves 28-40 B per lane spilled to scratch
+// inside the hop loop, every iteration waiting for a scratch reload; at 4 waves no spill)
+#ifndef OVS_K1_SHARD_WAVES
+#define OVS_K1_SHARD_WAVES 5
+#endif
 template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
-__global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
+__global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -545,15 +551,12 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
     bool gTx = false;                 // temp == K (node-ID key): a finger hits only when it is K
     const uint4* lp = nullptr;        // the line requested for the next iteration
     uint4 L0 = make_uint4(0, 0, 0, 0), L1 = L0, L2 = L0, L3 = L0;
-    int hand = -1;                    // shard: this lane's lookup moves to arc `hand` this iteration
     // shard with replicated top finger levels (V.ftl > 0): `remote` -- the current responder lies off
     // this arc and is being decided from the replicated levels; `redo` -- the record arrived as a
-    // responder already reached whose decision needs its owner's rows (record local byte 2);
-    // `hl` -- the local byte of the record this lane hands off
+    // responder already reached whose decision needs its owner's rows (record local byte 2).
+    // A lookup's outcome of a shard step (hand-off record or done record) is staged where it is
+    // decided: holding it to the end of the iteration kept ~10 more VGPRs live across the loop
     bool remote = false, redo = false;
-    uint32_t hl = 0;
-    bool done_now = false;            // shard: this lane's lookup finished this iteration ...
-    ovs_route_out done_o{};           // ... with this result
 
     __shared__ uint4 xbuf[4][256];    // per wave: the 64 gathered lines, 4 chunks each
     uint4* const xb = xbuf[threadIdx.x >> 6];
@@ -566,8 +569,8 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
 #ifdef OVS_K1_NO_PRELOAD
     constexpr bool pre_ok = false;    // A/B build: the PH_FETCH iteration for every lookup
 #else
-    // (the shard step keeps the PH_FETCH iteration: its staging leaves no register for the
-    // preloaded source at 5 waves/SIMD -- 20 B of spills)
+    // (the shard step keeps the PH_FETCH iteration: a preloaded source spills 20 B per lane at 5
+    // waves/SIMD even with its outcomes staged where decided)
     constexpr bool pre_ok = !SHARD;
 #endif
     const K160* const pkeys = SHARD ? io.fkeys : io.qkeys;
@@ -659,7 +662,6 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
             uint8_t status = OVS_LOOKUP_OK;
             uint32_t R = NONE;
             Hdr A;
-            int emit = -1;            // shard: destination arc of a hand-off made this iteration
             uint32_t nxt = NONE;      // next hop chosen this iteration ...
             bool nxt_node = false;    // ... whose header must be read from its NodeRec
             bool nxt_sib = false;
@@ -668,8 +670,8 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
             // replicated levels, or its successor window): the lookup goes to the owner as a
             // responder already reached (its response accounted here), which decides there
             auto redo_hand = [&]() {
-                emit = shard_owner(io.shard_lo, io.nsh, cur);
-                hl = 2;
+                store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, 2);
+                io.stag[q] = (uint8_t)shard_owner(io.shard_lo, io.nsh, cur);
                 active = false;
                 lp = nullptr;
             };
@@ -827,8 +829,8 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                             t += DC.msgRoute + coord_ns(sx, sy, nxy.x, nxy.y, DC.round);
                         }
                         cur = nx;
-                        emit = dest;
-                        hl = 0;
+                        store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, 0);
+                        io.stag[q] = (uint8_t)dest;
                         active = false;
                         lp = nullptr;
                         return false;
@@ -949,32 +951,20 @@ __global__ __launch_bounds__(256, OVS_K1_WAVES) void k_chord_lanes(ChordView V, 
                 }
                 o.status = status;
                 if (SHARD) {
-                    done_o = o;           // appended below, one atomic per wave
-                    done_now = true;
+                    ovs_done_rec dr;
+                    dr.qid = qid; dr.pad = 0; dr.out = o;
+                    io.stage_done[q] = dr;
+                    io.stag[q] = (uint8_t)io.nsh;
                 } else {
                     io.out[q] = o;
                 }
                 active = false;
                 lp = nullptr;
             }
-            if (SHARD) hand = emit;
         }
-        if (SHARD) {
-            // ---- every input record has exactly one outcome this launch, staged at its own index
-            // (no atomics: compact_by_tag moves them to the per-arc segments and the done buffer)
-            if (done_now) {
-                ovs_done_rec dr;
-                dr.qid = qid; dr.pad = 0; dr.out = done_o;
-                io.stage_done[q] = dr;
-                io.stag[q] = (uint8_t)io.nsh;
-            }
-            if (hand >= 0) {
-                store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, (int)hl);
-                io.stag[q] = (uint8_t)hand;
-            }
-            done_now = false;
-            hand = -1;
-        }
+        // (shard: every input record has exactly one outcome this launch, staged at its own index
+        // where it was decided -- no atomics: compact_by_tag moves them to the per-arc segments and
+        // the done buffer)
         // ---- request the next line: a cooperative gather, 4 lanes fetch one 64 B line with one
         // 16 B load each, so one wave instruction touches 16 lines instead of 64 (on HBM-resident
         // tables this moves 2.3x the lines/s of per-lane 4 x 16 B loads: tools/ubench/gather.hip)

@@ -1,0 +1,33 @@
+# Round 5: rocprof of the Kademlia table build at 2^24, then the W = 8 cost models (C; E with migration).
+# usage: bash tools/gpu_r05_model.sh <outdir> [C] [E] [profC] [profE] [build]
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/$1; shift; mkdir -p $O
+export OVS_SKIP_BUILD=1
+for w in "$@"; do
+  case $w in
+    build)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/build -o b -- python3 -u tools/diag/kad_build_time.py --reps 2 > $O/build.out 2>&1 || { tail -20 $O/build.out; exit 1; }
+      tail -4 $O/build.out ;;
+    profC|profE)
+      w2=${w#prof}; extra=""; [ $w2 = E ] && extra="--mig"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/$w -o k -- python3 -u tools/diag/shard_w8_model.py --workload $w2 $extra > $O/$w.out 2>&1 || { tail -20 $O/$w.out; exit 1; }
+      grep summary $O/$w.out | cut -c1-400 ;;
+    C|E)
+      extra=""; [ $w = E ] && extra="--mig"
+      timeout -k 10 600 python3 -u tools/diag/shard_w8_model.py --workload $w $extra > $O/w8$w.out 2> $O/w8$w.err || { tail -20 $O/w8$w.err; exit 1; }
+      tail -6 $O/w8$w.out ;;
+  esac
+done
+# k1stats: the W = 8 and W = 1 C models on the OVS_CHORD_STATS library (lines by kind per K1 launch)
+if [ "${K1STATS:-0}" = 1 ]; then
+  for W in 8 1; do
+    OVS_LIB=$PWD/oversim_amd/libovs_kbr_k1stats.so timeout -k 10 600 python3 -u tools/diag/shard_w8_model.py --workload C --world $W > $O/k1s_w$W.out 2> $O/k1s_w$W.err || { tail -20 $O/k1s_w$W.err; exit 1; }
+    grep -c k1stats $O/k1s_w$W.err
+  done
+fi
+# ab: the C model on the in-tree library and on each oversim_amd/libovs_kbr_<tag>.so named in AB
+for tag in ${AB:-}; do
+  OVS_LIB=$PWD/oversim_amd/libovs_kbr_$tag.so timeout -k 10 600 python3 -u tools/diag/shard_w8_model.py --workload C > $O/ab_$tag.out 2> $O/ab_$tag.err || { tail -20 $O/ab_$tag.err; exit 1; }
+  echo "$tag: $(grep summary $O/ab_$tag.out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(max(d["step_ms_per_rank"]), d["rounds"])')"
+done
