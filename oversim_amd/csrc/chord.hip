@@ -626,11 +626,19 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
                 ph = PH_FETCH;
                 remote = false; redo = false;
                 if (SHARD && io.fkeys) {
-                    // a batch's first round: no record, the lookup starts from its key and source
+                    // a batch's first round: no record, the lookup starts from its key and source,
+                    // whose line is requested in this refill iteration (what PH_FETCH would do one
+                    // iteration later; the shard step has no register for the preloaded source)
                     K = io.fkeys[q];
                     S = io.fsrc[q];
                     qid = io.fqid + (uint32_t)q;
-                    lp = nullptr;
+                    if (S < V.n) {
+                        cur = S; t = 0; hops = 0; local = true;
+                        lp = reinterpret_cast<const uint4*>(V.nodes + cur);
+                        ph = PH_START;
+                    } else {
+                        lp = nullptr;          // PH_FETCH reports the source outside the ring
+                    }
                 } else if (SHARD) {
                     // the 48 B hand-off record comes through the cooperative gather (tag 1: 3 chunks)
                     lp = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(io.in + q) | 1u);

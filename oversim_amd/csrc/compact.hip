@@ -67,10 +67,15 @@ __global__ __launch_bounds__(64) void k_compact_scatter(const uint8_t* __restric
     const uint64_t b = blockIdx.x;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (int c = lane; c < nclass; c += 64) off[c] = cbase[c] + (long long)scan[(uint64_t)c * nb + b];
+    // the tile's tags, all requested before the first step needs one
+    uint8_t tt[CT_STEPS];
+#pragma unroll
+    for (int k = 0; k < CT_STEPS; ++k) tt[k] = tag_at(tags, n, b * CT_TILE + (uint64_t)k * 64 + lane);
     __syncthreads();
+#pragma unroll
     for (int k = 0; k < CT_STEPS; ++k) {
         const uint64_t e = b * CT_TILE + (uint64_t)k * 64 + lane;
-        const uint8_t t = tag_at(tags, n, e);
+        const uint8_t t = tt[k];
         const bool mine = t < nclass;
         uint64_t rem = __ballot(mine);
         long long pos = -1;
@@ -91,9 +96,18 @@ __global__ __launch_bounds__(64) void k_compact_scatter(const uint8_t* __restric
         if (mine) {
             const CClass C = plan_class(P, t);
             if (C.dst && pos >= 0 && (uint64_t)pos < C.cap) {
-                const uint2* s = reinterpret_cast<const uint2*>(C.src + e * C.src_stride);
-                uint2* d = reinterpret_cast<uint2*>(C.dst + (uint64_t)pos * C.rec_bytes);
-                for (uint32_t w = 0; w < C.rec_bytes / 8; ++w) d[w] = s[w];
+                const uint8_t* sp = C.src + e * C.src_stride;
+                uint8_t* dp = C.dst + (uint64_t)pos * C.rec_bytes;
+                if (((C.rec_bytes | (uint32_t)C.src_stride | (uint32_t)(uintptr_t)sp | (uint32_t)(uintptr_t)dp) & 15) == 0) {
+                    // 16 B moves (the 48 B hand-off records: 3 per record)
+                    const uint4* s = reinterpret_cast<const uint4*>(sp);
+                    uint4* d = reinterpret_cast<uint4*>(dp);
+                    for (uint32_t w = 0; w < C.rec_bytes / 16; ++w) d[w] = s[w];
+                } else {
+                    const uint2* s = reinterpret_cast<const uint2*>(sp);
+                    uint2* d = reinterpret_cast<uint2*>(dp);
+                    for (uint32_t w = 0; w < C.rec_bytes / 8; ++w) d[w] = s[w];
+                }
                 if (C.lab) C.lab[pos] = C.label;
             }
         }
