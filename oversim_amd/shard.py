@@ -578,7 +578,7 @@ class TorchExchange:
     def records(self, send, scl, rcl):
         """all-to-allv of rows of `send` (uint8, one record per row, grouped by destination rank)
         with explicit splits: point-to-point pieces to the other ranks, a device copy of this
-        rank's own share (RCCL's all_to_all_single lost records at world size 1 beyond ~1 GB)."""
+        rank's own share (one RCCL message above 2^30 bytes delivers only its first half: DESIGN.md §6)."""
         torch = self.torch
         send = send.to(self.comm_dev)
         recv = torch.full((sum(rcl), send.shape[1]), 0xFF, dtype=torch.uint8, device=self.comm_dev)   # sentinel

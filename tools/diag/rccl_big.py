@@ -43,12 +43,21 @@ def pattern(nbytes: int) -> torch.Tensor:
 
 
 def check(tag: str, send: torch.Tensor, recv: torch.Tensor, **kw):
+    # compared in 256 MiB pieces (boolean indexing / nonzero of > 2^31 elements is not safe here)
     torch.cuda.synchronize()
-    bad = (send != recv)
-    nbad = int(bad.sum())
-    first = int(bad.to(torch.uint8).argmax()) if nbad else -1
-    last = int(bad.numel() - 1 - bad.flip(0).to(torch.uint8).argmax()) if nbad else -1
-    untouched = int((recv[bad] == 0xFF).sum()) if nbad else 0
+    nbad = untouched = 0
+    first = last = -1
+    piece = 256 * MB
+    for o in range(0, send.numel(), piece):
+        a, b = send[o:o + piece], recv[o:o + piece]
+        bad = a != b
+        k = int(bad.sum())
+        if k:
+            nbad += k
+            untouched += int((bad & (b == 0xFF)).sum())
+            if first < 0:
+                first = o + int(bad.to(torch.uint8).argmax())
+            last = o + int(bad.numel() - 1 - bad.flip(0).to(torch.uint8).argmax())
     print(json.dumps(dict(probe=tag, bytes=int(send.numel()), mismatched=nbad, first_bad=first, last_bad=last,
                           bad_still_sentinel=untouched, **kw)), flush=True)
 

@@ -1,0 +1,15 @@
+# Round 5: the driver's default bench line (C, with the oracle parity check and CPU baseline), then
+# the RCCL > 1 GB probe.  usage: bash tools/gpu_r05_bench.sh <outdir> [workloads...] [rccl]
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/$1; shift; mkdir -p $O
+export OVS_SKIP_BUILD=1
+for w in "$@"; do
+  if [ $w = rccl ]; then
+    timeout -k 10 300 python3 -u tools/diag/rccl_big.py ${RCCL_ARGS:-} > $O/rccl.out 2> $O/rccl.err || { tail -20 $O/rccl.err; exit 1; }
+    cat $O/rccl.out
+  else
+    timeout -k 10 600 python3 -u bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
+    cut -c1-1500 $O/bench_$w.json
+  fi
+done
