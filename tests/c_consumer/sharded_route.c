@@ -8,7 +8,7 @@
  * the output file, which tests/test_gpu_c_consumer.py compares with each other and with the oracle.
  *
  * input  (little endian): u32 overlay, u64 n, u64 m, n x 5 u32 ids, n x 2 f64 xy, m x 5 u32 keys,
- *                         m x u32 src, u32 world, i32 top_levels (Chord)
+ *                         m x u32 src, u32 world, i32 top_levels (replicated levels / buckets)
  * output: m x ovs_route_out of the sharded route (batch order), m x u32 FindNodeCall counts
  *         (Kademlia; 0 for Chord), m x ovs_route_out of ovs_route_batch, u32 rounds
  * usage: sharded_route <in> <out>
@@ -150,9 +150,12 @@ int main(int argc, char** argv)
             if (!rc && top > 0) rc |= check(R->ctx, ovs_chord_shard_replicate(R->ctx, top), "ovs_chord_shard_replicate");
         } else {
             rc |= check(R->ctx, ovs_kad_load_shard(R->ctx, ids, n, xy, bounds[r], bounds[r + 1], 0), "ovs_kad_load_shard");
+            /* replicated top buckets: the one-way lookups migrate between the arcs */
+            if (!rc && top > 0) rc |= check(R->ctx, ovs_kad_shard_replicate(R->ctx, top), "ovs_kad_shard_replicate");
         }
-        /* a Chord lookup may finish on any rank: every done buffer holds the whole batch */
-        R->done_cap = overlay == OVS_OVERLAY_CHORD ? (m ? m : 1) : (R->m ? R->m : 1);
+        /* a Chord lookup (or a migrating Kademlia one) may finish on any rank: every done buffer
+         * holds the whole batch */
+        R->done_cap = (overlay == OVS_OVERLAY_CHORD || top > 0) ? (m ? m : 1) : (R->m ? R->m : 1);
         ovs_key160* hk = (ovs_key160*)malloc(sizeof(ovs_key160) * (R->m ? R->m : 1));
         uint32_t* hs = (uint32_t*)malloc(sizeof(uint32_t) * (R->m ? R->m : 1));
         for (uint64_t j = 0; j < R->m; ++j) { hk[j] = keys[order[off[r] + j]]; hs[j] = src[order[off[r] + j]]; }

@@ -69,7 +69,7 @@ EXE2 = ROOT / "tests" / "c_consumer" / "sharded_route"
 
 
 @pytest.mark.parametrize("overlay,world,top", [(kbr.OVERLAY_CHORD, 3, 6), (kbr.OVERLAY_CHORD, 4, 0),
-                                               (kbr.OVERLAY_KADEMLIA, 3, 0)])
+                                               (kbr.OVERLAY_KADEMLIA, 3, 0), (kbr.OVERLAY_KADEMLIA, 3, 3)])
 def test_c_consumer_sharded_route(tmp_path, overlay, world, top):
     """The multi-GPU route from C: tests/c_consumer/sharded_route runs W ranks as
     pthreads, one context per arc, over the library's in-process exchange through
