@@ -45,8 +45,10 @@ def test_chunked_rccl_transfer_above_1gib_is_complete():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     lib = _rccl()
-    uid = C.create_string_buffer(128)
-    assert lib.ncclGetUniqueId(uid) == 0
+    class UID(C.Structure):                     # ncclUniqueId: 128 bytes, passed by value
+        _fields_ = [("internal", C.c_char * 128)]
+    uid = UID()
+    assert lib.ncclGetUniqueId(C.byref(uid)) == 0
     comm = C.c_void_p()
     assert lib.ncclCommInitRank(C.byref(comm), 1, uid, 0) == 0
     try:
