@@ -40,14 +40,15 @@ __device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2*
         const K160 d = k_xor(kload(recs, L[i]), me);
         if (k_gt(d, R)) R = d;
         const int mb = k_msb(d);
-        M.w[mb >> 5] |= 1u << (mb & 31);
+#pragma unroll
+        for (int w = 0; w < 5; ++w) M.w[w] |= (mb >> 5) == w ? 1u << (mb & 31) : 0u;   // selects: no scratch
     }
     const int end = cnt > 0 ? k_msb(R) : -1;
     const int mlo = end > 63 ? end - 63 : 0;
     // mask window: bits [mlo, mlo + 63]
     const int wi = mlo >> 5, sh = mlo & 31;
-    const uint64_t lo = (uint64_t)M.w[wi] | ((uint64_t)(wi + 1 < 5 ? M.w[wi + 1] : 0u) << 32);
-    const uint64_t hi = wi + 2 < 5 ? (uint64_t)M.w[wi + 2] : 0ull;
+    const uint64_t lo = (uint64_t)kword(M, wi) | ((uint64_t)kword(M, wi + 1) << 32);   // kword: 5+ reads 0
+    const uint64_t hi = (uint64_t)kword(M, wi + 2);
     const uint64_t win = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
     bool out_bits = false;
     for (int b = 0; b < mlo; ++b) out_bits |= kbit(M, b) != 0;
@@ -76,23 +77,114 @@ __device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2*
     ox[v] = x;
 }
 
+// top 64 key bits (96..159) of every node: the bucket builder's searches and member tops read this
+// 8 B array (128 MB at 2^24 nodes, resident in the MALL) instead of the 24 B key records
+__global__ void k_kad_tops(const KeyRec* __restrict__ recs, uint32_t n, uint64_t* __restrict__ tops)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) tops[i] = ktop(kload(recs, i));
+}
+
+constexpr int KB_DMAX = 26;    // prefix tables for depths 1 .. D <= 26 (2^(D+1) entries, 4 B each)
+
+// first entry of depth d's prefix table: tables of 2^j + 1 entries for j = 1 .. d-1 precede it
+__host__ __device__ __forceinline__ uint64_t kb_tab_off(int d) { return ((1ull << d) - 2) + (uint64_t)(d - 1); }
+
+// prefix tables: B_d[P] = the first node whose top d key bits are >= P (d = 1 .. D, P = 0 .. 2^d;
+// B_d[2^d] = n).  One pass over the sorted top keys: node i fills the prefixes between its
+// predecessor's and its own.  T_m of any node is then [B_d[Q], B_d[Q + 1]) with d = 160 - m.
+__global__ void k_kad_prefix_tables(const uint64_t* __restrict__ tops, uint32_t n, int D, uint32_t* __restrict__ tab)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t t = tops[i], tp = i ? tops[i - 1] : 0ull;
+    for (int d = 1; d <= D; ++d) {
+        uint32_t* B = tab + kb_tab_off(d);
+        const uint64_t p = t >> (64 - d);
+        const uint64_t from = i ? (tp >> (64 - d)) + 1 : 0ull;
+        for (uint64_t P = from; P <= p; ++P) B[P] = i;
+        if (i == n - 1)
+            for (uint64_t P = p + 1; P <= (1ull << d); ++P) B[P] = n;
+    }
+}
+
 // snapshot pass A: sibling table (the 5s XOR-closest nodes, what routingAdd converges to:
 // Kademlia.cc:537-616) and the node summary; the row length for the owned arc
-__global__ void k_kad_siblings(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t n, int S5,
-                               int bpb, uint32_t own_lo, uint32_t own_hi, uint32_t* __restrict__ sib,
-                               KadNode* __restrict__ out, KadX* __restrict__ ox, uint64_t* __restrict__ rowlen)
+// a block's sibling lists live in LDS (row stride KS_STRIDE words, 5s <= 64): built, read and written
+// out as whole rows with coalesced copies -- per-lane lists at a 4 * 5s byte stride touch a line per
+// lane for every entry
+constexpr int KS_BLOCK = 128;
+constexpr int KS_STRIDE = 65;
+
+__device__ __forceinline__ void ks_load_rows(uint32_t* lsb, const uint32_t* __restrict__ sib, uint32_t v0, uint32_t nv,
+                                             int S5)
 {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
+    const uint32_t tot = nv * (uint32_t)S5;
+    for (uint32_t i = threadIdx.x; i < tot; i += blockDim.x) {
+        const uint32_t r = i / (uint32_t)S5, c = i - r * (uint32_t)S5;
+        lsb[r * KS_STRIDE + c] = sib[(uint64_t)v0 * S5 + i];
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(KS_BLOCK) void k_kad_siblings(const KeyRec* __restrict__ recs,
+                                                            const double2* __restrict__ xy, uint32_t n, int S5, int bpb,
+                                                            uint32_t own_lo, uint32_t own_hi,
+                                                            const uint64_t* __restrict__ tops,
+                                                            const uint32_t* __restrict__ tab, int D, int dg,
+                                                            uint32_t* __restrict__ sib, KadNode* __restrict__ out,
+                                                            KadX* __restrict__ ox, uint64_t* __restrict__ rowlen)
+{
+    __shared__ uint32_t lsb[KS_BLOCK * KS_STRIDE];
+    const uint32_t v0 = blockIdx.x * KS_BLOCK;
+    const uint32_t v = v0 + threadIdx.x;
+    uint32_t* L = lsb + threadIdx.x * KS_STRIDE;
+    if (v < n) {
     const K160 me = kload(recs, v);
-    uint32_t* L = sib + (uint64_t)v * S5;
     int cnt = 0;
     if (n - 1 < (uint32_t)S5) {
         for (uint32_t x = 0; x < n; ++x)
             if (x != v) L[cnt++] = x;
     } else {
-        uint32_t lo = 0, hi = n;
-        for (int b = KEYBITS - 1; b >= 0; --b) {
+        // the descent below starts at the first bit whose split leaves the node's block with fewer
+        // than 5s+1 nodes: found in the prefix tables (v's block at depth d = [B_d[P], B_d[P+1]),
+        // sizes shrink with d), not by one binary search per level
+        const uint64_t mtop = tops[v];
+        auto range = [&](int d, uint32_t& a, uint32_t& z) {
+            if (d == 0) { a = 0; z = n; return; }
+            const uint32_t* B = tab + kb_tab_off(d);
+            const uint64_t P = mtop >> (64 - d);
+            a = B[P]; z = B[P + 1];
+        };
+        // deepest depth whose block still holds >= 5s+1 nodes: a linear walk from the depth where
+        // an average block holds that many (dg, the same for every lane, so a wave's table reads
+        // stay in a few lines; a per-lane binary search over the depths scattered them over
+        // every table and ran 2.5x slower)
+        int d0 = dg;
+#ifdef OVS_KS_NOTAB
+        d0 = 0;                                    // A/B build: the whole descent by binary searches
+        if (false)
+#endif
+        {
+            uint32_t ra, rz;
+            range(d0, ra, rz);
+            if (rz - ra >= (uint32_t)S5 + 1) {
+                while (d0 < D) {
+                    range(d0 + 1, ra, rz);
+                    if (rz - ra < (uint32_t)S5 + 1) break;
+                    ++d0;
+                }
+            } else {
+                while (d0 > 0) {
+                    --d0;
+                    range(d0, ra, rz);
+                    if (rz - ra >= (uint32_t)S5 + 1) break;
+                }
+            }
+        }
+        uint32_t lo, hi;
+        range(d0, lo, hi);
+        for (int b = KEYBITS - 1 - d0; b >= 0; --b) {
             const uint32_t mid = split_bit(recs, lo, hi, b);
             const uint32_t nb = kbit(me, b);
             const uint32_t nlo = nb ? mid : lo, nhi = nb ? hi : mid;
@@ -137,6 +229,13 @@ __global__ void k_kad_siblings(const KeyRec* __restrict__ recs, const double2* _
     }
     kad_node_summary(recs, xy, v, L, cnt, end, out, ox);
     rowlen[v] = (v >= own_lo && v < own_hi && end >= 0) ? (uint64_t)(KEYBITS - end) * (uint64_t)bpb : 0;
+    }
+    __syncthreads();
+    const uint32_t nv = min((uint32_t)KS_BLOCK, n > v0 ? n - v0 : 0u), tot = nv * (uint32_t)S5;
+    for (uint32_t i = threadIdx.x; i < tot; i += blockDim.x) {
+        const uint32_t r = i / (uint32_t)S5, c = i - r * (uint32_t)S5;
+        sib[(uint64_t)v0 * S5 + i] = lsb[r * KS_STRIDE + c];
+    }
 }
 
 // 1 when two node IDs share their top 63 bits (then top-64 XOR distances of distinct nodes can
@@ -214,7 +313,7 @@ __device__ int kad_bucket_fill(const KeyRec* __restrict__ recs, uint32_t v, int 
         for (uint32_t j = 0; j < c; ++j) chosen[nch++] = j;
     } else {
         for (uint32_t j = c - (uint32_t)k; j < c; ++j) {
-            const uint32_t t = (uint32_t)(kad_hash(seed, v, (uint32_t)m, j) % (uint64_t)(j + 1));
+            const uint32_t t = mod_u64_u32(kad_hash(seed, v, (uint32_t)m, j), j + 1);
             bool dup = false;
             for (int q = 0; q < nch; ++q) dup |= (chosen[q] == t);
             chosen[nch++] = dup ? j : t;
@@ -242,14 +341,6 @@ __device__ int kad_bucket_fill(const KeyRec* __restrict__ recs, uint32_t v, int 
     }
     for (int q = outn; q < bpb * KBLK; ++q) put_entry(blks, blk0, q, NONE, recs);
     return outn;
-}
-
-// top 64 key bits (96..159) of every node: the bucket builder's searches and member tops read this
-// 8 B array (128 MB at 2^24 nodes, resident in the MALL) instead of the 24 B key records
-__global__ void k_kad_tops(const KeyRec* __restrict__ recs, uint32_t n, uint64_t* __restrict__ tops)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) tops[i] = ktop(kload(recs, i));
 }
 
 // first x in [lo, hi) whose key bits m..159 are >= Q's (upper: > Q's); keys sorted ascending, so the
@@ -286,19 +377,156 @@ __device__ uint32_t kad_prefix_bound(const KeyRec* __restrict__ recs, const uint
     return lo;
 }
 
-constexpr int KB_LANES = 32;   // k_kad_bucket_rows: lanes per node, lane j builds buckets m = 159 - j - 32 i
+constexpr int KB_LANES = 24;   // k_kad_bucket_rows: lanes per node, lane j builds buckets m = 159 - j - 24 i (rows ~ log2 n - 4 long)
+// bucket m of node v under the snapshot rule: up to k members of T_m (the nodes at
+// msb(x ^ v) = m, one contiguous index range [flo, fhi) of the sorted keys) minus v's siblings,
+// chosen by Floyd sampling with kad_hash(seed, v, m, j), in ascending index order, written as bpb
+// KadBlks.  T_m comes from two prefix-table reads (depth 160 - m <= D; deeper levels search the few
+// nodes of v's own depth-D prefix).  SIB: the bucket m = endIndex, the only one that can hold
+// siblings (they lie at levels <= endIndex): the c-th non-sibling member is the least fixed point
+// of x = flo + c + #{siblings in [flo, x]}.  Same blocks as kad_bucket_fill.
+template <int KC, bool SIB>
+__device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, const uint64_t* __restrict__ tops,
+                                               const uint32_t* __restrict__ tab, int D, uint32_t n, int k, int S5,
+                                               uint64_t seed, const uint32_t* __restrict__ L, KadBlk* __restrict__ blks,
+                                               uint32_t v, const K160& me, uint32_t boff, int m)
+{
+    const uint64_t mtop = ktop(me);
+    const int bpb = (k + KBLK - 1) / KBLK;
+    const int d = KEYBITS - m;
+    uint32_t flo, fhi;
+    if (d <= D) {
+        const uint64_t Q = (mtop >> (64 - d)) ^ 1ull;              // v's top d bits, bit m flipped
+        const uint32_t* B = tab + kb_tab_off(d);
+        flo = B[Q];
+        fhi = B[Q + 1];
+    } else {
+        // T_m lies inside v's own depth-D prefix range: search there
+        const uint64_t PD = mtop >> (64 - D);
+        const uint32_t* B = tab + kb_tab_off(D);
+        const bool below = kbit(me, m) != 0;
+        const uint32_t slo = below ? B[PD] : v + 1, shi = below ? v : B[PD + 1];
+        K160 Q = me;
+#pragma unroll
+        for (int w = 0; w < 5; ++w) Q.w[w] ^= (m >> 5) == w ? 1u << (m & 31) : 0u;   // selects: no scratch
+        flo = kad_prefix_bound(recs, tops, slo, shi, m, Q, false);
+        fhi = kad_prefix_bound(recs, tops, flo, shi, m, Q, true);
+    }
+    uint32_t nsin = 0;
+    if (SIB)
+        for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
+    const uint32_t c = (fhi - flo) - nsin;
+    // Floyd sampling of min(k, c) ranks out of c, then ascending
+    uint32_t ch[KC];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+        uint32_t t = NONE;
+        if (i < k && (uint32_t)i < c) {
+            if (c <= (uint32_t)k) {
+                t = (uint32_t)i;
+            } else {
+                const uint32_t j = c - (uint32_t)k + (uint32_t)i;
+                t = mod_u64_u32(kad_hash(seed, v, (uint32_t)m, j), j + 1);
+                bool dup = false;
+#pragma unroll
+                for (int q = 0; q < i; ++q) dup |= ch[q] == t;
+                t = dup ? j : t;
+            }
+        }
+        ch[i] = t;
+    }
+#pragma unroll
+    for (int a = 0; a < KC; ++a)          // odd-even transposition sort (NONE = the largest)
+#pragma unroll
+        for (int b = a & 1; b + 1 < KC; b += 2) {
+            const uint32_t x = ch[b], y = ch[b + 1];
+            ch[b] = x < y ? x : y;
+            ch[b + 1] = x < y ? y : x;
+        }
+    if (SIB && nsin && fhi - flo <= 256) {
+        // T_m spans at most 256 nodes (the usual case: T_endIndex holds a few dozen): the siblings as
+        // a bit mask over it, the c-th non-sibling = the c-th zero bit
+        uint64_t mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
+        for (int i = 0; i < S5; ++i) {
+            const uint32_t x = L[i];
+            if (x != NONE && x >= flo && x < fhi) {
+                const uint32_t o = x - flo;
+                const uint64_t bit = 1ull << (o & 63);
+                mk0 |= (o >> 6) == 0 ? bit : 0ull;
+                mk1 |= (o >> 6) == 1 ? bit : 0ull;
+                mk2 |= (o >> 6) == 2 ? bit : 0ull;
+                mk3 |= (o >> 6) == 3 ? bit : 0ull;
+            }
+        }
+        const uint32_t span = fhi - flo;
+        auto valid = [&](int w) -> uint64_t {    // the bits of word w inside T_m
+            const int b = (int)span - 64 * w;
+            return b >= 64 ? ~0ull : b <= 0 ? 0ull : ((1ull << b) - 1);
+        };
+        const uint64_t z0 = ~mk0 & valid(0), z1 = ~mk1 & valid(1), z2 = ~mk2 & valid(2), z3 = ~mk3 & valid(3);
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            if (ch[q] == NONE) continue;
+            uint32_t rnk = ch[q];
+            const uint32_t c0 = __popcll(z0), c1 = __popcll(z1), c2 = __popcll(z2);
+            uint64_t z = z0;
+            uint32_t base = 0;
+            if (rnk >= c0) { rnk -= c0; z = z1; base = 64;
+                if (rnk >= c1) { rnk -= c1; z = z2; base = 128;
+                    if (rnk >= c2) { rnk -= c2; z = z3; base = 192; } } }
+            uint32_t pos = 0;                      // the rnk-th set bit of z
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                const uint32_t c = __popcll(z & ((1ull << sh) - 1));
+                if (rnk >= c) { rnk -= c; z >>= sh; pos += sh; }
+            }
+            ch[q] = flo + base + pos;
+        }
+    } else if (SIB && nsin) {
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            if (ch[q] == NONE) continue;
+            const uint32_t base = flo + ch[q];
+            uint32_t x = base;
+            for (;;) {
+                uint32_t cs = 0;
+                for (int i = 0; i < S5; ++i) cs += (L[i] != NONE && L[i] >= flo && L[i] <= x) ? 1u : 0u;
+                if (base + cs == x) break;
+                x = base + cs;
+            }
+            ch[q] = x;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < KC; ++q) ch[q] = ch[q] == NONE ? NONE : flo + ch[q];
+    }
+    uint64_t tp[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) tp[q] = ch[q] == NONE ? ~0ull : tops[ch[q]];
+    KadBlk* B = blks + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
+#pragma unroll
+    for (int b = 0; b < KC / KBLK; ++b) {
+        if (b >= bpb) break;
+        uint4* dd = reinterpret_cast<uint4*>(B + b);
+#pragma unroll
+        for (int q = 0; q < KBLK; q += 2) {
+            const uint64_t t0 = tp[b * KBLK + q], t1 = tp[b * KBLK + q + 1];
+            dd[q / 2] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+        }
+        dd[4] = make_uint4(ch[b * KBLK], ch[b * KBLK + 1], ch[b * KBLK + 2], ch[b * KBLK + 3]);
+        dd[5] = make_uint4(ch[b * KBLK + 4], ch[b * KBLK + 5], ch[b * KBLK + 6], ch[b * KBLK + 7]);
+    }
+}
 
-// snapshot pass B: bucket m = 159 .. endIndex of every owned node -- up to k members of T_m (the
-// nodes at msb(x ^ v) = m, one contiguous index range [flo, fhi) of the sorted keys) minus the
-// node's siblings, chosen by Floyd sampling with kad_hash(seed, v, m, j) (snapshot rule, DESIGN.md
-// §4), in ascending index order.  One lane per (node, bucket): consecutive lanes write consecutive
-// KadBlks of the row, so every store is a coalesced run; T_m comes from two prefix searches over
-// the whole sorted array (their top levels are shared by every lane and stay in the caches), and
-// the c-th non-sibling member is found without scanning T_m.  Only bucket endIndex can hold
-// siblings (siblings lie at levels <= endIndex).  Same blocks as kad_bucket_fill (k_kad_top_buckets).
+// snapshot pass B: the buckets m = 159 .. endIndex + 1 of every owned node, one lane per (node,
+// bucket): consecutive lanes write consecutive KadBlks of a row (coalesced runs), and a lane's
+// dependent chain is the node line, the prefix table, the members' tops.  The bucket endIndex
+// (sibling exclusion: a scan of the 5s siblings per member) runs in k_kad_bucket_sib, one lane per
+// node -- inside this kernel its two lanes a wave would hold every wave for the scans.
 template <int KC>
 __global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restrict__ recs,
                                                           const uint64_t* __restrict__ tops,
+                                                          const uint32_t* __restrict__ tab, int D,
                                                           const KadNode* __restrict__ nodes, uint32_t n, int k, int S5,
                                                           uint64_t seed, const uint32_t* __restrict__ sib,
                                                           KadBlk* __restrict__ blks, uint32_t own_lo, uint32_t own_hi)
@@ -311,95 +539,94 @@ __global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restric
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     const K160 me = as_key(r.key);
-    const int bpb = (k + KBLK - 1) / KBLK;
-    const uint32_t* L = sib + (uint64_t)v * S5;
-    for (int m = KEYBITS - 1 - lane; m >= endIndex; m -= KB_LANES) {
-        // T_m: the prefix of bits m..159 equal to the node's with bit m flipped
-        K160 Q = me;
-#pragma unroll
-        for (int w = 0; w < 5; ++w) Q.w[w] ^= (m >> 5) == w ? 1u << (m & 31) : 0u;   // selects: no scratch
-        const bool below = kbit(me, m) != 0;     // T_m lies below v in the sorted order
-        const uint32_t flo = kad_prefix_bound(recs, tops, below ? 0u : v + 1, below ? v : n, m, Q, false);
-        const uint32_t fhi = kad_prefix_bound(recs, tops, flo, below ? v : n, m, Q, true);
-        uint32_t nsin = 0;
-        if (m == endIndex)
-            for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
-        const uint32_t c = (fhi - flo) - nsin;
-        // Floyd sampling of min(k, c) ranks out of c, then ascending
-        uint32_t ch[KC];
-#pragma unroll
-        for (int i = 0; i < KC; ++i) {
-            uint32_t t = NONE;
-            if (i < k && (uint32_t)i < c) {
-                if (c <= (uint32_t)k) {
-                    t = (uint32_t)i;
-                } else {
-                    const uint32_t j = c - (uint32_t)k + (uint32_t)i;
-                    t = (uint32_t)(kad_hash(seed, v, (uint32_t)m, j) % (uint64_t)(j + 1));
-                    bool dup = false;
-#pragma unroll
-                    for (int q = 0; q < i; ++q) dup |= ch[q] == t;
-                    t = dup ? j : t;
-                }
-            }
-            ch[i] = t;
-        }
-#pragma unroll
-        for (int a = 0; a < KC; ++a)          // odd-even transposition sort (NONE = the largest)
-#pragma unroll
-            for (int b = a & 1; b + 1 < KC; b += 2) {
-                const uint32_t x = ch[b], y = ch[b + 1];
-                ch[b] = x < y ? x : y;
-                ch[b + 1] = x < y ? y : x;
-            }
-        // rank -> node: flo + rank, stepped over the siblings inside T_m (least fixed point of
-        // x = flo + rank + #{siblings in [flo, x]})
-        if (nsin) {
-#pragma unroll
-            for (int q = 0; q < KC; ++q) {
-                if (ch[q] == NONE) continue;
-                const uint32_t base = flo + ch[q];
-                uint32_t x = base;
-                for (;;) {
-                    uint32_t cs = 0;
-                    for (int i = 0; i < S5; ++i) cs += (L[i] != NONE && L[i] >= flo && L[i] <= x) ? 1u : 0u;
-                    if (base + cs == x) break;
-                    x = base + cs;
-                }
-                ch[q] = x;
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < KC; ++q) ch[q] = ch[q] == NONE ? NONE : flo + ch[q];
-        }
-        uint64_t tp[KC];
-#pragma unroll
-        for (int q = 0; q < KC; ++q) tp[q] = ch[q] == NONE ? ~0ull : tops[ch[q]];
-        KadBlk* B = blks + (uint64_t)r.boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb;
-#pragma unroll
-        for (int b = 0; b < KC / KBLK; ++b) {
-            if (b >= bpb) break;
-            uint4* d = reinterpret_cast<uint4*>(B + b);
-#pragma unroll
-            for (int q = 0; q < KBLK; q += 2) {
-                const uint64_t t0 = tp[b * KBLK + q], t1 = tp[b * KBLK + q + 1];
-                d[q / 2] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
-            }
-            d[4] = make_uint4(ch[b * KBLK], ch[b * KBLK + 1], ch[b * KBLK + 2], ch[b * KBLK + 3]);
-            d[5] = make_uint4(ch[b * KBLK + 4], ch[b * KBLK + 5], ch[b * KBLK + 6], ch[b * KBLK + 7]);
-        }
-    }
+    for (int m = KEYBITS - 1 - lane; m > endIndex; m -= KB_LANES)
+        kad_bucket_row<KC, false>(recs, tops, tab, D, n, k, S5, seed, nullptr, blks, v, me, r.boff, m);
 }
 
-// the owned nodes' sibling rows
-__global__ void k_kad_sib_rows(const KeyRec* __restrict__ recs, const KadNode* __restrict__ nodes, int S5, int sbn,
-                               const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks, uint64_t sib_base,
-                               uint32_t own_lo, uint32_t own_hi)
+template <int KC>
+__global__ __launch_bounds__(KS_BLOCK) void k_kad_bucket_sib(const KeyRec* __restrict__ recs,
+                                                              const uint64_t* __restrict__ tops,
+                                                              const uint32_t* __restrict__ tab, int D,
+                                                              const KadNode* __restrict__ nodes, uint32_t n, int k,
+                                                              int S5, uint64_t seed, const uint32_t* __restrict__ sib,
+                                                              KadBlk* __restrict__ blks, uint32_t own_lo,
+                                                              uint32_t own_hi)
 {
-    const uint32_t v = own_lo + blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t lsb[KS_BLOCK * KS_STRIDE];
+    const uint32_t v0 = own_lo + blockIdx.x * KS_BLOCK;
+    ks_load_rows(lsb, sib, v0, min((uint32_t)KS_BLOCK, own_hi - v0), S5);
+    const uint32_t v = v0 + threadIdx.x;
     if (v >= own_hi) return;
-    put_sibling_row(blks, sib_base + (uint64_t)(v - own_lo) * sbn, sbn, sib + (uint64_t)v * S5, S5, v,
-                    as_key(nodes[v].key), recs);
+    const KadNode r = nodes[v];
+    const int endIndex = kad_end(r.meta);
+    if (endIndex < 0) return;
+    kad_bucket_row<KC, true>(recs, tops, tab, D, n, k, S5, seed, lsb + threadIdx.x * KS_STRIDE, blks, v, as_key(r.key),
+                             r.boff, endIndex);
+}
+
+// the owned nodes' sibling rows (put_sibling_row's layout): the node, then its siblings stable by
+// level msb(x ^ v) -- levels computed once (top 64 bits, the full keys on a tie) and kept in LDS,
+// the row emitted one level at a time (a handful of distinct levels) instead of an insertion sort
+// through scratch
+__global__ __launch_bounds__(KS_BLOCK) void k_kad_sib_rows(const KeyRec* __restrict__ recs,
+                                                            const uint64_t* __restrict__ tops,
+                                                            const KadNode* __restrict__ nodes, int S5, int sbn,
+                                                            const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks,
+                                                            uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
+{
+    __shared__ uint8_t lev[64][KS_BLOCK];
+    __shared__ uint32_t lsb[KS_BLOCK * KS_STRIDE];
+    const uint32_t v0 = own_lo + blockIdx.x * KS_BLOCK;
+    ks_load_rows(lsb, sib, v0, min((uint32_t)KS_BLOCK, own_hi - v0), S5);
+    const uint32_t v = v0 + threadIdx.x;
+    if (v >= own_hi) return;
+    const uint32_t* L = lsb + threadIdx.x * KS_STRIDE;
+    const uint64_t mt = tops[v];
+    int lmin = 255, cnt = 0;
+    for (int i = 0; i < S5 && i < 64; ++i) {
+        const uint32_t x = L[i];
+        int l = 255;
+        if (x != NONE) {
+            const uint64_t d = tops[x] ^ mt;
+            l = d ? 96 + (63 - __clzll((long long)d)) : k_msb(k_xor(kload(recs, x), kload(recs, v)));
+            lmin = min(lmin, l);
+            ++cnt;
+        }
+        lev[i][threadIdx.x] = (uint8_t)l;
+    }
+    const uint64_t blk0 = sib_base + (uint64_t)(v - own_lo) * sbn;
+    KadBlk* B = blks + blk0;
+    // a block's 8 entries gathered in registers, then written as six 16 B stores
+    uint32_t bx[KBLK];
+    uint64_t bt[KBLK];
+    int q = 0;
+    auto put = [&](uint32_t x) {
+        const int sl = q & (KBLK - 1);
+        const uint64_t tp = x == NONE ? ~0ull : tops[x];
+#pragma unroll
+        for (int j = 0; j < KBLK; ++j)
+            if (j == sl) { bx[j] = x; bt[j] = tp; }
+        if (sl == KBLK - 1) {
+            uint4* d = reinterpret_cast<uint4*>(B + (q >> 3));
+#pragma unroll
+            for (int j = 0; j < KBLK; j += 2)
+                d[j / 2] = make_uint4((uint32_t)bt[j], (uint32_t)(bt[j] >> 32), (uint32_t)bt[j + 1], (uint32_t)(bt[j + 1] >> 32));
+            d[4] = make_uint4(bx[0], bx[1], bx[2], bx[3]);
+            d[5] = make_uint4(bx[4], bx[5], bx[6], bx[7]);
+        }
+        ++q;
+    };
+    put(v);
+    for (int l = lmin; l < 255 && q < cnt + 1;) {
+        int next = 255;
+        for (int i = 0; i < S5 && i < 64; ++i) {
+            const int li = lev[i][threadIdx.x];
+            if (li == l) put(L[i]);
+            else if (li > l) next = min(next, li);
+        }
+        l = next;
+    }
+    while (q < sbn * KBLK) put(NONE);
 }
 
 // sharded networks (KadTables::tl > 0): the top tl buckets m = 159 .. 160 - tl of EVERY node, at
@@ -672,6 +899,7 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     const uint32_t nown = hi - lo;
     uint64_t *rowlen = nullptr, *off = nullptr;
     uint32_t* sib_all = nullptr;
+    uint64_t* tops = nullptr;
     void* tmp = nullptr;
     size_t tmpb = 0;
     auto cleanup = [&]() {
@@ -679,6 +907,7 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
         if (off) hipFree(off);
         if (tmp) hipFree(tmp);
         if (sib_all) hipFree(sib_all);
+        if (tops) hipFree(tops);
     };
     // node lines for the whole network (a lookup needs every target's summary when it sends the
     // call); sibling lists are a build temporary
@@ -687,8 +916,20 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     if ((e = hipMalloc(&sib_all, sizeof(uint32_t) * (uint64_t)n * S5)) != hipSuccess) return e;
     if ((e = hipMalloc(&rowlen, sizeof(uint64_t) * (n + 1))) != hipSuccess) { cleanup(); return e; }
     if ((e = hipMalloc(&off, sizeof(uint64_t) * (n + 1))) != hipSuccess) { cleanup(); return e; }
-    hipLaunchKernelGGL(k_kad_siblings, dim3(nblk(n, 128)), dim3(128), 0, st, recs, xy, n, S5, bpb, lo, hi, sib_all,
-                       t.nodes, t.nodex, rowlen);
+    // top-key array (8 B a node) and the prefix tables: read by the sibling, bucket and sibling-row builders
+    int D = 1;
+    while (D < KB_DMAX && (1ull << D) < 2ull * n) ++D;
+    if ((e = hipMalloc(&tops, sizeof(uint64_t) * n + sizeof(uint32_t) * kb_tab_off(D + 1))) != hipSuccess) {
+        cleanup();
+        return e;
+    }
+    uint32_t* tab = reinterpret_cast<uint32_t*>(tops + n);
+    hipLaunchKernelGGL(k_kad_tops, dim3(nblk(n, 256)), dim3(256), 0, st, recs, n, tops);
+    hipLaunchKernelGGL(k_kad_prefix_tables, dim3(nblk(n, 256)), dim3(256), 0, st, tops, n, D, tab);
+    int dg = 0;                                    // log2(n / (5s + 1)): the typical sibling-block depth
+    while (dg < D && ((uint64_t)n >> (dg + 1)) >= (uint64_t)S5 + 1) ++dg;
+    hipLaunchKernelGGL(k_kad_siblings, dim3(nblk(n, KS_BLOCK)), dim3(KS_BLOCK), 0, st, recs, xy, n, S5, bpb, lo, hi, tops, tab, D,
+                       dg, sib_all, t.nodes, t.nodex, rowlen);
     hipMemsetAsync(rowlen + n, 0, sizeof(uint64_t), st);
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmpb, rowlen, off, n + 1, st);
     if ((e = hipMalloc(&tmp, tmpb)) != hipSuccess) { cleanup(); return e; }
@@ -708,22 +949,22 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     hipLaunchKernelGGL(k_kad_set_boff, dim3(nblk(n, 256)), dim3(256), 0, st, t.nodes, off, lo, hi, tend, n);
     if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)nown * S5)) != hipSuccess) { cleanup(); return e; }
     hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5, hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, 128)), dim3(128), 0, st, recs, t.nodes, S5, sbn, sib_all,
-                       t.blks, t.rows_blks, lo, hi);
     {
-        uint64_t* tops = nullptr;
-        if ((e = hipMalloc(&tops, sizeof(uint64_t) * n)) != hipSuccess) { cleanup(); return e; }
-        hipLaunchKernelGGL(k_kad_tops, dim3(nblk(n, 256)), dim3(256), 0, st, recs, n, tops);
-        const dim3 grid((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256));
-        if (k <= KBLK)
-            hipLaunchKernelGGL(k_kad_bucket_rows<KBLK>, grid, dim3(256), 0, st, recs, tops, t.nodes, n, k, S5, seed,
+        hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, KS_BLOCK)), dim3(KS_BLOCK), 0, st, recs, tops, t.nodes, S5,
+                           sbn, sib_all, t.blks, t.rows_blks, lo, hi);
+        const dim3 grid((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256)), blk(256);
+        const dim3 grid1(nblk(nown, KS_BLOCK)), blk1(KS_BLOCK);
+        if (k <= KBLK) {
+            hipLaunchKernelGGL(k_kad_bucket_rows<KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, n, k, S5, seed,
                                sib_all, t.blks, lo, hi);
-        else
-            hipLaunchKernelGGL(k_kad_bucket_rows<2 * KBLK>, grid, dim3(256), 0, st, recs, tops, t.nodes, n, k, S5,
+            hipLaunchKernelGGL(k_kad_bucket_sib<KBLK>, grid1, blk1, 0, st, recs, tops, tab, D, t.nodes, n, k, S5, seed,
+                               sib_all, t.blks, lo, hi);
+        } else {
+            hipLaunchKernelGGL(k_kad_bucket_rows<2 * KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, n, k, S5,
                                seed, sib_all, t.blks, lo, hi);
-        e = hipStreamSynchronize(st);
-        hipFree(tops);
-        if (e != hipSuccess) { cleanup(); return e; }
+            hipLaunchKernelGGL(k_kad_bucket_sib<2 * KBLK>, grid1, blk1, 0, st, recs, tops, tab, D, t.nodes, n, k, S5,
+                               seed, sib_all, t.blks, lo, hi);
+        }
     }
     if (tl > 0)
         hipLaunchKernelGGL(k_kad_top_buckets, dim3(nblk(n, 64)), dim3(64), 0, st, recs, t.nodes, n, k, S5, seed, sib_all,

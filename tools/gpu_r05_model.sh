@@ -31,3 +31,20 @@ for tag in ${AB:-}; do
   OVS_LIB=$PWD/oversim_amd/libovs_kbr_$tag.so timeout -k 10 600 python3 -u tools/diag/shard_w8_model.py --workload C > $O/ab_$tag.out 2> $O/ab_$tag.err || { tail -20 $O/ab_$tag.err; exit 1; }
   echo "$tag: $(grep summary $O/ab_$tag.out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(max(d["step_ms_per_rank"]), d["rounds"])')"
 done
+# buildab: the 2^24 Kademlia build on each oversim_amd/libovs_kbr_<tag>.so named in BUILDAB (kernel trace)
+for tag in ${BUILDAB:-}; do
+  OVS_LIB=$PWD/oversim_amd/libovs_kbr_$tag.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/build_$tag -o b -- python3 -u tools/diag/kad_build_time.py --reps 2 > $O/build_$tag.out 2>&1 || { tail -20 $O/build_$tag.out; exit 1; }
+  grep tables_sha $O/build_$tag.out
+done
+# buildpmc: kernel trace + SQ / FETCH / WRITE passes of the 2^24 Kademlia build (summary.txt)
+if [ "${BUILDPMC:-0}" = 1 ]; then
+  P=$O/buildpmc; mkdir -p $P
+  A="tools/diag/kad_build_time.py --reps 1 --check-nodes 4096"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $P/kt -o run -- python3 -u $A > $P/kt.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD -d $P/sq -o run -- python3 -u $A > $P/sq.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- python3 -u $A > $P/fetch.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- python3 -u $A > $P/write.log 2>&1
+  python3 tools/prof_summary.py $P k_kad > $P/summary.txt
+  rm -rf $P/kt $P/sq $P/fetch $P/write
+  grep -E "bucket_rows|sib_rows|k_kad_siblings" $P/summary.txt | cut -c1-200
+fi
