@@ -574,13 +574,11 @@ __global__ __launch_bounds__(KS_BLOCK) void k_kad_sib_rows(const KeyRec* __restr
                                                             const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks,
                                                             uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
 {
+    // (the lists read from HBM here: staged through LDS the kernel ran at 2 waves/SIMD, 1.8x slower)
     __shared__ uint8_t lev[64][KS_BLOCK];
-    __shared__ uint32_t lsb[KS_BLOCK * KS_STRIDE];
-    const uint32_t v0 = own_lo + blockIdx.x * KS_BLOCK;
-    ks_load_rows(lsb, sib, v0, min((uint32_t)KS_BLOCK, own_hi - v0), S5);
-    const uint32_t v = v0 + threadIdx.x;
+    const uint32_t v = own_lo + blockIdx.x * KS_BLOCK + threadIdx.x;
     if (v >= own_hi) return;
-    const uint32_t* L = lsb + threadIdx.x * KS_STRIDE;
+    const uint32_t* L = sib + (uint64_t)v * S5;
     const uint64_t mt = tops[v];
     int lmin = 255, cnt = 0;
     for (int i = 0; i < S5 && i < 64; ++i) {
