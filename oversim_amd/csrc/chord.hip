@@ -560,6 +560,22 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
 
     __shared__ uint4 xbuf[4][256];    // per wave: the 64 gathered lines, 4 chunks each
     uint4* const xb = xbuf[threadIdx.x >> 6];
+    // shard: the arcs' bounds in LDS and this rank's in registers -- a next hop's owner was a loop
+    // of global reads of shard_lo per hop (most hops stay on the arc: one compare)
+    __shared__ uint32_t sbnd[SHARD ? MAXSHARDS + 1 : 1];
+    uint32_t arc_lo = 0, arc_hi = 0;
+    if (SHARD) {
+        for (int i = threadIdx.x; i <= io.nsh && i <= MAXSHARDS; i += blockDim.x) sbnd[i] = (uint32_t)io.shard_lo[i];
+        __syncthreads();
+        arc_lo = sbnd[io.me];
+        arc_hi = sbnd[io.me + 1];
+    }
+    auto owner = [&](uint32_t c) -> int {
+        if (c >= arc_lo && c < arc_hi) return io.me;
+        int r = 0;
+        for (int i = 1; i < io.nsh; ++i) r += c >= sbnd[i] ? 1 : 0;
+        return r;
+    };
 
     // Lookups started from their key and source (the single-GPU route): the sources of the wave's
     // next 64 candidates are preloaded one per lane, so a refilled lane has its source at once and
@@ -679,7 +695,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             // responder already reached (its response accounted here), which decides there
             auto redo_hand = [&]() {
                 store_lrec(io.stage_hand, q, K, S, cur, qid, t, hops, 2);
-                io.stag[q] = (uint8_t)shard_owner(io.shard_lo, io.nsh, cur);
+                io.stag[q] = (uint8_t)owner(cur);
                 active = false;
                 lp = nullptr;
             };
@@ -822,7 +838,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
                     fin = true; status = OVS_LOOKUP_NO_NEXT; return false;                             // visitOnlyOnce
                 }
                 if (SHARD) {
-                    const int dest = shard_owner(io.shard_lo, io.nsh, nx);
+                    const int dest = owner(nx);
                     remote = false;
                     // an off-arc responder reached through a finger entry (its header in A) whose first
                     // probe lies in the replicated top levels -- or which is the key's node, decided

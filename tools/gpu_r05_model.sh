@@ -48,3 +48,17 @@ if [ "${BUILDPMC:-0}" = 1 ]; then
   rm -rf $P/kt $P/sq $P/fetch $P/write
   grep -E "bucket_rows|sib_rows|k_kad_siblings" $P/summary.txt | cut -c1-200
 fi
+# toplev: the C model at each replicated-level count in TOPLEV
+for L in ${TOPLEV:-}; do
+  timeout -k 10 600 python3 -u tools/diag/shard_w8_model.py --workload C --top-levels $L > $O/c_top$L.out 2> $O/c_top$L.err || { tail -20 $O/c_top$L.err; exit 1; }
+  echo "top $L: $(grep summary $O/c_top$L.out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(max(d["step_ms_per_rank"]), d["rounds"])')"
+done
+# cpmc: SQ counters of the C model's kernels (the shard step K1 against the single-context check route)
+if [ "${CPMC:-0}" = 1 ]; then
+  P=$O/cpmc; mkdir -p $P
+  timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD -d $P/sq -o run -- python3 -u tools/diag/shard_w8_model.py --workload C > $P/sq.log 2>&1
+  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- python3 -u tools/diag/shard_w8_model.py --workload C > $P/fetch.log 2>&1
+  python3 tools/prof_summary.py $P k_chord_lanes > $P/summary.txt
+  rm -rf $P/sq $P/fetch
+  grep -E "k_chord_lanes" $P/summary.txt | cut -c1-220
+fi
