@@ -56,6 +56,12 @@ t_start = time.time()
 if mig:
     tl = 3 if a.top_levels is None else a.top_levels
     steppers = [KadMigStepper(ids, xy, bounds, r, dev, params=params, top_levels=tl, capacity=Wn * m) for r in range(Wn)]
+    # warm-up: one step of 256 lookups per arc (first-use allocations of the staging buffers)
+    for r in range(Wn):
+        steppers[r].step(steppers[r].first_batch(inputs[r]["keys_t"][:256], inputs[r]["src_t"][:256], r * m))
+    torch.cuda.synchronize()
+    for st in steppers:
+        st.reset(Wn * m)
     inbox = [steppers[r].first_batch(inputs[r]["keys_t"], inputs[r]["src_t"], r * m) for r in range(Wn)]
     kad = False          # the record loop below (as Chord's)
 elif kad:
