@@ -656,8 +656,28 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
                         lp = nullptr;          // PH_FETCH reports the source outside the ring
                     }
                 } else if (SHARD) {
-                    // the 48 B hand-off record comes through the cooperative gather (tag 1: 3 chunks)
-                    lp = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(io.in + q) | 1u);
+                    // the 48 B hand-off record, read here (a wave's records are consecutive: coalesced
+                    // 16 B loads) so that its responder's line is requested in this refill iteration --
+                    // through the cooperative gather it took an iteration of its own
+                    const uint4* rp = reinterpret_cast<const uint4*>(io.in + q);
+                    const uint4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+                    K.w[0] = r0.x; K.w[1] = r0.y; K.w[2] = r0.z; K.w[3] = r0.w; K.w[4] = r1.x;
+                    S = r1.y; cur = r1.z; qid = r1.w;
+                    t = (int64_t)u64(r2.x, r2.y);
+                    hops = (int)(r2.z & 0xFFFF);
+                    const uint32_t lb = (r2.z >> 16) & 0xFF;
+                    local = lb == 1;
+                    redo = lb == 2;
+                    if (S < V.n && cur < V.n) {
+                        if (!REC) {
+                            const double2 sxy = V.xy[S];      // coordinates are replicated on every rank
+                            sx = sxy.x; sy = sxy.y;
+                        }
+                        lp = reinterpret_cast<const uint4*>(V.nodes + cur);
+                        ph = PH_START;
+                    } else {
+                        lp = nullptr;          // PH_FETCH finishes it as BROKEN
+                    }
                 } else {
                     K = io.qkeys[q];
                     S = io.qsrc[q];
@@ -713,17 +733,8 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             // ---- consume the pending line
             if (ph == PH_FETCH) {
                 if (SHARD) {
-                    if (io.fkeys) {
-                        cur = S; t = 0; hops = 0; local = true;
-                    } else {
-                        K.w[0] = L0.x; K.w[1] = L0.y; K.w[2] = L0.z; K.w[3] = L0.w; K.w[4] = L1.x;
-                        S = L1.y; cur = L1.z; qid = L1.w;
-                        t = (int64_t)u64(L2.x, L2.y);
-                        hops = (int)(L2.z & 0xFFFF);
-                        const uint32_t lb = (L2.z >> 16) & 0xFF;
-                        local = lb == 1;
-                        redo = lb == 2;
-                    }
+                    // (a received record was decoded at the refill: only an invalid one gets here)
+                    if (io.fkeys) { cur = S; t = 0; hops = 0; local = true; }
                     if (S >= V.n || cur >= V.n) {
                         // a row the exchange never wrote (receive buffers are 0xFF-filled) or a corrupted
                         // record: finished as BROKEN with its qid (0xFFFFFFFF for the sentinel), which
