@@ -7,7 +7,10 @@ namespace ovs {
 
 namespace {
 
-constexpr int CT_STEPS = 16;                 // one wave per tile, 16 elements per lane
+#ifndef OVS_CT_STEPS
+#define OVS_CT_STEPS 16
+#endif
+constexpr int CT_STEPS = OVS_CT_STEPS;         // one wave per tile, CT_STEPS elements per lane
 constexpr uint64_t CT_TILE = 64 * CT_STEPS;
 
 __device__ __forceinline__ uint8_t tag_at(const uint8_t* __restrict__ tags, uint64_t n, uint64_t e)
