@@ -457,8 +457,9 @@ def main():
             cfg.update({"hop_rounds": sh.rounds,
                         "round_loop": "C++ (ovs_shard_route_batch)" if getattr(sh, "native", False) else "python",
                         "shard_stats_rank0": getattr(sh, "stats", None)})
-            if kind == "chord":
-                cfg["replicated_top_levels"] = sh.stepper.top_levels
+            cfg["replicated_top_levels"] = getattr(sh.stepper, "top_levels", 0)
+            if kind == "kademlia":
+                cfg["lookups_migrate"] = bool(getattr(sh.stepper, "top_levels", 0))
         line = {
             "metric": "routed lookup hops/sec (whole node)",
             "value": value,

@@ -1082,10 +1082,16 @@ class ShardedKademlia:
     """bench.py driver for one rank: Kademlia arc + lookups resident in HBM + request/response exchange
     (the round loop in C++, ovs_kad_shard_route_batch, unless OVS_SHARD_PYLOOP=1)."""
 
-    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None, native=None):
+    def __init__(self, rank, world, ids, xy, keys_t, src_t, device, comm_dev=None, params=None, native=None,
+                 top_levels=None):
         import os
         self.bounds = arc_bounds(len(ids), world)
-        self.stepper = KadShardStepper(ids, xy, self.bounds, rank, device, params=params)
+        # one-way routes on W > 1 arcs migrate over replicated top buckets (3 levels; the W = 8 E model:
+        # 8.4 ms per arc against 32.8 ms with request/response rounds); OVS_KAD_TOP_LEVELS=0 keeps the
+        # request/response rounds
+        if top_levels is None:
+            top_levels = int(os.environ.get("OVS_KAD_TOP_LEVELS", "3")) if world > 1 else 0
+        self.stepper = KadShardStepper(ids, xy, self.bounds, rank, device, params=params, top_levels=top_levels)
         self.stepper.timing = True
         self.native = (os.environ.get("OVS_SHARD_PYLOOP") != "1") if native is None else native
         if self.native:
