@@ -439,6 +439,8 @@ def main():
         cfg = {"workload": wl["desc"], "overlay": kind, "nodes_total": n_total, "lookups_per_gpu": m,
                "hopCountMax": 50,
                "parallelism": ((f"ring sharded over {world} GPUs ({xname} all-to-allv per hop round)" if kind == "chord"
+                                else (f"ID arcs over {world} GPUs, lookups migrate between arcs ({xname} all-to-allv "
+                                      "per round)") if getattr(sh.stepper, "top_levels", 0)
                                 else f"ID arcs over {world} GPUs, FindNodeCall request/response {xname} all-to-allv per round")
                                if sharded else ("replicas" if world > 1 else "1 GPU")),
                "lookups_per_s": ok_all * a.steps / wall_max, "mean_hops": hop_all / max(ok_all, 1),
