@@ -879,7 +879,9 @@ def _native_gloo_body(rank, world, port, q, kind):
         st.reset(world * m)
         done, stats = native_route(st, cx.ex, kt, st_, rank * m, cohorts=2)
     else:
-        st = KadShardStepper(net.ids, net.xy, bounds, rank, dev, params=Params.kademlia())
+        # kademlia_mig: replicated top buckets, the one-way lookups migrate between the two processes
+        st = KadShardStepper(net.ids, net.xy, bounds, rank, dev, params=Params.kademlia(),
+                             top_levels=3 if kind == "kademlia_mig" else 0)
         done, stats = native_kad_route(st, cx.ex, kt, st_, rank * m)
     q.put((rank, done_to_numpy(done), k, s, int(stats.rounds)))
     dist.barrier()
@@ -887,7 +889,7 @@ def _native_gloo_body(rank, world, port, q, kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["chord", "kademlia"])
+@pytest.mark.parametrize("kind", ["chord", "kademlia", "kademlia_mig"])
 def test_native_round_loop_gloo_two_processes(kind):
     """The native loop over a caller-supplied exchange: Python callbacks running torch.distributed
     gloo collectives (CallbackExchange), two processes sharing the GPU."""
@@ -922,6 +924,7 @@ def test_native_round_loop_gloo_two_processes(kind):
     net = W.population(1 << 14, 0x5E)
     keys, src = np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res])
     ref = _single_gpu_reference(net, keys, src) if kind == "chord" else _kad_reference(net, keys, src, Params.kademlia())
+    # (kademlia_mig: lookups that migrate finish on either rank; the qids cover the batch once)
     for f in ROUTE_FIELDS:
         assert np.array_equal(d[f].astype(np.int64), ref[f].astype(np.int64)), f
 
