@@ -441,6 +441,12 @@ __device__ __forceinline__ const KadBlk* slot_blk(const KadView& V, uint32_t bof
 // level-sorted row can enter the result (kad_sib_prefix); the rest are counted, not read.
 // r0 > 0: the entries before row entry r0 cannot enter the result either (kad_sib_range: the
 // siblings at level m alone fill it); they are counted, not read.
+// KAD_FN_HOOK(kind): a census build's count of the table blocks one findNode reads -- kind 0 bucket
+// m, 1 the buckets m-1 .. endIndex, 2 sibling-row blocks, 3 buckets above m (a translation unit
+// defines it before including this header; nothing by default)
+#ifndef KAD_FN_HOOK
+#define KAD_FN_HOOK(kind) ((void)0)
+#endif
 template <bool EX, int C = 8>
 __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, const RespGeo& g, const K160& K,
                                                  int numRedundant, bool sib, BlkN<C>& res, int numSiblings = 1,
@@ -488,6 +494,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
     auto add_slot = [&](int bucket) {
         if (g.rowlo < 0 || bucket < g.rowlo) return;      // buckets below the stored row are empty
         const KadBlk* blk = slot_blk(V, g.boff, bucket);
+        KAD_FN_HOOK(bucket == g.m ? 0 : bucket < g.m ? 1 : 3);
         // the 8-entry instantiations run only on tables with k <= 8 (one block per bucket; the
         // launchers pick C = 16 otherwise)
         if constexpr (C == 8) add_blk(blk);
@@ -504,7 +511,7 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
         const int tot = g.nsib + 1;
         const int rd = pre < 0 ? tot : min(tot, kad_row_read(pre));
         const int j0 = r0 / KBLK;
-        for (int j = j0; j * KBLK < rd; ++j) add_blk(L + j);
+        for (int j = j0; j * KBLK < rd; ++j) { KAD_FN_HOOK(2); add_blk(L + j); }
         seen += tot - (rd - j0 * KBLK);
     }
     for (int b = g.m + 1; seen < rs && b < KEYBITS; ++b) add_slot(b);

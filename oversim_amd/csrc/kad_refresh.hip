@@ -22,7 +22,22 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdio>
 #include <mutex>
+
+#include <hip/hip_runtime.h>
+
+#ifdef OVS_KX_STATS
+// census build (-DOVS_KX_STATS): what one K2x launch reads and writes, by kind (kad_exhaustive
+// prints the counts to stderr as "kxstats ...")
+namespace ovs {
+__device__ unsigned long long g_kx_stats[16];
+}
+#define KAD_FN_HOOK(kind) atomicAdd(&::ovs::g_kx_stats[4 + (kind)], 1ull)
+#define KX_STAT(i, v) atomicAdd(&::ovs::g_kx_stats[i], (unsigned long long)(v))
+#else
+#define KX_STAT(i, v) ((void)0)
+#endif
 
 #include "kad_dev.hpp"
 
@@ -343,8 +358,10 @@ struct XCtx {
         if (x == L.S) return true;
         if (!L.any_to) return false;
         const int t = (int)(threadIdx.x);
-        for (int i = 0; i < L.nhop; ++i)
+        for (int i = 0; i < L.nhop; ++i) {
+            KX_STAT(11, (C.lvis && i < KXVL) ? 0 : 1);
             if ((C.lvis && i < KXVL ? vis[i][t] : resp[i]) == x) return true;
+        }
         return false;
     }
 
@@ -368,6 +385,7 @@ struct XCtx {
         if (slot < 0) { L.err = true; return; }
         int64_t d1 = 0, d2 = 0;
         if (x != L.S) {                         // SimpleUDP delivers to itself without delay
+            KX_STAT(3, 1);
             const KadNode rr = load_node(V.nodes, x);
             const int rn = find_node_size(x, resp_geo(rr, L.K), C.R);
             const int64_t cd = coord_ns(L.sx, L.sy, rr.x, rr.y, DC.round);
@@ -404,6 +422,7 @@ struct XCtx {
         }
         L.pvalid |= 1u << slot;
         ++L.nsent;
+        KX_STAT(12, 1);
     }
 
     // IterativePathLookup::sendRpc (1067-1170), exhaustive
@@ -429,6 +448,7 @@ struct XCtx {
             // the numSiblings-sized vector has room (1147-1156, 436-440)
             int m = L.nnh < C.R ? L.nnh : C.R;
             m = m < C.ns ? m : C.ns;
+            KX_STAT(10, m);
             if constexpr (REG) {
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
@@ -516,6 +536,7 @@ struct XCtx {
         L.pvalid &= ~(1u << e);
         L.now = bt;
         if (cur.to) {
+            KX_STAT(13, 1);
             L.any_to = true;                 // setDead(dest)
             if (L.nd < XMAXDEAD) X.dead[at(L.nd++)] = cur.node;
             else { L.err = true; return true; }
@@ -553,8 +574,8 @@ struct XCtx {
                     if (cur.node != L.S) {
                         if (L.nhop < C.hcm) {
                             if (C.lvis && L.nhop < KXVL) vis[L.nhop][threadIdx.x] = cur.node;
-                            else resp[L.nhop] = cur.node;
-                            if (rtt) rtt[L.nhop] = L.now - cur.tsend;
+                            else { resp[L.nhop] = cur.node; KX_STAT(8, 1); }
+                            if (rtt) { rtt[L.nhop] = L.now - cur.tsend; KX_STAT(9, 1); }
                             if constexpr (TR) tarr[L.nhop] = L.now;
                         }
                         ++L.nhop;
@@ -567,6 +588,8 @@ struct XCtx {
             if (merge) {
                 // the responder's findNode (the source's own at the start) into nextHops (2R)
                 const KadNode rn = load_node(V.nodes, cur.node);
+                KX_STAT(2, 1);
+                KX_STAT(1, R.start ? 0 : 1);
                 const RespGeo g = resp_geo(rn, L.K);
                 const int rs = R.start ? C.k : C.R;
                 int numNew = 0, cnt = 0;
@@ -637,6 +660,8 @@ __device__ __forceinline__ void kx_init_lookup(XLookup<XA>& L, const KadView& V,
     }
     uint32_t* sib = sib_out + q * (uint64_t)C.ns;
     for (int j = 0; j < C.ns; ++j) sib[j] = NONE;
+    KX_STAT(0, 1);
+    KX_STAT(10, C.ns);
 }
 
 // SendToKeyListener / LookupResponse fields of a finished lookup (as ovs_lookup_batch; the
@@ -960,6 +985,18 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     const hipError_t e2 = hipStreamSynchronize(st);
     if (e == hipSuccess) e = e2;
     *capacity_error = herr != 0;
+#ifdef OVS_KX_STATS
+    {
+        unsigned long long s[16] = {};
+        hipMemcpyFromSymbol(s, HIP_SYMBOL(g_kx_stats), sizeof(s));
+        fprintf(stderr,
+                "kxstats lookups=%llu responses=%llu node_handle=%llu node_send=%llu blk_main=%llu blk_lower=%llu "
+                "blk_row=%llu blk_higher=%llu resp_w=%llu rtt_w=%llu sib_w=%llu vis_r=%llu rpcs=%llu timeouts=%llu\n",
+                s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13]);
+        const unsigned long long z[16] = {};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_kx_stats), z, sizeof(z));
+    }
+#endif
     return e;
 }
 
