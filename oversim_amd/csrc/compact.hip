@@ -7,11 +7,11 @@ namespace ovs {
 
 namespace {
 
-#ifndef OVS_CT_STEPS
-#define OVS_CT_STEPS 16
-#endif
-constexpr int CT_STEPS = OVS_CT_STEPS;         // one wave per tile, CT_STEPS elements per lane
+// one wave per tile of CT_STEPS elements per lane: 8 measured 0.34 ms against 0.41 for 16 (10M
+// elements at W = 8's tag mix, tools/diag/compact_bench.hip, profiles/r05_cbench)
+constexpr int CT_STEPS = 8;
 constexpr uint64_t CT_TILE = 64 * CT_STEPS;
+constexpr int CT_BATCH = 4;                     // steps whose record loads precede their stores
 
 __device__ __forceinline__ uint8_t tag_at(const uint8_t* __restrict__ tags, uint64_t n, uint64_t e)
 {
@@ -60,6 +60,11 @@ __global__ void k_compact_base(CPlan P, int nclass, uint64_t nb, const unsigned 
     }
 }
 
+// The tile's ranks first (ballots and the LDS class offsets only), then its copies in batches of
+// CT_BATCH steps whose record loads are all issued before their stores (ranking, loading and
+// storing step by step measured 0.41 ms against 0.34; staging the tile's records in LDS by class
+// to write each class's run as whole lines, 0.40-0.78 ms: 25-50 KB of LDS a wave left too few
+// waves resident).  Records above 48 B (Kademlia migration records) are copied where ranked.
 __global__ __launch_bounds__(64) void k_compact_scatter(const uint8_t* __restrict__ tags, uint64_t n, CPlan P,
                                                         int nclass, uint64_t nb,
                                                         const unsigned long long* __restrict__ scan,
@@ -75,20 +80,20 @@ __global__ __launch_bounds__(64) void k_compact_scatter(const uint8_t* __restric
 #pragma unroll
     for (int k = 0; k < CT_STEPS; ++k) tt[k] = tag_at(tags, n, b * CT_TILE + (uint64_t)k * 64 + lane);
     __syncthreads();
+    long long pos[CT_STEPS];
 #pragma unroll
     for (int k = 0; k < CT_STEPS; ++k) {
-        const uint64_t e = b * CT_TILE + (uint64_t)k * 64 + lane;
         const uint8_t t = tt[k];
         const bool mine = t < nclass;
         uint64_t rem = __ballot(mine);
-        long long pos = -1;
+        long long p = -1;
         // one pass per class present in this group of 64: stable ranks by ballot
         while (rem) {
             const int l0 = __ffsll((long long)rem) - 1;
             const int c = __shfl((int)t, l0);
             const uint64_t m = __ballot(mine && (int)t == c);
             const long long o = off[c];
-            if (mine && (int)t == c) pos = o + (long long)__popcll(m & lt);
+            if (mine && (int)t == c) p = o + (long long)__popcll(m & lt);
             __builtin_amdgcn_wave_barrier();
             if (lane == l0) off[c] = o + (long long)__popcll(m);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -96,22 +101,67 @@ __global__ __launch_bounds__(64) void k_compact_scatter(const uint8_t* __restric
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             rem &= ~m;
         }
-        if (mine) {
-            const CClass C = plan_class(P, t);
-            if (C.dst && pos >= 0 && (uint64_t)pos < C.cap) {
-                const uint8_t* sp = C.src + e * C.src_stride;
-                uint8_t* dp = C.dst + (uint64_t)pos * C.rec_bytes;
-                if (((C.rec_bytes | (uint32_t)C.src_stride | (uint32_t)(uintptr_t)sp | (uint32_t)(uintptr_t)dp) & 15) == 0) {
-                    // 16 B moves (the 48 B hand-off records: 3 per record)
-                    const uint4* s = reinterpret_cast<const uint4*>(sp);
-                    uint4* d = reinterpret_cast<uint4*>(dp);
-                    for (uint32_t w = 0; w < C.rec_bytes / 16; ++w) d[w] = s[w];
-                } else {
-                    const uint2* s = reinterpret_cast<const uint2*>(sp);
-                    uint2* d = reinterpret_cast<uint2*>(dp);
-                    for (uint32_t w = 0; w < C.rec_bytes / 8; ++w) d[w] = s[w];
+        pos[k] = p;
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < CT_STEPS; k0 += CT_BATCH) {
+        uint4 q[CT_BATCH][3];
+        uint8_t* dp[CT_BATCH];
+        int mode[CT_BATCH];     // 0: nothing, 1: 16 B words, 2: 8 B words, 3: copied already (> 48 B)
+        uint32_t nw[CT_BATCH];
+#pragma unroll
+        for (int kk = 0; kk < CT_BATCH; ++kk) {
+            const int k = k0 + kk;
+            const uint64_t e = b * CT_TILE + (uint64_t)k * 64 + lane;
+            const uint8_t t = tt[k];
+            mode[kk] = 0; dp[kk] = nullptr; nw[kk] = 0;
+            if (t < nclass) {
+                const CClass C = plan_class(P, t);
+                if (C.dst && pos[k] >= 0 && (uint64_t)pos[k] < C.cap) {
+                    const uint8_t* sp = C.src + e * C.src_stride;
+                    dp[kk] = C.dst + (uint64_t)pos[k] * C.rec_bytes;
+                    if (C.lab) C.lab[pos[k]] = C.label;
+                    if (C.rec_bytes > 48) {
+                        mode[kk] = 3;
+                        const uint2* s = reinterpret_cast<const uint2*>(sp);
+                        uint2* d = reinterpret_cast<uint2*>(dp[kk]);
+                        for (uint32_t w = 0; w < C.rec_bytes / 8; ++w) d[w] = s[w];
+                    } else if (((C.rec_bytes | (uint32_t)C.src_stride | (uint32_t)(uintptr_t)sp |
+                                 (uint32_t)(uintptr_t)dp[kk]) & 15) == 0) {
+                        // 16 B moves (the 48 B hand-off records: 3 per record)
+                        mode[kk] = 1; nw[kk] = C.rec_bytes / 16;
+                        const uint4* s = reinterpret_cast<const uint4*>(sp);
+#pragma unroll
+                        for (int w = 0; w < 3; ++w)
+                            if ((uint32_t)w < nw[kk]) q[kk][w] = s[w];
+                    } else {
+                        mode[kk] = 2; nw[kk] = C.rec_bytes / 8;
+                        const uint2* s = reinterpret_cast<const uint2*>(sp);
+#pragma unroll
+                        for (int w = 0; w < 6; ++w)
+                            if ((uint32_t)w < nw[kk]) {
+                                const uint2 x = s[w];
+                                if (w & 1) { q[kk][w >> 1].z = x.x; q[kk][w >> 1].w = x.y; }
+                                else { q[kk][w >> 1].x = x.x; q[kk][w >> 1].y = x.y; }
+                            }
+                    }
                 }
-                if (C.lab) C.lab[pos] = C.label;
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < CT_BATCH; ++kk) {
+            if (mode[kk] == 1) {
+                uint4* d = reinterpret_cast<uint4*>(dp[kk]);
+#pragma unroll
+                for (int w = 0; w < 3; ++w)
+                    if ((uint32_t)w < nw[kk]) d[w] = q[kk][w];
+            } else if (mode[kk] == 2) {
+                uint2* d = reinterpret_cast<uint2*>(dp[kk]);
+#pragma unroll
+                for (int w = 0; w < 6; ++w)
+                    if ((uint32_t)w < nw[kk])
+                        d[w] = (w & 1) ? make_uint2(q[kk][w >> 1].z, q[kk][w >> 1].w)
+                                       : make_uint2(q[kk][w >> 1].x, q[kk][w >> 1].y);
             }
         }
     }
