@@ -565,66 +565,91 @@ __global__ __launch_bounds__(KS_BLOCK) void k_kad_bucket_sib(const KeyRec* __res
 }
 
 // the owned nodes' sibling rows (put_sibling_row's layout): the node, then its siblings stable by
-// level msb(x ^ v) -- levels computed once (top 64 bits, the full keys on a tie) and kept in LDS,
-// the row emitted one level at a time (a handful of distinct levels) instead of an insertion sort
-// through scratch
-__global__ __launch_bounds__(KS_BLOCK) void k_kad_sib_rows(const KeyRec* __restrict__ recs,
-                                                            const uint64_t* __restrict__ tops,
-                                                            const KadNode* __restrict__ nodes, int S5, int sbn,
-                                                            const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks,
-                                                            uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
+// level msb(x ^ v).  Eight lanes a node: lane r takes list entries r, r+8, ... (coalesced reads of
+// the list), computes their levels (top 64 bits, the full keys on a tie) and ranks every entry by
+// the key level * 64 + position against the node's 64 keys in LDS (stable by construction); the
+// row is assembled in LDS and written as consecutive 16 B pieces, 128 B per node and instruction.
+// (One lane a node, emitting level by level, had each lane's 16 B stores 576 B apart: 15.9 GB
+// written for 9.7 GB of rows at 2^24 nodes, and the lists read at a 160 B lane stride.)
+// a wave's LDS stores before its lanes' loads of them (a node's lanes lie in one wave)
+__device__ __forceinline__ void sr_wave_fence()
 {
-    // (the lists read from HBM here: staged through LDS the kernel ran at 2 waves/SIMD, 1.8x slower)
-    __shared__ uint8_t lev[64][KS_BLOCK];
-    const uint32_t v = own_lo + blockIdx.x * KS_BLOCK + threadIdx.x;
-    if (v >= own_hi) return;
-    const uint32_t* L = sib + (uint64_t)v * S5;
-    const uint64_t mt = tops[v];
-    int lmin = 255, cnt = 0;
-    for (int i = 0; i < S5 && i < 64; ++i) {
-        const uint32_t x = L[i];
-        int l = 255;
-        if (x != NONE) {
-            const uint64_t d = tops[x] ^ mt;
-            l = d ? 96 + (63 - __clzll((long long)d)) : k_msb(k_xor(kload(recs, x), kload(recs, v)));
-            lmin = min(lmin, l);
-            ++cnt;
-        }
-        lev[i][threadIdx.x] = (uint8_t)l;
-    }
-    const uint64_t blk0 = sib_base + (uint64_t)(v - own_lo) * sbn;
-    KadBlk* B = blks + blk0;
-    // a block's 8 entries gathered in registers, then written as six 16 B stores
-    uint32_t bx[KBLK];
-    uint64_t bt[KBLK];
-    int q = 0;
-    auto put = [&](uint32_t x) {
-        const int sl = q & (KBLK - 1);
-        const uint64_t tp = x == NONE ? ~0ull : tops[x];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int SR_G = 8;                 // lanes per node
+constexpr int SR_NPB = 256 / SR_G;      // nodes per block
+constexpr int SR_ROW = 72;              // row entries: 8 * ceil((1 + 5s) / 8) for 5s <= 64
+
+__global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__ recs,
+                                                      const uint64_t* __restrict__ tops, int S5, int sbn,
+                                                      const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks,
+                                                      uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
+{
+    __shared__ uint32_t rowx[SR_NPB][SR_ROW];
+    __shared__ uint4 keys[SR_NPB][8];        // the node's 64 keys, 16 bits each
+    const int g = threadIdx.x / SR_G, r = threadIdx.x % SR_G;
+    const uint32_t v = own_lo + blockIdx.x * SR_NPB + (uint32_t)g;
+    const bool ok = v < own_hi;
+    const uint64_t mt = ok ? tops[v] : 0ull;
+    uint32_t x[8], key[8];
+    int nval = 0;
 #pragma unroll
-        for (int j = 0; j < KBLK; ++j)
-            if (j == sl) { bx[j] = x; bt[j] = tp; }
-        if (sl == KBLK - 1) {
-            uint4* d = reinterpret_cast<uint4*>(B + (q >> 3));
-#pragma unroll
-            for (int j = 0; j < KBLK; j += 2)
-                d[j / 2] = make_uint4((uint32_t)bt[j], (uint32_t)(bt[j] >> 32), (uint32_t)bt[j + 1], (uint32_t)(bt[j + 1] >> 32));
-            d[4] = make_uint4(bx[0], bx[1], bx[2], bx[3]);
-            d[5] = make_uint4(bx[4], bx[5], bx[6], bx[7]);
+    for (int j = 0; j < 8; ++j) {
+        const int i = r + SR_G * j;
+        uint32_t xx = NONE;
+        if (ok && i < S5) xx = sib[(uint64_t)v * S5 + i];
+        uint32_t k = 0xFFFFu;
+        if (xx != NONE) {
+            const uint64_t d = tops[xx] ^ mt;
+            const int l = d ? 96 + (63 - __clzll((long long)d)) : k_msb(k_xor(kload(recs, xx), kload(recs, v)));
+            k = (uint32_t)l * 64u + (uint32_t)i;
+            ++nval;
         }
-        ++q;
-    };
-    put(v);
-    for (int l = lmin; l < 255 && q < cnt + 1;) {
-        int next = 255;
-        for (int i = 0; i < S5 && i < 64; ++i) {
-            const int li = lev[i][threadIdx.x];
-            if (li == l) put(L[i]);
-            else if (li > l) next = min(next, li);
-        }
-        l = next;
+        x[j] = xx;
+        key[j] = k;
     }
-    while (q < sbn * KBLK) put(NONE);
+    uint16_t* kh = reinterpret_cast<uint16_t*>(keys[g]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kh[r + SR_G * j] = (uint16_t)key[j];
+    uint32_t* row = rowx[g];
+    for (int q = r; q < SR_ROW; q += SR_G) row[q] = q == 0 ? v : NONE;
+    sr_wave_fence();
+    // rank = keys below mine among the node's 64 (the invalid ones are 0xFFFF)
+    uint32_t rank[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const uint4 q = keys[g][w];
+        const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint32_t a0 = ws[h] & 0xFFFFu, a1 = ws[h] >> 16;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rank[j] += (a0 < key[j] ? 1u : 0u) + (a1 < key[j] ? 1u : 0u);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (key[j] != 0xFFFFu) row[1 + rank[j]] = x[j];
+    sr_wave_fence();
+    if (!ok) return;
+    // block b of the row: tops of its 8 entries (four 16 B pieces), then their indices (two)
+    uint4* out = reinterpret_cast<uint4*>(blks + sib_base + (uint64_t)(v - own_lo) * sbn);
+    for (int p = r; p < sbn * 6; p += SR_G) {
+        const int b = p / 6, w = p - 6 * (p / 6);
+        uint4 val;
+        if (w < 4) {
+            const uint32_t e0 = row[b * KBLK + 2 * w], e1 = row[b * KBLK + 2 * w + 1];
+            const uint64_t t0 = e0 == NONE ? ~0ull : tops[e0], t1 = e1 == NONE ? ~0ull : tops[e1];
+            val = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+        } else {
+            const int o = b * KBLK + 4 * (w - 4);
+            val = make_uint4(row[o], row[o + 1], row[o + 2], row[o + 3]);
+        }
+        out[p] = val;
+    }
 }
 
 // sharded networks (KadTables::tl > 0): the top tl buckets m = 159 .. 160 - tl of EVERY node, at
@@ -948,8 +973,9 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     if ((e = hipMalloc(&t.sib, sizeof(uint32_t) * (uint64_t)nown * S5)) != hipSuccess) { cleanup(); return e; }
     hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5, hipMemcpyDeviceToDevice, st);
     {
-        hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, KS_BLOCK)), dim3(KS_BLOCK), 0, st, recs, tops, t.nodes, S5,
-                           sbn, sib_all, t.blks, t.rows_blks, lo, hi);
+        if (S5 > 64 || sbn * KBLK > SR_ROW) { cleanup(); return hipErrorInvalidValue; }
+        hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, SR_NPB)), dim3(256), 0, st, recs, tops, S5, sbn, sib_all,
+                           t.blks, t.rows_blks, lo, hi);
         const dim3 grid((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256)), blk(256);
         const dim3 grid1(nblk(nown, KS_BLOCK)), blk1(KS_BLOCK);
         if (k <= KBLK) {

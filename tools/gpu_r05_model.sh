@@ -33,7 +33,8 @@ for tag in ${AB:-}; do
 done
 # buildab: the 2^24 Kademlia build on each oversim_amd/libovs_kbr_<tag>.so named in BUILDAB (kernel trace)
 for tag in ${BUILDAB:-}; do
-  OVS_LIB=$PWD/oversim_amd/libovs_kbr_$tag.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/build_$tag -o b -- python3 -u tools/diag/kad_build_time.py --reps 2 > $O/build_$tag.out 2>&1 || { tail -20 $O/build_$tag.out; exit 1; }
+  if [ $tag = main ]; then L=$PWD/oversim_amd/libovs_kbr.so; else L=$PWD/oversim_amd/libovs_kbr_$tag.so; fi
+  OVS_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/build_$tag -o b -- python3 -u tools/diag/kad_build_time.py --reps 2 > $O/build_$tag.out 2>&1 || { tail -20 $O/build_$tag.out; exit 1; }
   grep tables_sha $O/build_$tag.out
 done
 # buildpmc: kernel trace + SQ / FETCH / WRITE passes of the 2^24 Kademlia build (summary.txt)
