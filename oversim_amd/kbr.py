@@ -28,7 +28,7 @@ from pathlib import Path
 
 import numpy as np
 
-# OVS_LIB selects an experimental build of the same engine (tools/variants.sh); default: the in-tree build
+# OVS_LIB selects an experimental build of the same engine (tools/build_alt_src.sh); default: the in-tree build
 _LIB_PATH = Path(os.environ.get("OVS_LIB") or Path(__file__).resolve().parent / "libovs_kbr.so")
 
 OVERLAY_CHORD = 1

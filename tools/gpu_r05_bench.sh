@@ -13,12 +13,14 @@ for w in "$@"; do
     cut -c1-1500 $O/bench_$w.json
   fi
 done
-# k1stats: bench C on the OVS_CHORD_STATS library -- K1's lines by kind (the per-launch line census)
+# k1stats: bench C on the OVS_CHORD_STATS library -- K1's lines by kind (the per-launch line census;
+# built by tools/build_alt_src.sh k1stats chord.hip -DOVS_CHORD_STATS)
 if [ "${K1STATS:-0}" = 1 ]; then
   OVS_LIB=$PWD/oversim_amd/libovs_kbr_k1stats.so timeout -k 10 300 python3 -u bench.py --workload C --steps 1 --warmup 0 --no-cpu-baseline > $O/k1stats_C.json 2> $O/k1stats_C.err || { tail -5 $O/k1stats_C.err; exit 1; }
   grep k1stats $O/k1stats_C.err | tail -2
 fi
 # kxstats: bench R on the OVS_KX_STATS library -- K2x's reads and writes by kind per launch
+# (tools/build_alt_src.sh kxstats kad_refresh.hip -DOVS_KX_STATS)
 if [ "${KXSTATS:-0}" = 1 ]; then
   OVS_LIB=$PWD/oversim_amd/libovs_kbr_kxstats.so timeout -k 10 300 python3 -u bench.py --workload R --steps 1 --warmup 0 --no-cpu-baseline > $O/kxstats_R.json 2> $O/kxstats_R.err || { tail -5 $O/kxstats_R.err; exit 1; }
   grep kxstats $O/kxstats_R.err | tail -2
