@@ -129,6 +129,38 @@ def test_refresh_large_network_sample(engine):
         assert list(r["siblings"][i]) == sorted(range(n), key=lambda v: ids[v] ^ K)[:8], i
 
 
+@pytest.mark.parametrize("name", ["default", "a3_rpcto", "a2"])
+def test_refresh_without_responders_device(engine, net, name):
+    """The device-pointer refresh with no responder record (the bench's call): the responders stay
+    in LDS, and the default configuration (R = k = 8, alpha 3, hopCountMax 50, strict, visitOnlyOnce)
+    takes K2x's compile-time-configured instantiation (kad_refresh.hip kad_def_cfg).  Result,
+    status, hops, duration and FindNodeCall count equal the oracle's."""
+    import torch
+    from oversim_amd.kbr import LOOKUP_OUT_DTYPE
+    kw = {} if name == "default" else VARIANTS[name]
+    engine.set_params(_params(**kw))
+    engine.kad_load(net.ids, net.xy)
+    o = OracleNet("kademlia", net.ids, net.xy, kad_params(**kw))
+    keys, src = o.refresh_keys(np.arange(0, len(net.ids), 7, dtype=np.uint32))
+    e = o.exhaustive(keys, src, 8)
+    m = len(keys)
+    dev = torch.device("cuda", 0)
+    dk = torch.from_numpy(np.ascontiguousarray(keys).view(np.int32)).to(dev)
+    ds = torch.from_numpy(np.ascontiguousarray(src).view(np.int32)).to(dev)
+    dout = torch.empty((m, 16), dtype=torch.uint8, device=dev)
+    dsib = torch.empty((m, 8), dtype=torch.int32, device=dev)
+    drpc = torch.empty(m, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    engine.kad_refresh_device(dk.data_ptr(), ds.data_ptr(), m, 8, dout.data_ptr(), dsib.data_ptr(), drpc.data_ptr())
+    torch.cuda.synchronize()
+    r = dout.cpu().numpy().reshape(-1).view(LOOKUP_OUT_DTYPE)
+    for f in FIELDS:
+        bad = np.nonzero(r[f] != e[f])[0]
+        assert len(bad) == 0, f"{name}: {f} differs at {bad[:5]}: gpu {r[f][bad[:5]]} oracle {e[f][bad[:5]]}"
+    assert np.array_equal(drpc.cpu().numpy().view(np.uint32), e["rpcs"]), f"{name}: rpcs"
+    assert np.array_equal(dsib.cpu().numpy().view(np.uint32), e["siblings"]), f"{name}: siblings"
+
+
 def test_refresh_rejects_unsupported(engine, net):
     engine.set_params(_params(lookupParallelRpcs=3))
     engine.kad_load(net.ids, net.xy)
