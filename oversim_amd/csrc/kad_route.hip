@@ -179,13 +179,31 @@ struct KadRouteIO {
 // SM: 0 single GPU; 1 shard step, request/response (lookups stay home, remote findNodes answered by
 // their owners); 2 shard step, migration (a lookup moves to the rank whose rows its next findNode
 // needs; the replicated top buckets answer the long first hops anywhere)
-template <int A, bool RECORD, bool EX, bool LK, int SM, int C, bool SH>
+// DEF (single GPU, one-way, snapshot tables): the default configuration's lookup rules (default.ini:
+// hopCountMax 50, lookupRedundantNodes = k = 8, numSiblings 1, strictParallelRpcs, visitOnlyOnce,
+// acceptLateSiblings and merge on, the useAll / newRpcOn* / finishOnFirstUnchanged rules off) as
+// compile-time constants (alpha is A already); kad_is_def_lc picks it
+__host__ __device__ inline bool kad_is_def_lc(const KadLC& L)
+{
+    return L.hopCountMax == 50 && L.numSiblings == 1 && L.redundant == 8 && L.strict == 1 && L.visitOnlyOnce == 1 &&
+           L.acceptLateSiblings == 1 && L.useAll == 0 && L.merge == 1 && L.newOnResp == 0 && L.newOnTimeout == 0 &&
+           L.finishOnFirst == 0 && L.maxRedundantLocal == 8;
+}
+__device__ __forceinline__ KadLC kad_def_lc(KadLC L)
+{
+    L.hopCountMax = 50; L.numSiblings = 1; L.redundant = 8; L.strict = 1; L.visitOnlyOnce = 1; L.acceptLateSiblings = 1;
+    L.useAll = 0; L.merge = 1; L.newOnResp = 0; L.newOnTimeout = 0; L.finishOnFirst = 0; L.maxRedundantLocal = 8;
+    return L;
+}
+
+template <int A, bool RECORD, bool EX, bool LK, int SM, int C, bool SH, bool DEF = false>
 // the shard step's exact-compare and LookupCall instantiations run at 2 waves/SIMD: their HBM state
 // traffic and request staging need the registers (at 3 the exact-compare ones spilled in misaligned
 // 96-bit pieces gfx950 rejects, the LookupCall one 109 VGPRs); the one-way route step keeps K2's 3
-__global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_MIG2) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC,
+__global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_MIG2) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC0,
                                                                             KadRouteIO io)
 {
+    const KadLC LC = DEF ? kad_def_lc(LC0) : LC0;
     constexpr bool SHARD = SM == 1;
     constexpr bool MIG = SM == 2;
     const int lane = threadIdx.x & 63;
@@ -470,7 +488,7 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
 }  // namespace
 
 // persistent grid: as many waves as are resident, each with a contiguous slice of the batch
-template <int A, bool RECORD, bool EX, bool LK, int SM, int C = 8, bool SH = true>
+template <int A, bool RECORD, bool EX, bool LK, int SM, int C = 8, bool SH = true, bool DEF = false>
 static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, KadRouteIO io, int num_cu,
                              hipStream_t st)
 {
@@ -478,7 +496,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     // initialised once, thread-safely)
     static const int bpc = [] {
         int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SM, C, SH>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_kad_route<A, RECORD, EX, LK, SM, C, SH, DEF>, 256, 0) !=
                 hipSuccess ||
             b < 1)
             b = 1;
@@ -497,7 +515,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kad_stats), z, sizeof z, 0, hipMemcpyHostToDevice, st);
 #endif
-    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SM, C, SH>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC,
+    hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SM, C, SH, DEF>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC,
                        io);
 #ifdef OVS_KAD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
@@ -529,6 +547,9 @@ hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC
     }
     if (sibs) return kad_launch<A, false, EX, true, 0, 8, false>(V, DC, LC, io, num_cu, st);
     if (hopseq) return kad_launch<A, true, EX, false, 0, 8, false>(V, DC, LC, io, num_cu, st);
+#ifndef OVS_KAD_NO_DEF
+    if (kad_is_def_lc(LC)) return kad_launch<A, false, EX, false, 0, 8, false, true>(V, DC, LC, io, num_cu, st);
+#endif
     return kad_launch<A, false, EX, false, 0, 8, false>(V, DC, LC, io, num_cu, st);
 }
 
