@@ -521,7 +521,10 @@ __device__ unsigned long long g_k1_stats[8];
 #ifndef OVS_K1_SHARD_WAVES
 #define OVS_K1_SHARD_WAVES 5
 #endif
-template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
+// DEF: the default configuration (successorListSize 8 on a ring of more than 8 nodes, hopCountMax
+// 50) with those two as compile-time constants -- 1694 -> 1599 static instructions for the one-way
+// route (the successor-window scans and hop checks fold); lanes_launch picks it
+template <bool REC, bool RECORD, bool SHARD, bool LKC = false, bool DEF = false>
 __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) void k_chord_lanes(ChordView V, DelayConsts DC, LookupConsts LC, LaneIO io)
 {
     const int lane = threadIdx.x & 63;
@@ -529,8 +532,8 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
     uint64_t cursor = wave * io.chunk;                    // wave-uniform
     const uint64_t end = min(cursor + io.chunk, io.n);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int ns = V.ns;
-    const int hcm = LC.hopCountMax;
+    const int ns = DEF ? 8 : V.ns;
+    const int hcm = DEF ? 50 : LC.hopCountMax;
 
     bool active = false;
     uint32_t ph = PH_FETCH;
@@ -1208,19 +1211,19 @@ static uint64_t persistent_chunk(Kern k, int* cache, uint64_t n, int num_cu, uin
     return chunk;
 }
 
-template <bool REC, bool RECORD, bool SHARD, bool LKC = false>
+template <bool REC, bool RECORD, bool SHARD, bool LKC = false, bool DEF = false>
 static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC, LaneIO io,
                                int num_cu, hipStream_t s)
 {
     static int bpc = 0;
     uint64_t blocks = 0;
-    io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD, LKC>, &bpc, io.n, num_cu, &blocks);
+    io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD, LKC, DEF>, &bpc, io.n, num_cu, &blocks);
 #ifdef OVS_CHORD_STATS
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_k1_stats), z, sizeof z, 0, hipMemcpyHostToDevice, s);
 #endif
-    hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD, LKC>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC, LC,
-                       io);
+    hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD, LKC, DEF>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC,
+                       LC, io);
 #ifdef OVS_CHORD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_k1_stats), sizeof z, 0, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
@@ -1243,6 +1246,11 @@ static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, 
             if (DC.lookupCall) return lanes_launch<false, false, false, true>(V, DC, LC, io, num_cu, s);
         }
         if (DC.lookupCall) return hipErrorNotSupported;
+#ifndef OVS_K1_NO_DEF
+        if constexpr (!REC && !RECORD) {
+            if (V.ns == 8 && LC.hopCountMax == 50) return lanes_launch<false, false, false, false, true>(V, DC, LC, io, num_cu, s);
+        }
+#endif
         return lanes_launch<REC, RECORD, false>(V, DC, LC, io, num_cu, s);
     } else {
         static int bpc = 0;
