@@ -1481,6 +1481,9 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
     // DC.lookupCall: a LookupCall batch (the responsible node's larger answer, no route message)
     e = LC.recursive ? lanes_launch<true, false, true>(V, DC, LC, io, num_cu, s)
         : DC.lookupCall ? lanes_launch<false, false, true, true>(V, DC, LC, io, num_cu, s)
+#ifndef OVS_K1_NO_DEF
+                        : (V.ns == 8 && LC.hopCountMax == 50) ? lanes_launch<false, false, true, false, true>(V, DC, LC, io, num_cu, s)
+#endif
                         : lanes_launch<false, false, true>(V, DC, LC, io, num_cu, s);
     if (e != hipSuccess) return e;
     // outcomes to their outputs: class d < nsh = hand-offs to arc d (segment d of out), nsh = done
