@@ -433,8 +433,11 @@ constexpr int KVL = 16;
 // KR: the record form (KoordeRec), else the list walks on recs[].  RECORD: hopseq is the caller's
 // hop sequence (every responder written); otherwise it is scratch for responders past the first
 // KVL.  OVS_KOORDE_WAVES: minimum waves per SIMD the record form's register allocation must allow
-template <bool KR, bool RECORD>
-__global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route(KView V, const double2* __restrict__ xy, DelayConsts DC, int hcm,
+// DEF: the default configuration (default.ini: successorListSize 16, shiftingBits 4, useOtherLookup
+// and useSucList on, hopCountMax 50) as compile-time constants -- the start-key arithmetic's
+// modulo by shiftingBits folds to a mask: 5963 -> 4931 static instructions
+template <bool KR, bool RECORD, bool DEF = false>
+__global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route(KView V0, const double2* __restrict__ xy, DelayConsts DC, int hcm0,
                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
                                                       uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
                                                       uint32_t* __restrict__ hopseq, uint32_t* __restrict__ rpcs)
@@ -444,6 +447,9 @@ __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route
     uint64_t cursor = wave * chunk;
     const uint64_t end = min(cursor + chunk, nq);
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    KView V = V0;
+    if (DEF) { V.ns = 16; V.sb = 4; V.useOther = 1; V.useSuc = 1; }
+    const int hcm = DEF ? 50 : hcm0;
     const uint64_t H = hcm > 0 ? (uint64_t)hcm : 1ull;
 
     bool active = false, local = true;
@@ -664,7 +670,25 @@ hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2
     const uint64_t blocks = ((nq + chunk - 1) / chunk + 3) / 4;
 #define KRL(a, b) hipLaunchKernelGGL((KRT(a, b)), dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC, \
                                      hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs)
-    if (kr) { if (record) KRL(true, true); else KRL(true, false); }
+    const KView kv = make_view(t, recs);
+#ifdef OVS_KOORDE_NO_DEF
+    const bool def = false;             // A/B build: the generic instantiation
+#else
+    const bool def = kr && !record && kv.ns == 16 && kv.sb == 4 && kv.useOther == 1 && kv.useSuc == 1 && hopCountMax == 50;
+#endif
+    if (def) {
+        static int bpd = 0;
+        if (bpd == 0) {
+            int b = 0;
+            bpd = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_koorde_route<true, false, true>, 256, 0) == hipSuccess && b > 0) ? b : 1;
+        }
+        const uint64_t wd = (uint64_t)num_cu * (uint64_t)bpd * 4;
+        uint64_t cd = (nq + wd - 1) / wd;
+        if (cd < 1) cd = 1;
+        const uint64_t bd = ((nq + cd - 1) / cd + 3) / 4;
+        hipLaunchKernelGGL((k_koorde_route<true, false, true>), dim3((unsigned)bd), dim3(256), 0, st, kv, xy, DC, hopCountMax, keys,
+                           src, nq, cd, out, hopseq, rpcs);
+    } else if (kr) { if (record) KRL(true, true); else KRL(true, false); }
     else { if (record) KRL(false, true); else KRL(false, false); }
 #undef KRL
 #undef KRT
