@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define OVS_ABI_VERSION 11
+#define OVS_ABI_VERSION 12
 
 /* 160-bit OverlayKey: w[0] = least significant 32 bits.  Equal to the
  * reference's GMP limbs 0..2 with the top limb trimmed to 32 bits
@@ -134,6 +134,10 @@ typedef struct ovs_params {
     int32_t globalNodeLimit;            /* **.kademlia.globalNodeLimit = 1000 (nkademlia; ABI 10) */
     int32_t extraNodesFinalBucket;      /* **.kademlia.extraNodesFinalBucket = 0 (nr128; 0 = keyLength) */
     double  rpcKeyTimeout;              /* **.rpcKeyTimeout = 10 s: routed RPCs (recursive LookupCalls; ABI 10) */
+    int32_t measureAuthBlock;           /* **.overlay*.*.measureAuthBlock = false (default.ini:399).  true: every
+                                           RPC response carries AUTHBLOCK_L = SIGNATURE_L + CERT_L + PUBKEY_L
+                                           = 800 bits (CommonMessages.msg:45-47, 57, 73), i.e. +100 B on each
+                                           FindNodeResponse / LookupResponse length in the delay (ABI 12) */
 } ovs_params;
 
 /* Result of one one-way KBR test lookup (KBRTestApp with kbrOneWayTest). */
@@ -151,9 +155,20 @@ int         ovs_abi_version(void);
 void        ovs_params_default(int32_t overlay, ovs_params* out);
 /* Parse OMNeT++ .ini text (sections [General] / [Config X] with `extends`,
  * wildcard keys such as `**.overlay*.chord.successorListSize = 8`, units s/ms/B/Mbps)
- * and overwrite the matching fields of *p.  config_name may be NULL ([General]). */
+ * and overwrite the matching fields of *p.  config_name may be NULL ([General]).
+ * Keys the engine does not model but that would change a route, a response size or a
+ * delay are refused with OVS_ENOTSUP and a message naming the key (ABI 12): e.g.
+ * optimizeTimeouts = true, udp.delayFaultType != "no_fault", neighborCache.ncsType !=
+ * "none", kademlia.proximityRouting with a recursive routingType, the Kademlia
+ * routingAdd options (proximityNeighborSelection, enableManagedConnections, activePing,
+ * secureMaintenance, pingNewSiblings), chord.proximityRouting with extendedFingerTable,
+ * malicious nodes; the full list is in DESIGN.md §9. */
 ovs_status  ovs_params_from_ini(ovs_params* p, const char* ini_text, const char* config_name,
                                 char* err, int err_len);
+/* The same from a file, resolving OMNeT++ `include <file>` lines relative to the including
+ * file (omnetpp.ini:520 `include ./default.ini`), as Cmdenv reads it (ABI 12). */
+ovs_status  ovs_params_from_ini_file(ovs_params* p, const char* path, const char* config_name,
+                                     char* err, int err_len);
 
 ovs_status  ovs_ctx_create(int hip_device, ovs_ctx** out);
 void        ovs_ctx_destroy(ovs_ctx* ctx);

@@ -210,6 +210,14 @@ void orc_key_pow2(uint32_t e, orc_key* out) { OKey x = ok_pow2(e); ok_to(&x, out
 /* ===================================================================== */
 /* parameters                                                            */
 /* ===================================================================== */
+/* response length: BASERESPONSE_L (+ AUTHBLOCK_L when measureAuthBlock, CommonMessages.msg:57, 73)
+ * + NEIGHBORSFLAG_L + the carried NodeHandles (FINDNODERESPONSE_L, CommonMessages.msg:71-72) */
+#define AUTHBLOCK_BYTES ((40 * 8 + 40 * 8 + 20 * 8) / 8)   /* SIGNATURE_L + CERT_L + PUBKEY_L, msg:45-47 */
+static int32_t resp_bytes(const orc_params* p, int nodes)
+{
+    return p->respBaseBytes + (p->measureAuthBlock ? AUTHBLOCK_BYTES : 0) + p->respPerNodeBytes * nodes;
+}
+
 static void params_common(orc_params* p)
 {
     memset(p, 0, sizeof *p);
@@ -1624,7 +1632,7 @@ static void lk_sendRpc(Lookup* L, uint32_t handle, int rpcId)
         sflag = L->exh ? 0 : ov_isSiblingFor(L->net, handle, handle, &L->key, L->numSiblings, &err);
         (void)sflag;
         int64_t respTx = 0;   /* responder's tx queue idle */
-        int64_t d2 = calc_delay(L->net, handle, L->S, p->respBaseBytes + p->respPerNodeBytes * res.size, tArr, &respTx);
+        int64_t d2 = calc_delay(L->net, handle, L->S, resp_bytes(p, res.size), tArr, &respTx);
         r->tResp = tArr + d2;
         r->tIns = tArr;
         if (L->cnode) {
@@ -2114,7 +2122,7 @@ static void run_recursive_call(const orc_net* net, const OKey* key, uint32_t S, 
     const int flag = ov_isSiblingFor(net, d.node, d.node, key, numSiblings, &err);
     int64_t T = d.t;
     if (d.node != S) {
-        const int32_t resp = p->respBaseBytes + p->respPerNodeBytes * res.size;
+        const int32_t resp = resp_bytes(p, res.size);
         if (p->routingType == 1) {
             int64_t tx = d.tx;
             T += calc_delay(net, d.node, S, resp, d.t, &tx);

@@ -87,6 +87,9 @@ typedef struct {
      * FixfingersResponse candidates, getMaxNumRedundantNodes() = numFingerCandidates.  Stable
      * (orc_chord_build / _lazy) rings only: explicit tables do not carry the candidate lists */
     int32_t extendedFingerTable;
+    /* BaseOverlay.ned measureAuthBlock (default.ini:399 = false): every RPC response carries
+     * AUTHBLOCK_L = SIGNATURE_L + CERT_L + PUBKEY_L = 800 bits (CommonMessages.msg:45-47, 57, 73) */
+    int32_t measureAuthBlock;
 } orc_params;
 
 void orc_params_chord_default(orc_params* p);

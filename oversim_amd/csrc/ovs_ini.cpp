@@ -335,6 +335,28 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         double b;
         if (!to_bytes(unquote(v), &b)) bad = "testMsgSize"; else p->testMsgSize = (int32_t)b;
     }
+    // SimpleUnderlay channel of every terminal (SimpleUnderlayConfigurator: churnGenerator channelTypes,
+    // default.ini:559-562; channels.ned): one lossless type binds datarate and the access delay
+    const std::string churn = "SimpleUnderlayNetwork.churnGenerator[0].";
+    if (lookup(churn + "channelTypes", &v)) {
+        const std::string ct = trim(unquote(v));
+        if (ct.find(' ') != std::string::npos) {
+            set_err("channelTypes \"" + ct + "\": several channel types give nodes different datarates and "
+                    "access delays; the engine holds one channel for all nodes");
+            return OVS_ENOTSUP;
+        }
+        if (ct == "oversim.common.simple_ethernetline") { p->datarate = 10e6; p->accessDelay = 0.0; }
+        else if (ct == "oversim.common.simple_dsl") { p->datarate = 1e6; p->accessDelay = 0.020; }
+        else if (!ct.empty()) {
+            set_err("channelTypes \"" + ct + "\" not supported (simple_ethernetline, simple_dsl; the lossy "
+                    "channels drop packets at random, channels.ned:11-35)");
+            return OVS_ENOTSUP;
+        }
+    }
+    if (lookup(churn + "channelTypesRx", &v) && !trim(unquote(v)).empty()) {
+        set_err("channelTypesRx \"" + unquote(v) + "\": separate receive channels are not modelled");
+        return OVS_ENOTSUP;
+    }
     // channel parameters (channels.ned defaults unless overridden as ovs.datarate/ovs.accessDelay)
     if (lookup("ovs.datarate", &v) && !to_bps(unquote(v), &p->datarate)) bad = "datarate";
     if (lookup("ovs.accessDelay", &v) && !to_seconds(unquote(v), &p->accessDelay)) bad = "accessDelay";
@@ -344,12 +366,168 @@ extern "C" ovs_status ovs_params_from_ini(ovs_params* p, const char* ini_text, c
         else if (r == "truncate") p->simtimeRound = 0;
         else bad = "simtimeRounding";
     }
+    want_bool("measureAuthBlock", &p->measureAuthBlock);   // BaseOverlay.cc:113, CommonMessages.msg:57, 73
     if (!bad.empty()) { set_err("cannot parse value of " + bad + ": " + v); return OVS_EINVAL; }
+
+    // Keys the engine does not model but that change a route, a response size or a delay.  A
+    // stock config that sets one gets OVS_ENOTSUP naming the key, never a silently different
+    // result.  The default.ini values pass.
+    auto is_true = [&](const std::string& path, const char* name, bool* on) -> bool {
+        int32_t b = 0;
+        *on = false;
+        if (!lookup(path, &v)) return true;
+        if (!to_bool(unquote(v), &b)) { set_err(std::string("cannot parse value of ") + name + ": " + v); return false; }
+        *on = b != 0;
+        return true;
+    };
+    auto refuse = [&](const std::string& m) { set_err(m); return OVS_ENOTSUP; };
+    auto study = [&]() { return v.find("${") != std::string::npos; };   // reported below, by key
+    bool on = false;
+    // the network and its clock: SimpleUnderlayNetwork (the delay model restated), simtime-scale -9
+    // (int64 ns, default.ini:16, 27)
+    if (lookup("network", &v) && !study() && unquote(v) != "oversim.underlay.simpleunderlay.SimpleUnderlayNetwork")
+        return refuse("network = " + unquote(v) + " not supported: the engine restates SimpleUnderlay's delay "
+                      "model (SimpleNodeEntry.cc:155-195)");
+    if (lookup("simtime-scale", &v) && !study() && trim(v) != "-9")
+        return refuse("simtime-scale = " + trim(v) + " not supported: latencies are int64 ns (simtime-scale = -9)");
+    // overlayType (default.ini:624) must name the overlay these parameters are for
+    if (lookup(host + ".overlayType", &v) && !study()) {
+        std::string mod = unquote(v);
+        mod = mod.substr(mod.rfind('.') == std::string::npos ? 0 : mod.rfind('.') + 1);
+        const int32_t want = mod == "ChordModules" ? OVS_OVERLAY_CHORD : mod == "KademliaModules" ? OVS_OVERLAY_KADEMLIA
+                             : mod == "KoordeModules" ? OVS_OVERLAY_KOORDE : mod == "EpiChordModules" ? OVS_OVERLAY_EPICHORD
+                                                                                                      : -1;
+        if (want < 0)
+            return refuse("overlayType = " + unquote(v) + " not supported: the engine routes Chord, Kademlia, Koorde "
+                          "and EpiChord");
+        if (want != p->overlay) {
+            set_err("overlayType = " + unquote(v) + " but the parameters are bound for " + ov);
+            return OVS_EINVAL;
+        }
+    }
+    // BaseRpc::sendRpcCall (BaseRpc.cc:197-200): the timeout becomes NeighborCache::getNodeTimeout
+    // (RTT history or NCS estimate, NeighborCache.cc:802-850) -- entries are recorded from every
+    // response whether or not enableNeighborCache is set (BaseRpc.cc:455-461, NeighborCache.cc:229, 282)
+    if (!is_true(ovp + "optimizeTimeouts", "optimizeTimeouts", &on)) return OVS_EINVAL;
+    if (on) return refuse("optimizeTimeouts = true not supported: RPC timeouts from NeighborCache::getNodeTimeout "
+                          "(BaseRpc.cc:197-200) replace rpcUdpTimeout");
+    // SimpleUDP::initialize (SimpleUDP.cc:128-142): a known fault type adds a hashed error to every
+    // coordinate delay (SimpleNodeEntry.cc:188, 197-254); any other string is "no fault"
+    if (lookup(host + ".udp.delayFaultType", &v)) {
+        const std::string f = unquote(v);
+        if (f == "live_all" || f == "live_planetlab" || f == "simulation")
+            return refuse("udp.delayFaultType = \"" + f + "\" not supported: faulty coordinate delays "
+                          "(SimpleNodeEntry.cc:197-254)");
+    }
+    // BaseRpc::internalSendRpcResponse (BaseRpc.cc:543-550): with an NCS every response carries the
+    // node's coordinates (BASERESPONSE_L, CommonMessages.msg:73-76), which changes its length
+    const std::string nc = host + ".neighborCache.";
+    if (lookup(nc + "ncsType", &v) && unquote(v) != "none") {
+        const std::string ncs = unquote(v);
+        if (!is_true(nc + "ncsSendBackOwnCoords", "ncsSendBackOwnCoords", &on)) return OVS_EINVAL;
+        if (on || !lookup(nc + "ncsSendBackOwnCoords", &v))   // NeighborCache.ned default: true
+            return refuse("neighborCache.ncsType = \"" + ncs + "\" not supported: responses carry NcsInfo "
+                          "(BaseRpc.cc:543-550), which changes their size");
+    }
+    // malicious nodes answer FindNodeCalls with the configured attacks (BaseOverlay.cc:1844-1907)
+    const std::string gnl = "SimpleUnderlayNetwork.globalObserver.globalNodeList.";
+    if (lookup(gnl + "maliciousNodeProbability", &v)) {
+        double x; std::string u;
+        if (!parse_number(unquote(v), &x, &u) || !u.empty()) { set_err("cannot parse value of maliciousNodeProbability: " + v); return OVS_EINVAL; }
+        if (x > 0) return refuse("maliciousNodeProbability > 0 not supported: malicious nodes (GlobalNodeList.cc:221, "
+                                 "BaseOverlay.cc:1844-1907)");
+    }
+    if (!is_true(gnl + "maliciousNodeChange", "maliciousNodeChange", &on)) return OVS_EINVAL;
+    if (on) return refuse("maliciousNodeChange = true not supported: malicious nodes (GlobalNodeList.cc:79-80)");
+    const bool recursive = p->routingType == 1 || p->routingType == 2 || p->routingType == 4;
+    if (p->overlay == OVS_OVERLAY_KADEMLIA) {
+        // R/Kademlia: findNode ranks route-message next hops by proximity (Kademlia.cc:1144-1157,
+        // 1234-1241); with iterative routing every findNode serves a FindNodeCall and it has no effect
+        if (!is_true(ovp + "proximityRouting", "proximityRouting", &on)) return OVS_EINVAL;
+        if (on && recursive)
+            return refuse("kademlia.proximityRouting = true not supported with recursive routing: findNode "
+                          "orders route-message hops by proximity (Kademlia.cc:1144-1157, 1234-1241)");
+        // altRecMode sets recordRoute (Kademlia.cc:133) and changes recursiveRoutingHook (1029-1063)
+        if (!is_true(ovp + "altRecMode", "altRecMode", &on)) return OVS_EINVAL;
+        if (on) return refuse("kademlia.altRecMode = true not supported: it sets recordRoute (Kademlia.cc:133) and "
+                              "changes recursiveRoutingHook (Kademlia.cc:1029-1063)");
+        // Kademlia::routingAdd options: the maintenance rounds (ovs_kad_maintenance_round) restate
+        // routingAdd with them off, and the tables they converge to differ
+        static const struct { const char* key; const char* where; } radd[] = {
+            {"proximityNeighborSelection", "Kademlia.cc:682-756"},
+            {"enableManagedConnections", "Kademlia.cc:660, 698, 720"},
+            {"activePing", "Kademlia.cc:447, 682"},
+            {"secureMaintenance", "Kademlia.cc:284, 459-489, 539-729"},
+            {"pingNewSiblings", "Kademlia.cc:553"},
+        };
+        for (const auto& r : radd) {
+            if (!is_true(ovp + r.key, r.key, &on)) return OVS_EINVAL;
+            if (on)
+                return refuse(std::string("kademlia.") + r.key + " = true not supported: it changes "
+                              "Kademlia::routingAdd (" + r.where + "), which the maintenance rounds restate with it off");
+        }
+    }
+    if (p->overlay == OVS_OVERLAY_CHORD && p->extendedFingerTable) {
+        // handleRpcFixfingersResponse re-ranks a finger's candidates by measured proximity (Chord.cc:1290-1314)
+        if (!is_true(ovp + "proximityRouting", "proximityRouting", &on)) return OVS_EINVAL;
+        if (on)
+            return refuse("chord.proximityRouting = true not supported with extendedFingerTable: finger candidates "
+                          "ordered by proximity (Chord.cc:1290-1314)");
+    }
     if (!iter_key.empty()) {
         set_err("parameter studies (${...}) are not supported: " + iter_key);
         return OVS_ENOTSUP;
     }
     return OVS_OK;
+}
+
+// OMNeT++ `include <file>` lines are textual inclusion relative to the including file
+// (omnetpp.ini:520 `include ./default.ini`); resolved recursively, depth-limited against cycles.
+static bool read_ini_file(const std::string& path, int depth, std::string* out, std::string* err)
+{
+    if (depth > 16) { *err = "include nesting too deep at " + path; return false; }
+    std::FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) { *err = "cannot open " + path; return false; }
+    std::string text;
+    char buf[65536];
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, got);
+    std::fclose(f);
+    const size_t slash = path.rfind('/');
+    const std::string dir = slash == std::string::npos ? std::string() : path.substr(0, slash + 1);
+    size_t pos = 0;
+    while (pos <= text.size()) {
+        size_t nl = text.find('\n', pos);
+        if (nl == std::string::npos) nl = text.size();
+        const std::string raw = text.substr(pos, nl - pos), line = trim(raw);
+        pos = nl + 1;
+        if (line.rfind("include", 0) == 0 && line.size() > 7 && std::isspace((unsigned char)line[7])) {
+            std::string inc = trim(line.substr(8));
+            if (inc.empty()) { *err = "empty include in " + path; return false; }
+            if (inc[0] != '/') inc = dir + inc;
+            if (!read_ini_file(inc, depth + 1, out, err)) return false;
+            out->push_back('\n');
+        } else {
+            out->append(raw);
+            out->push_back('\n');
+        }
+    }
+    return true;
+}
+
+extern "C" ovs_status ovs_params_from_ini_file(ovs_params* p, const char* path, const char* config_name, char* err,
+                                               int err_len)
+{
+    if (!p || !path) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "null argument");
+        return OVS_EINVAL;
+    }
+    std::string text, e;
+    if (!read_ini_file(path, 0, &text, &e)) {
+        if (err && err_len > 0) std::snprintf(err, (size_t)err_len, "%s", e.c_str());
+        return OVS_EINVAL;
+    }
+    return ovs_params_from_ini(p, text.c_str(), config_name, err, err_len);
 }
 
 // defaults = the reference's default.ini values (host-only parameter handling, with the binder above)
@@ -388,6 +566,7 @@ extern "C" void ovs_params_default(int32_t overlay, ovs_params* p)
     p->globalNodeLimit = 1000;          // default.ini:210
     p->extraNodesFinalBucket = 0;       // default.ini:211
     p->rpcKeyTimeout = 10.0;            // default.ini:484
+    p->measureAuthBlock = 0;            // default.ini:399
     if (overlay == OVS_OVERLAY_KOORDE) p->successorListSize = 16;   // default.ini:275
     if (overlay == OVS_OVERLAY_EPICHORD) p->successorListSize = 4;  // default.ini:159
     if (overlay == OVS_OVERLAY_KADEMLIA) {

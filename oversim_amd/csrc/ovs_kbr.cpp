@@ -247,6 +247,9 @@ DelayConsts delay_consts(const ovs_params& P)
     d.access2 = 2 * acc;
     d.callBytes = 83;        // FINDNODECALL_L 440 bits + 28 B
     d.respBase = 61;         // FINDNODERESPONSE_L 264 bits + 28 B
+    // measureAuthBlock: BASERESPONSE_L adds AUTHBLOCK_L = SIGNATURE_L + CERT_L + PUBKEY_L = 800 bits to
+    // every response (CommonMessages.msg:45-47, 57, 73); calls and route messages are unchanged
+    if (P.measureAuthBlock) d.respBase += 100;
     if (P.overlay == OVS_OVERLAY_KOORDE) {
         // every Koorde FindNodeCall / FindNodeResponse carries a KoordeFindNodeExtMessage,
         // KEY_L + STEP_L = 168 bits (ChordMessage.msg:33,55; IterativeLookup.cc:385-388,

@@ -67,6 +67,7 @@ class Params(C.Structure):
         ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
         ("useSucList", C.c_int32), ("bucketType", C.c_int32), ("cacheTTL", C.c_double),
         ("globalNodeLimit", C.c_int32), ("extraNodesFinalBucket", C.c_int32), ("rpcKeyTimeout", C.c_double),
+        ("measureAuthBlock", C.c_int32),
     ]
 
     @classmethod
@@ -100,6 +101,17 @@ class Params(C.Structure):
         st = lib().ovs_params_from_ini(C.byref(p), text.encode(), config.encode() if config else None, err, 512)
         if st != 0:
             raise KbrError(f"ovs_params_from_ini: {STATUS.get(st, st)}: {err.value.decode()}")
+        return p
+
+    @classmethod
+    def from_ini_file(cls, path, config: str | None = None, overlay: int = OVERLAY_CHORD) -> "Params":
+        """Like from_ini, reading the file and its `include` lines as Cmdenv does."""
+        p = cls()
+        lib().ovs_params_default(overlay, C.byref(p))
+        err = C.create_string_buffer(512)
+        st = lib().ovs_params_from_ini_file(C.byref(p), str(path).encode(), config.encode() if config else None, err, 512)
+        if st != 0:
+            raise KbrError(f"ovs_params_from_ini_file: {STATUS.get(st, st)}: {err.value.decode()}")
         return p
 
     def as_dict(self) -> dict:
@@ -187,6 +199,7 @@ def lib() -> C.CDLL:
         "ovs_abi_version": ([], C.c_int),
         "ovs_params_default": ([i32, vp], None),
         "ovs_params_from_ini": ([vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int], C.c_int),
+        "ovs_params_from_ini_file": ([vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int], C.c_int),
         "ovs_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
         "ovs_ctx_destroy": ([vp], None),
         "ovs_last_error": ([vp], C.c_char_p),

@@ -46,6 +46,7 @@ int main(void)
     F(ovs_params, deBruijnListSize); F(ovs_params, useOtherLookup); F(ovs_params, useSucList);
     F(ovs_params, bucketType); F(ovs_params, cacheTTL);
     F(ovs_params, globalNodeLimit); F(ovs_params, extraNodesFinalBucket); F(ovs_params, rpcKeyTimeout);
+    F(ovs_params, measureAuthBlock);
     end();
     S(ovs_koorde_ext);
     F(ovs_koorde_ext, route_key); F(ovs_koorde_ext, step); F(ovs_koorde_ext, has_route_key);

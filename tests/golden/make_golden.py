@@ -12,7 +12,7 @@ generator in oversim_amd/workload.py; coordinates for N <= 15000 are records of
 the reference's simulations/nodes_2d_15000.xml.
 
 Each .npz records the SimTime rounding rule it was generated with.
-Run: python tests/golden/make_golden.py [--kad] [--rec] [--kadrec] [--koorde] [--check: with --koorde verify the
+Run: python tests/golden/make_golden.py [--kad] [--rec] [--auth] [--kadrec] [--koorde] [--check: with --koorde verify the
 committed Koorde vectors, alone the committed Kademlia vectors, instead of rewriting them]
 """
 from __future__ import annotations
@@ -31,17 +31,19 @@ from oracle_lib import OracleNet, chord_params, kad_params, koorde_params  # noq
 import refmodel  # noqa: E402
 
 
-def chord_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: int):
+def chord_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: int, auth: int = 0):
+    """auth: measureAuthBlock = true -- every FindNodeResponse 100 B longer (AUTHBLOCK_L,
+    CommonMessages.msg:45-47, 57, 73)."""
     net = W.population(n, seed)
     k1, s1 = W.lookups(net.ids, m_ids, seed + 1, node_ids=True)
     k2, s2 = W.lookups(net.ids, m_rand, seed + 2, node_ids=False)
     keys = np.concatenate([k1, k2])
     src = np.concatenate([s1, s2])
-    o = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd))
+    o = OracleNet("chord", net.ids, net.xy, chord_params(simtimeRound=rnd, measureAuthBlock=auth))
     r = o.route(keys, src, record_hops=True)
     ring = refmodel.ChordRing(net.ids, net.xy, rnd=bool(rnd))
     for i in range(len(keys)):
-        m = ring.lookup(keys[i], int(src[i]))
+        m = ring.lookup(keys[i], int(src[i]), resp=87 + 100 * auth)
         for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
             assert int(r[f][i]) == int(m[f]), (name, i, f, r[f][i], m[f])
         assert [int(x) for x in r["hop_seq"][i] if x != 0xFFFFFFFF] == m["hop_seq"], (name, i)
@@ -49,7 +51,8 @@ def chord_case(name: str, n: int, seed: int, m_ids: int, m_rand: int, rnd: int):
     np.savez_compressed(HERE / f"{name}.npz", ids=net.ids, xy=net.xy, keys=keys, src=src,
                         responsible=r["responsible"], hops=r["hops"], status=r["status"],
                         one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"],
-                        hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed))
+                        hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed),
+                        measure_auth_block=np.int32(auth))
     print(name, "lookups", len(keys), "mean hops", r["hops"].mean(), "status", np.bincount(r["status"]))
 
 
@@ -101,7 +104,8 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1, **k
         fn_sib[i] = flag
     r = o.route(k1, s1, record_hops=True, count_rpcs=True)
     # the lookups restated twice: oracle event list vs refmodel's message-level simulation
-    sim = refmodel.KadLookupSim(tab, net.xy, redundant=R, alpha=alpha, rnd=bool(rnd), k=p.k)
+    sim = refmodel.KadLookupSim(tab, net.xy, redundant=R, alpha=alpha, rnd=bool(rnd), k=p.k,
+                                resp_base=61 + 100 * p.measureAuthBlock)
     for i in range(len(k1)):
         mm = sim.run(k1[i], int(s1[i]))
         for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs"):
@@ -120,7 +124,8 @@ def kad_case(name: str, n: int, seed: int, m: int, alpha: int, rnd: int = 1, **k
                         one_way_hops=r["one_way_hops"], latency_ns=r["latency_ns"], rpcs=r["rpcs"],
                         hop_seq=r["hop_seq"][:, :H], simtime_round=np.int32(rnd), seed=np.int64(seed),
                         kad_seed=np.uint64(p.kadSeed), fn_node=fn_node, fn_key=fn_key, fn_out=fn_out,
-                        fn_sib=fn_sib, k=np.int32(p.k), s=np.int32(p.s), redundant=np.int32(R))
+                        fn_sib=fn_sib, k=np.int32(p.k), s=np.int32(p.s), redundant=np.int32(R),
+                        measure_auth_block=np.int32(p.measureAuthBlock))
     print(name, "lookups", len(k1), "mean hops", r["hops"].mean(), "rpcs", r["rpcs"].mean(),
           "status", np.bincount(r["status"]))
 
@@ -289,6 +294,10 @@ if __name__ == "__main__":
     if "--koorde" in sys.argv:   # (with --check: verify instead of writing)
         koorde_case("koorde_n2000", 2000, 0x4b4f, 1024, 1024)
         koorde_case("koorde_n2000_sb2_nosuc", 2000, 0x4b50, 512, 512, shiftingBits=2, useSucList=0)
+        sys.exit(0)
+    if "--auth" in sys.argv:   # measureAuthBlock = true (default.ini:399 flipped), Chord and Kademlia alpha 3
+        chord_case("chord_n1000_auth", 1000, 0x4215, 2048, 2048, 1, auth=1)
+        kad_case("kad_n2000_a3_auth", 2000, 0x4b44, 2048, 3, measureAuthBlock=1)
         sys.exit(0)
     if "--rec" in sys.argv:
         chord_rec_case("chord_n1000_semirec", 1000, 0x4213, 2048, 2048, 1)

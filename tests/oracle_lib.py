@@ -37,7 +37,7 @@ class OrcParams(C.Structure):
         ("shiftingBits", C.c_int32), ("deBruijnListSize", C.c_int32), ("useOtherLookup", C.c_int32),
         ("useSucList", C.c_int32),
         ("bucketType", C.c_int32), ("globalNodeLimit", C.c_int32), ("extraNodesFinalBucket", C.c_int32),
-        ("rpcKeyTimeout", C.c_double), ("extendedFingerTable", C.c_int32),
+        ("rpcKeyTimeout", C.c_double), ("extendedFingerTable", C.c_int32), ("measureAuthBlock", C.c_int32),
     ]
 
     def replace(self, **kw) -> "OrcParams":

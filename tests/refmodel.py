@@ -152,14 +152,14 @@ class ChordRing:
                 return dict(responsible=0xFFFFFFFF, hops=hops, status=4, one_way_hops=0, latency_ns=-1, hop_seq=seq)
             cur = nxt
 
-    def lookup_call(self, kw, S, num_siblings=8, hop_max=50, call=83, resp=87, rpc_to=1.5, lk_to=10.0):
+    def lookup_call(self, kw, S, num_siblings=8, hop_max=50, call=83, resp=87, rpc_to=1.5, lk_to=10.0, resp_base=61):
         """KBRTestApp LookupCall: the same iterative path; the responsible node answers
         [R, succ...] cut to num_siblings (a bigger FindNodeResponse: 61 B + 26 B per node), the
         response ends the lookup (no route message) and the siblings vector is that answer."""
         k = to_int(kw)
         rnd = self.rnd
         m = min(num_siblings, 1 + self.ns)
-        resp_sib = 61 + 26 * m
+        resp_sib = resp_base + 26 * m
         sib, nxt = self.decide(S, k)
         if sib:
             return dict(siblings=[(S + j) % self.n for j in range(m)], hops=0, status=0, latency_ns=0)

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 15
     for s in sorted(syms):
         assert hasattr(L, s), f"{s} declared in include/ but not exported"
-    assert L.ovs_abi_version() == 11
+    assert L.ovs_abi_version() == 12
 
 
 def test_params_default_matches_default_ini():

@@ -116,20 +116,26 @@ def test_key_ops_match_bigint():
         assert L.orc_key_bit_range(O._p(K(a)), p, n) == (a >> p) & ((1 << n) - 1)
 
 
-@pytest.mark.parametrize("name", ["chord_n1000_round", "chord_n1000_trunc", "chord_n9", "chord_n2"])
+def _auth(g) -> int:
+    return int(g["measure_auth_block"]) if "measure_auth_block" in g.files else 0
+
+
+@pytest.mark.parametrize("name", ["chord_n1000_round", "chord_n1000_trunc", "chord_n9", "chord_n2", "chord_n1000_auth"])
 def test_oracle_reproduces_chord_golden(name):
     g = np.load(GOLD / f"{name}.npz")
-    o = O.OracleNet("chord", g["ids"], g["xy"], O.chord_params(simtimeRound=int(g["simtime_round"])))
+    o = O.OracleNet("chord", g["ids"], g["xy"], O.chord_params(simtimeRound=int(g["simtime_round"]),
+                                                               measureAuthBlock=_auth(g)))
     r = o.route(g["keys"], g["src"], record_hops=True)
     for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns"):
         assert np.array_equal(r[f], g[f]), f
     assert np.array_equal(r["hop_seq"][:, :g["hop_seq"].shape[1]], g["hop_seq"])
 
 
-@pytest.mark.parametrize("name", ["kad_n2000_a1", "kad_n2000_a3"])
+@pytest.mark.parametrize("name", ["kad_n2000_a1", "kad_n2000_a3", "kad_n2000_a3_auth"])
 def test_oracle_reproduces_kad_golden(name):
     g = np.load(GOLD / f"{name}.npz")
-    p = O.kad_params(lookupParallelRpcs=int(g["alpha"]), simtimeRound=int(g["simtime_round"]), kadSeed=int(g["kad_seed"]))
+    p = O.kad_params(lookupParallelRpcs=int(g["alpha"]), simtimeRound=int(g["simtime_round"]), kadSeed=int(g["kad_seed"]),
+                     measureAuthBlock=_auth(g))
     o = O.OracleNet("kademlia", g["ids"], g["xy"], p)
     r = o.route(g["keys"], g["src"], record_hops=True, count_rpcs=True)
     for f in ("responsible", "hops", "status", "one_way_hops", "latency_ns", "rpcs"):
@@ -326,3 +332,16 @@ def test_oracle_kademlia_lookup_call_properties(alpha):
         exact += row == sorted(range(2000), key=lambda x: ids[x] ^ kk)[:8]
     assert exact > len(k) // 2
     assert np.all(r["hops"] <= a["hops"])
+
+
+def test_auth_block_adds_100_bytes_per_response():
+    """measureAuthBlock (CommonMessages.msg:45-47, 57, 73): on a 10 Mbps channel each FindNodeResponse
+    serialises 2 x 80 us longer (sender and receiver access links), calls and the route message do
+    not change; with alpha = 1 Chord every accepted hop is one response, so routes are unchanged and
+    latency grows by exactly hops x 160 us."""
+    g = np.load(GOLD / "chord_n1000_auth.npz")
+    plain = O.OracleNet("chord", g["ids"], g["xy"], O.chord_params()).route(g["keys"], g["src"], record_hops=False)
+    for f in ("responsible", "hops", "status", "one_way_hops"):
+        assert np.array_equal(plain[f], g[f]), f
+    assert np.array_equal(g["latency_ns"] - plain["latency_ns"], g["hops"].astype(np.int64) * 160_000)
+    assert (g["hops"] > 0).mean() > 0.9
