@@ -182,6 +182,97 @@ def parity_check(gpu: dict, orc: dict, m: int, fields) -> dict:
     return out
 
 
+class Watchdog:
+    """Ends a stuck run instead of letting it block the job: when the current stage has not moved on
+    within its limit, the stage -- and, inside the native round loop, the collective it is in
+    (ovs_exchange_stage) -- goes to stderr and the process exits 124.  A collective that hangs on one
+    rank thus fails every rank's job with a named stage (init, warmup, timed step, count allgather,
+    records alltoallv, completeness allreduce, parity gather, ...)."""
+
+    def __init__(self, rank: int):
+        import threading
+        self.rank = rank
+        self.scale = float(os.environ.get("OVS_BENCH_STAGE_SCALE", "1.0"))
+        self.stage, self.limit, self.t = "start", 600.0, time.monotonic()
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def set(self, stage: str, limit: float):
+        self.stage, self.limit, self.t = stage, limit * self.scale, time.monotonic()
+
+    def _run(self):
+        while True:
+            time.sleep(2.0)
+            if time.monotonic() - self.t > self.limit:
+                inner = ""
+                try:
+                    import ctypes as C
+                    from oversim_amd.kbr import lib
+                    f = lib().ovs_exchange_stage
+                    f.argtypes, f.restype = [C.POINTER(C.c_uint32)], C.c_char_p
+                    rnd = C.c_uint32(0)
+                    inner = f" (round loop: {f(C.byref(rnd)).decode()}, round {rnd.value})"
+                except Exception:       # noqa: BLE001
+                    pass
+                sys.stderr.write(f"bench.py rank {self.rank}: stage '{self.stage}' stuck for more than "
+                                 f"{self.limit:.0f} s{inner}; exiting\n")
+                sys.stderr.flush()
+                os._exit(124)
+
+
+# lookups of each rank's batch the N > 1 line checks against the oracle (lazy tables above 2^22 nodes)
+PARITY_SAMPLE = {"C": 50_000, "D": 20_000, "E": 10_000}
+
+
+def sharded_parity(sh, kind, ids, xy, keys_t, src_t, m, world, comm_dev, sample, alpha, routing_type) -> dict:
+    """The N > 1 line's correctness evidence.  Lookups migrate, so a lookup's done record lives on the
+    rank where it finished: every rank takes the records it holds of the first `sample` lookups of any
+    rank's batch (qid = home rank x m + index), routes those same (key, source) pairs through the CPU
+    oracle -- the checker cpu_baseline() uses -- and compares every field; the counts are summed over
+    the ranks, so each sampled lookup is checked exactly once, wherever it finished."""
+    import torch
+    import torch.distributed as dist
+    from oversim_amd.shard import done_to_numpy
+    sys.path.insert(0, str(ROOT / "tests"))
+    from oracle_lib import OracleNet, chord_params, kad_params
+    S = int(min(sample, m))
+    kk, ss = keys_t[:S].contiguous().to(comm_dev), src_t[:S].contiguous().to(comm_dev)
+    gk = [torch.empty_like(kk) for _ in range(world)]
+    gs = [torch.empty_like(ss) for _ in range(world)]
+    dist.all_gather(gk, kk)
+    dist.all_gather(gs, ss)
+    K = torch.stack(gk).cpu().numpy().view(np.uint32).reshape(world, S, 5)
+    Sr = torch.stack(gs).cpu().numpy().view(np.uint32).reshape(world, S)
+    d = done_to_numpy(sh._done)
+    q = d["qid"].astype(np.int64)
+    home, idx = q // m, q % m
+    sel = idx < S
+    keys, src = np.ascontiguousarray(K[home[sel], idx[sel]]), np.ascontiguousarray(Sr[home[sel], idx[sel]])
+    fields = ROUTE_FIELDS + (("rpcs",) if kind == "kademlia" else ())
+    per = np.zeros(len(fields), dtype=np.int64)
+    bad = 0
+    if len(keys):
+        o = OracleNet(kind, ids, xy, kad_params(lookupParallelRpcs=alpha) if kind == "kademlia"
+                      else chord_params(routingType=routing_type), lazy=len(ids) > (1 << 22))
+        nthreads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+        r = o.route(keys, src, record_hops=False, count_rpcs=kind == "kademlia", nthreads=nthreads)
+        got = {f: d[f][sel] for f in ROUTE_FIELDS}
+        if kind == "kademlia":
+            got["rpcs"] = d["pad"][sel]
+        wrong = np.zeros(len(keys), dtype=bool)
+        for i, f in enumerate(fields):
+            x = np.asarray(got[f]).astype(np.int64) != np.asarray(r[f]).astype(np.int64)
+            per[i] = int(x.sum())
+            wrong |= x
+        bad = int(wrong.sum())
+    t = torch.tensor([len(keys), bad] + per.tolist(), dtype=torch.int64, device=comm_dev)
+    dist.all_reduce(t)
+    t = t.cpu().tolist()
+    return {"checked": int(t[0]), "expected": world * S, "mismatches": int(t[1]), "fields": list(fields),
+            "per_field": dict(zip(fields, (int(x) for x in t[2:]))), "sample_per_rank": S,
+            "reference": "oracle/ovs_oracle.c (CPU restatement) on each rank's held done records of the sample"
+                         + (" (lazy tables)" if len(ids) > (1 << 22) else "")}
+
+
 def traffic_from_json(path: str | None, workload: str, kname: str):
     """HBM bytes per launch of the dominant kernel from a committed PMC summary
     (profiles/pmc/<workload>.json, written by tools/pmc_json.py from rocprofv3 --pmc FETCH_SIZE and
@@ -243,6 +334,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    wd = Watchdog(rank)
+    wd.set("init", 600)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("OVS_BENCH_BACKEND", "nccl")      # gloo: rehearse N ranks on one GPU
     ndev = torch.cuda.device_count()
@@ -258,10 +351,13 @@ def main():
         json_fd = os.dup(1)
         os.dup2(2, 1)
     if dist_on:
+        from datetime import timedelta
+        # torch's own collectives (barriers, the result all-reduces) give up after 5 minutes
+        tmo = timedelta(seconds=float(os.environ.get("OVS_BENCH_COLLECTIVE_TIMEOUT", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
 
     from oversim_amd import KbrEngine, Params, workload as W
 
@@ -282,6 +378,7 @@ def main():
         sharded = True
 
     # ---- population (identical on every rank) and this rank's lookups, resident in HBM
+    wd.set("population and table build", 600)
     I = W.bench_inputs(a.workload, dev, world=world, rank=rank, seed=a.seed, nodes=a.nodes, n_lookups=a.lookups,
                        sharded=sharded)
     n_total, m, lo, hi = I["n_total"], I["m"], I["lo"], I["hi"]
@@ -345,12 +442,15 @@ def main():
 
     torch.cuda.synchronize()
     torch.cuda.set_stream(stream)        # every launch of a step is ordered on `stream`
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        wd.set(f"warmup step {i}", 180)
         step()
     torch.cuda.synchronize()
+    wd.set("barrier before the timed region", 300)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    wd.set("timed region", 120 + 60 * a.steps)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -363,6 +463,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    wd.set("results", 300)
     step_ms = ev0.elapsed_time(ev1) / max(a.steps, 1)
 
     # ---- work of one step (identical every step: same inputs)
@@ -389,6 +490,14 @@ def main():
             gres["siblings"] = dsib.cpu().numpy().view(np.uint32)
         kern_ms = step_ms
 
+    sparity = None
+    if sharded and world > 1 and os.environ.get("OVS_BENCH_PARITY", "1") != "0":
+        wd.set("sharded parity check (oracle)", 900)
+        sample = int(os.environ.get("OVS_BENCH_PARITY_SAMPLE", PARITY_SAMPLE.get(a.workload, 20_000)))
+        sparity = sharded_parity(sh, kind, ids_np, xy_np, dkeys, dsrc, m, world,
+                                 dev if backend == "nccl" else torch.device("cpu"), sample, wl.get("alpha", 1),
+                                 routing_type)
+        wd.set("results", 300)
     t = torch.tensor([wall, float(hop_total), float(n_ok), float(rpc_total or 0)], dtype=torch.float64, device=dev)
     if world > 1:
         tt = t.to("cpu") if backend != "nccl" else t
@@ -418,8 +527,9 @@ def main():
         if a.traffic_csv:
             traffic, traffic_src = traffic_from_csv(a.traffic_csv, kname), a.traffic_csv
         cpu = None
-        parity = None
+        parity = sparity
         if world == 1 and not a.no_cpu_baseline:
+            wd.set("cpu baseline", 900)
             if ids is None:       # device-generated population (D, E): the oracle needs host copies
                 ids, xy = ids_t.cpu().numpy().view(np.uint32), xy_t.cpu().numpy()
                 keys, src = dkeys[:1 << 20].cpu().numpy().view(np.uint32), dsrc[:1 << 20].cpu().numpy().view(np.uint32)
@@ -502,6 +612,7 @@ def main():
             os.write(json_fd, (json.dumps(line) + "\n").encode())
         else:
             print(json.dumps(line), flush=True)
+    wd.set("teardown", 300)
     if dist_on:
         dist.destroy_process_group()
 

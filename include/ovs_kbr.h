@@ -755,6 +755,12 @@ ovs_status  ovs_exchange_local_create(uint32_t world, ovs_exchange* out);
 void        ovs_exchange_destroy(ovs_exchange* ex);
 /* The last RCCL / exchange error text of this thread (ovs_exchange_* calls have no context) */
 const char* ovs_exchange_last_error(void);
+/* The collective the process's round loop last entered ("count allgather", "records alltoallv",
+ * "completeness allreduce", ..., "idle") and its round: for a caller's watchdog to name a stuck
+ * stage.  Safe to call from any thread (ABI 12).  A failure only one rank sees (allocation, launch,
+ * segment or done-buffer overflow, a rank-local precondition) is carried by the next collective,
+ * so every rank of a sharded route returns a failure from the same round instead of blocking. */
+const char* ovs_exchange_stage(uint32_t* round);
 
 typedef struct ovs_shard_route_stats {
     uint32_t rounds;         /* hop rounds (Chord) / request rounds (Kademlia) of the batch */

@@ -121,6 +121,8 @@ struct KadView {
     uint32_t lo, hi;   // owned arc: sibling / bucket rows of nodes [lo, hi)
     int tl;            // replicated top buckets (KadTables::tl) ...
     uint32_t tend;     // ... in blocks [0, tend): a row offset below tend is a replicated (virtual) row
+    uint32_t nblk;     // blocks of blks[] before the sibling rows (rows_blks): every valid row offset is
+                       // <= nblk, so a larger one names no row of this rank (checked in sharded kernels)
     int maybe_short;
     int snapshot;      // tables built by the snapshot rule (ovs_kad_load), not imported
     unsigned long long* err;   // sharded kernels: a table read this arc cannot serve is counted here

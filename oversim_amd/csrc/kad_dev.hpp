@@ -453,10 +453,11 @@ __device__ __forceinline__ int kad_find_node_blk(const KadView& V, uint32_t c, c
                                                  int pre = -1, int r0 = 0)
 {
     blk_clear(res);
-    if (V.err && kad_off_arc(V, c) && g.boff >= V.tend) {
+    if (V.err && ((kad_off_arc(V, c) && g.boff >= V.tend) || g.boff > V.nblk)) {
         // sharded kernels: c's bucket and sibling rows live on its owner only -- counted
         // (ovs_kad_shard_errors), answered empty.  (A row offset below V.tend names c's replicated
-        // top buckets, which every rank holds.)
+        // top buckets, which every rank holds.)  A row offset past this rank's rows (another arc's
+        // layout, the round-5 fault) is counted the same way, never dereferenced.
         kad_count_error(V);
         return 0;
     }
@@ -1358,7 +1359,11 @@ __device__ __forceinline__ void kad_coop_sibzone(const KadView& V, bool want, ui
         for (int w = 0; w < 5; ++w) oK.w[w] = __shfl(K.w[w], owner);
         const int nmain = og.m >= 0 && og.rowlo >= 0 && og.m >= og.rowlo ? 1 : 0;   // k <= 8: one block
         const int j0 = orb & 15, nsb = (orb >> 4) - j0 + 1;   // the row blocks that matter (kad_row_blocks)
-        const int nitems = live ? nmain + nsb : 0;
+        // sharded kernels: a responder whose rows this rank does not hold (off the arc, or a row
+        // offset past its rows) is counted and answered empty, as in kad_find_node_blk
+        const bool foreign = V.err && live && (kad_off_arc(V, oc) || og.boff > V.nblk);
+        if (foreign && j == 0) kad_count_error(V);
+        const int nitems = live && !foreign ? nmain + nsb : 0;
         auto load_item = [&](int i, Blk8& b) -> int {
             if (i < nmain) return blk_load_block(b, slot_blk(V, og.boff, og.m), oK);
             return blk_load_block(b, V.sibb + (uint64_t)(oc - V.lo) * V.sbn + (uint64_t)(j0 + i - nmain), oK);
@@ -1481,6 +1486,7 @@ inline KadView kad_make_view(const KadTables& t, const double2* xy, uint32_t n)
     V.sbn = (V.S5 + 1 + KBLK - 1) / KBLK;     // c itself + its siblings
     V.lo = t.lo; V.hi = t.hi;
     V.tl = t.tl; V.tend = (uint32_t)t.tend;
+    V.nblk = t.rows_blks < 0xFFFFFFFFull ? (uint32_t)t.rows_blks : 0xFFFFFFFFu;
     V.maybe_short = t.maybe_short;
     V.snapshot = t.snapshot;
     return V;

@@ -22,6 +22,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -144,12 +145,62 @@ ovs_status check_exchange(ovs_ctx* c, const ovs_exchange* ex, const uint64_t* sh
     return OVS_OK;
 }
 
-// the batch is complete on every rank: finished records (all ranks) == lookups started (all ranks)
-ovs_status check_totals(ovs_ctx* c, const ovs_exchange* ex, int64_t have, int64_t want, int64_t sentinel,
-                        double& xms, const char* what)
+// A failure only one rank sees (an allocation, a step that did not launch, a segment or done-buffer
+// overflow) must not leave the other ranks blocked in the next collective.  It is recorded here and
+// carried by that collective -- a status slot of the count all-gather, or a term of check_totals' sum
+// -- so every rank returns a failure from the same round.  (no early return between
+// collectives.)
+struct LocalErr {
+    ovs_status st = OVS_OK;
+    std::string msg;
+    void set(ovs_status s, const std::string& m)
+    {
+        if (st == OVS_OK) { st = s; msg = m; }
+    }
+    void hip(hipError_t e, const char* what)
+    {
+        if (e != hipSuccess) set(OVS_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    }
+    bool ok() const { return st == OVS_OK; }
+};
+
+// the collective every rank is in (read by a caller's watchdog through ovs_exchange_stage)
+std::atomic<const char*> g_stage{"idle"};
+std::atomic<uint32_t> g_stage_round{0};
+
+void stage(const char* s, uint32_t round)
 {
-    int64_t v[3] = {have, want, sentinel};
-    XCHK(ex->allreduce_sum_i64(ex->user, v, 3), "allreduce");
+    g_stage_round.store(round, std::memory_order_relaxed);
+    g_stage.store(s, std::memory_order_release);
+}
+
+// after a gathered status slot: every rank fails when any did (its own message, or the failing rank)
+ovs_status gathered_failure(ovs_ctx* c, const LocalErr& le, const int64_t* M, uint32_t W, uint32_t stride,
+                            uint32_t slot, const char* what)
+{
+    int first = -1, nfail = 0;
+    for (uint32_t r = 0; r < W; ++r)
+        if (M[(size_t)r * stride + slot] != 0) { if (first < 0) first = (int)r; ++nfail; }
+    if (nfail == 0) return OVS_OK;
+    if (!le.ok()) return ctx_fail(c, le.st, std::string(what) + ": " + le.msg);
+    return ctx_fail(c, (ovs_status)M[(size_t)first * stride + slot],
+                    std::string(what) + ": rank " + std::to_string(first) + " failed (" + std::to_string(nfail) +
+                        " rank(s)); its error names the cause");
+}
+
+// the batch is complete on every rank: finished records (all ranks) == lookups started (all ranks);
+// a local failure on any rank fails all of them here
+ovs_status check_totals(ovs_ctx* c, const ovs_exchange* ex, int64_t have, int64_t want, int64_t sentinel,
+                        const LocalErr& le, double& xms, const char* what)
+{
+    int64_t v[4] = {have, want, sentinel, le.ok() ? 0 : 1};
+    stage("completeness allreduce", 0);
+    XCHK(ex->allreduce_sum_i64(ex->user, v, 4), "allreduce");
+    if (v[3] != 0) {
+        if (!le.ok()) return ctx_fail(c, le.st, std::string(what) + ": " + le.msg);
+        return ctx_fail(c, OVS_EDEVICE, std::string(what) + ": " + std::to_string(v[3]) +
+                                            " other rank(s) failed; their errors name the cause");
+    }
     if (v[2] != 0)
         return ctx_fail(c, OVS_EDEVICE, std::string(what) + ": " + std::to_string(v[2]) +
                                             " finished records came from exchange rows nobody wrote");
@@ -180,105 +231,154 @@ ovs_status route_records(ovs_ctx* c, const ovs_exchange* ex, uint64_t n, uint32_
     // the cohort count must be the same on every rank (every cohort takes part in every round's
     // collectives until the gathered counts say it is done everywhere): not derived from n
     const int nc = cohorts == 0 ? 2 : (int)std::min<uint32_t>(cohorts, 4);
+    // a cohort's all-gather row: [0, W) records for each destination, W = this rank's status
+    // (LocalErr), W + 1 = its receive buffer's capacity in rows
+    const uint32_t SW = W + 2, SLOT_ST = W, SLOT_CAP = W + 1;
+    LocalErr le;
     RCHK(hipSetDevice(ctx_device(c)));
     RouteScratch* R = scratch(c);
     hipStream_t s0 = (hipStream_t)stream;
     hipStream_t cs[4];
     for (int k = 0; k < nc; ++k) {
         cs[k] = ctx_cohort_stream(c, k);
-        if (!cs[k]) return ctx_fail(c, OVS_EDEVICE, "cohort stream");
+        if (!cs[k]) le.set(OVS_EDEVICE, "cohort stream");
     }
-    RCHK(ensure(R->done_cnt, sizeof(unsigned long long), s0));
-    unsigned long long* dcnt = static_cast<unsigned long long*>(R->done_cnt.p);
-    RCHK(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long), s0));
-    // every cohort stream starts after the caller's stream (inputs, the counter reset)
-    RCHK(hipEventRecord(mk_event(&R->ev, false), s0));
+    unsigned long long* dcnt = nullptr;
+    if (le.ok()) {
+        le.hip(ensure(R->done_cnt, sizeof(unsigned long long), s0), "done counter");
+        if (le.ok()) {
+            dcnt = static_cast<unsigned long long*>(R->done_cnt.p);
+            le.hip(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long), s0), "done counter reset");
+        }
+        // every cohort stream starts after the caller's stream (inputs, the counter reset)
+        if (le.ok()) le.hip(hipEventRecord(mk_event(&R->ev, false), s0), "start event");
+    }
     uint64_t nin[4] = {0, 0, 0, 0}, cap[4] = {0, 0, 0, 0};
     bool live[4] = {false, false, false, false};
-    std::vector<int64_t> M((size_t)W * W);
+    std::vector<int64_t> M((size_t)W * SW);
     std::vector<uint64_t> scl(W), rcl(W), roff(W);
     std::vector<const void*> sendp(W);
     uint64_t sent = 0, sent_bytes = 0;
-    auto issue = [&](int k, bool first, uint64_t b0) -> ovs_status {
+    // queue one round of cohort k; a failure is recorded, not returned (the cohort's next all-gather
+    // carries it)
+    auto issue = [&](int k, bool first, uint64_t b0) {
+        if (!le.ok()) return;
         CohortBufs& B = R->coh[k];
         // a segment receives at most the step's input records
         cap[k] = std::max<uint64_t>(nin[k], 1);
         if (ensure(B.out, (size_t)W * cap[k] * RB, cs[k]) != hipSuccess ||
-            ensure(B.cnt, sizeof(unsigned long long) * W, cs[k]) != hipSuccess)
-            return ctx_fail(c, OVS_ENOMEM, "shard route: segment allocation");
+            ensure(B.cnt, sizeof(unsigned long long) * W, cs[k]) != hipSuccess) {
+            le.set(OVS_ENOMEM, "shard route: segment allocation");
+            return;
+        }
         cap[k] = B.out.cap / ((size_t)W * RB);
-        RCHK(hipMemsetAsync(B.cnt.p, 0, sizeof(unsigned long long) * W, cs[k]));
-        RCHK(hipEventRecord(mk_event(&B.e0, true), cs[k]));
-        const ovs_status s = step(k, first, first ? nullptr : B.recv.p, nin[k], b0, B.out.p, cap[k],
-                                  static_cast<unsigned long long*>(B.cnt.p), dcnt, cs[k]);
-        if (s != OVS_OK) return s;
-        RCHK(hipEventRecord(mk_event(&B.e1, true), cs[k]));
-        return OVS_OK;
+        le.hip(hipMemsetAsync(B.cnt.p, 0, sizeof(unsigned long long) * W, cs[k]), "count reset");
+        if (le.ok()) le.hip(hipEventRecord(mk_event(&B.e0, true), cs[k]), "step event");
+        if (!le.ok()) return;
+        const ovs_status st = step(k, first, first ? nullptr : B.recv.p, nin[k], b0, B.out.p, cap[k],
+                                   static_cast<unsigned long long*>(B.cnt.p), dcnt, cs[k]);
+        if (st != OVS_OK) { le.set(st, ovs_last_error(c)); return; }
+        le.hip(hipEventRecord(mk_event(&B.e1, true), cs[k]), "step event");
     };
-    ovs_status st;
     for (int k = 0; k < nc; ++k) {
-        RCHK(hipStreamWaitEvent(cs[k], R->ev, 0));
+        if (le.ok()) le.hip(hipStreamWaitEvent(cs[k], R->ev, 0), "cohort start");
         const uint64_t b0 = (uint64_t)k * n / nc, b1 = (uint64_t)(k + 1) * n / nc;
         nin[k] = b1 - b0;
         live[k] = true;
-        st = issue(k, true, b0);
-        if (st != OVS_OK) return st;
+        issue(k, true, b0);
     }
     uint32_t rounds = 1;
-    std::vector<int64_t> hc(W);
+    std::vector<int64_t> hc(SW);
     while (true) {
         bool any = false;
         for (int k = 0; k < nc; ++k) {
             if (!live[k]) continue;
             CohortBufs& B = R->coh[k];
             // this cohort's counts on the host (waits for its step), then every rank's
-            RCHK(hipMemcpyAsync(hc.data(), B.cnt.p, sizeof(int64_t) * W, hipMemcpyDeviceToHost, cs[k]));
-            RCHK(hipStreamSynchronize(cs[k]));
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, B.e0, B.e1) == hipSuccess) kms += ms;
-            XCHK(ex->allgather_i64(ex->user, hc.data(), W, M.data()), "allgather");
+            std::fill(hc.begin(), hc.end(), 0);
+            if (le.ok()) {
+                le.hip(hipMemcpyAsync(hc.data(), B.cnt.p, sizeof(int64_t) * W, hipMemcpyDeviceToHost, cs[k]), "counts");
+                if (le.ok()) le.hip(hipStreamSynchronize(cs[k]), "cohort step");
+                float ms = 0;
+                if (le.ok() && hipEventElapsedTime(&ms, B.e0, B.e1) == hipSuccess) kms += ms;
+                for (uint32_t r = 0; r < W && le.ok(); ++r)
+                    if ((uint64_t)hc[r] > cap[k]) le.set(OVS_EDEVICE, "shard route: a segment overflowed");
+                if (!le.ok()) std::fill(hc.begin(), hc.end(), 0);
+            }
+            hc[SLOT_ST] = le.st;
+            hc[SLOT_CAP] = (int64_t)(B.recv.cap / RB);
+            stage("count allgather", rounds);
+            XCHK(ex->allgather_i64(ex->user, hc.data(), SW, M.data()), "allgather");
+            const ovs_status gf = gathered_failure(c, le, M.data(), W, SW, SLOT_ST, what);
+            if (gf != OVS_OK) return gf;
             int64_t tot = 0;
-            for (int64_t v : M) tot += v;
+            for (uint32_t r = 0; r < W; ++r)
+                for (uint32_t d = 0; d < W; ++d) tot += M[(size_t)r * SW + d];
             if (tot == 0) { live[k] = false; continue; }
             any = true;
+            // receive buffers: every rank sees which ones must grow; if any, one allreduce tells all
+            // ranks whether every allocation succeeded before anyone enters the all-to-allv
+            bool grow = false;
             uint64_t tin = 0;
             for (uint32_t r = 0; r < W; ++r) {
-                scl[r] = (uint64_t)M[(size_t)me * W + r];
-                rcl[r] = (uint64_t)M[(size_t)r * W + me];
-                roff[r] = tin;
-                tin += rcl[r];
+                uint64_t in_r = 0;
+                for (uint32_t s = 0; s < W; ++s) in_r += (uint64_t)M[(size_t)s * SW + r];
+                if (in_r > (uint64_t)M[(size_t)r * SW + SLOT_CAP]) grow = true;
+                if (r == me) tin = in_r;
+            }
+            if (grow) {
+                int64_t bad[1] = {ensure(B.recv, std::max<size_t>((size_t)tin * RB, RB), cs[k]) != hipSuccess ? 1 : 0};
+                stage("buffer allreduce", rounds);
+                XCHK(ex->allreduce_sum_i64(ex->user, bad, 1), "allreduce");
+                if (bad[0] != 0) return ctx_fail(c, OVS_ENOMEM, std::string(what) + ": receive buffer allocation failed on " +
+                                                                   std::to_string(bad[0]) + " rank(s)");
+            }
+            uint64_t off = 0;
+            for (uint32_t r = 0; r < W; ++r) {
+                scl[r] = (uint64_t)M[(size_t)me * SW + r];
+                rcl[r] = (uint64_t)M[(size_t)r * SW + me];
+                roff[r] = off;
+                off += rcl[r];
                 if (r != me) { sent += scl[r]; sent_bytes += scl[r] * RB; }
                 sendp[r] = static_cast<const uint8_t*>(B.out.p) + (size_t)r * cap[k] * RB;
-                if (scl[r] > cap[k]) return ctx_fail(c, OVS_EDEVICE, "shard route: a segment overflowed");
             }
-            if (ensure(B.recv, std::max<size_t>((size_t)tin * RB, RB), cs[k]) != hipSuccess)
-                return ctx_fail(c, OVS_ENOMEM, "shard route: receive buffer");
             // sentinel: a row the exchange never writes reads as an impossible record
-            RCHK(hipMemsetAsync(B.recv.p, 0xFF, (size_t)tin * RB, cs[k]));
+            le.hip(hipMemsetAsync(B.recv.p, 0xFF, (size_t)tin * RB, cs[k]), "receive sentinel");
+            stage("records alltoallv", rounds);
             XCHK(ex->alltoallv(ex->user, sendp.data(), scl.data(), B.recv.p, roff.data(), rcl.data(), RB, cs[k]),
                  "alltoallv");
             nin[k] = tin;
-            st = issue(k, false, 0);
-            if (st != OVS_OK) return st;
+            issue(k, false, 0);
         }
         if (!any) break;
-        if (++rounds > 10000) return ctx_fail(c, OVS_EDEVICE, std::string(what) + " did not terminate");
+        if (++rounds > 10000) {
+            // every rank counts the same rounds: all stop here
+            return ctx_fail(c, OVS_EDEVICE, std::string(what) + " did not terminate");
+        }
     }
     // the caller's stream continues after every cohort
     R->cev.resize(std::max<size_t>(R->cev.size(), (size_t)nc), nullptr);
-    for (int k = 0; k < nc; ++k) {
-        RCHK(hipEventRecord(mk_event(&R->cev[k], false), cs[k]));
-        RCHK(hipStreamWaitEvent(s0, R->cev[k], 0));
+    for (int k = 0; k < nc && le.ok(); ++k) {
+        le.hip(hipEventRecord(mk_event(&R->cev[k], false), cs[k]), "cohort end event");
+        if (le.ok()) le.hip(hipStreamWaitEvent(s0, R->cev[k], 0), "cohort join");
     }
     unsigned long long hd = 0, hs = 0;
-    RCHK(hipMemcpyAsync(&hd, dcnt, sizeof hd, hipMemcpyDeviceToHost, s0));
-    RCHK(hipStreamSynchronize(s0));
-    if (hd > done_cap) return ctx_fail(c, OVS_EINVAL, "done buffer overflow (done_cap too small)");
-    RCHK(ensure(R->sentinel, sizeof(unsigned long long), s0));
-    RCHK(count_sentinel_records(done, hd, static_cast<unsigned long long*>(R->sentinel.p), s0));
-    RCHK(hipMemcpyAsync(&hs, R->sentinel.p, sizeof hs, hipMemcpyDeviceToHost, s0));
-    RCHK(hipStreamSynchronize(s0));
-    st = check_totals(c, ex, (int64_t)hd, (int64_t)n, (int64_t)hs, xms, what);
+    if (le.ok()) {
+        le.hip(hipMemcpyAsync(&hd, dcnt, sizeof hd, hipMemcpyDeviceToHost, s0), "done count");
+        if (le.ok()) le.hip(hipStreamSynchronize(s0), "done count");
+    }
+    if (le.ok() && hd > done_cap)
+        le.set(OVS_EINVAL, "done buffer overflow (done_cap " + std::to_string(done_cap) + " < " + std::to_string(hd) +
+                               " finished records)");
+    if (le.ok()) {
+        le.hip(ensure(R->sentinel, sizeof(unsigned long long), s0), "sentinel counter");
+        if (le.ok())
+            le.hip(count_sentinel_records(done, hd, static_cast<unsigned long long*>(R->sentinel.p), s0), "sentinel count");
+        if (le.ok()) le.hip(hipMemcpyAsync(&hs, R->sentinel.p, sizeof hs, hipMemcpyDeviceToHost, s0), "sentinel count");
+        if (le.ok()) le.hip(hipStreamSynchronize(s0), "sentinel count");
+    }
+    const ovs_status st = check_totals(c, ex, (int64_t)hd, (int64_t)n, (int64_t)hs, le, xms, what);
+    stage("idle", 0);
     if (st != OVS_OK) return st;
     *n_done = hd;
     if (stats) {
@@ -346,101 +446,164 @@ ovs_status ovs_kad_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const u
                            "sharded Kademlia (migration)");
         if (st != OVS_OK) return st;
         uint64_t bad = 0;
-        if ((st = ovs_kad_shard_errors(c, &bad)) != OVS_OK) return st;
-        int64_t v[1] = {(int64_t)bad};
+        LocalErr le;
+        const ovs_status es = ovs_kad_shard_errors(c, &bad);
+        if (es != OVS_OK) le.set(es, ovs_last_error(c));
+        int64_t v[2] = {(int64_t)bad, le.ok() ? 0 : 1};
         double xms = 0;
-        XCHK(ex->allreduce_sum_i64(ex->user, v, 1), "allreduce");
+        stage("error allreduce", 0);
+        XCHK(ex->allreduce_sum_i64(ex->user, v, 2), "allreduce");
+        stage("idle", 0);
         if (stats) stats->exchange_ms += xms;
+        if (!le.ok()) return ctx_fail(c, le.st, le.msg);
+        if (v[1] != 0) return ctx_fail(c, OVS_EDEVICE, "sharded Kademlia (migration): another rank failed");
         if (v[0] != 0)
             return ctx_fail(c, OVS_EDEVICE, std::to_string(v[0]) + " Kademlia shard errors (table reads off an arc)");
         return OVS_OK;
     }
-    if (done_cap < n) return ctx_fail(c, OVS_EINVAL, "done_cap must hold the batch (Kademlia lookups finish at home)");
     const double t_start = now_ms();
     double xms = 0, kms = 0;
     const uint32_t W = ex->world, me = ex->rank;
+    // local failures ride the next collective (LocalErr): preconditions that depend on this rank's
+    // own batch, allocations, launches
+    LocalErr le;
+    if (done_cap < n) le.set(OVS_EINVAL, "done_cap must hold the batch (Kademlia lookups finish at home)");
     RCHK(hipSetDevice(ctx_device(c)));
     RouteScratch* R = scratch(c);
     hipStream_t s = (hipStream_t)stream;
     ovs_params P;
     if ((st = ovs_get_params(c, &P)) != OVS_OK) return st;
-    if (num_siblings >= -1) st = ovs_kad_shard_begin_lookup(c, num_siblings, keys, src, n, qid_base, siblings, stream);
-    else st = ovs_kad_shard_begin(c, keys, src, n, qid_base, stream);
-    if (st != OVS_OK) return st;
+    if (le.ok()) {
+        if (num_siblings >= -1) st = ovs_kad_shard_begin_lookup(c, num_siblings, keys, src, n, qid_base, siblings, stream);
+        else st = ovs_kad_shard_begin(c, keys, src, n, qid_base, stream);
+        if (st != OVS_OK) le.set(st, ovs_last_error(c));
+    }
     const int rb = ovs_kad_shard_resp_bytes(c);
     if (rb <= 0) return ctx_fail(c, OVS_ESTATE, "no Kademlia network loaded");
     const uint32_t RB = (uint32_t)rb, QB = sizeof(ovs_kad_req);
     // one round sends at most one request per pending-call slot of every lookup
     const uint64_t slots = P.lookupParallelRpcs <= 4 ? (uint64_t)P.lookupParallelRpcs : 8;
     const uint64_t seg = std::max<uint64_t>(n * slots, 1);
-    if (ensure(R->kout, (size_t)W * seg * QB, s) != hipSuccess || ensure(R->kcnt, sizeof(unsigned long long) * (W + 2), s) != hipSuccess)
-        return ctx_fail(c, OVS_ENOMEM, "kademlia shard route: buffers");
+    if (le.ok() && (ensure(R->kout, (size_t)W * seg * QB, s) != hipSuccess ||
+                    ensure(R->kcnt, sizeof(unsigned long long) * (W + 2), s) != hipSuccess))
+        le.set(OVS_ENOMEM, "kademlia shard route: buffers");
     auto* cnt = static_cast<unsigned long long*>(R->kcnt.p);
-    RCHK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * (W + 2), s));
+    if (le.ok()) le.hip(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * (W + 2), s), "counter reset");
     hipEvent_t e0 = nullptr, e1 = nullptr;
     RCHK(hipEventCreate(&e0));
     RCHK(hipEventCreate(&e1));
     struct EvFree { hipEvent_t a, b; ~EvFree() { hipEventDestroy(a); hipEventDestroy(b); } } evf{e0, e1};
-    std::vector<int64_t> M((size_t)W * (W + 1)), hc(W + 1);
+    // all-gather row: [0, W) requests to each rank, W = lookups still active here, W + 1 = status,
+    // W + 2 = request/response rows the receive buffers hold, W + 3 = rows the response buffer holds
+    const uint32_t SW = W + 4, SLOT_ACT = W, SLOT_ST = W + 1, SLOT_CIN = W + 2, SLOT_CBK = W + 3;
+    std::vector<int64_t> M((size_t)W * SW), hc(SW);
     std::vector<uint64_t> scl(W), rcl(W), roff(W), boff(W);
     std::vector<const void*> sendp(W), backp(W);
     uint64_t sent = 0, sent_bytes = 0;
     uint32_t rounds = 0;
+    auto rows = [](const DevBuf& b, uint32_t row) { return (int64_t)(b.cap / row); };
     while (true) {
         if (++rounds > 5000) return ctx_fail(c, OVS_EDEVICE, "sharded Kademlia routing did not terminate");
-        RCHK(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * W, s));
-        RCHK(hipEventRecord(e0, s));
-        st = ovs_kad_shard_step(c, static_cast<ovs_kad_req*>(R->kout.p), seg, cnt, done, done_cap, cnt + W + 1, cnt + W,
-                                shard_lo, W, stream);
-        if (st != OVS_OK) return st;
-        RCHK(hipEventRecord(e1, s));
-        RCHK(hipMemcpyAsync(hc.data(), cnt, sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, s));
-        RCHK(hipStreamSynchronize(s));
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) kms += ms;
+        std::fill(hc.begin(), hc.end(), 0);
+        if (le.ok()) {
+            le.hip(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * W, s), "counter reset");
+            if (le.ok()) le.hip(hipEventRecord(e0, s), "step event");
+            if (le.ok()) {
+                st = ovs_kad_shard_step(c, static_cast<ovs_kad_req*>(R->kout.p), seg, cnt, done, done_cap, cnt + W + 1,
+                                        cnt + W, shard_lo, W, stream);
+                if (st != OVS_OK) le.set(st, ovs_last_error(c));
+            }
+            if (le.ok()) le.hip(hipEventRecord(e1, s), "step event");
+            if (le.ok()) le.hip(hipMemcpyAsync(hc.data(), cnt, sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, s), "counts");
+            if (le.ok()) le.hip(hipStreamSynchronize(s), "step");
+            float ms = 0;
+            if (le.ok() && hipEventElapsedTime(&ms, e0, e1) == hipSuccess) kms += ms;
+            if (!le.ok()) std::fill(hc.begin(), hc.end(), 0);
+        }
+        hc[SLOT_ST] = le.st;
+        hc[SLOT_CIN] = std::min(rows(R->kreq, QB), rows(R->kresp, RB));
+        hc[SLOT_CBK] = rows(R->kback, RB);
         // M[r, d] requests r -> d, M[r, W] lookups still active on r
-        XCHK(ex->allgather_i64(ex->user, hc.data(), W + 1, M.data()), "allgather");
+        stage("request-count allgather", rounds);
+        XCHK(ex->allgather_i64(ex->user, hc.data(), SW, M.data()), "allgather");
+        const ovs_status gf = gathered_failure(c, le, M.data(), W, SW, SLOT_ST, "sharded Kademlia");
+        if (gf != OVS_OK) return gf;
         int64_t tot = 0;
-        for (int64_t v : M) tot += v;
+        for (uint32_t r = 0; r < W; ++r)
+            for (uint32_t d = 0; d <= W; ++d) tot += M[(size_t)r * SW + d];
         if (tot == 0) break;
+        // buffer growth decided identically on every rank (see route_records)
+        bool grow = false;
         uint64_t tin = 0, tback = 0;
         for (uint32_t r = 0; r < W; ++r) {
-            scl[r] = (uint64_t)M[(size_t)me * (W + 1) + r];
-            rcl[r] = (uint64_t)M[(size_t)r * (W + 1) + me];
-            roff[r] = tin; tin += rcl[r];
-            boff[r] = tback; tback += scl[r];
+            uint64_t in_r = 0, back_r = 0;
+            for (uint32_t q = 0; q < W; ++q) {
+                in_r += (uint64_t)M[(size_t)q * SW + r];
+                back_r += (uint64_t)M[(size_t)r * SW + q];
+            }
+            if (in_r > (uint64_t)M[(size_t)r * SW + SLOT_CIN] || back_r > (uint64_t)M[(size_t)r * SW + SLOT_CBK]) grow = true;
+            if (r == me) { tin = in_r; tback = back_r; }
+        }
+        if (grow) {
+            int64_t bad[1] = {(ensure(R->kreq, std::max<size_t>((size_t)tin * QB, QB), s) != hipSuccess ||
+                               ensure(R->kresp, std::max<size_t>((size_t)tin * RB, RB), s) != hipSuccess ||
+                               ensure(R->kback, std::max<size_t>((size_t)tback * RB, RB), s) != hipSuccess) ? 1 : 0};
+            stage("buffer allreduce", rounds);
+            XCHK(ex->allreduce_sum_i64(ex->user, bad, 1), "allreduce");
+            if (bad[0] != 0)
+                return ctx_fail(c, OVS_ENOMEM, "kademlia shard route: exchange buffers failed on " + std::to_string(bad[0]) +
+                                                   " rank(s)");
+        }
+        uint64_t oin = 0, oback = 0;
+        for (uint32_t r = 0; r < W; ++r) {
+            scl[r] = (uint64_t)M[(size_t)me * SW + r];
+            rcl[r] = (uint64_t)M[(size_t)r * SW + me];
+            roff[r] = oin; oin += rcl[r];
+            boff[r] = oback; oback += scl[r];
             if (r != me) { sent += scl[r]; sent_bytes += scl[r] * (QB + RB); }
             sendp[r] = static_cast<const uint8_t*>(R->kout.p) + (size_t)r * seg * QB;
         }
-        if (ensure(R->kreq, std::max<size_t>((size_t)tin * QB, QB), s) != hipSuccess ||
-            ensure(R->kresp, std::max<size_t>((size_t)tin * RB, RB), s) != hipSuccess ||
-            ensure(R->kback, std::max<size_t>((size_t)tback * RB, RB), s) != hipSuccess)
-            return ctx_fail(c, OVS_ENOMEM, "kademlia shard route: exchange buffers");
         // requests to the responders' owners (0xFF-filled: a request nobody wrote is refused by serve)
-        RCHK(hipMemsetAsync(R->kreq.p, 0xFF, (size_t)tin * QB, s));
+        le.hip(hipMemsetAsync(R->kreq.p, 0xFF, (size_t)tin * QB, s), "request sentinel");
+        stage("request alltoallv", rounds);
         XCHK(ex->alltoallv(ex->user, sendp.data(), scl.data(), R->kreq.p, roff.data(), rcl.data(), QB, stream),
              "alltoallv (requests)");
-        st = ovs_kad_shard_serve(c, static_cast<const ovs_kad_req*>(R->kreq.p), tin, R->kresp.p, stream);
-        if (st != OVS_OK) return st;
+        if (le.ok()) {
+            st = ovs_kad_shard_serve(c, static_cast<const ovs_kad_req*>(R->kreq.p), tin, R->kresp.p, stream);
+            if (st != OVS_OK) le.set(st, ovs_last_error(c));
+        }
+        // a rank whose serve failed still answers (0xFF rows: unknown tags, deliver counts them as
+        // errors), so nobody waits; the failure is gathered next round
+        if (!le.ok()) le.hip(hipMemsetAsync(R->kresp.p, 0xFF, (size_t)tin * RB, s), "response sentinel");
         // the responses back with the reverse splits (a response nobody wrote has an unknown tag:
         // deliver counts it as an error)
         for (uint32_t r = 0; r < W; ++r) backp[r] = static_cast<const uint8_t*>(R->kresp.p) + (size_t)roff[r] * RB;
-        RCHK(hipMemsetAsync(R->kback.p, 0xFF, (size_t)tback * RB, s));
+        le.hip(hipMemsetAsync(R->kback.p, 0xFF, (size_t)tback * RB, s), "response buffer sentinel");
+        stage("response alltoallv", rounds);
         XCHK(ex->alltoallv(ex->user, backp.data(), rcl.data(), R->kback.p, boff.data(), scl.data(), RB, stream),
              "alltoallv (responses)");
-        st = ovs_kad_shard_deliver(c, R->kback.p, tback, stream);
-        if (st != OVS_OK) return st;
+        if (le.ok()) {
+            st = ovs_kad_shard_deliver(c, R->kback.p, tback, stream);
+            if (st != OVS_OK) le.set(st, ovs_last_error(c));
+        }
     }
     unsigned long long hd = 0;
-    RCHK(hipMemcpyAsync(&hd, cnt + W + 1, sizeof hd, hipMemcpyDeviceToHost, s));
-    RCHK(hipStreamSynchronize(s));
+    le.hip(hipMemcpyAsync(&hd, cnt + W + 1, sizeof hd, hipMemcpyDeviceToHost, s), "done count");
+    if (le.ok()) le.hip(hipStreamSynchronize(s), "done count");
     uint64_t bad = 0;
-    if ((st = ovs_kad_shard_errors(c, &bad)) != OVS_OK) return st;
-    if (hd > done_cap) return ctx_fail(c, OVS_EINVAL, "done buffer overflow");
+    if (le.ok()) {
+        const ovs_status es = ovs_kad_shard_errors(c, &bad);
+        if (es != OVS_OK) le.set(es, ovs_last_error(c));
+    }
+    if (le.ok() && hd > done_cap) le.set(OVS_EINVAL, "done buffer overflow");
     // every rank finishes exactly its own lookups; errors (undeliverable responses, reads off the arc,
-    // sources off the arc) fail the batch on every rank
-    int64_t v[3] = {(int64_t)hd == (int64_t)n ? 0 : 1, (int64_t)bad, 0};
+    // sources off the arc, local failures) fail the batch on every rank
+    int64_t v[3] = {(int64_t)hd == (int64_t)n ? 0 : 1, (int64_t)bad, le.ok() ? 0 : 1};
+    stage("completeness allreduce", 0);
     XCHK(ex->allreduce_sum_i64(ex->user, v, 3), "allreduce");
+    stage("idle", 0);
+    if (!le.ok()) return ctx_fail(c, le.st, "sharded Kademlia: " + le.msg);
+    if (v[2] != 0) return ctx_fail(c, OVS_EDEVICE, "sharded Kademlia: " + std::to_string(v[2]) + " other rank(s) failed");
     if (v[1] != 0)
         return ctx_fail(c, OVS_EDEVICE, std::to_string(v[1]) + " Kademlia shard errors: responses that could not be "
                                         "delivered, table reads off an arc, or sources off their rank's arc");
@@ -675,12 +838,14 @@ int local_allgather(void* user, const int64_t* host_send, uint32_t n, int64_t* h
     LocalShared* S = X->sh;
     S->vals[X->rank].assign(host_send, host_send + n);
     S->barrier();
+    int rc = 0;
     for (uint32_t r = 0; r < S->world; ++r) {
-        if (S->vals[r].size() != n) return ex_fail("local allgather: ranks disagree on the count");
+        if (S->vals[r].size() != n) { rc = ex_fail("local allgather: ranks disagree on the count"); break; }
         std::memcpy(host_recv + (size_t)r * n, S->vals[r].data(), sizeof(int64_t) * n);
     }
+    // every rank reaches the second barrier, failed or not, so the arrival count stays in step
     S->barrier();
-    return 0;
+    return rc;
 }
 
 int local_allreduce(void* user, int64_t* values, uint32_t n)
@@ -689,13 +854,16 @@ int local_allreduce(void* user, int64_t* values, uint32_t n)
     LocalShared* S = X->sh;
     S->vals[X->rank].assign(values, values + n);
     S->barrier();
-    for (uint32_t i = 0; i < n; ++i) {
+    int rc = 0;
+    for (uint32_t r = 0; r < S->world; ++r)
+        if (S->vals[r].size() != n) rc = ex_fail("local allreduce: ranks disagree on the count");
+    for (uint32_t i = 0; i < n && rc == 0; ++i) {
         int64_t t = 0;
         for (uint32_t r = 0; r < S->world; ++r) t += S->vals[r][i];
         values[i] = t;
     }
     S->barrier();
-    return 0;
+    return rc;
 }
 
 int local_alltoallv(void* user, const void* const* send, const uint64_t* send_rows, void* recv, const uint64_t* recv_off,
@@ -746,6 +914,12 @@ void local_destroy(void* user)
 extern "C" {
 
 const char* ovs_exchange_last_error(void) { return g_ex_err.c_str(); }
+
+const char* ovs_exchange_stage(uint32_t* round)
+{
+    if (round) *round = g_stage_round.load(std::memory_order_relaxed);
+    return g_stage.load(std::memory_order_acquire);
+}
 
 ovs_status ovs_rccl_unique_id(void* unique_id_128)
 {

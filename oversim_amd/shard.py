@@ -280,6 +280,8 @@ lib().ovs_exchange_destroy.argtypes = [C.c_void_p]
 lib().ovs_exchange_destroy.restype = None
 lib().ovs_exchange_last_error.argtypes = []
 lib().ovs_exchange_last_error.restype = C.c_char_p
+lib().ovs_exchange_stage.argtypes = [C.POINTER(C.c_uint32)]
+lib().ovs_exchange_stage.restype = C.c_char_p
 lib().ovs_chord_shard_levels.argtypes = [C.c_void_p]
 lib().ovs_chord_shard_levels.restype = C.c_int32
 lib().ovs_kad_shard_levels.argtypes = [C.c_void_p]
@@ -444,19 +446,30 @@ class CallbackExchange:
         return self._guard(run)
 
 
+def exchange_sum(ex: Exchange, values) -> list:
+    """Element-wise sum of int64 values over the exchange's ranks (its allreduce callback): a
+    collective -- every rank calls it."""
+    arr = (C.c_int64 * len(values))(*[int(v) for v in values])
+    if ex.allreduce_sum_i64(ex.user, arr, len(values)) != 0:
+        raise RuntimeError(f"exchange allreduce failed: {lib().ovs_exchange_last_error().decode()}")
+    return list(arr)
+
+
 def native_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, cohorts: int = 2, num_siblings: int = 0,
-                 stream=None) -> tuple:
+                 stream=None, done_cap: int | None = None) -> tuple:
     """Route this rank's Chord batch through ovs_shard_route_batch (the round loop in C++);
-    returns (done records [k, 24] uint8 on the device, RouteStats)."""
+    returns (done records [k, 24] uint8 on the device, RouteStats).  done_cap: at most the stepper's
+    (tests shrink it to provoke a one-rank failure)."""
     torch = stepper.torch
     n = int(keys_t.shape[0])
     bounds = (C.c_uint64 * (stepper.world + 1))(*stepper.bounds)
     nd = C.c_uint64(0)
     stats = RouteStats()
     s = stream if stream is not None else torch.cuda.current_stream(stepper.dev).cuda_stream
+    cap = stepper.done_cap if done_cap is None else min(int(done_cap), stepper.done_cap)
     st = lib().ovs_shard_route_batch(stepper.eng._h, C.byref(ex), bounds, num_siblings, C.c_void_p(keys_t.data_ptr()),
                                      C.c_void_p(src_t.data_ptr()), n, qid_base, C.c_void_p(stepper.done.data_ptr()),
-                                     stepper.done_cap, C.byref(nd), cohorts, C.byref(stats), C.c_void_p(s))
+                                     cap, C.byref(nd), cohorts, C.byref(stats), C.c_void_p(s))
     if st != 0 and isinstance(getattr(ex, "_owner", None), CallbackExchange) and ex._owner.error:
         raise RuntimeError(f"exchange callback failed: {ex._owner.error!r}")
     stepper.eng._chk(st, "ovs_shard_route_batch")
@@ -464,15 +477,16 @@ def native_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, cohorts: i
 
 
 def native_kad_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, num_siblings: int = -2,
-                     stream=None) -> tuple:
+                     stream=None, done_cap: int | None = None) -> tuple:
     """Route this rank's Kademlia batch through ovs_kad_shard_route_batch; returns (done [n, 24], RouteStats)."""
     torch = stepper.torch
     n = int(keys_t.shape[0])
     bounds = (C.c_uint64 * (stepper.world + 1))(*stepper.bounds)
     stepper.n = n
-    # migrating lookups (replicated top buckets, one-way routes) finish on any rank: room for all of
-    # them (every rank's batch is the same size here, as in bench.py and the tests)
-    rows = n * stepper.world if (num_siblings < -1 and getattr(stepper, "top_levels", 0)) else n
+    # migrating lookups (replicated top buckets, one-way routes) finish on any rank: room for every
+    # lookup of the batch, summed over the ranks (batches may differ in size)
+    migrate = num_siblings < -1 and getattr(stepper, "top_levels", 0)
+    rows = exchange_sum(ex, [n])[0] if migrate else n
     if getattr(stepper, "done", None) is None or stepper.done.shape[0] < max(rows, 1):
         stepper.done = torch.empty((max(rows, 1), DONE_BYTES), dtype=torch.uint8, device=stepper.dev)
     sib = None
@@ -486,7 +500,9 @@ def native_kad_route(stepper, ex: Exchange, keys_t, src_t, qid_base: int, num_si
     s = stream if stream is not None else torch.cuda.current_stream(stepper.dev).cuda_stream
     st = lib().ovs_kad_shard_route_batch(stepper.eng._h, C.byref(ex), bounds, num_siblings,
                                          C.c_void_p(keys_t.data_ptr()), C.c_void_p(src_t.data_ptr()), n, qid_base,
-                                         C.c_void_p(stepper.done.data_ptr()), stepper.done.shape[0], C.byref(nd), sib,
+                                         C.c_void_p(stepper.done.data_ptr()),
+                                         stepper.done.shape[0] if done_cap is None else min(int(done_cap), stepper.done.shape[0]),
+                                         C.byref(nd), sib,
                                          C.byref(stats), C.c_void_p(s))
     if st != 0 and isinstance(getattr(ex, "_owner", None), CallbackExchange) and ex._owner.error:
         raise RuntimeError(f"exchange callback failed: {ex._owner.error!r}")

@@ -815,6 +815,72 @@ def test_native_round_loop_threads(kind, world, top):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,top", [("chord", None), ("kademlia", 0), ("kademlia", 3)])
+def test_native_round_loop_one_rank_failure_fails_every_rank(kind, top):
+    """a failure only one rank sees (here rank 1's done buffer is too small) is carried by
+    the next collective, so every rank returns an error from the same call -- none blocks in a
+    collective the failed rank never joins.  The threads join within the timeout, all with errors."""
+    import threading
+    from oversim_amd import Params
+    from oversim_amd.shard import (GpuShardStepper, KadShardStepper, arc_bounds, local_exchanges, native_kad_route,
+                                   native_route, destroy_exchange)
+    world, n, m = 3, 1 << 14, 3000
+    net = W.population(n, 0x6A)
+    bounds = arc_bounds(n, world)
+    dev = torch.device("cuda", 0)
+    ks, ss, _, _ = _native_inputs(net, bounds, world, m, 0x6B)
+    if kind == "chord":
+        steppers = [GpuShardStepper(net.ids, net.xy, bounds, r, dev, capacity=m, top_levels=top) for r in range(world)]
+        for st in steppers:
+            st.reset(world * m)
+    else:
+        params = Params.kademlia().replace(lookupParallelRpcs=3)
+        steppers = [KadShardStepper(net.ids, net.xy, bounds, r, dev, params=params, top_levels=top)
+                    for r in range(world)]
+    exs = local_exchanges(world)
+    errs = [None] * world
+
+    def run(r):
+        cap = 10 if r == 1 else None
+        try:
+            with torch.cuda.device(dev):
+                if kind == "chord":
+                    native_route(steppers[r], exs[r], ks[r], ss[r], r * m, cohorts=2, done_cap=cap)
+                else:
+                    native_kad_route(steppers[r], exs[r], ks[r], ss[r], r * m, done_cap=cap)
+        except Exception as e:       # noqa: BLE001
+            errs[r] = e
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a rank is still blocked in a collective"
+    assert all(e is not None for e in errs), errs
+    assert "done" in str(errs[1]) or "done_cap" in str(errs[1]), errs[1]
+    for ex in exs:
+        destroy_exchange(ex)
+    # the contexts stay usable: the same batch with room for it routes
+    if kind == "chord":
+        res = [None] * world
+
+        def ok(r):
+            with torch.cuda.device(dev):
+                res[r] = native_route(steppers[r], exs2[r], ks[r], ss[r], r * m, cohorts=2)
+
+        exs2 = local_exchanges(world)
+        th = [threading.Thread(target=ok, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert sum(int(x[0].shape[0]) for x in res) == world * m
+        for ex in exs2:
+            destroy_exchange(ex)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["chord", "kademlia"])
 def test_native_round_loop_rccl_world1(kind):
     """The library's own RCCL exchange (ovs_rccl_unique_id + ovs_exchange_rccl_create, one
