@@ -1257,10 +1257,31 @@ int32_t ovs_kad_shard_rec_bytes(const ovs_ctx* c)
     return (int32_t)kad_rec_bytes(c->P.lookupParallelRpcs);
 }
 
+
 ovs_status ovs_kad_shard_mig_step(ovs_ctx* c, const void* in, uint64_t n_in, const ovs_key160* fkeys, const uint32_t* fsrc,
                                   uint32_t fqid, void* out, uint64_t out_cap, unsigned long long* out_count,
                                   ovs_done_rec* done, uint64_t done_cap, unsigned long long* done_count,
                                   const uint64_t* shard_lo, uint32_t nshards, void* stream)
+{
+    // a batch's first round (in == NULL) starts the error count afresh
+    return ovs::kad_mig_step_impl(c, in, n_in, fkeys, fsrc, fqid, out, out_cap, out_count, done, done_cap, done_count,
+                                  shard_lo, nshards, stream, in == nullptr);
+}
+
+extern "C++" {
+ovs_status ovs::kad_shard_reset_errors(ovs_ctx* c, void* stream)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->kbad) HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), (hipStream_t)stream));
+    return OVS_OK;
+}
+
+ovs_status ovs::kad_mig_step_impl(ovs_ctx* c, const void* in, uint64_t n_in, const ovs_key160* fkeys,
+                                  const uint32_t* fsrc, uint32_t fqid, void* out, uint64_t out_cap,
+                                  unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
+                                  unsigned long long* done_count, const uint64_t* shard_lo, uint32_t nshards,
+                                  void* stream, bool reset_errors)
 {
     if (!c || !shard_lo || nshards == 0 || nshards > (uint32_t)MAXSHARDS) return OVS_EINVAL;
     if (n_in && ((!in && !(fkeys && fsrc)) || !out || !out_count || !done || !done_count)) return OVS_EINVAL;
@@ -1288,13 +1309,14 @@ ovs_status ovs_kad_shard_mig_step(ovs_ctx* c, const void* in, uint64_t n_in, con
         HIPCHK(c, hipMalloc(&c->kbad, sizeof(unsigned long long)));
         HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
     }
-    if (!in) HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));   // a batch's first round
+    if (reset_errors) HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
     hipError_t e = kad_mig_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), in, n_in,
                                 reinterpret_cast<const K160*>(fkeys), fsrc, fqid, c->d_bounds, (int)nshards, me, out,
                                 out_cap, out_count, done, done_cap, done_count, c->kbad, c->num_cu, c->stage[s], s);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia migration step");
     return OVS_OK;
 }
+}  // extern "C++"
 
 ovs_status ovs_kad_shard_errors(ovs_ctx* c, uint64_t* bad)
 {

@@ -25,6 +25,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -437,12 +438,21 @@ ovs_status ovs_kad_shard_route_batch(ovs_ctx* c, const ovs_exchange* ex, const u
         const uint32_t W = ex->world;
         auto step = [&](int, bool first, const void* in, uint64_t nin, uint64_t b0, void* out, uint64_t cap,
                         unsigned long long* cnt, unsigned long long* dcnt, hipStream_t s) -> ovs_status {
-            return ovs_kad_shard_mig_step(c, first ? nullptr : in, nin, first ? keys + b0 : nullptr,
-                                          first ? src + b0 : nullptr, qid_base + (uint32_t)b0, out, cap, cnt, done,
-                                          done_cap, dcnt, shard_lo, W, s);
+            return kad_mig_step_impl(c, first ? nullptr : in, nin, first ? keys + b0 : nullptr,
+                                     first ? src + b0 : nullptr, qid_base + (uint32_t)b0, out, cap, cnt, done, done_cap,
+                                     dcnt, shard_lo, W, s, false);
         };
-        // one cohort: the migration step's records are large and a round's exchange is short
-        st = route_records(c, ex, n, (uint32_t)rb, step, done, done_cap, n_done, 1, stats, stream,
+        // the error count starts once per batch, before any cohort's first step (the cohort streams
+        // wait for the caller's stream)
+        if ((st = kad_shard_reset_errors(c, stream)) != OVS_OK) return st;
+        // two cohorts (OVS_KAD_MIG_COHORTS): one cohort's records are exchanged while the other's
+        // step runs, as for Chord
+        static const uint32_t mig_cohorts = [] {
+            const char* e = std::getenv("OVS_KAD_MIG_COHORTS");
+            const int v = e ? std::atoi(e) : 2;
+            return (uint32_t)std::max(1, std::min(v, 4));
+        }();
+        st = route_records(c, ex, n, (uint32_t)rb, step, done, done_cap, n_done, mig_cohorts, stats, stream,
                            "sharded Kademlia (migration)");
         if (st != OVS_OK) return st;
         uint64_t bad = 0;

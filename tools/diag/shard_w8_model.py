@@ -23,6 +23,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", choices=["C", "D", "E"], required=True)
 ap.add_argument("--lookups-per-rank", type=int, default=0)
 ap.add_argument("--world", type=int, default=8)
+ap.add_argument("--nodes", type=int, default=None,
+                help="ring size override (D: 2^26 does not fit eight emulated arcs in one GPU's 288 GB; 2^25 does)")
 ap.add_argument("--top-levels", type=int, default=None,
                 help="replicated top finger levels (Chord; default shard.default_top_levels) / buckets (Kademlia --mig; default 3)")
 ap.add_argument("--mig", action="store_true", help="Kademlia: migrating lookups over replicated top buckets, prefix arcs")
@@ -32,7 +34,7 @@ torch.cuda.set_device(dev)
 Wn = a.world
 wl = W.WORKLOADS[a.workload]
 m = a.lookups_per_rank or wl["lookups"]
-inputs = [W.bench_inputs(a.workload, dev, world=Wn, rank=r, n_lookups=m, sharded=True) for r in range(Wn)]
+inputs = [W.bench_inputs(a.workload, dev, world=Wn, rank=r, n_lookups=m, sharded=True, nodes=a.nodes) for r in range(Wn)]
 I0 = inputs[0]
 n = I0["n_total"]
 ids = I0["ids"] if I0["ids"] is not None else I0["ids_t"].cpu().numpy().view(np.uint32)

@@ -8,6 +8,10 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$1; shift; mkdir -p $O
 WLS="${*:-C D E}"
 export OVS_SKIP_BUILD=1 OVS_BENCH_BACKEND=gloo
+# a heartbeat file while the runs go (each run has its own time limit and bench.py its stage watchdog)
+( while sleep 30; do date +%T >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 for n in 2 4; do
   for w in $WLS; do
     extra=""
