@@ -34,7 +34,7 @@ CFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
     "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value", "-Wno-bitwise-instead-of-logical",
 ]
-SOURCES = ["chord.hip", "compact.hip", "epichord.hip", "kad.hip", "kad_general.hip", "kad_refresh.hip", "kad_route.hip", "kad_shard.hip", "koorde.hip", "stats.hip", "ovs_kbr.cpp", "shard_route.cpp",
+SOURCES = ["chord.hip", "compact.hip", "epichord.hip", "ksort.hip", "kad.hip", "kad_general.hip", "kad_refresh.hip", "kad_route.hip", "kad_shard.hip", "koorde.hip", "stats.hip", "ovs_kbr.cpp", "shard_route.cpp",
            "ovs_ini.cpp", "host_tables.cpp"]
 # translation units compiled more than once: (source, object stem, extra flags).  K2 is built per
 # (alpha, exact) pair so its instantiations compile in parallel; A = 8 serves alpha 5..8 (A is the

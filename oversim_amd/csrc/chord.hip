@@ -483,6 +483,9 @@ struct LaneIO {
     const uint32_t* __restrict__ qsrc;
     ovs_route_out* __restrict__ out;
     uint32_t* __restrict__ hopseq;
+    // key order (ksort.hip): qkeys / qsrc are the batch sorted by key bits, perm[q] the caller's index
+    // of sorted lookup q, where its result (and hop sequence) goes; nullptr = caller order
+    const uint32_t* __restrict__ perm;
     // one hop round of an arc (ovs_shard_step)
     const ovs_lookup_rec* __restrict__ in;
     const K160* __restrict__ fkeys;        // a batch's first round straight from its keys and sources
@@ -538,6 +541,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
     bool active = false;
     uint32_t ph = PH_FETCH;
     uint64_t q = 0;
+    uint32_t dst = 0;                 // the caller index of lookup q (io.perm)
     uint32_t qid = 0;
     K160 K;
     uint32_t S = 0, cur = 0;
@@ -619,6 +623,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             const uint32_t s0 = __shfl(pS, rank);
             if (!active && mine < end) {
                 q = mine;
+                if (!SHARD) dst = io.perm ? io.perm[q] : (uint32_t)q;
                 active = true;
                 fresh = true;
                 K = pkeys[q];
@@ -684,6 +689,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
                 } else {
                     K = io.qkeys[q];
                     S = io.qsrc[q];
+                    dst = io.perm ? io.perm[q] : (uint32_t)q;
                     lp = nullptr;
                 }
             }
@@ -846,7 +852,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             auto send = [&](uint32_t nx, bool via_node, bool nx_sib) -> bool {
                 if (REC) {
                     if (nx == S || nx == cur) { fin = true; status = OVS_LOOKUP_NO_NEXT; return false; }  // BaseOverlay.cc:1502-1516
-                    if (RECORD && !SHARD && hops < hcm) io.hopseq[q * (uint64_t)hcm + hops] = nx;
+                    if (RECORD && !SHARD && hops < hcm) io.hopseq[dst * (uint64_t)hcm + hops] = nx;
                     ++hops;
                 } else if (nx == S) {
                     fin = true; status = OVS_LOOKUP_NO_NEXT; return false;                             // visitOnlyOnce
@@ -918,7 +924,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
                         t += rtt;
                         if (t > DC.lookupTimeout) { fin = true; status = OVS_LOOKUP_TIMEOUT; }  // IterativeLookup.cc:808-815
                         else {
-                            if (RECORD && !SHARD && hops < hcm) io.hopseq[q * (uint64_t)hcm + hops] = cur;
+                            if (RECORD && !SHARD && hops < hcm) io.hopseq[dst * (uint64_t)hcm + hops] = cur;
                             ++hops;
                             if (asib) { fin = true; R = cur; }                                   // 896-905
                         }
@@ -994,7 +1000,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
                     io.stage_done[q] = dr;
                     io.stag[q] = (uint8_t)io.nsh;
                 } else {
-                    io.out[q] = o;
+                    io.out[dst] = o;
                 }
                 active = false;
                 lp = nullptr;
@@ -1237,11 +1243,11 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
 template <bool IDEAL, bool RECORD, bool REC>
 static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
                                      const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                                     uint32_t* hopseq, int num_cu, hipStream_t s)
+                                     uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm = nullptr)
 {
     if constexpr (IDEAL) {
         LaneIO io{};
-        io.qkeys = qkeys; io.qsrc = qsrc; io.out = out; io.hopseq = hopseq; io.n = nq;
+        io.qkeys = qkeys; io.qsrc = qsrc; io.out = out; io.hopseq = hopseq; io.n = nq; io.perm = perm;
         if constexpr (!REC && !RECORD) {
             if (DC.lookupCall) return lanes_launch<false, false, false, true>(V, DC, LC, io, num_cu, s);
         }
@@ -1264,9 +1270,16 @@ static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, 
 
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                              uint32_t* hopseq, int num_cu, hipStream_t s)
+                              uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm)
 {
     if (nq == 0) return hipSuccess;
+    if (perm) {
+        // key order: one-way iterative routes on a converged ring only (the LookupCall finish and the
+        // recursive and explicit-table kernels index their outputs by batch position)
+        if (!ideal || LC.recursive || DC.lookupCall) return hipErrorNotSupported;
+        return hopseq ? chord_route_launch<true, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, perm)
+                      : chord_route_launch<true, false, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, perm);
+    }
     if (LC.recursive) {
         if (!ideal) return hipErrorNotSupported;
         return hopseq ? chord_route_launch<true, true, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s)

@@ -23,9 +23,16 @@ hipError_t launch_chord_top(const KeyRec* recs, uint32_t n, int L, FingerEnt* ft
 hipError_t launch_chord_entries(const NodeRec* nodes, FingerEnt* ents, uint64_t total, hipStream_t s);
 hipError_t launch_chord_export(const KeyRec* recs, const FingerEnt* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s);
+// perm != nullptr: qkeys / qsrc are the batch in key order (ksort_launch), perm[q] the caller index of
+// sorted lookup q, where its result goes (one-way iterative routes on a converged ring)
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                              uint32_t* hopseq, int num_cu, hipStream_t s);
+                              uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm = nullptr);
+// ksort.hip: the batch's keys and sources in the order of their top key bits (a counting sort), with
+// the caller index of each; scratch = ksort_scratch_words() u32
+uint64_t ksort_scratch_words();
+hipError_t ksort_launch(const K160* keys, const uint32_t* src, uint64_t n, uint32_t* scratch, K160* skeys,
+                        uint32_t* ssrc, uint32_t* perm, int bits, hipStream_t s);
 hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,
                                   uint64_t n, int numRedundant, int numSiblings, uint32_t* out_nodes,
                                   uint32_t max_out, uint8_t* out_count, uint8_t* out_sib, hipStream_t s);

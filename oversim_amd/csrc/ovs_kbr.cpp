@@ -72,6 +72,12 @@ struct ovs_ctx {
     uint64_t kvis_cap = 0;
     hipEvent_t kvis_ev = nullptr;        // recorded after the last launch that used kvis (kvis_acquire)
     bool kvis_used = false;
+    // K1's key-order buffers (ksort.hip): sorted keys, sources, caller indices and the sort's
+    // histograms, one allocation shared by the calls on this context like kvis (ks_ev orders them)
+    uint8_t* ks = nullptr;
+    uint64_t ks_cap = 0;
+    hipEvent_t ks_ev = nullptr;
+    bool ks_used = false;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
     uint8_t* kact = nullptr;             // 0 never runs, 1 suspended in kst, 2 not started
@@ -163,6 +169,8 @@ void free_tables(ovs_ctx* c)
     epichord_free(c->epi);
     if (c->kvis) hipFree(c->kvis);      // hipFree waits for the launches that use it
     c->kvis = nullptr; c->kvis_cap = 0; c->kvis_used = false;
+    if (c->ks) hipFree(c->ks);
+    c->ks = nullptr; c->ks_cap = 0; c->ks_used = false;
     c->overlay = 0; c->n = 0; c->nfing = 0;
     c->bbox_ok = false;
     c->ch.clear();
@@ -215,6 +223,59 @@ ovs_status kvis_acquire(ovs_ctx* c, uint64_t need, hipStream_t s, uint32_t** out
 void kvis_release(ovs_ctx* c, hipStream_t s)
 {
     if (c->kvis_ev && hipEventRecord(c->kvis_ev, s) == hipSuccess) c->kvis_used = true;
+}
+
+// K1 key order, opt-in (OVS_K1_SORT=1): one-way iterative Chord batches of at least
+// OVS_K1_SORT_MIN lookups (default 2^20) routed in the order of their keys' top bits.  Off by default:
+// measured, the sort costs more than the locality it buys at any bin width one pass can sort
+bool ksort_wanted(uint64_t n)
+{
+    const char* o = std::getenv("OVS_K1_SORT");      // read per call (one getenv per batch)
+    const int on = o ? std::atoi(o) : 0;
+    const char* m = std::getenv("OVS_K1_SORT_MIN");
+    const uint64_t lim = m ? (uint64_t)std::strtoull(m, nullptr, 10) : (1ull << 20);
+    return on != 0 && n >= lim && n < 0xFFFFFFFFull;
+}
+
+// the key-order buffers for n lookups: sorted keys, sources, caller indices, the sort's scratch
+ovs_status ks_acquire(ovs_ctx* c, uint64_t n, hipStream_t s, K160** skeys, uint32_t** ssrc, uint32_t** perm,
+                      uint32_t** scr)
+{
+    const uint64_t need = n * (sizeof(K160) + 8) + 4 * ksort_scratch_words() + 256;
+    if (!c->ks_ev) {
+        const hipError_t e = hipEventCreateWithFlags(&c->ks_ev, hipEventDisableTiming);
+        if (e != hipSuccess) { c->ks_ev = nullptr; return fail(c, OVS_EDEVICE, std::string("ks event: ") + hipGetErrorString(e)); }
+    }
+    if (c->ks_cap < need) {
+        if (c->ks) {
+            if (c->ks_used) {
+                const hipError_t e = hipEventSynchronize(c->ks_ev);
+                if (e != hipSuccess) return fail(c, OVS_EDEVICE, std::string("ks wait: ") + hipGetErrorString(e));
+            }
+            hipFree(c->ks);
+            c->ks = nullptr; c->ks_cap = 0; c->ks_used = false;
+        }
+        const hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->ks), need);
+        if (e != hipSuccess) { c->ks = nullptr; return fail(c, OVS_ENOMEM, "key-order buffers"); }
+        c->ks_cap = need;
+    } else if (c->ks_used) {
+        const hipError_t e = hipStreamWaitEvent(s, c->ks_ev, 0);
+        if (e != hipSuccess) return fail(c, OVS_EDEVICE, std::string("ks stream wait: ") + hipGetErrorString(e));
+    }
+    uint8_t* p = c->ks;
+    *scr = reinterpret_cast<uint32_t*>(p);
+    p += 4 * ksort_scratch_words();
+    *perm = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    *ssrc = reinterpret_cast<uint32_t*>(p);
+    p += 4 * n;
+    *skeys = reinterpret_cast<K160*>(p);
+    return OVS_OK;
+}
+
+void ks_release(ovs_ctx* c, hipStream_t s)
+{
+    if (c->ks_ev && hipEventRecord(c->ks_ev, s) == hipSuccess) c->ks_used = true;
 }
 
 void free_scratch(ovs_ctx* c)
@@ -511,6 +572,7 @@ void ovs_ctx_destroy(ovs_ctx* c)
     kad_exhaustive_release(c->device);
     if (c->d_bounds) hipFree(c->d_bounds);
     if (c->kvis_ev) hipEventDestroy(c->kvis_ev);
+    if (c->ks_ev) hipEventDestroy(c->ks_ev);
     if (c->route_scratch && c->route_scratch_release) c->route_scratch_release(c->route_scratch);
     for (auto& kv : c->stage) stage_free(kv.second);
     for (hipStream_t cs : c->cohort)
@@ -1605,7 +1667,21 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         if (drpc) {
             // Chord with alpha = 1: one FindNodeCall per hop; filled after the route below
         }
-        e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, dk, ds, n, dout, dhop, c->num_cu, s);
+        if (c->ideal && !LC.recursive && ksort_wanted(n)) {
+            // key order: the batch sorted by its keys' top bits, results written at the caller's indices
+            K160* sk = nullptr;
+            uint32_t *ss = nullptr, *pm = nullptr, *scr = nullptr;
+            const ovs_status ks = ks_acquire(c, n, s, &sk, &ss, &pm, &scr);
+            if (ks != OVS_OK) return ks;
+            const char* kb = std::getenv("OVS_K1_SORT_BITS");
+            e = ksort_launch(dk, ds, n, scr, sk, ss, pm, kb ? std::atoi(kb) : 14, s);
+            if (e == hipSuccess)
+                e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, sk, ss, n, dout, dhop, c->num_cu,
+                                       s, pm);
+            ks_release(c, s);
+        } else {
+            e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, dk, ds, n, dout, dhop, c->num_cu, s);
+        }
         if (e == hipSuccess && drpc) {
             if (LC.recursive) e = hipMemsetAsync(drpc, 0, sizeof(uint32_t) * n, s);   // no FindNodeCalls
             else e = launch_fill_rpcs_from_hops(dout, n, drpc, s);

@@ -372,3 +372,30 @@ def test_extended_finger_table_refusals(engine: KbrEngine):
     engine.set_params(Params.chord().replace(extendedFingerTable=1))
     with pytest.raises(KbrError, match="explicit tables"):
         engine.lookup(k, s)
+
+
+def test_key_order_matches_caller_order(engine: KbrEngine, monkeypatch):
+    """K1 key order (ksort.hip): a batch routed in the order of its keys' top bits, every result and
+    hop sequence written at its caller index, equals the batch routed in caller order and the golden
+    vectors.  The key order is opt-in: OVS_K1_SORT=1 and OVS_K1_SORT_MIN (default 2^20 lookups), read
+    per call."""
+    g = np.load(GOLD / "chord_n1000_round.npz")
+    engine.set_params(Params.chord())
+    engine.chord_load(g["ids"], g["xy"])
+    monkeypatch.setenv("OVS_K1_SORT", "1")
+    monkeypatch.setenv("OVS_K1_SORT_MIN", "1")
+    r = engine.lookup(g["keys"], g["src"], record_hops=True)
+    H = g["hop_seq"].shape[1]
+    _eq(r, {f: g[f] for f in FIELDS} | {"hop_seq": g["hop_seq"]}, "key order, golden", hop_cols=H)
+    net = W.population(1 << 20, 0x50F)
+    engine.chord_load(net.ids, net.xy)
+    keys, src = W.lookups(net.ids, 1 << 21, 0x510, node_ids=False)
+    keys[:4096] = net.ids[src[:4096]]          # node-ID keys and equal keys land in the same bins
+    keys[4096:8192] = keys[0]
+    monkeypatch.setenv("OVS_K1_SORT_MIN", "1")
+    a = engine.lookup(keys, src)
+    monkeypatch.setenv("OVS_K1_SORT_MIN", str(1 << 40))
+    b = engine.lookup(keys, src)
+    _eq(a, b, "key order vs caller order")
+    o = OracleNet("chord", net.ids, net.xy).route(keys[:50000], src[:50000], record_hops=False)
+    _eq({f: a[f][:50000] for f in FIELDS}, o, "key order vs oracle")
