@@ -28,6 +28,8 @@ ap.add_argument("--nodes", type=int, default=None,
 ap.add_argument("--top-levels", type=int, default=None,
                 help="replicated top finger levels (Chord; default shard.default_top_levels) / buckets (Kademlia --mig; default 3)")
 ap.add_argument("--mig", action="store_true", help="Kademlia: migrating lookups over replicated top buckets, prefix arcs")
+ap.add_argument("--xgmi-gbs", type=float, default=64.0,
+                help="sustained GB/s per xGMI link and direction for the exchange estimate (7 links per GPU)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -88,6 +90,7 @@ torch.cuda.synchronize()
 print(json.dumps(dict(workload=a.workload, world=Wn, nodes=n, lookups_per_rank=m, setup_s=round(time.time() - t_start, 1))),
       flush=True)
 rounds, tot = 0, dict(step_ms=np.zeros(Wn), serve_ms=np.zeros(Wn), deliver_ms=np.zeros(Wn), sent=np.zeros(Wn))
+per_round = []      # (max step ms over the arcs, max bytes an arc sends) per round: the exchange estimate
 while True:
     rounds += 1
     segs, rows, kms = [], [], []
@@ -154,6 +157,7 @@ while True:
     tot["serve_ms"] += serve_ms
     tot["deliver_ms"] += deliver_ms
     tot["sent"] += bytes_out
+    per_round.append((float((step_ms + serve_ms + deliver_ms).max()), float(bytes_out.max())))
     print(json.dumps(dict(round=rounds, step_ms_max=round(float(step_ms.max()), 3), step_ms_mean=round(float(step_ms.mean()), 3),
                           serve_ms_max=round(float(serve_ms.max()), 3), deliver_ms_max=round(float(deliver_ms.max()), 3),
                           remote_records=[int(x) for x in remote], bytes_out_max=int(bytes_out.max()),
@@ -191,6 +195,14 @@ if (not kad or mig) and os.environ.get("OVS_MODEL_CHECK", "1") == "1":
         bad = int((d["pad"].astype(np.int64) != rp.cpu().numpy().astype(np.int64)).sum())
         assert bad == 0, f"rpcs: {bad} lookups differ from the single-context route"
     print(json.dumps(dict(check="sharded == single-context route", lookups=int(len(d)))), flush=True)
+# a real node's round: the arcs' kernels, then the records over xGMI -- spread over the 7 links of a
+# GPU (all-to-all: each peer gets ~1/7), at --xgmi-gbs per link and direction.  One cohort pays kernel
+# + exchange per round; with two cohorts (the native loop's default) one cohort's exchange runs under
+# the other's kernel, so a round costs about max(kernel, exchange) + min(kernel, exchange) / 2.
+xs = [(k, b / (Wn - 1 if Wn > 1 else 1) / (a.xgmi_gbs * 1e9) * 1e3) for k, b in per_round]
+model = dict(exchange_ms=round(sum(x for _, x in xs), 3), one_cohort_ms=round(sum(k + x for k, x in xs), 3),
+             two_cohorts_ms=round(sum(max(k, x) + min(k, x) / 2 for k, x in xs), 3), xgmi_gbs_per_link=a.xgmi_gbs)
+print(json.dumps(dict(model_per_arc=model)), flush=True)
 print(json.dumps(dict(summary=True, workload=a.workload, world=Wn, rounds=rounds, lookups=int(len(d)),
                       ok=int((d["status"] == 0).sum()), mean_hops=float(d["hops"].mean()),
                       step_ms_per_rank=[round(float(x), 3) for x in tot["step_ms"]],
