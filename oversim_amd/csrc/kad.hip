@@ -29,38 +29,56 @@ void kad_free(KadTables& t)
 // ---------------------------------------------------------------------------
 // builders
 
-// the KadNode summary of a node's sibling set: R = max (s ^ key), level mask = OR 2^msb(s ^ key)
-__device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t v,
-                                 const uint32_t* L, int cnt, int rowlo, KadNode* __restrict__ out, KadX* __restrict__ ox)
+// the KadNode summary of a node's sibling set: R = max (s ^ key), level mask = OR 2^msb(s ^ key).
+// One pass over the siblings' keys: endIndex = msb(R) is the largest level, and the siblings at the
+// four levels endIndex .. endIndex - 3 are counted while it rises (kad_sib_prefix's counts follow).
+// rowlo = -2: the row starts at endIndex.  Returns endIndex.
+__device__ int kad_node_summary(const KeyRec* __restrict__ recs, const double2* __restrict__ xy, uint32_t v,
+                                const uint32_t* L, int cnt, int rowlo, KadNode* __restrict__ out, KadX* __restrict__ ox)
 {
     const K160 me = kload(recs, v);
     K160 R{}, M{};
     for (int i = 0; i < 5; ++i) { R.w[i] = 0; M.w[i] = 0; }
+    int end = -1;
+    uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;     // siblings at levels end, end - 1, end - 2, end - 3
     for (int i = 0; i < cnt; ++i) {
         const K160 d = k_xor(kload(recs, L[i]), me);
         if (k_gt(d, R)) R = d;
         const int mb = k_msb(d);
 #pragma unroll
         for (int w = 0; w < 5; ++w) M.w[w] |= (mb >> 5) == w ? 1u << (mb & 31) : 0u;   // selects: no scratch
+        if (mb > end) {
+            const int s = mb - end;               // the counts move s levels down
+            const uint32_t a0 = n0, a1 = n1, a2 = n2;
+            n3 = s == 1 ? a2 : s == 2 ? a1 : s == 3 ? a0 : 0u;
+            n2 = s == 1 ? a1 : s == 2 ? a0 : 0u;
+            n1 = s == 1 ? a0 : 0u;
+            n0 = 1;
+            end = mb;
+        } else {
+            const int j = end - mb;
+            n0 += j == 0 ? 1u : 0u;
+            n1 += j == 1 ? 1u : 0u;
+            n2 += j == 2 ? 1u : 0u;
+            n3 += j == 3 ? 1u : 0u;
+        }
     }
-    const int end = cnt > 0 ? k_msb(R) : -1;
+    if (rowlo == -2) rowlo = end;
     const int mlo = end > 63 ? end - 63 : 0;
     // mask window: bits [mlo, mlo + 63]
     const int wi = mlo >> 5, sh = mlo & 31;
     const uint64_t lo = (uint64_t)kword(M, wi) | ((uint64_t)kword(M, wi + 1) << 32);   // kword: 5+ reads 0
     const uint64_t hi = (uint64_t)kword(M, wi + 2);
     const uint64_t win = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
-    bool out_bits = false;
-    for (int b = 0; b < mlo; ++b) out_bits |= kbit(M, b) != 0;
-    // siblings at levels <= endIndex - k, k = 1..4 (kad_sib_prefix)
-    uint32_t c1 = 0, c2 = 0, c3 = 0, c4 = 0;
-    for (int i = 0; i < cnt; ++i) {
-        const int l = k_msb(k_xor(kload(recs, L[i]), me));
-        c1 += l <= end - 1 ? 1u : 0u;
-        c2 += l <= end - 2 ? 1u : 0u;
-        c3 += l <= end - 3 ? 1u : 0u;
-        c4 += l <= end - 4 ? 1u : 0u;
+    bool out_bits = false;                        // any mask bit below mlo
+#pragma unroll
+    for (int w = 0; w < 5; ++w) {
+        const int b0 = 32 * w;
+        const uint32_t below = b0 + 32 <= mlo ? ~0u : b0 >= mlo ? 0u : (1u << (mlo - b0)) - 1u;
+        out_bits |= (M.w[w] & below) != 0;
     }
+    // siblings at levels <= endIndex - k, k = 1..4 (kad_sib_prefix)
+    const uint32_t c1 = (uint32_t)cnt - n0, c2 = c1 - n1, c3 = c2 - n2, c4 = c3 - n3;
     const uint32_t lev = c1 | (c2 << 8) | (c3 << 16) | (c4 << 24);
     const double2 p = xy[v];
     KadNode o;
@@ -75,6 +93,7 @@ __device__ void kad_node_summary(const KeyRec* __restrict__ recs, const double2*
     KadX x;
     for (int i = 0; i < 5; ++i) { x.R[i] = R.w[i]; x.mask[i] = M.w[i]; }
     ox[v] = x;
+    return end;
 }
 
 // top 64 key bits (96..159) of every node: the bucket builder's searches and member tops read this
@@ -217,17 +236,7 @@ __global__ __launch_bounds__(KS_BLOCK) void k_kad_siblings(const KeyRec* __restr
     }
     for (int i = cnt; i < S5; ++i) L[i] = NONE;
     // buckets below endIndex hold only siblings: the stored row starts at endIndex
-    int end = -1;
-    {
-        K160 R{};
-        for (int i = 0; i < 5; ++i) R.w[i] = 0;
-        for (int i = 0; i < cnt; ++i) {
-            const K160 d = k_xor(kload(recs, L[i]), me);
-            if (k_gt(d, R)) R = d;
-        }
-        end = cnt > 0 ? k_msb(R) : -1;
-    }
-    kad_node_summary(recs, xy, v, L, cnt, end, out, ox);
+    const int end = kad_node_summary(recs, xy, v, L, cnt, -2, out, ox);
     rowlen[v] = (v >= own_lo && v < own_hi && end >= 0) ? (uint64_t)(KEYBITS - end) * (uint64_t)bpb : 0;
     }
     __syncthreads();
@@ -389,9 +398,8 @@ template <int KC, bool SIB>
 __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, const uint64_t* __restrict__ tops,
                                                const uint32_t* __restrict__ tab, int D, uint32_t n, int k, int S5,
                                                uint64_t seed, const uint32_t* __restrict__ L, KadBlk* __restrict__ blks,
-                                               uint32_t v, const K160& me, uint32_t boff, int m)
+                                               uint32_t v, uint64_t mtop, uint32_t boff, int m)
 {
-    const uint64_t mtop = ktop(me);
     const int bpb = (k + KBLK - 1) / KBLK;
     const int d = KEYBITS - m;
     uint32_t flo, fhi;
@@ -401,7 +409,9 @@ __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, 
         flo = B[Q];
         fhi = B[Q + 1];
     } else {
-        // T_m lies inside v's own depth-D prefix range: search there
+        // T_m lies inside v's own depth-D prefix range: search there (small or irregular networks:
+        // the full key is read only here)
+        const K160 me = kload(recs, v);
         const uint64_t PD = mtop >> (64 - D);
         const uint32_t* B = tab + kb_tab_off(D);
         const bool below = kbit(me, m) != 0;
@@ -523,13 +533,16 @@ __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, 
 // dependent chain is the node line, the prefix table, the members' tops.  The bucket endIndex
 // (sibling exclusion: a scan of the 5s siblings per member) runs in k_kad_bucket_sib, one lane per
 // node -- inside this kernel its two lanes a wave would hold every wave for the scans.
+// (A packed layout -- one lane per bucket actually built, a wave's tasks assigned through a scan of
+// its 64 nodes' bucket counts, no idle lanes -- measured 26.5 vs 25.5 ms at 2^24: the kernel is bound
+// by the top buckets' random member-top reads, not by its lanes)
 template <int KC>
 __global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restrict__ recs,
                                                           const uint64_t* __restrict__ tops,
                                                           const uint32_t* __restrict__ tab, int D,
                                                           const KadNode* __restrict__ nodes, uint32_t n, int k, int S5,
-                                                          uint64_t seed, const uint32_t* __restrict__ sib,
-                                                          KadBlk* __restrict__ blks, uint32_t own_lo, uint32_t own_hi)
+                                                          uint64_t seed, KadBlk* __restrict__ blks, uint32_t own_lo,
+                                                          uint32_t own_hi)
 {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t v = own_lo + (uint32_t)(g / KB_LANES);
@@ -538,10 +551,10 @@ __global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restric
     const KadNode r = nodes[v];
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
-    const K160 me = as_key(r.key);
     for (int m = KEYBITS - 1 - lane; m > endIndex; m -= KB_LANES)
-        kad_bucket_row<KC, false>(recs, tops, tab, D, n, k, S5, seed, nullptr, blks, v, me, r.boff, m);
+        kad_bucket_row<KC, false>(recs, tops, tab, D, n, k, S5, seed, nullptr, blks, v, ktop(as_key(r.key)), r.boff, m);
 }
+static inline dim3 kb_rows_grid(uint32_t nown) { return dim3((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256)); }
 
 template <int KC>
 __global__ __launch_bounds__(KS_BLOCK) void k_kad_bucket_sib(const KeyRec* __restrict__ recs,
@@ -560,8 +573,8 @@ __global__ __launch_bounds__(KS_BLOCK) void k_kad_bucket_sib(const KeyRec* __res
     const KadNode r = nodes[v];
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
-    kad_bucket_row<KC, true>(recs, tops, tab, D, n, k, S5, seed, lsb + threadIdx.x * KS_STRIDE, blks, v, as_key(r.key),
-                             r.boff, endIndex);
+    kad_bucket_row<KC, true>(recs, tops, tab, D, n, k, S5, seed, lsb + threadIdx.x * KS_STRIDE, blks, v,
+                             ktop(as_key(r.key)), r.boff, endIndex);
 }
 
 // the owned nodes' sibling rows (put_sibling_row's layout): the node, then its siblings stable by
@@ -601,7 +614,7 @@ __global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__
         const int i = r + SR_G * j;
         uint32_t xx = NONE;
         if (ok && i < S5) xx = sib[(uint64_t)v * S5 + i];
-        uint32_t k = 0xFFFFu;
+        uint32_t k = 0x7FFFu;                // past every valid key (level * 64 + i <= 10239)
         if (xx != NONE) {
             const uint64_t d = tops[xx] ^ mt;
             const int l = d ? 96 + (63 - __clzll((long long)d)) : k_msb(k_xor(kload(recs, xx), kload(recs, v)));
@@ -617,22 +630,34 @@ __global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__
     uint32_t* row = rowx[g];
     for (int q = r; q < SR_ROW; q += SR_G) row[q] = q == 0 ? v : NONE;
     sr_wave_fence();
-    // rank = keys below mine among the node's 64 (the invalid ones are 0xFFFF)
-    uint32_t rank[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // rank = keys below mine among the node's 64 (the invalid ones are 0x7FFF), two keys per packed
+    // 16-bit subtract: a - key < 0 (all keys < 2^15) sets the half's sign bit, an arithmetic shift turns
+    // it into -1 and a packed subtract counts it -- 1.5 instructions a comparison (a compare, a select
+    // and an add per comparison took 80 % of the kernel's VALU)
+    typedef short sr_s2 __attribute__((ext_vector_type(2)));
+    sr_s2 acc[8];
+    sr_s2 kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        acc[j] = sr_s2{0, 0};
+        kk[j] = sr_s2{(short)key[j], (short)key[j]};
+    }
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
         const uint4 q = keys[g][w];
         const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-            const uint32_t a0 = ws[h] & 0xFFFFu, a1 = ws[h] >> 16;
+            const sr_s2 a = __builtin_bit_cast(sr_s2, ws[h]);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) rank[j] += (a0 < key[j] ? 1u : 0u) + (a1 < key[j] ? 1u : 0u);
+            for (int j = 0; j < 8; ++j) acc[j] -= (a - kk[j]) >> 15;
         }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (key[j] != 0xFFFFu) row[1 + rank[j]] = x[j];
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t rank = (uint32_t)(uint16_t)acc[j].x + (uint32_t)(uint16_t)acc[j].y;
+        if (key[j] != 0x7FFFu) row[1 + rank] = x[j];
+    }
     sr_wave_fence();
     if (!ok) return;
     // block b of the row: tops of its 8 entries (four 16 B pieces), then their indices (two)
@@ -974,18 +999,20 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
     hipMemcpyAsync(t.sib, sib_all + (uint64_t)lo * S5, sizeof(uint32_t) * (uint64_t)nown * S5, hipMemcpyDeviceToDevice, st);
     {
         if (S5 > 64 || sbn * KBLK > SR_ROW) { cleanup(); return hipErrorInvalidValue; }
+        // (the sibling rows and sibling buckets on a second stream beside the bucket rows measured no
+        // faster: all three are bound by gathers and stretched each other)
         hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, SR_NPB)), dim3(256), 0, st, recs, tops, S5, sbn, sib_all,
                            t.blks, t.rows_blks, lo, hi);
-        const dim3 grid((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256)), blk(256);
+        const dim3 grid = kb_rows_grid(nown), blk(256);
         const dim3 grid1(nblk(nown, KS_BLOCK)), blk1(KS_BLOCK);
         if (k <= KBLK) {
             hipLaunchKernelGGL(k_kad_bucket_rows<KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, n, k, S5, seed,
-                               sib_all, t.blks, lo, hi);
+                               t.blks, lo, hi);
             hipLaunchKernelGGL(k_kad_bucket_sib<KBLK>, grid1, blk1, 0, st, recs, tops, tab, D, t.nodes, n, k, S5, seed,
                                sib_all, t.blks, lo, hi);
         } else {
             hipLaunchKernelGGL(k_kad_bucket_rows<2 * KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, n, k, S5,
-                               seed, sib_all, t.blks, lo, hi);
+                               seed, t.blks, lo, hi);
             hipLaunchKernelGGL(k_kad_bucket_sib<2 * KBLK>, grid1, blk1, 0, st, recs, tops, tab, D, t.nodes, n, k, S5,
                                seed, sib_all, t.blks, lo, hi);
         }

@@ -119,9 +119,18 @@ __host__ __device__ __forceinline__ uint32_t mod_step48(uint64_t x, uint32_t d, 
 __host__ __device__ __forceinline__ uint32_t mod_u64_u32(uint64_t h, uint32_t d)
 {
     const double rd = 1.0 / (double)d;
+#ifndef OVS_MOD3
+    // two steps: h >> 21 (< 2^43), then (r << 21) | low 21 bits (< d * 2^21 <= 2^53).  Both dividends
+    // convert to double exactly and their quotients stay below 2^52, where x * rd (two roundings,
+    // relative error <= 2^-52) is off the true quotient by less than one: the step's +-1 correction
+    // suffices (checked against % by tests/test_mod.py's host build)
+    const uint32_t r = mod_step48(h >> 21, d, rd);
+    return mod_step48(((uint64_t)r << 21) | (h & 0x1FFFFFull), d, rd);
+#else
     uint32_t r = mod_step48(h >> 32, d, rd);
     r = mod_step48(((uint64_t)r << 16) | ((h >> 16) & 0xFFFFull), d, rd);
     return mod_step48(((uint64_t)r << 16) | (h & 0xFFFFull), d, rd);
+#endif
 }
 
 // identical to the oracle's kad_hash (bucket sampling of the snapshot rule)
