@@ -387,22 +387,14 @@ __device__ uint32_t kad_prefix_bound(const KeyRec* __restrict__ recs, const uint
 }
 
 constexpr int KB_LANES = 24;   // k_kad_bucket_rows: lanes per node, lane j builds buckets m = 159 - j - 24 i (rows ~ log2 n - 4 long)
-// bucket m of node v under the snapshot rule: up to k members of T_m (the nodes at
-// msb(x ^ v) = m, one contiguous index range [flo, fhi) of the sorted keys) minus v's siblings,
-// chosen by Floyd sampling with kad_hash(seed, v, m, j), in ascending index order, written as bpb
-// KadBlks.  T_m comes from two prefix-table reads (depth 160 - m <= D; deeper levels search the few
-// nodes of v's own depth-D prefix).  SIB: the bucket m = endIndex, the only one that can hold
-// siblings (they lie at levels <= endIndex): the c-th non-sibling member is the least fixed point
-// of x = flo + c + #{siblings in [flo, x]}.  Same blocks as kad_bucket_fill.
-template <int KC, bool SIB>
-__device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, const uint64_t* __restrict__ tops,
-                                               const uint32_t* __restrict__ tab, int D, uint32_t n, int k, int S5,
-                                               uint64_t seed, const uint32_t* __restrict__ L, KadBlk* __restrict__ blks,
-                                               uint32_t v, uint64_t mtop, uint32_t boff, int m)
+// T_m of node v = [flo, fhi): the nodes at msb(x ^ v) = m, one contiguous index range of the sorted
+// keys, from two prefix-table reads (depth 160 - m <= D; deeper levels search the few nodes of v's own
+// depth-D prefix)
+__device__ __forceinline__ void kb_tm_range(const KeyRec* __restrict__ recs, const uint64_t* __restrict__ tops,
+                                            const uint32_t* __restrict__ tab, int D, uint32_t v, uint64_t mtop, int m,
+                                            uint32_t& flo, uint32_t& fhi)
 {
-    const int bpb = (k + KBLK - 1) / KBLK;
     const int d = KEYBITS - m;
-    uint32_t flo, fhi;
     if (d <= D) {
         const uint64_t Q = (mtop >> (64 - d)) ^ 1ull;              // v's top d bits, bit m flipped
         const uint32_t* B = tab + kb_tab_off(d);
@@ -422,28 +414,31 @@ __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, 
         flo = kad_prefix_bound(recs, tops, slo, shi, m, Q, false);
         fhi = kad_prefix_bound(recs, tops, flo, shi, m, Q, true);
     }
-    uint32_t nsin = 0;
-    if (SIB)
-        for (int i = 0; i < S5; ++i) nsin += (L[i] != NONE && L[i] >= flo && L[i] < fhi) ? 1u : 0u;
-    const uint32_t c = (fhi - flo) - nsin;
-    // Floyd sampling of min(k, c) ranks out of c, then ascending
-    uint32_t ch[KC];
+}
+
+// Floyd's draw i (i < k) of the snapshot rule: min(k, c) ranks out of the c candidates of bucket m
+// of node v; the draws are resolved in order (a repeat of an earlier draw takes j), kb_floyd_resolve
+__device__ __forceinline__ uint32_t kb_floyd_draw(uint64_t seed, uint32_t v, int m, uint32_t c, int k, int i)
+{
+    if (i >= k || (uint32_t)i >= c) return NONE;
+    if (c <= (uint32_t)k) return (uint32_t)i;
+    const uint32_t j = c - (uint32_t)k + (uint32_t)i;
+    return mod_u64_u32(kad_hash(seed, v, (uint32_t)m, j), j + 1);
+}
+
+// ch[0..KC) <- the resolved draws in ascending order (NONE = unused, the largest)
+template <int KC>
+__device__ __forceinline__ void kb_floyd_resolve(uint32_t (&ch)[KC], uint32_t c, int k)
+{
 #pragma unroll
     for (int i = 0; i < KC; ++i) {
-        uint32_t t = NONE;
-        if (i < k && (uint32_t)i < c) {
-            if (c <= (uint32_t)k) {
-                t = (uint32_t)i;
-            } else {
-                const uint32_t j = c - (uint32_t)k + (uint32_t)i;
-                t = mod_u64_u32(kad_hash(seed, v, (uint32_t)m, j), j + 1);
-                bool dup = false;
+        if (c > (uint32_t)k && i < k) {
+            const uint32_t j = c - (uint32_t)k + (uint32_t)i;
+            bool dup = false;
 #pragma unroll
-                for (int q = 0; q < i; ++q) dup |= ch[q] == t;
-                t = dup ? j : t;
-            }
+            for (int q = 0; q < i; ++q) dup |= ch[q] == ch[i];
+            ch[i] = dup ? j : ch[i];
         }
-        ch[i] = t;
     }
 #pragma unroll
     for (int a = 0; a < KC; ++a)          // odd-even transposition sort (NONE = the largest)
@@ -453,63 +448,45 @@ __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, 
             ch[b] = x < y ? x : y;
             ch[b + 1] = x < y ? y : x;
         }
-    if (SIB && nsin && fhi - flo <= 256) {
-        // T_m spans at most 256 nodes (the usual case: T_endIndex holds a few dozen): the siblings as
-        // a bit mask over it, the c-th non-sibling = the c-th zero bit
-        uint64_t mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
-        for (int i = 0; i < S5; ++i) {
-            const uint32_t x = L[i];
-            if (x != NONE && x >= flo && x < fhi) {
-                const uint32_t o = x - flo;
-                const uint64_t bit = 1ull << (o & 63);
-                mk0 |= (o >> 6) == 0 ? bit : 0ull;
-                mk1 |= (o >> 6) == 1 ? bit : 0ull;
-                mk2 |= (o >> 6) == 2 ? bit : 0ull;
-                mk3 |= (o >> 6) == 3 ? bit : 0ull;
-            }
-        }
-        const uint32_t span = fhi - flo;
-        auto valid = [&](int w) -> uint64_t {    // the bits of word w inside T_m
-            const int b = (int)span - 64 * w;
-            return b >= 64 ? ~0ull : b <= 0 ? 0ull : ((1ull << b) - 1);
-        };
-        const uint64_t z0 = ~mk0 & valid(0), z1 = ~mk1 & valid(1), z2 = ~mk2 & valid(2), z3 = ~mk3 & valid(3);
+}
+
+// the rank-th set bit of the 256-bit mask z0..z3
+__device__ __forceinline__ uint32_t kb_nth_bit256(uint64_t z0, uint64_t z1, uint64_t z2, uint64_t z3, uint32_t rnk)
+{
+    const uint32_t c0 = __popcll(z0), c1 = __popcll(z1), c2 = __popcll(z2);
+    uint64_t z = z0;
+    uint32_t base = 0;
+    if (rnk >= c0) { rnk -= c0; z = z1; base = 64;
+        if (rnk >= c1) { rnk -= c1; z = z2; base = 128;
+            if (rnk >= c2) { rnk -= c2; z = z3; base = 192; } } }
+    uint32_t pos = 0;
 #pragma unroll
-        for (int q = 0; q < KC; ++q) {
-            if (ch[q] == NONE) continue;
-            uint32_t rnk = ch[q];
-            const uint32_t c0 = __popcll(z0), c1 = __popcll(z1), c2 = __popcll(z2);
-            uint64_t z = z0;
-            uint32_t base = 0;
-            if (rnk >= c0) { rnk -= c0; z = z1; base = 64;
-                if (rnk >= c1) { rnk -= c1; z = z2; base = 128;
-                    if (rnk >= c2) { rnk -= c2; z = z3; base = 192; } } }
-            uint32_t pos = 0;                      // the rnk-th set bit of z
-#pragma unroll
-            for (int sh = 32; sh > 0; sh >>= 1) {
-                const uint32_t c = __popcll(z & ((1ull << sh) - 1));
-                if (rnk >= c) { rnk -= c; z >>= sh; pos += sh; }
-            }
-            ch[q] = flo + base + pos;
-        }
-    } else if (SIB && nsin) {
-#pragma unroll
-        for (int q = 0; q < KC; ++q) {
-            if (ch[q] == NONE) continue;
-            const uint32_t base = flo + ch[q];
-            uint32_t x = base;
-            for (;;) {
-                uint32_t cs = 0;
-                for (int i = 0; i < S5; ++i) cs += (L[i] != NONE && L[i] >= flo && L[i] <= x) ? 1u : 0u;
-                if (base + cs == x) break;
-                x = base + cs;
-            }
-            ch[q] = x;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < KC; ++q) ch[q] = ch[q] == NONE ? NONE : flo + ch[q];
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const uint32_t c = __popcll(z & ((1ull << sh) - 1));
+        if (rnk >= c) { rnk -= c; z >>= sh; pos += sh; }
     }
+    return base + pos;
+}
+
+// bucket m > endIndex of node v under the snapshot rule: up to k members of T_m chosen
+// by Floyd sampling with kad_hash(seed, v, m, j), in ascending index order, written as bpb KadBlks.
+// (The bucket m = endIndex, the only one that can hold siblings, is built in k_kad_sib_rows.)  Same
+// blocks as kad_bucket_fill.
+template <int KC>
+__device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, const uint64_t* __restrict__ tops,
+                                               const uint32_t* __restrict__ tab, int D, int k, uint64_t seed,
+                                               KadBlk* __restrict__ blks, uint32_t v, uint64_t mtop, uint32_t boff, int m)
+{
+    const int bpb = (k + KBLK - 1) / KBLK;
+    uint32_t flo, fhi;
+    kb_tm_range(recs, tops, tab, D, v, mtop, m, flo, fhi);
+    const uint32_t c = fhi - flo;
+    uint32_t ch[KC];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) ch[i] = kb_floyd_draw(seed, v, m, c, k, i);
+    kb_floyd_resolve(ch, c, k);
+#pragma unroll
+    for (int q = 0; q < KC; ++q) ch[q] = ch[q] == NONE ? NONE : flo + ch[q];
     uint64_t tp[KC];
 #pragma unroll
     for (int q = 0; q < KC; ++q) tp[q] = ch[q] == NONE ? ~0ull : tops[ch[q]];
@@ -531,8 +508,8 @@ __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, 
 // snapshot pass B: the buckets m = 159 .. endIndex + 1 of every owned node, one lane per (node,
 // bucket): consecutive lanes write consecutive KadBlks of a row (coalesced runs), and a lane's
 // dependent chain is the node line, the prefix table, the members' tops.  The bucket endIndex
-// (sibling exclusion: a scan of the 5s siblings per member) runs in k_kad_bucket_sib, one lane per
-// node -- inside this kernel its two lanes a wave would hold every wave for the scans.
+// (sibling exclusion) is built with the sibling rows (k_kad_sib_rows), eight lanes a node -- inside
+// this kernel its sibling scans would hold every wave.
 // (A packed layout -- one lane per bucket actually built, a wave's tasks assigned through a scan of
 // its 64 nodes' bucket counts, no idle lanes -- measured 26.5 vs 25.5 ms at 2^24: the kernel is bound
 // by the top buckets' random member-top reads, not by its lanes)
@@ -540,9 +517,8 @@ template <int KC>
 __global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restrict__ recs,
                                                           const uint64_t* __restrict__ tops,
                                                           const uint32_t* __restrict__ tab, int D,
-                                                          const KadNode* __restrict__ nodes, uint32_t n, int k, int S5,
-                                                          uint64_t seed, KadBlk* __restrict__ blks, uint32_t own_lo,
-                                                          uint32_t own_hi)
+                                                          const KadNode* __restrict__ nodes, int k, uint64_t seed,
+                                                          KadBlk* __restrict__ blks, uint32_t own_lo, uint32_t own_hi)
 {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t v = own_lo + (uint32_t)(g / KB_LANES);
@@ -552,30 +528,9 @@ __global__ __launch_bounds__(256) void k_kad_bucket_rows(const KeyRec* __restric
     const int endIndex = kad_end(r.meta);
     if (endIndex < 0) return;
     for (int m = KEYBITS - 1 - lane; m > endIndex; m -= KB_LANES)
-        kad_bucket_row<KC, false>(recs, tops, tab, D, n, k, S5, seed, nullptr, blks, v, ktop(as_key(r.key)), r.boff, m);
+        kad_bucket_row<KC>(recs, tops, tab, D, k, seed, blks, v, ktop(as_key(r.key)), r.boff, m);
 }
 static inline dim3 kb_rows_grid(uint32_t nown) { return dim3((unsigned)(((uint64_t)nown * KB_LANES + 255) / 256)); }
-
-template <int KC>
-__global__ __launch_bounds__(KS_BLOCK) void k_kad_bucket_sib(const KeyRec* __restrict__ recs,
-                                                              const uint64_t* __restrict__ tops,
-                                                              const uint32_t* __restrict__ tab, int D,
-                                                              const KadNode* __restrict__ nodes, uint32_t n, int k,
-                                                              int S5, uint64_t seed, const uint32_t* __restrict__ sib,
-                                                              KadBlk* __restrict__ blks, uint32_t own_lo,
-                                                              uint32_t own_hi)
-{
-    __shared__ uint32_t lsb[KS_BLOCK * KS_STRIDE];
-    const uint32_t v0 = own_lo + blockIdx.x * KS_BLOCK;
-    ks_load_rows(lsb, sib, v0, min((uint32_t)KS_BLOCK, own_hi - v0), S5);
-    const uint32_t v = v0 + threadIdx.x;
-    if (v >= own_hi) return;
-    const KadNode r = nodes[v];
-    const int endIndex = kad_end(r.meta);
-    if (endIndex < 0) return;
-    kad_bucket_row<KC, true>(recs, tops, tab, D, n, k, S5, seed, lsb + threadIdx.x * KS_STRIDE, blks, v,
-                             ktop(as_key(r.key)), r.boff, endIndex);
-}
 
 // the owned nodes' sibling rows (put_sibling_row's layout): the node, then its siblings stable by
 // level msb(x ^ v).  Eight lanes a node: lane r takes list entries r, r+8, ... (coalesced reads of
@@ -584,6 +539,13 @@ __global__ __launch_bounds__(KS_BLOCK) void k_kad_bucket_sib(const KeyRec* __res
 // row is assembled in LDS and written as consecutive 16 B pieces, 128 B per node and instruction.
 // (One lane a node, emitting level by level, had each lane's 16 B stores 576 B apart: 15.9 GB
 // written for 9.7 GB of rows at 2^24 nodes, and the lists read at a 160 B lane stride.)
+// Then the node's bucket m = endIndex, the only one that can hold siblings (they lie at levels <=
+// endIndex), with the same eight lanes: T_m from the prefix tables, the siblings inside it counted
+// and masked over the lanes' list entries, Floyd's k draws computed one a lane (the hash and
+// remainder dominate) and resolved in order on every lane, the c-th non-sibling of T_m = the c-th zero
+// bit of the sibling mask (a fixed-point count over the row beyond 256 nodes), and the 96 B block
+// written as six 16 B pieces.  (Round 5 ran this bucket as its own kernel, one lane a node, re-reading
+// the lists: 4.0 ms at 2^24.)
 // a wave's LDS stores before its lanes' loads of them (a node's lanes lie in one wave)
 __device__ __forceinline__ void sr_wave_fence()
 {
@@ -596,10 +558,13 @@ constexpr int SR_G = 8;                 // lanes per node
 constexpr int SR_NPB = 256 / SR_G;      // nodes per block
 constexpr int SR_ROW = 72;              // row entries: 8 * ceil((1 + 5s) / 8) for 5s <= 64
 
+template <int KC>
 __global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__ recs,
-                                                      const uint64_t* __restrict__ tops, int S5, int sbn,
-                                                      const uint32_t* __restrict__ sib, KadBlk* __restrict__ blks,
-                                                      uint64_t sib_base, uint32_t own_lo, uint32_t own_hi)
+                                                      const uint64_t* __restrict__ tops, const uint32_t* __restrict__ tab,
+                                                      int D, const KadNode* __restrict__ nodes, int k, uint64_t seed,
+                                                      int S5, int sbn, const uint32_t* __restrict__ sib,
+                                                      KadBlk* __restrict__ blks, uint64_t sib_base, uint32_t own_lo,
+                                                      uint32_t own_hi)
 {
     __shared__ uint32_t rowx[SR_NPB][SR_ROW];
     __shared__ uint4 keys[SR_NPB][8];        // the node's 64 keys, 16 bits each
@@ -608,21 +573,19 @@ __global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__
     const bool ok = v < own_hi;
     const uint64_t mt = ok ? tops[v] : 0ull;
     uint32_t x[8], key[8];
-    int nval = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int i = r + SR_G * j;
         uint32_t xx = NONE;
         if (ok && i < S5) xx = sib[(uint64_t)v * S5 + i];
-        uint32_t k = 0x7FFFu;                // past every valid key (level * 64 + i <= 10239)
+        uint32_t kq = 0x7FFFu;               // past every valid key (level * 64 + i <= 10239)
         if (xx != NONE) {
             const uint64_t d = tops[xx] ^ mt;
             const int l = d ? 96 + (63 - __clzll((long long)d)) : k_msb(k_xor(kload(recs, xx), kload(recs, v)));
-            k = (uint32_t)l * 64u + (uint32_t)i;
-            ++nval;
+            kq = (uint32_t)l * 64u + (uint32_t)i;
         }
         x[j] = xx;
-        key[j] = k;
+        key[j] = kq;
     }
     uint16_t* kh = reinterpret_cast<uint16_t*>(keys[g]);
 #pragma unroll
@@ -631,9 +594,9 @@ __global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__
     for (int q = r; q < SR_ROW; q += SR_G) row[q] = q == 0 ? v : NONE;
     sr_wave_fence();
     // rank = keys below mine among the node's 64 (the invalid ones are 0x7FFF), two keys per packed
-    // 16-bit subtract: a - key < 0 (all keys < 2^15) sets the half's sign bit, an arithmetic shift turns
-    // it into -1 and a packed subtract counts it -- 1.5 instructions a comparison (a compare, a select
-    // and an add per comparison took 80 % of the kernel's VALU)
+    // 16-bit subtract: a - key < 0 (all keys < 2^15) sets the half's sign bit, a shift turns it into
+    // 1 and a packed add counts it -- 1.5 instructions a comparison (a compare, a select and an add
+    // per comparison took 80 % of the kernel's VALU)
     typedef short sr_s2 __attribute__((ext_vector_type(2)));
     sr_s2 acc[8];
     sr_s2 kk[8];
@@ -659,21 +622,128 @@ __global__ __launch_bounds__(256) void k_kad_sib_rows(const KeyRec* __restrict__
         if (key[j] != 0x7FFFu) row[1 + rank] = x[j];
     }
     sr_wave_fence();
-    if (!ok) return;
-    // block b of the row: tops of its 8 entries (four 16 B pieces), then their indices (two)
-    uint4* out = reinterpret_cast<uint4*>(blks + sib_base + (uint64_t)(v - own_lo) * sbn);
-    for (int p = r; p < sbn * 6; p += SR_G) {
-        const int b = p / 6, w = p - 6 * (p / 6);
-        uint4 val;
-        if (w < 4) {
-            const uint32_t e0 = row[b * KBLK + 2 * w], e1 = row[b * KBLK + 2 * w + 1];
-            const uint64_t t0 = e0 == NONE ? ~0ull : tops[e0], t1 = e1 == NONE ? ~0ull : tops[e1];
-            val = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
-        } else {
-            const int o = b * KBLK + 4 * (w - 4);
-            val = make_uint4(row[o], row[o + 1], row[o + 2], row[o + 3]);
+    if (ok) {
+        // block b of the row: tops of its 8 entries (four 16 B pieces), then their indices (two)
+        uint4* out = reinterpret_cast<uint4*>(blks + sib_base + (uint64_t)(v - own_lo) * sbn);
+        for (int p = r; p < sbn * 6; p += SR_G) {
+            const int b = p / 6, w = p - 6 * (p / 6);
+            uint4 val;
+            if (w < 4) {
+                const uint32_t e0 = row[b * KBLK + 2 * w], e1 = row[b * KBLK + 2 * w + 1];
+                const uint64_t t0 = e0 == NONE ? ~0ull : tops[e0], t1 = e1 == NONE ? ~0ull : tops[e1];
+                val = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+            } else {
+                const int o = b * KBLK + 4 * (w - 4);
+                val = make_uint4(row[o], row[o + 1], row[o + 2], row[o + 3]);
+            }
+            out[p] = val;
         }
-        out[p] = val;
+    }
+
+    // ---- the bucket m = endIndex (every lane of the group takes part in the shuffles) ----
+    int m = -1;
+    uint32_t boff = 0;
+    if (ok) {
+        const uint4* pn = reinterpret_cast<const uint4*>(nodes + v);
+        boff = pn[1].y;
+        m = kad_end(pn[3].z);
+    }
+    const bool act = m >= 0;                 // the same on the group's eight lanes
+    uint32_t flo = 0, fhi = 0;
+    if (act) kb_tm_range(recs, tops, tab, D, v, mt, m, flo, fhi);
+    const uint32_t span = fhi - flo;
+    // the siblings inside T_m: counted, and as a mask over T_m's first 256 nodes
+    uint32_t nsin = 0;
+    uint64_t mk[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t xx = x[j];
+        const bool in = xx != NONE && xx >= flo && xx < fhi;
+        nsin += in ? 1u : 0u;
+        const uint32_t o = xx - flo;
+        const uint64_t bit = (in && o < 256) ? 1ull << (o & 63) : 0ull;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) mk[w] |= (o >> 6) == (uint32_t)w ? bit : 0ull;
+    }
+#pragma unroll
+    for (int s2 = 1; s2 < SR_G; s2 <<= 1) {
+        nsin += __shfl_xor(nsin, s2, SR_G);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) mk[w] |= __shfl_xor(mk[w], s2, SR_G);
+    }
+    const uint32_t c = span - nsin;
+    // Floyd: lane r computes draws r, r + 8, ...; every lane gathers and resolves all of them
+    constexpr int DPL = KC / SR_G;           // draws a lane
+    uint32_t mine[DPL];
+#pragma unroll
+    for (int h = 0; h < DPL; ++h) mine[h] = act ? kb_floyd_draw(seed, v, m, c, k, r + SR_G * h) : NONE;
+    uint32_t ch[KC];
+#pragma unroll
+    for (int i = 0; i < KC; ++i) ch[i] = __shfl(mine[i / SR_G], i % SR_G, SR_G);
+    kb_floyd_resolve(ch, c, k);
+    // this lane's members (ranks r, r + 8, ...) as node indices, and their tops
+    uint32_t mem[DPL];
+    uint64_t mtp[DPL];
+    const auto valid = [&](int w) -> uint64_t {    // the bits of word w inside T_m
+        const int b = (int)span - 64 * w;
+        return b >= 64 ? ~0ull : b <= 0 ? 0ull : ((1ull << b) - 1);
+    };
+#pragma unroll
+    for (int h = 0; h < DPL; ++h) {
+        uint32_t rk = NONE;
+#pragma unroll
+        for (int i = 0; i < KC; ++i)
+            if (i == r + SR_G * h) rk = ch[i];
+        uint32_t xm = NONE;
+        if (rk != NONE) {
+            if (nsin == 0) {
+                xm = flo + rk;
+            } else if (span <= 256) {
+                xm = flo + kb_nth_bit256(~mk[0] & valid(0), ~mk[1] & valid(1), ~mk[2] & valid(2), ~mk[3] & valid(3), rk);
+            } else {
+                // the least fixed point of x = flo + rank + #{siblings in [flo, x]} (row entries 1..S5)
+                const uint32_t base = flo + rk;
+                uint32_t xx = base;
+                for (;;) {
+                    uint32_t cs = 0;
+                    for (int i = 1; i <= S5; ++i) {
+                        const uint32_t y = row[i];
+                        cs += (y != NONE && y >= flo && y <= xx) ? 1u : 0u;
+                    }
+                    if (base + cs == xx) break;
+                    xx = base + cs;
+                }
+                xm = xx;
+            }
+        }
+        mem[h] = xm;
+        mtp[h] = xm == NONE ? ~0ull : tops[xm];
+    }
+    // the block(s): piece p of block b -- tops of entries 2p, 2p + 1 (p < 4), indices 4(p - 4) .. + 3
+    const int bpb = (k + KBLK - 1) / KBLK;
+#pragma unroll
+    for (int b = 0; b < KC / KBLK; ++b) {
+        uint32_t e[8];
+        uint64_t t[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {        // entry b * 8 + q is lane q's member h = b
+            e[q] = __shfl(mem[b], q, SR_G);
+            t[q] = __shfl(mtp[b], q, SR_G);
+        }
+        if (act && b < bpb && r < 6) {
+            uint4* dd = reinterpret_cast<uint4*>(blks + (uint64_t)boff + (uint64_t)(KEYBITS - 1 - m) * (uint64_t)bpb + b);
+            uint4 val;
+            if (r < 4) {
+                uint64_t t0 = t[0], t1 = t[1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q == r) { t0 = t[2 * q]; t1 = t[2 * q + 1]; }
+                val = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+            } else {
+                val = r == 4 ? make_uint4(e[0], e[1], e[2], e[3]) : make_uint4(e[4], e[5], e[6], e[7]);
+            }
+            dd[r] = val;
+        }
     }
 }
 
@@ -1001,20 +1071,17 @@ hipError_t kad_build(const KeyRec* recs, const double2* xy, uint32_t n, int k, i
         if (S5 > 64 || sbn * KBLK > SR_ROW) { cleanup(); return hipErrorInvalidValue; }
         // (the sibling rows and sibling buckets on a second stream beside the bucket rows measured no
         // faster: all three are bound by gathers and stretched each other)
-        hipLaunchKernelGGL(k_kad_sib_rows, dim3(nblk(nown, SR_NPB)), dim3(256), 0, st, recs, tops, S5, sbn, sib_all,
-                           t.blks, t.rows_blks, lo, hi);
-        const dim3 grid = kb_rows_grid(nown), blk(256);
-        const dim3 grid1(nblk(nown, KS_BLOCK)), blk1(KS_BLOCK);
+        const dim3 grid = kb_rows_grid(nown), blk(256), grid1(nblk(nown, SR_NPB));
         if (k <= KBLK) {
-            hipLaunchKernelGGL(k_kad_bucket_rows<KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, n, k, S5, seed,
-                               t.blks, lo, hi);
-            hipLaunchKernelGGL(k_kad_bucket_sib<KBLK>, grid1, blk1, 0, st, recs, tops, tab, D, t.nodes, n, k, S5, seed,
-                               sib_all, t.blks, lo, hi);
+            hipLaunchKernelGGL(k_kad_sib_rows<KBLK>, grid1, blk, 0, st, recs, tops, tab, D, t.nodes, k, seed, S5, sbn,
+                               sib_all, t.blks, t.rows_blks, lo, hi);
+            hipLaunchKernelGGL(k_kad_bucket_rows<KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, k, seed, t.blks,
+                               lo, hi);
         } else {
-            hipLaunchKernelGGL(k_kad_bucket_rows<2 * KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, n, k, S5,
-                               seed, t.blks, lo, hi);
-            hipLaunchKernelGGL(k_kad_bucket_sib<2 * KBLK>, grid1, blk1, 0, st, recs, tops, tab, D, t.nodes, n, k, S5,
-                               seed, sib_all, t.blks, lo, hi);
+            hipLaunchKernelGGL(k_kad_sib_rows<2 * KBLK>, grid1, blk, 0, st, recs, tops, tab, D, t.nodes, k, seed, S5,
+                               sbn, sib_all, t.blks, t.rows_blks, lo, hi);
+            hipLaunchKernelGGL(k_kad_bucket_rows<2 * KBLK>, grid, blk, 0, st, recs, tops, tab, D, t.nodes, k, seed,
+                               t.blks, lo, hi);
         }
     }
     if (tl > 0)
