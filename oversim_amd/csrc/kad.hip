@@ -468,6 +468,18 @@ __device__ __forceinline__ uint32_t kb_nth_bit256(uint64_t z0, uint64_t z1, uint
     return base + pos;
 }
 
+// the row blocks' 16 B stores (OVS_KB_NT: non-temporal, so the 29 GB of rows a 2^24 build writes
+// do not displace the 128 MB top-key array the member gathers read from the MALL -- an A/B build)
+typedef unsigned int kb_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void kb_store(kb_u4* p, kb_u4 v)
+{
+#ifdef OVS_KB_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // bucket m > endIndex of node v under the snapshot rule: up to k members of T_m chosen
 // by Floyd sampling with kad_hash(seed, v, m, j), in ascending index order, written as bpb KadBlks.
 // (The bucket m = endIndex, the only one that can hold siblings, is built in k_kad_sib_rows.)  Same
@@ -494,14 +506,14 @@ __device__ __forceinline__ void kad_bucket_row(const KeyRec* __restrict__ recs, 
 #pragma unroll
     for (int b = 0; b < KC / KBLK; ++b) {
         if (b >= bpb) break;
-        uint4* dd = reinterpret_cast<uint4*>(B + b);
+        kb_u4* dd = reinterpret_cast<kb_u4*>(B + b);
 #pragma unroll
         for (int q = 0; q < KBLK; q += 2) {
             const uint64_t t0 = tp[b * KBLK + q], t1 = tp[b * KBLK + q + 1];
-            dd[q / 2] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32));
+            kb_store(dd + q / 2, kb_u4{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32)});
         }
-        dd[4] = make_uint4(ch[b * KBLK], ch[b * KBLK + 1], ch[b * KBLK + 2], ch[b * KBLK + 3]);
-        dd[5] = make_uint4(ch[b * KBLK + 4], ch[b * KBLK + 5], ch[b * KBLK + 6], ch[b * KBLK + 7]);
+        kb_store(dd + 4, kb_u4{ch[b * KBLK], ch[b * KBLK + 1], ch[b * KBLK + 2], ch[b * KBLK + 3]});
+        kb_store(dd + 5, kb_u4{ch[b * KBLK + 4], ch[b * KBLK + 5], ch[b * KBLK + 6], ch[b * KBLK + 7]});
     }
 }
 
