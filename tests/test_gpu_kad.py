@@ -45,6 +45,66 @@ def test_snapshot_tables_match_oracle(engine: KbrEngine, n, seed):
     assert np.array_equal(nodes, onodes)
 
 
+@pytest.mark.parametrize("n,k,s,seed,kseed", [(3000, 16, 8, 7, 0), (3000, 4, 2, 8, 0), (3000, 8, 1, 9, 5),
+                                               (5000, 12, 12, 10, 11), (700, 16, 12, 11, 3), (64, 8, 8, 12, 0)])
+def test_snapshot_tables_other_sizes_match_oracle(engine: KbrEngine, n, k, s, seed, kseed):
+    """The builder's bucket rows, sibling rows and the sibling bucket (built with the sibling rows,
+    kad.hip k_kad_sib_rows) for bucket sizes k = 4..16 (one and two blocks a bucket), sibling tables
+    5s = 5..60 and other snapshot seeds, against the oracle's tables."""
+    net = W.population(n, seed)
+    _load(engine, net.ids, net.xy, k=k, s=s, lookupRedundantNodes=min(k, 8), kadSeed=kseed)
+    sib, cnt, nodes = engine.kad_tables()
+    o = OracleNet("kademlia", net.ids, net.xy, params=kad_params(k=k, s=s, lookupRedundantNodes=min(k, 8), kadSeed=kseed))
+    osib, ocnt, onodes = o.kad_tables()
+    for v in range(n):
+        assert set(sib[v][sib[v] != 0xFFFFFFFF]) == set(osib[v][osib[v] != 0xFFFFFFFF]), f"siblings of {v}"
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(nodes, onodes)
+
+
+def _clustered_ids(rng, base_top, offsets, n_far):
+    """IDs sharing their top 128 bits (base_top, then low word = offset) plus n_far uniform IDs,
+    sorted ascending by the 160-bit value (w[0] least significant)."""
+    from oversim_amd import workload as Wl
+    near = np.zeros((len(offsets), 5), dtype=np.uint32)
+    near[:, 1:] = base_top
+    near[:, 0] = offsets
+    far = Wl.random_keys(n_far, rng)
+    allk = np.concatenate([near, far])
+    order = np.lexsort(tuple(allk[:, w] for w in range(5)))
+    allk = allk[order]
+    keep = np.ones(len(allk), bool)
+    keep[1:] = np.any(allk[1:] != allk[:-1], axis=1)
+    return np.ascontiguousarray(allk[keep])
+
+
+def test_snapshot_tables_clustered_ids_match_oracle(engine: KbrEngine):
+    """A cluster of IDs sharing their top 128 bits: 10 nodes within 2^10 of a base key and 300 at
+    level 20 from it, among 2 000 uniform IDs.  For the cluster's nodes the sibling bucket's T_m
+    spans more than 256 nodes with siblings inside (the builder's fixed-point member walk), the
+    prefix searches run below the prefix tables' depth, and every top-64 comparison ties (the exact
+    instantiations)."""
+    rng = np.random.default_rng(21)
+    base = rng.integers(0, 1 << 32, 4, dtype=np.uint64).astype(np.uint32)
+    offs = np.concatenate([rng.choice(1 << 10, 10, replace=False), (1 << 20) + rng.choice(1 << 20, 300, replace=False)])
+    ids = _clustered_ids(rng, base, offs.astype(np.uint32), 2000)
+    xy = W.coordinates(len(ids), 22)
+    _load(engine, ids, xy)
+    sib, cnt, nodes = engine.kad_tables()
+    o = OracleNet("kademlia", ids, xy)
+    osib, ocnt, onodes = o.kad_tables()
+    for v in range(len(ids)):
+        assert set(sib[v][sib[v] != 0xFFFFFFFF]) == set(osib[v][osib[v] != 0xFFFFFFFF]), f"siblings of {v}"
+    assert np.array_equal(cnt, ocnt)
+    assert np.array_equal(nodes, onodes)
+    # and routes over them (exact comparisons) equal the oracle's
+    keys = np.concatenate([ids[rng.integers(0, len(ids), 300)], W.random_keys(300, rng)])
+    src = rng.integers(0, len(ids), len(keys)).astype(np.uint32)
+    r = engine.lookup(keys, src, record_hops=True, count_rpcs=True)
+    ref = o.route(keys, src, record_hops=True, count_rpcs=True)
+    _eq(r, ref, "clustered", hop_cols=8, rpcs=True)
+
+
 @pytest.mark.parametrize("name", ["kad_n2000_a1", "kad_n2000_a3"])
 def test_golden_vectors(engine: KbrEngine, name):
     g = np.load(GOLD / f"{name}.npz")
