@@ -337,7 +337,9 @@ ovs_status  ovs_chord_export_tables(ovs_ctx* ctx, uint32_t* pred, uint32_t* succ
  * (KBRTestApp one-way test: createDestKey -> callRoute -> sendToKey ->
  * IterativeLookup -> sendRouteMessage).  hop_seq may be NULL, else
  * n*hopCountMax node indices (accepted responders in order, 0xFFFFFFFF padded).
- * rpcs may be NULL, else n FindNodeCall counts. */
+ * rpcs may be NULL, else n FindNodeCall counts.  src[i] < n: a host-pointer call
+ * returns OVS_EINVAL for a source outside the network; device-pointer calls do not
+ * check (the caller's sources must be node indices). */
 ovs_status  ovs_route_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
                             uint64_t n, ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs,
                             uint32_t flags, void* stream);
@@ -361,7 +363,7 @@ typedef struct ovs_lookup_out {
  * response that carries the key's node, IterativeLookup.cc:171-184, 862-870;
  * Chord's responsible node answers nothing then, Chord.cc:573-580).  siblings = n*max(num_siblings, 1) node indices, the
  * response's sibling vector in order, 0xFFFFFFFF padded.  Iterative routing,
- * single-context (unsharded) networks. */
+ * single-context (unsharded) networks.  Sources as ovs_route_batch (host calls check them). */
 ovs_status  ovs_lookup_batch(ovs_ctx* ctx, const ovs_key160* keys, const uint32_t* src,
                              uint64_t n, int32_t num_siblings, ovs_lookup_out* out,
                              uint32_t* siblings, uint32_t flags, void* stream);

@@ -1571,6 +1571,16 @@ ovs_status ovs_epichord_find_node_batch(ovs_ctx* c, const uint32_t* node, const 
     return OVS_OK;
 }
 
+// host-pointer calls: every lookup's source must be a node of the network (a source past it would
+// be read out of bounds by the lookup kernels); device-pointer calls leave that to the caller (ovs_kbr.h)
+static ovs_status check_sources(ovs_ctx* c, const uint32_t* src, uint64_t n, bool dev)
+{
+    if (dev) return OVS_OK;
+    for (uint64_t i = 0; i < n; ++i)
+        if (src[i] >= c->n) return fail(c, OVS_EINVAL, "source index out of range (lookup " + std::to_string(i) + ")");
+    return OVS_OK;
+}
+
 ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* src, uint64_t n,
                            ovs_route_out* out, uint32_t* hop_seq, uint32_t* rpcs, uint32_t flags, void* stream)
 {
@@ -1610,6 +1620,8 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: use ovs_kad_shard_step");
     }
     if (n == 0) return OVS_OK;
+    st = check_sources(c, src, n, dev);
+    if (st != OVS_OK) return st;
     // stage inputs
     K160* dk = nullptr; uint32_t* ds = nullptr; ovs_route_out* dout = nullptr;
     uint32_t* dhop = nullptr; uint32_t* drpc = nullptr;
@@ -1779,6 +1791,8 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
         return fail(c, OVS_ESTATE, "context holds one arc of a sharded network: LookupCall needs the whole network");
     }
     if (n == 0) return OVS_OK;
+    st = check_sources(c, src, n, dev);
+    if (st != OVS_OK) return st;
     P.numSiblings = ns;
     const int nslots = ns ? ns : 1;      // an exact-key lookup keeps a one-slot sibling vector (IterativeLookup.cc:149)
     DelayConsts DC = delay_consts(P);
