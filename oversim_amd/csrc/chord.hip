@@ -18,7 +18,9 @@
 #include "engine.hpp"
 #include "launch.hpp"
 
+#include <algorithm>
 #include <cstdio>
+#include <vector>
 
 namespace ovs {
 
@@ -506,6 +508,12 @@ struct LaneIO {
     uint8_t* __restrict__ stag;            // arc of the hand-off, or nsh: finished
 };
 
+#ifdef OVS_K1_TAIL
+// tail census (-DOVS_K1_TAIL builds): each wave's start and exit on the 100 MHz real-time clock, so
+// the spread of the persistent waves' finishing times (the kernel's tail) can be read off one launch
+constexpr int K1_TAIL_MAX = 1 << 16;
+__device__ unsigned long long g_k1_tail[2 * K1_TAIL_MAX];
+#endif
 #ifdef OVS_CHORD_STATS
 // lines consumed by kind: [0] FETCH, [1] START, [2] NODE, [3] first probe of a hop, [4] a further probe
 // (the finger at msb(D) overshot K), [5] WIN
@@ -538,6 +546,9 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
     const int ns = DEF ? 8 : V.ns;
     const int hcm = DEF ? 50 : LC.hopCountMax;
 
+#ifdef OVS_K1_TAIL
+    if (lane == 0 && wave < K1_TAIL_MAX) g_k1_tail[2 * wave] = wall_clock64();
+#endif
     bool active = false;
     uint32_t ph = PH_FETCH;
     uint64_t q = 0;
@@ -695,7 +706,12 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             }
             cursor += (uint64_t)__popcll(need);
         }
-        if (!__any(active)) break;
+        if (!__any(active)) {
+#ifdef OVS_K1_TAIL
+            if (lane == 0 && wave < K1_TAIL_MAX) g_k1_tail[2 * wave + 1] = wall_clock64();
+#endif
+            break;
+        }
 #ifdef OVS_CHORD_STATS
         {   // [6] wave iterations, [7] lanes that consume a line in them (diagnostic build)
             const uint64_t w = __ballot(active && !fresh);
@@ -1230,6 +1246,24 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
 #endif
     hipLaunchKernelGGL((k_chord_lanes<REC, RECORD, SHARD, LKC, DEF>), dim3((unsigned)blocks), dim3(256), 0, s, V, DC,
                        LC, io);
+#ifdef OVS_K1_TAIL
+    if (!SHARD) {
+        const uint64_t nw = blocks * 4 < (uint64_t)K1_TAIL_MAX ? blocks * 4 : (uint64_t)K1_TAIL_MAX;
+        std::vector<unsigned long long> tt(2 * nw);
+        hipMemcpyFromSymbolAsync(tt.data(), HIP_SYMBOL(g_k1_tail), sizeof(unsigned long long) * 2 * nw, 0,
+                                 hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        unsigned long long t0 = ~0ull;
+        std::vector<double> fin;
+        for (uint64_t w = 0; w < nw; ++w) t0 = tt[2 * w] < t0 ? tt[2 * w] : t0;
+        for (uint64_t w = 0; w < nw; ++w) fin.push_back((double)(tt[2 * w + 1] - t0) * 0.01);   // 100 MHz -> us
+        std::sort(fin.begin(), fin.end());
+        auto pct = [&](double f) { return fin[(size_t)(f * (fin.size() - 1))]; };
+        fprintf(stderr, "k1tail waves=%llu chunk=%llu finish_us p0=%.1f p10=%.1f p50=%.1f p90=%.1f p99=%.1f max=%.1f\n",
+                (unsigned long long)nw, (unsigned long long)io.chunk, pct(0), pct(0.1), pct(0.5), pct(0.9), pct(0.99),
+                fin.back());
+    }
+#endif
 #ifdef OVS_CHORD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_k1_stats), sizeof z, 0, hipMemcpyDeviceToHost, s);
     hipStreamSynchronize(s);
