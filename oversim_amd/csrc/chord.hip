@@ -506,13 +506,37 @@ struct LaneIO {
     ovs_lookup_rec* __restrict__ stage_hand;
     ovs_done_rec* __restrict__ stage_done;
     uint8_t* __restrict__ stag;            // arc of the hand-off, or nsh: finished
+    // dynamic tail (single-GPU routes, dyn != nullptr): each wave's static slice covers [0, dyn_from);
+    // the rest is handed out K1_DYN_CH lookups at a time from the zeroed counter *dyn
+    unsigned long long* dyn;
+    uint64_t dyn_from;
 };
+
+// Persistent waves finish their static slices up to a quarter of the kernel apart (a census of
+// their exit times, -DOVS_K1_TAIL): the last ~30 % of a batch is handed out dynamically instead, in
+// chunks of one refill, so that the waves that run ahead take more
+#ifndef K1_DYN_CH
+#define K1_DYN_CH 64
+#endif
+#ifndef K1_DYN_STATIC
+#define K1_DYN_STATIC 0.70
+#endif
 
 #ifdef OVS_K1_TAIL
 // tail census (-DOVS_K1_TAIL builds): each wave's start and exit on the 100 MHz real-time clock, so
 // the spread of the persistent waves' finishing times (the kernel's tail) can be read off one launch
 constexpr int K1_TAIL_MAX = 1 << 16;
 __device__ unsigned long long g_k1_tail[2 * K1_TAIL_MAX];
+// lane 0 of the wave records the real-time counter in slot 2 * wave + which; the slot comes from
+// wave-uniform values, so nothing stays live across the kernel's loop (a first version that kept the
+// wave index and the start time live spilled the kernel)
+__device__ __forceinline__ void ovs_tail_mark(unsigned long long* arr, int max, int which)
+{
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wib;
+    const unsigned long long t = wall_clock64();
+    if (__lane_id() == 0 && w < (uint64_t)max) arr[2 * w + which] = t;
+}
 #endif
 #ifdef OVS_CHORD_STATS
 // lines consumed by kind: [0] FETCH, [1] START, [2] NODE, [3] first probe of a hop, [4] a further probe
@@ -541,14 +565,13 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     uint64_t cursor = wave * io.chunk;                    // wave-uniform
-    const uint64_t end = min(cursor + io.chunk, io.n);
+    const bool dyn = !SHARD && io.dyn != nullptr;
+    uint64_t end = min(cursor + io.chunk, dyn ? io.dyn_from : io.n);
+    bool more = dyn;                                      // dynamic chunks may be left
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int ns = DEF ? 8 : V.ns;
     const int hcm = DEF ? 50 : LC.hopCountMax;
 
-#ifdef OVS_K1_TAIL
-    if (lane == 0 && wave < K1_TAIL_MAX) g_k1_tail[2 * wave] = wall_clock64();
-#endif
     bool active = false;
     uint32_t ph = PH_FETCH;
     uint64_t q = 0;
@@ -628,6 +651,20 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
         // ---- refill: lanes without a lookup take the next of the wave's slice
         bool fresh = false;
         const uint64_t need = __ballot(!active);
+        if (!SHARD && more && need != 0 && cursor >= end) {
+            // the static slice is spent: the next dynamic chunk (one atomic a chunk, lane 0)
+            unsigned long long b = 0;
+            if (lane == 0) b = atomicAdd(io.dyn, (unsigned long long)K1_DYN_CH);
+            const uint64_t nb = io.dyn_from + (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                                               (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b));
+            if (nb < io.n) {
+                cursor = nb;
+                end = min(nb + (uint64_t)K1_DYN_CH, io.n);
+                preload(cursor);
+            } else {
+                more = false;
+            }
+        }
         if (need != 0 && cursor < end && pre_ok) {
             const int rank = __popcll(need & lt_mask);
             const uint64_t mine = cursor + (uint64_t)rank;
@@ -706,12 +743,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             }
             cursor += (uint64_t)__popcll(need);
         }
-        if (!__any(active)) {
-#ifdef OVS_K1_TAIL
-            if (lane == 0 && wave < K1_TAIL_MAX) g_k1_tail[2 * wave + 1] = wall_clock64();
-#endif
-            break;
-        }
+        if (!__any(active)) break;
 #ifdef OVS_CHORD_STATS
         {   // [6] wave iterations, [7] lanes that consume a line in them (diagnostic build)
             const uint64_t w = __ballot(active && !fresh);
@@ -1044,6 +1076,9 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
             L0 = v[0]; L1 = v[1]; L2 = v[2]; L3 = v[3];
         }
     }
+#ifdef OVS_K1_TAIL
+    ovs_tail_mark(g_k1_tail, K1_TAIL_MAX, 1);
+#endif
 }
 
 __global__ void k_make_records(const KeyRec* __restrict__ recs, const K160* __restrict__ keys,
@@ -1240,6 +1275,17 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
     static int bpc = 0;
     uint64_t blocks = 0;
     io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD, LKC, DEF>, &bpc, io.n, num_cu, &blocks);
+    if (!SHARD && io.dyn) {
+        // static slices cover K1_DYN_STATIC of the batch, the rest goes out in chunks (tiny batches: static)
+        const uint64_t waves = blocks * 4;
+        const uint64_t cs = (uint64_t)((double)io.n * K1_DYN_STATIC) / waves;
+        if (cs < (uint64_t)K1_DYN_CH) {
+            io.dyn = nullptr;
+        } else {
+            io.chunk = cs;
+            io.dyn_from = cs * waves;
+        }
+    }
 #ifdef OVS_CHORD_STATS
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_k1_stats), z, sizeof z, 0, hipMemcpyHostToDevice, s);
@@ -1255,11 +1301,11 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
         hipStreamSynchronize(s);
         unsigned long long t0 = ~0ull;
         std::vector<double> fin;
-        for (uint64_t w = 0; w < nw; ++w) t0 = tt[2 * w] < t0 ? tt[2 * w] : t0;
+        for (uint64_t w = 0; w < nw; ++w) t0 = tt[2 * w + 1] < t0 ? tt[2 * w + 1] : t0;
         for (uint64_t w = 0; w < nw; ++w) fin.push_back((double)(tt[2 * w + 1] - t0) * 0.01);   // 100 MHz -> us
         std::sort(fin.begin(), fin.end());
         auto pct = [&](double f) { return fin[(size_t)(f * (fin.size() - 1))]; };
-        fprintf(stderr, "k1tail waves=%llu chunk=%llu finish_us p0=%.1f p10=%.1f p50=%.1f p90=%.1f p99=%.1f max=%.1f\n",
+        fprintf(stderr, "k1tail waves=%llu chunk=%llu finish_us_after_first_exit p0=%.1f p10=%.1f p50=%.1f p90=%.1f p99=%.1f max=%.1f\n",
                 (unsigned long long)nw, (unsigned long long)io.chunk, pct(0), pct(0.1), pct(0.5), pct(0.9), pct(0.99),
                 fin.back());
     }
@@ -1277,11 +1323,13 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
 template <bool IDEAL, bool RECORD, bool REC>
 static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, const LookupConsts& LC,
                                      const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                                     uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm = nullptr)
+                                     uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm = nullptr,
+                                     unsigned long long* dyn = nullptr)
 {
     if constexpr (IDEAL) {
         LaneIO io{};
         io.qkeys = qkeys; io.qsrc = qsrc; io.out = out; io.hopseq = hopseq; io.n = nq; io.perm = perm;
+        io.dyn = dyn;
         if constexpr (!REC && !RECORD) {
             if (DC.lookupCall) return lanes_launch<false, false, false, true>(V, DC, LC, io, num_cu, s);
         }
@@ -1304,24 +1352,25 @@ static hipError_t chord_route_launch(const ChordView& V, const DelayConsts& DC, 
 
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                              uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm)
+                              uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm,
+                              unsigned long long* dyn)
 {
     if (nq == 0) return hipSuccess;
     if (perm) {
         // key order: one-way iterative routes on a converged ring only (the LookupCall finish and the
         // recursive and explicit-table kernels index their outputs by batch position)
         if (!ideal || LC.recursive || DC.lookupCall) return hipErrorNotSupported;
-        return hopseq ? chord_route_launch<true, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, perm)
-                      : chord_route_launch<true, false, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, perm);
+        return hopseq ? chord_route_launch<true, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, perm, dyn)
+                      : chord_route_launch<true, false, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, perm, dyn);
     }
     if (LC.recursive) {
         if (!ideal) return hipErrorNotSupported;
-        return hopseq ? chord_route_launch<true, true, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s)
-                      : chord_route_launch<true, false, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s);
+        return hopseq ? chord_route_launch<true, true, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, nullptr, dyn)
+                      : chord_route_launch<true, false, true>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, nullptr, dyn);
     }
-    if (!ideal) return chord_route_launch<false, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s);
-    return hopseq ? chord_route_launch<true, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s)
-                  : chord_route_launch<true, false, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s);
+    if (!ideal) return chord_route_launch<false, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, nullptr, dyn);
+    return hopseq ? chord_route_launch<true, true, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, nullptr, dyn)
+                  : chord_route_launch<true, false, false>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, num_cu, s, nullptr, dyn);
 }
 
 hipError_t launch_chord_find_node(const ChordView& V, bool ideal, const uint32_t* node, const K160* keys,

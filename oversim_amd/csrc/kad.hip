@@ -1254,7 +1254,7 @@ hipError_t kad_export(const KadTables& t, uint32_t n, uint32_t* siblings, uint8_
 
 hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P, const DelayConsts& DC,
                      const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq,
-                     uint32_t* rpcs, int num_cu, hipStream_t st, uint32_t* sibs)
+                     uint32_t* rpcs, int num_cu, hipStream_t st, uint32_t* sibs, unsigned long long* dyn)
 {
     if (nq == 0) return hipSuccess;
     if (!kad_params_supported(P, t)) return hipErrorNotSupported;
@@ -1265,7 +1265,7 @@ hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ov
     const int A = P.lookupParallelRpcs;
     // LookupCall batches (sibs != nullptr) record no hop sequence
     if (sibs && hopseq) return hipErrorNotSupported;
-#define KLX(a, x) kad_route_launch<a, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st)
+#define KLX(a, x) kad_route_launch<a, x>(V, DC, LC, qkeys, qsrc, nq, out, hopseq, rpcs, sibs, num_cu, st, dyn)
 #define KL(a) (t.exact ? KLX(a, true) : KLX(a, false))
     switch (A) {
     case 1: return KL(1);

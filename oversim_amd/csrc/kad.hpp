@@ -170,7 +170,7 @@ hipError_t kad_find_node_general(const KadTables& t, uint32_t n, const uint32_t*
 hipError_t kad_route(const KadTables& t, const double2* xy, uint32_t n, const ovs_params& P,
                      const DelayConsts& DC, const K160* qkeys, const uint32_t* qsrc, uint64_t nq,
                      ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs, int num_cu, hipStream_t st,
-                     uint32_t* sibs = nullptr);
+                     uint32_t* sibs = nullptr, unsigned long long* dyn = nullptr);
 // exhaustive-iterative lookups (K2x, kad_refresh.hip): config.redundantNodes = R, a siblings vector
 // of ns <= R; out = ovs_route_out (oneway: KBRTestApp one-way test) or ovs_lookup_out; responders =
 // the accepted responders in order (= hop_seq); *capacity_error: a lookup ran past the kernel's

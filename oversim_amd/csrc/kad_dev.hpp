@@ -1558,6 +1558,6 @@ hipError_t kad_shard_step_launch(const KadView& V, const DelayConsts& DC, const 
 template <int A, bool EX>
 hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
                             const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
-                            uint32_t* sibs, int num_cu, hipStream_t st);
+                            uint32_t* sibs, int num_cu, hipStream_t st, unsigned long long* dyn = nullptr);
 
 }  // namespace ovs

@@ -22,7 +22,9 @@
 #include "kad_dev.hpp"
 #include "kad_shard.hpp"
 
+#include <algorithm>
 #include <cstdio>
+#include <vector>
 
 #ifndef OVS_KAD_A
 #error "kad_route.hip is compiled with -DOVS_KAD_A=<alpha> -DOVS_KAD_EX=<0|1> (oversim_amd/build.py)"
@@ -40,6 +42,23 @@
 namespace ovs {
 
 namespace {
+
+#ifdef OVS_KAD_TAIL
+// tail census (-DOVS_KAD_TAIL builds): each persistent wave's start and exit on the real-time
+// counter, read back and summarised by kad_launch (the spread of the waves' finishing times)
+constexpr int KAD_TAIL_MAX = 1 << 16;
+__device__ unsigned long long g_kad_tail[2 * KAD_TAIL_MAX];
+// lane 0 of the wave records the real-time counter in slot 2 * wave + which; the slot comes from
+// wave-uniform values, so nothing stays live across the kernel's loop (a first version that kept the
+// wave index and the start time live spilled the kernel)
+__device__ __forceinline__ void ovs_tail_mark(unsigned long long* arr, int max, int which)
+{
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wib;
+    const unsigned long long t = wall_clock64();
+    if (__lane_id() == 0 && w < (uint64_t)max) arr[2 * w + which] = t;
+}
+#endif
 
 struct SendNothing {
     __device__ __forceinline__ void operator()(int, uint32_t, bool) const {}
@@ -172,7 +191,18 @@ struct KadRouteIO {
     uint8_t* __restrict__ mtag;
     int me;
     int tl, bpb, full_ok;
+    // dynamic tail (single-GPU batches, dyn != nullptr): static slices cover [0, dyn_from), the rest
+    // goes out KAD_DYN_CH lookups at a time from the zeroed counter *dyn (as K1's, chord.hip)
+    unsigned long long* dyn;
+    uint64_t dyn_from;
 };
+
+#ifndef KAD_DYN_CH
+#define KAD_DYN_CH 64
+#endif
+#ifndef KAD_DYN_STATIC
+#define KAD_DYN_STATIC 0.70
+#endif
 
 // SH: explicit tables with short sibling tables (KadTables::maybe_short): a send may have to count
 // the responder's scan (kad_response_size); snapshot tables never do
@@ -216,7 +246,9 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
         chunk = (nq + waves - 1) / waves;
     }
     uint64_t cursor = wave * chunk;
-    const uint64_t end = min(cursor + chunk, nq);
+    const bool dyn = SM == 0 && io.dyn != nullptr;
+    uint64_t end = min(cursor + chunk, dyn ? io.dyn_from : nq);
+    bool more = dyn;                                      // dynamic chunks may be left
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int ns = LK ? LC.numSiblings : 1;
     uint32_t* st = static_cast<uint32_t*>(io.st);
@@ -235,6 +267,19 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
 
     while (true) {
         const uint64_t need = __ballot(!active);
+        if (SM == 0 && more && need != 0 && cursor >= end) {
+            // the static slice is spent: the next dynamic chunk (one atomic a chunk, lane 0)
+            unsigned long long b = 0;
+            if (lane == 0) b = atomicAdd(io.dyn, (unsigned long long)KAD_DYN_CH);
+            const uint64_t nb = io.dyn_from + (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                                               (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b));
+            if (nb < nq) {
+                cursor = nb;
+                end = min(nb + (uint64_t)KAD_DYN_CH, nq);
+            } else {
+                more = false;
+            }
+        }
         if (need != 0 && cursor < end) {
             const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
             if (!active && mine < end) {
@@ -483,6 +528,9 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
             }
         }
     }
+#ifdef OVS_KAD_TAIL
+    ovs_tail_mark(g_kad_tail, KAD_TAIL_MAX, 1);
+#endif
 }
 
 }  // namespace
@@ -511,12 +559,40 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     if (io.chunk < 1) io.chunk = 1;
     const uint64_t need_waves = (io.nq + io.chunk - 1) / io.chunk;
     const uint64_t blocks = (need_waves + 3) / 4;
+    if (SM == 0 && io.dyn) {
+        // static slices cover KAD_DYN_STATIC of the batch, the rest goes out in chunks (small batches: static)
+        const uint64_t cs = (uint64_t)((double)io.nq * KAD_DYN_STATIC) / (blocks * 4);
+        if (cs < (uint64_t)KAD_DYN_CH) {
+            io.dyn = nullptr;
+        } else {
+            io.chunk = cs;
+            io.dyn_from = cs * blocks * 4;
+        }
+    }
 #ifdef OVS_KAD_STATS
     unsigned long long z[8] = {};
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_kad_stats), z, sizeof z, 0, hipMemcpyHostToDevice, st);
 #endif
     hipLaunchKernelGGL((k_kad_route<A, RECORD, EX, LK, SM, C, SH, DEF>), dim3((unsigned)blocks), dim3(256), 0, st, V, DC, LC,
                        io);
+#ifdef OVS_KAD_TAIL
+    if (!SM) {
+        const uint64_t nw = blocks * 4 < (uint64_t)KAD_TAIL_MAX ? blocks * 4 : (uint64_t)KAD_TAIL_MAX;
+        std::vector<unsigned long long> tt(2 * nw);
+        hipMemcpyFromSymbolAsync(tt.data(), HIP_SYMBOL(g_kad_tail), sizeof(unsigned long long) * 2 * nw, 0,
+                                 hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        unsigned long long t0 = ~0ull;
+        std::vector<double> fin;
+        for (uint64_t w = 0; w < nw; ++w) t0 = tt[2 * w + 1] < t0 ? tt[2 * w + 1] : t0;
+        for (uint64_t w = 0; w < nw; ++w) fin.push_back((double)(tt[2 * w + 1] - t0) * 0.01);   // 100 MHz -> us
+        std::sort(fin.begin(), fin.end());
+        auto pct = [&](double f) { return fin[(size_t)(f * (fin.size() - 1))]; };
+        fprintf(stderr, "kadtail waves=%llu chunk=%llu finish_us_after_first_exit p0=%.1f p10=%.1f p50=%.1f p90=%.1f p99=%.1f max=%.1f\n",
+                (unsigned long long)nw, (unsigned long long)io.chunk, pct(0), pct(0.1), pct(0.5), pct(0.9), pct(0.99),
+                fin.back());
+    }
+#endif
 #ifdef OVS_KAD_STATS
     hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_kad_stats), sizeof z, 0, hipMemcpyDeviceToHost, st);
     hipStreamSynchronize(st);
@@ -529,10 +605,11 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
 template <int A, bool EX>
 hipError_t kad_route_launch(const KadView& V, const DelayConsts& DC, const KadLC& LC, const K160* qkeys,
                             const uint32_t* qsrc, uint64_t nq, ovs_route_out* out, uint32_t* hopseq, uint32_t* rpcs,
-                            uint32_t* sibs, int num_cu, hipStream_t st)
+                            uint32_t* sibs, int num_cu, hipStream_t st, unsigned long long* dyn)
 {
     KadRouteIO io{};
     io.qkeys = qkeys; io.qsrc = qsrc; io.nq = nq; io.out = out; io.hopseq = hopseq; io.rpcs_out = rpcs; io.sib_out = sibs;
+    io.dyn = dyn;
     // LookupCall batches (sibs != nullptr) record no hop sequence.  KademliaLarge (k or
     // lookupRedundantNodes above 8) takes the 16-entry LookupVector / findNode instantiation.
     if (LC.redundant > 8 || LC.maxRedundantLocal > 8) {
@@ -595,7 +672,8 @@ template hipError_t kad_mig_step_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadVie
                                                                     const KadMigStepArgs&, int, hipStream_t);
 template hipError_t kad_route_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
                                                                  const K160*, const uint32_t*, uint64_t, ovs_route_out*,
-                                                                 uint32_t*, uint32_t*, uint32_t*, int, hipStream_t);
+                                                                 uint32_t*, uint32_t*, uint32_t*, int, hipStream_t,
+                                                                 unsigned long long*);
 template hipError_t kad_shard_step_launch<OVS_KAD_A, OVS_KAD_EX != 0>(const KadView&, const DelayConsts&, const KadLC&,
                                                                       const KadShardStepArgs&, int, hipStream_t);
 

@@ -24,10 +24,13 @@ hipError_t launch_chord_entries(const NodeRec* nodes, FingerEnt* ents, uint64_t 
 hipError_t launch_chord_export(const KeyRec* recs, const FingerEnt* fingers, uint32_t n, uint32_t* out,
                                hipStream_t s);
 // perm != nullptr: qkeys / qsrc are the batch in key order (ksort_launch), perm[q] the caller index of
-// sorted lookup q, where its result goes (one-way iterative routes on a converged ring)
+// sorted lookup q, where its result goes (one-way iterative routes on a converged ring).  dyn: a zeroed
+// device counter for this launch alone -- K1 then hands out the batch's last ~30 % dynamically
+// (ctx_dyn_acquire); nullptr: static slices only
 hipError_t launch_chord_route(const ChordView& V, bool ideal, const DelayConsts& DC, const LookupConsts& LC,
                               const K160* qkeys, const uint32_t* qsrc, uint64_t nq, ovs_route_out* out,
-                              uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm = nullptr);
+                              uint32_t* hopseq, int num_cu, hipStream_t s, const uint32_t* perm = nullptr,
+                              unsigned long long* dyn = nullptr);
 // ksort.hip: the batch's keys and sources in the order of their top key bits (a counting sort), with
 // the caller index of each; scratch = ksort_scratch_words() u32
 uint64_t ksort_scratch_words();

@@ -78,6 +78,14 @@ struct ovs_ctx {
     uint64_t ks_cap = 0;
     hipEvent_t ks_ev = nullptr;
     bool ks_used = false;
+    // the persistent route kernels' dynamic-tail counters (dyn_acquire): one 64 B slot per launch, a
+    // slot's previous launch ordered before its reuse by an event, so concurrent calls on different
+    // streams never share a counter
+    static constexpr int DYN_SLOTS = 32;
+    unsigned long long* dyn = nullptr;
+    hipEvent_t dyn_ev[DYN_SLOTS] = {};
+    bool dyn_used[DYN_SLOTS] = {};
+    uint32_t dyn_seq = 0;
     // multi-GPU Kademlia: this rank's in-flight lookups (ovs_kad_shard_begin)
     void* kst = nullptr;                 // KadLookup<alpha> state records
     uint8_t* kact = nullptr;             // 0 never runs, 1 suspended in kst, 2 not started
@@ -573,6 +581,9 @@ void ovs_ctx_destroy(ovs_ctx* c)
     if (c->d_bounds) hipFree(c->d_bounds);
     if (c->kvis_ev) hipEventDestroy(c->kvis_ev);
     if (c->ks_ev) hipEventDestroy(c->ks_ev);
+    for (int i = 0; i < ovs_ctx::DYN_SLOTS; ++i)
+        if (c->dyn_ev[i]) hipEventDestroy(c->dyn_ev[i]);
+    if (c->dyn) hipFree(c->dyn);
     if (c->route_scratch && c->route_scratch_release) c->route_scratch_release(c->route_scratch);
     for (auto& kv : c->stage) stage_free(kv.second);
     for (hipStream_t cs : c->cohort)
@@ -1571,6 +1582,33 @@ ovs_status ovs_epichord_find_node_batch(ovs_ctx* c, const uint32_t* node, const 
     return OVS_OK;
 }
 
+// A zeroed work counter for one launch of a persistent route kernel (the dynamic tail of K1,
+// launch_chord_route, and K2, kad_route): nullptr when none can be had -- the kernel then runs static slices only.
+static unsigned long long* dyn_acquire(ovs_ctx* c, uint64_t n, hipStream_t s, int* slot)
+{
+    *slot = -1;
+    if (std::getenv("OVS_NO_DYN")) return nullptr;       // A/B: static slices only
+    if (n < (1ull << 18)) return nullptr;                 // small batches: static slices (no memset, no event)
+    if (!c->dyn && hipMalloc(&c->dyn, 64 * ovs_ctx::DYN_SLOTS) != hipSuccess) { c->dyn = nullptr; return nullptr; }
+    const int k = (int)(c->dyn_seq++ % ovs_ctx::DYN_SLOTS);
+    if (!c->dyn_ev[k] && hipEventCreateWithFlags(&c->dyn_ev[k], hipEventDisableTiming) != hipSuccess) {
+        c->dyn_ev[k] = nullptr;
+        return nullptr;
+    }
+    if (c->dyn_used[k] && hipStreamWaitEvent(s, c->dyn_ev[k], 0) != hipSuccess) return nullptr;
+    unsigned long long* p = c->dyn + 8 * k;
+    if (hipMemsetAsync(p, 0, sizeof *p, s) != hipSuccess) return nullptr;
+    *slot = k;
+    return p;
+}
+
+static void dyn_release(ovs_ctx* c, hipStream_t s, int slot)
+{
+    if (slot < 0) return;
+    if (hipEventRecord(c->dyn_ev[slot], s) == hipSuccess) c->dyn_used[slot] = true;
+    else hipStreamSynchronize(s);                          // no event: the slot is free once the stream is
+}
+
 // host-pointer calls: every lookup's source must be a node of the network (a source past it would
 // be read out of bounds by the lookup kernels); device-pointer calls leave that to the caller (ovs_kbr.h)
 static ovs_status check_sources(ovs_ctx* c, const uint32_t* src, uint64_t n, bool dev)
@@ -1692,7 +1730,11 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
                                        s, pm);
             ks_release(c, s);
         } else {
-            e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, dk, ds, n, dout, dhop, c->num_cu, s);
+            int slot = -1;
+            unsigned long long* dyn = dyn_acquire(c, n, s, &slot);
+            e = launch_chord_route(chord_view(c), c->ideal, delay_consts(c->P), LC, dk, ds, n, dout, dhop, c->num_cu, s,
+                                   nullptr, dyn);
+            dyn_release(c, s, slot);
         }
         if (e == hipSuccess && drpc) {
             if (LC.recursive) e = hipMemsetAsync(drpc, 0, sizeof(uint32_t) * n, s);   // no FindNodeCalls
@@ -1722,8 +1764,11 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
         e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc, s,
                               nullptr);
     } else {
+        int slot = -1;
+        unsigned long long* dyn = dyn_acquire(c, n, s, &slot);
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), dk, ds, n, dout, dhop, drpc,
-                      c->num_cu, s);
+                      c->num_cu, s, nullptr, dyn);
+        dyn_release(c, s, slot);
     }
     if (dhop && dhop == c->kvis) kvis_release(c, s);
     if (e != hipSuccess) return hip_fail(c, e, "route kernel");
@@ -1844,7 +1889,10 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
             e = launch_chord_exact_finish(chord_view(c), delay_consts(P), P.hopCountMax, dk, ds, dhop, H, dout, n, s);
     } else if (chord) {
         LookupConsts LC{P.hopCountMax, ns, P.lookupRedundantNodes, 0};
-        e = launch_chord_route(chord_view(c), c->ideal, DC, LC, dk, ds, n, dout, dhop, c->num_cu, s);
+        int slot = -1;
+        unsigned long long* dyn = dyn_acquire(c, n, s, &slot);
+        e = launch_chord_route(chord_view(c), c->ideal, DC, LC, dk, ds, n, dout, dhop, c->num_cu, s, nullptr, dyn);
+        dyn_release(c, s, slot);
     } else if (kad_exh) {
         // lookupRpc with EXHAUSTIVE_ITERATIVE_ROUTING: redundantNodes = lookupRedundantNodes, numSiblings = ns
         bool cap_err = false;
@@ -1862,8 +1910,11 @@ ovs_status ovs_lookup_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* 
     } else if (c->kad.general) {
         e = kad_route_general(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, s, dsib);
     } else {
+        int slot = -1;
+        unsigned long long* dyn = dyn_acquire(c, n, s, &slot);
         e = kad_route(c->kad, c->xy, (uint32_t)c->n, P, DC, dk, ds, n, dout, nullptr, nullptr, c->num_cu, s,
-                      dsib);
+                      dsib, dyn);
+        dyn_release(c, s, slot);
     }
     if (e == hipSuccess && !kad_exh) e = launch_lookup_finish(chord_view(c), chord, c->ideal, nslots, dout, dsib, n, s);
     if (dhop && dhop == c->kvis) kvis_release(c, s);
