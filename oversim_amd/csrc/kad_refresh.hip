@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <mutex>
 
@@ -754,10 +755,19 @@ __device__ __forceinline__ XCfg kad_def_cfg(XCfg C)
     return C;
 }
 
+// the dynamic tail (as K1's and K2's): static slices cover KX_DYN_STATIC of the batch, the rest goes
+// out KX_DYN_CH lookups at a time from a zeroed counter at the front of the lanes' scratch
+#ifndef KX_DYN_CH
+#define KX_DYN_CH 32
+#endif
+#ifndef KX_DYN_STATIC
+#define KX_DYN_STATIC 0.70
+#endif
 template <bool EX, bool REG, int XA, bool TR, bool DEF = false>
 __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C0, XScratch X,
                                                      const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
-                                                     uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
+                                                     uint64_t nq, uint64_t chunk, unsigned long long* dyn, uint64_t dyn_from,
+                                                     ovs_route_out* __restrict__ out,
                                                      uint32_t* __restrict__ sib_out, uint32_t* __restrict__ resp_out,
                                                      int64_t* __restrict__ rtt_out, uint32_t* __restrict__ rpcs_out,
                                                      uint32_t* __restrict__ err, XTrace T)
@@ -767,7 +777,8 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     const int wl = threadIdx.x & 63;
     const uint64_t wave = lane >> 6;
     uint64_t cursor = wave * chunk;
-    const uint64_t end = min(cursor + chunk, nq);
+    uint64_t end = min(cursor + chunk, dyn ? dyn_from : nq);
+    bool more = dyn != nullptr;       // the dynamic tail (as K2's): chunks of KX_DYN_CH may be left
     const uint64_t lt_mask = (wl == 0) ? 0ull : (~0ull >> (64 - wl));
     bool active = false;
     uint64_t q = 0;
@@ -788,6 +799,19 @@ __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(Kad
     if (pre_ok && cursor + (uint64_t)wl < end) pS = qsrc[cursor + wl];
     while (true) {
         const uint64_t need = __ballot(!active);
+        if (more && need != 0 && cursor >= end) {
+            unsigned long long b = 0;
+            if (wl == 0) b = atomicAdd(dyn, (unsigned long long)KX_DYN_CH);
+            const uint64_t nb = dyn_from + (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                                            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b));
+            if (nb < nq) {
+                cursor = nb;
+                end = min(nb + (uint64_t)KX_DYN_CH, nq);
+                if (pre_ok && cursor + (uint64_t)wl < end) pS = qsrc[cursor + wl];
+            } else {
+                more = false;
+            }
+        }
         if (need != 0 && cursor < end) {
             const int rank = __popcll(need & lt_mask);
             const uint64_t mine = cursor + (uint64_t)rank;
@@ -964,7 +988,7 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     if (lanes > nq) lanes = nq;
     lanes = (lanes + 255) / 256 * 256;
     const uint64_t nhE = reg ? 0 : 2ull * R, resE = reg ? 0 : (uint64_t)(R > t.k ? R : t.k);
-    const uint64_t bytes = lanes * (nhE * (4 + 8 + 1) + resE * (4 + 8) + XMAXDEAD * 4) + 4;
+    const uint64_t bytes = 8 + lanes * (nhE * (4 + 8 + 1) + resE * (4 + 8) + XMAXDEAD * 4) + 4;
     if (g_scratch_cap[dev] < bytes) {
         if (g_scratch[dev]) { hipDeviceSynchronize(); hipFree(g_scratch[dev]); }
         g_scratch[dev] = nullptr; g_scratch_cap[dev] = 0;
@@ -973,7 +997,8 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     }
     char* buf = g_scratch[dev];
     XScratch X;
-    char* p = buf;
+    unsigned long long* dyn = reinterpret_cast<unsigned long long*>(buf);   // the dynamic tail's counter
+    char* p = buf + 8;
     X.nh_d = reinterpret_cast<uint64_t*>(p); p += lanes * nhE * 8;
     X.res_d = reinterpret_cast<uint64_t*>(p); p += lanes * resE * 8;
     X.nh_idx = reinterpret_cast<uint32_t*>(p); p += lanes * nhE * 4;
@@ -985,16 +1010,27 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
     hipMemsetAsync(err, 0, 4, st);
     const unsigned blocks = (unsigned)(lanes / 256);
     const uint64_t waves = lanes / 64;
-    const uint64_t chunk = (nq + waves - 1) / waves;
+    uint64_t chunk = (nq + waves - 1) / waves;
+    uint64_t dyn_from = nq;
+    {
+        const uint64_t cs = (uint64_t)((double)nq * KX_DYN_STATIC) / waves;
+        if (cs >= (uint64_t)KX_DYN_CH && !std::getenv("OVS_NO_DYN")) {
+            chunk = cs;
+            dyn_from = cs * waves;
+            hipMemsetAsync(dyn, 0, sizeof *dyn, st);
+        } else {
+            dyn = nullptr;
+        }
+    }
     ovs_route_out* o = reinterpret_cast<ovs_route_out*>(out);   // or ovs_lookup_out (same size)
     XTrace T{};
     if (tr) { T.tarr = trace->tarr; T.cnode = trace->cnode; T.ctime = trace->ctime; T.ccap = trace->ccap; }
 #define KRL(ex, rg, xa)                                                                                                 \
     do {                                                                                                                \
         if (tr) hipLaunchKernelGGL((k_kad_refresh<ex, rg, xa, true>), dim3(blocks), dim3(256), 0, st, V, DC, C, X,    \
-                                   qkeys, qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err, T);                  \
+                                   qkeys, qsrc, nq, chunk, dyn, dyn_from, o, sibs, responders, rtts, rpcs, err, T);                  \
         else hipLaunchKernelGGL((k_kad_refresh<ex, rg, xa, false>), dim3(blocks), dim3(256), 0, st, V, DC, C, X,      \
-                                qkeys, qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err, T);                     \
+                                qkeys, qsrc, nq, chunk, dyn, dyn_from, o, sibs, responders, rtts, rpcs, err, T);                     \
     } while (0)
     if (a8) {
         if (t.exact) { if (reg) KRL(true, true, 8); else KRL(true, false, 8); }
@@ -1003,7 +1039,7 @@ hipError_t kad_exhaustive(const KadTables& t, const double2* xy, uint32_t n, con
         if (t.exact) { if (reg) KRL(true, true, 4); else KRL(true, false, 4); }
         else if (def)
             hipLaunchKernelGGL((k_kad_refresh<false, true, 3, false, true>), dim3(blocks), dim3(256), 0, st, V, DC, C, X,
-                               qkeys, qsrc, nq, chunk, o, sibs, responders, rtts, rpcs, err, T);
+                               qkeys, qsrc, nq, chunk, dyn, dyn_from, o, sibs, responders, rtts, rpcs, err, T);
         else { if (reg) KRL(false, true, 4); else KRL(false, false, 4); }
     }
 #undef KRL

@@ -192,13 +192,14 @@ struct KadRouteIO {
     int me;
     int tl, bpb, full_ok;
     // dynamic tail (single-GPU batches, dyn != nullptr): static slices cover [0, dyn_from), the rest
-    // goes out KAD_DYN_CH lookups at a time from the zeroed counter *dyn (as K1's, chord.hip)
+    // goes out KAD_DYN_CH lookups at a time from the zeroed counter *dyn (as K1's, chord.hip; K2's
+    // lookups run longer, so half K1's chunk: E 4.01 -> 3.97 ms against 64, profiles/r06_dyn/tune.txt)
     unsigned long long* dyn;
     uint64_t dyn_from;
 };
 
 #ifndef KAD_DYN_CH
-#define KAD_DYN_CH 64
+#define KAD_DYN_CH 32
 #endif
 #ifndef KAD_DYN_STATIC
 #define KAD_DYN_STATIC 0.70

@@ -436,16 +436,30 @@ constexpr int KVL = 16;
 // DEF: the default configuration (default.ini: successorListSize 16, shiftingBits 4, useOtherLookup
 // and useSucList on, hopCountMax 50) as compile-time constants -- the start-key arithmetic's
 // modulo by shiftingBits folds to a mask: 5963 -> 4931 static instructions
+// the dynamic tail (as K1's, chord.hip): static slices cover [0, from), the rest goes out
+// K3_DYN_CH lookups at a time from the zeroed per-launch counter *ctr (nullptr: static slices only)
+struct KDyn {
+    unsigned long long* ctr;
+    uint64_t from;
+};
+#ifndef K3_DYN_CH
+#define K3_DYN_CH 64
+#endif
+#ifndef K3_DYN_STATIC
+#define K3_DYN_STATIC 0.70
+#endif
+
 template <bool KR, bool RECORD, bool DEF = false>
 __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route(KView V0, const double2* __restrict__ xy, DelayConsts DC, int hcm0,
                                                       const K160* __restrict__ qkeys, const uint32_t* __restrict__ qsrc,
-                                                      uint64_t nq, uint64_t chunk, ovs_route_out* __restrict__ out,
+                                                      uint64_t nq, uint64_t chunk, KDyn dy, ovs_route_out* __restrict__ out,
                                                       uint32_t* __restrict__ hopseq, uint32_t* __restrict__ rpcs)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     uint64_t cursor = wave * chunk;
-    const uint64_t end = min(cursor + chunk, nq);
+    uint64_t end = min(cursor + chunk, dy.ctr ? dy.from : nq);
+    bool more = dy.ctr != nullptr;                // dynamic chunks may be left
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     KView V = V0;
     if (DEF) { V.ns = 16; V.sb = 4; V.useOther = 1; V.useSuc = 1; }
@@ -468,6 +482,18 @@ __global__ __launch_bounds__(256, KR ? OVS_KOORDE_WAVES : 1) void k_koorde_route
     e.has = 0; e.step = 1;
     while (true) {
         const uint64_t need = __ballot(!active);
+        if (more && need != 0 && cursor >= end) {
+            unsigned long long b = 0;
+            if (lane == 0) b = atomicAdd(dy.ctr, (unsigned long long)K3_DYN_CH);
+            const uint64_t nb = dy.from + (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                                           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b));
+            if (nb < nq) {
+                cursor = nb;
+                end = min(nb + (uint64_t)K3_DYN_CH, nq);
+            } else {
+                more = false;
+            }
+        }
         if (need != 0 && cursor < end) {
             const uint64_t mine = cursor + (uint64_t)__popcll(need & lt_mask);
             if (!active && mine < end) {
@@ -647,8 +673,24 @@ hipError_t koorde_build(const KeyRec* recs, const double2* xy, uint32_t n, int s
 
 hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2* xy, const DelayConsts& DC,
                         int hopCountMax, const K160* keys, const uint32_t* src, uint64_t nq, ovs_route_out* out,
-                        uint32_t* hopseq, bool record, uint32_t* rpcs, int num_cu, hipStream_t st)
+                        uint32_t* hopseq, bool record, uint32_t* rpcs, int num_cu, hipStream_t st,
+                        unsigned long long* dyn)
 {
+    // a grid of `waves` persistent waves: static slices, with the dynamic tail when dyn is given
+    auto slices = [&](uint64_t waves, uint64_t* chunk, uint64_t* blocks, KDyn* dy) {
+        uint64_t c = (nq + waves - 1) / waves;
+        if (c < 1) c = 1;
+        *blocks = ((nq + c - 1) / c + 3) / 4;
+        dy->ctr = nullptr;
+        dy->from = nq;
+        const uint64_t cs = dyn ? (uint64_t)((double)nq * K3_DYN_STATIC) / (*blocks * 4) : 0;
+        if (cs >= (uint64_t)K3_DYN_CH) {
+            c = cs;
+            dy->ctr = dyn;
+            dy->from = cs * *blocks * 4;
+        }
+        *chunk = c;
+    };
     if (nq == 0) return hipSuccess;
     if (!hopseq) return hipErrorInvalidValue;
     static int bpc[4] = {0, 0, 0, 0};
@@ -665,11 +707,11 @@ hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2
         bpc[ki] = (oe == hipSuccess && b > 0) ? b : 1;
     }
     const uint64_t waves = (uint64_t)num_cu * (uint64_t)bpc[ki] * 4;
-    uint64_t chunk = (nq + waves - 1) / waves;
-    if (chunk < 1) chunk = 1;
-    const uint64_t blocks = ((nq + chunk - 1) / chunk + 3) / 4;
+    uint64_t chunk = 0, blocks = 0;
+    KDyn dy;
+    slices(waves, &chunk, &blocks, &dy);
 #define KRL(a, b) hipLaunchKernelGGL((KRT(a, b)), dim3((unsigned)blocks), dim3(256), 0, st, make_view(t, recs), xy, DC, \
-                                     hopCountMax, keys, src, nq, chunk, out, hopseq, rpcs)
+                                     hopCountMax, keys, src, nq, chunk, dy, out, hopseq, rpcs)
     const KView kv = make_view(t, recs);
 #ifdef OVS_KOORDE_NO_DEF
     const bool def = false;             // A/B build: the generic instantiation
@@ -683,11 +725,11 @@ hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2
             bpd = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_koorde_route<true, false, true>, 256, 0) == hipSuccess && b > 0) ? b : 1;
         }
         const uint64_t wd = (uint64_t)num_cu * (uint64_t)bpd * 4;
-        uint64_t cd = (nq + wd - 1) / wd;
-        if (cd < 1) cd = 1;
-        const uint64_t bd = ((nq + cd - 1) / cd + 3) / 4;
+        uint64_t cd = 0, bd = 0;
+        KDyn dd;
+        slices(wd, &cd, &bd, &dd);
         hipLaunchKernelGGL((k_koorde_route<true, false, true>), dim3((unsigned)bd), dim3(256), 0, st, kv, xy, DC, hopCountMax, keys,
-                           src, nq, cd, out, hopseq, rpcs);
+                           src, nq, cd, dd, out, hopseq, rpcs);
     } else if (kr) { if (record) KRL(true, true); else KRL(true, false); }
     else { if (record) KRL(false, true); else KRL(false, false); }
 #undef KRL

@@ -62,7 +62,8 @@ hipError_t koorde_build(const KeyRec* recs, const double2* xy, uint32_t n, int s
 // (n * hopCountMax) is required: it is also the lookup's visited set
 hipError_t koorde_route(const KoordeTables& t, const KeyRec* recs, const double2* xy, const DelayConsts& DC,
                         int hopCountMax, const K160* keys, const uint32_t* src, uint64_t nq, ovs_route_out* out,
-                        uint32_t* hopseq, bool record, uint32_t* rpcs, int num_cu, hipStream_t st);
+                        uint32_t* hopseq, bool record, uint32_t* rpcs, int num_cu, hipStream_t st,
+                        unsigned long long* dyn = nullptr);
 // Koorde::findNode at node[i] for keys[i] with extension ext[i] (updated in place); next[i] =
 // the hop, 0xFFFFFFFF where the reference throws
 hipError_t koorde_find_node(const KoordeTables& t, const KeyRec* recs, const uint32_t* node, const K160* keys,

@@ -1741,8 +1741,11 @@ ovs_status ovs_route_batch(ovs_ctx* c, const ovs_key160* keys, const uint32_t* s
             else e = launch_fill_rpcs_from_hops(dout, n, drpc, s);
         }
     } else if (c->overlay == OVS_OVERLAY_KOORDE) {
+        int slot = -1;
+        unsigned long long* dyn = dyn_acquire(c, n, s, &slot);
         e = koorde_route(c->koorde, c->recs, c->xy, delay_consts(c->P), c->P.hopCountMax, dk, ds, n, dout, dhop,
-                         !koorde_scratch, drpc, c->num_cu, s);
+                         !koorde_scratch, drpc, c->num_cu, s, dyn);
+        dyn_release(c, s, slot);
     } else if (kad_exh) {
         // sendToKey with EXHAUSTIVE_ITERATIVE_ROUTING (BaseOverlay.cc:1434-1442): lookup(key, numSiblings = 1)
         // with redundantNodes = lookupRedundantNodes, the route message to getResult()[0]
