@@ -756,12 +756,14 @@ __device__ __forceinline__ XCfg kad_def_cfg(XCfg C)
 }
 
 // the dynamic tail (as K1's and K2's): static slices cover KX_DYN_STATIC of the batch, the rest goes
-// out KX_DYN_CH lookups at a time from a zeroed counter at the front of the lanes' scratch
+// out KX_DYN_CH lookups at a time from a zeroed counter at the front of the lanes' scratch.  The
+// exhaustive lookups run long (17 RPCs each on R), so smaller chunks and a larger dynamic share than
+// K1's: R 5.34 (0.7, 32) -> 5.24 ms (0.4, 16), profiles/r06_dyn/tune_kx.txt
 #ifndef KX_DYN_CH
-#define KX_DYN_CH 32
+#define KX_DYN_CH 16
 #endif
 #ifndef KX_DYN_STATIC
-#define KX_DYN_STATIC 0.70
+#define KX_DYN_STATIC 0.40
 #endif
 template <bool EX, bool REG, int XA, bool TR, bool DEF = false>
 __global__ __launch_bounds__(256, REG ? OVS_KX_WAVES : 1) void k_kad_refresh(KadView V, DelayConsts DC, XCfg C0, XScratch X,
