@@ -506,7 +506,7 @@ struct LaneIO {
     ovs_lookup_rec* __restrict__ stage_hand;
     ovs_done_rec* __restrict__ stage_done;
     uint8_t* __restrict__ stag;            // arc of the hand-off, or nsh: finished
-    // dynamic tail (single-GPU routes, dyn != nullptr): each wave's static slice covers [0, dyn_from);
+    // dynamic tail (dyn != nullptr; routes and shard steps): each wave's static slice covers [0, dyn_from);
     // the rest is handed out K1_DYN_CH lookups at a time from the zeroed counter *dyn
     unsigned long long* dyn;
     uint64_t dyn_from;
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     uint64_t cursor = wave * io.chunk;                    // wave-uniform
-    const bool dyn = !SHARD && io.dyn != nullptr;
+    const bool dyn = io.dyn != nullptr;
     uint64_t end = min(cursor + io.chunk, dyn ? io.dyn_from : io.n);
     bool more = dyn;                                      // dynamic chunks may be left
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(256, SHARD ? OVS_K1_SHARD_WAVES : OVS_K1_WAVES) voi
         // ---- refill: lanes without a lookup take the next of the wave's slice
         bool fresh = false;
         const uint64_t need = __ballot(!active);
-        if (!SHARD && more && need != 0 && cursor >= end) {
+        if (more && need != 0 && cursor >= end) {
             // the static slice is spent: the next dynamic chunk (one atomic a chunk, lane 0)
             unsigned long long b = 0;
             if (lane == 0) b = atomicAdd(io.dyn, (unsigned long long)K1_DYN_CH);
@@ -1275,7 +1275,7 @@ static hipError_t lanes_launch(const ChordView& V, const DelayConsts& DC, const 
     static int bpc = 0;
     uint64_t blocks = 0;
     io.chunk = persistent_chunk(k_chord_lanes<REC, RECORD, SHARD, LKC, DEF>, &bpc, io.n, num_cu, &blocks);
-    if (!SHARD && io.dyn) {
+    if (io.dyn) {
         // static slices cover K1_DYN_STATIC of the batch, the rest goes out in chunks (tiny batches: static)
         const uint64_t waves = blocks * 4;
         const uint64_t cs = (uint64_t)((double)io.n * K1_DYN_STATIC) / waves;
@@ -1556,7 +1556,7 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    ovs_lookup_rec* out, uint64_t out_cap,
                                    unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                                    unsigned long long* done_count, StageBuf& stage, int num_cu, hipStream_t s,
-                                   const K160* fkeys, const uint32_t* fsrc, uint32_t fqid)
+                                   const K160* fkeys, const uint32_t* fsrc, uint32_t fqid, unsigned long long* dyn)
 {
     if (nin == 0) return hipSuccess;
     if (nsh < 1 || nsh + 1 > CMAX) return hipErrorInvalidValue;
@@ -1570,6 +1570,7 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
     io.fkeys = fkeys; io.fsrc = fsrc; io.fqid = fqid;
     io.done = done; io.dcap = done_cap; io.dcount = done_count;
     io.shard_lo = shard_lo; io.nsh = nsh; io.me = me; io.n = nin;
+    io.dyn = dyn;
     io.stage_hand = reinterpret_cast<ovs_lookup_rec*>(sb + oh);
     io.stage_done = reinterpret_cast<ovs_done_rec*>(sb + od);
     io.stag = sb + ot;

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
         chunk = (nq + waves - 1) / waves;
     }
     uint64_t cursor = wave * chunk;
-    const bool dyn = SM == 0 && io.dyn != nullptr;
+    const bool dyn = SM != 1 && io.dyn != nullptr;      // single GPU and the migration step
     uint64_t end = min(cursor + chunk, dyn ? io.dyn_from : nq);
     bool more = dyn;                                      // dynamic chunks may be left
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_
 
     while (true) {
         const uint64_t need = __ballot(!active);
-        if (SM == 0 && more && need != 0 && cursor >= end) {
+        if (SM != 1 && more && need != 0 && cursor >= end) {
             // the static slice is spent: the next dynamic chunk (one atomic a chunk, lane 0)
             unsigned long long b = 0;
             if (lane == 0) b = atomicAdd(io.dyn, (unsigned long long)KAD_DYN_CH);
@@ -560,7 +560,7 @@ static hipError_t kad_launch(const KadView& V, const DelayConsts& DC, const KadL
     if (io.chunk < 1) io.chunk = 1;
     const uint64_t need_waves = (io.nq + io.chunk - 1) / io.chunk;
     const uint64_t blocks = (need_waves + 3) / 4;
-    if (SM == 0 && io.dyn) {
+    if (SM != 1 && io.dyn) {
         // static slices cover KAD_DYN_STATIC of the batch, the rest goes out in chunks (small batches: static)
         const uint64_t cs = (uint64_t)((double)io.nq * KAD_DYN_STATIC) / (blocks * 4);
         if (cs < (uint64_t)KAD_DYN_CH) {
@@ -664,6 +664,7 @@ hipError_t kad_mig_step_launch(const KadView& V, const DelayConsts& DC, const Ka
     io.shard_lo = a.shard_lo; io.nsh = a.nsh; io.me = a.me;
     io.mstage = a.mstage; io.mtag = a.mtag; io.dstage = a.dstage;
     io.tl = V.tl; io.bpb = V.bpb; io.full_ok = LC.redundant <= V.k ? 1 : 0;
+    io.dyn = a.dyn;
     // one-way routes on snapshot tables, findNode results of up to 8 nodes (kad_mig_supported)
     if (V.maybe_short || LC.redundant > 8 || LC.maxRedundantLocal > 8) return hipErrorNotSupported;
     return kad_launch<A, false, EX, false, 2, 8, false>(V, DC, LC, io, num_cu, st);

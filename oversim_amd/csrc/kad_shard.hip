@@ -181,7 +181,7 @@ hipError_t kad_mig_step(const KadTables& t, const double2* xy, uint32_t n, const
                         const uint64_t* shard_lo, int nsh, int me, void* out, uint64_t out_cap,
                         unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                         unsigned long long* done_count, unsigned long long* bad, int num_cu, StageBuf& stage,
-                        hipStream_t s)
+                        hipStream_t s, unsigned long long* dyn)
 {
     if (!kad_mig_supported(P, t)) return hipErrorNotSupported;
     if (nsh < 1 || nsh + 1 > CMAX) return hipErrorInvalidValue;
@@ -205,6 +205,7 @@ hipError_t kad_mig_step(const KadTables& t, const double2* xy, uint32_t n, const
     a.mstage = reinterpret_cast<uint32_t*>(sb + om);
     a.dstage = reinterpret_cast<ovs_done_rec*>(sb + od);
     a.mtag = sb + ot;
+    a.dyn = dyn;
     if ((e = hipMemsetAsync(a.mtag, 0xFF, nin, s)) != hipSuccess) return e;
     const int A = kad_pend_slots(LC.alpha);
     e = t.exact ? kad_mig_step_dispatch<true>(A, V, DL, LC, a, num_cu, s)

@@ -60,6 +60,7 @@ struct KadMigStepArgs {
     uint32_t* mstage;
     uint8_t* mtag;
     ovs_done_rec* dstage;
+    unsigned long long* dyn;           // the dynamic tail's zeroed counter (nullptr: static slices)
 };
 
 size_t kad_lookup_state_bytes(int alpha, int cap);
@@ -75,7 +76,7 @@ hipError_t kad_mig_step(const KadTables& t, const double2* xy, uint32_t n, const
                         const uint64_t* shard_lo, int nsh, int me, void* out, uint64_t out_cap,
                         unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                         unsigned long long* done_count, unsigned long long* bad, int num_cu, StageBuf& stage,
-                        hipStream_t s);
+                        hipStream_t s, unsigned long long* dyn = nullptr);
 bool kad_params_supported_host(const ovs_params& P, const KadTables& t);
 // lookups of this rank: their keys and sources (copied to qkeys / qsrc), act = 2 (not started), qids,
 // the round-1 list (indices 0..n-1) and its count; sources off [lo, hi) are counted in *bad and never run

@@ -13,7 +13,8 @@ hipError_t launch_chord_shard_step(const ChordView& V, const DelayConsts& DC, co
                                    ovs_lookup_rec* out, uint64_t out_cap,
                                    unsigned long long* out_count, ovs_done_rec* done, uint64_t done_cap,
                                    unsigned long long* done_count, StageBuf& stage, int num_cu, hipStream_t s,
-                                   const K160* fkeys = nullptr, const uint32_t* fsrc = nullptr, uint32_t fqid = 0);
+                                   const K160* fkeys = nullptr, const uint32_t* fsrc = nullptr, uint32_t fqid = 0,
+                                   unsigned long long* dyn = nullptr);
 hipError_t launch_make_records(const KeyRec* recs, const K160* keys, const uint32_t* src, uint64_t n, uint32_t qid_base,
                                ovs_lookup_rec* out, hipStream_t s);
 hipError_t launch_chord_nodes(const KeyRec* recs, const double2* xy, uint32_t n, int ns, NodeRec* nodes,

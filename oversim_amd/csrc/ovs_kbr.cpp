@@ -202,6 +202,33 @@ void free_kad_shard(ovs_ctx* c)
 // whichever stream that was) and records its own use after its launch (kvis_release), so calls on
 // different streams -- device-pointer calls return while their kernels run -- never rewrite each
 // other's rows.  Growing the buffer waits for that last use only, not for the whole device.
+// A zeroed work counter for one launch of a persistent route kernel (the dynamic tail of K1,
+// launch_chord_route, and K2, kad_route): nullptr when none can be had -- the kernel then runs static slices only.
+static unsigned long long* dyn_acquire(ovs_ctx* c, uint64_t n, hipStream_t s, int* slot)
+{
+    *slot = -1;
+    if (std::getenv("OVS_NO_DYN")) return nullptr;       // A/B: static slices only
+    if (n < (1ull << 18)) return nullptr;                 // small batches: static slices (no memset, no event)
+    if (!c->dyn && hipMalloc(&c->dyn, 64 * ovs_ctx::DYN_SLOTS) != hipSuccess) { c->dyn = nullptr; return nullptr; }
+    const int k = (int)(c->dyn_seq++ % ovs_ctx::DYN_SLOTS);
+    if (!c->dyn_ev[k] && hipEventCreateWithFlags(&c->dyn_ev[k], hipEventDisableTiming) != hipSuccess) {
+        c->dyn_ev[k] = nullptr;
+        return nullptr;
+    }
+    if (c->dyn_used[k] && hipStreamWaitEvent(s, c->dyn_ev[k], 0) != hipSuccess) return nullptr;
+    unsigned long long* p = c->dyn + 8 * k;
+    if (hipMemsetAsync(p, 0, sizeof *p, s) != hipSuccess) return nullptr;
+    *slot = k;
+    return p;
+}
+
+static void dyn_release(ovs_ctx* c, hipStream_t s, int slot)
+{
+    if (slot < 0) return;
+    if (hipEventRecord(c->dyn_ev[slot], s) == hipSuccess) c->dyn_used[slot] = true;
+    else hipStreamSynchronize(s);                          // no event: the slot is free once the stream is
+}
+
 ovs_status kvis_acquire(ovs_ctx* c, uint64_t need, hipStream_t s, uint32_t** out)
 {
     if (!c->kvis_ev) {
@@ -742,9 +769,13 @@ static ovs_status shard_step(ovs_ctx* c, int ns, const ovs_lookup_rec* in, uint6
     }
     st = ensure_nodes(c, s);
     if (st != OVS_OK) return st;
-    HIPCHK(c, launch_chord_shard_step(chord_view(c), DC, LC, c->d_bounds, (int)nshards, me, in, n_in, out, out_cap,
-                                      out_count, done, done_cap, done_count, c->stage[s], c->num_cu, s,
-                                      reinterpret_cast<const K160*>(fkeys), fsrc, fqid));
+    int slot = -1;
+    unsigned long long* dyn = dyn_acquire(c, n_in, s, &slot);
+    const hipError_t e = launch_chord_shard_step(chord_view(c), DC, LC, c->d_bounds, (int)nshards, me, in, n_in, out,
+                                                 out_cap, out_count, done, done_cap, done_count, c->stage[s], c->num_cu,
+                                                 s, reinterpret_cast<const K160*>(fkeys), fsrc, fqid, dyn);
+    dyn_release(c, s, slot);
+    HIPCHK(c, e);
     return OVS_OK;
 }
 
@@ -1383,9 +1414,12 @@ ovs_status ovs::kad_mig_step_impl(ovs_ctx* c, const void* in, uint64_t n_in, con
         HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
     }
     if (reset_errors) HIPCHK(c, hipMemsetAsync(c->kbad, 0, sizeof(unsigned long long), s));
+    int slot = -1;
+    unsigned long long* dyn = dyn_acquire(c, n_in, s, &slot);
     hipError_t e = kad_mig_step(c->kad, c->xy, (uint32_t)c->n, c->P, delay_consts(c->P), in, n_in,
                                 reinterpret_cast<const K160*>(fkeys), fsrc, fqid, c->d_bounds, (int)nshards, me, out,
-                                out_cap, out_count, done, done_cap, done_count, c->kbad, c->num_cu, c->stage[s], s);
+                                out_cap, out_count, done, done_cap, done_count, c->kbad, c->num_cu, c->stage[s], s, dyn);
+    dyn_release(c, s, slot);
     if (e != hipSuccess) return hip_fail(c, e, "kademlia migration step");
     return OVS_OK;
 }
@@ -1580,33 +1614,6 @@ ovs_status ovs_epichord_find_node_batch(ovs_ctx* c, const uint32_t* node, const 
         HIPCHK(c, hipStreamSynchronize(s));
     }
     return OVS_OK;
-}
-
-// A zeroed work counter for one launch of a persistent route kernel (the dynamic tail of K1,
-// launch_chord_route, and K2, kad_route): nullptr when none can be had -- the kernel then runs static slices only.
-static unsigned long long* dyn_acquire(ovs_ctx* c, uint64_t n, hipStream_t s, int* slot)
-{
-    *slot = -1;
-    if (std::getenv("OVS_NO_DYN")) return nullptr;       // A/B: static slices only
-    if (n < (1ull << 18)) return nullptr;                 // small batches: static slices (no memset, no event)
-    if (!c->dyn && hipMalloc(&c->dyn, 64 * ovs_ctx::DYN_SLOTS) != hipSuccess) { c->dyn = nullptr; return nullptr; }
-    const int k = (int)(c->dyn_seq++ % ovs_ctx::DYN_SLOTS);
-    if (!c->dyn_ev[k] && hipEventCreateWithFlags(&c->dyn_ev[k], hipEventDisableTiming) != hipSuccess) {
-        c->dyn_ev[k] = nullptr;
-        return nullptr;
-    }
-    if (c->dyn_used[k] && hipStreamWaitEvent(s, c->dyn_ev[k], 0) != hipSuccess) return nullptr;
-    unsigned long long* p = c->dyn + 8 * k;
-    if (hipMemsetAsync(p, 0, sizeof *p, s) != hipSuccess) return nullptr;
-    *slot = k;
-    return p;
-}
-
-static void dyn_release(ovs_ctx* c, hipStream_t s, int slot)
-{
-    if (slot < 0) return;
-    if (hipEventRecord(c->dyn_ev[slot], s) == hipSuccess) c->dyn_used[slot] = true;
-    else hipStreamSynchronize(s);                          // no event: the slot is free once the stream is
 }
 
 // host-pointer calls: every lookup's source must be a node of the network (a source past it would
