@@ -34,9 +34,12 @@
 #define OVS_KAD_WAVES 3
 #endif
 #ifndef OVS_KAD_MIG2
-// the migration step (SM = 2) runs at 2 waves/SIMD: at 3 its record load / store spilled 34 VGPRs
-// (186 VGPRs at 2, no spill); -DOVS_KAD_MIG2=-1 builds it at OVS_KAD_WAVES (A/B)
-#define OVS_KAD_MIG2 2
+// the migration step (SM = 2) runs at OVS_KAD_WAVES = 3 waves/SIMD although its record load / store
+// then spill 34 VGPRs (186 VGPRs at 2, no spill): with the dynamic tail the W = 8 model's E step is
+// 9.72 ms per arc at 2 waves and 8.96 ms at 3 (same box, profiles/r06_shard/w8_E_mig_w2_vs_w3.txt);
+// -DOVS_KAD_MIG2=2 builds it at 2 (A/B).  The A = 8 objects (alpha 5..8) keep 2: at 3 their spills
+// come out as misaligned 64-bit scratch loads gfx950 rejects
+#define OVS_KAD_MIG2 -1
 #endif
 
 namespace ovs {
@@ -231,7 +234,7 @@ template <int A, bool RECORD, bool EX, bool LK, int SM, int C, bool SH, bool DEF
 // the shard step's exact-compare and LookupCall instantiations run at 2 waves/SIMD: their HBM state
 // traffic and request staging need the registers (at 3 the exact-compare ones spilled in misaligned
 // 96-bit pieces gfx950 rejects, the LookupCall one 109 VGPRs); the one-way route step keeps K2's 3
-__global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || SM == OVS_KAD_MIG2) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC0,
+__global__ __launch_bounds__(256, ((SM && (EX || LK)) || C > 8 || (SM == 2 && (OVS_KAD_MIG2 == 2 || A > 4))) ? 2 : OVS_KAD_WAVES) void k_kad_route(KadView V, DelayConsts DC, KadLC LC0,
                                                                             KadRouteIO io)
 {
     const KadLC LC = DEF ? kad_def_lc(LC0) : LC0;
